@@ -1,0 +1,234 @@
+#!/usr/bin/env python
+"""Headline benchmark: DeepFM training throughput on MI355X (BASELINE.json metric).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--dist uniform|zipf] [--no-cpu-baseline]
+
+Workload (BASELINE.json configs[1], "C2"): deepfm_pipeline, 13 dense + 26
+categorical fields x 1M vocab each (table 26,000,013 x 16 fp32), MLP
+[400,400,400], batch 65,536 per GPU, fp32, TF1-dense Adam.  One step = one full
+training step (embedding gather + FM + MLP fwd/bwd + log-loss + Adam over every
+table row) on a synthetic batch already resident in HBM.  The timed region
+replays the hipGraph of the step K times, bracketed by barrier + synchronize.
+
+Then, inside the same run, one extra eager step per timed step is bracketed per
+kernel with HIP events on the launch stream: those durations give the per-kernel
+algorithmic GB/s and TFLOP/s (`kernels`) and the `roofline` of the dominant
+kernel.  Rank 0 at N=1 also times the CPU oracle (oracle/ctr_ref.py) on a bounded
+sample of the same workload (`cpu_baseline`).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md)
+F32_MFMA_PEAK_TFLOPS = 157.3    # v_mfma_f32_16x16x4_f32 dense peak
+
+C2 = dict(C=13, V=0, S=26, E=16, per_field_vocab=1_000_000, hidden=[400, 400, 400], B=65536)
+
+
+def log(*a):
+    print("[bench %s]" % time.strftime("%H:%M:%S"), *a, file=sys.stderr, flush=True)
+
+
+def kernel_work(spec, B, touched_rows):
+    """Algorithmic bytes / flops per launch."""
+    E, S, C = spec.E, spec.S, spec.C
+    N = spec.n_rows
+    w = {}
+    # gather: FM rows (c+C) + deep rows (c) x 64 B + first-order 4 B + ids 8 B  (3,640 B/sample)
+    w["embed_fwd"] = ("hbm", B * (S * (2 * E * 4 + 4 + 8)))
+    # dense TF1 Adam: read+write p, m, v for every element; gradient rows read+reset only where touched
+    w["adam_table"] = ("hbm", N * E * 4 * 6 + touched_rows * E * 4 * 2 + N)
+    w["adam_first"] = ("hbm", N * 4 * 6 + touched_rows * 4 * 2 + N)
+    dims = [C + spec.V + S * E] + spec.hidden
+    for l in range(len(spec.hidden)):
+        f = 2.0 * B * (dims[l] + 1) * dims[l + 1]
+        w["gemm_fwd_l%d" % l] = ("mfma", f)
+        w["gemm_dw_l%d" % l] = ("mfma", f)
+        w["gemm_dx_l%d" % l] = ("mfma", 2.0 * B * dims[l + 1] * (dims[l] if l else S * E))
+    # backward scatter: FM + deep row gradients (f32 adds) + ids + dx0 read
+    w["embed_bwd"] = ("hbm", B * (S * (E * 4 * 2 + 4 * 2 + 8) + S * E * 4))
+    H = spec.hidden[-1]
+    w["head"] = ("hbm", B * (spec.fm_cols + H) * 4 * 2)
+    return w
+
+
+def cpu_baseline(spec_kw, B, budget_s=25.0):
+    """Times the numpy oracle (oracle/ctr_ref.py, the CPU restatement of
+    models/deepfm_pipeline.py) on the host: full C2 table, bounded steps."""
+    from oracle import ctr_ref as R
+    from deep_learning_amd.synthetic import make_batch
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or os.cpu_count()
+    cfg = R.make_cfg("deepfm_pipeline", C=spec_kw["C"], V=0, S=spec_kw["S"], E=spec_kw["E"],
+                     cate_index_size=spec_kw["S"] * spec_kw["per_field_vocab"], hidden=spec_kw["hidden"])
+    rng = np.random.default_rng(0)
+    P = R.init_params(cfg, rng)
+    opt = R.AdamTF1(cfg, P)
+    b = make_batch(B, cate_index_size=cfg.cate_index_size, seed=7)
+    t0 = time.time()
+    steps = 0
+    while True:
+        R.train_step(cfg, P, opt, b)
+        steps += 1
+        if time.time() - t0 > budget_s * 0.5 or steps >= 3:
+            break
+    dt = time.time() - t0
+    return {"value": steps * B / dt, "unit": "samples/s", "cores": threads, "kind": "port",
+            "sample": "%d full training step(s) of C2 (B=%d, 26M-row table, dense TF1 Adam) in the numpy "
+                      "oracle; BLAS threads=%d, numpy elementwise/scatter single-threaded; %.1f s" %
+                      (steps, B, threads, dt)}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--dist", default="uniform", choices=["uniform", "zipf"])
+    ap.add_argument("--batch", type=int, default=C2["B"])
+    ap.add_argument("--vocab", type=int, default=C2["per_field_vocab"])
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+    from deep_learning_amd.engine import CTREngine, ModelSpec
+    from deep_learning_amd.synthetic import make_batch
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+
+    B = args.batch
+    spec = ModelSpec("deepfm_pipeline", C=C2["C"], V=0, S=C2["S"], E=C2["E"],
+                     cate_index_size=C2["S"] * args.vocab, hidden=C2["hidden"])
+    log("rank %d/%d: building engine, table rows %d" % (rank, world, spec.n_rows))
+    eng = CTREngine(spec, max_batch=B, seed=2019)
+    nb = 4
+    dev_batches = []
+    for i in range(nb):
+        b = make_batch(B, cate_index_size=spec.cate_index_size, seed=1000 * rank + i, dist=args.dist)
+        dev_batches.append({k: torch.from_numpy(v).cuda() for k, v in b.items()})
+    torch.cuda.synchronize()
+    log("warmup %d" % args.warmup)
+    for i in range(max(1, args.warmup)):
+        eng.train_step(dev_batches[i % nb], graph=True)
+    torch.cuda.synchronize()
+    eng.check_error()
+
+    log("timed %d steps" % args.steps)
+    barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        eng.train_step(dev_batches[i % nb], graph=True)
+    torch.cuda.synchronize()
+    barrier()
+    t1 = time.perf_counter()
+    dt = t1 - t0
+    if world > 1:
+        tt = torch.tensor([dt], device="cuda", dtype=torch.float64)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        dt = tt.item()
+    ms = dt / args.steps * 1e3
+    value = world * B * args.steps / dt
+    loss = eng.loss()
+
+    # ---- live per-kernel timing (HIP events on the launch stream)
+    log("per-kernel event pass")
+    touched = int(eng.touched.sum().item()) if False else None
+    eng.prof = []
+    ksteps = min(args.steps, 10)
+    for i in range(ksteps):
+        eng.train_step(dev_batches[i % nb], graph=False)
+    torch.cuda.synchronize()
+    times = {}
+    for label, e0, e1 in eng.prof:
+        times.setdefault(label, []).append(e0.elapsed_time(e1) * 1e3)   # us
+    eng.prof = None
+    # unique rows touched per step (sets how much of the gradient table Adam reads)
+    ids = dev_batches[0]["cate_feats"]
+    touched_rows = int(torch.unique(torch.cat([ids.reshape(-1) + spec.C, ids.reshape(-1)])).numel()) + spec.C
+    work = kernel_work(spec, B, touched_rows)
+    kernels = {}
+    for label, ts in times.items():
+        us = float(np.mean(ts))
+        ent = {"us": round(us, 2), "launches": len(ts)}
+        if label in work:
+            kind, amount = work[label]
+            if kind == "hbm":
+                ent["GB/s"] = round(amount / (us * 1e-6) / 1e9, 1)
+                ent["frac_hbm"] = round(amount / (us * 1e-6) / 1e9 / HBM_PEAK_GBS, 3)
+            else:
+                ent["TFLOP/s"] = round(amount / (us * 1e-6) / 1e12, 2)
+                ent["frac_mfma"] = round(amount / (us * 1e-6) / 1e12 / F32_MFMA_PEAK_TFLOPS, 3)
+        kernels[label] = ent
+    dom = max((l for l in kernels), key=lambda l: kernels[l]["us"])
+    kind, amount = work.get(dom, ("hbm", 0))
+    us = kernels[dom]["us"]
+    if kind == "hbm":
+        ach = amount / (us * 1e-6) / 1e9
+        roof = {"kernel": dom, "bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": round(ach / HBM_PEAK_GBS, 3), "traffic": None, "algorithmic_bytes": amount}
+    else:
+        ach = amount / (us * 1e-6) / 1e12
+        roof = {"kernel": dom, "bound": "mfma", "achieved": round(ach, 2), "peak": F32_MFMA_PEAK_TFLOPS,
+                "unit": "TFLOP/s", "frac": round(ach / F32_MFMA_PEAK_TFLOPS, 3), "traffic": None,
+                "algorithmic_flops": amount}
+    step_kernel_us = sum(k["us"] for k in kernels.values())
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        log("cpu baseline (numpy oracle)")
+        del eng
+        torch.cuda.empty_cache()
+        try:
+            cpu = cpu_baseline(C2, B)
+        except Exception as e:  # reported, never fatal for the GPU number
+            cpu = {"value": None, "error": repr(e)}
+
+    if rank == 0:
+        out = {
+            "metric": "train samples/sec + achieved HBM GB/s, DeepFM Criteo-shape bsz=65536, 1/2/4/8 GPU",
+            "value": round(value, 1),
+            "unit": "samples/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic (seeded Criteo-shaped batches, %s ids, resident in HBM)" % args.dist,
+            "config": {"workload": "C2 deepfm_pipeline: 13 dense + 26 cat x %d vocab (table %d x 16 f32), "
+                                   "MLP [400,400,400], TF1-dense Adam" % (args.vocab, spec.n_rows),
+                       "global_batch": B * world, "per_gpu_batch": B, "parallelism": "dp%d" % world,
+                       "id_dist": args.dist},
+            "roofline": roof,
+            "cpu_baseline": cpu,
+            "kernels": kernels,
+            "kernel_sum_us_per_step": round(step_kernel_us, 1),
+            "loss": round(loss, 6),
+        }
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,89 @@
+"""ctypes binding of the HIP C ABI (include/dlamd.h) — the only way the package
+reaches the GPU kernels.  There is no CPU fallback: if the in-tree
+``libdlamd.so`` is missing or a call fails, an exception is raised.
+"""
+import ctypes as C
+import os
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libdlamd.so")
+
+
+class DLError(RuntimeError):
+    pass
+
+
+class EmbLayout(C.Structure):
+    """Mirror of ``dl_emb_layout`` (include/dlamd.h)."""
+    _fields_ = [
+        ("n_rows", C.c_int64), ("fm_cont_offset", C.c_int64), ("fm_cate_offset", C.c_int64),
+        ("deep_cate_offset", C.c_int64),
+        ("batch", C.c_int32), ("emb_dim", C.c_int32), ("cont_fields", C.c_int32),
+        ("vector_size", C.c_int32), ("cate_fields", C.c_int32), ("cate_ld", C.c_int32),
+        ("fm_cont", C.c_int32), ("use_fm", C.c_int32), ("fm_extra", C.c_int32),
+        ("zero_row0", C.c_int32), ("x0_ld", C.c_int32), ("x0_cont_col", C.c_int32),
+        ("x0_vec_col", C.c_int32), ("x0_cat_col", C.c_int32), ("x0_pool_col", C.c_int32),
+        ("fm_ld", C.c_int32), ("dx0_ld", C.c_int32), ("dx0_cat_col", C.c_int32), ("pad_", C.c_int32),
+    ]
+
+
+P = C.c_void_p
+I32, I64, U64, F = C.c_int32, C.c_int64, C.c_uint64, C.c_float
+LP = C.POINTER(EmbLayout)
+
+# name -> (restype, argtypes); the authoritative list of exported entry points
+SIGNATURES = {
+    "dl_abi_version": (I32, []),
+    "dl_last_error": (C.c_char_p, []),
+    "dl_device_sync": (I32, []),
+    "dl_embed_fwd": (I32, [LP, P, P, P, P, P, P, P, P, P, P]),
+    "dl_embed_bwd": (I32, [LP, P, P, P, P, P, P, P, P, P, P, P, I32, P]),
+    "dl_embed_bwd_grid": (I32, [LP]),
+    "dl_embed_cont_reduce": (I32, [LP, P, I32, P, P, P, P]),
+    "dl_pool_fwd": (I32, [LP, P, P, P, I32, P, P, I32, I32, P, P, P, P, P, P]),
+    "dl_pool_bwd": (I32, [LP, P, I32, P, P, I32, I32, P, P, P, P, P, I32, P, P, P, P, P, P]),
+    "dl_gemm_f32": (I32, [I32, I32, I32, I32, I32, P, I32, P, I32, P, I32, I32, P, I32, I32, I64, P]),
+    "dl_gemm_bf16": (I32, [I32, I32, I32, I32, I32, P, I32, P, I32, P, I32, I32, I32, P, I32, I32, I64, P]),
+    "dl_head_fwd_bwd": (I32, [I32, I32, I32, P, I32, P, I32, P, P, F, F, P, P, P, P, P, I32, P]),
+    "dl_head_grid": (I32, [I32]),
+    "dl_adam_begin_step": (I32, [P, F, F, P]),
+    "dl_adam_dense": (I32, [P, P, P, P, I32, I64, I64, F, I64, P, P]),
+    "dl_adam_rows": (I32, [P, P, P, P, P, I64, I32, F, I32, P, P]),
+    "dl_init_random": (I32, [P, I64, I32, F, F, U64, U64, P]),
+}
+
+_LIB = None
+
+
+def lib():
+    """Load (once) and return the ctypes library; raises if it is not built."""
+    global _LIB
+    if _LIB is None:
+        if not os.path.exists(LIB_PATH):
+            raise DLError("libdlamd.so not found at %s — build it with `python -m deep_learning_amd.build`"
+                          % LIB_PATH)
+        L = C.CDLL(LIB_PATH)
+        for name, (res, args) in SIGNATURES.items():
+            fn = getattr(L, name)
+            fn.restype = res
+            fn.argtypes = args
+        _LIB = L
+    return _LIB
+
+
+def call(name, *args):
+    rc = getattr(lib(), name)(*args)
+    if rc != 0:
+        raise DLError("%s failed (rc=%d): %s" % (name, rc, lib().dl_last_error().decode()))
+    return rc
+
+
+def ptr(t):
+    """Device pointer of a torch tensor (None -> NULL)."""
+    return None if t is None else C.c_void_p(t.data_ptr())
+
+
+def stream_handle(stream=None):
+    import torch
+    s = stream if stream is not None else torch.cuda.current_stream()
+    return C.c_void_p(s.cuda_stream)

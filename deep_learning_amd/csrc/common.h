@@ -1,0 +1,56 @@
+// Shared helpers for the libdlamd HIP sources (gfx950 / CDNA4 only).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <string.h>
+
+#include "../../include/dlamd.h"
+
+namespace dl {
+
+void set_error(const char* fmt, ...);
+
+#define DL_CHECK_ARG(cond, ...)        \
+  do {                                 \
+    if (!(cond)) {                     \
+      ::dl::set_error(__VA_ARGS__);    \
+      return 22; /* EINVAL */          \
+    }                                  \
+  } while (0)
+
+#define DL_RETURN_LAUNCH(name)                                                  \
+  do {                                                                          \
+    hipError_t e_ = hipGetLastError();                                          \
+    if (e_ != hipSuccess) {                                                     \
+      ::dl::set_error("%s: launch failed: %s", name, hipGetErrorString(e_));    \
+      return 1000 + (int)e_;                                                    \
+    }                                                                           \
+    return 0;                                                                   \
+  } while (0)
+
+inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
+
+constexpr int kWave = 64;
+
+__device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+// Reads id and validates it against [0, n); out-of-range -> row -1 + error word.
+__device__ __forceinline__ int64_t checked_row(int64_t id, int64_t off, int64_t n, int32_t* err) {
+  int64_t r = id + off;
+  if (r < 0 || r >= n) {
+    if (err) atomicOr(err, 1);
+    return -1;
+  }
+  return r;
+}
+
+inline int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }
+
+}  // namespace dl

@@ -1,0 +1,524 @@
+// Embedding gather / FM / multi-hot pooling kernels (forward and backward).
+//
+// Reference semantics (paths relative to the reference repo):
+//   models/deepfm_pipeline.py:83-123   row-0 zero, dual FM/deep indexing, FM 1st/2nd order
+//   models/deepfm_multi_cate.py:71-111 nonzero-mean pooling of multi-hot slots
+//   models/dnn_pipeline.py:72-83, models/wdl.py:132-179 deep lookups
+//
+// Layout on the MI355X:
+//   forward  — one wave per sample; a table row of E floats is read by E/4 lanes
+//              as float4 (E=16: 64 B row = 4 lanes, 16 rows per wave
+//              instruction); the FM sums reduce over the row lanes with
+//              xor-shuffles, nothing is materialised in HBM except the outputs.
+//   backward — one wave per sample; a row is E lanes x 4 B so every atomic
+//              wave instruction adds whole rows (E=16: 4 rows x 64 B); the hot
+//              cont-field rows (hit by every sample) accumulate in registers
+//              and leave the block once as a partial slab.
+#include "common.h"
+
+namespace dl {
+
+struct EmbArgs {
+  dl_emb_layout L;
+  const float* table;
+  const float* first_order;
+  const int64_t* cate;
+  const float* cont;
+  const float* vec;
+  float* x0;
+  float* fm_out;
+  float* fm_sum;
+  int32_t* err;
+};
+
+__device__ __forceinline__ bool row_ok(int64_t row, int zero_row0) {
+  return row > 0 || (row == 0 && !zero_row0);
+}
+
+__device__ __forceinline__ float4 f4_zero() { return make_float4(0.f, 0.f, 0.f, 0.f); }
+
+template <int E>
+__global__ __launch_bounds__(256) void embed_fwd_kernel(EmbArgs a) {
+  constexpr int LPR = E / 4;   // lanes per row
+  constexpr int RPI = 64 / LPR;  // rows per wave instruction
+  const dl_emb_layout& L = a.L;
+  const int lane = threadIdx.x & 63;
+  const int r = lane / LPR, q = lane % LPR;
+  const int wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int nwaves = (gridDim.x * blockDim.x) >> 6;
+  const int Cf = L.fm_cont ? L.cont_fields : 0;
+  const int S = L.cate_fields;
+  const int Fs = Cf + S;
+  const int F = Fs + L.fm_extra;
+  const float4* tab4 = reinterpret_cast<const float4*>(a.table);
+
+  for (int b = wave; b < L.batch; b += nwaves) {
+    const int64_t* ids = a.cate + (int64_t)b * L.cate_ld;
+    const float* cb = a.cont + (int64_t)b * L.cont_fields;
+    float* xb = a.x0 + (int64_t)b * L.x0_ld;
+    if (L.use_fm) {
+      float4 s = f4_zero(), ss = f4_zero();
+      for (int f0 = 0; f0 < Fs; f0 += RPI) {
+        const int f = f0 + r;
+        if (f < Fs) {
+          int64_t row;
+          float val;
+          if (f < Cf) {
+            row = L.fm_cont_offset + f;
+            val = cb[f];
+          } else {
+            row = checked_row(ids[f - Cf], L.fm_cate_offset, L.n_rows, a.err);
+            val = 1.f;
+          }
+          float4 e = f4_zero();
+          if (row_ok(row, L.zero_row0)) e = tab4[row * LPR + q];
+          e.x *= val; e.y *= val; e.z *= val; e.w *= val;
+          s.x += e.x; s.y += e.y; s.z += e.z; s.w += e.w;
+          ss.x += e.x * e.x; ss.y += e.y * e.y; ss.z += e.z * e.z; ss.w += e.w * e.w;
+        }
+      }
+      for (int f0 = 0; f0 < L.fm_extra; f0 += RPI) {
+        const int f = f0 + r;
+        if (f < L.fm_extra) {
+          const float4 e = *reinterpret_cast<const float4*>(xb + L.x0_pool_col + f * E + 4 * q);
+          s.x += e.x; s.y += e.y; s.z += e.z; s.w += e.w;
+          ss.x += e.x * e.x; ss.y += e.y * e.y; ss.z += e.z * e.z; ss.w += e.w * e.w;
+        }
+      }
+#pragma unroll
+      for (int o = LPR; o < 64; o <<= 1) {
+        s.x += __shfl_xor(s.x, o, 64); s.y += __shfl_xor(s.y, o, 64);
+        s.z += __shfl_xor(s.z, o, 64); s.w += __shfl_xor(s.w, o, 64);
+        ss.x += __shfl_xor(ss.x, o, 64); ss.y += __shfl_xor(ss.y, o, 64);
+        ss.z += __shfl_xor(ss.z, o, 64); ss.w += __shfl_xor(ss.w, o, 64);
+      }
+      if (r == 0) {
+        float4 sec;
+        sec.x = 0.5f * (s.x * s.x - ss.x); sec.y = 0.5f * (s.y * s.y - ss.y);
+        sec.z = 0.5f * (s.z * s.z - ss.z); sec.w = 0.5f * (s.w * s.w - ss.w);
+        float* fo = a.fm_out + (int64_t)b * L.fm_ld + F + 4 * q;
+        fo[0] = sec.x; fo[1] = sec.y; fo[2] = sec.z; fo[3] = sec.w;
+        if (a.fm_sum) *reinterpret_cast<float4*>(a.fm_sum + (int64_t)b * E + 4 * q) = s;
+      }
+      for (int f = lane; f < Fs; f += 64) {
+        int64_t row;
+        float val;
+        if (f < Cf) {
+          row = L.fm_cont_offset + f;
+          val = cb[f];
+        } else {
+          row = checked_row(ids[f - Cf], L.fm_cate_offset, L.n_rows, a.err);
+          val = 1.f;
+        }
+        const float w = row_ok(row, L.zero_row0) ? a.first_order[row] : 0.f;
+        a.fm_out[(int64_t)b * L.fm_ld + f] = w * val;
+      }
+    }
+    // deep lookups: x0[b][cat_col + f*E ..] = table'[id_f + deep_off]
+    for (int f0 = 0; f0 < S; f0 += RPI) {
+      const int f = f0 + r;
+      if (f < S) {
+        const int64_t row = checked_row(ids[f], L.deep_cate_offset, L.n_rows, a.err);
+        float4 e = f4_zero();
+        if (row_ok(row, L.zero_row0)) e = tab4[row * LPR + q];
+        *reinterpret_cast<float4*>(xb + L.x0_cat_col + f * E + 4 * q) = e;
+      }
+    }
+    if (L.x0_cont_col >= 0)
+      for (int j = lane; j < L.cont_fields; j += 64) xb[L.x0_cont_col + j] = cb[j];
+    if (L.x0_vec_col >= 0)
+      for (int j = lane; j < L.vector_size; j += 64)
+        xb[L.x0_vec_col + j] = a.vec[(int64_t)b * L.vector_size + j];
+  }
+}
+
+struct EmbBwdArgs {
+  dl_emb_layout L;
+  const float* table;
+  const int64_t* cate;
+  const float* cont;
+  const float* dz;
+  const float* w_head;
+  const float* fm_sum;
+  const float* dx0;
+  float* g_table;
+  float* g_first;
+  uint8_t* touched;
+  float* cont_slab;
+};
+
+constexpr int kMaxHotCont = 32;  // cont fields kept in registers on the backward
+
+template <int E>
+__global__ __launch_bounds__(256) void embed_bwd_kernel(EmbBwdArgs a) {
+  constexpr int RPI = 64 / E;  // rows per wave instruction (lane = dim)
+  constexpr int NCP = (kMaxHotCont + RPI - 1) / RPI;
+  const dl_emb_layout& L = a.L;
+  const int lane = threadIdx.x & 63;
+  const int r = lane / E, d = lane % E;
+  const int wid = threadIdx.x >> 6;
+  const int wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int nwaves = (gridDim.x * blockDim.x) >> 6;
+  const int Cf = (L.use_fm && L.fm_cont) ? L.cont_fields : 0;
+  const int S = L.cate_fields;
+  const int Fs = Cf + S;
+  const int F = Fs + L.fm_extra;
+
+  float gc[NCP];
+#pragma unroll
+  for (int p = 0; p < NCP; ++p) gc[p] = 0.f;
+  float g1c = 0.f;
+
+  for (int b = wave; b < L.batch; b += nwaves) {
+    const int64_t* ids = a.cate + (int64_t)b * L.cate_ld;
+    if (L.use_fm) {
+      const float dzb = a.dz[b];
+      const float* cb = a.cont + (int64_t)b * L.cont_fields;
+      const float dsec = dzb * a.w_head[F + d];
+      const float sd = a.fm_sum[(int64_t)b * E + d];
+      // hot cont-field rows: register accumulation
+#pragma unroll
+      for (int p = 0; p < NCP; ++p) {
+        const int f = p * RPI + r;
+        if (p * RPI < Cf && f < Cf) {
+          const int64_t row = L.fm_cont_offset + f;
+          const float val = cb[f];
+          const float e = row_ok(row, L.zero_row0) ? a.table[row * E + d] * val : 0.f;
+          gc[p] += val * dsec * (sd - e);
+        }
+      }
+      // single cate FM fields: scatter-add
+      for (int f0 = 0; f0 < S; f0 += RPI) {
+        const int f = f0 + r;
+        if (f < S) {
+          const int64_t row = ids[f] + L.fm_cate_offset;
+          if (row < L.n_rows && row_ok(row, L.zero_row0)) {
+            const float e = a.table[row * E + d];
+            atomicAdd(a.g_table + row * E + d, dsec * (sd - e));
+            if (d == 0) a.touched[row] = 1;
+          }
+        }
+      }
+      for (int f = lane; f < Fs; f += 64) {
+        if (f < Cf) {
+          g1c += dzb * a.w_head[f] * cb[f];
+        } else {
+          const int64_t row = ids[f - Cf] + L.fm_cate_offset;
+          if (row < L.n_rows && row_ok(row, L.zero_row0)) {
+            atomicAdd(a.g_first + row, dzb * a.w_head[f]);
+            a.touched[row] = 1;
+          }
+        }
+      }
+    }
+    // deep lookups
+    const float* gx = a.dx0 + (int64_t)b * L.dx0_ld + L.dx0_cat_col;
+    for (int f0 = 0; f0 < S; f0 += RPI) {
+      const int f = f0 + r;
+      if (f < S) {
+        const int64_t row = ids[f] + L.deep_cate_offset;
+        if (row < L.n_rows && row_ok(row, L.zero_row0)) {
+          atomicAdd(a.g_table + row * E + d, gx[f * E + d]);
+          if (d == 0) a.touched[row] = 1;
+        }
+      }
+    }
+  }
+
+  if (Cf > 0) {
+    // block reduction of the hot rows -> cont_slab[block][Cf*(E+1)]
+    __shared__ float red[4][kMaxHotCont * 65];
+    const int width = Cf * (E + 1);
+#pragma unroll
+    for (int p = 0; p < NCP; ++p) {
+      const int f = p * RPI + r;
+      if (p * RPI < Cf && f < Cf) red[wid][f * E + d] = gc[p];
+    }
+    if (lane < Cf) red[wid][Cf * E + lane] = g1c;
+    __syncthreads();
+    for (int k = threadIdx.x; k < width; k += blockDim.x)
+      a.cont_slab[(int64_t)blockIdx.x * width + k] = red[0][k] + red[1][k] + red[2][k] + red[3][k];
+  }
+}
+
+// Folds the cont-field partial slabs into the dense gradient tables.
+__global__ __launch_bounds__(256) void cont_reduce_kernel(dl_emb_layout L, const float* slab,
+                                                          int blocks, float* g_table,
+                                                          float* g_first, uint8_t* touched) {
+  const int E = L.emb_dim, Cf = L.cont_fields;
+  const int width = Cf * (E + 1);
+  const int k = blockIdx.x;
+  if (k >= width) return;
+  float acc = 0.f;
+  for (int t = threadIdx.x; t < blocks; t += blockDim.x) acc += slab[(int64_t)t * width + k];
+  acc = wave_sum(acc);
+  __shared__ float part[4];
+  if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const float tot = part[0] + part[1] + part[2] + part[3];
+    int64_t row;
+    if (k < Cf * E) {
+      row = L.fm_cont_offset + k / E;
+      if (!row_ok(row, L.zero_row0)) return;
+      g_table[row * E + (k % E)] += tot;
+    } else {
+      row = L.fm_cont_offset + (k - Cf * E);
+      if (!row_ok(row, L.zero_row0)) return;
+      g_first[row] += tot;
+    }
+    touched[row] = 1;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// multi-hot nonzero-mean pooling (deepfm_multi_cate.py:71-111)
+
+struct PoolArgs {
+  dl_emb_layout L;
+  const float* table;
+  const float* first_order;
+  const int64_t* ids;
+  int ids_col;
+  const int32_t* slot_start;
+  const int32_t* slot_end;
+  int n_slots;
+  int fm_col;
+  float* x0;
+  float* fm_out;
+  float* cnt_emb;
+  float* cnt_first;
+  int32_t* err;
+};
+
+template <int E>
+__global__ __launch_bounds__(256) void pool_fwd_kernel(PoolArgs a) {
+  constexpr int LPR = E / 4;
+  constexpr int RPI = 64 / LPR;
+  const dl_emb_layout& L = a.L;
+  const int lane = threadIdx.x & 63;
+  const int r = lane / LPR, q = lane % LPR;
+  const int wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int nwaves = (gridDim.x * blockDim.x) >> 6;
+  const float4* tab4 = reinterpret_cast<const float4*>(a.table);
+  for (int b = wave; b < L.batch; b += nwaves) {
+    const int64_t* ids = a.ids + (int64_t)b * L.cate_ld + a.ids_col;
+    for (int m = 0; m < a.n_slots; ++m) {
+      const int s0 = a.slot_start[m], s1 = a.slot_end[m];
+      float4 s = f4_zero();
+      float cnt = 0.f;
+      for (int l0 = s0; l0 < s1; l0 += RPI) {
+        const int l = l0 + r;
+        float4 e = f4_zero();
+        if (l < s1) {
+          const int64_t row = checked_row(ids[l], 0, L.n_rows, a.err);
+          if (row_ok(row, L.zero_row0)) e = tab4[row * LPR + q];
+        }
+        // tf.reduce_sum(emb, axis=2) then count_nonzero over the slot
+        float rs = (e.x + e.y) + (e.z + e.w);
+#pragma unroll
+        for (int o = 1; o < LPR; o <<= 1) rs += __shfl_xor(rs, o, 64);
+        if (q == 0 && l < s1 && rs != 0.f) cnt += 1.f;
+        s.x += e.x; s.y += e.y; s.z += e.z; s.w += e.w;
+      }
+#pragma unroll
+      for (int o = LPR; o < 64; o <<= 1) {
+        s.x += __shfl_xor(s.x, o, 64); s.y += __shfl_xor(s.y, o, 64);
+        s.z += __shfl_xor(s.z, o, 64); s.w += __shfl_xor(s.w, o, 64);
+      }
+      cnt = wave_sum(cnt);
+      if (r == 0) {
+        float4 o4 = f4_zero();
+        if (cnt > 0.f) { o4.x = s.x / cnt; o4.y = s.y / cnt; o4.z = s.z / cnt; o4.w = s.w / cnt; }
+        *reinterpret_cast<float4*>(a.x0 + (int64_t)b * L.x0_ld + L.x0_pool_col + m * E + 4 * q) = o4;
+      }
+      if (lane == 0) a.cnt_emb[(int64_t)b * a.n_slots + m] = cnt;
+      if (a.first_order) {
+        float s1v = 0.f, c1 = 0.f;
+        for (int l = s0 + lane; l < s1; l += 64) {
+          const int64_t row = checked_row(ids[l], 0, L.n_rows, a.err);
+          const float w = row_ok(row, L.zero_row0) ? a.first_order[row] : 0.f;
+          s1v += w;
+          c1 += (w != 0.f) ? 1.f : 0.f;
+        }
+        s1v = wave_sum(s1v);
+        c1 = wave_sum(c1);
+        if (lane == 0) {
+          a.fm_out[(int64_t)b * L.fm_ld + a.fm_col + m] = c1 > 0.f ? s1v / c1 : 0.f;
+          a.cnt_first[(int64_t)b * a.n_slots + m] = c1;
+        }
+      }
+    }
+  }
+}
+
+struct PoolBwdArgs {
+  dl_emb_layout L;
+  const int64_t* ids;
+  int ids_col;
+  const int32_t* slot_start;
+  const int32_t* slot_end;
+  int n_slots;
+  int fm_col;
+  const float* x0;
+  const float* fm_sum;
+  const float* dz;
+  const float* w_head;
+  const float* dx0;
+  int dx0_pool_col;
+  const float* cnt_emb;
+  const float* cnt_first;
+  float* g_table;
+  float* g_first;
+  uint8_t* touched;
+};
+
+template <int E>
+__global__ __launch_bounds__(256) void pool_bwd_kernel(PoolBwdArgs a) {
+  constexpr int RPI = 64 / E;
+  const dl_emb_layout& L = a.L;
+  const int lane = threadIdx.x & 63;
+  const int r = lane / E, d = lane % E;
+  const int wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int nwaves = (gridDim.x * blockDim.x) >> 6;
+  const int F = (L.fm_cont ? L.cont_fields : 0) + L.cate_fields + L.fm_extra;
+  for (int b = wave; b < L.batch; b += nwaves) {
+    const int64_t* ids = a.ids + (int64_t)b * L.cate_ld + a.ids_col;
+    const float dzb = L.use_fm ? a.dz[b] : 0.f;
+    const float dsec = L.use_fm ? dzb * a.w_head[F + d] : 0.f;
+    const float sd = L.use_fm ? a.fm_sum[(int64_t)b * E + d] : 0.f;
+    for (int m = 0; m < a.n_slots; ++m) {
+      const int s0 = a.slot_start[m], s1 = a.slot_end[m];
+      const float pooled = a.x0[(int64_t)b * L.x0_ld + L.x0_pool_col + m * E + d];
+      float dp = a.dx0[(int64_t)b * L.dx0_ld + a.dx0_pool_col + m * E + d];
+      if (L.use_fm) dp += dsec * (sd - pooled);
+      const float c = a.cnt_emb[(int64_t)b * a.n_slots + m];
+      const float gv = c > 0.f ? dp / c : 0.f;   // div_no_nan gradient
+      for (int l0 = s0; l0 < s1; l0 += RPI) {
+        const int l = l0 + r;
+        if (l < s1) {
+          const int64_t row = ids[l];
+          if (row < L.n_rows && row_ok(row, L.zero_row0)) {
+            atomicAdd(a.g_table + row * E + d, gv);
+            if (d == 0) a.touched[row] = 1;
+          }
+        }
+      }
+      if (L.use_fm && a.g_first) {
+        const float c1 = a.cnt_first[(int64_t)b * a.n_slots + m];
+        const float g1 = c1 > 0.f ? dzb * a.w_head[a.fm_col + m] / c1 : 0.f;
+        for (int l = s0 + lane; l < s1; l += 64) {
+          const int64_t row = ids[l];
+          if (row < L.n_rows && row_ok(row, L.zero_row0)) {
+            atomicAdd(a.g_first + row, g1);
+            a.touched[row] = 1;
+          }
+        }
+      }
+    }
+  }
+}
+
+static int check_layout(const dl_emb_layout* L) {
+  DL_CHECK_ARG(L != nullptr, "layout is NULL");
+  const int E = L->emb_dim;
+  DL_CHECK_ARG(E == 4 || E == 8 || E == 16 || E == 32 || E == 64, "emb_dim %d not in {4,8,16,32,64}", E);
+  DL_CHECK_ARG(L->batch >= 0 && L->n_rows > 0, "bad batch/n_rows");
+  DL_CHECK_ARG(L->x0_ld % 4 == 0 && L->x0_cat_col % 4 == 0, "x0_ld and x0_cat_col must be multiples of 4");
+  DL_CHECK_ARG(!L->fm_extra || L->x0_pool_col % 4 == 0, "x0_pool_col must be a multiple of 4");
+  DL_CHECK_ARG(L->cont_fields <= kMaxHotCont || !(L->use_fm && L->fm_cont),
+               "at most %d FM cont fields", kMaxHotCont);
+  return 0;
+}
+
+static int emb_grid(int B) {
+  int g = (B + 3) / 4;
+  if (g > 4096) g = 4096;
+  return g < 1 ? 1 : g;
+}
+
+}  // namespace dl
+
+using namespace dl;
+
+#define DL_DISPATCH_E(E, ...)                    \
+  switch (E) {                                   \
+    case 4: { constexpr int kE = 4; __VA_ARGS__; break; }   \
+    case 8: { constexpr int kE = 8; __VA_ARGS__; break; }   \
+    case 16: { constexpr int kE = 16; __VA_ARGS__; break; } \
+    case 32: { constexpr int kE = 32; __VA_ARGS__; break; } \
+    case 64: { constexpr int kE = 64; __VA_ARGS__; break; } \
+  }
+
+extern "C" int dl_embed_fwd(const dl_emb_layout* L, const float* table, const float* first_order,
+                            const int64_t* cate, const float* cont, const float* vector,
+                            float* x0, float* fm_out, float* fm_sum, int32_t* err, void* stream) {
+  if (int rc = check_layout(L)) return rc;
+  DL_CHECK_ARG(table && cate && x0, "NULL table/cate/x0");
+  DL_CHECK_ARG(!L->use_fm || (first_order && fm_out && fm_sum), "FM outputs required");
+  if (L->batch == 0) return 0;
+  EmbArgs a{*L, table, first_order, cate, cont, vector, x0, fm_out, fm_sum, err};
+  DL_DISPATCH_E(L->emb_dim, hipLaunchKernelGGL(embed_fwd_kernel<kE>, dim3(emb_grid(L->batch)),
+                                               dim3(256), 0, as_stream(stream), a));
+  DL_RETURN_LAUNCH("dl_embed_fwd");
+}
+
+extern "C" int dl_embed_bwd_grid(const dl_emb_layout* L) { return emb_grid(L->batch) < 1024 ? emb_grid(L->batch) : 1024; }
+
+extern "C" int dl_embed_bwd(const dl_emb_layout* L, const float* table, const int64_t* cate,
+                            const float* cont, const float* dz, const float* w_head,
+                            const float* fm_sum, const float* dx0, float* g_table, float* g_first,
+                            uint8_t* touched, float* cont_slab, int32_t cont_slab_blocks,
+                            void* stream) {
+  if (int rc = check_layout(L)) return rc;
+  if (L->batch == 0) return 0;
+  const int grid = dl_embed_bwd_grid(L);
+  const bool hot = L->use_fm && L->fm_cont && L->cont_fields > 0;
+  DL_CHECK_ARG(!hot || (cont_slab && cont_slab_blocks >= grid), "cont_slab needs %d blocks", grid);
+  DL_CHECK_ARG(!L->use_fm || (dz && w_head && fm_sum && g_first), "FM backward inputs required");
+  EmbBwdArgs a{*L, table, cate, cont, dz, w_head, fm_sum, dx0, g_table, g_first, touched, cont_slab};
+  DL_DISPATCH_E(L->emb_dim, hipLaunchKernelGGL(embed_bwd_kernel<kE>, dim3(grid), dim3(256), 0,
+                                               as_stream(stream), a));
+  DL_RETURN_LAUNCH("dl_embed_bwd");
+}
+
+extern "C" int dl_embed_cont_reduce(const dl_emb_layout* L, const float* cont_slab, int32_t blocks,
+                                    float* g_table, float* g_first, uint8_t* touched, void* stream) {
+  if (int rc = check_layout(L)) return rc;
+  if (!(L->use_fm && L->fm_cont && L->cont_fields > 0)) return 0;
+  const int width = L->cont_fields * (L->emb_dim + 1);
+  hipLaunchKernelGGL(cont_reduce_kernel, dim3(width), dim3(256), 0, as_stream(stream), *L,
+                     cont_slab, blocks, g_table, g_first, touched);
+  DL_RETURN_LAUNCH("dl_embed_cont_reduce");
+}
+
+extern "C" int dl_pool_fwd(const dl_emb_layout* L, const float* table, const float* first_order,
+                           const int64_t* ids, int32_t ids_col, const int32_t* slot_start,
+                           const int32_t* slot_end, int32_t n_slots, int32_t fm_col, float* x0,
+                           float* fm_out, float* cnt_emb, float* cnt_first, int32_t* err,
+                           void* stream) {
+  if (int rc = check_layout(L)) return rc;
+  DL_CHECK_ARG(n_slots >= 0 && slot_start && slot_end, "bad slots");
+  DL_CHECK_ARG(!first_order || (fm_out && cnt_first), "first-order pooling needs fm_out/cnt_first");
+  if (L->batch == 0 || n_slots == 0) return 0;
+  PoolArgs a{*L, table, first_order, ids, ids_col, slot_start, slot_end, n_slots, fm_col,
+             x0, fm_out, cnt_emb, cnt_first, err};
+  DL_DISPATCH_E(L->emb_dim, hipLaunchKernelGGL(pool_fwd_kernel<kE>, dim3(emb_grid(L->batch)),
+                                               dim3(256), 0, as_stream(stream), a));
+  DL_RETURN_LAUNCH("dl_pool_fwd");
+}
+
+extern "C" int dl_pool_bwd(const dl_emb_layout* L, const int64_t* ids, int32_t ids_col,
+                           const int32_t* slot_start, const int32_t* slot_end, int32_t n_slots,
+                           int32_t fm_col, const float* x0, const float* fm_sum, const float* dz,
+                           const float* w_head, const float* dx0, int32_t dx0_pool_col,
+                           const float* cnt_emb, const float* cnt_first, float* g_table,
+                           float* g_first, uint8_t* touched, void* stream) {
+  if (int rc = check_layout(L)) return rc;
+  if (L->batch == 0 || n_slots == 0) return 0;
+  PoolBwdArgs a{*L, ids, ids_col, slot_start, slot_end, n_slots, fm_col, x0, fm_sum, dz, w_head,
+                dx0, dx0_pool_col, cnt_emb, cnt_first, g_table, g_first, touched};
+  DL_DISPATCH_E(L->emb_dim, hipLaunchKernelGGL(pool_bwd_kernel<kE>, dim3(emb_grid(L->batch)),
+                                               dim3(256), 0, as_stream(stream), a));
+  DL_RETURN_LAUNCH("dl_pool_bwd");
+}

@@ -1,0 +1,414 @@
+// Dense-tower GEMMs on the CDNA4 matrix cores.
+//
+// fp32: v_mfma_f32_16x16x4_f32 (exact f32 in / f32 accumulate, a k-ordered fma
+// chain — the fp32 reference numerics of deepfm_pipeline.py:150-152 and the
+// MatMul gradients, at the f32 matrix peak of 157 TF).
+// bf16: v_mfma_f32_16x16x32_bf16 for the Wide&Deep bf16 tower (config C5).
+//
+// One kernel template covers the three products of a layer:
+//   forward  H  = X  . W        (A row-major [i][r], B row-major [r][j])
+//   dX       dX = dY . W^T      (B read transposed)
+//   dW       dW = X^T . dY      (A read transposed, split-K over the batch into
+//                                partial slabs that the Adam kernel sums)
+// Bias is folded in: every activation matrix carries a ones column and every
+// weight matrix an extra bias row, so dW's extra row IS the bias gradient.
+//
+// Block: 256 threads = 4 waves; tile BM x BN, K-step 16, LDS double buffer with
+// register-staged prefetch (issue-early / write-late).  LDS images are k-major
+// ([k][i], [k][j]) with the row stride padded to 16 mod 32 words so the two
+// 16-lane k-rows of an MFMA operand read land in disjoint banks.
+// Block -> tile mapping is XCD-aware: tiles that share the A rows are dealt to
+// blocks b, b+8, ... which the dispatcher places on one XCD (speed only).
+#include "common.h"
+
+namespace dl {
+
+typedef float floatx4 __attribute__((ext_vector_type(4)));
+
+struct GemmParams {
+  const void* A;
+  const void* B;
+  void* C;
+  const void* mask;
+  int M, N, K;
+  int lda, ldb, ldc, ldm;
+  int k_per_split;
+  long long c_split_stride;
+};
+
+enum { EPI_STORE = 0, EPI_RELU = 1, EPI_MASK = 2, EPI_SPLIT = 3 };
+
+__device__ __forceinline__ int xcd_tile(int bid, int T) {
+  const int x = bid & 7;
+  const int q = T >> 3, rm = T & 7;
+  return (x < rm ? x * (q + 1) : rm * (q + 1) + (x - rm) * q) + (bid >> 3);
+}
+
+template <int BM, int BN, int WM, int WN, bool TA, bool TB, int EPI>
+__global__ __launch_bounds__(256) void gemm_f32_kernel(GemmParams p) {
+  constexpr int BK = 16;
+  constexpr int PADA = (48 - (BM % 32)) % 32;
+  constexpr int PADB = (48 - (BN % 32)) % 32;
+  constexpr int SA = BM + PADA, SB = BN + PADB;
+  constexpr int WTM = BM / WM, WTN = BN / WN;
+  constexpr int FM = WTM / 16, FN = WTN / 16;
+  constexpr int QA = (BM * BK / 4 + 255) / 256;  // float4 staged per thread
+  constexpr int QB = (BN * BK / 4 + 255) / 256;
+  static_assert(WM * WN == 4, "4 waves");
+  static_assert(WTM % 16 == 0 && WTN % 16 == 0, "wave tile");
+
+  __shared__ __attribute__((aligned(16))) float As[2][BK][SA];
+  __shared__ __attribute__((aligned(16))) float Bs[2][BK][SB];
+
+  const float* __restrict__ A = reinterpret_cast<const float*>(p.A);
+  const float* __restrict__ Bm = reinterpret_cast<const float*>(p.B);
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wid = tid >> 6;
+  const int wm = wid / WN, wn = wid % WN;
+
+  const int ntm = (p.M + BM - 1) / BM, ntn = (p.N + BN - 1) / BN;
+  const int t = xcd_tile(blockIdx.x, ntm * ntn);
+  const int i0 = (t / ntn) * BM, j0 = (t % ntn) * BN;
+  const int kbeg = blockIdx.z * p.k_per_split;
+  const int kend = min(p.K, kbeg + p.k_per_split);
+  const int nk = (kend - kbeg + BK - 1) / BK;
+
+  floatx4 acc[FM][FN];
+#pragma unroll
+  for (int a = 0; a < FM; ++a)
+#pragma unroll
+    for (int b = 0; b < FN; ++b) acc[a][b] = floatx4{0.f, 0.f, 0.f, 0.f};
+
+  float4 ra[QA], rb[QB];
+
+  auto load_tile = [&](int k0) {
+#pragma unroll
+    for (int u = 0; u < QA; ++u) {
+      const int qi = tid + u * 256;
+      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (qi < BM * BK / 4) {
+        if (TA) {  // A stored [r][i]
+          const int r = qi / (BM / 4), i4 = qi % (BM / 4);
+          const int gr = k0 + r, gi = i0 + 4 * i4;
+          if (gr < kend && gi < p.M) v = *reinterpret_cast<const float4*>(A + (long long)gr * p.lda + gi);
+        } else {   // A stored [i][r]
+          const int i = qi / 4, r4 = qi % 4;
+          const int gi = i0 + i, gr = k0 + 4 * r4;
+          if (gi < p.M && gr < kend) v = *reinterpret_cast<const float4*>(A + (long long)gi * p.lda + gr);
+        }
+      }
+      ra[u] = v;
+    }
+#pragma unroll
+    for (int u = 0; u < QB; ++u) {
+      const int qi = tid + u * 256;
+      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (qi < BN * BK / 4) {
+        if (!TB) {  // B stored [r][j]
+          const int r = qi / (BN / 4), j4 = qi % (BN / 4);
+          const int gr = k0 + r, gj = j0 + 4 * j4;
+          if (gr < kend && gj < p.N) v = *reinterpret_cast<const float4*>(Bm + (long long)gr * p.ldb + gj);
+        } else {    // B stored [j][r]
+          const int j = qi / 4, r4 = qi % 4;
+          const int gj = j0 + j, gr = k0 + 4 * r4;
+          if (gj < p.N && gr < kend) v = *reinterpret_cast<const float4*>(Bm + (long long)gj * p.ldb + gr);
+        }
+      }
+      rb[u] = v;
+    }
+  };
+  auto store_tile = [&](int buf) {
+#pragma unroll
+    for (int u = 0; u < QA; ++u) {
+      const int qi = tid + u * 256;
+      if (qi < BM * BK / 4) {
+        if (TA) {
+          const int r = qi / (BM / 4), i4 = qi % (BM / 4);
+          *reinterpret_cast<float4*>(&As[buf][r][4 * i4]) = ra[u];
+        } else {
+          const int i = qi / 4, r4 = qi % 4;
+          As[buf][4 * r4 + 0][i] = ra[u].x;
+          As[buf][4 * r4 + 1][i] = ra[u].y;
+          As[buf][4 * r4 + 2][i] = ra[u].z;
+          As[buf][4 * r4 + 3][i] = ra[u].w;
+        }
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < QB; ++u) {
+      const int qi = tid + u * 256;
+      if (qi < BN * BK / 4) {
+        if (!TB) {
+          const int r = qi / (BN / 4), j4 = qi % (BN / 4);
+          *reinterpret_cast<float4*>(&Bs[buf][r][4 * j4]) = rb[u];
+        } else {
+          const int j = qi / 4, r4 = qi % 4;
+          Bs[buf][4 * r4 + 0][j] = rb[u].x;
+          Bs[buf][4 * r4 + 1][j] = rb[u].y;
+          Bs[buf][4 * r4 + 2][j] = rb[u].z;
+          Bs[buf][4 * r4 + 3][j] = rb[u].w;
+        }
+      }
+    }
+  };
+
+  if (nk > 0) {
+    load_tile(kbeg);
+    store_tile(0);
+    __syncthreads();
+  }
+  const int kr = lane >> 4, cl = lane & 15;
+  for (int kt = 0; kt < nk; ++kt) {
+    const int cur = kt & 1;
+    if (kt + 1 < nk) load_tile(kbeg + (kt + 1) * BK);
+#pragma unroll
+    for (int s = 0; s < BK / 4; ++s) {
+      float av[FM], bv[FN];
+#pragma unroll
+      for (int a = 0; a < FM; ++a) av[a] = As[cur][4 * s + kr][wm * WTM + a * 16 + cl];
+#pragma unroll
+      for (int b = 0; b < FN; ++b) bv[b] = Bs[cur][4 * s + kr][wn * WTN + b * 16 + cl];
+#pragma unroll
+      for (int a = 0; a < FM; ++a)
+#pragma unroll
+        for (int b = 0; b < FN; ++b)
+          acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[a], bv[b], acc[a][b], 0, 0, 0);
+    }
+    if (kt + 1 < nk) store_tile(cur ^ 1);
+    __syncthreads();
+  }
+
+  float* __restrict__ C = reinterpret_cast<float*>(p.C);
+  if (EPI == EPI_SPLIT) C += (long long)blockIdx.z * p.c_split_stride;
+  const float* __restrict__ Mk = reinterpret_cast<const float*>(p.mask);
+#pragma unroll
+  for (int a = 0; a < FM; ++a)
+#pragma unroll
+    for (int b = 0; b < FN; ++b) {
+      const int col = j0 + wn * WTN + b * 16 + cl;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int row = i0 + wm * WTM + a * 16 + kr * 4 + j;
+        if (row < p.M && col < p.N) {
+          float v = acc[a][b][j];
+          if (EPI == EPI_RELU) v = fmaxf(v, 0.f);
+          if (EPI == EPI_MASK) v = Mk[(long long)row * p.ldm + col] > 0.f ? v : 0.f;
+          C[(long long)row * p.ldc + col] = v;
+        }
+      }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// bf16 variant (Wide&Deep tower): 16x16x32 bf16 MFMA, K-step 32, fp32 accumulate.
+typedef short shortx8 __attribute__((ext_vector_type(8)));
+
+__device__ __forceinline__ float bf2f(unsigned short h) { return __uint_as_float(((unsigned)h) << 16); }
+__device__ __forceinline__ unsigned short f2bf(float f) {
+  // round-to-nearest-even; NaN kept NaN
+  unsigned u = __float_as_uint(f);
+  if ((u & 0x7f800000u) == 0x7f800000u && (u & 0x7fffffu)) return (unsigned short)((u >> 16) | 0x40);
+  u += 0x7fffu + ((u >> 16) & 1u);
+  return (unsigned short)(u >> 16);
+}
+
+template <int BM, int BN, int WM, int WN, bool TA, bool TB, int EPI, bool CBF16>
+__global__ __launch_bounds__(256) void gemm_bf16_kernel(GemmParams p) {
+  constexpr int BK = 32;
+  constexpr int WTM = BM / WM, WTN = BN / WN;
+  constexpr int FM = WTM / 16, FN = WTN / 16;
+  // LDS images: [i][k] and [j][k] with k contiguous (8 bf16 = 16 B per lane read)
+  constexpr int SK = BK + 8;  // pad 16 B per row: rows shift banks by 4 words
+  __shared__ __attribute__((aligned(16))) unsigned short As[2][BM][SK];
+  __shared__ __attribute__((aligned(16))) unsigned short Bs[2][BN][SK];
+  const unsigned short* __restrict__ A = reinterpret_cast<const unsigned short*>(p.A);
+  const unsigned short* __restrict__ Bm = reinterpret_cast<const unsigned short*>(p.B);
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm = wid / WN, wn = wid % WN;
+  const int ntm = (p.M + BM - 1) / BM, ntn = (p.N + BN - 1) / BN;
+  const int t = xcd_tile(blockIdx.x, ntm * ntn);
+  const int i0 = (t / ntn) * BM, j0 = (t % ntn) * BN;
+  const int kbeg = blockIdx.z * p.k_per_split;
+  const int kend = min(p.K, kbeg + p.k_per_split);
+  const int nk = (kend - kbeg + BK - 1) / BK;
+  floatx4 acc[FM][FN];
+#pragma unroll
+  for (int a = 0; a < FM; ++a)
+#pragma unroll
+    for (int b = 0; b < FN; ++b) acc[a][b] = floatx4{0.f, 0.f, 0.f, 0.f};
+
+  // element-wise staging (general transposes); bf16 tower is a secondary path
+  auto stage = [&](int buf, int k0) {
+    for (int e = tid; e < BM * BK; e += 256) {
+      const int i = e / BK, k = e % BK;
+      const int gi = i0 + i, gk = k0 + k;
+      unsigned short v = 0;
+      if (gi < p.M && gk < kend) v = TA ? A[(long long)gk * p.lda + gi] : A[(long long)gi * p.lda + gk];
+      As[buf][i][k] = v;
+    }
+    for (int e = tid; e < BN * BK; e += 256) {
+      const int j = e / BK, k = e % BK;
+      const int gj = j0 + j, gk = k0 + k;
+      unsigned short v = 0;
+      if (gj < p.N && gk < kend) v = TB ? Bm[(long long)gj * p.ldb + gk] : Bm[(long long)gk * p.ldb + gj];
+      Bs[buf][j][k] = v;
+    }
+  };
+  if (nk > 0) { stage(0, kbeg); __syncthreads(); }
+  const int cl = lane & 15, kq = lane >> 4;
+  for (int kt = 0; kt < nk; ++kt) {
+    const int cur = kt & 1;
+    shortx8 av[FM], bv[FN];
+#pragma unroll
+    for (int a = 0; a < FM; ++a)
+      av[a] = *reinterpret_cast<const shortx8*>(&As[cur][wm * WTM + a * 16 + cl][8 * kq]);
+#pragma unroll
+    for (int b = 0; b < FN; ++b)
+      bv[b] = *reinterpret_cast<const shortx8*>(&Bs[cur][wn * WTN + b * 16 + cl][8 * kq]);
+    if (kt + 1 < nk) stage(cur ^ 1, kbeg + (kt + 1) * BK);
+#pragma unroll
+    for (int a = 0; a < FM; ++a)
+#pragma unroll
+      for (int b = 0; b < FN; ++b)
+        acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[a], bv[b], acc[a][b], 0, 0, 0);
+    __syncthreads();
+  }
+  const int kr = lane >> 4;
+  const long long zoff = (EPI == EPI_SPLIT) ? (long long)blockIdx.z * p.c_split_stride : 0;
+#pragma unroll
+  for (int a = 0; a < FM; ++a)
+#pragma unroll
+    for (int b = 0; b < FN; ++b) {
+      const int col = j0 + wn * WTN + b * 16 + cl;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int row = i0 + wm * WTM + a * 16 + kr * 4 + j;
+        if (row < p.M && col < p.N) {
+          float v = acc[a][b][j];
+          if (EPI == EPI_RELU) v = fmaxf(v, 0.f);
+          if (EPI == EPI_MASK) {
+            const unsigned short* mk = reinterpret_cast<const unsigned short*>(p.mask);
+            v = bf2f(mk[(long long)row * p.ldm + col]) > 0.f ? v : 0.f;
+          }
+          const long long o = zoff + (long long)row * p.ldc + col;
+          if (CBF16) reinterpret_cast<unsigned short*>(p.C)[o] = f2bf(v);
+          else reinterpret_cast<float*>(p.C)[o] = v;
+        }
+      }
+    }
+}
+
+template <int BM, int BN, int WM, int WN, bool TA, bool TB>
+static void launch_f32(const GemmParams& gp, int epi, int splits, hipStream_t s) {
+  const int tiles = (int)(ceil_div(gp.M, BM) * ceil_div(gp.N, BN));
+  dim3 grid(tiles, 1, splits);
+  switch (epi) {
+    case EPI_STORE: hipLaunchKernelGGL((gemm_f32_kernel<BM, BN, WM, WN, TA, TB, EPI_STORE>), grid, dim3(256), 0, s, gp); break;
+    case EPI_RELU: hipLaunchKernelGGL((gemm_f32_kernel<BM, BN, WM, WN, TA, TB, EPI_RELU>), grid, dim3(256), 0, s, gp); break;
+    case EPI_MASK: hipLaunchKernelGGL((gemm_f32_kernel<BM, BN, WM, WN, TA, TB, EPI_MASK>), grid, dim3(256), 0, s, gp); break;
+    default: hipLaunchKernelGGL((gemm_f32_kernel<BM, BN, WM, WN, TA, TB, EPI_SPLIT>), grid, dim3(256), 0, s, gp); break;
+  }
+}
+
+template <bool TA, bool TB>
+static void dispatch_bn_f32(const GemmParams& gp, int epi, int splits, hipStream_t s) {
+  // pick the N tile with the least padding (ties -> wider tile)
+  const int cand[4] = {208, 128, 80, 64};
+  int best = 64;
+  long long bestpad = 1LL << 60;
+  for (int c : cand) {
+    const long long pad = ceil_div(gp.N, c) * c;
+    if (pad < bestpad) { bestpad = pad; best = c; }
+  }
+  switch (best) {
+    case 208: launch_f32<128, 208, 4, 1, TA, TB>(gp, epi, splits, s); break;
+    case 128: launch_f32<128, 128, 2, 2, TA, TB>(gp, epi, splits, s); break;
+    case 80: launch_f32<128, 80, 4, 1, TA, TB>(gp, epi, splits, s); break;
+    default: launch_f32<128, 64, 4, 1, TA, TB>(gp, epi, splits, s); break;
+  }
+}
+
+template <int BM, int BN, int WM, int WN, bool TA, bool TB, bool CB>
+static void launch_bf16(const GemmParams& gp, int epi, int splits, hipStream_t s) {
+  const int tiles = (int)(ceil_div(gp.M, BM) * ceil_div(gp.N, BN));
+  dim3 grid(tiles, 1, splits);
+  switch (epi) {
+    case EPI_STORE: hipLaunchKernelGGL((gemm_bf16_kernel<BM, BN, WM, WN, TA, TB, EPI_STORE, CB>), grid, dim3(256), 0, s, gp); break;
+    case EPI_RELU: hipLaunchKernelGGL((gemm_bf16_kernel<BM, BN, WM, WN, TA, TB, EPI_RELU, CB>), grid, dim3(256), 0, s, gp); break;
+    case EPI_MASK: hipLaunchKernelGGL((gemm_bf16_kernel<BM, BN, WM, WN, TA, TB, EPI_MASK, CB>), grid, dim3(256), 0, s, gp); break;
+    default: hipLaunchKernelGGL((gemm_bf16_kernel<BM, BN, WM, WN, TA, TB, EPI_SPLIT, false>), grid, dim3(256), 0, s, gp); break;
+  }
+}
+
+}  // namespace dl
+
+using namespace dl;
+
+extern "C" int dl_gemm_f32(int32_t ta, int32_t tb, int32_t M, int32_t N, int32_t K, const float* A,
+                           int32_t lda, const float* B, int32_t ldb, float* C, int32_t ldc,
+                           int32_t epi, const float* mask, int32_t ldm, int32_t splits,
+                           int64_t c_split_stride, void* stream) {
+  DL_CHECK_ARG(M >= 0 && N >= 0 && K >= 0, "negative dims");
+  DL_CHECK_ARG(A && B && C, "NULL operand");
+  DL_CHECK_ARG(lda % 4 == 0 && ldb % 4 == 0 && ldc >= N, "lda/ldb must be multiples of 4, ldc >= N");
+  DL_CHECK_ARG(((uintptr_t)A % 16) == 0 && ((uintptr_t)B % 16) == 0, "A/B must be 16-byte aligned");
+  // float4 staging reads whole 4-element groups of the contiguous dimension:
+  // the rows must be allocated (and finite, normally zero) up to the next multiple of 4.
+  DL_CHECK_ARG(lda >= (ta ? (M + 3) / 4 * 4 : (K + 3) / 4 * 4),
+               "lda %d < padded contiguous extent of A (ta=%d M=%d K=%d)", lda, ta, M, K);
+  DL_CHECK_ARG(ldb >= (tb ? (K + 3) / 4 * 4 : (N + 3) / 4 * 4),
+               "ldb %d < padded contiguous extent of B (tb=%d N=%d K=%d)", ldb, tb, N, K);
+  DL_CHECK_ARG(epi >= 0 && epi <= 3, "bad epilogue %d", epi);
+  DL_CHECK_ARG(epi != EPI_MASK || mask, "mask epilogue needs mask");
+  if (splits < 1) splits = 1;
+  DL_CHECK_ARG(splits == 1 || epi == EPI_SPLIT, "splits > 1 requires the split epilogue");
+  if (M == 0 || N == 0) return 0;
+  GemmParams gp;
+  gp.A = A; gp.B = B; gp.C = C; gp.mask = mask;
+  gp.M = M; gp.N = N; gp.K = K; gp.lda = lda; gp.ldb = ldb; gp.ldc = ldc; gp.ldm = ldm;
+  int kps = (int)ceil_div(K, splits);
+  kps = (kps + 15) / 16 * 16;
+  if (kps == 0) kps = 16;
+  gp.k_per_split = kps;
+  splits = (int)ceil_div(K > 0 ? K : 1, kps);
+  gp.c_split_stride = c_split_stride;
+  hipStream_t s = as_stream(stream);
+  if (!ta && !tb) dispatch_bn_f32<false, false>(gp, epi, splits, s);
+  else if (!ta && tb) dispatch_bn_f32<false, true>(gp, epi, splits, s);
+  else if (ta && !tb) dispatch_bn_f32<true, false>(gp, epi, splits, s);
+  else dispatch_bn_f32<true, true>(gp, epi, splits, s);
+  DL_RETURN_LAUNCH("dl_gemm_f32");
+}
+
+extern "C" int dl_gemm_bf16(int32_t ta, int32_t tb, int32_t M, int32_t N, int32_t K,
+                            const uint16_t* A, int32_t lda, const uint16_t* B, int32_t ldb, void* C,
+                            int32_t ldc, int32_t c_bf16, int32_t epi, const void* mask, int32_t ldm,
+                            int32_t splits, int64_t c_split_stride, void* stream) {
+  DL_CHECK_ARG(M >= 0 && N >= 0 && K >= 0, "negative dims");
+  DL_CHECK_ARG(A && B && C, "NULL operand");
+  DL_CHECK_ARG(epi >= 0 && epi <= 3, "bad epilogue %d", epi);
+  DL_CHECK_ARG(epi != EPI_MASK || mask, "mask epilogue needs mask");
+  DL_CHECK_ARG(!(epi == EPI_SPLIT && c_bf16), "split slabs are fp32");
+  if (splits < 1) splits = 1;
+  DL_CHECK_ARG(splits == 1 || epi == EPI_SPLIT, "splits > 1 requires the split epilogue");
+  if (M == 0 || N == 0) return 0;
+  GemmParams gp;
+  gp.A = A; gp.B = B; gp.C = C; gp.mask = mask;
+  gp.M = M; gp.N = N; gp.K = K; gp.lda = lda; gp.ldb = ldb; gp.ldc = ldc; gp.ldm = ldm;
+  int kps = (int)ceil_div(K, splits);
+  kps = (kps + 31) / 32 * 32;
+  if (kps == 0) kps = 32;
+  gp.k_per_split = kps;
+  splits = (int)ceil_div(K > 0 ? K : 1, kps);
+  gp.c_split_stride = c_split_stride;
+  hipStream_t s = as_stream(stream);
+#define DL_BF(TA_, TB_)                                                              \
+  if (c_bf16) launch_bf16<128, 64, 4, 1, TA_, TB_, true>(gp, epi, splits, s);        \
+  else launch_bf16<128, 64, 4, 1, TA_, TB_, false>(gp, epi, splits, s);
+  if (!ta && !tb) { DL_BF(false, false) }
+  else if (!ta && tb) { DL_BF(false, true) }
+  else if (ta && !tb) { DL_BF(true, false) }
+  else { DL_BF(true, true) }
+#undef DL_BF
+  DL_RETURN_LAUNCH("dl_gemm_bf16");
+}

@@ -1,0 +1,157 @@
+// Output layer + sigmoid + eps-clipped log-loss, forward and backward in one pass.
+//
+// Reference: models/deepfm_pipeline.py:155-183 (z = concat([first, second, deep]) @ W + b,
+// score = sigmoid(z), loss = tf.losses.log_loss(label, score) = mean_B of
+// -y ln(p+1e-7) - (1-y) ln(1-p+1e-7)); models/dnn_pipeline.py:114-131 (no FM part).
+//
+// One wave per sample: the feature row (FM part + last hidden layer) is read
+// once, z is a wave reduction, and the same registers then produce
+//   dh = dz * w_h * (h > 0)   (ReluGrad of the last hidden layer, fused)
+// and the per-lane partial sums of dW = sum_b dz_b * feat_b.  Blocks leave
+// their partials in a slab that dl_adam_dense reduces (deterministic; no atomics).
+#include "common.h"
+
+namespace dl {
+
+constexpr int kHeadMaxFm = 128;   // FM columns (F + E)
+constexpr int kHeadMaxH4 = 4;     // hidden float4 chunks per lane: H <= 1024
+
+__global__ __launch_bounds__(256) void head_kernel(int B, int fm_cols, int H, const float* __restrict__ fm_out,
+                                                   int fm_ld, const float* __restrict__ h, int ldh,
+                                                   const float* __restrict__ w, const float* __restrict__ label,
+                                                   float eps, float inv_batch, float* __restrict__ score,
+                                                   float* __restrict__ z_out, float* __restrict__ dz,
+                                                   float* __restrict__ dh, float* __restrict__ slab) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int nwaves = (gridDim.x * blockDim.x) >> 6;
+  const int H4 = (H + 3) / 4;
+  const float bias = w[fm_cols + H];
+  // per-lane weights (held in registers across samples)
+  float wf[kHeadMaxFm / 64];
+  float4 wh[kHeadMaxH4];
+#pragma unroll
+  for (int k = 0; k < kHeadMaxFm / 64; ++k) {
+    const int c = lane + 64 * k;
+    wf[k] = c < fm_cols ? w[c] : 0.f;
+  }
+#pragma unroll
+  for (int k = 0; k < kHeadMaxH4; ++k) {
+    const int c = 4 * (lane + 64 * k);
+    wh[k].x = c + 0 < H ? w[fm_cols + c + 0] : 0.f;
+    wh[k].y = c + 1 < H ? w[fm_cols + c + 1] : 0.f;
+    wh[k].z = c + 2 < H ? w[fm_cols + c + 2] : 0.f;
+    wh[k].w = c + 3 < H ? w[fm_cols + c + 3] : 0.f;
+  }
+  float gf[kHeadMaxFm / 64] = {};
+  float4 gh[kHeadMaxH4];
+#pragma unroll
+  for (int k = 0; k < kHeadMaxH4; ++k) gh[k] = make_float4(0.f, 0.f, 0.f, 0.f);
+  float gb = 0.f, lsum = 0.f;
+
+  for (int b = wave; b < B; b += nwaves) {
+    float ff[kHeadMaxFm / 64];
+    float4 hh[kHeadMaxH4];
+    float part = 0.f;
+#pragma unroll
+    for (int k = 0; k < kHeadMaxFm / 64; ++k) {
+      const int c = lane + 64 * k;
+      ff[k] = c < fm_cols ? fm_out[(long long)b * fm_ld + c] : 0.f;
+      part += ff[k] * wf[k];
+    }
+    const float* hb = h + (long long)b * ldh;
+#pragma unroll
+    for (int k = 0; k < kHeadMaxH4; ++k) {
+      const int c4 = lane + 64 * k;
+      hh[k] = c4 < H4 ? *reinterpret_cast<const float4*>(hb + 4 * c4) : make_float4(0.f, 0.f, 0.f, 0.f);
+      part += hh[k].x * wh[k].x + hh[k].y * wh[k].y + hh[k].z * wh[k].z + hh[k].w * wh[k].w;
+    }
+    const float z = wave_sum(part) + bias;
+    const float p = 1.f / (1.f + expf(-z));
+    const float y = label[b];
+    const float dp = (-y / (p + eps) + (1.f - y) / (1.f - p + eps)) * inv_batch;
+    const float g = dp * p * (1.f - p);   // SigmoidGrad
+    if (lane == 0) {
+      score[b] = p;
+      if (z_out) z_out[b] = z;
+      dz[b] = g;
+      gb += g;
+      lsum += -y * logf(p + eps) - (1.f - y) * logf(1.f - p + eps);
+    }
+#pragma unroll
+    for (int k = 0; k < kHeadMaxFm / 64; ++k) gf[k] += g * ff[k];
+    float* dhb = dh + (long long)b * ldh;
+#pragma unroll
+    for (int k = 0; k < kHeadMaxH4; ++k) {
+      const int c4 = lane + 64 * k;
+      gh[k].x += g * hh[k].x; gh[k].y += g * hh[k].y; gh[k].z += g * hh[k].z; gh[k].w += g * hh[k].w;
+      if (c4 < H4) {
+        const int c = 4 * c4;
+        float4 o;
+        o.x = hh[k].x > 0.f ? g * wh[k].x : 0.f;
+        o.y = hh[k].y > 0.f ? g * wh[k].y : 0.f;
+        o.z = hh[k].z > 0.f ? g * wh[k].z : 0.f;
+        o.w = hh[k].w > 0.f ? g * wh[k].w : 0.f;
+        if (c + 3 < H) *reinterpret_cast<float4*>(dhb + c) = o;
+        else {
+          if (c + 0 < H) dhb[c + 0] = o.x;
+          if (c + 1 < H) dhb[c + 1] = o.y;
+          if (c + 2 < H) dhb[c + 2] = o.z;
+        }
+      }
+    }
+  }
+  // block reduction -> slab[block][fm_cols + H + 2]
+  const int width = fm_cols + H + 2;
+  extern __shared__ __attribute__((aligned(16))) float red[];  // [4][width]
+#pragma unroll
+  for (int k = 0; k < kHeadMaxFm / 64; ++k) {
+    const int c = lane + 64 * k;
+    if (c < fm_cols) red[wid * width + c] = gf[k];
+  }
+#pragma unroll
+  for (int k = 0; k < kHeadMaxH4; ++k) {
+    const int c = 4 * (lane + 64 * k);
+    float* o = red + wid * width + fm_cols;
+    if (c + 0 < H) o[c + 0] = gh[k].x;
+    if (c + 1 < H) o[c + 1] = gh[k].y;
+    if (c + 2 < H) o[c + 2] = gh[k].z;
+    if (c + 3 < H) o[c + 3] = gh[k].w;
+  }
+  if (lane == 0) {
+    red[wid * width + fm_cols + H] = gb;
+    red[wid * width + fm_cols + H + 1] = lsum;
+  }
+  __syncthreads();
+  for (int c = threadIdx.x; c < width; c += blockDim.x)
+    slab[(long long)blockIdx.x * width + c] =
+        red[c] + red[width + c] + red[2 * width + c] + red[3 * width + c];
+}
+
+}  // namespace dl
+
+using namespace dl;
+
+extern "C" int dl_head_grid(int32_t B) {
+  int g = (B + 63) / 64;   // ~16 samples per wave
+  if (g > 512) g = 512;
+  return g < 1 ? 1 : g;
+}
+
+extern "C" int dl_head_fwd_bwd(int32_t B, int32_t fm_cols, int32_t H, const float* fm_out,
+                               int32_t fm_ld, const float* h, int32_t ldh, const float* w,
+                               const float* label, float eps, float inv_batch, float* score,
+                               float* z_out, float* dz, float* dh, float* slab,
+                               int32_t slab_blocks, void* stream) {
+  DL_CHECK_ARG(fm_cols >= 0 && fm_cols <= kHeadMaxFm, "fm_cols %d > %d", fm_cols, kHeadMaxFm);
+  DL_CHECK_ARG(H > 0 && H <= 4 * 64 * kHeadMaxH4, "H %d > %d", H, 4 * 64 * kHeadMaxH4);
+  DL_CHECK_ARG(ldh % 4 == 0 && ldh >= H && ((uintptr_t)h % 16) == 0, "h must be 16-B aligned, ldh %% 4 == 0");
+  DL_CHECK_ARG(!fm_cols || fm_out, "fm_out required");
+  const int grid = dl_head_grid(B);
+  DL_CHECK_ARG(slab_blocks >= grid, "slab needs %d blocks", grid);
+  if (B == 0) return 0;
+  const size_t lds = 4 * (size_t)(fm_cols + H + 2) * sizeof(float);
+  hipLaunchKernelGGL(head_kernel, dim3(grid), dim3(256), lds, as_stream(stream), B, fm_cols, H,
+                     fm_out, fm_ld, h, ldh, w, label, eps, inv_batch, score, z_out, dz, dh, slab);
+  DL_RETURN_LAUNCH("dl_head_fwd_bwd");
+}

@@ -1,0 +1,255 @@
+// TF1-faithful Adam (training_ops.cc ApplyAdam, non-Nesterov) and parameter init.
+//
+// Reference: models/deepfm_pipeline.py:184-188 — exponential_decay(staircase) +
+// tf.train.AdamOptimizer(...).minimize(loss, global_step).  The embedding
+// gradient reaches its Variable densified (concat + strided-slice, :83-86), so
+// TF applies the DENSE update: every element's m and v decay every step and
+// every row with m != 0 moves (SURVEY.md ledger item 6).  Here that dense sweep
+// is one streaming pass over p, m, v; the gradient table is only read (and
+// reset) for rows the step touched, which a uint8 flag per row records — an
+// untouched row's gradient is exactly zero, so the result is the dense one.
+#include "common.h"
+
+namespace dl {
+
+// opt: [0] b1p [1] b2p [2] lr [3] alpha [4] b1 [5] b2 [6] eps [7] step
+__global__ void adam_begin_kernel(float* opt, float decay_rate, float decay_steps) {
+  const float step = opt[7];
+  const float pw = floorf(step / decay_steps);                   // staircase=True
+  const float lr_t = opt[2] * powf(decay_rate, pw);
+  const float b1p = opt[0], b2p = opt[1];
+  opt[3] = lr_t * sqrtf(1.f - b2p) / (1.f - b1p);                // ApplyAdamNonCuda alpha
+  opt[0] = b1p * opt[4];                                         // Adam._finish
+  opt[1] = b2p * opt[5];
+  opt[7] = step + 1.f;                                           // global_step += 1
+}
+
+__device__ __forceinline__ void adam_elem(float& p, float& m, float& v, float g, float alpha,
+                                          float omb1, float omb2, float eps) {
+  m += (g - m) * omb1;
+  v += (g * g - v) * omb2;
+  p -= (m * alpha) / (sqrtf(v) + eps);
+}
+
+// Dense parameter, gradient = sum of partial slabs (+ l2 * p for i < l2_count).
+__global__ __launch_bounds__(256) void adam_dense_thread_kernel(float* __restrict__ p, float* __restrict__ m,
+                                                                float* __restrict__ v,
+                                                                const float* __restrict__ slab, int nslab,
+                                                                long long stride, long long n, float l2,
+                                                                long long l2_count, const float* __restrict__ opt) {
+  const float alpha = opt[3], omb1 = 1.f - opt[4], omb2 = 1.f - opt[5], eps = opt[6];
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (long long)gridDim.x * blockDim.x) {
+    float g = 0.f;
+    int s = 0;
+    for (; s + 4 <= nslab; s += 4) {
+      const float a0 = slab[(s + 0) * stride + i], a1 = slab[(s + 1) * stride + i];
+      const float a2 = slab[(s + 2) * stride + i], a3 = slab[(s + 3) * stride + i];
+      g += a0; g += a1; g += a2; g += a3;
+    }
+    for (; s < nslab; ++s) g += slab[s * stride + i];
+    float pi = p[i], mi = m[i], vi = v[i];
+    if (i < l2_count) g += l2 * pi;
+    adam_elem(pi, mi, vi, g, alpha, omb1, omb2, eps);
+    p[i] = pi; m[i] = mi; v[i] = vi;
+  }
+}
+
+// Few elements, many slabs (head weights): one wave per element.
+__global__ __launch_bounds__(256) void adam_dense_wave_kernel(float* __restrict__ p, float* __restrict__ m,
+                                                              float* __restrict__ v,
+                                                              const float* __restrict__ slab, int nslab,
+                                                              long long stride, long long n, float l2,
+                                                              long long l2_count, const float* __restrict__ opt) {
+  const long long i = ((long long)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int lane = threadIdx.x & 63;
+  if (i >= n) return;
+  float g = 0.f;
+  for (int s = lane; s < nslab; s += 64) g += slab[s * stride + i];
+  g = wave_sum(g);
+  if (lane == 0) {
+    float pi = p[i], mi = m[i], vi = v[i];
+    if (i < l2_count) g += l2 * pi;
+    adam_elem(pi, mi, vi, g, opt[3], 1.f - opt[4], 1.f - opt[5], opt[6]);
+    p[i] = pi; m[i] = mi; v[i] = vi;
+  }
+}
+
+// Embedding table rows of width W (multiple of 4): one thread per float4.
+__global__ __launch_bounds__(256) void adam_rows4_kernel(float4* __restrict__ p, float4* __restrict__ m,
+                                                         float4* __restrict__ v, float4* __restrict__ g,
+                                                         const uint8_t* __restrict__ touched, long long n4,
+                                                         int lpr, float l2, const float* __restrict__ opt) {
+  const float alpha = opt[3], omb1 = 1.f - opt[4], omb2 = 1.f - opt[5], eps = opt[6];
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n4;
+       i += (long long)gridDim.x * blockDim.x) {
+    const long long row = i / lpr;
+    float4 gi = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (touched[row]) {
+      gi = g[i];
+      g[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+    float4 pi = p[i], mi = m[i], vi = v[i];
+    if (l2 != 0.f) { gi.x += l2 * pi.x; gi.y += l2 * pi.y; gi.z += l2 * pi.z; gi.w += l2 * pi.w; }
+    adam_elem(pi.x, mi.x, vi.x, gi.x, alpha, omb1, omb2, eps);
+    adam_elem(pi.y, mi.y, vi.y, gi.y, alpha, omb1, omb2, eps);
+    adam_elem(pi.z, mi.z, vi.z, gi.z, alpha, omb1, omb2, eps);
+    adam_elem(pi.w, mi.w, vi.w, gi.w, alpha, omb1, omb2, eps);
+    p[i] = pi; m[i] = mi; v[i] = vi;
+  }
+}
+
+// Width-1 tables (first-order weights): one thread per 4 rows.
+__global__ __launch_bounds__(256) void adam_rows1_kernel(float* __restrict__ p, float* __restrict__ m,
+                                                         float* __restrict__ v, float* __restrict__ g,
+                                                         uint8_t* __restrict__ touched, long long n,
+                                                         float l2, int clear, const float* __restrict__ opt) {
+  const float alpha = opt[3], omb1 = 1.f - opt[4], omb2 = 1.f - opt[5], eps = opt[6];
+  const long long n4 = n / 4;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < (n + 3) / 4;
+       i += (long long)gridDim.x * blockDim.x) {
+    if (i < n4) {
+      const uchar4 t = reinterpret_cast<const uchar4*>(touched)[i];
+      float4 gi = make_float4(0.f, 0.f, 0.f, 0.f);
+      float4* g4 = reinterpret_cast<float4*>(g) + i;
+      if (t.x | t.y | t.z | t.w) {
+        gi = *g4;
+        *g4 = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (!t.x) gi.x = 0.f; if (!t.y) gi.y = 0.f; if (!t.z) gi.z = 0.f; if (!t.w) gi.w = 0.f;
+        if (clear) reinterpret_cast<uchar4*>(touched)[i] = make_uchar4(0, 0, 0, 0);
+      }
+      float4 pi = reinterpret_cast<float4*>(p)[i], mi = reinterpret_cast<float4*>(m)[i],
+             vi = reinterpret_cast<float4*>(v)[i];
+      if (l2 != 0.f) { gi.x += l2 * pi.x; gi.y += l2 * pi.y; gi.z += l2 * pi.z; gi.w += l2 * pi.w; }
+      adam_elem(pi.x, mi.x, vi.x, gi.x, alpha, omb1, omb2, eps);
+      adam_elem(pi.y, mi.y, vi.y, gi.y, alpha, omb1, omb2, eps);
+      adam_elem(pi.z, mi.z, vi.z, gi.z, alpha, omb1, omb2, eps);
+      adam_elem(pi.w, mi.w, vi.w, gi.w, alpha, omb1, omb2, eps);
+      reinterpret_cast<float4*>(p)[i] = pi; reinterpret_cast<float4*>(m)[i] = mi;
+      reinterpret_cast<float4*>(v)[i] = vi;
+    } else {
+      for (long long r = 4 * i; r < n; ++r) {
+        float gi = 0.f;
+        if (touched[r]) { gi = g[r]; g[r] = 0.f; if (clear) touched[r] = 0; }
+        float pi = p[r], mi = m[r], vi = v[r];
+        if (l2 != 0.f) gi += l2 * pi;
+        adam_elem(pi, mi, vi, gi, alpha, omb1, omb2, eps);
+        p[r] = pi; m[r] = mi; v[r] = vi;
+      }
+    }
+  }
+}
+
+__global__ void clear_touched_kernel(uint8_t* touched, long long n) {
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < (n + 15) / 16;
+       i += (long long)gridDim.x * blockDim.x) {
+    if (16 * i + 16 <= n) reinterpret_cast<uint4*>(touched)[i] = make_uint4(0, 0, 0, 0);
+    else for (long long r = 16 * i; r < n; ++r) touched[r] = 0;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Philox-4x32-10 counter-based RNG
+__device__ __forceinline__ uint4 philox(uint4 c, uint2 k) {
+#pragma unroll
+  for (int r = 0; r < 10; ++r) {
+    const unsigned long long p0 = (unsigned long long)0xD2511F53u * c.x;
+    const unsigned long long p1 = (unsigned long long)0xCD9E8D57u * c.z;
+    c = make_uint4((unsigned)(p1 >> 32) ^ c.y ^ k.x, (unsigned)p1, (unsigned)(p0 >> 32) ^ c.w ^ k.y,
+                   (unsigned)p0);
+    k.x += 0x9E3779B9u;
+    k.y += 0xBB67AE85u;
+  }
+  return c;
+}
+
+__global__ __launch_bounds__(256) void init_random_kernel(float* p, long long n, int dist, float mean,
+                                                          float scale, unsigned long long seed,
+                                                          unsigned long long offset) {
+  const uint2 key = make_uint2((unsigned)seed, (unsigned)(seed >> 32));
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; 4 * i < n;
+       i += (long long)gridDim.x * blockDim.x) {
+    const unsigned long long ctr = offset / 4 + (unsigned long long)i;
+    const uint4 r = philox(make_uint4((unsigned)ctr, (unsigned)(ctr >> 32), 0x5eedu, 0u), key);
+    const float u0 = (r.x >> 8) * (1.f / 16777216.f), u1 = (r.y >> 8) * (1.f / 16777216.f);
+    const float u2 = (r.z >> 8) * (1.f / 16777216.f), u3 = (r.w >> 8) * (1.f / 16777216.f);
+    float o[4];
+    if (dist == 0) {  // Box-Muller
+      const float a = sqrtf(-2.f * logf(1.f - u0)), b = sqrtf(-2.f * logf(1.f - u2));
+      o[0] = a * cospif(2.f * u1); o[1] = a * sinpif(2.f * u1);
+      o[2] = b * cospif(2.f * u3); o[3] = b * sinpif(2.f * u3);
+      for (int j = 0; j < 4; ++j) o[j] = mean + scale * o[j];
+    } else {
+      o[0] = mean + scale * u0; o[1] = mean + scale * u1; o[2] = mean + scale * u2; o[3] = mean + scale * u3;
+    }
+    for (int j = 0; j < 4; ++j)
+      if (4 * i + j < n) p[4 * i + j] = o[j];
+  }
+}
+
+static int grid_for(long long n, int per_thread = 1) {
+  long long g = (n / per_thread + 255) / 256;
+  if (g > 256 * 16) g = 256 * 16;
+  return g < 1 ? 1 : (int)g;
+}
+
+}  // namespace dl
+
+using namespace dl;
+
+extern "C" int dl_adam_begin_step(float* opt, float decay_rate, float decay_steps, void* stream) {
+  DL_CHECK_ARG(opt != nullptr, "opt is NULL");
+  hipLaunchKernelGGL(adam_begin_kernel, dim3(1), dim3(1), 0, as_stream(stream), opt, decay_rate, decay_steps);
+  DL_RETURN_LAUNCH("dl_adam_begin_step");
+}
+
+extern "C" int dl_adam_dense(float* p, float* m, float* v, const float* slab, int32_t nslab,
+                             int64_t slab_stride, int64_t n, float l2, int64_t l2_count,
+                             const float* opt, void* stream) {
+  DL_CHECK_ARG(p && m && v && slab && opt, "NULL pointer");
+  DL_CHECK_ARG(nslab >= 1 && slab_stride >= n, "bad slabs");
+  if (n == 0) return 0;
+  if (n < 16384 && nslab >= 32) {
+    const long long blocks = (n * 64 + 255) / 256;
+    hipLaunchKernelGGL(adam_dense_wave_kernel, dim3((unsigned)blocks), dim3(256), 0, as_stream(stream), p, m,
+                       v, slab, nslab, (long long)slab_stride, (long long)n, l2, (long long)l2_count, opt);
+  } else {
+    hipLaunchKernelGGL(adam_dense_thread_kernel, dim3(grid_for(n)), dim3(256), 0, as_stream(stream), p, m,
+                       v, slab, nslab, (long long)slab_stride, (long long)n, l2, (long long)l2_count, opt);
+  }
+  DL_RETURN_LAUNCH("dl_adam_dense");
+}
+
+extern "C" int dl_adam_rows(float* p, float* m, float* v, float* g, uint8_t* touched, int64_t n_rows,
+                            int32_t width, float l2, int32_t clear_touched, const float* opt,
+                            void* stream) {
+  DL_CHECK_ARG(p && m && v && g && touched && opt, "NULL pointer");
+  DL_CHECK_ARG(width == 1 || width % 4 == 0, "width must be 1 or a multiple of 4");
+  DL_CHECK_ARG(((uintptr_t)p | (uintptr_t)m | (uintptr_t)v | (uintptr_t)g) % 16 == 0, "16-B alignment");
+  if (n_rows == 0) return 0;
+  hipStream_t s = as_stream(stream);
+  if (width == 1) {
+    DL_CHECK_ARG(((uintptr_t)touched % 4) == 0, "touched must be 4-B aligned");
+    hipLaunchKernelGGL(adam_rows1_kernel, dim3(grid_for(n_rows, 4)), dim3(256), 0, s, p, m, v, g, touched,
+                       (long long)n_rows, l2, clear_touched, opt);
+  } else {
+    const long long n4 = n_rows * (width / 4);
+    hipLaunchKernelGGL(adam_rows4_kernel, dim3(grid_for(n4)), dim3(256), 0, s, (float4*)p, (float4*)m,
+                       (float4*)v, (float4*)g, touched, n4, width / 4, l2, opt);
+    if (clear_touched) {
+      DL_CHECK_ARG(((uintptr_t)touched % 16) == 0, "touched must be 16-B aligned");
+      hipLaunchKernelGGL(clear_touched_kernel, dim3(grid_for(n_rows, 16)), dim3(256), 0, s, touched,
+                         (long long)n_rows);
+    }
+  }
+  DL_RETURN_LAUNCH("dl_adam_rows");
+}
+
+extern "C" int dl_init_random(float* p, int64_t n, int32_t dist, float mean, float scale, uint64_t seed,
+                              uint64_t offset, void* stream) {
+  DL_CHECK_ARG(p && n >= 0 && offset % 4 == 0, "bad args");
+  if (n == 0) return 0;
+  hipLaunchKernelGGL(init_random_kernel, dim3(grid_for(n, 4)), dim3(256), 0, as_stream(stream), p,
+                     (long long)n, dist, mean, scale, (unsigned long long)seed, (unsigned long long)offset);
+  DL_RETURN_LAUNCH("dl_init_random");
+}

@@ -1,0 +1,472 @@
+"""MI355X training engine for the reference's CTR models (DeepFM / DNN / Wide&Deep).
+
+One ``CTREngine`` holds every device buffer of a model (parameters, TF1-Adam
+state, activations, gradient tables, partial-sum slabs) and runs a training
+step as a fixed sequence of HIP kernels from ``libdlamd.so`` on one stream —
+so the whole step can be captured into a hipGraph and replayed.
+
+Step (deepfm_pipeline, reference models/deepfm_pipeline.py:76-191):
+  adam_begin_step                       alpha_t, beta powers, global_step
+  embed_fwd                             gather + FM 1st/2nd order + x0 assembly
+  gemm_f32 x L (ReLU)                   deep tower forward (bias = ones column)
+  head_fwd_bwd                          logit, sigmoid, log-loss, dz, dh_L, dW_head partials
+  for l = L-1..0: gemm dW (split-K) ; gemm dX (ReluGrad) ; adam_dense(W_l)
+  embed_bwd + cont_reduce               FM/deep row gradients -> dense gradient table
+  adam_dense(head) ; adam_rows(table) ; adam_rows(first-order)
+
+Internal layouts (import/export map to the reference's):
+  x0  = [cate embeddings (S*E) | pooled (M*E) | cont (C) | vector (V) | 1 | 0-pad]
+  W_l = [in_ld, out_ld] row-major; row in_dim holds the bias, pads are zero
+  head w = [first (F) | second (E) | deep (H) | bias]   (deepfm; dnn: [H | bias])
+"""
+import math
+
+import numpy as np
+import torch
+
+from . import _lib
+from ._lib import call, ptr
+
+F32 = torch.float32
+
+
+def _ru(x, m):
+    return (x + m - 1) // m * m
+
+
+class ModelSpec:
+    """Shape/hyper-parameter description of one reference model.
+
+    model: 'deepfm_pipeline' | 'dnn_pipeline' | 'deepfm_multi_cate' | 'wdl'
+    C cont fields, V vector size, S single cate fields, E embedding size,
+    cate_index_size (reference `cate_feats_size`), hidden units, multi_ranges
+    [[start, end, name], ...] (multi-hot slots), Fw wide ids (wdl), lr, l2,
+    decay_steps/decay_rate (exponential_decay), Adam betas/eps.
+    """
+
+    def __init__(self, model, C=13, V=0, S=26, E=16, cate_index_size=1000, hidden=(400, 400, 400),
+                 multi_ranges=(), Fw=0, lr=0.001, l2=1e-5, decay_steps=10000000, decay_rate=0.9,
+                 beta1=0.9, beta2=0.999, eps=1e-8, logloss_eps=1e-7):
+        if model not in ("deepfm_pipeline", "dnn_pipeline", "deepfm_multi_cate"):
+            raise ValueError("unsupported model %r" % model)
+        self.model = model
+        self.C = 0 if model == "deepfm_multi_cate" else C
+        self.V, self.S, self.E = V, S, E
+        self.cate_index_size = cate_index_size
+        self.hidden = list(hidden)
+        self.multi_ranges = [list(r) for r in multi_ranges]
+        self.Fw = Fw
+        self.lr, self.l2 = lr, l2
+        self.decay_steps, self.decay_rate = decay_steps, decay_rate
+        self.beta1, self.beta2, self.eps, self.logloss_eps = beta1, beta2, eps, logloss_eps
+
+    @property
+    def fm(self):
+        return self.model in ("deepfm_pipeline", "deepfm_multi_cate")
+
+    @property
+    def M(self):
+        return len(self.multi_ranges)
+
+    @property
+    def multi_width(self):
+        return sum(e - s for s, e, *_ in self.multi_ranges)
+
+    @property
+    def n_rows(self):
+        return self.C + self.cate_index_size if self.model == "deepfm_pipeline" else self.cate_index_size
+
+    @property
+    def deep_in(self):
+        return self.S * self.E + self.M * self.E + self.C + self.V
+
+    @property
+    def F(self):
+        if self.model == "deepfm_pipeline":
+            return self.C + self.S
+        if self.model == "deepfm_multi_cate":
+            return self.S + self.M
+        return 0
+
+    @property
+    def fm_cols(self):
+        return self.F + self.E if self.fm else 0
+
+    @property
+    def cate_ld(self):
+        return self.S + self.multi_width
+
+    def x0_ref_rows(self):
+        """Reference row of W_0 for each internal x0 column < deep_in."""
+        S, E, M, C, V = self.S, self.E, self.M, self.C, self.V
+        if self.model == "deepfm_multi_cate":       # ref x0 = [vector, single, pooled]
+            cat = np.arange(S * E) + V
+            pool = np.arange(M * E) + V + S * E
+            vec = np.arange(V)
+            return np.concatenate([cat, pool, vec])
+        # ref x0 = [cont, vector, cat]  (deepfm_pipeline.py:123, dnn_pipeline.py:82)
+        cat = np.arange(S * E) + C + V
+        cont = np.arange(C)
+        vec = np.arange(V) + C
+        return np.concatenate([cat, cont, vec])
+
+
+class CTREngine:
+    def __init__(self, spec, max_batch, device="cuda", seed=2019, init="device"):
+        if not torch.cuda.is_available():
+            raise _lib.DLError("CTREngine needs a HIP device (no CPU fallback)")
+        _lib.lib()
+        self.spec = sp = spec
+        self.dev = torch.device(device)
+        self.B = max_batch
+        dev = self.dev
+        z = lambda *s, dt=F32: torch.zeros(*s, dtype=dt, device=dev)
+        E, S, M = sp.E, sp.S, sp.M
+        N = sp.n_rows
+        self.N = N
+        # ---- layout
+        self.cat_col = 0
+        self.pool_col = S * E
+        self.cont_col = (S + M) * E
+        self.vec_col = self.cont_col + sp.C
+        self.D0 = sp.deep_in
+        dims = [self.D0] + sp.hidden
+        self.in_ld = [_ru(d + 1, 16) for d in dims[:-1]]
+        self.out_ld = [_ru(h, 16) for h in sp.hidden]
+        self.h_ld = [_ru(h + 1, 16) for h in sp.hidden]
+        self.fm_ld = _ru(max(sp.fm_cols, 1), 4)
+        self.dx_cols = (S + M) * E
+        self.dx_ld = _ru(max(self.dx_cols, 4), 4)
+        # ---- parameters + Adam state
+        rows_pad = _ru(N, 16)
+        self.table = z(rows_pad, E)
+        self.tm, self.tv, self.tg = z(rows_pad, E), z(rows_pad, E), z(rows_pad, E)
+        self.touched = z(rows_pad, dt=torch.uint8)
+        if sp.fm:
+            self.first = z(rows_pad)
+            self.fmm, self.fmv, self.fmg = z(rows_pad), z(rows_pad), z(rows_pad)
+        else:
+            self.first = self.fmm = self.fmv = self.fmg = None
+        self.W = [z(self.in_ld[l], self.out_ld[l]) for l in range(len(sp.hidden))]
+        self.Wm = [torch.zeros_like(w) for w in self.W]
+        self.Wv = [torch.zeros_like(w) for w in self.W]
+        H = sp.hidden[-1]
+        self.head_n = sp.fm_cols + H + 1
+        self.w_head = z(_ru(self.head_n, 4))
+        self.hm, self.hv = torch.zeros_like(self.w_head), torch.zeros_like(self.w_head)
+        self.w_head_prev = torch.zeros_like(self.w_head)
+        self.opt = z(8)
+        self.opt.copy_(torch.tensor([sp.beta1, sp.beta2, sp.lr, 0.0, sp.beta1, sp.beta2, sp.eps, 0.0]))
+        self.err = z(4, dt=torch.int32)
+        # ---- activations / workspaces
+        B = max_batch
+        self.x0 = z(B, self.in_ld[0])
+        self.x0[:, self.D0] = 1.0
+        self.h = []
+        for l, hdim in enumerate(sp.hidden):
+            t = z(B, self.h_ld[l])
+            t[:, hdim] = 1.0
+            self.h.append(t)
+        self.dh = [z(B, self.h_ld[l]) for l in range(len(sp.hidden))]
+        self.dx0 = z(B, self.dx_ld)
+        self.fm_out = z(B, self.fm_ld)
+        self.fm_sum = z(B, E)
+        self.score, self.z, self.dz = z(B), z(B), z(B)
+        self.head_blocks = call_int("dl_head_grid", B)
+        self.head_slab = z(self.head_blocks, sp.fm_cols + H + 2)
+        self.splits = max(1, min(64, B // 1024))
+        self.w_slab = z(self.splits * max(i * o for i, o in zip(self.in_ld, self.out_ld)))
+        self.layout = self._layout(B)
+        self.bwd_blocks = _lib.lib().dl_embed_bwd_grid(C_ref(self.layout))
+        self.cont_slab = z(max(1, self.bwd_blocks * sp.C * (E + 1)))
+        if M:
+            self.slot_start = torch.tensor([r[0] for r in sp.multi_ranges], dtype=torch.int32, device=dev)
+            self.slot_end = torch.tensor([r[1] for r in sp.multi_ranges], dtype=torch.int32, device=dev)
+            self.cnt_emb, self.cnt_first = z(B, M), z(B, M)
+        # static input slots (graph capture reads from these)
+        self.in_label = z(B)
+        self.in_cont = z(B, max(sp.C, 1))
+        self.in_vec = z(B, max(sp.V, 1))
+        self.in_cate = z(B, max(sp.cate_ld, 1), dt=torch.int64)
+        self.graph = None
+        self.graph_batch = None
+        self.prof = None
+        self.steps = 0
+        if init == "device":
+            self.init_device(seed)
+
+    # ------------------------------------------------------------------ layout
+    def _layout(self, B):
+        sp = self.spec
+        L = _lib.EmbLayout()
+        L.n_rows = self.N
+        L.fm_cont_offset = 0
+        L.fm_cate_offset = sp.C if sp.model == "deepfm_pipeline" else 0   # deepfm_pipeline.py:89
+        L.deep_cate_offset = 0                                          # :120 raw ids
+        L.batch = B
+        L.emb_dim = sp.E
+        L.cont_fields = sp.C
+        L.vector_size = sp.V
+        L.cate_fields = sp.S
+        L.cate_ld = sp.cate_ld
+        L.fm_cont = 1 if sp.model == "deepfm_pipeline" else 0
+        L.use_fm = 1 if sp.fm else 0
+        L.fm_extra = sp.M if sp.fm else 0
+        L.zero_row0 = 1                                                 # :83-86
+        L.x0_ld = self.in_ld[0]
+        L.x0_cont_col = self.cont_col if sp.C else -1
+        L.x0_vec_col = self.vec_col if sp.V else -1
+        L.x0_cat_col = self.cat_col
+        L.x0_pool_col = self.pool_col
+        L.fm_ld = self.fm_ld
+        L.dx0_ld = self.dx_ld
+        L.dx0_cat_col = 0
+        return L
+
+    # ------------------------------------------------------------------ params
+    def init_device(self, seed):
+        """Reference initialisers (deepfm_pipeline.py:78-80,131-169): table ~ N(0, 0.01),
+        first-order ~ U[0,1), dense weights/biases ~ N(0, glorot) (numpy, seeded)."""
+        sp = self.spec
+        s = _lib.stream_handle()
+        call("dl_init_random", ptr(self.table), self.table.numel(), 0, 0.0, 0.01, seed, 0, s)
+        if self.first is not None:
+            call("dl_init_random", ptr(self.first), self.first.numel(), 1, 0.0, 1.0, seed + 1, 0, s)
+        rng = np.random.default_rng(seed)
+        dims = [self.D0] + sp.hidden
+        for l in range(len(sp.hidden)):
+            g = math.sqrt(2.0 / (dims[l] + dims[l + 1]))
+            self._set_layer(l, (rng.standard_normal((dims[l], dims[l + 1])) * g).astype(np.float32),
+                            (rng.standard_normal((1, dims[l + 1])) * g).astype(np.float32), ref_order=False)
+        H = sp.hidden[-1]
+        g = math.sqrt(2.0 / (self.head_n))
+        w = np.zeros(self.head_n, np.float32)
+        w[:-1] = rng.standard_normal(self.head_n - 1) * g
+        w[-1] = rng.standard_normal()
+        self.w_head[: self.head_n].copy_(torch.from_numpy(w))
+        torch.cuda.synchronize()
+
+    def _set_layer(self, l, W, b, ref_order=True):
+        din = W.shape[0]
+        Wi = np.zeros((self.in_ld[l], self.out_ld[l]), np.float32)
+        if l == 0 and ref_order:
+            Wi[:din, : W.shape[1]] = W[self.spec.x0_ref_rows()]
+        else:
+            Wi[:din, : W.shape[1]] = W
+        Wi[din, : W.shape[1]] = b.reshape(-1)
+        self.W[l].copy_(torch.from_numpy(Wi))
+
+    def load_params(self, P):
+        """Inject reference-layout parameters (dict of numpy arrays as in oracle/ctr_ref.py)."""
+        sp = self.spec
+        N = self.N
+        self.table.zero_()
+        self.table[:N].copy_(torch.from_numpy(np.ascontiguousarray(P["feats_emb"], np.float32)))
+        if self.first is not None:
+            self.first.zero_()
+            self.first[:N].copy_(torch.from_numpy(np.ascontiguousarray(P["fm_first_order_emb"][:, 0], np.float32)))
+        for l in range(len(sp.hidden)):
+            self._set_layer(l, P["deep_%d" % l], P["deep_bias_%d" % l])
+        if sp.fm:
+            w = np.concatenate([P["deep_fm_weight"][:, 0], P["deep_fm_bias"].reshape(-1)]).astype(np.float32)
+        else:
+            w = np.concatenate([P["deep_res"][:, 0], P["deep_res_bias"].reshape(-1)]).astype(np.float32)
+        self.w_head.zero_()
+        self.w_head[: self.head_n].copy_(torch.from_numpy(w))
+        torch.cuda.synchronize()
+
+    def params(self):
+        """Export parameters in the reference layout (numpy)."""
+        sp = self.spec
+        N = self.N
+        P = {"feats_emb": self.table[:N].cpu().numpy()}
+        if self.first is not None:
+            P["fm_first_order_emb"] = self.first[:N].cpu().numpy()[:, None]
+        dims = [self.D0] + sp.hidden
+        for l in range(len(sp.hidden)):
+            Wi = self.W[l].cpu().numpy()
+            W = Wi[: dims[l], : dims[l + 1]]
+            if l == 0:
+                Wr = np.zeros_like(W)
+                Wr[sp.x0_ref_rows()] = W
+                W = Wr
+            P["deep_%d" % l] = W.copy()
+            P["deep_bias_%d" % l] = Wi[dims[l], : dims[l + 1]][None, :].copy()
+        w = self.w_head[: self.head_n].cpu().numpy()
+        if sp.fm:
+            P["deep_fm_weight"], P["deep_fm_bias"] = w[:-1, None].copy(), w[-1:].copy()
+        else:
+            P["deep_res"], P["deep_res_bias"] = w[:-1, None].copy(), w[-1:].reshape(1, 1).copy()
+        return P
+
+    # ------------------------------------------------------------------ inputs
+    def stage(self, batch):
+        """Copy one batch (dict of tensors/arrays, reference keys) into the static slots."""
+        sp = self.spec
+        lab = _as_dev(batch["label"], F32, self.dev).reshape(-1)
+        B = lab.shape[0]
+        if B > self.B:
+            raise ValueError("batch %d > engine max_batch %d" % (B, self.B))
+        self.in_label[:B].copy_(lab)
+        if sp.C:
+            self.in_cont[:B, : sp.C].copy_(_as_dev(batch["cont_feats"], F32, self.dev))
+        if sp.V:
+            self.in_vec[:B, : sp.V].copy_(_as_dev(batch["vector_feats"], F32, self.dev))
+        self.in_cate[:B, : sp.cate_ld].copy_(_as_dev(batch["cate_feats"], torch.int64, self.dev))
+        return B
+
+    # ------------------------------------------------------------------ step
+    def _cont(self):
+        return self.in_cont if self.spec.C else None
+
+    def _c(self, label, name, *args):
+        """Launch one C-ABI entry point; with profiling on, bracket it with events
+        on the launch stream (bench.py's live per-kernel timing)."""
+        if self.prof is None:
+            return call(name, *args)
+        e0 = torch.cuda.Event(enable_timing=True)
+        e1 = torch.cuda.Event(enable_timing=True)
+        e0.record()
+        call(name, *args)
+        e1.record()
+        self.prof.append((label, e0, e1))
+
+    def _forward(self, B, s):
+        sp = self.spec
+        L = self.layout
+        L.batch = B
+        if sp.M:  # pooled vectors must be in x0 before the FM second order reads them
+            self._c("pool_fwd", "dl_pool_fwd", C_ref(L), ptr(self.table), ptr(self.first) if sp.fm else None,
+                 ptr(self.in_cate), sp.S, ptr(self.slot_start), ptr(self.slot_end), sp.M, sp.S,
+                 ptr(self.x0), ptr(self.fm_out), ptr(self.cnt_emb), ptr(self.cnt_first), ptr(self.err), s)
+        self._c("embed_fwd", "dl_embed_fwd", C_ref(L), ptr(self.table), ptr(self.first), ptr(self.in_cate),
+             ptr(self.in_cont), ptr(self.in_vec), ptr(self.x0), ptr(self.fm_out), ptr(self.fm_sum),
+             ptr(self.err), s)
+        x = self.x0
+        for l, hdim in enumerate(sp.hidden):
+            self._c("gemm_fwd_l%d" % l, "dl_gemm_f32", 0, 0, B, hdim, self.in_ld[l], ptr(x), self.in_ld[l], ptr(self.W[l]),
+                 self.out_ld[l], ptr(self.h[l]), self.h_ld[l], 1, None, 0, 1, 0, s)
+            x = self.h[l]
+        H = sp.hidden[-1]
+        self._c("head", "dl_head_fwd_bwd", B, sp.fm_cols, H, ptr(self.fm_out), self.fm_ld, ptr(self.h[-1]),
+             self.h_ld[-1], ptr(self.w_head), ptr(self.in_label), sp.logloss_eps, 1.0 / B,
+             ptr(self.score), ptr(self.z), ptr(self.dz), ptr(self.dh[-1]), ptr(self.head_slab),
+             self.head_blocks, s)
+
+    def _train(self, B):
+        sp = self.spec
+        s = _lib.stream_handle()
+        L = self.layout
+        self._c("adam_begin", "dl_adam_begin_step", ptr(self.opt), sp.decay_rate, float(sp.decay_steps), s)
+        self._forward(B, s)
+        nl = len(sp.hidden)
+        splits = max(1, min(self.splits, B // 1024))
+        for l in reversed(range(nl)):
+            xin = self.x0 if l == 0 else self.h[l - 1]
+            hdim = sp.hidden[l]
+            stride = self.in_ld[l] * self.out_ld[l]
+            self._c("gemm_dw_l%d" % l, "dl_gemm_f32", 1, 0, self.in_ld[l], hdim, B, ptr(xin), self.in_ld[l], ptr(self.dh[l]),
+                 self.h_ld[l], ptr(self.w_slab), self.out_ld[l], 3, None, 0, splits, stride, s)
+            nsplit = _num_splits(B, splits)
+            if l > 0:
+                self._c("gemm_dx_l%d" % l, "dl_gemm_f32", 0, 1, B, sp.hidden[l - 1], self.out_ld[l], ptr(self.dh[l]), self.h_ld[l],
+                     ptr(self.W[l]), self.out_ld[l], ptr(self.dh[l - 1]), self.h_ld[l - 1], 2,
+                     ptr(self.h[l - 1]), self.h_ld[l - 1], 1, 0, s)
+            else:
+                self._c("gemm_dx_l0", "dl_gemm_f32", 0, 1, B, self.dx_cols, self.out_ld[0], ptr(self.dh[0]), self.h_ld[0],
+                     ptr(self.W[0]), self.out_ld[0], ptr(self.dx0), self.dx_ld, 0, None, 0, 1, 0, s)
+            l2 = 0.0
+            self._c("adam_dense_l%d" % l, "dl_adam_dense", ptr(self.W[l]), ptr(self.Wm[l]), ptr(self.Wv[l]), ptr(self.w_slab),
+                 nsplit, stride, stride, l2, 0, ptr(self.opt), s)
+        # embedding backward (uses pre-update table and head weights)
+        bwd_blocks = call_int("dl_embed_bwd_grid", C_ref(L))
+        self._c("embed_bwd", "dl_embed_bwd", C_ref(L), ptr(self.table), ptr(self.in_cate), ptr(self._cont()), ptr(self.dz),
+             ptr(self.w_head), ptr(self.fm_sum), ptr(self.dx0), ptr(self.tg), ptr(self.fmg),
+             ptr(self.touched), ptr(self.cont_slab), self.bwd_blocks, s)
+        self._c("cont_reduce", "dl_embed_cont_reduce", C_ref(L), ptr(self.cont_slab), bwd_blocks, ptr(self.tg),
+             ptr(self.fmg), ptr(self.touched), s)
+        if sp.M:
+            self._c("pool_bwd", "dl_pool_bwd", C_ref(L), ptr(self.in_cate), sp.S, ptr(self.slot_start), ptr(self.slot_end),
+                 sp.M, sp.S, ptr(self.x0), ptr(self.fm_sum), ptr(self.dz), ptr(self.w_head), ptr(self.dx0),
+                 sp.S * sp.E, ptr(self.cnt_emb), ptr(self.cnt_first), ptr(self.tg), ptr(self.fmg),
+                 ptr(self.touched), s)
+        # head Adam: L2 on the output weights only (deepfm_pipeline.py:183 / dnn_pipeline.py:131)
+        self.w_head_prev.copy_(self.w_head)
+        H = sp.hidden[-1]
+        self._c("adam_head", "dl_adam_dense", ptr(self.w_head), ptr(self.hm), ptr(self.hv), ptr(self.head_slab),
+             call_int("dl_head_grid", B), sp.fm_cols + H + 2, self.head_n, sp.l2, self.head_n - 1,
+             ptr(self.opt), s)
+        if sp.fm:
+            self._c("adam_table", "dl_adam_rows", ptr(self.table), ptr(self.tm), ptr(self.tv), ptr(self.tg), ptr(self.touched),
+                 self.table.shape[0], sp.E, 0.0, 0, ptr(self.opt), s)
+            self._c("adam_first", "dl_adam_rows", ptr(self.first), ptr(self.fmm), ptr(self.fmv), ptr(self.fmg),
+                 ptr(self.touched), self.first.shape[0], 1, 0.0, 1, ptr(self.opt), s)
+        else:
+            self._c("adam_table", "dl_adam_rows", ptr(self.table), ptr(self.tm), ptr(self.tv), ptr(self.tg), ptr(self.touched),
+                 self.table.shape[0], sp.E, 0.0, 1, ptr(self.opt), s)
+
+    def train_step(self, batch=None, graph=False):
+        """One training step on `batch` (or on the already-staged slots if None)."""
+        B = self.stage(batch) if batch is not None else self.B
+        if graph:
+            if self.graph is None or self.graph_batch != B:
+                self._capture(B)
+            self.graph.replay()
+        else:
+            self._train(B)
+        self.steps += 1
+        self.last_batch = B
+        return B
+
+    def _capture(self, B):
+        # warm up allocations on a side stream, then capture the whole step
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, stream=s):
+            self._train(B)
+        torch.cuda.current_stream().wait_stream(s)
+        self.graph, self.graph_batch = g, B
+
+    def predict(self, batch):
+        """Forward only: returns sigmoid scores [B] (host numpy)."""
+        B = self.stage(batch)
+        s = _lib.stream_handle()
+        self._forward(B, s)
+        self.check_error()
+        return self.score[:B].cpu().numpy()
+
+    def loss(self):
+        """Loss of the last training step (data term + L2 on the pre-update head weights)."""
+        sp = self.spec
+        H = sp.hidden[-1]
+        B = self.last_batch
+        data = self.head_slab[:, sp.fm_cols + H + 1].double().sum().item() / B
+        w = self.w_head_prev[: self.head_n - 1].double()
+        return data + sp.l2 * 0.5 * float((w * w).sum().item())
+
+    def check_error(self):
+        if int(self.err[0].item()) != 0:
+            self.err.zero_()
+            raise _lib.DLError("InvalidArgumentError: categorical id out of range [0, %d)" % self.N)
+
+
+def _num_splits(K, splits):
+    kps = -(-K // splits)
+    kps = -(-kps // 16) * 16
+    return -(-K // kps)
+
+
+def call_int(name, *args):
+    return getattr(_lib.lib(), name)(*args)
+
+
+def C_ref(L):
+    import ctypes
+    return ctypes.byref(L)
+
+
+def _as_dev(x, dtype, dev):
+    if isinstance(x, torch.Tensor):
+        return x.to(device=dev, dtype=dtype, non_blocking=True)
+    return torch.from_numpy(np.ascontiguousarray(x)).to(device=dev, dtype=dtype, non_blocking=True)

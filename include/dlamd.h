@@ -1,0 +1,183 @@
+/*
+ * dlamd.h — C ABI of the MI355X-native CTR training hot path (libdlamd.so).
+ *
+ * The reference (RodJohn/deep_learning) is TensorFlow-1.x graph code: its hot
+ * path is TF's own C++ kernels behind `sess.run(op)` ("Third-party
+ * native arithmetic").  Each entry point below replaces one group of those TF
+ * ops at a reference call site (cited per function).  Host code (Python,
+ * deep_learning_amd/_lib.py) binds this header through ctypes.
+ *
+ * Conventions:
+ *   - extern "C" only; device pointers (row-major, contiguous); explicit dims.
+ *   - every call is asynchronous on the given HIP stream (`stream` is a
+ *     hipStream_t passed as void*; NULL = default stream); no allocation and no
+ *     host synchronisation inside any call, so a caller may capture a whole
+ *     training step into a hipGraph.
+ *   - return 0 on success, otherwise a nonzero code; the message is available
+ *     from dl_last_error() (thread-local).  No C++ exception crosses the ABI.
+ *   - out-of-range ids never fault: they read as zero rows and raise the
+ *     caller-provided device error word (`err`, may be NULL) which the host
+ *     turns into an exception (TF's InvalidArgumentError "indices[...] = k is
+ *     not in [0, N)").
+ */
+#ifndef DLAMD_H
+#define DLAMD_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define DL_ABI_VERSION 1
+
+int dl_abi_version(void);
+const char* dl_last_error(void);
+/* hipDeviceSynchronize + error check (host utility, never inside a step). */
+int dl_device_sync(void);
+
+/* ------------------------------------------------------------------------
+ * Embedding layout shared by the forward and backward embedding kernels.
+ * One instance describes how a model maps a batch onto the table rows:
+ *   FM fields  = [C cont fields (row fm_cont_offset+j, value cont[b][j]) if fm_cont]
+ *              + [S single cate fields (row id+fm_cate_offset, value 1)]
+ *              + [fm_extra pooled fields (vectors already in x0 at x0_pool_col,
+ *                 first-order values already in fm_out at column fm_single)]
+ *   deep input = x0[b][x0_cont_col..+C] = cont, x0[b][x0_vec_col..+V] = vector,
+ *                x0[b][x0_cat_col + f*E ..] = table[id_f + deep_cate_offset]
+ *   fm_out[b]  = [first (F = fm_single + fm_extra) | second (E)]
+ * -------------------------------------------------------------------- */
+typedef struct dl_emb_layout {
+  int64_t n_rows;           /* rows of table [n_rows, E] and first-order [n_rows]   */
+  int64_t fm_cont_offset;   /* deepfm_pipeline.py:58-61,89 (0); deepfm_multi.py:139 */
+  int64_t fm_cate_offset;   /* deepfm_pipeline.py:89 (+C)                            */
+  int64_t deep_cate_offset; /* deepfm_pipeline.py:120 (0: raw ids — ledger item 1)   */
+  int32_t batch;            /* B                                                     */
+  int32_t emb_dim;          /* E in {4, 8, 16, 32, 64}                               */
+  int32_t cont_fields;      /* C                                                     */
+  int32_t vector_size;      /* V                                                     */
+  int32_t cate_fields;      /* S single-valued ids per sample                        */
+  int32_t cate_ld;          /* int64 elements between samples in the id matrix       */
+  int32_t fm_cont;          /* 1: the C cont fields are FM fields                    */
+  int32_t use_fm;           /* 0: no FM outputs (dnn / wdl)                           */
+  int32_t fm_extra;         /* M pooled multi-hot fields appended to the FM           */
+  int32_t zero_row0;        /* 1: row 0 reads as zeros and gets no gradient (:83-86) */
+  int32_t x0_ld;            /* floats between samples in x0                          */
+  int32_t x0_cont_col;      /* -1: cont not copied into x0                           */
+  int32_t x0_vec_col;       /* -1: vector not copied into x0                         */
+  int32_t x0_cat_col;       /* column of the first single-cate embedding in x0       */
+  int32_t x0_pool_col;      /* column of the first pooled vector in x0 (fm_extra>0)  */
+  int32_t fm_ld;            /* floats between samples in fm_out                      */
+  int32_t dx0_ld;           /* floats between samples in dx0 (backward)              */
+  int32_t dx0_cat_col;      /* column of the first single-cate gradient in dx0       */
+  int32_t pad_;
+} dl_emb_layout;
+
+/* Embedding gather + FM first/second order + deep-input assembly (forward).
+ * Replaces GatherV2 x3, ConcatV2 (row-0 zero), Mul/Sum/Square/Sub at
+ * models/deepfm_pipeline.py:83-123 (also dnn_pipeline.py:72-83, wdl.py:132-179,
+ * deepfm_multi_cate.py:127-171 for the single fields).
+ * fm_sum [B, E] keeps sum_f e_f for the backward (may be NULL when !use_fm). */
+int dl_embed_fwd(const dl_emb_layout* L, const float* table, const float* first_order,
+                 const int64_t* cate, const float* cont, const float* vector,
+                 float* x0, float* fm_out, float* fm_sum, int32_t* err, void* stream);
+
+/* Backward of dl_embed_fwd for the FM (single fields) and deep lookups.
+ * dz [B] = dL/dlogit, w_head = head weights whose first F+E entries weight
+ * [first | second]; dx0 = dL/dx0.  Scatter-adds row gradients into the dense
+ * gradient tables g_table [n_rows, E], g_first [n_rows] (f32 atomics), marks
+ * touched rows in `touched` [n_rows] (uint8), and writes the hot cont-field
+ * rows as per-block partials into cont_slab [grid][C*(E+1)] which
+ * dl_embed_cont_reduce folds in.  Replaces the Gather gradients
+ * (UnsortedSegmentSum) + StridedSliceGrad of deepfm_pipeline.py:188. */
+int dl_embed_bwd(const dl_emb_layout* L, const float* table, const int64_t* cate,
+                 const float* cont, const float* dz, const float* w_head,
+                 const float* fm_sum, const float* dx0, float* g_table, float* g_first,
+                 uint8_t* touched, float* cont_slab, int32_t cont_slab_blocks, void* stream);
+int dl_embed_bwd_grid(const dl_emb_layout* L);   /* grid size = cont_slab blocks */
+int dl_embed_cont_reduce(const dl_emb_layout* L, const float* cont_slab, int32_t blocks,
+                         float* g_table, float* g_first, uint8_t* touched, void* stream);
+
+/* Multi-hot nonzero-mean pooling (deepfm_multi_cate.py:71-111).
+ * ids [B, ids_ld] int64 (padding id 0); slot m covers columns
+ * [slot_start[m], slot_end[m]) of the multi-hot block that starts at column
+ * ids_col.  Writes pooled vectors to x0[b][x0_pool_col + m*E ..], pooled
+ * first-order to fm_out[b][fm_col + m] (if first_order != NULL) and the
+ * integer counts cnt_emb / cnt_first [B, M] (float-valued, bit-exact). */
+int dl_pool_fwd(const dl_emb_layout* L, const float* table, const float* first_order,
+                const int64_t* ids, int32_t ids_col, const int32_t* slot_start,
+                const int32_t* slot_end, int32_t n_slots, int32_t fm_col, float* x0,
+                float* fm_out, float* cnt_emb, float* cnt_first, int32_t* err, void* stream);
+/* Backward of pooling: d pooled = dsecond*(fm_sum - pooled) + dx0[pool cols];
+ * each slot id gets d/cnt (div_no_nan gradient), first-order likewise. */
+int dl_pool_bwd(const dl_emb_layout* L, const int64_t* ids, int32_t ids_col,
+                const int32_t* slot_start, const int32_t* slot_end, int32_t n_slots,
+                int32_t fm_col, const float* x0, const float* fm_sum, const float* dz,
+                const float* w_head, const float* dx0, int32_t dx0_pool_col,
+                const float* cnt_emb, const float* cnt_first, float* g_table,
+                float* g_first, uint8_t* touched, void* stream);
+
+/* ------------------------------------------------------------------------
+ * Dense tower: fp32 GEMM on v_mfma_f32_16x16x4_f32 (exact fp32, k-ordered fma).
+ * C[i][j] (op) sum_r A(i,r) B(r,j); A(i,r) = ta ? A[r*lda+i] : A[i*lda+r];
+ * B(r,j) = tb ? B[j*ldb+r] : B[r*ldb+j].
+ * epi: 0 store, 1 ReLU (bias folded as a ones column), 2 multiply by
+ * (mask[i*ldm+j] > 0) (ReluGrad), 3 split-K partial slabs:
+ * C + z*c_split_stride for split z of `splits` (K chunks of a multiple of 16).
+ * Requirements: lda, ldb, ldc multiples of 4; the contiguous extent of each
+ * operand a multiple of 4 (zero padded). Replaces MatMul+Add+Relu
+ * (deepfm_pipeline.py:150-152) and their gradients. */
+int dl_gemm_f32(int32_t ta, int32_t tb, int32_t M, int32_t N, int32_t K, const float* A,
+                int32_t lda, const float* B, int32_t ldb, float* C, int32_t ldc, int32_t epi,
+                const float* mask, int32_t ldm, int32_t splits, int64_t c_split_stride,
+                void* stream);
+/* bf16 variant for the Wide&Deep tower (config C5): A, B bf16 (uint16 bits),
+ * fp32 accumulate, C fp32 or bf16 (c_bf16 = 1). Same semantics otherwise. */
+int dl_gemm_bf16(int32_t ta, int32_t tb, int32_t M, int32_t N, int32_t K, const uint16_t* A,
+                 int32_t lda, const uint16_t* B, int32_t ldb, void* C, int32_t ldc,
+                 int32_t c_bf16, int32_t epi, const void* mask, int32_t ldm, int32_t splits,
+                 int64_t c_split_stride, void* stream);
+
+/* ------------------------------------------------------------------------
+ * Output layer + sigmoid + eps-log-loss, forward and backward fused
+ * (deepfm_pipeline.py:157-183, dnn_pipeline.py:119-131):
+ * z = [fm_out(F+E) | h(H)] . w + w[F+E+H];  p = sigmoid(z);
+ * loss_b = -y ln(p+eps) - (1-y) ln(1-p+eps);  dz = (dL/dp) p (1-p) / B;
+ * dh = dz * w_h * (h > 0) written into dh [B, ldh] (cols < H);
+ * per-block partials: slab[block][0..F+E+H) = sum dz*feat, [F+E+H] = sum dz,
+ * [F+E+H+1] = sum loss_b.  `fm_cols` = F+E (0 for dnn). inv_batch = 1/B_global. */
+int dl_head_fwd_bwd(int32_t B, int32_t fm_cols, int32_t H, const float* fm_out, int32_t fm_ld,
+                    const float* h, int32_t ldh, const float* w, const float* label,
+                    float eps, float inv_batch, float* score, float* z_out, float* dz,
+                    float* dh, float* slab, int32_t slab_blocks, void* stream);
+int dl_head_grid(int32_t B);
+
+/* ------------------------------------------------------------------------
+ * TF1 Adam (training_ops.cc ApplyAdam, dense semantics: every element's m, v
+ * decay each step — SURVEY.md ledger item 6).  `opt` is a device float[8]:
+ * [0] beta1_power [1] beta2_power [2] lr [3] alpha [4] beta1 [5] beta2
+ * [6] epsilon [7] step (as float, exact < 2^24); dl_adam_begin_step computes
+ * alpha = lr_t*sqrt(1-b2p)/(1-b1p) with lr_t = lr*rate^floor(step/decay_steps)
+ * and then advances b1p*=b1, b2p*=b2, step+=1 (TF's _finish + global_step). */
+int dl_adam_begin_step(float* opt, float decay_rate, float decay_steps, void* stream);
+/* Dense parameter whose gradient is the sum of `nslab` partial slabs
+ * (g = sum_s slab[s*slab_stride + i]); l2 * p is added for i < l2_count. */
+int dl_adam_dense(float* p, float* m, float* v, const float* slab, int32_t nslab,
+                  int64_t slab_stride, int64_t n, float l2, int64_t l2_count, const float* opt,
+                  void* stream);
+/* Embedding tables with dense-Adam semantics: g = g_table row if touched else 0;
+ * consumed gradients are reset to 0; `clear_touched` resets the flags (pass 1
+ * on the last table that shares them).  width = E (table) or 1 (first-order). */
+int dl_adam_rows(float* p, float* m, float* v, float* g, uint8_t* touched, int64_t n_rows,
+                 int32_t width, float l2, int32_t clear_touched, const float* opt, void* stream);
+
+/* ------------------------------------------------------------------------
+ * Utilities. */
+/* Counter-based (Philox-4x32-10) init: dist 0 normal(mean, scale), 1 uniform[mean, mean+scale). */
+int dl_init_random(float* p, int64_t n, int32_t dist, float mean, float scale, uint64_t seed,
+                   uint64_t offset, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* DLAMD_H */

@@ -1,0 +1,158 @@
+"""Kernel-level GPU tests: each HIP entry point against an independent reference
+(torch fp64 for the GEMM, the numpy oracle for the embedding/FM/pooling math).
+Integer/index outputs (gathered rows, pooling counts) are compared bit-exact."""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+from deep_learning_amd import _lib  # noqa: E402
+from deep_learning_amd._lib import call, ptr  # noqa: E402
+
+
+def _s():
+    return _lib.stream_handle()
+
+
+@pytest.mark.parametrize("ta,tb", [(0, 0), (0, 1), (1, 0), (1, 1)])
+@pytest.mark.parametrize("M,N,K", [(300, 400, 432), (257, 416, 400), (64, 10, 16), (1000, 128, 64)])
+def test_gemm_f32_matches_fp64(hip_lib, ta, tb, M, N, K):
+    g = torch.Generator().manual_seed(M * 7 + N + K)
+    r4 = lambda x: (x + 3) // 4 * 4
+    A = torch.randn(M, K, generator=g)
+    B = torch.randn(K, N, generator=g)
+    ref = A.double() @ B.double()
+    # store in the requested orientations with padded leading dims (zero pads)
+    if ta:
+        lda = r4(M) + 4
+        Ad = torch.zeros(K, lda); Ad[:, :M] = A.t()
+    else:
+        lda = r4(K) + 4
+        Ad = torch.zeros(M, lda); Ad[:, :K] = A
+    if tb:
+        ldb = r4(K)
+        Bd = torch.zeros(N, ldb); Bd[:, :K] = B.t()
+    else:
+        ldb = r4(N)
+        Bd = torch.zeros(K, ldb); Bd[:, :N] = B
+    Ad, Bd = Ad.cuda(), Bd.cuda()
+    ldc = N + 3
+    C = torch.full((M, ldc), 7.0, device="cuda")
+    call("dl_gemm_f32", ta, tb, M, N, K, ptr(Ad), lda, ptr(Bd), ldb, ptr(C), ldc, 0, None, 0, 1, 0, _s())
+    torch.cuda.synchronize()
+    out = C[:, :N].double().cpu()
+    scale = (A.abs().double() @ B.abs().double()).clamp(min=1.0)
+    assert ((out - ref).abs() / scale).max().item() < 2e-6
+    assert (C[:, N:].cpu() == 7.0).all()   # columns >= N untouched
+
+
+def test_gemm_f32_epilogues_and_split(hip_lib):
+    g = torch.Generator().manual_seed(1)
+    M, N, K = 512, 80, 2048
+    A = torch.randn(K, M, generator=g).cuda()     # stored [r][i] (ta=1)
+    B = torch.randn(K, N, generator=g).cuda()
+    ref = (A.t().double() @ B.double()).cpu()
+    splits = 8
+    slab = torch.zeros(splits, M, N, device="cuda")
+    call("dl_gemm_f32", 1, 0, M, N, K, ptr(A), M, ptr(B), N, ptr(slab), N, 3, None, 0, splits, M * N, _s())
+    torch.cuda.synchronize()
+    assert torch.allclose(slab.double().sum(0).cpu(), ref, rtol=1e-5, atol=1e-3)
+    # relu + mask epilogues
+    X = torch.randn(M, K, generator=g).cuda()
+    C = torch.zeros(M, N, device="cuda")
+    call("dl_gemm_f32", 0, 0, M, N, K, ptr(X), K, ptr(B), N, ptr(C), N, 1, None, 0, 1, 0, _s())
+    mask = torch.randn(M, N, generator=g).cuda()
+    C2 = torch.zeros(M, N, device="cuda")
+    call("dl_gemm_f32", 0, 0, M, N, K, ptr(X), K, ptr(B), N, ptr(C2), N, 2, ptr(mask), N, 1, 0, _s())
+    torch.cuda.synchronize()
+    r = (X.double() @ B.double())
+    assert torch.allclose(C.double(), r.clamp(min=0), rtol=1e-5, atol=1e-3)
+    assert torch.allclose(C2.double(), torch.where(mask > 0, r, torch.zeros_like(r)), rtol=1e-5, atol=1e-3)
+
+
+def test_gemm_bf16(hip_lib):
+    g = torch.Generator().manual_seed(2)
+    M, N, K = 300, 200, 256
+    A = torch.randn(M, K, generator=g).bfloat16()
+    B = torch.randn(K, N, generator=g).bfloat16()
+    ref = A.double() @ B.double()
+    Ad, Bd = A.cuda(), B.cuda()
+    C = torch.zeros(M, N, device="cuda")
+    call("dl_gemm_bf16", 0, 0, M, N, K, ptr(Ad), K, ptr(Bd), N, ptr(C), N, 0, 0, None, 0, 1, 0, _s())
+    torch.cuda.synchronize()
+    assert torch.allclose(C.double().cpu(), ref, rtol=1e-4, atol=1e-3)
+
+
+def _engine(model, **kw):
+    from deep_learning_amd.engine import CTREngine, ModelSpec
+    spec = ModelSpec(model, **kw)
+    return spec, CTREngine(spec, max_batch=kw.pop("B", 256) if "B" in kw else 256, init="none")
+
+
+def test_embed_fwd_bit_exact_gather(hip_lib):
+    from deep_learning_amd.engine import CTREngine, ModelSpec
+    from deep_learning_amd.synthetic import make_batch
+    from oracle import ctr_ref as R
+    cfg = R.make_cfg("deepfm_pipeline", C=13, S=26, E=16, cate_index_size=5000, hidden=[32, 16])
+    spec = ModelSpec("deepfm_pipeline", C=13, S=26, E=16, cate_index_size=5000, hidden=[32, 16])
+    eng = CTREngine(spec, max_batch=200, init="none")
+    P = R.init_params(cfg, np.random.default_rng(0))
+    eng.load_params(P)
+    b = make_batch(200, cate_index_size=5000, seed=5)
+    b["cate_feats"][0, :3] = 0          # row-0 / cont-row collisions
+    b["cate_feats"][1, :] = np.arange(26) % 13
+    eng.stage(b)
+    eng._forward(200, _s())
+    torch.cuda.synchronize()
+    fw = R.forward(cfg, P, b)
+    x0 = eng.x0.cpu().numpy()
+    # gathered embeddings are copies: bit-exact
+    np.testing.assert_array_equal(x0[:, :26 * 16], fw["x0"][:, 13:13 + 26 * 16])
+    np.testing.assert_array_equal(x0[:, 26 * 16:26 * 16 + 13], fw["x0"][:, :13])
+    fo = eng.fm_out.cpu().numpy()
+    np.testing.assert_array_equal(fo[:, :39], fw["first"])           # single multiply: exact
+    np.testing.assert_allclose(fo[:, 39:55], fw["second"], rtol=1e-5, atol=1e-6)
+    np.testing.assert_allclose(eng.z[:200].cpu().numpy(), fw["z"], atol=1e-5)
+
+
+def test_pool_counts_bit_exact(hip_lib):
+    from deep_learning_amd.engine import CTREngine, ModelSpec
+    from deep_learning_amd.synthetic import make_batch
+    from oracle import ctr_ref as R
+    ranges = [[0, 30, "a"], [30, 90, "b"], [90, 97, "c"]]
+    cfg = R.make_cfg("deepfm_multi_cate", V=4, S=5, E=16, cate_index_size=3000, hidden=[32, 16],
+                     multi_ranges=ranges)
+    spec = ModelSpec("deepfm_multi_cate", V=4, S=5, E=16, cate_index_size=3000, hidden=[32, 16],
+                     multi_ranges=ranges)
+    eng = CTREngine(spec, max_batch=128, init="none")
+    P = R.init_params(cfg, np.random.default_rng(1))
+    P["feats_emb"][17] = 0.0            # an id whose row sums to zero: not counted
+    eng.load_params(P)
+    rng = np.random.default_rng(3)
+    b = make_batch(128, cont=0, vector=4, cate_fields=5, cate_index_size=3000, seed=9, cate_only=True)
+    multi = rng.integers(1, 3000, size=(128, 97))
+    multi[rng.random((128, 97)) < 0.5] = 0
+    multi[0] = 0
+    multi[1, :5] = 17
+    b["cate_feats"] = np.concatenate([b["cate_feats"], multi], 1)
+    eng.stage(b)
+    eng._forward(128, _s())
+    torch.cuda.synchronize()
+    fw = R.forward(cfg, P, b)
+    np.testing.assert_array_equal(eng.cnt_emb.cpu().numpy(), fw["cnt_emb"])
+    np.testing.assert_array_equal(eng.cnt_first.cpu().numpy(), fw["cnt_first"])
+    x0 = eng.x0.cpu().numpy()
+    np.testing.assert_allclose(x0[:, 80:80 + 48], fw["pooled"].reshape(128, -1), rtol=1e-6, atol=1e-7)
+    np.testing.assert_allclose(eng.z[:128].cpu().numpy(), fw["z"], atol=1e-5)
+
+
+def test_out_of_range_id_raises(hip_lib):
+    from deep_learning_amd.engine import CTREngine, ModelSpec
+    from deep_learning_amd.synthetic import make_batch
+    spec = ModelSpec("dnn_pipeline", C=13, S=26, E=8, cate_index_size=1000, hidden=[16])
+    eng = CTREngine(spec, max_batch=64)
+    b = make_batch(64, cate_index_size=1000, seed=1)
+    b["cate_feats"][3, 4] = 1000
+    with pytest.raises(_lib.DLError, match="out of range"):
+        eng.predict(b)

@@ -1,0 +1,147 @@
+"""Oracle self-checks (CPU): analytic backward vs torch autograd (fp64), TF1-Adam
+formula, AUC vs sklearn (the reference's own AUC call)."""
+import numpy as np
+import pytest
+import torch
+
+from deep_learning_amd.synthetic import make_batch
+from oracle import ctr_ref as R
+
+
+def _cfg(model):
+    if model == "deepfm_pipeline":
+        return R.make_cfg(model, C=5, S=4, E=8, cate_index_size=200, hidden=[12, 10])
+    if model == "dnn_pipeline":
+        return R.make_cfg(model, C=5, V=3, S=4, E=8, cate_index_size=200, hidden=[12, 10])
+    if model == "deepfm_multi_cate":
+        return R.make_cfg(model, C=0, V=2, S=4, E=8, cate_index_size=300, hidden=[12, 10],
+                          multi_ranges=[[0, 6, "a"], [6, 11, "b"]])
+    return R.make_cfg("wdl", C=5, S=4, E=8, cate_index_size=200, hidden=[12, 10])
+
+
+def _batch(cfg, B=16, seed=3):
+    M = len(cfg.multi_ranges)
+    if cfg.model == "deepfm_multi_cate":
+        b = make_batch(B, cont=0, vector=cfg.V, cate_fields=cfg.S, cate_index_size=cfg.cate_index_size,
+                       multi_slots=0, seed=seed, cate_only=True)
+        rng = np.random.default_rng(seed)
+        W = R.multi_width(cfg)
+        multi = rng.integers(1, cfg.cate_index_size, size=(B, W))
+        multi[rng.random((B, W)) < 0.4] = 0
+        multi[0, :] = 0  # an all-padding sample: div_no_nan path
+        b["cate_feats"] = np.concatenate([b["cate_feats"], multi], 1)
+        return b
+    b = make_batch(B, cont=cfg.C, vector=cfg.V, cate_fields=cfg.S, cate_index_size=cfg.cate_index_size,
+                   seed=seed, wide_fields=6 if cfg.model == "wdl" else 0)
+    b["cate_feats"][1, 0] = 0   # padding id hits the zeroed row
+    return b
+
+
+def _torch_loss(cfg, P, batch):
+    """Independent torch fp64 restatement used only to check the analytic grads."""
+    T = {k: torch.tensor(v, dtype=torch.float64, requires_grad=True) for k, v in P.items()}
+    E, S, C = cfg.E, cfg.S, cfg.C
+    lab = torch.tensor(batch["label"][:, 0], dtype=torch.float64)
+    B = lab.shape[0]
+    vec = torch.tensor(batch["vector_feats"], dtype=torch.float64)
+    cate = torch.tensor(batch["cate_feats"], dtype=torch.long)
+
+    def z0(t):
+        return torch.cat([torch.zeros_like(t[:1]), t[1:]], 0)
+
+    if cfg.model == "deepfm_pipeline":
+        V, w1 = z0(T["feats_emb"]), z0(T["fm_first_order_emb"])[:, 0]
+        cont = torch.tensor(batch["cont_feats"], dtype=torch.float64)
+        idx = torch.cat([torch.arange(C).repeat(B, 1), cate + C], 1)
+        val = torch.cat([cont, torch.ones(B, S, dtype=torch.float64)], 1)
+        first = w1[idx] * val
+        e = V[idx] * val[:, :, None]
+        s = e.sum(1)
+        second = 0.5 * (s * s - (e * e).sum(1))
+        x = torch.cat([cont, vec, V[cate].reshape(B, -1)], 1)
+    elif cfg.model == "dnn_pipeline":
+        V = z0(T["feats_emb"])
+        cont = torch.tensor(batch["cont_feats"], dtype=torch.float64)
+        x = torch.cat([cont, vec, V[cate].reshape(B, -1)], 1)
+    elif cfg.model == "deepfm_multi_cate":
+        V, w1 = z0(T["feats_emb"]), z0(T["fm_first_order_emb"])
+        single, multi = cate[:, :S], cate[:, S:]
+        pf, pv = [], []
+        for a, b_, _ in cfg.multi_ranges:
+            for tab, lst in ((w1, pf), (V, pv)):
+                emb = tab[multi[:, a:b_]]
+                cnt = (emb.sum(2) != 0).sum(1, keepdim=True).double()
+                s_ = emb.sum(1)
+                lst.append(torch.where(cnt > 0, s_ / torch.clamp(cnt, min=1), torch.zeros_like(s_)))
+        first = torch.cat([w1[single][:, :, 0]] + pf, 1)
+        e = torch.cat([V[single], torch.stack(pv, 1)], 1)
+        s = e.sum(1)
+        second = 0.5 * (s * s - (e * e).sum(1))
+        x = torch.cat([vec, V[single].reshape(B, -1), torch.stack(pv, 1).reshape(B, -1)], 1)
+    else:
+        V = T["weight_mat"]
+        cont = torch.tensor(batch["cont_feats"], dtype=torch.float64)
+        x = torch.cat([cont, V[cate].reshape(B, -1)], 1)
+    h = x
+    for i in range(len(cfg.hidden)):
+        h = torch.relu(h @ T["deep_%d" % i] + T["deep_bias_%d" % i])
+    if cfg.model in ("deepfm_pipeline", "deepfm_multi_cate"):
+        z = (torch.cat([first, second, h], 1) @ T["deep_fm_weight"])[:, 0] + T["deep_fm_bias"][0]
+        reg = 0.5 * (T["deep_fm_weight"] ** 2).sum()
+    elif cfg.model == "dnn_pipeline":
+        z = (h @ T["deep_res"])[:, 0] + T["deep_res_bias"][0, 0]
+        reg = 0.5 * (T["deep_res"] ** 2).sum()
+    else:
+        wide = torch.tensor(batch["wide_feats"], dtype=torch.long)
+        w = T["wdl_weights"][:, 0]
+        Fw, H = wide.shape[1], cfg.hidden[-1]
+        z = w[wide].sum(1) + (w[Fw:Fw + H][None, :] * h).sum(1) + T["wdl_bias"][0]
+        reg = 0.5 * (T["wdl_weights"] ** 2).sum() + sum(0.5 * (T["deep_%d" % i] ** 2).sum()
+                                                       for i in range(len(cfg.hidden)))
+    p = torch.sigmoid(z)
+    eps = cfg.logloss_eps
+    loss = (-lab * torch.log(p + eps) - (1 - lab) * torch.log(1 - p + eps)).mean() + cfg.l2 * reg
+    loss.backward()
+    return loss.item(), z.detach().numpy(), {k: t.grad.numpy() for k, t in T.items()}
+
+
+@pytest.mark.parametrize("model", ["deepfm_pipeline", "dnn_pipeline", "deepfm_multi_cate", "wdl"])
+def test_backward_matches_autograd(model):
+    cfg = _cfg(model)
+    P = R.init_params(cfg, np.random.default_rng(7))
+    P64 = {k: v.astype(np.float64) for k, v in P.items()}
+    batch = _batch(cfg)
+    fw = R.forward(cfg, P64, batch, dtype=np.float64)
+    G, _ = R.backward(cfg, P64, batch, fw, dtype=np.float64)
+    loss_t, z_t, G_t = _torch_loss(cfg, P, batch)
+    np.testing.assert_allclose(fw["z"], z_t, rtol=1e-10, atol=1e-12)
+    assert abs(fw["loss"] - loss_t) < 1e-10
+    for k in P:
+        np.testing.assert_allclose(G[k], G_t[k], rtol=1e-8, atol=1e-12, err_msg=k)
+
+
+def test_adam_tf1_formula():
+    cfg = R.make_cfg("dnn_pipeline")
+    P = {"w": np.array([1.0, -2.0, 0.5], np.float32)}
+    opt = R.AdamTF1(cfg, P)
+    g = {"w": np.array([0.1, 0.0, -0.3], np.float32)}
+    m = np.zeros(3); v = np.zeros(3); w = P["w"].astype(np.float64).copy()
+    for t in range(1, 4):
+        opt.apply(P, g)
+        a = 0.001 * np.sqrt(1 - 0.999 ** t) / (1 - 0.9 ** t)
+        m = m + (g["w"] - m) * 0.1
+        v = v + (g["w"] ** 2 - v) * 0.001
+        w = w - m * a / (np.sqrt(v) + 1e-8)
+    np.testing.assert_allclose(P["w"], w, rtol=1e-6)
+    assert opt.step == 3
+
+
+def test_auc_matches_sklearn():
+    from sklearn.metrics import roc_auc_score
+    rng = np.random.default_rng(0)
+    y = (rng.random(5000) < 0.3).astype(np.float32)
+    s = np.round(rng.random(5000) * 20) / 20  # heavy ties
+    assert abs(R.auc(y, s) - roc_auc_score(y, s)) < 1e-12
+    s2 = rng.random(777)
+    y2 = (rng.random(777) < s2).astype(np.float32)
+    assert abs(R.auc(y2, s2) - roc_auc_score(y2, s2)) < 1e-12
