@@ -37,98 +37,147 @@ __device__ __forceinline__ bool row_ok(int64_t row, int zero_row0) {
 
 __device__ __forceinline__ float4 f4_zero() { return make_float4(0.f, 0.f, 0.f, 0.f); }
 
-template <int E>
-__global__ __launch_bounds__(256) void embed_fwd_kernel(EmbArgs a) {
-  constexpr int LPR = E / 4;   // lanes per row
-  constexpr int RPI = 64 / LPR;  // rows per wave instruction
-  const dl_emb_layout& L = a.L;
-  const int lane = threadIdx.x & 63;
-  const int r = lane / LPR, q = lane % LPR;
-  const int wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-  const int nwaves = (gridDim.x * blockDim.x) >> 6;
-  const int Cf = L.fm_cont ? L.cont_fields : 0;
-  const int S = L.cate_fields;
-  const int Fs = Cf + S;
-  const int F = Fs + L.fm_extra;
-  const float4* tab4 = reinterpret_cast<const float4*>(a.table);
+constexpr int kMaxHotContFwd = 32;
 
-  for (int b = wave; b < L.batch; b += nwaves) {
-    const int64_t* ids = a.cate + (int64_t)b * L.cate_ld;
-    const float* cb = a.cont + (int64_t)b * L.cont_fields;
-    float* xb = a.x0 + (int64_t)b * L.x0_ld;
-    if (L.use_fm) {
-      float4 s = f4_zero(), ss = f4_zero();
-      for (int f0 = 0; f0 < Fs; f0 += RPI) {
-        const int f = f0 + r;
-        if (f < Fs) {
-          int64_t row;
-          float val;
-          if (f < Cf) {
-            row = L.fm_cont_offset + f;
-            val = cb[f];
-          } else {
-            row = checked_row(ids[f - Cf], L.fm_cate_offset, L.n_rows, a.err);
-            val = 1.f;
+constexpr int kTileSamples = 16;   // samples staged per block iteration
+constexpr int kMaxSlots = 128;     // FM slots + deep slots per sample
+
+template <int E, int NPS>
+__global__ __launch_bounds__(256) void embed_fwd_kernel(EmbArgs a) {
+  // Per block iteration a tile of 16 samples is staged: every (sample, slot)
+  // row index is resolved once into LDS by a coalesced pass over the id matrix
+  // (slot = FM field f < Fs, or deep field Fs + f).  Each wave then owns 4
+  // samples; for a sample it issues ALL its row loads back to back (packed
+  // slots, E/4 lanes per row, float4 per lane) before consuming any, so a wave
+  // keeps a whole sample's rows in flight.  Masked slots read row 0 and are
+  // zeroed by select, never by a branch around the load.
+  constexpr int LPR = E / 4;
+  constexpr int RPI = 64 / LPR;
+  __shared__ int rows_s[kTileSamples][kMaxSlots];
+  __shared__ float vals_s[kTileSamples][kMaxHotContFwd];
+  const dl_emb_layout& L = a.L;
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int r = lane / LPR, q = lane % LPR;
+  const int Cf = (L.use_fm && L.fm_cont) ? L.cont_fields : 0;
+  const int S = L.cate_fields;
+  const int Fs = L.use_fm ? Cf + S : 0;
+  const int F = Fs + L.fm_extra;
+  const int nslot = Fs + S;
+  const float4* tab4 = reinterpret_cast<const float4*>(a.table);
+  const float4 z4 = f4_zero();
+  const int ntiles = (L.batch + kTileSamples - 1) / kTileSamples;
+
+  for (int t = blockIdx.x; t < ntiles; t += gridDim.x) {
+    const int b0 = t * kTileSamples;
+    const int nb = min(kTileSamples, L.batch - b0);
+    // stage row indices: one id feeds its FM slot (Cf + f) and its deep slot (Fs + f).
+    // Loads are unconditional (clamped index) so all of a thread's id loads are in flight together.
+    {
+      const int tot = nb * S;
+      for (int k0 = 0; k0 < tot; k0 += 4 * 256) {
+        int64_t idv[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          int k = k0 + threadIdx.x + u * 256;
+          k = k < tot ? k : tot - 1;
+          idv[u] = a.cate[(int64_t)(b0 + k / S) * L.cate_ld + k % S];
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const int k = k0 + threadIdx.x + u * 256;
+          if (k < tot) {
+            const int j = k / S, f = k % S;
+            const int dr = (int)checked_row(idv[u], L.deep_cate_offset, L.n_rows, a.err);
+            rows_s[j][Fs + f] = row_ok(dr, L.zero_row0) ? dr : -1;
+            if (L.use_fm) {
+              const int fr = (int)checked_row(idv[u], L.fm_cate_offset, L.n_rows, a.err);
+              rows_s[j][Cf + f] = row_ok(fr, L.zero_row0) ? fr : -1;
+            }
           }
-          float4 e = f4_zero();
-          if (row_ok(row, L.zero_row0)) e = tab4[row * LPR + q];
-          e.x *= val; e.y *= val; e.z *= val; e.w *= val;
-          s.x += e.x; s.y += e.y; s.z += e.z; s.w += e.w;
-          ss.x += e.x * e.x; ss.y += e.y * e.y; ss.z += e.z * e.z; ss.w += e.w * e.w;
         }
       }
-      for (int f0 = 0; f0 < L.fm_extra; f0 += RPI) {
-        const int f = f0 + r;
-        if (f < L.fm_extra) {
-          const float4 e = *reinterpret_cast<const float4*>(xb + L.x0_pool_col + f * E + 4 * q);
-          s.x += e.x; s.y += e.y; s.z += e.z; s.w += e.w;
-          ss.x += e.x * e.x; ss.y += e.y * e.y; ss.z += e.z * e.z; ss.w += e.w * e.w;
-        }
+      for (int k = threadIdx.x; k < nb * Cf; k += blockDim.x) {
+        const int row = (int)(L.fm_cont_offset + k % Cf);
+        rows_s[k / Cf][k % Cf] = row_ok(row, L.zero_row0) ? row : -1;
+      }
+    }
+    for (int k = threadIdx.x; k < nb * Cf; k += blockDim.x)
+      vals_s[k / Cf][k % Cf] = a.cont[(int64_t)(b0 + k / Cf) * L.cont_fields + k % Cf];
+    __syncthreads();
+    for (int j = wid; j < nb; j += 4) {
+      const int b = b0 + j;
+      float* xb = a.x0 + (int64_t)b * L.x0_ld;
+      float4 v[NPS];
+      int rw[NPS];
+#pragma unroll
+      for (int p = 0; p < NPS; ++p) {
+        const int sl = p * RPI + r;
+        rw[p] = rows_s[j][sl < nslot ? sl : 0];
+        if (sl >= nslot) rw[p] = -1;
       }
 #pragma unroll
-      for (int o = LPR; o < 64; o <<= 1) {
-        s.x += __shfl_xor(s.x, o, 64); s.y += __shfl_xor(s.y, o, 64);
-        s.z += __shfl_xor(s.z, o, 64); s.w += __shfl_xor(s.w, o, 64);
-        ss.x += __shfl_xor(ss.x, o, 64); ss.y += __shfl_xor(ss.y, o, 64);
-        ss.z += __shfl_xor(ss.z, o, 64); ss.w += __shfl_xor(ss.w, o, 64);
+      for (int p = 0; p < NPS; ++p) v[p] = tab4[(rw[p] < 0 ? 0 : rw[p]) * LPR + q];
+      // first-order terms (one lane per FM field)
+      float w1 = 0.f, val = 0.f;
+      int frow = -1;
+      if (lane < Fs) {
+        frow = rows_s[j][lane];
+        val = lane < Cf ? vals_s[j][lane] : 1.f;
+        w1 = a.first_order[frow < 0 ? 0 : frow];
       }
-      if (r == 0) {
-        float4 sec;
-        sec.x = 0.5f * (s.x * s.x - ss.x); sec.y = 0.5f * (s.y * s.y - ss.y);
-        sec.z = 0.5f * (s.z * s.z - ss.z); sec.w = 0.5f * (s.w * s.w - ss.w);
-        float* fo = a.fm_out + (int64_t)b * L.fm_ld + F + 4 * q;
-        fo[0] = sec.x; fo[1] = sec.y; fo[2] = sec.z; fo[3] = sec.w;
-        if (a.fm_sum) *reinterpret_cast<float4*>(a.fm_sum + (int64_t)b * E + 4 * q) = s;
-      }
-      for (int f = lane; f < Fs; f += 64) {
-        int64_t row;
-        float val;
-        if (f < Cf) {
-          row = L.fm_cont_offset + f;
-          val = cb[f];
-        } else {
-          row = checked_row(ids[f - Cf], L.fm_cate_offset, L.n_rows, a.err);
-          val = 1.f;
+      float4 s = z4, ss = z4;
+#pragma unroll
+      for (int p = 0; p < NPS; ++p) {
+        {
+          const int sl = p * RPI + r;
+          const float4 t4 = rw[p] < 0 ? z4 : v[p];
+          if (sl < Fs) {
+            const float vv = sl < Cf ? vals_s[j][sl] : 1.f;
+            const float4 ev = make_float4(t4.x * vv, t4.y * vv, t4.z * vv, t4.w * vv);
+            s.x += ev.x; s.y += ev.y; s.z += ev.z; s.w += ev.w;
+            ss.x += ev.x * ev.x; ss.y += ev.y * ev.y; ss.z += ev.z * ev.z; ss.w += ev.w * ev.w;
+          } else if (sl < nslot) {
+            *reinterpret_cast<float4*>(xb + L.x0_cat_col + (sl - Fs) * E + 4 * q) = t4;
+          }
         }
-        const float w = row_ok(row, L.zero_row0) ? a.first_order[row] : 0.f;
-        a.fm_out[(int64_t)b * L.fm_ld + f] = w * val;
       }
-    }
-    // deep lookups: x0[b][cat_col + f*E ..] = table'[id_f + deep_off]
-    for (int f0 = 0; f0 < S; f0 += RPI) {
-      const int f = f0 + r;
-      if (f < S) {
-        const int64_t row = checked_row(ids[f], L.deep_cate_offset, L.n_rows, a.err);
-        float4 e = f4_zero();
-        if (row_ok(row, L.zero_row0)) e = tab4[row * LPR + q];
-        *reinterpret_cast<float4*>(xb + L.x0_cat_col + f * E + 4 * q) = e;
+      if (lane < Fs) a.fm_out[(int64_t)b * L.fm_ld + lane] = frow < 0 ? 0.f : w1 * val;
+      for (int f = 64 + lane; f < Fs; f += 64) {   // > 64 FM fields (rare)
+        const int fr = rows_s[j][f];
+        const float vv = f < Cf ? vals_s[j][f] : 1.f;
+        a.fm_out[(int64_t)b * L.fm_ld + f] = fr < 0 ? 0.f : a.first_order[fr] * vv;
       }
+      if (L.use_fm) {
+        for (int f0 = 0; f0 < L.fm_extra; f0 += RPI) {
+          const int f = f0 + r;
+          if (f < L.fm_extra) {
+            const float4 ev = *reinterpret_cast<const float4*>(xb + L.x0_pool_col + f * E + 4 * q);
+            s.x += ev.x; s.y += ev.y; s.z += ev.z; s.w += ev.w;
+            ss.x += ev.x * ev.x; ss.y += ev.y * ev.y; ss.z += ev.z * ev.z; ss.w += ev.w * ev.w;
+          }
+        }
+#pragma unroll
+        for (int o = LPR; o < 64; o <<= 1) {
+          s.x += __shfl_xor(s.x, o, 64); s.y += __shfl_xor(s.y, o, 64);
+          s.z += __shfl_xor(s.z, o, 64); s.w += __shfl_xor(s.w, o, 64);
+          ss.x += __shfl_xor(ss.x, o, 64); ss.y += __shfl_xor(ss.y, o, 64);
+          ss.z += __shfl_xor(ss.z, o, 64); ss.w += __shfl_xor(ss.w, o, 64);
+        }
+        if (r == 0) {
+          float* fo = a.fm_out + (int64_t)b * L.fm_ld + F + 4 * q;
+          fo[0] = 0.5f * (s.x * s.x - ss.x); fo[1] = 0.5f * (s.y * s.y - ss.y);
+          fo[2] = 0.5f * (s.z * s.z - ss.z); fo[3] = 0.5f * (s.w * s.w - ss.w);
+          if (a.fm_sum) *reinterpret_cast<float4*>(a.fm_sum + (int64_t)b * E + 4 * q) = s;
+        }
+      }
+      if (L.x0_cont_col >= 0)
+        for (int jj = lane; jj < L.cont_fields; jj += 64)
+          xb[L.x0_cont_col + jj] = a.cont[(int64_t)b * L.cont_fields + jj];
+      if (L.x0_vec_col >= 0)
+        for (int jj = lane; jj < L.vector_size; jj += 64)
+          xb[L.x0_vec_col + jj] = a.vec[(int64_t)b * L.vector_size + jj];
     }
-    if (L.x0_cont_col >= 0)
-      for (int j = lane; j < L.cont_fields; j += 64) xb[L.x0_cont_col + j] = cb[j];
-    if (L.x0_vec_col >= 0)
-      for (int j = lane; j < L.vector_size; j += 64)
-        xb[L.x0_vec_col + j] = a.vec[(int64_t)b * L.vector_size + j];
+    __syncthreads();
   }
 }
 
@@ -458,8 +507,34 @@ extern "C" int dl_embed_fwd(const dl_emb_layout* L, const float* table, const fl
   DL_CHECK_ARG(!L->use_fm || (first_order && fm_out && fm_sum), "FM outputs required");
   if (L->batch == 0) return 0;
   EmbArgs a{*L, table, first_order, cate, cont, vector, x0, fm_out, fm_sum, err};
-  DL_DISPATCH_E(L->emb_dim, hipLaunchKernelGGL(embed_fwd_kernel<kE>, dim3(emb_grid(L->batch)),
-                                               dim3(256), 0, as_stream(stream), a));
+  DL_CHECK_ARG((L->use_fm ? (L->fm_cont ? L->cont_fields : 0) + 2 * L->cate_fields : L->cate_fields) <= kMaxSlots,
+               "too many fields per sample for the gather kernel (max %d slots)", kMaxSlots);
+  const int tiles = (L->batch + kTileSamples - 1) / kTileSamples;
+  const dim3 grid(tiles < 8192 ? tiles : 8192), block(256);
+  const int nslot = (L->use_fm ? (L->fm_cont ? L->cont_fields : 0) + L->cate_fields : 0) + L->cate_fields;
+  const int rpi = 64 / (L->emb_dim / 4);
+  const int nps = (nslot + rpi - 1) / rpi;
+  hipStream_t st = as_stream(stream);
+#define DL_FWD(E_, N_) hipLaunchKernelGGL((embed_fwd_kernel<E_, N_>), grid, block, 0, st, a)
+  switch (L->emb_dim) {
+    case 16:
+      switch (nps) {
+        case 1: DL_FWD(16, 1); break; case 2: DL_FWD(16, 2); break; case 3: DL_FWD(16, 3); break;
+        case 4: DL_FWD(16, 4); break; case 5: DL_FWD(16, 5); break; case 6: DL_FWD(16, 6); break;
+        case 7: DL_FWD(16, 7); break; default: DL_FWD(16, 8); break;
+      }
+      break;
+    case 8:
+      switch (nps) {
+        case 1: DL_FWD(8, 1); break; case 2: DL_FWD(8, 2); break; case 3: DL_FWD(8, 3); break;
+        default: DL_FWD(8, 4); break;
+      }
+      break;
+    case 4: DL_FWD(4, 2); break;
+    case 32: DL_FWD(32, 16); break;
+    case 64: DL_FWD(64, 32); break;
+  }
+#undef DL_FWD
   DL_RETURN_LAUNCH("dl_embed_fwd");
 }
 
