@@ -198,7 +198,7 @@ struct EmbBwdArgs {
 
 constexpr int kMaxHotCont = 32;  // cont fields kept in registers on the backward
 
-template <int E>
+template <int E, bool CONT_ONLY>
 __global__ __launch_bounds__(256) void embed_bwd_kernel(EmbBwdArgs a) {
   constexpr int RPI = 64 / E;  // rows per wave instruction (lane = dim)
   constexpr int NCP = (kMaxHotCont + RPI - 1) / RPI;
@@ -237,7 +237,7 @@ __global__ __launch_bounds__(256) void embed_bwd_kernel(EmbBwdArgs a) {
         }
       }
       // single cate FM fields: scatter-add
-      for (int f0 = 0; f0 < S; f0 += RPI) {
+      for (int f0 = 0; f0 < (CONT_ONLY ? 0 : S); f0 += RPI) {
         const int f = f0 + r;
         if (f < S) {
           const int64_t row = ids[f] + L.fm_cate_offset;
@@ -251,7 +251,7 @@ __global__ __launch_bounds__(256) void embed_bwd_kernel(EmbBwdArgs a) {
       for (int f = lane; f < Fs; f += 64) {
         if (f < Cf) {
           g1c += dzb * a.w_head[f] * cb[f];
-        } else {
+        } else if (!CONT_ONLY) {
           const int64_t row = ids[f - Cf] + L.fm_cate_offset;
           if (row < L.n_rows && row_ok(row, L.zero_row0)) {
             atomicAdd(a.g_first + row, dzb * a.w_head[f]);
@@ -260,6 +260,7 @@ __global__ __launch_bounds__(256) void embed_bwd_kernel(EmbBwdArgs a) {
         }
       }
     }
+    if (CONT_ONLY) continue;
     // deep lookups
     const float* gx = a.dx0 + (int64_t)b * L.dx0_ld + L.dx0_cat_col;
     for (int f0 = 0; f0 < S; f0 += RPI) {
@@ -552,7 +553,7 @@ extern "C" int dl_embed_bwd(const dl_emb_layout* L, const float* table, const in
   DL_CHECK_ARG(!hot || (cont_slab && cont_slab_blocks >= grid), "cont_slab needs %d blocks", grid);
   DL_CHECK_ARG(!L->use_fm || (dz && w_head && fm_sum && g_first), "FM backward inputs required");
   EmbBwdArgs a{*L, table, cate, cont, dz, w_head, fm_sum, dx0, g_table, g_first, touched, cont_slab};
-  DL_DISPATCH_E(L->emb_dim, hipLaunchKernelGGL(embed_bwd_kernel<kE>, dim3(grid), dim3(256), 0,
+  DL_DISPATCH_E(L->emb_dim, hipLaunchKernelGGL((embed_bwd_kernel<kE, false>), dim3(grid), dim3(256), 0,
                                                as_stream(stream), a));
   DL_RETURN_LAUNCH("dl_embed_bwd");
 }
@@ -596,4 +597,122 @@ extern "C" int dl_pool_bwd(const dl_emb_layout* L, const int64_t* ids, int32_t i
   DL_DISPATCH_E(L->emb_dim, hipLaunchKernelGGL(pool_bwd_kernel<kE>, dim3(emb_grid(L->batch)),
                                                dim3(256), 0, as_stream(stream), a));
   DL_RETURN_LAUNCH("dl_pool_bwd");
+}
+
+// ---------------------------------------------------------------------------
+// Deterministic backward from the batch index (index.hip): one group of E lanes
+// per unique row sums its references in sorted order.  For FM references
+//   d/dV[row] = dsec_b * (fm_sum_b - V[row])   (d second / d e_f, value 1)
+// so a row's FM part is  sum_b dsec_b*fm_sum_b - V[row] * sum_b dsec_b.
+
+namespace dl {
+
+struct BwdSortedArgs {
+  dl_emb_layout L;
+  const float* table;      // local table (single GPU) or NULL
+  const float* rows_u;     // gathered rows per unique id [u][E] (sharded) or NULL
+  const uint32_t* uniq;
+  const int32_t* seg_off;
+  const int32_t* n_uniq;
+  const int32_t* refs;
+  int world;
+  const float* dz;
+  const float* w_head;
+  const float* fm_sum;
+  const float* dx0;
+  float* g_out;
+  float* g1_out;
+  uint8_t* touched;
+  int compact;
+};
+
+__device__ __forceinline__ int64_t decode_key(uint32_t k, int world) {
+  const uint32_t owner = k >> 27, local = k & ((1u << 27) - 1);
+  return owner >= (uint32_t)world ? (int64_t)local : (int64_t)local * world + owner;
+}
+
+template <int E>
+__global__ __launch_bounds__(256) void embed_bwd_sorted_kernel(BwdSortedArgs a) {
+  constexpr int RPI = 64 / E;
+  const dl_emb_layout& L = a.L;
+  const int lane = threadIdx.x & 63;
+  const int r = lane / E, d = lane % E;
+  const int S = L.cate_fields;
+  const int ns = (L.use_fm ? S : 0) + S;
+  const int Cf = (L.use_fm && L.fm_cont) ? L.cont_fields : 0;
+  const int F = Cf + S + L.fm_extra;
+  const int nu = a.n_uniq[0];
+  const long long group = ((long long)blockIdx.x * blockDim.x + threadIdx.x) / 64 * RPI + r;
+  const long long ngroups = (long long)gridDim.x * blockDim.x / 64 * RPI;
+  const float wsec = L.use_fm ? a.w_head[F + d] : 0.f;
+  for (long long u = group; u < nu; u += ngroups) {
+    const int e0 = a.seg_off[u], e1 = a.seg_off[u + 1];
+    float acc_s = 0.f, acc_d = 0.f, acc_x = 0.f, g1 = 0.f;
+    for (int e = e0; e < e1; ++e) {
+      const int k = a.refs[e];
+      const int b = k / ns, sl = k % ns;
+      if (L.use_fm && sl < S) {
+        const float dzb = a.dz[b];
+        const float ds = dzb * wsec;
+        acc_s += ds * a.fm_sum[(long long)b * E + d];
+        acc_d += ds;
+        g1 += dzb * a.w_head[Cf + sl];
+      } else {
+        const int f = L.use_fm ? sl - S : sl;
+        acc_x += a.dx0[(long long)b * L.dx0_ld + L.dx0_cat_col + f * E + d];
+      }
+    }
+    const uint32_t key = a.uniq[u];
+    const int64_t row = decode_key(key, a.world);
+    float v = 0.f;
+    if (acc_d != 0.f) v = a.rows_u ? a.rows_u[u * E + d] : a.table[row * E + d];
+    const float g = acc_s - v * acc_d + acc_x;
+    if (a.compact) {
+      a.g_out[u * E + d] = g;
+      if (a.g1_out && d == 0) a.g1_out[u] = g1;
+    } else {
+      a.g_out[row * E + d] = g;
+      if (d == 0) {
+        if (a.g1_out && L.use_fm) a.g1_out[row] = g1;
+        a.touched[row] = 1;
+      }
+    }
+  }
+}
+
+}  // namespace dl
+
+extern "C" int dl_embed_bwd_sorted(const dl_emb_layout* L, const float* table, const float* rows_u,
+                                   const uint32_t* uniq_keys, const int32_t* seg_off, const int32_t* n_uniq,
+                                   const int32_t* sorted_refs, int32_t world, int64_t max_uniq,
+                                   const float* dz, const float* w_head, const float* fm_sum,
+                                   const float* dx0, float* g_out, float* g1_out, uint8_t* touched,
+                                   int32_t compact, void* stream) {
+  if (int rc = check_layout(L)) return rc;
+  DL_CHECK_ARG(uniq_keys && seg_off && n_uniq && sorted_refs && dx0 && g_out, "NULL argument");
+  DL_CHECK_ARG(table || rows_u, "need the table or the gathered rows");
+  DL_CHECK_ARG(compact || touched, "dense output needs the touched flags");
+  DL_CHECK_ARG(!L->use_fm || (dz && w_head && fm_sum), "FM backward inputs required");
+  if (max_uniq <= 0) return 0;
+  const int rpi = 64 / L->emb_dim;
+  long long blocks = (max_uniq + 4 * rpi - 1) / (4 * rpi);
+  if (blocks > 8192) blocks = 8192;
+  BwdSortedArgs a{*L, table, rows_u, uniq_keys, seg_off, n_uniq, sorted_refs, world, dz, w_head, fm_sum, dx0,
+                  g_out, g1_out, touched, compact};
+  DL_DISPATCH_E(L->emb_dim, hipLaunchKernelGGL(embed_bwd_sorted_kernel<kE>, dim3((unsigned)blocks), dim3(256), 0,
+                                               as_stream(stream), a));
+  DL_RETURN_LAUNCH("dl_embed_bwd_sorted");
+}
+
+extern "C" int dl_embed_cont_bwd(const dl_emb_layout* L, const float* table, const float* cont,
+                                 const float* dz, const float* w_head, const float* fm_sum, float* cont_slab,
+                                 int32_t cont_slab_blocks, void* stream) {
+  if (int rc = check_layout(L)) return rc;
+  if (L->batch == 0 || !(L->use_fm && L->fm_cont && L->cont_fields > 0)) return 0;
+  const int grid = dl_embed_bwd_grid(L);
+  DL_CHECK_ARG(cont_slab && cont_slab_blocks >= grid, "cont_slab needs %d blocks", grid);
+  EmbBwdArgs a{*L, table, nullptr, cont, dz, w_head, fm_sum, nullptr, nullptr, nullptr, nullptr, cont_slab};
+  DL_DISPATCH_E(L->emb_dim, hipLaunchKernelGGL((embed_bwd_kernel<kE, true>), dim3(grid), dim3(256), 0,
+                                               as_stream(stream), a));
+  DL_RETURN_LAUNCH("dl_embed_cont_bwd");
 }

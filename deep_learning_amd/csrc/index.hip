@@ -1,0 +1,164 @@
+// Reference index of one batch: every (sample, slot) table reference sorted by
+// row, deduplicated into unique rows with segment offsets and an inverse map.
+//
+// Uses: (1) a deterministic, atomic-free embedding backward — each unique row's
+// gradient is the ordered sum over its segment (replaces the Gather gradient
+// UnsortedSegmentSum of deepfm_pipeline.py:188); (2) the row-sharded multi-GPU
+// lookup: unique rows grouped by owner rank form the
+// all-to-all send lists, the inverse map expands received rows back to slots.
+//
+// Key of a reference to row r (owner = r % world, local = r / world):
+//   (owner << 27) | local     (replicated rows r < replicated_below: owner = world)
+// so a sort by key groups rows by owner, then by local row.  Invalid refs
+// (row 0 under the zero-row rule, out-of-range ids) get key 0xFFFFFFFF and sort last.
+#include <hipcub/hipcub.hpp>
+
+#include "common.h"
+
+namespace dl {
+
+constexpr uint32_t kInvalidKey = 0xFFFFFFFFu;
+constexpr int kLocalBits = 27;
+
+__device__ __forceinline__ bool row_ok_i(int64_t row, int zero_row0) {
+  return row > 0 || (row == 0 && !zero_row0);
+}
+
+__global__ __launch_bounds__(256) void make_refs_kernel(dl_emb_layout L, const int64_t* __restrict__ cate, int world,
+                                                        int rep_below, uint32_t* __restrict__ keys,
+                                                        int32_t* __restrict__ refs, int32_t* err) {
+  const int S = L.cate_fields;
+  const int ns = (L.use_fm ? S : 0) + S;
+  const long long n = (long long)L.batch * ns;
+  for (long long k = (long long)blockIdx.x * blockDim.x + threadIdx.x; k < n; k += (long long)gridDim.x * blockDim.x) {
+    const int b = (int)(k / ns), s = (int)(k % ns);
+    int64_t row;
+    if (L.use_fm && s < S) row = cate[(long long)b * L.cate_ld + s] + L.fm_cate_offset;
+    else row = cate[(long long)b * L.cate_ld + (L.use_fm ? s - S : s)] + L.deep_cate_offset;
+    uint32_t key = kInvalidKey;
+    if (row < 0 || row >= L.n_rows) {
+      if (err) atomicOr(err, 1);
+    } else if (row_ok_i(row, L.zero_row0)) {
+      if (row < rep_below) key = ((uint32_t)world << kLocalBits) | (uint32_t)row;
+      else key = ((uint32_t)(row % world) << kLocalBits) | (uint32_t)(row / world);
+    }
+    keys[k] = key;
+    refs[k] = (int32_t)k;
+  }
+}
+
+__global__ __launch_bounds__(256) void head_flags_kernel(const uint32_t* __restrict__ keys, int n, int32_t* __restrict__ flags) {
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    const uint32_t k = keys[i];
+    flags[i] = (k != kInvalidKey && (i == 0 || keys[i - 1] != k)) ? 1 : 0;
+  }
+}
+
+__global__ __launch_bounds__(256) void scatter_index_kernel(const uint32_t* __restrict__ keys, const int32_t* __restrict__ refs,
+                                                            const int32_t* __restrict__ uid1, int n, int world,
+                                                            uint32_t* __restrict__ uniq, int32_t* __restrict__ seg_off,
+                                                            int32_t* __restrict__ n_uniq, int32_t* __restrict__ inv,
+                                                            int32_t* __restrict__ owner_counts) {
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    const uint32_t k = keys[i];
+    if (k == kInvalidKey) {
+      if (inv) inv[refs[i]] = -1;
+      continue;
+    }
+    const int u = uid1[i] - 1;
+    const bool head = (i == 0 || keys[i - 1] != k);
+    if (head) {
+      uniq[u] = k;
+      seg_off[u] = i;
+      if (owner_counts) atomicAdd(owner_counts + (k >> kLocalBits), 1);
+    }
+    if (i + 1 == n || keys[i + 1] == kInvalidKey) {
+      seg_off[u + 1] = i + 1;
+      n_uniq[0] = u + 1;
+    }
+    if (inv) inv[refs[i]] = u;
+  }
+}
+
+struct IndexWs {
+  uint32_t* keys_in;
+  int32_t* refs_in;
+  int32_t* flags;
+  int32_t* uid1;
+  void* temp;
+  size_t temp_bytes;
+};
+
+static size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
+
+static size_t cub_temp_bytes(int n) {
+  size_t a = 0, b = 0;
+  hipcub::DeviceRadixSort::SortPairs(nullptr, a, (uint32_t*)nullptr, (uint32_t*)nullptr, (int32_t*)nullptr,
+                                     (int32_t*)nullptr, n, 0, 32);
+  hipcub::DeviceScan::InclusiveSum(nullptr, b, (int32_t*)nullptr, (int32_t*)nullptr, n);
+  return a > b ? a : b;
+}
+
+static IndexWs carve(void* ws, int n) {
+  char* p = reinterpret_cast<char*>(ws);
+  IndexWs w;
+  w.keys_in = reinterpret_cast<uint32_t*>(p); p += align256((size_t)n * 4);
+  w.refs_in = reinterpret_cast<int32_t*>(p); p += align256((size_t)n * 4);
+  w.flags = reinterpret_cast<int32_t*>(p); p += align256((size_t)n * 4);
+  w.uid1 = reinterpret_cast<int32_t*>(p); p += align256((size_t)n * 4);
+  w.temp = p;
+  w.temp_bytes = cub_temp_bytes(n);
+  return w;
+}
+
+}  // namespace dl
+
+using namespace dl;
+
+extern "C" int64_t dl_index_workspace_bytes(int64_t n_refs) {
+  if (n_refs <= 0 || n_refs > (1LL << 30)) return -1;
+  const int n = (int)n_refs;
+  return (int64_t)(4 * align256((size_t)n * 4) + align256(cub_temp_bytes(n)));
+}
+
+extern "C" int dl_index_build(const dl_emb_layout* L, const int64_t* cate, int32_t world,
+                              int32_t replicated_below, void* ws, int64_t ws_bytes,
+                              uint32_t* sorted_keys, int32_t* sorted_refs, uint32_t* uniq_keys,
+                              int32_t* seg_off, int32_t* n_uniq, int32_t* inv, int32_t* owner_counts,
+                              int32_t* err, void* stream) {
+  DL_CHECK_ARG(L && cate && ws && sorted_keys && sorted_refs && uniq_keys && seg_off && n_uniq, "NULL argument");
+  DL_CHECK_ARG(world >= 1 && world < 32, "world %d out of range", world);
+  DL_CHECK_ARG(L->n_rows / world < (1LL << kLocalBits), "too many rows per shard for the 27-bit local key");
+  const int S = L->cate_fields;
+  const long long n_ll = (long long)L->batch * ((L->use_fm ? S : 0) + S);
+  DL_CHECK_ARG(n_ll < (1LL << 30), "too many references");
+  const int n = (int)n_ll;
+  DL_CHECK_ARG(ws_bytes >= dl_index_workspace_bytes(n > 0 ? n : 1), "workspace too small");
+  hipStream_t s = as_stream(stream);
+  if (hipMemsetAsync(n_uniq, 0, sizeof(int32_t), s) != hipSuccess ||
+      hipMemsetAsync(seg_off, 0, sizeof(int32_t), s) != hipSuccess ||
+      (owner_counts && hipMemsetAsync(owner_counts, 0, sizeof(int32_t) * (world + 1), s) != hipSuccess)) {
+    set_error("dl_index_build: memset failed");
+    return 1;
+  }
+  if (n == 0) return 0;
+  IndexWs w = carve(ws, n);
+  const int grid = (int)((n + 255) / 256 < 8192 ? (n + 255) / 256 : 8192);
+  hipLaunchKernelGGL(make_refs_kernel, dim3(grid), dim3(256), 0, s, *L, cate, world, replicated_below, w.keys_in,
+                     w.refs_in, err);
+  size_t tb = w.temp_bytes;
+  if (hipcub::DeviceRadixSort::SortPairs(w.temp, tb, w.keys_in, sorted_keys, w.refs_in, sorted_refs, n, 0, 32, s) !=
+      hipSuccess) {
+    set_error("dl_index_build: radix sort failed");
+    return 2;
+  }
+  hipLaunchKernelGGL(head_flags_kernel, dim3(grid), dim3(256), 0, s, sorted_keys, n, w.flags);
+  tb = w.temp_bytes;
+  if (hipcub::DeviceScan::InclusiveSum(w.temp, tb, w.flags, w.uid1, n, s) != hipSuccess) {
+    set_error("dl_index_build: scan failed");
+    return 3;
+  }
+  hipLaunchKernelGGL(scatter_index_kernel, dim3(grid), dim3(256), 0, s, sorted_keys, sorted_refs, w.uid1, n, world,
+                     uniq_keys, seg_off, n_uniq, inv, owner_counts);
+  DL_RETURN_LAUNCH("dl_index_build");
+}

@@ -112,7 +112,7 @@ class ModelSpec:
 
 
 class CTREngine:
-    def __init__(self, spec, max_batch, device="cuda", seed=2019, init="device"):
+    def __init__(self, spec, max_batch, device="cuda", seed=2019, init="device", bwd="sorted"):
         if not torch.cuda.is_available():
             raise _lib.DLError("CTREngine needs a HIP device (no CPU fallback)")
         _lib.lib()
@@ -183,6 +183,18 @@ class CTREngine:
             self.slot_start = torch.tensor([r[0] for r in sp.multi_ranges], dtype=torch.int32, device=dev)
             self.slot_end = torch.tensor([r[1] for r in sp.multi_ranges], dtype=torch.int32, device=dev)
             self.cnt_emb, self.cnt_first = z(B, M), z(B, M)
+        # batch reference index (deterministic backward)
+        self.bwd = bwd
+        self.n_slot = (S if sp.fm else 0) + S
+        self.n_refs = B * self.n_slot
+        if bwd == "sorted":
+            wsb = _lib.lib().dl_index_workspace_bytes(max(1, self.n_refs))
+            self.idx_ws = z(wsb, dt=torch.uint8)
+            self.idx_keys = z(self.n_refs, dt=torch.int32)
+            self.idx_refs = z(self.n_refs, dt=torch.int32)
+            self.idx_uniq = z(self.n_refs, dt=torch.int32)
+            self.idx_off = z(self.n_refs + 1, dt=torch.int32)
+            self.idx_n = z(4, dt=torch.int32)
         # static input slots (graph capture reads from these)
         self.in_label = z(B)
         self.in_cont = z(B, max(sp.C, 1))
@@ -380,11 +392,22 @@ class CTREngine:
                  nsplit, stride, stride, l2, 0, ptr(self.opt), s)
         # embedding backward (uses pre-update table and head weights)
         bwd_blocks = call_int("dl_embed_bwd_grid", C_ref(L))
-        self._c("embed_bwd", "dl_embed_bwd", C_ref(L), ptr(self.table), ptr(self.in_cate), ptr(self._cont()), ptr(self.dz),
-             ptr(self.w_head), ptr(self.fm_sum), ptr(self.dx0), ptr(self.tg), ptr(self.fmg),
-             ptr(self.touched), ptr(self.cont_slab), self.bwd_blocks, s)
+        if self.bwd == "sorted":
+            self._c("index_build", "dl_index_build", C_ref(L), ptr(self.in_cate), 1, 0, ptr(self.idx_ws),
+                    self.idx_ws.numel(), ptr(self.idx_keys), ptr(self.idx_refs), ptr(self.idx_uniq),
+                    ptr(self.idx_off), ptr(self.idx_n), None, None, ptr(self.err), s)
+            self._c("embed_bwd", "dl_embed_bwd_sorted", C_ref(L), ptr(self.table), None, ptr(self.idx_uniq),
+                    ptr(self.idx_off), ptr(self.idx_n), ptr(self.idx_refs), 1, B * self.n_slot, ptr(self.dz),
+                    ptr(self.w_head), ptr(self.fm_sum), ptr(self.dx0), ptr(self.tg), ptr(self.fmg),
+                    ptr(self.touched), 0, s)
+            self._c("cont_bwd", "dl_embed_cont_bwd", C_ref(L), ptr(self.table), ptr(self._cont()), ptr(self.dz),
+                    ptr(self.w_head), ptr(self.fm_sum), ptr(self.cont_slab), self.bwd_blocks, s)
+        else:
+            self._c("embed_bwd", "dl_embed_bwd", C_ref(L), ptr(self.table), ptr(self.in_cate), ptr(self._cont()),
+                    ptr(self.dz), ptr(self.w_head), ptr(self.fm_sum), ptr(self.dx0), ptr(self.tg), ptr(self.fmg),
+                    ptr(self.touched), ptr(self.cont_slab), self.bwd_blocks, s)
         self._c("cont_reduce", "dl_embed_cont_reduce", C_ref(L), ptr(self.cont_slab), bwd_blocks, ptr(self.tg),
-             ptr(self.fmg), ptr(self.touched), s)
+                ptr(self.fmg), ptr(self.touched), s)
         if sp.M:
             self._c("pool_bwd", "dl_pool_bwd", C_ref(L), ptr(self.in_cate), sp.S, ptr(self.slot_start), ptr(self.slot_end),
                  sp.M, sp.S, ptr(self.x0), ptr(self.fm_sum), ptr(self.dz), ptr(self.w_head), ptr(self.dx0),

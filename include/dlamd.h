@@ -98,6 +98,38 @@ int dl_embed_bwd_grid(const dl_emb_layout* L);   /* grid size = cont_slab blocks
 int dl_embed_cont_reduce(const dl_emb_layout* L, const float* cont_slab, int32_t blocks,
                          float* g_table, float* g_first, uint8_t* touched, void* stream);
 
+/* Hot cont-field rows only (the FM cont part of dl_embed_bwd): per-block
+ * partials into cont_slab, folded in by dl_embed_cont_reduce. */
+int dl_embed_cont_bwd(const dl_emb_layout* L, const float* table, const float* cont,
+                      const float* dz, const float* w_head, const float* fm_sum, float* cont_slab,
+                      int32_t cont_slab_blocks, void* stream);
+
+/* Batch reference index (index.hip): every (sample, slot) reference — slots are
+ * the S FM cate fields (if use_fm) then the S deep fields — keyed by
+ * (owner << 27 | local) with owner = row % world, local = row / world (rows below
+ * replicated_below: owner = world, local = row); sorted (radix), deduplicated:
+ * uniq_keys[0..n_uniq), segment offsets seg_off[0..n_uniq] into sorted_refs
+ * (ref = b * n_slot + slot), inverse map inv[ref] -> unique id (-1 invalid; may be
+ * NULL), owner_counts[world+1] unique rows per owner (may be NULL).
+ * Invalid refs (row 0 under zero_row0, out-of-range -> err) are excluded. */
+int64_t dl_index_workspace_bytes(int64_t n_refs);
+int dl_index_build(const dl_emb_layout* L, const int64_t* cate, int32_t world,
+                   int32_t replicated_below, void* ws, int64_t ws_bytes, uint32_t* sorted_keys,
+                   int32_t* sorted_refs, uint32_t* uniq_keys, int32_t* seg_off, int32_t* n_uniq,
+                   int32_t* inv, int32_t* owner_counts, int32_t* err, void* stream);
+/* Deterministic (atomic-free) embedding backward over the index: each unique
+ * row's gradient is the ordered sum of its references.  compact=0: plain stores
+ * into the dense gradient tables g_out [n_rows, E] / g1_out [n_rows] + touched
+ * flags (single GPU); compact=1: g_out [u][E], g1_out [u] per unique id (the
+ * sharded path sends these to the owners).  rows_u: gathered rows per unique id
+ * (sharded) or NULL to read `table`. */
+int dl_embed_bwd_sorted(const dl_emb_layout* L, const float* table, const float* rows_u,
+                        const uint32_t* uniq_keys, const int32_t* seg_off, const int32_t* n_uniq,
+                        const int32_t* sorted_refs, int32_t world, int64_t max_uniq,
+                        const float* dz, const float* w_head, const float* fm_sum,
+                        const float* dx0, float* g_out, float* g1_out, uint8_t* touched,
+                        int32_t compact, void* stream);
+
 /* Multi-hot nonzero-mean pooling (deepfm_multi_cate.py:71-111).
  * ids [B, ids_ld] int64 (padding id 0); slot m covers columns
  * [slot_start[m], slot_end[m]) of the multi-hot block that starts at column

@@ -156,3 +156,68 @@ def test_out_of_range_id_raises(hip_lib):
     b["cate_feats"][3, 4] = 1000
     with pytest.raises(_lib.DLError, match="out of range"):
         eng.predict(b)
+
+
+def test_index_build_matches_numpy(hip_lib):
+    """Sort/dedup/inverse map: bit-exact against numpy (unique rows, segment
+    boundaries, per-owner counts) for a sharded key encoding."""
+    from deep_learning_amd.engine import CTREngine, ModelSpec
+    from deep_learning_amd.synthetic import make_batch
+    B, world, C = 300, 4, 13
+    spec = ModelSpec("deepfm_pipeline", C=C, S=26, E=16, cate_index_size=2000, hidden=[16])
+    eng = CTREngine(spec, max_batch=B, init="none")
+    b = make_batch(B, cate_index_size=2000, seed=4)
+    b["cate_feats"][0, :5] = [0, 0, 3, 3, 1999]
+    eng.stage(b)
+    L = eng.layout
+    L.batch = B
+    import ctypes
+    n = B * 52
+    ws = torch.zeros(hip_lib.dl_index_workspace_bytes(n), dtype=torch.uint8, device="cuda")
+    keys = torch.zeros(n, dtype=torch.int32, device="cuda")
+    refs = torch.zeros(n, dtype=torch.int32, device="cuda")
+    uniq = torch.zeros(n, dtype=torch.int32, device="cuda")
+    off = torch.zeros(n + 1, dtype=torch.int32, device="cuda")
+    nu = torch.zeros(1, dtype=torch.int32, device="cuda")
+    inv = torch.zeros(n, dtype=torch.int32, device="cuda")
+    oc = torch.zeros(world + 1, dtype=torch.int32, device="cuda")
+    call("dl_index_build", ctypes.byref(L), ptr(eng.in_cate), world, C, ptr(ws), ws.numel(), ptr(keys), ptr(refs),
+         ptr(uniq), ptr(off), ptr(nu), ptr(inv), ptr(oc), ptr(eng.err), _s())
+    torch.cuda.synchronize()
+    cate = b["cate_feats"].astype(np.int64)
+    rows = np.concatenate([cate + C, cate], 1).reshape(-1)          # FM slots then deep slots
+    ref_rows = np.concatenate([cate[:, :, None] + C, cate[:, :, None]], 2)  # not used: order check below
+    rows = np.concatenate([cate + C, cate], 1)                       # [B, 52]
+    flat = rows.reshape(-1)
+    valid = flat > 0
+    own = np.where(flat < C, world, flat % world)
+    loc = np.where(flat < C, flat, flat // world)
+    key = (own.astype(np.uint64) << 27) | loc.astype(np.uint64)
+    key = np.where(valid, key, 0xFFFFFFFF)
+    u_ref, cnt_ref = np.unique(key[valid], return_counts=True)
+    nuv = int(nu.item())
+    assert nuv == len(u_ref)
+    got_u = uniq[:nuv].cpu().numpy().astype(np.uint32).astype(np.uint64)
+    np.testing.assert_array_equal(got_u, u_ref)
+    np.testing.assert_array_equal(np.diff(off[:nuv + 1].cpu().numpy()), cnt_ref)
+    invc = inv.cpu().numpy()
+    np.testing.assert_array_equal(invc[~valid], -1)
+    np.testing.assert_array_equal(u_ref[invc[valid]], key[valid])
+    own_u = (u_ref >> 27).astype(np.int64)
+    np.testing.assert_array_equal(oc.cpu().numpy(), np.bincount(own_u, minlength=world + 1))
+
+
+@pytest.mark.parametrize("model", ["deepfm_pipeline", "dnn_pipeline"])
+def test_sorted_backward_equals_atomic(hip_lib, model):
+    from deep_learning_amd.engine import CTREngine, ModelSpec
+    from deep_learning_amd.synthetic import make_batch
+    spec = ModelSpec(model, C=13, V=0, S=26, E=16, cate_index_size=3000, hidden=[32, 16])
+    outs = []
+    for mode in ("atomic", "sorted"):
+        eng = CTREngine(spec, max_batch=700, seed=3, bwd=mode)
+        for i in range(3):
+            eng.train_step(make_batch(700, cate_index_size=3000, seed=20 + i))
+        torch.cuda.synchronize()
+        outs.append(eng.params())
+    for k in outs[0]:
+        np.testing.assert_allclose(outs[0][k], outs[1][k], atol=2e-6, rtol=0, err_msg=k)
