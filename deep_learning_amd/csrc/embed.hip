@@ -20,6 +20,8 @@ namespace dl {
 
 struct EmbArgs {
   dl_emb_layout L;
+  const int32_t* inv;      // indexed mode (sharded): row of a reference = inv_base + inv[ref]
+  int inv_base;
   const float* table;
   const float* first_order;
   const int64_t* cate;
@@ -74,24 +76,39 @@ __global__ __launch_bounds__(256) void embed_fwd_kernel(EmbArgs a) {
     // Loads are unconditional (clamped index) so all of a thread's id loads are in flight together.
     {
       const int tot = nb * S;
-      for (int k0 = 0; k0 < tot; k0 += 4 * 256) {
-        int64_t idv[4];
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-          int k = k0 + threadIdx.x + u * 256;
-          k = k < tot ? k : tot - 1;
-          idv[u] = a.cate[(int64_t)(b0 + k / S) * L.cate_ld + k % S];
+      if (a.inv) {
+        // sharded: rows were exchanged per unique reference; ref = b * ns + slot
+        const int ns = (L.use_fm ? S : 0) + S;
+        for (int k = threadIdx.x; k < tot; k += blockDim.x) {
+          const int j = k / S, f = k % S;
+          const int64_t rb = (int64_t)(b0 + j) * ns;
+          const int di = a.inv[rb + (L.use_fm ? S : 0) + f];
+          rows_s[j][Fs + f] = di < 0 ? -1 : a.inv_base + di;
+          if (L.use_fm) {
+            const int fi = a.inv[rb + f];
+            rows_s[j][Cf + f] = fi < 0 ? -1 : a.inv_base + fi;
+          }
         }
+      } else {
+        for (int k0 = 0; k0 < tot; k0 += 4 * 256) {
+          int64_t idv[4];
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
-          const int k = k0 + threadIdx.x + u * 256;
-          if (k < tot) {
-            const int j = k / S, f = k % S;
-            const int dr = (int)checked_row(idv[u], L.deep_cate_offset, L.n_rows, a.err);
-            rows_s[j][Fs + f] = row_ok(dr, L.zero_row0) ? dr : -1;
-            if (L.use_fm) {
-              const int fr = (int)checked_row(idv[u], L.fm_cate_offset, L.n_rows, a.err);
-              rows_s[j][Cf + f] = row_ok(fr, L.zero_row0) ? fr : -1;
+          for (int u = 0; u < 4; ++u) {
+            int k = k0 + threadIdx.x + u * 256;
+            k = k < tot ? k : tot - 1;
+            idv[u] = a.cate[(int64_t)(b0 + k / S) * L.cate_ld + k % S];
+          }
+#pragma unroll
+          for (int u = 0; u < 4; ++u) {
+            const int k = k0 + threadIdx.x + u * 256;
+            if (k < tot) {
+              const int j = k / S, f = k % S;
+              const int dr = (int)checked_row(idv[u], L.deep_cate_offset, L.n_rows, a.err);
+              rows_s[j][Fs + f] = row_ok(dr, L.zero_row0) ? dr : -1;
+              if (L.use_fm) {
+                const int fr = (int)checked_row(idv[u], L.fm_cate_offset, L.n_rows, a.err);
+                rows_s[j][Cf + f] = row_ok(fr, L.zero_row0) ? fr : -1;
+              }
             }
           }
         }
@@ -500,6 +517,8 @@ using namespace dl;
     case 64: { constexpr int kE = 64; __VA_ARGS__; break; } \
   }
 
+static int launch_embed_fwd(const dl_emb_layout* L, const EmbArgs& a, void* stream);
+
 extern "C" int dl_embed_fwd(const dl_emb_layout* L, const float* table, const float* first_order,
                             const int64_t* cate, const float* cont, const float* vector,
                             float* x0, float* fm_out, float* fm_sum, int32_t* err, void* stream) {
@@ -507,7 +526,22 @@ extern "C" int dl_embed_fwd(const dl_emb_layout* L, const float* table, const fl
   DL_CHECK_ARG(table && cate && x0, "NULL table/cate/x0");
   DL_CHECK_ARG(!L->use_fm || (first_order && fm_out && fm_sum), "FM outputs required");
   if (L->batch == 0) return 0;
-  EmbArgs a{*L, table, first_order, cate, cont, vector, x0, fm_out, fm_sum, err};
+  EmbArgs a{*L, nullptr, 0, table, first_order, cate, cont, vector, x0, fm_out, fm_sum, err};
+  return launch_embed_fwd(L, a, stream);
+}
+
+extern "C" int dl_embed_fwd_indexed(const dl_emb_layout* L, const float* rows, const float* rows_first,
+                                    const int32_t* inv, int32_t inv_base, const float* cont, const float* vector,
+                                    float* x0, float* fm_out, float* fm_sum, void* stream) {
+  if (int rc = check_layout(L)) return rc;
+  DL_CHECK_ARG(rows && inv && x0, "NULL rows/inv/x0");
+  DL_CHECK_ARG(!L->use_fm || (rows_first && fm_out && fm_sum), "FM outputs required");
+  if (L->batch == 0) return 0;
+  EmbArgs a{*L, inv, inv_base, rows, rows_first, nullptr, cont, vector, x0, fm_out, fm_sum, nullptr};
+  return launch_embed_fwd(L, a, stream);
+}
+
+static int launch_embed_fwd(const dl_emb_layout* L, const EmbArgs& a, void* stream) {
   DL_CHECK_ARG((L->use_fm ? (L->fm_cont ? L->cont_fields : 0) + 2 * L->cate_fields : L->cate_fields) <= kMaxSlots,
                "too many fields per sample for the gather kernel (max %d slots)", kMaxSlots);
   const int tiles = (L->batch + kTileSamples - 1) / kTileSamples;

@@ -1,0 +1,107 @@
+// Row-sharded embedding tables across GPUs: owner-side
+// gather / scatter-add of exchanged rows and the dense-gradient slab reducer.
+//
+// Row r of the logical table lives on rank r % world at local row r / world
+// (cyclic: Zipf-hot low ids spread over all ranks); rows below `replicated`
+// (the deepfm_pipeline cont-field rows hit by every sample) are replicated and
+// their gradients all-reduced with the dense parameters.
+#include "common.h"
+
+namespace dl {
+
+// out[i] = table[ids[i]] (E floats), out1[i] = first[ids[i]]; E/4 lanes per row.
+__global__ __launch_bounds__(256) void shard_gather_kernel(const float4* __restrict__ table, const float* __restrict__ first,
+                                                           const int32_t* __restrict__ ids, long long n, int lpr,
+                                                           float4* __restrict__ out, float* __restrict__ out1) {
+  const long long total = n * lpr;
+  for (long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x; t < total; t += (long long)gridDim.x * blockDim.x) {
+    const long long i = t / lpr;
+    const int q = (int)(t % lpr);
+    const int r = ids[i];
+    out[t] = table[(long long)r * lpr + q];
+    if (first && q == 0) out1[i] = first[r];
+  }
+}
+
+// G[ids[i]] += g[i], G1[ids[i]] += g1[i]; duplicates across peers -> f32 atomics.
+__global__ __launch_bounds__(256) void shard_scatter_kernel(const float* __restrict__ g, const float* __restrict__ g1,
+                                                            const int32_t* __restrict__ ids, long long n, int E,
+                                                            float* __restrict__ G, float* __restrict__ G1,
+                                                            uint8_t* __restrict__ touched) {
+  const long long total = n * E;
+  for (long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x; t < total; t += (long long)gridDim.x * blockDim.x) {
+    const long long i = t / E;
+    const int d = (int)(t % E);
+    const int r = ids[i];
+    atomicAdd(G + (long long)r * E + d, g[t]);
+    if (d == 0) {
+      if (g1 && G1) atomicAdd(G1 + r, g1[i]);
+      touched[r] = 1;
+    }
+  }
+}
+
+// out[i] = sum_s slab[s*stride + i]
+__global__ __launch_bounds__(256) void slab_sum_kernel(const float* __restrict__ slab, int nslab, long long stride,
+                                                       long long n, float* __restrict__ out) {
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x) {
+    float g = 0.f;
+    for (int s = 0; s < nslab; ++s) g += slab[s * stride + i];
+    out[i] = g;
+  }
+}
+
+// local row of each unique key (key & (2^27-1)); the send list of the id exchange
+__global__ void keys_to_local_kernel(const uint32_t* __restrict__ keys, const int32_t* __restrict__ n_uniq,
+                                     long long cap, int32_t* __restrict__ out) {
+  const long long nu = n_uniq[0];
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < nu && i < cap;
+       i += (long long)gridDim.x * blockDim.x)
+    out[i] = (int32_t)(keys[i] & ((1u << 27) - 1));
+}
+
+static int grid_of(long long n) {
+  long long g = (n + 255) / 256;
+  if (g > 8192) g = 8192;
+  return g < 1 ? 1 : (int)g;
+}
+
+}  // namespace dl
+
+using namespace dl;
+
+extern "C" int dl_shard_gather(const float* table, const float* first, const int32_t* ids, int64_t n,
+                               int32_t emb_dim, float* out, float* out_first, void* stream) {
+  DL_CHECK_ARG(table && ids && out && emb_dim % 4 == 0, "bad args");
+  DL_CHECK_ARG(!first || out_first, "out_first required");
+  if (n <= 0) return 0;
+  hipLaunchKernelGGL(shard_gather_kernel, dim3(grid_of(n * (emb_dim / 4))), dim3(256), 0, as_stream(stream),
+                     (const float4*)table, first, ids, (long long)n, emb_dim / 4, (float4*)out, out_first);
+  DL_RETURN_LAUNCH("dl_shard_gather");
+}
+
+extern "C" int dl_shard_scatter_add(const float* g, const float* g_first, const int32_t* ids, int64_t n,
+                                    int32_t emb_dim, float* G, float* G_first, uint8_t* touched, void* stream) {
+  DL_CHECK_ARG(g && ids && G && touched, "bad args");
+  if (n <= 0) return 0;
+  hipLaunchKernelGGL(shard_scatter_kernel, dim3(grid_of(n * emb_dim)), dim3(256), 0, as_stream(stream), g, g_first,
+                     ids, (long long)n, emb_dim, G, G_first, touched);
+  DL_RETURN_LAUNCH("dl_shard_scatter_add");
+}
+
+extern "C" int dl_slab_sum(const float* slab, int32_t nslab, int64_t stride, int64_t n, float* out, void* stream) {
+  DL_CHECK_ARG(slab && out && nslab >= 1 && stride >= n, "bad args");
+  if (n <= 0) return 0;
+  hipLaunchKernelGGL(slab_sum_kernel, dim3(grid_of(n)), dim3(256), 0, as_stream(stream), slab, nslab,
+                     (long long)stride, (long long)n, out);
+  DL_RETURN_LAUNCH("dl_slab_sum");
+}
+
+extern "C" int dl_keys_to_local(const uint32_t* keys, const int32_t* n_uniq, int64_t cap, int32_t* out,
+                                void* stream) {
+  DL_CHECK_ARG(keys && n_uniq && out, "bad args");
+  if (cap <= 0) return 0;
+  hipLaunchKernelGGL(keys_to_local_kernel, dim3(grid_of(cap)), dim3(256), 0, as_stream(stream), keys, n_uniq,
+                     (long long)cap, out);
+  DL_RETURN_LAUNCH("dl_keys_to_local");
+}

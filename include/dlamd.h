@@ -98,6 +98,15 @@ int dl_embed_bwd_grid(const dl_emb_layout* L);   /* grid size = cont_slab blocks
 int dl_embed_cont_reduce(const dl_emb_layout* L, const float* cont_slab, int32_t blocks,
                          float* g_table, float* g_first, uint8_t* touched, void* stream);
 
+/* Indexed forward (row-sharded tables): the row of reference ref = b*n_slot + slot
+ * (index order of dl_index_build) is inv_base + inv[ref] in `rows` / `rows_first`
+ * (the rows exchanged for this batch; rows below inv_base hold the replicated
+ * cont-field rows read by the FM cont fields). */
+int dl_embed_fwd_indexed(const dl_emb_layout* L, const float* rows, const float* rows_first,
+                         const int32_t* inv, int32_t inv_base, const float* cont,
+                         const float* vector, float* x0, float* fm_out, float* fm_sum,
+                         void* stream);
+
 /* Hot cont-field rows only (the FM cont part of dl_embed_bwd): per-block
  * partials into cont_slab, folded in by dl_embed_cont_reduce. */
 int dl_embed_cont_bwd(const dl_emb_layout* L, const float* table, const float* cont,
@@ -202,6 +211,21 @@ int dl_adam_dense(float* p, float* m, float* v, const float* slab, int32_t nslab
  * on the last table that shares them).  width = E (table) or 1 (first-order). */
 int dl_adam_rows(float* p, float* m, float* v, float* g, uint8_t* touched, int64_t n_rows,
                  int32_t width, float l2, int32_t clear_touched, const float* opt, void* stream);
+
+/* ------------------------------------------------------------------------
+ * Row-sharded tables (shard.hip).  Owner side of the all-to-all lookup:
+ * out[i] = table[ids[i]], out_first[i] = first[ids[i]] (first may be NULL);
+ * and of the gradient return: G[ids[i]] += g[i] (f32 atomics: a row may come
+ * from several peers), touched[ids[i]] = 1. */
+int dl_shard_gather(const float* table, const float* first, const int32_t* ids, int64_t n,
+                    int32_t emb_dim, float* out, float* out_first, void* stream);
+int dl_shard_scatter_add(const float* g, const float* g_first, const int32_t* ids, int64_t n,
+                         int32_t emb_dim, float* G, float* G_first, uint8_t* touched, void* stream);
+/* out[i] = sum_s slab[s*stride + i] (dense gradients before the all-reduce). */
+int dl_slab_sum(const float* slab, int32_t nslab, int64_t stride, int64_t n, float* out, void* stream);
+/* out[i] = local row of uniq key i (i < min(n_uniq, cap)): the id send list. */
+int dl_keys_to_local(const uint32_t* keys, const int32_t* n_uniq, int64_t cap, int32_t* out,
+                     void* stream);
 
 /* ------------------------------------------------------------------------
  * Utilities. */
