@@ -675,15 +675,20 @@ __global__ __launch_bounds__(256) void embed_bwd_sorted_kernel(BwdSortedArgs a) 
   const int ns = (L.use_fm ? S : 0) + S;
   const int Cf = (L.use_fm && L.fm_cont) ? L.cont_fields : 0;
   const int F = Cf + S + L.fm_extra;
-  const int nu = a.n_uniq[0];
+  // every index derived from another kernel's output is clamped: a stale or
+  // racing index can cost accuracy, never an out-of-bounds access
+  const long long nrefs = (long long)L.batch * ns;
+  int nu = a.n_uniq[0];
+  nu = nu < 0 ? 0 : (nu > nrefs ? (int)nrefs : nu);
   const long long group = ((long long)blockIdx.x * blockDim.x + threadIdx.x) / 64 * RPI + r;
   const long long ngroups = (long long)gridDim.x * blockDim.x / 64 * RPI;
   const float wsec = L.use_fm ? a.w_head[F + d] : 0.f;
   for (long long u = group; u < nu; u += ngroups) {
-    const int e0 = a.seg_off[u], e1 = a.seg_off[u + 1];
+    const int e0 = max(0, a.seg_off[u]), e1 = min((int)nrefs, a.seg_off[u + 1]);
     float acc_s = 0.f, acc_d = 0.f, acc_x = 0.f, g1 = 0.f;
     for (int e = e0; e < e1; ++e) {
       const int k = a.refs[e];
+      if (k < 0 || k >= nrefs) continue;
       const int b = k / ns, sl = k % ns;
       if (L.use_fm && sl < S) {
         const float dzb = a.dz[b];
@@ -698,6 +703,7 @@ __global__ __launch_bounds__(256) void embed_bwd_sorted_kernel(BwdSortedArgs a) 
     }
     const uint32_t key = a.uniq[u];
     const int64_t row = decode_key(key, a.world);
+    if (row < 0 || row >= L.n_rows) continue;
     float v = 0.f;
     if (acc_d != 0.f) v = a.rows_u ? a.rows_u[u * E + d] : a.table[row * E + d];
     const float g = acc_s - v * acc_d + acc_x;

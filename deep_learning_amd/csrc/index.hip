@@ -80,6 +80,13 @@ __global__ __launch_bounds__(256) void scatter_index_kernel(const uint32_t* __re
   }
 }
 
+__global__ void index_init_kernel(int32_t* n_uniq, int32_t* seg_off, int32_t* owner_counts, int n_owner) {
+  const int t = threadIdx.x;
+  if (t == 0) { n_uniq[0] = 0; seg_off[0] = 0; }
+  if (owner_counts)
+    for (int i = t; i < n_owner; i += blockDim.x) owner_counts[i] = 0;
+}
+
 struct IndexWs {
   uint32_t* keys_in;
   int32_t* refs_in;
@@ -135,12 +142,8 @@ extern "C" int dl_index_build(const dl_emb_layout* L, const int64_t* cate, int32
   const int n = (int)n_ll;
   DL_CHECK_ARG(ws_bytes >= dl_index_workspace_bytes(n > 0 ? n : 1), "workspace too small");
   hipStream_t s = as_stream(stream);
-  if (hipMemsetAsync(n_uniq, 0, sizeof(int32_t), s) != hipSuccess ||
-      hipMemsetAsync(seg_off, 0, sizeof(int32_t), s) != hipSuccess ||
-      (owner_counts && hipMemsetAsync(owner_counts, 0, sizeof(int32_t) * (world + 1), s) != hipSuccess)) {
-    set_error("dl_index_build: memset failed");
-    return 1;
-  }
+  // zeroing by a kernel (not a memset node): keeps every node of a captured step a kernel
+  hipLaunchKernelGGL(index_init_kernel, dim3(1), dim3(64), 0, s, n_uniq, seg_off, owner_counts, world + 1);
   if (n == 0) return 0;
   IndexWs w = carve(ws, n);
   const int grid = (int)((n + 255) / 256 < 8192 ? (n + 255) / 256 : 8192);

@@ -36,7 +36,8 @@ __global__ __launch_bounds__(256) void adam_dense_thread_kernel(float* __restric
                                                                 float* __restrict__ v,
                                                                 const float* __restrict__ slab, int nslab,
                                                                 long long stride, long long n, float l2,
-                                                                long long l2_count, const float* __restrict__ opt) {
+                                                                long long l2_count, const float* __restrict__ opt,
+                                                                float* __restrict__ p_prev) {
   const float alpha = opt[3], omb1 = 1.f - opt[4], omb2 = 1.f - opt[5], eps = opt[6];
   for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n;
        i += (long long)gridDim.x * blockDim.x) {
@@ -49,6 +50,7 @@ __global__ __launch_bounds__(256) void adam_dense_thread_kernel(float* __restric
     }
     for (; s < nslab; ++s) g += slab[s * stride + i];
     float pi = p[i], mi = m[i], vi = v[i];
+    if (p_prev) p_prev[i] = pi;
     if (i < l2_count) g += l2 * pi;
     adam_elem(pi, mi, vi, g, alpha, omb1, omb2, eps);
     p[i] = pi; m[i] = mi; v[i] = vi;
@@ -60,7 +62,8 @@ __global__ __launch_bounds__(256) void adam_dense_wave_kernel(float* __restrict_
                                                               float* __restrict__ v,
                                                               const float* __restrict__ slab, int nslab,
                                                               long long stride, long long n, float l2,
-                                                              long long l2_count, const float* __restrict__ opt) {
+                                                              long long l2_count, const float* __restrict__ opt,
+                                                              float* __restrict__ p_prev) {
   const long long i = ((long long)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   const int lane = threadIdx.x & 63;
   if (i >= n) return;
@@ -69,6 +72,7 @@ __global__ __launch_bounds__(256) void adam_dense_wave_kernel(float* __restrict_
   g = wave_sum(g);
   if (lane == 0) {
     float pi = p[i], mi = m[i], vi = v[i];
+    if (p_prev) p_prev[i] = pi;
     if (i < l2_count) g += l2 * pi;
     adam_elem(pi, mi, vi, g, opt[3], 1.f - opt[4], 1.f - opt[5], opt[6]);
     p[i] = pi; m[i] = mi; v[i] = vi;
@@ -205,17 +209,17 @@ extern "C" int dl_adam_begin_step(float* opt, float decay_rate, float decay_step
 
 extern "C" int dl_adam_dense(float* p, float* m, float* v, const float* slab, int32_t nslab,
                              int64_t slab_stride, int64_t n, float l2, int64_t l2_count,
-                             const float* opt, void* stream) {
+                             const float* opt, float* p_prev, void* stream) {
   DL_CHECK_ARG(p && m && v && slab && opt, "NULL pointer");
   DL_CHECK_ARG(nslab >= 1 && slab_stride >= n, "bad slabs");
   if (n == 0) return 0;
   if (n < 16384 && nslab >= 32) {
     const long long blocks = (n * 64 + 255) / 256;
     hipLaunchKernelGGL(adam_dense_wave_kernel, dim3((unsigned)blocks), dim3(256), 0, as_stream(stream), p, m,
-                       v, slab, nslab, (long long)slab_stride, (long long)n, l2, (long long)l2_count, opt);
+                       v, slab, nslab, (long long)slab_stride, (long long)n, l2, (long long)l2_count, opt, p_prev);
   } else {
     hipLaunchKernelGGL(adam_dense_thread_kernel, dim3(grid_for(n)), dim3(256), 0, as_stream(stream), p, m,
-                       v, slab, nslab, (long long)slab_stride, (long long)n, l2, (long long)l2_count, opt);
+                       v, slab, nslab, (long long)slab_stride, (long long)n, l2, (long long)l2_count, opt, p_prev);
   }
   DL_RETURN_LAUNCH("dl_adam_dense");
 }

@@ -389,7 +389,7 @@ class CTREngine:
                      ptr(self.W[0]), self.out_ld[0], ptr(self.dx0), self.dx_ld, 0, None, 0, 1, 0, s)
             l2 = 0.0
             self._c("adam_dense_l%d" % l, "dl_adam_dense", ptr(self.W[l]), ptr(self.Wm[l]), ptr(self.Wv[l]), ptr(self.w_slab),
-                 nsplit, stride, stride, l2, 0, ptr(self.opt), s)
+                 nsplit, stride, stride, l2, 0, ptr(self.opt), None, s)
         # embedding backward (uses pre-update table and head weights)
         bwd_blocks = call_int("dl_embed_bwd_grid", C_ref(L))
         if self.bwd == "sorted":
@@ -414,11 +414,10 @@ class CTREngine:
                  sp.S * sp.E, ptr(self.cnt_emb), ptr(self.cnt_first), ptr(self.tg), ptr(self.fmg),
                  ptr(self.touched), s)
         # head Adam: L2 on the output weights only (deepfm_pipeline.py:183 / dnn_pipeline.py:131)
-        self.w_head_prev.copy_(self.w_head)
         H = sp.hidden[-1]
         self._c("adam_head", "dl_adam_dense", ptr(self.w_head), ptr(self.hm), ptr(self.hv), ptr(self.head_slab),
              call_int("dl_head_grid", B), sp.fm_cols + H + 2, self.head_n, sp.l2, self.head_n - 1,
-             ptr(self.opt), s)
+             ptr(self.opt), ptr(self.w_head_prev), s)
         if sp.fm:
             self._c("adam_table", "dl_adam_rows", ptr(self.table), ptr(self.tm), ptr(self.tv), ptr(self.tg), ptr(self.touched),
                  self.table.shape[0], sp.E, 0.0, 0, ptr(self.opt), s)

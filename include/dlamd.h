@@ -202,10 +202,11 @@ int dl_head_grid(int32_t B);
  * and then advances b1p*=b1, b2p*=b2, step+=1 (TF's _finish + global_step). */
 int dl_adam_begin_step(float* opt, float decay_rate, float decay_steps, void* stream);
 /* Dense parameter whose gradient is the sum of `nslab` partial slabs
- * (g = sum_s slab[s*slab_stride + i]); l2 * p is added for i < l2_count. */
+ * (g = sum_s slab[s*slab_stride + i]); l2 * p is added for i < l2_count;
+ * p_prev (may be NULL) receives the pre-update values (the loss's L2 term). */
 int dl_adam_dense(float* p, float* m, float* v, const float* slab, int32_t nslab,
                   int64_t slab_stride, int64_t n, float l2, int64_t l2_count, const float* opt,
-                  void* stream);
+                  float* p_prev, void* stream);
 /* Embedding tables with dense-Adam semantics: g = g_table row if touched else 0;
  * consumed gradients are reset to 0; `clear_touched` resets the flags (pass 1
  * on the last table that shares them).  width = E (table) or 1 (first-order). */
