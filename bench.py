@@ -37,10 +37,10 @@ def log(*a):
     print("[bench %s]" % time.strftime("%H:%M:%S"), *a, file=sys.stderr, flush=True)
 
 
-def kernel_work(spec, B, touched_rows):
+def kernel_work(spec, B, touched_rows, rows=None):
     """Algorithmic bytes / flops per launch."""
     E, S, C = spec.E, spec.S, spec.C
-    N = spec.n_rows
+    N = rows if rows is not None else spec.n_rows
     w = {}
     # gather: FM rows (c+C) + deep rows (c) x 64 B + first-order 4 B + ids 8 B  (SURVEY §8(d): 3,640 B/sample)
     w["embed_fwd"] = ("hbm", B * (S * (2 * E * 4 + 4 + 8)))
@@ -93,7 +93,8 @@ def main():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--dist", default="uniform", choices=["uniform", "zipf"])
     ap.add_argument("--batch", type=int, default=C2["B"])
-    ap.add_argument("--vocab", type=int, default=C2["per_field_vocab"])
+    ap.add_argument("--vocab", type=int, default=0,
+                    help="per-field vocab (default: 1M at N=1 = C2; 100M/26 at N>1 = C4's 100M-row table)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
 
@@ -114,10 +115,18 @@ def main():
             dist.barrier()
 
     B = args.batch
+    if not args.vocab:
+        args.vocab = C2["per_field_vocab"] if world == 1 else 100_000_000 // C2["S"]
     spec = ModelSpec("deepfm_pipeline", C=C2["C"], V=0, S=C2["S"], E=C2["E"],
                      cate_index_size=C2["S"] * args.vocab, hidden=C2["hidden"])
     log("rank %d/%d: building engine, table rows %d" % (rank, world, spec.n_rows))
-    eng = CTREngine(spec, max_batch=B, seed=2019)
+    use_graph = world == 1
+    if world == 1:
+        eng = CTREngine(spec, max_batch=B, seed=2019)
+    else:
+        from deep_learning_amd.shard import Exchange, ShardedCTREngine
+        eng = ShardedCTREngine(spec, B, Exchange(), seed=2019)
+        eng.init_device(2019)
     nb = 4
     dev_batches = []
     for i in range(nb):
@@ -126,7 +135,7 @@ def main():
     torch.cuda.synchronize()
     log("warmup %d" % args.warmup)
     for i in range(max(1, args.warmup)):
-        eng.train_step(dev_batches[i % nb], graph=True)
+        eng.train_step(dev_batches[i % nb], graph=use_graph)
     torch.cuda.synchronize()
     eng.check_error()
 
@@ -135,7 +144,7 @@ def main():
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for i in range(args.steps):
-        eng.train_step(dev_batches[i % nb], graph=True)
+        eng.train_step(dev_batches[i % nb], graph=use_graph)
     torch.cuda.synchronize()
     barrier()
     t1 = time.perf_counter()
@@ -163,7 +172,7 @@ def main():
     # unique rows touched per step (sets how much of the gradient table Adam reads)
     ids = dev_batches[0]["cate_feats"]
     touched_rows = int(torch.unique(torch.cat([ids.reshape(-1) + spec.C, ids.reshape(-1)])).numel()) + spec.C
-    work = kernel_work(spec, B, touched_rows)
+    work = kernel_work(spec, B, touched_rows, rows=getattr(eng, "local_rows", spec.n_rows))
     kernels = {}
     for label, ts in times.items():
         us = float(np.mean(ts))
@@ -217,7 +226,9 @@ def main():
             "data": "synthetic (seeded Criteo-shaped batches, %s ids, resident in HBM)" % args.dist,
             "config": {"workload": "C2 deepfm_pipeline: 13 dense + 26 cat x %d vocab (table %d x 16 f32), "
                                    "MLP [400,400,400], TF1-dense Adam" % (args.vocab, spec.n_rows),
-                       "global_batch": B * world, "per_gpu_batch": B, "parallelism": "dp%d" % world,
+                       "global_batch": B * world, "per_gpu_batch": B,
+                       "parallelism": "dp%d" % world if world == 1 else
+                       "dp%d + row-sharded table (RCCL all-to-all lookup, all-reduce dense grads)" % world,
                        "id_dist": args.dist},
             "roofline": roof,
             "cpu_baseline": cpu,

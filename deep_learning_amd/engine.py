@@ -112,7 +112,8 @@ class ModelSpec:
 
 
 class CTREngine:
-    def __init__(self, spec, max_batch, device="cuda", seed=2019, init="device", bwd="sorted"):
+    def __init__(self, spec, max_batch, device="cuda", seed=2019, init="device", bwd="atomic",
+                 table_rows=None):
         if not torch.cuda.is_available():
             raise _lib.DLError("CTREngine needs a HIP device (no CPU fallback)")
         _lib.lib()
@@ -138,7 +139,7 @@ class CTREngine:
         self.dx_cols = (S + M) * E
         self.dx_ld = _ru(max(self.dx_cols, 4), 4)
         # ---- parameters + Adam state
-        rows_pad = _ru(N, 16)
+        rows_pad = _ru(table_rows if table_rows is not None else N, 16)
         self.table = z(rows_pad, E)
         self.tm, self.tv, self.tg = z(rows_pad, E), z(rows_pad, E), z(rows_pad, E)
         self.touched = z(rows_pad, dt=torch.uint8)
@@ -365,6 +366,20 @@ class CTREngine:
              ptr(self.score), ptr(self.z), ptr(self.dz), ptr(self.dh[-1]), ptr(self.head_slab),
              self.head_blocks, s)
 
+    def _pre(self, B):
+        """Work that must stay OUTSIDE a captured hipGraph: the batch index build
+        (rocPRIM onesweep radix sort faulted under hipGraph replay on this stack —
+        DESIGN.md §Known issues); it runs eagerly on the same stream before the
+        graph replay of the rest of the step."""
+        if self.bwd != "sorted":
+            return
+        s = _lib.stream_handle()
+        L = self.layout
+        L.batch = B
+        self._c("index_build", "dl_index_build", C_ref(L), ptr(self.in_cate), 1, 0, ptr(self.idx_ws),
+                self.idx_ws.numel(), ptr(self.idx_keys), ptr(self.idx_refs), ptr(self.idx_uniq),
+                ptr(self.idx_off), ptr(self.idx_n), None, None, ptr(self.err), s)
+
     def _train(self, B):
         sp = self.spec
         s = _lib.stream_handle()
@@ -393,9 +408,6 @@ class CTREngine:
         # embedding backward (uses pre-update table and head weights)
         bwd_blocks = call_int("dl_embed_bwd_grid", C_ref(L))
         if self.bwd == "sorted":
-            self._c("index_build", "dl_index_build", C_ref(L), ptr(self.in_cate), 1, 0, ptr(self.idx_ws),
-                    self.idx_ws.numel(), ptr(self.idx_keys), ptr(self.idx_refs), ptr(self.idx_uniq),
-                    ptr(self.idx_off), ptr(self.idx_n), None, None, ptr(self.err), s)
             self._c("embed_bwd", "dl_embed_bwd_sorted", C_ref(L), ptr(self.table), None, ptr(self.idx_uniq),
                     ptr(self.idx_off), ptr(self.idx_n), ptr(self.idx_refs), 1, B * self.n_slot, ptr(self.dz),
                     ptr(self.w_head), ptr(self.fm_sum), ptr(self.dx0), ptr(self.tg), ptr(self.fmg),
@@ -430,6 +442,7 @@ class CTREngine:
     def train_step(self, batch=None, graph=False):
         """One training step on `batch` (or on the already-staged slots if None)."""
         B = self.stage(batch) if batch is not None else self.B
+        self._pre(B)
         if graph:
             if self.graph is None or self.graph_batch != B:
                 self._capture(B)

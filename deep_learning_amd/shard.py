@@ -1,0 +1,332 @@
+"""Row-sharded multi-GPU training (BASELINE config C4).
+
+One process per GPU.  The embedding table (and its first-order column and TF1
+Adam state) is split by rows: row r lives on rank r % world at local row
+r // world (cyclic, so Zipf-hot low ids spread over all ranks).  The rows
+below ``replicated`` (deepfm_pipeline's 13 cont-field rows, hit by every
+sample) are replicated on every rank.  Dense parameters are replicated.
+
+Step on every rank (local batch B, global batch B*world):
+  1. index: sort/dedup this batch's row references; unique rows grouped by owner
+  2. all-to-all of the per-owner unique-row counts, then of the row ids
+  3. owners gather the requested rows (E floats + first-order weight)
+  4. all-to-all of the rows back; the forward expands them through the inverse map
+  5. MLP + head forward/backward on the local batch (loss scaled by 1/(B*world))
+  6. per-unique-row gradient (deterministic segment sum), all-to-all to owners,
+     owner scatter-add (f32 atomics: a row may arrive from several peers)
+  7. one all-reduce (sum) of the dense gradients + replicated-row gradients
+  8. TF1 Adam: dense + replicated parameters identically everywhere, the shard
+     rows locally (dense semantics over the shard)
+The result equals single-GPU training on the concatenated global batch.
+
+Collectives go through torch.distributed: backend "nccl" is RCCL (xGMI) and
+exchanges device tensors directly; backend "gloo" (CPU tests, and several ranks
+sharing one GPU) stages them through host memory.
+"""
+import numpy as np
+import torch
+import torch.distributed as dist
+
+from . import _lib
+from ._lib import call, ptr
+from .engine import CTREngine, C_ref, _num_splits, _ru, call_int
+
+
+class Exchange:
+    """Thin wrapper over torch.distributed collectives for the sharded step."""
+
+    def __init__(self, group=None):
+        self.group = group
+        self.world = dist.get_world_size(group)
+        self.rank = dist.get_rank(group)
+        self.backend = dist.get_backend(group)
+        self.staged = self.backend != "nccl"
+
+    def _dev(self, t):
+        return t.cpu() if self.staged and t.is_cuda else t
+
+    def counts(self, send_counts):
+        """All-to-all of one int per peer -> list of received counts."""
+        dev = "cpu" if self.staged else "cuda"
+        s = torch.tensor(send_counts, dtype=torch.int64, device=dev)
+        r = torch.empty_like(s)
+        dist.all_to_all_single(r, s, group=self.group)
+        return [int(x) for x in r.cpu().tolist()]
+
+    def all_to_all(self, send, send_splits, recv_splits):
+        """Variable all-to-all along dim 0 (splits in rows)."""
+        shape = (sum(recv_splits),) + tuple(send.shape[1:])
+        src = self._dev(send.contiguous())
+        out = torch.empty(shape, dtype=send.dtype, device=src.device)
+        dist.all_to_all_single(out, src, output_split_sizes=list(recv_splits),
+                               input_split_sizes=list(send_splits), group=self.group)
+        return out.to(send.device, non_blocking=False) if out.device != send.device else out
+
+    def all_reduce(self, t):
+        if self.staged and t.is_cuda:
+            c = t.cpu()
+            dist.all_reduce(c, group=self.group)
+            t.copy_(c)
+        else:
+            dist.all_reduce(t, group=self.group)
+        return t
+
+
+class ShardedCTREngine(CTREngine):
+    """CTREngine whose embedding tables are row-sharded across the ranks of `exch`."""
+
+    def __init__(self, spec, max_batch, exch, device="cuda", seed=2019):
+        if spec.model not in ("deepfm_pipeline", "dnn_pipeline"):
+            raise ValueError("sharded path supports deepfm_pipeline / dnn_pipeline")
+        self.exch = exch
+        self.W, self.rank = exch.world, exch.rank
+        N = spec.n_rows
+        self.rep = spec.C if spec.model == "deepfm_pipeline" else 0
+        local_rows = -(-N // self.W)
+        super().__init__(spec, max_batch, device=device, seed=seed, init="none", bwd="sorted",
+                         table_rows=local_rows)
+        dev = self.dev
+        z = lambda *sh, dt=torch.float32: torch.zeros(*sh, dtype=dt, device=dev)
+        E = spec.E
+        self.local_rows = local_rows
+        R = max(self.rep, 1)
+        rp = _ru(R, 16)
+        self.rep_t, self.rep_m, self.rep_v, self.rep_g = z(rp, E), z(rp, E), z(rp, E), z(rp, E)
+        self.rep_f, self.rep_fm, self.rep_fv, self.rep_fg = z(rp), z(rp), z(rp), z(rp)
+        self.rep_touched = z(rp, dt=torch.uint8)
+        n = self.n_refs
+        self.inv = z(n, dt=torch.int32)
+        self.owner_counts = z(self.W + 1, dt=torch.int32)
+        self.send_ids = z(n, dt=torch.int32)
+        self.gU = z(n, E)
+        self.g1U = z(n)
+        self.rows_u = z(self.rep + n, E)
+        self.rows_u1 = z(self.rep + n)
+        # flat dense-gradient buffer: every layer's W_aug, the head, replicated rows
+        self.seg = []
+        off = 0
+        for l in range(len(spec.hidden)):
+            sz = self.in_ld[l] * self.out_ld[l]
+            self.seg.append(("W%d" % l, off, sz))
+            off += sz
+        H = spec.hidden[-1]
+        self.head_w = spec.fm_cols + H + 2          # weights + bias + loss sum
+        self.seg.append(("head", off, self.head_w))
+        off += self.head_w
+        self.rep_off = off
+        off += rp * E + rp
+        self.flat = z(off)
+        if self.rep:
+            self.rep_touched[: self.rep] = 1
+
+    # ------------------------------------------------------------ parameters
+    def owned_rows(self):
+        """Global rows stored locally (local row i <-> global rank + i*W)."""
+        return np.arange(self.local_rows) * self.W + self.rank
+
+    def load_params(self, P):
+        """Inject reference-layout GLOBAL parameters; each rank keeps its rows."""
+        sp = self.spec
+        N = self.N
+        rows = self.owned_rows()
+        ok = rows < N
+        t = np.zeros((self.table.shape[0], sp.E), np.float32)
+        t[: self.local_rows][ok] = P["feats_emb"][rows[ok]]
+        self.table.copy_(torch.from_numpy(t))
+        if sp.fm:
+            f = np.zeros(self.first.shape[0], np.float32)
+            f[: self.local_rows][ok] = P["fm_first_order_emb"][rows[ok], 0]
+            self.first.copy_(torch.from_numpy(f))
+        if self.rep:
+            self.rep_t[: self.rep].copy_(torch.from_numpy(np.ascontiguousarray(P["feats_emb"][: self.rep])))
+            if sp.fm:
+                self.rep_f[: self.rep].copy_(torch.from_numpy(np.ascontiguousarray(P["fm_first_order_emb"][: self.rep, 0])))
+        for l in range(len(sp.hidden)):
+            self._set_layer(l, P["deep_%d" % l], P["deep_bias_%d" % l])
+        if sp.fm:
+            w = np.concatenate([P["deep_fm_weight"][:, 0], P["deep_fm_bias"].reshape(-1)]).astype(np.float32)
+        else:
+            w = np.concatenate([P["deep_res"][:, 0], P["deep_res_bias"].reshape(-1)]).astype(np.float32)
+        self.w_head.zero_()
+        self.w_head[: self.head_n].copy_(torch.from_numpy(w))
+        torch.cuda.synchronize()
+
+    def init_device(self, seed):
+        """Bench init: every rank draws its shard with a rank-distinct counter range."""
+        sp = self.spec
+        s = _lib.stream_handle()
+        call("dl_init_random", ptr(self.table), self.table.numel(), 0, 0.0, 0.01, seed,
+             self.rank * self.table.numel() * 4, s)
+        if self.first is not None:
+            call("dl_init_random", ptr(self.first), _ru(self.first.numel(), 4), 1, 0.0, 1.0, seed + 1,
+                 self.rank * _ru(self.first.numel(), 4), s)
+        if self.rep:
+            call("dl_init_random", ptr(self.rep_t), self.rep_t.numel(), 0, 0.0, 0.01, seed + 7, 0, s)
+            if sp.fm:
+                call("dl_init_random", ptr(self.rep_f), _ru(self.rep_f.numel(), 4), 1, 0.0, 1.0, seed + 8, 0, s)
+        rng = np.random.default_rng(seed)   # identical dense init on every rank
+        import math
+        dims = [self.D0] + sp.hidden
+        for l in range(len(sp.hidden)):
+            g = math.sqrt(2.0 / (dims[l] + dims[l + 1]))
+            self._set_layer(l, (rng.standard_normal((dims[l], dims[l + 1])) * g).astype(np.float32),
+                            (rng.standard_normal((1, dims[l + 1])) * g).astype(np.float32), ref_order=False)
+        g = math.sqrt(2.0 / self.head_n)
+        w = np.zeros(self.head_n, np.float32)
+        w[:-1] = rng.standard_normal(self.head_n - 1) * g
+        w[-1] = rng.standard_normal()
+        self.w_head[: self.head_n].copy_(torch.from_numpy(w))
+        torch.cuda.synchronize()
+
+    def params(self):
+        raise NotImplementedError("gather shards with gather_params()")
+
+    def shard_state(self):
+        """(global rows, table rows, first-order) of this rank's shard (host numpy)."""
+        rows = self.owned_rows()
+        ok = rows < self.N
+        t = self.table[: self.local_rows].cpu().numpy()[ok]
+        f = self.first[: self.local_rows].cpu().numpy()[ok] if self.first is not None else None
+        return rows[ok], t, f
+
+    # ------------------------------------------------------------ step
+    def train_step(self, batch=None, graph=False):
+        sp = self.spec
+        ex = self.exch
+        E = sp.E
+        B = self.stage(batch) if batch is not None else self.B
+        s = _lib.stream_handle()
+        L = self.layout
+        L.batch = B
+        W = self.W
+        # 1. index (rows grouped by owner; replicated rows last)
+        self._c("index_build", "dl_index_build", C_ref(L), ptr(self.in_cate), W, self.rep, ptr(self.idx_ws),
+                self.idx_ws.numel(), ptr(self.idx_keys), ptr(self.idx_refs), ptr(self.idx_uniq),
+                ptr(self.idx_off), ptr(self.idx_n), ptr(self.inv), ptr(self.owner_counts), ptr(self.err), s)
+        oc = self.owner_counts.cpu().tolist()
+        send = oc[:W]
+        nsend, nrep = sum(send), oc[W]
+        U = nsend + nrep
+        # 2. exchange counts and ids
+        recv = ex.counts(send)
+        nrecv = sum(recv)
+        call("dl_keys_to_local", ptr(self.idx_uniq), ptr(self.idx_n), U, ptr(self.send_ids), s)
+        recv_ids = ex.all_to_all(self.send_ids[:nsend], send, recv)
+        # 3. owners gather requested rows
+        out_v = torch.empty(max(nrecv, 1), E, device=self.dev)
+        out_1 = torch.empty(max(nrecv, 1), device=self.dev)
+        if nrecv:
+            call("dl_shard_gather", ptr(self.table), ptr(self.first), ptr(recv_ids), nrecv, E, ptr(out_v),
+                 ptr(out_1) if self.first is not None else None, s)
+        # 4. rows back, in unique-id order
+        rv = ex.all_to_all(out_v[:nrecv], recv, send)
+        rep = self.rep
+        self.rows_u[rep: rep + nsend].copy_(rv)
+        if self.first is not None:
+            r1 = ex.all_to_all(out_1[:nrecv], recv, send)
+            self.rows_u1[rep: rep + nsend].copy_(r1)
+        if rep:
+            self.rows_u[:rep].copy_(self.rep_t[:rep])
+            if sp.fm:
+                self.rows_u1[:rep].copy_(self.rep_f[:rep])
+        if nrep:   # replicated rows referenced by cate ids: local rows of the replica
+            call("dl_shard_gather", ptr(self.rep_t), ptr(self.rep_f) if sp.fm else None,
+                 ptr(self.send_ids[nsend:U]), nrep, E, ptr(self.rows_u[rep + nsend:]),
+                 ptr(self.rows_u1[rep + nsend:]) if sp.fm else None, s)
+        # 5. forward + dense backward
+        call("dl_adam_begin_step", ptr(self.opt), sp.decay_rate, float(sp.decay_steps), s)
+        self._c("embed_fwd", "dl_embed_fwd_indexed", C_ref(L), ptr(self.rows_u), ptr(self.rows_u1) if sp.fm else None,
+                ptr(self.inv), rep, ptr(self.in_cont), ptr(self.in_vec), ptr(self.x0), ptr(self.fm_out),
+                ptr(self.fm_sum), s)
+        x = self.x0
+        for l, hdim in enumerate(sp.hidden):
+            self._c("gemm_fwd_l%d" % l, "dl_gemm_f32", 0, 0, B, hdim, self.in_ld[l], ptr(x), self.in_ld[l],
+                    ptr(self.W[l]), self.out_ld[l], ptr(self.h[l]), self.h_ld[l], 1, None, 0, 1, 0, s)
+            x = self.h[l]
+        H = sp.hidden[-1]
+        inv_b = 1.0 / (B * W)
+        self._c("head", "dl_head_fwd_bwd", B, sp.fm_cols, H, ptr(self.fm_out), self.fm_ld, ptr(self.h[-1]),
+                self.h_ld[-1], ptr(self.w_head), ptr(self.in_label), sp.logloss_eps, inv_b, ptr(self.score),
+                ptr(self.z), ptr(self.dz), ptr(self.dh[-1]), ptr(self.head_slab), self.head_blocks, s)
+        nl = len(sp.hidden)
+        splits = max(1, min(self.splits, B // 1024))
+        for l in reversed(range(nl)):
+            xin = self.x0 if l == 0 else self.h[l - 1]
+            hdim = sp.hidden[l]
+            stride = self.in_ld[l] * self.out_ld[l]
+            self._c("gemm_dw_l%d" % l, "dl_gemm_f32", 1, 0, self.in_ld[l], hdim, B, ptr(xin), self.in_ld[l],
+                    ptr(self.dh[l]), self.h_ld[l], ptr(self.w_slab), self.out_ld[l], 3, None, 0, splits, stride, s)
+            call("dl_slab_sum", ptr(self.w_slab), _num_splits(B, splits), stride, stride,
+                 ptr(self.flat[self.seg[l][1]:]), s)
+            if l > 0:
+                self._c("gemm_dx_l%d" % l, "dl_gemm_f32", 0, 1, B, sp.hidden[l - 1], self.out_ld[l], ptr(self.dh[l]),
+                        self.h_ld[l], ptr(self.W[l]), self.out_ld[l], ptr(self.dh[l - 1]), self.h_ld[l - 1], 2,
+                        ptr(self.h[l - 1]), self.h_ld[l - 1], 1, 0, s)
+            else:
+                self._c("gemm_dx_l0", "dl_gemm_f32", 0, 1, B, self.dx_cols, self.out_ld[0], ptr(self.dh[0]),
+                        self.h_ld[0], ptr(self.W[0]), self.out_ld[0], ptr(self.dx0), self.dx_ld, 0, None, 0, 1, 0, s)
+        hoff = self.seg[nl][1]
+        call("dl_slab_sum", ptr(self.head_slab), call_int("dl_head_grid", B), self.head_w, self.head_w,
+             ptr(self.flat[hoff:]), s)
+        # 6. embedding gradients per unique row -> owners
+        self._c("embed_bwd", "dl_embed_bwd_sorted", C_ref(L), None, ptr(self.rows_u[rep:]), ptr(self.idx_uniq),
+                ptr(self.idx_off), ptr(self.idx_n), ptr(self.idx_refs), W, self.n_refs, ptr(self.dz),
+                ptr(self.w_head), ptr(self.fm_sum), ptr(self.dx0), ptr(self.gU), ptr(self.g1U), None, 1, s)
+        gb = ex.all_to_all(self.gU[:nsend], send, recv)
+        g1b = ex.all_to_all(self.g1U[:nsend], send, recv) if sp.fm else None
+        if nrecv:
+            call("dl_shard_scatter_add", ptr(gb), ptr(g1b) if sp.fm else None, ptr(recv_ids), nrecv, E,
+                 ptr(self.tg), ptr(self.fmg) if sp.fm else None, ptr(self.touched), s)
+        # replicated rows: cate-id refs + the FM cont fields, into the flat buffer
+        rg = self.flat[self.rep_off: self.rep_off + self.rep_g.numel()].view(-1, E)
+        rg1 = self.flat[self.rep_off + self.rep_g.numel():]
+        rg.zero_()
+        rg1.zero_()
+        tmp_touch = self.rep_touched.clone()
+        if nrep:
+            call("dl_shard_scatter_add", ptr(self.gU[nsend:U]), ptr(self.g1U[nsend:U]) if sp.fm else None,
+                 ptr(self.send_ids[nsend:U]), nrep, E, ptr(rg), ptr(rg1) if sp.fm else None, ptr(tmp_touch), s)
+        if rep and sp.fm:
+            bwd_blocks = call_int("dl_embed_bwd_grid", C_ref(L))
+            call("dl_embed_cont_bwd", C_ref(L), ptr(self.rows_u), ptr(self.in_cont), ptr(self.dz), ptr(self.w_head),
+                 ptr(self.fm_sum), ptr(self.cont_slab), self.bwd_blocks, s)
+            call("dl_embed_cont_reduce", C_ref(L), ptr(self.cont_slab), bwd_blocks, ptr(rg), ptr(rg1),
+                 ptr(tmp_touch), s)
+        # 7. one all-reduce of every replicated gradient
+        ex.all_reduce(self.flat)
+        # 8. TF1 Adam
+        for l in range(nl):
+            off, sz = self.seg[l][1], self.seg[l][2]
+            self._c("adam_dense_l%d" % l, "dl_adam_dense", ptr(self.W[l]), ptr(self.Wm[l]), ptr(self.Wv[l]),
+                    ptr(self.flat[off:]), 1, sz, sz, 0.0, 0, ptr(self.opt), None, s)
+        self._c("adam_head", "dl_adam_dense", ptr(self.w_head), ptr(self.hm), ptr(self.hv), ptr(self.flat[hoff:]),
+                1, self.head_w, self.head_n, sp.l2, self.head_n - 1, ptr(self.opt), ptr(self.w_head_prev), s)
+        if rep:
+            self.rep_g.view(-1)[: rg.numel()].copy_(rg.reshape(-1))
+            self.rep_fg[: rg1.numel()].copy_(rg1)
+            self.rep_touched[: self.rep] = 1
+            call("dl_adam_rows", ptr(self.rep_t), ptr(self.rep_m), ptr(self.rep_v), ptr(self.rep_g),
+                 ptr(self.rep_touched), self.rep_t.shape[0], E, 0.0, 0, ptr(self.opt), s)
+            if sp.fm:
+                call("dl_adam_rows", ptr(self.rep_f), ptr(self.rep_fm), ptr(self.rep_fv), ptr(self.rep_fg),
+                     ptr(self.rep_touched), self.rep_f.shape[0], 1, 0.0, 0, ptr(self.opt), s)
+        if sp.fm:
+            self._c("adam_table", "dl_adam_rows", ptr(self.table), ptr(self.tm), ptr(self.tv), ptr(self.tg),
+                    ptr(self.touched), self.table.shape[0], E, 0.0, 0, ptr(self.opt), s)
+            self._c("adam_first", "dl_adam_rows", ptr(self.first), ptr(self.fmm), ptr(self.fmv), ptr(self.fmg),
+                    ptr(self.touched), self.first.shape[0], 1, 0.0, 1, ptr(self.opt), s)
+        else:
+            self._c("adam_table", "dl_adam_rows", ptr(self.table), ptr(self.tm), ptr(self.tv), ptr(self.tg),
+                    ptr(self.touched), self.table.shape[0], E, 0.0, 1, ptr(self.opt), s)
+        self.steps += 1
+        self.last_batch = B
+        self.last_loss_sum = None
+        return B
+
+    def loss(self):
+        """Global loss of the last step: the all-reduced loss column + L2 on the head weights."""
+        sp = self.spec
+        hoff = self.seg[len(sp.hidden)][1]
+        data = float(self.flat[hoff + self.head_w - 1].item())
+        w = self.w_head_prev[: self.head_n - 1].double()
+        return data / (self.last_batch * self.W) + sp.l2 * 0.5 * float((w * w).sum().item())

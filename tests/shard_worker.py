@@ -1,0 +1,159 @@
+"""Worker for the multi-rank tests (launched by torch.distributed.run, 127.0.0.1).
+
+mode "sim"  (CPU, gloo): numpy restatement of the sharded step — ids partitioned by
+            owner (row % world), deduplicated, exchanged with the real Exchange
+            all-to-alls, rows gathered from per-rank shards, gradients returned to
+            owners, dense gradients all-reduced — must equal the single-process
+            oracle at the global batch.
+mode "gpu"  (ranks share cuda:0, gloo-staged exchange): the real ShardedCTREngine.
+Writes rank-local results to OUT_DIR/rank{r}.npz.
+"""
+import os
+import sys
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+from deep_learning_amd.synthetic import make_batch  # noqa: E402
+from oracle import ctr_ref as R  # noqa: E402
+
+KW = dict(C=13, V=0, S=26, E=8, cate_index_size=4000, hidden=[24, 16])
+
+
+def global_batches(Bg, steps):
+    out = []
+    for i in range(steps):
+        b = make_batch(Bg, cont=KW["C"], vector=KW["V"], cate_fields=KW["S"], cate_index_size=KW["cate_index_size"],
+                       seed=100 + i)
+        b["cate_feats"][0, :4] = [0, 1, 5, 12]
+        b["cate_feats"][1, :3] = [2, 2, 2]
+        out.append(b)
+    return out
+
+
+def local(b, rank, world):
+    B = b["label"].shape[0] // world
+    return {k: v[rank * B:(rank + 1) * B] for k, v in b.items()}
+
+
+def run_sim(rank, world, steps, Bl, out_dir):
+    """numpy sharded step using the real Exchange over gloo."""
+    from deep_learning_amd.shard import Exchange
+    ex = Exchange()
+    cfg = R.make_cfg("deepfm_pipeline", **KW)
+    P = R.init_params(cfg, np.random.default_rng(42))          # same global init everywhere
+    N = R.n_rows(cfg)
+    C, E = cfg.C, cfg.E
+    own = lambda r: r % world
+    mine = np.arange(N)[np.arange(N) % world == rank]
+    # shard state: this rank's rows of the tables (+ Adam moments) keyed by global row
+    opt = R.AdamTF1(cfg, P)
+    for step, bg in enumerate(global_batches(Bl * world, steps)):
+        b = local(bg, rank, world)
+        cate = b["cate_feats"].astype(np.int64)
+        rows = np.unique(np.concatenate([(cate + C).reshape(-1), cate.reshape(-1)]))
+        rows = rows[rows >= C]                                  # replicated rows stay local
+        owners = own(rows)
+        send = [rows[owners == p] for p in range(world)]
+        counts = ex.counts([len(x) for x in send])
+        req = ex.all_to_all(torch.from_numpy(np.concatenate(send)), [len(x) for x in send], counts).numpy()
+        # owner side: answer from its own rows only
+        assert np.all(own(req) == rank)
+        ans = torch.from_numpy(np.concatenate([P["feats_emb"][req], P["fm_first_order_emb"][req]], 1))
+        back = ex.all_to_all(ans, counts, [len(x) for x in send]).numpy()
+        # the local view of the table: own/exchanged rows + replicated rows; others poisoned
+        view = {k: np.full_like(v, np.nan) for k, v in P.items() if k in ("feats_emb", "fm_first_order_emb")}
+        got = np.concatenate(send)
+        view["feats_emb"][got] = back[:, :E]
+        view["fm_first_order_emb"][got] = back[:, E:]
+        view["feats_emb"][:C] = P["feats_emb"][:C]
+        view["fm_first_order_emb"][:C] = P["fm_first_order_emb"][:C]
+        Pl = dict(P)
+        Pl.update(view)
+        fw = R.forward(cfg, Pl, b)
+        # global-batch mean: scale the local loss gradient by B_local / B_global
+        G, dz = R.backward(cfg, Pl, b, fw)
+        for k in G:
+            if k not in ("feats_emb", "fm_first_order_emb"):
+                G[k] = (G[k] - (cfg.l2 * P[k] if k == "deep_fm_weight" else 0)) / world \
+                       + (cfg.l2 * P[k] if k == "deep_fm_weight" else 0)
+        Gt = G["feats_emb"] / world
+        G1 = G["fm_first_order_emb"] / world
+        # embedding grads: requested rows go back to their owners
+        gsend = torch.from_numpy(np.concatenate([Gt[got], G1[got]], 1).astype(np.float32))
+        grecv = ex.all_to_all(gsend, [len(x) for x in send], counts).numpy()
+        full_t = np.zeros_like(P["feats_emb"])
+        full_1 = np.zeros_like(P["fm_first_order_emb"])
+        np.add.at(full_t, req, grecv[:, :E])
+        np.add.at(full_1, req, grecv[:, E:])
+        # dense + replicated grads: one all-reduce (emulated per tensor)
+        dense = {k: torch.from_numpy(np.ascontiguousarray(G[k])) for k in G if k not in ("feats_emb", "fm_first_order_emb")}
+        l2w = cfg.l2 * P["deep_fm_weight"]
+        dense["deep_fm_weight"] = torch.from_numpy(np.ascontiguousarray(G["deep_fm_weight"] - l2w))
+        for k, t in dense.items():
+            ex.all_reduce(t)
+        rep_t = torch.from_numpy(np.ascontiguousarray(Gt[:C]))
+        rep_1 = torch.from_numpy(np.ascontiguousarray(G1[:C]))
+        ex.all_reduce(rep_t)
+        ex.all_reduce(rep_1)
+        Gall = {k: t.numpy() for k, t in dense.items()}
+        Gall["deep_fm_weight"] = Gall["deep_fm_weight"] + l2w
+        full_t[:C] = rep_t.numpy()
+        full_1[:C] = rep_1.numpy()
+        # rows not owned here keep zero gradient; after Adam only owned rows are meaningful
+        Gall["feats_emb"], Gall["fm_first_order_emb"] = full_t, full_1
+        opt.apply(P, Gall)
+        # exchange the owned rows so every rank holds the true global table (test-only broadcast)
+        for key in ("feats_emb", "fm_first_order_emb"):
+            part = torch.from_numpy(np.ascontiguousarray(P[key]))
+            mask = torch.from_numpy((np.arange(N) % world == rank) | (np.arange(N) < C))
+            part[~mask] = 0
+            if rank != 0:
+                part[:C] = 0
+            ex.all_reduce(part)
+            P[key] = part.numpy()
+            for mk in (opt.m, opt.v):
+                mm = torch.from_numpy(np.ascontiguousarray(mk[key]))
+                mm[~mask] = 0
+                if rank != 0:
+                    mm[:C] = 0
+                ex.all_reduce(mm)
+                mk[key] = mm.numpy()
+        np.savez(os.path.join(out_dir, "rank%d_step%d.npz" % (rank, step)), z=fw["z"])
+    np.savez(os.path.join(out_dir, "rank%d.npz" % rank), **P)
+
+
+def run_gpu(rank, world, steps, Bl, out_dir):
+    from deep_learning_amd.engine import ModelSpec
+    from deep_learning_amd.shard import Exchange, ShardedCTREngine
+    torch.cuda.set_device(0)
+    ex = Exchange()
+    cfg = R.make_cfg("deepfm_pipeline", **KW)
+    P = R.init_params(cfg, np.random.default_rng(42))
+    eng = ShardedCTREngine(ModelSpec("deepfm_pipeline", **KW), Bl, ex)
+    eng.load_params(P)
+    for step, bg in enumerate(global_batches(Bl * world, steps)):
+        eng.train_step(local(bg, rank, world))
+        torch.cuda.synchronize()
+        np.savez(os.path.join(out_dir, "rank%d_step%d.npz" % (rank, step)), z=eng.z[:Bl].cpu().numpy(),
+                 loss=eng.loss())
+    rows, t, f = eng.shard_state()
+    dense = {"W%d" % l: eng.W[l].cpu().numpy() for l in range(len(KW["hidden"]))}
+    np.savez(os.path.join(out_dir, "rank%d.npz" % rank), rows=rows, table=t, first=f,
+             rep=eng.rep_t[:KW["C"]].cpu().numpy(), head=eng.w_head.cpu().numpy(), **dense)
+
+
+if __name__ == "__main__":
+    mode, steps, Bl, out_dir = sys.argv[1], int(sys.argv[2]), int(sys.argv[3]), sys.argv[4]
+    dist.init_process_group("gloo")
+    rank, world = dist.get_rank(), dist.get_world_size()
+    if mode == "sim":
+        run_sim(rank, world, steps, Bl, out_dir)
+    else:
+        run_gpu(rank, world, steps, Bl, out_dir)
+    dist.barrier()
+    dist.destroy_process_group()

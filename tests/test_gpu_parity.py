@@ -47,15 +47,16 @@ def _batches(name, kw, B, n, seed=11):
     return out
 
 
+@pytest.mark.parametrize("bwd", ["atomic", "sorted"])
 @pytest.mark.parametrize("name", list(CASES))
 @pytest.mark.parametrize("B", [256, 1536])
-def test_train_steps_match_oracle(hip_lib, name, B):
+def test_train_steps_match_oracle(hip_lib, name, B, bwd):
     kw = CASES[name]
     model = _model(name)
     cfg = R.make_cfg(model, **kw)
     spec = ModelSpec(model, **kw)
     P = R.init_params(cfg, np.random.default_rng(42))
-    eng = CTREngine(spec, max_batch=B, init="none")
+    eng = CTREngine(spec, max_batch=B, init="none", bwd=bwd)
     eng.load_params(P)
     opt = R.AdamTF1(cfg, P)
     for step, b in enumerate(_batches(name, kw, B, 4)):
