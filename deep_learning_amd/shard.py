@@ -79,10 +79,10 @@ class ShardedCTREngine(CTREngine):
         if spec.model not in ("deepfm_pipeline", "dnn_pipeline"):
             raise ValueError("sharded path supports deepfm_pipeline / dnn_pipeline")
         self.exch = exch
-        self.W, self.rank = exch.world, exch.rank
+        self.world, self.rank = exch.world, exch.rank
         N = spec.n_rows
         self.rep = spec.C if spec.model == "deepfm_pipeline" else 0
-        local_rows = -(-N // self.W)
+        local_rows = -(-N // self.world)
         super().__init__(spec, max_batch, device=device, seed=seed, init="none", bwd="sorted",
                          table_rows=local_rows)
         dev = self.dev
@@ -96,7 +96,7 @@ class ShardedCTREngine(CTREngine):
         self.rep_touched = z(rp, dt=torch.uint8)
         n = self.n_refs
         self.inv = z(n, dt=torch.int32)
-        self.owner_counts = z(self.W + 1, dt=torch.int32)
+        self.owner_counts = z(self.world + 1, dt=torch.int32)
         self.send_ids = z(n, dt=torch.int32)
         self.gU = z(n, E)
         self.g1U = z(n)
@@ -122,7 +122,7 @@ class ShardedCTREngine(CTREngine):
     # ------------------------------------------------------------ parameters
     def owned_rows(self):
         """Global rows stored locally (local row i <-> global rank + i*W)."""
-        return np.arange(self.local_rows) * self.W + self.rank
+        return np.arange(self.local_rows) * self.world + self.rank
 
     def load_params(self, P):
         """Inject reference-layout GLOBAL parameters; each rank keeps its rows."""
@@ -198,7 +198,7 @@ class ShardedCTREngine(CTREngine):
         s = _lib.stream_handle()
         L = self.layout
         L.batch = B
-        W = self.W
+        W = self.world
         # 1. index (rows grouped by owner; replicated rows last)
         self._c("index_build", "dl_index_build", C_ref(L), ptr(self.in_cate), W, self.rep, ptr(self.idx_ws),
                 self.idx_ws.numel(), ptr(self.idx_keys), ptr(self.idx_refs), ptr(self.idx_uniq),
@@ -329,4 +329,4 @@ class ShardedCTREngine(CTREngine):
         hoff = self.seg[len(sp.hidden)][1]
         data = float(self.flat[hoff + self.head_w - 1].item())
         w = self.w_head_prev[: self.head_n - 1].double()
-        return data / (self.last_batch * self.W) + sp.l2 * 0.5 * float((w * w).sum().item())
+        return data / (self.last_batch * self.world) + sp.l2 * 0.5 * float((w * w).sum().item())
