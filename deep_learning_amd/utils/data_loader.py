@@ -1,0 +1,155 @@
+"""TFRecord batch iterator with the reference loader's contract
+(utils/data_loader.py:7-58).
+
+    data = load_input_file(mp, input_path, action_type)   # 'train' repeats mp.epochs times
+    for batch in data: ...   # dict: label [B,1] f32, cont_feats [B,C] f32 (non-cate algs),
+                             #       vector_feats [B,V] f32, cate_feats [B,S+M] int64
+
+Semantics kept from the reference:
+  * files = entries of `input_path` whose name starts with "part", path = input_path + name
+    (string concatenation, so a trailing slash is required), in directory-listing order;
+  * FixedLenFeature: every record must carry exactly the configured sizes, else ValueError
+    (TF raises InvalidArgumentError);
+  * cate algorithms (deepfm_cate, dnn_cate, dnn_multi_cate, deepfm_multi_cate) parse no
+    cont_feats;
+  * shuffle buffer of batch_size*10 records, batch(drop_remainder=True), repeat(epochs) for 'train'.
+Differences: end of data is StopIteration (the reference raises tf.errors.OutOfRangeError);
+the iterator is re-iterable (each `iter()` starts over, like a fresh tf.Session); the
+shuffle is seeded by ``mp.shuffle_seed`` (None = unseeded like the reference) and can be
+disabled with ``mp.shuffle = 0`` so parity runs see identical batches.
+"""
+import os
+import queue
+import threading
+
+import numpy as np
+
+from . import tfrecord
+
+CATE_ALGS = ("deepfm_cate", "dnn_cate", "dnn_multi_cate", "deepfm_multi_cate")
+
+
+def _spec(mp):
+    if mp.alg_name in CATE_ALGS:
+        print("-----------tf_cate-----------")
+        return {"cate_feats": ("int64", mp.cate_field_size + mp.multi_feats_size),
+                "label": ("float", 1), "vector_feats": ("float", mp.vector_feats_size)}
+    print("-----------tf_pipeline-----------")
+    return {"label": ("float", 1), "cont_feats": ("float", mp.cont_field_size),
+            "vector_feats": ("float", mp.vector_feats_size),
+            "cate_feats": ("int64", mp.cate_field_size + mp.multi_feats_size)}
+
+
+def parse_example(data, spec):
+    ex = tfrecord.decode_example(data)
+    out = {}
+    for key, (kind, size) in spec.items():
+        k, vals = ex.get(key, (kind, []))
+        if len(vals) != size:
+            raise ValueError("Key: %s. Can't parse serialized Example: expected %d values, got %d"
+                             % (key, size, len(vals)))
+        out[key] = vals
+    return out
+
+
+class BatchStream:
+    """Re-iterable stream of batches (dicts of numpy arrays)."""
+
+    def __init__(self, mp, files, action_type, prefetch=4):
+        self.mp = mp
+        self.files = list(files)
+        self.repeat = int(mp.epochs) if action_type == "train" else 1
+        self.spec = _spec(mp)
+        self.bsz = int(mp.batch_size)
+        self.shuffle = int(getattr(mp, "shuffle", 1))
+        self.seed = getattr(mp, "shuffle_seed", None)
+        self.prefetch = prefetch
+
+    def _records(self):
+        for _ in range(self.repeat):
+            for f in self.files:
+                yield from tfrecord.read_records(f)
+
+    def _examples(self):
+        spec = self.spec
+        if not self.shuffle:
+            for r in self._records():
+                yield parse_example(r, spec)
+            return
+        rng = np.random.default_rng(self.seed)
+        buf = []
+        cap = self.bsz * 10
+        for r in self._records():
+            buf.append(parse_example(r, spec))
+            if len(buf) >= cap:
+                j = rng.integers(len(buf))
+                buf[j], buf[-1] = buf[-1], buf[j]
+                yield buf.pop()
+        while buf:
+            j = rng.integers(len(buf))
+            buf[j], buf[-1] = buf[-1], buf[j]
+            yield buf.pop()
+
+    def _batches(self):
+        keys = list(self.spec)
+        cur = []
+        for ex in self._examples():
+            cur.append(ex)
+            if len(cur) == self.bsz:
+                out = {}
+                for k in keys:
+                    kind = self.spec[k][0]
+                    arr = np.asarray([e[k] for e in cur], dtype=np.int64 if kind == "int64" else np.float32)
+                    out[k] = arr.reshape(self.bsz, -1)
+                yield out
+                cur = []
+        # drop_remainder=True
+
+    def __iter__(self):
+        q = queue.Queue(maxsize=self.prefetch)
+        stop = object()
+
+        def work():
+            try:
+                for b in self._batches():
+                    q.put(b)
+            except Exception as e:   # surfaced in the consumer
+                q.put(e)
+            q.put(stop)
+
+        threading.Thread(target=work, daemon=True).start()
+        while True:
+            item = q.get()
+            if item is stop:
+                return
+            if isinstance(item, Exception):
+                raise item
+            yield item
+
+
+def get_file_list(input_path):
+    files = os.listdir(input_path)
+    print("file_list_len:", len(files))
+    return [input_path + f for f in files if f[:4] == "part"]
+
+
+def pipeline_process(mp, file_dir_list, action_type):
+    return BatchStream(mp, file_dir_list, action_type)
+
+
+def load_input_file(mp, input_path, action_type):
+    return pipeline_process(mp, get_file_list(input_path), action_type)
+
+
+def write_tfrecord_part(path, batch):
+    """Writes a batch dict (reference keys) as one TFRecord part file (test/fixture helper)."""
+    n = batch["label"].shape[0]
+    recs = []
+    for i in range(n):
+        feats = {"label": ("float", batch["label"][i].reshape(-1).tolist()),
+                 "cate_feats": ("int64", batch["cate_feats"][i].reshape(-1).tolist()),
+                 "vector_feats": ("float", batch.get("vector_feats", np.zeros((n, 0)))[i].reshape(-1).tolist())}
+        if "cont_feats" in batch:
+            feats["cont_feats"] = ("float", batch["cont_feats"][i].reshape(-1).tolist())
+        recs.append(tfrecord.encode_example(feats))
+    tfrecord.write_records(path, recs)
