@@ -60,6 +60,26 @@ def kernel_work(spec, B, touched_rows, rows=None):
     return w
 
 
+# bench label -> rocprofv3 kernel name in profiles/*/pmc_summary.json
+PMC_KERNEL = {"adam_table": "adam_rows4_kernel", "adam_first": "adam_rows1_kernel",
+              "embed_fwd": "embed_fwd_kernel<16, 5>", "embed_bwd": "embed_bwd_kernel<16, false>",
+              "head": "head_kernel"}
+
+
+def pmc_traffic(label, world):
+    """HBM bytes per launch of `label` from the newest committed PMC summary
+    (scripts/pmc_summary.py: (2*FETCH_SIZE + WRITE_SIZE)*1024, gfx950 correction)."""
+    import glob
+    if world != 1 or label not in PMC_KERNEL:
+        return None
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*", "pmc_summary.json")), key=os.path.getmtime)
+    for f in reversed(files):
+        k = json.load(open(f))["kernels"].get(PMC_KERNEL[label])
+        if k and "hbm_bytes" in k:
+            return {"hbm_bytes": int(k["hbm_bytes"]), "source": os.path.relpath(f, ROOT)}
+    return None
+
+
 def cpu_baseline(spec_kw, B, budget_s=25.0):
     """Times the numpy oracle (oracle/ctr_ref.py, the CPU restatement of
     models/deepfm_pipeline.py) on the host: full C2 table, bounded steps."""
@@ -199,6 +219,10 @@ def main():
                 "unit": "TFLOP/s", "frac": round(ach / F32_MFMA_PEAK_TFLOPS, 3), "traffic": None,
                 "algorithmic_flops": amount}
     step_kernel_us = sum(k["us"] for k in kernels.values())
+    pmc = pmc_traffic(dom, world)
+    if pmc is not None:
+        roof["traffic"] = pmc["hbm_bytes"]
+        roof["traffic_source"] = pmc["source"]
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
