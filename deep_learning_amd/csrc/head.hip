@@ -128,9 +128,152 @@ __global__ __launch_bounds__(256) void head_kernel(int B, int fm_cols, int H, co
         red[c] + red[width + c] + red[2 * width + c] + red[3 * width + c];
 }
 
+// Wide&Deep cross logit (models/wdl.py:225-264):
+//   z = sum_f w[wide_f] + sum_j w[Fw + j] * h_j + bias    (w = wdl_weights [N + H])
+// The deep-output weights are rows Fw..Fw+H of the same vector, aliasing wide ids
+// in that range.  Wide rows get dz by f32 atomics into g_w (+ touched flag); the
+// dense part leaves per-block partials slab[block][0..H) = sum dz*h_j,
+// [H] = sum dz (bias), [H+1] = sum loss_b.
+__global__ __launch_bounds__(256) void wdl_head_kernel(int B, int Fw, int H, const int64_t* __restrict__ wide,
+                                                       int wide_ld, const float* __restrict__ h, int ldh,
+                                                       const float* __restrict__ w, const float* __restrict__ bias,
+                                                       long long w_rows, const float* __restrict__ label, float eps,
+                                                       float inv_batch, float* __restrict__ score,
+                                                       float* __restrict__ z_out, float* __restrict__ dz,
+                                                       float* __restrict__ dh, float* __restrict__ g_w,
+                                                       uint8_t* __restrict__ touched, float* __restrict__ slab,
+                                                       int32_t* err) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int nwaves = (gridDim.x * blockDim.x) >> 6;
+  const int H4 = (H + 3) / 4;
+  const float b0 = bias[0];
+  float4 wh[kHeadMaxH4], gh[kHeadMaxH4];
+#pragma unroll
+  for (int k = 0; k < kHeadMaxH4; ++k) {
+    const int c = 4 * (lane + 64 * k);
+    wh[k].x = c + 0 < H ? w[Fw + c + 0] : 0.f;
+    wh[k].y = c + 1 < H ? w[Fw + c + 1] : 0.f;
+    wh[k].z = c + 2 < H ? w[Fw + c + 2] : 0.f;
+    wh[k].w = c + 3 < H ? w[Fw + c + 3] : 0.f;
+    gh[k] = make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+  float gb = 0.f, lsum = 0.f;
+  for (int b = wave; b < B; b += nwaves) {
+    float part = 0.f;
+    long long wr = -1;
+    if (lane < Fw) {
+      wr = wide[(long long)b * wide_ld + lane];
+      if (wr < 0 || wr >= w_rows) { if (err) atomicOr(err, 1); wr = -1; }
+      else part += w[wr];
+    }
+    float4 hh[kHeadMaxH4];
+    const float* hb = h + (long long)b * ldh;
+#pragma unroll
+    for (int k = 0; k < kHeadMaxH4; ++k) {
+      const int c4 = lane + 64 * k;
+      hh[k] = c4 < H4 ? *reinterpret_cast<const float4*>(hb + 4 * c4) : make_float4(0.f, 0.f, 0.f, 0.f);
+      part += hh[k].x * wh[k].x + hh[k].y * wh[k].y + hh[k].z * wh[k].z + hh[k].w * wh[k].w;
+    }
+    const float z = wave_sum(part) + b0;
+    const float p = 1.f / (1.f + expf(-z));
+    const float y = label[b];
+    const float g = (-y / (p + eps) + (1.f - y) / (1.f - p + eps)) * inv_batch * p * (1.f - p);
+    if (lane == 0) {
+      score[b] = p;
+      if (z_out) z_out[b] = z;
+      dz[b] = g;
+      gb += g;
+      lsum += -y * logf(p + eps) - (1.f - y) * logf(1.f - p + eps);
+    }
+    if (wr >= 0 && g_w) {
+      atomicAdd(g_w + wr, g);
+      touched[wr] = 1;
+    }
+    float* dhb = dh + (long long)b * ldh;
+#pragma unroll
+    for (int k = 0; k < kHeadMaxH4; ++k) {
+      const int c4 = lane + 64 * k;
+      gh[k].x += g * hh[k].x; gh[k].y += g * hh[k].y; gh[k].z += g * hh[k].z; gh[k].w += g * hh[k].w;
+      if (c4 < H4) {
+        const int c = 4 * c4;
+        float o[4] = {hh[k].x > 0.f ? g * wh[k].x : 0.f, hh[k].y > 0.f ? g * wh[k].y : 0.f,
+                      hh[k].z > 0.f ? g * wh[k].z : 0.f, hh[k].w > 0.f ? g * wh[k].w : 0.f};
+        for (int e = 0; e < 4; ++e)
+          if (c + e < H) dhb[c + e] = o[e];
+      }
+    }
+  }
+  const int width = H + 2;
+  extern __shared__ __attribute__((aligned(16))) float red[];
+#pragma unroll
+  for (int k = 0; k < kHeadMaxH4; ++k) {
+    const int c = 4 * (lane + 64 * k);
+    float* o = red + wid * width;
+    if (c + 0 < H) o[c + 0] = gh[k].x;
+    if (c + 1 < H) o[c + 1] = gh[k].y;
+    if (c + 2 < H) o[c + 2] = gh[k].z;
+    if (c + 3 < H) o[c + 3] = gh[k].w;
+  }
+  if (lane == 0) {
+    red[wid * width + H] = gb;
+    red[wid * width + H + 1] = lsum;
+  }
+  __syncthreads();
+  for (int c = threadIdx.x; c < width; c += blockDim.x)
+    slab[(long long)blockIdx.x * width + c] = red[c] + red[width + c] + red[2 * width + c] + red[3 * width + c];
+}
+
+// g[row0 + j] += sum_blocks slab[blk*width + col0 + j]; touched[row0 + j] = 1
+__global__ __launch_bounds__(256) void slab_fold_rows_kernel(const float* __restrict__ slab, int blocks, int width,
+                                                             int col0, int n, float* __restrict__ g, long long row0,
+                                                             uint8_t* __restrict__ touched) {
+  const int j = blockIdx.x;
+  if (j >= n) return;
+  float acc = 0.f;
+  for (int t = threadIdx.x; t < blocks; t += blockDim.x) acc += slab[(long long)t * width + col0 + j];
+  acc = wave_sum(acc);
+  __shared__ float part[4];
+  if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    g[row0 + j] += part[0] + part[1] + part[2] + part[3];
+    if (touched) touched[row0 + j] = 1;
+  }
+}
+
 }  // namespace dl
 
 using namespace dl;
+
+extern "C" int dl_wdl_head_fwd_bwd(int32_t B, int32_t Fw, int32_t H, const int64_t* wide, int32_t wide_ld,
+                                   const float* h, int32_t ldh, const float* w, const float* bias, int64_t w_rows,
+                                   const float* label, float eps, float inv_batch, float* score, float* z_out,
+                                   float* dz, float* dh, float* g_w, uint8_t* touched, float* slab,
+                                   int32_t slab_blocks, int32_t* err, void* stream) {
+  DL_CHECK_ARG(Fw >= 0 && Fw <= 64, "Fw %d not in [0, 64]", Fw);
+  DL_CHECK_ARG(H > 0 && H <= 4 * 64 * kHeadMaxH4, "H %d too large", H);
+  DL_CHECK_ARG(w_rows >= Fw + H, "wdl_weights must have >= Fw + H rows");
+  DL_CHECK_ARG(ldh % 4 == 0 && ldh >= H && ((uintptr_t)h % 16) == 0, "h must be 16-B aligned, ldh %% 4 == 0");
+  DL_CHECK_ARG(w && bias && label && score && dz && dh && slab && (!g_w || touched), "NULL argument");
+  const int grid = dl_head_grid(B);
+  DL_CHECK_ARG(slab_blocks >= grid, "slab needs %d blocks", grid);
+  if (B == 0) return 0;
+  const size_t lds = 4 * (size_t)(H + 2) * sizeof(float);
+  hipLaunchKernelGGL(wdl_head_kernel, dim3(grid), dim3(256), lds, as_stream(stream), B, Fw, H, wide, wide_ld, h,
+                     ldh, w, bias, (long long)w_rows, label, eps, inv_batch, score, z_out, dz, dh, g_w, touched,
+                     slab, err);
+  DL_RETURN_LAUNCH("dl_wdl_head_fwd_bwd");
+}
+
+extern "C" int dl_slab_fold_rows(const float* slab, int32_t blocks, int32_t width, int32_t col0, int32_t n,
+                                 float* g, int64_t row0, uint8_t* touched, void* stream) {
+  DL_CHECK_ARG(slab && g && blocks >= 1 && col0 + n <= width, "bad args");
+  if (n <= 0) return 0;
+  hipLaunchKernelGGL(slab_fold_rows_kernel, dim3(n), dim3(256), 0, as_stream(stream), slab, blocks, width, col0, n,
+                     g, (long long)row0, touched);
+  DL_RETURN_LAUNCH("dl_slab_fold_rows");
+}
 
 extern "C" int dl_head_grid(int32_t B) {
   int g = (B + 63) / 64;   // ~16 samples per wave

@@ -22,6 +22,7 @@ __global__ void adam_begin_kernel(float* opt, float decay_rate, float decay_step
   opt[0] = b1p * opt[4];                                         // Adam._finish
   opt[1] = b2p * opt[5];
   opt[7] = step + 1.f;                                           // global_step += 1
+  for (int i = 8; i < 16; ++i) opt[i] = 0.f;                     // per-step L2 accumulators
 }
 
 __device__ __forceinline__ void adam_elem(float& p, float& m, float& v, float g, float alpha,
@@ -37,8 +38,9 @@ __global__ __launch_bounds__(256) void adam_dense_thread_kernel(float* __restric
                                                                 const float* __restrict__ slab, int nslab,
                                                                 long long stride, long long n, float l2,
                                                                 long long l2_count, const float* __restrict__ opt,
-                                                                float* __restrict__ p_prev) {
+                                                                float* __restrict__ p_prev, float* __restrict__ sq_out) {
   const float alpha = opt[3], omb1 = 1.f - opt[4], omb2 = 1.f - opt[5], eps = opt[6];
+  float sq = 0.f;
   for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n;
        i += (long long)gridDim.x * blockDim.x) {
     float g = 0.f;
@@ -51,9 +53,13 @@ __global__ __launch_bounds__(256) void adam_dense_thread_kernel(float* __restric
     for (; s < nslab; ++s) g += slab[s * stride + i];
     float pi = p[i], mi = m[i], vi = v[i];
     if (p_prev) p_prev[i] = pi;
-    if (i < l2_count) g += l2 * pi;
+    if (i < l2_count) { g += l2 * pi; sq += pi * pi; }
     adam_elem(pi, mi, vi, g, alpha, omb1, omb2, eps);
     p[i] = pi; m[i] = mi; v[i] = vi;
+  }
+  if (sq_out) {
+    sq = wave_sum(sq);
+    if ((threadIdx.x & 63) == 0) atomicAdd(sq_out, sq);
   }
 }
 
@@ -63,7 +69,7 @@ __global__ __launch_bounds__(256) void adam_dense_wave_kernel(float* __restrict_
                                                               const float* __restrict__ slab, int nslab,
                                                               long long stride, long long n, float l2,
                                                               long long l2_count, const float* __restrict__ opt,
-                                                              float* __restrict__ p_prev) {
+                                                              float* __restrict__ p_prev, float* __restrict__ sq_out) {
   const long long i = ((long long)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   const int lane = threadIdx.x & 63;
   if (i >= n) return;
@@ -73,7 +79,10 @@ __global__ __launch_bounds__(256) void adam_dense_wave_kernel(float* __restrict_
   if (lane == 0) {
     float pi = p[i], mi = m[i], vi = v[i];
     if (p_prev) p_prev[i] = pi;
-    if (i < l2_count) g += l2 * pi;
+    if (i < l2_count) {
+      g += l2 * pi;
+      if (sq_out) atomicAdd(sq_out, pi * pi);
+    }
     adam_elem(pi, mi, vi, g, opt[3], 1.f - opt[4], 1.f - opt[5], opt[6]);
     p[i] = pi; m[i] = mi; v[i] = vi;
   }
@@ -83,8 +92,10 @@ __global__ __launch_bounds__(256) void adam_dense_wave_kernel(float* __restrict_
 __global__ __launch_bounds__(256) void adam_rows4_kernel(float4* __restrict__ p, float4* __restrict__ m,
                                                          float4* __restrict__ v, float4* __restrict__ g,
                                                          const uint8_t* __restrict__ touched, long long n4,
-                                                         int lpr, float l2, const float* __restrict__ opt) {
+                                                         int lpr, float l2, const float* __restrict__ opt,
+                                                         float* __restrict__ sq_out) {
   const float alpha = opt[3], omb1 = 1.f - opt[4], omb2 = 1.f - opt[5], eps = opt[6];
+  float sq = 0.f;
   for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n4;
        i += (long long)gridDim.x * blockDim.x) {
     const long long row = i / lpr;
@@ -95,11 +106,16 @@ __global__ __launch_bounds__(256) void adam_rows4_kernel(float4* __restrict__ p,
     }
     float4 pi = p[i], mi = m[i], vi = v[i];
     if (l2 != 0.f) { gi.x += l2 * pi.x; gi.y += l2 * pi.y; gi.z += l2 * pi.z; gi.w += l2 * pi.w; }
+    if (sq_out) sq += pi.x * pi.x + pi.y * pi.y + pi.z * pi.z + pi.w * pi.w;
     adam_elem(pi.x, mi.x, vi.x, gi.x, alpha, omb1, omb2, eps);
     adam_elem(pi.y, mi.y, vi.y, gi.y, alpha, omb1, omb2, eps);
     adam_elem(pi.z, mi.z, vi.z, gi.z, alpha, omb1, omb2, eps);
     adam_elem(pi.w, mi.w, vi.w, gi.w, alpha, omb1, omb2, eps);
     p[i] = pi; m[i] = mi; v[i] = vi;
+  }
+  if (sq_out) {
+    sq = wave_sum(sq);
+    if ((threadIdx.x & 63) == 0) atomicAdd(sq_out, sq);
   }
 }
 
@@ -107,9 +123,11 @@ __global__ __launch_bounds__(256) void adam_rows4_kernel(float4* __restrict__ p,
 __global__ __launch_bounds__(256) void adam_rows1_kernel(float* __restrict__ p, float* __restrict__ m,
                                                          float* __restrict__ v, float* __restrict__ g,
                                                          uint8_t* __restrict__ touched, long long n,
-                                                         float l2, int clear, const float* __restrict__ opt) {
+                                                         float l2, int clear, const float* __restrict__ opt,
+                                                         float* __restrict__ sq_out) {
   const float alpha = opt[3], omb1 = 1.f - opt[4], omb2 = 1.f - opt[5], eps = opt[6];
   const long long n4 = n / 4;
+  float sq = 0.f;
   for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < (n + 3) / 4;
        i += (long long)gridDim.x * blockDim.x) {
     if (i < n4) {
@@ -125,6 +143,7 @@ __global__ __launch_bounds__(256) void adam_rows1_kernel(float* __restrict__ p, 
       float4 pi = reinterpret_cast<float4*>(p)[i], mi = reinterpret_cast<float4*>(m)[i],
              vi = reinterpret_cast<float4*>(v)[i];
       if (l2 != 0.f) { gi.x += l2 * pi.x; gi.y += l2 * pi.y; gi.z += l2 * pi.z; gi.w += l2 * pi.w; }
+      sq += pi.x * pi.x + pi.y * pi.y + pi.z * pi.z + pi.w * pi.w;
       adam_elem(pi.x, mi.x, vi.x, gi.x, alpha, omb1, omb2, eps);
       adam_elem(pi.y, mi.y, vi.y, gi.y, alpha, omb1, omb2, eps);
       adam_elem(pi.z, mi.z, vi.z, gi.z, alpha, omb1, omb2, eps);
@@ -137,10 +156,15 @@ __global__ __launch_bounds__(256) void adam_rows1_kernel(float* __restrict__ p, 
         if (touched[r]) { gi = g[r]; g[r] = 0.f; if (clear) touched[r] = 0; }
         float pi = p[r], mi = m[r], vi = v[r];
         if (l2 != 0.f) gi += l2 * pi;
+        sq += pi * pi;
         adam_elem(pi, mi, vi, gi, alpha, omb1, omb2, eps);
         p[r] = pi; m[r] = mi; v[r] = vi;
       }
     }
+  }
+  if (sq_out) {
+    sq = wave_sum(sq);
+    if ((threadIdx.x & 63) == 0) atomicAdd(sq_out, sq);
   }
 }
 
@@ -209,23 +233,23 @@ extern "C" int dl_adam_begin_step(float* opt, float decay_rate, float decay_step
 
 extern "C" int dl_adam_dense(float* p, float* m, float* v, const float* slab, int32_t nslab,
                              int64_t slab_stride, int64_t n, float l2, int64_t l2_count,
-                             const float* opt, float* p_prev, void* stream) {
+                             const float* opt, float* p_prev, float* sq_out, void* stream) {
   DL_CHECK_ARG(p && m && v && slab && opt, "NULL pointer");
   DL_CHECK_ARG(nslab >= 1 && slab_stride >= n, "bad slabs");
   if (n == 0) return 0;
   if (n < 16384 && nslab >= 32) {
     const long long blocks = (n * 64 + 255) / 256;
     hipLaunchKernelGGL(adam_dense_wave_kernel, dim3((unsigned)blocks), dim3(256), 0, as_stream(stream), p, m,
-                       v, slab, nslab, (long long)slab_stride, (long long)n, l2, (long long)l2_count, opt, p_prev);
+                       v, slab, nslab, (long long)slab_stride, (long long)n, l2, (long long)l2_count, opt, p_prev, sq_out);
   } else {
     hipLaunchKernelGGL(adam_dense_thread_kernel, dim3(grid_for(n)), dim3(256), 0, as_stream(stream), p, m,
-                       v, slab, nslab, (long long)slab_stride, (long long)n, l2, (long long)l2_count, opt, p_prev);
+                       v, slab, nslab, (long long)slab_stride, (long long)n, l2, (long long)l2_count, opt, p_prev, sq_out);
   }
   DL_RETURN_LAUNCH("dl_adam_dense");
 }
 
 extern "C" int dl_adam_rows(float* p, float* m, float* v, float* g, uint8_t* touched, int64_t n_rows,
-                            int32_t width, float l2, int32_t clear_touched, const float* opt,
+                            int32_t width, float l2, int32_t clear_touched, const float* opt, float* sq_out,
                             void* stream) {
   DL_CHECK_ARG(p && m && v && g && touched && opt, "NULL pointer");
   DL_CHECK_ARG(width == 1 || width % 4 == 0, "width must be 1 or a multiple of 4");
@@ -235,11 +259,11 @@ extern "C" int dl_adam_rows(float* p, float* m, float* v, float* g, uint8_t* tou
   if (width == 1) {
     DL_CHECK_ARG(((uintptr_t)touched % 4) == 0, "touched must be 4-B aligned");
     hipLaunchKernelGGL(adam_rows1_kernel, dim3(grid_for(n_rows, 4)), dim3(256), 0, s, p, m, v, g, touched,
-                       (long long)n_rows, l2, clear_touched, opt);
+                       (long long)n_rows, l2, clear_touched, opt, sq_out);
   } else {
     const long long n4 = n_rows * (width / 4);
     hipLaunchKernelGGL(adam_rows4_kernel, dim3(grid_for(n4)), dim3(256), 0, s, (float4*)p, (float4*)m,
-                       (float4*)v, (float4*)g, touched, n4, width / 4, l2, opt);
+                       (float4*)v, (float4*)g, touched, n4, width / 4, l2, opt, sq_out);
     if (clear_touched) {
       DL_CHECK_ARG(((uintptr_t)touched % 16) == 0, "touched must be 16-B aligned");
       hipLaunchKernelGGL(clear_touched_kernel, dim3(grid_for(n_rows, 16)), dim3(256), 0, s, touched,

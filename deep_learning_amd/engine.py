@@ -47,11 +47,12 @@ class ModelSpec:
     def __init__(self, model, C=13, V=0, S=26, E=16, cate_index_size=1000, hidden=(400, 400, 400),
                  multi_ranges=(), Fw=0, lr=0.001, l2=1e-5, decay_steps=10000000, decay_rate=0.9,
                  beta1=0.9, beta2=0.999, eps=1e-8, logloss_eps=1e-7):
-        if model not in ("deepfm_pipeline", "dnn_pipeline", "deepfm_multi_cate"):
+        if model not in ("deepfm_pipeline", "dnn_pipeline", "deepfm_multi_cate", "wdl"):
             raise ValueError("unsupported model %r" % model)
         self.model = model
         self.C = 0 if model == "deepfm_multi_cate" else C
-        self.V, self.S, self.E = V, S, E
+        self.V = 0 if model == "wdl" else V
+        self.S, self.E = S, E
         self.cate_index_size = cate_index_size
         self.hidden = list(hidden)
         self.multi_ranges = [list(r) for r in multi_ranges]
@@ -156,8 +157,15 @@ class CTREngine:
         self.w_head = z(_ru(self.head_n, 4))
         self.hm, self.hv = torch.zeros_like(self.w_head), torch.zeros_like(self.w_head)
         self.w_head_prev = torch.zeros_like(self.w_head)
-        self.opt = z(8)
-        self.opt.copy_(torch.tensor([sp.beta1, sp.beta2, sp.lr, 0.0, sp.beta1, sp.beta2, sp.eps, 0.0]))
+        self.opt = z(16)
+        self.opt[:8].copy_(torch.tensor([sp.beta1, sp.beta2, sp.lr, 0.0, sp.beta1, sp.beta2, sp.eps, 0.0]))
+        self.wdl = sp.model == "wdl"
+        if self.wdl:   # wdl_weights [N + H] (deep-output rows alias wide ids, wdl.py:241-248) + bias
+            self.w_rows = N + sp.hidden[-1]
+            wr = _ru(self.w_rows, 16)
+            self.ww, self.wm, self.wv, self.wg = z(wr), z(wr), z(wr), z(wr)
+            self.w_touched = z(wr, dt=torch.uint8)
+            self.wb, self.wbm, self.wbv = z(4), z(4), z(4)
         self.err = z(4, dt=torch.int32)
         # ---- activations / workspaces
         B = max_batch
@@ -175,6 +183,7 @@ class CTREngine:
         self.score, self.z, self.dz = z(B), z(B), z(B)
         self.head_blocks = call_int("dl_head_grid", B)
         self.head_slab = z(self.head_blocks, sp.fm_cols + H + 2)
+        self.in_wide = z(B, max(sp.Fw, 1), dt=torch.int64)
         self.splits = max(1, min(64, B // 1024))
         self.w_slab = z(self.splits * max(i * o for i, o in zip(self.in_ld, self.out_ld)))
         self.layout = self._layout(B)
@@ -225,7 +234,7 @@ class CTREngine:
         L.fm_cont = 1 if sp.model == "deepfm_pipeline" else 0
         L.use_fm = 1 if sp.fm else 0
         L.fm_extra = sp.M if sp.fm else 0
-        L.zero_row0 = 1                                                 # :83-86
+        L.zero_row0 = 0 if sp.model == "wdl" else 1                     # :83-86 (wdl.py:49: none)
         L.x0_ld = self.in_ld[0]
         L.x0_cont_col = self.cont_col if sp.C else -1
         L.x0_vec_col = self.vec_col if sp.V else -1
@@ -242,7 +251,15 @@ class CTREngine:
         first-order ~ U[0,1), dense weights/biases ~ N(0, glorot) (numpy, seeded)."""
         sp = self.spec
         s = _lib.stream_handle()
-        call("dl_init_random", ptr(self.table), self.table.numel(), 0, 0.0, 0.01, seed, 0, s)
+        if self.wdl:   # xavier_initializer (wdl.py:44-47): U(-lim, lim), lim = sqrt(6/(N+E))
+            lim = math.sqrt(6.0 / (self.N + sp.E))
+            call("dl_init_random", ptr(self.table), self.table.numel(), 1, -lim, 2 * lim, seed, 0, s)
+            call("dl_init_random", ptr(self.ww), _ru(self.ww.numel(), 4), 0, 0.0,
+                 math.sqrt(2.0 / self.w_rows), seed + 3, 0, s)                           # wdl.py:241-244
+            self.ww[self.w_rows:].zero_()
+            self.wb[0] = float(np.random.default_rng(seed).standard_normal())
+        else:
+            call("dl_init_random", ptr(self.table), self.table.numel(), 0, 0.0, 0.01, seed, 0, s)
         if self.first is not None:
             call("dl_init_random", ptr(self.first), self.first.numel(), 1, 0.0, 1.0, seed + 1, 0, s)
         rng = np.random.default_rng(seed)
@@ -274,12 +291,20 @@ class CTREngine:
         sp = self.spec
         N = self.N
         self.table.zero_()
-        self.table[:N].copy_(torch.from_numpy(np.ascontiguousarray(P["feats_emb"], np.float32)))
+        tab = P["weight_mat"] if self.wdl else P["feats_emb"]
+        self.table[:N].copy_(torch.from_numpy(np.ascontiguousarray(tab, np.float32)))
         if self.first is not None:
             self.first.zero_()
             self.first[:N].copy_(torch.from_numpy(np.ascontiguousarray(P["fm_first_order_emb"][:, 0], np.float32)))
         for l in range(len(sp.hidden)):
             self._set_layer(l, P["deep_%d" % l], P["deep_bias_%d" % l])
+        if self.wdl:
+            self.ww.zero_()
+            self.ww[: self.w_rows].copy_(torch.from_numpy(np.ascontiguousarray(P["wdl_weights"][:, 0], np.float32)))
+            self.wb.zero_()
+            self.wb[:1].copy_(torch.from_numpy(np.asarray(P["wdl_bias"], np.float32).reshape(-1)))
+            torch.cuda.synchronize()
+            return
         if sp.fm:
             w = np.concatenate([P["deep_fm_weight"][:, 0], P["deep_fm_bias"].reshape(-1)]).astype(np.float32)
         else:
@@ -292,7 +317,7 @@ class CTREngine:
         """Export parameters in the reference layout (numpy)."""
         sp = self.spec
         N = self.N
-        P = {"feats_emb": self.table[:N].cpu().numpy()}
+        P = {("weight_mat" if self.wdl else "feats_emb"): self.table[:N].cpu().numpy()}
         if self.first is not None:
             P["fm_first_order_emb"] = self.first[:N].cpu().numpy()[:, None]
         dims = [self.D0] + sp.hidden
@@ -305,6 +330,10 @@ class CTREngine:
                 W = Wr
             P["deep_%d" % l] = W.copy()
             P["deep_bias_%d" % l] = Wi[dims[l], : dims[l + 1]][None, :].copy()
+        if self.wdl:
+            P["wdl_weights"] = self.ww[: self.w_rows].cpu().numpy()[:, None].copy()
+            P["wdl_bias"] = self.wb[:1].cpu().numpy().copy()
+            return P
         w = self.w_head[: self.head_n].cpu().numpy()
         if sp.fm:
             P["deep_fm_weight"], P["deep_fm_bias"] = w[:-1, None].copy(), w[-1:].copy()
@@ -326,6 +355,8 @@ class CTREngine:
         if sp.V:
             self.in_vec[:B, : sp.V].copy_(_as_dev(batch["vector_feats"], F32, self.dev))
         self.in_cate[:B, : sp.cate_ld].copy_(_as_dev(batch["cate_feats"], torch.int64, self.dev))
+        if sp.Fw:
+            self.in_wide[:B, : sp.Fw].copy_(_as_dev(batch["wide_feats"], torch.int64, self.dev))
         return B
 
     # ------------------------------------------------------------------ step
@@ -344,7 +375,7 @@ class CTREngine:
         e1.record()
         self.prof.append((label, e0, e1))
 
-    def _forward(self, B, s):
+    def _forward(self, B, s, train=False):
         sp = self.spec
         L = self.layout
         L.batch = B
@@ -361,6 +392,13 @@ class CTREngine:
                  self.out_ld[l], ptr(self.h[l]), self.h_ld[l], 1, None, 0, 1, 0, s)
             x = self.h[l]
         H = sp.hidden[-1]
+        if self.wdl:
+            self._c("head", "dl_wdl_head_fwd_bwd", B, sp.Fw, H, ptr(self.in_wide), self.in_wide.shape[1],
+                    ptr(self.h[-1]), self.h_ld[-1], ptr(self.ww), ptr(self.wb), self.w_rows, ptr(self.in_label),
+                    sp.logloss_eps, 1.0 / B, ptr(self.score), ptr(self.z), ptr(self.dz), ptr(self.dh[-1]),
+                    ptr(self.wg) if train else None, ptr(self.w_touched) if train else None,
+                    ptr(self.head_slab), self.head_blocks, ptr(self.err), s)
+            return
         self._c("head", "dl_head_fwd_bwd", B, sp.fm_cols, H, ptr(self.fm_out), self.fm_ld, ptr(self.h[-1]),
              self.h_ld[-1], ptr(self.w_head), ptr(self.in_label), sp.logloss_eps, 1.0 / B,
              ptr(self.score), ptr(self.z), ptr(self.dz), ptr(self.dh[-1]), ptr(self.head_slab),
@@ -385,7 +423,7 @@ class CTREngine:
         s = _lib.stream_handle()
         L = self.layout
         self._c("adam_begin", "dl_adam_begin_step", ptr(self.opt), sp.decay_rate, float(sp.decay_steps), s)
-        self._forward(B, s)
+        self._forward(B, s, train=True)
         nl = len(sp.hidden)
         splits = max(1, min(self.splits, B // 1024))
         for l in reversed(range(nl)):
@@ -402,9 +440,11 @@ class CTREngine:
             else:
                 self._c("gemm_dx_l0", "dl_gemm_f32", 0, 1, B, self.dx_cols, self.out_ld[0], ptr(self.dh[0]), self.h_ld[0],
                      ptr(self.W[0]), self.out_ld[0], ptr(self.dx0), self.dx_ld, 0, None, 0, 1, 0, s)
-            l2 = 0.0
-            self._c("adam_dense_l%d" % l, "dl_adam_dense", ptr(self.W[l]), ptr(self.Wm[l]), ptr(self.Wv[l]), ptr(self.w_slab),
-                 nsplit, stride, stride, l2, 0, ptr(self.opt), None, s)
+            # L2 on every hidden weight matrix only for wdl (wdl.py:272-275); bias row excluded
+            l2, l2n = (sp.l2, ([self.D0] + sp.hidden)[l] * self.out_ld[l]) if self.wdl else (0.0, 0)
+            self._c("adam_dense_l%d" % l, "dl_adam_dense", ptr(self.W[l]), ptr(self.Wm[l]), ptr(self.Wv[l]),
+                    ptr(self.w_slab), nsplit, stride, stride, l2, l2n, ptr(self.opt), None,
+                    ptr(self.opt[8:]) if self.wdl else None, s)
         # embedding backward (uses pre-update table and head weights)
         bwd_blocks = call_int("dl_embed_bwd_grid", C_ref(L))
         if self.bwd == "sorted":
@@ -425,19 +465,32 @@ class CTREngine:
                  sp.M, sp.S, ptr(self.x0), ptr(self.fm_sum), ptr(self.dz), ptr(self.w_head), ptr(self.dx0),
                  sp.S * sp.E, ptr(self.cnt_emb), ptr(self.cnt_first), ptr(self.tg), ptr(self.fmg),
                  ptr(self.touched), s)
-        # head Adam: L2 on the output weights only (deepfm_pipeline.py:183 / dnn_pipeline.py:131)
         H = sp.hidden[-1]
+        hb = call_int("dl_head_grid", B)
+        if self.wdl:
+            # wdl_weights: dense Adam with L2 on every row (wdl.py:270-271); the deep-output
+            # rows get their batch sums folded in from the head slab first
+            self._c("wdl_fold", "dl_slab_fold_rows", ptr(self.head_slab), hb, H + 2, 0, H, ptr(self.wg), sp.Fw,
+                    ptr(self.w_touched), s)
+            self._c("adam_bias", "dl_adam_dense", ptr(self.wb), ptr(self.wbm), ptr(self.wbv),
+                    ptr(self.head_slab[:, H:]), hb, H + 2, 1, 0.0, 0, ptr(self.opt), None, None, s)
+            self._c("adam_wide", "dl_adam_rows", ptr(self.ww), ptr(self.wm), ptr(self.wv), ptr(self.wg),
+                    ptr(self.w_touched), self.ww.shape[0], 1, sp.l2, 1, ptr(self.opt), ptr(self.opt[8:]), s)
+            self._c("adam_table", "dl_adam_rows", ptr(self.table), ptr(self.tm), ptr(self.tv), ptr(self.tg),
+                    ptr(self.touched), self.table.shape[0], sp.E, 0.0, 1, ptr(self.opt), None, s)
+            return
+        # head Adam: L2 on the output weights only (deepfm_pipeline.py:183 / dnn_pipeline.py:131)
         self._c("adam_head", "dl_adam_dense", ptr(self.w_head), ptr(self.hm), ptr(self.hv), ptr(self.head_slab),
-             call_int("dl_head_grid", B), sp.fm_cols + H + 2, self.head_n, sp.l2, self.head_n - 1,
-             ptr(self.opt), ptr(self.w_head_prev), s)
+                hb, sp.fm_cols + H + 2, self.head_n, sp.l2, self.head_n - 1, ptr(self.opt), ptr(self.w_head_prev),
+                ptr(self.opt[8:]), s)
         if sp.fm:
-            self._c("adam_table", "dl_adam_rows", ptr(self.table), ptr(self.tm), ptr(self.tv), ptr(self.tg), ptr(self.touched),
-                 self.table.shape[0], sp.E, 0.0, 0, ptr(self.opt), s)
+            self._c("adam_table", "dl_adam_rows", ptr(self.table), ptr(self.tm), ptr(self.tv), ptr(self.tg),
+                    ptr(self.touched), self.table.shape[0], sp.E, 0.0, 0, ptr(self.opt), None, s)
             self._c("adam_first", "dl_adam_rows", ptr(self.first), ptr(self.fmm), ptr(self.fmv), ptr(self.fmg),
-                 ptr(self.touched), self.first.shape[0], 1, 0.0, 1, ptr(self.opt), s)
+                    ptr(self.touched), self.first.shape[0], 1, 0.0, 1, ptr(self.opt), None, s)
         else:
-            self._c("adam_table", "dl_adam_rows", ptr(self.table), ptr(self.tm), ptr(self.tv), ptr(self.tg), ptr(self.touched),
-                 self.table.shape[0], sp.E, 0.0, 1, ptr(self.opt), s)
+            self._c("adam_table", "dl_adam_rows", ptr(self.table), ptr(self.tm), ptr(self.tv), ptr(self.tg),
+                    ptr(self.touched), self.table.shape[0], sp.E, 0.0, 1, ptr(self.opt), None, s)
 
     def train_step(self, batch=None, graph=False):
         """One training step on `batch` (or on the already-staged slots if None)."""
@@ -472,13 +525,15 @@ class CTREngine:
         return self.score[:B].cpu().numpy()
 
     def loss(self):
-        """Loss of the last training step (data term + L2 on the pre-update head weights)."""
+        """Loss of the last training step: data term + the L2 terms on the pre-update
+        weights (accumulated by the Adam kernels into opt[8])."""
         sp = self.spec
         H = sp.hidden[-1]
         B = self.last_batch
-        data = self.head_slab[:, sp.fm_cols + H + 1].double().sum().item() / B
-        w = self.w_head_prev[: self.head_n - 1].double()
-        return data + sp.l2 * 0.5 * float((w * w).sum().item())
+        width = self.head_slab.shape[1]
+        rows = call_int("dl_head_grid", B)
+        data = self.head_slab[:rows, width - 1].double().sum().item() / B
+        return data + sp.l2 * 0.5 * float(self.opt[8].item())
 
     def check_error(self):
         if int(self.err[0].item()) != 0:

@@ -298,26 +298,26 @@ class ShardedCTREngine(CTREngine):
         for l in range(nl):
             off, sz = self.seg[l][1], self.seg[l][2]
             self._c("adam_dense_l%d" % l, "dl_adam_dense", ptr(self.W[l]), ptr(self.Wm[l]), ptr(self.Wv[l]),
-                    ptr(self.flat[off:]), 1, sz, sz, 0.0, 0, ptr(self.opt), None, s)
+                    ptr(self.flat[off:]), 1, sz, sz, 0.0, 0, ptr(self.opt), None, None, s)
         self._c("adam_head", "dl_adam_dense", ptr(self.w_head), ptr(self.hm), ptr(self.hv), ptr(self.flat[hoff:]),
-                1, self.head_w, self.head_n, sp.l2, self.head_n - 1, ptr(self.opt), ptr(self.w_head_prev), s)
+                1, self.head_w, self.head_n, sp.l2, self.head_n - 1, ptr(self.opt), ptr(self.w_head_prev), None, s)
         if rep:
             self.rep_g.view(-1)[: rg.numel()].copy_(rg.reshape(-1))
             self.rep_fg[: rg1.numel()].copy_(rg1)
             self.rep_touched[: self.rep] = 1
             call("dl_adam_rows", ptr(self.rep_t), ptr(self.rep_m), ptr(self.rep_v), ptr(self.rep_g),
-                 ptr(self.rep_touched), self.rep_t.shape[0], E, 0.0, 0, ptr(self.opt), s)
+                 ptr(self.rep_touched), self.rep_t.shape[0], E, 0.0, 0, ptr(self.opt), None, s)
             if sp.fm:
                 call("dl_adam_rows", ptr(self.rep_f), ptr(self.rep_fm), ptr(self.rep_fv), ptr(self.rep_fg),
-                     ptr(self.rep_touched), self.rep_f.shape[0], 1, 0.0, 0, ptr(self.opt), s)
+                     ptr(self.rep_touched), self.rep_f.shape[0], 1, 0.0, 0, ptr(self.opt), None, s)
         if sp.fm:
             self._c("adam_table", "dl_adam_rows", ptr(self.table), ptr(self.tm), ptr(self.tv), ptr(self.tg),
-                    ptr(self.touched), self.table.shape[0], E, 0.0, 0, ptr(self.opt), s)
+                    ptr(self.touched), self.table.shape[0], E, 0.0, 0, ptr(self.opt), None, s)
             self._c("adam_first", "dl_adam_rows", ptr(self.first), ptr(self.fmm), ptr(self.fmv), ptr(self.fmg),
-                    ptr(self.touched), self.first.shape[0], 1, 0.0, 1, ptr(self.opt), s)
+                    ptr(self.touched), self.first.shape[0], 1, 0.0, 1, ptr(self.opt), None, s)
         else:
             self._c("adam_table", "dl_adam_rows", ptr(self.table), ptr(self.tm), ptr(self.tv), ptr(self.tg),
-                    ptr(self.touched), self.table.shape[0], E, 0.0, 1, ptr(self.opt), s)
+                    ptr(self.touched), self.table.shape[0], E, 0.0, 1, ptr(self.opt), None, s)
         self.steps += 1
         self.last_batch = B
         self.last_loss_sum = None

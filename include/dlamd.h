@@ -193,25 +193,44 @@ int dl_head_fwd_bwd(int32_t B, int32_t fm_cols, int32_t H, const float* fm_out, 
                     float* dh, float* slab, int32_t slab_blocks, void* stream);
 int dl_head_grid(int32_t B);
 
+/* Wide&Deep cross logit, forward and backward fused (models/wdl.py:225-275):
+ * z = sum_f w[wide_f] + sum_j w[Fw+j] h_j + bias[0] (w = wdl_weights [w_rows]; the
+ * deep-output rows Fw..Fw+H alias wide ids); sigmoid + eps-log-loss as dl_head_fwd_bwd.
+ * Wide-row gradients dz go to g_w by f32 atomics (+ touched); the dense part leaves
+ * slab[block][0..H) = sum dz*h, [H] = sum dz, [H+1] = sum loss (fold with
+ * dl_slab_fold_rows into g_w rows Fw..Fw+H).  g_w = NULL: forward only (predict). */
+int dl_wdl_head_fwd_bwd(int32_t B, int32_t Fw, int32_t H, const int64_t* wide, int32_t wide_ld,
+                        const float* h, int32_t ldh, const float* w, const float* bias, int64_t w_rows,
+                        const float* label, float eps, float inv_batch, float* score, float* z_out,
+                        float* dz, float* dh, float* g_w, uint8_t* touched, float* slab,
+                        int32_t slab_blocks, int32_t* err, void* stream);
+/* g[row0+j] += sum over `blocks` slab rows of slab[blk*width + col0 + j], j < n. */
+int dl_slab_fold_rows(const float* slab, int32_t blocks, int32_t width, int32_t col0, int32_t n,
+                      float* g, int64_t row0, uint8_t* touched, void* stream);
+
 /* ------------------------------------------------------------------------
  * TF1 Adam (training_ops.cc ApplyAdam, dense semantics: every element's m, v
- * decay each step — SURVEY.md ledger item 6).  `opt` is a device float[8]:
+ * decay each step — SURVEY.md ledger item 6).  `opt` is a device float[16]:
  * [0] beta1_power [1] beta2_power [2] lr [3] alpha [4] beta1 [5] beta2
- * [6] epsilon [7] step (as float, exact < 2^24); dl_adam_begin_step computes
+ * [6] epsilon [7] step (as float, exact < 2^24), [8..15] per-step accumulators
+ * (zeroed by dl_adam_begin_step; sq_out targets); dl_adam_begin_step computes
  * alpha = lr_t*sqrt(1-b2p)/(1-b1p) with lr_t = lr*rate^floor(step/decay_steps)
  * and then advances b1p*=b1, b2p*=b2, step+=1 (TF's _finish + global_step). */
 int dl_adam_begin_step(float* opt, float decay_rate, float decay_steps, void* stream);
 /* Dense parameter whose gradient is the sum of `nslab` partial slabs
  * (g = sum_s slab[s*slab_stride + i]); l2 * p is added for i < l2_count;
- * p_prev (may be NULL) receives the pre-update values (the loss's L2 term). */
+ * p_prev (may be NULL) receives the pre-update values; sq_out (may be NULL) gets
+ * sum p_pre^2 over the L2-regularised elements added (atomically) — the loss's
+ * l2_regularizer term of the step, read back without copying the parameters. */
 int dl_adam_dense(float* p, float* m, float* v, const float* slab, int32_t nslab,
                   int64_t slab_stride, int64_t n, float l2, int64_t l2_count, const float* opt,
-                  float* p_prev, void* stream);
+                  float* p_prev, float* sq_out, void* stream);
 /* Embedding tables with dense-Adam semantics: g = g_table row if touched else 0;
  * consumed gradients are reset to 0; `clear_touched` resets the flags (pass 1
  * on the last table that shares them).  width = E (table) or 1 (first-order). */
 int dl_adam_rows(float* p, float* m, float* v, float* g, uint8_t* touched, int64_t n_rows,
-                 int32_t width, float l2, int32_t clear_touched, const float* opt, void* stream);
+                 int32_t width, float l2, int32_t clear_touched, const float* opt, float* sq_out,
+                 void* stream);
 
 /* ------------------------------------------------------------------------
  * Row-sharded tables (shard.hip).  Owner side of the all-to-all lookup:

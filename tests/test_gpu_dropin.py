@@ -81,3 +81,26 @@ def test_local_run_train_and_pred_end_to_end(hip_lib, tmp_path):
     fw = R.forward(cfg, P, b)
     auc_oracle = R.auc(b["label"], fw["p"])
     assert abs(auc_oracle - auc_gpu) < 1e-4
+
+
+def test_wdl_load_style_fit_evaluate_predict(hip_lib, tmp_path):
+    from deep_learning_amd.models import wdl
+    from deep_learning_amd.synthetic import make_batch
+    from deep_learning_amd.utils import data_loader_load as dll
+
+    class Args:
+        hidden_units, epochs, batch_size, learning_rate = [32, 16], 2, 64, 0.001
+        model_pb, learning_rate_decay_steps, learning_rate_decay_rate, l2_reg = str(tmp_path / "pb"), 10000000, 0.9, 1e-5
+        cont_field_size, cate_field_size, cate_index_size, embedding_size, wide_field_size = 13, 26, 4000, 8, 26
+        alg_name, vector_field_size = "wdl", 0
+    (tmp_path / "tr").mkdir()
+    (tmp_path / "va").mkdir()
+    dll.write_lines(str(tmp_path / "tr" / "part-0"), make_batch(300, cate_index_size=4000, seed=1, wide_fields=26))
+    dll.write_lines(str(tmp_path / "va" / "part-0"), make_batch(200, cate_index_size=4000, seed=2, wide_fields=26))
+    tr = dll.load_input_file(Args, str(tmp_path / "tr"))
+    va = dll.load_input_file(Args, str(tmp_path / "va"))
+    m = wdl.DeepModel(Args)
+    m.fit(tr, va)
+    auc_eval = m.evaluate(None, va)
+    auc_pred = m.predict(va)
+    assert abs(auc_eval - auc_pred) < 1e-6 and 0.0 < auc_pred < 1.0

@@ -21,6 +21,7 @@ CASES = {
     "dnn_pipeline": dict(C=13, V=3, S=26, E=8, cate_index_size=10000, hidden=[64, 32, 16]),
     "deepfm_multi_cate": dict(V=4, S=8, E=16, cate_index_size=6000, hidden=[48, 32],
                               multi_ranges=[[0, 30, "a"], [30, 50, "b"]]),
+    "wdl": dict(C=13, S=26, E=16, cate_index_size=8000, hidden=[64, 32], Fw=26),
 }
 
 
@@ -40,8 +41,8 @@ def _batches(name, kw, B, n, seed=11):
             multi[rng.random((B, W)) < 0.5] = 0
             b["cate_feats"] = np.concatenate([b["cate_feats"], multi], 1)
         else:
-            b = make_batch(B, cont=kw["C"], vector=kw["V"], cate_fields=kw["S"],
-                           cate_index_size=kw["cate_index_size"], seed=seed + i)
+            b = make_batch(B, cont=kw["C"], vector=kw.get("V", 0), cate_fields=kw["S"],
+                           cate_index_size=kw["cate_index_size"], seed=seed + i, wide_fields=kw.get("Fw", 0))
             b["cate_feats"][0, :4] = [0, 1, 5, 12]   # padding id + ids that alias cont rows
         out.append(b)
     return out

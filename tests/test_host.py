@@ -144,3 +144,21 @@ def test_oracle_reproduces_fixtures(name):
         np.testing.assert_array_equal(fw["z"], d["z%d" % i])
     for k in P:
         np.testing.assert_array_equal(P[k], d["final/" + k])
+
+
+def test_load_style_loader(tmp_path):
+    from deep_learning_amd.utils import data_loader_load as dll
+    import pickle
+
+    class MP:
+        alg_name, cont_field_size, cate_field_size, wide_field_size, batch_size, vector_field_size = \
+            "wdl", 13, 26, 26, 40, 0
+    b = make_batch(100, cate_index_size=5000, seed=3, wide_fields=26)
+    dll.write_lines(str(tmp_path / "part-0"), b)
+    out = dll.load_input_file(MP, str(tmp_path))
+    assert len(out) == 3                                  # last partial batch kept (40, 40, 20)
+    d0 = pickle.loads(out[0])
+    np.testing.assert_array_equal(d0["cate_feats"], b["cate_feats"][:40])
+    np.testing.assert_array_equal(d0["wide_feats"], b["wide_feats"][:40])
+    np.testing.assert_allclose(d0["cont_feats"], b["cont_feats"][:40])
+    assert pickle.loads(out[2])["labels"].shape == (20, 1)
