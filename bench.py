@@ -37,7 +37,7 @@ def log(*a):
     print("[bench %s]" % time.strftime("%H:%M:%S"), *a, file=sys.stderr, flush=True)
 
 
-def kernel_work(spec, B, touched_rows, rows=None):
+def kernel_work(spec, B, touched_rows, rows=None, uniq=None):
     """Algorithmic bytes / flops per launch."""
     E, S, C = spec.E, spec.S, spec.C
     N = rows if rows is not None else spec.n_rows
@@ -55,6 +55,15 @@ def kernel_work(spec, B, touched_rows, rows=None):
         w["gemm_dx_l%d" % l] = ("mfma", 2.0 * B * dims[l + 1] * (dims[l] if l else S * E))
     # backward scatter: FM + deep row gradients (f32 adds) + ids + dx0 read
     w["embed_bwd"] = ("hbm", B * (S * (E * 4 * 2 + 4 * 2 + 8) + S * E * 4))
+    if uniq is not None:
+        # row records (adam='lazy'): U unique rows of the batch, record = p, w1 triple + stamp, m, v
+        rec_b = (3 * E + 4) * 4
+        # gather: read U records, write the compact rows (E + 1 floats) + keys
+        w["rec_gather"] = ("hbm", uniq * (rec_b + (E + 1) * 4 + 4))
+        # indexed x0 assembly: 2S refs/sample x (compact row + inv) + first-order + x0 cat write
+        w["embed_fwd"] = ("hbm", B * (2 * S * (E * 4 + 4) + S * 4 + S * E * 4))
+        # fused backward + Adam: U records read + written, per ref: ref id + dx0/fm_sum row + dz
+        w["embed_bwd"] = ("hbm", uniq * (2 * rec_b + 4 + 8) + B * 2 * S * (4 + E * 4 + 4))
     H = spec.hidden[-1]
     w["head"] = ("hbm", B * (spec.fm_cols + H) * 4 * 2)
     return w
@@ -64,17 +73,20 @@ def kernel_work(spec, B, touched_rows, rows=None):
 PMC_KERNEL = {"adam_table": "adam_rows4_kernel", "adam_first": "adam_rows1_kernel",
               "embed_fwd": "embed_fwd_kernel<16, 5>", "embed_bwd": "embed_bwd_kernel<16, false>",
               "head": "head_kernel"}
+PMC_KERNEL_LAZY = {"rec_gather": "rec_gather_kernel<16>", "embed_bwd": "rec_bwd_adam_kernel<16>",
+                   "head": "head_kernel"}
 
 
-def pmc_traffic(label, world):
+def pmc_traffic(label, world, lazy=False):
     """HBM bytes per launch of `label` from the newest committed PMC summary
     (scripts/pmc_summary.py: (2*FETCH_SIZE + WRITE_SIZE)*1024, gfx950 correction)."""
     import glob
-    if world != 1 or label not in PMC_KERNEL:
+    names = PMC_KERNEL_LAZY if lazy else PMC_KERNEL
+    if world != 1 or label not in names:
         return None
     files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*", "pmc_summary.json")), key=os.path.getmtime)
     for f in reversed(files):
-        k = json.load(open(f))["kernels"].get(PMC_KERNEL[label])
+        k = json.load(open(f))["kernels"].get(names[label])
         if k and "hbm_bytes" in k:
             return {"hbm_bytes": int(k["hbm_bytes"]), "source": os.path.relpath(f, ROOT)}
     return None
@@ -116,6 +128,8 @@ def main():
     ap.add_argument("--vocab", type=int, default=0,
                     help="per-field vocab (default: 1M at N=1 = C2; 100M/26 at N>1 = C4's 100M-row table)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--adam", default="dense", choices=["dense", "lazy"],
+                    help="table Adam: dense sweep, or row records with lazy-exact catch-up (same result)")
     args = ap.parse_args()
 
     import torch
@@ -142,7 +156,7 @@ def main():
     log("rank %d/%d: building engine, table rows %d" % (rank, world, spec.n_rows))
     use_graph = world == 1
     if world == 1:
-        eng = CTREngine(spec, max_batch=B, seed=2019)
+        eng = CTREngine(spec, max_batch=B, seed=2019, adam=args.adam)
     else:
         from deep_learning_amd.shard import Exchange, ShardedCTREngine
         eng = ShardedCTREngine(spec, B, Exchange(), seed=2019)
@@ -192,7 +206,8 @@ def main():
     # unique rows touched per step (sets how much of the gradient table Adam reads)
     ids = dev_batches[0]["cate_feats"]
     touched_rows = int(torch.unique(torch.cat([ids.reshape(-1) + spec.C, ids.reshape(-1)])).numel()) + spec.C
-    work = kernel_work(spec, B, touched_rows, rows=getattr(eng, "local_rows", spec.n_rows))
+    uniq = int(eng.idx_n[0].item()) if getattr(eng, "lazy", False) else None
+    work = kernel_work(spec, B, touched_rows, rows=getattr(eng, "local_rows", spec.n_rows), uniq=uniq)
     kernels = {}
     for label, ts in times.items():
         us = float(np.mean(ts))
@@ -219,7 +234,7 @@ def main():
                 "unit": "TFLOP/s", "frac": round(ach / F32_MFMA_PEAK_TFLOPS, 3), "traffic": None,
                 "algorithmic_flops": amount}
     step_kernel_us = sum(k["us"] for k in kernels.values())
-    pmc = pmc_traffic(dom, world)
+    pmc = pmc_traffic(dom, world, lazy=uniq is not None)
     if pmc is not None:
         roof["traffic"] = pmc["hbm_bytes"]
         roof["traffic_source"] = pmc["source"]
@@ -253,7 +268,7 @@ def main():
                        "global_batch": B * world, "per_gpu_batch": B,
                        "parallelism": "dp%d" % world if world == 1 else
                        "dp%d + row-sharded table (RCCL all-to-all lookup, all-reduce dense grads)" % world,
-                       "id_dist": args.dist},
+                       "id_dist": args.dist, "table_adam": args.adam},
             "roofline": roof,
             "cpu_baseline": cpu,
             "kernels": kernels,

@@ -51,6 +51,33 @@ __device__ __forceinline__ int64_t checked_row(int64_t id, int64_t off, int64_t 
   return r;
 }
 
+// One TF1 ApplyAdam element update (training_ops.cc, non-Nesterov):
+//   m += (g - m)(1 - b1);  v += (g^2 - v)(1 - b2);  p -= m * alpha / (sqrt(v) + eps)
+// Shared by the dense sweep (optim.hip) and the lazy row-record path (rec.hip) so the
+// two compile to the same float operations: a zero-gradient step replayed later by
+// rec.hip's catch-up is bit-identical to the step the dense sweep would have taken.
+__device__ __forceinline__ void adam_elem(float& p, float& m, float& v, float g, float alpha,
+                                          float omb1, float omb2, float eps) {
+  m += (g - m) * omb1;
+  v += (g * g - v) * omb2;
+  p -= (m * alpha) / (sqrtf(v) + eps);
+}
+
+#define DL_DISPATCH_E(E, ...)                    \
+  switch (E) {                                   \
+    case 4: { constexpr int kE = 4; __VA_ARGS__; break; }   \
+    case 8: { constexpr int kE = 8; __VA_ARGS__; break; }   \
+    case 16: { constexpr int kE = 16; __VA_ARGS__; break; } \
+    case 32: { constexpr int kE = 32; __VA_ARGS__; break; } \
+    case 64: { constexpr int kE = 64; __VA_ARGS__; break; } \
+  }
+
+// Batch-index key (index.hip): (owner << 27) | local; owner == world marks a replicated row.
+__device__ __forceinline__ int64_t decode_key(uint32_t k, int world) {
+  const uint32_t owner = k >> 27, local = k & ((1u << 27) - 1);
+  return owner >= (uint32_t)world ? (int64_t)local : (int64_t)local * world + owner;
+}
+
 inline int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }
 
 }  // namespace dl

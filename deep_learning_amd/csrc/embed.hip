@@ -15,6 +15,7 @@
 //              cont-field rows (hit by every sample) accumulate in registers
 //              and leave the block once as a partial slab.
 #include "common.h"
+#include "segment.h"
 
 namespace dl {
 
@@ -508,15 +509,6 @@ static int emb_grid(int B) {
 
 using namespace dl;
 
-#define DL_DISPATCH_E(E, ...)                    \
-  switch (E) {                                   \
-    case 4: { constexpr int kE = 4; __VA_ARGS__; break; }   \
-    case 8: { constexpr int kE = 8; __VA_ARGS__; break; }   \
-    case 16: { constexpr int kE = 16; __VA_ARGS__; break; } \
-    case 32: { constexpr int kE = 32; __VA_ARGS__; break; } \
-    case 64: { constexpr int kE = 64; __VA_ARGS__; break; } \
-  }
-
 static int launch_embed_fwd(const dl_emb_layout* L, const EmbArgs& a, void* stream);
 
 extern "C" int dl_embed_fwd(const dl_emb_layout* L, const float* table, const float* first_order,
@@ -660,10 +652,6 @@ struct BwdSortedArgs {
   int compact;
 };
 
-__device__ __forceinline__ int64_t decode_key(uint32_t k, int world) {
-  const uint32_t owner = k >> 27, local = k & ((1u << 27) - 1);
-  return owner >= (uint32_t)world ? (int64_t)local : (int64_t)local * world + owner;
-}
 
 template <int E>
 __global__ __launch_bounds__(256) void embed_bwd_sorted_kernel(BwdSortedArgs a) {
@@ -675,45 +663,27 @@ __global__ __launch_bounds__(256) void embed_bwd_sorted_kernel(BwdSortedArgs a) 
   const int ns = (L.use_fm ? S : 0) + S;
   const int Cf = (L.use_fm && L.fm_cont) ? L.cont_fields : 0;
   const int F = Cf + S + L.fm_extra;
-  // every index derived from another kernel's output is clamped: a stale or
-  // racing index can cost accuracy, never an out-of-bounds access
   const long long nrefs = (long long)L.batch * ns;
-  int nu = a.n_uniq[0];
-  nu = nu < 0 ? 0 : (nu > nrefs ? (int)nrefs : nu);
+  const int nu = clamp_uniq(a.n_uniq, nrefs);
   const long long group = ((long long)blockIdx.x * blockDim.x + threadIdx.x) / 64 * RPI + r;
   const long long ngroups = (long long)gridDim.x * blockDim.x / 64 * RPI;
   const float wsec = L.use_fm ? a.w_head[F + d] : 0.f;
+  const SegGradIn sg{L, a.seg_off, a.refs, a.dz, a.w_head, a.fm_sum, a.dx0};
   for (long long u = group; u < nu; u += ngroups) {
-    const int e0 = max(0, a.seg_off[u]), e1 = min((int)nrefs, a.seg_off[u + 1]);
-    float acc_s = 0.f, acc_d = 0.f, acc_x = 0.f, g1 = 0.f;
-    for (int e = e0; e < e1; ++e) {
-      const int k = a.refs[e];
-      if (k < 0 || k >= nrefs) continue;
-      const int b = k / ns, sl = k % ns;
-      if (L.use_fm && sl < S) {
-        const float dzb = a.dz[b];
-        const float ds = dzb * wsec;
-        acc_s += ds * a.fm_sum[(long long)b * E + d];
-        acc_d += ds;
-        g1 += dzb * a.w_head[Cf + sl];
-      } else {
-        const int f = L.use_fm ? sl - S : sl;
-        acc_x += a.dx0[(long long)b * L.dx0_ld + L.dx0_cat_col + f * E + d];
-      }
-    }
+    const SegGrad sgr = segment_grad<E>(sg, u, d, nrefs, wsec);
     const uint32_t key = a.uniq[u];
     const int64_t row = decode_key(key, a.world);
     if (row < 0 || row >= L.n_rows) continue;
     float v = 0.f;
-    if (acc_d != 0.f) v = a.rows_u ? a.rows_u[u * E + d] : a.table[row * E + d];
-    const float g = acc_s - v * acc_d + acc_x;
+    if (sgr.dsum != 0.f) v = a.rows_u ? a.rows_u[u * E + d] : a.table[row * E + d];
+    const float g = sgr.s - v * sgr.dsum + sgr.x;
     if (a.compact) {
       a.g_out[u * E + d] = g;
-      if (a.g1_out && d == 0) a.g1_out[u] = g1;
+      if (a.g1_out && d == 0) a.g1_out[u] = sgr.g1;
     } else {
       a.g_out[row * E + d] = g;
       if (d == 0) {
-        if (a.g1_out && L.use_fm) a.g1_out[row] = g1;
+        if (a.g1_out && L.use_fm) a.g1_out[row] = sgr.g1;
         a.touched[row] = 1;
       }
     }

@@ -25,12 +25,6 @@ __global__ void adam_begin_kernel(float* opt, float decay_rate, float decay_step
   for (int i = 8; i < 16; ++i) opt[i] = 0.f;                     // per-step L2 accumulators
 }
 
-__device__ __forceinline__ void adam_elem(float& p, float& m, float& v, float g, float alpha,
-                                          float omb1, float omb2, float eps) {
-  m += (g - m) * omb1;
-  v += (g * g - v) * omb2;
-  p -= (m * alpha) / (sqrtf(v) + eps);
-}
 
 // Dense parameter, gradient = sum of partial slabs (+ l2 * p for i < l2_count).
 __global__ __launch_bounds__(256) void adam_dense_thread_kernel(float* __restrict__ p, float* __restrict__ m,

@@ -1,0 +1,320 @@
+// Lazy-exact TF1 Adam on interleaved embedding row records.
+//
+// The reference applies the DENSE Adam update to the embedding table every step
+// (deepfm_pipeline.py:184-188; the gradient reaches the Variable densified, SURVEY.md
+// ledger item 6): every row's m and v decay and every row with m != 0 moves, even
+// when the batch never referenced it.  Sweeping p, m, v of a 26M x 16 table is
+// ~10.4 GB of HBM traffic per step — the single largest cost of the step.
+//
+// Here a row that the batch does not reference is left alone and its pending
+// zero-gradient steps are replayed ("caught up") the next time it is read:
+//   for j = stamp+1 .. target:   adam_elem(p, m, v, g = 0, alpha_j)
+// with alpha_j from a ring of per-step alphas written by dl_adam_hist_record.
+// adam_elem is the same inline function the dense sweep uses (common.h), so the
+// replayed steps are the same float operations in the same order: the result is
+// bit-identical to the dense update, only the time at which it is computed moves.
+// The host bounds every row's lag below the ring length by calling dl_rec_flush
+// (catch every row up) at least once per hist_len steps, and before any export.
+//
+// Row record (rec_ld floats, rec_ld % 32 == 0 so a record starts a 128-B line):
+//   [0, E)        p                   (the embedding row)
+//   E .. E+2      w1, m(w1), v(w1)    (FM first-order weight of the row, if any)
+//   E+3           stamp               (int32 bits: last step applied to the row)
+//   [E+4, 2E+4)   m
+//   [2E+4, 3E+4)  v
+// p and w1 share the first 128-B line: the forward's useful bytes sit together,
+// and one record is two lines for E = 16.
+#include "common.h"
+#include "segment.h"
+
+namespace dl {
+
+struct RecCfg {
+  int E, ld, has_first, hist_mask;
+  float omb1, omb2, eps;   // filled on the device from opt (rec_load_hyper)
+};
+
+__device__ __forceinline__ void rec_load_hyper(RecCfg& c, const float* opt) {
+  c.omb1 = 1.f - opt[4];
+  c.omb2 = 1.f - opt[5];
+  c.eps = opt[6];
+}
+
+// Replays zero-gradient steps (from, to] on one float4 of p/m/v (and the
+// first-order triple when `first` is set).
+__device__ __forceinline__ void catch_up4(float4& p, float4& m, float4& v, float& w, float& wm, float& wv,
+                                          bool first, int from, int to, const float* __restrict__ hist,
+                                          const RecCfg& c) {
+  if (to - from > c.hist_mask + 1) from = to - (c.hist_mask + 1);   // host bounds the lag; never read past the ring
+  for (int j = from + 1; j <= to; ++j) {
+    const float al = hist[j & c.hist_mask];
+    adam_elem(p.x, m.x, v.x, 0.f, al, c.omb1, c.omb2, c.eps);
+    adam_elem(p.y, m.y, v.y, 0.f, al, c.omb1, c.omb2, c.eps);
+    adam_elem(p.z, m.z, v.z, 0.f, al, c.omb1, c.omb2, c.eps);
+    adam_elem(p.w, m.w, v.w, 0.f, al, c.omb1, c.omb2, c.eps);
+    if (first) adam_elem(w, wm, wv, 0.f, al, c.omb1, c.omb2, c.eps);
+  }
+}
+
+__device__ __forceinline__ void catch_up1(float& p, float& m, float& v, float& w, float& wm, float& wv,
+                                          bool first, int from, int to, const float* __restrict__ hist,
+                                          const RecCfg& c) {
+  if (to - from > c.hist_mask + 1) from = to - (c.hist_mask + 1);
+  for (int j = from + 1; j <= to; ++j) {
+    const float al = hist[j & c.hist_mask];
+    adam_elem(p, m, v, 0.f, al, c.omb1, c.omb2, c.eps);
+    if (first) adam_elem(w, wm, wv, 0.f, al, c.omb1, c.omb2, c.eps);
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Forward gather of the batch's rows, caught up to step opt[7] - lag:
+//   out[i] = p(row_i), out1[i] = w1(row_i),   row_i = i (i < n_rep), else uniq[i - n_rep]
+// Records are only read: the catch-up is recomputed (cheaply, in registers) by the
+// backward's update, which is the one that writes.  E/4 lanes per row, float4 each.
+template <int E>
+__global__ __launch_bounds__(256) void rec_gather_kernel(const float* __restrict__ rec, RecCfg c, int64_t n_rows,
+                                                         int n_rep, const uint32_t* __restrict__ uniq,
+                                                         const int32_t* __restrict__ n_uniq, long long max_u,
+                                                         int world, const float* __restrict__ hist,
+                                                         const float* __restrict__ opt, int lag,
+                                                         float* __restrict__ out, float* __restrict__ out1) {
+  rec_load_hyper(c, opt);
+  constexpr int LPR = E / 4;
+  const long long gt = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  const int q = (int)(gt % LPR);
+  const long long group0 = gt / LPR, ngroups = (long long)gridDim.x * blockDim.x / LPR;
+  const long long total = n_rep + (long long)clamp_uniq(n_uniq, max_u);
+  const int target = (int)opt[7] - lag;
+  for (long long i = group0; i < total; i += ngroups) {
+    const int64_t row = i < n_rep ? i : decode_key(uniq[i - n_rep], world);
+    float4 p = make_float4(0.f, 0.f, 0.f, 0.f);
+    float w = 0.f;
+    if (row >= 0 && row < n_rows) {
+      const float* r = rec + row * c.ld;
+      p = *reinterpret_cast<const float4*>(r + 4 * q);
+      const float4 tail = *reinterpret_cast<const float4*>(r + E);
+      const int stamp = __float_as_int(tail.w);
+      w = tail.x;
+      if (stamp < target) {
+        float4 m = *reinterpret_cast<const float4*>(r + E + 4 + 4 * q);
+        float4 v = *reinterpret_cast<const float4*>(r + 2 * E + 4 + 4 * q);
+        float wm = tail.y, wv = tail.z;
+        catch_up4(p, m, v, w, wm, wv, c.has_first && q == 0, stamp, target, hist, c);
+      }
+    }
+    *reinterpret_cast<float4*>(out + i * E + 4 * q) = p;
+    if (out1 && q == 0) out1[i] = w;
+  }
+}
+
+// One row's step-t update: catch up to t-1, then apply gradient (g, g1) with alpha_t.
+// Lane d of an E-lane group owns dim d; lane 0 also owns the first-order triple and
+// the stamp (every lane reads the stamp before lane 0 rewrites it: same wave).
+__device__ __forceinline__ void rec_update(float* __restrict__ r, int E, int d, float g, float g1, int t,
+                                           float alpha_t, const float* __restrict__ hist, const RecCfg& c) {
+  const int stamp = __float_as_int(r[E + 3]);
+  float p = r[d], m = r[E + 4 + d], v = r[2 * E + 4 + d];
+  const bool first = c.has_first && d == 0;
+  float w = 0.f, wm = 0.f, wv = 0.f;
+  if (first) { w = r[E]; wm = r[E + 1]; wv = r[E + 2]; }
+  if (stamp < t - 1) catch_up1(p, m, v, w, wm, wv, first, stamp, t - 1, hist, c);
+  adam_elem(p, m, v, g, alpha_t, c.omb1, c.omb2, c.eps);
+  r[d] = p; r[E + 4 + d] = m; r[2 * E + 4 + d] = v;
+  if (first) {
+    adam_elem(w, wm, wv, g1, alpha_t, c.omb1, c.omb2, c.eps);
+    r[E] = w; r[E + 1] = wm; r[E + 2] = wv;
+  }
+  if (d == 0) r[E + 3] = __int_as_float(t);
+}
+
+// Backward + Adam fused: per unique row of the batch, the ordered segment sum of its
+// references (segment.h) is applied to the record immediately — no gradient table,
+// no atomics, no touched flags.  Replicated rows (row < n_rep, hit by every sample
+// through the FM cont fields) only deposit their cate-reference gradient into
+// g_rep/g1_rep; dl_rec_apply_rows updates them after the cont part is added.
+template <int E>
+__global__ __launch_bounds__(256) void rec_bwd_adam_kernel(SegGradIn sg, float* __restrict__ rec, RecCfg c,
+                                                           int n_rep, const float* __restrict__ rows_u,
+                                                           const uint32_t* __restrict__ uniq,
+                                                           const int32_t* __restrict__ n_uniq, int world,
+                                                           float* __restrict__ g_rep, float* __restrict__ g1_rep,
+                                                           const float* __restrict__ hist,
+                                                           const float* __restrict__ opt) {
+  rec_load_hyper(c, opt);
+  constexpr int RPI = 64 / E;
+  const dl_emb_layout& L = sg.L;
+  const int lane = threadIdx.x & 63;
+  const int rr = lane / E, d = lane % E;
+  const int S = L.cate_fields;
+  const int ns = (L.use_fm ? S : 0) + S;
+  const int Cf = (L.use_fm && L.fm_cont) ? L.cont_fields : 0;
+  const int F = Cf + S + L.fm_extra;
+  const long long nrefs = (long long)L.batch * ns;
+  const int nu = clamp_uniq(n_uniq, nrefs);
+  const long long group = ((long long)blockIdx.x * blockDim.x + threadIdx.x) / 64 * RPI + rr;
+  const long long ngroups = (long long)gridDim.x * blockDim.x / 64 * RPI;
+  const float wsec = L.use_fm ? sg.w_head[F + d] : 0.f;
+  const int t = (int)opt[7];
+  const float alpha_t = opt[3];
+  for (long long u = group; u < nu; u += ngroups) {
+    const SegGrad s = segment_grad<E>(sg, u, d, nrefs, wsec);
+    const int64_t row = decode_key(uniq[u], world);
+    if (row < 0 || row >= L.n_rows) continue;
+    const float v = s.dsum != 0.f ? rows_u[u * E + d] : 0.f;
+    const float g = s.s - v * s.dsum + s.x;
+    if (row < n_rep) {
+      g_rep[row * E + d] += g;
+      if (g1_rep && d == 0) g1_rep[row] += s.g1;
+      continue;
+    }
+    rec_update(rec + row * c.ld, E, d, g, s.g1, t, alpha_t, hist, c);
+  }
+}
+
+// Rows [row0, row0 + n) updated with dense gradients g [n][E], g1 [n] (then zeroed).
+__global__ __launch_bounds__(256) void rec_apply_rows_kernel(float* __restrict__ rec, RecCfg c, long long row0,
+                                                             long long n, float* __restrict__ g,
+                                                             float* __restrict__ g1, const float* __restrict__ hist,
+                                                             const float* __restrict__ opt) {
+  rec_load_hyper(c, opt);
+  const int E = c.E;
+  const int t = (int)opt[7];
+  const float alpha_t = opt[3];
+  for (long long k = (long long)blockIdx.x * blockDim.x + threadIdx.x; k < n * E;
+       k += (long long)gridDim.x * blockDim.x) {
+    const long long i = k / E;
+    const int d = (int)(k % E);
+    const float gi = g[k];
+    const float g1i = (g1 && d == 0) ? g1[i] : 0.f;
+    rec_update(rec + (row0 + i) * c.ld, E, d, gi, g1i, t, alpha_t, hist, c);
+    g[k] = 0.f;
+    if (g1 && d == 0) g1[i] = 0.f;
+  }
+}
+
+// Every row caught up to step opt[7] (zero-gradient steps only).
+template <int E>
+__global__ __launch_bounds__(256) void rec_flush_kernel(float* __restrict__ rec, RecCfg c, long long n_rows,
+                                                        const float* __restrict__ hist,
+                                                        const float* __restrict__ opt) {
+  rec_load_hyper(c, opt);
+  constexpr int LPR = E / 4;
+  const long long gt = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  const int q = (int)(gt % LPR);
+  const int target = (int)opt[7];
+  for (long long row = gt / LPR; row < n_rows; row += (long long)gridDim.x * blockDim.x / LPR) {
+    float* r = rec + row * c.ld;
+    const float4 tail = *reinterpret_cast<const float4*>(r + E);
+    const int stamp = __float_as_int(tail.w);
+    if (stamp >= target) continue;
+    float4 p = *reinterpret_cast<const float4*>(r + 4 * q);
+    float4 m = *reinterpret_cast<const float4*>(r + E + 4 + 4 * q);
+    float4 v = *reinterpret_cast<const float4*>(r + 2 * E + 4 + 4 * q);
+    float w = tail.x, wm = tail.y, wv = tail.z;
+    const bool first = c.has_first && q == 0;
+    catch_up4(p, m, v, w, wm, wv, first, stamp, target, hist, c);
+    *reinterpret_cast<float4*>(r + 4 * q) = p;
+    *reinterpret_cast<float4*>(r + E + 4 + 4 * q) = m;
+    *reinterpret_cast<float4*>(r + 2 * E + 4 + 4 * q) = v;
+    if (q == 0) *reinterpret_cast<float4*>(r + E) = make_float4(w, wm, wv, __int_as_float(target));
+  }
+}
+
+__global__ void hist_record_kernel(const float* opt, float* hist, int mask) {
+  hist[(int)opt[7] & mask] = opt[3];
+}
+
+static int rec_check(int E, int ld, int hist_len) {
+  DL_CHECK_ARG(E == 4 || E == 8 || E == 16 || E == 32 || E == 64, "emb_dim %d not in {4,8,16,32,64}", E);
+  DL_CHECK_ARG(ld >= 3 * E + 4 && ld % 32 == 0, "rec_ld %d: need >= 3E+4 and a multiple of 32", ld);
+  DL_CHECK_ARG(hist_len >= 2 && (hist_len & (hist_len - 1)) == 0, "hist_len %d must be a power of two", hist_len);
+  return 0;
+}
+
+static unsigned grid_cap(long long threads) {
+  long long b = (threads + 255) / 256;
+  if (b > 8192) b = 8192;
+  return (unsigned)(b < 1 ? 1 : b);
+}
+
+}  // namespace dl
+
+using namespace dl;
+
+extern "C" int dl_adam_hist_record(const float* opt, float* hist, int32_t hist_len, void* stream) {
+  DL_CHECK_ARG(opt && hist && hist_len >= 2 && (hist_len & (hist_len - 1)) == 0, "bad hist");
+  hipLaunchKernelGGL(hist_record_kernel, dim3(1), dim3(1), 0, as_stream(stream), opt, hist, hist_len - 1);
+  DL_RETURN_LAUNCH("dl_adam_hist_record");
+}
+
+extern "C" int dl_rec_gather(const dl_emb_layout* L, const float* rec, int32_t rec_ld, int32_t has_first,
+                             int32_t n_rep, const uint32_t* uniq_keys, const int32_t* n_uniq, int64_t max_uniq,
+                             int32_t world, const float* hist, int32_t hist_len, const float* opt, int32_t lag,
+                             float* rows_u, float* rows_u1, void* stream) {
+  DL_CHECK_ARG(L && rec && hist && opt && rows_u, "NULL argument");
+  if (int rc = rec_check(L->emb_dim, rec_ld, hist_len)) return rc;
+  DL_CHECK_ARG(n_rep >= 0 && n_rep <= L->n_rows && world >= 1, "bad n_rep/world");
+  DL_CHECK_ARG(max_uniq == 0 || (uniq_keys && n_uniq), "uniq keys required");
+  DL_CHECK_ARG(!has_first || rows_u1, "rows_u1 required with first-order weights");
+  const long long total = n_rep + (max_uniq > 0 ? max_uniq : 0);
+  if (total == 0) return 0;
+  DL_DISPATCH_E(L->emb_dim, {
+    const unsigned grid = grid_cap(total * (kE / 4));
+    hipLaunchKernelGGL(rec_gather_kernel<kE>, dim3(grid), dim3(256), 0, as_stream(stream), rec,
+                       RecCfg{kE, rec_ld, has_first, hist_len - 1, 0.f, 0.f, 0.f}, (int64_t)L->n_rows, n_rep,
+                       uniq_keys, n_uniq, (long long)max_uniq, world, hist, opt, lag, rows_u,
+                       has_first ? rows_u1 : nullptr);
+  });
+  DL_RETURN_LAUNCH("dl_rec_gather");
+}
+
+extern "C" int dl_rec_bwd_adam(const dl_emb_layout* L, float* rec, int32_t rec_ld, int32_t has_first, int32_t n_rep,
+                               const float* rows_u, const uint32_t* uniq_keys, const int32_t* seg_off,
+                               const int32_t* n_uniq, const int32_t* sorted_refs, int32_t world, int64_t max_uniq,
+                               const float* dz, const float* w_head, const float* fm_sum, const float* dx0,
+                               float* g_rep, float* g1_rep, const float* hist, int32_t hist_len, const float* opt,
+                               void* stream) {
+  DL_CHECK_ARG(L && rec && rows_u && uniq_keys && seg_off && n_uniq && sorted_refs && dx0 && hist && opt,
+               "NULL argument");
+  if (int rc = rec_check(L->emb_dim, rec_ld, hist_len)) return rc;
+  DL_CHECK_ARG(!L->use_fm || (dz && w_head && fm_sum), "FM backward inputs required");
+  DL_CHECK_ARG(n_rep == 0 || g_rep, "g_rep required with replicated rows");
+  DL_CHECK_ARG(!(n_rep && has_first) || g1_rep, "g1_rep required");
+  if (max_uniq <= 0) return 0;
+  const SegGradIn sg{*L, seg_off, sorted_refs, dz, w_head, fm_sum, dx0};
+  DL_DISPATCH_E(L->emb_dim, {
+    const unsigned grid = grid_cap(max_uniq * kE);
+    hipLaunchKernelGGL(rec_bwd_adam_kernel<kE>, dim3(grid), dim3(256), 0, as_stream(stream), sg, rec,
+                       RecCfg{kE, rec_ld, has_first, hist_len - 1, 0.f, 0.f, 0.f}, n_rep, rows_u, uniq_keys,
+                       n_uniq, world, g_rep, has_first ? g1_rep : nullptr, hist, opt);
+  });
+  DL_RETURN_LAUNCH("dl_rec_bwd_adam");
+}
+
+extern "C" int dl_rec_apply_rows(float* rec, int32_t rec_ld, int32_t emb_dim, int32_t has_first, int64_t row0,
+                                 int64_t n, float* g, float* g1, const float* hist, int32_t hist_len,
+                                 const float* opt, void* stream) {
+  DL_CHECK_ARG(rec && g && hist && opt, "NULL argument");
+  if (int rc = rec_check(emb_dim, rec_ld, hist_len)) return rc;
+  DL_CHECK_ARG(!has_first || g1, "g1 required with first-order weights");
+  DL_CHECK_ARG(row0 >= 0 && n >= 0, "bad row range");
+  if (n == 0) return 0;
+  hipLaunchKernelGGL(rec_apply_rows_kernel, dim3(grid_cap(n * emb_dim)), dim3(256), 0, as_stream(stream), rec,
+                     RecCfg{emb_dim, rec_ld, has_first, hist_len - 1, 0.f, 0.f, 0.f}, (long long)row0,
+                     (long long)n, g, has_first ? g1 : nullptr, hist, opt);
+  DL_RETURN_LAUNCH("dl_rec_apply_rows");
+}
+
+extern "C" int dl_rec_flush(float* rec, int32_t rec_ld, int32_t emb_dim, int32_t has_first, int64_t n_rows,
+                            const float* hist, int32_t hist_len, const float* opt, void* stream) {
+  DL_CHECK_ARG(rec && hist && opt, "NULL argument");
+  if (int rc = rec_check(emb_dim, rec_ld, hist_len)) return rc;
+  if (n_rows <= 0) return 0;
+  DL_DISPATCH_E(emb_dim, {
+    hipLaunchKernelGGL(rec_flush_kernel<kE>, dim3(grid_cap(n_rows * (kE / 4))), dim3(256), 0, as_stream(stream),
+                       rec, RecCfg{kE, rec_ld, has_first, hist_len - 1, 0.f, 0.f, 0.f}, (long long)n_rows, hist,
+                       opt);
+  });
+  DL_RETURN_LAUNCH("dl_rec_flush");
+}

@@ -114,7 +114,7 @@ class ModelSpec:
 
 class CTREngine:
     def __init__(self, spec, max_batch, device="cuda", seed=2019, init="device", bwd="atomic",
-                 table_rows=None):
+                 table_rows=None, adam="dense", hist_len=4096):
         if not torch.cuda.is_available():
             raise _lib.DLError("CTREngine needs a HIP device (no CPU fallback)")
         _lib.lib()
@@ -141,14 +141,35 @@ class CTREngine:
         self.dx_ld = _ru(max(self.dx_cols, 4), 4)
         # ---- parameters + Adam state
         rows_pad = _ru(table_rows if table_rows is not None else N, 16)
-        self.table = z(rows_pad, E)
-        self.tm, self.tv, self.tg = z(rows_pad, E), z(rows_pad, E), z(rows_pad, E)
-        self.touched = z(rows_pad, dt=torch.uint8)
-        if sp.fm:
-            self.first = z(rows_pad)
-            self.fmm, self.fmv, self.fmg = z(rows_pad), z(rows_pad), z(rows_pad)
-        else:
+        self.rows_pad = rows_pad
+        if adam not in ("dense", "lazy"):
+            raise ValueError("adam must be 'dense' or 'lazy'")
+        self.lazy = adam == "lazy"
+        if self.lazy:
+            # row records + lazy-exact Adam (rec.hip); needs the batch index
+            if sp.M:
+                raise ValueError("adam='lazy' does not support multi-hot slots yet")
+            bwd = "sorted"
+            self.rec_ld = _ru(3 * E + 4, 32)
+            self.rec = z(rows_pad, self.rec_ld)
+            self.hist_len = hist_len
+            self.hist = z(hist_len)
+            self.n_rep = sp.C if sp.model == "deepfm_pipeline" else 0     # FM cont-field rows
+            R = max(self.n_rep, 1)
+            self.g_rep, self.g1_rep = z(_ru(R * E, 4)), z(_ru(R, 4))
+            self.rep_touched = z(_ru(R, 16), dt=torch.uint8)
+            self.since_flush = 0
+            self.table = self.tm = self.tv = self.tg = self.touched = None
             self.first = self.fmm = self.fmv = self.fmg = None
+        else:
+            self.table = z(rows_pad, E)
+            self.tm, self.tv, self.tg = z(rows_pad, E), z(rows_pad, E), z(rows_pad, E)
+            self.touched = z(rows_pad, dt=torch.uint8)
+            if sp.fm:
+                self.first = z(rows_pad)
+                self.fmm, self.fmv, self.fmg = z(rows_pad), z(rows_pad), z(rows_pad)
+            else:
+                self.first = self.fmm = self.fmv = self.fmg = None
         self.W = [z(self.in_ld[l], self.out_ld[l]) for l in range(len(sp.hidden))]
         self.Wm = [torch.zeros_like(w) for w in self.W]
         self.Wv = [torch.zeros_like(w) for w in self.W]
@@ -205,6 +226,10 @@ class CTREngine:
             self.idx_uniq = z(self.n_refs, dt=torch.int32)
             self.idx_off = z(self.n_refs + 1, dt=torch.int32)
             self.idx_n = z(4, dt=torch.int32)
+            self.idx_inv = z(self.n_refs, dt=torch.int32) if self.lazy else None
+        if self.lazy:
+            self.rows_u = z(self.n_rep + self.n_refs, E)
+            self.rows_u1 = z(self.n_rep + self.n_refs)
         # static input slots (graph capture reads from these)
         self.in_label = z(B)
         self.in_cont = z(B, max(sp.C, 1))
@@ -251,6 +276,9 @@ class CTREngine:
         first-order ~ U[0,1), dense weights/biases ~ N(0, glorot) (numpy, seeded)."""
         sp = self.spec
         s = _lib.stream_handle()
+        if self.lazy:   # same values as the dense engine: initialise dense, then pack
+            self.table = torch.zeros(self.rows_pad, sp.E, device=self.dev)
+            self.first = torch.zeros(self.rows_pad, device=self.dev) if sp.fm else None
         if self.wdl:   # xavier_initializer (wdl.py:44-47): U(-lim, lim), lim = sqrt(6/(N+E))
             lim = math.sqrt(6.0 / (self.N + sp.E))
             call("dl_init_random", ptr(self.table), self.table.numel(), 1, -lim, 2 * lim, seed, 0, s)
@@ -262,6 +290,9 @@ class CTREngine:
             call("dl_init_random", ptr(self.table), self.table.numel(), 0, 0.0, 0.01, seed, 0, s)
         if self.first is not None:
             call("dl_init_random", ptr(self.first), self.first.numel(), 1, 0.0, 1.0, seed + 1, 0, s)
+        if self.lazy:
+            self._pack(self.table, self.first)
+            self.table = self.first = None
         rng = np.random.default_rng(seed)
         dims = [self.D0] + sp.hidden
         for l in range(len(sp.hidden)):
@@ -290,12 +321,18 @@ class CTREngine:
         """Inject reference-layout parameters (dict of numpy arrays as in oracle/ctr_ref.py)."""
         sp = self.spec
         N = self.N
-        self.table.zero_()
         tab = P["weight_mat"] if self.wdl else P["feats_emb"]
-        self.table[:N].copy_(torch.from_numpy(np.ascontiguousarray(tab, np.float32)))
-        if self.first is not None:
-            self.first.zero_()
-            self.first[:N].copy_(torch.from_numpy(np.ascontiguousarray(P["fm_first_order_emb"][:, 0], np.float32)))
+        tab = torch.from_numpy(np.ascontiguousarray(tab, np.float32))
+        first = (torch.from_numpy(np.ascontiguousarray(P["fm_first_order_emb"][:, 0], np.float32))
+                 if sp.fm else None)
+        if self.lazy:
+            self._pack(tab.to(self.dev), first.to(self.dev) if first is not None else None)
+        else:
+            self.table.zero_()
+            self.table[:N].copy_(tab)
+            if self.first is not None:
+                self.first.zero_()
+                self.first[:N].copy_(first)
         for l in range(len(sp.hidden)):
             self._set_layer(l, P["deep_%d" % l], P["deep_bias_%d" % l])
         if self.wdl:
@@ -317,9 +354,16 @@ class CTREngine:
         """Export parameters in the reference layout (numpy)."""
         sp = self.spec
         N = self.N
-        P = {("weight_mat" if self.wdl else "feats_emb"): self.table[:N].cpu().numpy()}
-        if self.first is not None:
-            P["fm_first_order_emb"] = self.first[:N].cpu().numpy()[:, None]
+        if self.lazy:
+            self.flush()
+            rec = self.rec[:N]
+            P = {("weight_mat" if self.wdl else "feats_emb"): rec[:, : sp.E].cpu().numpy()}
+            if sp.fm:
+                P["fm_first_order_emb"] = rec[:, sp.E: sp.E + 1].cpu().numpy()
+        else:
+            P = {("weight_mat" if self.wdl else "feats_emb"): self.table[:N].cpu().numpy()}
+            if self.first is not None:
+                P["fm_first_order_emb"] = self.first[:N].cpu().numpy()[:, None]
         dims = [self.D0] + sp.hidden
         for l in range(len(sp.hidden)):
             Wi = self.W[l].cpu().numpy()
@@ -340,6 +384,62 @@ class CTREngine:
         else:
             P["deep_res"], P["deep_res_bias"] = w[:-1, None].copy(), w[-1:].reshape(1, 1).copy()
         return P
+
+    # ------------------------------------------------------------------ row records
+    def _pack(self, table, first):
+        """Dense table (+ first-order) -> row records with zero Adam moments, stamped
+        with the current step (a fully caught-up state)."""
+        E = self.spec.E
+        n = table.shape[0]
+        self.rec.zero_()
+        self.rec[:n, :E].copy_(table)
+        if first is not None:
+            self.rec[: first.shape[0], E].copy_(first)
+        self.rec.view(torch.int32)[:, E + 3] = int(self.opt[7].item())
+        self.since_flush = 0
+        torch.cuda.synchronize()
+
+    def flush(self):
+        """Catch every row record up to the current step (no-op for the dense engine)."""
+        if not self.lazy:
+            return
+        self._c("rec_flush", "dl_rec_flush", ptr(self.rec), self.rec_ld, self.spec.E, int(self.spec.fm),
+                self.rec.shape[0], ptr(self.hist), self.hist_len, ptr(self.opt), _lib.stream_handle())
+        self.since_flush = 0
+
+    def adam_state(self):
+        """Table Adam state in the dense layout (tests): dict of m, v (+ m1, v1) as numpy."""
+        E, N = self.spec.E, self.N
+        if not self.lazy:
+            d = {"m": self.tm[:N].cpu().numpy(), "v": self.tv[:N].cpu().numpy()}
+            if self.first is not None:
+                d["m1"], d["v1"] = self.fmm[:N].cpu().numpy(), self.fmv[:N].cpu().numpy()
+            return d
+        self.flush()
+        r = self.rec[:N]
+        d = {"m": r[:, E + 4: 2 * E + 4].cpu().numpy(), "v": r[:, 2 * E + 4: 3 * E + 4].cpu().numpy()}
+        if self.spec.fm:
+            d["m1"], d["v1"] = r[:, E + 1].cpu().numpy(), r[:, E + 2].cpu().numpy()
+        return d
+
+    def set_adam_state(self, d):
+        """Inverse of adam_state(); for records, stamps the rows with the current step."""
+        E, N = self.spec.E, self.N
+        t = lambda k: torch.from_numpy(np.ascontiguousarray(d[k], np.float32)).to(self.dev)
+        if not self.lazy:
+            self.tm[:N].copy_(t("m"))
+            self.tv[:N].copy_(t("v"))
+            if self.first is not None and "m1" in d:
+                self.fmm[:N].copy_(t("m1"))
+                self.fmv[:N].copy_(t("v1"))
+            return
+        self.rec[:N, E + 4: 2 * E + 4].copy_(t("m"))
+        self.rec[:N, 2 * E + 4: 3 * E + 4].copy_(t("v"))
+        if self.spec.fm and "m1" in d:
+            self.rec[:N, E + 1].copy_(t("m1"))
+            self.rec[:N, E + 2].copy_(t("v1"))
+        self.rec.view(torch.int32)[:, E + 3] = int(self.opt[7].item())
+        self.since_flush = 0
 
     # ------------------------------------------------------------------ inputs
     def stage(self, batch):
@@ -383,9 +483,18 @@ class CTREngine:
             self._c("pool_fwd", "dl_pool_fwd", C_ref(L), ptr(self.table), ptr(self.first) if sp.fm else None,
                  ptr(self.in_cate), sp.S, ptr(self.slot_start), ptr(self.slot_end), sp.M, sp.S,
                  ptr(self.x0), ptr(self.fm_out), ptr(self.cnt_emb), ptr(self.cnt_first), ptr(self.err), s)
-        self._c("embed_fwd", "dl_embed_fwd", C_ref(L), ptr(self.table), ptr(self.first), ptr(self.in_cate),
-             ptr(self.in_cont), ptr(self.in_vec), ptr(self.x0), ptr(self.fm_out), ptr(self.fm_sum),
-             ptr(self.err), s)
+        if self.lazy:
+            # rows of the batch (index built by _pre), caught up to the step being taken
+            self._c("rec_gather", "dl_rec_gather", C_ref(L), ptr(self.rec), self.rec_ld, int(sp.fm), self.n_rep,
+                    ptr(self.idx_uniq), ptr(self.idx_n), B * self.n_slot, 1, ptr(self.hist), self.hist_len,
+                    ptr(self.opt), 1 if train else 0, ptr(self.rows_u), ptr(self.rows_u1), s)
+            self._c("embed_fwd", "dl_embed_fwd_indexed", C_ref(L), ptr(self.rows_u),
+                    ptr(self.rows_u1) if sp.fm else None, ptr(self.idx_inv), self.n_rep, ptr(self.in_cont),
+                    ptr(self.in_vec), ptr(self.x0), ptr(self.fm_out), ptr(self.fm_sum), s)
+        else:
+            self._c("embed_fwd", "dl_embed_fwd", C_ref(L), ptr(self.table), ptr(self.first), ptr(self.in_cate),
+                    ptr(self.in_cont), ptr(self.in_vec), ptr(self.x0), ptr(self.fm_out), ptr(self.fm_sum),
+                    ptr(self.err), s)
         x = self.x0
         for l, hdim in enumerate(sp.hidden):
             self._c("gemm_fwd_l%d" % l, "dl_gemm_f32", 0, 0, B, hdim, self.in_ld[l], ptr(x), self.in_ld[l], ptr(self.W[l]),
@@ -414,15 +523,19 @@ class CTREngine:
         s = _lib.stream_handle()
         L = self.layout
         L.batch = B
-        self._c("index_build", "dl_index_build", C_ref(L), ptr(self.in_cate), 1, 0, ptr(self.idx_ws),
+        self._c("index_build", "dl_index_build", C_ref(L), ptr(self.in_cate), 1,
+                self.n_rep if self.lazy else 0, ptr(self.idx_ws),
                 self.idx_ws.numel(), ptr(self.idx_keys), ptr(self.idx_refs), ptr(self.idx_uniq),
-                ptr(self.idx_off), ptr(self.idx_n), None, None, ptr(self.err), s)
+                ptr(self.idx_off), ptr(self.idx_n), ptr(self.idx_inv) if self.lazy else None, None,
+                ptr(self.err), s)
 
     def _train(self, B):
         sp = self.spec
         s = _lib.stream_handle()
         L = self.layout
         self._c("adam_begin", "dl_adam_begin_step", ptr(self.opt), sp.decay_rate, float(sp.decay_steps), s)
+        if self.lazy:
+            self._c("adam_hist", "dl_adam_hist_record", ptr(self.opt), ptr(self.hist), self.hist_len, s)
         self._forward(B, s, train=True)
         nl = len(sp.hidden)
         splits = max(1, min(self.splits, B // 1024))
@@ -447,7 +560,22 @@ class CTREngine:
                     ptr(self.opt[8:]) if self.wdl else None, s)
         # embedding backward (uses pre-update table and head weights)
         bwd_blocks = call_int("dl_embed_bwd_grid", C_ref(L))
-        if self.bwd == "sorted":
+        if self.lazy:
+            E, R = sp.E, self.n_rep
+            self._c("embed_bwd", "dl_rec_bwd_adam", C_ref(L), ptr(self.rec), self.rec_ld, int(sp.fm), R,
+                    ptr(self.rows_u[R:]), ptr(self.idx_uniq), ptr(self.idx_off), ptr(self.idx_n),
+                    ptr(self.idx_refs), 1, B * self.n_slot, ptr(self.dz), ptr(self.w_head), ptr(self.fm_sum),
+                    ptr(self.dx0), ptr(self.g_rep), ptr(self.g1_rep), ptr(self.hist), self.hist_len,
+                    ptr(self.opt), s)
+            if R:
+                # FM cont-field rows: per-block register partials, folded into g_rep, then updated
+                self._c("cont_bwd", "dl_embed_cont_bwd", C_ref(L), ptr(self.rows_u), ptr(self._cont()),
+                        ptr(self.dz), ptr(self.w_head), ptr(self.fm_sum), ptr(self.cont_slab), self.bwd_blocks, s)
+                self._c("cont_reduce", "dl_embed_cont_reduce", C_ref(L), ptr(self.cont_slab), bwd_blocks,
+                        ptr(self.g_rep), ptr(self.g1_rep), ptr(self.rep_touched), s)
+                self._c("adam_rep", "dl_rec_apply_rows", ptr(self.rec), self.rec_ld, E, int(sp.fm), 0, R,
+                        ptr(self.g_rep), ptr(self.g1_rep), ptr(self.hist), self.hist_len, ptr(self.opt), s)
+        elif self.bwd == "sorted":
             self._c("embed_bwd", "dl_embed_bwd_sorted", C_ref(L), ptr(self.table), None, ptr(self.idx_uniq),
                     ptr(self.idx_off), ptr(self.idx_n), ptr(self.idx_refs), 1, B * self.n_slot, ptr(self.dz),
                     ptr(self.w_head), ptr(self.fm_sum), ptr(self.dx0), ptr(self.tg), ptr(self.fmg),
@@ -458,8 +586,9 @@ class CTREngine:
             self._c("embed_bwd", "dl_embed_bwd", C_ref(L), ptr(self.table), ptr(self.in_cate), ptr(self._cont()),
                     ptr(self.dz), ptr(self.w_head), ptr(self.fm_sum), ptr(self.dx0), ptr(self.tg), ptr(self.fmg),
                     ptr(self.touched), ptr(self.cont_slab), self.bwd_blocks, s)
-        self._c("cont_reduce", "dl_embed_cont_reduce", C_ref(L), ptr(self.cont_slab), bwd_blocks, ptr(self.tg),
-                ptr(self.fmg), ptr(self.touched), s)
+        if not self.lazy:
+            self._c("cont_reduce", "dl_embed_cont_reduce", C_ref(L), ptr(self.cont_slab), bwd_blocks, ptr(self.tg),
+                    ptr(self.fmg), ptr(self.touched), s)
         if sp.M:
             self._c("pool_bwd", "dl_pool_bwd", C_ref(L), ptr(self.in_cate), sp.S, ptr(self.slot_start), ptr(self.slot_end),
                  sp.M, sp.S, ptr(self.x0), ptr(self.fm_sum), ptr(self.dz), ptr(self.w_head), ptr(self.dx0),
@@ -476,6 +605,8 @@ class CTREngine:
                     ptr(self.head_slab[:, H:]), hb, H + 2, 1, 0.0, 0, ptr(self.opt), None, None, s)
             self._c("adam_wide", "dl_adam_rows", ptr(self.ww), ptr(self.wm), ptr(self.wv), ptr(self.wg),
                     ptr(self.w_touched), self.ww.shape[0], 1, sp.l2, 1, ptr(self.opt), ptr(self.opt[8:]), s)
+            if self.lazy:
+                return
             self._c("adam_table", "dl_adam_rows", ptr(self.table), ptr(self.tm), ptr(self.tv), ptr(self.tg),
                     ptr(self.touched), self.table.shape[0], sp.E, 0.0, 1, ptr(self.opt), None, s)
             return
@@ -483,6 +614,8 @@ class CTREngine:
         self._c("adam_head", "dl_adam_dense", ptr(self.w_head), ptr(self.hm), ptr(self.hv), ptr(self.head_slab),
                 hb, sp.fm_cols + H + 2, self.head_n, sp.l2, self.head_n - 1, ptr(self.opt), ptr(self.w_head_prev),
                 ptr(self.opt[8:]), s)
+        if self.lazy:
+            return
         if sp.fm:
             self._c("adam_table", "dl_adam_rows", ptr(self.table), ptr(self.tm), ptr(self.tv), ptr(self.tg),
                     ptr(self.touched), self.table.shape[0], sp.E, 0.0, 0, ptr(self.opt), None, s)
@@ -495,6 +628,11 @@ class CTREngine:
     def train_step(self, batch=None, graph=False):
         """One training step on `batch` (or on the already-staged slots if None)."""
         B = self.stage(batch) if batch is not None else self.B
+        if self.lazy:
+            # every row's lag must stay below the alpha ring (rec.hip)
+            if self.since_flush >= self.hist_len - 2:
+                self.flush()
+            self.since_flush += 1
         self._pre(B)
         if graph:
             if self.graph is None or self.graph_batch != B:
@@ -520,6 +658,7 @@ class CTREngine:
         """Forward only: returns sigmoid scores [B] (host numpy)."""
         B = self.stage(batch)
         s = _lib.stream_handle()
+        self._pre(B)
         self._forward(B, s)
         self.check_error()
         return self.score[:B].cpu().numpy()

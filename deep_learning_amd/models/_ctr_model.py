@@ -163,10 +163,8 @@ class CTRModel:
 
 def _adam_state(eng):
     out = {"adam/opt": eng.opt.cpu().numpy(), "adam/steps": np.array([eng.steps])}
-    for name in ("tm", "tv", "fmm", "fmv", "hm", "hv"):
-        t = getattr(eng, name)
-        if t is not None:
-            out["adam/" + name] = t.cpu().numpy()
+    out.update({"adam/table_" + k: v for k, v in eng.adam_state().items()})
+    out["adam/hm"], out["adam/hv"] = eng.hm.cpu().numpy(), eng.hv.cpu().numpy()
     for l in range(len(eng.W)):
         out["adam/Wm%d" % l] = eng.Wm[l].cpu().numpy()
         out["adam/Wv%d" % l] = eng.Wv[l].cpu().numpy()
@@ -176,9 +174,9 @@ def _adam_state(eng):
 def _load_adam_state(eng, d):
     eng.opt.copy_(torch.from_numpy(d["adam/opt"]))
     eng.steps = int(d["adam/steps"][0])
-    for name in ("tm", "tv", "fmm", "fmv", "hm", "hv"):
-        if "adam/" + name in d.files and getattr(eng, name) is not None:
-            getattr(eng, name).copy_(torch.from_numpy(d["adam/" + name]))
+    eng.set_adam_state({k[len("adam/table_"):]: d[k] for k in d.files if k.startswith("adam/table_")})
+    eng.hm.copy_(torch.from_numpy(d["adam/hm"]))
+    eng.hv.copy_(torch.from_numpy(d["adam/hv"]))
     for l in range(len(eng.W)):
         eng.Wm[l].copy_(torch.from_numpy(d["adam/Wm%d" % l]))
         eng.Wv[l].copy_(torch.from_numpy(d["adam/Wv%d" % l]))

@@ -233,6 +233,44 @@ int dl_adam_rows(float* p, float* m, float* v, float* g, uint8_t* touched, int64
                  void* stream);
 
 /* ------------------------------------------------------------------------
+ * Lazy-exact Adam on interleaved row records (rec.hip).  Same result as the
+ * dense sweep of dl_adam_rows (bit-identical: the skipped zero-gradient steps
+ * are replayed with the same float operations when a row is next read), but a
+ * step only touches the rows its batch references.  Record of rec_ld floats
+ * (rec_ld >= 3E+4, multiple of 32): [p(E) | w1 m1 v1 stamp | m(E) | v(E) | pad];
+ * stamp = int32 bits of the last step applied.  hist = ring of hist_len (power
+ * of two) per-step alphas; the caller keeps every row's lag < hist_len by
+ * calling dl_rec_flush at least once per hist_len steps.
+ * Replaces, for the table and first-order Variables, the dense ApplyAdam of
+ * deepfm_pipeline.py:184-188 / dnn_pipeline.py:132-136 / wdl.py:277-285. */
+/* hist[step & (hist_len-1)] = alpha of the step dl_adam_begin_step just began. */
+int dl_adam_hist_record(const float* opt, float* hist, int32_t hist_len, void* stream);
+/* rows_u[i] = p(row_i) caught up to step opt[7]-lag (rows_u1[i] = w1), row_i = i
+ * for i < n_rep (replicated rows) else the row of uniq_keys[i-n_rep] (batch index,
+ * dl_index_build keys).  Read only. lag = 1 inside a training step, 0 for predict. */
+int dl_rec_gather(const dl_emb_layout* L, const float* rec, int32_t rec_ld, int32_t has_first,
+                  int32_t n_rep, const uint32_t* uniq_keys, const int32_t* n_uniq, int64_t max_uniq,
+                  int32_t world, const float* hist, int32_t hist_len, const float* opt, int32_t lag,
+                  float* rows_u, float* rows_u1, void* stream);
+/* Fused backward + Adam: per unique row the ordered segment sum of its references
+ * (as dl_embed_bwd_sorted; rows_u = the gathered rows of uniq order) is applied to
+ * the record (catch-up to step t-1, then step t).  Rows < n_rep instead add their
+ * gradient into g_rep[row][E] / g1_rep[row] (finished by dl_rec_apply_rows). */
+int dl_rec_bwd_adam(const dl_emb_layout* L, float* rec, int32_t rec_ld, int32_t has_first, int32_t n_rep,
+                    const float* rows_u, const uint32_t* uniq_keys, const int32_t* seg_off,
+                    const int32_t* n_uniq, const int32_t* sorted_refs, int32_t world, int64_t max_uniq,
+                    const float* dz, const float* w_head, const float* fm_sum, const float* dx0,
+                    float* g_rep, float* g1_rep, const float* hist, int32_t hist_len, const float* opt,
+                    void* stream);
+/* Rows [row0, row0+n): step-t update with dense gradients g[n][E], g1[n] (zeroed after). */
+int dl_rec_apply_rows(float* rec, int32_t rec_ld, int32_t emb_dim, int32_t has_first, int64_t row0,
+                      int64_t n, float* g, float* g1, const float* hist, int32_t hist_len,
+                      const float* opt, void* stream);
+/* Every row caught up to step opt[7] (before export/checkpoint, and every hist_len steps). */
+int dl_rec_flush(float* rec, int32_t rec_ld, int32_t emb_dim, int32_t has_first, int64_t n_rows,
+                 const float* hist, int32_t hist_len, const float* opt, void* stream);
+
+/* ------------------------------------------------------------------------
  * Row-sharded tables (shard.hip).  Owner side of the all-to-all lookup:
  * out[i] = table[ids[i]], out_first[i] = first[ids[i]] (first may be NULL);
  * and of the gradient return: G[ids[i]] += g[i] (f32 atomics: a row may come

@@ -48,16 +48,21 @@ def _batches(name, kw, B, n, seed=11):
     return out
 
 
-@pytest.mark.parametrize("bwd", ["atomic", "sorted"])
+@pytest.mark.parametrize("bwd", ["atomic", "sorted", "lazy"])
 @pytest.mark.parametrize("name", list(CASES))
 @pytest.mark.parametrize("B", [256, 1536])
 def test_train_steps_match_oracle(hip_lib, name, B, bwd):
     kw = CASES[name]
     model = _model(name)
+    if bwd == "lazy" and kw.get("multi_ranges"):
+        pytest.skip("row records: single-hot models only")
     cfg = R.make_cfg(model, **kw)
     spec = ModelSpec(model, **kw)
     P = R.init_params(cfg, np.random.default_rng(42))
-    eng = CTREngine(spec, max_batch=B, init="none", bwd=bwd)
+    if bwd == "lazy":
+        eng = CTREngine(spec, max_batch=B, init="none", adam="lazy")
+    else:
+        eng = CTREngine(spec, max_batch=B, init="none", bwd=bwd)
     eng.load_params(P)
     opt = R.AdamTF1(cfg, P)
     for step, b in enumerate(_batches(name, kw, B, 4)):
@@ -84,3 +89,33 @@ def test_graph_replay_equals_eager(hip_lib):
         torch.cuda.synchronize()
         res.append(eng.z[:512].cpu().numpy())
     np.testing.assert_allclose(res[0], res[1], atol=1e-6)
+
+
+@pytest.mark.parametrize("name", ["deepfm_pipeline", "dnn_pipeline", "wdl"])
+def test_lazy_adam_bit_identical_to_dense(hip_lib, name):
+    """Row records + lazy catch-up (rec.hip) against the dense sweep with the same
+    (sorted, deterministic) gradients: parameters, Adam moments, logits and
+    predictions must be bit-identical.  A large table, a small batch and an 8-entry
+    alpha ring make rows lag many steps and force periodic flushes."""
+    kw = dict(CASES[name], cate_index_size=50000)
+    model = _model(name)
+    spec = ModelSpec(model, **kw)
+    dense = CTREngine(spec, max_batch=128, seed=3, bwd="sorted")
+    lazy = CTREngine(spec, max_batch=128, seed=3, adam="lazy", hist_len=8)
+    np.testing.assert_array_equal(lazy.params()["weight_mat" if model == "wdl" else "feats_emb"],
+                                  dense.params()["weight_mat" if model == "wdl" else "feats_emb"])
+    bs = _batches(name, kw, 128, 21, seed=7)
+    for i, b in enumerate(bs):
+        dense.train_step(b, graph=i >= 3)
+        lazy.train_step(b, graph=i >= 3)
+        torch.cuda.synchronize()
+        np.testing.assert_array_equal(lazy.z[:128].cpu().numpy(), dense.z[:128].cpu().numpy(),
+                                      err_msg="logits step %d" % i)
+        if i == 10:
+            np.testing.assert_array_equal(lazy.predict(bs[0]), dense.predict(bs[0]))
+    pd, pl = dense.params(), lazy.params()
+    for k in pd:
+        np.testing.assert_array_equal(pl[k], pd[k], err_msg=k)
+    sd, sl = dense.adam_state(), lazy.adam_state()
+    for k in sd:
+        np.testing.assert_array_equal(sl[k], sd[k], err_msg=k)
