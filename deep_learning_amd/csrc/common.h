@@ -56,10 +56,12 @@ __device__ __forceinline__ int64_t checked_row(int64_t id, int64_t off, int64_t 
 // Shared by the dense sweep (optim.hip) and the lazy row-record path (rec.hip) so the
 // two compile to the same float operations: a zero-gradient step replayed later by
 // rec.hip's catch-up is bit-identical to the step the dense sweep would have taken.
+// The fusions are spelled out with fmaf: left to -ffp-contract, the backend fuses
+// per call site (it kept one first-order update unfused), which broke that identity.
 __device__ __forceinline__ void adam_elem(float& p, float& m, float& v, float g, float alpha,
                                           float omb1, float omb2, float eps) {
-  m += (g - m) * omb1;
-  v += (g * g - v) * omb2;
+  m = fmaf(g - m, omb1, m);
+  v = fmaf(fmaf(g, g, -v), omb2, v);
   p -= (m * alpha) / (sqrtf(v) + eps);
 }
 

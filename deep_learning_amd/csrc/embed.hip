@@ -676,7 +676,7 @@ __global__ __launch_bounds__(256) void embed_bwd_sorted_kernel(BwdSortedArgs a) 
     if (row < 0 || row >= L.n_rows) continue;
     float v = 0.f;
     if (sgr.dsum != 0.f) v = a.rows_u ? a.rows_u[u * E + d] : a.table[row * E + d];
-    const float g = sgr.s - v * sgr.dsum + sgr.x;
+    const float g = seg_row_grad(sgr.s, sgr.dsum, sgr.x, v);
     if (a.compact) {
       a.g_out[u * E + d] = g;
       if (a.g1_out && d == 0) a.g1_out[u] = sgr.g1;

@@ -78,7 +78,8 @@ __global__ __launch_bounds__(256) void rec_gather_kernel(const float* __restrict
                                                          const int32_t* __restrict__ n_uniq, long long max_u,
                                                          int world, const float* __restrict__ hist,
                                                          const float* __restrict__ opt, int lag,
-                                                         float* __restrict__ out, float* __restrict__ out1) {
+                                                         float* __restrict__ out, float* __restrict__ out1,
+                                                         float* __restrict__ mv) {
   rec_load_hyper(c, opt);
   constexpr int LPR = E / 4;
   const long long gt = (long long)blockIdx.x * blockDim.x + threadIdx.x;
@@ -88,23 +89,27 @@ __global__ __launch_bounds__(256) void rec_gather_kernel(const float* __restrict
   const int target = (int)opt[7] - lag;
   for (long long i = group0; i < total; i += ngroups) {
     const int64_t row = i < n_rep ? i : decode_key(uniq[i - n_rep], world);
-    float4 p = make_float4(0.f, 0.f, 0.f, 0.f);
-    float w = 0.f;
+    const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
+    float4 p = z, m = z, v = z;
+    float w = 0.f, wm = 0.f, wv = 0.f;
     if (row >= 0 && row < n_rows) {
       const float* r = rec + row * c.ld;
       p = *reinterpret_cast<const float4*>(r + 4 * q);
+      m = *reinterpret_cast<const float4*>(r + E + 4 + 4 * q);
+      v = *reinterpret_cast<const float4*>(r + 2 * E + 4 + 4 * q);
       const float4 tail = *reinterpret_cast<const float4*>(r + E);
       const int stamp = __float_as_int(tail.w);
-      w = tail.x;
-      if (stamp < target) {
-        float4 m = *reinterpret_cast<const float4*>(r + E + 4 + 4 * q);
-        float4 v = *reinterpret_cast<const float4*>(r + 2 * E + 4 + 4 * q);
-        float wm = tail.y, wv = tail.z;
-        catch_up4(p, m, v, w, wm, wv, c.has_first && q == 0, stamp, target, hist, c);
-      }
+      w = tail.x; wm = tail.y; wv = tail.z;
+      if (stamp < target) catch_up4(p, m, v, w, wm, wv, c.has_first && q == 0, stamp, target, hist, c);
     }
     *reinterpret_cast<float4*>(out + i * E + 4 * q) = p;
     if (out1 && q == 0) out1[i] = w;
+    if (mv) {   // caught-up moments for the backward's update: [m(E) | v(E) | m1 v1 0 0]
+      float* o = mv + i * (2 * E + 4);
+      *reinterpret_cast<float4*>(o + 4 * q) = m;
+      *reinterpret_cast<float4*>(o + E + 4 * q) = v;
+      if (q == 0) *reinterpret_cast<float4*>(o + 2 * E) = make_float4(wm, wv, 0.f, 0.f);
+    }
   }
 }
 
@@ -129,46 +134,75 @@ __device__ __forceinline__ void rec_update(float* __restrict__ r, int E, int d, 
 }
 
 // Backward + Adam fused: per unique row of the batch, the ordered segment sum of its
-// references (segment.h) is applied to the record immediately — no gradient table,
-// no atomics, no touched flags.  Replicated rows (row < n_rep, hit by every sample
-// through the FM cont fields) only deposit their cate-reference gradient into
-// g_rep/g1_rep; dl_rec_apply_rows updates them after the cont part is added.
+// references (segment.h) is applied at once — no gradient table, no atomics, no
+// touched flags.  The row's caught-up state comes from the gather's compact outputs
+// (p: rows_u, w1: rows_u1, m/v: mv), read in u order, so the record is only WRITTEN
+// here (one random 208-B store per row instead of a read-modify-write).
+// Replicated rows (row < n_rep, hit by every sample through the FM cont fields)
+// only deposit their cate-reference gradient into g_rep/g1_rep; dl_rec_apply_rows
+// updates them after the cont part is added.  E/4 lanes per row, float4 each.
 template <int E>
 __global__ __launch_bounds__(256) void rec_bwd_adam_kernel(SegGradIn sg, float* __restrict__ rec, RecCfg c,
                                                            int n_rep, const float* __restrict__ rows_u,
+                                                           const float* __restrict__ rows_u1,
+                                                           const float* __restrict__ mv,
                                                            const uint32_t* __restrict__ uniq,
                                                            const int32_t* __restrict__ n_uniq, int world,
                                                            float* __restrict__ g_rep, float* __restrict__ g1_rep,
-                                                           const float* __restrict__ hist,
                                                            const float* __restrict__ opt) {
   rec_load_hyper(c, opt);
-  constexpr int RPI = 64 / E;
+  constexpr int LPR = E / 4;
   const dl_emb_layout& L = sg.L;
-  const int lane = threadIdx.x & 63;
-  const int rr = lane / E, d = lane % E;
+  const long long gt = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  const int q = (int)(gt % LPR);
+  const long long group0 = gt / LPR, ngroups = (long long)gridDim.x * blockDim.x / LPR;
   const int S = L.cate_fields;
   const int ns = (L.use_fm ? S : 0) + S;
   const int Cf = (L.use_fm && L.fm_cont) ? L.cont_fields : 0;
   const int F = Cf + S + L.fm_extra;
   const long long nrefs = (long long)L.batch * ns;
   const int nu = clamp_uniq(n_uniq, nrefs);
-  const long long group = ((long long)blockIdx.x * blockDim.x + threadIdx.x) / 64 * RPI + rr;
-  const long long ngroups = (long long)gridDim.x * blockDim.x / 64 * RPI;
-  const float wsec = L.use_fm ? sg.w_head[F + d] : 0.f;
+  // head weights of the FM second-order outputs (offset F: not 16-B aligned)
+  const float* ws = sg.w_head + F + 4 * q;
+  const float4 wsec = L.use_fm ? make_float4(ws[0], ws[1], ws[2], ws[3]) : make_float4(0.f, 0.f, 0.f, 0.f);
   const int t = (int)opt[7];
-  const float alpha_t = opt[3];
-  for (long long u = group; u < nu; u += ngroups) {
-    const SegGrad s = segment_grad<E>(sg, u, d, nrefs, wsec);
+  const float alpha = opt[3];
+  const bool first = c.has_first && q == 0;
+  for (long long u = group0; u < nu; u += ngroups) {
     const int64_t row = decode_key(uniq[u], world);
+    // the row's caught-up state (independent of the segment walk: issued first)
+    const long long iu = n_rep + u;
+    float4 p = *reinterpret_cast<const float4*>(rows_u + iu * E + 4 * q);
+    const float* o = mv + iu * (2 * E + 4);
+    float4 m = *reinterpret_cast<const float4*>(o + 4 * q);
+    float4 v = *reinterpret_cast<const float4*>(o + E + 4 * q);
+    float w = 0.f, wm = 0.f, wv = 0.f;
+    if (first) { w = rows_u1[iu]; wm = o[2 * E]; wv = o[2 * E + 1]; }
+    const SegGrad4 s = segment_grad4<E>(sg, u, q, nrefs, wsec);
     if (row < 0 || row >= L.n_rows) continue;
-    const float v = s.dsum != 0.f ? rows_u[u * E + d] : 0.f;
-    const float g = s.s - v * s.dsum + s.x;
+    float4 g;
+    g.x = seg_row_grad(s.s.x, s.dsum.x, s.x.x, s.dsum.x != 0.f ? p.x : 0.f);
+    g.y = seg_row_grad(s.s.y, s.dsum.y, s.x.y, s.dsum.y != 0.f ? p.y : 0.f);
+    g.z = seg_row_grad(s.s.z, s.dsum.z, s.x.z, s.dsum.z != 0.f ? p.z : 0.f);
+    g.w = seg_row_grad(s.s.w, s.dsum.w, s.x.w, s.dsum.w != 0.f ? p.w : 0.f);
     if (row < n_rep) {
-      g_rep[row * E + d] += g;
-      if (g1_rep && d == 0) g1_rep[row] += s.g1;
+      float* gr = g_rep + row * E + 4 * q;
+      gr[0] += g.x; gr[1] += g.y; gr[2] += g.z; gr[3] += g.w;
+      if (g1_rep && q == 0) g1_rep[row] += s.g1;
       continue;
     }
-    rec_update(rec + row * c.ld, E, d, g, s.g1, t, alpha_t, hist, c);
+    adam_elem(p.x, m.x, v.x, g.x, alpha, c.omb1, c.omb2, c.eps);
+    adam_elem(p.y, m.y, v.y, g.y, alpha, c.omb1, c.omb2, c.eps);
+    adam_elem(p.z, m.z, v.z, g.z, alpha, c.omb1, c.omb2, c.eps);
+    adam_elem(p.w, m.w, v.w, g.w, alpha, c.omb1, c.omb2, c.eps);
+    float* r = rec + row * c.ld;
+    *reinterpret_cast<float4*>(r + 4 * q) = p;
+    *reinterpret_cast<float4*>(r + E + 4 + 4 * q) = m;
+    *reinterpret_cast<float4*>(r + 2 * E + 4 + 4 * q) = v;
+    if (q == 0) {
+      if (first) adam_elem(w, wm, wv, s.g1, alpha, c.omb1, c.omb2, c.eps);
+      *reinterpret_cast<float4*>(r + E) = make_float4(w, wm, wv, __int_as_float(t));
+    }
   }
 }
 
@@ -251,7 +285,7 @@ extern "C" int dl_adam_hist_record(const float* opt, float* hist, int32_t hist_l
 extern "C" int dl_rec_gather(const dl_emb_layout* L, const float* rec, int32_t rec_ld, int32_t has_first,
                              int32_t n_rep, const uint32_t* uniq_keys, const int32_t* n_uniq, int64_t max_uniq,
                              int32_t world, const float* hist, int32_t hist_len, const float* opt, int32_t lag,
-                             float* rows_u, float* rows_u1, void* stream) {
+                             float* rows_u, float* rows_u1, float* mv_u, void* stream) {
   DL_CHECK_ARG(L && rec && hist && opt && rows_u, "NULL argument");
   if (int rc = rec_check(L->emb_dim, rec_ld, hist_len)) return rc;
   DL_CHECK_ARG(n_rep >= 0 && n_rep <= L->n_rows && world >= 1, "bad n_rep/world");
@@ -264,30 +298,33 @@ extern "C" int dl_rec_gather(const dl_emb_layout* L, const float* rec, int32_t r
     hipLaunchKernelGGL(rec_gather_kernel<kE>, dim3(grid), dim3(256), 0, as_stream(stream), rec,
                        RecCfg{kE, rec_ld, has_first, hist_len - 1, 0.f, 0.f, 0.f}, (int64_t)L->n_rows, n_rep,
                        uniq_keys, n_uniq, (long long)max_uniq, world, hist, opt, lag, rows_u,
-                       has_first ? rows_u1 : nullptr);
+                       has_first ? rows_u1 : nullptr, mv_u);
   });
   DL_RETURN_LAUNCH("dl_rec_gather");
 }
 
 extern "C" int dl_rec_bwd_adam(const dl_emb_layout* L, float* rec, int32_t rec_ld, int32_t has_first, int32_t n_rep,
-                               const float* rows_u, const uint32_t* uniq_keys, const int32_t* seg_off,
-                               const int32_t* n_uniq, const int32_t* sorted_refs, int32_t world, int64_t max_uniq,
-                               const float* dz, const float* w_head, const float* fm_sum, const float* dx0,
-                               float* g_rep, float* g1_rep, const float* hist, int32_t hist_len, const float* opt,
-                               void* stream) {
-  DL_CHECK_ARG(L && rec && rows_u && uniq_keys && seg_off && n_uniq && sorted_refs && dx0 && hist && opt,
+                               const float* rows_u, const float* rows_u1, const float* mv_u,
+                               const uint32_t* uniq_keys, const int32_t* seg_off, const int32_t* n_uniq,
+                               const int32_t* sorted_refs, int32_t world, int64_t max_uniq, const float* dz,
+                               const float* w_head, const float* fm_sum, const float* dx0, float* g_rep,
+                               float* g1_rep, const float* opt, void* stream) {
+  DL_CHECK_ARG(L && rec && rows_u && mv_u && uniq_keys && seg_off && n_uniq && sorted_refs && dx0 && opt,
                "NULL argument");
-  if (int rc = rec_check(L->emb_dim, rec_ld, hist_len)) return rc;
+  if (int rc = rec_check(L->emb_dim, rec_ld, 2)) return rc;
   DL_CHECK_ARG(!L->use_fm || (dz && w_head && fm_sum), "FM backward inputs required");
+  DL_CHECK_ARG(!has_first || rows_u1, "rows_u1 required with first-order weights");
   DL_CHECK_ARG(n_rep == 0 || g_rep, "g_rep required with replicated rows");
   DL_CHECK_ARG(!(n_rep && has_first) || g1_rep, "g1_rep required");
+  DL_CHECK_ARG(L->dx0_ld % 4 == 0 && L->dx0_cat_col % 4 == 0, "dx0 must be float4 aligned");
   if (max_uniq <= 0) return 0;
   const SegGradIn sg{*L, seg_off, sorted_refs, dz, w_head, fm_sum, dx0};
   DL_DISPATCH_E(L->emb_dim, {
-    const unsigned grid = grid_cap(max_uniq * kE);
+    const unsigned grid = grid_cap(max_uniq * (kE / 4));
     hipLaunchKernelGGL(rec_bwd_adam_kernel<kE>, dim3(grid), dim3(256), 0, as_stream(stream), sg, rec,
-                       RecCfg{kE, rec_ld, has_first, hist_len - 1, 0.f, 0.f, 0.f}, n_rep, rows_u, uniq_keys,
-                       n_uniq, world, g_rep, has_first ? g1_rep : nullptr, hist, opt);
+                       RecCfg{kE, rec_ld, has_first, 1, 0.f, 0.f, 0.f}, n_rep, rows_u,
+                       has_first ? rows_u1 : nullptr, mv_u, uniq_keys, n_uniq, world, g_rep,
+                       has_first ? g1_rep : nullptr, opt);
   });
   DL_RETURN_LAUNCH("dl_rec_bwd_adam");
 }

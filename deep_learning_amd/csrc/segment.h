@@ -26,8 +26,8 @@ struct SegGrad {
   float s, dsum, x, g1;   // sum dsec*fm_sum, sum dsec, sum dx0, first-order gradient
 };
 
-// every index derived from another kernel's output is clamped: a stale or
-// racing index can cost accuracy, never an out-of-bounds access
+// Products are fused explicitly (fmaf) so the per-dim and the float4 forms below —
+// and every kernel that inlines them — produce bit-identical sums.
 template <int E>
 __device__ __forceinline__ SegGrad segment_grad(const SegGradIn& a, long long u, int d, long long nrefs,
                                                 float wsec) {
@@ -45,12 +45,56 @@ __device__ __forceinline__ SegGrad segment_grad(const SegGradIn& a, long long u,
     if (L.use_fm && sl < S) {
       const float dzb = a.dz[b];
       const float ds = dzb * wsec;
-      r.s += ds * a.fm_sum[(long long)b * E + d];
+      r.s = fmaf(ds, a.fm_sum[(long long)b * E + d], r.s);
       r.dsum += ds;
-      r.g1 += dzb * a.w_head[Cf + sl];
+      r.g1 = fmaf(dzb, a.w_head[Cf + sl], r.g1);
     } else {
       const int f = L.use_fm ? sl - S : sl;
       r.x += a.dx0[(long long)b * L.dx0_ld + L.dx0_cat_col + f * E + d];
+    }
+  }
+  return r;
+}
+
+// Row gradient from the sums: FM part  s - V[row]*dsum, plus the deep part.
+__device__ __forceinline__ float seg_row_grad(float s, float dsum, float x, float v) {
+  return fmaf(-v, dsum, s) + x;
+}
+
+struct SegGrad4 {
+  float4 s, x;
+  float4 dsum;   // per-dim sum of dsec (wsec differs per dim)
+  float g1;
+};
+
+// Same sums for dims 4q..4q+3 of one row (one lane, float4 loads).
+template <int E>
+__device__ __forceinline__ SegGrad4 segment_grad4(const SegGradIn& a, long long u, int q, long long nrefs,
+                                                  float4 wsec) {
+  const dl_emb_layout& L = a.L;
+  const int S = L.cate_fields;
+  const int ns = (L.use_fm ? S : 0) + S;
+  const int Cf = (L.use_fm && L.fm_cont) ? L.cont_fields : 0;
+  const int e0 = max(0, a.seg_off[u]);
+  const int e1 = (int)min(nrefs, (long long)a.seg_off[u + 1]);
+  const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
+  SegGrad4 r{z, z, z, 0.f};
+  for (int e = e0; e < e1; ++e) {
+    const int k = a.refs[e];
+    if (k < 0 || k >= nrefs) continue;
+    const int b = k / ns, sl = k % ns;
+    if (L.use_fm && sl < S) {
+      const float dzb = a.dz[b];
+      const float4 fs = *reinterpret_cast<const float4*>(a.fm_sum + (long long)b * E + 4 * q);
+      const float4 ds = make_float4(dzb * wsec.x, dzb * wsec.y, dzb * wsec.z, dzb * wsec.w);
+      r.s.x = fmaf(ds.x, fs.x, r.s.x); r.s.y = fmaf(ds.y, fs.y, r.s.y);
+      r.s.z = fmaf(ds.z, fs.z, r.s.z); r.s.w = fmaf(ds.w, fs.w, r.s.w);
+      r.dsum.x += ds.x; r.dsum.y += ds.y; r.dsum.z += ds.z; r.dsum.w += ds.w;
+      r.g1 = fmaf(dzb, a.w_head[Cf + sl], r.g1);
+    } else {
+      const int f = L.use_fm ? sl - S : sl;
+      const float4 gx = *reinterpret_cast<const float4*>(a.dx0 + (long long)b * L.dx0_ld + L.dx0_cat_col + f * E + 4 * q);
+      r.x.x += gx.x; r.x.y += gx.y; r.x.z += gx.z; r.x.w += gx.w;
     }
   }
   return r;

@@ -230,6 +230,7 @@ class CTREngine:
         if self.lazy:
             self.rows_u = z(self.n_rep + self.n_refs, E)
             self.rows_u1 = z(self.n_rep + self.n_refs)
+            self.mv_u = z(self.n_rep + self.n_refs, 2 * E + 4)
         # static input slots (graph capture reads from these)
         self.in_label = z(B)
         self.in_cont = z(B, max(sp.C, 1))
@@ -487,7 +488,8 @@ class CTREngine:
             # rows of the batch (index built by _pre), caught up to the step being taken
             self._c("rec_gather", "dl_rec_gather", C_ref(L), ptr(self.rec), self.rec_ld, int(sp.fm), self.n_rep,
                     ptr(self.idx_uniq), ptr(self.idx_n), B * self.n_slot, 1, ptr(self.hist), self.hist_len,
-                    ptr(self.opt), 1 if train else 0, ptr(self.rows_u), ptr(self.rows_u1), s)
+                    ptr(self.opt), 1 if train else 0, ptr(self.rows_u), ptr(self.rows_u1),
+                    ptr(self.mv_u) if train else None, s)
             self._c("embed_fwd", "dl_embed_fwd_indexed", C_ref(L), ptr(self.rows_u),
                     ptr(self.rows_u1) if sp.fm else None, ptr(self.idx_inv), self.n_rep, ptr(self.in_cont),
                     ptr(self.in_vec), ptr(self.x0), ptr(self.fm_out), ptr(self.fm_sum), s)
@@ -563,10 +565,9 @@ class CTREngine:
         if self.lazy:
             E, R = sp.E, self.n_rep
             self._c("embed_bwd", "dl_rec_bwd_adam", C_ref(L), ptr(self.rec), self.rec_ld, int(sp.fm), R,
-                    ptr(self.rows_u[R:]), ptr(self.idx_uniq), ptr(self.idx_off), ptr(self.idx_n),
-                    ptr(self.idx_refs), 1, B * self.n_slot, ptr(self.dz), ptr(self.w_head), ptr(self.fm_sum),
-                    ptr(self.dx0), ptr(self.g_rep), ptr(self.g1_rep), ptr(self.hist), self.hist_len,
-                    ptr(self.opt), s)
+                    ptr(self.rows_u), ptr(self.rows_u1), ptr(self.mv_u), ptr(self.idx_uniq), ptr(self.idx_off),
+                    ptr(self.idx_n), ptr(self.idx_refs), 1, B * self.n_slot, ptr(self.dz), ptr(self.w_head),
+                    ptr(self.fm_sum), ptr(self.dx0), ptr(self.g_rep), ptr(self.g1_rep), ptr(self.opt), s)
             if R:
                 # FM cont-field rows: per-block register partials, folded into g_rep, then updated
                 self._c("cont_bwd", "dl_embed_cont_bwd", C_ref(L), ptr(self.rows_u), ptr(self._cont()),

@@ -247,21 +247,24 @@ int dl_adam_rows(float* p, float* m, float* v, float* g, uint8_t* touched, int64
 int dl_adam_hist_record(const float* opt, float* hist, int32_t hist_len, void* stream);
 /* rows_u[i] = p(row_i) caught up to step opt[7]-lag (rows_u1[i] = w1), row_i = i
  * for i < n_rep (replicated rows) else the row of uniq_keys[i-n_rep] (batch index,
- * dl_index_build keys).  Read only. lag = 1 inside a training step, 0 for predict. */
+ * dl_index_build keys).  Records are only read.  mv_u (may be NULL) receives the
+ * caught-up moments [i][2E+4] = m(E) | v(E) | m1 v1 0 0 for dl_rec_bwd_adam.
+ * lag = 1 inside a training step, 0 for predict. */
 int dl_rec_gather(const dl_emb_layout* L, const float* rec, int32_t rec_ld, int32_t has_first,
                   int32_t n_rep, const uint32_t* uniq_keys, const int32_t* n_uniq, int64_t max_uniq,
                   int32_t world, const float* hist, int32_t hist_len, const float* opt, int32_t lag,
-                  float* rows_u, float* rows_u1, void* stream);
+                  float* rows_u, float* rows_u1, float* mv_u, void* stream);
 /* Fused backward + Adam: per unique row the ordered segment sum of its references
- * (as dl_embed_bwd_sorted; rows_u = the gathered rows of uniq order) is applied to
- * the record (catch-up to step t-1, then step t).  Rows < n_rep instead add their
- * gradient into g_rep[row][E] / g1_rep[row] (finished by dl_rec_apply_rows). */
+ * (as dl_embed_bwd_sorted) is applied with step opt[7]'s alpha to the caught-up
+ * state of dl_rec_gather (rows_u, rows_u1, mv_u — full arrays, replicated rows
+ * first), and the record is written with stamp = step.  Rows < n_rep instead add
+ * their gradient into g_rep[row][E] / g1_rep[row] (finished by dl_rec_apply_rows). */
 int dl_rec_bwd_adam(const dl_emb_layout* L, float* rec, int32_t rec_ld, int32_t has_first, int32_t n_rep,
-                    const float* rows_u, const uint32_t* uniq_keys, const int32_t* seg_off,
-                    const int32_t* n_uniq, const int32_t* sorted_refs, int32_t world, int64_t max_uniq,
-                    const float* dz, const float* w_head, const float* fm_sum, const float* dx0,
-                    float* g_rep, float* g1_rep, const float* hist, int32_t hist_len, const float* opt,
-                    void* stream);
+                    const float* rows_u, const float* rows_u1, const float* mv_u,
+                    const uint32_t* uniq_keys, const int32_t* seg_off, const int32_t* n_uniq,
+                    const int32_t* sorted_refs, int32_t world, int64_t max_uniq, const float* dz,
+                    const float* w_head, const float* fm_sum, const float* dx0, float* g_rep,
+                    float* g1_rep, const float* opt, void* stream);
 /* Rows [row0, row0+n): step-t update with dense gradients g[n][E], g1[n] (zeroed after). */
 int dl_rec_apply_rows(float* rec, int32_t rec_ld, int32_t emb_dim, int32_t has_first, int64_t row0,
                       int64_t n, float* g, float* g1, const float* hist, int32_t hist_len,
