@@ -44,21 +44,42 @@ __device__ __forceinline__ int xcd_tile(int bid, int T) {
   return (x < rm ? x * (q + 1) : rm * (q + 1) + (x - rm) * q) + (bid >> 3);
 }
 
-template <int BM, int BN, int WM, int WN, bool TA, bool TB, int EPI>
-__global__ __launch_bounds__(256) void gemm_f32_kernel(GemmParams p) {
-  constexpr int BK = 16;
-  constexpr int PADA = (48 - (BM % 32)) % 32;
-  constexpr int PADB = (48 - (BN % 32)) % 32;
-  constexpr int SA = BM + PADA, SB = BN + PADB;
+// LDS images follow the operand's layout in HBM, so every global float4 goes to
+// LDS as one ds_write_b128 (no transposing scalar stores):
+//   k-contiguous operand (A when !TA, B when TB): image [m][BK + 4] — written and
+//     read as b128 fragments of 4 consecutive k (stride 20 words: 2-way conflicts
+//     on the b128 reads, accepted so that 5 blocks of 128x80 fit a CU's LDS and the
+//     2560 tiles of a 65536 x 400 product run in exactly two rounds);
+//   m-contiguous operand (A when TA, B when !TB): image [k][BM + pad], read as
+//     ds_read_b32 (pad keeps the two 32-lane groups on disjoint banks).
+// With a k-contiguous operand the 16 k of a slab are handed to the 4 MFMA steps as
+// k = 4*kr + s (lane group kr owns 4 consecutive k); otherwise k = 4*s + kr.  Each
+// output is still one exact f32 fma chain over all K (in a permuted k order).
+// Occupancy: the 128 x 80 tiles are held to <= 96 registers (40 accumulators in
+// AGPRs) so 5 waves share a SIMD — 5 blocks per CU, and a 65536 x 400 product's
+// 2560 tiles fill exactly two rounds of the 256 CUs (at 3 blocks/CU, 3.3 rounds
+// left a 17 % tail).
+template <int BM, int BN>
+struct GemmOcc { static constexpr int waves = (BM == 128 && BN <= 80) ? 5 : 2; };
+
+template <int BM, int BN, int WM, int WN, bool TA, bool TB, int EPI, int BK>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GemmOcc<BM, BN>::waves)))
+void gemm_f32_kernel(GemmParams p) {
+  constexpr bool AKC = !TA, BKC = TB, KPERM = AKC || BKC;
+  constexpr int KCS = BK + 4;   // k-contiguous row stride: 2-way b128 read conflicts, but 5 blocks/CU fit
+  constexpr int MCPAD_A = KPERM ? (4 - BM % 8 + 8) % 8 : (48 - BM % 32) % 32;
+  constexpr int MCPAD_B = KPERM ? (4 - BN % 8 + 8) % 8 : (48 - BN % 32) % 32;
+  constexpr int A_ROWS = AKC ? BM : BK, A_LD = AKC ? KCS : BM + MCPAD_A;
+  constexpr int B_ROWS = BKC ? BN : BK, B_LD = BKC ? KCS : BN + MCPAD_B;
   constexpr int WTM = BM / WM, WTN = BN / WN;
   constexpr int FM = WTM / 16, FN = WTN / 16;
   constexpr int QA = (BM * BK / 4 + 255) / 256;  // float4 staged per thread
   constexpr int QB = (BN * BK / 4 + 255) / 256;
   static_assert(WM * WN == 4, "4 waves");
-  static_assert(WTM % 16 == 0 && WTN % 16 == 0, "wave tile");
+  static_assert(WTM % 16 == 0 && WTN % 16 == 0 && BK % 16 == 0, "tile shape");
 
-  __shared__ __attribute__((aligned(16))) float As[2][BK][SA];
-  __shared__ __attribute__((aligned(16))) float Bs[2][BK][SB];
+  __shared__ __attribute__((aligned(16))) float As[2][A_ROWS][A_LD];
+  __shared__ __attribute__((aligned(16))) float Bs[2][B_ROWS][B_LD];
 
   const float* __restrict__ A = reinterpret_cast<const float*>(p.A);
   const float* __restrict__ Bm = reinterpret_cast<const float*>(p.B);
@@ -92,7 +113,7 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(GemmParams p) {
           const int gr = k0 + r, gi = i0 + 4 * i4;
           if (gr < kend && gi < p.M) v = *reinterpret_cast<const float4*>(A + (long long)gr * p.lda + gi);
         } else {   // A stored [i][r]
-          const int i = qi / 4, r4 = qi % 4;
+          const int i = qi / (BK / 4), r4 = qi % (BK / 4);
           const int gi = i0 + i, gr = k0 + 4 * r4;
           if (gi < p.M && gr < kend) v = *reinterpret_cast<const float4*>(A + (long long)gi * p.lda + gr);
         }
@@ -109,7 +130,7 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(GemmParams p) {
           const int gr = k0 + r, gj = j0 + 4 * j4;
           if (gr < kend && gj < p.N) v = *reinterpret_cast<const float4*>(Bm + (long long)gr * p.ldb + gj);
         } else {    // B stored [j][r]
-          const int j = qi / 4, r4 = qi % 4;
+          const int j = qi / (BK / 4), r4 = qi % (BK / 4);
           const int gj = j0 + j, gr = k0 + 4 * r4;
           if (gj < p.N && gr < kend) v = *reinterpret_cast<const float4*>(Bm + (long long)gj * p.ldb + gr);
         }
@@ -126,11 +147,8 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(GemmParams p) {
           const int r = qi / (BM / 4), i4 = qi % (BM / 4);
           *reinterpret_cast<float4*>(&As[buf][r][4 * i4]) = ra[u];
         } else {
-          const int i = qi / 4, r4 = qi % 4;
-          As[buf][4 * r4 + 0][i] = ra[u].x;
-          As[buf][4 * r4 + 1][i] = ra[u].y;
-          As[buf][4 * r4 + 2][i] = ra[u].z;
-          As[buf][4 * r4 + 3][i] = ra[u].w;
+          const int i = qi / (BK / 4), r4 = qi % (BK / 4);
+          *reinterpret_cast<float4*>(&As[buf][i][4 * r4]) = ra[u];
         }
       }
     }
@@ -142,11 +160,8 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(GemmParams p) {
           const int r = qi / (BN / 4), j4 = qi % (BN / 4);
           *reinterpret_cast<float4*>(&Bs[buf][r][4 * j4]) = rb[u];
         } else {
-          const int j = qi / 4, r4 = qi % 4;
-          Bs[buf][4 * r4 + 0][j] = rb[u].x;
-          Bs[buf][4 * r4 + 1][j] = rb[u].y;
-          Bs[buf][4 * r4 + 2][j] = rb[u].z;
-          Bs[buf][4 * r4 + 3][j] = rb[u].w;
+          const int j = qi / (BK / 4), r4 = qi % (BK / 4);
+          *reinterpret_cast<float4*>(&Bs[buf][j][4 * r4]) = rb[u];
         }
       }
     }
@@ -162,17 +177,38 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(GemmParams p) {
     const int cur = kt & 1;
     if (kt + 1 < nk) load_tile(kbeg + (kt + 1) * BK);
 #pragma unroll
-    for (int s = 0; s < BK / 4; ++s) {
-      float av[FM], bv[FN];
+    for (int s16 = 0; s16 < BK / 16; ++s16) {
+      float4 a4[AKC ? FM : 1], b4[BKC ? FN : 1];
+      if (AKC) {
 #pragma unroll
-      for (int a = 0; a < FM; ++a) av[a] = As[cur][4 * s + kr][wm * WTM + a * 16 + cl];
-#pragma unroll
-      for (int b = 0; b < FN; ++b) bv[b] = Bs[cur][4 * s + kr][wn * WTN + b * 16 + cl];
-#pragma unroll
-      for (int a = 0; a < FM; ++a)
+        for (int a = 0; a < FM; ++a)
+          a4[a] = *reinterpret_cast<const float4*>(&As[cur][AKC ? wm * WTM + a * 16 + cl : 0][s16 * 16 + 4 * kr]);
+      }
+      if (BKC) {
 #pragma unroll
         for (int b = 0; b < FN; ++b)
-          acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[a], bv[b], acc[a][b], 0, 0, 0);
+          b4[b] = *reinterpret_cast<const float4*>(&Bs[cur][BKC ? wn * WTN + b * 16 + cl : 0][s16 * 16 + 4 * kr]);
+      }
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        const int k = s16 * 16 + (KPERM ? 4 * kr + s : 4 * s + kr);
+        float av[FM], bv[FN];
+#pragma unroll
+        for (int a = 0; a < FM; ++a) {
+          if (AKC) av[a] = s == 0 ? a4[a].x : s == 1 ? a4[a].y : s == 2 ? a4[a].z : a4[a].w;
+          else av[a] = As[cur][AKC ? 0 : k][wm * WTM + a * 16 + cl];
+        }
+#pragma unroll
+        for (int b = 0; b < FN; ++b) {
+          if (BKC) bv[b] = s == 0 ? b4[b].x : s == 1 ? b4[b].y : s == 2 ? b4[b].z : b4[b].w;
+          else bv[b] = Bs[cur][BKC ? 0 : k][wn * WTN + b * 16 + cl];
+        }
+#pragma unroll
+        for (int a = 0; a < FM; ++a)
+#pragma unroll
+          for (int b = 0; b < FN; ++b)
+            acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[a], bv[b], acc[a][b], 0, 0, 0);
+      }
     }
     if (kt + 1 < nk) store_tile(cur ^ 1);
     __syncthreads();
@@ -300,13 +336,14 @@ __global__ __launch_bounds__(256) void gemm_bf16_kernel(GemmParams p) {
 
 template <int BM, int BN, int WM, int WN, bool TA, bool TB>
 static void launch_f32(const GemmParams& gp, int epi, int splits, hipStream_t s) {
+  constexpr int BK = 16;
   const int tiles = (int)(ceil_div(gp.M, BM) * ceil_div(gp.N, BN));
   dim3 grid(tiles, 1, splits);
   switch (epi) {
-    case EPI_STORE: hipLaunchKernelGGL((gemm_f32_kernel<BM, BN, WM, WN, TA, TB, EPI_STORE>), grid, dim3(256), 0, s, gp); break;
-    case EPI_RELU: hipLaunchKernelGGL((gemm_f32_kernel<BM, BN, WM, WN, TA, TB, EPI_RELU>), grid, dim3(256), 0, s, gp); break;
-    case EPI_MASK: hipLaunchKernelGGL((gemm_f32_kernel<BM, BN, WM, WN, TA, TB, EPI_MASK>), grid, dim3(256), 0, s, gp); break;
-    default: hipLaunchKernelGGL((gemm_f32_kernel<BM, BN, WM, WN, TA, TB, EPI_SPLIT>), grid, dim3(256), 0, s, gp); break;
+    case EPI_STORE: hipLaunchKernelGGL((gemm_f32_kernel<BM, BN, WM, WN, TA, TB, EPI_STORE, BK>), grid, dim3(256), 0, s, gp); break;
+    case EPI_RELU: hipLaunchKernelGGL((gemm_f32_kernel<BM, BN, WM, WN, TA, TB, EPI_RELU, BK>), grid, dim3(256), 0, s, gp); break;
+    case EPI_MASK: hipLaunchKernelGGL((gemm_f32_kernel<BM, BN, WM, WN, TA, TB, EPI_MASK, BK>), grid, dim3(256), 0, s, gp); break;
+    default: hipLaunchKernelGGL((gemm_f32_kernel<BM, BN, WM, WN, TA, TB, EPI_SPLIT, BK>), grid, dim3(256), 0, s, gp); break;
   }
 }
 
@@ -340,9 +377,35 @@ static void launch_bf16(const GemmParams& gp, int epi, int splits, hipStream_t s
   }
 }
 
+// dst[c][r] = src[r][c] through a 32x33 LDS tile.
+__global__ __launch_bounds__(256) void transpose_kernel(const float* __restrict__ src, int rows, int cols, int lds,
+                                                        float* __restrict__ dst, int ldd) {
+  __shared__ float t[32][33];
+  const int c0 = blockIdx.x * 32, r0 = blockIdx.y * 32;
+  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;
+  for (int y = ty; y < 32; y += 8) {
+    const int r = r0 + y, c = c0 + tx;
+    t[y][tx] = (r < rows && c < cols) ? src[(long long)r * lds + c] : 0.f;
+  }
+  __syncthreads();
+  for (int y = ty; y < 32; y += 8) {
+    const int c = c0 + y, r = r0 + tx;
+    if (c < cols && r < rows) dst[(long long)c * ldd + r] = t[tx][y];
+  }
+}
+
 }  // namespace dl
 
 using namespace dl;
+
+extern "C" int dl_transpose_f32(const float* src, int32_t rows, int32_t cols, int32_t lds, float* dst, int32_t ldd,
+                                void* stream) {
+  DL_CHECK_ARG(src && dst && rows >= 0 && cols >= 0 && lds >= cols && ldd >= rows, "bad transpose args");
+  if (rows == 0 || cols == 0) return 0;
+  hipLaunchKernelGGL(transpose_kernel, dim3((unsigned)ceil_div(cols, 32), (unsigned)ceil_div(rows, 32)), dim3(256), 0,
+                     as_stream(stream), src, rows, cols, lds, dst, ldd);
+  DL_RETURN_LAUNCH("dl_transpose_f32");
+}
 
 extern "C" int dl_gemm_f32(int32_t ta, int32_t tb, int32_t M, int32_t N, int32_t K, const float* A,
                            int32_t lda, const float* B, int32_t ldb, float* C, int32_t ldc,

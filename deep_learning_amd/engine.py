@@ -173,6 +173,7 @@ class CTREngine:
         self.W = [z(self.in_ld[l], self.out_ld[l]) for l in range(len(sp.hidden))]
         self.Wm = [torch.zeros_like(w) for w in self.W]
         self.Wv = [torch.zeros_like(w) for w in self.W]
+        self.Wt = z(max(o * i for o, i in zip(self.out_ld, self.in_ld)))   # W_l^T scratch for dX
         H = sp.hidden[-1]
         self.head_n = sp.fm_cols + H + 1
         self.w_head = z(_ru(self.head_n, 4))
@@ -548,13 +549,15 @@ class CTREngine:
             self._c("gemm_dw_l%d" % l, "dl_gemm_f32", 1, 0, self.in_ld[l], hdim, B, ptr(xin), self.in_ld[l], ptr(self.dh[l]),
                  self.h_ld[l], ptr(self.w_slab), self.out_ld[l], 3, None, 0, splits, stride, s)
             nsplit = _num_splits(B, splits)
+            self._c("transpose_l%d" % l, "dl_transpose_f32", ptr(self.W[l]), self.in_ld[l], self.out_ld[l],
+                    self.out_ld[l], ptr(self.Wt), self.in_ld[l], s)
             if l > 0:
-                self._c("gemm_dx_l%d" % l, "dl_gemm_f32", 0, 1, B, sp.hidden[l - 1], self.out_ld[l], ptr(self.dh[l]), self.h_ld[l],
-                     ptr(self.W[l]), self.out_ld[l], ptr(self.dh[l - 1]), self.h_ld[l - 1], 2,
-                     ptr(self.h[l - 1]), self.h_ld[l - 1], 1, 0, s)
+                self._c("gemm_dx_l%d" % l, "dl_gemm_f32", 0, 0, B, sp.hidden[l - 1], self.out_ld[l], ptr(self.dh[l]),
+                        self.h_ld[l], ptr(self.Wt), self.in_ld[l], ptr(self.dh[l - 1]), self.h_ld[l - 1], 2,
+                        ptr(self.h[l - 1]), self.h_ld[l - 1], 1, 0, s)
             else:
-                self._c("gemm_dx_l0", "dl_gemm_f32", 0, 1, B, self.dx_cols, self.out_ld[0], ptr(self.dh[0]), self.h_ld[0],
-                     ptr(self.W[0]), self.out_ld[0], ptr(self.dx0), self.dx_ld, 0, None, 0, 1, 0, s)
+                self._c("gemm_dx_l0", "dl_gemm_f32", 0, 0, B, self.dx_cols, self.out_ld[0], ptr(self.dh[0]),
+                        self.h_ld[0], ptr(self.Wt), self.in_ld[0], ptr(self.dx0), self.dx_ld, 0, None, 0, 1, 0, s)
             # L2 on every hidden weight matrix only for wdl (wdl.py:272-275); bias row excluded
             l2, l2n = (sp.l2, ([self.D0] + sp.hidden)[l] * self.out_ld[l]) if self.wdl else (0.0, 0)
             self._c("adam_dense_l%d" % l, "dl_adam_dense", ptr(self.W[l]), ptr(self.Wm[l]), ptr(self.Wv[l]),

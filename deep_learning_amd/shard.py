@@ -258,13 +258,15 @@ class ShardedCTREngine(CTREngine):
                     ptr(self.dh[l]), self.h_ld[l], ptr(self.w_slab), self.out_ld[l], 3, None, 0, splits, stride, s)
             call("dl_slab_sum", ptr(self.w_slab), _num_splits(B, splits), stride, stride,
                  ptr(self.flat[self.seg[l][1]:]), s)
+            self._c("transpose_l%d" % l, "dl_transpose_f32", ptr(self.W[l]), self.in_ld[l], self.out_ld[l],
+                    self.out_ld[l], ptr(self.Wt), self.in_ld[l], s)
             if l > 0:
-                self._c("gemm_dx_l%d" % l, "dl_gemm_f32", 0, 1, B, sp.hidden[l - 1], self.out_ld[l], ptr(self.dh[l]),
-                        self.h_ld[l], ptr(self.W[l]), self.out_ld[l], ptr(self.dh[l - 1]), self.h_ld[l - 1], 2,
+                self._c("gemm_dx_l%d" % l, "dl_gemm_f32", 0, 0, B, sp.hidden[l - 1], self.out_ld[l], ptr(self.dh[l]),
+                        self.h_ld[l], ptr(self.Wt), self.in_ld[l], ptr(self.dh[l - 1]), self.h_ld[l - 1], 2,
                         ptr(self.h[l - 1]), self.h_ld[l - 1], 1, 0, s)
             else:
-                self._c("gemm_dx_l0", "dl_gemm_f32", 0, 1, B, self.dx_cols, self.out_ld[0], ptr(self.dh[0]),
-                        self.h_ld[0], ptr(self.W[0]), self.out_ld[0], ptr(self.dx0), self.dx_ld, 0, None, 0, 1, 0, s)
+                self._c("gemm_dx_l0", "dl_gemm_f32", 0, 0, B, self.dx_cols, self.out_ld[0], ptr(self.dh[0]),
+                        self.h_ld[0], ptr(self.Wt), self.in_ld[0], ptr(self.dx0), self.dx_ld, 0, None, 0, 1, 0, s)
         hoff = self.seg[nl][1]
         call("dl_slab_sum", ptr(self.head_slab), call_int("dl_head_grid", B), self.head_w, self.head_w,
              ptr(self.flat[hoff:]), s)

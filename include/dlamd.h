@@ -172,6 +172,10 @@ int dl_gemm_f32(int32_t ta, int32_t tb, int32_t M, int32_t N, int32_t K, const f
                 int32_t lda, const float* B, int32_t ldb, float* C, int32_t ldc, int32_t epi,
                 const float* mask, int32_t ldm, int32_t splits, int64_t c_split_stride,
                 void* stream);
+/* dst[c*ldd + r] = src[r*lds + c] (r < rows, c < cols): W^T for the dX product, so
+ * both dX operands are read from LDS images in their HBM layout. */
+int dl_transpose_f32(const float* src, int32_t rows, int32_t cols, int32_t lds, float* dst, int32_t ldd,
+                     void* stream);
 /* bf16 variant for the Wide&Deep tower (config C5): A, B bf16 (uint16 bits),
  * fp32 accumulate, C fp32 or bf16 (c_bf16 = 1). Same semantics otherwise. */
 int dl_gemm_bf16(int32_t ta, int32_t tb, int32_t M, int32_t N, int32_t K, const uint16_t* A,
