@@ -17,7 +17,6 @@
 
 namespace dl {
 
-constexpr uint32_t kInvalidKey = 0xFFFFFFFFu;
 constexpr int kLocalBits = 27;
 
 __device__ __forceinline__ bool row_ok_i(int64_t row, int zero_row0) {
@@ -25,7 +24,8 @@ __device__ __forceinline__ bool row_ok_i(int64_t row, int zero_row0) {
 }
 
 __global__ __launch_bounds__(256) void make_refs_kernel(dl_emb_layout L, const int64_t* __restrict__ cate, int world,
-                                                        int rep_below, uint32_t* __restrict__ keys,
+                                                        int rep_below, uint32_t kInvalidKey,
+                                                        uint32_t* __restrict__ keys,
                                                         int32_t* __restrict__ refs, int32_t* err) {
   const int S = L.cate_fields;
   const int ns = (L.use_fm ? S : 0) + S;
@@ -47,7 +47,8 @@ __global__ __launch_bounds__(256) void make_refs_kernel(dl_emb_layout L, const i
   }
 }
 
-__global__ __launch_bounds__(256) void head_flags_kernel(const uint32_t* __restrict__ keys, int n, int32_t* __restrict__ flags) {
+__global__ __launch_bounds__(256) void head_flags_kernel(const uint32_t* __restrict__ keys, int n, uint32_t kInvalidKey,
+                                                         int32_t* __restrict__ flags) {
   for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
     const uint32_t k = keys[i];
     flags[i] = (k != kInvalidKey && (i == 0 || keys[i - 1] != k)) ? 1 : 0;
@@ -56,6 +57,7 @@ __global__ __launch_bounds__(256) void head_flags_kernel(const uint32_t* __restr
 
 __global__ __launch_bounds__(256) void scatter_index_kernel(const uint32_t* __restrict__ keys, const int32_t* __restrict__ refs,
                                                             const int32_t* __restrict__ uid1, int n, int world,
+                                                            uint32_t kInvalidKey,
                                                             uint32_t* __restrict__ uniq, int32_t* __restrict__ seg_off,
                                                             int32_t* __restrict__ n_uniq, int32_t* __restrict__ inv,
                                                             int32_t* __restrict__ owner_counts) {
@@ -98,12 +100,29 @@ struct IndexWs {
 
 static size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
 
+// Onesweep radix sort over the key's significant bits only (25 for a 26M-row table).
+// (11-bit digits would save a pass, but rocPRIM's match-rank variant that fits them
+// in LDS ran 3x slower on gfx950 — measured; the default 8-bit digits stay.)
+static hipError_t sort_pairs(void* temp, size_t& bytes, const uint32_t* kin, uint32_t* kout, const int32_t* vin,
+                             int32_t* vout, int n, int end_bit, hipStream_t s) {
+  return hipcub::DeviceRadixSort::SortPairs(temp, bytes, kin, kout, vin, vout, n, 0, end_bit, s);
+}
+
 static size_t cub_temp_bytes(int n) {
   size_t a = 0, b = 0;
-  hipcub::DeviceRadixSort::SortPairs(nullptr, a, (uint32_t*)nullptr, (uint32_t*)nullptr, (int32_t*)nullptr,
-                                     (int32_t*)nullptr, n, 0, 32);
+  sort_pairs(nullptr, a, nullptr, nullptr, nullptr, nullptr, n, 32, 0);
   hipcub::DeviceScan::InclusiveSum(nullptr, b, (int32_t*)nullptr, (int32_t*)nullptr, n);
   return a > b ? a : b;
+}
+
+// Bits of the sorted key range: keys are < 2^end_bit, the all-ones value marks invalid refs.
+static int key_bits(int64_t n_rows, int world, int rep_below) {
+  uint64_t max_key;
+  if (world == 1 && rep_below == 0) max_key = (uint64_t)n_rows;            // row; n_rows itself = headroom
+  else max_key = ((uint64_t)(rep_below > 0 ? world : world - 1) << kLocalBits) | ((1u << kLocalBits) - 1);
+  int b = 1;
+  while (b < 32 && (max_key + 1) > (1ull << b) - 1) ++b;
+  return b;
 }
 
 static IndexWs carve(void* ws, int n) {
@@ -147,21 +166,22 @@ extern "C" int dl_index_build(const dl_emb_layout* L, const int64_t* cate, int32
   if (n == 0) return 0;
   IndexWs w = carve(ws, n);
   const int grid = (int)((n + 255) / 256 < 8192 ? (n + 255) / 256 : 8192);
-  hipLaunchKernelGGL(make_refs_kernel, dim3(grid), dim3(256), 0, s, *L, cate, world, replicated_below, w.keys_in,
-                     w.refs_in, err);
+  const int end_bit = key_bits(L->n_rows, world, replicated_below);
+  const uint32_t invalid = end_bit >= 32 ? 0xFFFFFFFFu : (uint32_t)((1ull << end_bit) - 1);
+  hipLaunchKernelGGL(make_refs_kernel, dim3(grid), dim3(256), 0, s, *L, cate, world, replicated_below, invalid,
+                     w.keys_in, w.refs_in, err);
   size_t tb = w.temp_bytes;
-  if (hipcub::DeviceRadixSort::SortPairs(w.temp, tb, w.keys_in, sorted_keys, w.refs_in, sorted_refs, n, 0, 32, s) !=
-      hipSuccess) {
+  if (sort_pairs(w.temp, tb, w.keys_in, sorted_keys, w.refs_in, sorted_refs, n, end_bit, s) != hipSuccess) {
     set_error("dl_index_build: radix sort failed");
     return 2;
   }
-  hipLaunchKernelGGL(head_flags_kernel, dim3(grid), dim3(256), 0, s, sorted_keys, n, w.flags);
+  hipLaunchKernelGGL(head_flags_kernel, dim3(grid), dim3(256), 0, s, sorted_keys, n, invalid, w.flags);
   tb = w.temp_bytes;
   if (hipcub::DeviceScan::InclusiveSum(w.temp, tb, w.flags, w.uid1, n, s) != hipSuccess) {
     set_error("dl_index_build: scan failed");
     return 3;
   }
   hipLaunchKernelGGL(scatter_index_kernel, dim3(grid), dim3(256), 0, s, sorted_keys, sorted_refs, w.uid1, n, world,
-                     uniq_keys, seg_off, n_uniq, inv, owner_counts);
+                     invalid, uniq_keys, seg_off, n_uniq, inv, owner_counts);
   DL_RETURN_LAUNCH("dl_index_build");
 }

@@ -526,8 +526,9 @@ class CTREngine:
         s = _lib.stream_handle()
         L = self.layout
         L.batch = B
-        self._c("index_build", "dl_index_build", C_ref(L), ptr(self.in_cate), 1,
-                self.n_rep if self.lazy else 0, ptr(self.idx_ws),
+        # single GPU: keys are the rows themselves (replicated rows need no owner group;
+        # the record kernels recognise them by row < n_rep) — the narrowest sort range
+        self._c("index_build", "dl_index_build", C_ref(L), ptr(self.in_cate), 1, 0, ptr(self.idx_ws),
                 self.idx_ws.numel(), ptr(self.idx_keys), ptr(self.idx_refs), ptr(self.idx_uniq),
                 ptr(self.idx_off), ptr(self.idx_n), ptr(self.idx_inv) if self.lazy else None, None,
                 ptr(self.err), s)
