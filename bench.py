@@ -128,7 +128,7 @@ def main():
     ap.add_argument("--vocab", type=int, default=0,
                     help="per-field vocab (default: 1M at N=1 = C2; 100M/26 at N>1 = C4's 100M-row table)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--adam", default="dense", choices=["dense", "lazy"],
+    ap.add_argument("--adam", default="lazy", choices=["dense", "lazy"],
                     help="table Adam: dense sweep, or row records with lazy-exact catch-up (same result)")
     args = ap.parse_args()
 
@@ -159,7 +159,7 @@ def main():
         eng = CTREngine(spec, max_batch=B, seed=2019, adam=args.adam)
     else:
         from deep_learning_amd.shard import Exchange, ShardedCTREngine
-        eng = ShardedCTREngine(spec, B, Exchange(), seed=2019)
+        eng = ShardedCTREngine(spec, B, Exchange(), seed=2019, adam=args.adam)
         eng.init_device(2019)
     nb = 4
     dev_batches = []

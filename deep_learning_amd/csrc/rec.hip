@@ -85,7 +85,7 @@ __global__ __launch_bounds__(256) void rec_gather_kernel(const float* __restrict
   const long long gt = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   const int q = (int)(gt % LPR);
   const long long group0 = gt / LPR, ngroups = (long long)gridDim.x * blockDim.x / LPR;
-  const long long total = n_rep + (long long)clamp_uniq(n_uniq, max_u);
+  const long long total = n_rep + (n_uniq ? (long long)clamp_uniq(n_uniq, max_u) : max_u);
   const int target = (int)opt[7] - lag;
   for (long long i = group0; i < total; i += ngroups) {
     const int64_t row = i < n_rep ? i : decode_key(uniq[i - n_rep], world);
@@ -255,6 +255,57 @@ __global__ __launch_bounds__(256) void rec_flush_kernel(float* __restrict__ rec,
   }
 }
 
+// Owner side of the sharded step: peers' per-row gradients are summed into the dense
+// local gradient table G/G1 (f32 atomics: a row may arrive from several peers), and
+// the first arrival of a row appends it to `list` (flag exchange), so the update
+// below visits each touched row once without a sort.
+__global__ __launch_bounds__(256) void rec_scatter_list_kernel(const float* __restrict__ g, const float* __restrict__ g1,
+                                                               const int32_t* __restrict__ ids, long long n, int E,
+                                                               float* __restrict__ G, float* __restrict__ G1,
+                                                               int32_t* __restrict__ flags, int32_t* __restrict__ list,
+                                                               int32_t* __restrict__ list_n) {
+  for (long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x; t < n * E;
+       t += (long long)gridDim.x * blockDim.x) {
+    const long long i = t / E;
+    const int d = (int)(t % E);
+    const int r = ids[i];
+    atomicAdd(G + (long long)r * E + d, g[t]);
+    if (d == 0) {
+      if (g1) atomicAdd(G1 + r, g1[i]);
+      if (atomicExch(flags + r, 1) == 0) list[atomicAdd(list_n, 1)] = r;
+    }
+  }
+}
+
+// Step-t update of the listed rows from G/G1 (then zeroed, flags cleared).
+__global__ __launch_bounds__(256) void rec_apply_list_kernel(float* __restrict__ rec, RecCfg c,
+                                                             const int32_t* __restrict__ list,
+                                                             const int32_t* __restrict__ list_n, long long cap,
+                                                             float* __restrict__ G, float* __restrict__ G1,
+                                                             int32_t* __restrict__ flags, const float* __restrict__ hist,
+                                                             const float* __restrict__ opt) {
+  rec_load_hyper(c, opt);
+  const int E = c.E;
+  const int t = (int)opt[7];
+  const float alpha_t = opt[3];
+  long long n = list_n[0];
+  n = n < 0 ? 0 : (n > cap ? cap : n);
+  for (long long k = (long long)blockIdx.x * blockDim.x + threadIdx.x; k < n * E;
+       k += (long long)gridDim.x * blockDim.x) {
+    const long long i = k / E;
+    const int d = (int)(k % E);
+    const long long row = list[i];
+    const float gi = G[row * E + d];
+    const float g1i = (G1 && d == 0) ? G1[row] : 0.f;
+    rec_update(rec + row * c.ld, E, d, gi, g1i, t, alpha_t, hist, c);
+    G[row * E + d] = 0.f;
+    if (d == 0) {
+      if (G1) G1[row] = 0.f;
+      flags[row] = 0;
+    }
+  }
+}
+
 __global__ void hist_record_kernel(const float* opt, float* hist, int mask) {
   hist[(int)opt[7] & mask] = opt[3];
 }
@@ -289,7 +340,7 @@ extern "C" int dl_rec_gather(const dl_emb_layout* L, const float* rec, int32_t r
   DL_CHECK_ARG(L && rec && hist && opt && rows_u, "NULL argument");
   if (int rc = rec_check(L->emb_dim, rec_ld, hist_len)) return rc;
   DL_CHECK_ARG(n_rep >= 0 && n_rep <= L->n_rows && world >= 1, "bad n_rep/world");
-  DL_CHECK_ARG(max_uniq == 0 || (uniq_keys && n_uniq), "uniq keys required");
+  DL_CHECK_ARG(max_uniq == 0 || uniq_keys, "uniq keys required");
   DL_CHECK_ARG(!has_first || rows_u1, "rows_u1 required with first-order weights");
   const long long total = n_rep + (max_uniq > 0 ? max_uniq : 0);
   if (total == 0) return 0;
@@ -354,4 +405,28 @@ extern "C" int dl_rec_flush(float* rec, int32_t rec_ld, int32_t emb_dim, int32_t
                        opt);
   });
   DL_RETURN_LAUNCH("dl_rec_flush");
+}
+
+extern "C" int dl_rec_scatter_list(const float* g, const float* g1, const int32_t* ids, int64_t n, int32_t emb_dim,
+                                   float* G, float* G1, int32_t* flags, int32_t* list, int32_t* list_n,
+                                   void* stream) {
+  DL_CHECK_ARG(g && ids && G && flags && list && list_n, "NULL argument");
+  DL_CHECK_ARG(!g1 || G1, "G1 required with g1");
+  if (n <= 0) return 0;
+  hipLaunchKernelGGL(rec_scatter_list_kernel, dim3(grid_cap(n * emb_dim)), dim3(256), 0, as_stream(stream), g, g1,
+                     ids, (long long)n, emb_dim, G, g1 ? G1 : nullptr, flags, list, list_n);
+  DL_RETURN_LAUNCH("dl_rec_scatter_list");
+}
+
+extern "C" int dl_rec_apply_list(float* rec, int32_t rec_ld, int32_t emb_dim, int32_t has_first, const int32_t* list,
+                                 const int32_t* list_n, int64_t cap, float* G, float* G1, int32_t* flags,
+                                 const float* hist, int32_t hist_len, const float* opt, void* stream) {
+  DL_CHECK_ARG(rec && list && list_n && G && flags && hist && opt, "NULL argument");
+  if (int rc = rec_check(emb_dim, rec_ld, hist_len)) return rc;
+  DL_CHECK_ARG(!has_first || G1, "G1 required with first-order weights");
+  if (cap <= 0) return 0;
+  hipLaunchKernelGGL(rec_apply_list_kernel, dim3(grid_cap(cap * emb_dim)), dim3(256), 0, as_stream(stream), rec,
+                     RecCfg{emb_dim, rec_ld, has_first, hist_len - 1, 0.f, 0.f, 0.f}, list, list_n,
+                     (long long)cap, G, has_first ? G1 : nullptr, flags, hist, opt);
+  DL_RETURN_LAUNCH("dl_rec_apply_list");
 }

@@ -685,6 +685,12 @@ class CTREngine:
             raise _lib.DLError("InvalidArgumentError: categorical id out of range [0, %d)" % self.N)
 
 
+def default_adam(spec):
+    """Table Adam used by the drop-in model classes: row records with lazy-exact
+    catch-up (bit-identical to the dense sweep, rec.hip) wherever supported."""
+    return "dense" if spec.M else "lazy"
+
+
 def _num_splits(K, splits):
     kps = -(-K // splits)
     kps = -(-kps // 16) * 16

@@ -29,7 +29,7 @@ import time
 import numpy as np
 import torch
 
-from ..engine import CTREngine, ModelSpec
+from ..engine import CTREngine, ModelSpec, default_adam
 from ..metrics import roc_auc
 
 
@@ -70,7 +70,8 @@ class CTRModel:
         """Builds the engine (the reference builds the graph here): returns
         (loss_fn, train_fn, global_step_fn)."""
         if self.engine is None:
-            self.engine = CTREngine(self.spec, max_batch=self.batch_size, seed=self.random_seed)
+            self.engine = CTREngine(self.spec, max_batch=self.batch_size, seed=self.random_seed,
+                                    adam=default_adam(self.spec))
         eng = self.engine
         return eng.loss, lambda batch: eng.train_step(batch, graph=True), lambda: eng.steps
 
@@ -210,7 +211,7 @@ def load_model(model_pb, max_batch=None):
     with open(os.path.join(model_pb, "signature.json")) as f:
         meta = json.load(f)
     spec = ModelSpec(meta["model"], **{k: v for k, v in meta["spec"].items() if k != "model"})
-    eng = CTREngine(spec, max_batch=max_batch or meta["batch_size"], init="none")
+    eng = CTREngine(spec, max_batch=max_batch or meta["batch_size"], init="none", adam=default_adam(spec))
     d = np.load(os.path.join(model_pb, "variables.npz"), allow_pickle=False)
     eng.load_params({k: d[k] for k in d.files})
     return eng

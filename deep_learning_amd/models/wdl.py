@@ -18,7 +18,7 @@ import time
 
 import numpy as np
 
-from ..engine import CTREngine, ModelSpec
+from ..engine import CTREngine, ModelSpec, default_adam
 from ..metrics import roc_auc
 from ._ctr_model import _predict_batches, export_model, load_model
 
@@ -55,7 +55,8 @@ class DeepModel:
 
     def model_optimizer(self):
         if self.engine is None:
-            self.engine = CTREngine(self.spec, max_batch=self.batch_size, seed=self.random_seed)
+            self.engine = CTREngine(self.spec, max_batch=self.batch_size, seed=self.random_seed,
+                                    adam=default_adam(self.spec))
         return self.engine
 
     def fit(self, train_data, val_data):

@@ -75,7 +75,7 @@ class Exchange:
 class ShardedCTREngine(CTREngine):
     """CTREngine whose embedding tables are row-sharded across the ranks of `exch`."""
 
-    def __init__(self, spec, max_batch, exch, device="cuda", seed=2019):
+    def __init__(self, spec, max_batch, exch, device="cuda", seed=2019, adam="dense", hist_len=4096):
         if spec.model not in ("deepfm_pipeline", "dnn_pipeline"):
             raise ValueError("sharded path supports deepfm_pipeline / dnn_pipeline")
         self.exch = exch
@@ -84,11 +84,20 @@ class ShardedCTREngine(CTREngine):
         self.rep = spec.C if spec.model == "deepfm_pipeline" else 0
         local_rows = -(-N // self.world)
         super().__init__(spec, max_batch, device=device, seed=seed, init="none", bwd="sorted",
-                         table_rows=local_rows)
+                         table_rows=local_rows, adam=adam, hist_len=hist_len)
         dev = self.dev
         z = lambda *sh, dt=torch.float32: torch.zeros(*sh, dtype=dt, device=dev)
         E = spec.E
         self.local_rows = local_rows
+        if self.lazy:
+            # shard rows as records (rec.hip); owners accumulate peers' gradients in a dense
+            # local table and update only the rows that arrived (list built by flag exchange)
+            self.mv_u = None
+            self.tg = z(self.rows_pad, E)
+            self.fmg = z(self.rows_pad) if spec.fm else None
+            self.row_flags = z(self.rows_pad, dt=torch.int32)
+            self.row_list = z(self.rows_pad, dt=torch.int32)
+            self.row_list_n = z(4, dt=torch.int32)
         R = max(self.rep, 1)
         rp = _ru(R, 16)
         self.rep_t, self.rep_m, self.rep_v, self.rep_g = z(rp, E), z(rp, E), z(rp, E), z(rp, E)
@@ -130,13 +139,18 @@ class ShardedCTREngine(CTREngine):
         N = self.N
         rows = self.owned_rows()
         ok = rows < N
-        t = np.zeros((self.table.shape[0], sp.E), np.float32)
+        t = np.zeros((self.rows_pad, sp.E), np.float32)
         t[: self.local_rows][ok] = P["feats_emb"][rows[ok]]
-        self.table.copy_(torch.from_numpy(t))
+        f = None
         if sp.fm:
-            f = np.zeros(self.first.shape[0], np.float32)
+            f = np.zeros(self.rows_pad, np.float32)
             f[: self.local_rows][ok] = P["fm_first_order_emb"][rows[ok], 0]
-            self.first.copy_(torch.from_numpy(f))
+        if self.lazy:
+            self._pack(torch.from_numpy(t).to(self.dev), torch.from_numpy(f).to(self.dev) if f is not None else None)
+        else:
+            self.table.copy_(torch.from_numpy(t))
+            if f is not None:
+                self.first.copy_(torch.from_numpy(f))
         if self.rep:
             self.rep_t[: self.rep].copy_(torch.from_numpy(np.ascontiguousarray(P["feats_emb"][: self.rep])))
             if sp.fm:
@@ -155,11 +169,17 @@ class ShardedCTREngine(CTREngine):
         """Bench init: every rank draws its shard with a rank-distinct counter range."""
         sp = self.spec
         s = _lib.stream_handle()
+        if self.lazy:
+            self.table = torch.zeros(self.rows_pad, sp.E, device=self.dev)
+            self.first = torch.zeros(self.rows_pad, device=self.dev) if sp.fm else None
         call("dl_init_random", ptr(self.table), self.table.numel(), 0, 0.0, 0.01, seed,
              self.rank * self.table.numel() * 4, s)
         if self.first is not None:
             call("dl_init_random", ptr(self.first), _ru(self.first.numel(), 4), 1, 0.0, 1.0, seed + 1,
                  self.rank * _ru(self.first.numel(), 4), s)
+        if self.lazy:
+            self._pack(self.table, self.first)
+            self.table = self.first = None
         if self.rep:
             call("dl_init_random", ptr(self.rep_t), self.rep_t.numel(), 0, 0.0, 0.01, seed + 7, 0, s)
             if sp.fm:
@@ -185,6 +205,13 @@ class ShardedCTREngine(CTREngine):
         """(global rows, table rows, first-order) of this rank's shard (host numpy)."""
         rows = self.owned_rows()
         ok = rows < self.N
+        if self.lazy:
+            self.flush()
+            E = self.spec.E
+            r = self.rec[: self.local_rows]
+            t = r[:, :E].cpu().numpy()[ok]
+            f = r[:, E].cpu().numpy()[ok] if self.spec.fm else None
+            return rows[ok], t, f
         t = self.table[: self.local_rows].cpu().numpy()[ok]
         f = self.first[: self.local_rows].cpu().numpy()[ok] if self.first is not None else None
         return rows[ok], t, f
@@ -199,6 +226,15 @@ class ShardedCTREngine(CTREngine):
         L = self.layout
         L.batch = B
         W = self.world
+        lazy = self.lazy
+        if lazy:
+            if self.since_flush >= self.hist_len - 2:   # bound every row's lag below the alpha ring
+                self.flush()
+            self.since_flush += 1
+            self.row_list_n.zero_()
+        call("dl_adam_begin_step", ptr(self.opt), sp.decay_rate, float(sp.decay_steps), s)
+        if lazy:
+            call("dl_adam_hist_record", ptr(self.opt), ptr(self.hist), self.hist_len, s)
         # 1. index (rows grouped by owner; replicated rows last)
         self._c("index_build", "dl_index_build", C_ref(L), ptr(self.in_cate), W, self.rep, ptr(self.idx_ws),
                 self.idx_ws.numel(), ptr(self.idx_keys), ptr(self.idx_refs), ptr(self.idx_uniq),
@@ -215,14 +251,18 @@ class ShardedCTREngine(CTREngine):
         # 3. owners gather requested rows
         out_v = torch.empty(max(nrecv, 1), E, device=self.dev)
         out_1 = torch.empty(max(nrecv, 1), device=self.dev)
-        if nrecv:
+        if nrecv and lazy:   # rows caught up to the previous step (read only)
+            self._c("rec_gather", "dl_rec_gather", C_ref(L), ptr(self.rec), self.rec_ld, int(sp.fm), 0,
+                    ptr(recv_ids), None, nrecv, 1, ptr(self.hist), self.hist_len, ptr(self.opt), 1, ptr(out_v),
+                    ptr(out_1) if sp.fm else None, None, s)
+        elif nrecv:
             call("dl_shard_gather", ptr(self.table), ptr(self.first), ptr(recv_ids), nrecv, E, ptr(out_v),
                  ptr(out_1) if self.first is not None else None, s)
         # 4. rows back, in unique-id order
         rv = ex.all_to_all(out_v[:nrecv], recv, send)
         rep = self.rep
         self.rows_u[rep: rep + nsend].copy_(rv)
-        if self.first is not None:
+        if sp.fm:
             r1 = ex.all_to_all(out_1[:nrecv], recv, send)
             self.rows_u1[rep: rep + nsend].copy_(r1)
         if rep:
@@ -234,7 +274,6 @@ class ShardedCTREngine(CTREngine):
                  ptr(self.send_ids[nsend:U]), nrep, E, ptr(self.rows_u[rep + nsend:]),
                  ptr(self.rows_u1[rep + nsend:]) if sp.fm else None, s)
         # 5. forward + dense backward
-        call("dl_adam_begin_step", ptr(self.opt), sp.decay_rate, float(sp.decay_steps), s)
         self._c("embed_fwd", "dl_embed_fwd_indexed", C_ref(L), ptr(self.rows_u), ptr(self.rows_u1) if sp.fm else None,
                 ptr(self.inv), rep, ptr(self.in_cont), ptr(self.in_vec), ptr(self.x0), ptr(self.fm_out),
                 ptr(self.fm_sum), s)
@@ -276,7 +315,11 @@ class ShardedCTREngine(CTREngine):
                 ptr(self.w_head), ptr(self.fm_sum), ptr(self.dx0), ptr(self.gU), ptr(self.g1U), None, 1, s)
         gb = ex.all_to_all(self.gU[:nsend], send, recv)
         g1b = ex.all_to_all(self.g1U[:nsend], send, recv) if sp.fm else None
-        if nrecv:
+        if nrecv and lazy:
+            call("dl_rec_scatter_list", ptr(gb), ptr(g1b) if sp.fm else None, ptr(recv_ids), nrecv, E,
+                 ptr(self.tg), ptr(self.fmg) if sp.fm else None, ptr(self.row_flags), ptr(self.row_list),
+                 ptr(self.row_list_n), s)
+        elif nrecv:
             call("dl_shard_scatter_add", ptr(gb), ptr(g1b) if sp.fm else None, ptr(recv_ids), nrecv, E,
                  ptr(self.tg), ptr(self.fmg) if sp.fm else None, ptr(self.touched), s)
         # replicated rows: cate-id refs + the FM cont fields, into the flat buffer
@@ -312,7 +355,13 @@ class ShardedCTREngine(CTREngine):
             if sp.fm:
                 call("dl_adam_rows", ptr(self.rep_f), ptr(self.rep_fm), ptr(self.rep_fv), ptr(self.rep_fg),
                      ptr(self.rep_touched), self.rep_f.shape[0], 1, 0.0, 0, ptr(self.opt), None, s)
-        if sp.fm:
+        if lazy:
+            if nrecv:
+                self._c("adam_table", "dl_rec_apply_list", ptr(self.rec), self.rec_ld, E, int(sp.fm),
+                        ptr(self.row_list), ptr(self.row_list_n), min(nrecv, self.rows_pad), ptr(self.tg),
+                        ptr(self.fmg) if sp.fm else None, ptr(self.row_flags), ptr(self.hist), self.hist_len,
+                        ptr(self.opt), s)
+        elif sp.fm:
             self._c("adam_table", "dl_adam_rows", ptr(self.table), ptr(self.tm), ptr(self.tv), ptr(self.tg),
                     ptr(self.touched), self.table.shape[0], E, 0.0, 0, ptr(self.opt), None, s)
             self._c("adam_first", "dl_adam_rows", ptr(self.first), ptr(self.fmm), ptr(self.fmv), ptr(self.fmg),

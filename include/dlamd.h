@@ -251,7 +251,8 @@ int dl_adam_rows(float* p, float* m, float* v, float* g, uint8_t* touched, int64
 int dl_adam_hist_record(const float* opt, float* hist, int32_t hist_len, void* stream);
 /* rows_u[i] = p(row_i) caught up to step opt[7]-lag (rows_u1[i] = w1), row_i = i
  * for i < n_rep (replicated rows) else the row of uniq_keys[i-n_rep] (batch index,
- * dl_index_build keys).  Records are only read.  mv_u (may be NULL) receives the
+ * dl_index_build keys; n_uniq = NULL: max_uniq keys, e.g. an owner's received local
+ * rows with world = 1).  Records are only read.  mv_u (may be NULL) receives the
  * caught-up moments [i][2E+4] = m(E) | v(E) | m1 v1 0 0 for dl_rec_bwd_adam.
  * lag = 1 inside a training step, 0 for predict. */
 int dl_rec_gather(const dl_emb_layout* L, const float* rec, int32_t rec_ld, int32_t has_first,
@@ -273,6 +274,16 @@ int dl_rec_bwd_adam(const dl_emb_layout* L, float* rec, int32_t rec_ld, int32_t 
 int dl_rec_apply_rows(float* rec, int32_t rec_ld, int32_t emb_dim, int32_t has_first, int64_t row0,
                       int64_t n, float* g, float* g1, const float* hist, int32_t hist_len,
                       const float* opt, void* stream);
+/* Sharded owners: G[ids[i]] += g[i] (E floats), G1[ids[i]] += g1[i] (f32 atomics; a row
+ * may come from several peers); the first arrival of a row sets flags[row] and appends
+ * it to list (list_n[0] = count, zeroed by the caller before the step). */
+int dl_rec_scatter_list(const float* g, const float* g1, const int32_t* ids, int64_t n, int32_t emb_dim,
+                        float* G, float* G1, int32_t* flags, int32_t* list, int32_t* list_n, void* stream);
+/* Step-t update (catch-up, then the gradient G[row], G1[row]) of the min(list_n, cap)
+ * listed rows; G, G1 and flags of those rows are reset. */
+int dl_rec_apply_list(float* rec, int32_t rec_ld, int32_t emb_dim, int32_t has_first, const int32_t* list,
+                      const int32_t* list_n, int64_t cap, float* G, float* G1, int32_t* flags,
+                      const float* hist, int32_t hist_len, const float* opt, void* stream);
 /* Every row caught up to step opt[7] (before export/checkpoint, and every hist_len steps). */
 int dl_rec_flush(float* rec, int32_t rec_ld, int32_t emb_dim, int32_t has_first, int64_t n_rows,
                  const float* hist, int32_t hist_len, const float* opt, void* stream);

@@ -127,14 +127,14 @@ def run_sim(rank, world, steps, Bl, out_dir):
     np.savez(os.path.join(out_dir, "rank%d.npz" % rank), **P)
 
 
-def run_gpu(rank, world, steps, Bl, out_dir):
+def run_gpu(rank, world, steps, Bl, out_dir, adam="dense"):
     from deep_learning_amd.engine import ModelSpec
     from deep_learning_amd.shard import Exchange, ShardedCTREngine
     torch.cuda.set_device(0)
     ex = Exchange()
     cfg = R.make_cfg("deepfm_pipeline", **KW)
     P = R.init_params(cfg, np.random.default_rng(42))
-    eng = ShardedCTREngine(ModelSpec("deepfm_pipeline", **KW), Bl, ex)
+    eng = ShardedCTREngine(ModelSpec("deepfm_pipeline", **KW), Bl, ex, adam=adam, hist_len=4)
     eng.load_params(P)
     for step, bg in enumerate(global_batches(Bl * world, steps)):
         eng.train_step(local(bg, rank, world))
@@ -154,6 +154,6 @@ if __name__ == "__main__":
     if mode == "sim":
         run_sim(rank, world, steps, Bl, out_dir)
     else:
-        run_gpu(rank, world, steps, Bl, out_dir)
+        run_gpu(rank, world, steps, Bl, out_dir, adam="lazy" if mode == "gpu_lazy" else "dense")
     dist.barrier()
     dist.destroy_process_group()

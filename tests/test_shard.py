@@ -17,7 +17,7 @@ sys.path.insert(0, ROOT)
 from oracle import ctr_ref as R  # noqa: E402
 from tests.shard_worker import KW, global_batches  # noqa: E402
 
-STEPS, BL, WORLD = 3, 96, 2
+STEPS, BL, WORLD = 5, 96, 2
 
 
 def _free_port():
@@ -59,8 +59,11 @@ def test_shard_sim_gloo_equals_global_batch(tmp_path):
 
 
 @pytest.mark.gpu
-def test_sharded_engine_two_ranks_equals_global_batch(tmp_path):
-    _launch("gpu", tmp_path)
+@pytest.mark.parametrize("mode", ["gpu", "gpu_lazy"])
+def test_sharded_engine_two_ranks_equals_global_batch(tmp_path, mode):
+    """gpu_lazy: shard rows as records with lazy-exact Adam and a 4-entry alpha ring
+    (flushes inside the 5 steps)."""
+    _launch(mode, tmp_path)
     P, zs = _oracle()
     for step in range(STEPS):
         z = np.concatenate([np.load(tmp_path / ("rank%d_step%d.npz" % (r, step)))["z"] for r in range(WORLD)])
