@@ -149,6 +149,7 @@ __global__ __launch_bounds__(256) void rec_bwd_adam_kernel(SegGradIn sg, float* 
                                                            const uint32_t* __restrict__ uniq,
                                                            const int32_t* __restrict__ n_uniq, int world,
                                                            float* __restrict__ g_rep, float* __restrict__ g1_rep,
+                                                           const float* __restrict__ hist,
                                                            const float* __restrict__ opt) {
   rec_load_hyper(c, opt);
   constexpr int LPR = E / 4;
@@ -172,14 +173,27 @@ __global__ __launch_bounds__(256) void rec_bwd_adam_kernel(SegGradIn sg, float* 
     const int64_t row = decode_key(uniq[u], world);
     // the row's caught-up state (independent of the segment walk: issued first)
     const long long iu = n_rep + u;
-    float4 p = *reinterpret_cast<const float4*>(rows_u + iu * E + 4 * q);
-    const float* o = mv + iu * (2 * E + 4);
-    float4 m = *reinterpret_cast<const float4*>(o + 4 * q);
-    float4 v = *reinterpret_cast<const float4*>(o + E + 4 * q);
+    float4 p, m, v;
     float w = 0.f, wm = 0.f, wv = 0.f;
-    if (first) { w = rows_u1[iu]; wm = o[2 * E]; wv = o[2 * E + 1]; }
+    const bool row_ok = row >= 0 && row < L.n_rows;
+    if (mv) {
+      p = *reinterpret_cast<const float4*>(rows_u + iu * E + 4 * q);
+      const float* o = mv + iu * (2 * E + 4);
+      m = *reinterpret_cast<const float4*>(o + 4 * q);
+      v = *reinterpret_cast<const float4*>(o + E + 4 * q);
+      if (first) { w = rows_u1[iu]; wm = o[2 * E]; wv = o[2 * E + 1]; }
+    } else if (row_ok) {   // no stash: re-read the record and replay its catch-up
+      const float* r = rec + row * c.ld;
+      p = *reinterpret_cast<const float4*>(r + 4 * q);
+      m = *reinterpret_cast<const float4*>(r + E + 4 + 4 * q);
+      v = *reinterpret_cast<const float4*>(r + 2 * E + 4 + 4 * q);
+      const float4 tail = *reinterpret_cast<const float4*>(r + E);
+      w = tail.x; wm = tail.y; wv = tail.z;
+      const int stamp = __float_as_int(tail.w);
+      if (stamp < t - 1) catch_up4(p, m, v, w, wm, wv, first, stamp, t - 1, hist, c);
+    }
     const SegGrad4 s = segment_grad4<E>(sg, u, q, nrefs, wsec);
-    if (row < 0 || row >= L.n_rows) continue;
+    if (!row_ok) continue;
     float4 g;
     g.x = seg_row_grad(s.s.x, s.dsum.x, s.x.x, s.dsum.x != 0.f ? p.x : 0.f);
     g.y = seg_row_grad(s.s.y, s.dsum.y, s.x.y, s.dsum.y != 0.f ? p.y : 0.f);
@@ -359,10 +373,12 @@ extern "C" int dl_rec_bwd_adam(const dl_emb_layout* L, float* rec, int32_t rec_l
                                const uint32_t* uniq_keys, const int32_t* seg_off, const int32_t* n_uniq,
                                const int32_t* sorted_refs, int32_t world, int64_t max_uniq, const float* dz,
                                const float* w_head, const float* fm_sum, const float* dx0, float* g_rep,
-                               float* g1_rep, const float* opt, void* stream) {
-  DL_CHECK_ARG(L && rec && rows_u && mv_u && uniq_keys && seg_off && n_uniq && sorted_refs && dx0 && opt,
+                               float* g1_rep, const float* hist, int32_t hist_len, const float* opt,
+                               void* stream) {
+  DL_CHECK_ARG(L && rec && rows_u && uniq_keys && seg_off && n_uniq && sorted_refs && dx0 && opt,
                "NULL argument");
-  if (int rc = rec_check(L->emb_dim, rec_ld, 2)) return rc;
+  DL_CHECK_ARG(mv_u || hist, "without the moment stash the alpha ring is required");
+  if (int rc = rec_check(L->emb_dim, rec_ld, mv_u ? 2 : hist_len)) return rc;
   DL_CHECK_ARG(!L->use_fm || (dz && w_head && fm_sum), "FM backward inputs required");
   DL_CHECK_ARG(!has_first || rows_u1, "rows_u1 required with first-order weights");
   DL_CHECK_ARG(n_rep == 0 || g_rep, "g_rep required with replicated rows");
@@ -373,9 +389,9 @@ extern "C" int dl_rec_bwd_adam(const dl_emb_layout* L, float* rec, int32_t rec_l
   DL_DISPATCH_E(L->emb_dim, {
     const unsigned grid = grid_cap(max_uniq * (kE / 4));
     hipLaunchKernelGGL(rec_bwd_adam_kernel<kE>, dim3(grid), dim3(256), 0, as_stream(stream), sg, rec,
-                       RecCfg{kE, rec_ld, has_first, 1, 0.f, 0.f, 0.f}, n_rep, rows_u,
+                       RecCfg{kE, rec_ld, has_first, (mv_u ? 2 : hist_len) - 1, 0.f, 0.f, 0.f}, n_rep, rows_u,
                        has_first ? rows_u1 : nullptr, mv_u, uniq_keys, n_uniq, world, g_rep,
-                       has_first ? g1_rep : nullptr, opt);
+                       has_first ? g1_rep : nullptr, hist, opt);
   });
   DL_RETURN_LAUNCH("dl_rec_bwd_adam");
 }

@@ -114,7 +114,7 @@ class ModelSpec:
 
 class CTREngine:
     def __init__(self, spec, max_batch, device="cuda", seed=2019, init="device", bwd="atomic",
-                 table_rows=None, adam="dense", hist_len=4096):
+                 table_rows=None, adam="dense", hist_len=4096, rec_stash=False):
         if not torch.cuda.is_available():
             raise _lib.DLError("CTREngine needs a HIP device (no CPU fallback)")
         _lib.lib()
@@ -231,7 +231,10 @@ class CTREngine:
         if self.lazy:
             self.rows_u = z(self.n_rep + self.n_refs, E)
             self.rows_u1 = z(self.n_rep + self.n_refs)
-            self.mv_u = z(self.n_rep + self.n_refs, 2 * E + 4)
+            # rec_stash: the gather also stashes the caught-up moments for the backward's update.
+            # Off by default — re-reading the record in the backward measured faster on both
+            # kernels (gather 328 -> 232 us, backward 505 -> 447 us at C2; profiles/r01l).
+            self.mv_u = z(self.n_rep + self.n_refs, 2 * E + 4) if rec_stash else None
         # static input slots (graph capture reads from these)
         self.in_label = z(B)
         self.in_cont = z(B, max(sp.C, 1))
@@ -490,7 +493,7 @@ class CTREngine:
             self._c("rec_gather", "dl_rec_gather", C_ref(L), ptr(self.rec), self.rec_ld, int(sp.fm), self.n_rep,
                     ptr(self.idx_uniq), ptr(self.idx_n), B * self.n_slot, 1, ptr(self.hist), self.hist_len,
                     ptr(self.opt), 1 if train else 0, ptr(self.rows_u), ptr(self.rows_u1),
-                    ptr(self.mv_u) if train else None, s)
+                    ptr(self.mv_u) if (train and self.mv_u is not None) else None, s)
             self._c("embed_fwd", "dl_embed_fwd_indexed", C_ref(L), ptr(self.rows_u),
                     ptr(self.rows_u1) if sp.fm else None, ptr(self.idx_inv), self.n_rep, ptr(self.in_cont),
                     ptr(self.in_vec), ptr(self.x0), ptr(self.fm_out), ptr(self.fm_sum), s)
@@ -571,7 +574,8 @@ class CTREngine:
             self._c("embed_bwd", "dl_rec_bwd_adam", C_ref(L), ptr(self.rec), self.rec_ld, int(sp.fm), R,
                     ptr(self.rows_u), ptr(self.rows_u1), ptr(self.mv_u), ptr(self.idx_uniq), ptr(self.idx_off),
                     ptr(self.idx_n), ptr(self.idx_refs), 1, B * self.n_slot, ptr(self.dz), ptr(self.w_head),
-                    ptr(self.fm_sum), ptr(self.dx0), ptr(self.g_rep), ptr(self.g1_rep), ptr(self.opt), s)
+                    ptr(self.fm_sum), ptr(self.dx0), ptr(self.g_rep), ptr(self.g1_rep), ptr(self.hist),
+                    self.hist_len, ptr(self.opt), s)
             if R:
                 # FM cont-field rows: per-block register partials, folded into g_rep, then updated
                 self._c("cont_bwd", "dl_embed_cont_bwd", C_ref(L), ptr(self.rows_u), ptr(self._cont()),

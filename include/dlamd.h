@@ -262,14 +262,15 @@ int dl_rec_gather(const dl_emb_layout* L, const float* rec, int32_t rec_ld, int3
 /* Fused backward + Adam: per unique row the ordered segment sum of its references
  * (as dl_embed_bwd_sorted) is applied with step opt[7]'s alpha to the caught-up
  * state of dl_rec_gather (rows_u, rows_u1, mv_u — full arrays, replicated rows
- * first), and the record is written with stamp = step.  Rows < n_rep instead add
+ * first; mv_u = NULL: the record is re-read and its catch-up replayed, using
+ * hist), and the record is written with stamp = step.  Rows < n_rep instead add
  * their gradient into g_rep[row][E] / g1_rep[row] (finished by dl_rec_apply_rows). */
 int dl_rec_bwd_adam(const dl_emb_layout* L, float* rec, int32_t rec_ld, int32_t has_first, int32_t n_rep,
                     const float* rows_u, const float* rows_u1, const float* mv_u,
                     const uint32_t* uniq_keys, const int32_t* seg_off, const int32_t* n_uniq,
                     const int32_t* sorted_refs, int32_t world, int64_t max_uniq, const float* dz,
                     const float* w_head, const float* fm_sum, const float* dx0, float* g_rep,
-                    float* g1_rep, const float* opt, void* stream);
+                    float* g1_rep, const float* hist, int32_t hist_len, const float* opt, void* stream);
 /* Rows [row0, row0+n): step-t update with dense gradients g[n][E], g1[n] (zeroed after). */
 int dl_rec_apply_rows(float* rec, int32_t rec_ld, int32_t emb_dim, int32_t has_first, int64_t row0,
                       int64_t n, float* g, float* g1, const float* hist, int32_t hist_len,

@@ -91,8 +91,9 @@ def test_graph_replay_equals_eager(hip_lib):
     np.testing.assert_allclose(res[0], res[1], atol=1e-6)
 
 
+@pytest.mark.parametrize("stash", [False, True])
 @pytest.mark.parametrize("name", ["deepfm_pipeline", "dnn_pipeline", "wdl"])
-def test_lazy_adam_bit_identical_to_dense(hip_lib, name):
+def test_lazy_adam_bit_identical_to_dense(hip_lib, name, stash):
     """Row records + lazy catch-up (rec.hip) against the dense sweep with the same
     (sorted, deterministic) gradients: parameters, Adam moments, logits and
     predictions must be bit-identical.  A large table, a small batch and an 8-entry
@@ -101,7 +102,7 @@ def test_lazy_adam_bit_identical_to_dense(hip_lib, name):
     model = _model(name)
     spec = ModelSpec(model, **kw)
     dense = CTREngine(spec, max_batch=128, seed=3, bwd="sorted")
-    lazy = CTREngine(spec, max_batch=128, seed=3, adam="lazy", hist_len=8)
+    lazy = CTREngine(spec, max_batch=128, seed=3, adam="lazy", hist_len=8, rec_stash=stash)
     np.testing.assert_array_equal(lazy.params()["weight_mat" if model == "wdl" else "feats_emb"],
                                   dense.params()["weight_mat" if model == "wdl" else "feats_emb"])
     bs = _batches(name, kw, 128, 21, seed=7)
