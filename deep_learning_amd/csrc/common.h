@@ -62,6 +62,8 @@ __device__ __forceinline__ void adam_elem(float& p, float& m, float& v, float g,
                                           float omb1, float omb2, float eps) {
   m = fmaf(g - m, omb1, m);
   v = fmaf(fmaf(g, g, -v), omb2, v);
+  // correctly rounded sqrt and divide, as TF's Eigen kernel: the hardware v_sqrt/v_rcp
+  // forms measured no faster in the record kernels (profiles/r01l), so exactness stays
   p -= (m * alpha) / (sqrtf(v) + eps);
 }
 
