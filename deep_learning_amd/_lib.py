@@ -6,7 +6,8 @@ import ctypes as C
 import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libdlamd.so")
+LIB_PATH = os.path.join(HERE, "libdlamd%s.so" % ("_" + os.environ["DLAMD_VARIANT"]
+                                                   if os.environ.get("DLAMD_VARIANT") else ""))
 
 
 class DLError(RuntimeError):

@@ -13,12 +13,16 @@ import sys
 HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 CSRC = os.path.join(HERE, "csrc")
-OUT = os.path.join(HERE, "libdlamd.so")
-OBJ = os.path.join(HERE, "_build")
+# DLAMD_VARIANT=name builds an experiment variant (extra -D flags from DLAMD_DEFINES)
+# into libdlamd_<name>.so with its own object directory; the default build is untouched.
+VARIANT = os.environ.get("DLAMD_VARIANT", "")
+OUT = os.path.join(HERE, "libdlamd%s.so" % ("_" + VARIANT if VARIANT else ""))
+OBJ = os.path.join(HERE, "_build" + ("_" + VARIANT if VARIANT else ""))
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = os.environ.get("DLAMD_ARCH", "gfx950")
 FLAGS = ["-O3", "-std=c++17", "-fPIC", "--offload-arch=" + ARCH, "-munsafe-fp-atomics",
-         "-Wno-unused-result", "-I" + os.path.join(ROOT, "include")]
+         "-Wno-unused-result", "-I" + os.path.join(ROOT, "include")] + \
+    (["-D" + d for d in os.environ.get("DLAMD_DEFINES", "").split()] if VARIANT else [])
 
 
 def _sources():

@@ -25,6 +25,13 @@ namespace dl {
 
 typedef float floatx4 __attribute__((ext_vector_type(4)));
 
+#ifndef DL_GEMM_BK
+#define DL_GEMM_BK 16   // k-slab per LDS stage of the f32 GEMM
+#endif
+#ifndef DL_GEMM_GLDS
+#define DL_GEMM_GLDS 0  // LDS-DMA for the k-contiguous A tile (correct, measured neutral: DESIGN.md §4)
+#endif
+
 struct GemmParams {
   const void* A;
   const void* B;
@@ -60,13 +67,13 @@ __device__ __forceinline__ int xcd_tile(int bid, int T) {
 // 2560 tiles fill exactly two rounds of the 256 CUs (at 3 blocks/CU, 3.3 rounds
 // left a 17 % tail).
 template <int BM, int BN>
-struct GemmOcc { static constexpr int waves = (BM == 128 && BN <= 80) ? 5 : 2; };
+struct GemmOcc { static constexpr int waves = (BM == 128 && BN <= 80 && DL_GEMM_BK == 16) ? 5 : 2; };
 
 template <int BM, int BN, int WM, int WN, bool TA, bool TB, int EPI, int BK>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GemmOcc<BM, BN>::waves)))
 void gemm_f32_kernel(GemmParams p) {
   constexpr bool AKC = !TA, BKC = TB, KPERM = AKC || BKC;
-  constexpr int KCS = BK + 4;   // k-contiguous row stride: 2-way b128 read conflicts, but 5 blocks/CU fit
+  constexpr int KCS = BK == 16 ? BK + 4 : BK + 8;  // BK=16: 2-way b128 read conflicts, but 5 blocks/CU fit
   constexpr int MCPAD_A = KPERM ? (4 - BM % 8 + 8) % 8 : (48 - BM % 32) % 32;
   constexpr int MCPAD_B = KPERM ? (4 - BN % 8 + 8) % 8 : (48 - BN % 32) % 32;
   constexpr int A_ROWS = AKC ? BM : BK, A_LD = AKC ? KCS : BM + MCPAD_A;
@@ -78,7 +85,13 @@ void gemm_f32_kernel(GemmParams p) {
   static_assert(WM * WN == 4, "4 waves");
   static_assert(WTM % 16 == 0 && WTN % 16 == 0 && BK % 16 == 0, "tile shape");
 
-  __shared__ __attribute__((aligned(16))) float As[2][A_ROWS][A_LD];
+  // GLDS: the k-contiguous A tile is filled by LDS-DMA (global_load_lds_dwordx4), which
+  // writes lane-linear 1 KB pieces: the image is unpadded [row][16] and conflict-free
+  // b128 reads come from an XOR swizzle of the 16-B chunks, applied on the SOURCE
+  // address: slot(row, chunk) = 4*row + (chunk ^ ((row >> 1) & 3)).
+  constexpr bool GLDS = DL_GEMM_GLDS && AKC && BK == 16;
+  constexpr int A_LD_EFF = GLDS ? BK : A_LD;
+  __shared__ __attribute__((aligned(16))) float As[2][A_ROWS][A_LD_EFF];
   __shared__ __attribute__((aligned(16))) float Bs[2][B_ROWS][B_LD];
 
   const float* __restrict__ A = reinterpret_cast<const float*>(p.A);
@@ -102,9 +115,23 @@ void gemm_f32_kernel(GemmParams p) {
 
   float4 ra[QA], rb[QB];
 
+  auto glds_a = [&](int k0, int buf) {
+    // 8 pieces of 16 rows for BM = 128: wave w issues pieces w, w + 4, ...
+#pragma unroll
+    for (int g = wid; g < BM / 16; g += 4) {
+      const int row = g * 16 + (lane >> 2);
+      const int chunk = (lane & 3) ^ ((row >> 1) & 3);
+      int gi = i0 + row;
+      gi = gi < p.M ? gi : p.M - 1;                    // rows past M: any valid row (outputs dropped)
+      int gr = k0 + 4 * chunk;
+      gr = gr < kend ? gr : kend - 4;                  // k past kend: B is zero there
+      const float* src = A + (long long)gi * p.lda + gr;
+      __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)&As[buf][g * 16][0], 16, 0, 0);
+    }
+  };
   auto load_tile = [&](int k0) {
 #pragma unroll
-    for (int u = 0; u < QA; ++u) {
+    for (int u = 0; u < (GLDS ? 0 : QA); ++u) {
       const int qi = tid + u * 256;
       float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
       if (qi < BM * BK / 4) {
@@ -140,7 +167,7 @@ void gemm_f32_kernel(GemmParams p) {
   };
   auto store_tile = [&](int buf) {
 #pragma unroll
-    for (int u = 0; u < QA; ++u) {
+    for (int u = 0; u < (GLDS ? 0 : QA); ++u) {
       const int qi = tid + u * 256;
       if (qi < BM * BK / 4) {
         if (TA) {
@@ -168,6 +195,7 @@ void gemm_f32_kernel(GemmParams p) {
   };
 
   if (nk > 0) {
+    if (GLDS) glds_a(kbeg, 0);
     load_tile(kbeg);
     store_tile(0);
     __syncthreads();
@@ -175,14 +203,19 @@ void gemm_f32_kernel(GemmParams p) {
   const int kr = lane >> 4, cl = lane & 15;
   for (int kt = 0; kt < nk; ++kt) {
     const int cur = kt & 1;
+    if (GLDS && kt + 1 < nk) glds_a(kbeg + (kt + 1) * BK, cur ^ 1);
     if (kt + 1 < nk) load_tile(kbeg + (kt + 1) * BK);
 #pragma unroll
     for (int s16 = 0; s16 < BK / 16; ++s16) {
       float4 a4[AKC ? FM : 1], b4[BKC ? FN : 1];
       if (AKC) {
 #pragma unroll
-        for (int a = 0; a < FM; ++a)
-          a4[a] = *reinterpret_cast<const float4*>(&As[cur][AKC ? wm * WTM + a * 16 + cl : 0][s16 * 16 + 4 * kr]);
+        for (int a = 0; a < FM; ++a) {
+          if (GLDS)
+            a4[a] = *reinterpret_cast<const float4*>(&As[cur][wm * WTM + a * 16 + cl][4 * (kr ^ ((cl >> 1) & 3))]);
+          else
+            a4[a] = *reinterpret_cast<const float4*>(&As[cur][AKC ? wm * WTM + a * 16 + cl : 0][s16 * 16 + 4 * kr]);
+        }
       }
       if (BKC) {
 #pragma unroll
@@ -336,7 +369,7 @@ __global__ __launch_bounds__(256) void gemm_bf16_kernel(GemmParams p) {
 
 template <int BM, int BN, int WM, int WN, bool TA, bool TB>
 static void launch_f32(const GemmParams& gp, int epi, int splits, hipStream_t s) {
-  constexpr int BK = 16;
+  constexpr int BK = DL_GEMM_BK;
   const int tiles = (int)(ceil_div(gp.M, BM) * ceil_div(gp.N, BN));
   dim3 grid(tiles, 1, splits);
   switch (epi) {
