@@ -140,9 +140,16 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    torch.cuda.set_device(local)
+    # DLAMD_BENCH_BACKEND=gloo: rehearsal of the multi-rank flow with ranks sharing one GPU
+    # (host-staged exchange); the measured configuration is nccl = RCCL, one GPU per rank.
+    backend = os.environ.get("DLAMD_BENCH_BACKEND", "nccl")
+    dev_index = local if backend == "nccl" else local % max(1, torch.cuda.device_count())
+    torch.cuda.set_device(dev_index)
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", dev_index))
+        else:
+            dist.init_process_group(backend)
 
     def barrier():
         if world > 1:
