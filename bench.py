@@ -29,6 +29,7 @@ sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md)
 F32_MFMA_PEAK_TFLOPS = 157.3    # v_mfma_f32_16x16x4_f32 dense peak
+BF16_MFMA_PEAK_TFLOPS = 2516.6  # dense bf16 MFMA peak (MI355X_MICROARCH.md; no sparsity)
 
 C2 = dict(C=13, V=0, S=26, E=16, per_field_vocab=1_000_000, hidden=[400, 400, 400], B=65536)
 
@@ -47,7 +48,7 @@ def kernel_work(spec, B, touched_rows, rows=None, uniq=None):
     # dense TF1 Adam: read+write p, m, v for every element; gradient rows read+reset only where touched
     w["adam_table"] = ("hbm", N * E * 4 * 6 + touched_rows * E * 4 * 2 + N)
     w["adam_first"] = ("hbm", N * 4 * 6 + touched_rows * 4 * 2 + N)
-    dims = [C + spec.V + S * E] + spec.hidden
+    dims = [spec.deep_in] + spec.hidden
     for l in range(len(spec.hidden)):
         f = 2.0 * B * (dims[l] + 1) * dims[l + 1]
         w["gemm_fwd_l%d" % l] = ("mfma", f)
@@ -128,6 +129,9 @@ def main():
     ap.add_argument("--vocab", type=int, default=0,
                     help="per-field vocab (default: 1M at N=1 = C2; 100M/26 at N>1 = C4's 100M-row table)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--workload", default="c2", choices=["c2", "c3", "c5"],
+                    help="c2 DeepFM (the headline, default); c3 deepfm_multi_cate 6 multi-hot slots x 60; "
+                         "c5 Wide&Deep with the bf16 tower (single GPU)")
     ap.add_argument("--adam", default="lazy", choices=["dense", "lazy"],
                     help="table Adam: dense sweep, or row records with lazy-exact catch-up (same result)")
     args = ap.parse_args()
@@ -158,8 +162,19 @@ def main():
     B = args.batch
     if not args.vocab:
         args.vocab = C2["per_field_vocab"] if world == 1 else 100_000_000 // C2["S"]
-    spec = ModelSpec("deepfm_pipeline", C=C2["C"], V=0, S=C2["S"], E=C2["E"],
-                     cate_index_size=C2["S"] * args.vocab, hidden=C2["hidden"])
+    wl = args.workload
+    if wl != "c2" and world > 1:
+        raise SystemExit("--workload %s is single-GPU here; the multi-GPU path is C4 (default)" % wl)
+    if wl == "c3":
+        args.adam = "dense"            # row records do not cover multi-hot pooling yet
+        spec = ModelSpec("deepfm_multi_cate", C=0, V=0, S=C2["S"], E=C2["E"], cate_index_size=C2["S"] * args.vocab,
+                         hidden=C2["hidden"], multi_ranges=[[60 * i, 60 * (i + 1), "slot%d" % i] for i in range(6)])
+    elif wl == "c5":
+        spec = ModelSpec("wdl", C=C2["C"], S=C2["S"], E=C2["E"], cate_index_size=C2["S"] * args.vocab,
+                         hidden=C2["hidden"], Fw=26, tower="bf16")
+    else:
+        spec = ModelSpec("deepfm_pipeline", C=C2["C"], V=0, S=C2["S"], E=C2["E"],
+                         cate_index_size=C2["S"] * args.vocab, hidden=C2["hidden"])
     log("rank %d/%d: building engine, table rows %d" % (rank, world, spec.n_rows))
     use_graph = world == 1
     if world == 1:
@@ -171,7 +186,12 @@ def main():
     nb = 4
     dev_batches = []
     for i in range(nb):
-        b = make_batch(B, cate_index_size=spec.cate_index_size, seed=1000 * rank + i, dist=args.dist)
+        if wl == "c3":
+            b = make_batch(B, cont=0, cate_fields=C2["S"], cate_index_size=spec.cate_index_size, multi_slots=6,
+                           multi_width=60, seed=1000 * rank + i, dist=args.dist, cate_only=True)
+        else:
+            b = make_batch(B, cate_index_size=spec.cate_index_size, seed=1000 * rank + i, dist=args.dist,
+                           wide_fields=spec.Fw)
         dev_batches.append({k: torch.from_numpy(v).cuda() for k, v in b.items()})
     torch.cuda.synchronize()
     log("warmup %d" % args.warmup)
@@ -225,8 +245,9 @@ def main():
                 ent["GB/s"] = round(amount / (us * 1e-6) / 1e9, 1)
                 ent["frac_hbm"] = round(amount / (us * 1e-6) / 1e9 / HBM_PEAK_GBS, 3)
             else:
+                peak = BF16_MFMA_PEAK_TFLOPS if spec.tower == "bf16" else F32_MFMA_PEAK_TFLOPS
                 ent["TFLOP/s"] = round(amount / (us * 1e-6) / 1e12, 2)
-                ent["frac_mfma"] = round(amount / (us * 1e-6) / 1e12 / F32_MFMA_PEAK_TFLOPS, 3)
+                ent["frac_mfma"] = round(amount / (us * 1e-6) / 1e12 / peak, 3)
         kernels[label] = ent
     dom = max((l for l in kernels), key=lambda l: kernels[l]["us"])
     kind, amount = work.get(dom, ("hbm", 0))
@@ -237,8 +258,9 @@ def main():
                 "frac": round(ach / HBM_PEAK_GBS, 3), "traffic": None, "algorithmic_bytes": amount}
     else:
         ach = amount / (us * 1e-6) / 1e12
-        roof = {"kernel": dom, "bound": "mfma", "achieved": round(ach, 2), "peak": F32_MFMA_PEAK_TFLOPS,
-                "unit": "TFLOP/s", "frac": round(ach / F32_MFMA_PEAK_TFLOPS, 3), "traffic": None,
+        peak = BF16_MFMA_PEAK_TFLOPS if spec.tower == "bf16" else F32_MFMA_PEAK_TFLOPS
+        roof = {"kernel": dom, "bound": "mfma", "achieved": round(ach, 2), "peak": peak,
+                "unit": "TFLOP/s", "frac": round(ach / peak, 3), "traffic": None,
                 "algorithmic_flops": amount}
     step_kernel_us = sum(k["us"] for k in kernels.values())
     pmc = pmc_traffic(dom, world, lazy=uniq is not None)
@@ -268,10 +290,15 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "f32",
+            "dtype": "bf16+f32" if wl == "c5" else "f32",
             "data": "synthetic (seeded Criteo-shaped batches, %s ids, resident in HBM)" % args.dist,
-            "config": {"workload": "C2 deepfm_pipeline: 13 dense + 26 cat x %d vocab (table %d x 16 f32), "
-                                   "MLP [400,400,400], TF1-dense Adam" % (args.vocab, spec.n_rows),
+            "config": {"workload": {"c2": "C2 deepfm_pipeline: 13 dense + 26 cat x %d vocab (table %d x 16 f32), "
+                                          "MLP [400,400,400], TF1-dense Adam",
+                                    "c3": "C3 deepfm_multi_cate: 26 cat + 6 multi-hot slots x 60 over %d vocab "
+                                          "(table %d x 16 f32), MLP [400,400,400], TF1-dense Adam",
+                                    "c5": "C5 wdl: 13 dense + 26 deep cat + 26 wide ids x %d vocab (table %d x 16), "
+                                          "bf16 MLP [400,400,400] (fp32 master), fp32 wide logit, TF1-dense Adam",
+                                    }[wl] % (args.vocab, spec.n_rows),
                        "global_batch": B * world, "per_gpu_batch": B,
                        "parallelism": "dp%d" % world if world == 1 else
                        "dp%d + row-sharded table (RCCL all-to-all lookup, all-reduce dense grads)" % world,

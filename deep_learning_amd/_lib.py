@@ -63,6 +63,8 @@ SIGNATURES = {
     "dl_adam_rows": (I32, [P, P, P, P, P, I64, I32, F, I32, P, P, P]),
     "dl_init_random": (I32, [P, I64, I32, F, F, U64, U64, P]),
     "dl_transpose_f32": (I32, [P, I32, I32, I32, P, I32, P]),
+    "dl_cast_bf16": (I32, [P, I32, I32, I32, P, I32, P]),
+    "dl_transpose_bf16": (I32, [P, I32, I32, I32, I32, P, I32, P]),
     "dl_adam_hist_record": (I32, [P, P, I32, P]),
     "dl_rec_gather": (I32, [LP, P, I32, I32, I32, P, P, I64, I32, P, I32, P, I32, P, P, P, P]),
     "dl_rec_bwd_adam": (I32, [LP, P, I32, I32, I32, P, P, P, P, P, P, P, I32, I64, P, P, P, P, P, P, P, I32, P, P]),

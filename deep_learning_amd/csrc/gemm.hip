@@ -367,6 +367,152 @@ __global__ __launch_bounds__(256) void gemm_bf16_kernel(GemmParams p) {
     }
 }
 
+// dst[r*ldd + c] = bf16(src[r*lds + c]) (round to nearest even), r < rows, c < cols.
+__global__ __launch_bounds__(256) void cast_bf16_kernel(const float* __restrict__ src, int rows, int cols, int lds,
+                                                        unsigned short* __restrict__ dst, int ldd) {
+  const long long n = (long long)rows * cols;
+  for (long long k = (long long)blockIdx.x * blockDim.x + threadIdx.x; k < n; k += (long long)gridDim.x * blockDim.x) {
+    const long long r = k / cols;
+    const int c = (int)(k % cols);
+    dst[r * ldd + c] = f2bf(src[r * lds + c]);
+  }
+}
+
+// bf16 GEMM with both operands k-contiguous in HBM (A [i][k], B given as [j][k], i.e.
+// ta = 0, tb = 1): the tower's forward (B = W^T copy), dX (B = W) and dW (A = X^T, B = dY^T
+// copies) are all put in this form by the engine, so every LDS image is a straight b128
+// copy and every MFMA fragment one ds_read_b128: lane (cl, kq) holds A[i = cl][k = 8kq..8kq+7]
+// and B[k = 8kq..8kq+7][j = cl] of v_mfma_f32_16x16x32_bf16.  BK = 64 (two MFMA k-steps),
+// LDS rows padded to 80 bf16 = 40 words (conflict-free for the b128 lane groups).
+template <int BM, int BN, int WM, int WN, int EPI, bool CBF16>
+__global__ __launch_bounds__(256) void gemm_bf16_kc_kernel(GemmParams p) {
+  constexpr int BK = 64, SK = BK + 16;
+  constexpr int WTM = BM / WM, WTN = BN / WN;
+  constexpr int FM = WTM / 16, FN = WTN / 16;
+  constexpr int QA = (BM * BK / 8 + 255) / 256, QB = (BN * BK / 8 + 255) / 256;   // uint4 per thread
+  static_assert(WM * WN == 4 && WTM % 16 == 0 && WTN % 16 == 0, "tile");
+  __shared__ __attribute__((aligned(16))) unsigned short As[2][BM][SK];
+  __shared__ __attribute__((aligned(16))) unsigned short Bs[2][BN][SK];
+  const unsigned short* __restrict__ A = reinterpret_cast<const unsigned short*>(p.A);
+  const unsigned short* __restrict__ Bm = reinterpret_cast<const unsigned short*>(p.B);
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm = wid / WN, wn = wid % WN;
+  const int ntm = (p.M + BM - 1) / BM, ntn = (p.N + BN - 1) / BN;
+  const int t = xcd_tile(blockIdx.x, ntm * ntn);
+  const int i0 = (t / ntn) * BM, j0 = (t % ntn) * BN;
+  const int kbeg = blockIdx.z * p.k_per_split;
+  const int kend = min(p.K, kbeg + p.k_per_split);
+  const int nk = (kend - kbeg + BK - 1) / BK;
+  floatx4 acc[FM][FN];
+#pragma unroll
+  for (int a = 0; a < FM; ++a)
+#pragma unroll
+    for (int b = 0; b < FN; ++b) acc[a][b] = floatx4{0.f, 0.f, 0.f, 0.f};
+  uint4 ra[QA], rb[QB];
+  const uint4 z4 = make_uint4(0u, 0u, 0u, 0u);
+  auto load_tile = [&](int k0) {
+#pragma unroll
+    for (int u = 0; u < QA; ++u) {
+      const int q = tid + u * 256, i = q / (BK / 8), k8 = q % (BK / 8);
+      const int gi = i0 + i, gk = k0 + 8 * k8;
+      ra[u] = (q < BM * BK / 8 && gi < p.M && gk < kend)
+                  ? *reinterpret_cast<const uint4*>(A + (long long)gi * p.lda + gk) : z4;
+    }
+#pragma unroll
+    for (int u = 0; u < QB; ++u) {
+      const int q = tid + u * 256, j = q / (BK / 8), k8 = q % (BK / 8);
+      const int gj = j0 + j, gk = k0 + 8 * k8;
+      rb[u] = (q < BN * BK / 8 && gj < p.N && gk < kend)
+                  ? *reinterpret_cast<const uint4*>(Bm + (long long)gj * p.ldb + gk) : z4;
+    }
+  };
+  auto store_tile = [&](int buf) {
+#pragma unroll
+    for (int u = 0; u < QA; ++u) {
+      const int q = tid + u * 256;
+      if (q < BM * BK / 8) *reinterpret_cast<uint4*>(&As[buf][q / (BK / 8)][8 * (q % (BK / 8))]) = ra[u];
+    }
+#pragma unroll
+    for (int u = 0; u < QB; ++u) {
+      const int q = tid + u * 256;
+      if (q < BN * BK / 8) *reinterpret_cast<uint4*>(&Bs[buf][q / (BK / 8)][8 * (q % (BK / 8))]) = rb[u];
+    }
+  };
+  if (nk > 0) {
+    load_tile(kbeg);
+    store_tile(0);
+    __syncthreads();
+  }
+  const int cl = lane & 15, kq = lane >> 4;
+  for (int kt = 0; kt < nk; ++kt) {
+    const int cur = kt & 1;
+    if (kt + 1 < nk) load_tile(kbeg + (kt + 1) * BK);
+#pragma unroll
+    for (int s = 0; s < BK / 32; ++s) {
+      shortx8 av[FM], bv[FN];
+#pragma unroll
+      for (int a = 0; a < FM; ++a)
+        av[a] = *reinterpret_cast<const shortx8*>(&As[cur][wm * WTM + a * 16 + cl][32 * s + 8 * kq]);
+#pragma unroll
+      for (int b = 0; b < FN; ++b)
+        bv[b] = *reinterpret_cast<const shortx8*>(&Bs[cur][wn * WTN + b * 16 + cl][32 * s + 8 * kq]);
+#pragma unroll
+      for (int a = 0; a < FM; ++a)
+#pragma unroll
+        for (int b = 0; b < FN; ++b)
+          acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[a], bv[b], acc[a][b], 0, 0, 0);
+    }
+    if (kt + 1 < nk) store_tile(cur ^ 1);
+    __syncthreads();
+  }
+  const int kr = lane >> 4;
+  const long long zoff = (EPI == EPI_SPLIT) ? (long long)blockIdx.z * p.c_split_stride : 0;
+#pragma unroll
+  for (int a = 0; a < FM; ++a)
+#pragma unroll
+    for (int b = 0; b < FN; ++b) {
+      const int col = j0 + wn * WTN + b * 16 + cl;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int row = i0 + wm * WTM + a * 16 + kr * 4 + j;
+        if (row < p.M && col < p.N) {
+          float v = acc[a][b][j];
+          if (EPI == EPI_RELU) v = fmaxf(v, 0.f);
+          if (EPI == EPI_MASK) {
+            const unsigned short* mk = reinterpret_cast<const unsigned short*>(p.mask);
+            v = bf2f(mk[(long long)row * p.ldm + col]) > 0.f ? v : 0.f;
+          }
+          const long long o = zoff + (long long)row * p.ldc + col;
+          if (CBF16) reinterpret_cast<unsigned short*>(p.C)[o] = f2bf(v);
+          else reinterpret_cast<float*>(p.C)[o] = v;
+        }
+      }
+    }
+}
+
+// dst[c*ldd + r] = bf16(src[r*lds + c]) through a 32x33 LDS tile; src f32 or bf16.
+template <bool SRC_F32>
+__global__ __launch_bounds__(256) void transpose_bf16_kernel(const void* __restrict__ src, int rows, int cols, int lds,
+                                                             unsigned short* __restrict__ dst, int ldd) {
+  __shared__ unsigned short t[32][34];
+  const int c0 = blockIdx.x * 32, r0 = blockIdx.y * 32;
+  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;
+  for (int y = ty; y < 32; y += 8) {
+    const int r = r0 + y, c = c0 + tx;
+    unsigned short v = 0;
+    if (r < rows && c < cols) {
+      const long long o = (long long)r * lds + c;
+      v = SRC_F32 ? f2bf(reinterpret_cast<const float*>(src)[o]) : reinterpret_cast<const unsigned short*>(src)[o];
+    }
+    t[y][tx] = v;
+  }
+  __syncthreads();
+  for (int y = ty; y < 32; y += 8) {
+    const int c = c0 + y, r = r0 + tx;
+    if (c < cols && r < rows) dst[(long long)c * ldd + r] = t[tx][y];
+  }
+}
+
 template <int BM, int BN, int WM, int WN, bool TA, bool TB>
 static void launch_f32(const GemmParams& gp, int epi, int splits, hipStream_t s) {
   constexpr int BK = DL_GEMM_BK;
@@ -427,9 +573,42 @@ __global__ __launch_bounds__(256) void transpose_kernel(const float* __restrict_
   }
 }
 
+template <int BN, int EPI, bool CB>
+static void launch_bf16_kc(const GemmParams& gp, int splits, hipStream_t s) {
+  const int tiles = (int)(ceil_div(gp.M, 128) * ceil_div(gp.N, BN));
+  hipLaunchKernelGGL((gemm_bf16_kc_kernel<128, BN, 4, 1, EPI, CB>), dim3(tiles, 1, splits), dim3(256), 0, s, gp);
+}
+
+template <int BN>
+static void dispatch_bf16_kc_bn(const GemmParams& gp, int epi, int splits, bool cb, hipStream_t s) {
+  switch (epi) {
+    case EPI_STORE: cb ? launch_bf16_kc<BN, EPI_STORE, true>(gp, splits, s) : launch_bf16_kc<BN, EPI_STORE, false>(gp, splits, s); break;
+    case EPI_RELU: cb ? launch_bf16_kc<BN, EPI_RELU, true>(gp, splits, s) : launch_bf16_kc<BN, EPI_RELU, false>(gp, splits, s); break;
+    case EPI_MASK: cb ? launch_bf16_kc<BN, EPI_MASK, true>(gp, splits, s) : launch_bf16_kc<BN, EPI_MASK, false>(gp, splits, s); break;
+    default: launch_bf16_kc<BN, EPI_SPLIT, false>(gp, splits, s); break;
+  }
+}
+
+static void dispatch_bf16_kc(const GemmParams& gp, int epi, int splits, bool cb, int bn, hipStream_t s) {
+  if (bn == 208) dispatch_bf16_kc_bn<208>(gp, epi, splits, cb, s);
+  else dispatch_bf16_kc_bn<80>(gp, epi, splits, cb, s);
+}
+
 }  // namespace dl
 
 using namespace dl;
+
+extern "C" int dl_transpose_bf16(const void* src, int32_t src_f32, int32_t rows, int32_t cols, int32_t lds,
+                                 uint16_t* dst, int32_t ldd, void* stream) {
+  DL_CHECK_ARG(src && dst && rows >= 0 && cols >= 0 && lds >= cols && ldd >= rows, "bad transpose args");
+  if (rows == 0 || cols == 0) return 0;
+  const dim3 grid((unsigned)ceil_div(cols, 32), (unsigned)ceil_div(rows, 32));
+  if (src_f32)
+    hipLaunchKernelGGL(transpose_bf16_kernel<true>, grid, dim3(256), 0, as_stream(stream), src, rows, cols, lds, dst, ldd);
+  else
+    hipLaunchKernelGGL(transpose_bf16_kernel<false>, grid, dim3(256), 0, as_stream(stream), src, rows, cols, lds, dst, ldd);
+  DL_RETURN_LAUNCH("dl_transpose_bf16");
+}
 
 extern "C" int dl_transpose_f32(const float* src, int32_t rows, int32_t cols, int32_t lds, float* dst, int32_t ldd,
                                 void* stream) {
@@ -498,6 +677,18 @@ extern "C" int dl_gemm_bf16(int32_t ta, int32_t tb, int32_t M, int32_t N, int32_
   splits = (int)ceil_div(K > 0 ? K : 1, kps);
   gp.c_split_stride = c_split_stride;
   hipStream_t s = as_stream(stream);
+  if (!ta && tb && lda % 8 == 0 && ldb % 8 == 0 && ((uintptr_t)A % 16) == 0 && ((uintptr_t)B % 16) == 0 &&
+      lda >= (K + 7) / 8 * 8 && ldb >= (K + 7) / 8 * 8) {
+    // k-contiguous fast path (the tower's products are arranged into this form)
+    int kps2 = (int)ceil_div(K, splits);
+    kps2 = (kps2 + 63) / 64 * 64;
+    if (kps2 == 0) kps2 = 64;
+    gp.k_per_split = kps2;
+    const int sp2 = (int)ceil_div(K > 0 ? K : 1, kps2);
+    const int bn = (N + 79) / 80 * 80 <= (N + 207) / 208 * 208 ? 80 : 208;
+    dispatch_bf16_kc(gp, epi, sp2, c_bf16 != 0, bn, s);
+    DL_RETURN_LAUNCH("dl_gemm_bf16");
+  }
 #define DL_BF(TA_, TB_)                                                              \
   if (c_bf16) launch_bf16<128, 64, 4, 1, TA_, TB_, true>(gp, epi, splits, s);        \
   else launch_bf16<128, 64, 4, 1, TA_, TB_, false>(gp, epi, splits, s);
@@ -507,4 +698,15 @@ extern "C" int dl_gemm_bf16(int32_t ta, int32_t tb, int32_t M, int32_t N, int32_
   else { DL_BF(true, true) }
 #undef DL_BF
   DL_RETURN_LAUNCH("dl_gemm_bf16");
+}
+
+extern "C" int dl_cast_bf16(const float* src, int32_t rows, int32_t cols, int32_t lds, uint16_t* dst, int32_t ldd,
+                            void* stream) {
+  DL_CHECK_ARG(src && dst && rows >= 0 && cols >= 0 && lds >= cols && ldd >= cols, "bad cast args");
+  if (rows == 0 || cols == 0) return 0;
+  long long blocks = ((long long)rows * cols + 255) / 256;
+  if (blocks > 8192) blocks = 8192;
+  hipLaunchKernelGGL(cast_bf16_kernel, dim3((unsigned)blocks), dim3(256), 0, as_stream(stream), src, rows, cols, lds,
+                     dst, ldd);
+  DL_RETURN_LAUNCH("dl_cast_bf16");
 }

@@ -46,7 +46,7 @@ class ModelSpec:
 
     def __init__(self, model, C=13, V=0, S=26, E=16, cate_index_size=1000, hidden=(400, 400, 400),
                  multi_ranges=(), Fw=0, lr=0.001, l2=1e-5, decay_steps=10000000, decay_rate=0.9,
-                 beta1=0.9, beta2=0.999, eps=1e-8, logloss_eps=1e-7):
+                 beta1=0.9, beta2=0.999, eps=1e-8, logloss_eps=1e-7, tower="f32"):
         if model not in ("deepfm_pipeline", "dnn_pipeline", "deepfm_multi_cate", "wdl"):
             raise ValueError("unsupported model %r" % model)
         self.model = model
@@ -60,6 +60,9 @@ class ModelSpec:
         self.lr, self.l2 = lr, l2
         self.decay_steps, self.decay_rate = decay_steps, decay_rate
         self.beta1, self.beta2, self.eps, self.logloss_eps = beta1, beta2, eps, logloss_eps
+        if tower not in ("f32", "bf16"):
+            raise ValueError("tower must be 'f32' or 'bf16'")
+        self.tower = tower      # bf16: the deep tower's GEMMs on bf16 MFMA (config C5), fp32 master weights
 
     @property
     def fm(self):
@@ -199,6 +202,25 @@ class CTREngine:
             t[:, hdim] = 1.0
             self.h.append(t)
         self.dh = [z(B, self.h_ld[l]) for l in range(len(sp.hidden))]
+        self.bf = sp.tower == "bf16"
+        if self.bf:
+            # bf16 tower operands: x0 and hidden activations (bias ones columns included),
+            # gradients, and bf16 copies of the fp32 master weights (refreshed after each update)
+            zb = lambda *sh: torch.zeros(*sh, dtype=torch.bfloat16, device=dev)
+            self.x0b = zb(B, self.in_ld[0])
+            self.hb = []
+            for l, hdim in enumerate(sp.hidden[:-1]):
+                t = zb(B, self.h_ld[l])
+                t[:, hdim] = 1.0
+                self.hb.append(t)
+            self.dhb = [zb(B, self.h_ld[l]) for l in range(len(sp.hidden))]
+            self.Wb = [zb(self.in_ld[l], self.out_ld[l]) for l in range(len(sp.hidden))]
+            # k-contiguous copies for the fast bf16 kernel (ta = 0, tb = 1 form of every product):
+            # W^T for the forward, X^T and dY^T (batch-contiguous) for dW
+            self.WbT = [zb(self.out_ld[l], self.in_ld[l]) for l in range(len(sp.hidden))]
+            self.x0bT = zb(self.in_ld[0], B)
+            self.hbT = [zb(self.h_ld[l], B) for l in range(len(sp.hidden) - 1)]
+            self.dhbT = [zb(self.h_ld[l], B) for l in range(len(sp.hidden))]
         self.dx0 = z(B, self.dx_ld)
         self.fm_out = z(B, self.fm_ld)
         self.fm_sum = z(B, E)
@@ -321,6 +343,16 @@ class CTREngine:
             Wi[:din, : W.shape[1]] = W
         Wi[din, : W.shape[1]] = b.reshape(-1)
         self.W[l].copy_(torch.from_numpy(Wi))
+        self._refresh_wb(l)
+
+    def _refresh_wb(self, l, s=None):
+        """bf16 tower: the bf16 operand copy of the fp32 master weights W_l."""
+        if self.bf:
+            s = s if s is not None else _lib.stream_handle()
+            call("dl_cast_bf16", ptr(self.W[l]), self.in_ld[l], self.out_ld[l], self.out_ld[l], ptr(self.Wb[l]),
+                 self.out_ld[l], s)
+            call("dl_transpose_bf16", ptr(self.W[l]), 1, self.in_ld[l], self.out_ld[l], self.out_ld[l],
+                 ptr(self.WbT[l]), self.in_ld[l], s)
 
     def load_params(self, P):
         """Inject reference-layout parameters (dict of numpy arrays as in oracle/ctr_ref.py)."""
@@ -501,11 +533,33 @@ class CTREngine:
             self._c("embed_fwd", "dl_embed_fwd", C_ref(L), ptr(self.table), ptr(self.first), ptr(self.in_cate),
                     ptr(self.in_cont), ptr(self.in_vec), ptr(self.x0), ptr(self.fm_out), ptr(self.fm_sum),
                     ptr(self.err), s)
-        x = self.x0
-        for l, hdim in enumerate(sp.hidden):
-            self._c("gemm_fwd_l%d" % l, "dl_gemm_f32", 0, 0, B, hdim, self.in_ld[l], ptr(x), self.in_ld[l], ptr(self.W[l]),
-                 self.out_ld[l], ptr(self.h[l]), self.h_ld[l], 1, None, 0, 1, 0, s)
-            x = self.h[l]
+        nl = len(sp.hidden)
+        if self.bf:
+            # bf16 tower: x0 -> bf16, ReLU layers on bf16 MFMA (fp32 accumulate), the last layer's
+            # output kept fp32 for the fp32 head / wide cross logit (config C5)
+            self._c("cast_x0", "dl_cast_bf16", ptr(self.x0), B, self.in_ld[0], self.in_ld[0], ptr(self.x0b),
+                    self.in_ld[0], s)
+            if train:
+                self._c("cast_x0T", "dl_transpose_bf16", ptr(self.x0), 1, B, self.in_ld[0], self.in_ld[0],
+                        ptr(self.x0bT), self.B, s)
+            xb = self.x0b
+            for l, hdim in enumerate(sp.hidden):
+                last = l == nl - 1
+                out = self.h[l] if last else self.hb[l]
+                self._c("gemm_fwd_l%d" % l, "dl_gemm_bf16", 0, 1, B, hdim, self.in_ld[l], ptr(xb), self.in_ld[l],
+                        ptr(self.WbT[l]), self.in_ld[l], ptr(out), self.h_ld[l], 0 if last else 1, 1, None, 0, 1,
+                        0, s)
+                if not last:
+                    xb = self.hb[l]
+                    if train:
+                        self._c("hT_l%d" % l, "dl_transpose_bf16", ptr(self.hb[l]), 0, B, self.h_ld[l],
+                                self.h_ld[l], ptr(self.hbT[l]), self.B, s)
+        else:
+            x = self.x0
+            for l, hdim in enumerate(sp.hidden):
+                self._c("gemm_fwd_l%d" % l, "dl_gemm_f32", 0, 0, B, hdim, self.in_ld[l], ptr(x), self.in_ld[l],
+                        ptr(self.W[l]), self.out_ld[l], ptr(self.h[l]), self.h_ld[l], 1, None, 0, 1, 0, s)
+                x = self.h[l]
         H = sp.hidden[-1]
         if self.wdl:
             self._c("head", "dl_wdl_head_fwd_bwd", B, sp.Fw, H, ptr(self.in_wide), self.in_wide.shape[1],
@@ -546,27 +600,50 @@ class CTREngine:
         self._forward(B, s, train=True)
         nl = len(sp.hidden)
         splits = max(1, min(self.splits, B // 1024))
+        if self.bf:
+            self._c("cast_dh", "dl_cast_bf16", ptr(self.dh[-1]), B, self.h_ld[-1], self.h_ld[-1], ptr(self.dhb[-1]),
+                    self.h_ld[-1], s)
+            self._c("cast_dhT", "dl_transpose_bf16", ptr(self.dh[-1]), 1, B, self.h_ld[-1], self.h_ld[-1],
+                    ptr(self.dhbT[-1]), self.B, s)
         for l in reversed(range(nl)):
-            xin = self.x0 if l == 0 else self.h[l - 1]
             hdim = sp.hidden[l]
             stride = self.in_ld[l] * self.out_ld[l]
-            self._c("gemm_dw_l%d" % l, "dl_gemm_f32", 1, 0, self.in_ld[l], hdim, B, ptr(xin), self.in_ld[l], ptr(self.dh[l]),
-                 self.h_ld[l], ptr(self.w_slab), self.out_ld[l], 3, None, 0, splits, stride, s)
-            nsplit = _num_splits(B, splits)
-            self._c("transpose_l%d" % l, "dl_transpose_f32", ptr(self.W[l]), self.in_ld[l], self.out_ld[l],
-                    self.out_ld[l], ptr(self.Wt), self.in_ld[l], s)
-            if l > 0:
-                self._c("gemm_dx_l%d" % l, "dl_gemm_f32", 0, 0, B, sp.hidden[l - 1], self.out_ld[l], ptr(self.dh[l]),
-                        self.h_ld[l], ptr(self.Wt), self.in_ld[l], ptr(self.dh[l - 1]), self.h_ld[l - 1], 2,
-                        ptr(self.h[l - 1]), self.h_ld[l - 1], 1, 0, s)
+            nsplit = _num_splits(B, splits, 64 if self.bf else 16)
+            if self.bf:
+                # dW = X^T dY as (X^T)(dY^T)^T: both operands batch-contiguous copies
+                xT = self.x0bT if l == 0 else self.hbT[l - 1]
+                self._c("gemm_dw_l%d" % l, "dl_gemm_bf16", 0, 1, self.in_ld[l], hdim, B, ptr(xT), self.B,
+                        ptr(self.dhbT[l]), self.B, ptr(self.w_slab), self.out_ld[l], 0, 3, None, 0, splits,
+                        stride, s)
+                if l > 0:   # dX = dY . W^T, ReluGrad by the bf16 activations, bf16 out
+                    self._c("gemm_dx_l%d" % l, "dl_gemm_bf16", 0, 1, B, sp.hidden[l - 1], self.out_ld[l],
+                            ptr(self.dhb[l]), self.h_ld[l], ptr(self.Wb[l]), self.out_ld[l], ptr(self.dhb[l - 1]),
+                            self.h_ld[l - 1], 1, 2, ptr(self.hb[l - 1]), self.h_ld[l - 1], 1, 0, s)
+                    self._c("dhT_l%d" % (l - 1), "dl_transpose_bf16", ptr(self.dhb[l - 1]), 0, B, self.h_ld[l - 1],
+                            self.h_ld[l - 1], ptr(self.dhbT[l - 1]), self.B, s)
+                else:       # dx0 stays fp32 for the embedding backward
+                    self._c("gemm_dx_l0", "dl_gemm_bf16", 0, 1, B, self.dx_cols, self.out_ld[0], ptr(self.dhb[0]),
+                            self.h_ld[0], ptr(self.Wb[0]), self.out_ld[0], ptr(self.dx0), self.dx_ld, 0, 0, None, 0,
+                            1, 0, s)
             else:
-                self._c("gemm_dx_l0", "dl_gemm_f32", 0, 0, B, self.dx_cols, self.out_ld[0], ptr(self.dh[0]),
-                        self.h_ld[0], ptr(self.Wt), self.in_ld[0], ptr(self.dx0), self.dx_ld, 0, None, 0, 1, 0, s)
+                xin = self.x0 if l == 0 else self.h[l - 1]
+                self._c("gemm_dw_l%d" % l, "dl_gemm_f32", 1, 0, self.in_ld[l], hdim, B, ptr(xin), self.in_ld[l],
+                        ptr(self.dh[l]), self.h_ld[l], ptr(self.w_slab), self.out_ld[l], 3, None, 0, splits, stride, s)
+                self._c("transpose_l%d" % l, "dl_transpose_f32", ptr(self.W[l]), self.in_ld[l], self.out_ld[l],
+                        self.out_ld[l], ptr(self.Wt), self.in_ld[l], s)
+                if l > 0:
+                    self._c("gemm_dx_l%d" % l, "dl_gemm_f32", 0, 0, B, sp.hidden[l - 1], self.out_ld[l],
+                            ptr(self.dh[l]), self.h_ld[l], ptr(self.Wt), self.in_ld[l], ptr(self.dh[l - 1]),
+                            self.h_ld[l - 1], 2, ptr(self.h[l - 1]), self.h_ld[l - 1], 1, 0, s)
+                else:
+                    self._c("gemm_dx_l0", "dl_gemm_f32", 0, 0, B, self.dx_cols, self.out_ld[0], ptr(self.dh[0]),
+                            self.h_ld[0], ptr(self.Wt), self.in_ld[0], ptr(self.dx0), self.dx_ld, 0, None, 0, 1, 0, s)
             # L2 on every hidden weight matrix only for wdl (wdl.py:272-275); bias row excluded
             l2, l2n = (sp.l2, ([self.D0] + sp.hidden)[l] * self.out_ld[l]) if self.wdl else (0.0, 0)
             self._c("adam_dense_l%d" % l, "dl_adam_dense", ptr(self.W[l]), ptr(self.Wm[l]), ptr(self.Wv[l]),
                     ptr(self.w_slab), nsplit, stride, stride, l2, l2n, ptr(self.opt), None,
                     ptr(self.opt[8:]) if self.wdl else None, s)
+            self._refresh_wb(l, s)
         # embedding backward (uses pre-update table and head weights)
         bwd_blocks = call_int("dl_embed_bwd_grid", C_ref(L))
         if self.lazy:
@@ -695,9 +772,11 @@ def default_adam(spec):
     return "dense" if spec.M else "lazy"
 
 
-def _num_splits(K, splits):
+def _num_splits(K, splits, align=16):
+    """Split-K slabs the GEMM actually writes (K chunks rounded up to `align`: 16 for the f32
+    kernel, 64 for the bf16 fast kernel)."""
     kps = -(-K // splits)
-    kps = -(-kps // 16) * 16
+    kps = -(-kps // align) * align
     return -(-K // kps)
 
 

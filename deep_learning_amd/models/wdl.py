@@ -10,7 +10,8 @@ Math (engine, model "wdl"): xavier embedding table with no zero row, deep tower
 over [cont, V[cate]], cross logit sum_f w[wide_f] + sum_j w[Fw+j] h_j + b with the
 deep-output weights aliasing wide rows (wdl.py:225-253), eps-log-loss, L2 on
 wdl_weights and every hidden weight matrix (:269-275), TF1 Adam.  The deep tower
-runs the fp32 MFMA GEMMs (the reference's numerics).
+runs the fp32 MFMA GEMMs (the reference's numerics) unless ``args.tower_dtype == "bf16"``
+(BASELINE config C5: bf16 MFMA tower, fp32 master weights and fp32 wide cross logit).
 """
 import pickle
 import sys
@@ -50,7 +51,8 @@ class DeepModel:
                               cate_index_size=self.cate_index_size, hidden=self.hidden_units,
                               Fw=self.wide_feats_field_size, lr=float(args.learning_rate), l2=float(args.l2_reg),
                               decay_steps=float(args.learning_rate_decay_steps),
-                              decay_rate=float(args.learning_rate_decay_rate))
+                              decay_rate=float(args.learning_rate_decay_rate),
+                              tower=str(getattr(args, "tower_dtype", "f32")))
         self.engine = None
 
     def model_optimizer(self):

@@ -176,8 +176,17 @@ int dl_gemm_f32(int32_t ta, int32_t tb, int32_t M, int32_t N, int32_t K, const f
  * both dX operands are read from LDS images in their HBM layout. */
 int dl_transpose_f32(const float* src, int32_t rows, int32_t cols, int32_t lds, float* dst, int32_t ldd,
                      void* stream);
+/* dst[r*ldd + c] = bf16(src[r*lds + c]), round to nearest even (bf16 tower operands). */
+int dl_cast_bf16(const float* src, int32_t rows, int32_t cols, int32_t lds, uint16_t* dst, int32_t ldd,
+                 void* stream);
+/* dst[c*ldd + r] = bf16(src[r*lds + c]) (src f32 when src_f32, else bf16): the k-contiguous
+ * operand copies of the bf16 tower (W^T, X^T, dY^T). */
+int dl_transpose_bf16(const void* src, int32_t src_f32, int32_t rows, int32_t cols, int32_t lds,
+                      uint16_t* dst, int32_t ldd, void* stream);
 /* bf16 variant for the Wide&Deep tower (config C5): A, B bf16 (uint16 bits),
- * fp32 accumulate, C fp32 or bf16 (c_bf16 = 1). Same semantics otherwise. */
+ * fp32 accumulate, C fp32 or bf16 (c_bf16 = 1). Same semantics otherwise.  ta = 0, tb = 1
+ * with lda, ldb multiples of 8 and 16-B aligned operands takes the fast k-contiguous
+ * kernel (b128 LDS images, BK = 64); other forms a general element-staged kernel. */
 int dl_gemm_bf16(int32_t ta, int32_t tb, int32_t M, int32_t N, int32_t K, const uint16_t* A,
                  int32_t lda, const uint16_t* B, int32_t ldb, void* C, int32_t ldc,
                  int32_t c_bf16, int32_t epi, const void* mask, int32_t ldm, int32_t splits,

@@ -84,6 +84,34 @@ def test_gemm_bf16(hip_lib):
     assert torch.allclose(C.double().cpu(), ref, rtol=1e-4, atol=1e-3)
 
 
+@pytest.mark.parametrize("ta,tb,epi,cbf", [(1, 0, 3, 0), (0, 1, 2, 1), (0, 1, 0, 0), (0, 0, 1, 1), (0, 1, 3, 0), (0, 1, 1, 1)])
+def test_gemm_bf16_variants(hip_lib, ta, tb, epi, cbf):
+    """The bf16 tower's products: dW (A^T, split-K slabs), dX (B^T, ReluGrad mask, bf16 out),
+    dx0 (B^T, fp32 out), forward (ReLU, bf16 out) — against fp64 on the same bf16 inputs."""
+    g = torch.Generator().manual_seed(3)
+    M, N, K = 272, 208, 320
+    A = torch.randn(M, K, generator=g).bfloat16()
+    B = torch.randn(K, N, generator=g).bfloat16()
+    mask = (torch.rand(M, N, generator=g) > 0.5).bfloat16()
+    ref = A.double() @ B.double()
+    if epi == 1:
+        ref = ref.clamp_min(0)
+    if epi == 2:
+        ref = ref * mask.double()
+    Ad = (A.t().contiguous() if ta else A).cuda()
+    Bd = (B.t().contiguous() if tb else B).cuda()
+    lda = M if ta else K
+    ldb = K if tb else N
+    splits = 4 if epi == 3 else 1
+    C = torch.zeros(splits * M * N, dtype=torch.bfloat16 if cbf else torch.float32, device="cuda")
+    call("dl_gemm_bf16", ta, tb, M, N, K, ptr(Ad), lda, ptr(Bd), ldb, ptr(C), N, cbf, epi,
+         ptr(mask.cuda()) if epi == 2 else None, N, splits, M * N, _s())
+    torch.cuda.synchronize()
+    got = C.double().cpu().view(splits, M, N).sum(0)
+    tol = 2e-2 if cbf else 1e-3          # bf16 output: one bf16 rounding (2^-8 relative)
+    np.testing.assert_allclose(got.numpy(), ref.numpy(), rtol=tol, atol=tol)
+
+
 def _engine(model, **kw):
     from deep_learning_amd.engine import CTREngine, ModelSpec
     spec = ModelSpec(model, **kw)

@@ -120,3 +120,26 @@ def test_lazy_adam_bit_identical_to_dense(hip_lib, name, stash):
     sd, sl = dense.adam_state(), lazy.adam_state()
     for k in sd:
         np.testing.assert_array_equal(sl[k], sd[k], err_msg=k)
+
+
+@pytest.mark.parametrize("adam", ["dense", "lazy"])
+def test_wdl_bf16_tower_tracks_oracle(hip_lib, adam):
+    """Config C5: the deep tower on bf16 MFMA (fp32 master weights, fp32 wide cross logit).
+    Stated bf16 tolerance: logits within 3e-2 absolute of the fp32 oracle over
+    4 steps, loss within 5e-3, and the AUC of the scores within 2e-3."""
+    kw = CASES["wdl"]
+    cfg = R.make_cfg("wdl", **kw)
+    P = R.init_params(cfg, np.random.default_rng(42))
+    eng = CTREngine(ModelSpec("wdl", tower="bf16", **kw), max_batch=1536, init="none", adam=adam)
+    eng.load_params(P)
+    opt = R.AdamTF1(cfg, P)
+    worst = 0.0
+    for step, b in enumerate(_batches("wdl", kw, 1536, 4)):
+        fw = R.train_step(cfg, P, opt, b)
+        eng.train_step(b, graph=(step >= 2))
+        torch.cuda.synchronize()
+        z = eng.z[:1536].cpu().numpy()
+        worst = max(worst, float(np.abs(z - fw["z"]).max()))
+        assert abs(eng.loss() - fw["loss"]) < 5e-3
+        assert abs(R.auc(b["label"], eng.score[:1536].cpu().numpy()) - R.auc(b["label"], fw["p"])) < 2e-3
+    assert worst < 3e-2, worst
