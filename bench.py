@@ -120,6 +120,11 @@ def cpu_baseline(spec_kw, B, budget_s=25.0):
 
 
 def main():
+    # stdout carries exactly one JSON line: libraries that print banners at init (RCCL does)
+    # are sent to stderr by pointing fd 1 there; the result goes to the saved stdout fd.
+    sys.stdout.flush()
+    json_fd = os.dup(1)
+    os.dup2(2, 1)
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
@@ -132,6 +137,8 @@ def main():
     ap.add_argument("--workload", default="c2", choices=["c2", "c3", "c5"],
                     help="c2 DeepFM (the headline, default); c3 deepfm_multi_cate 6 multi-hot slots x 60; "
                          "c5 Wide&Deep with the bf16 tower (single GPU)")
+    ap.add_argument("--sharded", action="store_true",
+                    help="run the row-sharded multi-GPU engine even at N=1 (measures its overhead)")
     ap.add_argument("--adam", default="lazy", choices=["dense", "lazy"],
                     help="table Adam: dense sweep, or row records with lazy-exact catch-up (same result)")
     args = ap.parse_args()
@@ -149,7 +156,13 @@ def main():
     backend = os.environ.get("DLAMD_BENCH_BACKEND", "nccl")
     dev_index = local if backend == "nccl" else local % max(1, torch.cuda.device_count())
     torch.cuda.set_device(dev_index)
-    if world > 1:
+    sharded = world > 1 or args.sharded
+    if sharded:
+        if world == 1:   # --sharded at N=1: the multi-GPU code path on one rank (overhead measurement)
+            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+            os.environ.setdefault("MASTER_PORT", "29533")
+            os.environ.setdefault("RANK", "0")
+            os.environ.setdefault("WORLD_SIZE", "1")
         if backend == "nccl":
             dist.init_process_group("nccl", device_id=torch.device("cuda", dev_index))
         else:
@@ -161,7 +174,7 @@ def main():
 
     B = args.batch
     if not args.vocab:
-        args.vocab = C2["per_field_vocab"] if world == 1 else 100_000_000 // C2["S"]
+        args.vocab = C2["per_field_vocab"] if not sharded else 100_000_000 // C2["S"]
     wl = args.workload
     if wl != "c2" and world > 1:
         raise SystemExit("--workload %s is single-GPU here; the multi-GPU path is C4 (default)" % wl)
@@ -176,8 +189,8 @@ def main():
         spec = ModelSpec("deepfm_pipeline", C=C2["C"], V=0, S=C2["S"], E=C2["E"],
                          cate_index_size=C2["S"] * args.vocab, hidden=C2["hidden"])
     log("rank %d/%d: building engine, table rows %d" % (rank, world, spec.n_rows))
-    use_graph = world == 1
-    if world == 1:
+    use_graph = not sharded
+    if not sharded:
         eng = CTREngine(spec, max_batch=B, seed=2019, adam=args.adam)
     else:
         from deep_learning_amd.shard import Exchange, ShardedCTREngine
@@ -309,8 +322,8 @@ def main():
             "kernel_sum_us_per_step": round(step_kernel_us, 1),
             "loss": round(loss, 6),
         }
-        print(json.dumps(out), flush=True)
-    if world > 1:
+        os.write(json_fd, (json.dumps(out) + "\n").encode())
+    if sharded:
         dist.destroy_process_group()
 
 

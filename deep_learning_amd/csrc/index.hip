@@ -72,7 +72,11 @@ __global__ __launch_bounds__(256) void scatter_index_kernel(const uint32_t* __re
     if (head) {
       uniq[u] = k;
       seg_off[u] = i;
-      if (owner_counts) atomicAdd(owner_counts + (k >> kLocalBits), 1);
+      // first unique row of an owner group (keys are sorted by owner): its start index.
+      // Counts follow from the starts (owner_counts_kernel) — no per-row atomics on the
+      // world+1 counters, which serialised 3.2 M updates (38 ms at one rank).
+      if (owner_counts && (i == 0 || (keys[i - 1] >> kLocalBits) != (k >> kLocalBits)))
+        owner_counts[k >> kLocalBits] = u;
     }
     if (i + 1 == n || keys[i + 1] == kInvalidKey) {
       seg_off[u + 1] = i + 1;
@@ -86,7 +90,22 @@ __global__ void index_init_kernel(int32_t* n_uniq, int32_t* seg_off, int32_t* ow
   const int t = threadIdx.x;
   if (t == 0) { n_uniq[0] = 0; seg_off[0] = 0; }
   if (owner_counts)
-    for (int i = t; i < n_owner; i += blockDim.x) owner_counts[i] = 0;
+    for (int i = t; i < n_owner; i += blockDim.x) owner_counts[i] = -1;   // group starts, -1 = absent
+}
+
+// owner group starts (scatter_index_kernel) -> counts, in owner order.
+__global__ void owner_counts_kernel(int32_t* owner_counts, int n_owner, const int32_t* n_uniq) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  int end = n_uniq[0];
+  for (int o = n_owner - 1; o >= 0; --o) {
+    const int start = owner_counts[o];
+    if (start < 0) {
+      owner_counts[o] = 0;
+    } else {
+      owner_counts[o] = end - start;
+      end = start;
+    }
+  }
 }
 
 struct IndexWs {
@@ -183,5 +202,7 @@ extern "C" int dl_index_build(const dl_emb_layout* L, const int64_t* cate, int32
   }
   hipLaunchKernelGGL(scatter_index_kernel, dim3(grid), dim3(256), 0, s, sorted_keys, sorted_refs, w.uid1, n, world,
                      invalid, uniq_keys, seg_off, n_uniq, inv, owner_counts);
+  if (owner_counts)
+    hipLaunchKernelGGL(owner_counts_kernel, dim3(1), dim3(64), 0, s, owner_counts, world + 1, n_uniq);
   DL_RETURN_LAUNCH("dl_index_build");
 }

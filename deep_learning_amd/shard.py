@@ -53,14 +53,22 @@ class Exchange:
         dist.all_to_all_single(r, s, group=self.group)
         return [int(x) for x in r.cpu().tolist()]
 
-    def all_to_all(self, send, send_splits, recv_splits):
-        """Variable all-to-all along dim 0 (splits in rows)."""
+    def all_to_all(self, send, send_splits, recv_splits, out=None):
+        """Variable all-to-all along dim 0 (splits in rows).  `out` (device, contiguous,
+        sum(recv_splits) rows) receives in place — RCCL writes straight into it."""
         shape = (sum(recv_splits),) + tuple(send.shape[1:])
         src = self._dev(send.contiguous())
-        out = torch.empty(shape, dtype=send.dtype, device=src.device)
-        dist.all_to_all_single(out, src, output_split_sizes=list(recv_splits),
+        direct = out is not None and not self.staged and out.is_contiguous()
+        res = out if direct else torch.empty(shape, dtype=send.dtype, device=src.device)
+        dist.all_to_all_single(res, src, output_split_sizes=list(recv_splits),
                                input_split_sizes=list(send_splits), group=self.group)
-        return out.to(send.device, non_blocking=False) if out.device != send.device else out
+        if direct:
+            return out
+        res = res.to(send.device, non_blocking=False) if res.device != send.device else res
+        if out is not None:
+            out.copy_(res)
+            return out
+        return res
 
     def all_reduce(self, t):
         if self.staged and t.is_cuda:
@@ -259,12 +267,10 @@ class ShardedCTREngine(CTREngine):
             call("dl_shard_gather", ptr(self.table), ptr(self.first), ptr(recv_ids), nrecv, E, ptr(out_v),
                  ptr(out_1) if self.first is not None else None, s)
         # 4. rows back, in unique-id order
-        rv = ex.all_to_all(out_v[:nrecv], recv, send)
         rep = self.rep
-        self.rows_u[rep: rep + nsend].copy_(rv)
+        ex.all_to_all(out_v[:nrecv], recv, send, out=self.rows_u[rep: rep + nsend])
         if sp.fm:
-            r1 = ex.all_to_all(out_1[:nrecv], recv, send)
-            self.rows_u1[rep: rep + nsend].copy_(r1)
+            ex.all_to_all(out_1[:nrecv], recv, send, out=self.rows_u1[rep: rep + nsend])
         if rep:
             self.rows_u[:rep].copy_(self.rep_t[:rep])
             if sp.fm:
