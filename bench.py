@@ -189,7 +189,7 @@ def main():
         spec = ModelSpec("deepfm_pipeline", C=C2["C"], V=0, S=C2["S"], E=C2["E"],
                          cate_index_size=C2["S"] * args.vocab, hidden=C2["hidden"])
     log("rank %d/%d: building engine, table rows %d" % (rank, world, spec.n_rows))
-    use_graph = not sharded
+    use_graph = True   # single GPU: the whole step after the index build; sharded: the dense middle
     if not sharded:
         eng = CTREngine(spec, max_batch=B, seed=2019, adam=args.adam)
     else:

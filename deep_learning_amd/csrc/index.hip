@@ -206,3 +206,45 @@ extern "C" int dl_index_build(const dl_emb_layout* L, const int64_t* cate, int32
     hipLaunchKernelGGL(owner_counts_kernel, dim3(1), dim3(64), 0, s, owner_counts, world + 1, n_uniq);
   DL_RETURN_LAUNCH("dl_index_build");
 }
+
+namespace dl {
+__global__ __launch_bounds__(256) void iota_copy_kernel(const int32_t* __restrict__ keys, int n, int32_t* __restrict__ kout,
+                                                        int32_t* __restrict__ pos) {
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    kout[i] = keys[i];
+    pos[i] = i;
+  }
+}
+}  // namespace dl
+
+extern "C" int dl_sort_unique(const int32_t* keys, int64_t n_keys, int32_t key_bits, void* ws, int64_t ws_bytes,
+                              int32_t* sorted_keys, int32_t* sorted_pos, int32_t* uniq_keys, int32_t* seg_off,
+                              int32_t* n_uniq, int32_t* inv, void* stream) {
+  DL_CHECK_ARG(keys && ws && sorted_keys && sorted_pos && uniq_keys && seg_off && n_uniq, "NULL argument");
+  DL_CHECK_ARG(key_bits >= 1 && key_bits <= 31, "key_bits %d out of range", key_bits);
+  DL_CHECK_ARG(n_keys >= 0 && n_keys < (1LL << 30), "bad n_keys");
+  const int n = (int)n_keys;
+  DL_CHECK_ARG(ws_bytes >= dl_index_workspace_bytes(n > 0 ? n : 1), "workspace too small");
+  hipStream_t s = as_stream(stream);
+  hipLaunchKernelGGL(index_init_kernel, dim3(1), dim3(64), 0, s, n_uniq, seg_off, (int32_t*)nullptr, 0);
+  if (n == 0) return 0;
+  IndexWs w = carve(ws, n);
+  const int grid = (int)((n + 255) / 256 < 8192 ? (n + 255) / 256 : 8192);
+  const uint32_t invalid = 0xFFFFFFFFu;   // keys are non-negative (< 2^key_bits): never equal
+  hipLaunchKernelGGL(iota_copy_kernel, dim3(grid), dim3(256), 0, s, keys, n, (int32_t*)w.keys_in, w.refs_in);
+  size_t tb = w.temp_bytes;
+  if (sort_pairs(w.temp, tb, w.keys_in, (uint32_t*)sorted_keys, w.refs_in, sorted_pos, n, key_bits, s) !=
+      hipSuccess) {
+    set_error("dl_sort_unique: radix sort failed");
+    return 2;
+  }
+  hipLaunchKernelGGL(head_flags_kernel, dim3(grid), dim3(256), 0, s, (const uint32_t*)sorted_keys, n, invalid, w.flags);
+  tb = w.temp_bytes;
+  if (hipcub::DeviceScan::InclusiveSum(w.temp, tb, w.flags, w.uid1, n, s) != hipSuccess) {
+    set_error("dl_sort_unique: scan failed");
+    return 3;
+  }
+  hipLaunchKernelGGL(scatter_index_kernel, dim3(grid), dim3(256), 0, s, (const uint32_t*)sorted_keys, sorted_pos,
+                     w.uid1, n, 1, invalid, (uint32_t*)uniq_keys, seg_off, n_uniq, inv, (int32_t*)nullptr);
+  DL_RETURN_LAUNCH("dl_sort_unique");
+}

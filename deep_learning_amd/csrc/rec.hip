@@ -269,73 +269,59 @@ __global__ __launch_bounds__(256) void rec_flush_kernel(float* __restrict__ rec,
   }
 }
 
-// Owner side of the sharded step: peers' per-row gradients are summed into the dense
-// local gradient table G/G1 (f32 atomics: a row may arrive from several peers), and
-// the first arrival of a row appends it to `list` (flag exchange), so the update
-// below visits each touched row once without a sort.
-__global__ __launch_bounds__(256) void rec_scatter_list_kernel(const float* __restrict__ g, const float* __restrict__ g1,
-                                                               const int32_t* __restrict__ ids, long long n, int E,
-                                                               float* __restrict__ G, float* __restrict__ G1) {
-  for (long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x; t < n * E;
-       t += (long long)gridDim.x * blockDim.x) {
-    const long long i = t / E;
-    const int d = (int)(t % E);
-    const int r = ids[i];
-    atomicAdd(G + (long long)r * E + d, g[t]);
-    if (d == 0 && g1) atomicAdd(G1 + r, g1[i]);
-  }
-}
-
-// One thread per received id: the first arrival of a row (flag exchange) appends it to
-// `list`.  Appends are aggregated per wave (one atomic per wave, lane offsets by
-// popcount) — a per-row atomic on the single counter serialised 3.2 M updates.
-__global__ __launch_bounds__(256) void rec_list_kernel(const int32_t* __restrict__ ids, long long n,
-                                                       int32_t* __restrict__ flags, int32_t* __restrict__ list,
-                                                       int32_t* __restrict__ list_n) {
-  const int lane = threadIdx.x & 63;
-  for (long long i0 = (long long)blockIdx.x * blockDim.x; i0 < n; i0 += (long long)gridDim.x * blockDim.x) {
-    const long long i = i0 + threadIdx.x;
-    int r = -1;
-    bool fresh = false;
-    if (i < n) {
-      r = ids[i];
-      fresh = atomicExch(flags + r, 1) == 0;
-    }
-    const unsigned long long mask = __ballot(fresh);
-    if (mask == 0ull) continue;
-    const int leader = __ffsll((long long)mask) - 1;
-    int base = 0;
-    if (lane == leader) base = atomicAdd(list_n, __popcll(mask));
-    base = __shfl(base, leader, 64);
-    if (fresh) list[base + __popcll(mask & ((1ull << lane) - 1ull))] = r;
-  }
-}
-
-// Step-t update of the listed rows from G/G1 (then zeroed, flags cleared).
-__global__ __launch_bounds__(256) void rec_apply_list_kernel(float* __restrict__ rec, RecCfg c,
-                                                             const int32_t* __restrict__ list,
-                                                             const int32_t* __restrict__ list_n, long long cap,
-                                                             float* __restrict__ G, float* __restrict__ G1,
-                                                             int32_t* __restrict__ flags, const float* __restrict__ hist,
-                                                             const float* __restrict__ opt) {
+// Owner side of the sharded step, deterministic form: the received gradients g [n][E],
+// g1 [n] of one step, grouped by row by dl_sort_unique over the received ids, are summed
+// per row in sorted (position) order and applied: catch-up + TF1 Adam step t.
+// E/4 lanes per row, float4 each (as the gather).
+template <int E>
+__global__ __launch_bounds__(256) void rec_apply_segments_kernel(float* __restrict__ rec, RecCfg c,
+                                                                 const int32_t* __restrict__ uniq,
+                                                                 const int32_t* __restrict__ seg_off,
+                                                                 const int32_t* __restrict__ n_uniq, long long cap,
+                                                                 long long n, const int32_t* __restrict__ pos,
+                                                                 const float* __restrict__ g,
+                                                                 const float* __restrict__ g1,
+                                                                 const float* __restrict__ hist,
+                                                                 const float* __restrict__ opt) {
   rec_load_hyper(c, opt);
-  const int E = c.E;
+  constexpr int LPR = E / 4;
+  const long long gt = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  const int q = (int)(gt % LPR);
   const int t = (int)opt[7];
-  const float alpha_t = opt[3];
-  long long n = list_n[0];
-  n = n < 0 ? 0 : (n > cap ? cap : n);
-  for (long long k = (long long)blockIdx.x * blockDim.x + threadIdx.x; k < n * E;
-       k += (long long)gridDim.x * blockDim.x) {
-    const long long i = k / E;
-    const int d = (int)(k % E);
-    const long long row = list[i];
-    const float gi = G[row * E + d];
-    const float g1i = (G1 && d == 0) ? G1[row] : 0.f;
-    rec_update(rec + row * c.ld, E, d, gi, g1i, t, alpha_t, hist, c);
-    G[row * E + d] = 0.f;
-    if (d == 0) {
-      if (G1) G1[row] = 0.f;
-      flags[row] = 0;
+  const float alpha = opt[3];
+  const long long nu = n_uniq ? (long long)clamp_uniq(n_uniq, cap) : cap;
+  const bool first = c.has_first && q == 0;
+  for (long long u = gt / LPR; u < nu; u += (long long)gridDim.x * blockDim.x / LPR) {
+    const long long row = uniq[u];
+    float* r = rec + row * c.ld;
+    float4 p = *reinterpret_cast<const float4*>(r + 4 * q);
+    float4 m = *reinterpret_cast<const float4*>(r + E + 4 + 4 * q);
+    float4 v = *reinterpret_cast<const float4*>(r + 2 * E + 4 + 4 * q);
+    const float4 tail = *reinterpret_cast<const float4*>(r + E);
+    float w = tail.x, wm = tail.y, wv = tail.z;
+    const int e0 = max(0, seg_off[u]);
+    const int e1 = (int)min(n, (long long)seg_off[u + 1]);
+    float4 gs = make_float4(0.f, 0.f, 0.f, 0.f);
+    float g1s = 0.f;
+    for (int e = e0; e < e1; ++e) {
+      const int k = pos[e];
+      if (k < 0 || k >= n) continue;
+      const float4 gk = *reinterpret_cast<const float4*>(g + (long long)k * E + 4 * q);
+      gs.x += gk.x; gs.y += gk.y; gs.z += gk.z; gs.w += gk.w;
+      if (first) g1s += g1[k];
+    }
+    const int stamp = __float_as_int(tail.w);
+    if (stamp < t - 1) catch_up4(p, m, v, w, wm, wv, first, stamp, t - 1, hist, c);
+    adam_elem(p.x, m.x, v.x, gs.x, alpha, c.omb1, c.omb2, c.eps);
+    adam_elem(p.y, m.y, v.y, gs.y, alpha, c.omb1, c.omb2, c.eps);
+    adam_elem(p.z, m.z, v.z, gs.z, alpha, c.omb1, c.omb2, c.eps);
+    adam_elem(p.w, m.w, v.w, gs.w, alpha, c.omb1, c.omb2, c.eps);
+    *reinterpret_cast<float4*>(r + 4 * q) = p;
+    *reinterpret_cast<float4*>(r + E + 4 + 4 * q) = m;
+    *reinterpret_cast<float4*>(r + 2 * E + 4 + 4 * q) = v;
+    if (q == 0) {
+      if (first) adam_elem(w, wm, wv, g1s, alpha, c.omb1, c.omb2, c.eps);
+      *reinterpret_cast<float4*>(r + E) = make_float4(w, wm, wv, __int_as_float(t));
     }
   }
 }
@@ -443,28 +429,20 @@ extern "C" int dl_rec_flush(float* rec, int32_t rec_ld, int32_t emb_dim, int32_t
   DL_RETURN_LAUNCH("dl_rec_flush");
 }
 
-extern "C" int dl_rec_scatter_list(const float* g, const float* g1, const int32_t* ids, int64_t n, int32_t emb_dim,
-                                   float* G, float* G1, int32_t* flags, int32_t* list, int32_t* list_n,
-                                   void* stream) {
-  DL_CHECK_ARG(g && ids && G && flags && list && list_n, "NULL argument");
-  DL_CHECK_ARG(!g1 || G1, "G1 required with g1");
-  if (n <= 0) return 0;
-  hipLaunchKernelGGL(rec_scatter_list_kernel, dim3(grid_cap(n * emb_dim)), dim3(256), 0, as_stream(stream), g, g1,
-                     ids, (long long)n, emb_dim, G, g1 ? G1 : nullptr);
-  hipLaunchKernelGGL(rec_list_kernel, dim3(grid_cap(n)), dim3(256), 0, as_stream(stream), ids, (long long)n, flags,
-                     list, list_n);
-  DL_RETURN_LAUNCH("dl_rec_scatter_list");
-}
-
-extern "C" int dl_rec_apply_list(float* rec, int32_t rec_ld, int32_t emb_dim, int32_t has_first, const int32_t* list,
-                                 const int32_t* list_n, int64_t cap, float* G, float* G1, int32_t* flags,
-                                 const float* hist, int32_t hist_len, const float* opt, void* stream) {
-  DL_CHECK_ARG(rec && list && list_n && G && flags && hist && opt, "NULL argument");
+extern "C" int dl_rec_apply_segments(float* rec, int32_t rec_ld, int32_t emb_dim, int32_t has_first,
+                                     const int32_t* uniq, const int32_t* seg_off, const int32_t* n_uniq,
+                                     int64_t max_uniq, int64_t n, const int32_t* sorted_pos, const float* g,
+                                     const float* g1, const float* hist, int32_t hist_len, const float* opt,
+                                     void* stream) {
+  DL_CHECK_ARG(rec && uniq && seg_off && sorted_pos && g && hist && opt, "NULL argument");
   if (int rc = rec_check(emb_dim, rec_ld, hist_len)) return rc;
-  DL_CHECK_ARG(!has_first || G1, "G1 required with first-order weights");
-  if (cap <= 0) return 0;
-  hipLaunchKernelGGL(rec_apply_list_kernel, dim3(grid_cap(cap * emb_dim)), dim3(256), 0, as_stream(stream), rec,
-                     RecCfg{emb_dim, rec_ld, has_first, hist_len - 1, 0.f, 0.f, 0.f}, list, list_n,
-                     (long long)cap, G, has_first ? G1 : nullptr, flags, hist, opt);
-  DL_RETURN_LAUNCH("dl_rec_apply_list");
+  DL_CHECK_ARG(!has_first || g1, "g1 required with first-order weights");
+  if (max_uniq <= 0 || n <= 0) return 0;
+  DL_DISPATCH_E(emb_dim, {
+    hipLaunchKernelGGL(rec_apply_segments_kernel<kE>, dim3(grid_cap(max_uniq * (kE / 4))), dim3(256), 0,
+                       as_stream(stream), rec, RecCfg{kE, rec_ld, has_first, hist_len - 1, 0.f, 0.f, 0.f}, uniq,
+                       seg_off, n_uniq, (long long)max_uniq, (long long)n, sorted_pos, g, has_first ? g1 : nullptr,
+                       hist, opt);
+  });
+  DL_RETURN_LAUNCH("dl_rec_apply_segments");
 }

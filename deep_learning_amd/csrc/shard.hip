@@ -51,6 +51,18 @@ __global__ __launch_bounds__(256) void slab_sum_kernel(const float* __restrict__
   }
 }
 
+// few elements, many slabs (the head's per-block partials): one wave per element
+__global__ __launch_bounds__(256) void slab_sum_wave_kernel(const float* __restrict__ slab, int nslab, long long stride,
+                                                            long long n, float* __restrict__ out) {
+  const long long i = ((long long)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int lane = threadIdx.x & 63;
+  if (i >= n) return;
+  float g = 0.f;
+  for (int s = lane; s < nslab; s += 64) g += slab[s * stride + i];
+  g = wave_sum(g);
+  if (lane == 0) out[i] = g;
+}
+
 // local row of each unique key (key & (2^27-1)); the send list of the id exchange
 __global__ void keys_to_local_kernel(const uint32_t* __restrict__ keys, const int32_t* __restrict__ n_uniq,
                                      long long cap, int32_t* __restrict__ out) {
@@ -92,8 +104,12 @@ extern "C" int dl_shard_scatter_add(const float* g, const float* g_first, const 
 extern "C" int dl_slab_sum(const float* slab, int32_t nslab, int64_t stride, int64_t n, float* out, void* stream) {
   DL_CHECK_ARG(slab && out && nslab >= 1 && stride >= n, "bad args");
   if (n <= 0) return 0;
-  hipLaunchKernelGGL(slab_sum_kernel, dim3(grid_of(n)), dim3(256), 0, as_stream(stream), slab, nslab,
-                     (long long)stride, (long long)n, out);
+  if (nslab >= 32 && n < 16384)
+    hipLaunchKernelGGL(slab_sum_wave_kernel, dim3((unsigned)((n * 64 + 255) / 256)), dim3(256), 0, as_stream(stream),
+                       slab, nslab, (long long)stride, (long long)n, out);
+  else
+    hipLaunchKernelGGL(slab_sum_kernel, dim3(grid_of(n)), dim3(256), 0, as_stream(stream), slab, nslab,
+                       (long long)stride, (long long)n, out);
   DL_RETURN_LAUNCH("dl_slab_sum");
 }
 

@@ -98,14 +98,13 @@ class ShardedCTREngine(CTREngine):
         E = spec.E
         self.local_rows = local_rows
         if self.lazy:
-            # shard rows as records (rec.hip); owners accumulate peers' gradients in a dense
-            # local table and update only the rows that arrived (list built by flag exchange)
+            # shard rows as records (rec.hip).  Owners sort the ids they receive once per step
+            # (dl_sort_unique); the gradients come back in the same order, so each requested
+            # row's arrivals are summed in that fixed order and applied once
+            # (dl_rec_apply_segments) — deterministic, no dense gradient table, no atomics.
             self.mv_u = None
-            self.tg = z(self.rows_pad, E)
-            self.fmg = z(self.rows_pad) if spec.fm else None
-            self.row_flags = z(self.rows_pad, dt=torch.int32)
-            self.row_list = z(self.rows_pad, dt=torch.int32)
-            self.row_list_n = z(4, dt=torch.int32)
+            self.own_cap = 0
+            self.own_bits = max(1, int(self.rows_pad - 1).bit_length())
         R = max(self.rep, 1)
         rp = _ru(R, 16)
         self.rep_t, self.rep_m, self.rep_v, self.rep_g = z(rp, E), z(rp, E), z(rp, E), z(rp, E)
@@ -135,6 +134,17 @@ class ShardedCTREngine(CTREngine):
         self.flat = z(off)
         if self.rep:
             self.rep_touched[: self.rep] = 1
+
+    def _owner_buffers(self, n):
+        """(Re)size the owner-side sort buffers for n received ids."""
+        if n <= self.own_cap:
+            return
+        cap = max(n, int(self.own_cap * 1.25), 1 << 16)
+        z = lambda *sh, dt=torch.int32: torch.zeros(*sh, dtype=dt, device=self.dev)
+        self.own_ws = z(_lib.lib().dl_index_workspace_bytes(cap), dt=torch.uint8)
+        self.own_keys, self.own_pos, self.own_uniq = z(cap), z(cap), z(cap)
+        self.own_off, self.own_n = z(cap + 1), z(4)
+        self.own_cap = cap
 
     # ------------------------------------------------------------ parameters
     def owned_rows(self):
@@ -224,61 +234,16 @@ class ShardedCTREngine(CTREngine):
         f = self.first[: self.local_rows].cpu().numpy()[ok] if self.first is not None else None
         return rows[ok], t, f
 
-    # ------------------------------------------------------------ step
-    def train_step(self, batch=None, graph=False):
+    def _mid(self, B):
+        """Steps 5-6: everything between the row exchange and the gradient exchange — fixed
+        buffers and sizes for a batch size, so train_step(graph=True) replays it as one
+        hipGraph (the exchanges around it need host-known sizes and stay eager)."""
         sp = self.spec
-        ex = self.exch
-        E = sp.E
-        B = self.stage(batch) if batch is not None else self.B
         s = _lib.stream_handle()
         L = self.layout
         L.batch = B
         W = self.world
-        lazy = self.lazy
-        if lazy:
-            if self.since_flush >= self.hist_len - 2:   # bound every row's lag below the alpha ring
-                self.flush()
-            self.since_flush += 1
-            self.row_list_n.zero_()
-        call("dl_adam_begin_step", ptr(self.opt), sp.decay_rate, float(sp.decay_steps), s)
-        if lazy:
-            call("dl_adam_hist_record", ptr(self.opt), ptr(self.hist), self.hist_len, s)
-        # 1. index (rows grouped by owner; replicated rows last)
-        self._c("index_build", "dl_index_build", C_ref(L), ptr(self.in_cate), W, self.rep, ptr(self.idx_ws),
-                self.idx_ws.numel(), ptr(self.idx_keys), ptr(self.idx_refs), ptr(self.idx_uniq),
-                ptr(self.idx_off), ptr(self.idx_n), ptr(self.inv), ptr(self.owner_counts), ptr(self.err), s)
-        oc = self.owner_counts.cpu().tolist()
-        send = oc[:W]
-        nsend, nrep = sum(send), oc[W]
-        U = nsend + nrep
-        # 2. exchange counts and ids
-        recv = ex.counts(send)
-        nrecv = sum(recv)
-        call("dl_keys_to_local", ptr(self.idx_uniq), ptr(self.idx_n), U, ptr(self.send_ids), s)
-        recv_ids = ex.all_to_all(self.send_ids[:nsend], send, recv)
-        # 3. owners gather requested rows
-        out_v = torch.empty(max(nrecv, 1), E, device=self.dev)
-        out_1 = torch.empty(max(nrecv, 1), device=self.dev)
-        if nrecv and lazy:   # rows caught up to the previous step (read only)
-            self._c("rec_gather", "dl_rec_gather", C_ref(L), ptr(self.rec), self.rec_ld, int(sp.fm), 0,
-                    ptr(recv_ids), None, nrecv, 1, ptr(self.hist), self.hist_len, ptr(self.opt), 1, ptr(out_v),
-                    ptr(out_1) if sp.fm else None, None, s)
-        elif nrecv:
-            call("dl_shard_gather", ptr(self.table), ptr(self.first), ptr(recv_ids), nrecv, E, ptr(out_v),
-                 ptr(out_1) if self.first is not None else None, s)
-        # 4. rows back, in unique-id order
         rep = self.rep
-        ex.all_to_all(out_v[:nrecv], recv, send, out=self.rows_u[rep: rep + nsend])
-        if sp.fm:
-            ex.all_to_all(out_1[:nrecv], recv, send, out=self.rows_u1[rep: rep + nsend])
-        if rep:
-            self.rows_u[:rep].copy_(self.rep_t[:rep])
-            if sp.fm:
-                self.rows_u1[:rep].copy_(self.rep_f[:rep])
-        if nrep:   # replicated rows referenced by cate ids: local rows of the replica
-            call("dl_shard_gather", ptr(self.rep_t), ptr(self.rep_f) if sp.fm else None,
-                 ptr(self.send_ids[nsend:U]), nrep, E, ptr(self.rows_u[rep + nsend:]),
-                 ptr(self.rows_u1[rep + nsend:]) if sp.fm else None, s)
         # 5. forward + dense backward
         self._c("embed_fwd", "dl_embed_fwd_indexed", C_ref(L), ptr(self.rows_u), ptr(self.rows_u1) if sp.fm else None,
                 ptr(self.inv), rep, ptr(self.in_cont), ptr(self.in_vec), ptr(self.x0), ptr(self.fm_out),
@@ -319,13 +284,87 @@ class ShardedCTREngine(CTREngine):
         self._c("embed_bwd", "dl_embed_bwd_sorted", C_ref(L), None, ptr(self.rows_u[rep:]), ptr(self.idx_uniq),
                 ptr(self.idx_off), ptr(self.idx_n), ptr(self.idx_refs), W, self.n_refs, ptr(self.dz),
                 ptr(self.w_head), ptr(self.fm_sum), ptr(self.dx0), ptr(self.gU), ptr(self.g1U), None, 1, s)
+
+    def _mid_graph(self, B):
+        if getattr(self, "mid_graph", None) is None or self.mid_batch != B:
+            st = torch.cuda.Stream()
+            st.wait_stream(torch.cuda.current_stream())
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g, stream=st):
+                self._mid(B)
+            torch.cuda.current_stream().wait_stream(st)
+            self.mid_graph, self.mid_batch = g, B
+        self.mid_graph.replay()
+
+    # ------------------------------------------------------------ step
+    def train_step(self, batch=None, graph=False):
+        sp = self.spec
+        ex = self.exch
+        E = sp.E
+        B = self.stage(batch) if batch is not None else self.B
+        s = _lib.stream_handle()
+        L = self.layout
+        L.batch = B
+        W = self.world
+        lazy = self.lazy
+        if lazy:
+            if self.since_flush >= self.hist_len - 2:   # bound every row's lag below the alpha ring
+                self.flush()
+            self.since_flush += 1
+        call("dl_adam_begin_step", ptr(self.opt), sp.decay_rate, float(sp.decay_steps), s)
+        if lazy:
+            call("dl_adam_hist_record", ptr(self.opt), ptr(self.hist), self.hist_len, s)
+        # 1. index (rows grouped by owner; replicated rows last)
+        self._c("index_build", "dl_index_build", C_ref(L), ptr(self.in_cate), W, self.rep, ptr(self.idx_ws),
+                self.idx_ws.numel(), ptr(self.idx_keys), ptr(self.idx_refs), ptr(self.idx_uniq),
+                ptr(self.idx_off), ptr(self.idx_n), ptr(self.inv), ptr(self.owner_counts), ptr(self.err), s)
+        oc = self.owner_counts.cpu().tolist()
+        send = oc[:W]
+        nsend, nrep = sum(send), oc[W]
+        U = nsend + nrep
+        # 2. exchange counts and ids
+        recv = ex.counts(send)
+        nrecv = sum(recv)
+        call("dl_keys_to_local", ptr(self.idx_uniq), ptr(self.idx_n), U, ptr(self.send_ids), s)
+        recv_ids = ex.all_to_all(self.send_ids[:nsend], send, recv)
+        # 3. owners gather requested rows
+        out_v = torch.empty(max(nrecv, 1), E, device=self.dev)
+        out_1 = torch.empty(max(nrecv, 1), device=self.dev)
+        if nrecv and lazy:
+            # group this step's arrivals by row once; reused by the backward's update
+            self._owner_buffers(nrecv)
+            call("dl_sort_unique", ptr(recv_ids), nrecv, self.own_bits, ptr(self.own_ws), self.own_ws.numel(),
+                 ptr(self.own_keys), ptr(self.own_pos), ptr(self.own_uniq), ptr(self.own_off), ptr(self.own_n),
+                 None, s)
+        if nrecv and lazy:   # rows caught up to the previous step (read only)
+            self._c("rec_gather", "dl_rec_gather", C_ref(L), ptr(self.rec), self.rec_ld, int(sp.fm), 0,
+                    ptr(recv_ids), None, nrecv, 1, ptr(self.hist), self.hist_len, ptr(self.opt), 1, ptr(out_v),
+                    ptr(out_1) if sp.fm else None, None, s)
+        elif nrecv:
+            call("dl_shard_gather", ptr(self.table), ptr(self.first), ptr(recv_ids), nrecv, E, ptr(out_v),
+                 ptr(out_1) if self.first is not None else None, s)
+        # 4. rows back, in unique-id order
+        rep = self.rep
+        ex.all_to_all(out_v[:nrecv], recv, send, out=self.rows_u[rep: rep + nsend])
+        if sp.fm:
+            ex.all_to_all(out_1[:nrecv], recv, send, out=self.rows_u1[rep: rep + nsend])
+        if rep:
+            self.rows_u[:rep].copy_(self.rep_t[:rep])
+            if sp.fm:
+                self.rows_u1[:rep].copy_(self.rep_f[:rep])
+        if nrep:   # replicated rows referenced by cate ids: local rows of the replica
+            call("dl_shard_gather", ptr(self.rep_t), ptr(self.rep_f) if sp.fm else None,
+                 ptr(self.send_ids[nsend:U]), nrep, E, ptr(self.rows_u[rep + nsend:]),
+                 ptr(self.rows_u1[rep + nsend:]) if sp.fm else None, s)
+        if graph and self.prof is None:
+            self._mid_graph(B)
+        else:
+            self._mid(B)
+        nl = len(sp.hidden)
+        hoff = self.seg[nl][1]
         gb = ex.all_to_all(self.gU[:nsend], send, recv)
         g1b = ex.all_to_all(self.g1U[:nsend], send, recv) if sp.fm else None
-        if nrecv and lazy:
-            call("dl_rec_scatter_list", ptr(gb), ptr(g1b) if sp.fm else None, ptr(recv_ids), nrecv, E,
-                 ptr(self.tg), ptr(self.fmg) if sp.fm else None, ptr(self.row_flags), ptr(self.row_list),
-                 ptr(self.row_list_n), s)
-        elif nrecv:
+        if nrecv and not lazy:
             call("dl_shard_scatter_add", ptr(gb), ptr(g1b) if sp.fm else None, ptr(recv_ids), nrecv, E,
                  ptr(self.tg), ptr(self.fmg) if sp.fm else None, ptr(self.touched), s)
         # replicated rows: cate-id refs + the FM cont fields, into the flat buffer
@@ -363,10 +402,9 @@ class ShardedCTREngine(CTREngine):
                      ptr(self.rep_touched), self.rep_f.shape[0], 1, 0.0, 0, ptr(self.opt), None, s)
         if lazy:
             if nrecv:
-                self._c("adam_table", "dl_rec_apply_list", ptr(self.rec), self.rec_ld, E, int(sp.fm),
-                        ptr(self.row_list), ptr(self.row_list_n), min(nrecv, self.rows_pad), ptr(self.tg),
-                        ptr(self.fmg) if sp.fm else None, ptr(self.row_flags), ptr(self.hist), self.hist_len,
-                        ptr(self.opt), s)
+                self._c("adam_table", "dl_rec_apply_segments", ptr(self.rec), self.rec_ld, E, int(sp.fm),
+                        ptr(self.own_uniq), ptr(self.own_off), ptr(self.own_n), nrecv, nrecv, ptr(self.own_pos),
+                        ptr(gb), ptr(g1b) if sp.fm else None, ptr(self.hist), self.hist_len, ptr(self.opt), s)
         elif sp.fm:
             self._c("adam_table", "dl_adam_rows", ptr(self.table), ptr(self.tm), ptr(self.tv), ptr(self.tg),
                     ptr(self.touched), self.table.shape[0], E, 0.0, 0, ptr(self.opt), None, s)

@@ -126,6 +126,12 @@ int dl_index_build(const dl_emb_layout* L, const int64_t* cate, int32_t world,
                    int32_t replicated_below, void* ws, int64_t ws_bytes, uint32_t* sorted_keys,
                    int32_t* sorted_refs, uint32_t* uniq_keys, int32_t* seg_off, int32_t* n_uniq,
                    int32_t* inv, int32_t* owner_counts, int32_t* err, void* stream);
+/* Generic form for the sharded owners: sort n non-negative int32 keys (< 2^key_bits) with
+ * their positions, dedup: uniq_keys [n_uniq], seg_off [n_uniq+1] into sorted_pos, and
+ * inv[i] = unique id of keys[i] (may be NULL).  Workspace: dl_index_workspace_bytes(n). */
+int dl_sort_unique(const int32_t* keys, int64_t n_keys, int32_t key_bits, void* ws, int64_t ws_bytes,
+                   int32_t* sorted_keys, int32_t* sorted_pos, int32_t* uniq_keys, int32_t* seg_off,
+                   int32_t* n_uniq, int32_t* inv, void* stream);
 /* Deterministic (atomic-free) embedding backward over the index: each unique
  * row's gradient is the ordered sum of its references.  compact=0: plain stores
  * into the dense gradient tables g_out [n_rows, E] / g1_out [n_rows] + touched
@@ -284,16 +290,12 @@ int dl_rec_bwd_adam(const dl_emb_layout* L, float* rec, int32_t rec_ld, int32_t 
 int dl_rec_apply_rows(float* rec, int32_t rec_ld, int32_t emb_dim, int32_t has_first, int64_t row0,
                       int64_t n, float* g, float* g1, const float* hist, int32_t hist_len,
                       const float* opt, void* stream);
-/* Sharded owners: G[ids[i]] += g[i] (E floats), G1[ids[i]] += g1[i] (f32 atomics; a row
- * may come from several peers); the first arrival of a row sets flags[row] and appends
- * it to list (list_n[0] = count, zeroed by the caller before the step). */
-int dl_rec_scatter_list(const float* g, const float* g1, const int32_t* ids, int64_t n, int32_t emb_dim,
-                        float* G, float* G1, int32_t* flags, int32_t* list, int32_t* list_n, void* stream);
-/* Step-t update (catch-up, then the gradient G[row], G1[row]) of the min(list_n, cap)
- * listed rows; G, G1 and flags of those rows are reset. */
-int dl_rec_apply_list(float* rec, int32_t rec_ld, int32_t emb_dim, int32_t has_first, const int32_t* list,
-                      const int32_t* list_n, int64_t cap, float* G, float* G1, int32_t* flags,
-                      const float* hist, int32_t hist_len, const float* opt, void* stream);
+/* Sharded owners, deterministic: per unique received row (dl_sort_unique over the received
+ * ids) the ordered sum of its arrivals g[pos][E], g1[pos] is applied (catch-up + step opt[7]). */
+int dl_rec_apply_segments(float* rec, int32_t rec_ld, int32_t emb_dim, int32_t has_first, const int32_t* uniq,
+                          const int32_t* seg_off, const int32_t* n_uniq, int64_t max_uniq, int64_t n,
+                          const int32_t* sorted_pos, const float* g, const float* g1, const float* hist,
+                          int32_t hist_len, const float* opt, void* stream);
 /* Every row caught up to step opt[7] (before export/checkpoint, and every hist_len steps). */
 int dl_rec_flush(float* rec, int32_t rec_ld, int32_t emb_dim, int32_t has_first, int64_t n_rows,
                  const float* hist, int32_t hist_len, const float* opt, void* stream);

@@ -137,7 +137,7 @@ def run_gpu(rank, world, steps, Bl, out_dir, adam="dense"):
     eng = ShardedCTREngine(ModelSpec("deepfm_pipeline", **KW), Bl, ex, adam=adam, hist_len=4)
     eng.load_params(P)
     for step, bg in enumerate(global_batches(Bl * world, steps)):
-        eng.train_step(local(bg, rank, world))
+        eng.train_step(local(bg, rank, world), graph=step >= 2)   # dense middle as a hipGraph from step 2
         torch.cuda.synchronize()
         np.savez(os.path.join(out_dir, "rank%d_step%d.npz" % (rank, step)), z=eng.z[:Bl].cpu().numpy(),
                  loss=eng.loss())
