@@ -179,7 +179,6 @@ def main():
     if wl != "c2" and world > 1:
         raise SystemExit("--workload %s is single-GPU here; the multi-GPU path is C4 (default)" % wl)
     if wl == "c3":
-        args.adam = "dense"            # row records do not cover multi-hot pooling yet
         spec = ModelSpec("deepfm_multi_cate", C=0, V=0, S=C2["S"], E=C2["E"], cate_index_size=C2["S"] * args.vocab,
                          hidden=C2["hidden"], multi_ranges=[[60 * i, 60 * (i + 1), "slot%d" % i] for i in range(6)])
     elif wl == "c5":

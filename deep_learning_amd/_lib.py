@@ -24,7 +24,16 @@ class EmbLayout(C.Structure):
         ("fm_cont", C.c_int32), ("use_fm", C.c_int32), ("fm_extra", C.c_int32),
         ("zero_row0", C.c_int32), ("x0_ld", C.c_int32), ("x0_cont_col", C.c_int32),
         ("x0_vec_col", C.c_int32), ("x0_cat_col", C.c_int32), ("x0_pool_col", C.c_int32),
-        ("fm_ld", C.c_int32), ("dx0_ld", C.c_int32), ("dx0_cat_col", C.c_int32), ("pad_", C.c_int32),
+        ("fm_ld", C.c_int32), ("dx0_ld", C.c_int32), ("dx0_cat_col", C.c_int32), ("multi_width", C.c_int32),
+    ]
+
+
+class PoolDesc(C.Structure):
+    """Mirror of ``dl_pool_desc`` (include/dlamd.h)."""
+    _fields_ = [
+        ("slot_start", C.c_void_p), ("slot_end", C.c_void_p), ("n_slots", C.c_int32), ("fm_col", C.c_int32),
+        ("dx0_pool_col", C.c_int32), ("pad_", C.c_int32), ("x0", C.c_void_p), ("cnt_emb", C.c_void_p),
+        ("cnt_first", C.c_void_p),
     ]
 
 
@@ -51,6 +60,7 @@ SIGNATURES = {
     "dl_index_build": (I32, [LP, P, I32, I32, P, I64, P, P, P, P, P, P, P, P, P]),
     "dl_embed_bwd_sorted": (I32, [LP, P, P, P, P, P, P, I32, I64, P, P, P, P, P, P, P, I32, P]),
     "dl_pool_fwd": (I32, [LP, P, P, P, I32, P, P, I32, I32, P, P, P, P, P, P]),
+    "dl_pool_fwd_indexed": (I32, [LP, P, P, P, I32, P, P, I32, I32, P, P, P, P, P]),
     "dl_pool_bwd": (I32, [LP, P, I32, P, P, I32, I32, P, P, P, P, P, I32, P, P, P, P, P, P]),
     "dl_gemm_f32": (I32, [I32, I32, I32, I32, I32, P, I32, P, I32, P, I32, I32, P, I32, I32, I64, P]),
     "dl_gemm_bf16": (I32, [I32, I32, I32, I32, I32, P, I32, P, I32, P, I32, I32, I32, P, I32, I32, I64, P]),
@@ -67,7 +77,8 @@ SIGNATURES = {
     "dl_transpose_bf16": (I32, [P, I32, I32, I32, I32, P, I32, P]),
     "dl_adam_hist_record": (I32, [P, P, I32, P]),
     "dl_rec_gather": (I32, [LP, P, I32, I32, I32, P, P, I64, I32, P, I32, P, I32, P, P, P, P]),
-    "dl_rec_bwd_adam": (I32, [LP, P, I32, I32, I32, P, P, P, P, P, P, P, I32, I64, P, P, P, P, P, P, P, I32, P, P]),
+    "dl_rec_bwd_adam": (I32, [LP, P, I32, I32, I32, P, P, P, P, P, P, P, I32, I64, P, P, P, P, P, P, P, I32, P,
+                              P, P]),
     "dl_rec_apply_rows": (I32, [P, I32, I32, I32, I64, I64, P, P, P, I32, P, P]),
     "dl_sort_unique": (I32, [P, I64, I32, P, I64, P, P, P, P, P, P, P]),
     "dl_rec_apply_segments": (I32, [P, I32, I32, I32, P, P, P, I64, I64, P, P, P, P, I32, P, P]),

@@ -76,6 +76,15 @@ __device__ __forceinline__ void adam_elem(float& p, float& m, float& v, float g,
     case 64: { constexpr int kE = 64; __VA_ARGS__; break; } \
   }
 
+// References per sample in the batch index: FM slots (use_fm), deep slots, multi-hot slots.
+__host__ __device__ __forceinline__ int index_slots(const dl_emb_layout& L) {
+  return (L.use_fm ? L.cate_fields : 0) + L.cate_fields + L.multi_width;
+}
+// first multi-hot reference of a sample
+__host__ __device__ __forceinline__ int index_multi_base(const dl_emb_layout& L) {
+  return (L.use_fm ? L.cate_fields : 0) + L.cate_fields;
+}
+
 // Batch-index key (index.hip): (owner << 27) | local; owner == world marks a replicated row.
 __device__ __forceinline__ int64_t decode_key(uint32_t k, int world) {
   const uint32_t owner = k >> 27, local = k & ((1u << 27) - 1);

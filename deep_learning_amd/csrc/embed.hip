@@ -79,7 +79,7 @@ __global__ __launch_bounds__(256) void embed_fwd_kernel(EmbArgs a) {
       const int tot = nb * S;
       if (a.inv) {
         // sharded: rows were exchanged per unique reference; ref = b * ns + slot
-        const int ns = (L.use_fm ? S : 0) + S;
+        const int ns = index_slots(L);
         for (int k = threadIdx.x; k < tot; k += blockDim.x) {
           const int j = k / S, f = k % S;
           const int64_t rb = (int64_t)(b0 + j) * ns;
@@ -344,6 +344,8 @@ __global__ __launch_bounds__(256) void cont_reduce_kernel(dl_emb_layout L, const
 
 struct PoolArgs {
   dl_emb_layout L;
+  const int32_t* inv;      // indexed mode (records): row of multi ref = inv_base + inv[b*ns + mb + l]
+  int inv_base;
   const float* table;
   const float* first_order;
   const int64_t* ids;
@@ -379,8 +381,13 @@ __global__ __launch_bounds__(256) void pool_fwd_kernel(PoolArgs a) {
         const int l = l0 + r;
         float4 e = f4_zero();
         if (l < s1) {
-          const int64_t row = checked_row(ids[l], 0, L.n_rows, a.err);
-          if (row_ok(row, L.zero_row0)) e = tab4[row * LPR + q];
+          if (a.inv) {
+            const int ri = a.inv[(int64_t)b * index_slots(L) + index_multi_base(L) + l];
+            if (ri >= 0) e = tab4[(int64_t)(a.inv_base + ri) * LPR + q];
+          } else {
+            const int64_t row = checked_row(ids[l], 0, L.n_rows, a.err);
+            if (row_ok(row, L.zero_row0)) e = tab4[row * LPR + q];
+          }
         }
         // tf.reduce_sum(emb, axis=2) then count_nonzero over the slot
         float rs = (e.x + e.y) + (e.z + e.w);
@@ -404,8 +411,14 @@ __global__ __launch_bounds__(256) void pool_fwd_kernel(PoolArgs a) {
       if (a.first_order) {
         float s1v = 0.f, c1 = 0.f;
         for (int l = s0 + lane; l < s1; l += 64) {
-          const int64_t row = checked_row(ids[l], 0, L.n_rows, a.err);
-          const float w = row_ok(row, L.zero_row0) ? a.first_order[row] : 0.f;
+          float w;
+          if (a.inv) {
+            const int ri = a.inv[(int64_t)b * index_slots(L) + index_multi_base(L) + l];
+            w = ri >= 0 ? a.first_order[a.inv_base + ri] : 0.f;
+          } else {
+            const int64_t row = checked_row(ids[l], 0, L.n_rows, a.err);
+            w = row_ok(row, L.zero_row0) ? a.first_order[row] : 0.f;
+          }
           s1v += w;
           c1 += (w != 0.f) ? 1.f : 0.f;
         }
@@ -603,11 +616,27 @@ extern "C" int dl_pool_fwd(const dl_emb_layout* L, const float* table, const flo
   DL_CHECK_ARG(n_slots >= 0 && slot_start && slot_end, "bad slots");
   DL_CHECK_ARG(!first_order || (fm_out && cnt_first), "first-order pooling needs fm_out/cnt_first");
   if (L->batch == 0 || n_slots == 0) return 0;
-  PoolArgs a{*L, table, first_order, ids, ids_col, slot_start, slot_end, n_slots, fm_col,
+  PoolArgs a{*L, nullptr, 0, table, first_order, ids, ids_col, slot_start, slot_end, n_slots, fm_col,
              x0, fm_out, cnt_emb, cnt_first, err};
   DL_DISPATCH_E(L->emb_dim, hipLaunchKernelGGL(pool_fwd_kernel<kE>, dim3(emb_grid(L->batch)),
                                                dim3(256), 0, as_stream(stream), a));
   DL_RETURN_LAUNCH("dl_pool_fwd");
+}
+
+extern "C" int dl_pool_fwd_indexed(const dl_emb_layout* L, const float* rows, const float* rows_first,
+                                   const int32_t* inv, int32_t inv_base, const int32_t* slot_start,
+                                   const int32_t* slot_end, int32_t n_slots, int32_t fm_col, float* x0,
+                                   float* fm_out, float* cnt_emb, float* cnt_first, void* stream) {
+  if (int rc = check_layout(L)) return rc;
+  DL_CHECK_ARG(rows && inv && x0 && cnt_emb && slot_start && slot_end && n_slots >= 0, "NULL argument");
+  DL_CHECK_ARG(L->multi_width > 0, "indexed pooling needs the multi-hot refs in the index (multi_width)");
+  DL_CHECK_ARG(!rows_first || (fm_out && cnt_first), "first-order pooling needs fm_out/cnt_first");
+  if (L->batch == 0 || n_slots == 0) return 0;
+  PoolArgs a{*L, inv, inv_base, rows, rows_first, nullptr, 0, slot_start, slot_end, n_slots, fm_col,
+             x0, fm_out, cnt_emb, cnt_first, nullptr};
+  DL_DISPATCH_E(L->emb_dim, hipLaunchKernelGGL(pool_fwd_kernel<kE>, dim3(emb_grid(L->batch)),
+                                               dim3(256), 0, as_stream(stream), a));
+  DL_RETURN_LAUNCH("dl_pool_fwd_indexed");
 }
 
 extern "C" int dl_pool_bwd(const dl_emb_layout* L, const int64_t* ids, int32_t ids_col,
@@ -660,7 +689,7 @@ __global__ __launch_bounds__(256) void embed_bwd_sorted_kernel(BwdSortedArgs a) 
   const int lane = threadIdx.x & 63;
   const int r = lane / E, d = lane % E;
   const int S = L.cate_fields;
-  const int ns = (L.use_fm ? S : 0) + S;
+  const int ns = index_slots(L);
   const int Cf = (L.use_fm && L.fm_cont) ? L.cont_fields : 0;
   const int F = Cf + S + L.fm_extra;
   const long long nrefs = (long long)L.batch * ns;

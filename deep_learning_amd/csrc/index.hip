@@ -28,13 +28,15 @@ __global__ __launch_bounds__(256) void make_refs_kernel(dl_emb_layout L, const i
                                                         uint32_t* __restrict__ keys,
                                                         int32_t* __restrict__ refs, int32_t* err) {
   const int S = L.cate_fields;
-  const int ns = (L.use_fm ? S : 0) + S;
+  const int ns = index_slots(L);
   const long long n = (long long)L.batch * ns;
   for (long long k = (long long)blockIdx.x * blockDim.x + threadIdx.x; k < n; k += (long long)gridDim.x * blockDim.x) {
     const int b = (int)(k / ns), s = (int)(k % ns);
     int64_t row;
+    const int mb = index_multi_base(L);
     if (L.use_fm && s < S) row = cate[(long long)b * L.cate_ld + s] + L.fm_cate_offset;
-    else row = cate[(long long)b * L.cate_ld + (L.use_fm ? s - S : s)] + L.deep_cate_offset;
+    else if (s < mb) row = cate[(long long)b * L.cate_ld + (L.use_fm ? s - S : s)] + L.deep_cate_offset;
+    else row = cate[(long long)b * L.cate_ld + S + (s - mb)] + L.deep_cate_offset;   // multi-hot id
     uint32_t key = kInvalidKey;
     if (row < 0 || row >= L.n_rows) {
       if (err) atomicOr(err, 1);
@@ -44,6 +46,29 @@ __global__ __launch_bounds__(256) void make_refs_kernel(dl_emb_layout L, const i
     }
     keys[k] = key;
     refs[k] = (int32_t)k;
+  }
+}
+
+// Multi-hot batches are mostly padding (id 0 -> invalid key): the valid (key, ref) pairs are
+// compacted in ref order before the sort, and inv starts at -1 for every reference.
+__global__ __launch_bounds__(256) void valid_flags_kernel(const uint32_t* __restrict__ keys, int n, uint32_t kInvalidKey,
+                                                          int32_t* __restrict__ flags, int32_t* __restrict__ inv) {
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    flags[i] = keys[i] != kInvalidKey ? 1 : 0;
+    if (inv) inv[i] = -1;
+  }
+}
+
+__global__ __launch_bounds__(256) void compact_kernel(const uint32_t* __restrict__ keys, const int32_t* __restrict__ pos1,
+                                                      int n, uint32_t kInvalidKey, uint32_t* __restrict__ kout,
+                                                      int32_t* __restrict__ rout, int32_t* __restrict__ n_valid) {
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    if (keys[i] != kInvalidKey) {
+      const int p = pos1[i] - 1;
+      kout[p] = keys[i];
+      rout[p] = i;
+    }
+    if (i + 1 == n) n_valid[0] = pos1[i];
   }
 }
 
@@ -83,6 +108,15 @@ __global__ __launch_bounds__(256) void scatter_index_kernel(const uint32_t* __re
       n_uniq[0] = u + 1;
     }
     if (inv) inv[refs[i]] = u;
+  }
+}
+
+// copies the compacted pairs back into the sort's input arrays
+__global__ __launch_bounds__(256) void iota_refs_copy_kernel(const uint32_t* __restrict__ kin, const int32_t* __restrict__ rin,
+                                                             int n, uint32_t* __restrict__ kout, int32_t* __restrict__ rout) {
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    kout[i] = kin[i];
+    rout[i] = rin[i];
   }
 }
 
@@ -175,9 +209,9 @@ extern "C" int dl_index_build(const dl_emb_layout* L, const int64_t* cate, int32
   DL_CHECK_ARG(world >= 1 && world < 32, "world %d out of range", world);
   DL_CHECK_ARG(L->n_rows / world < (1LL << kLocalBits), "too many rows per shard for the 27-bit local key");
   const int S = L->cate_fields;
-  const long long n_ll = (long long)L->batch * ((L->use_fm ? S : 0) + S);
+  const long long n_ll = (long long)L->batch * index_slots(*L);
   DL_CHECK_ARG(n_ll < (1LL << 30), "too many references");
-  const int n = (int)n_ll;
+  int n = (int)n_ll;
   DL_CHECK_ARG(ws_bytes >= dl_index_workspace_bytes(n > 0 ? n : 1), "workspace too small");
   hipStream_t s = as_stream(stream);
   // zeroing by a kernel (not a memset node): keeps every node of a captured step a kernel
@@ -190,10 +224,39 @@ extern "C" int dl_index_build(const dl_emb_layout* L, const int64_t* cate, int32
   hipLaunchKernelGGL(make_refs_kernel, dim3(grid), dim3(256), 0, s, *L, cate, world, replicated_below, invalid,
                      w.keys_in, w.refs_in, err);
   size_t tb = w.temp_bytes;
-  if (sort_pairs(w.temp, tb, w.keys_in, sorted_keys, w.refs_in, sorted_refs, n, end_bit, s) != hipSuccess) {
+  const uint32_t* sort_keys = w.keys_in;
+  const int32_t* sort_refs = w.refs_in;
+  int ns_sort = n;
+  if (L->multi_width > 0) {
+    // compact the valid references (ref order kept), then sort only those; the sorted
+    // arrays hold them first.  One stream sync to learn the count (the sort's size).
+    hipLaunchKernelGGL(valid_flags_kernel, dim3(grid), dim3(256), 0, s, w.keys_in, n, invalid, w.flags, inv);
+    if (hipcub::DeviceScan::InclusiveSum(w.temp, tb, w.flags, w.uid1, n, s) != hipSuccess) {
+      set_error("dl_index_build: scan failed");
+      return 3;
+    }
+    // compacted pairs go to the sorted_* arrays (free until the sort), then sort into place
+    uint32_t* ck = reinterpret_cast<uint32_t*>(w.flags);   // flags are consumed by the scan
+    hipLaunchKernelGGL(compact_kernel, dim3(grid), dim3(256), 0, s, w.keys_in, w.uid1, n, invalid, ck, sorted_refs,
+                       n_uniq);
+    int32_t nv = 0;
+    if (hipMemcpyAsync(&nv, n_uniq, sizeof(int32_t), hipMemcpyDeviceToHost, s) != hipSuccess ||
+        hipStreamSynchronize(s) != hipSuccess) {
+      set_error("dl_index_build: count readback failed");
+      return 4;
+    }
+    hipLaunchKernelGGL(iota_refs_copy_kernel, dim3(grid), dim3(256), 0, s, ck, sorted_refs, nv, w.keys_in, w.refs_in);
+    hipLaunchKernelGGL(index_init_kernel, dim3(1), dim3(64), 0, s, n_uniq, seg_off, owner_counts, world + 1);
+    ns_sort = nv;
+    tb = w.temp_bytes;
+  }
+  if (ns_sort > 0 &&
+      sort_pairs(w.temp, tb, sort_keys, sorted_keys, sort_refs, sorted_refs, ns_sort, end_bit, s) != hipSuccess) {
     set_error("dl_index_build: radix sort failed");
     return 2;
   }
+  n = ns_sort;
+  if (n == 0) DL_RETURN_LAUNCH("dl_index_build");
   hipLaunchKernelGGL(head_flags_kernel, dim3(grid), dim3(256), 0, s, sorted_keys, n, invalid, w.flags);
   tb = w.temp_bytes;
   if (hipcub::DeviceScan::InclusiveSum(w.temp, tb, w.flags, w.uid1, n, s) != hipSuccess) {

@@ -158,7 +158,7 @@ __global__ __launch_bounds__(256) void rec_bwd_adam_kernel(SegGradIn sg, float* 
   const int q = (int)(gt % LPR);
   const long long group0 = gt / LPR, ngroups = (long long)gridDim.x * blockDim.x / LPR;
   const int S = L.cate_fields;
-  const int ns = (L.use_fm ? S : 0) + S;
+  const int ns = index_slots(L);
   const int Cf = (L.use_fm && L.fm_cont) ? L.cont_fields : 0;
   const int F = Cf + S + L.fm_extra;
   const long long nrefs = (long long)L.batch * ns;
@@ -380,7 +380,7 @@ extern "C" int dl_rec_bwd_adam(const dl_emb_layout* L, float* rec, int32_t rec_l
                                const int32_t* sorted_refs, int32_t world, int64_t max_uniq, const float* dz,
                                const float* w_head, const float* fm_sum, const float* dx0, float* g_rep,
                                float* g1_rep, const float* hist, int32_t hist_len, const float* opt,
-                               void* stream) {
+                               const dl_pool_desc* pool, void* stream) {
   DL_CHECK_ARG(L && rec && rows_u && uniq_keys && seg_off && n_uniq && sorted_refs && dx0 && opt,
                "NULL argument");
   DL_CHECK_ARG(mv_u || hist, "without the moment stash the alpha ring is required");
@@ -391,7 +391,16 @@ extern "C" int dl_rec_bwd_adam(const dl_emb_layout* L, float* rec, int32_t rec_l
   DL_CHECK_ARG(!(n_rep && has_first) || g1_rep, "g1_rep required");
   DL_CHECK_ARG(L->dx0_ld % 4 == 0 && L->dx0_cat_col % 4 == 0, "dx0 must be float4 aligned");
   if (max_uniq <= 0) return 0;
-  const SegGradIn sg{*L, seg_off, sorted_refs, dz, w_head, fm_sum, dx0};
+  DL_CHECK_ARG(L->multi_width == 0 || (pool && pool->slot_start && pool->slot_end && pool->x0 && pool->cnt_emb),
+               "multi-hot references need the pool descriptor");
+  DL_CHECK_ARG(!pool || !L->use_fm || !has_first || pool->cnt_first, "cnt_first required");
+  DL_CHECK_ARG(!pool || (pool->dx0_pool_col % 4 == 0 && L->x0_pool_col % 4 == 0), "pool columns not float4 aligned");
+  SegGradIn sg{*L, seg_off, sorted_refs, dz, w_head, fm_sum, dx0};
+  if (L->multi_width > 0) {
+    sg.slot_start = pool->slot_start; sg.slot_end = pool->slot_end; sg.n_slots = pool->n_slots;
+    sg.fm_col = pool->fm_col; sg.dx0_pool_col = pool->dx0_pool_col; sg.x0 = pool->x0;
+    sg.cnt_emb = pool->cnt_emb; sg.cnt_first = has_first ? pool->cnt_first : nullptr;
+  }
   DL_DISPATCH_E(L->emb_dim, {
     const unsigned grid = grid_cap(max_uniq * (kE / 4));
     hipLaunchKernelGGL(rec_bwd_adam_kernel<kE>, dim3(grid), dim3(256), 0, as_stream(stream), sg, rec,

@@ -20,6 +20,16 @@ struct SegGradIn {
   const float* w_head;
   const float* fm_sum;
   const float* dx0;
+  // multi-hot references (index_multi_base(L) <= slot; records only): nonzero-mean pooling
+  // (deepfm_multi_cate.py:71-111) — slot ranges within the multi block, pooled x0 and counts
+  const int32_t* slot_start;
+  const int32_t* slot_end;
+  int n_slots;
+  int fm_col;        // head column of the pooled first-order outputs
+  int dx0_pool_col;
+  const float* x0;
+  const float* cnt_emb;
+  const float* cnt_first;
 };
 
 struct SegGrad {
@@ -33,15 +43,17 @@ __device__ __forceinline__ SegGrad segment_grad(const SegGradIn& a, long long u,
                                                 float wsec) {
   const dl_emb_layout& L = a.L;
   const int S = L.cate_fields;
-  const int ns = (L.use_fm ? S : 0) + S;
+  const int ns = index_slots(L);
   const int Cf = (L.use_fm && L.fm_cont) ? L.cont_fields : 0;
   const int e0 = max(0, a.seg_off[u]);
   const int e1 = (int)min(nrefs, (long long)a.seg_off[u + 1]);
   SegGrad r{0.f, 0.f, 0.f, 0.f};
+  const int mb = index_multi_base(L);   // multi-hot refs exist only with records (segment_grad4)
   for (int e = e0; e < e1; ++e) {
     const int k = a.refs[e];
     if (k < 0 || k >= nrefs) continue;
     const int b = k / ns, sl = k % ns;
+    if (sl >= mb) continue;
     if (L.use_fm && sl < S) {
       const float dzb = a.dz[b];
       const float ds = dzb * wsec;
@@ -73,17 +85,40 @@ __device__ __forceinline__ SegGrad4 segment_grad4(const SegGradIn& a, long long 
                                                   float4 wsec) {
   const dl_emb_layout& L = a.L;
   const int S = L.cate_fields;
-  const int ns = (L.use_fm ? S : 0) + S;
+  const int ns = index_slots(L);
   const int Cf = (L.use_fm && L.fm_cont) ? L.cont_fields : 0;
   const int e0 = max(0, a.seg_off[u]);
   const int e1 = (int)min(nrefs, (long long)a.seg_off[u + 1]);
   const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
   SegGrad4 r{z, z, z, 0.f};
+  const int mb = index_multi_base(L);
   for (int e = e0; e < e1; ++e) {
     const int k = a.refs[e];
     if (k < 0 || k >= nrefs) continue;
     const int b = k / ns, sl = k % ns;
-    if (L.use_fm && sl < S) {
+    if (sl >= mb) {
+      // pooled slot m of multi position l: d/d row = (dx0[pool m] + dsec*(fm_sum - pooled_m)) / cnt
+      const int l = sl - mb;
+      int m = 0;
+      while (m < a.n_slots && !(l >= a.slot_start[m] && l < a.slot_end[m])) ++m;
+      if (m == a.n_slots) continue;
+      const float c = a.cnt_emb[(long long)b * a.n_slots + m];
+      const float dzb = L.use_fm ? a.dz[b] : 0.f;
+      if (c > 0.f) {
+        float4 dp = *reinterpret_cast<const float4*>(a.dx0 + (long long)b * L.dx0_ld + a.dx0_pool_col + m * E + 4 * q);
+        if (L.use_fm) {
+          const float4 fs = *reinterpret_cast<const float4*>(a.fm_sum + (long long)b * E + 4 * q);
+          const float4 pv = *reinterpret_cast<const float4*>(a.x0 + (long long)b * L.x0_ld + L.x0_pool_col + m * E + 4 * q);
+          dp.x = fmaf(dzb * wsec.x, fs.x - pv.x, dp.x); dp.y = fmaf(dzb * wsec.y, fs.y - pv.y, dp.y);
+          dp.z = fmaf(dzb * wsec.z, fs.z - pv.z, dp.z); dp.w = fmaf(dzb * wsec.w, fs.w - pv.w, dp.w);
+        }
+        r.x.x += dp.x / c; r.x.y += dp.y / c; r.x.z += dp.z / c; r.x.w += dp.w / c;
+      }
+      if (L.use_fm && a.cnt_first) {
+        const float c1 = a.cnt_first[(long long)b * a.n_slots + m];
+        if (c1 > 0.f) r.g1 += dzb * a.w_head[a.fm_col + m] / c1;
+      }
+    } else if (L.use_fm && sl < S) {
       const float dzb = a.dz[b];
       const float4 fs = *reinterpret_cast<const float4*>(a.fm_sum + (long long)b * E + 4 * q);
       const float4 ds = make_float4(dzb * wsec.x, dzb * wsec.y, dzb * wsec.z, dzb * wsec.w);

@@ -149,9 +149,8 @@ class CTREngine:
             raise ValueError("adam must be 'dense' or 'lazy'")
         self.lazy = adam == "lazy"
         if self.lazy:
-            # row records + lazy-exact Adam (rec.hip); needs the batch index
-            if sp.M:
-                raise ValueError("adam='lazy' does not support multi-hot slots yet")
+            # row records + lazy-exact Adam (rec.hip); needs the batch index (with multi-hot
+            # slots it also indexes every multi-hot id position: pooling reads caught-up rows)
             bwd = "sorted"
             self.rec_ld = _ru(3 * E + 4, 32)
             self.rec = z(rows_pad, self.rec_ld)
@@ -237,9 +236,14 @@ class CTREngine:
             self.slot_start = torch.tensor([r[0] for r in sp.multi_ranges], dtype=torch.int32, device=dev)
             self.slot_end = torch.tensor([r[1] for r in sp.multi_ranges], dtype=torch.int32, device=dev)
             self.cnt_emb, self.cnt_first = z(B, M), z(B, M)
+            if self.lazy:
+                self.pool_desc = _lib.PoolDesc(
+                    slot_start=self.slot_start.data_ptr(), slot_end=self.slot_end.data_ptr(), n_slots=M,
+                    fm_col=S, dx0_pool_col=S * E, x0=self.x0.data_ptr(), cnt_emb=self.cnt_emb.data_ptr(),
+                    cnt_first=self.cnt_first.data_ptr())
         # batch reference index (deterministic backward)
         self.bwd = bwd
-        self.n_slot = (S if sp.fm else 0) + S
+        self.n_slot = (S if sp.fm else 0) + S + (sp.multi_width if self.lazy else 0)
         self.n_refs = B * self.n_slot
         if bwd == "sorted":
             wsb = _lib.lib().dl_index_workspace_bytes(max(1, self.n_refs))
@@ -295,6 +299,7 @@ class CTREngine:
         L.fm_ld = self.fm_ld
         L.dx0_ld = self.dx_ld
         L.dx0_cat_col = 0
+        L.multi_width = sp.multi_width if self.lazy else 0
         return L
 
     # ------------------------------------------------------------------ params
@@ -516,7 +521,7 @@ class CTREngine:
         sp = self.spec
         L = self.layout
         L.batch = B
-        if sp.M:  # pooled vectors must be in x0 before the FM second order reads them
+        if sp.M and not self.lazy:  # pooled vectors must be in x0 before the FM second order reads them
             self._c("pool_fwd", "dl_pool_fwd", C_ref(L), ptr(self.table), ptr(self.first) if sp.fm else None,
                  ptr(self.in_cate), sp.S, ptr(self.slot_start), ptr(self.slot_end), sp.M, sp.S,
                  ptr(self.x0), ptr(self.fm_out), ptr(self.cnt_emb), ptr(self.cnt_first), ptr(self.err), s)
@@ -526,6 +531,11 @@ class CTREngine:
                     ptr(self.idx_uniq), ptr(self.idx_n), B * self.n_slot, 1, ptr(self.hist), self.hist_len,
                     ptr(self.opt), 1 if train else 0, ptr(self.rows_u), ptr(self.rows_u1),
                     ptr(self.mv_u) if (train and self.mv_u is not None) else None, s)
+            if sp.M:
+                self._c("pool_fwd", "dl_pool_fwd_indexed", C_ref(L), ptr(self.rows_u),
+                        ptr(self.rows_u1) if sp.fm else None, ptr(self.idx_inv), self.n_rep, ptr(self.slot_start),
+                        ptr(self.slot_end), sp.M, sp.S, ptr(self.x0), ptr(self.fm_out), ptr(self.cnt_emb),
+                        ptr(self.cnt_first), s)
             self._c("embed_fwd", "dl_embed_fwd_indexed", C_ref(L), ptr(self.rows_u),
                     ptr(self.rows_u1) if sp.fm else None, ptr(self.idx_inv), self.n_rep, ptr(self.in_cont),
                     ptr(self.in_vec), ptr(self.x0), ptr(self.fm_out), ptr(self.fm_sum), s)
@@ -652,7 +662,7 @@ class CTREngine:
                     ptr(self.rows_u), ptr(self.rows_u1), ptr(self.mv_u), ptr(self.idx_uniq), ptr(self.idx_off),
                     ptr(self.idx_n), ptr(self.idx_refs), 1, B * self.n_slot, ptr(self.dz), ptr(self.w_head),
                     ptr(self.fm_sum), ptr(self.dx0), ptr(self.g_rep), ptr(self.g1_rep), ptr(self.hist),
-                    self.hist_len, ptr(self.opt), s)
+                    self.hist_len, ptr(self.opt), C_ref(self.pool_desc) if sp.M else None, s)
             if R:
                 # FM cont-field rows: per-block register partials, folded into g_rep, then updated
                 self._c("cont_bwd", "dl_embed_cont_bwd", C_ref(L), ptr(self.rows_u), ptr(self._cont()),
@@ -675,7 +685,7 @@ class CTREngine:
         if not self.lazy:
             self._c("cont_reduce", "dl_embed_cont_reduce", C_ref(L), ptr(self.cont_slab), bwd_blocks, ptr(self.tg),
                     ptr(self.fmg), ptr(self.touched), s)
-        if sp.M:
+        if sp.M and not self.lazy:
             self._c("pool_bwd", "dl_pool_bwd", C_ref(L), ptr(self.in_cate), sp.S, ptr(self.slot_start), ptr(self.slot_end),
                  sp.M, sp.S, ptr(self.x0), ptr(self.fm_sum), ptr(self.dz), ptr(self.w_head), ptr(self.dx0),
                  sp.S * sp.E, ptr(self.cnt_emb), ptr(self.cnt_first), ptr(self.tg), ptr(self.fmg),
@@ -769,7 +779,7 @@ class CTREngine:
 def default_adam(spec):
     """Table Adam used by the drop-in model classes: row records with lazy-exact
     catch-up (bit-identical to the dense sweep, rec.hip) wherever supported."""
-    return "dense" if spec.M else "lazy"
+    return "lazy"
 
 
 def _num_splits(K, splits, align=16):

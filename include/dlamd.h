@@ -70,7 +70,9 @@ typedef struct dl_emb_layout {
   int32_t fm_ld;            /* floats between samples in fm_out                      */
   int32_t dx0_ld;           /* floats between samples in dx0 (backward)              */
   int32_t dx0_cat_col;      /* column of the first single-cate gradient in dx0       */
-  int32_t pad_;
+  int32_t multi_width;      /* multi-hot id columns after the S singles that the batch
+                               index also covers (record path of deepfm_multi_cate; 0 = none):
+                               index refs per sample = (use_fm ? S : 0) + S + multi_width */
 } dl_emb_layout;
 
 /* Embedding gather + FM first/second order + deep-input assembly (forward).
@@ -155,6 +157,13 @@ int dl_pool_fwd(const dl_emb_layout* L, const float* table, const float* first_o
                 const int64_t* ids, int32_t ids_col, const int32_t* slot_start,
                 const int32_t* slot_end, int32_t n_slots, int32_t fm_col, float* x0,
                 float* fm_out, float* cnt_emb, float* cnt_first, int32_t* err, void* stream);
+/* Pooling over record rows (lazy Adam, L->multi_width > 0): the row of multi position l
+ * of sample b is inv_base + inv[b*ns + (use_fm ? S : 0) + S + l] of rows/rows_first
+ * (dl_rec_gather output, dl_index_build inv; -1 = padding id). */
+int dl_pool_fwd_indexed(const dl_emb_layout* L, const float* rows, const float* rows_first,
+                        const int32_t* inv, int32_t inv_base, const int32_t* slot_start,
+                        const int32_t* slot_end, int32_t n_slots, int32_t fm_col, float* x0,
+                        float* fm_out, float* cnt_emb, float* cnt_first, void* stream);
 /* Backward of pooling: d pooled = dsecond*(fm_sum - pooled) + dx0[pool cols];
  * each slot id gets d/cnt (div_no_nan gradient), first-order likewise. */
 int dl_pool_bwd(const dl_emb_layout* L, const int64_t* ids, int32_t ids_col,
@@ -280,12 +289,29 @@ int dl_rec_gather(const dl_emb_layout* L, const float* rec, int32_t rec_ld, int3
  * first; mv_u = NULL: the record is re-read and its catch-up replayed, using
  * hist), and the record is written with stamp = step.  Rows < n_rep instead add
  * their gradient into g_rep[row][E] / g1_rep[row] (finished by dl_rec_apply_rows). */
+/* Multi-hot pooling state for dl_rec_bwd_adam (deepfm_multi_cate.py:71-111): slot ranges
+ * within the multi block, the head column of the pooled first-order outputs, dx0's pooled
+ * columns, the pooled x0 (L->x0_pool_col) and the nonzero counts of dl_pool_fwd_indexed. */
+typedef struct dl_pool_desc {
+  const int32_t* slot_start;
+  const int32_t* slot_end;
+  int32_t n_slots;
+  int32_t fm_col;
+  int32_t dx0_pool_col;
+  int32_t pad_;
+  const float* x0;
+  const float* cnt_emb;
+  const float* cnt_first;
+} dl_pool_desc;
+/* pool: required when L->multi_width > 0 (multi refs add (dp/cnt) to the row gradient
+ * and dz*w_head[fm_col+m]/cnt_first to the first-order one), else may be NULL. */
 int dl_rec_bwd_adam(const dl_emb_layout* L, float* rec, int32_t rec_ld, int32_t has_first, int32_t n_rep,
                     const float* rows_u, const float* rows_u1, const float* mv_u,
                     const uint32_t* uniq_keys, const int32_t* seg_off, const int32_t* n_uniq,
                     const int32_t* sorted_refs, int32_t world, int64_t max_uniq, const float* dz,
                     const float* w_head, const float* fm_sum, const float* dx0, float* g_rep,
-                    float* g1_rep, const float* hist, int32_t hist_len, const float* opt, void* stream);
+                    float* g1_rep, const float* hist, int32_t hist_len, const float* opt,
+                    const dl_pool_desc* pool, void* stream);
 /* Rows [row0, row0+n): step-t update with dense gradients g[n][E], g1[n] (zeroed after). */
 int dl_rec_apply_rows(float* rec, int32_t rec_ld, int32_t emb_dim, int32_t has_first, int64_t row0,
                       int64_t n, float* g, float* g1, const float* hist, int32_t hist_len,

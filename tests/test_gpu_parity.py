@@ -54,8 +54,6 @@ def _batches(name, kw, B, n, seed=11):
 def test_train_steps_match_oracle(hip_lib, name, B, bwd):
     kw = CASES[name]
     model = _model(name)
-    if bwd == "lazy" and kw.get("multi_ranges"):
-        pytest.skip("row records: single-hot models only")
     cfg = R.make_cfg(model, **kw)
     spec = ModelSpec(model, **kw)
     P = R.init_params(cfg, np.random.default_rng(42))
@@ -120,6 +118,33 @@ def test_lazy_adam_bit_identical_to_dense(hip_lib, name, stash):
     sd, sl = dense.adam_state(), lazy.adam_state()
     for k in sd:
         np.testing.assert_array_equal(sl[k], sd[k], err_msg=k)
+
+
+def test_lazy_multi_hot_tracks_oracle(hip_lib):
+    """Multi-hot pooling on row records (deepfm_multi_cate): pooled rows come from the
+    caught-up records through the batch index, their gradients join each row's ordered
+    segment sum.  A large table and an 8-entry alpha ring force lagging rows and flushes;
+    the dense path's pooled scatter is atomic, so the bar is the oracle at TOL."""
+    name = "deepfm_multi_cate"
+    kw = dict(CASES[name], cate_index_size=40000)
+    cfg = R.make_cfg(name, **kw)
+    spec = ModelSpec(name, **kw)
+    P = R.init_params(cfg, np.random.default_rng(5))
+    eng = CTREngine(spec, max_batch=192, init="none", adam="lazy", hist_len=8)
+    eng.load_params(P)
+    opt = R.AdamTF1(cfg, P)
+    bs = _batches(name, kw, 192, 15, seed=21)
+    for step, b in enumerate(bs):
+        fw = R.train_step(cfg, P, opt, b)
+        eng.train_step(b, graph=(step >= 2))
+        torch.cuda.synchronize()
+        np.testing.assert_allclose(eng.z[:192].cpu().numpy(), fw["z"], atol=TOL, rtol=0,
+                                   err_msg="logits step %d" % step)
+        if step == 7:
+            np.testing.assert_allclose(eng.predict(bs[0]), R.forward(cfg, P, bs[0])["p"], atol=TOL, rtol=0)
+    got = eng.params()
+    for k in P:
+        np.testing.assert_allclose(got[k], P[k], atol=TOL, rtol=0, err_msg=k)
 
 
 @pytest.mark.parametrize("adam", ["dense", "lazy"])
