@@ -78,16 +78,20 @@ PMC_KERNEL_LAZY = {"rec_gather": "rec_gather_kernel<16>", "embed_bwd": "rec_bwd_
                    "head": "head_kernel"}
 
 
-def pmc_traffic(label, world, lazy=False):
-    """HBM bytes per launch of `label` from the newest committed PMC summary
-    (scripts/pmc_summary.py: (2*FETCH_SIZE + WRITE_SIZE)*1024, gfx950 correction)."""
+def pmc_traffic(label, world, lazy=False, workload="c2"):
+    """HBM bytes per launch of `label` from the newest committed PMC summary of the same
+    workload (scripts/pmc_summary.py: (2*FETCH_SIZE + WRITE_SIZE)*1024, gfx950 correction;
+    a summary without a "workload" key was collected on C2)."""
     import glob
     names = PMC_KERNEL_LAZY if lazy else PMC_KERNEL
     if world != 1 or label not in names:
         return None
     files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*", "pmc_summary.json")), key=os.path.getmtime)
     for f in reversed(files):
-        k = json.load(open(f))["kernels"].get(names[label])
+        d = json.load(open(f))
+        if d.get("workload", "c2") != workload:
+            continue
+        k = d["kernels"].get(names[label])
         if k and "hbm_bytes" in k:
             return {"hbm_bytes": int(k["hbm_bytes"]), "source": os.path.relpath(f, ROOT)}
     return None
@@ -275,7 +279,7 @@ def main():
                 "unit": "TFLOP/s", "frac": round(ach / peak, 3), "traffic": None,
                 "algorithmic_flops": amount}
     step_kernel_us = sum(k["us"] for k in kernels.values())
-    pmc = pmc_traffic(dom, world, lazy=uniq is not None)
+    pmc = pmc_traffic(dom, world, lazy=uniq is not None, workload=wl)
     if pmc is not None:
         roof["traffic"] = pmc["hbm_bytes"]
         roof["traffic_source"] = pmc["source"]

@@ -361,7 +361,12 @@ struct PoolArgs {
   int32_t* err;
 };
 
-template <int E>
+// One wave per sample.  A slot's positions are resolved 64 at a time, one per lane (ids or
+// the batch index: one coalesced load), then handed to the row loads by __shfl — the
+// 64/RPI row loads of a chunk are independent, so they are in flight together instead
+// of each waiting on its own id load.  Summation order (per lane, then the xor tree) is
+// the same for both modes and for any chunking: dense and record paths pool identically.
+template <int E, bool IDX>
 __global__ __launch_bounds__(256) void pool_fwd_kernel(PoolArgs a) {
   constexpr int LPR = E / 4;
   constexpr int RPI = 64 / LPR;
@@ -371,30 +376,45 @@ __global__ __launch_bounds__(256) void pool_fwd_kernel(PoolArgs a) {
   const int wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   const int nwaves = (gridDim.x * blockDim.x) >> 6;
   const float4* tab4 = reinterpret_cast<const float4*>(a.table);
+  const int ns = index_slots(L), mb = index_multi_base(L);
   for (int b = wave; b < L.batch; b += nwaves) {
-    const int64_t* ids = a.ids + (int64_t)b * L.cate_ld + a.ids_col;
+    const int64_t* ids = IDX ? nullptr : a.ids + (int64_t)b * L.cate_ld + a.ids_col;
+    const int32_t* invb = IDX ? a.inv + (int64_t)b * ns + mb : nullptr;
     for (int m = 0; m < a.n_slots; ++m) {
       const int s0 = a.slot_start[m], s1 = a.slot_end[m];
       float4 s = f4_zero();
-      float cnt = 0.f;
-      for (int l0 = s0; l0 < s1; l0 += RPI) {
-        const int l = l0 + r;
-        float4 e = f4_zero();
-        if (l < s1) {
-          if (a.inv) {
-            const int ri = a.inv[(int64_t)b * index_slots(L) + index_multi_base(L) + l];
-            if (ri >= 0) e = tab4[(int64_t)(a.inv_base + ri) * LPR + q];
+      float cnt = 0.f, s1v = 0.f, c1 = 0.f;
+      for (int c0 = s0; c0 < s1; c0 += 64) {
+        const int nl = min(64, s1 - c0);
+        // source row of position c0 + lane (-1: padding / zero row)
+        long long src = -1;
+        if (lane < nl) {
+          if (IDX) {
+            const int ri = invb[c0 + lane];
+            src = ri >= 0 ? (long long)a.inv_base + ri : -1;
           } else {
-            const int64_t row = checked_row(ids[l], 0, L.n_rows, a.err);
-            if (row_ok(row, L.zero_row0)) e = tab4[row * LPR + q];
+            const int64_t row = checked_row(ids[c0 + lane], 0, L.n_rows, a.err);
+            src = row_ok(row, L.zero_row0) ? row : -1;
           }
         }
-        // tf.reduce_sum(emb, axis=2) then count_nonzero over the slot
-        float rs = (e.x + e.y) + (e.z + e.w);
+        if (a.first_order) {
+          const float w = src >= 0 ? a.first_order[src] : 0.f;
+          s1v += w;
+          c1 += (w != 0.f) ? 1.f : 0.f;
+        }
 #pragma unroll
-        for (int o = 1; o < LPR; o <<= 1) rs += __shfl_xor(rs, o, 64);
-        if (q == 0 && l < s1 && rs != 0.f) cnt += 1.f;
-        s.x += e.x; s.y += e.y; s.z += e.z; s.w += e.w;
+        for (int it = 0; it < 64 / RPI; ++it) {
+          const int pl = it * RPI + r;
+          const long long row = __shfl(src, pl, 64);
+          float4 e = f4_zero();
+          if (pl < nl && row >= 0) e = tab4[row * LPR + q];
+          // tf.reduce_sum(emb, axis=2) then count_nonzero over the slot
+          float rs = (e.x + e.y) + (e.z + e.w);
+#pragma unroll
+          for (int o = 1; o < LPR; o <<= 1) rs += __shfl_xor(rs, o, 64);
+          if (q == 0 && pl < nl && rs != 0.f) cnt += 1.f;
+          s.x += e.x; s.y += e.y; s.z += e.z; s.w += e.w;
+        }
       }
 #pragma unroll
       for (int o = LPR; o < 64; o <<= 1) {
@@ -409,19 +429,6 @@ __global__ __launch_bounds__(256) void pool_fwd_kernel(PoolArgs a) {
       }
       if (lane == 0) a.cnt_emb[(int64_t)b * a.n_slots + m] = cnt;
       if (a.first_order) {
-        float s1v = 0.f, c1 = 0.f;
-        for (int l = s0 + lane; l < s1; l += 64) {
-          float w;
-          if (a.inv) {
-            const int ri = a.inv[(int64_t)b * index_slots(L) + index_multi_base(L) + l];
-            w = ri >= 0 ? a.first_order[a.inv_base + ri] : 0.f;
-          } else {
-            const int64_t row = checked_row(ids[l], 0, L.n_rows, a.err);
-            w = row_ok(row, L.zero_row0) ? a.first_order[row] : 0.f;
-          }
-          s1v += w;
-          c1 += (w != 0.f) ? 1.f : 0.f;
-        }
         s1v = wave_sum(s1v);
         c1 = wave_sum(c1);
         if (lane == 0) {
@@ -618,7 +625,7 @@ extern "C" int dl_pool_fwd(const dl_emb_layout* L, const float* table, const flo
   if (L->batch == 0 || n_slots == 0) return 0;
   PoolArgs a{*L, nullptr, 0, table, first_order, ids, ids_col, slot_start, slot_end, n_slots, fm_col,
              x0, fm_out, cnt_emb, cnt_first, err};
-  DL_DISPATCH_E(L->emb_dim, hipLaunchKernelGGL(pool_fwd_kernel<kE>, dim3(emb_grid(L->batch)),
+  DL_DISPATCH_E(L->emb_dim, hipLaunchKernelGGL((pool_fwd_kernel<kE, false>), dim3(emb_grid(L->batch)),
                                                dim3(256), 0, as_stream(stream), a));
   DL_RETURN_LAUNCH("dl_pool_fwd");
 }
@@ -634,7 +641,7 @@ extern "C" int dl_pool_fwd_indexed(const dl_emb_layout* L, const float* rows, co
   if (L->batch == 0 || n_slots == 0) return 0;
   PoolArgs a{*L, inv, inv_base, rows, rows_first, nullptr, 0, slot_start, slot_end, n_slots, fm_col,
              x0, fm_out, cnt_emb, cnt_first, nullptr};
-  DL_DISPATCH_E(L->emb_dim, hipLaunchKernelGGL(pool_fwd_kernel<kE>, dim3(emb_grid(L->batch)),
+  DL_DISPATCH_E(L->emb_dim, hipLaunchKernelGGL((pool_fwd_kernel<kE, true>), dim3(emb_grid(L->batch)),
                                                dim3(256), 0, as_stream(stream), a));
   DL_RETURN_LAUNCH("dl_pool_fwd_indexed");
 }

@@ -141,6 +141,45 @@ __device__ __forceinline__ void rec_update(float* __restrict__ r, int E, int d, 
 // Replicated rows (row < n_rep, hit by every sample through the FM cont fields)
 // only deposit their cate-reference gradient into g_rep/g1_rep; dl_rec_apply_rows
 // updates them after the cont part is added.  E/4 lanes per row, float4 each.
+// Per (sample, pooled slot): the gradient every member row of the slot receives,
+// (dx0[pool m] + dsec*(fm_sum - pooled_m)) / cnt  (div_no_nan; deepfm_multi_cate.py:71-111),
+// and dz * w_head[fm_col + m] / cnt_first for the first-order weights.
+template <int E>
+__global__ __launch_bounds__(256) void pool_grad_kernel(dl_emb_layout L, dl_pool_desc p, const float* __restrict__ dz,
+                                                        const float* __restrict__ w_head,
+                                                        const float* __restrict__ fm_sum,
+                                                        const float* __restrict__ dx0, bool g1) {
+  constexpr int LPR = E / 4;
+  const int S = L.cate_fields;
+  const int Cf = (L.use_fm && L.fm_cont) ? L.cont_fields : 0;
+  const int F = Cf + S + L.fm_extra;
+  const long long n = (long long)L.batch * p.n_slots * LPR;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x) {
+    const int q = (int)(i % LPR);
+    const long long bm = i / LPR;
+    const int b = (int)(bm / p.n_slots), m = (int)(bm % p.n_slots);
+    const float c = p.cnt_emb[bm];
+    float4 gv = make_float4(0.f, 0.f, 0.f, 0.f);
+    const float dzb = L.use_fm ? dz[b] : 0.f;
+    if (c > 0.f) {
+      float4 dp = *reinterpret_cast<const float4*>(dx0 + (long long)b * L.dx0_ld + p.dx0_pool_col + m * E + 4 * q);
+      if (L.use_fm) {
+        const float* ws = w_head + F + 4 * q;
+        const float4 fs = *reinterpret_cast<const float4*>(fm_sum + (long long)b * E + 4 * q);
+        const float4 pv = *reinterpret_cast<const float4*>(p.x0 + (long long)b * L.x0_ld + L.x0_pool_col + m * E + 4 * q);
+        dp.x = fmaf(dzb * ws[0], fs.x - pv.x, dp.x); dp.y = fmaf(dzb * ws[1], fs.y - pv.y, dp.y);
+        dp.z = fmaf(dzb * ws[2], fs.z - pv.z, dp.z); dp.w = fmaf(dzb * ws[3], fs.w - pv.w, dp.w);
+      }
+      gv = make_float4(dp.x / c, dp.y / c, dp.z / c, dp.w / c);
+    }
+    *reinterpret_cast<float4*>(p.g_pool + bm * E + 4 * q) = gv;
+    if (g1 && q == 0) {
+      const float c1 = p.cnt_first[bm];
+      p.g1_pool[bm] = c1 > 0.f ? dzb * w_head[p.fm_col + m] / c1 : 0.f;
+    }
+  }
+}
+
 template <int E>
 __global__ __launch_bounds__(256) void rec_bwd_adam_kernel(SegGradIn sg, float* __restrict__ rec, RecCfg c,
                                                            int n_rep, const float* __restrict__ rows_u,
@@ -391,15 +430,24 @@ extern "C" int dl_rec_bwd_adam(const dl_emb_layout* L, float* rec, int32_t rec_l
   DL_CHECK_ARG(!(n_rep && has_first) || g1_rep, "g1_rep required");
   DL_CHECK_ARG(L->dx0_ld % 4 == 0 && L->dx0_cat_col % 4 == 0, "dx0 must be float4 aligned");
   if (max_uniq <= 0) return 0;
-  DL_CHECK_ARG(L->multi_width == 0 || (pool && pool->slot_start && pool->slot_end && pool->x0 && pool->cnt_emb),
+  const bool multi = L->multi_width > 0;
+  DL_CHECK_ARG(!multi || (pool && pool->slot_start && pool->slot_end && pool->x0 && pool->cnt_emb &&
+                          pool->g_pool && pool->n_slots > 0),
                "multi-hot references need the pool descriptor");
-  DL_CHECK_ARG(!pool || !L->use_fm || !has_first || pool->cnt_first, "cnt_first required");
-  DL_CHECK_ARG(!pool || (pool->dx0_pool_col % 4 == 0 && L->x0_pool_col % 4 == 0), "pool columns not float4 aligned");
+  DL_CHECK_ARG(!multi || !L->use_fm || !has_first || (pool->cnt_first && pool->g1_pool),
+               "cnt_first / g1_pool required");
+  DL_CHECK_ARG(!multi || (pool->dx0_pool_col % 4 == 0 && L->x0_pool_col % 4 == 0),
+               "pool columns not float4 aligned");
   SegGradIn sg{*L, seg_off, sorted_refs, dz, w_head, fm_sum, dx0};
-  if (L->multi_width > 0) {
+  const bool g1p = multi && L->use_fm && has_first;
+  if (multi) {
     sg.slot_start = pool->slot_start; sg.slot_end = pool->slot_end; sg.n_slots = pool->n_slots;
-    sg.fm_col = pool->fm_col; sg.dx0_pool_col = pool->dx0_pool_col; sg.x0 = pool->x0;
-    sg.cnt_emb = pool->cnt_emb; sg.cnt_first = has_first ? pool->cnt_first : nullptr;
+    sg.g_pool = pool->g_pool; sg.g1_pool = g1p ? pool->g1_pool : nullptr;
+    if (L->batch > 0)
+      DL_DISPATCH_E(L->emb_dim, {
+        hipLaunchKernelGGL(pool_grad_kernel<kE>, dim3(grid_cap((long long)L->batch * pool->n_slots * (kE / 4))),
+                           dim3(256), 0, as_stream(stream), *L, *pool, dz, w_head, fm_sum, dx0, g1p);
+      });
   }
   DL_DISPATCH_E(L->emb_dim, {
     const unsigned grid = grid_cap(max_uniq * (kE / 4));

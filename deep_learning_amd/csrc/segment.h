@@ -21,15 +21,13 @@ struct SegGradIn {
   const float* fm_sum;
   const float* dx0;
   // multi-hot references (index_multi_base(L) <= slot; records only): nonzero-mean pooling
-  // (deepfm_multi_cate.py:71-111) — slot ranges within the multi block, pooled x0 and counts
+  // (deepfm_multi_cate.py:71-111) — slot ranges within the multi block and the per-sample
+  // pooled-slot gradients g_pool [B][n_slots][E], g1_pool [B][n_slots] (rec.hip pool_grad)
   const int32_t* slot_start;
   const int32_t* slot_end;
   int n_slots;
-  int fm_col;        // head column of the pooled first-order outputs
-  int dx0_pool_col;
-  const float* x0;
-  const float* cnt_emb;
-  const float* cnt_first;
+  const float* g_pool;
+  const float* g1_pool;
 };
 
 struct SegGrad {
@@ -97,27 +95,15 @@ __device__ __forceinline__ SegGrad4 segment_grad4(const SegGradIn& a, long long 
     if (k < 0 || k >= nrefs) continue;
     const int b = k / ns, sl = k % ns;
     if (sl >= mb) {
-      // pooled slot m of multi position l: d/d row = (dx0[pool m] + dsec*(fm_sum - pooled_m)) / cnt
+      // pooled slot m of multi position l: every member row gets the slot's gradient
       const int l = sl - mb;
       int m = 0;
       while (m < a.n_slots && !(l >= a.slot_start[m] && l < a.slot_end[m])) ++m;
       if (m == a.n_slots) continue;
-      const float c = a.cnt_emb[(long long)b * a.n_slots + m];
-      const float dzb = L.use_fm ? a.dz[b] : 0.f;
-      if (c > 0.f) {
-        float4 dp = *reinterpret_cast<const float4*>(a.dx0 + (long long)b * L.dx0_ld + a.dx0_pool_col + m * E + 4 * q);
-        if (L.use_fm) {
-          const float4 fs = *reinterpret_cast<const float4*>(a.fm_sum + (long long)b * E + 4 * q);
-          const float4 pv = *reinterpret_cast<const float4*>(a.x0 + (long long)b * L.x0_ld + L.x0_pool_col + m * E + 4 * q);
-          dp.x = fmaf(dzb * wsec.x, fs.x - pv.x, dp.x); dp.y = fmaf(dzb * wsec.y, fs.y - pv.y, dp.y);
-          dp.z = fmaf(dzb * wsec.z, fs.z - pv.z, dp.z); dp.w = fmaf(dzb * wsec.w, fs.w - pv.w, dp.w);
-        }
-        r.x.x += dp.x / c; r.x.y += dp.y / c; r.x.z += dp.z / c; r.x.w += dp.w / c;
-      }
-      if (L.use_fm && a.cnt_first) {
-        const float c1 = a.cnt_first[(long long)b * a.n_slots + m];
-        if (c1 > 0.f) r.g1 += dzb * a.w_head[a.fm_col + m] / c1;
-      }
+      const long long bm = (long long)b * a.n_slots + m;
+      const float4 gp = *reinterpret_cast<const float4*>(a.g_pool + bm * E + 4 * q);
+      r.x.x += gp.x; r.x.y += gp.y; r.x.z += gp.z; r.x.w += gp.w;
+      if (a.g1_pool) r.g1 += a.g1_pool[bm];
     } else if (L.use_fm && sl < S) {
       const float dzb = a.dz[b];
       const float4 fs = *reinterpret_cast<const float4*>(a.fm_sum + (long long)b * E + 4 * q);

@@ -291,7 +291,8 @@ int dl_rec_gather(const dl_emb_layout* L, const float* rec, int32_t rec_ld, int3
  * their gradient into g_rep[row][E] / g1_rep[row] (finished by dl_rec_apply_rows). */
 /* Multi-hot pooling state for dl_rec_bwd_adam (deepfm_multi_cate.py:71-111): slot ranges
  * within the multi block, the head column of the pooled first-order outputs, dx0's pooled
- * columns, the pooled x0 (L->x0_pool_col) and the nonzero counts of dl_pool_fwd_indexed. */
+ * columns, the pooled x0 (L->x0_pool_col), the nonzero counts of dl_pool_fwd_indexed and
+ * scratch g_pool [B][n_slots][E], g1_pool [B][n_slots] for the per-slot gradients. */
 typedef struct dl_pool_desc {
   const int32_t* slot_start;
   const int32_t* slot_end;
@@ -302,6 +303,8 @@ typedef struct dl_pool_desc {
   const float* x0;
   const float* cnt_emb;
   const float* cnt_first;
+  float* g_pool;
+  float* g1_pool;
 } dl_pool_desc;
 /* pool: required when L->multi_width > 0 (multi refs add (dp/cnt) to the row gradient
  * and dz*w_head[fm_col+m]/cnt_first to the first-order one), else may be NULL. */
