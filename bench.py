@@ -141,6 +141,10 @@ def main():
     ap.add_argument("--workload", default="c2", choices=["c2", "c3", "c5"],
                     help="c2 DeepFM (the headline, default); c3 deepfm_multi_cate 6 multi-hot slots x 60; "
                          "c5 Wide&Deep with the bf16 tower (single GPU)")
+    ap.add_argument("--no-graph", action="store_true", help="eager launches instead of hipGraph replay")
+    ap.add_argument("--no-prefetch", action="store_true",
+                    help="build each batch's index at the start of its own step (default: during the "
+                         "previous step, on a second hardware queue)")
     ap.add_argument("--sharded", action="store_true",
                     help="run the row-sharded multi-GPU engine even at N=1 (measures its overhead)")
     ap.add_argument("--adam", default="lazy", choices=["dense", "lazy"],
@@ -192,7 +196,13 @@ def main():
         spec = ModelSpec("deepfm_pipeline", C=C2["C"], V=0, S=C2["S"], E=C2["E"],
                          cate_index_size=C2["S"] * args.vocab, hidden=C2["hidden"])
     log("rank %d/%d: building engine, table rows %d" % (rank, world, spec.n_rows))
-    use_graph = True   # single GPU: the whole step after the index build; sharded: the dense middle
+    use_graph = not args.no_graph   # single GPU: the step after the index build; sharded: the dense middle
+    prefetch = not args.no_prefetch
+
+    def nxt(i):
+        # the batch after step i (each step still builds exactly one index: the last timed
+        # step builds the one after the timed region, the last warmup step the first one)
+        return {"next_batch": dev_batches[(i + 1) % nb]} if prefetch else {}
     if not sharded:
         eng = CTREngine(spec, max_batch=B, seed=2019, adam=args.adam)
     else:
@@ -212,16 +222,18 @@ def main():
     torch.cuda.synchronize()
     log("warmup %d" % args.warmup)
     for i in range(max(1, args.warmup)):
-        eng.train_step(dev_batches[i % nb], graph=use_graph)
+        eng.train_step(dev_batches[i % nb], graph=use_graph, **nxt(i))
     torch.cuda.synchronize()
     eng.check_error()
 
     log("timed %d steps" % args.steps)
+    if getattr(eng, "host_marks", None) is not None:
+        eng.host_marks.clear()
     barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for i in range(args.steps):
-        eng.train_step(dev_batches[i % nb], graph=use_graph)
+        eng.train_step(dev_batches[i % nb], graph=use_graph, **nxt(i))
     torch.cuda.synchronize()
     barrier()
     t1 = time.perf_counter()
@@ -235,6 +247,18 @@ def main():
     loss = eng.loss()
 
     # ---- live per-kernel timing (HIP events on the launch stream)
+    marks = getattr(eng, "host_marks", None)
+    if marks:
+        # host timeline of the timed steps: mean us from step start per phase
+        starts = [i for i, (n, _) in enumerate(marks) if n == "start"]
+        acc = {}
+        for a, b in zip(starts, starts[1:] + [len(marks)]):
+            t0 = marks[a][1]
+            for n, t in marks[a:b]:
+                acc.setdefault(n, []).append((t - t0) * 1e6)
+        log("host phases (us from step start): " +
+            ", ".join("%s %.0f" % (n, sum(v) / len(v)) for n, v in acc.items()))
+        marks.clear()
     log("per-kernel event pass")
     touched = int(eng.touched.sum().item()) if False else None
     eng.prof = []

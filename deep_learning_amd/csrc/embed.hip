@@ -689,39 +689,41 @@ struct BwdSortedArgs {
 };
 
 
+// float4 lanes (E/4 per unique row, as rec_bwd_adam_kernel): a wave keeps 64/(E/4)
+// rows' segment walks in flight; sums are bit-identical to the per-dim form.
 template <int E>
 __global__ __launch_bounds__(256) void embed_bwd_sorted_kernel(BwdSortedArgs a) {
-  constexpr int RPI = 64 / E;
+  constexpr int LPR = E / 4;
   const dl_emb_layout& L = a.L;
-  const int lane = threadIdx.x & 63;
-  const int r = lane / E, d = lane % E;
+  const long long gt = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  const int q = (int)(gt % LPR);
+  const long long group0 = gt / LPR, ngroups = (long long)gridDim.x * blockDim.x / LPR;
   const int S = L.cate_fields;
   const int ns = index_slots(L);
   const int Cf = (L.use_fm && L.fm_cont) ? L.cont_fields : 0;
   const int F = Cf + S + L.fm_extra;
   const long long nrefs = (long long)L.batch * ns;
   const int nu = clamp_uniq(a.n_uniq, nrefs);
-  const long long group = ((long long)blockIdx.x * blockDim.x + threadIdx.x) / 64 * RPI + r;
-  const long long ngroups = (long long)gridDim.x * blockDim.x / 64 * RPI;
-  const float wsec = L.use_fm ? a.w_head[F + d] : 0.f;
+  const float* ws = a.w_head + F + 4 * q;   // not 16-B aligned
+  const float4 wsec = L.use_fm ? make_float4(ws[0], ws[1], ws[2], ws[3]) : make_float4(0.f, 0.f, 0.f, 0.f);
   const SegGradIn sg{L, a.seg_off, a.refs, a.dz, a.w_head, a.fm_sum, a.dx0};
-  for (long long u = group; u < nu; u += ngroups) {
-    const SegGrad sgr = segment_grad<E>(sg, u, d, nrefs, wsec);
-    const uint32_t key = a.uniq[u];
-    const int64_t row = decode_key(key, a.world);
+  for (long long u = group0; u < nu; u += ngroups) {
+    const SegGrad4 sgr = segment_grad4<E>(sg, u, q, nrefs, wsec);
+    const int64_t row = decode_key(a.uniq[u], a.world);
     if (row < 0 || row >= L.n_rows) continue;
-    float v = 0.f;
-    if (sgr.dsum != 0.f) v = a.rows_u ? a.rows_u[u * E + d] : a.table[row * E + d];
-    const float g = seg_row_grad(sgr.s, sgr.dsum, sgr.x, v);
-    if (a.compact) {
-      a.g_out[u * E + d] = g;
-      if (a.g1_out && d == 0) a.g1_out[u] = sgr.g1;
-    } else {
-      a.g_out[row * E + d] = g;
-      if (d == 0) {
-        if (a.g1_out && L.use_fm) a.g1_out[row] = sgr.g1;
-        a.touched[row] = 1;
-      }
+    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (sgr.dsum.x != 0.f || sgr.dsum.y != 0.f || sgr.dsum.z != 0.f || sgr.dsum.w != 0.f)
+      v = *reinterpret_cast<const float4*>((a.rows_u ? a.rows_u + u * E : a.table + row * E) + 4 * q);
+    float4 g;
+    g.x = seg_row_grad(sgr.s.x, sgr.dsum.x, sgr.x.x, sgr.dsum.x != 0.f ? v.x : 0.f);
+    g.y = seg_row_grad(sgr.s.y, sgr.dsum.y, sgr.x.y, sgr.dsum.y != 0.f ? v.y : 0.f);
+    g.z = seg_row_grad(sgr.s.z, sgr.dsum.z, sgr.x.z, sgr.dsum.z != 0.f ? v.z : 0.f);
+    g.w = seg_row_grad(sgr.s.w, sgr.dsum.w, sgr.x.w, sgr.dsum.w != 0.f ? v.w : 0.f);
+    const long long o = a.compact ? u : row;
+    *reinterpret_cast<float4*>(a.g_out + o * E + 4 * q) = g;
+    if (q == 0) {
+      if (a.g1_out && (a.compact || L.use_fm)) a.g1_out[o] = sgr.g1;
+      if (!a.compact) a.touched[row] = 1;
     }
   }
 }
@@ -740,8 +742,8 @@ extern "C" int dl_embed_bwd_sorted(const dl_emb_layout* L, const float* table, c
   DL_CHECK_ARG(compact || touched, "dense output needs the touched flags");
   DL_CHECK_ARG(!L->use_fm || (dz && w_head && fm_sum), "FM backward inputs required");
   if (max_uniq <= 0) return 0;
-  const int rpi = 64 / L->emb_dim;
-  long long blocks = (max_uniq + 4 * rpi - 1) / (4 * rpi);
+  DL_CHECK_ARG(L->dx0_ld % 4 == 0 && L->dx0_cat_col % 4 == 0, "dx0 must be float4 aligned");
+  long long blocks = (max_uniq * (L->emb_dim / 4) + 255) / 256;
   if (blocks > 8192) blocks = 8192;
   BwdSortedArgs a{*L, table, rows_u, uniq_keys, seg_off, n_uniq, sorted_refs, world, dz, w_head, fm_sum, dx0,
                   g_out, g1_out, touched, compact};

@@ -268,8 +268,7 @@ class CTREngine:
         self.in_cont = z(B, max(sp.C, 1))
         self.in_vec = z(B, max(sp.V, 1))
         self.in_cate = z(B, max(sp.cate_ld, 1), dt=torch.int64)
-        self.graph = None
-        self.graph_batch = None
+        self.graphs = {}        # (buffer set, batch) -> captured step
         self.prof = None
         self.steps = 0
         if init == "device":
@@ -723,21 +722,101 @@ class CTREngine:
             self._c("adam_table", "dl_adam_rows", ptr(self.table), ptr(self.tm), ptr(self.tv), ptr(self.tg),
                     ptr(self.touched), self.table.shape[0], sp.E, 0.0, 1, ptr(self.opt), None, s)
 
-    def train_step(self, batch=None, graph=False):
-        """One training step on `batch` (or on the already-staged slots if None)."""
-        B = self.stage(batch) if batch is not None else self.B
+    # per-batch buffers: inputs and the batch index.  With prefetching they are double
+    # buffered — the next batch is staged and indexed into the other set on a side stream
+    # while the current step runs.
+    SLOT_ATTRS = ("in_label", "in_cont", "in_vec", "in_cate", "in_wide", "idx_ws", "idx_keys", "idx_refs",
+                  "idx_uniq", "idx_off", "idx_n", "idx_inv")
+
+    def _side_stream(self):
+        if getattr(self, "side", None) is None:
+            # high priority: a hardware queue of its own (a default-priority stream can share
+            # the compute stream's queue, which serialises the two)
+            self.side = torch.cuda.Stream(priority=-1)
+        return self.side
+
+    def _use_slot(self, k):
+        for n, t in self._slots[k].items():
+            setattr(self, n, t)
+        self._cur = k
+
+    def _enable_slots(self):
+        if getattr(self, "_slots", None) is not None:
+            return
+        a = {n: getattr(self, n) for n in self.SLOT_ATTRS if getattr(self, n, None) is not None}
+        self._slots = [a, {n: torch.zeros_like(t) for n, t in a.items()}]
+        self._cur = 0
+        self._slot_free = [None, None]    # event: the compute stream is done with a set
+        self._pf = None                   # (set, B, ready event, batch) of a prefetched batch
+
+    def prefetch(self, batch):
+        """Stage `batch` and build its index into the idle buffer set on the side stream;
+        train_step(batch) then starts from it.  Issued before the current step's work, so
+        the index build (memory bound) overlaps that step's GEMMs."""
+        self._enable_slots()
+        if self._pf is not None:
+            torch.cuda.current_stream().wait_event(self._pf[2])
+        cur = self._cur
+        k = 1 - cur
+        side = self._side_stream()
+        if self._slot_free[k] is not None:
+            side.wait_event(self._slot_free[k])
+        else:
+            side.wait_stream(torch.cuda.current_stream())
+        self._use_slot(k)
+        try:
+            with torch.cuda.stream(side):
+                B = self.stage(batch)
+                self._pre(B)
+                ev = torch.cuda.Event()
+                ev.record(side)
+        finally:
+            self._use_slot(cur)
+        self._pf = (k, B, ev, batch)
+
+    def _begin(self, batch):
+        """Buffers of this step's batch: the prefetched set if `batch` is the one prefetched,
+        else staged and indexed now on the compute stream."""
+        pf = getattr(self, "_pf", None)
+        if pf is not None and batch is not None and batch is pf[3]:
+            self._pf = None
+            self._use_slot(pf[0])
+            torch.cuda.current_stream().wait_event(pf[2])
+            return pf[1], True
+        if pf is not None:      # a different batch came: drop the prefetch (after it lands)
+            torch.cuda.current_stream().wait_event(pf[2])
+            self._pf = None
+        return (self.stage(batch) if batch is not None else self.B), False
+
+    def _release(self):
+        """Mark the current buffer set free once the compute stream's queued work is done."""
+        if getattr(self, "_slots", None) is not None:
+            ev = torch.cuda.Event()
+            ev.record()
+            self._slot_free[self._cur] = ev
+
+    def train_step(self, batch=None, graph=False, next_batch=None):
+        """One training step on `batch` (or on the already-staged slots if None).
+        next_batch: prefetch it (stage + index build on the side stream) during this step."""
+        B, indexed = self._begin(batch)
         if self.lazy:
             # every row's lag must stay below the alpha ring (rec.hip)
             if self.since_flush >= self.hist_len - 2:
                 self.flush()
             self.since_flush += 1
-        self._pre(B)
+        if not indexed:
+            self._pre(B)
+        if next_batch is not None:
+            self.prefetch(next_batch)
         if graph:
-            if self.graph is None or self.graph_batch != B:
-                self._capture(B)
-            self.graph.replay()
+            key = (getattr(self, "_cur", 0), B)
+            g = self.graphs.get(key)
+            if g is None:
+                g = self.graphs[key] = self._capture(B)
+            g.replay()
         else:
             self._train(B)
+        self._release()
         self.steps += 1
         self.last_batch = B
         return B
@@ -750,14 +829,16 @@ class CTREngine:
         with torch.cuda.graph(g, stream=s):
             self._train(B)
         torch.cuda.current_stream().wait_stream(s)
-        self.graph, self.graph_batch = g, B
+        return g
 
     def predict(self, batch):
         """Forward only: returns sigmoid scores [B] (host numpy)."""
-        B = self.stage(batch)
+        B, indexed = self._begin(batch)
         s = _lib.stream_handle()
-        self._pre(B)
+        if not indexed:
+            self._pre(B)
         self._forward(B, s)
+        self._release()
         self.check_error()
         return self.score[:B].cpu().numpy()
 

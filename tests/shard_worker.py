@@ -60,6 +60,10 @@ def run_sim(rank, world, steps, Bl, out_dir):
         owners = own(rows)
         send = [rows[owners == p] for p in range(world)]
         counts = ex.counts([len(x) for x in send])
+        # the engine's single-collective form: all ranks' per-owner counts (+ a replicated count)
+        cm = ex.count_matrix(torch.tensor([len(x) for x in send] + [7], dtype=torch.int32))
+        assert [cm[r][rank] for r in range(world)] == counts and cm[rank][:world] == [len(x) for x in send]
+        assert all(row[world] == 7 for row in cm)
         req = ex.all_to_all(torch.from_numpy(np.concatenate(send)), [len(x) for x in send], counts).numpy()
         # owner side: answer from its own rows only
         assert np.all(own(req) == rank)
@@ -127,7 +131,7 @@ def run_sim(rank, world, steps, Bl, out_dir):
     np.savez(os.path.join(out_dir, "rank%d.npz" % rank), **P)
 
 
-def run_gpu(rank, world, steps, Bl, out_dir, adam="dense"):
+def run_gpu(rank, world, steps, Bl, out_dir, adam="dense", prefetch=False):
     from deep_learning_amd.engine import ModelSpec
     from deep_learning_amd.shard import Exchange, ShardedCTREngine
     torch.cuda.set_device(0)
@@ -136,8 +140,12 @@ def run_gpu(rank, world, steps, Bl, out_dir, adam="dense"):
     P = R.init_params(cfg, np.random.default_rng(42))
     eng = ShardedCTREngine(ModelSpec("deepfm_pipeline", **KW), Bl, ex, adam=adam, hist_len=4)
     eng.load_params(P)
-    for step, bg in enumerate(global_batches(Bl * world, steps)):
-        eng.train_step(local(bg, rank, world), graph=step >= 2)   # dense middle as a hipGraph from step 2
+    batches = [local(bg, rank, world) for bg in global_batches(Bl * world, steps)]
+    for step, b in enumerate(batches):
+        # dense middle as a hipGraph from step 2; prefetch: the next batch's index and counts
+        # on the side stream during this step
+        nxt = batches[step + 1] if prefetch and step + 1 < len(batches) else None
+        eng.train_step(b, graph=step >= 2, next_batch=nxt)
         torch.cuda.synchronize()
         np.savez(os.path.join(out_dir, "rank%d_step%d.npz" % (rank, step)), z=eng.z[:Bl].cpu().numpy(),
                  loss=eng.loss())
@@ -154,6 +162,7 @@ if __name__ == "__main__":
     if mode == "sim":
         run_sim(rank, world, steps, Bl, out_dir)
     else:
-        run_gpu(rank, world, steps, Bl, out_dir, adam="lazy" if mode == "gpu_lazy" else "dense")
+        run_gpu(rank, world, steps, Bl, out_dir, adam="lazy" if mode.startswith("gpu_lazy") else "dense",
+                prefetch=mode.endswith("_pf"))
     dist.barrier()
     dist.destroy_process_group()

@@ -168,3 +168,36 @@ def test_wdl_bf16_tower_tracks_oracle(hip_lib, adam):
         assert abs(eng.loss() - fw["loss"]) < 5e-3
         assert abs(R.auc(b["label"], eng.score[:1536].cpu().numpy()) - R.auc(b["label"], fw["p"])) < 2e-3
     assert worst < 3e-2, worst
+
+
+@pytest.mark.parametrize("name,adam", [("deepfm_pipeline", "lazy"), ("deepfm_pipeline", "dense"),
+                                       ("deepfm_multi_cate", "lazy"), ("wdl", "lazy")])
+def test_prefetch_matches_inline_index(hip_lib, name, adam):
+    """train_step(next_batch=...) stages and indexes the next batch into the other buffer
+    set on the side stream during the current step: results are bit-identical to building
+    each index at the start of its own step (graph and eager replays, a predict between)."""
+    kw = CASES[name]
+    model = _model(name)
+    spec = ModelSpec(model, **kw)
+    bs = _batches(name, kw, 256, 7, seed=3)
+    runs = []
+    for pf in (False, True):
+        eng = CTREngine(spec, max_batch=256, seed=9, adam=adam, **({} if adam == "lazy" else {"bwd": "sorted"}))
+        zs = []
+        for i, b in enumerate(bs[:6]):
+            nxt = bs[i + 1] if pf and i != 3 else None      # step 3: no prefetch, step 4 indexes inline
+            eng.train_step(b, graph=i >= 2, next_batch=nxt)
+            torch.cuda.synchronize()
+            zs.append(eng.z[:256].cpu().numpy().copy())
+            if i == 4:
+                zs.append(eng.predict(bs[6]))
+        p = eng.params()
+        runs.append((zs, p))
+    # wdl's wide-weight gradients are scattered with float atomics (order-dependent in the
+    # last bit), so that model is held to 1e-6 instead of bit equality
+    eq = (lambda a, b, **k: np.testing.assert_allclose(a, b, atol=1e-6, rtol=0, **k)) if model == "wdl" \
+        else np.testing.assert_array_equal
+    for a, b in zip(runs[0][0], runs[1][0]):
+        eq(a, b)
+    for k in runs[0][1]:
+        eq(runs[0][1][k], runs[1][1][k], err_msg=k)
