@@ -142,6 +142,8 @@ def main():
                     help="c2 DeepFM (the headline, default); c3 deepfm_multi_cate 6 multi-hot slots x 60; "
                          "c5 Wide&Deep with the bf16 tower (single GPU)")
     ap.add_argument("--no-graph", action="store_true", help="eager launches instead of hipGraph replay")
+    ap.add_argument("--owner-update", default=None, choices=["sort", "chain"],
+                    help="sharded owners: group arriving rows by a sort (default) or by arrival chains")
     ap.add_argument("--no-prefetch", action="store_true",
                     help="build each batch's index at the start of its own step (default: during the "
                          "previous step, on a second hardware queue)")
@@ -207,7 +209,7 @@ def main():
         eng = CTREngine(spec, max_batch=B, seed=2019, adam=args.adam)
     else:
         from deep_learning_amd.shard import Exchange, ShardedCTREngine
-        eng = ShardedCTREngine(spec, B, Exchange(), seed=2019, adam=args.adam)
+        eng = ShardedCTREngine(spec, B, Exchange(), seed=2019, adam=args.adam, owner_update=args.owner_update)
         eng.init_device(2019)
     nb = 4
     dev_batches = []

@@ -25,6 +25,7 @@
 // p and w1 share the first 128-B line: the forward's useful bytes sit together,
 // and one record is two lines for E = 16.
 #include "common.h"
+#include <climits>
 #include "segment.h"
 
 namespace dl {
@@ -365,6 +366,89 @@ __global__ __launch_bounds__(256) void rec_apply_segments_kernel(float* __restri
   }
 }
 
+// Owner-side arrivals without a sort.  Each sender's ids are unique, so a row arrives at
+// most once per sender.  link: head[row] <- position (atomic exchange), next[pos] <- the
+// previous head: a per-row chain of its arrivals.  apply: the group whose position is the
+// row's head is its leader; it sums the chain's gradients in ascending position order
+// (selection over the short chain — the same order as a stable sort by row, so the result
+// does not depend on which arrival won the exchange), steps the record and resets head.
+constexpr int kMaxChain = 64;
+
+__global__ __launch_bounds__(256) void rec_chain_link_kernel(const int32_t* __restrict__ ids, long long n,
+                                                             int32_t* __restrict__ head, int32_t* __restrict__ next) {
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x)
+    next[i] = atomicExch(head + ids[i], (int32_t)i);
+}
+
+template <int E>
+__global__ __launch_bounds__(256) void rec_apply_chain_kernel(float* __restrict__ rec, RecCfg c,
+                                                              const int32_t* __restrict__ ids, long long n,
+                                                              int32_t* __restrict__ head,
+                                                              const int32_t* __restrict__ next,
+                                                              const float* __restrict__ g,
+                                                              const float* __restrict__ g1,
+                                                              const float* __restrict__ hist,
+                                                              const float* __restrict__ opt) {
+  rec_load_hyper(c, opt);
+  constexpr int LPR = E / 4;
+  const long long gt = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  const int q = (int)(gt % LPR);
+  const int t = (int)opt[7];
+  const float alpha = opt[3];
+  const bool first = c.has_first && q == 0;
+  for (long long i = gt / LPR; i < n; i += (long long)gridDim.x * blockDim.x / LPR) {
+    const long long row = ids[i];
+    if (head[row] != (int32_t)i) continue;   // not the leader of this row's arrivals
+    float* r = rec + row * c.ld;
+    float4 p = *reinterpret_cast<const float4*>(r + 4 * q);
+    float4 m = *reinterpret_cast<const float4*>(r + E + 4 + 4 * q);
+    float4 v = *reinterpret_cast<const float4*>(r + 2 * E + 4 + 4 * q);
+    const float4 tail = *reinterpret_cast<const float4*>(r + E);
+    float w = tail.x, wm = tail.y, wv = tail.z;
+    float4 gs = make_float4(0.f, 0.f, 0.f, 0.f);
+    float g1s = 0.f;
+    if (next[i] < 0) {   // one arrival (the common case)
+      gs = *reinterpret_cast<const float4*>(g + i * E + 4 * q);
+      if (first) g1s = g1[i];
+    } else {
+      // chains hold at most one arrival per sender (< kMaxChain): the walks are bounded so a
+      // corrupted chain can never spin a wave forever
+      long long last = -1;
+      for (int sel = 0; sel < kMaxChain; ++sel) {
+        long long best = LLONG_MAX;
+        int hops = 0;
+        for (long long j = i; j >= 0 && j < n && hops < kMaxChain; j = next[j], ++hops)
+          if (j > last && j < best) best = j;
+        if (best == LLONG_MAX) break;
+        const float4 gk = *reinterpret_cast<const float4*>(g + best * E + 4 * q);
+        gs.x += gk.x; gs.y += gk.y; gs.z += gk.z; gs.w += gk.w;
+        if (first) g1s += g1[best];
+        last = best;
+      }
+    }
+    const int stamp = __float_as_int(tail.w);
+    if (stamp < t - 1) catch_up4(p, m, v, w, wm, wv, first, stamp, t - 1, hist, c);
+    adam_elem(p.x, m.x, v.x, gs.x, alpha, c.omb1, c.omb2, c.eps);
+    adam_elem(p.y, m.y, v.y, gs.y, alpha, c.omb1, c.omb2, c.eps);
+    adam_elem(p.z, m.z, v.z, gs.z, alpha, c.omb1, c.omb2, c.eps);
+    adam_elem(p.w, m.w, v.w, gs.w, alpha, c.omb1, c.omb2, c.eps);
+    *reinterpret_cast<float4*>(r + 4 * q) = p;
+    *reinterpret_cast<float4*>(r + E + 4 + 4 * q) = m;
+    *reinterpret_cast<float4*>(r + 2 * E + 4 + 4 * q) = v;
+    if (q == 0) {
+      if (first) adam_elem(w, wm, wv, g1s, alpha, c.omb1, c.omb2, c.eps);
+      *reinterpret_cast<float4*>(r + E) = make_float4(w, wm, wv, __int_as_float(t));
+    }
+  }
+}
+
+// head reset after the apply, as a separate pass: the leader test reads a stable head.
+__global__ __launch_bounds__(256) void rec_chain_reset_kernel(const int32_t* __restrict__ ids, long long n,
+                                                              int32_t* __restrict__ head) {
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x)
+    head[ids[i]] = -1;
+}
+
 __global__ void hist_record_kernel(const float* opt, float* hist, int mask) {
   hist[(int)opt[7] & mask] = opt[3];
 }
@@ -502,4 +586,29 @@ extern "C" int dl_rec_apply_segments(float* rec, int32_t rec_ld, int32_t emb_dim
                        hist, opt);
   });
   DL_RETURN_LAUNCH("dl_rec_apply_segments");
+}
+
+extern "C" int dl_rec_chain_link(const int32_t* ids, int64_t n, int32_t* head, int32_t* next, void* stream) {
+  DL_CHECK_ARG(ids && head && next && n >= 0, "bad args");
+  if (n == 0) return 0;
+  hipLaunchKernelGGL(rec_chain_link_kernel, dim3(grid_cap(n)), dim3(256), 0, as_stream(stream), ids, (long long)n,
+                     head, next);
+  DL_RETURN_LAUNCH("dl_rec_chain_link");
+}
+
+extern "C" int dl_rec_apply_chain(float* rec, int32_t rec_ld, int32_t emb_dim, int32_t has_first, const int32_t* ids,
+                                  int64_t n, int32_t* head, const int32_t* next, const float* g, const float* g1,
+                                  const float* hist, int32_t hist_len, const float* opt, void* stream) {
+  DL_CHECK_ARG(rec && ids && head && next && g && hist && opt, "NULL argument");
+  if (int rc = rec_check(emb_dim, rec_ld, hist_len)) return rc;
+  DL_CHECK_ARG(!has_first || g1, "g1 required with first-order weights");
+  if (n <= 0) return 0;
+  DL_DISPATCH_E(emb_dim, {
+    hipLaunchKernelGGL(rec_apply_chain_kernel<kE>, dim3(grid_cap(n * (kE / 4))), dim3(256), 0, as_stream(stream), rec,
+                       RecCfg{kE, rec_ld, has_first, hist_len - 1, 0.f, 0.f, 0.f}, ids, (long long)n, head, next, g,
+                       has_first ? g1 : nullptr, hist, opt);
+  });
+  hipLaunchKernelGGL(rec_chain_reset_kernel, dim3(grid_cap(n)), dim3(256), 0, as_stream(stream), ids, (long long)n,
+                     head);
+  DL_RETURN_LAUNCH("dl_rec_apply_chain");
 }

@@ -8,16 +8,22 @@ sample) are replicated on every rank.  Dense parameters are replicated.
 
 Step on every rank (local batch B, global batch B*world):
   1. index: sort/dedup this batch's row references; unique rows grouped by owner
-  2. all-to-all of the per-owner unique-row counts, then of the row ids
+  2. all-gather of the per-owner unique-row counts, all-to-all of the row ids
   3. owners gather the requested rows (E floats + first-order weight)
   4. all-to-all of the rows back; the forward expands them through the inverse map
-  5. MLP + head forward/backward on the local batch (loss scaled by 1/(B*world))
+  5. MLP + head forward, input gradients down to the embeddings
   6. per-unique-row gradient (deterministic segment sum), all-to-all to owners,
-     owner scatter-add (f32 atomics: a row may arrive from several peers)
+     overlapping the weight gradients
   7. one all-reduce (sum) of the dense gradients + replicated-row gradients
-  8. TF1 Adam: dense + replicated parameters identically everywhere, the shard
-     rows locally (dense semantics over the shard)
+  8. TF1 Adam: dense + replicated parameters identically everywhere; the shard rows
+     by their owners — row records with lazy-exact catch-up: each row's arrivals
+     (at most one per sender) summed in a fixed order and applied once
 The result equals single-GPU training on the concatenated global batch.
+
+Off the critical path, on a second (high-priority) stream: the owners' arrival
+chains and record update of a step, and — with train_step(next_batch=...) — the
+next batch's staging, index build and count all-gather, so a step starts at its
+id exchange with the counts already on the host.
 
 Collectives go through torch.distributed: backend "nccl" is RCCL (xGMI) and
 exchanges device tensors directly; backend "gloo" (CPU tests, and several ranks
@@ -135,7 +141,8 @@ class Exchange:
 class ShardedCTREngine(CTREngine):
     """CTREngine whose embedding tables are row-sharded across the ranks of `exch`."""
 
-    def __init__(self, spec, max_batch, exch, device="cuda", seed=2019, adam="dense", hist_len=4096):
+    def __init__(self, spec, max_batch, exch, device="cuda", seed=2019, adam="dense", hist_len=4096,
+                 owner_update=None):
         if spec.model not in ("deepfm_pipeline", "dnn_pipeline"):
             raise ValueError("sharded path supports deepfm_pipeline / dnn_pipeline")
         self.exch = exch
@@ -149,21 +156,29 @@ class ShardedCTREngine(CTREngine):
         z = lambda *sh, dt=torch.float32: torch.zeros(*sh, dtype=dt, device=dev)
         E = spec.E
         self.local_rows = local_rows
-        # side stream (own hardware queue): the owner sort and the record update of a step run
-        # there, the update overlapping the next step's index build and exchanges
+        # side stream (own hardware queue): the owner arrival chains and the record update of
+        # a step run there, the update overlapping the next step's start
         self.side = None
         self.apply_done = None
         # DLAMD_HOST_TIMING=1: host-side timestamps of the step's phases (diagnostics)
         self.host_marks = [] if os.environ.get("DLAMD_HOST_TIMING") else None
         self.opt_snap = z(2, 16)
         if self.lazy:
-            # shard rows as records (rec.hip).  Owners sort the ids they receive once per step
-            # (dl_sort_unique); the gradients come back in the same order, so each requested
-            # row's arrivals are summed in that fixed order and applied once
-            # (dl_rec_apply_segments) — deterministic, no dense gradient table, no atomics.
+            # shard rows as records (rec.hip).  Owners group the ids they receive by row (a sort,
+            # or per-row arrival chains); the gradients come back in the same positions, so each
+            # row's arrivals are summed in ascending position order and applied once —
+            # deterministic, no dense gradient table.
+            # owner_update: "sort" (dl_sort_unique + dl_rec_apply_segments) or "chain"
+            # (dl_rec_chain_link + dl_rec_apply_chain: no sort; bit-identical records)
+            self.owner_update = owner_update or os.environ.get("DLAMD_OWNER_UPDATE", "sort")
+            if self.owner_update not in ("sort", "chain"):
+                raise ValueError("owner_update must be 'sort' or 'chain'")
             self.mv_u = None
             self.own_cap = 0
             self.own_bits = max(1, int(self.rows_pad - 1).bit_length())
+            if self.owner_update == "chain":
+                # arrival chains (rec.hip dl_rec_chain_link): head per local row, -1 = no arrival
+                self.own_head = torch.full((self.rows_pad,), -1, dtype=torch.int32, device=self.dev)
         R = max(self.rep, 1)
         rp = _ru(R, 16)
         self.rep_t, self.rep_m, self.rep_v, self.rep_g = z(rp, E), z(rp, E), z(rp, E), z(rp, E)
@@ -195,16 +210,21 @@ class ShardedCTREngine(CTREngine):
             self.rep_touched[: self.rep] = 1
 
     def _owner_buffers(self, n):
-        """(Re)size the owner-side sort buffers for n received ids."""
+        """(Re)size the owner-side arrival-chain buffer for n received ids."""
         if n > self.own_cap:
             self._join_side()   # the previous step's update on the side stream still reads them
         if n <= self.own_cap:
             return
         cap = max(n, int(self.own_cap * 1.25), 1 << 16)
-        z = lambda *sh, dt=torch.int32: torch.zeros(*sh, dtype=dt, device=self.dev)
-        self.own_ws = z(_lib.lib().dl_index_workspace_bytes(cap), dt=torch.uint8)
-        self.own_keys, self.own_pos, self.own_uniq = z(cap), z(cap), z(cap)
-        self.own_off, self.own_n = z(cap + 1), z(4)
+        # empty, not zeros: a fill queued on the compute stream could land after the side
+        # stream has written them (the sort / the link write every entry later read)
+        e = lambda k, dt=torch.int32: torch.empty(k, dtype=dt, device=self.dev)
+        if self.owner_update == "chain":
+            self.own_next = e(cap)
+        else:
+            self.own_ws = e(_lib.lib().dl_index_workspace_bytes(cap), torch.uint8)
+            self.own_keys, self.own_pos, self.own_uniq = e(cap), e(cap), e(cap)
+            self.own_off, self.own_n = e(cap + 1), e(4)
         self.own_cap = cap
 
     # ------------------------------------------------------------ parameters
@@ -279,6 +299,18 @@ class ShardedCTREngine(CTREngine):
 
     def params(self):
         raise NotImplementedError("gather shards with gather_params()")
+
+    def _owner_apply_args(self, recv_ids, nrecv, gb, g1b, opt, stream):
+        """Entry point + arguments of the owners' record update (one per arriving row)."""
+        sp = self.spec
+        g1 = ptr(g1b) if sp.fm else None
+        if self.owner_update == "chain":
+            return ("dl_rec_apply_chain", ptr(self.rec), self.rec_ld, sp.E, int(sp.fm), ptr(recv_ids), nrecv,
+                    ptr(self.own_head), ptr(self.own_next), ptr(gb), g1, ptr(self.hist), self.hist_len, ptr(opt),
+                    stream)
+        return ("dl_rec_apply_segments", ptr(self.rec), self.rec_ld, sp.E, int(sp.fm), ptr(self.own_uniq),
+                ptr(self.own_off), ptr(self.own_n), nrecv, nrecv, ptr(self.own_pos), ptr(gb), g1, ptr(self.hist),
+                self.hist_len, ptr(opt), stream)
 
     def _mark(self, name):
         if self.host_marks is not None:
@@ -492,21 +524,25 @@ class ShardedCTREngine(CTREngine):
             call("dl_shard_gather", ptr(self.table), ptr(self.first), ptr(recv_ids), nrecv, E, ptr(out_v),
                  ptr(out_1) if self.first is not None else None, s)
         self._mark("gather")
-        sort_done = None
+        link_done = None
         if nrecv and lazy:
-            # group this step's arrivals by row once, for the update at the end of the step:
-            # on a side stream, hidden under the gather, the row exchange and the dense middle
+            # link this step's arrivals into per-row chains, for the update at the end of the
+            # step: on the side stream, after the previous update reset the chain heads
             # (launched after the gather, so the host queues the critical path first)
             self._owner_buffers(nrecv)
             self._side_stream().wait_event(ids_ready)   # only the received ids, not the gather queued since
             with torch.cuda.stream(self.side):
-                call("dl_sort_unique", ptr(recv_ids), nrecv, self.own_bits, ptr(self.own_ws), self.own_ws.numel(),
-                     ptr(self.own_keys), ptr(self.own_pos), ptr(self.own_uniq), ptr(self.own_off),
-                     ptr(self.own_n), None, _lib.stream_handle(self.side))
-                sort_done = torch.cuda.Event()
-                sort_done.record(self.side)
+                if self.owner_update == "chain":
+                    call("dl_rec_chain_link", ptr(recv_ids), nrecv, ptr(self.own_head), ptr(self.own_next),
+                         _lib.stream_handle(self.side))
+                else:
+                    call("dl_sort_unique", ptr(recv_ids), nrecv, self.own_bits, ptr(self.own_ws),
+                         self.own_ws.numel(), ptr(self.own_keys), ptr(self.own_pos), ptr(self.own_uniq),
+                         ptr(self.own_off), ptr(self.own_n), None, _lib.stream_handle(self.side))
+                link_done = torch.cuda.Event()
+                link_done.record(self.side)
             recv_ids.record_stream(self.side)
-        self._mark("sort")
+        self._mark("link")
         # 4. rows back, in unique-id order
         rep = self.rep
         ex.all_to_all(out_v[:nrecv], recv, send, out=self.rows_u[rep: rep + nsend])
@@ -587,14 +623,12 @@ class ShardedCTREngine(CTREngine):
                      ptr(self.rep_touched), self.rep_f.shape[0], 1, 0.0, 0, ptr(self.opt), None, s)
         if lazy:
             if nrecv and self.prof is not None:   # bench's per-kernel pass: timed on the compute stream
-                torch.cuda.current_stream().wait_event(sort_done)
-                self._c("adam_table", "dl_rec_apply_segments", ptr(self.rec), self.rec_ld, E, int(sp.fm),
-                        ptr(self.own_uniq), ptr(self.own_off), ptr(self.own_n), nrecv, nrecv, ptr(self.own_pos),
-                        ptr(gb), ptr(g1b) if sp.fm else None, ptr(self.hist), self.hist_len, ptr(self.opt), s)
+                torch.cuda.current_stream().wait_event(link_done)
+                self._c("adam_table", *self._owner_apply_args(recv_ids, nrecv, gb, g1b, self.opt, s))
             elif nrecv:
-                # on the side stream (after the owner sort queued there): overlaps the next step's
-                # index build and exchanges; that step's gather waits for it (apply_done).  The
-                # optimizer scalars are snapshotted — the next adam_begin advances them.
+                # on the side stream (after the chain link queued there): overlaps the next step's
+                # start; that step's gather waits for it (apply_done).  The optimizer scalars
+                # are snapshotted — the next adam_begin advances them.
                 if ex.staged:   # host-staged exchange: the gradients were copied in on this stream
                     self.side.wait_stream(torch.cuda.current_stream())
                 with torch.cuda.stream(self.side):
@@ -603,10 +637,7 @@ class ShardedCTREngine(CTREngine):
                     for w in (w_g, w_g1):
                         if w is not None:
                             w.wait()
-                    call("dl_rec_apply_segments", ptr(self.rec), self.rec_ld, E, int(sp.fm), ptr(self.own_uniq),
-                         ptr(self.own_off), ptr(self.own_n), nrecv, nrecv, ptr(self.own_pos), ptr(gb),
-                         ptr(g1b) if sp.fm else None, ptr(self.hist), self.hist_len, ptr(snap),
-                         _lib.stream_handle(self.side))
+                    call(*self._owner_apply_args(recv_ids, nrecv, gb, g1b, snap, _lib.stream_handle(self.side)))
                     self.apply_done = torch.cuda.Event()
                     self.apply_done.record(self.side)
                 gb.record_stream(self.side)

@@ -315,6 +315,14 @@ int dl_rec_bwd_adam(const dl_emb_layout* L, float* rec, int32_t rec_ld, int32_t 
                     const float* w_head, const float* fm_sum, const float* dx0, float* g_rep,
                     float* g1_rep, const float* hist, int32_t hist_len, const float* opt,
                     const dl_pool_desc* pool, void* stream);
+/* Sharded owners without a sort: link every received position into its row's arrival
+ * chain (head[local_rows] starts at -1; next[n]).  Then apply: one leader per row sums its
+ * arrivals g[pos][E], g1[pos] in ascending position order (as dl_rec_apply_segments over a
+ * stable sort), catches the record up and steps it; head is reset to -1 afterwards. */
+int dl_rec_chain_link(const int32_t* ids, int64_t n, int32_t* head, int32_t* next, void* stream);
+int dl_rec_apply_chain(float* rec, int32_t rec_ld, int32_t emb_dim, int32_t has_first, const int32_t* ids,
+                       int64_t n, int32_t* head, const int32_t* next, const float* g, const float* g1,
+                       const float* hist, int32_t hist_len, const float* opt, void* stream);
 /* Rows [row0, row0+n): step-t update with dense gradients g[n][E], g1[n] (zeroed after). */
 int dl_rec_apply_rows(float* rec, int32_t rec_ld, int32_t emb_dim, int32_t has_first, int64_t row0,
                       int64_t n, float* g, float* g1, const float* hist, int32_t hist_len,

@@ -2,7 +2,7 @@
 # sharded path: GPU tests (2 gloo ranks on one GPU) + parity subset, one-rank RCCL bench, trace.
 TAG=${1:-shc}
 cd "$GRAFT_REPO_ROOT"; OUT=gpurun_out/$TAG; mkdir -p $OUT; export TMPDIR=/tmp
-timeout -k 10 900 python -m pytest tests/test_shard.py tests/test_gpu_parity.py -m gpu -q -p no:cacheprovider -x -k "shard or sorted or lazy" > $OUT/pytest.log 2>&1
+timeout -k 10 900 python -m pytest tests/test_shard.py tests/test_gpu_parity.py tests/test_gpu_kernels.py -m gpu -q -p no:cacheprovider -x -k "shard or sorted or lazy or chain" > $OUT/pytest.log 2>&1
 rc=$?; echo "pytest rc=$rc"; tail -5 $OUT/pytest.log
 if [ $rc -ne 0 ]; then exit $rc; fi
 timeout -k 10 600 python bench.py --sharded --steps 20 --warmup 5 --no-cpu-baseline > $OUT/bench.json 2> $OUT/bench.err

@@ -131,14 +131,15 @@ def run_sim(rank, world, steps, Bl, out_dir):
     np.savez(os.path.join(out_dir, "rank%d.npz" % rank), **P)
 
 
-def run_gpu(rank, world, steps, Bl, out_dir, adam="dense", prefetch=False):
+def run_gpu(rank, world, steps, Bl, out_dir, adam="dense", prefetch=False, owner_update=None):
     from deep_learning_amd.engine import ModelSpec
     from deep_learning_amd.shard import Exchange, ShardedCTREngine
     torch.cuda.set_device(0)
     ex = Exchange()
     cfg = R.make_cfg("deepfm_pipeline", **KW)
     P = R.init_params(cfg, np.random.default_rng(42))
-    eng = ShardedCTREngine(ModelSpec("deepfm_pipeline", **KW), Bl, ex, adam=adam, hist_len=4)
+    eng = ShardedCTREngine(ModelSpec("deepfm_pipeline", **KW), Bl, ex, adam=adam, hist_len=4,
+                           owner_update=owner_update)
     eng.load_params(P)
     batches = [local(bg, rank, world) for bg in global_batches(Bl * world, steps)]
     for step, b in enumerate(batches):
@@ -163,6 +164,6 @@ if __name__ == "__main__":
         run_sim(rank, world, steps, Bl, out_dir)
     else:
         run_gpu(rank, world, steps, Bl, out_dir, adam="lazy" if mode.startswith("gpu_lazy") else "dense",
-                prefetch=mode.endswith("_pf"))
+                prefetch=mode.endswith("_pf"), owner_update="chain" if "_chain" in mode else None)
     dist.barrier()
     dist.destroy_process_group()

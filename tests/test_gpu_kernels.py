@@ -249,3 +249,48 @@ def test_sorted_backward_equals_atomic(hip_lib, model):
         outs.append(eng.params())
     for k in outs[0]:
         np.testing.assert_allclose(outs[0][k], outs[1][k], atol=2e-6, rtol=0, err_msg=k)
+
+
+def test_chain_apply_equals_sorted_segment_apply(hip_lib):
+    """Owner update of the sharded path: arrival chains (dl_rec_chain_link +
+    dl_rec_apply_chain) against the sort + segment form (dl_sort_unique +
+    dl_rec_apply_segments) on the same arrivals — 8 senders with unique ids each, so
+    rows arrive up to 8 times, some rows lagging several steps: records bit-identical,
+    chain heads back to -1."""
+    E, ld, rows, W, per, hist_len = 16, 64, 5000, 8, 900, 8
+    g = torch.Generator().manual_seed(5)
+    rec0 = torch.zeros(rows, ld)
+    rec0[:, :E + 3] = torch.randn(rows, E + 3, generator=g) * 0.1
+    rec0[:, E + 4: 3 * E + 4] = torch.rand(rows, 2 * E, generator=g) * 0.01
+    stamps = torch.randint(3, 10, (rows,), generator=g, dtype=torch.int32)
+    rec0.view(torch.int32)[:, E + 3] = stamps
+    ids = torch.cat([torch.randperm(rows, generator=g)[:per] for _ in range(W)]).to(torch.int32)
+    n = ids.numel()
+    gr = torch.randn(n, E, generator=g)
+    g1 = torch.randn(n, generator=g)
+    hist = torch.rand(hist_len, generator=g) * 1e-3
+    opt = torch.zeros(16)
+    opt[3], opt[4], opt[5], opt[6], opt[7] = 1e-3, 0.9, 0.999, 1e-8, 10   # alpha, b1, b2, eps, step
+    ids_d, gr_d, g1_d, hist_d, opt_d = ids.cuda(), gr.cuda(), g1.cuda(), hist.cuda(), opt.cuda()
+    # sort + segments
+    recA = rec0.clone().cuda()
+    z = lambda *sh: torch.zeros(*sh, dtype=torch.int32, device="cuda")
+    ws = torch.zeros(hip_lib.dl_index_workspace_bytes(n), dtype=torch.uint8, device="cuda")
+    keys, pos, uniq, off, nu = z(n), z(n), z(n), z(n + 1), z(4)
+    call("dl_sort_unique", ptr(ids_d), n, 13, ptr(ws), ws.numel(), ptr(keys), ptr(pos), ptr(uniq), ptr(off),
+         ptr(nu), None, _s())
+    call("dl_rec_apply_segments", ptr(recA), ld, E, 1, ptr(uniq), ptr(off), ptr(nu), n, n, ptr(pos), ptr(gr_d),
+         ptr(g1_d), ptr(hist_d), hist_len, ptr(opt_d), _s())
+    # chains
+    recB = rec0.clone().cuda()
+    head = torch.full((rows,), -1, dtype=torch.int32, device="cuda")
+    nxt = z(n)
+    call("dl_rec_chain_link", ptr(ids_d), n, ptr(head), ptr(nxt), _s())
+    call("dl_rec_apply_chain", ptr(recB), ld, E, 1, ptr(ids_d), n, ptr(head), ptr(nxt), ptr(gr_d), ptr(g1_d),
+         ptr(hist_d), hist_len, ptr(opt_d), _s())
+    torch.cuda.synchronize()
+    assert int(nu[0]) == len(np.unique(ids.numpy()))
+    np.testing.assert_array_equal(recB.cpu().numpy().view(np.int32), recA.cpu().numpy().view(np.int32))
+    assert bool((head == -1).all())
+    touched = np.unique(ids.numpy())
+    assert (recB.view(torch.int32)[:, E + 3].cpu().numpy()[touched] == 10).all()

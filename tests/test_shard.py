@@ -59,11 +59,11 @@ def test_shard_sim_gloo_equals_global_batch(tmp_path):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("mode", ["gpu", "gpu_lazy", "gpu_lazy_pf"])
+@pytest.mark.parametrize("mode", ["gpu", "gpu_lazy", "gpu_lazy_pf", "gpu_lazy_chain_pf"])
 def test_sharded_engine_two_ranks_equals_global_batch(tmp_path, mode):
     """gpu_lazy: shard rows as records with lazy-exact Adam and a 4-entry alpha ring
     (flushes inside the 5 steps); _pf: each step prefetches the next batch's index and
-    counts on the side stream."""
+    counts on the side stream; _chain: owners group arrivals by chains instead of a sort."""
     _launch(mode, tmp_path)
     P, zs = _oracle()
     for step in range(STEPS):
