@@ -38,7 +38,7 @@ def log(*a):
     print("[bench %s]" % time.strftime("%H:%M:%S"), *a, file=sys.stderr, flush=True)
 
 
-def kernel_work(spec, B, touched_rows, rows=None, uniq=None):
+def kernel_work(spec, B, touched_rows, rows=None, uniq=None, shard=None):
     """Algorithmic bytes / flops per launch."""
     E, S, C = spec.E, spec.S, spec.C
     N = rows if rows is not None else spec.n_rows
@@ -65,6 +65,20 @@ def kernel_work(spec, B, touched_rows, rows=None, uniq=None):
         w["embed_fwd"] = ("hbm", B * (2 * S * (E * 4 + 4) + S * 4 + S * E * 4))
         # fused backward + Adam: U records read + written, per ref: ref id + dx0/fm_sum row + dz
         w["embed_bwd"] = ("hbm", uniq * (2 * rec_b + 4 + 8) + B * 2 * S * (4 + E * 4 + 4))
+    if shard is not None:
+        # row-sharded engine (shard.py): this rank's batch needs U = nsend + nrep unique rows;
+        # as an owner it serves nrecv of them (gather) and updates nrecv arrivals (rec_apply)
+        nsend, nrep, nrecv = shard
+        rec_b = (3 * E + 4) * 4
+        w["rec_gather"] = ("hbm", nrecv * (rec_b + (E + 1) * 4 + 4))
+        w["embed_fwd"] = ("hbm", B * (2 * S * (E * 4 + 4) + S * 4 + S * E * 4))
+        # per-unique-row gradient from its sorted references: ref + dx0/fm_sum row + dz per
+        # reference, compact (E + 1)-float gradient row out
+        w["embed_bwd"] = ("hbm", B * 2 * S * (4 + E * 4 + 4) + (nsend + nrep) * ((E + 1) * 4 + 8))
+        # owner update: record read + written, gradient row + id in
+        w["rec_apply"] = ("hbm", nrecv * (2 * rec_b + (E + 1) * 4 + 4))
+        w.pop("adam_table", None)
+        w.pop("adam_first", None)
     H = spec.hidden[-1]
     w["head"] = ("hbm", B * (spec.fm_cols + H) * 4 * 2)
     return w
@@ -275,8 +289,10 @@ def main():
     # unique rows touched per step (sets how much of the gradient table Adam reads)
     ids = dev_batches[0]["cate_feats"]
     touched_rows = int(torch.unique(torch.cat([ids.reshape(-1) + spec.C, ids.reshape(-1)])).numel()) + spec.C
-    uniq = int(eng.idx_n[0].item()) if getattr(eng, "lazy", False) else None
-    work = kernel_work(spec, B, touched_rows, rows=getattr(eng, "local_rows", spec.n_rows), uniq=uniq)
+    shard_counts = getattr(eng, "last_counts", None) if sharded and getattr(eng, "lazy", False) else None
+    uniq = int(eng.idx_n[0].item()) if getattr(eng, "lazy", False) and not sharded else None
+    work = kernel_work(spec, B, touched_rows, rows=getattr(eng, "local_rows", spec.n_rows), uniq=uniq,
+                       shard=shard_counts)
     kernels = {}
     for label, ts in times.items():
         us = float(np.mean(ts))

@@ -502,6 +502,7 @@ class ShardedCTREngine(CTREngine):
         U = nsend + nrep
         recv = [cm[r][self.rank] for r in range(W)]
         nrecv = sum(recv)
+        self.last_counts = (nsend, nrep, nrecv)   # bench.py prices the per-kernel work with these
         self._mark("counts")
         recv_ids = ex.all_to_all(self.send_ids[:nsend], send, recv)
         self._mark("ids_a2a")
@@ -624,7 +625,7 @@ class ShardedCTREngine(CTREngine):
         if lazy:
             if nrecv and self.prof is not None:   # bench's per-kernel pass: timed on the compute stream
                 torch.cuda.current_stream().wait_event(link_done)
-                self._c("adam_table", *self._owner_apply_args(recv_ids, nrecv, gb, g1b, self.opt, s))
+                self._c("rec_apply", *self._owner_apply_args(recv_ids, nrecv, gb, g1b, self.opt, s))
             elif nrecv:
                 # on the side stream (after the chain link queued there): overlaps the next step's
                 # start; that step's gather waits for it (apply_done).  The optimizer scalars
