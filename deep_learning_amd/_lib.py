@@ -25,6 +25,7 @@ class EmbLayout(C.Structure):
         ("zero_row0", C.c_int32), ("x0_ld", C.c_int32), ("x0_cont_col", C.c_int32),
         ("x0_vec_col", C.c_int32), ("x0_cat_col", C.c_int32), ("x0_pool_col", C.c_int32),
         ("fm_ld", C.c_int32), ("dx0_ld", C.c_int32), ("dx0_cat_col", C.c_int32), ("multi_width", C.c_int32),
+        ("cont_rows_compact", C.c_int32),
     ]
 
 

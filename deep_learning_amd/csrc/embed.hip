@@ -115,8 +115,8 @@ __global__ __launch_bounds__(256) void embed_fwd_kernel(EmbArgs a) {
         }
       }
       for (int k = threadIdx.x; k < nb * Cf; k += blockDim.x) {
-        const int row = (int)(L.fm_cont_offset + k % Cf);
-        rows_s[k / Cf][k % Cf] = row_ok(row, L.zero_row0) ? row : -1;
+        const int64_t row = L.fm_cont_offset + k % Cf;   // compact: rows 0..C-1 of the gathered rows
+        rows_s[k / Cf][k % Cf] = row_ok(row, L.zero_row0) ? (L.cont_rows_compact ? k % Cf : (int)row) : -1;
       }
     }
     for (int k = threadIdx.x; k < nb * Cf; k += blockDim.x)
@@ -250,7 +250,7 @@ __global__ __launch_bounds__(256) void embed_bwd_kernel(EmbBwdArgs a) {
         if (p * RPI < Cf && f < Cf) {
           const int64_t row = L.fm_cont_offset + f;
           const float val = cb[f];
-          const float e = row_ok(row, L.zero_row0) ? a.table[row * E + d] * val : 0.f;
+          const float e = row_ok(row, L.zero_row0) ? a.table[(L.cont_rows_compact ? f : row) * E + d] * val : 0.f;
           gc[p] += val * dsec * (sd - e);
         }
       }
@@ -326,13 +326,16 @@ __global__ __launch_bounds__(256) void cont_reduce_kernel(dl_emb_layout L, const
   if (threadIdx.x == 0) {
     const float tot = part[0] + part[1] + part[2] + part[3];
     int64_t row;
+    // compact: the gradients of the C cont rows are a [C] buffer (the record/sharded paths)
     if (k < Cf * E) {
       row = L.fm_cont_offset + k / E;
       if (!row_ok(row, L.zero_row0)) return;
+      if (L.cont_rows_compact) row = k / E;
       g_table[row * E + (k % E)] += tot;
     } else {
       row = L.fm_cont_offset + (k - Cf * E);
       if (!row_ok(row, L.zero_row0)) return;
+      if (L.cont_rows_compact) row = k - Cf * E;
       g_first[row] += tot;
     }
     touched[row] = 1;

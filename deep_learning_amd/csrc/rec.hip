@@ -70,12 +70,14 @@ __device__ __forceinline__ void catch_up1(float& p, float& m, float& v, float& w
 
 // ---------------------------------------------------------------------------
 // Forward gather of the batch's rows, caught up to step opt[7] - lag:
-//   out[i] = p(row_i), out1[i] = w1(row_i),   row_i = i (i < n_rep), else uniq[i - n_rep]
+//   out[i] = p(row_i), out1[i] = w1(row_i),   row_i = rep_base + i (i < n_rep), else uniq[i - n_rep]
+// (rep_base = the layout's fm_cont_offset: the replicated FM cont-field rows)
 // Records are only read: the catch-up is recomputed (cheaply, in registers) by the
 // backward's update, which is the one that writes.  E/4 lanes per row, float4 each.
 template <int E>
 __global__ __launch_bounds__(256) void rec_gather_kernel(const float* __restrict__ rec, RecCfg c, int64_t n_rows,
-                                                         int n_rep, const uint32_t* __restrict__ uniq,
+                                                         int n_rep, int64_t rep_base,
+                                                         const uint32_t* __restrict__ uniq,
                                                          const int32_t* __restrict__ n_uniq, long long max_u,
                                                          int world, const float* __restrict__ hist,
                                                          const float* __restrict__ opt, int lag,
@@ -89,7 +91,7 @@ __global__ __launch_bounds__(256) void rec_gather_kernel(const float* __restrict
   const long long total = n_rep + (n_uniq ? (long long)clamp_uniq(n_uniq, max_u) : max_u);
   const int target = (int)opt[7] - lag;
   for (long long i = group0; i < total; i += ngroups) {
-    const int64_t row = i < n_rep ? i : decode_key(uniq[i - n_rep], world);
+    const int64_t row = i < n_rep ? rep_base + i : decode_key(uniq[i - n_rep], world);
     const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
     float4 p = z, m = z, v = z;
     float w = 0.f, wm = 0.f, wv = 0.f;
@@ -139,7 +141,8 @@ __device__ __forceinline__ void rec_update(float* __restrict__ r, int E, int d, 
 // touched flags.  The row's caught-up state comes from the gather's compact outputs
 // (p: rows_u, w1: rows_u1, m/v: mv), read in u order, so the record is only WRITTEN
 // here (one random 208-B store per row instead of a read-modify-write).
-// Replicated rows (row < n_rep, hit by every sample through the FM cont fields)
+// Replicated rows (fm_cont_offset <= row < fm_cont_offset + n_rep, hit by every sample
+// through the FM cont fields)
 // only deposit their cate-reference gradient into g_rep/g1_rep; dl_rec_apply_rows
 // updates them after the cont part is added.  E/4 lanes per row, float4 each.
 // Per (sample, pooled slot): the gradient every member row of the slot receives,
@@ -239,10 +242,11 @@ __global__ __launch_bounds__(256) void rec_bwd_adam_kernel(SegGradIn sg, float* 
     g.y = seg_row_grad(s.s.y, s.dsum.y, s.x.y, s.dsum.y != 0.f ? p.y : 0.f);
     g.z = seg_row_grad(s.s.z, s.dsum.z, s.x.z, s.dsum.z != 0.f ? p.z : 0.f);
     g.w = seg_row_grad(s.s.w, s.dsum.w, s.x.w, s.dsum.w != 0.f ? p.w : 0.f);
-    if (row < n_rep) {
-      float* gr = g_rep + row * E + 4 * q;
+    const int64_t rrow = row - L.fm_cont_offset;   // replicated rows: [fm_cont_offset, + n_rep)
+    if (rrow >= 0 && rrow < n_rep) {
+      float* gr = g_rep + rrow * E + 4 * q;
       gr[0] += g.x; gr[1] += g.y; gr[2] += g.z; gr[3] += g.w;
-      if (g1_rep && q == 0) g1_rep[row] += s.g1;
+      if (g1_rep && q == 0) g1_rep[rrow] += s.g1;
       continue;
     }
     adam_elem(p.x, m.x, v.x, g.x, alpha, c.omb1, c.omb2, c.eps);
@@ -491,7 +495,8 @@ extern "C" int dl_rec_gather(const dl_emb_layout* L, const float* rec, int32_t r
     const unsigned grid = grid_cap(total * (kE / 4));
     hipLaunchKernelGGL(rec_gather_kernel<kE>, dim3(grid), dim3(256), 0, as_stream(stream), rec,
                        RecCfg{kE, rec_ld, has_first, hist_len - 1, 0.f, 0.f, 0.f}, (int64_t)L->n_rows, n_rep,
-                       uniq_keys, n_uniq, (long long)max_uniq, world, hist, opt, lag, rows_u,
+                       n_rep ? (int64_t)L->fm_cont_offset : (int64_t)0, uniq_keys, n_uniq, (long long)max_uniq,
+                       world, hist, opt, lag, rows_u,
                        has_first ? rows_u1 : nullptr, mv_u);
   });
   DL_RETURN_LAUNCH("dl_rec_gather");

@@ -34,28 +34,49 @@ def _ru(x, m):
     return (x + m - 1) // m * m
 
 
+# Model families of the reference's pipeline-style model files:
+#   fm     FM first/second order feeds the head (deepfm_*), else the deep_res head (dnn_*)
+#   cont   dense features present; "first": FM cont rows 0..C-1, cate ids at +C
+#          (deepfm_pipeline.py:58-61,89); "last": FM cont rows at cate_index_size + j,
+#          ids unshifted (deepfm_multi.py:139); "deep": cont only in the deep input (dnn_*)
+#   multi  nonzero-mean-pooled multi-hot slots after the S singles
+FAMILIES = {
+    "deepfm_pipeline": dict(fm=True, cont="first", multi=False),     # models/deepfm_pipeline.py:76-191
+    "deepfm_cate": dict(fm=True, cont=None, multi=False),            # models/deepfm_cate.py:73-169
+    "deepfm_multi_cate": dict(fm=True, cont=None, multi=True),       # models/deepfm_multi_cate.py:113-240
+    "deepfm_multi": dict(fm=True, cont="last", multi=True),          # models/deepfm_multi.py:124-260
+    "dnn_pipeline": dict(fm=False, cont="deep", multi=False),        # models/dnn_pipeline.py:68-137
+    "dnn_cate": dict(fm=False, cont=None, multi=False),              # models/dnn_cate.py:62-131
+    "dnn_multi": dict(fm=False, cont="deep", multi=True),            # models/dnn_multi.py:70-167
+    "dnn_multi_cate": dict(fm=False, cont=None, multi=True),         # models/dnn_multi_cate.py:64-162
+    "wdl": dict(fm=False, cont="deep", multi=False),                 # models/wdl.py:123-285
+}
+
+
 class ModelSpec:
     """Shape/hyper-parameter description of one reference model.
 
-    model: 'deepfm_pipeline' | 'dnn_pipeline' | 'deepfm_multi_cate' | 'wdl'
+    model: a key of FAMILIES (the reference's pipeline-style model files + wdl)
     C cont fields, V vector size, S single cate fields, E embedding size,
     cate_index_size (reference `cate_feats_size`), hidden units, multi_ranges
-    [[start, end, name], ...] (multi-hot slots), Fw wide ids (wdl), lr, l2,
-    decay_steps/decay_rate (exponential_decay), Adam betas/eps.
+    [[start, end, name], ...] (multi-hot slots, relative to the multi block), Fw wide
+    ids (wdl), lr, l2, decay_steps/decay_rate (exponential_decay), Adam betas/eps.
     """
 
     def __init__(self, model, C=13, V=0, S=26, E=16, cate_index_size=1000, hidden=(400, 400, 400),
                  multi_ranges=(), Fw=0, lr=0.001, l2=1e-5, decay_steps=10000000, decay_rate=0.9,
                  beta1=0.9, beta2=0.999, eps=1e-8, logloss_eps=1e-7, tower="f32"):
-        if model not in ("deepfm_pipeline", "dnn_pipeline", "deepfm_multi_cate", "wdl"):
+        if model not in FAMILIES:
             raise ValueError("unsupported model %r" % model)
+        fam = FAMILIES[model]
         self.model = model
-        self.C = 0 if model == "deepfm_multi_cate" else C
+        self.cont_mode = fam["cont"]
+        self.C = C if fam["cont"] else 0          # cate algs have no cont_feats (data_loader.py:8)
         self.V = 0 if model == "wdl" else V
         self.S, self.E = S, E
         self.cate_index_size = cate_index_size
         self.hidden = list(hidden)
-        self.multi_ranges = [list(r) for r in multi_ranges]
+        self.multi_ranges = [list(r) for r in multi_ranges] if fam["multi"] else []
         self.Fw = Fw
         self.lr, self.l2 = lr, l2
         self.decay_steps, self.decay_rate = decay_steps, decay_rate
@@ -66,7 +87,22 @@ class ModelSpec:
 
     @property
     def fm(self):
-        return self.model in ("deepfm_pipeline", "deepfm_multi_cate")
+        return FAMILIES[self.model]["fm"]
+
+    @property
+    def fm_cont(self):
+        """The cont fields are FM fields (deepfm_pipeline, deepfm_multi)."""
+        return self.fm and self.cont_mode in ("first", "last") and self.C > 0
+
+    @property
+    def fm_cont_offset(self):
+        """Table row of FM cont field 0."""
+        return self.cate_index_size if self.cont_mode == "last" else 0
+
+    @property
+    def fm_cate_offset(self):
+        """Added to a cate id for its FM row (deepfm_pipeline.py:89); the deep row is the raw id."""
+        return self.C if self.cont_mode == "first" and self.fm else 0
 
     @property
     def M(self):
@@ -78,7 +114,9 @@ class ModelSpec:
 
     @property
     def n_rows(self):
-        return self.C + self.cate_index_size if self.model == "deepfm_pipeline" else self.cate_index_size
+        if self.fm_cont:      # deepfm_pipeline.py:77 / deepfm_multi.py:125: cate_index_size + C
+            return self.C + self.cate_index_size
+        return self.cate_index_size
 
     @property
     def deep_in(self):
@@ -86,11 +124,10 @@ class ModelSpec:
 
     @property
     def F(self):
-        if self.model == "deepfm_pipeline":
-            return self.C + self.S
-        if self.model == "deepfm_multi_cate":
-            return self.S + self.M
-        return 0
+        """FM fields: [cont (fm_cont) | single cate | pooled slots]."""
+        if not self.fm:
+            return 0
+        return (self.C if self.fm_cont else 0) + self.S + self.M
 
     @property
     def fm_cols(self):
@@ -101,18 +138,16 @@ class ModelSpec:
         return self.S + self.multi_width
 
     def x0_ref_rows(self):
-        """Reference row of W_0 for each internal x0 column < deep_in."""
+        """Reference row of W_0 for each internal x0 column < deep_in.  Every pipeline-style
+        model concatenates its deep input as [cont, vector, single cate, pooled]
+        (deepfm_pipeline.py:123, deepfm_multi.py:188, dnn_multi.py:106, deepfm_multi_cate.py:169,
+        wdl.py:179); absent parts are empty."""
         S, E, M, C, V = self.S, self.E, self.M, self.C, self.V
-        if self.model == "deepfm_multi_cate":       # ref x0 = [vector, single, pooled]
-            cat = np.arange(S * E) + V
-            pool = np.arange(M * E) + V + S * E
-            vec = np.arange(V)
-            return np.concatenate([cat, pool, vec])
-        # ref x0 = [cont, vector, cat]  (deepfm_pipeline.py:123, dnn_pipeline.py:82)
         cat = np.arange(S * E) + C + V
+        pool = np.arange(M * E) + C + V + S * E
         cont = np.arange(C)
         vec = np.arange(V) + C
-        return np.concatenate([cat, cont, vec])
+        return np.concatenate([cat, pool, cont, vec])
 
 
 class CTREngine:
@@ -156,7 +191,7 @@ class CTREngine:
             self.rec = z(rows_pad, self.rec_ld)
             self.hist_len = hist_len
             self.hist = z(hist_len)
-            self.n_rep = sp.C if sp.model == "deepfm_pipeline" else 0     # FM cont-field rows
+            self.n_rep = sp.C if sp.fm_cont else 0     # FM cont-field rows (replicated, hot)
             R = max(self.n_rep, 1)
             self.g_rep, self.g1_rep = z(_ru(R * E, 4)), z(_ru(R, 4))
             self.rep_touched = z(_ru(R, 16), dt=torch.uint8)
@@ -232,6 +267,7 @@ class CTREngine:
         self.layout = self._layout(B)
         self.bwd_blocks = _lib.lib().dl_embed_bwd_grid(C_ref(self.layout))
         self.cont_slab = z(max(1, self.bwd_blocks * sp.C * (E + 1)))
+        self.fm_pool_col = sp.F - M      # head column of the first pooled first-order output
         if M:
             self.slot_start = torch.tensor([r[0] for r in sp.multi_ranges], dtype=torch.int32, device=dev)
             self.slot_end = torch.tensor([r[1] for r in sp.multi_ranges], dtype=torch.int32, device=dev)
@@ -240,7 +276,7 @@ class CTREngine:
                 self.g_pool, self.g1_pool = z(B, M, E), z(B, M)
                 self.pool_desc = _lib.PoolDesc(
                     slot_start=self.slot_start.data_ptr(), slot_end=self.slot_end.data_ptr(), n_slots=M,
-                    fm_col=S, dx0_pool_col=S * E, x0=self.x0.data_ptr(), cnt_emb=self.cnt_emb.data_ptr(),
+                    fm_col=self.fm_pool_col, dx0_pool_col=S * E, x0=self.x0.data_ptr(), cnt_emb=self.cnt_emb.data_ptr(),
                     cnt_first=self.cnt_first.data_ptr(), g_pool=self.g_pool.data_ptr(),
                     g1_pool=self.g1_pool.data_ptr())
         # batch reference index (deterministic backward)
@@ -279,8 +315,8 @@ class CTREngine:
         sp = self.spec
         L = _lib.EmbLayout()
         L.n_rows = self.N
-        L.fm_cont_offset = 0
-        L.fm_cate_offset = sp.C if sp.model == "deepfm_pipeline" else 0   # deepfm_pipeline.py:89
+        L.fm_cont_offset = sp.fm_cont_offset                            # deepfm_multi.py:139
+        L.fm_cate_offset = sp.fm_cate_offset                            # deepfm_pipeline.py:89
         L.deep_cate_offset = 0                                          # :120 raw ids
         L.batch = B
         L.emb_dim = sp.E
@@ -288,7 +324,7 @@ class CTREngine:
         L.vector_size = sp.V
         L.cate_fields = sp.S
         L.cate_ld = sp.cate_ld
-        L.fm_cont = 1 if sp.model == "deepfm_pipeline" else 0
+        L.fm_cont = 1 if sp.fm_cont else 0
         L.use_fm = 1 if sp.fm else 0
         L.fm_extra = sp.M if sp.fm else 0
         L.zero_row0 = 0 if sp.model == "wdl" else 1                     # :83-86 (wdl.py:49: none)
@@ -301,6 +337,7 @@ class CTREngine:
         L.dx0_ld = self.dx_ld
         L.dx0_cat_col = 0
         L.multi_width = sp.multi_width if self.lazy else 0
+        L.cont_rows_compact = 1 if self.lazy else 0     # records: cont rows gathered first into rows_u
         return L
 
     # ------------------------------------------------------------------ params
@@ -524,7 +561,7 @@ class CTREngine:
         L.batch = B
         if sp.M and not self.lazy:  # pooled vectors must be in x0 before the FM second order reads them
             self._c("pool_fwd", "dl_pool_fwd", C_ref(L), ptr(self.table), ptr(self.first) if sp.fm else None,
-                 ptr(self.in_cate), sp.S, ptr(self.slot_start), ptr(self.slot_end), sp.M, sp.S,
+                 ptr(self.in_cate), sp.S, ptr(self.slot_start), ptr(self.slot_end), sp.M, self.fm_pool_col,
                  ptr(self.x0), ptr(self.fm_out), ptr(self.cnt_emb), ptr(self.cnt_first), ptr(self.err), s)
         if self.lazy:
             # rows of the batch (index built by _pre), caught up to the step being taken
@@ -535,7 +572,7 @@ class CTREngine:
             if sp.M:
                 self._c("pool_fwd", "dl_pool_fwd_indexed", C_ref(L), ptr(self.rows_u),
                         ptr(self.rows_u1) if sp.fm else None, ptr(self.idx_inv), self.n_rep, ptr(self.slot_start),
-                        ptr(self.slot_end), sp.M, sp.S, ptr(self.x0), ptr(self.fm_out), ptr(self.cnt_emb),
+                        ptr(self.slot_end), sp.M, self.fm_pool_col, ptr(self.x0), ptr(self.fm_out), ptr(self.cnt_emb),
                         ptr(self.cnt_first), s)
             self._c("embed_fwd", "dl_embed_fwd_indexed", C_ref(L), ptr(self.rows_u),
                     ptr(self.rows_u1) if sp.fm else None, ptr(self.idx_inv), self.n_rep, ptr(self.in_cont),
@@ -670,7 +707,7 @@ class CTREngine:
                         ptr(self.dz), ptr(self.w_head), ptr(self.fm_sum), ptr(self.cont_slab), self.bwd_blocks, s)
                 self._c("cont_reduce", "dl_embed_cont_reduce", C_ref(L), ptr(self.cont_slab), bwd_blocks,
                         ptr(self.g_rep), ptr(self.g1_rep), ptr(self.rep_touched), s)
-                self._c("adam_rep", "dl_rec_apply_rows", ptr(self.rec), self.rec_ld, E, int(sp.fm), 0, R,
+                self._c("adam_rep", "dl_rec_apply_rows", ptr(self.rec), self.rec_ld, E, int(sp.fm), sp.fm_cont_offset, R,
                         ptr(self.g_rep), ptr(self.g1_rep), ptr(self.hist), self.hist_len, ptr(self.opt), s)
         elif self.bwd == "sorted":
             self._c("embed_bwd", "dl_embed_bwd_sorted", C_ref(L), ptr(self.table), None, ptr(self.idx_uniq),
@@ -688,7 +725,7 @@ class CTREngine:
                     ptr(self.fmg), ptr(self.touched), s)
         if sp.M and not self.lazy:
             self._c("pool_bwd", "dl_pool_bwd", C_ref(L), ptr(self.in_cate), sp.S, ptr(self.slot_start), ptr(self.slot_end),
-                 sp.M, sp.S, ptr(self.x0), ptr(self.fm_sum), ptr(self.dz), ptr(self.w_head), ptr(self.dx0),
+                 sp.M, self.fm_pool_col, ptr(self.x0), ptr(self.fm_sum), ptr(self.dz), ptr(self.w_head), ptr(self.dx0),
                  sp.S * sp.E, ptr(self.cnt_emb), ptr(self.cnt_first), ptr(self.tg), ptr(self.fmg),
                  ptr(self.touched), s)
         H = sp.hidden[-1]

@@ -15,7 +15,9 @@ import time
 from .utils import data_loader as data_load
 from .utils import my_utils
 
-ALGS = ("deepfm_pipeline", "dnn_pipeline", "deepfm_multi_cate")
+# local_run.py:47-68 dispatch (dnn_tensorboard is listed there but has no module in the reference)
+ALGS = ("deepfm_pipeline", "deepfm_cate", "deepfm_multi_cate", "deepfm_multi", "dnn_cate", "dnn_pipeline",
+        "dnn_multi_cate", "dnn_multi")
 
 
 class ModelParams:

@@ -29,7 +29,9 @@ import time
 import numpy as np
 import torch
 
-from ..engine import CTREngine, ModelSpec, default_adam
+import inspect
+
+from ..engine import FAMILIES, CTREngine, ModelSpec, default_adam
 from ..metrics import roc_auc
 
 
@@ -39,10 +41,9 @@ def _spec_from_args(model, args):
               lr=float(args.learning_rate), l2=float(args.l2_reg),
               decay_steps=float(args.learning_rate_decay_steps), decay_rate=float(args.learning_rate_decay_rate),
               V=int(getattr(args, "vector_feats_size", 0)))
-    if model == "deepfm_multi_cate":
-        kw.update(S=int(args.cate_field_size), multi_ranges=[list(r) for r in args.multi_feats_range])
-    else:
-        kw.update(C=int(args.cont_field_size), S=int(args.cate_field_size))
+    kw.update(S=int(args.cate_field_size), C=int(getattr(args, "cont_field_size", 0) or 0))
+    if FAMILIES[model]["multi"]:   # slot ranges within the multi block (my_utils.feat_size)
+        kw.update(multi_ranges=[list(r) for r in args.multi_feats_range])
     return ModelSpec(model, **kw)
 
 
@@ -210,7 +211,8 @@ def export_model(eng, model_pb):
 def load_model(model_pb, max_batch=None):
     with open(os.path.join(model_pb, "signature.json")) as f:
         meta = json.load(f)
-    spec = ModelSpec(meta["model"], **{k: v for k, v in meta["spec"].items() if k != "model"})
+    keys = set(inspect.signature(ModelSpec.__init__).parameters) - {"self", "model"}
+    spec = ModelSpec(meta["model"], **{k: v for k, v in meta["spec"].items() if k in keys})
     eng = CTREngine(spec, max_batch=max_batch or meta["batch_size"], init="none", adam=default_adam(spec))
     d = np.load(os.path.join(model_pb, "variables.npz"), allow_pickle=False)
     eng.load_params({k: d[k] for k in d.files})

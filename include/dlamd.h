@@ -73,6 +73,12 @@ typedef struct dl_emb_layout {
   int32_t multi_width;      /* multi-hot id columns after the S singles that the batch
                                index also covers (record path of deepfm_multi_cate; 0 = none):
                                index refs per sample = (use_fm ? S : 0) + S + multi_width */
+  int32_t cont_rows_compact;/* 1: the FM cont-field rows are addressed as rows 0..C-1 of the
+                               row buffer handed over (the gathered rows of the record and
+                               sharded paths; their gradients in a [C] buffer), while which
+                               of them is the zero row is still decided on the table row
+                               fm_cont_offset + f (deepfm_multi.py:139 puts them after the
+                               cate ids; deepfm_pipeline.py:58-61 at the top)           */
 } dl_emb_layout;
 
 /* Embedding gather + FM first/second order + deep-input assembly (forward).
@@ -273,8 +279,8 @@ int dl_adam_rows(float* p, float* m, float* v, float* g, uint8_t* touched, int64
  * deepfm_pipeline.py:184-188 / dnn_pipeline.py:132-136 / wdl.py:277-285. */
 /* hist[step & (hist_len-1)] = alpha of the step dl_adam_begin_step just began. */
 int dl_adam_hist_record(const float* opt, float* hist, int32_t hist_len, void* stream);
-/* rows_u[i] = p(row_i) caught up to step opt[7]-lag (rows_u1[i] = w1), row_i = i
- * for i < n_rep (replicated rows) else the row of uniq_keys[i-n_rep] (batch index,
+/* rows_u[i] = p(row_i) caught up to step opt[7]-lag (rows_u1[i] = w1), row_i =
+ * L->fm_cont_offset + i for i < n_rep (the replicated FM cont-field rows) else the row of uniq_keys[i-n_rep] (batch index,
  * dl_index_build keys; n_uniq = NULL: max_uniq keys, e.g. an owner's received local
  * rows with world = 1).  Records are only read.  mv_u (may be NULL) receives the
  * caught-up moments [i][2E+4] = m(E) | v(E) | m1 v1 0 0 for dl_rec_bwd_adam.
@@ -287,8 +293,9 @@ int dl_rec_gather(const dl_emb_layout* L, const float* rec, int32_t rec_ld, int3
  * (as dl_embed_bwd_sorted) is applied with step opt[7]'s alpha to the caught-up
  * state of dl_rec_gather (rows_u, rows_u1, mv_u — full arrays, replicated rows
  * first; mv_u = NULL: the record is re-read and its catch-up replayed, using
- * hist), and the record is written with stamp = step.  Rows < n_rep instead add
- * their gradient into g_rep[row][E] / g1_rep[row] (finished by dl_rec_apply_rows). */
+ * hist), and the record is written with stamp = step.  The replicated rows
+ * (L->fm_cont_offset + j, j < n_rep) instead add their gradient into g_rep[j][E] /
+ * g1_rep[j] (finished by dl_rec_apply_rows with row0 = L->fm_cont_offset). */
 /* Multi-hot pooling state for dl_rec_bwd_adam (deepfm_multi_cate.py:71-111): slot ranges
  * within the multi block, the head column of the pooled first-order outputs, dx0's pooled
  * columns, the pooled x0 (L->x0_pool_col), the nonzero counts of dl_pool_fwd_indexed and

@@ -7,8 +7,13 @@ bench.py's cpu_baseline leg may import this module.
 
 Models restated:
   deepfm_pipeline   models/deepfm_pipeline.py:43-191
-  dnn_pipeline      models/dnn_pipeline.py:40-137
+  deepfm_cate       models/deepfm_cate.py:73-182
   deepfm_multi_cate models/deepfm_multi_cate.py:45-240
+  deepfm_multi      models/deepfm_multi.py:46-260
+  dnn_pipeline      models/dnn_pipeline.py:40-137
+  dnn_cate          models/dnn_cate.py:62-131
+  dnn_multi         models/dnn_multi.py:70-167
+  dnn_multi_cate    models/dnn_multi_cate.py:64-162
   wdl               models/wdl.py:43-285
 Optimizer: tf.train.AdamOptimizer (TF1 ApplyAdam, dense — see ledger item 6
 in SURVEY.md: the embedding gradient reaches the Variable through
@@ -36,20 +41,48 @@ class Cfg(dict):
             raise AttributeError(k)
 
 
+# fm: FM outputs feed the head (deep_fm_weight), else deep_res; cont: "first" = FM cont rows
+# 0..C-1 with cate ids at +C (deepfm_pipeline.py:58-61,89), "last" = FM cont rows at
+# cate_index_size + j (deepfm_multi.py:139), "deep" = cont only in the deep input, None = no
+# cont_feats (the cate algs of utils/data_loader.py:8); multi: nonzero-mean pooled slots.
+FAMILIES = {
+    "deepfm_pipeline": dict(fm=True, cont="first", multi=False),
+    "deepfm_cate": dict(fm=True, cont=None, multi=False),
+    "deepfm_multi_cate": dict(fm=True, cont=None, multi=True),
+    "deepfm_multi": dict(fm=True, cont="last", multi=True),
+    "dnn_pipeline": dict(fm=False, cont="deep", multi=False),
+    "dnn_cate": dict(fm=False, cont=None, multi=False),
+    "dnn_multi": dict(fm=False, cont="deep", multi=True),
+    "dnn_multi_cate": dict(fm=False, cont=None, multi=True),
+    "wdl": dict(fm=False, cont="deep", multi=False),
+}
+
+
 def make_cfg(model, **kw):
     c = Cfg(model=model, C=13, V=0, S=26, E=16, cate_index_size=1000, hidden=[32, 32],
             multi_ranges=[], Fw=0, lr=0.001, l2=1e-5, decay_steps=10000000, decay_rate=0.9,
             beta1=0.9, beta2=0.999, eps=1e-8, logloss_eps=1e-7)
     c.update(kw)
-    if model in ("deepfm_multi_cate",):
+    fam = FAMILIES[model]
+    if not fam["cont"]:
         c["C"] = 0
+    if not fam["multi"]:
+        c["multi_ranges"] = []
     return c
+
+
+def is_fm(cfg):
+    return FAMILIES[cfg.model]["fm"]
+
+
+def fm_cont(cfg):
+    return is_fm(cfg) and FAMILIES[cfg.model]["cont"] in ("first", "last") and cfg.C > 0
 
 
 def n_rows(cfg):
     """Embedding-table rows (index_max_size)."""
-    if cfg.model == "deepfm_pipeline":
-        return cfg.C + cfg.cate_index_size          # deepfm_pipeline.py:77
+    if fm_cont(cfg):
+        return cfg.C + cfg.cate_index_size          # deepfm_pipeline.py:77, deepfm_multi.py:125
     return cfg.cate_index_size                      # dnn_pipeline.py:69, deepfm_multi_cate.py:114, wdl.py:46
 
 
@@ -58,24 +91,20 @@ def multi_width(cfg):
 
 
 def deep_in(cfg):
-    M = len(cfg.multi_ranges)
-    if cfg.model == "deepfm_multi_cate":
-        return cfg.V + cfg.S * cfg.E + M * cfg.E    # deepfm_multi_cate.py:169-174
-    if cfg.model == "wdl":
-        return cfg.C + cfg.S * cfg.E                # wdl.py:179-186
-    return cfg.C + cfg.V + cfg.S * cfg.E            # deepfm_pipeline.py:123-127
+    # [cont, vector, single cate, pooled]: deepfm_pipeline.py:123, deepfm_multi.py:188,
+    # dnn_multi.py:106, deepfm_multi_cate.py:169-174, wdl.py:179-186 (V = 0)
+    return cfg.C + cfg.V + cfg.S * cfg.E + len(cfg.multi_ranges) * cfg.E
 
 
 def fm_fields(cfg):
-    if cfg.model == "deepfm_pipeline":
-        return cfg.C + cfg.S                        # deepfm_pipeline.py:92
-    if cfg.model == "deepfm_multi_cate":
-        return cfg.S + len(cfg.multi_ranges)        # deepfm_multi_cate.py:128
-    return 0
+    if not is_fm(cfg):
+        return 0
+    # deepfm_pipeline.py:92 (C + S), deepfm_multi.py:128 (C + S + M), deepfm_multi_cate.py:128 (S + M)
+    return (cfg.C if fm_cont(cfg) else 0) + cfg.S + len(cfg.multi_ranges)
 
 
 def head_in(cfg):
-    if cfg.model in ("deepfm_pipeline", "deepfm_multi_cate"):
+    if is_fm(cfg):
         return fm_fields(cfg) + cfg.E + cfg.hidden[-1]   # deepfm_pipeline.py:158
     return cfg.hidden[-1]
 
@@ -94,7 +123,7 @@ def init_params(cfg, rng):
         P["weight_mat"] = rng.uniform(-lim, lim, (N, E)).astype(F32)
     else:
         P["feats_emb"] = (rng.standard_normal((N, E)) * 0.01).astype(F32)   # deepfm_pipeline.py:78
-    if cfg.model in ("deepfm_pipeline", "deepfm_multi_cate"):
+    if is_fm(cfg):
         P["fm_first_order_emb"] = rng.uniform(0.0, 1.0, (N, 1)).astype(F32)  # :80
     fan = deep_in(cfg)
     dims = [fan] + list(H)
@@ -102,12 +131,12 @@ def init_params(cfg, rng):
         g = math.sqrt(2.0 / (dims[i] + dims[i + 1]))                         # :131,140
         P["deep_%d" % i] = (rng.standard_normal((dims[i], dims[i + 1])) * g).astype(F32)
         P["deep_bias_%d" % i] = (rng.standard_normal((1, dims[i + 1])) * g).astype(F32)
-    if cfg.model in ("deepfm_pipeline", "deepfm_multi_cate"):
+    if is_fm(cfg):
         F = head_in(cfg)
         g = math.sqrt(2.0 / (F + 1))                                         # :166
         P["deep_fm_weight"] = (rng.standard_normal((F, 1)) * g).astype(F32)
         P["deep_fm_bias"] = rng.standard_normal((1,)).astype(F32)            # :169
-    elif cfg.model == "dnn_pipeline":
+    elif cfg.model != "wdl":
         g = math.sqrt(2.0 / (H[-1] + 1))                                     # dnn_pipeline.py:114
         P["deep_res"] = (rng.standard_normal((H[-1], 1)) * g).astype(F32)
         P["deep_res_bias"] = (rng.standard_normal((1, 1)) * g).astype(F32)   # :117
@@ -140,6 +169,26 @@ def _nonzero_reduce_mean(emb):
     return out, cnt
 
 
+def _pool(cfg, V, w1, multi):
+    """Per slot: nonzero-mean pooled V rows (and first-order weights when w1 is given),
+    concatenated in range order (deepfm_multi_cate.py:80-108, dnn_multi.py:83-104)."""
+    B, E = multi.shape[0], cfg.E
+    pf, pv, c1, cV = [], [], [], []
+    for (a, b_, *_) in cfg.multi_ranges:
+        ids = multi[:, a:b_]
+        if w1 is not None:
+            f1, n1 = _nonzero_reduce_mean(w1[ids])                               # :89,95
+            pf.append(f1); c1.append(n1)
+        fv, nv = _nonzero_reduce_mean(V[ids])                                    # :92,96
+        pv.append(fv); cV.append(nv)
+    M = len(cfg.multi_ranges)
+    dtype = V.dtype
+    pooled = np.stack(pv, 1) if M else np.zeros((B, 0, E), dtype)
+    pooled_first = np.concatenate(pf, 1) if (M and w1 is not None) else np.zeros((B, 0), dtype)
+    return (pooled, pooled_first, np.concatenate(cV, 1) if M else None,
+            np.concatenate(c1, 1) if (M and w1 is not None) else None)
+
+
 def forward(cfg, P, batch, dtype=F32):
     """Returns dict with x0, hs (post-ReLU activations), feats (head input),
     z (logit), p (score) and model-specific intermediates."""
@@ -149,54 +198,34 @@ def forward(cfg, P, batch, dtype=F32):
     out = {}
     vec = batch.get("vector_feats")
     vec = np.zeros((B, 0), dtype) if vec is None else vec.astype(dtype)
-    if cfg.model == "deepfm_pipeline":
-        V = _zero_row0(P["feats_emb"].astype(dtype))
-        w1 = _zero_row0(P["fm_first_order_emb"].astype(dtype))[:, 0]
-        cont = batch["cont_feats"].astype(dtype)
-        cate = batch["cate_feats"].astype(np.int64)
-        idx = np.concatenate([np.tile(np.arange(C, dtype=np.int64), (B, 1)), cate + C], 1)  # :58-61,89-90
-        val = np.concatenate([cont, np.ones((B, S), dtype)], 1)                              # :62,91
-        first = w1[idx] * val                                                                # :95-97
-        e = V[idx] * val[:, :, None]                                                         # :102-104
-        s = e.sum(1)                                                                         # :105
-        second = (dtype(0.5) * (s * s - (e * e).sum(1))).astype(dtype)                       # :106-109
-        cat_emb = V[cate].reshape(B, S * E)                                                  # :120-121
-        x0 = np.concatenate([cont, vec, cat_emb], 1)                                         # :123
-        out.update(idx=idx, val=val, e=e, s=s, first=first, second=second)
-    elif cfg.model == "dnn_pipeline":
-        V = _zero_row0(P["feats_emb"].astype(dtype))                                         # dnn_pipeline.py:72
-        cont = batch["cont_feats"].astype(dtype)
-        cate = batch["cate_feats"].astype(np.int64)
-        x0 = np.concatenate([cont, vec, V[cate].reshape(B, S * E)], 1)                       # :78-83
-    elif cfg.model == "deepfm_multi_cate":
-        V = _zero_row0(P["feats_emb"].astype(dtype))                                         # deepfm_multi_cate.py:120
-        w1 = _zero_row0(P["fm_first_order_emb"].astype(dtype))                               # :122 ([N,1])
-        cate = batch["cate_feats"].astype(np.int64)
-        single, multi = cate[:, :S], cate[:, S:]                                             # :58-59
-        pf, pv, c1, cV = [], [], [], []
-        for (a, b_, *_) in cfg.multi_ranges:                                                 # :80-108
-            ids = multi[:, a:b_]
-            f1, n1 = _nonzero_reduce_mean(w1[ids])                                           # :89,95
-            fv, nv = _nonzero_reduce_mean(V[ids])                                            # :92,96
-            pf.append(f1); pv.append(fv); c1.append(n1); cV.append(nv)
-        M = len(cfg.multi_ranges)
-        pooled_first = np.concatenate(pf, 1) if M else np.zeros((B, 0), dtype)
-        pooled = np.stack(pv, 1) if M else np.zeros((B, 0, E), dtype)
-        first = np.concatenate([w1[single][:, :, 0], pooled_first], 1)                       # :132-136
-        e = np.concatenate([V[single], pooled], 1)                                           # :142-147
-        s = e.sum(1)
-        second = (dtype(0.5) * (s * s - (e * e).sum(1))).astype(dtype)                       # :149-153
-        x0 = np.concatenate([vec, V[single].reshape(B, S * E), pooled.reshape(B, M * E)], 1)  # :169-171
-        out.update(single=single, multi=multi, e=e, s=s, first=first, second=second,
-                   cnt_first=np.concatenate(c1, 1) if M else None,
-                   cnt_emb=np.concatenate(cV, 1) if M else None, pooled=pooled)
-    elif cfg.model == "wdl":
+    cont = batch["cont_feats"].astype(dtype) if C else np.zeros((B, 0), dtype)
+    cate = batch["cate_feats"].astype(np.int64)
+    if cfg.model == "wdl":
         V = P["weight_mat"].astype(dtype)                                                    # wdl.py:44 (no zero row)
-        cont = batch["cont_feats"].astype(dtype)
-        cate = batch["cate_feats"].astype(np.int64)
         x0 = np.concatenate([cont, V[cate].reshape(B, S * E)], 1)                            # wdl.py:132-133,179
     else:
-        raise ValueError(cfg.model)
+        V = _zero_row0(P["feats_emb"].astype(dtype))                                         # deepfm_pipeline.py:83-86
+        w1 = _zero_row0(P["fm_first_order_emb"].astype(dtype)) if is_fm(cfg) else None      # :85-86
+        single, multi = cate[:, :S], cate[:, S:]                                             # deepfm_multi.py:64-65
+        M = len(cfg.multi_ranges)
+        pooled, pooled_first, cnt_emb, cnt_first = _pool(cfg, V, w1, multi)
+        if is_fm(cfg):
+            fam = FAMILIES[cfg.model]["cont"]
+            Cf = C if fm_cont(cfg) else 0
+            cont_off = cfg.cate_index_size if fam == "last" else 0                          # deepfm_multi.py:139
+            cate_off = C if fam == "first" else 0                                            # deepfm_pipeline.py:89
+            # FM fields [cont (row cont_off + j, value cont) | single (row id + cate_off, value 1)]
+            idx = np.concatenate([np.tile(np.arange(Cf, dtype=np.int64) + cont_off, (B, 1)),
+                                  single + cate_off], 1)                                     # :58-61,89-90
+            val = np.concatenate([cont[:, :Cf], np.ones((B, S), dtype)], 1)                  # :62,91
+            first = np.concatenate([w1[idx][:, :, 0] * val, pooled_first], 1)               # :95-97; multi :132-136
+            e = np.concatenate([V[idx] * val[:, :, None], pooled], 1)                        # :102-104; multi :142-147
+            s = e.sum(1)                                                                     # :105
+            second = (dtype(0.5) * (s * s - (e * e).sum(1))).astype(dtype)                   # :106-109
+            out.update(idx=idx, val=val, e=e, s=s, first=first, second=second)
+        # deep input [cont, vector, single (raw ids: deepfm_pipeline.py:120), pooled]
+        x0 = np.concatenate([cont, vec, V[single].reshape(B, S * E), pooled.reshape(B, M * E)], 1)
+        out.update(single=single, multi=multi, pooled=pooled, cnt_emb=cnt_emb, cnt_first=cnt_first)
 
     h = x0
     hs = []
@@ -204,10 +233,10 @@ def forward(cfg, P, batch, dtype=F32):
         h = np.maximum(h @ P["deep_%d" % i].astype(dtype) + P["deep_bias_%d" % i].astype(dtype), 0).astype(dtype)
         hs.append(h)
 
-    if cfg.model in ("deepfm_pipeline", "deepfm_multi_cate"):
+    if is_fm(cfg):
         feats = np.concatenate([out["first"], out["second"], h], 1)                          # :157
         z = (feats @ P["deep_fm_weight"].astype(dtype))[:, 0] + P["deep_fm_bias"].astype(dtype)[0]  # :171
-    elif cfg.model == "dnn_pipeline":
+    elif cfg.model != "wdl":
         feats = h
         z = (h @ P["deep_res"].astype(dtype))[:, 0] + P["deep_res_bias"].astype(dtype)[0, 0]  # dnn_pipeline.py:119
     else:
@@ -233,9 +262,9 @@ def _reg_loss(cfg, P):
     if cfg.l2 <= 0:
         return 0.0
     sq = lambda a: 0.5 * float((a.astype(np.float64) ** 2).sum())   # tf.nn.l2_loss
-    if cfg.model in ("deepfm_pipeline", "deepfm_multi_cate"):
+    if is_fm(cfg):
         return cfg.l2 * sq(P["deep_fm_weight"])                     # deepfm_pipeline.py:183
-    if cfg.model == "dnn_pipeline":
+    if cfg.model != "wdl":
         return cfg.l2 * sq(P["deep_res"])                           # dnn_pipeline.py:131
     r = cfg.l2 * sq(P["wdl_weights"])                               # wdl.py:270-271
     for i in range(len(cfg.hidden)):
@@ -264,14 +293,14 @@ def backward(cfg, P, batch, fw, dtype=F32):
     l2 = dtype(cfg.l2)
     H = cfg.hidden
     h = fw["hs"][-1]
-    if cfg.model in ("deepfm_pipeline", "deepfm_multi_cate"):
+    if is_fm(cfg):
         W = P["deep_fm_weight"].astype(dtype)
         G["deep_fm_weight"] = (fw["feats"].T @ dz[:, None]).astype(dtype) + l2 * W
         G["deep_fm_bias"] = np.array([dz.sum()], dtype)
         dfeats = dz[:, None] * W[:, 0][None, :]
         nF = fm_fields(cfg)
         dfirst, dsec, dh = dfeats[:, :nF], dfeats[:, nF:nF + E], dfeats[:, nF + E:]
-    elif cfg.model == "dnn_pipeline":
+    elif cfg.model != "wdl":
         W = P["deep_res"].astype(dtype)
         G["deep_res"] = (h.T @ dz[:, None]).astype(dtype) + l2 * W
         G["deep_res_bias"] = np.array([[dz.sum()]], dtype)
@@ -297,51 +326,39 @@ def backward(cfg, P, batch, fw, dtype=F32):
         g = (dx * (xs[i] > 0)).astype(dtype) if i > 0 else dx
     dx0 = g
     # embedding backward
-    if cfg.model == "deepfm_pipeline":
-        tab, t1 = "feats_emb", "fm_first_order_emb"
-        idx, val, e, s = fw["idx"], fw["val"], fw["e"], fw["s"]
-        de = dsec[:, None, :] * (s[:, None, :] - e)                 # d second / d e_f
-        gV = (de * val[:, :, None]).reshape(-1, E)
-        np.add.at(G[tab], idx.reshape(-1), gV)
-        np.add.at(G[t1][:, 0], idx.reshape(-1), (dfirst * val).reshape(-1))
-        cate = batch["cate_feats"].astype(np.int64)
-        col = C + cfg.V
-        np.add.at(G[tab], cate.reshape(-1), dx0[:, col:col + S * E].reshape(-1, E))
-        G[tab][0] = 0                                              # concat zero-row: no grad to Var row 0
-        G[t1][0] = 0
-    elif cfg.model == "dnn_pipeline":
-        cate = batch["cate_feats"].astype(np.int64)
-        col = C + cfg.V
-        np.add.at(G["feats_emb"], cate.reshape(-1), dx0[:, col:col + S * E].reshape(-1, E))
-        G["feats_emb"][0] = 0
-    elif cfg.model == "deepfm_multi_cate":
-        tab, t1 = "feats_emb", "fm_first_order_emb"
-        single, multi = fw["single"], fw["multi"]
-        M = len(cfg.multi_ranges)
-        e, s = fw["e"], fw["s"]
-        de = dsec[:, None, :] * (s[:, None, :] - e)                # [B, S+M, E]
-        # single fields: FM second + deep
-        np.add.at(G[tab], single.reshape(-1), de[:, :S].reshape(-1, E))
-        np.add.at(G[t1][:, 0], single.reshape(-1), dfirst[:, :S].reshape(-1))
-        col = cfg.V
-        np.add.at(G[tab], single.reshape(-1), dx0[:, col:col + S * E].reshape(-1, E))
-        dpool = de[:, S:] + dx0[:, col + S * E: col + S * E + M * E].reshape(B, M, E)
-        dpool1 = dfirst[:, S:]
-        for m, (a, b_, *_) in enumerate(cfg.multi_ranges):
-            ids = multi[:, a:b_]
-            L = b_ - a
-            cV = fw["cnt_emb"][:, m]
-            c1 = fw["cnt_first"][:, m]
-            gV = np.where(cV[:, None] > 0, dpool[:, m] / np.where(cV > 0, cV, 1)[:, None], 0).astype(dtype)
-            g1 = np.where(c1 > 0, dpool1[:, m] / np.where(c1 > 0, c1, 1), 0).astype(dtype)
-            np.add.at(G[tab], ids.reshape(-1), np.repeat(gV, L, axis=0).reshape(-1, E))
-            np.add.at(G[t1][:, 0], ids.reshape(-1), np.repeat(g1, L))
-        G[tab][0] = 0
-        G[t1][0] = 0
-    else:  # wdl
+    if cfg.model == "wdl":
         cate = batch["cate_feats"].astype(np.int64)
         col = C
         np.add.at(G["weight_mat"], cate.reshape(-1), dx0[:, col:col + S * E].reshape(-1, E))
+        return G, dz
+    tab, t1 = "feats_emb", "fm_first_order_emb"
+    single, multi = fw["single"], fw["multi"]
+    M = len(cfg.multi_ranges)
+    col = C + cfg.V
+    dpool = dx0[:, col + S * E: col + S * E + M * E].reshape(B, M, E)
+    if is_fm(cfg):
+        idx, val, e, s = fw["idx"], fw["val"], fw["e"], fw["s"]
+        nI = idx.shape[1]                                          # cont + single FM fields
+        de = dsec[:, None, :] * (s[:, None, :] - e)                # d second / d e_f
+        gV = (de[:, :nI] * val[:, :, None]).reshape(-1, E)
+        np.add.at(G[tab], idx.reshape(-1), gV)
+        np.add.at(G[t1][:, 0], idx.reshape(-1), (dfirst[:, :nI] * val).reshape(-1))
+        dpool = de[:, nI:] + dpool
+        dpool1 = dfirst[:, nI:]
+    np.add.at(G[tab], single.reshape(-1), dx0[:, col:col + S * E].reshape(-1, E))   # deep lookups (raw ids)
+    for m, (a, b_, *_) in enumerate(cfg.multi_ranges):         # div_no_nan gradient to every member
+        ids = multi[:, a:b_]
+        L = b_ - a
+        cV = fw["cnt_emb"][:, m]
+        gV = np.where(cV[:, None] > 0, dpool[:, m] / np.where(cV > 0, cV, 1)[:, None], 0).astype(dtype)
+        np.add.at(G[tab], ids.reshape(-1), np.repeat(gV, L, axis=0).reshape(-1, E))
+        if is_fm(cfg):
+            c1 = fw["cnt_first"][:, m]
+            g1 = np.where(c1 > 0, dpool1[:, m] / np.where(c1 > 0, c1, 1), 0).astype(dtype)
+            np.add.at(G[t1][:, 0], ids.reshape(-1), np.repeat(g1, L))
+    G[tab][0] = 0                                                  # concat zero-row: no grad to Var row 0
+    if is_fm(cfg):
+        G[t1][0] = 0
     return G, dz
 
 

@@ -83,6 +83,54 @@ def test_local_run_train_and_pred_end_to_end(hip_lib, tmp_path):
     assert abs(auc_oracle - auc_gpu) < 1e-4
 
 
+@pytest.mark.parametrize("alg", ["deepfm_multi", "dnn_multi_cate", "deepfm_cate", "dnn_multi"])
+def test_local_run_family_models_end_to_end(hip_lib, tmp_path, alg):
+    """local_run.py dispatch of the other pipeline-style models (local_run.py:47-62): a conf with
+    two multi-hot `arr` columns (feat_size -> multi ranges for the pool algs, plain cate columns
+    otherwise), TFRecord parts, train -> export -> pred, exported scores vs the oracle forward."""
+    from deep_learning_amd.synthetic import make_batch
+    from deep_learning_amd.utils import data_loader, my_utils
+    from oracle import ctr_ref as R
+    conf, tr, pr = tmp_path / "conf", tmp_path / "train", tmp_path / "pred"
+    for p in (conf, tr, pr):
+        p.mkdir()
+    lines = ["f%d\tx\tfloat" % i for i in range(5)] + ["c%d\tx\tstring" % i for i in range(8)]
+    lines += ["tags\tx\tarr\tx\tx\tx\tx\tk=12\ttags", "kw\tx\tarr\tx\tx\tx\tx\tk=7\tkw"]
+    with open(str(conf / "dnn.conf"), "w") as f:
+        f.write("\n".join(lines) + "\n")
+    C, S, Mw = 5, 8, 19
+    fs = my_utils.feat_size(str(conf), alg)
+    cate_alg = alg in data_loader.CATE_ALGS
+    V = 2000
+    rng = np.random.default_rng(5)
+
+    def part(n, seed):
+        b = make_batch(n, cont=0 if cate_alg else C, cate_fields=S, cate_index_size=V, seed=seed,
+                       cate_only=cate_alg)
+        multi = rng.integers(1, V, size=(n, Mw))
+        multi[rng.random((n, Mw)) < 0.5] = 0
+        b["cate_feats"] = np.concatenate([b["cate_feats"], multi], 1)
+        return b
+    for i in range(3):
+        data_loader.write_tfrecord_part(str(tr / ("part-%d" % i)), part(256, i))
+    pred_part = part(200, 99)
+    data_loader.write_tfrecord_part(str(pr / "part-0"), pred_part)
+    args = [alg, "train", "1", "8", str(V), "3", str(conf), str(tr) + "/", str(pr) + "/",
+            str(tmp_path / "model_pb"), str(tmp_path / "ckpt"), "0", str(tmp_path / "ckpt"),
+            "batch_size=64", "hidden_units=32,16", "shuffle=0"]
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "local_run.py")] + args, capture_output=True,
+                       text=True, timeout=900, cwd=ROOT)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-3000:]
+    auc_gpu = float(r.stdout.split("val of auc:")[-1].split()[0])
+    d = np.load(tmp_path / "model_pb" / "variables.npz")
+    P = {k: d[k] for k in d.files}
+    cfg = R.make_cfg(alg, C=fs[0], V=fs[1], S=fs[2], E=8, cate_index_size=V, hidden=[32, 16],
+                     multi_ranges=fs[5])
+    b = {k: v[:192] for k, v in pred_part.items()}
+    fw = R.forward(cfg, P, b)
+    assert abs(R.auc(b["label"], fw["p"]) - auc_gpu) < 1e-4
+
+
 def test_wdl_load_style_fit_evaluate_predict(hip_lib, tmp_path):
     from deep_learning_amd.models import wdl
     from deep_learning_amd.synthetic import make_batch
