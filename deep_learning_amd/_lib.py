@@ -71,6 +71,7 @@ SIGNATURES = {
     "dl_slab_fold_rows": (I32, [P, I32, I32, I32, I32, P, I64, P, P]),
     "dl_adam_begin_step": (I32, [P, F, F, P]),
     "dl_adam_dense": (I32, [P, P, P, P, I32, I64, I64, F, I64, P, P, P, P]),
+    "dl_adam_dense_reg": (I32, [P, P, P, P, I32, I64, I64, F, I64, I32, P, P, P, P]),
     "dl_adam_rows": (I32, [P, P, P, P, P, I64, I32, F, I32, P, P, P]),
     "dl_init_random": (I32, [P, I64, I32, F, F, U64, U64, P]),
     "dl_transpose_f32": (I32, [P, I32, I32, I32, P, I32, P]),

@@ -27,6 +27,9 @@ __global__ void adam_begin_kernel(float* opt, float decay_rate, float decay_step
 
 
 // Dense parameter, gradient = sum of partial slabs (+ l2 * p for i < l2_count).
+// REG: 0 = L2 (g += l2 * p, sq_out += p^2: tf.contrib.layers.l2_regularizer), 1 = L1
+// (g += l1 * sign(p), sq_out += |p|: l1_regularizer, models/dnn.py:88-90).
+template <int REG>
 __global__ __launch_bounds__(256) void adam_dense_thread_kernel(float* __restrict__ p, float* __restrict__ m,
                                                                 float* __restrict__ v,
                                                                 const float* __restrict__ slab, int nslab,
@@ -47,7 +50,10 @@ __global__ __launch_bounds__(256) void adam_dense_thread_kernel(float* __restric
     for (; s < nslab; ++s) g += slab[s * stride + i];
     float pi = p[i], mi = m[i], vi = v[i];
     if (p_prev) p_prev[i] = pi;
-    if (i < l2_count) { g += l2 * pi; sq += pi * pi; }
+    if (i < l2_count) {
+      if (REG == 0) { g += l2 * pi; sq += pi * pi; }
+      else { g += l2 * (pi > 0.f ? 1.f : pi < 0.f ? -1.f : 0.f); sq += fabsf(pi); }
+    }
     adam_elem(pi, mi, vi, g, alpha, omb1, omb2, eps);
     p[i] = pi; m[i] = mi; v[i] = vi;
   }
@@ -58,6 +64,7 @@ __global__ __launch_bounds__(256) void adam_dense_thread_kernel(float* __restric
 }
 
 // Few elements, many slabs (head weights): one wave per element.
+template <int REG>
 __global__ __launch_bounds__(256) void adam_dense_wave_kernel(float* __restrict__ p, float* __restrict__ m,
                                                               float* __restrict__ v,
                                                               const float* __restrict__ slab, int nslab,
@@ -74,8 +81,13 @@ __global__ __launch_bounds__(256) void adam_dense_wave_kernel(float* __restrict_
     float pi = p[i], mi = m[i], vi = v[i];
     if (p_prev) p_prev[i] = pi;
     if (i < l2_count) {
-      g += l2 * pi;
-      if (sq_out) atomicAdd(sq_out, pi * pi);
+      if (REG == 0) {
+        g += l2 * pi;
+        if (sq_out) atomicAdd(sq_out, pi * pi);
+      } else {
+        g += l2 * (pi > 0.f ? 1.f : pi < 0.f ? -1.f : 0.f);
+        if (sq_out) atomicAdd(sq_out, fabsf(pi));
+      }
     }
     adam_elem(pi, mi, vi, g, opt[3], 1.f - opt[4], 1.f - opt[5], opt[6]);
     p[i] = pi; m[i] = mi; v[i] = vi;
@@ -225,21 +237,33 @@ extern "C" int dl_adam_begin_step(float* opt, float decay_rate, float decay_step
   DL_RETURN_LAUNCH("dl_adam_begin_step");
 }
 
+extern "C" int dl_adam_dense_reg(float* p, float* m, float* v, const float* slab, int32_t nslab,
+                                 int64_t slab_stride, int64_t n, float reg, int64_t reg_count, int32_t reg_kind,
+                                 const float* opt, float* p_prev, float* acc_out, void* stream) {
+  DL_CHECK_ARG(p && m && v && slab && opt, "NULL pointer");
+  DL_CHECK_ARG(nslab >= 1 && slab_stride >= n, "bad slabs");
+  DL_CHECK_ARG(reg_kind == 0 || reg_kind == 1, "reg_kind must be 0 (L2) or 1 (L1)");
+  if (n == 0) return 0;
+#define DL_ADAM_DENSE(R)                                                                                      \
+  if (n < 16384 && nslab >= 32) {                                                                             \
+    const long long blocks = (n * 64 + 255) / 256;                                                            \
+    hipLaunchKernelGGL(adam_dense_wave_kernel<R>, dim3((unsigned)blocks), dim3(256), 0, as_stream(stream), p, \
+                       m, v, slab, nslab, (long long)slab_stride, (long long)n, reg, (long long)reg_count, opt, \
+                       p_prev, acc_out);                                                                      \
+  } else {                                                                                                    \
+    hipLaunchKernelGGL(adam_dense_thread_kernel<R>, dim3(grid_for(n)), dim3(256), 0, as_stream(stream), p, m, \
+                       v, slab, nslab, (long long)slab_stride, (long long)n, reg, (long long)reg_count, opt,    \
+                       p_prev, acc_out);                                                                      \
+  }
+  if (reg_kind == 0) { DL_ADAM_DENSE(0) } else { DL_ADAM_DENSE(1) }
+#undef DL_ADAM_DENSE
+  DL_RETURN_LAUNCH("dl_adam_dense_reg");
+}
+
 extern "C" int dl_adam_dense(float* p, float* m, float* v, const float* slab, int32_t nslab,
                              int64_t slab_stride, int64_t n, float l2, int64_t l2_count,
                              const float* opt, float* p_prev, float* sq_out, void* stream) {
-  DL_CHECK_ARG(p && m && v && slab && opt, "NULL pointer");
-  DL_CHECK_ARG(nslab >= 1 && slab_stride >= n, "bad slabs");
-  if (n == 0) return 0;
-  if (n < 16384 && nslab >= 32) {
-    const long long blocks = (n * 64 + 255) / 256;
-    hipLaunchKernelGGL(adam_dense_wave_kernel, dim3((unsigned)blocks), dim3(256), 0, as_stream(stream), p, m,
-                       v, slab, nslab, (long long)slab_stride, (long long)n, l2, (long long)l2_count, opt, p_prev, sq_out);
-  } else {
-    hipLaunchKernelGGL(adam_dense_thread_kernel, dim3(grid_for(n)), dim3(256), 0, as_stream(stream), p, m,
-                       v, slab, nslab, (long long)slab_stride, (long long)n, l2, (long long)l2_count, opt, p_prev, sq_out);
-  }
-  DL_RETURN_LAUNCH("dl_adam_dense");
+  return dl_adam_dense_reg(p, m, v, slab, nslab, slab_stride, n, l2, l2_count, 0, opt, p_prev, sq_out, stream);
 }
 
 extern "C" int dl_adam_rows(float* p, float* m, float* v, float* g, uint8_t* touched, int64_t n_rows,

@@ -50,6 +50,11 @@ FAMILIES = {
     "dnn_multi": dict(fm=False, cont="deep", multi=True),            # models/dnn_multi.py:70-167
     "dnn_multi_cate": dict(fm=False, cont=None, multi=True),         # models/dnn_multi_cate.py:64-162
     "wdl": dict(fm=False, cont="deep", multi=False),                 # models/wdl.py:123-285
+    # load-style models (int32 ids, no zero row):
+    #   deepfm: FM fields [cate | cont] with cont rows at cate_field_size + j (deepfm.py:66-73)
+    #   dnn:    xavier 'weight_mat' table, L1 on every hidden weight (dnn.py:49-52,88-90)
+    "deepfm": dict(fm=True, cont="field", multi=False),              # models/deepfm.py:39-162
+    "dnn": dict(fm=False, cont="deep", multi=False),                 # models/dnn.py:35-96
 }
 
 
@@ -91,13 +96,53 @@ class ModelSpec:
 
     @property
     def fm_cont(self):
-        """The cont fields are FM fields (deepfm_pipeline, deepfm_multi)."""
-        return self.fm and self.cont_mode in ("first", "last") and self.C > 0
+        """The cont fields are FM fields (deepfm_pipeline, deepfm_multi, deepfm)."""
+        return self.fm and self.cont_mode in ("first", "last", "field") and self.C > 0
 
     @property
     def fm_cont_offset(self):
         """Table row of FM cont field 0."""
-        return self.cate_index_size if self.cont_mode == "last" else 0
+        return {"last": self.cate_index_size, "field": self.S}.get(self.cont_mode, 0)
+
+    @property
+    def zero_row0(self):
+        """Row 0 is forced to zeros every step (deepfm_pipeline.py:83-86); wdl.py:44,
+        deepfm.py:58-60 and dnn.py:49-52 have no zero row."""
+        return self.model not in ("wdl", "deepfm", "dnn")
+
+    @property
+    def xavier_table(self):
+        """glorot-uniform table named weight_mat (wdl.py:44-47, dnn.py:49-52)."""
+        return self.model in ("wdl", "dnn")
+
+    @property
+    def table_key(self):
+        return "weight_mat" if self.xavier_table else "feats_emb"
+
+    @property
+    def first_key(self):
+        return "feats" if self.model == "deepfm" else "fm_first_order_emb"   # deepfm.py:60
+
+    @property
+    def hidden_reg(self):
+        """Regulariser on the hidden weight matrices: wdl.py:272-275 L2, dnn.py:88-90 L1."""
+        return {"wdl": "l2", "dnn": "l1"}.get(self.model)
+
+    @property
+    def head_l2(self):
+        """L2 on the output weights (deepfm_pipeline.py:183, dnn_pipeline.py:131); dnn.py has none."""
+        return self.model != "dnn"
+
+    def head_ref_index(self):
+        """Reference index of each internal head weight (FM fields internally [cont | cate |
+        pooled]; deepfm.py:70-71 orders its FM fields [cate | cont])."""
+        n = self.fm_cols + self.hidden[-1] + 1
+        idx = np.arange(n)
+        if self.model == "deepfm" and self.C:
+            C, S = self.C, self.S
+            idx[:C] = S + np.arange(C)
+            idx[C:C + S] = np.arange(S)
+        return idx
 
     @property
     def fm_cate_offset(self):
@@ -327,7 +372,7 @@ class CTREngine:
         L.fm_cont = 1 if sp.fm_cont else 0
         L.use_fm = 1 if sp.fm else 0
         L.fm_extra = sp.M if sp.fm else 0
-        L.zero_row0 = 0 if sp.model == "wdl" else 1                     # :83-86 (wdl.py:49: none)
+        L.zero_row0 = 1 if sp.zero_row0 else 0                         # :83-86 (wdl.py:49: none)
         L.x0_ld = self.in_ld[0]
         L.x0_cont_col = self.cont_col if sp.C else -1
         L.x0_vec_col = self.vec_col if sp.V else -1
@@ -349,14 +394,15 @@ class CTREngine:
         if self.lazy:   # same values as the dense engine: initialise dense, then pack
             self.table = torch.zeros(self.rows_pad, sp.E, device=self.dev)
             self.first = torch.zeros(self.rows_pad, device=self.dev) if sp.fm else None
-        if self.wdl:   # xavier_initializer (wdl.py:44-47): U(-lim, lim), lim = sqrt(6/(N+E))
+        if sp.xavier_table:   # xavier_initializer (wdl.py:44-47, dnn.py:49-52): U(-lim, lim), lim = sqrt(6/(N+E))
             lim = math.sqrt(6.0 / (self.N + sp.E))
             call("dl_init_random", ptr(self.table), self.table.numel(), 1, -lim, 2 * lim, seed, 0, s)
+        if self.wdl:
             call("dl_init_random", ptr(self.ww), _ru(self.ww.numel(), 4), 0, 0.0,
                  math.sqrt(2.0 / self.w_rows), seed + 3, 0, s)                           # wdl.py:241-244
             self.ww[self.w_rows:].zero_()
             self.wb[0] = float(np.random.default_rng(seed).standard_normal())
-        else:
+        if not sp.xavier_table:
             call("dl_init_random", ptr(self.table), self.table.numel(), 0, 0.0, 0.01, seed, 0, s)
         if self.first is not None:
             call("dl_init_random", ptr(self.first), self.first.numel(), 1, 0.0, 1.0, seed + 1, 0, s)
@@ -401,9 +447,8 @@ class CTREngine:
         """Inject reference-layout parameters (dict of numpy arrays as in oracle/ctr_ref.py)."""
         sp = self.spec
         N = self.N
-        tab = P["weight_mat"] if self.wdl else P["feats_emb"]
-        tab = torch.from_numpy(np.ascontiguousarray(tab, np.float32))
-        first = (torch.from_numpy(np.ascontiguousarray(P["fm_first_order_emb"][:, 0], np.float32))
+        tab = torch.from_numpy(np.ascontiguousarray(P[sp.table_key], np.float32))
+        first = (torch.from_numpy(np.ascontiguousarray(P[sp.first_key][:, 0], np.float32))
                  if sp.fm else None)
         if self.lazy:
             self._pack(tab.to(self.dev), first.to(self.dev) if first is not None else None)
@@ -426,6 +471,7 @@ class CTREngine:
             w = np.concatenate([P["deep_fm_weight"][:, 0], P["deep_fm_bias"].reshape(-1)]).astype(np.float32)
         else:
             w = np.concatenate([P["deep_res"][:, 0], P["deep_res_bias"].reshape(-1)]).astype(np.float32)
+        w = w[sp.head_ref_index()]
         self.w_head.zero_()
         self.w_head[: self.head_n].copy_(torch.from_numpy(w))
         torch.cuda.synchronize()
@@ -437,13 +483,13 @@ class CTREngine:
         if self.lazy:
             self.flush()
             rec = self.rec[:N]
-            P = {("weight_mat" if self.wdl else "feats_emb"): rec[:, : sp.E].cpu().numpy()}
+            P = {sp.table_key: rec[:, : sp.E].cpu().numpy()}
             if sp.fm:
-                P["fm_first_order_emb"] = rec[:, sp.E: sp.E + 1].cpu().numpy()
+                P[sp.first_key] = rec[:, sp.E: sp.E + 1].cpu().numpy()
         else:
-            P = {("weight_mat" if self.wdl else "feats_emb"): self.table[:N].cpu().numpy()}
+            P = {sp.table_key: self.table[:N].cpu().numpy()}
             if self.first is not None:
-                P["fm_first_order_emb"] = self.first[:N].cpu().numpy()[:, None]
+                P[sp.first_key] = self.first[:N].cpu().numpy()[:, None]
         dims = [self.D0] + sp.hidden
         for l in range(len(sp.hidden)):
             Wi = self.W[l].cpu().numpy()
@@ -458,7 +504,9 @@ class CTREngine:
             P["wdl_weights"] = self.ww[: self.w_rows].cpu().numpy()[:, None].copy()
             P["wdl_bias"] = self.wb[:1].cpu().numpy().copy()
             return P
-        w = self.w_head[: self.head_n].cpu().numpy()
+        wi = self.w_head[: self.head_n].cpu().numpy()
+        w = np.empty_like(wi)
+        w[sp.head_ref_index()] = wi
         if sp.fm:
             P["deep_fm_weight"], P["deep_fm_bias"] = w[:-1, None].copy(), w[-1:].copy()
         else:
@@ -687,10 +735,13 @@ class CTREngine:
                     self._c("gemm_dx_l0", "dl_gemm_f32", 0, 0, B, self.dx_cols, self.out_ld[0], ptr(self.dh[0]),
                             self.h_ld[0], ptr(self.Wt), self.in_ld[0], ptr(self.dx0), self.dx_ld, 0, None, 0, 1, 0, s)
             # L2 on every hidden weight matrix only for wdl (wdl.py:272-275); bias row excluded
-            l2, l2n = (sp.l2, ([self.D0] + sp.hidden)[l] * self.out_ld[l]) if self.wdl else (0.0, 0)
-            self._c("adam_dense_l%d" % l, "dl_adam_dense", ptr(self.W[l]), ptr(self.Wm[l]), ptr(self.Wv[l]),
-                    ptr(self.w_slab), nsplit, stride, stride, l2, l2n, ptr(self.opt), None,
-                    ptr(self.opt[8:]) if self.wdl else None, s)
+            # regulariser on every hidden weight matrix: wdl L2 (wdl.py:272-275), dnn L1 (dnn.py:88-90);
+            # bias row excluded
+            reg = sp.hidden_reg
+            l2, l2n = (sp.l2, ([self.D0] + sp.hidden)[l] * self.out_ld[l]) if reg else (0.0, 0)
+            self._c("adam_dense_l%d" % l, "dl_adam_dense_reg", ptr(self.W[l]), ptr(self.Wm[l]), ptr(self.Wv[l]),
+                    ptr(self.w_slab), nsplit, stride, stride, l2, l2n, 1 if reg == "l1" else 0, ptr(self.opt),
+                    None, ptr(self.opt[8:]) if reg else None, s)
             self._refresh_wb(l, s)
         # embedding backward (uses pre-update table and head weights)
         bwd_blocks = call_int("dl_embed_bwd_grid", C_ref(L))
@@ -746,8 +797,8 @@ class CTREngine:
             return
         # head Adam: L2 on the output weights only (deepfm_pipeline.py:183 / dnn_pipeline.py:131)
         self._c("adam_head", "dl_adam_dense", ptr(self.w_head), ptr(self.hm), ptr(self.hv), ptr(self.head_slab),
-                hb, sp.fm_cols + H + 2, self.head_n, sp.l2, self.head_n - 1, ptr(self.opt), ptr(self.w_head_prev),
-                ptr(self.opt[8:]), s)
+                hb, sp.fm_cols + H + 2, self.head_n, sp.l2 if sp.head_l2 else 0.0,
+                self.head_n - 1 if sp.head_l2 else 0, ptr(self.opt), ptr(self.w_head_prev), ptr(self.opt[8:]), s)
         if self.lazy:
             return
         if sp.fm:
@@ -868,8 +919,8 @@ class CTREngine:
         torch.cuda.current_stream().wait_stream(s)
         return g
 
-    def predict(self, batch):
-        """Forward only: returns sigmoid scores [B] (host numpy)."""
+    def predict(self, batch, logits=False):
+        """Forward only: returns sigmoid scores [B] (or the logits) as host numpy."""
         B, indexed = self._begin(batch)
         s = _lib.stream_handle()
         if not indexed:
@@ -877,7 +928,7 @@ class CTREngine:
         self._forward(B, s)
         self._release()
         self.check_error()
-        return self.score[:B].cpu().numpy()
+        return (self.z if logits else self.score)[:B].cpu().numpy()
 
     def loss(self):
         """Loss of the last training step: data term + the L2 terms on the pre-update
@@ -888,6 +939,8 @@ class CTREngine:
         width = self.head_slab.shape[1]
         rows = call_int("dl_head_grid", B)
         data = self.head_slab[:rows, width - 1].double().sum().item() / B
+        if sp.hidden_reg == "l1":   # l1_regularizer: scale * sum |W| (dnn.py:88-90)
+            return data + sp.l2 * float(self.opt[8].item())
         return data + sp.l2 * 0.5 * float(self.opt[8].item())
 
     def check_error(self):

@@ -184,13 +184,13 @@ def _load_adam_state(eng, d):
         eng.Wv[l].copy_(torch.from_numpy(d["adam/Wv%d" % l]))
 
 
-def _predict_batches(eng, batch):
-    """Forward in chunks of the engine's max batch; returns a list of scores."""
+def _predict_batches(eng, batch, logits=False):
+    """Forward in chunks of the engine's max batch; returns a list of scores (or logits)."""
     n = np.asarray(batch["label"]).shape[0]
     out = []
     for s in range(0, n, eng.B):
         part = {k: np.asarray(v)[s:s + eng.B] for k, v in batch.items()}
-        out.extend(eng.predict(part).tolist())
+        out.extend(eng.predict(part, logits=logits).tolist())
     return out
 
 

@@ -1,0 +1,105 @@
+"""Shared implementation of the reference's load-style model surface (models/wdl.py,
+models/deepfm.py, models/dnn.py): the models that train from lists of pickled batch
+dicts (utils/data_loader_load.py:61-139) instead of the TFRecord iterator.
+
+    DeepModel(args)                      (deepfm.py:15-37, dnn.py:15-33, wdl.py:19-51)
+    .model_optimizer()                   (deepfm.py:146-162; dnn.py builds it in __init_graph)
+    .fit(train_data, val_data)           (deepfm.py:164-214, dnn.py:98-145, wdl.py:287-341)
+    .evaluate(sess, data_val) -> auc     (deepfm.py:216-232, dnn.py:147-161, wdl.py:343-358)
+    .predict(data_val)                   (deepfm.py:234-255, dnn.py:163-185, wdl.py:360-384)
+
+Per epoch the reference prints '[%s] valid-%s=%.5f\tloss=%.5f [%.1f s]' with the loss
+averaged over the epoch's batches (each weighted by batch_size), then exports the model;
+predict prints 'val of auc:%.5f'.  The engine runs the step as one hipGraph replay for
+full batches.
+"""
+import pickle
+import sys
+import time
+
+import numpy as np
+
+from ..engine import CTREngine, default_adam
+from ..metrics import roc_auc
+from ._ctr_model import _predict_batches, export_model, load_model
+
+
+def unpickle(item):
+    return pickle.loads(item) if isinstance(item, (bytes, bytearray)) else item
+
+
+class LoadStyleModel:
+    # evaluate() scores: "score" (sigmoid) or "logit" (deepfm.py:229 evaluates the
+    # pre-sigmoid self.out)
+    EVAL_OUTPUT = "score"
+
+    def __init__(self, args):
+        self.hidden_units = [int(h) for h in args.hidden_units]
+        self.epochs = int(args.epochs)
+        self.batch_size = int(args.batch_size)
+        self.learning_rate = args.learning_rate
+        self.model_pb = args.model_pb
+        self.l2_reg = args.l2_reg
+        self.metric_type = "auc"
+        self.random_seed = 2019
+        self.spec = self.make_spec(args)
+        self.engine = None
+
+    def make_spec(self, args):
+        raise NotImplementedError
+
+    def batch(self, item):
+        """One pickled batch dict (data_loader_load.py:128-135 keys) -> engine batch."""
+        raise NotImplementedError
+
+    def model_optimizer(self):
+        if self.engine is None:
+            self.engine = CTREngine(self.spec, max_batch=self.batch_size, seed=self.random_seed,
+                                    adam=default_adam(self.spec))
+        return self.engine
+
+    def fit(self, train_data, val_data):
+        eng = self.model_optimizer()
+        losses = []
+        num_samples = 0
+        for epoch in range(self.epochs):
+            st = time.time()
+            for item in train_data:
+                b = self.batch(item)
+                eng.train_step(b, graph=b["label"].shape[0] == eng.B)
+                losses.append(eng.loss() * self.batch_size)
+                num_samples += self.batch_size
+            end_time = time.time()
+            total_loss = float(np.sum(losses) / num_samples)
+            valid_metric = self.evaluate(None, val_data)
+            print('[%s] valid-%s=%.5f\tloss=%.5f [%.1f s]' % (epoch + 1, self.metric_type, valid_metric,
+                                                               total_loss, end_time - st))
+            sys.stdout.flush()
+        eng.check_error()
+        try:
+            export_model(eng, self.model_pb)
+        except Exception as e:
+            print("Fail to export saved model, exception: {}".format(e))
+            sys.stdout.flush()
+
+    def evaluate(self, sess, data_val):
+        eng = self.model_optimizer()
+        preds, labels = [], []
+        for item in data_val:
+            b = self.batch(item)
+            labels.extend(b["label"].reshape(-1).tolist())
+            preds.extend(_predict_batches(eng, b, logits=self.EVAL_OUTPUT == "logit"))
+        return roc_auc(labels, preds)
+
+    def predict(self, data_val):
+        eng = load_model(self.model_pb, max_batch=self.batch_size)
+        preds, labels = [], []
+        for item in data_val:
+            b = self.batch(item)
+            labels.extend(b["label"].reshape(-1).tolist())
+            preds.extend(_predict_batches(eng, b))
+        auc = roc_auc(labels, preds)
+        print("val of auc:%.5f" % auc)
+        sys.stdout.flush()
+        print('---end---')
+        return auc

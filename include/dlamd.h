@@ -259,6 +259,12 @@ int dl_adam_begin_step(float* opt, float decay_rate, float decay_steps, void* st
 int dl_adam_dense(float* p, float* m, float* v, const float* slab, int32_t nslab,
                   int64_t slab_stride, int64_t n, float l2, int64_t l2_count, const float* opt,
                   float* p_prev, float* sq_out, void* stream);
+/* dl_adam_dense with the regulariser kind explicit: reg_kind 0 = L2 as above, 1 = L1
+ * (tf.contrib.layers.l1_regularizer at models/dnn.py:88-90: g += reg * sign(p) for
+ * i < reg_count, acc_out += |p_pre|). */
+int dl_adam_dense_reg(float* p, float* m, float* v, const float* slab, int32_t nslab,
+                      int64_t slab_stride, int64_t n, float reg, int64_t reg_count, int32_t reg_kind,
+                      const float* opt, float* p_prev, float* acc_out, void* stream);
 /* Embedding tables with dense-Adam semantics: g = g_table row if touched else 0;
  * consumed gradients are reset to 0; `clear_touched` resets the flags (pass 1
  * on the last table that shares them).  width = E (table) or 1 (first-order). */

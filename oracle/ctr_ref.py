@@ -15,6 +15,8 @@ Models restated:
   dnn_multi         models/dnn_multi.py:70-167
   dnn_multi_cate    models/dnn_multi_cate.py:64-162
   wdl               models/wdl.py:43-285
+  deepfm (load)     models/deepfm.py:39-162
+  dnn (load)        models/dnn.py:35-96
 Optimizer: tf.train.AdamOptimizer (TF1 ApplyAdam, dense — see ledger item 6
 in SURVEY.md: the embedding gradient reaches the Variable through
 concat/strided-slice and is densified, so every row's m, v decay each step).
@@ -55,7 +57,22 @@ FAMILIES = {
     "dnn_multi": dict(fm=False, cont="deep", multi=True),
     "dnn_multi_cate": dict(fm=False, cont=None, multi=True),
     "wdl": dict(fm=False, cont="deep", multi=False),
+    "deepfm": dict(fm=True, cont="field", multi=False),   # FM fields [cate | cont], cont rows at S + j
+    "dnn": dict(fm=False, cont="deep", multi=False),      # xavier weight_mat, L1 on hidden weights
 }
+
+
+def zero_row0(cfg):
+    # deepfm_pipeline.py:83-86; none in wdl.py:44, deepfm.py:58-60, dnn.py:49-52
+    return cfg.model not in ("wdl", "deepfm", "dnn")
+
+
+def table_key(cfg):
+    return "weight_mat" if cfg.model in ("wdl", "dnn") else "feats_emb"
+
+
+def first_key(cfg):
+    return "feats" if cfg.model == "deepfm" else "fm_first_order_emb"   # deepfm.py:60
 
 
 def make_cfg(model, **kw):
@@ -76,13 +93,13 @@ def is_fm(cfg):
 
 
 def fm_cont(cfg):
-    return is_fm(cfg) and FAMILIES[cfg.model]["cont"] in ("first", "last") and cfg.C > 0
+    return is_fm(cfg) and FAMILIES[cfg.model]["cont"] in ("first", "last", "field") and cfg.C > 0
 
 
 def n_rows(cfg):
     """Embedding-table rows (index_max_size)."""
     if fm_cont(cfg):
-        return cfg.C + cfg.cate_index_size          # deepfm_pipeline.py:77, deepfm_multi.py:125
+        return cfg.C + cfg.cate_index_size          # deepfm_pipeline.py:77, deepfm_multi.py:125, deepfm.py:57
     return cfg.cate_index_size                      # dnn_pipeline.py:69, deepfm_multi_cate.py:114, wdl.py:46
 
 
@@ -118,13 +135,13 @@ def init_params(cfg, rng):
     E, H = cfg.E, cfg.hidden
     N = n_rows(cfg)
     P = {}
-    if cfg.model == "wdl":
-        lim = math.sqrt(6.0 / (N + E))              # xavier_initializer, wdl.py:44-47
+    if table_key(cfg) == "weight_mat":
+        lim = math.sqrt(6.0 / (N + E))              # xavier_initializer, wdl.py:44-47, dnn.py:49-52
         P["weight_mat"] = rng.uniform(-lim, lim, (N, E)).astype(F32)
     else:
         P["feats_emb"] = (rng.standard_normal((N, E)) * 0.01).astype(F32)   # deepfm_pipeline.py:78
     if is_fm(cfg):
-        P["fm_first_order_emb"] = rng.uniform(0.0, 1.0, (N, 1)).astype(F32)  # :80
+        P[first_key(cfg)] = rng.uniform(0.0, 1.0, (N, 1)).astype(F32)       # :80
     fan = deep_in(cfg)
     dims = [fan] + list(H)
     for i in range(len(H)):
@@ -204,8 +221,9 @@ def forward(cfg, P, batch, dtype=F32):
         V = P["weight_mat"].astype(dtype)                                                    # wdl.py:44 (no zero row)
         x0 = np.concatenate([cont, V[cate].reshape(B, S * E)], 1)                            # wdl.py:132-133,179
     else:
-        V = _zero_row0(P["feats_emb"].astype(dtype))                                         # deepfm_pipeline.py:83-86
-        w1 = _zero_row0(P["fm_first_order_emb"].astype(dtype)) if is_fm(cfg) else None      # :85-86
+        zr = _zero_row0 if zero_row0(cfg) else (lambda t: t)
+        V = zr(P[table_key(cfg)].astype(dtype))                                              # deepfm_pipeline.py:83-86
+        w1 = zr(P[first_key(cfg)].astype(dtype)) if is_fm(cfg) else None                     # :85-86
         single, multi = cate[:, :S], cate[:, S:]                                             # deepfm_multi.py:64-65
         M = len(cfg.multi_ranges)
         pooled, pooled_first, cnt_emb, cnt_first = _pool(cfg, V, w1, multi)
@@ -215,9 +233,13 @@ def forward(cfg, P, batch, dtype=F32):
             cont_off = cfg.cate_index_size if fam == "last" else 0                          # deepfm_multi.py:139
             cate_off = C if fam == "first" else 0                                            # deepfm_pipeline.py:89
             # FM fields [cont (row cont_off + j, value cont) | single (row id + cate_off, value 1)]
-            idx = np.concatenate([np.tile(np.arange(Cf, dtype=np.int64) + cont_off, (B, 1)),
-                                  single + cate_off], 1)                                     # :58-61,89-90
-            val = np.concatenate([cont[:, :Cf], np.ones((B, S), dtype)], 1)                  # :62,91
+            cidx = np.tile(np.arange(Cf, dtype=np.int64) + cont_off, (B, 1))
+            if fam == "field":    # deepfm.py:66-73: [cate | cont], cont rows at cate_field_size + j
+                idx = np.concatenate([single, cidx + S], 1)
+                val = np.concatenate([np.ones((B, S), dtype), cont[:, :Cf]], 1)
+            else:
+                idx = np.concatenate([cidx, single + cate_off], 1)                           # :58-61,89-90
+                val = np.concatenate([cont[:, :Cf], np.ones((B, S), dtype)], 1)              # :62,91
             first = np.concatenate([w1[idx][:, :, 0] * val, pooled_first], 1)               # :95-97; multi :132-136
             e = np.concatenate([V[idx] * val[:, :, None], pooled], 1)                        # :102-104; multi :142-147
             s = e.sum(1)                                                                     # :105
@@ -264,6 +286,9 @@ def _reg_loss(cfg, P):
     sq = lambda a: 0.5 * float((a.astype(np.float64) ** 2).sum())   # tf.nn.l2_loss
     if is_fm(cfg):
         return cfg.l2 * sq(P["deep_fm_weight"])                     # deepfm_pipeline.py:183
+    if cfg.model == "dnn":                                          # dnn.py:88-90: L1 on every hidden W
+        return sum(cfg.l2 * float(np.abs(P["deep_%d" % i].astype(np.float64)).sum())
+                   for i in range(len(cfg.hidden)))
     if cfg.model != "wdl":
         return cfg.l2 * sq(P["deep_res"])                           # dnn_pipeline.py:131
     r = cfg.l2 * sq(P["wdl_weights"])                               # wdl.py:270-271
@@ -302,7 +327,7 @@ def backward(cfg, P, batch, fw, dtype=F32):
         dfirst, dsec, dh = dfeats[:, :nF], dfeats[:, nF:nF + E], dfeats[:, nF + E:]
     elif cfg.model != "wdl":
         W = P["deep_res"].astype(dtype)
-        G["deep_res"] = (h.T @ dz[:, None]).astype(dtype) + l2 * W
+        G["deep_res"] = (h.T @ dz[:, None]).astype(dtype) + (l2 * W if cfg.model != "dnn" else 0)
         G["deep_res_bias"] = np.array([[dz.sum()]], dtype)
         dh = dz[:, None] * W[:, 0][None, :]
     else:
@@ -321,6 +346,8 @@ def backward(cfg, P, batch, fw, dtype=F32):
         G["deep_%d" % i] = (xs[i].T @ g).astype(dtype)
         if cfg.model == "wdl":
             G["deep_%d" % i] += l2 * Wi
+        elif cfg.model == "dnn":
+            G["deep_%d" % i] += l2 * np.sign(Wi)                    # d/dW l1_regularizer
         G["deep_bias_%d" % i] = g.sum(0, keepdims=True).astype(dtype)
         dx = (g @ Wi.T).astype(dtype)
         g = (dx * (xs[i] > 0)).astype(dtype) if i > 0 else dx
@@ -331,7 +358,7 @@ def backward(cfg, P, batch, fw, dtype=F32):
         col = C
         np.add.at(G["weight_mat"], cate.reshape(-1), dx0[:, col:col + S * E].reshape(-1, E))
         return G, dz
-    tab, t1 = "feats_emb", "fm_first_order_emb"
+    tab, t1 = table_key(cfg), first_key(cfg)
     single, multi = fw["single"], fw["multi"]
     M = len(cfg.multi_ranges)
     col = C + cfg.V
@@ -356,9 +383,10 @@ def backward(cfg, P, batch, fw, dtype=F32):
             c1 = fw["cnt_first"][:, m]
             g1 = np.where(c1 > 0, dpool1[:, m] / np.where(c1 > 0, c1, 1), 0).astype(dtype)
             np.add.at(G[t1][:, 0], ids.reshape(-1), np.repeat(g1, L))
-    G[tab][0] = 0                                                  # concat zero-row: no grad to Var row 0
-    if is_fm(cfg):
-        G[t1][0] = 0
+    if zero_row0(cfg):
+        G[tab][0] = 0                                              # concat zero-row: no grad to Var row 0
+        if is_fm(cfg):
+            G[t1][0] = 0
     return G, dz
 
 

@@ -30,6 +30,8 @@ CASES = {
                       multi_ranges=[[0, 30, "a"], [30, 50, "b"]]),
     "dnn_multi_cate": dict(V=4, S=8, E=8, cate_index_size=6000, hidden=[40, 24],
                            multi_ranges=[[0, 20, "a"], [20, 64, "b"]]),
+    "deepfm": dict(C=13, V=3, S=26, E=8, cate_index_size=5000, hidden=[48, 32]),
+    "dnn": dict(C=16, S=26, E=16, cate_index_size=6000, hidden=[64, 32], l2=1e-3),
 }
 
 
@@ -55,6 +57,7 @@ def _batches(name, kw, B, n, seed=11):
                            cate_index_size=kw["cate_index_size"], seed=seed + i, wide_fields=kw.get("Fw", 0),
                            cate_only=C == 0)
             b["cate_feats"][0, :4] = [0, 1, 5, 12]   # padding id + ids that alias cont rows
+            b["cate_feats"][1, :2] = [27, 30]        # deepfm.py: ids aliasing its cont rows (S + j)
         out.append(b)
     return out
 
@@ -103,7 +106,8 @@ def test_graph_replay_equals_eager(hip_lib):
 @pytest.mark.parametrize("stash", [False, True])
 # (multi-hot models are left out: the dense engine adds pooled gradients with atomics, whose
 # order varies, while the record path sums every row's references in a fixed order)
-@pytest.mark.parametrize("name", ["deepfm_pipeline", "dnn_pipeline", "wdl", "deepfm_cate", "dnn_cate"])
+@pytest.mark.parametrize("name", ["deepfm_pipeline", "dnn_pipeline", "wdl", "deepfm_cate", "dnn_cate", "deepfm",
+                                  "dnn"])
 def test_lazy_adam_bit_identical_to_dense(hip_lib, name, stash):
     """Row records + lazy catch-up (rec.hip) against the dense sweep with the same
     (sorted, deterministic) gradients: parameters, Adam moments, logits and
@@ -114,8 +118,7 @@ def test_lazy_adam_bit_identical_to_dense(hip_lib, name, stash):
     spec = ModelSpec(model, **kw)
     dense = CTREngine(spec, max_batch=128, seed=3, bwd="sorted")
     lazy = CTREngine(spec, max_batch=128, seed=3, adam="lazy", hist_len=8, rec_stash=stash)
-    np.testing.assert_array_equal(lazy.params()["weight_mat" if model == "wdl" else "feats_emb"],
-                                  dense.params()["weight_mat" if model == "wdl" else "feats_emb"])
+    np.testing.assert_array_equal(lazy.params()[spec.table_key], dense.params()[spec.table_key])
     bs = _batches(name, kw, 128, 21, seed=7)
     for i, b in enumerate(bs):
         dense.train_step(b, graph=i >= 3)

@@ -17,6 +17,10 @@ def _cfg(model):
         return R.make_cfg(model, C=5, **kw)
     if model in ("dnn_pipeline", "dnn_cate"):
         return R.make_cfg(model, C=5, V=3, **kw)
+    if model == "deepfm":
+        return R.make_cfg(model, C=5, V=3, **kw)
+    if model == "dnn":
+        return R.make_cfg(model, C=7, **kw)
     if model == "deepfm_cate":
         return R.make_cfg(model, V=2, **kw)
     if model in ("deepfm_multi_cate", "dnn_multi_cate"):
@@ -104,7 +108,13 @@ def _torch_loss(cfg, P, batch):
         first, second = fm([w1[cidx][:, :, 0] * cont, w1[single][:, :, 0]] + pf,
                            [V[cidx] * cont[:, :, None], V[single], torch.stack(pv, 1)])
         x = torch.cat([cont, vec, V[single].reshape(B, -1), torch.stack(pv, 1).reshape(B, -1)], 1)
-    else:
+    elif cfg.model == "deepfm":                  # deepfm.py:56-115 (no zero row; FM fields [cate | cont])
+        V, w1 = T["feats_emb"], T["feats"][:, 0]
+        idx = torch.cat([cate, torch.arange(C).repeat(B, 1) + S], 1)
+        val = torch.cat([ones, cont], 1)
+        first, second = fm([w1[idx] * val], [V[idx] * val[:, :, None]])
+        x = torch.cat([cont, vec, V[cate].reshape(B, -1)], 1)
+    else:                                        # wdl.py:132-179, dnn.py:49-60
         V = T["weight_mat"]
         x = torch.cat([cont, V[cate].reshape(B, -1)], 1)
     h = x
@@ -113,6 +123,9 @@ def _torch_loss(cfg, P, batch):
     if cfg.model.startswith("deepfm"):
         z = (torch.cat([first, second, h], 1) @ T["deep_fm_weight"])[:, 0] + T["deep_fm_bias"][0]
         reg = 0.5 * (T["deep_fm_weight"] ** 2).sum()
+    elif cfg.model == "dnn":
+        z = (h @ T["deep_res"])[:, 0] + T["deep_res_bias"][0, 0]
+        reg = sum(T["deep_%d" % i].abs().sum() for i in range(len(cfg.hidden)))   # l1_regularizer
     elif cfg.model.startswith("dnn"):
         z = (h @ T["deep_res"])[:, 0] + T["deep_res_bias"][0, 0]
         reg = 0.5 * (T["deep_res"] ** 2).sum()
@@ -131,7 +144,7 @@ def _torch_loss(cfg, P, batch):
 
 
 ALL_MODELS = ["deepfm_pipeline", "deepfm_cate", "deepfm_multi_cate", "deepfm_multi", "dnn_pipeline", "dnn_cate",
-              "dnn_multi", "dnn_multi_cate", "wdl"]
+              "dnn_multi", "dnn_multi_cate", "wdl", "deepfm", "dnn"]
 
 
 @pytest.mark.parametrize("model", ALL_MODELS)
