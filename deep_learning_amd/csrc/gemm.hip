@@ -69,7 +69,10 @@ __device__ __forceinline__ int xcd_tile(int bid, int T) {
 template <int BM, int BN>
 struct GemmOcc { static constexpr int waves = (BM == 128 && BN <= 80 && DL_GEMM_BK == 16) ? 5 : 2; };
 
-template <int BM, int BN, int WM, int WN, bool TA, bool TB, int EPI, int BK>
+// FAST: M % BM == 0, N % BN == 0 and every split's k range whole BK slabs (the tower's
+// products: batch rows, 400-wide layers, zero-padded K = leading dims): no bounds checks,
+// each thread's staging addresses computed once and advanced by a constant per slab.
+template <int BM, int BN, int WM, int WN, bool TA, bool TB, int EPI, int BK, bool FAST>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GemmOcc<BM, BN>::waves)))
 void gemm_f32_kernel(GemmParams p) {
   constexpr bool AKC = !TA, BKC = TB, KPERM = AKC || BKC;
@@ -115,6 +118,29 @@ void gemm_f32_kernel(GemmParams p) {
 
   float4 ra[QA], rb[QB];
 
+  // FAST staging: buffer loads, SGPR resource + per-thread 32-bit byte offset (fixed) +
+  // SGPR slab offset (advanced by a_step / b_step bytes per slab)
+  unsigned a_off[QA], b_off[QB];
+  const unsigned a_step = TA ? (unsigned)(BK * p.lda * 4) : (unsigned)(BK * 4);
+  const unsigned b_step = TB ? (unsigned)(BK * 4) : (unsigned)(BK * p.ldb * 4);
+  const float* a_base = A + (TA ? (long long)kbeg * p.lda + i0 : (long long)i0 * p.lda + kbeg);
+  const float* b_base = Bm + (TB ? (long long)j0 * p.ldb + kbeg : (long long)kbeg * p.ldb + j0);
+  const auto a_rsrc = __builtin_amdgcn_make_buffer_rsrc((void*)a_base, (short)0, 0x7fffffff, 0x00020000);
+  const auto b_rsrc = __builtin_amdgcn_make_buffer_rsrc((void*)b_base, (short)0, 0x7fffffff, 0x00020000);
+  if (FAST) {
+#pragma unroll
+    for (int u = 0; u < QA; ++u) {
+      const int qi = min(tid + u * 256, BM * BK / 4 - 1);
+      if (TA) a_off[u] = 4u * (unsigned)((qi / (BM / 4)) * p.lda + 4 * (qi % (BM / 4)));
+      else a_off[u] = 4u * (unsigned)((qi / (BK / 4)) * p.lda + 4 * (qi % (BK / 4)));
+    }
+#pragma unroll
+    for (int u = 0; u < QB; ++u) {
+      const int qi = min(tid + u * 256, BN * BK / 4 - 1);
+      if (!TB) b_off[u] = 4u * (unsigned)((qi / (BN / 4)) * p.ldb + 4 * (qi % (BN / 4)));
+      else b_off[u] = 4u * (unsigned)((qi / (BK / 4)) * p.ldb + 4 * (qi % (BK / 4)));
+    }
+  }
   auto glds_a = [&](int k0, int buf) {
     // 8 pieces of 16 rows for BM = 128: wave w issues pieces w, w + 4, ...
 #pragma unroll
@@ -130,6 +156,20 @@ void gemm_f32_kernel(GemmParams p) {
     }
   };
   auto load_tile = [&](int k0) {
+    if (FAST) {
+      const unsigned ks = (unsigned)((k0 - kbeg) / BK);
+      const int sa = (int)(ks * a_step), sb = (int)(ks * b_step);
+#pragma unroll
+      for (int u = 0; u < (GLDS ? 0 : QA); ++u) {
+        const auto v = __builtin_amdgcn_raw_buffer_load_b128(a_rsrc, (int)a_off[u], sa, 0);
+        ra[u] = make_float4(__uint_as_float(v[0]), __uint_as_float(v[1]), __uint_as_float(v[2]), __uint_as_float(v[3]));
+      }
+#pragma unroll
+      for (int u = 0; u < QB; ++u) {
+        const auto v = __builtin_amdgcn_raw_buffer_load_b128(b_rsrc, (int)b_off[u], sb, 0);
+        rb[u] = make_float4(__uint_as_float(v[0]), __uint_as_float(v[1]), __uint_as_float(v[2]), __uint_as_float(v[3]));
+      }
+    } else {
 #pragma unroll
     for (int u = 0; u < (GLDS ? 0 : QA); ++u) {
       const int qi = tid + u * 256;
@@ -163,6 +203,7 @@ void gemm_f32_kernel(GemmParams p) {
         }
       }
       rb[u] = v;
+    }
     }
   };
   auto store_tile = [&](int buf) {
@@ -258,7 +299,7 @@ void gemm_f32_kernel(GemmParams p) {
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const int row = i0 + wm * WTM + a * 16 + kr * 4 + j;
-        if (row < p.M && col < p.N) {
+        if (FAST || (row < p.M && col < p.N)) {
           float v = acc[a][b][j];
           if (EPI == EPI_RELU) v = fmaxf(v, 0.f);
           if (EPI == EPI_MASK) v = Mk[(long long)row * p.ldm + col] > 0.f ? v : 0.f;
@@ -513,17 +554,25 @@ __global__ __launch_bounds__(256) void transpose_bf16_kernel(const void* __restr
   }
 }
 
+template <int BM, int BN, int WM, int WN, bool TA, bool TB, bool FAST>
+static void launch_f32_v(const GemmParams& gp, int epi, dim3 grid, hipStream_t s) {
+  constexpr int BK = DL_GEMM_BK;
+  switch (epi) {
+    case EPI_STORE: hipLaunchKernelGGL((gemm_f32_kernel<BM, BN, WM, WN, TA, TB, EPI_STORE, BK, FAST>), grid, dim3(256), 0, s, gp); break;
+    case EPI_RELU: hipLaunchKernelGGL((gemm_f32_kernel<BM, BN, WM, WN, TA, TB, EPI_RELU, BK, FAST>), grid, dim3(256), 0, s, gp); break;
+    case EPI_MASK: hipLaunchKernelGGL((gemm_f32_kernel<BM, BN, WM, WN, TA, TB, EPI_MASK, BK, FAST>), grid, dim3(256), 0, s, gp); break;
+    default: hipLaunchKernelGGL((gemm_f32_kernel<BM, BN, WM, WN, TA, TB, EPI_SPLIT, BK, FAST>), grid, dim3(256), 0, s, gp); break;
+  }
+}
+
 template <int BM, int BN, int WM, int WN, bool TA, bool TB>
 static void launch_f32(const GemmParams& gp, int epi, int splits, hipStream_t s) {
   constexpr int BK = DL_GEMM_BK;
   const int tiles = (int)(ceil_div(gp.M, BM) * ceil_div(gp.N, BN));
   dim3 grid(tiles, 1, splits);
-  switch (epi) {
-    case EPI_STORE: hipLaunchKernelGGL((gemm_f32_kernel<BM, BN, WM, WN, TA, TB, EPI_STORE, BK>), grid, dim3(256), 0, s, gp); break;
-    case EPI_RELU: hipLaunchKernelGGL((gemm_f32_kernel<BM, BN, WM, WN, TA, TB, EPI_RELU, BK>), grid, dim3(256), 0, s, gp); break;
-    case EPI_MASK: hipLaunchKernelGGL((gemm_f32_kernel<BM, BN, WM, WN, TA, TB, EPI_MASK, BK>), grid, dim3(256), 0, s, gp); break;
-    default: hipLaunchKernelGGL((gemm_f32_kernel<BM, BN, WM, WN, TA, TB, EPI_SPLIT, BK>), grid, dim3(256), 0, s, gp); break;
-  }
+  const bool fast = gp.M % BM == 0 && gp.N % BN == 0 && gp.K % BK == 0 && gp.k_per_split % BK == 0 && !DL_GEMM_GLDS;
+  if (fast) launch_f32_v<BM, BN, WM, WN, TA, TB, true>(gp, epi, grid, s);
+  else launch_f32_v<BM, BN, WM, WN, TA, TB, false>(gp, epi, grid, s);
 }
 
 template <bool TA, bool TB>

@@ -16,7 +16,8 @@ def _s():
 
 
 @pytest.mark.parametrize("ta,tb", [(0, 0), (0, 1), (1, 0), (1, 1)])
-@pytest.mark.parametrize("M,N,K", [(300, 400, 432), (257, 416, 400), (64, 10, 16), (1000, 128, 64)])
+@pytest.mark.parametrize("M,N,K", [(300, 400, 432), (257, 416, 400), (64, 10, 16), (1000, 128, 64),
+                                   (256, 400, 448), (384, 416, 400), (128, 80, 16)])   # last three: FAST path
 def test_gemm_f32_matches_fp64(hip_lib, ta, tb, M, N, K):
     g = torch.Generator().manual_seed(M * 7 + N + K)
     r4 = lambda x: (x + 3) // 4 * 4
