@@ -63,6 +63,8 @@ SIGNATURES = {
     "dl_pool_fwd": (I32, [LP, P, P, P, I32, P, P, I32, I32, P, P, P, P, P, P]),
     "dl_pool_fwd_indexed": (I32, [LP, P, P, P, I32, P, P, I32, I32, P, P, P, P, P]),
     "dl_pool_bwd": (I32, [LP, P, I32, P, P, I32, I32, P, P, P, P, P, I32, P, P, P, P, P, P]),
+    "dl_pool_fwd_weighted": (I32, [LP, P, P, I32, P, I32, P, P, I32, P, P, P, P]),
+    "dl_pool_bwd_weighted": (I32, [LP, P, I32, P, I32, P, P, I32, P, I32, P, P, P, P]),
     "dl_gemm_f32": (I32, [I32, I32, I32, I32, I32, P, I32, P, I32, P, I32, I32, P, I32, I32, I64, P]),
     "dl_gemm_bf16": (I32, [I32, I32, I32, I32, I32, P, I32, P, I32, P, I32, I32, I32, P, I32, I32, I64, P]),
     "dl_head_fwd_bwd": (I32, [I32, I32, I32, P, I32, P, I32, P, P, F, F, P, P, P, P, P, I32, P]),
@@ -87,6 +89,8 @@ SIGNATURES = {
     "dl_rec_flush": (I32, [P, I32, I32, I32, I64, P, I32, P, P]),
     "dl_rec_chain_link": (I32, [P, I64, P, P, P]),
     "dl_rec_apply_chain": (I32, [P, I32, I32, I32, P, I64, P, P, P, P, P, I32, P, P]),
+    "dl_auc_workspace_bytes": (I64, [I64]),
+    "dl_auc": (I32, [P, I64, P, I64, I64, P, I64, P, P]),
 }
 
 _LIB = None

@@ -362,6 +362,8 @@ struct PoolArgs {
   float* cnt_emb;
   float* cnt_first;
   int32_t* err;
+  const float* vals;       // weighted mode: value of multi position l of sample b = vals[b*vals_ld + l]
+  int vals_ld;
 };
 
 // One wave per sample.  A slot's positions are resolved 64 at a time, one per lane (ids or
@@ -369,7 +371,9 @@ struct PoolArgs {
 // 64/RPI row loads of a chunk are independent, so they are in flight together instead
 // of each waiting on its own id load.  Summation order (per lane, then the xor tree) is
 // the same for both modes and for any chunking: dense and record paths pool identically.
-template <int E, bool IDX>
+// WT (dnn_multi_textline.py:94-103): each row is scaled by its position's value before the
+// sum, while the count still tests the unscaled row (count_nonzero of the plain lookup).
+template <int E, bool IDX, bool WT = false>
 __global__ __launch_bounds__(256) void pool_fwd_kernel(PoolArgs a) {
   constexpr int LPR = E / 4;
   constexpr int RPI = 64 / LPR;
@@ -383,6 +387,7 @@ __global__ __launch_bounds__(256) void pool_fwd_kernel(PoolArgs a) {
   for (int b = wave; b < L.batch; b += nwaves) {
     const int64_t* ids = IDX ? nullptr : a.ids + (int64_t)b * L.cate_ld + a.ids_col;
     const int32_t* invb = IDX ? a.inv + (int64_t)b * ns + mb : nullptr;
+    const float* valb = WT ? a.vals + (int64_t)b * a.vals_ld : nullptr;
     for (int m = 0; m < a.n_slots; ++m) {
       const int s0 = a.slot_start[m], s1 = a.slot_end[m];
       float4 s = f4_zero();
@@ -391,6 +396,8 @@ __global__ __launch_bounds__(256) void pool_fwd_kernel(PoolArgs a) {
         const int nl = min(64, s1 - c0);
         // source row of position c0 + lane (-1: padding / zero row)
         long long src = -1;
+        float wv = 0.f;
+        if (WT && lane < nl) wv = valb[c0 + lane];
         if (lane < nl) {
           if (IDX) {
             const int ri = invb[c0 + lane];
@@ -416,6 +423,10 @@ __global__ __launch_bounds__(256) void pool_fwd_kernel(PoolArgs a) {
 #pragma unroll
           for (int o = 1; o < LPR; o <<= 1) rs += __shfl_xor(rs, o, 64);
           if (q == 0 && pl < nl && rs != 0.f) cnt += 1.f;
+          if (WT) {
+            const float w = __shfl(wv, pl, 64);
+            e.x *= w; e.y *= w; e.z *= w; e.w *= w;   // tf.multiply(emb, value), then the sum
+          }
           s.x += e.x; s.y += e.y; s.z += e.z; s.w += e.w;
         }
       }
@@ -462,9 +473,11 @@ struct PoolBwdArgs {
   float* g_table;
   float* g_first;
   uint8_t* touched;
+  const float* vals;       // weighted mode (see PoolArgs)
+  int vals_ld;
 };
 
-template <int E>
+template <int E, bool WT = false>
 __global__ __launch_bounds__(256) void pool_bwd_kernel(PoolBwdArgs a) {
   constexpr int RPI = 64 / E;
   const dl_emb_layout& L = a.L;
@@ -490,7 +503,7 @@ __global__ __launch_bounds__(256) void pool_bwd_kernel(PoolBwdArgs a) {
         if (l < s1) {
           const int64_t row = ids[l];
           if (row < L.n_rows && row_ok(row, L.zero_row0)) {
-            atomicAdd(a.g_table + row * E + d, gv);
+            atomicAdd(a.g_table + row * E + d, WT ? gv * a.vals[(int64_t)b * a.vals_ld + l] : gv);
             if (d == 0) a.touched[row] = 1;
           }
         }
@@ -627,7 +640,7 @@ extern "C" int dl_pool_fwd(const dl_emb_layout* L, const float* table, const flo
   DL_CHECK_ARG(!first_order || (fm_out && cnt_first), "first-order pooling needs fm_out/cnt_first");
   if (L->batch == 0 || n_slots == 0) return 0;
   PoolArgs a{*L, nullptr, 0, table, first_order, ids, ids_col, slot_start, slot_end, n_slots, fm_col,
-             x0, fm_out, cnt_emb, cnt_first, err};
+             x0, fm_out, cnt_emb, cnt_first, err, nullptr, 0};
   DL_DISPATCH_E(L->emb_dim, hipLaunchKernelGGL((pool_fwd_kernel<kE, false>), dim3(emb_grid(L->batch)),
                                                dim3(256), 0, as_stream(stream), a));
   DL_RETURN_LAUNCH("dl_pool_fwd");
@@ -643,7 +656,7 @@ extern "C" int dl_pool_fwd_indexed(const dl_emb_layout* L, const float* rows, co
   DL_CHECK_ARG(!rows_first || (fm_out && cnt_first), "first-order pooling needs fm_out/cnt_first");
   if (L->batch == 0 || n_slots == 0) return 0;
   PoolArgs a{*L, inv, inv_base, rows, rows_first, nullptr, 0, slot_start, slot_end, n_slots, fm_col,
-             x0, fm_out, cnt_emb, cnt_first, nullptr};
+             x0, fm_out, cnt_emb, cnt_first, nullptr, nullptr, 0};
   DL_DISPATCH_E(L->emb_dim, hipLaunchKernelGGL((pool_fwd_kernel<kE, true>), dim3(emb_grid(L->batch)),
                                                dim3(256), 0, as_stream(stream), a));
   DL_RETURN_LAUNCH("dl_pool_fwd_indexed");
@@ -658,10 +671,44 @@ extern "C" int dl_pool_bwd(const dl_emb_layout* L, const int64_t* ids, int32_t i
   if (int rc = check_layout(L)) return rc;
   if (L->batch == 0 || n_slots == 0) return 0;
   PoolBwdArgs a{*L, ids, ids_col, slot_start, slot_end, n_slots, fm_col, x0, fm_sum, dz, w_head,
-                dx0, dx0_pool_col, cnt_emb, cnt_first, g_table, g_first, touched};
+                dx0, dx0_pool_col, cnt_emb, cnt_first, g_table, g_first, touched, nullptr, 0};
   DL_DISPATCH_E(L->emb_dim, hipLaunchKernelGGL(pool_bwd_kernel<kE>, dim3(emb_grid(L->batch)),
                                                dim3(256), 0, as_stream(stream), a));
   DL_RETURN_LAUNCH("dl_pool_bwd");
+}
+
+extern "C" int dl_pool_fwd_weighted(const dl_emb_layout* L, const float* table, const int64_t* ids,
+                                    int32_t ids_col, const float* values, int32_t values_ld,
+                                    const int32_t* slot_start, const int32_t* slot_end, int32_t n_slots,
+                                    float* x0, float* cnt_emb, int32_t* err, void* stream) {
+  if (int rc = check_layout(L)) return rc;
+  DL_CHECK_ARG(table && ids && values && x0 && cnt_emb && slot_start && slot_end && n_slots >= 0,
+               "NULL argument");
+  DL_CHECK_ARG(values_ld >= 0, "bad values_ld");
+  DL_CHECK_ARG(L->x0_pool_col % 4 == 0, "x0_pool_col must be a multiple of 4");
+  if (L->batch == 0 || n_slots == 0) return 0;
+  PoolArgs a{*L, nullptr, 0, table, nullptr, ids, ids_col, slot_start, slot_end, n_slots, 0,
+             x0, nullptr, cnt_emb, nullptr, err, values, values_ld};
+  DL_DISPATCH_E(L->emb_dim, hipLaunchKernelGGL((pool_fwd_kernel<kE, false, true>), dim3(emb_grid(L->batch)),
+                                               dim3(256), 0, as_stream(stream), a));
+  DL_RETURN_LAUNCH("dl_pool_fwd_weighted");
+}
+
+extern "C" int dl_pool_bwd_weighted(const dl_emb_layout* L, const int64_t* ids, int32_t ids_col,
+                                    const float* values, int32_t values_ld, const int32_t* slot_start,
+                                    const int32_t* slot_end, int32_t n_slots, const float* dx0,
+                                    int32_t dx0_pool_col, const float* cnt_emb, float* g_table,
+                                    uint8_t* touched, void* stream) {
+  if (int rc = check_layout(L)) return rc;
+  DL_CHECK_ARG(!L->use_fm, "weighted pooling is a deep-only lookup (dnn_multi_textline.py:94-103)");
+  DL_CHECK_ARG(ids && values && dx0 && cnt_emb && g_table && touched && slot_start && slot_end,
+               "NULL argument");
+  if (L->batch == 0 || n_slots == 0) return 0;
+  PoolBwdArgs a{*L, ids, ids_col, slot_start, slot_end, n_slots, 0, nullptr, nullptr, nullptr, nullptr,
+                dx0, dx0_pool_col, cnt_emb, nullptr, g_table, nullptr, touched, values, values_ld};
+  DL_DISPATCH_E(L->emb_dim, hipLaunchKernelGGL((pool_bwd_kernel<kE, true>), dim3(emb_grid(L->batch)),
+                                               dim3(256), 0, as_stream(stream), a));
+  DL_RETURN_LAUNCH("dl_pool_bwd_weighted");
 }
 
 // ---------------------------------------------------------------------------

@@ -919,8 +919,9 @@ class CTREngine:
         torch.cuda.current_stream().wait_stream(s)
         return g
 
-    def predict(self, batch, logits=False):
-        """Forward only: returns sigmoid scores [B] (or the logits) as host numpy."""
+    def predict(self, batch, logits=False, device=False):
+        """Forward only: returns sigmoid scores [B] (or the logits) as host numpy, or as a
+        device tensor (a copy) with device=True."""
         B, indexed = self._begin(batch)
         s = _lib.stream_handle()
         if not indexed:
@@ -928,7 +929,8 @@ class CTREngine:
         self._forward(B, s)
         self._release()
         self.check_error()
-        return (self.z if logits else self.score)[:B].cpu().numpy()
+        out = (self.z if logits else self.score)[:B]
+        return out.clone() if device else out.cpu().numpy()
 
     def loss(self):
         """Loss of the last training step: data term + the L2 terms on the pre-update

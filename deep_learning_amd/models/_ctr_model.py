@@ -32,7 +32,7 @@ import torch
 import inspect
 
 from ..engine import FAMILIES, CTREngine, ModelSpec, default_adam
-from ..metrics import roc_auc
+from ..metrics import AucAccumulator
 
 
 def _spec_from_args(model, args):
@@ -130,16 +130,15 @@ class CTRModel:
     def eval(self, sess, val_data):
         if self.engine is None:
             self.model_optimizer()
-        preds, labels = [], []
+        acc = AucAccumulator()
         for i in range(len(val_data[0])):
             batch = {"label": val_data[0][i], "cate_feats": val_data[2][i]}
             if val_data[1][i] is not None:
                 batch["cont_feats"] = val_data[1][i]
             if val_data[3][i] is not None:
                 batch["vector_feats"] = val_data[3][i]
-            preds.extend(_predict_batches(self.engine, batch))
-            labels.extend(np.asarray(val_data[0][i]).reshape(-1).tolist())
-        return roc_auc(labels, preds)
+            acc.add(val_data[0][i], _predict_batches(self.engine, batch))
+        return acc.result()
 
     # --------------------------------------------------------------- checkpoints
     def _save_checkpoint(self, directory):
@@ -185,13 +184,14 @@ def _load_adam_state(eng, d):
 
 
 def _predict_batches(eng, batch, logits=False):
-    """Forward in chunks of the engine's max batch; returns a list of scores (or logits)."""
+    """Forward in chunks of the engine's max batch; returns the scores (or logits) as one
+    device tensor."""
     n = np.asarray(batch["label"]).shape[0]
     out = []
     for s in range(0, n, eng.B):
         part = {k: np.asarray(v)[s:s + eng.B] for k, v in batch.items()}
-        out.extend(eng.predict(part, logits=logits).tolist())
-    return out
+        out.append(eng.predict(part, logits=logits, device=True))
+    return torch.cat(out) if len(out) > 1 else out[0]
 
 
 SIGNATURE = {"inputs": ["cont_feats", "cate_feats", "vector_feats", "input_data_size"], "outputs": ["score"],
@@ -222,14 +222,13 @@ def load_model(model_pb, max_batch=None):
 def predict(predict_data, model_pb):
     """Loads the exported model and scores predict_data (deepfm_pipeline.py:314-346)."""
     eng = None
-    preds, labels = [], []
+    acc = AucAccumulator()
     for b in predict_data:
         if eng is None:
             eng = load_model(model_pb, max_batch=np.asarray(b["label"]).shape[0])
-        preds.extend(_predict_batches(eng, b))
-        labels.extend(np.asarray(b["label"]).reshape(-1).tolist())
+        acc.add(b["label"], _predict_batches(eng, b))
     print("-----------end of data_set-----------")
-    auc = roc_auc(labels, preds)
+    auc = acc.result()
     print("val of auc:%.5f" % auc)
     sys.stdout.flush()
     print('---end---')

@@ -20,7 +20,7 @@ import time
 import numpy as np
 
 from ..engine import CTREngine, default_adam
-from ..metrics import roc_auc
+from ..metrics import AucAccumulator
 from ._ctr_model import _predict_batches, export_model, load_model
 
 
@@ -84,21 +84,19 @@ class LoadStyleModel:
 
     def evaluate(self, sess, data_val):
         eng = self.model_optimizer()
-        preds, labels = [], []
+        acc = AucAccumulator()
         for item in data_val:
             b = self.batch(item)
-            labels.extend(b["label"].reshape(-1).tolist())
-            preds.extend(_predict_batches(eng, b, logits=self.EVAL_OUTPUT == "logit"))
-        return roc_auc(labels, preds)
+            acc.add(b["label"], _predict_batches(eng, b, logits=self.EVAL_OUTPUT == "logit"))
+        return acc.result()
 
     def predict(self, data_val):
         eng = load_model(self.model_pb, max_batch=self.batch_size)
-        preds, labels = [], []
+        acc = AucAccumulator()
         for item in data_val:
             b = self.batch(item)
-            labels.extend(b["label"].reshape(-1).tolist())
-            preds.extend(_predict_batches(eng, b))
-        auc = roc_auc(labels, preds)
+            acc.add(b["label"], _predict_batches(eng, b))
+        auc = acc.result()
         print("val of auc:%.5f" % auc)
         sys.stdout.flush()
         print('---end---')

@@ -178,6 +178,22 @@ int dl_pool_bwd(const dl_emb_layout* L, const int64_t* ids, int32_t ids_col,
                 const float* w_head, const float* dx0, int32_t dx0_pool_col,
                 const float* cnt_emb, const float* cnt_first, float* g_table,
                 float* g_first, uint8_t* touched, void* stream);
+/* Weighted nonzero-mean pooling (models/dnn_multi_textline.py:94-103, the deep-only
+ * multi-hot lookup of the textline DNN): pooled = div_no_nan(sum_l value_l * V[id_l], cnt)
+ * with cnt = count_nonzero(sum_E V[id_l]) of the UNweighted rows (:94-95).  values [B,
+ * values_ld] f32, the value of multi position l (same column numbering as the slot ranges,
+ * relative to ids_col).  The frozen word2vec table of slot 'tag' (:45-47,85-88) is a
+ * separate dl_pool_fwd_weighted call with that table and no backward.  The backward
+ * scatter-adds value_l * d pooled / cnt into g_table (f32 atomics) and marks touched. */
+int dl_pool_fwd_weighted(const dl_emb_layout* L, const float* table, const int64_t* ids,
+                         int32_t ids_col, const float* values, int32_t values_ld,
+                         const int32_t* slot_start, const int32_t* slot_end, int32_t n_slots,
+                         float* x0, float* cnt_emb, int32_t* err, void* stream);
+int dl_pool_bwd_weighted(const dl_emb_layout* L, const int64_t* ids, int32_t ids_col,
+                         const float* values, int32_t values_ld, const int32_t* slot_start,
+                         const int32_t* slot_end, int32_t n_slots, const float* dx0,
+                         int32_t dx0_pool_col, const float* cnt_emb, float* g_table,
+                         uint8_t* touched, void* stream);
 
 /* ------------------------------------------------------------------------
  * Dense tower: fp32 GEMM on v_mfma_f32_16x16x4_f32 (exact fp32, k-ordered fma).
@@ -370,6 +386,18 @@ int dl_keys_to_local(const uint32_t* keys, const int32_t* n_uniq, int64_t cap, i
 /* Counter-based (Philox-4x32-10) init: dist 0 normal(mean, scale), 1 uniform[mean, mean+scale). */
 int dl_init_random(float* p, int64_t n, int32_t dist, float mean, float scale, uint64_t seed,
                    uint64_t offset, void* stream);
+
+/* ------------------------------------------------------------------------
+ * Evaluation metric (metrics.hip): exact tie-aware ROC-AUC, the semantics of
+ * sklearn.metrics.roc_auc_score that the reference calls on the collected scores
+ * (models/deepfm_pipeline.py:311,344; wdl.py:343-358; deepfm.py:229).
+ * scores[i * s_stride], labels[i * l_stride] (label > 0.5 = positive), n <= 2^31-1.
+ * Writes the AUC to out[0] (device double; NaN when only one class is present, where
+ * sklearn raises).  The numerator is an exact integer count (ties: 1/2), so the result
+ * is deterministic.  Workspace: dl_auc_workspace_bytes(n). */
+int64_t dl_auc_workspace_bytes(int64_t n);
+int dl_auc(const float* scores, int64_t s_stride, const float* labels, int64_t l_stride, int64_t n,
+           void* ws, int64_t ws_bytes, double* out, void* stream);
 
 #ifdef __cplusplus
 }

@@ -206,6 +206,40 @@ def _pool(cfg, V, w1, multi):
             np.concatenate(c1, 1) if (M and w1 is not None) else None)
 
 
+def pool_weighted(V, ids, values, ranges):
+    """Weighted nonzero-mean pooling of models/dnn_multi_textline.py:89-103 (deep-only).
+    V: table with row 0 already zeroed (:43); ids, values: [B, W] multi-hot block and its
+    per-position values (mul_cat_feats / mul_cat_feats_value, :57-58).  Per slot:
+    cnt = count_nonzero(reduce_sum(V[ids], axis=2)) (:94-95, UNweighted rows),
+    out = div_no_nan(reduce_sum(V[ids] * value, axis=1), cnt) (:97-102).
+    Returns pooled [B, M, E] and cnt [B, M]."""
+    outs, cnts = [], []
+    for (a, b_, *_) in ranges:
+        emb = V[ids[:, a:b_]]                                                    # :88-89
+        cnt = (emb.sum(axis=2) != 0).sum(axis=1, keepdims=True).astype(V.dtype)  # :94-95
+        s = (emb * values[:, a:b_, None].astype(V.dtype)).sum(axis=1)            # :97-101
+        outs.append(np.where(cnt > 0, s / np.where(cnt > 0, cnt, 1), 0).astype(V.dtype))  # :102
+        cnts.append(cnt)
+    return np.stack(outs, 1), np.concatenate(cnts, 1)
+
+
+def pool_weighted_bwd(n_rows, ids, values, ranges, cnt, d_pooled, zero_row0=True):
+    """Gradient of pool_weighted w.r.t. the table (dense [n_rows, E]): every position l of
+    slot m adds value_l * d_pooled[b, m] / cnt[b, m] (0 when cnt = 0) to its row; row 0
+    (the concatenated zero row, :43) receives none."""
+    E = d_pooled.shape[2]
+    G = np.zeros((n_rows, E), d_pooled.dtype)
+    for m, (a, b_, *_) in enumerate(ranges):
+        c = cnt[:, m:m + 1]
+        gv = np.where(c > 0, d_pooled[:, m] / np.where(c > 0, c, 1), 0)         # [B, E]
+        idl = ids[:, a:b_]
+        contrib = values[:, a:b_, None].astype(G.dtype) * gv[:, None, :]
+        np.add.at(G, idl.reshape(-1), contrib.reshape(-1, E))
+    if zero_row0:
+        G[0] = 0
+    return G
+
+
 def forward(cfg, P, batch, dtype=F32):
     """Returns dict with x0, hs (post-ReLU activations), feats (head input),
     z (logit), p (score) and model-specific intermediates."""

@@ -1,6 +1,7 @@
 """Kernel-level GPU tests: each HIP entry point against an independent reference
 (torch fp64 for the GEMM, the numpy oracle for the embedding/FM/pooling math).
 Integer/index outputs (gathered rows, pooling counts) are compared bit-exact."""
+import ctypes as C
 import numpy as np
 import pytest
 import torch
@@ -295,3 +296,87 @@ def test_chain_apply_equals_sorted_segment_apply(hip_lib):
     assert bool((head == -1).all())
     touched = np.unique(ids.numpy())
     assert (recB.view(torch.int32)[:, E + 3].cpu().numpy()[touched] == 10).all()
+
+
+@pytest.mark.parametrize("E", [8, 16])
+def test_pool_weighted_matches_oracle(hip_lib, E):
+    """dl_pool_fwd_weighted / dl_pool_bwd_weighted (dnn_multi_textline.py:89-103) against
+    oracle.pool_weighted: counts bit-exact, pooled vectors and table gradients at 1e-6."""
+    from oracle import ctr_ref as R
+    rng = np.random.default_rng(E)
+    B, N, W, S = 300, 5000, 97, 3
+    ranges = [[0, 30, "a"], [30, 90, "b"], [90, 97, "c"]]
+    V = rng.standard_normal((N, E)).astype(np.float32) * 0.1
+    V[11] = 0.0                                           # a real id with a zero row
+    ids = np.zeros((B, S + W), np.int64)                  # [S singles | multi block]
+    ids[:, :S] = rng.integers(1, N, (B, S))
+    multi = rng.integers(1, N, (B, W))
+    multi[rng.random((B, W)) < 0.5] = 0
+    multi[0] = 0
+    multi[1, :7] = 11
+    ids[:, S:] = multi
+    vals = (rng.random((B, W)) * 2).astype(np.float32)
+    vals[2, :10] = 0.0
+    Vz = V.copy(); Vz[0] = 0
+    ref_pooled, ref_cnt = R.pool_weighted(Vz, multi, vals, ranges)
+    M = len(ranges)
+    x0_ld, pool_col = 64 + M * E, 64
+    L = _lib.EmbLayout(n_rows=N, batch=B, emb_dim=E, cate_fields=S, cate_ld=S + W, use_fm=0, zero_row0=1,
+                       x0_ld=x0_ld, x0_pool_col=pool_col, dx0_ld=x0_ld)
+    dev = lambda a: torch.from_numpy(np.ascontiguousarray(a)).cuda()
+    tab, idt, vt = dev(V), dev(ids), dev(vals)
+    s0 = torch.tensor([r[0] for r in ranges], dtype=torch.int32, device="cuda")
+    s1 = torch.tensor([r[1] for r in ranges], dtype=torch.int32, device="cuda")
+    x0 = torch.zeros(B, x0_ld, device="cuda")
+    cnt = torch.zeros(B, M, device="cuda")
+    err = torch.zeros(4, dtype=torch.int32, device="cuda")
+    call("dl_pool_fwd_weighted", C.byref(L), ptr(tab), ptr(idt), S, ptr(vt), W, ptr(s0), ptr(s1), M,
+         ptr(x0), ptr(cnt), ptr(err), _s())
+    torch.cuda.synchronize()
+    assert int(err[0]) == 0
+    np.testing.assert_array_equal(cnt.cpu().numpy(), ref_cnt)
+    got = x0[:, pool_col:].cpu().numpy().reshape(B, M, E)
+    np.testing.assert_allclose(got, ref_pooled, rtol=1e-5, atol=1e-6)
+    assert (x0[:, :pool_col] == 0).all()
+    # backward: dx0 at the pooled columns
+    d = rng.standard_normal((B, M, E)).astype(np.float32)
+    dx0 = torch.zeros(B, x0_ld, device="cuda")
+    dx0[:, pool_col:] = dev(d.reshape(B, -1))
+    g = torch.zeros(N, E, device="cuda")
+    touched = torch.zeros(N, dtype=torch.uint8, device="cuda")
+    call("dl_pool_bwd_weighted", C.byref(L), ptr(idt), S, ptr(vt), W, ptr(s0), ptr(s1), M, ptr(dx0), pool_col,
+         ptr(cnt), ptr(g), ptr(touched), _s())
+    torch.cuda.synchronize()
+    G = R.pool_weighted_bwd(N, multi, vals.astype(np.float64), ranges, ref_cnt.astype(np.float64),
+                            d.astype(np.float64))
+    np.testing.assert_allclose(g.cpu().numpy(), G, rtol=1e-5, atol=1e-6)
+    want_touched = np.zeros(N, np.uint8)
+    for a, b_, _ in ranges:
+        want_touched[multi[:, a:b_].reshape(-1)] = 1
+    want_touched[0] = 0
+    np.testing.assert_array_equal(touched.cpu().numpy(), want_touched)
+
+
+def test_auc_gpu_matches_sklearn_goldens_and_oracle(hip_lib):
+    """dl_auc (metrics.hip) against the committed sklearn goldens and the oracle on a
+    tie-heavy 2M-sample set (float32 scores, as the reference's score tensor)."""
+    import os
+    from deep_learning_amd.metrics import AucAccumulator, roc_auc
+    from oracle import ctr_ref as R
+    d = np.load(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "auc_golden.npz"))
+    for case in ("ties", "random", "all_tied"):
+        y, s = d[case + "_y"], d[case + "_s"].astype(np.float32)
+        assert abs(roc_auc(y, s) - R.auc(y, s)) < 1e-12
+        assert abs(roc_auc(y, s) - d[case + "_auc"][0]) < 1e-7
+    rng = np.random.default_rng(11)
+    n = 2_000_003
+    s = (np.round(rng.random(n) * 1000) / 1000 - 0.5).astype(np.float32)   # ties, both signs
+    s[:1000] = -0.0                                                        # -0.0 ties with +0.0
+    s[1000:2000] = 0.0
+    y = (rng.random(n) < 0.5 + 0.3 * s).astype(np.float32)
+    acc = AucAccumulator()
+    for a in range(0, n, 700_001):                                        # ragged batches
+        acc.add(torch.from_numpy(y[a:a + 700_001]).cuda(), torch.from_numpy(s[a:a + 700_001]).cuda())
+    assert abs(acc.result() - R.auc(y, s)) < 1e-12
+    with pytest.raises(ValueError, match="one class"):
+        roc_auc(np.ones(10), np.arange(10.0))

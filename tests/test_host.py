@@ -10,7 +10,6 @@ import tempfile
 import numpy as np
 import pytest
 
-from deep_learning_amd.metrics import roc_auc
 from deep_learning_amd.synthetic import make_batch
 from deep_learning_amd.utils import data_loader, my_utils, tfrecord
 
@@ -123,10 +122,13 @@ def test_loader_fixed_len_and_cate_algs(tmp_path):
 
 
 # ------------------------------------------------------------------ AUC
-def test_auc_matches_sklearn_goldens():
+def test_oracle_auc_matches_sklearn_goldens():
+    """The oracle AUC (the checker of the GPU dl_auc, tests/test_gpu_kernels.py) against
+    the sklearn goldens."""
+    from oracle import ctr_ref as R
     d = np.load(os.path.join(GOLD, "auc_golden.npz"))
     for case in ("ties", "random", "all_tied"):
-        assert abs(roc_auc(d[case + "_y"], d[case + "_s"]) - d[case + "_auc"][0]) < 1e-12
+        assert abs(R.auc(d[case + "_y"], d[case + "_s"]) - d[case + "_auc"][0]) < 1e-12
 
 
 # ------------------------------------------------------------------ oracle fixtures

@@ -178,6 +178,37 @@ def test_adam_tf1_formula():
     assert opt.step == 3
 
 
+def test_weighted_pool_matches_autograd():
+    """dnn_multi_textline.py:89-103 weighted nonzero-mean pooling: forward vs a torch
+    restatement, backward vs autograd (fp64); the count ignores the values."""
+    rng = np.random.default_rng(5)
+    V = rng.standard_normal((50, 8))
+    V[0] = 0                      # the concatenated zero row (:43)
+    V[7] = 0                      # a real id whose row is zero: not counted
+    ids = rng.integers(0, 50, (9, 11))
+    ids[0] = 0                    # an all-padding sample: div_no_nan -> 0
+    ids[1, :6] = 7
+    vals = rng.random((9, 11)) * 3
+    vals[2, 1] = 0.0              # a zero value still counts (count is on the plain row)
+    ranges = [[0, 6, "a"], [6, 11, "b"]]
+    pooled, cnt = R.pool_weighted(V, ids, vals, ranges)
+    Vt = torch.tensor(V, requires_grad=True)
+    tab = torch.cat([torch.zeros(1, 8, dtype=torch.float64), Vt[1:]], 0)
+    outs = []
+    for a, b_, _ in ranges:
+        e = tab[torch.tensor(ids[:, a:b_])]
+        c = (e.sum(2) != 0).sum(1, keepdim=True).double()
+        s = (e * torch.tensor(vals[:, a:b_, None])).sum(1)
+        outs.append(torch.where(c > 0, s / c.clamp(min=1), torch.zeros_like(s)))
+    pt = torch.stack(outs, 1)
+    np.testing.assert_allclose(pooled, pt.detach().numpy(), rtol=1e-12, atol=1e-14)
+    assert cnt[0].tolist() == [0, 0] and cnt[1, 0] == 0
+    d = rng.standard_normal(pooled.shape)
+    (pt * torch.tensor(d)).sum().backward()
+    G = R.pool_weighted_bwd(50, ids, vals, ranges, cnt, d)
+    np.testing.assert_allclose(G, Vt.grad.numpy(), rtol=1e-10, atol=1e-12)
+
+
 def test_auc_matches_sklearn():
     from sklearn.metrics import roc_auc_score
     rng = np.random.default_rng(0)
