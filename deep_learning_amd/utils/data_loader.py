@@ -17,14 +17,14 @@ Differences: end of data is StopIteration (the reference raises tf.errors.OutOfR
 the iterator is re-iterable (each `iter()` starts over, like a fresh tf.Session); the
 shuffle is seeded by ``mp.shuffle_seed`` (None = unseeded like the reference) and can be
 disabled with ``mp.shuffle = 0`` so parity runs see identical batches.
+The reading itself is native (``NativeReader`` over libdlio.so, include/dlio.h).
 """
 import os
-import queue
-import threading
 
 import numpy as np
 
 from . import tfrecord
+from .native_reader import NativeReader
 
 CATE_ALGS = ("deepfm_cate", "dnn_cate", "dnn_multi_cate", "deepfm_multi_cate")
 
@@ -53,9 +53,11 @@ def parse_example(data, spec):
 
 
 class BatchStream:
-    """Re-iterable stream of batches (dicts of numpy arrays)."""
+    """Re-iterable stream of batches (dicts of numpy arrays).  Each ``iter()`` opens the
+    native reader (libdlio.so: framing + CRC-32C, shuffle buffer, FixedLenFeature parse on
+    ``threads`` C++ threads — num_parallel_calls=10 at data_loader.py:31 — and batching)."""
 
-    def __init__(self, mp, files, action_type, prefetch=4):
+    def __init__(self, mp, files, action_type, threads=10, depth=4):
         self.mp = mp
         self.files = list(files)
         self.repeat = int(mp.epochs) if action_type == "train" else 1
@@ -63,68 +65,14 @@ class BatchStream:
         self.bsz = int(mp.batch_size)
         self.shuffle = int(getattr(mp, "shuffle", 1))
         self.seed = getattr(mp, "shuffle_seed", None)
-        self.prefetch = prefetch
-
-    def _records(self):
-        for _ in range(self.repeat):
-            for f in self.files:
-                yield from tfrecord.read_records(f)
-
-    def _examples(self):
-        spec = self.spec
-        if not self.shuffle:
-            for r in self._records():
-                yield parse_example(r, spec)
-            return
-        rng = np.random.default_rng(self.seed)
-        buf = []
-        cap = self.bsz * 10
-        for r in self._records():
-            buf.append(parse_example(r, spec))
-            if len(buf) >= cap:
-                j = rng.integers(len(buf))
-                buf[j], buf[-1] = buf[-1], buf[j]
-                yield buf.pop()
-        while buf:
-            j = rng.integers(len(buf))
-            buf[j], buf[-1] = buf[-1], buf[j]
-            yield buf.pop()
-
-    def _batches(self):
-        keys = list(self.spec)
-        cur = []
-        for ex in self._examples():
-            cur.append(ex)
-            if len(cur) == self.bsz:
-                out = {}
-                for k in keys:
-                    kind = self.spec[k][0]
-                    arr = np.asarray([e[k] for e in cur], dtype=np.int64 if kind == "int64" else np.float32)
-                    out[k] = arr.reshape(self.bsz, -1)
-                yield out
-                cur = []
-        # drop_remainder=True
+        self.threads = int(getattr(mp, "reader_threads", threads))
+        self.depth = depth
 
     def __iter__(self):
-        q = queue.Queue(maxsize=self.prefetch)
-        stop = object()
-
-        def work():
-            try:
-                for b in self._batches():
-                    q.put(b)
-            except Exception as e:   # surfaced in the consumer
-                q.put(e)
-            q.put(stop)
-
-        threading.Thread(target=work, daemon=True).start()
-        while True:
-            item = q.get()
-            if item is stop:
-                return
-            if isinstance(item, Exception):
-                raise item
-            yield item
+        spec = [(k, kind, size) for k, (kind, size) in self.spec.items()]
+        return NativeReader(self.files, spec, self.bsz, repeat=self.repeat,
+                            shuffle_buf=self.bsz * 10 if self.shuffle else 0,   # shuffle(bsz*10), :34
+                            seed=self.seed, threads=self.threads, depth=self.depth)
 
 
 def get_file_list(input_path):

@@ -45,3 +45,19 @@ def test_library_loads_and_reports_errors(lib):
 def test_layout_struct_size(lib):
     import ctypes
     assert ctypes.sizeof(lib.EmbLayout) == 4 * 8 + 19 * 4 + 4  # 4 int64 + 19 int32 + pad
+
+
+def test_reader_header_symbols_exported():
+    """libdlio.so (native TFRecord reader) exports exactly what include/dlio.h declares."""
+    from deep_learning_amd.utils import native_reader as nr
+    if not os.path.exists(nr.LIB_PATH):
+        from deep_learning_amd import build
+        build.build_host(verbose=False)
+    src = open(os.path.join(ROOT, "include", "dlio.h")).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    declared = set(re.findall(r"^\s*(?:void\*|void|int32_t|int64_t|uint32_t|const char\*)\s+(dlio_\w+)\s*\(",
+                              src, flags=re.M))
+    out = subprocess.run(["nm", "-D", "--defined-only", nr.LIB_PATH], capture_output=True, text=True).stdout
+    exported = {l.split()[-1] for l in out.splitlines() if " T dlio_" in l}
+    assert len(declared) == 8 and declared == exported == set(nr.SIGNATURES)
+    nr.lib()

@@ -164,3 +164,101 @@ def test_load_style_loader(tmp_path):
     np.testing.assert_array_equal(d0["wide_feats"], b["wide_feats"][:40])
     np.testing.assert_allclose(d0["cont_feats"], b["cont_feats"][:40])
     assert pickle.loads(out[2])["labels"].shape == (20, 1)
+
+
+# ------------------------------------------------------------------ native reader (libdlio.so)
+def test_native_crc32c_known_answers():
+    from deep_learning_amd.utils import native_reader as nr
+    assert nr.crc32c(b"123456789") == 0xE3069283                 # CRC-32C check value
+    assert nr.crc32c(bytes(32)) == 0x8A9136AA                    # RFC 3720 B.4: 32 zero bytes
+    assert nr.crc32c(b"\xff" * 32) == 0x62A8AB43                 # RFC 3720 B.4: 32 0xff bytes
+    rng = np.random.default_rng(0)
+    for n in (0, 1, 7, 8, 9, 63, 1000):
+        b = rng.integers(0, 256, n, dtype=np.uint8).tobytes()
+        assert nr.crc32c(b) == tfrecord.crc32c(b)
+
+
+@pytest.mark.parametrize("threads", [1, 3, 10])
+def test_native_reader_matches_python_decoder(tmp_path, threads):
+    """Unshuffled batches of the native reader equal the pure-Python decode of the same
+    files (file order, drop_remainder, repeat), for any decoder thread count."""
+    src = _write_parts(str(tmp_path), n_parts=3, per=70)
+    files = sorted(data_loader.get_file_list(str(tmp_path) + "/"))
+    spec = data_loader._spec(_MP())
+    exs = [data_loader.parse_example(r, spec) for _ in range(2) for f in files for r in tfrecord.read_records(f)]
+    from deep_learning_amd.utils.native_reader import NativeReader
+    got = list(NativeReader(files, [(k, kd, s) for k, (kd, s) in spec.items()], 32, repeat=2, threads=threads))
+    assert len(got) == (2 * 210) // 32
+    for i, b in enumerate(got):
+        for k, (kind, size) in spec.items():
+            want = np.asarray([e[k] for e in exs[i * 32:(i + 1) * 32]],
+                              np.int64 if kind == "int64" else np.float32).reshape(32, size)
+            np.testing.assert_array_equal(b[k], want, err_msg=k)
+    flat = np.concatenate([s["cate_feats"] for s in src])
+    np.testing.assert_array_equal(got[0]["cate_feats"], flat[:32])
+
+
+def test_native_reader_seeded_shuffle(tmp_path):
+    _write_parts(str(tmp_path), n_parts=2, per=100)
+    files = sorted(data_loader.get_file_list(str(tmp_path) + "/"))
+    run = lambda seed: np.concatenate([b["cate_feats"] for b in data_loader.pipeline_process(
+        _MP(shuffle=1, shuffle_seed=seed, batch_size=20), files, "pred")])
+    plain = np.concatenate([b["cate_feats"] for b in data_loader.pipeline_process(_MP(batch_size=20), files, "pred")])
+    a, a2, b = run(5), run(5), run(6)
+    np.testing.assert_array_equal(a, a2)                         # deterministic for a seed
+    assert not np.array_equal(a, plain) and not np.array_equal(a, b)
+    key = lambda m: sorted(map(tuple, m))
+    assert key(a) == key(plain)                                  # a permutation of the records
+
+
+def test_native_reader_errors(tmp_path):
+    from deep_learning_amd.utils.native_reader import NativeReader
+    _write_parts(str(tmp_path), n_parts=1, per=40)
+    f = str(tmp_path / "part-00000")
+    spec = [(k, kd, s) for k, (kd, s) in data_loader._spec(_MP()).items()]
+    with pytest.raises(ValueError, match="Key: cont_feats. Can't parse serialized Example: expected 12"):
+        list(NativeReader([f], [(k, kd, 12 if k == "cont_feats" else s) for k, kd, s in spec], 8))
+    with pytest.raises(ValueError, match="Data types don't match"):
+        list(NativeReader([f], [(k, "float" if k == "cate_feats" else kd, s) for k, kd, s in spec], 8))
+    with pytest.raises(IOError, match="No such file"):
+        NativeReader([f + "x"], spec, 8)
+    raw = bytearray(open(f, "rb").read())
+    bad = tmp_path / "part-bad"
+    raw2 = bytearray(raw)
+    raw2[30] ^= 0x01                                             # payload byte of record 0
+    bad.write_bytes(bytes(raw2))
+    with pytest.raises(IOError, match="corrupted record data"):
+        list(NativeReader([str(bad)], spec, 8))
+    raw3 = bytearray(raw)
+    raw3[0] ^= 0x01                                              # length field of record 0
+    bad.write_bytes(bytes(raw3))
+    with pytest.raises(IOError, match="corrupted record length"):
+        list(NativeReader([str(bad)], spec, 8))
+    bad.write_bytes(bytes(raw[:-3]))                             # truncated last record
+    with pytest.raises(IOError, match="truncated"):
+        list(NativeReader([str(bad)], spec, 8))
+
+
+def test_native_reader_wire_variants(tmp_path):
+    """Unpacked float/int64 lists, a feature outside the spec, a repeated key (map
+    semantics: the last entry wins) and negative int64 varints decode like the spec says."""
+    from deep_learning_amd.utils.native_reader import NativeReader
+    v = tfrecord._varint
+    ld = tfrecord._len_field
+
+    def entry(name, feat):
+        return ld(1, ld(1, name.encode()) + ld(2, feat))
+
+    unpacked_f = ld(2, b"".join(v((1 << 3) | 5) + struct.pack("<f", x) for x in (1.5, -2.0)))
+    unpacked_i = ld(3, b"".join(v((1 << 3) | 0) + v(x) for x in (7, -3)))
+    stale = ld(3, ld(1, v(99) + v(98)))
+    label = ld(2, ld(1, struct.pack("<f", 1.0)))
+    extra = ld(1, ld(1, b"abc"))
+    ex = ld(1, entry("cont", unpacked_f) + entry("ids", stale) + entry("junk", extra) + entry("ids", unpacked_i)
+            + entry("label", label))
+    p = str(tmp_path / "part-w")
+    tfrecord.write_records(p, [ex] * 3)
+    b = next(NativeReader([p], [("label", "float", 1), ("cont", "float", 2), ("ids", "int64", 2)], 3))
+    np.testing.assert_array_equal(b["cont"], [[1.5, -2.0]] * 3)
+    np.testing.assert_array_equal(b["ids"], [[7, -3]] * 3)
+    np.testing.assert_array_equal(b["label"], [[1.0]] * 3)
