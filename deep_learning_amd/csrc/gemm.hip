@@ -242,12 +242,16 @@ void gemm_f32_kernel(GemmParams p) {
     __syncthreads();
   }
   const int kr = lane >> 4, cl = lane & 15;
+  // A wave whose rows (or columns) all lie past M (N) still stages and meets the barriers
+  // but issues no LDS reads or MFMAs: the ragged last M tile of the dW products (M = 416 /
+  // 432 in 128-row tiles) then costs its staging, not four waves of MFMA time.
+  const bool live = FAST || (i0 + wm * WTM < p.M && j0 + wn * WTN < p.N);
   for (int kt = 0; kt < nk; ++kt) {
     const int cur = kt & 1;
     if (GLDS && kt + 1 < nk) glds_a(kbeg + (kt + 1) * BK, cur ^ 1);
     if (kt + 1 < nk) load_tile(kbeg + (kt + 1) * BK);
 #pragma unroll
-    for (int s16 = 0; s16 < BK / 16; ++s16) {
+    for (int s16 = 0; s16 < (live ? BK / 16 : 0); ++s16) {
       float4 a4[AKC ? FM : 1], b4[BKC ? FN : 1];
       if (AKC) {
 #pragma unroll

@@ -22,8 +22,10 @@ cases = {
     "dx_l1": lambda: call("dl_gemm_f32", 0, 0, B, 400, 400, ptr(dh), 416, ptr(Wt), 432, ptr(h), 416, 2, ptr(x0), 432, 1, 0, s),
     "dw_l1": lambda: call("dl_gemm_f32", 1, 0, 416, 400, B, ptr(h), 416, ptr(dh), 416, ptr(slab), 400, 3, None, 0, 64,
                           416 * 400, s),
+    "dw_l0": lambda: call("dl_gemm_f32", 1, 0, 432, 400, B, ptr(x0), 432, ptr(dh), 416, ptr(slab), 400, 3, None, 0, 64,
+                          432 * 400, s),
 }
-flops = {"fwd_l0": 2 * B * 433 * 400, "fwd_l1": 2 * B * 417 * 400, "dx_l1": 2 * B * 400 * 400, "dw_l1": 2 * B * 417 * 400}
+flops = {"fwd_l0": 2 * B * 433 * 400, "fwd_l1": 2 * B * 417 * 400, "dx_l1": 2 * B * 400 * 400, "dw_l1": 2 * B * 417 * 400, "dw_l0": 2 * B * 433 * 400}
 for name, fn in cases.items():
     for _ in range(3):
         fn()
