@@ -15,6 +15,7 @@
 //              cont-field rows (hit by every sample) accumulate in registers
 //              and leave the block once as a partial slab.
 #include "common.h"
+#include "rec.h"
 #include "segment.h"
 
 namespace dl {
@@ -32,6 +33,14 @@ struct EmbArgs {
   float* fm_out;
   float* fm_sum;
   int32_t* err;
+  // record mode (single GPU, lazy Adam): the cate rows are read straight from the row
+  // records and caught up to step opt[7] - lag in registers; `table` / `first_order`
+  // then hold only the C replicated FM cont-field rows (compact, caught up by dl_rec_gather)
+  const float* rec;
+  RecCfg rc;
+  const float* hist;
+  const float* opt;
+  int lag;
 };
 
 __device__ __forceinline__ bool row_ok(int64_t row, int zero_row0) {
@@ -45,7 +54,7 @@ constexpr int kMaxHotContFwd = 32;
 constexpr int kTileSamples = 16;   // samples staged per block iteration
 constexpr int kMaxSlots = 128;     // FM slots + deep slots per sample
 
-template <int E, int NPS>
+template <int E, int NPS, bool REC = false>
 __global__ __launch_bounds__(256) void embed_fwd_kernel(EmbArgs a) {
   // Per block iteration a tile of 16 samples is staged: every (sample, slot)
   // row index is resolved once into LDS by a coalesced pass over the id matrix
@@ -69,6 +78,16 @@ __global__ __launch_bounds__(256) void embed_fwd_kernel(EmbArgs a) {
   const float4* tab4 = reinterpret_cast<const float4*>(a.table);
   const float4 z4 = f4_zero();
   const int ntiles = (L.batch + kTileSamples - 1) / kTileSamples;
+  RecCfg rc = a.rc;
+  int target = 0;
+  extern __shared__ float hist_s[];   // record mode: the alpha ring, so the catch-up loop's
+                                      // per-step reads are LDS hits, not L2 round trips
+  if (REC) {
+    rec_load_hyper(rc, a.opt);
+    target = (int)a.opt[7] - a.lag;
+    for (int k = threadIdx.x; k <= rc.hist_mask; k += blockDim.x) hist_s[k] = a.hist[k];
+    __syncthreads();
+  }
 
   for (int t = blockIdx.x; t < ntiles; t += gridDim.x) {
     const int b0 = t * kTileSamples;
@@ -133,12 +152,44 @@ __global__ __launch_bounds__(256) void embed_fwd_kernel(EmbArgs a) {
         rw[p] = rows_s[j][sl < nslot ? sl : 0];
         if (sl >= nslot) rw[p] = -1;
       }
+      if (!REC) {
 #pragma unroll
-      for (int p = 0; p < NPS; ++p) v[p] = tab4[(rw[p] < 0 ? 0 : rw[p]) * LPR + q];
-      // first-order terms (one lane per FM field)
+        for (int p = 0; p < NPS; ++p) v[p] = tab4[(rw[p] < 0 ? 0 : rw[p]) * LPR + q];
+      } else {
+        // slots >= Cf: the whole record (p, m, v, first-order triple + stamp) is loaded for
+        // every pass before any is consumed, then caught up exactly as dl_rec_gather does
+        // (same catch_up4 on the same float4): the values are bit-identical to the
+        // gathered rows the indexed forward reads.
+        float4 m4[NPS], v4[NPS], t4[NPS];
+#pragma unroll
+        for (int p = 0; p < NPS; ++p) {
+          const int sl = p * RPI + r;
+          if (sl < Cf) {
+            v[p] = tab4[(rw[p] < 0 ? 0 : rw[p]) * LPR + q];
+          } else {
+            const float* rr = a.rec + (int64_t)(rw[p] < 0 ? 0 : rw[p]) * rc.ld;
+            v[p] = *reinterpret_cast<const float4*>(rr + 4 * q);
+            m4[p] = *reinterpret_cast<const float4*>(rr + E + 4 + 4 * q);
+            v4[p] = *reinterpret_cast<const float4*>(rr + 2 * E + 4 + 4 * q);
+            t4[p] = *reinterpret_cast<const float4*>(rr + E);
+          }
+        }
+#pragma unroll
+        for (int p = 0; p < NPS; ++p) {
+          const int sl = p * RPI + r;
+          if (sl >= Cf && sl < nslot) {
+            const bool fmf = sl < Fs && rc.has_first && q == 0;   // FM slot: its first-order weight too
+            float w = t4[p].x, wm = t4[p].y, wv = t4[p].z;
+            const int stamp = __float_as_int(t4[p].w);
+            if (stamp < target) catch_up4(v[p], m4[p], v4[p], w, wm, wv, fmf, stamp, target, hist_s, rc);
+            if (fmf) a.fm_out[(int64_t)b * L.fm_ld + sl] = rw[p] < 0 ? 0.f : w * 1.f;
+          }
+        }
+      }
+      // first-order terms (one lane per FM field; record mode: the cont fields only)
       float w1 = 0.f, val = 0.f;
       int frow = -1;
-      if (lane < Fs) {
+      if (lane < (REC ? Cf : Fs)) {
         frow = rows_s[j][lane];
         val = lane < Cf ? vals_s[j][lane] : 1.f;
         w1 = a.first_order[frow < 0 ? 0 : frow];
@@ -151,16 +202,20 @@ __global__ __launch_bounds__(256) void embed_fwd_kernel(EmbArgs a) {
           const float4 t4 = rw[p] < 0 ? z4 : v[p];
           if (sl < Fs) {
             const float vv = sl < Cf ? vals_s[j][sl] : 1.f;
-            const float4 ev = make_float4(t4.x * vv, t4.y * vv, t4.z * vv, t4.w * vv);
+            // explicit roundings (no contraction left to the compiler): every instantiation
+            // of this kernel (table, indexed, record) must produce the same FM sums
+            const float4 ev = make_float4(__fmul_rn(t4.x, vv), __fmul_rn(t4.y, vv), __fmul_rn(t4.z, vv),
+                                          __fmul_rn(t4.w, vv));
             s.x += ev.x; s.y += ev.y; s.z += ev.z; s.w += ev.w;
-            ss.x += ev.x * ev.x; ss.y += ev.y * ev.y; ss.z += ev.z * ev.z; ss.w += ev.w * ev.w;
+            ss.x = fmaf(ev.x, ev.x, ss.x); ss.y = fmaf(ev.y, ev.y, ss.y);
+            ss.z = fmaf(ev.z, ev.z, ss.z); ss.w = fmaf(ev.w, ev.w, ss.w);
           } else if (sl < nslot) {
             *reinterpret_cast<float4*>(xb + L.x0_cat_col + (sl - Fs) * E + 4 * q) = t4;
           }
         }
       }
-      if (lane < Fs) a.fm_out[(int64_t)b * L.fm_ld + lane] = frow < 0 ? 0.f : w1 * val;
-      for (int f = 64 + lane; f < Fs; f += 64) {   // > 64 FM fields (rare)
+      if (lane < (REC ? Cf : Fs)) a.fm_out[(int64_t)b * L.fm_ld + lane] = frow < 0 ? 0.f : w1 * val;
+      for (int f = 64 + lane; f < (REC ? 0 : Fs); f += 64) {   // > 64 FM fields (rare; record mode: <= 64)
         const int fr = rows_s[j][f];
         const float vv = f < Cf ? vals_s[j][f] : 1.f;
         a.fm_out[(int64_t)b * L.fm_ld + f] = fr < 0 ? 0.f : a.first_order[fr] * vv;
@@ -171,7 +226,8 @@ __global__ __launch_bounds__(256) void embed_fwd_kernel(EmbArgs a) {
           if (f < L.fm_extra) {
             const float4 ev = *reinterpret_cast<const float4*>(xb + L.x0_pool_col + f * E + 4 * q);
             s.x += ev.x; s.y += ev.y; s.z += ev.z; s.w += ev.w;
-            ss.x += ev.x * ev.x; ss.y += ev.y * ev.y; ss.z += ev.z * ev.z; ss.w += ev.w * ev.w;
+            ss.x = fmaf(ev.x, ev.x, ss.x); ss.y = fmaf(ev.y, ev.y, ss.y);
+            ss.z = fmaf(ev.z, ev.z, ss.z); ss.w = fmaf(ev.w, ev.w, ss.w);
           }
         }
 #pragma unroll
@@ -183,8 +239,8 @@ __global__ __launch_bounds__(256) void embed_fwd_kernel(EmbArgs a) {
         }
         if (r == 0) {
           float* fo = a.fm_out + (int64_t)b * L.fm_ld + F + 4 * q;
-          fo[0] = 0.5f * (s.x * s.x - ss.x); fo[1] = 0.5f * (s.y * s.y - ss.y);
-          fo[2] = 0.5f * (s.z * s.z - ss.z); fo[3] = 0.5f * (s.w * s.w - ss.w);
+          fo[0] = 0.5f * fmaf(s.x, s.x, -ss.x); fo[1] = 0.5f * fmaf(s.y, s.y, -ss.y);
+          fo[2] = 0.5f * fmaf(s.z, s.z, -ss.z); fo[3] = 0.5f * fmaf(s.w, s.w, -ss.w);
           if (a.fm_sum) *reinterpret_cast<float4*>(a.fm_sum + (int64_t)b * E + 4 * q) = s;
         }
       }
@@ -545,6 +601,7 @@ static int emb_grid(int B) {
 
 using namespace dl;
 
+template <bool REC>
 static int launch_embed_fwd(const dl_emb_layout* L, const EmbArgs& a, void* stream);
 
 extern "C" int dl_embed_fwd(const dl_emb_layout* L, const float* table, const float* first_order,
@@ -555,7 +612,7 @@ extern "C" int dl_embed_fwd(const dl_emb_layout* L, const float* table, const fl
   DL_CHECK_ARG(!L->use_fm || (first_order && fm_out && fm_sum), "FM outputs required");
   if (L->batch == 0) return 0;
   EmbArgs a{*L, nullptr, 0, table, first_order, cate, cont, vector, x0, fm_out, fm_sum, err};
-  return launch_embed_fwd(L, a, stream);
+  return launch_embed_fwd<false>(L, a, stream);
 }
 
 extern "C" int dl_embed_fwd_indexed(const dl_emb_layout* L, const float* rows, const float* rows_first,
@@ -566,19 +623,43 @@ extern "C" int dl_embed_fwd_indexed(const dl_emb_layout* L, const float* rows, c
   DL_CHECK_ARG(!L->use_fm || (rows_first && fm_out && fm_sum), "FM outputs required");
   if (L->batch == 0) return 0;
   EmbArgs a{*L, inv, inv_base, rows, rows_first, nullptr, cont, vector, x0, fm_out, fm_sum, nullptr};
-  return launch_embed_fwd(L, a, stream);
+  return launch_embed_fwd<false>(L, a, stream);
 }
 
+extern "C" int dl_embed_fwd_rec(const dl_emb_layout* L, const float* rec, int32_t rec_ld, int32_t has_first,
+                                const float* rows_rep, const float* rows_rep1, const int64_t* cate,
+                                const float* cont, const float* vector, const float* hist, int32_t hist_len,
+                                const float* opt, int32_t lag, float* x0, float* fm_out, float* fm_sum,
+                                int32_t* err, void* stream) {
+  if (int rc = check_layout(L)) return rc;
+  DL_CHECK_ARG(rec && cate && x0 && hist && opt, "NULL argument");
+  DL_CHECK_ARG(hist_len >= 2 && hist_len <= 8192 && (hist_len & (hist_len - 1)) == 0,
+               "hist_len must be a power of two in [2, 8192] (the ring is staged in LDS)");
+  DL_CHECK_ARG(rec_ld % 4 == 0 && rec_ld >= 3 * L->emb_dim + 4, "rec_ld %d too small", rec_ld);
+  DL_CHECK_ARG(L->multi_width == 0 && L->fm_extra == 0, "record forward: single-valued fields only");
+  const int Cf = (L->use_fm && L->fm_cont) ? L->cont_fields : 0;
+  DL_CHECK_ARG(Cf == 0 || (L->cont_rows_compact && rows_rep && (!has_first || rows_rep1)),
+               "the FM cont-field rows come compact in rows_rep / rows_rep1");
+  DL_CHECK_ARG(!L->use_fm || (fm_out && fm_sum && Cf + L->cate_fields <= 64), "FM outputs required (<= 64 fields)");
+  if (L->batch == 0) return 0;
+  EmbArgs a{*L, nullptr, 0, rows_rep, rows_rep1, cate, cont, vector, x0, fm_out, fm_sum, err,
+            rec, RecCfg{L->emb_dim, rec_ld, has_first, hist_len - 1, 0.f, 0.f, 0.f}, hist, opt, lag};
+  return launch_embed_fwd<true>(L, a, stream);
+}
+
+template <bool REC>
 static int launch_embed_fwd(const dl_emb_layout* L, const EmbArgs& a, void* stream) {
   DL_CHECK_ARG((L->use_fm ? (L->fm_cont ? L->cont_fields : 0) + 2 * L->cate_fields : L->cate_fields) <= kMaxSlots,
                "too many fields per sample for the gather kernel (max %d slots)", kMaxSlots);
   const int tiles = (L->batch + kTileSamples - 1) / kTileSamples;
-  const dim3 grid(tiles < 8192 ? tiles : 8192), block(256);
+  const int gmax = REC ? 1024 : 8192;   // record mode: each block stages the alpha ring once
+  const dim3 grid(tiles < gmax ? tiles : gmax), block(256);
   const int nslot = (L->use_fm ? (L->fm_cont ? L->cont_fields : 0) + L->cate_fields : 0) + L->cate_fields;
   const int rpi = 64 / (L->emb_dim / 4);
   const int nps = (nslot + rpi - 1) / rpi;
+  const size_t lds = REC ? (size_t)(a.rc.hist_mask + 1) * sizeof(float) : 0;
   hipStream_t st = as_stream(stream);
-#define DL_FWD(E_, N_) hipLaunchKernelGGL((embed_fwd_kernel<E_, N_>), grid, block, 0, st, a)
+#define DL_FWD(E_, N_) hipLaunchKernelGGL((embed_fwd_kernel<E_, N_, REC>), grid, block, lds, st, a)
   switch (L->emb_dim) {
     case 16:
       switch (nps) {

@@ -111,6 +111,139 @@ __global__ __launch_bounds__(256) void scatter_index_kernel(const uint32_t* __re
   }
 }
 
+// ---------------------------------------------------------------------------
+// Segmented unique over the sorted keys in two passes (replaces head flags + a device
+// scan + the scatter: three full passes and a decoupled-lookback scan):
+//   unique_count_kernel: heads per chunk of kUqChunk sorted keys -> chunk_cnt[c]
+//   unique_emit_kernel : one block per chunk; the chunk's exclusive offset is the sum of
+//                        the earlier chunks' counts (read from chunk_cnt, summed by the
+//                        block — a few thousand ints), then a block scan of the chunk's
+//                        head flags gives every element its unique id u, and the same
+//                        outputs as before are written (uniq, seg_off, n_uniq, inv,
+//                        owner group starts).
+constexpr int kUqIpt = 16;                  // keys per thread
+constexpr int kUqChunk = 256 * kUqIpt;      // keys per block
+
+__device__ __forceinline__ bool uq_head(const uint32_t* __restrict__ keys, int i, uint32_t k, uint32_t invalid) {
+  return k != invalid && (i == 0 || keys[i - 1] != k);
+}
+
+__global__ __launch_bounds__(256) void unique_count_kernel(const uint32_t* __restrict__ keys, int n, uint32_t invalid,
+                                                           int32_t* __restrict__ chunk_cnt) {
+  const int base = blockIdx.x * kUqChunk;
+  int c = 0;
+#pragma unroll
+  for (int u = 0; u < kUqIpt; ++u) {
+    const int i = base + u * 256 + threadIdx.x;   // coalesced: the count does not need the order
+    if (i < n) c += uq_head(keys, i, keys[i], invalid) ? 1 : 0;
+  }
+  c = __reduce_add_sync(~0ull, c);   // wave sum
+  __shared__ int ws[4];
+  if ((threadIdx.x & 63) == 0) ws[threadIdx.x >> 6] = c;
+  __syncthreads();
+  if (threadIdx.x == 0) chunk_cnt[blockIdx.x] = ws[0] + ws[1] + ws[2] + ws[3];
+}
+
+__global__ __launch_bounds__(256) void unique_emit_kernel(const uint32_t* __restrict__ keys, const int32_t* __restrict__ refs,
+                                                          int n, uint32_t invalid, const int32_t* __restrict__ chunk_cnt,
+                                                          uint32_t* __restrict__ uniq, int32_t* __restrict__ seg_off,
+                                                          int32_t* __restrict__ n_uniq, int32_t* __restrict__ inv,
+                                                          int32_t* __restrict__ owner_counts) {
+  __shared__ int wsum[4];
+  __shared__ int base_s;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  // exclusive offset of this chunk: sum of the earlier chunks' head counts
+  int off = 0;
+  for (int c = tid; c < (int)blockIdx.x; c += 256) off += chunk_cnt[c];
+  off = __reduce_add_sync(~0ull, off);
+  if (lane == 0) wsum[wid] = off;
+  __syncthreads();
+  if (tid == 0) base_s = wsum[0] + wsum[1] + wsum[2] + wsum[3];
+  __syncthreads();
+  const int base = base_s;
+  // this thread's kUqIpt consecutive keys
+  const int i0 = blockIdx.x * kUqChunk + tid * kUqIpt;
+  uint32_t k[kUqIpt];
+  int h = 0;
+  uint32_t prev = (i0 > 0 && i0 - 1 < n) ? keys[i0 - 1] : 0u;
+  if (i0 + kUqIpt <= n) {   // 64-B aligned run: four 16-B loads
+#pragma unroll
+    for (int q = 0; q < kUqIpt / 4; ++q) {
+      const uint4 v = reinterpret_cast<const uint4*>(keys + i0)[q];
+      k[4 * q] = v.x; k[4 * q + 1] = v.y; k[4 * q + 2] = v.z; k[4 * q + 3] = v.w;
+    }
+  } else {
+#pragma unroll
+    for (int u = 0; u < kUqIpt; ++u) k[u] = i0 + u < n ? keys[i0 + u] : invalid;
+  }
+#pragma unroll
+  for (int u = 0; u < kUqIpt; ++u) {
+    const int i = i0 + u;
+    const bool hd = i < n && k[u] != invalid && (i == 0 || (u == 0 ? prev : k[u - 1]) != k[u]);
+    h += hd ? 1 : 0;
+  }
+  // block exclusive scan of the per-thread head counts (wave scan + wave totals)
+  int x = h;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int y = __shfl_up(x, o, 64);
+    if (lane >= o) x += y;
+  }
+  __syncthreads();
+  if (lane == 63) wsum[wid] = x;
+  __syncthreads();
+  int wbase = 0;
+  for (int w = 0; w < wid; ++w) wbase += wsum[w];
+  int run = base + wbase + x - h;   // heads before this thread's first key
+  // the key after this thread's run and the refs of the run (16-B loads when whole);
+  // the loop below is fully unrolled (no break/continue: k[] stays in registers)
+  const uint32_t after = i0 + kUqIpt < n ? keys[i0 + kUqIpt] : invalid;
+  int32_t rf[kUqIpt];
+  if (inv) {
+    if (i0 + kUqIpt <= n) {
+#pragma unroll
+      for (int q = 0; q < kUqIpt / 4; ++q) {
+        const int4 v = reinterpret_cast<const int4*>(refs + i0)[q];
+        rf[4 * q] = v.x; rf[4 * q + 1] = v.y; rf[4 * q + 2] = v.z; rf[4 * q + 3] = v.w;
+      }
+    } else {
+#pragma unroll
+      for (int u = 0; u < kUqIpt; ++u) rf[u] = i0 + u < n ? refs[i0 + u] : 0;
+    }
+  }
+#pragma unroll
+  for (int u = 0; u < kUqIpt; ++u) {
+    const int i = i0 + u;
+    const uint32_t kk = k[u];
+    const uint32_t pk = u == 0 ? prev : k[u - 1];
+    const uint32_t nk = u + 1 < kUqIpt ? k[u + 1] : after;
+    const bool valid = i < n && kk != invalid;
+    const bool hd = valid && (i == 0 || pk != kk);
+    run += hd ? 1 : 0;
+    const int uu = run - 1;
+    if (hd) {
+      uniq[uu] = kk;
+      seg_off[uu] = i;
+      // first unique row of an owner group (keys sorted by owner): counts follow from the starts
+      if (owner_counts && (i == 0 || (pk >> kLocalBits) != (kk >> kLocalBits))) owner_counts[kk >> kLocalBits] = uu;
+    }
+    if (valid && (i + 1 == n || nk == invalid)) {
+      seg_off[uu + 1] = i + 1;
+      n_uniq[0] = uu + 1;
+    }
+    if (inv && i < n) inv[rf[u]] = valid ? uu : -1;
+  }
+}
+
+static void unique_from_sorted(const uint32_t* keys, const int32_t* refs, int n, uint32_t invalid, int32_t* chunk_cnt,
+                               uint32_t* uniq, int32_t* seg_off, int32_t* n_uniq, int32_t* inv,
+                               int32_t* owner_counts, hipStream_t s) {
+  const int chunks = (n + kUqChunk - 1) / kUqChunk;
+  hipLaunchKernelGGL(unique_count_kernel, dim3(chunks), dim3(256), 0, s, keys, n, invalid, chunk_cnt);
+  hipLaunchKernelGGL(unique_emit_kernel, dim3(chunks), dim3(256), 0, s, keys, refs, n, invalid, chunk_cnt, uniq,
+                     seg_off, n_uniq, inv, owner_counts);
+}
+
 // copies the compacted pairs back into the sort's input arrays
 __global__ __launch_bounds__(256) void iota_refs_copy_kernel(const uint32_t* __restrict__ kin, const int32_t* __restrict__ rin,
                                                              int n, uint32_t* __restrict__ kout, int32_t* __restrict__ rout) {
@@ -257,14 +390,7 @@ extern "C" int dl_index_build(const dl_emb_layout* L, const int64_t* cate, int32
   }
   n = ns_sort;
   if (n == 0) DL_RETURN_LAUNCH("dl_index_build");
-  hipLaunchKernelGGL(head_flags_kernel, dim3(grid), dim3(256), 0, s, sorted_keys, n, invalid, w.flags);
-  tb = w.temp_bytes;
-  if (hipcub::DeviceScan::InclusiveSum(w.temp, tb, w.flags, w.uid1, n, s) != hipSuccess) {
-    set_error("dl_index_build: scan failed");
-    return 3;
-  }
-  hipLaunchKernelGGL(scatter_index_kernel, dim3(grid), dim3(256), 0, s, sorted_keys, sorted_refs, w.uid1, n, world,
-                     invalid, uniq_keys, seg_off, n_uniq, inv, owner_counts);
+  unique_from_sorted(sorted_keys, sorted_refs, n, invalid, w.flags, uniq_keys, seg_off, n_uniq, inv, owner_counts, s);
   if (owner_counts)
     hipLaunchKernelGGL(owner_counts_kernel, dim3(1), dim3(64), 0, s, owner_counts, world + 1, n_uniq);
   DL_RETURN_LAUNCH("dl_index_build");
@@ -301,13 +427,7 @@ extern "C" int dl_sort_unique(const int32_t* keys, int64_t n_keys, int32_t key_b
     set_error("dl_sort_unique: radix sort failed");
     return 2;
   }
-  hipLaunchKernelGGL(head_flags_kernel, dim3(grid), dim3(256), 0, s, (const uint32_t*)sorted_keys, n, invalid, w.flags);
-  tb = w.temp_bytes;
-  if (hipcub::DeviceScan::InclusiveSum(w.temp, tb, w.flags, w.uid1, n, s) != hipSuccess) {
-    set_error("dl_sort_unique: scan failed");
-    return 3;
-  }
-  hipLaunchKernelGGL(scatter_index_kernel, dim3(grid), dim3(256), 0, s, (const uint32_t*)sorted_keys, sorted_pos,
-                     w.uid1, n, 1, invalid, (uint32_t*)uniq_keys, seg_off, n_uniq, inv, (int32_t*)nullptr);
+  unique_from_sorted((const uint32_t*)sorted_keys, sorted_pos, n, invalid, w.flags, (uint32_t*)uniq_keys, seg_off,
+                     n_uniq, inv, (int32_t*)nullptr, s);
   DL_RETURN_LAUNCH("dl_sort_unique");
 }

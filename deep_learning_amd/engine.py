@@ -197,7 +197,7 @@ class ModelSpec:
 
 class CTREngine:
     def __init__(self, spec, max_batch, device="cuda", seed=2019, init="device", bwd="atomic",
-                 table_rows=None, adam="dense", hist_len=4096, rec_stash=False):
+                 table_rows=None, adam="dense", hist_len=4096, rec_stash=False, fwd_rec=False):
         if not torch.cuda.is_available():
             raise _lib.DLError("CTREngine needs a HIP device (no CPU fallback)")
         _lib.lib()
@@ -344,6 +344,14 @@ class CTREngine:
             # Off by default — re-reading the record in the backward measured faster on both
             # kernels (gather 328 -> 232 us, backward 505 -> 447 us at C2; profiles/r01l).
             self.mv_u = z(self.n_rep + self.n_refs, 2 * E + 4) if rec_stash else None
+        # fwd_rec: the forward reads the cate rows straight from the records (dl_embed_fwd_rec)
+        # instead of gathering the batch's unique rows and reading them back through the
+        # inverse map; only the C replicated cont rows are gathered.  Single-valued fields.
+        # Off by default: bit-identical, but at C2 it measured 444 us against 214 + 123 us for
+        # the gather + indexed pair — the in-register catch-up of every reference at 2
+        # waves/SIMD (169 VGPRs) costs ~190 us that the gather's catch-up hides (253 us with
+        # no rows lagging; scripts/catchup_cost.py).
+        self.fwd_rec = bool(fwd_rec and self.lazy and not M and not rec_stash)
         # static input slots (graph capture reads from these)
         self.in_label = z(B)
         self.in_cont = z(B, max(sp.C, 1))
@@ -611,7 +619,16 @@ class CTREngine:
             self._c("pool_fwd", "dl_pool_fwd", C_ref(L), ptr(self.table), ptr(self.first) if sp.fm else None,
                  ptr(self.in_cate), sp.S, ptr(self.slot_start), ptr(self.slot_end), sp.M, self.fm_pool_col,
                  ptr(self.x0), ptr(self.fm_out), ptr(self.cnt_emb), ptr(self.cnt_first), ptr(self.err), s)
-        if self.lazy:
+        if self.fwd_rec:
+            if self.n_rep:   # the replicated FM cont-field rows, caught up, compact
+                self._c("rec_gather", "dl_rec_gather", C_ref(L), ptr(self.rec), self.rec_ld, int(sp.fm), self.n_rep,
+                        ptr(self.idx_uniq), None, 0, 1, ptr(self.hist), self.hist_len, ptr(self.opt),
+                        1 if train else 0, ptr(self.rows_u), ptr(self.rows_u1), None, s)
+            self._c("embed_fwd", "dl_embed_fwd_rec", C_ref(L), ptr(self.rec), self.rec_ld, int(sp.fm),
+                    ptr(self.rows_u), ptr(self.rows_u1) if sp.fm else None, ptr(self.in_cate), ptr(self.in_cont),
+                    ptr(self.in_vec), ptr(self.hist), self.hist_len, ptr(self.opt), 1 if train else 0,
+                    ptr(self.x0), ptr(self.fm_out), ptr(self.fm_sum), ptr(self.err), s)
+        elif self.lazy:
             # rows of the batch (index built by _pre), caught up to the step being taken
             self._c("rec_gather", "dl_rec_gather", C_ref(L), ptr(self.rec), self.rec_ld, int(sp.fm), self.n_rep,
                     ptr(self.idx_uniq), ptr(self.idx_n), B * self.n_slot, 1, ptr(self.hist), self.hist_len,

@@ -74,7 +74,8 @@ class CTRModel:
             self.engine = CTREngine(self.spec, max_batch=self.batch_size, seed=self.random_seed,
                                     adam=default_adam(self.spec))
         eng = self.engine
-        return eng.loss, lambda batch: eng.train_step(batch, graph=True), lambda: eng.steps
+        return (eng.loss, lambda batch, next_batch=None: eng.train_step(batch, graph=True, next_batch=next_batch),
+                lambda: eng.steps)
 
     # --------------------------------------------------------------- training
     def fit(self, print_num_batch, predict_data=None):
@@ -93,8 +94,10 @@ class CTRModel:
         start_time = time.time()
         batch_count = 0
         i = 0
-        for batch in self.data_dict:
-            train_fn(batch)
+        feed = _Feed(self.data_dict)
+        for batch, nxt in feed:
+            train_fn(batch, nxt)
+            feed.mark(self.engine)
             if batch_count == print_num_batch:
                 batch_end_time = time.time()
                 loss = loss_fn()
@@ -181,6 +184,44 @@ def _load_adam_state(eng, d):
     for l in range(len(eng.W)):
         eng.Wm[l].copy_(torch.from_numpy(d["adam/Wm%d" % l]))
         eng.Wv[l].copy_(torch.from_numpy(d["adam/Wv%d" % l]))
+
+
+class _Feed:
+    """Training batches as (batch, next batch) pairs.  From the native TFRecord reader the
+    batches are decoded into pinned host buffers (PinnedFeed) and the next one is handed to
+    train_step as next_batch, so its upload and index build run on the engine's side
+    stream during the current step.  Other iterables (lists, generators) pass through
+    with no lookahead."""
+
+    def __init__(self, data):
+        from ..utils.native_reader import NativeReader, PinnedFeed
+        self.it = iter(data)
+        self.pinned = PinnedFeed(self.it) if isinstance(self.it, NativeReader) else None
+        self.pair = None
+
+    def __iter__(self):
+        if self.pinned is None:
+            for b in self.it:
+                yield b, None
+            return
+        cur = self.pinned.next()
+        while cur is not None:
+            nxt = self.pinned.next()
+            self.pair = (cur, nxt)
+            yield cur, nxt
+            cur = nxt
+
+    def mark(self, eng):
+        """After train_step(cur, next_batch=nxt): cur's buffers were read by copies queued on
+        the compute stream (or by an earlier prefetch), nxt's by the side-stream prefetch."""
+        if self.pinned is None or self.pair is None:
+            return
+        cur, nxt = self.pair
+        ev = torch.cuda.Event()
+        ev.record()
+        self.pinned.mark(cur, ev)
+        if nxt is not None and getattr(eng, "_pf", None) is not None:
+            self.pinned.mark(nxt, eng._pf[2])
 
 
 def _predict_batches(eng, batch, logits=False):

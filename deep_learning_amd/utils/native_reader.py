@@ -54,6 +54,41 @@ def crc32c(data):
     return lib().dlio_crc32c(b, len(b))
 
 
+class PinnedFeed:
+    """Host-to-device double buffering for a NativeReader: the reader's
+    decoder threads write each batch straight into one of `depth` pinned host buffer sets,
+    so the engine's staging copy (CTREngine.stage / prefetch, non_blocking) is an async DMA
+    that overlaps the running step.  A set is reused only after the event recorded behind
+    its copy has completed (`mark`)."""
+
+    def __init__(self, reader, depth=4):
+        import torch
+        self.reader, self.depth, self.n = reader, depth, 0
+        self.sets = [{name: torch.empty((reader.batch, max(sz, 0)), dtype=torch.int64 if k == "int64" else torch.float32,
+                                        pin_memory=True) for name, k, sz in reader.spec} for _ in range(depth)]
+        self.events = [None] * depth
+
+    def next(self):
+        """The next batch as a dict of pinned CPU tensors (None at the end of the data)."""
+        k = self.n % self.depth
+        if self.events[k] is not None:
+            self.events[k].synchronize()        # its previous batch's copy has landed
+            self.events[k] = None
+        try:
+            b = self.reader.next_into(self.sets[k])
+        except StopIteration:
+            return None
+        self.n += 1
+        b = dict(b)
+        b["_slot"] = k
+        return b
+
+    def mark(self, batch, event):
+        """`event` completes after every read of `batch`'s host buffers."""
+        if batch is not None:
+            self.events[batch["_slot"]] = event
+
+
 class NativeReader:
     """Iterator of batches: dict name -> array [batch, size] (float32 / int64).
 
@@ -78,10 +113,17 @@ class NativeReader:
         return self
 
     def __next__(self):
+        return self.next_into(None)
+
+    def next_into(self, out):
+        """Next batch into `out` (dict name -> preallocated contiguous host buffers with a
+        ``data_ptr()`` or numpy ``ctypes.data``, e.g. pinned torch tensors) or fresh arrays."""
         if self.h is None:
             raise StopIteration
-        out = {n: np.empty((self.batch, s), np.int64 if k == "int64" else np.float32) for n, k, s in self.spec}
-        ptrs = (C.c_void_p * len(self.spec))(*[out[n].ctypes.data for n, _, _ in self.spec])
+        if out is None:
+            out = {n: np.empty((self.batch, s), np.int64 if k == "int64" else np.float32) for n, k, s in self.spec}
+        addr = lambda a: a.data_ptr() if hasattr(a, "data_ptr") else a.ctypes.data
+        ptrs = (C.c_void_p * len(self.spec))(*[addr(out[n]) for n, _, _ in self.spec])
         rc = lib().dlio_next(self.h, ptrs)
         if rc == 1:
             return out

@@ -115,6 +115,19 @@ int dl_embed_fwd_indexed(const dl_emb_layout* L, const float* rows, const float*
                          const float* vector, float* x0, float* fm_out, float* fm_sum,
                          void* stream);
 
+/* Record forward (single GPU, lazy-exact Adam): dl_embed_fwd with the cate rows read
+ * straight from the row records (rec.hip layout) and caught up to step opt[7] - lag in
+ * registers (lag 1 in training, 0 for predict), instead of dl_rec_gather writing the
+ * batch's unique rows and dl_embed_fwd_indexed reading them back.  The C FM cont-field
+ * rows (every sample's) come compact and caught up in rows_rep / rows_rep1 (dl_rec_gather
+ * with no unique rows); needs L->cont_rows_compact when there are any.  Outputs are
+ * bit-identical to the gather + indexed pair.  Single-valued fields only (multi_width 0). */
+int dl_embed_fwd_rec(const dl_emb_layout* L, const float* rec, int32_t rec_ld, int32_t has_first,
+                     const float* rows_rep, const float* rows_rep1, const int64_t* cate,
+                     const float* cont, const float* vector, const float* hist, int32_t hist_len,
+                     const float* opt, int32_t lag, float* x0, float* fm_out, float* fm_sum,
+                     int32_t* err, void* stream);
+
 /* Hot cont-field rows only (the FM cont part of dl_embed_bwd): per-block
  * partials into cont_slab, folded in by dl_embed_cont_reduce. */
 int dl_embed_cont_bwd(const dl_emb_layout* L, const float* table, const float* cont,

@@ -380,3 +380,28 @@ def test_auc_gpu_matches_sklearn_goldens_and_oracle(hip_lib):
     assert abs(acc.result() - R.auc(y, s)) < 1e-12
     with pytest.raises(ValueError, match="one class"):
         roc_auc(np.ones(10), np.arange(10.0))
+
+
+@pytest.mark.parametrize("n,distinct", [(1, 1), (4096 * 3, 5), (100_003, 50), (262_147, 200_000), (5000, 4999)])
+def test_sort_unique_matches_numpy(hip_lib, n, distinct):
+    """dl_sort_unique (radix sort + the two-pass segmented unique): unique keys, segment
+    bounds, positions in stable order and the inverse map bit-exact against numpy, with
+    segments that span many 4096-key chunks and ragged tails."""
+    rng = np.random.default_rng(n)
+    ids = rng.integers(0, distinct, n).astype(np.int32)
+    d = torch.from_numpy(ids).cuda()
+    ws = torch.zeros(hip_lib.dl_index_workspace_bytes(n), dtype=torch.uint8, device="cuda")
+    z = lambda m: torch.full((m,), -7, dtype=torch.int32, device="cuda")
+    keys, pos, uniq, off, nu, inv = z(n), z(n), z(n), z(n + 1), z(1), z(n)
+    call("dl_sort_unique", ptr(d), n, 18, ptr(ws), ws.numel(), ptr(keys), ptr(pos), ptr(uniq), ptr(off), ptr(nu),
+         ptr(inv), _s())
+    torch.cuda.synchronize()
+    u_ref, first, inv_ref, cnt_ref = np.unique(ids, return_index=True, return_inverse=True, return_counts=True)
+    k = int(nu.item())
+    assert k == len(u_ref)
+    np.testing.assert_array_equal(uniq[:k].cpu().numpy(), u_ref)
+    o = off[:k + 1].cpu().numpy()
+    assert o[0] == 0 and o[-1] == n
+    np.testing.assert_array_equal(np.diff(o), cnt_ref)
+    np.testing.assert_array_equal(inv.cpu().numpy(), inv_ref.reshape(-1))
+    np.testing.assert_array_equal(pos.cpu().numpy(), np.argsort(ids, kind="stable"))

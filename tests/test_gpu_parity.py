@@ -136,6 +136,29 @@ def test_lazy_adam_bit_identical_to_dense(hip_lib, name, stash):
         np.testing.assert_array_equal(sl[k], sd[k], err_msg=k)
 
 
+@pytest.mark.parametrize("name", ["deepfm_pipeline", "dnn_pipeline", "wdl"])
+def test_record_forward_bit_identical_to_gather(hip_lib, name):
+    """dl_embed_fwd_rec (cate rows read and caught up straight from the records) against
+    the gather + indexed forward pair: logits every step, predictions and all parameters
+    bit-identical (8-entry alpha ring: lagging rows and flushes included)."""
+    kw = dict(CASES[name], cate_index_size=50000)
+    spec = ModelSpec(_model(name), **kw)
+    a = CTREngine(spec, max_batch=128, seed=3, adam="lazy", hist_len=8, fwd_rec=True)
+    b = CTREngine(spec, max_batch=128, seed=3, adam="lazy", hist_len=8, fwd_rec=False)
+    assert a.fwd_rec and not b.fwd_rec
+    bs = _batches(name, kw, 128, 15, seed=11)
+    for i, bt in enumerate(bs):
+        a.train_step(bt, graph=i >= 2)
+        b.train_step(bt, graph=i >= 2)
+        torch.cuda.synchronize()
+        np.testing.assert_array_equal(a.z[:128].cpu().numpy(), b.z[:128].cpu().numpy(), err_msg="step %d" % i)
+        np.testing.assert_array_equal(a.fm_out[:128].cpu().numpy(), b.fm_out[:128].cpu().numpy())
+    np.testing.assert_array_equal(a.predict(bs[0]), b.predict(bs[0]))
+    pa, pb = a.params(), b.params()
+    for k in pa:
+        np.testing.assert_array_equal(pa[k], pb[k], err_msg=k)
+
+
 def test_lazy_multi_hot_tracks_oracle(hip_lib):
     """Multi-hot pooling on row records (deepfm_multi_cate): pooled rows come from the
     caught-up records through the batch index, their gradients join each row's ordered
