@@ -67,14 +67,17 @@ __device__ __forceinline__ int xcd_tile(int bid, int T) {
 // 2560 tiles fill exactly two rounds of the 256 CUs (at 3 blocks/CU, 3.3 rounds
 // left a 17 % tail).
 template <int BM, int BN>
-struct GemmOcc { static constexpr int waves = (BM == 128 && BN <= 80 && DL_GEMM_BK == 16) ? 5 : 2; };
+struct GemmOcc {
+  static constexpr int waves = (BM == 128 && BN <= 80 && DL_GEMM_BK == 16) ? 5 : (BM > 128 ? 3 : 2);
+};
 
 // FAST: M % BM == 0, N % BN == 0 and every split's k range whole BK slabs (the tower's
 // products: batch rows, 400-wide layers, zero-padded K = leading dims): no bounds checks,
 // each thread's staging addresses computed once and advanced by a constant per slab.
 template <int BM, int BN, int WM, int WN, bool TA, bool TB, int EPI, int BK, bool FAST>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GemmOcc<BM, BN>::waves)))
+__global__ __launch_bounds__(64 * WM * WN) __attribute__((amdgpu_waves_per_eu(GemmOcc<BM, BN>::waves)))
 void gemm_f32_kernel(GemmParams p) {
+  constexpr int NT = 64 * WM * WN;   // threads: 4 waves, or 5 for the tall dW tiles (WM 1 x WN 5)
   constexpr bool AKC = !TA, BKC = TB, KPERM = AKC || BKC;
   constexpr int KCS = BK == 16 ? BK + 4 : BK + 8;  // BK=16: 2-way b128 read conflicts, but 5 blocks/CU fit
   constexpr int MCPAD_A = KPERM ? (4 - BM % 8 + 8) % 8 : (48 - BM % 32) % 32;
@@ -83,9 +86,9 @@ void gemm_f32_kernel(GemmParams p) {
   constexpr int B_ROWS = BKC ? BN : BK, B_LD = BKC ? KCS : BN + MCPAD_B;
   constexpr int WTM = BM / WM, WTN = BN / WN;
   constexpr int FM = WTM / 16, FN = WTN / 16;
-  constexpr int QA = (BM * BK / 4 + 255) / 256;  // float4 staged per thread
-  constexpr int QB = (BN * BK / 4 + 255) / 256;
-  static_assert(WM * WN == 4, "4 waves");
+  constexpr int QA = (BM * BK / 4 + NT - 1) / NT;  // float4 staged per thread
+  constexpr int QB = (BN * BK / 4 + NT - 1) / NT;
+  static_assert(WM * WN == 4 || (WM * WN == 5 && !(DL_GEMM_GLDS && !TA)), "4 waves (or 5 without LDS-DMA)");
   static_assert(WTM % 16 == 0 && WTN % 16 == 0 && BK % 16 == 0, "tile shape");
 
   // GLDS: the k-contiguous A tile is filled by LDS-DMA (global_load_lds_dwordx4), which
@@ -130,13 +133,13 @@ void gemm_f32_kernel(GemmParams p) {
   if (FAST) {
 #pragma unroll
     for (int u = 0; u < QA; ++u) {
-      const int qi = min(tid + u * 256, BM * BK / 4 - 1);
+      const int qi = min(tid + u * NT, BM * BK / 4 - 1);
       if (TA) a_off[u] = 4u * (unsigned)((qi / (BM / 4)) * p.lda + 4 * (qi % (BM / 4)));
       else a_off[u] = 4u * (unsigned)((qi / (BK / 4)) * p.lda + 4 * (qi % (BK / 4)));
     }
 #pragma unroll
     for (int u = 0; u < QB; ++u) {
-      const int qi = min(tid + u * 256, BN * BK / 4 - 1);
+      const int qi = min(tid + u * NT, BN * BK / 4 - 1);
       if (!TB) b_off[u] = 4u * (unsigned)((qi / (BN / 4)) * p.ldb + 4 * (qi % (BN / 4)));
       else b_off[u] = 4u * (unsigned)((qi / (BK / 4)) * p.ldb + 4 * (qi % (BK / 4)));
     }
@@ -172,7 +175,7 @@ void gemm_f32_kernel(GemmParams p) {
     } else {
 #pragma unroll
     for (int u = 0; u < (GLDS ? 0 : QA); ++u) {
-      const int qi = tid + u * 256;
+      const int qi = tid + u * NT;
       float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
       if (qi < BM * BK / 4) {
         if (TA) {  // A stored [r][i]
@@ -189,7 +192,7 @@ void gemm_f32_kernel(GemmParams p) {
     }
 #pragma unroll
     for (int u = 0; u < QB; ++u) {
-      const int qi = tid + u * 256;
+      const int qi = tid + u * NT;
       float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
       if (qi < BN * BK / 4) {
         if (!TB) {  // B stored [r][j]
@@ -209,7 +212,7 @@ void gemm_f32_kernel(GemmParams p) {
   auto store_tile = [&](int buf) {
 #pragma unroll
     for (int u = 0; u < (GLDS ? 0 : QA); ++u) {
-      const int qi = tid + u * 256;
+      const int qi = tid + u * NT;
       if (qi < BM * BK / 4) {
         if (TA) {
           const int r = qi / (BM / 4), i4 = qi % (BM / 4);
@@ -222,7 +225,7 @@ void gemm_f32_kernel(GemmParams p) {
     }
 #pragma unroll
     for (int u = 0; u < QB; ++u) {
-      const int qi = tid + u * 256;
+      const int qi = tid + u * NT;
       if (qi < BN * BK / 4) {
         if (!TB) {
           const int r = qi / (BN / 4), j4 = qi % (BN / 4);
@@ -561,11 +564,12 @@ __global__ __launch_bounds__(256) void transpose_bf16_kernel(const void* __restr
 template <int BM, int BN, int WM, int WN, bool TA, bool TB, bool FAST>
 static void launch_f32_v(const GemmParams& gp, int epi, dim3 grid, hipStream_t s) {
   constexpr int BK = DL_GEMM_BK;
+  constexpr int NT = 64 * WM * WN;
   switch (epi) {
-    case EPI_STORE: hipLaunchKernelGGL((gemm_f32_kernel<BM, BN, WM, WN, TA, TB, EPI_STORE, BK, FAST>), grid, dim3(256), 0, s, gp); break;
-    case EPI_RELU: hipLaunchKernelGGL((gemm_f32_kernel<BM, BN, WM, WN, TA, TB, EPI_RELU, BK, FAST>), grid, dim3(256), 0, s, gp); break;
-    case EPI_MASK: hipLaunchKernelGGL((gemm_f32_kernel<BM, BN, WM, WN, TA, TB, EPI_MASK, BK, FAST>), grid, dim3(256), 0, s, gp); break;
-    default: hipLaunchKernelGGL((gemm_f32_kernel<BM, BN, WM, WN, TA, TB, EPI_SPLIT, BK, FAST>), grid, dim3(256), 0, s, gp); break;
+    case EPI_STORE: hipLaunchKernelGGL((gemm_f32_kernel<BM, BN, WM, WN, TA, TB, EPI_STORE, BK, FAST>), grid, dim3(NT), 0, s, gp); break;
+    case EPI_RELU: hipLaunchKernelGGL((gemm_f32_kernel<BM, BN, WM, WN, TA, TB, EPI_RELU, BK, FAST>), grid, dim3(NT), 0, s, gp); break;
+    case EPI_MASK: hipLaunchKernelGGL((gemm_f32_kernel<BM, BN, WM, WN, TA, TB, EPI_MASK, BK, FAST>), grid, dim3(NT), 0, s, gp); break;
+    default: hipLaunchKernelGGL((gemm_f32_kernel<BM, BN, WM, WN, TA, TB, EPI_SPLIT, BK, FAST>), grid, dim3(NT), 0, s, gp); break;
   }
 }
 
@@ -581,6 +585,15 @@ static void launch_f32(const GemmParams& gp, int epi, int splits, hipStream_t s)
 
 template <bool TA, bool TB>
 static void dispatch_bn_f32(const GemmParams& gp, int epi, int splits, hipStream_t s) {
+  // Weight gradients (split-K slabs of x^T dh: M = K_in + bias row padded to 16, N = 400):
+  // the 128-row tiles leave a ragged last tile (432 -> 512 rows).  Tall 144 x 80 tiles
+  // (9 fragments, 5 waves of 16 columns) divide M = 432 exactly: C2's layer-0 dW 229 ->
+  // 215 us.  (208-row tiles for M = 416 measured slower than the 128-row tiles with the
+  // wave skip — 233-248 vs 229 us — and are not used.)
+  if (epi == EPI_SPLIT && gp.N % 80 == 0 && gp.K >= 4096 && gp.M % 144 == 0 && gp.M % 128 != 0) {
+    launch_f32<144, 80, 1, 5, TA, TB>(gp, epi, splits, s);
+    return;
+  }
   // pick the N tile with the least padding (ties -> wider tile)
   const int cand[4] = {208, 128, 80, 64};
   int best = 64;

@@ -38,3 +38,20 @@ for name, fn in cases.items():
     torch.cuda.synchronize()
     us = e0.elapsed_time(e1) * 1e3 / reps
     print("%-7s %8.1f us  %6.1f TF/s" % (name, us, flops[name] / us / 1e6), flush=True)
+
+# split-K sweep of the dW product (layer 1 shape)
+slab2 = torch.zeros(256 * 416 * 400, device="cuda")
+for sp in (16, 32, 48, 64, 96, 128, 192, 256):
+    fn = lambda: call("dl_gemm_f32", 1, 0, 416, 400, B, ptr(h), 416, ptr(dh), 416, ptr(slab2), 400, 3, None, 0, sp,
+                      416 * 400, s)
+    for _ in range(3):
+        fn()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        fn()
+    e1.record()
+    torch.cuda.synchronize()
+    us = e0.elapsed_time(e1) * 1e3 / reps
+    print("dw_l1 splits %3d %8.1f us  %6.1f TF/s" % (sp, us, flops["dw_l1"] / us / 1e6), flush=True)

@@ -73,6 +73,26 @@ def test_gemm_f32_epilogues_and_split(hip_lib):
     assert torch.allclose(C2.double(), torch.where(mask > 0, r, torch.zeros_like(r)), rtol=1e-5, atol=1e-3)
 
 
+@pytest.mark.parametrize("M,N,K,splits", [(416, 400, 8192, 8), (432, 400, 4096 + 16, 3), (208, 160, 65536, 64),
+                                            (144, 80, 5000 * 4, 5), (416, 400, 65536, 64)])
+def test_gemm_f32_tall_split_tiles(hip_lib, M, N, K, splits):
+    """Weight-gradient products (ta=1, split-K slabs; M a multiple of 144 and N of 80 run
+    on the tall 5-wave tiles, the others on the 128-row tiles with the wave skip): slab
+    sums against fp64."""
+    g = torch.Generator().manual_seed(M + N + K)
+    A = torch.randn(K, M, generator=g).cuda()     # x stored [k][m]
+    B = torch.randn(K, N, generator=g).cuda()     # dh stored [k][n]
+    ref = (A.t().double() @ B.double()).cpu()
+    slab = torch.full((splits, M, N), 7.0, device="cuda")
+    call("dl_gemm_f32", 1, 0, M, N, K, ptr(A), M, ptr(B), N, ptr(slab), N, 3, None, 0, splits, M * N, _s())
+    torch.cuda.synchronize()
+    from deep_learning_amd.engine import _num_splits
+    used = _num_splits(K, splits)
+    got = slab[:used].double().sum(0).cpu()
+    scale = (A.abs().t().double() @ B.abs().double()).cpu().clamp(min=1.0)
+    assert ((got - ref).abs() / scale).max().item() < 2e-6
+
+
 def test_gemm_bf16(hip_lib):
     g = torch.Generator().manual_seed(2)
     M, N, K = 300, 200, 256
