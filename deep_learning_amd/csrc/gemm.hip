@@ -538,6 +538,120 @@ __global__ __launch_bounds__(256) void gemm_bf16_kc_kernel(GemmParams p) {
     }
 }
 
+// Tall-skinny bf16 product with the B tile resident in LDS (the C5 tower's forward and dX:
+// M = batch rows, N <= 416, K <= 448, both operands k-contiguous).  A block owns 256 rows x
+// 80 columns: its whole B slab (80 x K bf16, <= 72 KB) is loaded into LDS once, and each
+// of its 8 waves streams its own 32 rows of A straight into MFMA fragments (16 B per lane
+// per 32-deep k-chunk; A is read once per column tile, the column tiles of a row tile
+// placed on one XCD) with a KC-chunk fully unrolled loop whose loads run DEPTH chunks
+// ahead.  The generic kc kernel re-staged both operands every 64-deep step and waited a
+// full memory round trip per step (7 steps per tile): 139 us for the 65536 x 400 x 432
+// forward; this one is bound by streaming A.
+template <int KC, int EPI, bool CBF16>
+__global__ __launch_bounds__(512) void gemm_bf16_bres_kernel(GemmParams p) {
+  constexpr int BM = 256, BN = 80, NF = BN / 16, DEPTH = 3;
+  constexpr int KP = KC * 32 + 8;                 // LDS row pitch (bf16): +16 B keeps b128 reads conflict-free
+  extern __shared__ __attribute__((aligned(16))) unsigned short Bs[];   // [BN][KP]
+  const unsigned short* __restrict__ A = reinterpret_cast<const unsigned short*>(p.A);
+  const unsigned short* __restrict__ Bm = reinterpret_cast<const unsigned short*>(p.B);
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int ntm = (p.M + BM - 1) / BM, ntn = (p.N + BN - 1) / BN;
+  const int t = xcd_tile(blockIdx.x, ntm * ntn);
+  const int i0 = (t / ntn) * BM, j0 = (t % ntn) * BN;
+  const int cl = lane & 15, kq = lane >> 4;
+  const uint4 z4 = make_uint4(0u, 0u, 0u, 0u);
+  // A fragments of this wave: rows r0 + cl and r0 + 16 + cl, k = 32c + 8kq .. +7
+  const int r0 = i0 + wid * 32;
+  const unsigned short* a0 = A + (long long)min(r0 + cl, p.M - 1) * p.lda + 8 * kq;
+  const unsigned short* a1 = A + (long long)min(r0 + 16 + cl, p.M - 1) * p.lda + 8 * kq;
+  const bool ok0 = r0 + cl < p.M, ok1 = r0 + 16 + cl < p.M;
+  uint4 ra[KC][2];
+#pragma unroll
+  for (int c = 0; c < DEPTH && c < KC; ++c) {
+    const bool kin = 32 * c + 8 * kq < p.K;
+    ra[c][0] = (ok0 && kin) ? *reinterpret_cast<const uint4*>(a0 + 32 * c) : z4;
+    ra[c][1] = (ok1 && kin) ? *reinterpret_cast<const uint4*>(a1 + 32 * c) : z4;
+  }
+  // B slab -> LDS: row j (column j0 + j of the product), k contiguous, zero past N and K
+  for (int q = tid; q < BN * KC * 4; q += 512) {
+    const int j = q / (KC * 4), k8 = q % (KC * 4);
+    const int gj = j0 + j, gk = 8 * k8;
+    const uint4 v = (gj < p.N && gk < p.K) ? *reinterpret_cast<const uint4*>(Bm + (long long)gj * p.ldb + gk) : z4;
+    *reinterpret_cast<uint4*>(&Bs[j * KP + gk]) = v;
+  }
+  __syncthreads();
+  floatx4 acc[2][NF];
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int f = 0; f < NF; ++f) acc[a][f] = floatx4{0.f, 0.f, 0.f, 0.f};
+  const int nf_live = min(NF, (p.N - j0 + 15) / 16);   // column fragments inside N (wave-uniform)
+#pragma unroll
+  for (int c = 0; c < KC; ++c) {
+    if (c + DEPTH < KC) {
+      const bool kin = 32 * (c + DEPTH) + 8 * kq < p.K;
+      ra[c + DEPTH][0] = (ok0 && kin) ? *reinterpret_cast<const uint4*>(a0 + 32 * (c + DEPTH)) : z4;
+      ra[c + DEPTH][1] = (ok1 && kin) ? *reinterpret_cast<const uint4*>(a1 + 32 * (c + DEPTH)) : z4;
+    }
+    const shortx8 av0 = __builtin_bit_cast(shortx8, ra[c][0]);
+    const shortx8 av1 = __builtin_bit_cast(shortx8, ra[c][1]);
+#pragma unroll
+    for (int f = 0; f < NF; ++f) {
+      if (f < nf_live) {
+        const shortx8 bv = *reinterpret_cast<const shortx8*>(&Bs[(16 * f + cl) * KP + 32 * c + 8 * kq]);
+        acc[0][f] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av0, bv, acc[0][f], 0, 0, 0);
+        acc[1][f] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av1, bv, acc[1][f], 0, 0, 0);
+      }
+    }
+  }
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int f = 0; f < NF; ++f) {
+      const int col = j0 + 16 * f + cl;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int row = r0 + 16 * a + 4 * kq + j;
+        if (row < p.M && col < p.N) {
+          float v = acc[a][f][j];
+          if (EPI == EPI_RELU) v = fmaxf(v, 0.f);
+          if (EPI == EPI_MASK) {
+            const unsigned short* mk = reinterpret_cast<const unsigned short*>(p.mask);
+            v = bf2f(mk[(long long)row * p.ldm + col]) > 0.f ? v : 0.f;
+          }
+          const long long o = (long long)row * p.ldc + col;
+          if (CBF16) reinterpret_cast<unsigned short*>(p.C)[o] = f2bf(v);
+          else reinterpret_cast<float*>(p.C)[o] = v;
+        }
+      }
+    }
+}
+
+template <int KC>
+static void launch_bf16_bres_kc(const GemmParams& gp, int epi, bool cb, hipStream_t s) {
+  const int tiles = (int)(ceil_div(gp.M, 256) * ceil_div(gp.N, 80));
+  const size_t lds = (size_t)80 * (KC * 32 + 8) * sizeof(unsigned short);
+  const dim3 grid(tiles), block(512);
+#define DL_BRES(E_, C_) hipLaunchKernelGGL((gemm_bf16_bres_kernel<KC, E_, C_>), grid, block, lds, s, gp)
+  if (epi == EPI_STORE) {
+    if (cb) DL_BRES(EPI_STORE, true); else DL_BRES(EPI_STORE, false);
+  } else if (epi == EPI_RELU) {
+    if (cb) DL_BRES(EPI_RELU, true); else DL_BRES(EPI_RELU, false);
+  } else {
+    if (cb) DL_BRES(EPI_MASK, true); else DL_BRES(EPI_MASK, false);
+  }
+#undef DL_BRES
+}
+
+// true if the B-resident kernel takes the product (and launches it)
+static bool launch_bf16_bres(const GemmParams& gp, int epi, bool cb, hipStream_t s) {
+  if (epi == EPI_SPLIT || gp.K <= 0 || gp.K > 448 || gp.K % 8 || gp.lda % 8 || gp.ldb % 8 || gp.M < 4096) return false;
+  const int kc = (gp.K + 31) / 32;
+  if (kc <= 13) launch_bf16_bres_kc<13>(gp, epi, cb, s);
+  else launch_bf16_bres_kc<14>(gp, epi, cb, s);
+  return true;
+}
+
 // dst[c*ldd + r] = bf16(src[r*lds + c]) through a 32x33 LDS tile; src f32 or bf16.
 template <bool SRC_F32>
 __global__ __launch_bounds__(256) void transpose_bf16_kernel(const void* __restrict__ src, int rows, int cols, int lds,
@@ -751,6 +865,7 @@ extern "C" int dl_gemm_bf16(int32_t ta, int32_t tb, int32_t M, int32_t N, int32_
     if (kps2 == 0) kps2 = 64;
     gp.k_per_split = kps2;
     const int sp2 = (int)ceil_div(K > 0 ? K : 1, kps2);
+    if (sp2 == 1 && launch_bf16_bres(gp, epi, c_bf16 != 0, s)) DL_RETURN_LAUNCH("dl_gemm_bf16");
     const int bn = (N + 79) / 80 * 80 <= (N + 207) / 208 * 208 ? 80 : 208;
     dispatch_bf16_kc(gp, epi, sp2, c_bf16 != 0, bn, s);
     DL_RETURN_LAUNCH("dl_gemm_bf16");
