@@ -604,27 +604,82 @@ __global__ __launch_bounds__(512) void gemm_bf16_bres_kernel(GemmParams p) {
       }
     }
   }
+  // Epilogue through LDS (the B slab is dead now): each wave writes its 32 x 80 tile row-major
+  // (element stores from the MFMA layout), then every lane moves whole 16-B row pieces, so the
+  // output (and the ReluGrad mask) go to HBM as full row segments instead of 2/4-byte
+  // scatters.  f32 output goes in two 16-row halves (32 x 80 x 4 B would not fit beside the
+  // other waves' tiles).
+  __syncthreads();
+  constexpr int ES = CBF16 ? 2 : 4;                 // output element bytes
+  constexpr int HR = CBF16 ? 32 : 16;               // rows per pass
+  constexpr int TP = BN + (CBF16 ? 8 : 4);          // tile pitch (elements): rows start 16-B aligned
+  constexpr int EPP = 16 / ES;                      // elements per 16-B piece
+  constexpr int VPR = BN / EPP;                     // pieces per row (10 or 20)
+  unsigned char* tile = reinterpret_cast<unsigned char*>(Bs) + (size_t)wid * HR * TP * ES;
 #pragma unroll
-  for (int a = 0; a < 2; ++a)
+  for (int h = 0; h < 32 / HR; ++h) {
 #pragma unroll
-    for (int f = 0; f < NF; ++f) {
-      const int col = j0 + 16 * f + cl;
+    for (int a = 0; a < 2; ++a) {
+      if (16 * a < HR * h || 16 * a >= HR * (h + 1)) continue;
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int row = r0 + 16 * a + 4 * kq + j;
-        if (row < p.M && col < p.N) {
+      for (int f = 0; f < NF; ++f)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int rl = 16 * a + 4 * kq + j - HR * h, cc = 16 * f + cl;
           float v = acc[a][f][j];
           if (EPI == EPI_RELU) v = fmaxf(v, 0.f);
-          if (EPI == EPI_MASK) {
-            const unsigned short* mk = reinterpret_cast<const unsigned short*>(p.mask);
-            v = bf2f(mk[(long long)row * p.ldm + col]) > 0.f ? v : 0.f;
+          if (CBF16) reinterpret_cast<unsigned short*>(tile)[rl * TP + cc] = f2bf(v);
+          else reinterpret_cast<float*>(tile)[rl * TP + cc] = v;
+        }
+    }
+    __builtin_amdgcn_s_waitcnt(0xc07f);             // lgkmcnt(0): this wave's tile writes landed
+    __builtin_amdgcn_wave_barrier();
+    for (int q = lane; q < HR * VPR; q += 64) {
+      const int rl = q / VPR, pc = q % VPR;
+      const int row = r0 + HR * h + rl, col = j0 + pc * EPP;
+      if (row >= p.M || col >= p.N) continue;
+      uint4 v = *reinterpret_cast<const uint4*>(tile + ((size_t)rl * TP * ES + pc * 16));
+      const int nv = min(EPP, p.N - col);           // elements of this piece inside N
+      if (EPI == EPI_MASK) {
+        const unsigned short* mk = reinterpret_cast<const unsigned short*>(p.mask) + (long long)row * p.ldm + col;
+        unsigned short mv[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        if (nv == EPP && (reinterpret_cast<uintptr_t>(mk) & (2 * EPP - 1)) == 0) {
+          if (CBF16) {
+            const uint4 m4 = *reinterpret_cast<const uint4*>(mk);
+            memcpy(mv, &m4, 16);
+          } else {
+            const uint2 m2 = *reinterpret_cast<const uint2*>(mk);
+            memcpy(mv, &m2, 8);
           }
-          const long long o = (long long)row * p.ldc + col;
-          if (CBF16) reinterpret_cast<unsigned short*>(p.C)[o] = f2bf(v);
-          else reinterpret_cast<float*>(p.C)[o] = v;
+        } else {
+          for (int e = 0; e < nv; ++e) mv[e] = mk[e];
+        }
+        if (CBF16) {
+          unsigned short x[8];
+          memcpy(x, &v, 16);
+          for (int e = 0; e < 8; ++e) x[e] = bf2f(mv[e]) > 0.f ? x[e] : (unsigned short)0;
+          memcpy(&v, x, 16);
+        } else {
+          float x[4];
+          memcpy(x, &v, 16);
+          for (int e = 0; e < 4; ++e) x[e] = bf2f(mv[e]) > 0.f ? x[e] : 0.f;
+          memcpy(&v, x, 16);
+        }
+      }
+      unsigned char* dst = reinterpret_cast<unsigned char*>(p.C) + ((long long)row * p.ldc + col) * ES;
+      if (nv == EPP && (reinterpret_cast<uintptr_t>(dst) & 15) == 0) {
+        *reinterpret_cast<uint4*>(dst) = v;
+      } else {
+        unsigned char src[16];
+        memcpy(src, &v, 16);
+        for (int e = 0; e < nv; ++e) {
+          if (CBF16) { unsigned short w; memcpy(&w, src + 2 * e, 2); reinterpret_cast<unsigned short*>(dst)[e] = w; }
+          else { float w; memcpy(&w, src + 4 * e, 4); reinterpret_cast<float*>(dst)[e] = w; }
         }
       }
     }
+    __builtin_amdgcn_wave_barrier();
+  }
 }
 
 template <int KC>
@@ -645,10 +700,144 @@ static void launch_bf16_bres_kc(const GemmParams& gp, int epi, bool cb, hipStrea
 
 // true if the B-resident kernel takes the product (and launches it)
 static bool launch_bf16_bres(const GemmParams& gp, int epi, bool cb, hipStream_t s) {
-  if (epi == EPI_SPLIT || gp.K <= 0 || gp.K > 448 || gp.K % 8 || gp.lda % 8 || gp.ldb % 8 || gp.M < 4096) return false;
+  if (epi == EPI_SPLIT || gp.K <= 0 || gp.K > 448 || gp.K % 8 || gp.lda % 8 || gp.ldb % 8 || gp.M < 256) return false;
   const int kc = (gp.K + 31) / 32;
   if (kc <= 13) launch_bf16_bres_kc<13>(gp, epi, cb, s);
   else launch_bf16_bres_kc<14>(gp, epi, cb, s);
+  return true;
+}
+
+// Weight gradients of the bf16 tower without transposed operand copies (ta = 1, tb = 0,
+// split-K slabs): slab z of C = sum over the batch rows k of split z of X[k][m] dY[k][n], with
+// X [K][lda] bf16 (m contiguous: the activations as the forward wrote them) and dY [K][ldb]
+// (n contiguous: the layer's output gradient).  32 batch rows of each are copied into LDS as
+// plain rows and read as MFMA fragments with ds_read_b64_tr_b16 (CDNA4's transposing LDS
+// read): lane group kq takes batch rows 4kq..4kq+3 and 16+4kq..16+4kq+3 of the step for both
+// operands (the same k set, so the product is unchanged), and row pitches of 8 x odd words
+// make every transposed read conflict-free.  Block: 5 waves, 64 rows (m) x 400 columns (n);
+// wave w owns columns 80w..80w+79 (4 x 5 fragments).  The m tiles of one split are
+// consecutive tiles of the XCD-aware order: dY's slice comes from HBM once, then from L2.
+typedef __attribute__((__vector_size__(4 * sizeof(__fp16)))) __fp16 dl_fp16x4_t;
+
+__device__ __forceinline__ uint2 lds_tr16(const unsigned short* ptr_) {
+  auto lp = (__attribute__((address_space(3))) unsigned short*)(const_cast<unsigned short*>(ptr_));
+  const dl_fp16x4_t v =
+      __builtin_amdgcn_ds_read_tr16_b64_v4f16(reinterpret_cast<__attribute__((address_space(3))) dl_fp16x4_t*>(lp));
+  return __builtin_bit_cast(uint2, v);
+}
+
+__global__ __launch_bounds__(320) void gemm_bf16_dw_kernel(GemmParams p) {
+  constexpr int BM = 64, BN = 400, NT = 320, KS = 32;
+  constexpr int PA = 80, PB = 400;                      // row pitches: 40 and 200 words = 8 x odd
+  constexpr int A_EL = KS * PA, B_EL = KS * PB;         // elements per buffer
+  constexpr int QA_N = KS * BM / 8, QB_N = KS * BN / 8; // 16-B pieces per step
+  constexpr int Q = (QA_N + QB_N + NT - 1) / NT;
+  __shared__ __attribute__((aligned(16))) unsigned short lds[2 * (A_EL + B_EL)];
+  const unsigned short* __restrict__ X = reinterpret_cast<const unsigned short*>(p.A);
+  const unsigned short* __restrict__ Y = reinterpret_cast<const unsigned short*>(p.B);
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int mtiles = (p.M + BM - 1) / BM;
+  const int t = xcd_tile(blockIdx.x, gridDim.x);
+  const int m0 = (t % mtiles) * BM, z = t / mtiles;
+  const int kbeg = z * p.k_per_split;
+  const int kend = min(p.K, kbeg + p.k_per_split);
+  const int nk = (kend - kbeg + KS - 1) / KS;
+  const uint4 z4 = make_uint4(0u, 0u, 0u, 0u);
+  uint4 rs[Q];
+  auto load = [&](int k0) {
+#pragma unroll
+    for (int u = 0; u < Q; ++u) {
+      const int q = tid + u * NT;
+      uint4 v = z4;
+      if (q < QA_N) {
+        const int r = q / (BM / 8), c8 = q % (BM / 8);
+        const int gk = k0 + r, gm = m0 + 8 * c8;
+        if (gk < kend && gm < p.M) v = *reinterpret_cast<const uint4*>(X + (long long)gk * p.lda + gm);
+      } else if (q < QA_N + QB_N) {
+        const int qq = q - QA_N, r = qq / (BN / 8), c8 = qq % (BN / 8);
+        const int gk = k0 + r, gn = 8 * c8;
+        if (gk < kend && gn < p.N) v = *reinterpret_cast<const uint4*>(Y + (long long)gk * p.ldb + gn);
+      }
+      rs[u] = v;
+    }
+  };
+  auto store = [&](int buf) {
+    unsigned short* As = lds + buf * (A_EL + B_EL);
+    unsigned short* Bs = As + A_EL;
+#pragma unroll
+    for (int u = 0; u < Q; ++u) {
+      const int q = tid + u * NT;
+      if (q < QA_N) {
+        const int r = q / (BM / 8), c8 = q % (BM / 8);
+        *reinterpret_cast<uint4*>(&As[r * PA + 8 * c8]) = rs[u];
+      } else if (q < QA_N + QB_N) {
+        const int qq = q - QA_N, r = qq / (BN / 8), c8 = qq % (BN / 8);
+        *reinterpret_cast<uint4*>(&Bs[r * PB + 8 * c8]) = rs[u];
+      }
+    }
+  };
+  floatx4 acc[4][5];
+#pragma unroll
+  for (int a = 0; a < 4; ++a)
+#pragma unroll
+    for (int b = 0; b < 5; ++b) acc[a][b] = floatx4{0.f, 0.f, 0.f, 0.f};
+  if (nk > 0) {
+    load(kbeg);
+    store(0);
+    __syncthreads();
+  }
+  const int cl = lane & 15, kq = lane >> 4, rq = cl >> 2, cp = cl & 3;
+  const int ra = 4 * kq + rq, rb = 16 + 4 * kq + rq;   // this lane's rows of the two transposed reads
+  for (int kt = 0; kt < nk; ++kt) {
+    const int cur = kt & 1;
+    if (kt + 1 < nk) load(kbeg + (kt + 1) * KS);
+    const unsigned short* As = lds + cur * (A_EL + B_EL);
+    const unsigned short* Bs = As + A_EL;
+    shortx8 af[4];
+#pragma unroll
+    for (int a = 0; a < 4; ++a) {
+      const uint2 lo = lds_tr16(&As[ra * PA + 16 * a + 4 * cp]);
+      const uint2 hi = lds_tr16(&As[rb * PA + 16 * a + 4 * cp]);
+      af[a] = __builtin_bit_cast(shortx8, make_uint4(lo.x, lo.y, hi.x, hi.y));
+    }
+#pragma unroll
+    for (int b = 0; b < 5; ++b) {
+      const int c0 = 80 * wid + 16 * b + 4 * cp;
+      const uint2 lo = lds_tr16(&Bs[ra * PB + c0]);
+      const uint2 hi = lds_tr16(&Bs[rb * PB + c0]);
+      const shortx8 bf = __builtin_bit_cast(shortx8, make_uint4(lo.x, lo.y, hi.x, hi.y));
+#pragma unroll
+      for (int a = 0; a < 4; ++a) acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[a], bf, acc[a][b], 0, 0, 0);
+    }
+    if (kt + 1 < nk) store(cur ^ 1);
+    __syncthreads();
+  }
+  float* __restrict__ C = reinterpret_cast<float*>(p.C) + (long long)z * p.c_split_stride;
+#pragma unroll
+  for (int a = 0; a < 4; ++a)
+#pragma unroll
+    for (int b = 0; b < 5; ++b) {
+      const int col = 80 * wid + 16 * b + cl;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int row = m0 + 16 * a + 4 * kq + j;
+        if (row < p.M && col < p.N) C[(long long)row * p.ldc + col] = acc[a][b][j];
+      }
+    }
+}
+
+// true if the transposed-read kernel takes the product (ta = 1, tb = 0, split slabs)
+static bool launch_bf16_dw(const GemmParams& gp0, int splits_req, hipStream_t s) {
+  if (gp0.N > 400 || gp0.N % 8 || gp0.M % 8 || gp0.lda % 8 || gp0.ldb % 8 || gp0.lda < gp0.M ||
+      gp0.ldb < gp0.N || (reinterpret_cast<uintptr_t>(gp0.A) & 15) || (reinterpret_cast<uintptr_t>(gp0.B) & 15))
+    return false;
+  GemmParams gp = gp0;
+  int kps = (int)ceil_div(gp.K > 0 ? gp.K : 1, splits_req);
+  kps = (kps + 63) / 64 * 64;                 // the engine sums ceil(K / kps) slabs at this rounding
+  gp.k_per_split = kps;
+  const int splits = (int)ceil_div(gp.K > 0 ? gp.K : 1, kps);
+  const int mtiles = (int)ceil_div(gp.M, 64);
+  hipLaunchKernelGGL(gemm_bf16_dw_kernel, dim3((unsigned)(mtiles * splits)), dim3(320), 0, s, gp);
   return true;
 }
 
@@ -845,6 +1034,7 @@ extern "C" int dl_gemm_bf16(int32_t ta, int32_t tb, int32_t M, int32_t N, int32_
   DL_CHECK_ARG(epi != EPI_MASK || mask, "mask epilogue needs mask");
   DL_CHECK_ARG(!(epi == EPI_SPLIT && c_bf16), "split slabs are fp32");
   if (splits < 1) splits = 1;
+  const int splits_req = splits;
   DL_CHECK_ARG(splits == 1 || epi == EPI_SPLIT, "splits > 1 requires the split epilogue");
   if (M == 0 || N == 0) return 0;
   GemmParams gp;
@@ -857,6 +1047,7 @@ extern "C" int dl_gemm_bf16(int32_t ta, int32_t tb, int32_t M, int32_t N, int32_
   splits = (int)ceil_div(K > 0 ? K : 1, kps);
   gp.c_split_stride = c_split_stride;
   hipStream_t s = as_stream(stream);
+  if (ta && !tb && epi == EPI_SPLIT && launch_bf16_dw(gp, splits_req, s)) DL_RETURN_LAUNCH("dl_gemm_bf16");
   if (!ta && tb && lda % 8 == 0 && ldb % 8 == 0 && ((uintptr_t)A % 16) == 0 && ((uintptr_t)B % 16) == 0 &&
       lda >= (K + 7) / 8 * 8 && ldb >= (K + 7) / 8 * 8) {
     // k-contiguous fast path (the tower's products are arranged into this form)

@@ -105,12 +105,12 @@ __global__ __launch_bounds__(256) void adam_rows4_kernel(float4* __restrict__ p,
   for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n4;
        i += (long long)gridDim.x * blockDim.x) {
     const long long row = i / lpr;
+    float4 pi = p[i], mi = m[i], vi = v[i];   // issued before the touched test: one round trip
     float4 gi = make_float4(0.f, 0.f, 0.f, 0.f);
     if (touched[row]) {
       gi = g[i];
       g[i] = make_float4(0.f, 0.f, 0.f, 0.f);
     }
-    float4 pi = p[i], mi = m[i], vi = v[i];
     if (l2 != 0.f) { gi.x += l2 * pi.x; gi.y += l2 * pi.y; gi.z += l2 * pi.z; gi.w += l2 * pi.w; }
     if (sq_out) sq += pi.x * pi.x + pi.y * pi.y + pi.z * pi.z + pi.w * pi.w;
     adam_elem(pi.x, mi.x, vi.x, gi.x, alpha, omb1, omb2, eps);
@@ -137,6 +137,9 @@ __global__ __launch_bounds__(256) void adam_rows1_kernel(float* __restrict__ p, 
   for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < (n + 3) / 4;
        i += (long long)gridDim.x * blockDim.x) {
     if (i < n4) {
+      // p, m, v issued before the touched test: one round trip instead of two
+      float4 pi = reinterpret_cast<float4*>(p)[i], mi = reinterpret_cast<float4*>(m)[i],
+             vi = reinterpret_cast<float4*>(v)[i];
       const uchar4 t = reinterpret_cast<const uchar4*>(touched)[i];
       float4 gi = make_float4(0.f, 0.f, 0.f, 0.f);
       float4* g4 = reinterpret_cast<float4*>(g) + i;
@@ -146,8 +149,6 @@ __global__ __launch_bounds__(256) void adam_rows1_kernel(float* __restrict__ p, 
         if (!t.x) gi.x = 0.f; if (!t.y) gi.y = 0.f; if (!t.z) gi.z = 0.f; if (!t.w) gi.w = 0.f;
         if (clear) reinterpret_cast<uchar4*>(touched)[i] = make_uchar4(0, 0, 0, 0);
       }
-      float4 pi = reinterpret_cast<float4*>(p)[i], mi = reinterpret_cast<float4*>(m)[i],
-             vi = reinterpret_cast<float4*>(v)[i];
       if (l2 != 0.f) { gi.x += l2 * pi.x; gi.y += l2 * pi.y; gi.z += l2 * pi.z; gi.w += l2 * pi.w; }
       sq += pi.x * pi.x + pi.y * pi.y + pi.z * pi.z + pi.w * pi.w;
       adam_elem(pi.x, mi.x, vi.x, gi.x, alpha, omb1, omb2, eps);

@@ -294,12 +294,9 @@ class CTREngine:
                 self.hb.append(t)
             self.dhb = [zb(B, self.h_ld[l]) for l in range(len(sp.hidden))]
             self.Wb = [zb(self.in_ld[l], self.out_ld[l]) for l in range(len(sp.hidden))]
-            # k-contiguous copies for the fast bf16 kernel (ta = 0, tb = 1 form of every product):
-            # W^T for the forward, X^T and dY^T (batch-contiguous) for dW
+            # W^T (k-contiguous) for the forward product; dW reads the batch-major X and dY
+            # directly (transposing LDS reads in the kernel), so there are no X^T / dY^T copies
             self.WbT = [zb(self.out_ld[l], self.in_ld[l]) for l in range(len(sp.hidden))]
-            self.x0bT = zb(self.in_ld[0], B)
-            self.hbT = [zb(self.h_ld[l], B) for l in range(len(sp.hidden) - 1)]
-            self.dhbT = [zb(self.h_ld[l], B) for l in range(len(sp.hidden))]
         self.dx0 = z(B, self.dx_ld)
         self.fm_out = z(B, self.fm_ld)
         self.fm_sum = z(B, E)
@@ -652,9 +649,6 @@ class CTREngine:
             # output kept fp32 for the fp32 head / wide cross logit (config C5)
             self._c("cast_x0", "dl_cast_bf16", ptr(self.x0), B, self.in_ld[0], self.in_ld[0], ptr(self.x0b),
                     self.in_ld[0], s)
-            if train:
-                self._c("cast_x0T", "dl_transpose_bf16", ptr(self.x0), 1, B, self.in_ld[0], self.in_ld[0],
-                        ptr(self.x0bT), self.B, s)
             xb = self.x0b
             for l, hdim in enumerate(sp.hidden):
                 last = l == nl - 1
@@ -664,9 +658,6 @@ class CTREngine:
                         0, s)
                 if not last:
                     xb = self.hb[l]
-                    if train:
-                        self._c("hT_l%d" % l, "dl_transpose_bf16", ptr(self.hb[l]), 0, B, self.h_ld[l],
-                                self.h_ld[l], ptr(self.hbT[l]), self.B, s)
         else:
             x = self.x0
             for l, hdim in enumerate(sp.hidden):
@@ -716,24 +707,21 @@ class CTREngine:
         if self.bf:
             self._c("cast_dh", "dl_cast_bf16", ptr(self.dh[-1]), B, self.h_ld[-1], self.h_ld[-1], ptr(self.dhb[-1]),
                     self.h_ld[-1], s)
-            self._c("cast_dhT", "dl_transpose_bf16", ptr(self.dh[-1]), 1, B, self.h_ld[-1], self.h_ld[-1],
-                    ptr(self.dhbT[-1]), self.B, s)
         for l in reversed(range(nl)):
             hdim = sp.hidden[l]
             stride = self.in_ld[l] * self.out_ld[l]
             nsplit = _num_splits(B, splits, 64 if self.bf else 16)
             if self.bf:
-                # dW = X^T dY as (X^T)(dY^T)^T: both operands batch-contiguous copies
-                xT = self.x0bT if l == 0 else self.hbT[l - 1]
-                self._c("gemm_dw_l%d" % l, "dl_gemm_bf16", 0, 1, self.in_ld[l], hdim, B, ptr(xT), self.B,
-                        ptr(self.dhbT[l]), self.B, ptr(self.w_slab), self.out_ld[l], 0, 3, None, 0, splits,
+                # dW = X^T dY straight from the batch-major bf16 activations and gradients
+                # (transposing LDS reads inside the kernel: no X^T / dY^T copies)
+                xl = self.x0b if l == 0 else self.hb[l - 1]
+                self._c("gemm_dw_l%d" % l, "dl_gemm_bf16", 1, 0, self.in_ld[l], hdim, B, ptr(xl), self.in_ld[l],
+                        ptr(self.dhb[l]), self.h_ld[l], ptr(self.w_slab), self.out_ld[l], 0, 3, None, 0, splits,
                         stride, s)
                 if l > 0:   # dX = dY . W^T, ReluGrad by the bf16 activations, bf16 out
                     self._c("gemm_dx_l%d" % l, "dl_gemm_bf16", 0, 1, B, sp.hidden[l - 1], self.out_ld[l],
                             ptr(self.dhb[l]), self.h_ld[l], ptr(self.Wb[l]), self.out_ld[l], ptr(self.dhb[l - 1]),
                             self.h_ld[l - 1], 1, 2, ptr(self.hb[l - 1]), self.h_ld[l - 1], 1, 0, s)
-                    self._c("dhT_l%d" % (l - 1), "dl_transpose_bf16", ptr(self.dhb[l - 1]), 0, B, self.h_ld[l - 1],
-                            self.h_ld[l - 1], ptr(self.dhbT[l - 1]), self.B, s)
                 else:       # dx0 stays fp32 for the embedding backward
                     self._c("gemm_dx_l0", "dl_gemm_bf16", 0, 1, B, self.dx_cols, self.out_ld[0], ptr(self.dhb[0]),
                             self.h_ld[0], ptr(self.Wb[0]), self.out_ld[0], ptr(self.dx0), self.dx_ld, 0, 0, None, 0,

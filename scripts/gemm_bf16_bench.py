@@ -31,6 +31,8 @@ cases = {
                                      u16(h), 416, 1, 0, s), 2 * B * 400 * 400),
     "dw_l1 split64": (lambda: call("dl_gemm_bf16", 0, 1, 416, 400, B, u16(hT), B, u16(dhT), B, ptr(slab), 400, 0, 3, None, 0,
                                    64, 416 * 400, s), 2 * B * 417 * 400),
+    "dw_l1 direct (ta=1) split64": (lambda: call("dl_gemm_bf16", 1, 0, 416, 400, B, u16(h), 416, u16(out_b), 416,
+                                                 ptr(slab), 400, 0, 3, None, 0, 64, 416 * 400, s), 2 * B * 417 * 400),
     "transpose_bf16 [B,416]": (lambda: call("dl_transpose_bf16", u16(h), 0, B, 416, 416, u16(hT), B, s), 0),
     "cast_bf16 [B,416]": (lambda: call("dl_cast_bf16", ptr(out_f), B, 416, 416, u16(out_b), 416, s), 0),
 }

@@ -126,8 +126,9 @@ def test_gemm_bf16_variants(hip_lib, ta, tb, epi, cbf):
     ldb = K if tb else N
     splits = 4 if epi == 3 else 1
     C = torch.zeros(splits * M * N, dtype=torch.bfloat16 if cbf else torch.float32, device="cuda")
+    md = mask.cuda()
     call("dl_gemm_bf16", ta, tb, M, N, K, ptr(Ad), lda, ptr(Bd), ldb, ptr(C), N, cbf, epi,
-         ptr(mask.cuda()) if epi == 2 else None, N, splits, M * N, _s())
+         ptr(md) if epi == 2 else None, N, splits, M * N, _s())
     torch.cuda.synchronize()
     got = C.double().cpu().view(splits, M, N).sum(0)
     tol = 2e-2 if cbf else 1e-3          # bf16 output: one bf16 rounding (2^-8 relative)
@@ -447,8 +448,8 @@ def test_gemm_bf16_b_resident(hip_lib, M, N, K, epi, cbf):
         ref = torch.where(mask.double() > 0, ref, torch.zeros_like(ref))
     ldc = N + 3
     C = torch.full((M, ldc), 5.0, device="cuda", dtype=torch.bfloat16 if cbf else torch.float32)
-    md = mask.cuda()
-    call("dl_gemm_bf16", 0, 1, M, N, K, ptr(A.cuda()), lda, ptr(Bt.cuda()), lda, ptr(C), ldc, cbf, epi,
+    md, Ad, Bd = mask.cuda(), A.cuda(), Bt.cuda()    # held for the launch (no freed temporaries)
+    call("dl_gemm_bf16", 0, 1, M, N, K, ptr(Ad), lda, ptr(Bd), lda, ptr(C), ldc, cbf, epi,
          ptr(md) if epi == 2 else None, N, 1, 0, _s())
     torch.cuda.synchronize()
     out = C[:, :N].double().cpu()
@@ -456,3 +457,23 @@ def test_gemm_bf16_b_resident(hip_lib, M, N, K, epi, cbf):
     tol = 1e-2 if cbf else 1e-5                      # bf16 output rounding vs fp32 accumulation
     assert ((out - ref).abs() / scale).max().item() < tol
     assert (C[:, N:].float().cpu() == 5.0).all()
+
+
+@pytest.mark.parametrize("M,N,K,splits", [(432, 400, 65536, 64), (416, 400, 40000, 7), (264, 208, 1000, 3),
+                                          (64, 16, 96, 1)])
+def test_gemm_bf16_dw_transposed_reads(hip_lib, M, N, K, splits):
+    """Weight gradients of the bf16 tower from batch-major operands (ta=1, tb=0, split slabs):
+    the transposing-LDS-read kernel against an fp64 product of the same bf16 inputs, with
+    ragged M tiles, K steps and splits."""
+    g = torch.Generator().manual_seed(M + N + K)
+    X = torch.randn(K, M, generator=g).bfloat16()
+    Y = torch.randn(K, N, generator=g).bfloat16()
+    ref = X.double().t() @ Y.double()
+    slab = torch.full((splits, M, N), 0.0, device="cuda")
+    Xd, Yd = X.cuda(), Y.cuda()     # held: a freed temporary's block can be handed to the next .cuda()
+    call("dl_gemm_bf16", 1, 0, M, N, K, ptr(Xd), M, ptr(Yd), N, ptr(slab), N, 0, 3, None, 0, splits,
+         M * N, _s())
+    torch.cuda.synchronize()
+    got = slab.double().sum(0).cpu()
+    scale = (X.double().abs().t() @ Y.double().abs()).clamp(min=1.0)
+    assert ((got - ref).abs() / scale).max().item() < 5e-4
