@@ -25,7 +25,7 @@ class EmbLayout(C.Structure):
         ("zero_row0", C.c_int32), ("x0_ld", C.c_int32), ("x0_cont_col", C.c_int32),
         ("x0_vec_col", C.c_int32), ("x0_cat_col", C.c_int32), ("x0_pool_col", C.c_int32),
         ("fm_ld", C.c_int32), ("dx0_ld", C.c_int32), ("dx0_cat_col", C.c_int32), ("multi_width", C.c_int32),
-        ("cont_rows_compact", C.c_int32),
+        ("cont_rows_compact", C.c_int32), ("x0_bf16", C.c_int32),
     ]
 
 
@@ -71,6 +71,8 @@ SIGNATURES = {
     "dl_head_fwd_bwd": (I32, [I32, I32, I32, P, I32, P, I32, P, P, F, F, P, P, P, P, P, I32, P]),
     "dl_head_grid": (I32, [I32]),
     "dl_wdl_head_fwd_bwd": (I32, [I32, I32, I32, P, I32, P, I32, P, P, I64, P, F, F, P, P, P, P, P, P, P, I32, P, P]),
+    "dl_wdl_head_fwd_bwd_bf16": (I32, [I32, I32, I32, P, I32, P, I32, P, P, I64, P, F, F, P, P, P, P, P, P, P, I32, P,
+                                       P]),
     "dl_slab_fold_rows": (I32, [P, I32, I32, I32, I32, P, I64, P, P]),
     "dl_adam_begin_step": (I32, [P, F, F, P]),
     "dl_adam_dense": (I32, [P, P, P, P, I32, I64, I64, F, I64, P, P, P, P]),

@@ -144,6 +144,8 @@ __global__ __launch_bounds__(256) void embed_fwd_kernel(EmbArgs a) {
     for (int j = wid; j < nb; j += 4) {
       const int b = b0 + j;
       float* xb = a.x0 + (int64_t)b * L.x0_ld;
+      // bf16 x0 (L.x0_bf16): the same columns, as bf16 (a.x0 then points at uint16 storage)
+      unsigned short* xbb = reinterpret_cast<unsigned short*>(a.x0) + (int64_t)b * L.x0_ld;
       float4 v[NPS];
       int rw[NPS];
 #pragma unroll
@@ -210,7 +212,12 @@ __global__ __launch_bounds__(256) void embed_fwd_kernel(EmbArgs a) {
             ss.x = fmaf(ev.x, ev.x, ss.x); ss.y = fmaf(ev.y, ev.y, ss.y);
             ss.z = fmaf(ev.z, ev.z, ss.z); ss.w = fmaf(ev.w, ev.w, ss.w);
           } else if (sl < nslot) {
-            *reinterpret_cast<float4*>(xb + L.x0_cat_col + (sl - Fs) * E + 4 * q) = t4;
+            const int col = L.x0_cat_col + (sl - Fs) * E + 4 * q;
+            if (L.x0_bf16)
+              *reinterpret_cast<uint2*>(xbb + col) = make_uint2(f2bf(t4.x) | ((unsigned)f2bf(t4.y) << 16),
+                                                                f2bf(t4.z) | ((unsigned)f2bf(t4.w) << 16));
+            else
+              *reinterpret_cast<float4*>(xb + col) = t4;
           }
         }
       }
@@ -245,11 +252,15 @@ __global__ __launch_bounds__(256) void embed_fwd_kernel(EmbArgs a) {
         }
       }
       if (L.x0_cont_col >= 0)
-        for (int jj = lane; jj < L.cont_fields; jj += 64)
-          xb[L.x0_cont_col + jj] = a.cont[(int64_t)b * L.cont_fields + jj];
+        for (int jj = lane; jj < L.cont_fields; jj += 64) {
+          const float c = a.cont[(int64_t)b * L.cont_fields + jj];
+          if (L.x0_bf16) xbb[L.x0_cont_col + jj] = f2bf(c); else xb[L.x0_cont_col + jj] = c;
+        }
       if (L.x0_vec_col >= 0)
-        for (int jj = lane; jj < L.vector_size; jj += 64)
-          xb[L.x0_vec_col + jj] = a.vec[(int64_t)b * L.vector_size + jj];
+        for (int jj = lane; jj < L.vector_size; jj += 64) {
+          const float c = a.vec[(int64_t)b * L.vector_size + jj];
+          if (L.x0_bf16) xbb[L.x0_vec_col + jj] = f2bf(c); else xb[L.x0_vec_col + jj] = c;
+        }
     }
     __syncthreads();
   }
@@ -585,6 +596,7 @@ static int check_layout(const dl_emb_layout* L) {
   DL_CHECK_ARG(E == 4 || E == 8 || E == 16 || E == 32 || E == 64, "emb_dim %d not in {4,8,16,32,64}", E);
   DL_CHECK_ARG(L->batch >= 0 && L->n_rows > 0, "bad batch/n_rows");
   DL_CHECK_ARG(L->x0_ld % 4 == 0 && L->x0_cat_col % 4 == 0, "x0_ld and x0_cat_col must be multiples of 4");
+  DL_CHECK_ARG(!L->x0_bf16 || L->fm_extra == 0, "bf16 x0 needs fm_extra == 0 (pooled vectors are read as f32)");
   DL_CHECK_ARG(!L->fm_extra || L->x0_pool_col % 4 == 0, "x0_pool_col must be a multiple of 4");
   DL_CHECK_ARG(L->cont_fields <= kMaxHotCont || !(L->use_fm && L->fm_cont),
                "at most %d FM cont fields", kMaxHotCont);

@@ -320,14 +320,6 @@ void gemm_f32_kernel(GemmParams p) {
 // bf16 variant (Wide&Deep tower): 16x16x32 bf16 MFMA, K-step 32, fp32 accumulate.
 typedef short shortx8 __attribute__((ext_vector_type(8)));
 
-__device__ __forceinline__ float bf2f(unsigned short h) { return __uint_as_float(((unsigned)h) << 16); }
-__device__ __forceinline__ unsigned short f2bf(float f) {
-  // round-to-nearest-even; NaN kept NaN
-  unsigned u = __float_as_uint(f);
-  if ((u & 0x7f800000u) == 0x7f800000u && (u & 0x7fffffu)) return (unsigned short)((u >> 16) | 0x40);
-  u += 0x7fffu + ((u >> 16) & 1u);
-  return (unsigned short)(u >> 16);
-}
 
 template <int BM, int BN, int WM, int WN, bool TA, bool TB, int EPI, bool CBF16>
 __global__ __launch_bounds__(256) void gemm_bf16_kernel(GemmParams p) {

@@ -134,13 +134,20 @@ __global__ __launch_bounds__(256) void head_kernel(int B, int fm_cols, int H, co
 // in that range.  Wide rows get dz by f32 atomics into g_w (+ touched flag); the
 // dense part leaves per-block partials slab[block][0..H) = sum dz*h_j,
 // [H] = sum dz (bias), [H+1] = sum loss_b.
+//
+// One wave per sample, samples strided over the grid.  The wide lookups are two
+// dependent round trips (ids, then weights), so they run ahead of the sample being
+// reduced: ids two samples ahead, weights one ahead; only the h row load is left on
+// a sample's critical path.  DHB: dh written as bf16 (the bf16 tower's dY operand,
+// no separate cast pass).
+template <bool DHB>
 __global__ __launch_bounds__(256) void wdl_head_kernel(int B, int Fw, int H, const int64_t* __restrict__ wide,
                                                        int wide_ld, const float* __restrict__ h, int ldh,
                                                        const float* __restrict__ w, const float* __restrict__ bias,
                                                        long long w_rows, const float* __restrict__ label, float eps,
                                                        float inv_batch, float* __restrict__ score,
                                                        float* __restrict__ z_out, float* __restrict__ dz,
-                                                       float* __restrict__ dh, float* __restrict__ g_w,
+                                                       void* __restrict__ dh_out, float* __restrict__ g_w,
                                                        uint8_t* __restrict__ touched, float* __restrict__ slab,
                                                        int32_t* err) {
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
@@ -158,15 +165,23 @@ __global__ __launch_bounds__(256) void wdl_head_kernel(int B, int Fw, int H, con
     wh[k].w = c + 3 < H ? w[Fw + c + 3] : 0.f;
     gh[k] = make_float4(0.f, 0.f, 0.f, 0.f);
   }
+  // this lane's wide id of sample bb, validated (-1: none or out of range)
+  auto load_id = [&](int bb) -> long long {
+    if (bb >= B || lane >= Fw) return -1;
+    const long long r = wide[(long long)bb * wide_ld + lane];
+    if (r < 0 || r >= w_rows) { if (err) atomicOr(err, 1); return -1; }
+    return r;
+  };
+  long long id_n = load_id(wave);
+  float wv_n = id_n >= 0 ? w[id_n] : 0.f;
+  long long id_nn = load_id(wave + nwaves);
   float gb = 0.f, lsum = 0.f;
   for (int b = wave; b < B; b += nwaves) {
-    float part = 0.f;
-    long long wr = -1;
-    if (lane < Fw) {
-      wr = wide[(long long)b * wide_ld + lane];
-      if (wr < 0 || wr >= w_rows) { if (err) atomicOr(err, 1); wr = -1; }
-      else part += w[wr];
-    }
+    const long long wr = id_n;
+    float part = wv_n;
+    id_n = id_nn;
+    wv_n = id_n >= 0 ? w[id_n] : 0.f;
+    id_nn = load_id(b + 2 * nwaves);
     float4 hh[kHeadMaxH4];
     const float* hb = h + (long long)b * ldh;
 #pragma unroll
@@ -190,7 +205,6 @@ __global__ __launch_bounds__(256) void wdl_head_kernel(int B, int Fw, int H, con
       atomicAdd(g_w + wr, g);
       touched[wr] = 1;
     }
-    float* dhb = dh + (long long)b * ldh;
 #pragma unroll
     for (int k = 0; k < kHeadMaxH4; ++k) {
       const int c4 = lane + 64 * k;
@@ -199,8 +213,24 @@ __global__ __launch_bounds__(256) void wdl_head_kernel(int B, int Fw, int H, con
         const int c = 4 * c4;
         float o[4] = {hh[k].x > 0.f ? g * wh[k].x : 0.f, hh[k].y > 0.f ? g * wh[k].y : 0.f,
                       hh[k].z > 0.f ? g * wh[k].z : 0.f, hh[k].w > 0.f ? g * wh[k].w : 0.f};
-        for (int e = 0; e < 4; ++e)
-          if (c + e < H) dhb[c + e] = o[e];
+        if (DHB) {
+          unsigned short* d = reinterpret_cast<unsigned short*>(dh_out) + (long long)b * ldh + c;
+          if (c + 4 <= H) {
+            *reinterpret_cast<uint2*>(d) = make_uint2(f2bf(o[0]) | ((unsigned)f2bf(o[1]) << 16),
+                                                      f2bf(o[2]) | ((unsigned)f2bf(o[3]) << 16));
+          } else {
+            for (int e = 0; e < 4; ++e)
+              if (c + e < H) d[e] = f2bf(o[e]);
+          }
+        } else {
+          float* d = reinterpret_cast<float*>(dh_out) + (long long)b * ldh + c;
+          if (c + 4 <= H) {
+            *reinterpret_cast<float4*>(d) = make_float4(o[0], o[1], o[2], o[3]);
+          } else {
+            for (int e = 0; e < 4; ++e)
+              if (c + e < H) d[e] = o[e];
+          }
+        }
       }
     }
   }
@@ -246,24 +276,43 @@ __global__ __launch_bounds__(256) void slab_fold_rows_kernel(const float* __rest
 
 using namespace dl;
 
-extern "C" int dl_wdl_head_fwd_bwd(int32_t B, int32_t Fw, int32_t H, const int64_t* wide, int32_t wide_ld,
-                                   const float* h, int32_t ldh, const float* w, const float* bias, int64_t w_rows,
-                                   const float* label, float eps, float inv_batch, float* score, float* z_out,
-                                   float* dz, float* dh, float* g_w, uint8_t* touched, float* slab,
-                                   int32_t slab_blocks, int32_t* err, void* stream) {
+template <bool DHB>
+static int wdl_head(int32_t B, int32_t Fw, int32_t H, const int64_t* wide, int32_t wide_ld, const float* h,
+                    int32_t ldh, const float* w, const float* bias, int64_t w_rows, const float* label, float eps,
+                    float inv_batch, float* score, float* z_out, float* dz, void* dh, float* g_w, uint8_t* touched,
+                    float* slab, int32_t slab_blocks, int32_t* err, void* stream) {
   DL_CHECK_ARG(Fw >= 0 && Fw <= 64, "Fw %d not in [0, 64]", Fw);
   DL_CHECK_ARG(H > 0 && H <= 4 * 64 * kHeadMaxH4, "H %d too large", H);
   DL_CHECK_ARG(w_rows >= Fw + H, "wdl_weights must have >= Fw + H rows");
   DL_CHECK_ARG(ldh % 4 == 0 && ldh >= H && ((uintptr_t)h % 16) == 0, "h must be 16-B aligned, ldh %% 4 == 0");
+  DL_CHECK_ARG(((uintptr_t)dh % (DHB ? 8 : 16)) == 0, "dh must be %d-B aligned", DHB ? 8 : 16);
   DL_CHECK_ARG(w && bias && label && score && dz && dh && slab && (!g_w || touched), "NULL argument");
   const int grid = dl_head_grid(B);
   DL_CHECK_ARG(slab_blocks >= grid, "slab needs %d blocks", grid);
   if (B == 0) return 0;
   const size_t lds = 4 * (size_t)(H + 2) * sizeof(float);
-  hipLaunchKernelGGL(wdl_head_kernel, dim3(grid), dim3(256), lds, as_stream(stream), B, Fw, H, wide, wide_ld, h,
-                     ldh, w, bias, (long long)w_rows, label, eps, inv_batch, score, z_out, dz, dh, g_w, touched,
+  hipLaunchKernelGGL(wdl_head_kernel<DHB>, dim3(grid), dim3(256), lds, as_stream(stream), B, Fw, H, wide, wide_ld,
+                     h, ldh, w, bias, (long long)w_rows, label, eps, inv_batch, score, z_out, dz, dh, g_w, touched,
                      slab, err);
-  DL_RETURN_LAUNCH("dl_wdl_head_fwd_bwd");
+  DL_RETURN_LAUNCH(DHB ? "dl_wdl_head_fwd_bwd_bf16" : "dl_wdl_head_fwd_bwd");
+}
+
+extern "C" int dl_wdl_head_fwd_bwd(int32_t B, int32_t Fw, int32_t H, const int64_t* wide, int32_t wide_ld,
+                                   const float* h, int32_t ldh, const float* w, const float* bias, int64_t w_rows,
+                                   const float* label, float eps, float inv_batch, float* score, float* z_out,
+                                   float* dz, float* dh, float* g_w, uint8_t* touched, float* slab,
+                                   int32_t slab_blocks, int32_t* err, void* stream) {
+  return wdl_head<false>(B, Fw, H, wide, wide_ld, h, ldh, w, bias, w_rows, label, eps, inv_batch, score, z_out, dz,
+                         dh, g_w, touched, slab, slab_blocks, err, stream);
+}
+
+extern "C" int dl_wdl_head_fwd_bwd_bf16(int32_t B, int32_t Fw, int32_t H, const int64_t* wide, int32_t wide_ld,
+                                        const float* h, int32_t ldh, const float* w, const float* bias,
+                                        int64_t w_rows, const float* label, float eps, float inv_batch, float* score,
+                                        float* z_out, float* dz, uint16_t* dh, float* g_w, uint8_t* touched,
+                                        float* slab, int32_t slab_blocks, int32_t* err, void* stream) {
+  return wdl_head<true>(B, Fw, H, wide, wide_ld, h, ldh, w, bias, w_rows, label, eps, inv_batch, score, z_out, dz,
+                        dh, g_w, touched, slab, slab_blocks, err, stream);
 }
 
 extern "C" int dl_slab_fold_rows(const float* slab, int32_t blocks, int32_t width, int32_t col0, int32_t n,

@@ -282,11 +282,14 @@ class CTREngine:
             self.h.append(t)
         self.dh = [z(B, self.h_ld[l]) for l in range(len(sp.hidden))]
         self.bf = sp.tower == "bf16"
+        # bf16 tower without pooled fields: the embedding forward writes the bf16 x0 itself
+        self.x0_direct = self.bf and not sp.M
         if self.bf:
             # bf16 tower operands: x0 and hidden activations (bias ones columns included),
             # gradients, and bf16 copies of the fp32 master weights (refreshed after each update)
             zb = lambda *sh: torch.zeros(*sh, dtype=torch.bfloat16, device=dev)
             self.x0b = zb(B, self.in_ld[0])
+            self.x0b[:, self.D0] = 1.0
             self.hb = []
             for l, hdim in enumerate(sp.hidden[:-1]):
                 t = zb(B, self.h_ld[l])
@@ -388,6 +391,7 @@ class CTREngine:
         L.dx0_cat_col = 0
         L.multi_width = sp.multi_width if self.lazy else 0
         L.cont_rows_compact = 1 if self.lazy else 0     # records: cont rows gathered first into rows_u
+        L.x0_bf16 = 1 if self.x0_direct else 0           # bf16 tower: the forward writes x0 as bf16
         return L
 
     # ------------------------------------------------------------------ params
@@ -612,6 +616,7 @@ class CTREngine:
         sp = self.spec
         L = self.layout
         L.batch = B
+        x0 = self.x0b if self.x0_direct else self.x0
         if sp.M and not self.lazy:  # pooled vectors must be in x0 before the FM second order reads them
             self._c("pool_fwd", "dl_pool_fwd", C_ref(L), ptr(self.table), ptr(self.first) if sp.fm else None,
                  ptr(self.in_cate), sp.S, ptr(self.slot_start), ptr(self.slot_end), sp.M, self.fm_pool_col,
@@ -624,7 +629,7 @@ class CTREngine:
             self._c("embed_fwd", "dl_embed_fwd_rec", C_ref(L), ptr(self.rec), self.rec_ld, int(sp.fm),
                     ptr(self.rows_u), ptr(self.rows_u1) if sp.fm else None, ptr(self.in_cate), ptr(self.in_cont),
                     ptr(self.in_vec), ptr(self.hist), self.hist_len, ptr(self.opt), 1 if train else 0,
-                    ptr(self.x0), ptr(self.fm_out), ptr(self.fm_sum), ptr(self.err), s)
+                    ptr(x0), ptr(self.fm_out), ptr(self.fm_sum), ptr(self.err), s)
         elif self.lazy:
             # rows of the batch (index built by _pre), caught up to the step being taken
             self._c("rec_gather", "dl_rec_gather", C_ref(L), ptr(self.rec), self.rec_ld, int(sp.fm), self.n_rep,
@@ -638,17 +643,18 @@ class CTREngine:
                         ptr(self.cnt_first), s)
             self._c("embed_fwd", "dl_embed_fwd_indexed", C_ref(L), ptr(self.rows_u),
                     ptr(self.rows_u1) if sp.fm else None, ptr(self.idx_inv), self.n_rep, ptr(self.in_cont),
-                    ptr(self.in_vec), ptr(self.x0), ptr(self.fm_out), ptr(self.fm_sum), s)
+                    ptr(self.in_vec), ptr(x0), ptr(self.fm_out), ptr(self.fm_sum), s)
         else:
             self._c("embed_fwd", "dl_embed_fwd", C_ref(L), ptr(self.table), ptr(self.first), ptr(self.in_cate),
-                    ptr(self.in_cont), ptr(self.in_vec), ptr(self.x0), ptr(self.fm_out), ptr(self.fm_sum),
+                    ptr(self.in_cont), ptr(self.in_vec), ptr(x0), ptr(self.fm_out), ptr(self.fm_sum),
                     ptr(self.err), s)
         nl = len(sp.hidden)
         if self.bf:
             # bf16 tower: x0 -> bf16, ReLU layers on bf16 MFMA (fp32 accumulate), the last layer's
             # output kept fp32 for the fp32 head / wide cross logit (config C5)
-            self._c("cast_x0", "dl_cast_bf16", ptr(self.x0), B, self.in_ld[0], self.in_ld[0], ptr(self.x0b),
-                    self.in_ld[0], s)
+            if not self.x0_direct:
+                self._c("cast_x0", "dl_cast_bf16", ptr(self.x0), B, self.in_ld[0], self.in_ld[0], ptr(self.x0b),
+                        self.in_ld[0], s)
             xb = self.x0b
             for l, hdim in enumerate(sp.hidden):
                 last = l == nl - 1
@@ -666,9 +672,11 @@ class CTREngine:
                 x = self.h[l]
         H = sp.hidden[-1]
         if self.wdl:
-            self._c("head", "dl_wdl_head_fwd_bwd", B, sp.Fw, H, ptr(self.in_wide), self.in_wide.shape[1],
+            # bf16 tower: dY of the last layer written as bf16 by the head itself (no cast pass)
+            fn, dh_last = ("dl_wdl_head_fwd_bwd_bf16", self.dhb[-1]) if self.bf else ("dl_wdl_head_fwd_bwd", self.dh[-1])
+            self._c("head", fn, B, sp.Fw, H, ptr(self.in_wide), self.in_wide.shape[1],
                     ptr(self.h[-1]), self.h_ld[-1], ptr(self.ww), ptr(self.wb), self.w_rows, ptr(self.in_label),
-                    sp.logloss_eps, 1.0 / B, ptr(self.score), ptr(self.z), ptr(self.dz), ptr(self.dh[-1]),
+                    sp.logloss_eps, 1.0 / B, ptr(self.score), ptr(self.z), ptr(self.dz), ptr(dh_last),
                     ptr(self.wg) if train else None, ptr(self.w_touched) if train else None,
                     ptr(self.head_slab), self.head_blocks, ptr(self.err), s)
             return
@@ -704,7 +712,7 @@ class CTREngine:
         self._forward(B, s, train=True)
         nl = len(sp.hidden)
         splits = max(1, min(self.splits, B // 1024))
-        if self.bf:
+        if self.bf and not self.wdl:      # the wdl head writes its bf16 dY itself
             self._c("cast_dh", "dl_cast_bf16", ptr(self.dh[-1]), B, self.h_ld[-1], self.h_ld[-1], ptr(self.dhb[-1]),
                     self.h_ld[-1], s)
         for l in reversed(range(nl)):

@@ -79,6 +79,10 @@ typedef struct dl_emb_layout {
                                of them is the zero row is still decided on the table row
                                fm_cont_offset + f (deepfm_multi.py:139 puts them after the
                                cate ids; deepfm_pipeline.py:58-61 at the top)           */
+  int32_t x0_bf16;          /* 1: the forward's x0 is a bf16 matrix (uint16, x0_ld elements per
+                               sample; the bf16 tower's first operand, config C5): cate, cont
+                               and vector columns are written rounded to nearest-even.
+                               Requires fm_extra == 0 (pooled vectors are read back as f32) */
 } dl_emb_layout;
 
 /* Embedding gather + FM first/second order + deep-input assembly (forward).
@@ -267,6 +271,13 @@ int dl_wdl_head_fwd_bwd(int32_t B, int32_t Fw, int32_t H, const int64_t* wide, i
                         const float* label, float eps, float inv_batch, float* score, float* z_out,
                         float* dz, float* dh, float* g_w, uint8_t* touched, float* slab,
                         int32_t slab_blocks, int32_t* err, void* stream);
+/* As dl_wdl_head_fwd_bwd with dh written as bf16 (round-to-nearest-even): the bf16
+ * tower's dY operand (config C5), 8-B aligned, same leading dimension ldh as h. */
+int dl_wdl_head_fwd_bwd_bf16(int32_t B, int32_t Fw, int32_t H, const int64_t* wide, int32_t wide_ld,
+                             const float* h, int32_t ldh, const float* w, const float* bias, int64_t w_rows,
+                             const float* label, float eps, float inv_batch, float* score, float* z_out,
+                             float* dz, uint16_t* dh, float* g_w, uint8_t* touched, float* slab,
+                             int32_t slab_blocks, int32_t* err, void* stream);
 /* g[row0+j] += sum over `blocks` slab rows of slab[blk*width + col0 + j], j < n. */
 int dl_slab_fold_rows(const float* slab, int32_t blocks, int32_t width, int32_t col0, int32_t n,
                       float* g, int64_t row0, uint8_t* touched, void* stream);

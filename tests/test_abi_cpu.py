@@ -44,7 +44,7 @@ def test_library_loads_and_reports_errors(lib):
 
 def test_layout_struct_size(lib):
     import ctypes
-    assert ctypes.sizeof(lib.EmbLayout) == 4 * 8 + 19 * 4 + 4  # 4 int64 + 19 int32 + pad
+    assert ctypes.sizeof(lib.EmbLayout) == 4 * 8 + 21 * 4 + 4  # 4 int64 + 21 int32 + pad
 
 
 def test_reader_header_symbols_exported():

@@ -477,3 +477,41 @@ def test_gemm_bf16_dw_transposed_reads(hip_lib, M, N, K, splits):
     got = slab.double().sum(0).cpu()
     scale = (X.double().abs().t() @ Y.double().abs()).clamp(min=1.0)
     assert ((got - ref).abs() / scale).max().item() < 5e-4
+
+
+@pytest.mark.parametrize("B", [3000, 70])
+def test_wdl_head_bf16_dy_is_rounded_f32_dy(hip_lib, B):
+    """dl_wdl_head_fwd_bwd_bf16 (the C5 head writing the bf16 tower's dY itself, with the
+    wide ids and weights loaded ahead of the sample being reduced): score, z, dz and the
+    block partials bit-identical to the f32 head, dY equal to the f32 dY rounded to
+    nearest-even, z against an fp64 restatement of models/wdl.py:225-264."""
+    g = torch.Generator().manual_seed(B)
+    Fw, H, rows, ldh = 26, 400, 5000, 404
+    wide = torch.randint(0, rows, (B, Fw), generator=g)
+    h = torch.randn(B, ldh, generator=g).clamp_min(0)
+    w = torch.randn(rows, generator=g) * 0.1
+    bias = torch.tensor([0.1, 0.0, 0.0, 0.0])
+    label = (torch.rand(B, generator=g) > 0.5).float()
+    wide_d, h_d, w_d, bias_d, label_d = wide.cuda(), h.cuda(), w.cuda(), bias.cuda(), label.cuda()
+    grid = _lib.lib().dl_head_grid(B)
+    outs = []
+    for bf in (0, 1):
+        score, z, dz = (torch.zeros(B, device="cuda") for _ in range(3))
+        dh = torch.zeros(B, ldh, device="cuda", dtype=torch.bfloat16 if bf else torch.float32)
+        gw = torch.zeros(rows, device="cuda")
+        touched = torch.zeros(rows, device="cuda", dtype=torch.uint8)
+        slab = torch.zeros(grid * (H + 2), device="cuda")
+        err = torch.zeros(4, device="cuda", dtype=torch.int32)
+        call("dl_wdl_head_fwd_bwd_bf16" if bf else "dl_wdl_head_fwd_bwd", B, Fw, H, ptr(wide_d), Fw, ptr(h_d), ldh,
+             ptr(w_d), ptr(bias_d), rows, ptr(label_d), 1e-7, 1.0 / B, ptr(score), ptr(z), ptr(dz), ptr(dh), ptr(gw),
+             ptr(touched), ptr(slab), grid, ptr(err), _s())
+        torch.cuda.synchronize()
+        assert err.cpu().sum().item() == 0
+        outs.append((score.cpu(), z.cpu(), dz.cpu(), dh[:, :H].cpu(), gw.cpu(), touched.cpu(), slab.cpu()))
+    f, b = outs
+    for i in (0, 1, 2, 5, 6):
+        assert torch.equal(f[i], b[i])
+    assert torch.equal(b[3], f[3].bfloat16())
+    np.testing.assert_allclose(b[4].numpy(), f[4].numpy(), rtol=1e-5, atol=1e-9)   # atomics: order differs
+    z_ref = w.double()[wide].sum(1) + h[:, :H].double() @ w.double()[Fw:Fw + H] + 0.1
+    np.testing.assert_allclose(f[1].double().numpy(), z_ref.numpy(), rtol=0, atol=1e-4)
