@@ -38,7 +38,7 @@ def log(*a):
     print("[bench %s]" % time.strftime("%H:%M:%S"), *a, file=sys.stderr, flush=True)
 
 
-def kernel_work(spec, B, touched_rows, rows=None, uniq=None, shard=None):
+def kernel_work(spec, B, touched_rows, rows=None, uniq=None, shard=None, wide_rows=None):
     """Algorithmic bytes / flops per launch."""
     E, S, C = spec.E, spec.S, spec.C
     N = rows if rows is not None else spec.n_rows
@@ -59,12 +59,14 @@ def kernel_work(spec, B, touched_rows, rows=None, uniq=None, shard=None):
     if uniq is not None:
         # row records (adam='lazy'): U unique rows of the batch, record = p, w1 triple + stamp, m, v
         rec_b = (3 * E + 4) * 4
+        refs = 2 * S if spec.fm else S            # FM + deep references per sample (wdl/dnn: deep only)
+        xb = 2 if spec.tower == "bf16" else 4      # x0 element bytes (the bf16 tower's x0 is written as bf16)
         # gather: read U records, write the compact rows (E + 1 floats) + keys
         w["rec_gather"] = ("hbm", uniq * (rec_b + (E + 1) * 4 + 4))
-        # indexed x0 assembly: 2S refs/sample x (compact row + inv) + first-order + x0 cat write
-        w["embed_fwd"] = ("hbm", B * (2 * S * (E * 4 + 4) + S * 4 + S * E * 4))
+        # indexed x0 assembly: refs/sample x (compact row + inv) + first-order (FM) + x0 cat write
+        w["embed_fwd"] = ("hbm", B * (refs * (E * 4 + 4) + (S * 4 if spec.fm else 0) + S * E * xb))
         # fused backward + Adam: U records read + written, per ref: ref id + dx0/fm_sum row + dz
-        w["embed_bwd"] = ("hbm", uniq * (2 * rec_b + 4 + 8) + B * 2 * S * (4 + E * 4 + 4))
+        w["embed_bwd"] = ("hbm", uniq * (2 * rec_b + 4 + 8) + B * refs * (4 + E * 4 + 4))
     if shard is not None:
         # row-sharded engine (shard.py): this rank's batch needs U = nsend + nrep unique rows;
         # as an owner it serves nrecv of them (gather) and updates nrecv arrivals (rec_apply)
@@ -81,6 +83,15 @@ def kernel_work(spec, B, touched_rows, rows=None, uniq=None, shard=None):
         w.pop("adam_first", None)
     H = spec.hidden[-1]
     w["head"] = ("hbm", B * (spec.fm_cols + H) * 4 * 2)
+    Fw = getattr(spec, "Fw", 0)
+    if Fw:
+        # wdl cross logit: per sample Fw ids + weights + gradient atomics + touched bytes, the h row,
+        # the dY row (bf16 tower: bf16), label/score/z/dz
+        dyb = 2 if spec.tower == "bf16" else 4
+        w["head"] = ("hbm", B * (Fw * (8 + 4 + 4 + 1) + H * 4 + H * dyb + 16))
+        # wide Adam (L2 on every row: a dense sweep): p, m, v read + written, touched flag read;
+        # gradient read + reset where touched (at most B * Fw rows)
+        w["adam_wide"] = ("hbm", (wide_rows or 0) * (12 * 2 + 1) + B * Fw * 8)
     return w
 
 
@@ -291,8 +302,9 @@ def main():
     touched_rows = int(torch.unique(torch.cat([ids.reshape(-1) + spec.C, ids.reshape(-1)])).numel()) + spec.C
     shard_counts = getattr(eng, "last_counts", None) if sharded and getattr(eng, "lazy", False) else None
     uniq = int(eng.idx_n[0].item()) if getattr(eng, "lazy", False) and not sharded else None
+    ww = getattr(eng, "ww", None)
     work = kernel_work(spec, B, touched_rows, rows=getattr(eng, "local_rows", spec.n_rows), uniq=uniq,
-                       shard=shard_counts)
+                       shard=shard_counts, wide_rows=int(ww.shape[0]) if ww is not None else None)
     kernels = {}
     for label, ts in times.items():
         us = float(np.mean(ts))
@@ -307,7 +319,8 @@ def main():
                 ent["TFLOP/s"] = round(amount / (us * 1e-6) / 1e12, 2)
                 ent["frac_mfma"] = round(amount / (us * 1e-6) / 1e12 / peak, 3)
         kernels[label] = ent
-    dom = max((l for l in kernels), key=lambda l: kernels[l]["us"])
+    # the dominant kernel among those with an algorithmic work figure
+    dom = max((l for l in kernels if l in work), key=lambda l: kernels[l]["us"])
     kind, amount = work.get(dom, ("hbm", 0))
     us = kernels[dom]["us"]
     if kind == "hbm":
