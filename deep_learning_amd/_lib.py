@@ -70,6 +70,7 @@ SIGNATURES = {
     "dl_gemm_bf16": (I32, [I32, I32, I32, I32, I32, P, I32, P, I32, P, I32, I32, I32, P, I32, I32, I64, P]),
     "dl_head_fwd_bwd": (I32, [I32, I32, I32, P, I32, P, I32, P, P, F, F, P, P, P, P, P, I32, P]),
     "dl_head_grid": (I32, [I32]),
+    "dl_wdl_head_grid": (I32, [I32]),
     "dl_wdl_head_fwd_bwd": (I32, [I32, I32, I32, P, I32, P, I32, P, P, I64, P, F, F, P, P, P, P, P, P, P, I32, P, P]),
     "dl_wdl_head_fwd_bwd_bf16": (I32, [I32, I32, I32, P, I32, P, I32, P, P, I64, P, F, F, P, P, P, P, P, P, P, I32, P,
                                        P]),

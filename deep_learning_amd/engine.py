@@ -304,7 +304,8 @@ class CTREngine:
         self.fm_out = z(B, self.fm_ld)
         self.fm_sum = z(B, E)
         self.score, self.z, self.dz = z(B), z(B), z(B)
-        self.head_blocks = call_int("dl_head_grid", B)
+        self.head_grid = "dl_wdl_head_grid" if self.wdl else "dl_head_grid"   # slab rows per batch size
+        self.head_blocks = call_int(self.head_grid, B)
         self.head_slab = z(self.head_blocks, sp.fm_cols + H + 2)
         self.in_wide = z(B, max(sp.Fw, 1), dt=torch.int64)
         self.splits = max(1, min(64, B // 1024))
@@ -793,7 +794,7 @@ class CTREngine:
                  sp.S * sp.E, ptr(self.cnt_emb), ptr(self.cnt_first), ptr(self.tg), ptr(self.fmg),
                  ptr(self.touched), s)
         H = sp.hidden[-1]
-        hb = call_int("dl_head_grid", B)
+        hb = call_int(self.head_grid, B)
         if self.wdl:
             # wdl_weights: dense Adam with L2 on every row (wdl.py:270-271); the deep-output
             # rows get their batch sums folded in from the head slab first
@@ -952,7 +953,7 @@ class CTREngine:
         H = sp.hidden[-1]
         B = self.last_batch
         width = self.head_slab.shape[1]
-        rows = call_int("dl_head_grid", B)
+        rows = call_int(self.head_grid, B)
         data = self.head_slab[:rows, width - 1].double().sum().item() / B
         if sp.hidden_reg == "l1":   # l1_regularizer: scale * sum |W| (dnn.py:88-90)
             return data + sp.l2 * float(self.opt[8].item())

@@ -259,6 +259,8 @@ int dl_head_fwd_bwd(int32_t B, int32_t fm_cols, int32_t H, const float* fm_out, 
                     float eps, float inv_batch, float* score, float* z_out, float* dz,
                     float* dh, float* slab, int32_t slab_blocks, void* stream);
 int dl_head_grid(int32_t B);
+/* Blocks (= slab rows) of dl_wdl_head_fwd_bwd[_bf16] for batch B. */
+int dl_wdl_head_grid(int32_t B);
 
 /* Wide&Deep cross logit, forward and backward fused (models/wdl.py:225-275):
  * z = sum_f w[wide_f] + sum_j w[Fw+j] h_j + bias[0] (w = wdl_weights [w_rows]; the

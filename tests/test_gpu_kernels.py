@@ -493,7 +493,7 @@ def test_wdl_head_bf16_dy_is_rounded_f32_dy(hip_lib, B):
     bias = torch.tensor([0.1, 0.0, 0.0, 0.0])
     label = (torch.rand(B, generator=g) > 0.5).float()
     wide_d, h_d, w_d, bias_d, label_d = wide.cuda(), h.cuda(), w.cuda(), bias.cuda(), label.cuda()
-    grid = _lib.lib().dl_head_grid(B)
+    grid = _lib.lib().dl_wdl_head_grid(B)
     outs = []
     for bf in (0, 1):
         score, z, dz = (torch.zeros(B, device="cuda") for _ in range(3))

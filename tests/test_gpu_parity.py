@@ -112,8 +112,17 @@ def test_lazy_adam_bit_identical_to_dense(hip_lib, name, stash):
     """Row records + lazy catch-up (rec.hip) against the dense sweep with the same
     (sorted, deterministic) gradients: parameters, Adam moments, logits and
     predictions must be bit-identical.  A large table, a small batch and an 8-entry
-    alpha ring make rows lag many steps and force periodic flushes."""
+    alpha ring make rows lag many steps and force periodic flushes.
+
+    wdl: the wide-weight gradient (wdl_weights rows hit by wide ids) is accumulated by
+    f32 atomics in the head in both modes — order-dependent, like TF's GPU
+    UnsortedSegmentSum — so two runs may differ by an ulp there and through it in
+    everything downstream; that case is held to 1e-6 relative instead."""
     kw = dict(CASES[name], cate_index_size=50000)
+    if name == "wdl":
+        same = lambda a, b, err_msg="": np.testing.assert_allclose(a, b, rtol=1e-6, atol=1e-9, err_msg=err_msg)
+    else:
+        same = np.testing.assert_array_equal
     model = _model(name)
     spec = ModelSpec(model, **kw)
     dense = CTREngine(spec, max_batch=128, seed=3, bwd="sorted")
@@ -124,16 +133,15 @@ def test_lazy_adam_bit_identical_to_dense(hip_lib, name, stash):
         dense.train_step(b, graph=i >= 3)
         lazy.train_step(b, graph=i >= 3)
         torch.cuda.synchronize()
-        np.testing.assert_array_equal(lazy.z[:128].cpu().numpy(), dense.z[:128].cpu().numpy(),
-                                      err_msg="logits step %d" % i)
+        same(lazy.z[:128].cpu().numpy(), dense.z[:128].cpu().numpy(), err_msg="logits step %d" % i)
         if i == 10:
-            np.testing.assert_array_equal(lazy.predict(bs[0]), dense.predict(bs[0]))
+            same(lazy.predict(bs[0]), dense.predict(bs[0]))
     pd, pl = dense.params(), lazy.params()
     for k in pd:
-        np.testing.assert_array_equal(pl[k], pd[k], err_msg=k)
+        same(pl[k], pd[k], err_msg=k)
     sd, sl = dense.adam_state(), lazy.adam_state()
     for k in sd:
-        np.testing.assert_array_equal(sl[k], sd[k], err_msg=k)
+        same(sl[k], sd[k], err_msg=k)
 
 
 @pytest.mark.parametrize("name", ["deepfm_pipeline", "dnn_pipeline", "wdl"])
