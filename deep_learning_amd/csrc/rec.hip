@@ -175,8 +175,23 @@ __global__ __launch_bounds__(256) void rec_bwd_adam_kernel(SegGradIn sg, float* 
   const int t = (int)opt[7];
   const float alpha = opt[3];
   const bool first = c.has_first && q == 0;
+  // Software pipelining across this group's rows (each row is a chain of dependent loads:
+  // segment bounds -> first reference -> dz / fm_sum / dx0 rows): the bounds are loaded
+  // two rows ahead and the first reference one row ahead, so a row's own chain starts at
+  // its data loads.  The references are still summed in the same order.
+  SegRange nx = seg_range(sg, group0, nu, nrefs);
+  int kx = nx.e0 < nx.e1 ? sg.refs[nx.e0] : -1;
+  SegRange nn = seg_range(sg, group0 + ngroups, nu, nrefs);
+  uint32_t key_n = group0 < nu ? uniq[group0] : 0u;   // the row key too (the record load waits on it)
   for (long long u = group0; u < nu; u += ngroups) {
-    const int64_t row = decode_key(uniq[u], world);
+    const SegRange cr = nx;
+    const int kc = kx;
+    const uint32_t key = key_n;
+    nx = nn;
+    kx = nx.e0 < nx.e1 ? sg.refs[nx.e0] : -1;
+    nn = seg_range(sg, u + 2 * ngroups, nu, nrefs);
+    key_n = u + ngroups < nu ? uniq[u + ngroups] : 0u;
+    const int64_t row = decode_key(key, world);
     // the row's caught-up state (independent of the segment walk: issued first)
     const long long iu = n_rep + u;
     float4 p, m, v;
@@ -198,7 +213,7 @@ __global__ __launch_bounds__(256) void rec_bwd_adam_kernel(SegGradIn sg, float* 
       const int stamp = __float_as_int(tail.w);
       if (stamp < t - 1) catch_up4(p, m, v, w, wm, wv, first, stamp, t - 1, hist, c);
     }
-    const SegGrad4 s = segment_grad4<E>(sg, u, q, nrefs, wsec);
+    const SegGrad4 s = segment_grad4_range<E>(sg, cr.e0, cr.e1, kc, q, nrefs, wsec);
     if (!row_ok) continue;
     float4 g;
     g.x = seg_row_grad(s.s.x, s.dsum.x, s.x.x, s.dsum.x != 0.f ? p.x : 0.f);

@@ -78,20 +78,27 @@ struct SegGrad4 {
 };
 
 // Same sums for dims 4q..4q+3 of one row (one lane, float4 loads).
+// A unique row's reference range [e0, e1) in the sorted refs (empty past nu).
+struct SegRange { int e0, e1; };
+__device__ __forceinline__ SegRange seg_range(const SegGradIn& a, long long u, long long nu, long long nrefs) {
+  if (u >= nu) return SegRange{0, 0};
+  return SegRange{max(0, a.seg_off[u]), (int)min(nrefs, (long long)a.seg_off[u + 1])};
+}
+
+// Sums over the references e0..e1 of one row; k_first = refs[e0] when the caller has
+// already loaded it (software pipelining across rows), -2 to load it here.
 template <int E>
-__device__ __forceinline__ SegGrad4 segment_grad4(const SegGradIn& a, long long u, int q, long long nrefs,
-                                                  float4 wsec) {
+__device__ __forceinline__ SegGrad4 segment_grad4_range(const SegGradIn& a, int e0, int e1, int k_first, int q,
+                                                        long long nrefs, float4 wsec) {
   const dl_emb_layout& L = a.L;
   const int S = L.cate_fields;
   const int ns = index_slots(L);
   const int Cf = (L.use_fm && L.fm_cont) ? L.cont_fields : 0;
-  const int e0 = max(0, a.seg_off[u]);
-  const int e1 = (int)min(nrefs, (long long)a.seg_off[u + 1]);
   const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
   SegGrad4 r{z, z, z, 0.f};
   const int mb = index_multi_base(L);
   for (int e = e0; e < e1; ++e) {
-    const int k = a.refs[e];
+    const int k = (e == e0 && k_first != -2) ? k_first : a.refs[e];
     if (k < 0 || k >= nrefs) continue;
     const int b = k / ns, sl = k % ns;
     if (sl >= mb) {
@@ -119,6 +126,14 @@ __device__ __forceinline__ SegGrad4 segment_grad4(const SegGradIn& a, long long 
     }
   }
   return r;
+}
+
+template <int E>
+__device__ __forceinline__ SegGrad4 segment_grad4(const SegGradIn& a, long long u, int q, long long nrefs,
+                                                  float4 wsec) {
+  const int e0 = max(0, a.seg_off[u]);
+  const int e1 = (int)min(nrefs, (long long)a.seg_off[u + 1]);
+  return segment_grad4_range<E>(a, e0, e1, -2, q, nrefs, wsec);
 }
 
 __device__ __forceinline__ int clamp_uniq(const int32_t* n_uniq, long long cap) {
