@@ -224,6 +224,9 @@ struct Reader {
       buf.pop_back();
       return f;
     };
+    // utils/data_loader.py:30-37 orders the pipeline shuffle -> batch(drop_remainder) -> repeat:
+    // every epoch fills and drains its own shuffle buffer and drops its own partial batch, so no
+    // batch mixes records of two epochs and each epoch yields floor(records / B) batches.
     for (int ep = 0; ep < repeat; ++ep) {
       for (size_t fi = 0; fi < files.size(); ++fi) {
         const uint8_t* p = maps[fi].first;
@@ -248,10 +251,11 @@ struct Reader {
           }
         }
       }
+      while (!buf.empty())               // end of the epoch: drain its shuffle buffer
+        if (!push(pick())) return;
+      plan.clear();                      // and drop its partial batch (drop_remainder=True)
     }
-    while (!buf.empty())
-      if (!push(pick())) return;
-    std::lock_guard<std::mutex> g(mu);   // a partial last plan is dropped (drop_remainder=True)
+    std::lock_guard<std::mutex> g(mu);
     scan_done = true;
     cv_ready.notify_all();
   }

@@ -97,7 +97,7 @@ def test_loader_batches_drop_remainder_and_repeat(tmp_path):
     assert sorted(os.path.basename(f) for f in files) == ["part-00000", "part-00001"]
     stream = data_loader.pipeline_process(mp, sorted(files), "train")
     got = list(stream)
-    assert len(got) == (2 * 100) // 32              # 2 epochs x 100 records, remainder dropped
+    assert len(got) == 2 * (100 // 32)              # per epoch: batch(drop_remainder) then repeat
     flat = {k: np.concatenate([b[k] for b in src]) for k in src[0]}
     np.testing.assert_array_equal(got[0]["cate_feats"], flat["cate_feats"][:32])
     np.testing.assert_array_equal(got[0]["cont_feats"], flat["cont_feats"][:32])
@@ -188,10 +188,16 @@ def test_native_reader_matches_python_decoder(tmp_path, threads):
     exs = [data_loader.parse_example(r, spec) for _ in range(2) for f in files for r in tfrecord.read_records(f)]
     from deep_learning_amd.utils.native_reader import NativeReader
     got = list(NativeReader(files, [(k, kd, s) for k, (kd, s) in spec.items()], 32, repeat=2, threads=threads))
-    assert len(got) == (2 * 210) // 32
+    # utils/data_loader.py:30-37: batch(drop_remainder) inside each epoch, then repeat:
+    # 2 x floor(210 / 32) = 12 batches, epoch 2 starts again at record 0 (records 192..209
+    # of epoch 1 are dropped, never mixed into a batch with epoch 2's)
+    assert len(got) == 2 * (210 // 32)
+    per_epoch = 210 // 32
     for i, b in enumerate(got):
+        ep, j = divmod(i, per_epoch)
+        r0 = ep * 210 + j * 32
         for k, (kind, size) in spec.items():
-            want = np.asarray([e[k] for e in exs[i * 32:(i + 1) * 32]],
+            want = np.asarray([e[k] for e in exs[r0:r0 + 32]],
                               np.int64 if kind == "int64" else np.float32).reshape(32, size)
             np.testing.assert_array_equal(b[k], want, err_msg=k)
     flat = np.concatenate([s["cate_feats"] for s in src])
@@ -209,6 +215,25 @@ def test_native_reader_seeded_shuffle(tmp_path):
     assert not np.array_equal(a, plain) and not np.array_equal(a, b)
     key = lambda m: sorted(map(tuple, m))
     assert key(a) == key(plain)                                  # a permutation of the records
+
+
+def test_native_reader_shuffled_epochs_do_not_mix(tmp_path):
+    """shuffle -> batch(drop_remainder) -> repeat (utils/data_loader.py:30-37) with a shuffle
+    buffer: every epoch is its own shuffled permutation cut into floor(N/B) batches; the
+    records a batch holds all come from one epoch, and each epoch drops its own remainder."""
+    from deep_learning_amd.utils.native_reader import NativeReader
+    src = _write_parts(str(tmp_path), n_parts=1, per=70)           # 70 records, B = 16 -> 4 per epoch
+    files = sorted(data_loader.get_file_list(str(tmp_path) + "/"))
+    spec = [(k, kd, s) for k, (kd, s) in data_loader._spec(_MP()).items()]
+    got = list(NativeReader(files, spec, 16, repeat=3, shuffle_buf=40, seed=11, threads=2))
+    assert len(got) == 3 * (70 // 16)
+    rec_id = {tuple(r): i for i, r in enumerate(src[0]["cate_feats"])}
+    for ep in range(3):
+        ids = [rec_id[tuple(r)] for b in got[4 * ep:4 * ep + 4] for r in b["cate_feats"]]
+        assert len(set(ids)) == 64                                 # no record twice within an epoch
+    first = [rec_id[tuple(r)] for b in got[:4] for r in b["cate_feats"]]
+    second = [rec_id[tuple(r)] for b in got[4:8] for r in b["cate_feats"]]
+    assert first != second                                         # reshuffled each iteration
 
 
 def test_native_reader_errors(tmp_path):
