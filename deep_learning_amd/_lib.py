@@ -38,6 +38,12 @@ class PoolDesc(C.Structure):
     ]
 
 
+# include/dlamd.h constants
+OPT_LEN, OPT_STATUS = 32, 16
+STATUS_BAD_ID, STATUS_LAG = 1, 2
+REC_FIRST, REC_SPARSE_ADAM = 1, 2
+ROWS_CLEAR_TOUCHED, ROWS_SPARSE_ADAM = 1, 2
+
 P = C.c_void_p
 I32, I64, U64, F = C.c_int32, C.c_int64, C.c_uint64, C.c_float
 LP = C.POINTER(EmbLayout)
@@ -76,6 +82,7 @@ SIGNATURES = {
                                        P]),
     "dl_slab_fold_rows": (I32, [P, I32, I32, I32, I32, P, I64, P, P]),
     "dl_adam_begin_step": (I32, [P, F, F, P]),
+    "dl_step_guard": (I32, [P, P, P]),
     "dl_adam_dense": (I32, [P, P, P, P, I32, I64, I64, F, I64, P, P, P, P]),
     "dl_adam_dense_reg": (I32, [P, P, P, P, I32, I64, I64, F, I64, I32, P, P, P, P]),
     "dl_adam_rows": (I32, [P, P, P, P, P, I64, I32, F, I32, P, P, P]),

@@ -51,20 +51,47 @@ __device__ __forceinline__ int64_t checked_row(int64_t id, int64_t off, int64_t 
   return r;
 }
 
-// One TF1 ApplyAdam element update (training_ops.cc, non-Nesterov):
+// Optimizer state block (include/dlamd.h, DL_OPT_*): [0..7] Adam scalars, [8..15] per-step
+// regulariser sums, [16] the sticky status word (int32 bits).  A set status word poisons the
+// step: every kernel that writes parameters or optimizer state returns without doing so (the
+// gradients it would have consumed are still reset), so a batch with an out-of-range id
+// changes nothing — as TF's failing sess.run applies nothing before raising.
+__device__ __forceinline__ bool step_poisoned(const float* opt) {
+  return __float_as_int(opt[DL_OPT_STATUS]) != 0;
+}
+__device__ __forceinline__ int* opt_status(const float* opt) {
+  return const_cast<int*>(reinterpret_cast<const int*>(opt + DL_OPT_STATUS));
+}
+
+// One TF1 ApplyAdam element update (training_ops.cc ApplyAdam, non-Nesterov):
 //   m += (g - m)(1 - b1);  v += (g^2 - v)(1 - b2);  p -= m * alpha / (sqrt(v) + eps)
 // Shared by the dense sweep (optim.hip) and the lazy row-record path (rec.hip) so the
 // two compile to the same float operations: a zero-gradient step replayed later by
 // rec.hip's catch-up is bit-identical to the step the dense sweep would have taken.
-// The fusions are spelled out with fmaf: left to -ffp-contract, the backend fuses
-// per call site (it kept one first-order update unfused), which broke that identity.
+// No contraction: each operation is rounded on its own, as in TF's CPU kernel (and the
+// numpy oracle), so for the same gradient the update is the reference's bit for bit.
+// sqrt and divide are correctly rounded (hipcc's default), as Eigen's.
 __device__ __forceinline__ void adam_elem(float& p, float& m, float& v, float g, float alpha,
                                           float omb1, float omb2, float eps) {
-  m = fmaf(g - m, omb1, m);
-  v = fmaf(fmaf(g, g, -v), omb2, v);
-  // correctly rounded sqrt and divide, as TF's Eigen kernel: the hardware v_sqrt/v_rcp
-  // forms measured no faster in the record kernels (profiles/r01l), so exactness stays
-  p -= (m * alpha) / (sqrtf(v) + eps);
+#pragma clang fp contract(off)
+  m = m + (g - m) * omb1;
+  v = v + (g * g - v) * omb2;
+  p = p - (m * alpha) / (sqrtf(v) + eps);
+}
+
+// TF1 Adam._apply_sparse_shared (adam.py), the update of a Variable whose gradient arrives
+// as IndexedSlices — one read by tf.nn.embedding_lookup directly, with no concat in between:
+// wdl.py:44-47,132 weight_mat, deepfm.py:57-60,78,85,98 feats_emb / feats, dnn.py:49-54
+// weight_mat.  m = m*b1 for every row, then scatter_add(g*(1-b1)) on the batch's (deduplicated,
+// summed) rows; v likewise with (g*g)*(1-b2); every row then moves by lr*m/(sqrt(v)+eps).  A
+// row outside the batch is the g = 0 case of the same formula (x + 0 = x), so one function
+// serves the touched rows, the dense sweep and the lazy catch-up alike.
+__device__ __forceinline__ void adam_elem_sparse(float& p, float& m, float& v, float g, float alpha, float b1,
+                                                 float b2, float omb1, float omb2, float eps) {
+#pragma clang fp contract(off)
+  m = m * b1 + g * omb1;
+  v = v * b2 + (g * g) * omb2;
+  p = p - (alpha * m) / (sqrtf(v) + eps);
 }
 
 #define DL_DISPATCH_E(E, ...)                    \

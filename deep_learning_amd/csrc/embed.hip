@@ -638,11 +638,12 @@ extern "C" int dl_embed_fwd_indexed(const dl_emb_layout* L, const float* rows, c
   return launch_embed_fwd<false>(L, a, stream);
 }
 
-extern "C" int dl_embed_fwd_rec(const dl_emb_layout* L, const float* rec, int32_t rec_ld, int32_t has_first,
+extern "C" int dl_embed_fwd_rec(const dl_emb_layout* L, const float* rec, int32_t rec_ld, int32_t rec_flags,
                                 const float* rows_rep, const float* rows_rep1, const int64_t* cate,
                                 const float* cont, const float* vector, const float* hist, int32_t hist_len,
                                 const float* opt, int32_t lag, float* x0, float* fm_out, float* fm_sum,
                                 int32_t* err, void* stream) {
+  const int32_t has_first = rec_flags & DL_REC_FIRST;
   if (int rc = check_layout(L)) return rc;
   DL_CHECK_ARG(rec && cate && x0 && hist && opt, "NULL argument");
   DL_CHECK_ARG(hist_len >= 2 && hist_len <= 8192 && (hist_len & (hist_len - 1)) == 0,
@@ -655,7 +656,7 @@ extern "C" int dl_embed_fwd_rec(const dl_emb_layout* L, const float* rec, int32_
   DL_CHECK_ARG(!L->use_fm || (fm_out && fm_sum && Cf + L->cate_fields <= 64), "FM outputs required (<= 64 fields)");
   if (L->batch == 0) return 0;
   EmbArgs a{*L, nullptr, 0, rows_rep, rows_rep1, cate, cont, vector, x0, fm_out, fm_sum, err,
-            rec, RecCfg{L->emb_dim, rec_ld, has_first, hist_len - 1, 0.f, 0.f, 0.f}, hist, opt, lag};
+            rec, make_rec_cfg(L->emb_dim, rec_ld, rec_flags, hist_len), hist, opt, lag};
   return launch_embed_fwd<true>(L, a, stream);
 }
 

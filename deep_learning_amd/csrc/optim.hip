@@ -29,6 +29,7 @@ __device__ __forceinline__ void block_atomic_add(float x, float* out) {
 
 // opt: [0] b1p [1] b2p [2] lr [3] alpha [4] b1 [5] b2 [6] eps [7] step
 __global__ void adam_begin_kernel(float* opt, float decay_rate, float decay_steps) {
+  if (step_poisoned(opt)) return;   // a failed batch: the step does not begin (common.h)
   const float step = opt[7];
   const float pw = floorf(step / decay_steps);                   // staircase=True
   const float lr_t = opt[2] * powf(decay_rate, pw);
@@ -40,6 +41,12 @@ __global__ void adam_begin_kernel(float* opt, float decay_rate, float decay_step
   for (int i = 8; i < 16; ++i) opt[i] = 0.f;                     // per-step L2 accumulators
 }
 
+// The batch's id validation (dl_index_build / the forward's err word) poisons the step it
+// belongs to: opt's sticky status word gets the batch's error bits before the step begins.
+__global__ void step_guard_kernel(const int32_t* batch_err, float* opt) {
+  const int e = batch_err[0];
+  if (e) opt_status(opt)[0] |= (e & DL_STATUS_BAD_ID) ? DL_STATUS_BAD_ID : e;
+}
 
 // Dense parameter, gradient = sum of partial slabs (+ l2 * p for i < l2_count).
 // REG: 0 = L2 (g += l2 * p, sq_out += p^2: tf.contrib.layers.l2_regularizer), 1 = L1
@@ -51,6 +58,7 @@ __global__ __launch_bounds__(256) void adam_dense_thread_kernel(float* __restric
                                                                 long long stride, long long n, float l2,
                                                                 long long l2_count, const float* __restrict__ opt,
                                                                 float* __restrict__ p_prev, float* __restrict__ sq_out) {
+  if (step_poisoned(opt)) return;
   const float alpha = opt[3], omb1 = 1.f - opt[4], omb2 = 1.f - opt[5], eps = opt[6];
   float sq = 0.f;
   for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n;
@@ -83,6 +91,7 @@ __global__ __launch_bounds__(256) void adam_dense_wave_kernel(float* __restrict_
                                                               long long stride, long long n, float l2,
                                                               long long l2_count, const float* __restrict__ opt,
                                                               float* __restrict__ p_prev, float* __restrict__ sq_out) {
+  if (step_poisoned(opt)) return;
   const long long i = ((long long)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   const int lane = threadIdx.x & 63;
   float sq = 0.f;
@@ -104,13 +113,24 @@ __global__ __launch_bounds__(256) void adam_dense_wave_kernel(float* __restrict_
   if (sq_out) block_atomic_add(sq, sq_out);
 }
 
+// Table element update in the reference's form for the table: ApplyAdam (dense) or the
+// sparse-apply form of Variables read by embedding_lookup directly (common.h).
+template <bool SPARSE>
+__device__ __forceinline__ void table_adam(float& p, float& m, float& v, float g, float alpha, float b1, float b2,
+                                           float omb1, float omb2, float eps) {
+  if (SPARSE) adam_elem_sparse(p, m, v, g, alpha, b1, b2, omb1, omb2, eps);
+  else adam_elem(p, m, v, g, alpha, omb1, omb2, eps);
+}
+
 // Embedding table rows of width W (multiple of 4): one thread per float4.
+template <bool SPARSE>
 __global__ __launch_bounds__(256) void adam_rows4_kernel(float4* __restrict__ p, float4* __restrict__ m,
                                                          float4* __restrict__ v, float4* __restrict__ g,
                                                          const uint8_t* __restrict__ touched, long long n4,
                                                          int lpr, float l2, const float* __restrict__ opt,
                                                          float* __restrict__ sq_out) {
-  const float alpha = opt[3], omb1 = 1.f - opt[4], omb2 = 1.f - opt[5], eps = opt[6];
+  const float alpha = opt[3], b1 = opt[4], b2 = opt[5], omb1 = 1.f - opt[4], omb2 = 1.f - opt[5], eps = opt[6];
+  const bool skip = step_poisoned(opt);   // consume the gradients, apply nothing
   float sq = 0.f;
   for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n4;
        i += (long long)gridDim.x * blockDim.x) {
@@ -121,24 +141,27 @@ __global__ __launch_bounds__(256) void adam_rows4_kernel(float4* __restrict__ p,
       gi = g[i];
       g[i] = make_float4(0.f, 0.f, 0.f, 0.f);
     }
+    if (skip) continue;
     if (l2 != 0.f) { gi.x += l2 * pi.x; gi.y += l2 * pi.y; gi.z += l2 * pi.z; gi.w += l2 * pi.w; }
     if (sq_out) sq += pi.x * pi.x + pi.y * pi.y + pi.z * pi.z + pi.w * pi.w;
-    adam_elem(pi.x, mi.x, vi.x, gi.x, alpha, omb1, omb2, eps);
-    adam_elem(pi.y, mi.y, vi.y, gi.y, alpha, omb1, omb2, eps);
-    adam_elem(pi.z, mi.z, vi.z, gi.z, alpha, omb1, omb2, eps);
-    adam_elem(pi.w, mi.w, vi.w, gi.w, alpha, omb1, omb2, eps);
+    table_adam<SPARSE>(pi.x, mi.x, vi.x, gi.x, alpha, b1, b2, omb1, omb2, eps);
+    table_adam<SPARSE>(pi.y, mi.y, vi.y, gi.y, alpha, b1, b2, omb1, omb2, eps);
+    table_adam<SPARSE>(pi.z, mi.z, vi.z, gi.z, alpha, b1, b2, omb1, omb2, eps);
+    table_adam<SPARSE>(pi.w, mi.w, vi.w, gi.w, alpha, b1, b2, omb1, omb2, eps);
     p[i] = pi; m[i] = mi; v[i] = vi;
   }
   if (sq_out) block_atomic_add(sq, sq_out);
 }
 
 // Width-1 tables (first-order weights): one thread per 4 rows.
+template <bool SPARSE>
 __global__ __launch_bounds__(256) void adam_rows1_kernel(float* __restrict__ p, float* __restrict__ m,
                                                          float* __restrict__ v, float* __restrict__ g,
                                                          uint8_t* __restrict__ touched, long long n,
                                                          float l2, int clear, const float* __restrict__ opt,
                                                          float* __restrict__ sq_out) {
-  const float alpha = opt[3], omb1 = 1.f - opt[4], omb2 = 1.f - opt[5], eps = opt[6];
+  const float alpha = opt[3], b1 = opt[4], b2 = opt[5], omb1 = 1.f - opt[4], omb2 = 1.f - opt[5], eps = opt[6];
+  const bool skip = step_poisoned(opt);
   const long long n4 = n / 4;
   float sq = 0.f;
   for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < (n + 3) / 4;
@@ -156,22 +179,24 @@ __global__ __launch_bounds__(256) void adam_rows1_kernel(float* __restrict__ p, 
         if (!t.x) gi.x = 0.f; if (!t.y) gi.y = 0.f; if (!t.z) gi.z = 0.f; if (!t.w) gi.w = 0.f;
         if (clear) reinterpret_cast<uchar4*>(touched)[i] = make_uchar4(0, 0, 0, 0);
       }
+      if (skip) continue;
       if (l2 != 0.f) { gi.x += l2 * pi.x; gi.y += l2 * pi.y; gi.z += l2 * pi.z; gi.w += l2 * pi.w; }
       sq += pi.x * pi.x + pi.y * pi.y + pi.z * pi.z + pi.w * pi.w;
-      adam_elem(pi.x, mi.x, vi.x, gi.x, alpha, omb1, omb2, eps);
-      adam_elem(pi.y, mi.y, vi.y, gi.y, alpha, omb1, omb2, eps);
-      adam_elem(pi.z, mi.z, vi.z, gi.z, alpha, omb1, omb2, eps);
-      adam_elem(pi.w, mi.w, vi.w, gi.w, alpha, omb1, omb2, eps);
+      table_adam<SPARSE>(pi.x, mi.x, vi.x, gi.x, alpha, b1, b2, omb1, omb2, eps);
+      table_adam<SPARSE>(pi.y, mi.y, vi.y, gi.y, alpha, b1, b2, omb1, omb2, eps);
+      table_adam<SPARSE>(pi.z, mi.z, vi.z, gi.z, alpha, b1, b2, omb1, omb2, eps);
+      table_adam<SPARSE>(pi.w, mi.w, vi.w, gi.w, alpha, b1, b2, omb1, omb2, eps);
       reinterpret_cast<float4*>(p)[i] = pi; reinterpret_cast<float4*>(m)[i] = mi;
       reinterpret_cast<float4*>(v)[i] = vi;
     } else {
       for (long long r = 4 * i; r < n; ++r) {
         float gi = 0.f;
         if (touched[r]) { gi = g[r]; g[r] = 0.f; if (clear) touched[r] = 0; }
+        if (skip) continue;
         float pi = p[r], mi = m[r], vi = v[r];
         if (l2 != 0.f) gi += l2 * pi;
         sq += pi * pi;
-        adam_elem(pi, mi, vi, gi, alpha, omb1, omb2, eps);
+        table_adam<SPARSE>(pi, mi, vi, gi, alpha, b1, b2, omb1, omb2, eps);
         p[r] = pi; m[r] = mi; v[r] = vi;
       }
     }
@@ -242,6 +267,12 @@ extern "C" int dl_adam_begin_step(float* opt, float decay_rate, float decay_step
   DL_RETURN_LAUNCH("dl_adam_begin_step");
 }
 
+extern "C" int dl_step_guard(const int32_t* batch_err, float* opt, void* stream) {
+  DL_CHECK_ARG(batch_err && opt, "NULL pointer");
+  hipLaunchKernelGGL(step_guard_kernel, dim3(1), dim3(1), 0, as_stream(stream), batch_err, opt);
+  DL_RETURN_LAUNCH("dl_step_guard");
+}
+
 extern "C" int dl_adam_dense_reg(float* p, float* m, float* v, const float* slab, int32_t nslab,
                                  int64_t slab_stride, int64_t n, float reg, int64_t reg_count, int32_t reg_kind,
                                  const float* opt, float* p_prev, float* acc_out, void* stream) {
@@ -272,8 +303,10 @@ extern "C" int dl_adam_dense(float* p, float* m, float* v, const float* slab, in
 }
 
 extern "C" int dl_adam_rows(float* p, float* m, float* v, float* g, uint8_t* touched, int64_t n_rows,
-                            int32_t width, float l2, int32_t clear_touched, const float* opt, float* sq_out,
+                            int32_t width, float l2, int32_t rows_flags, const float* opt, float* sq_out,
                             void* stream) {
+  const int clear_touched = rows_flags & DL_ROWS_CLEAR_TOUCHED;
+  const bool sparse = (rows_flags & DL_ROWS_SPARSE_ADAM) != 0;
   DL_CHECK_ARG(p && m && v && g && touched && opt, "NULL pointer");
   DL_CHECK_ARG(width == 1 || width % 4 == 0, "width must be 1 or a multiple of 4");
   DL_CHECK_ARG(((uintptr_t)p | (uintptr_t)m | (uintptr_t)v | (uintptr_t)g) % 16 == 0, "16-B alignment");
@@ -281,12 +314,13 @@ extern "C" int dl_adam_rows(float* p, float* m, float* v, float* g, uint8_t* tou
   hipStream_t s = as_stream(stream);
   if (width == 1) {
     DL_CHECK_ARG(((uintptr_t)touched % 4) == 0, "touched must be 4-B aligned");
-    hipLaunchKernelGGL(adam_rows1_kernel, dim3(grid_for(n_rows, 4)), dim3(256), 0, s, p, m, v, g, touched,
-                       (long long)n_rows, l2, clear_touched, opt, sq_out);
+    hipLaunchKernelGGL(sparse ? adam_rows1_kernel<true> : adam_rows1_kernel<false>, dim3(grid_for(n_rows, 4)),
+                       dim3(256), 0, s, p, m, v, g, touched, (long long)n_rows, l2, clear_touched, opt, sq_out);
   } else {
     const long long n4 = n_rows * (width / 4);
-    hipLaunchKernelGGL(adam_rows4_kernel, dim3(grid_for(n4)), dim3(256), 0, s, (float4*)p, (float4*)m,
-                       (float4*)v, (float4*)g, touched, n4, width / 4, l2, opt, sq_out);
+    hipLaunchKernelGGL(sparse ? adam_rows4_kernel<true> : adam_rows4_kernel<false>, dim3(grid_for(n4)), dim3(256),
+                       0, s, (float4*)p, (float4*)m, (float4*)v, (float4*)g, touched, n4, width / 4, l2, opt,
+                       sq_out);
     if (clear_touched) {
       DL_CHECK_ARG(((uintptr_t)touched % 16) == 0, "touched must be 16-B aligned");
       hipLaunchKernelGGL(clear_touched_kernel, dim3(grid_for(n_rows, 16)), dim3(256), 0, s, touched,

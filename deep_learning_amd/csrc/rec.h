@@ -8,13 +8,46 @@ namespace dl {
 
 struct RecCfg {
   int E, ld, has_first, hist_mask;
-  float omb1, omb2, eps;   // filled on the device from opt (rec_load_hyper)
+  int sparse;                          // TF's sparse-apply Adam form (DL_REC_SPARSE_ADAM)
+  float b1, b2, omb1, omb2, eps;       // filled on the device from opt (rec_load_hyper)
+  int* status;                         // opt's status word (lag overflow is reported there)
 };
 
+// rec_flags of the C ABI (DL_REC_FIRST | DL_REC_SPARSE_ADAM) -> the kernel config
+inline RecCfg make_rec_cfg(int E, int ld, int rec_flags, int hist_len) {
+  RecCfg c{};
+  c.E = E;
+  c.ld = ld;
+  c.has_first = (rec_flags & DL_REC_FIRST) ? 1 : 0;
+  c.sparse = (rec_flags & DL_REC_SPARSE_ADAM) ? 1 : 0;
+  c.hist_mask = hist_len - 1;
+  return c;
+}
+
 __device__ __forceinline__ void rec_load_hyper(RecCfg& c, const float* opt) {
+  c.b1 = opt[4];
+  c.b2 = opt[5];
   c.omb1 = 1.f - opt[4];
   c.omb2 = 1.f - opt[5];
   c.eps = opt[6];
+  c.status = opt_status(opt);
+}
+
+// The table's TF1 Adam element update in the form the reference applies to it.
+__device__ __forceinline__ void rec_adam(float& p, float& m, float& v, float g, float alpha, const RecCfg& c) {
+  if (c.sparse) adam_elem_sparse(p, m, v, g, alpha, c.b1, c.b2, c.omb1, c.omb2, c.eps);
+  else adam_elem(p, m, v, g, alpha, c.omb1, c.omb2, c.eps);
+}
+
+// A row lagging more steps than the alpha ring holds cannot be caught up exactly: the host
+// flushes on schedule so this never happens; if it does, the status word says so (the host
+// raises) and the replay covers the ring's steps only.
+__device__ __forceinline__ int catch_up_from(int from, int to, const RecCfg& c) {
+  if (to - from > c.hist_mask + 1) {
+    atomicOr(c.status, DL_STATUS_LAG);
+    return to - (c.hist_mask + 1);
+  }
+  return from;
 }
 
 // Replays zero-gradient steps (from, to] on one float4 of p/m/v (and the
@@ -22,25 +55,25 @@ __device__ __forceinline__ void rec_load_hyper(RecCfg& c, const float* opt) {
 __device__ __forceinline__ void catch_up4(float4& p, float4& m, float4& v, float& w, float& wm, float& wv,
                                           bool first, int from, int to, const float* __restrict__ hist,
                                           const RecCfg& c) {
-  if (to - from > c.hist_mask + 1) from = to - (c.hist_mask + 1);   // host bounds the lag; never read past the ring
+  from = catch_up_from(from, to, c);
   for (int j = from + 1; j <= to; ++j) {
     const float al = hist[j & c.hist_mask];
-    adam_elem(p.x, m.x, v.x, 0.f, al, c.omb1, c.omb2, c.eps);
-    adam_elem(p.y, m.y, v.y, 0.f, al, c.omb1, c.omb2, c.eps);
-    adam_elem(p.z, m.z, v.z, 0.f, al, c.omb1, c.omb2, c.eps);
-    adam_elem(p.w, m.w, v.w, 0.f, al, c.omb1, c.omb2, c.eps);
-    if (first) adam_elem(w, wm, wv, 0.f, al, c.omb1, c.omb2, c.eps);
+    rec_adam(p.x, m.x, v.x, 0.f, al, c);
+    rec_adam(p.y, m.y, v.y, 0.f, al, c);
+    rec_adam(p.z, m.z, v.z, 0.f, al, c);
+    rec_adam(p.w, m.w, v.w, 0.f, al, c);
+    if (first) rec_adam(w, wm, wv, 0.f, al, c);
   }
 }
 
 __device__ __forceinline__ void catch_up1(float& p, float& m, float& v, float& w, float& wm, float& wv,
                                           bool first, int from, int to, const float* __restrict__ hist,
                                           const RecCfg& c) {
-  if (to - from > c.hist_mask + 1) from = to - (c.hist_mask + 1);
+  from = catch_up_from(from, to, c);
   for (int j = from + 1; j <= to; ++j) {
     const float al = hist[j & c.hist_mask];
-    adam_elem(p, m, v, 0.f, al, c.omb1, c.omb2, c.eps);
-    if (first) adam_elem(w, wm, wv, 0.f, al, c.omb1, c.omb2, c.eps);
+    rec_adam(p, m, v, 0.f, al, c);
+    if (first) rec_adam(w, wm, wv, 0.f, al, c);
   }
 }
 

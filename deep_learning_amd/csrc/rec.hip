@@ -90,10 +90,10 @@ __device__ __forceinline__ void rec_update(float* __restrict__ r, int E, int d, 
   float w = 0.f, wm = 0.f, wv = 0.f;
   if (first) { w = r[E]; wm = r[E + 1]; wv = r[E + 2]; }
   if (stamp < t - 1) catch_up1(p, m, v, w, wm, wv, first, stamp, t - 1, hist, c);
-  adam_elem(p, m, v, g, alpha_t, c.omb1, c.omb2, c.eps);
+  rec_adam(p, m, v, g, alpha_t, c);
   r[d] = p; r[E + 4 + d] = m; r[2 * E + 4 + d] = v;
   if (first) {
-    adam_elem(w, wm, wv, g1, alpha_t, c.omb1, c.omb2, c.eps);
+    rec_adam(w, wm, wv, g1, alpha_t, c);
     r[E] = w; r[E + 1] = wm; r[E + 2] = wv;
   }
   if (d == 0) r[E + 3] = __int_as_float(t);
@@ -157,6 +157,7 @@ __global__ __launch_bounds__(256) void rec_bwd_adam_kernel(SegGradIn sg, float* 
                                                            float* __restrict__ g_rep, float* __restrict__ g1_rep,
                                                            const float* __restrict__ hist,
                                                            const float* __restrict__ opt) {
+  if (step_poisoned(opt)) return;   // the batch failed validation: no update (common.h)
   rec_load_hyper(c, opt);
   constexpr int LPR = E / 4;
   const dl_emb_layout& L = sg.L;
@@ -227,16 +228,16 @@ __global__ __launch_bounds__(256) void rec_bwd_adam_kernel(SegGradIn sg, float* 
       if (g1_rep && q == 0) g1_rep[rrow] += s.g1;
       continue;
     }
-    adam_elem(p.x, m.x, v.x, g.x, alpha, c.omb1, c.omb2, c.eps);
-    adam_elem(p.y, m.y, v.y, g.y, alpha, c.omb1, c.omb2, c.eps);
-    adam_elem(p.z, m.z, v.z, g.z, alpha, c.omb1, c.omb2, c.eps);
-    adam_elem(p.w, m.w, v.w, g.w, alpha, c.omb1, c.omb2, c.eps);
+    rec_adam(p.x, m.x, v.x, g.x, alpha, c);
+    rec_adam(p.y, m.y, v.y, g.y, alpha, c);
+    rec_adam(p.z, m.z, v.z, g.z, alpha, c);
+    rec_adam(p.w, m.w, v.w, g.w, alpha, c);
     float* r = rec + row * c.ld;
     *reinterpret_cast<float4*>(r + 4 * q) = p;
     *reinterpret_cast<float4*>(r + E + 4 + 4 * q) = m;
     *reinterpret_cast<float4*>(r + 2 * E + 4 + 4 * q) = v;
     if (q == 0) {
-      if (first) adam_elem(w, wm, wv, s.g1, alpha, c.omb1, c.omb2, c.eps);
+      if (first) rec_adam(w, wm, wv, s.g1, alpha, c);
       *reinterpret_cast<float4*>(r + E) = make_float4(w, wm, wv, __int_as_float(t));
     }
   }
@@ -251,13 +252,14 @@ __global__ __launch_bounds__(256) void rec_apply_rows_kernel(float* __restrict__
   const int E = c.E;
   const int t = (int)opt[7];
   const float alpha_t = opt[3];
+  const bool skip = step_poisoned(opt);   // consume the gradients, apply nothing
   for (long long k = (long long)blockIdx.x * blockDim.x + threadIdx.x; k < n * E;
        k += (long long)gridDim.x * blockDim.x) {
     const long long i = k / E;
     const int d = (int)(k % E);
     const float gi = g[k];
     const float g1i = (g1 && d == 0) ? g1[i] : 0.f;
-    rec_update(rec + (row0 + i) * c.ld, E, d, gi, g1i, t, alpha_t, hist, c);
+    if (!skip) rec_update(rec + (row0 + i) * c.ld, E, d, gi, g1i, t, alpha_t, hist, c);
     g[k] = 0.f;
     if (g1 && d == 0) g1[i] = 0.f;
   }
@@ -305,6 +307,7 @@ __global__ __launch_bounds__(256) void rec_apply_segments_kernel(float* __restri
                                                                  const float* __restrict__ g1,
                                                                  const float* __restrict__ hist,
                                                                  const float* __restrict__ opt) {
+  if (step_poisoned(opt)) return;
   rec_load_hyper(c, opt);
   constexpr int LPR = E / 4;
   const long long gt = (long long)blockIdx.x * blockDim.x + threadIdx.x;
@@ -334,15 +337,15 @@ __global__ __launch_bounds__(256) void rec_apply_segments_kernel(float* __restri
     }
     const int stamp = __float_as_int(tail.w);
     if (stamp < t - 1) catch_up4(p, m, v, w, wm, wv, first, stamp, t - 1, hist, c);
-    adam_elem(p.x, m.x, v.x, gs.x, alpha, c.omb1, c.omb2, c.eps);
-    adam_elem(p.y, m.y, v.y, gs.y, alpha, c.omb1, c.omb2, c.eps);
-    adam_elem(p.z, m.z, v.z, gs.z, alpha, c.omb1, c.omb2, c.eps);
-    adam_elem(p.w, m.w, v.w, gs.w, alpha, c.omb1, c.omb2, c.eps);
+    rec_adam(p.x, m.x, v.x, gs.x, alpha, c);
+    rec_adam(p.y, m.y, v.y, gs.y, alpha, c);
+    rec_adam(p.z, m.z, v.z, gs.z, alpha, c);
+    rec_adam(p.w, m.w, v.w, gs.w, alpha, c);
     *reinterpret_cast<float4*>(r + 4 * q) = p;
     *reinterpret_cast<float4*>(r + E + 4 + 4 * q) = m;
     *reinterpret_cast<float4*>(r + 2 * E + 4 + 4 * q) = v;
     if (q == 0) {
-      if (first) adam_elem(w, wm, wv, g1s, alpha, c.omb1, c.omb2, c.eps);
+      if (first) rec_adam(w, wm, wv, g1s, alpha, c);
       *reinterpret_cast<float4*>(r + E) = make_float4(w, wm, wv, __int_as_float(t));
     }
   }
@@ -371,6 +374,7 @@ __global__ __launch_bounds__(256) void rec_apply_chain_kernel(float* __restrict_
                                                               const float* __restrict__ g1,
                                                               const float* __restrict__ hist,
                                                               const float* __restrict__ opt) {
+  if (step_poisoned(opt)) return;
   rec_load_hyper(c, opt);
   constexpr int LPR = E / 4;
   const long long gt = (long long)blockIdx.x * blockDim.x + threadIdx.x;
@@ -410,15 +414,15 @@ __global__ __launch_bounds__(256) void rec_apply_chain_kernel(float* __restrict_
     }
     const int stamp = __float_as_int(tail.w);
     if (stamp < t - 1) catch_up4(p, m, v, w, wm, wv, first, stamp, t - 1, hist, c);
-    adam_elem(p.x, m.x, v.x, gs.x, alpha, c.omb1, c.omb2, c.eps);
-    adam_elem(p.y, m.y, v.y, gs.y, alpha, c.omb1, c.omb2, c.eps);
-    adam_elem(p.z, m.z, v.z, gs.z, alpha, c.omb1, c.omb2, c.eps);
-    adam_elem(p.w, m.w, v.w, gs.w, alpha, c.omb1, c.omb2, c.eps);
+    rec_adam(p.x, m.x, v.x, gs.x, alpha, c);
+    rec_adam(p.y, m.y, v.y, gs.y, alpha, c);
+    rec_adam(p.z, m.z, v.z, gs.z, alpha, c);
+    rec_adam(p.w, m.w, v.w, gs.w, alpha, c);
     *reinterpret_cast<float4*>(r + 4 * q) = p;
     *reinterpret_cast<float4*>(r + E + 4 + 4 * q) = m;
     *reinterpret_cast<float4*>(r + 2 * E + 4 + 4 * q) = v;
     if (q == 0) {
-      if (first) adam_elem(w, wm, wv, g1s, alpha, c.omb1, c.omb2, c.eps);
+      if (first) rec_adam(w, wm, wv, g1s, alpha, c);
       *reinterpret_cast<float4*>(r + E) = make_float4(w, wm, wv, __int_as_float(t));
     }
   }
@@ -458,10 +462,11 @@ extern "C" int dl_adam_hist_record(const float* opt, float* hist, int32_t hist_l
   DL_RETURN_LAUNCH("dl_adam_hist_record");
 }
 
-extern "C" int dl_rec_gather(const dl_emb_layout* L, const float* rec, int32_t rec_ld, int32_t has_first,
+extern "C" int dl_rec_gather(const dl_emb_layout* L, const float* rec, int32_t rec_ld, int32_t rec_flags,
                              int32_t n_rep, const uint32_t* uniq_keys, const int32_t* n_uniq, int64_t max_uniq,
                              int32_t world, const float* hist, int32_t hist_len, const float* opt, int32_t lag,
                              float* rows_u, float* rows_u1, float* mv_u, void* stream) {
+  const int32_t has_first = rec_flags & DL_REC_FIRST;
   DL_CHECK_ARG(L && rec && hist && opt && rows_u, "NULL argument");
   if (int rc = rec_check(L->emb_dim, rec_ld, hist_len)) return rc;
   DL_CHECK_ARG(n_rep >= 0 && n_rep <= L->n_rows && world >= 1, "bad n_rep/world");
@@ -472,7 +477,7 @@ extern "C" int dl_rec_gather(const dl_emb_layout* L, const float* rec, int32_t r
   DL_DISPATCH_E(L->emb_dim, {
     const unsigned grid = grid_cap(total * (kE / 4));
     hipLaunchKernelGGL(rec_gather_kernel<kE>, dim3(grid), dim3(256), 0, as_stream(stream), rec,
-                       RecCfg{kE, rec_ld, has_first, hist_len - 1, 0.f, 0.f, 0.f}, (int64_t)L->n_rows, n_rep,
+                       make_rec_cfg(kE, rec_ld, rec_flags, hist_len), (int64_t)L->n_rows, n_rep,
                        n_rep ? (int64_t)L->fm_cont_offset : (int64_t)0, uniq_keys, n_uniq, (long long)max_uniq,
                        world, hist, opt, lag, rows_u,
                        has_first ? rows_u1 : nullptr, mv_u);
@@ -480,13 +485,14 @@ extern "C" int dl_rec_gather(const dl_emb_layout* L, const float* rec, int32_t r
   DL_RETURN_LAUNCH("dl_rec_gather");
 }
 
-extern "C" int dl_rec_bwd_adam(const dl_emb_layout* L, float* rec, int32_t rec_ld, int32_t has_first, int32_t n_rep,
+extern "C" int dl_rec_bwd_adam(const dl_emb_layout* L, float* rec, int32_t rec_ld, int32_t rec_flags, int32_t n_rep,
                                const float* rows_u, const float* rows_u1, const float* mv_u,
                                const uint32_t* uniq_keys, const int32_t* seg_off, const int32_t* n_uniq,
                                const int32_t* sorted_refs, int32_t world, int64_t max_uniq, const float* dz,
                                const float* w_head, const float* fm_sum, const float* dx0, float* g_rep,
                                float* g1_rep, const float* hist, int32_t hist_len, const float* opt,
                                const dl_pool_desc* pool, void* stream) {
+  const int32_t has_first = rec_flags & DL_REC_FIRST;
   DL_CHECK_ARG(L && rec && rows_u && uniq_keys && seg_off && n_uniq && sorted_refs && dx0 && opt,
                "NULL argument");
   DL_CHECK_ARG(mv_u || hist, "without the moment stash the alpha ring is required");
@@ -519,52 +525,55 @@ extern "C" int dl_rec_bwd_adam(const dl_emb_layout* L, float* rec, int32_t rec_l
   DL_DISPATCH_E(L->emb_dim, {
     const unsigned grid = grid_cap(max_uniq * (kE / 4));
     hipLaunchKernelGGL(rec_bwd_adam_kernel<kE>, dim3(grid), dim3(256), 0, as_stream(stream), sg, rec,
-                       RecCfg{kE, rec_ld, has_first, (mv_u ? 2 : hist_len) - 1, 0.f, 0.f, 0.f}, n_rep, rows_u,
+                       make_rec_cfg(kE, rec_ld, rec_flags, (mv_u ? 2 : hist_len)), n_rep, rows_u,
                        has_first ? rows_u1 : nullptr, mv_u, uniq_keys, n_uniq, world, g_rep,
                        has_first ? g1_rep : nullptr, hist, opt);
   });
   DL_RETURN_LAUNCH("dl_rec_bwd_adam");
 }
 
-extern "C" int dl_rec_apply_rows(float* rec, int32_t rec_ld, int32_t emb_dim, int32_t has_first, int64_t row0,
+extern "C" int dl_rec_apply_rows(float* rec, int32_t rec_ld, int32_t emb_dim, int32_t rec_flags, int64_t row0,
                                  int64_t n, float* g, float* g1, const float* hist, int32_t hist_len,
                                  const float* opt, void* stream) {
+  const int32_t has_first = rec_flags & DL_REC_FIRST;
   DL_CHECK_ARG(rec && g && hist && opt, "NULL argument");
   if (int rc = rec_check(emb_dim, rec_ld, hist_len)) return rc;
   DL_CHECK_ARG(!has_first || g1, "g1 required with first-order weights");
   DL_CHECK_ARG(row0 >= 0 && n >= 0, "bad row range");
   if (n == 0) return 0;
   hipLaunchKernelGGL(rec_apply_rows_kernel, dim3(grid_cap(n * emb_dim)), dim3(256), 0, as_stream(stream), rec,
-                     RecCfg{emb_dim, rec_ld, has_first, hist_len - 1, 0.f, 0.f, 0.f}, (long long)row0,
+                     make_rec_cfg(emb_dim, rec_ld, rec_flags, hist_len), (long long)row0,
                      (long long)n, g, has_first ? g1 : nullptr, hist, opt);
   DL_RETURN_LAUNCH("dl_rec_apply_rows");
 }
 
-extern "C" int dl_rec_flush(float* rec, int32_t rec_ld, int32_t emb_dim, int32_t has_first, int64_t n_rows,
+extern "C" int dl_rec_flush(float* rec, int32_t rec_ld, int32_t emb_dim, int32_t rec_flags, int64_t n_rows,
                             const float* hist, int32_t hist_len, const float* opt, void* stream) {
+  const int32_t has_first = rec_flags & DL_REC_FIRST;
   DL_CHECK_ARG(rec && hist && opt, "NULL argument");
   if (int rc = rec_check(emb_dim, rec_ld, hist_len)) return rc;
   if (n_rows <= 0) return 0;
   DL_DISPATCH_E(emb_dim, {
     hipLaunchKernelGGL(rec_flush_kernel<kE>, dim3(grid_cap(n_rows * (kE / 4))), dim3(256), 0, as_stream(stream),
-                       rec, RecCfg{kE, rec_ld, has_first, hist_len - 1, 0.f, 0.f, 0.f}, (long long)n_rows, hist,
+                       rec, make_rec_cfg(kE, rec_ld, rec_flags, hist_len), (long long)n_rows, hist,
                        opt);
   });
   DL_RETURN_LAUNCH("dl_rec_flush");
 }
 
-extern "C" int dl_rec_apply_segments(float* rec, int32_t rec_ld, int32_t emb_dim, int32_t has_first,
+extern "C" int dl_rec_apply_segments(float* rec, int32_t rec_ld, int32_t emb_dim, int32_t rec_flags,
                                      const int32_t* uniq, const int32_t* seg_off, const int32_t* n_uniq,
                                      int64_t max_uniq, int64_t n, const int32_t* sorted_pos, const float* g,
                                      const float* g1, const float* hist, int32_t hist_len, const float* opt,
                                      void* stream) {
+  const int32_t has_first = rec_flags & DL_REC_FIRST;
   DL_CHECK_ARG(rec && uniq && seg_off && sorted_pos && g && hist && opt, "NULL argument");
   if (int rc = rec_check(emb_dim, rec_ld, hist_len)) return rc;
   DL_CHECK_ARG(!has_first || g1, "g1 required with first-order weights");
   if (max_uniq <= 0 || n <= 0) return 0;
   DL_DISPATCH_E(emb_dim, {
     hipLaunchKernelGGL(rec_apply_segments_kernel<kE>, dim3(grid_cap(max_uniq * (kE / 4))), dim3(256), 0,
-                       as_stream(stream), rec, RecCfg{kE, rec_ld, has_first, hist_len - 1, 0.f, 0.f, 0.f}, uniq,
+                       as_stream(stream), rec, make_rec_cfg(kE, rec_ld, rec_flags, hist_len), uniq,
                        seg_off, n_uniq, (long long)max_uniq, (long long)n, sorted_pos, g, has_first ? g1 : nullptr,
                        hist, opt);
   });
@@ -579,16 +588,17 @@ extern "C" int dl_rec_chain_link(const int32_t* ids, int64_t n, int32_t* head, i
   DL_RETURN_LAUNCH("dl_rec_chain_link");
 }
 
-extern "C" int dl_rec_apply_chain(float* rec, int32_t rec_ld, int32_t emb_dim, int32_t has_first, const int32_t* ids,
+extern "C" int dl_rec_apply_chain(float* rec, int32_t rec_ld, int32_t emb_dim, int32_t rec_flags, const int32_t* ids,
                                   int64_t n, int32_t* head, const int32_t* next, const float* g, const float* g1,
                                   const float* hist, int32_t hist_len, const float* opt, void* stream) {
+  const int32_t has_first = rec_flags & DL_REC_FIRST;
   DL_CHECK_ARG(rec && ids && head && next && g && hist && opt, "NULL argument");
   if (int rc = rec_check(emb_dim, rec_ld, hist_len)) return rc;
   DL_CHECK_ARG(!has_first || g1, "g1 required with first-order weights");
   if (n <= 0) return 0;
   DL_DISPATCH_E(emb_dim, {
     hipLaunchKernelGGL(rec_apply_chain_kernel<kE>, dim3(grid_cap(n * (kE / 4))), dim3(256), 0, as_stream(stream), rec,
-                       RecCfg{kE, rec_ld, has_first, hist_len - 1, 0.f, 0.f, 0.f}, ids, (long long)n, head, next, g,
+                       make_rec_cfg(kE, rec_ld, rec_flags, hist_len), ids, (long long)n, head, next, g,
                        has_first ? g1 : nullptr, hist, opt);
   });
   hipLaunchKernelGGL(rec_chain_reset_kernel, dim3(grid_cap(n)), dim3(256), 0, as_stream(stream), ids, (long long)n,

@@ -124,6 +124,15 @@ class ModelSpec:
         return "feats" if self.model == "deepfm" else "fm_first_order_emb"   # deepfm.py:60
 
     @property
+    def sparse_table(self):
+        """The table (and first-order) Variables are read by tf.nn.embedding_lookup directly,
+        so TF updates them with Adam's sparse-apply form (Adam._apply_sparse_shared): wdl.py:44-47,
+        132 weight_mat, deepfm.py:57-60,78,85,98 feats_emb / feats, dnn.py:49-54 weight_mat.  The
+        pipeline models concat a zero row 0 first (deepfm_pipeline.py:83-86), which densifies the
+        gradient: ApplyAdam."""
+        return self.model in ("wdl", "deepfm", "dnn")
+
+    @property
     def hidden_reg(self):
         """Regulariser on the hidden weight matrices: wdl.py:272-275 L2, dnn.py:88-90 L1."""
         return {"wdl": "l2", "dnn": "l1"}.get(self.model)
@@ -261,7 +270,7 @@ class CTREngine:
         self.w_head = z(_ru(self.head_n, 4))
         self.hm, self.hv = torch.zeros_like(self.w_head), torch.zeros_like(self.w_head)
         self.w_head_prev = torch.zeros_like(self.w_head)
-        self.opt = z(16)
+        self.opt = z(_lib.OPT_LEN)   # include/dlamd.h: Adam scalars, per-step sums, status word
         self.opt[:8].copy_(torch.tensor([sp.beta1, sp.beta2, sp.lr, 0.0, sp.beta1, sp.beta2, sp.eps, 0.0]))
         self.wdl = sp.model == "wdl"
         if self.wdl:   # wdl_weights [N + H] (deep-output rows alias wide ids, wdl.py:241-248) + bias
@@ -270,7 +279,12 @@ class CTREngine:
             self.ww, self.wm, self.wv, self.wg = z(wr), z(wr), z(wr), z(wr)
             self.w_touched = z(wr, dt=torch.uint8)
             self.wb, self.wbm, self.wbv = z(4), z(4), z(4)
-        self.err = z(4, dt=torch.int32)
+        self.err = z(4, dt=torch.int32)       # the batch's id-validation word (per buffer set)
+        # table update form (TF: ApplyAdam, or the sparse-apply form for direct lookups)
+        self.rec_flags = (_lib.REC_FIRST if sp.fm else 0) | (_lib.REC_SPARSE_ADAM if sp.sparse_table else 0)
+        self.rows_sparse = _lib.ROWS_SPARSE_ADAM if sp.sparse_table else 0
+        self._status_q = []
+        self._status_host = None
         # ---- activations / workspaces
         B = max_batch
         self.x0 = z(B, self.in_ld[0])
@@ -541,7 +555,7 @@ class CTREngine:
         """Catch every row record up to the current step (no-op for the dense engine)."""
         if not self.lazy:
             return
-        self._c("rec_flush", "dl_rec_flush", ptr(self.rec), self.rec_ld, self.spec.E, int(self.spec.fm),
+        self._c("rec_flush", "dl_rec_flush", ptr(self.rec), self.rec_ld, self.spec.E, self.rec_flags,
                 self.rec.shape[0], ptr(self.hist), self.hist_len, ptr(self.opt), _lib.stream_handle())
         self.since_flush = 0
 
@@ -624,16 +638,16 @@ class CTREngine:
                  ptr(self.x0), ptr(self.fm_out), ptr(self.cnt_emb), ptr(self.cnt_first), ptr(self.err), s)
         if self.fwd_rec:
             if self.n_rep:   # the replicated FM cont-field rows, caught up, compact
-                self._c("rec_gather", "dl_rec_gather", C_ref(L), ptr(self.rec), self.rec_ld, int(sp.fm), self.n_rep,
+                self._c("rec_gather", "dl_rec_gather", C_ref(L), ptr(self.rec), self.rec_ld, self.rec_flags, self.n_rep,
                         ptr(self.idx_uniq), None, 0, 1, ptr(self.hist), self.hist_len, ptr(self.opt),
                         1 if train else 0, ptr(self.rows_u), ptr(self.rows_u1), None, s)
-            self._c("embed_fwd", "dl_embed_fwd_rec", C_ref(L), ptr(self.rec), self.rec_ld, int(sp.fm),
+            self._c("embed_fwd", "dl_embed_fwd_rec", C_ref(L), ptr(self.rec), self.rec_ld, self.rec_flags,
                     ptr(self.rows_u), ptr(self.rows_u1) if sp.fm else None, ptr(self.in_cate), ptr(self.in_cont),
                     ptr(self.in_vec), ptr(self.hist), self.hist_len, ptr(self.opt), 1 if train else 0,
                     ptr(x0), ptr(self.fm_out), ptr(self.fm_sum), ptr(self.err), s)
         elif self.lazy:
             # rows of the batch (index built by _pre), caught up to the step being taken
-            self._c("rec_gather", "dl_rec_gather", C_ref(L), ptr(self.rec), self.rec_ld, int(sp.fm), self.n_rep,
+            self._c("rec_gather", "dl_rec_gather", C_ref(L), ptr(self.rec), self.rec_ld, self.rec_flags, self.n_rep,
                     ptr(self.idx_uniq), ptr(self.idx_n), B * self.n_slot, 1, ptr(self.hist), self.hist_len,
                     ptr(self.opt), 1 if train else 0, ptr(self.rows_u), ptr(self.rows_u1),
                     ptr(self.mv_u) if (train and self.mv_u is not None) else None, s)
@@ -707,10 +721,16 @@ class CTREngine:
         sp = self.spec
         s = _lib.stream_handle()
         L = self.layout
+        # a batch whose ids failed validation (index build) poisons the step: nothing is applied
+        self._c("step_guard", "dl_step_guard", ptr(self.err), ptr(self.opt), s)
         self._c("adam_begin", "dl_adam_begin_step", ptr(self.opt), sp.decay_rate, float(sp.decay_steps), s)
         if self.lazy:
             self._c("adam_hist", "dl_adam_hist_record", ptr(self.opt), ptr(self.hist), self.hist_len, s)
         self._forward(B, s, train=True)
+        if not self.lazy or self.wdl:
+            # ids validated inside the forward (dense-layout gather, wdl wide ids): the updates
+            # after it are skipped (the step counter has already advanced)
+            self._c("step_guard2", "dl_step_guard", ptr(self.err), ptr(self.opt), s)
         nl = len(sp.hidden)
         splits = max(1, min(self.splits, B // 1024))
         if self.bf and not self.wdl:      # the wdl head writes its bf16 dY itself
@@ -761,7 +781,7 @@ class CTREngine:
         bwd_blocks = call_int("dl_embed_bwd_grid", C_ref(L))
         if self.lazy:
             E, R = sp.E, self.n_rep
-            self._c("embed_bwd", "dl_rec_bwd_adam", C_ref(L), ptr(self.rec), self.rec_ld, int(sp.fm), R,
+            self._c("embed_bwd", "dl_rec_bwd_adam", C_ref(L), ptr(self.rec), self.rec_ld, self.rec_flags, R,
                     ptr(self.rows_u), ptr(self.rows_u1), ptr(self.mv_u), ptr(self.idx_uniq), ptr(self.idx_off),
                     ptr(self.idx_n), ptr(self.idx_refs), 1, B * self.n_slot, ptr(self.dz), ptr(self.w_head),
                     ptr(self.fm_sum), ptr(self.dx0), ptr(self.g_rep), ptr(self.g1_rep), ptr(self.hist),
@@ -772,7 +792,7 @@ class CTREngine:
                         ptr(self.dz), ptr(self.w_head), ptr(self.fm_sum), ptr(self.cont_slab), self.bwd_blocks, s)
                 self._c("cont_reduce", "dl_embed_cont_reduce", C_ref(L), ptr(self.cont_slab), bwd_blocks,
                         ptr(self.g_rep), ptr(self.g1_rep), ptr(self.rep_touched), s)
-                self._c("adam_rep", "dl_rec_apply_rows", ptr(self.rec), self.rec_ld, E, int(sp.fm), sp.fm_cont_offset, R,
+                self._c("adam_rep", "dl_rec_apply_rows", ptr(self.rec), self.rec_ld, E, self.rec_flags, sp.fm_cont_offset, R,
                         ptr(self.g_rep), ptr(self.g1_rep), ptr(self.hist), self.hist_len, ptr(self.opt), s)
         elif self.bwd == "sorted":
             self._c("embed_bwd", "dl_embed_bwd_sorted", C_ref(L), ptr(self.table), None, ptr(self.idx_uniq),
@@ -807,7 +827,7 @@ class CTREngine:
             if self.lazy:
                 return
             self._c("adam_table", "dl_adam_rows", ptr(self.table), ptr(self.tm), ptr(self.tv), ptr(self.tg),
-                    ptr(self.touched), self.table.shape[0], sp.E, 0.0, 1, ptr(self.opt), None, s)
+                    ptr(self.touched), self.table.shape[0], sp.E, 0.0, 1 | self.rows_sparse, ptr(self.opt), None, s)
             return
         # head Adam: L2 on the output weights only (deepfm_pipeline.py:183 / dnn_pipeline.py:131)
         self._c("adam_head", "dl_adam_dense", ptr(self.w_head), ptr(self.hm), ptr(self.hv), ptr(self.head_slab),
@@ -817,18 +837,18 @@ class CTREngine:
             return
         if sp.fm:
             self._c("adam_table", "dl_adam_rows", ptr(self.table), ptr(self.tm), ptr(self.tv), ptr(self.tg),
-                    ptr(self.touched), self.table.shape[0], sp.E, 0.0, 0, ptr(self.opt), None, s)
+                    ptr(self.touched), self.table.shape[0], sp.E, 0.0, self.rows_sparse, ptr(self.opt), None, s)
             self._c("adam_first", "dl_adam_rows", ptr(self.first), ptr(self.fmm), ptr(self.fmv), ptr(self.fmg),
-                    ptr(self.touched), self.first.shape[0], 1, 0.0, 1, ptr(self.opt), None, s)
+                    ptr(self.touched), self.first.shape[0], 1, 0.0, 1 | self.rows_sparse, ptr(self.opt), None, s)
         else:
             self._c("adam_table", "dl_adam_rows", ptr(self.table), ptr(self.tm), ptr(self.tv), ptr(self.tg),
-                    ptr(self.touched), self.table.shape[0], sp.E, 0.0, 1, ptr(self.opt), None, s)
+                    ptr(self.touched), self.table.shape[0], sp.E, 0.0, 1 | self.rows_sparse, ptr(self.opt), None, s)
 
     # per-batch buffers: inputs and the batch index.  With prefetching they are double
     # buffered — the next batch is staged and indexed into the other set on a side stream
     # while the current step runs.
     SLOT_ATTRS = ("in_label", "in_cont", "in_vec", "in_cate", "in_wide", "idx_ws", "idx_keys", "idx_refs",
-                  "idx_uniq", "idx_off", "idx_n", "idx_inv")
+                  "idx_uniq", "idx_off", "idx_n", "idx_inv", "err")
 
     def _side_stream(self):
         if getattr(self, "side", None) is None:
@@ -919,6 +939,7 @@ class CTREngine:
         else:
             self._train(B)
         self._release()
+        self._queue_status()
         self.steps += 1
         self.last_batch = B
         return B
@@ -959,10 +980,54 @@ class CTREngine:
             return data + sp.l2 * float(self.opt[8].item())
         return data + sp.l2 * 0.5 * float(self.opt[8].item())
 
+    # ------------------------------------------------------------------ errors
+    def _queue_status(self):
+        """After each step: an asynchronous read-back of the status word into pinned host
+        memory.  Completed read-backs are checked at the next steps without waiting; at most
+        two may be outstanding, so a bad batch raises within two train_step calls (TF raises
+        in the failing sess.run; here the failing step itself has applied nothing)."""
+        if self._status_host is None:
+            self._status_host = torch.zeros(4, dtype=torch.int32, pin_memory=True)
+        k = self.steps % 4
+        self._status_host[k:k + 1].copy_(self.opt.view(torch.int32)[_lib.OPT_STATUS:_lib.OPT_STATUS + 1],
+                                         non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record()
+        self._status_q.append((k, ev))
+        while self._status_q:
+            k0, e0 = self._status_q[0]
+            if len(self._status_q) > 2:
+                e0.synchronize()
+            elif not e0.query():
+                break
+            self._status_q.pop(0)
+            if int(self._status_host[k0]) != 0:
+                self._status_q.clear()
+                self.check_error()
+
+    def _error_words(self):
+        words = [self.err]
+        for sl in (getattr(self, "_slots", None) or []):
+            if sl.get("err") is not None and sl["err"] is not self.err:
+                words.append(sl["err"])
+        return words
+
     def check_error(self):
-        if int(self.err[0].item()) != 0:
-            self.err.zero_()
-            raise _lib.DLError("InvalidArgumentError: categorical id out of range [0, %d)" % self.N)
+        """Raise (and clear) a pending device error: out-of-range ids of any batch buffer set
+        or the optimizer's status word."""
+        st = self.opt.view(torch.int32)[_lib.OPT_STATUS:_lib.OPT_STATUS + 1]
+        status = int(st.item())
+        bad = any(int(w[0].item()) != 0 for w in self._error_words())
+        if not status and not bad:
+            return
+        for w in self._error_words():
+            w.zero_()
+        st.zero_()
+        self._status_q.clear()
+        if status & _lib.STATUS_LAG:
+            raise _lib.DLError("internal: a row record lagged past the alpha ring (flush schedule)")
+        raise _lib.DLError("InvalidArgumentError: categorical id out of range [0, %d) — the step of the "
+                           "offending batch applied no update" % self.N)
 
 
 def default_adam(spec):

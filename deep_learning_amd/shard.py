@@ -162,7 +162,7 @@ class ShardedCTREngine(CTREngine):
         self.apply_done = None
         # DLAMD_HOST_TIMING=1: host-side timestamps of the step's phases (diagnostics)
         self.host_marks = [] if os.environ.get("DLAMD_HOST_TIMING") else None
-        self.opt_snap = z(2, 16)
+        self.opt_snap = z(2, _lib.OPT_LEN)
         if self.lazy:
             # shard rows as records (rec.hip).  Owners group the ids they receive by row (a sort,
             # or per-row arrival chains); the gradients come back in the same positions, so each

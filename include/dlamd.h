@@ -126,7 +126,7 @@ int dl_embed_fwd_indexed(const dl_emb_layout* L, const float* rows, const float*
  * rows (every sample's) come compact and caught up in rows_rep / rows_rep1 (dl_rec_gather
  * with no unique rows); needs L->cont_rows_compact when there are any.  Outputs are
  * bit-identical to the gather + indexed pair.  Single-valued fields only (multi_width 0). */
-int dl_embed_fwd_rec(const dl_emb_layout* L, const float* rec, int32_t rec_ld, int32_t has_first,
+int dl_embed_fwd_rec(const dl_emb_layout* L, const float* rec, int32_t rec_ld, int32_t rec_flags,
                      const float* rows_rep, const float* rows_rep1, const int64_t* cate,
                      const float* cont, const float* vector, const float* hist, int32_t hist_len,
                      const float* opt, int32_t lag, float* x0, float* fm_out, float* fm_sum,
@@ -289,10 +289,27 @@ int dl_slab_fold_rows(const float* slab, int32_t blocks, int32_t width, int32_t 
  * decay each step — SURVEY.md ledger item 6).  `opt` is a device float[16]:
  * [0] beta1_power [1] beta2_power [2] lr [3] alpha [4] beta1 [5] beta2
  * [6] epsilon [7] step (as float, exact < 2^24), [8..15] per-step accumulators
- * (zeroed by dl_adam_begin_step; sq_out targets); dl_adam_begin_step computes
- * alpha = lr_t*sqrt(1-b2p)/(1-b1p) with lr_t = lr*rate^floor(step/decay_steps)
- * and then advances b1p*=b1, b2p*=b2, step+=1 (TF's _finish + global_step). */
+ * (zeroed by dl_adam_begin_step; sq_out targets), [16] the status word (int32
+ * bits, sticky until the host clears it); DL_OPT_LEN floats in all.
+ * dl_adam_begin_step computes alpha = lr_t*sqrt(1-b2p)/(1-b1p) with
+ * lr_t = lr*rate^floor(step/decay_steps) and then advances b1p*=b1, b2p*=b2,
+ * step+=1 (TF's _finish + global_step).
+ *
+ * A nonzero status word POISONS the step: dl_adam_begin_step and every call that
+ * writes parameters or Adam state (dl_adam_*, dl_rec_bwd_adam, dl_rec_apply_*)
+ * return without writing them; gradient buffers they would consume are still
+ * reset.  A batch whose ids fail validation therefore changes nothing, as TF's
+ * failing sess.run applies nothing before raising InvalidArgumentError
+ * (deepfm_pipeline.py:219-221); the host reads the word back and raises. */
+#define DL_OPT_LEN 32
+#define DL_OPT_STATUS 16
+#define DL_STATUS_BAD_ID 1   /* a categorical / wide id outside [0, N) */
+#define DL_STATUS_LAG 2      /* a row record lagged past the alpha ring (flush schedule broken) */
 int dl_adam_begin_step(float* opt, float decay_rate, float decay_steps, void* stream);
+/* opt[DL_OPT_STATUS] |= batch_err[0] (the batch's id-validation word, written by
+ * dl_index_build / the forward kernels): issued before dl_adam_begin_step so the
+ * step of a bad batch is poisoned from its start. */
+int dl_step_guard(const int32_t* batch_err, float* opt, void* stream);
 /* Dense parameter whose gradient is the sum of `nslab` partial slabs
  * (g = sum_s slab[s*slab_stride + i]); l2 * p is added for i < l2_count;
  * p_prev (may be NULL) receives the pre-update values; sq_out (may be NULL) gets
@@ -307,11 +324,18 @@ int dl_adam_dense(float* p, float* m, float* v, const float* slab, int32_t nslab
 int dl_adam_dense_reg(float* p, float* m, float* v, const float* slab, int32_t nslab,
                       int64_t slab_stride, int64_t n, float reg, int64_t reg_count, int32_t reg_kind,
                       const float* opt, float* p_prev, float* acc_out, void* stream);
-/* Embedding tables with dense-Adam semantics: g = g_table row if touched else 0;
- * consumed gradients are reset to 0; `clear_touched` resets the flags (pass 1
- * on the last table that shares them).  width = E (table) or 1 (first-order). */
+/* Embedding tables, every row updated: g = g_table row if touched else 0;
+ * consumed gradients are reset to 0.  rows_flags: DL_ROWS_CLEAR_TOUCHED resets the
+ * flags (on the last table that shares them); DL_ROWS_SPARSE_ADAM selects the update
+ * TF applies to a Variable read by embedding_lookup directly (Adam._apply_sparse_shared:
+ * m = m*b1 + g*(1-b1), v = v*b2 + (g*g)*(1-b2), p -= lr*m/(sqrt(v)+eps); wdl.py:44-47,132,
+ * deepfm.py:57-60, dnn.py:49-54), else ApplyAdam's (the pipeline models' tables, whose
+ * gradient is densified by the row-0 concat, deepfm_pipeline.py:83-86).
+ * width = E (table) or 1 (first-order). */
+#define DL_ROWS_CLEAR_TOUCHED 1
+#define DL_ROWS_SPARSE_ADAM 2
 int dl_adam_rows(float* p, float* m, float* v, float* g, uint8_t* touched, int64_t n_rows,
-                 int32_t width, float l2, int32_t clear_touched, const float* opt, float* sq_out,
+                 int32_t width, float l2, int32_t rows_flags, const float* opt, float* sq_out,
                  void* stream);
 
 /* ------------------------------------------------------------------------
@@ -324,7 +348,13 @@ int dl_adam_rows(float* p, float* m, float* v, float* g, uint8_t* touched, int64
  * of two) per-step alphas; the caller keeps every row's lag < hist_len by
  * calling dl_rec_flush at least once per hist_len steps.
  * Replaces, for the table and first-order Variables, the dense ApplyAdam of
- * deepfm_pipeline.py:184-188 / dnn_pipeline.py:132-136 / wdl.py:277-285. */
+ * deepfm_pipeline.py:184-188 / dnn_pipeline.py:132-136 and the sparse-apply Adam
+ * of wdl.py:277-285 / deepfm.py:157-162 / dnn.py:92-93.
+ * rec_flags: DL_REC_FIRST = the record carries a first-order weight (FM models);
+ * DL_REC_SPARSE_ADAM = the table is updated in TF's sparse-apply form (see
+ * dl_adam_rows), else ApplyAdam's.  The catch-up replays the same form. */
+#define DL_REC_FIRST 1
+#define DL_REC_SPARSE_ADAM 2
 /* hist[step & (hist_len-1)] = alpha of the step dl_adam_begin_step just began. */
 int dl_adam_hist_record(const float* opt, float* hist, int32_t hist_len, void* stream);
 /* rows_u[i] = p(row_i) caught up to step opt[7]-lag (rows_u1[i] = w1), row_i =
@@ -333,7 +363,7 @@ int dl_adam_hist_record(const float* opt, float* hist, int32_t hist_len, void* s
  * rows with world = 1).  Records are only read.  mv_u (may be NULL) receives the
  * caught-up moments [i][2E+4] = m(E) | v(E) | m1 v1 0 0 for dl_rec_bwd_adam.
  * lag = 1 inside a training step, 0 for predict. */
-int dl_rec_gather(const dl_emb_layout* L, const float* rec, int32_t rec_ld, int32_t has_first,
+int dl_rec_gather(const dl_emb_layout* L, const float* rec, int32_t rec_ld, int32_t rec_flags,
                   int32_t n_rep, const uint32_t* uniq_keys, const int32_t* n_uniq, int64_t max_uniq,
                   int32_t world, const float* hist, int32_t hist_len, const float* opt, int32_t lag,
                   float* rows_u, float* rows_u1, float* mv_u, void* stream);
@@ -363,7 +393,7 @@ typedef struct dl_pool_desc {
 } dl_pool_desc;
 /* pool: required when L->multi_width > 0 (multi refs add (dp/cnt) to the row gradient
  * and dz*w_head[fm_col+m]/cnt_first to the first-order one), else may be NULL. */
-int dl_rec_bwd_adam(const dl_emb_layout* L, float* rec, int32_t rec_ld, int32_t has_first, int32_t n_rep,
+int dl_rec_bwd_adam(const dl_emb_layout* L, float* rec, int32_t rec_ld, int32_t rec_flags, int32_t n_rep,
                     const float* rows_u, const float* rows_u1, const float* mv_u,
                     const uint32_t* uniq_keys, const int32_t* seg_off, const int32_t* n_uniq,
                     const int32_t* sorted_refs, int32_t world, int64_t max_uniq, const float* dz,
@@ -375,21 +405,21 @@ int dl_rec_bwd_adam(const dl_emb_layout* L, float* rec, int32_t rec_ld, int32_t 
  * arrivals g[pos][E], g1[pos] in ascending position order (as dl_rec_apply_segments over a
  * stable sort), catches the record up and steps it; head is reset to -1 afterwards. */
 int dl_rec_chain_link(const int32_t* ids, int64_t n, int32_t* head, int32_t* next, void* stream);
-int dl_rec_apply_chain(float* rec, int32_t rec_ld, int32_t emb_dim, int32_t has_first, const int32_t* ids,
+int dl_rec_apply_chain(float* rec, int32_t rec_ld, int32_t emb_dim, int32_t rec_flags, const int32_t* ids,
                        int64_t n, int32_t* head, const int32_t* next, const float* g, const float* g1,
                        const float* hist, int32_t hist_len, const float* opt, void* stream);
 /* Rows [row0, row0+n): step-t update with dense gradients g[n][E], g1[n] (zeroed after). */
-int dl_rec_apply_rows(float* rec, int32_t rec_ld, int32_t emb_dim, int32_t has_first, int64_t row0,
+int dl_rec_apply_rows(float* rec, int32_t rec_ld, int32_t emb_dim, int32_t rec_flags, int64_t row0,
                       int64_t n, float* g, float* g1, const float* hist, int32_t hist_len,
                       const float* opt, void* stream);
 /* Sharded owners, deterministic: per unique received row (dl_sort_unique over the received
  * ids) the ordered sum of its arrivals g[pos][E], g1[pos] is applied (catch-up + step opt[7]). */
-int dl_rec_apply_segments(float* rec, int32_t rec_ld, int32_t emb_dim, int32_t has_first, const int32_t* uniq,
+int dl_rec_apply_segments(float* rec, int32_t rec_ld, int32_t emb_dim, int32_t rec_flags, const int32_t* uniq,
                           const int32_t* seg_off, const int32_t* n_uniq, int64_t max_uniq, int64_t n,
                           const int32_t* sorted_pos, const float* g, const float* g1, const float* hist,
                           int32_t hist_len, const float* opt, void* stream);
 /* Every row caught up to step opt[7] (before export/checkpoint, and every hist_len steps). */
-int dl_rec_flush(float* rec, int32_t rec_ld, int32_t emb_dim, int32_t has_first, int64_t n_rows,
+int dl_rec_flush(float* rec, int32_t rec_ld, int32_t emb_dim, int32_t rec_flags, int64_t n_rows,
                  const float* hist, int32_t hist_len, const float* opt, void* stream);
 
 /* ------------------------------------------------------------------------

@@ -17,9 +17,14 @@ Models restated:
   wdl               models/wdl.py:43-285
   deepfm (load)     models/deepfm.py:39-162
   dnn (load)        models/dnn.py:35-96
-Optimizer: tf.train.AdamOptimizer (TF1 ApplyAdam, dense — see ledger item 6
-in SURVEY.md: the embedding gradient reaches the Variable through
-concat/strided-slice and is densified, so every row's m, v decay each step).
+Optimizer: tf.train.AdamOptimizer.  Pipeline models: TF1 ApplyAdam, dense — see
+ledger item 6 in SURVEY.md: the embedding gradient reaches the Variable through
+concat/strided-slice and is densified, so every row's m, v decay each step.
+wdl / deepfm / dnn (load-style): the table Variables are read by
+tf.nn.embedding_lookup directly, so their gradient is an IndexedSlices and TF
+applies Adam._apply_sparse_shared (tensorflow/python/training/adam.py, TF 1.x):
+dedup-sum the slices (unsorted_segment_sum), m = m*b1 then scatter_add(g*(1-b1)),
+v = v*b2 then scatter_add((g*g)*(1-b2)), var -= lr*m/(sqrt(v)+eps) over every row.
 """
 import math
 
@@ -65,6 +70,19 @@ FAMILIES = {
 def zero_row0(cfg):
     # deepfm_pipeline.py:83-86; none in wdl.py:44, deepfm.py:58-60, dnn.py:49-52
     return cfg.model not in ("wdl", "deepfm", "dnn")
+
+
+def sparse_keys(cfg):
+    """Variables TF updates with the sparse-apply Adam: read by embedding_lookup with no
+    concat in between (wdl.py:44-47,132; deepfm.py:57-60,78,85,98; dnn.py:49-54).  wdl's
+    wdl_weights is also looked up directly (wdl.py:250) but its L2 term (:270-271) adds a
+    dense gradient, and TF's aggregation of an IndexedSlices with a Tensor is a dense add_n:
+    ApplyAdam."""
+    if cfg.model in ("wdl", "dnn"):
+        return {"weight_mat"}
+    if cfg.model == "deepfm":
+        return {"feats_emb", "feats"}
+    return set()
 
 
 def table_key(cfg):
@@ -436,6 +454,7 @@ class AdamTF1:
 
     def __init__(self, cfg, P, chunk=1 << 22):
         self.cfg = cfg
+        self.sparse = sparse_keys(cfg)
         self.m = {k: np.zeros_like(v) for k, v in P.items()}
         self.v = {k: np.zeros_like(v) for k, v in P.items()}
         self.b1p = F32(cfg.beta1)
@@ -456,14 +475,21 @@ class AdamTF1:
         c = self.cfg
         a = self.alpha()
         b1, b2, eps = F32(1) - F32(c.beta1), F32(1) - F32(c.beta2), F32(c.eps)   # T(1) - beta1() in f32
+        beta1, beta2 = F32(c.beta1), F32(c.beta2)
         for k in P:
             p, m, v, g = P[k].reshape(-1), self.m[k].reshape(-1), self.v[k].reshape(-1), G[k].reshape(-1)
             for s in range(0, p.size, self.chunk):
                 sl = slice(s, s + self.chunk)
                 gs = g[sl].astype(F32)
-                m[sl] += (gs - m[sl]) * b1
-                v[sl] += (gs * gs - v[sl]) * b2
-                p[sl] -= (m[sl] * a) / (np.sqrt(v[sl]) + eps)
+                if k in self.sparse:
+                    # _apply_sparse_shared: rows outside the batch are the g = 0 case (x + 0 = x)
+                    m[sl] = m[sl] * beta1 + gs * b1
+                    v[sl] = v[sl] * beta2 + (gs * gs) * b2
+                    p[sl] -= (a * m[sl]) / (np.sqrt(v[sl]) + eps)
+                else:
+                    m[sl] += (gs - m[sl]) * b1
+                    v[sl] += (gs * gs - v[sl]) * b2
+                    p[sl] -= (m[sl] * a) / (np.sqrt(v[sl]) + eps)
         self.b1p = F32(self.b1p * F32(c.beta1))
         self.b2p = F32(self.b2p * F32(c.beta2))
         self.step += 1

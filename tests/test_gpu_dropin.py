@@ -188,3 +188,63 @@ def test_load_style_deepfm_dnn_fit_evaluate_predict(hip_lib, tmp_path, alg):
     cfg = R.make_cfg(alg, C=13, V=0, S=26, E=8, cate_index_size=4000, hidden=[32, 16])
     fw = R.forward(cfg, P, va_b)
     assert abs(R.auc(va_b["label"], fw["p"]) - auc_pred) < 1e-4
+
+
+def test_tfrecord_two_epoch_trajectory_matches_oracle(hip_lib, tmp_path):
+    """The drop-in fit() fed by the native TFRecord reader (utils/data_loader.py:29-40 order:
+    shuffle(off) -> batch(drop_remainder) -> repeat(2)) trains on exactly the batches the
+    reference iterator yields: 3 part files of 70 + 90 + 50 records at B = 64 give 3 batches per
+    epoch (18 records dropped per epoch, never carried into epoch 2).  The oracle trained on those
+    reference-ordered batches from the same injected parameters matches every step's logits and
+    the final parameters at 1e-5."""
+    from deep_learning_amd.local_run import ModelParams
+    from deep_learning_amd.models import deepfm_pipeline as M
+    from deep_learning_amd.synthetic import make_batch
+    from deep_learning_amd.utils import data_loader
+    from oracle import ctr_ref as R
+    conf, tr, pr = tmp_path / "conf", tmp_path / "train", tmp_path / "pred"
+    for p in (conf, tr, pr):
+        p.mkdir()
+    _conf(str(conf))
+    V, Bsz = 3000, 64
+    parts = {"part-a": make_batch(70, cate_index_size=V, seed=1), "part-b": make_batch(90, cate_index_size=V, seed=2),
+             "part-c": make_batch(50, cate_index_size=V, seed=3)}
+    for n, b in parts.items():
+        data_loader.write_tfrecord_part(str(tr / n), b)
+    data_loader.write_tfrecord_part(str(pr / "part-0"), make_batch(128, cate_index_size=V, seed=9))
+    argv = ["local_run.py", "deepfm_pipeline", "train", "2", "8", str(V), "1000", str(conf), str(tr) + "/",
+            str(pr) + "/", str(tmp_path / "model_pb"), str(tmp_path / "ckpt"), "0", str(tmp_path / "ckpt"),
+            "batch_size=%d" % Bsz, "hidden_units=32,16", "shuffle=0"]
+    mp = ModelParams(argv)
+    m = M.DeepModel(mp, data_loader.load_input_file(mp, mp.train_path, "train"),
+                    data_loader.load_input_file(mp, mp.predict_path, "pred"))
+    m.model_optimizer()
+    eng = m.engine
+    cfg = R.make_cfg("deepfm_pipeline", C=13, V=0, S=26, E=8, cate_index_size=V, hidden=[32, 16])
+    P = R.init_params(cfg, np.random.default_rng(17))
+    eng.load_params(P)
+    zs = []
+    inner = eng.train_step
+
+    def hooked(*a, **k):
+        r = inner(*a, **k)
+        torch.cuda.synchronize()
+        zs.append(eng.z[:Bsz].cpu().numpy().copy())
+        return r
+    eng.train_step = hooked
+    m.fit(mp.num_batch_size)
+    # the reference's batches: files in get_file_list (directory-listing) order, per epoch
+    order = [os.path.basename(f) for f in data_loader.get_file_list(str(tr) + "/")]
+    recs = {k: np.concatenate([parts[n][k] for n in order]) for k in parts["part-a"]}
+    n_per_epoch = 210 // Bsz
+    assert len(zs) == 2 * n_per_epoch
+    opt = R.AdamTF1(cfg, P)
+    for ep in range(2):
+        for j in range(n_per_epoch):
+            b = {k: v[j * Bsz:(j + 1) * Bsz] for k, v in recs.items()}
+            fw = R.train_step(cfg, P, opt, b)
+            np.testing.assert_allclose(zs[ep * n_per_epoch + j], fw["z"], atol=1e-5, rtol=0,
+                                       err_msg="epoch %d batch %d" % (ep, j))
+    got = eng.params()
+    for k in P:
+        np.testing.assert_allclose(got[k], P[k], atol=1e-5, rtol=0, err_msg=k)

@@ -248,3 +248,39 @@ def test_prefetch_matches_inline_index(hip_lib, name, adam):
         eq(a, b)
     for k in runs[0][1]:
         eq(runs[0][1][k], runs[1][1][k], err_msg=k)
+
+
+@pytest.mark.parametrize("name", ["deepfm_pipeline", "wdl", "deepfm_multi_cate"])
+def test_bad_id_step_applies_nothing_and_raises(hip_lib, name):
+    """TF raises InvalidArgumentError inside the failing sess.run, before anything is applied
+    (deepfm_pipeline.py:219-221).  Here the batch index validates the ids and poisons the step
+    (include/dlamd.h, status word): the bad step and any step issued before the host notices
+    apply nothing, and train_step raises within two calls.  Parameters, Adam moments and the
+    step counter are then exactly those of the last good step, and training continues."""
+    from deep_learning_amd import _lib
+    kw = CASES[name]
+    spec = ModelSpec(_model(name), **kw)
+    eng = CTREngine(spec, max_batch=256, seed=4, adam="lazy")
+    bs = _batches(name, kw, 256, 5, seed=13)
+    for i, b in enumerate(bs[:3]):
+        eng.train_step(b, graph=i >= 1)
+    p0, s0 = eng.params(), eng.adam_state()
+    step0 = float(eng.opt[7].item())
+    bad = {k: v.copy() for k, v in bs[3].items()}
+    bad["cate_feats"][5, 3] = kw["cate_index_size"] + 7
+    with pytest.raises(_lib.DLError, match="out of range"):
+        eng.train_step(bad, graph=True)
+        for b in bs[:3]:
+            eng.train_step(b, graph=True)
+        torch.cuda.synchronize()
+        eng.check_error()
+    assert float(eng.opt[7].item()) == step0
+    p1, s1 = eng.params(), eng.adam_state()
+    for k in p0:
+        np.testing.assert_array_equal(p1[k], p0[k], err_msg=k)
+    for k in s0:
+        np.testing.assert_array_equal(s1[k], s0[k], err_msg=k)
+    eng.train_step(bs[4], graph=True)        # the engine trains on after the error
+    torch.cuda.synchronize()
+    eng.check_error()
+    assert float(eng.opt[7].item()) == step0 + 1
