@@ -68,15 +68,32 @@ __device__ __forceinline__ int* opt_status(const float* opt) {
 // Shared by the dense sweep (optim.hip) and the lazy row-record path (rec.hip) so the
 // two compile to the same float operations: a zero-gradient step replayed later by
 // rec.hip's catch-up is bit-identical to the step the dense sweep would have taken.
-// No contraction: each operation is rounded on its own, as in TF's CPU kernel (and the
-// numpy oracle), so for the same gradient the update is the reference's bit for bit.
-// sqrt and divide are correctly rounded (hipcc's default), as Eigen's.
+//
+// The square root and the reciprocal are the hardware's single instructions
+// (v_sqrt_f32, v_rcp_f32: <= 1 ulp each) rather than the correctly rounded sequences of
+// Eigen / numpy (~28 instructions): an update differs from TF's by a few ulp of the update
+// itself (relative ~2e-7 of |delta p| <= ~1e-3), far inside the 1e-5 parity tolerance, and
+// the catch-up replay — the zero-gradient steps of every row a batch touches, ~8 per row
+// per step at C2's steady state — runs ~4x faster (it bound the lazy step: DESIGN.md §5).
+// DL_ADAM_IEEE=1 builds the correctly rounded form for diagnostics.
+#ifndef DL_ADAM_IEEE
+#define DL_ADAM_IEEE 0
+#endif
+__device__ __forceinline__ float adam_step_size(float m, float v, float alpha, float eps) {
+#pragma clang fp contract(off)
+#if DL_ADAM_IEEE
+  return (m * alpha) / (sqrtf(v) + eps);
+#else
+  return (m * alpha) * __builtin_amdgcn_rcpf(__builtin_amdgcn_sqrtf(v) + eps);
+#endif
+}
+
 __device__ __forceinline__ void adam_elem(float& p, float& m, float& v, float g, float alpha,
                                           float omb1, float omb2, float eps) {
 #pragma clang fp contract(off)
   m = m + (g - m) * omb1;
   v = v + (g * g - v) * omb2;
-  p = p - (m * alpha) / (sqrtf(v) + eps);
+  p = p - adam_step_size(m, v, alpha, eps);
 }
 
 // TF1 Adam._apply_sparse_shared (adam.py), the update of a Variable whose gradient arrives
@@ -91,7 +108,7 @@ __device__ __forceinline__ void adam_elem_sparse(float& p, float& m, float& v, f
 #pragma clang fp contract(off)
   m = m * b1 + g * omb1;
   v = v * b2 + (g * g) * omb2;
-  p = p - (alpha * m) / (sqrtf(v) + eps);
+  p = p - adam_step_size(m, v, alpha, eps);
 }
 
 #define DL_DISPATCH_E(E, ...)                    \

@@ -183,7 +183,7 @@ __global__ __launch_bounds__(256) void embed_fwd_kernel(EmbArgs a) {
             const bool fmf = sl < Fs && rc.has_first && q == 0;   // FM slot: its first-order weight too
             float w = t4[p].x, wm = t4[p].y, wv = t4[p].z;
             const int stamp = __float_as_int(t4[p].w);
-            if (stamp < target) catch_up4(v[p], m4[p], v4[p], w, wm, wv, fmf, stamp, target, hist_s, rc);
+            if (stamp < target) catch_up4(v[p], m4[p], v4[p], w, wm, wv, fmf, stamp, target, RingG{hist_s, rc.hist_mask}, rc);
             if (fmf) a.fm_out[(int64_t)b * L.fm_ld + sl] = rw[p] < 0 ? 0.f : w * 1.f;
           }
         }

@@ -1,0 +1,456 @@
+// fp32 tower GEMMs on the bf16 matrix cores, three-plane split ("s3").
+//
+// Every f32 x splits exactly into three bf16 planes, x = hi + mid + lo:
+//   hi = rn_bf16(x), mid = rn_bf16(x - hi), lo = rn_bf16(x - hi - mid)
+// (x - hi is exact in f32 and spans <= 16 significant bits, x - hi - mid <= 8, so lo is
+// exact: a lossless 6-byte encoding of a normal f32).  A product a.b is then
+//   hi.hi + hi.mid + mid.hi + mid.mid + hi.lo + lo.hi        (dropped: mid.lo, lo.mid, lo.lo)
+// with each bf16 x bf16 product exact in the f32 accumulator of v_mfma_f32_16x16x32_bf16;
+// the dropped terms are <= 2^-25 |a.b|, below one f32 rounding.  Six bf16 MFMAs (6 x 16
+// cycles) replace the eight f32 v_mfma_f32_16x16x4_f32 (8 x 32 cycles) of a 32-deep k
+// step: the f32 products of deepfm_pipeline.py:150-152 and their gradients at f32
+// accuracy (tests: fp64 reference, relative error <= 2e-6) at up to 2.7x the f32 rate.
+//
+// Products (all operands f32 in HBM; the split happens in registers):
+//   NT  C[M][N] = A[M][K] . B[N][K]^T   forward (B = W^T) and dX (B = W): A streamed
+//       from HBM straight into MFMA fragments and split in registers; B pre-split into
+//       planes (dl_split3, the weights: a few hundred KB) staged through LDS per 32-deep
+//       k chunk.  Block 256 x 208 (8 waves x 32 rows x 13 column fragments).
+//   TN  C[M][N] = sum_k X[k][M] Y[k][N]  weight gradients, split-K slabs over the batch:
+//       both operands batch-major f32, split into planes on their way into LDS, read back as
+//       MFMA fragments by CDNA4's transposing ds_read_b64_tr_b16.  Block 128 x 416
+//       (8 waves x 32 rows x 13 column fragments).
+#include "common.h"
+
+namespace dl {
+
+typedef float floatx4 __attribute__((ext_vector_type(4)));
+typedef short shortx8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
+typedef float floatx2_t __attribute__((ext_vector_type(2)));
+typedef __attribute__((__vector_size__(4 * sizeof(__fp16)))) __fp16 s3_fp16x4_t;
+
+// two f32 -> packed bf16 (v_cvt_pk_bf16_f32, round to nearest even; element 0 low)
+__device__ __forceinline__ uint32_t pk_bf16(float a, float b) {
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector((floatx2_t){a, b}, bf16x2_t));
+}
+
+// planes of two consecutive elements
+__device__ __forceinline__ void split2(float x0, float x1, uint32_t& h, uint32_t& m, uint32_t& l) {
+#pragma clang fp contract(off)
+  h = pk_bf16(x0, x1);
+  const float r0 = x0 - __uint_as_float(h << 16), r1 = x1 - __uint_as_float(h & 0xffff0000u);
+  m = pk_bf16(r0, r1);
+  const float s0 = r0 - __uint_as_float(m << 16), s1 = r1 - __uint_as_float(m & 0xffff0000u);
+  l = pk_bf16(s0, s1);
+}
+
+// 8 consecutive f32 (two float4) -> the three 8 x bf16 MFMA operands
+__device__ __forceinline__ void split8(const float4& a, const float4& b, shortx8& h, shortx8& m, shortx8& l) {
+  uint4 H, M, L;
+  split2(a.x, a.y, H.x, M.x, L.x);
+  split2(a.z, a.w, H.y, M.y, L.y);
+  split2(b.x, b.y, H.z, M.z, L.z);
+  split2(b.z, b.w, H.w, M.w, L.w);
+  h = __builtin_bit_cast(shortx8, H);
+  m = __builtin_bit_cast(shortx8, M);
+  l = __builtin_bit_cast(shortx8, L);
+}
+
+// acc += a.b over the six significant plane products (small terms first)
+__device__ __forceinline__ floatx4 mfma_s3(const shortx8& ah, const shortx8& am, const shortx8& al,
+                                           const shortx8& bh, const shortx8& bm, const shortx8& bl,
+                                           floatx4 acc) {
+  acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al, bh, acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bl, acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(am, bm, acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(am, bh, acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bm, acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bh, acc, 0, 0, 0);
+  return acc;
+}
+
+__device__ __forceinline__ int s3_xcd_tile(int bid, int T) {
+  const int x = bid & 7;
+  const int q = T >> 3, rm = T & 7;
+  return (x < rm ? x * (q + 1) : rm * (q + 1) + (x - rm) * q) + (bid >> 3);
+}
+
+struct S3Params {
+  const float* A;
+  const void* B;
+  float* C;
+  const float* mask;
+  int M, N, K;
+  int lda, ldb, ldc, ldm;
+  long long b_plane;         // NT: elements between the planes of B
+  int k_per_split;           // TN
+  long long c_split_stride;  // TN
+};
+
+enum { S3_STORE = 0, S3_RELU = 1, S3_MASK = 2 };
+
+#ifndef DL_S3_DIAG
+#define DL_S3_DIAG 0   // diagnostics builds: 1 = no epilogue stores, 2 = no MFMAs either
+#endif
+
+// ---------------------------------------------------------------------------- NT
+constexpr int kNtBM = 256, kNtBN = 208, kNtNF = 13, kNtKP = 40;   // LDS row pitch 40 bf16 = 80 B
+constexpr int kNtPlane = kNtBN * kNtKP;                          // elements of one plane image
+constexpr int kNtBuf = 3 * kNtPlane;
+constexpr int kNtQB = 3 * kNtBN * 4;                             // 16-B pieces of a B chunk
+constexpr int kNtQPT = (kNtQB + 511) / 512;
+constexpr size_t kNtLds = 2 * kNtBuf * sizeof(unsigned short);
+
+template <int EPI>
+__global__ __launch_bounds__(512) void gemm_s3_nt_kernel(S3Params p) {
+  extern __shared__ __attribute__((aligned(16))) unsigned short lds[];   // [2][3][BN][KP]
+  const unsigned short* __restrict__ Bp = reinterpret_cast<const unsigned short*>(p.B);
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int ntm = (p.M + kNtBM - 1) / kNtBM, ntn = (p.N + kNtBN - 1) / kNtBN;
+  const int t = s3_xcd_tile(blockIdx.x, ntm * ntn);
+  const int i0 = (t / ntn) * kNtBM, j0 = (t % ntn) * kNtBN;
+  const int cl = lane & 15, kq = lane >> 4;
+  const int r0 = i0 + wid * 32;
+  const bool ok0 = r0 + cl < p.M, ok1 = r0 + 16 + cl < p.M;
+  const float* a0 = p.A + (long long)min(r0 + cl, p.M - 1) * p.lda + 8 * kq;
+  const float* a1 = p.A + (long long)min(r0 + 16 + cl, p.M - 1) * p.lda + 8 * kq;
+  const int KC = (p.K + 31) / 32;
+  const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
+  const uint4 zu = make_uint4(0u, 0u, 0u, 0u);
+  const int nf_live = min(kNtNF, (p.N - j0 + 15) / 16);   // column fragments inside N (wave-uniform)
+
+  uint4 rb[kNtQPT];
+  auto load_b = [&](int c) {
+#pragma unroll
+    for (int u = 0; u < kNtQPT; ++u) {
+      const int q = tid + u * 512;
+      uint4 v = zu;
+      if (q < kNtQB) {
+        const int pl = q / (kNtBN * 4), rem = q % (kNtBN * 4);
+        const int j = rem >> 2, c4 = rem & 3;
+        const int gj = j0 + j, gk = 32 * c + 8 * c4;
+        if (gj < p.N && gk < p.K)
+          v = *reinterpret_cast<const uint4*>(Bp + pl * p.b_plane + (long long)gj * p.ldb + gk);
+      }
+      rb[u] = v;
+    }
+  };
+  auto store_b = [&](int buf) {
+#pragma unroll
+    for (int u = 0; u < kNtQPT; ++u) {
+      const int q = tid + u * 512;
+      if (q < kNtQB) {
+        const int pl = q / (kNtBN * 4), rem = q % (kNtBN * 4);
+        const int j = rem >> 2, c4 = rem & 3;
+        *reinterpret_cast<uint4*>(&lds[buf * kNtBuf + pl * kNtPlane + j * kNtKP + 8 * c4]) = rb[u];
+      }
+    }
+  };
+  // A: this lane's 8 floats of rows r0 + cl, r0 + 16 + cl at k = 32c + 8kq
+  auto load_a = [&](int c, float4 (&ra)[4]) {
+    const bool kin = 32 * c + 8 * kq < p.K;
+    ra[0] = (ok0 && kin) ? *reinterpret_cast<const float4*>(a0 + 32 * c) : z4;
+    ra[1] = (ok0 && kin) ? *reinterpret_cast<const float4*>(a0 + 32 * c + 4) : z4;
+    ra[2] = (ok1 && kin) ? *reinterpret_cast<const float4*>(a1 + 32 * c) : z4;
+    ra[3] = (ok1 && kin) ? *reinterpret_cast<const float4*>(a1 + 32 * c + 4) : z4;
+  };
+
+  floatx4 acc[2][kNtNF];
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int f = 0; f < kNtNF; ++f) acc[a][f] = floatx4{0.f, 0.f, 0.f, 0.f};
+
+  float4 raA[4], raB[4];
+  load_b(0);
+  store_b(0);
+  load_a(0, raA);
+  if (KC > 1) load_a(1, raB);
+  __syncthreads();
+
+  auto step = [&](int c, float4 (&ra)[4]) {
+    shortx8 ah[2], am[2], al[2];
+    split8(ra[0], ra[1], ah[0], am[0], al[0]);
+    split8(ra[2], ra[3], ah[1], am[1], al[1]);
+    // B of the next chunk first, then A two chunks ahead: store_b at the end of this step
+    // waits only for the B loads (vmcnt leaves the younger A loads in flight)
+    if (c + 1 < KC) load_b(c + 1);
+    if (c + 2 < KC) load_a(c + 2, ra);          // the registers are free again
+    const unsigned short* Bs = lds + (c & 1) * kNtBuf;
+#pragma unroll
+    for (int f = 0; f < kNtNF; ++f) {
+      if (f < nf_live) {
+        const int o = (16 * f + cl) * kNtKP + 8 * kq;
+        const shortx8 bh = *reinterpret_cast<const shortx8*>(&Bs[o]);
+        const shortx8 bm = *reinterpret_cast<const shortx8*>(&Bs[kNtPlane + o]);
+        const shortx8 bl = *reinterpret_cast<const shortx8*>(&Bs[2 * kNtPlane + o]);
+        if (DL_S3_DIAG >= 2) {
+          acc[0][f][0] += (float)(bh[0] ^ ah[0][1] ^ bm[2] ^ bl[3] ^ am[0][0] ^ al[0][2]);
+          acc[1][f][0] += (float)(bh[1] ^ ah[1][1] ^ bm[3] ^ bl[4] ^ am[1][0] ^ al[1][2]);
+        } else {
+          acc[0][f] = mfma_s3(ah[0], am[0], al[0], bh, bm, bl, acc[0][f]);
+          acc[1][f] = mfma_s3(ah[1], am[1], al[1], bh, bm, bl, acc[1][f]);
+        }
+      }
+    }
+    if (c + 1 < KC) store_b((c + 1) & 1);
+    __syncthreads();
+  };
+  for (int c = 0; c < KC; c += 2) {
+    step(c, raA);
+    if (c + 1 < KC) step(c + 1, raB);
+  }
+
+  const float* __restrict__ Mk = p.mask;
+  if (DL_S3_DIAG) {   // keep the loop's results live without storing them
+    float t = 0.f;
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+      for (int f = 0; f < kNtNF; ++f) t += acc[a][f][0] + acc[a][f][3];
+    if (t == 12345.f) p.C[0] = t;
+    return;
+  }
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int f = 0; f < kNtNF; ++f) {
+      const int col = j0 + 16 * f + cl;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int row = r0 + 16 * a + 4 * kq + j;
+        if (row < p.M && col < p.N) {
+          float v = acc[a][f][j];
+          if (EPI == S3_RELU) v = fmaxf(v, 0.f);
+          if (EPI == S3_MASK) v = Mk[(long long)row * p.ldm + col] > 0.f ? v : 0.f;
+          p.C[(long long)row * p.ldc + col] = v;
+        }
+      }
+    }
+}
+
+// ---------------------------------------------------------------------------- TN
+// Block: 128 rows (m) x 416 columns (n) of a split-K slab, 8 waves: wave w owns rows
+// 32 (w & 3) .. +32 (2 fragments) x columns 208 (w >> 2) .. +208 (13 fragments).  Per
+// 32-deep batch step the f32 tiles X[k][m0..m0+128) and Y[k][0..416) are loaded into
+// registers one step ahead, split, and written to LDS as three plane images each
+// ([k][m], [k][n]; pitches 144 and 432 bf16 = 8 x odd words: conflict-free transposed
+// reads).  Lane group kq reads batch rows 4kq..4kq+3 and 16+4kq..16+4kq+3 for both operands
+// (the same k set, so the sum is unchanged).
+constexpr int kTnBM = 128, kTnBN = 416, kTnKS = 32, kTnPA = 144, kTnPB = 432;
+constexpr int kTnAE = kTnKS * kTnPA, kTnBE = kTnKS * kTnPB;          // elements per plane image
+constexpr int kTnQA = kTnKS * kTnBM / 4, kTnQB = kTnKS * kTnBN / 4;  // float4 pieces per step
+constexpr int kTnQ = (kTnQA + kTnQB + 511) / 512;
+constexpr size_t kTnLds = 3 * (kTnAE + kTnBE) * sizeof(unsigned short);
+
+__device__ __forceinline__ uint2 s3_lds_tr16(const unsigned short* ptr_) {
+  auto lp = (__attribute__((address_space(3))) unsigned short*)(const_cast<unsigned short*>(ptr_));
+  const s3_fp16x4_t v =
+      __builtin_amdgcn_ds_read_tr16_b64_v4f16(reinterpret_cast<__attribute__((address_space(3))) s3_fp16x4_t*>(lp));
+  return __builtin_bit_cast(uint2, v);
+}
+
+__device__ __forceinline__ shortx8 s3_tr_frag(const unsigned short* img, int pitch, int ra, int rb, int col) {
+  const uint2 lo = s3_lds_tr16(&img[ra * pitch + col]);
+  const uint2 hi = s3_lds_tr16(&img[rb * pitch + col]);
+  return __builtin_bit_cast(shortx8, make_uint4(lo.x, lo.y, hi.x, hi.y));
+}
+
+__global__ __launch_bounds__(512) void gemm_s3_tn_kernel(S3Params p) {
+  extern __shared__ __attribute__((aligned(16))) unsigned short lds[];   // [3][KS][PA] then [3][KS][PB]
+  unsigned short* As = lds;
+  unsigned short* Bs = lds + 3 * kTnAE;
+  const float* __restrict__ X = p.A;
+  const float* __restrict__ Y = reinterpret_cast<const float*>(p.B);
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int mtiles = (p.M + kTnBM - 1) / kTnBM;
+  const int t = s3_xcd_tile(blockIdx.x, gridDim.x);
+  const int m0 = (t % mtiles) * kTnBM, z = t / mtiles;
+  const int kbeg = z * p.k_per_split;
+  const int kend = min(p.K, kbeg + p.k_per_split);
+  const int nk = (kend - kbeg + kTnKS - 1) / kTnKS;
+  const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
+  float4 rs[kTnQ];
+  auto load = [&](int k0) {
+#pragma unroll
+    for (int u = 0; u < kTnQ; ++u) {
+      const int q = tid + u * 512;
+      float4 v = z4;
+      if (q < kTnQA) {
+        const int r = q / (kTnBM / 4), c4 = q % (kTnBM / 4);
+        const int gk = k0 + r, gm = m0 + 4 * c4;
+        if (gk < kend && gm < p.M) v = *reinterpret_cast<const float4*>(X + (long long)gk * p.lda + gm);
+      } else if (q < kTnQA + kTnQB) {
+        const int qq = q - kTnQA, r = qq / (kTnBN / 4), c4 = qq % (kTnBN / 4);
+        const int gk = k0 + r, gn = 4 * c4;
+        if (gk < kend && gn < p.N) v = *reinterpret_cast<const float4*>(Y + (long long)gk * p.ldb + gn);
+      }
+      rs[u] = v;
+    }
+  };
+  auto store = [&]() {
+#pragma unroll
+    for (int u = 0; u < kTnQ; ++u) {
+      const int q = tid + u * 512;
+      uint32_t h0, m0_, l0, h1, m1_, l1;
+      split2(rs[u].x, rs[u].y, h0, m0_, l0);
+      split2(rs[u].z, rs[u].w, h1, m1_, l1);
+      if (q < kTnQA) {
+        const int r = q / (kTnBM / 4), c4 = q % (kTnBM / 4);
+        const int o = r * kTnPA + 4 * c4;
+        *reinterpret_cast<uint2*>(&As[o]) = make_uint2(h0, h1);
+        *reinterpret_cast<uint2*>(&As[kTnAE + o]) = make_uint2(m0_, m1_);
+        *reinterpret_cast<uint2*>(&As[2 * kTnAE + o]) = make_uint2(l0, l1);
+      } else if (q < kTnQA + kTnQB) {
+        const int qq = q - kTnQA, r = qq / (kTnBN / 4), c4 = qq % (kTnBN / 4);
+        const int o = r * kTnPB + 4 * c4;
+        *reinterpret_cast<uint2*>(&Bs[o]) = make_uint2(h0, h1);
+        *reinterpret_cast<uint2*>(&Bs[kTnBE + o]) = make_uint2(m0_, m1_);
+        *reinterpret_cast<uint2*>(&Bs[2 * kTnBE + o]) = make_uint2(l0, l1);
+      }
+    }
+  };
+  floatx4 acc[2][13];
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 13; ++b) acc[a][b] = floatx4{0.f, 0.f, 0.f, 0.f};
+  const int wm = wid & 3, wn = wid >> 2;
+  const int cl = lane & 15, kq = lane >> 4, rq = cl >> 2, cp = cl & 3;
+  const int ra = 4 * kq + rq, rb = 16 + 4 * kq + rq;
+  // fragments whose rows / columns lie past M / N are skipped (wave-uniform)
+  const int ma_live = min(2, max(0, (p.M - (m0 + 32 * wm) + 15) / 16));
+  const int nb_live = min(13, max(0, (p.N - 208 * wn + 15) / 16));
+  if (nk > 0) {
+    load(kbeg);
+    store();
+    __syncthreads();
+  }
+  for (int kt = 0; kt < nk; ++kt) {
+    if (kt + 1 < nk) load(kbeg + (kt + 1) * kTnKS);
+    shortx8 ah[2], am[2], al[2];
+#pragma unroll
+    for (int a = 0; a < 2; ++a) {
+      const int col = 32 * wm + 16 * a + 4 * cp;
+      ah[a] = s3_tr_frag(As, kTnPA, ra, rb, col);
+      am[a] = s3_tr_frag(As + kTnAE, kTnPA, ra, rb, col);
+      al[a] = s3_tr_frag(As + 2 * kTnAE, kTnPA, ra, rb, col);
+    }
+#pragma unroll
+    for (int b = 0; b < 13; ++b) {
+      if (b < nb_live) {
+        const int col = 208 * wn + 16 * b + 4 * cp;
+        const shortx8 bh = s3_tr_frag(Bs, kTnPB, ra, rb, col);
+        const shortx8 bm = s3_tr_frag(Bs + kTnBE, kTnPB, ra, rb, col);
+        const shortx8 bl = s3_tr_frag(Bs + 2 * kTnBE, kTnPB, ra, rb, col);
+#pragma unroll
+        for (int a = 0; a < 2; ++a)
+          if (a < ma_live) acc[a][b] = mfma_s3(ah[a], am[a], al[a], bh, bm, bl, acc[a][b]);
+      }
+    }
+    __syncthreads();
+    if (kt + 1 < nk) {
+      store();
+      __syncthreads();
+    }
+  }
+  float* __restrict__ C = p.C + (long long)z * p.c_split_stride;
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 13; ++b) {
+      const int col = 208 * wn + 16 * b + cl;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int row = m0 + 32 * wm + 16 * a + 4 * kq + j;
+        if (row < p.M && col < p.N) C[(long long)row * p.ldc + col] = acc[a][b][j];
+      }
+    }
+}
+
+// ---------------------------------------------------------------------------- split
+// dst plane q (q = 0 hi, 1 mid, 2 lo) at dst + q * plane: element (r, c) of src [rows][cols]
+// (ld lds) goes to [r][c] (ldd), or to [c][r] when transposed.
+__global__ __launch_bounds__(256) void split3_kernel(const float* __restrict__ src, int rows, int cols, int lds,
+                                                     int transpose, unsigned short* __restrict__ dst, int ldd,
+                                                     long long plane) {
+  const long long n = (long long)rows * cols;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x) {
+    const int r = (int)(i / cols), c = (int)(i % cols);
+    uint32_t h, m, l;
+    split2(src[(long long)r * lds + c], 0.f, h, m, l);
+    const long long o = transpose ? (long long)c * ldd + r : (long long)r * ldd + c;
+    dst[o] = (unsigned short)h;
+    dst[plane + o] = (unsigned short)m;
+    dst[2 * plane + o] = (unsigned short)l;
+  }
+}
+
+}  // namespace dl
+
+using namespace dl;
+
+extern "C" int dl_split3(const float* src, int32_t rows, int32_t cols, int32_t lds, int32_t transpose,
+                         uint16_t* dst, int32_t ldd, int64_t plane_stride, void* stream) {
+  DL_CHECK_ARG(src && dst, "NULL pointer");
+  DL_CHECK_ARG(rows >= 0 && cols >= 0 && lds >= cols, "bad src shape");
+  DL_CHECK_ARG(ldd >= (transpose ? rows : cols), "ldd too small");
+  DL_CHECK_ARG(plane_stride >= (long long)ldd * (transpose ? cols : rows), "plane stride too small");
+  const long long n = (long long)rows * cols;
+  if (n == 0) return 0;
+  long long blocks = (n + 255) / 256;
+  if (blocks > 4096) blocks = 4096;
+  hipLaunchKernelGGL(split3_kernel, dim3((unsigned)blocks), dim3(256), 0, as_stream(stream), src, rows, cols, lds,
+                     transpose, reinterpret_cast<unsigned short*>(dst), ldd, (long long)plane_stride);
+  DL_RETURN_LAUNCH("dl_split3");
+}
+
+extern "C" int dl_gemm_s3_nt(int32_t M, int32_t N, int32_t K, const float* A, int32_t lda, const uint16_t* Bp,
+                             int32_t ldb, int64_t b_plane, float* C, int32_t ldc, int32_t epi, const float* mask,
+                             int32_t ldm, void* stream) {
+  DL_CHECK_ARG(M >= 0 && N >= 0 && K >= 0, "negative dims");
+  DL_CHECK_ARG(A && Bp && C, "NULL operand");
+  DL_CHECK_ARG(K % 8 == 0, "K %d must be a multiple of 8", K);
+  DL_CHECK_ARG(lda % 4 == 0 && lda >= K && ldb % 8 == 0 && ldb >= K && ldc >= N, "bad leading dims");
+  DL_CHECK_ARG(((uintptr_t)A % 16) == 0 && ((uintptr_t)Bp % 16) == 0 && b_plane % 8 == 0,
+               "A / B planes must be 16-byte aligned");
+  DL_CHECK_ARG(b_plane >= (long long)ldb * N, "plane stride too small");
+  DL_CHECK_ARG(epi >= 0 && epi <= 2, "bad epilogue %d", epi);
+  DL_CHECK_ARG(epi != S3_MASK || mask, "mask epilogue needs mask");
+  if (M == 0 || N == 0) return 0;
+  S3Params p{};
+  p.A = A; p.B = Bp; p.C = C; p.mask = mask;
+  p.M = M; p.N = N; p.K = K; p.lda = lda; p.ldb = ldb; p.ldc = ldc; p.ldm = ldm; p.b_plane = b_plane;
+  const int tiles = (int)(ceil_div(M, kNtBM) * ceil_div(N, kNtBN));
+  hipStream_t s = as_stream(stream);
+  if (epi == S3_STORE) hipLaunchKernelGGL(gemm_s3_nt_kernel<S3_STORE>, dim3(tiles), dim3(512), kNtLds, s, p);
+  else if (epi == S3_RELU) hipLaunchKernelGGL(gemm_s3_nt_kernel<S3_RELU>, dim3(tiles), dim3(512), kNtLds, s, p);
+  else hipLaunchKernelGGL(gemm_s3_nt_kernel<S3_MASK>, dim3(tiles), dim3(512), kNtLds, s, p);
+  DL_RETURN_LAUNCH("dl_gemm_s3_nt");
+}
+
+extern "C" int dl_gemm_s3_tn(int32_t M, int32_t N, int32_t K, const float* X, int32_t lda, const float* Y,
+                             int32_t ldb, float* C, int32_t ldc, int32_t splits, int64_t c_split_stride,
+                             void* stream) {
+  DL_CHECK_ARG(M >= 0 && N >= 0 && K >= 0, "negative dims");
+  DL_CHECK_ARG(X && Y && C, "NULL operand");
+  DL_CHECK_ARG(N <= kTnBN, "N %d > %d", N, kTnBN);
+  DL_CHECK_ARG(lda % 4 == 0 && ldb % 4 == 0 && lda >= (M + 3) / 4 * 4 && ldb >= (N + 3) / 4 * 4 && ldc >= N,
+               "bad leading dims");
+  DL_CHECK_ARG(((uintptr_t)X % 16) == 0 && ((uintptr_t)Y % 16) == 0, "X / Y must be 16-byte aligned");
+  if (splits < 1) splits = 1;
+  DL_CHECK_ARG(splits == 1 || c_split_stride >= (long long)ldc * M, "slab stride too small");
+  if (M == 0 || N == 0) return 0;
+  S3Params p{};
+  p.A = X; p.B = Y; p.C = C;
+  p.M = M; p.N = N; p.K = K; p.lda = lda; p.ldb = ldb; p.ldc = ldc;
+  int kps = (int)ceil_div(K > 0 ? K : 1, splits);
+  kps = (kps + 63) / 64 * 64;                    // callers sum ceil(K / kps) slabs at this rounding
+  p.k_per_split = kps;
+  p.c_split_stride = c_split_stride;
+  splits = (int)ceil_div(K > 0 ? K : 1, kps);
+  const int mtiles = (int)ceil_div(M, kTnBM);
+  hipLaunchKernelGGL(gemm_s3_tn_kernel, dim3((unsigned)(mtiles * splits)), dim3(512), kTnLds, as_stream(stream), p);
+  DL_RETURN_LAUNCH("dl_gemm_s3_tn");
+}

@@ -50,14 +50,44 @@ __device__ __forceinline__ int catch_up_from(int from, int to, const RecCfg& c) 
   return from;
 }
 
+// The per-step alphas of the zero-gradient steps a catch-up replays.  RingG reads the ring
+// where it lies (global memory, or an LDS copy of the whole ring); RingW keeps the newest
+// kHistWin steps before t0 in LDS (filled once per block by load_hist_window) and reads only
+// older steps from the global ring: one replayed step used to wait a full global-load round
+// trip for its alpha, which bound the catch-up loop by memory latency at realistic row lags.
+constexpr int kHistWin = 256;
+
+struct RingG {
+  const float* h;
+  int mask;
+  __device__ __forceinline__ float operator()(int j) const { return h[j & mask]; }
+};
+
+struct RingW {
+  const float* sh;   // sh[d] = alpha of step t0 - d, d < kHistWin
+  const float* h;
+  int mask, t0;
+  __device__ __forceinline__ float operator()(int j) const {
+    const int d = t0 - j;
+    return d < kHistWin ? sh[d] : h[j & mask];
+  }
+};
+
+// Whole block: the window of the kHistWin steps up to t0 (entries past the ring's length are
+// never read: a row's lag never exceeds the ring).  Call before any divergent return.
+__device__ __forceinline__ RingW load_hist_window(float* sh, const float* __restrict__ hist, int t0, const RecCfg& c) {
+  for (int d = threadIdx.x; d < kHistWin; d += blockDim.x) sh[d] = hist ? hist[(t0 - d) & c.hist_mask] : 0.f;
+  __syncthreads();
+  return RingW{sh, hist, c.hist_mask, t0};
+}
+
 // Replays zero-gradient steps (from, to] on one float4 of p/m/v (and the
 // first-order triple when `first` is set).
-__device__ __forceinline__ void catch_up4(float4& p, float4& m, float4& v, float& w, float& wm, float& wv,
-                                          bool first, int from, int to, const float* __restrict__ hist,
-                                          const RecCfg& c) {
-  from = catch_up_from(from, to, c);
+template <class Ring>
+__device__ __forceinline__ void catch_up4_loop(float4& p, float4& m, float4& v, float& w, float& wm, float& wv,
+                                               bool first, int from, int to, const Ring& ring, const RecCfg& c) {
   for (int j = from + 1; j <= to; ++j) {
-    const float al = hist[j & c.hist_mask];
+    const float al = ring(j);
     rec_adam(p.x, m.x, v.x, 0.f, al, c);
     rec_adam(p.y, m.y, v.y, 0.f, al, c);
     rec_adam(p.z, m.z, v.z, 0.f, al, c);
@@ -66,15 +96,59 @@ __device__ __forceinline__ void catch_up4(float4& p, float4& m, float4& v, float
   }
 }
 
-__device__ __forceinline__ void catch_up1(float& p, float& m, float& v, float& w, float& wm, float& wv,
-                                          bool first, int from, int to, const float* __restrict__ hist,
-                                          const RecCfg& c) {
-  from = catch_up_from(from, to, c);
+template <class Ring>
+__device__ __forceinline__ void catch_up1_loop(float& p, float& m, float& v, float& w, float& wm, float& wv,
+                                               bool first, int from, int to, const Ring& ring, const RecCfg& c) {
   for (int j = from + 1; j <= to; ++j) {
-    const float al = hist[j & c.hist_mask];
+    const float al = ring(j);
     rec_adam(p, m, v, 0.f, al, c);
     if (first) rec_adam(w, wm, wv, 0.f, al, c);
   }
+}
+
+// LDS-only reads of the alpha window
+struct RingWin {
+  const float* sh;
+  int t0;
+  __device__ __forceinline__ float operator()(int j) const { return sh[t0 - j]; }
+};
+
+template <class Ring>
+__device__ __forceinline__ void catch_up4(float4& p, float4& m, float4& v, float& w, float& wm, float& wv,
+                                          bool first, int from, int to, const Ring& ring, const RecCfg& c) {
+  from = catch_up_from(from, to, c);
+  catch_up4_loop(p, m, v, w, wm, wv, first, from, to, ring, c);
+}
+
+// the window form: steps inside the LDS window are read from LDS only (a row lagging
+// further first replays its older steps from the global ring)
+__device__ __forceinline__ void catch_up4(float4& p, float4& m, float4& v, float& w, float& wm, float& wv,
+                                          bool first, int from, int to, const RingW& ring, const RecCfg& c) {
+  from = catch_up_from(from, to, c);
+  const int lo = ring.t0 - kHistWin;   // steps > lo are in the window
+  if (from < lo) {
+    catch_up4_loop(p, m, v, w, wm, wv, first, from, lo, RingG{ring.h, ring.mask}, c);
+    from = lo;
+  }
+  catch_up4_loop(p, m, v, w, wm, wv, first, from, to, RingWin{ring.sh, ring.t0}, c);
+}
+
+template <class Ring>
+__device__ __forceinline__ void catch_up1(float& p, float& m, float& v, float& w, float& wm, float& wv,
+                                          bool first, int from, int to, const Ring& ring, const RecCfg& c) {
+  from = catch_up_from(from, to, c);
+  catch_up1_loop(p, m, v, w, wm, wv, first, from, to, ring, c);
+}
+
+__device__ __forceinline__ void catch_up1(float& p, float& m, float& v, float& w, float& wm, float& wv,
+                                          bool first, int from, int to, const RingW& ring, const RecCfg& c) {
+  from = catch_up_from(from, to, c);
+  const int lo = ring.t0 - kHistWin;
+  if (from < lo) {
+    catch_up1_loop(p, m, v, w, wm, wv, first, from, lo, RingG{ring.h, ring.mask}, c);
+    from = lo;
+  }
+  catch_up1_loop(p, m, v, w, wm, wv, first, from, to, RingWin{ring.sh, ring.t0}, c);
 }
 
 }  // namespace dl

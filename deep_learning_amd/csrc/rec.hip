@@ -35,8 +35,17 @@ namespace dl {
 // Forward gather of the batch's rows, caught up to step opt[7] - lag:
 //   out[i] = p(row_i), out1[i] = w1(row_i),   row_i = rep_base + i (i < n_rep), else uniq[i - n_rep]
 // (rep_base = the layout's fm_cont_offset: the replicated FM cont-field rows)
-// Records are only read: the catch-up is recomputed (cheaply, in registers) by the
-// backward's update, which is the one that writes.  E/4 lanes per row, float4 each.
+// Records are only read: the backward's update writes (it takes the caught-up moments
+// from `mv` when given, or replays the catch-up itself).  E/4 lanes per row, float4 each.
+//
+// Lag-balanced catch-up.  A wave holds RPW = 256/E rows, and row lags differ (geometric at
+// steady state: C2 mean ~8, max of 16 rows ~25): with each row replayed by its own lanes the
+// wave runs as long as its worst row while every lane carries E/4 + 1 element chains.
+// Instead the wave stages its rows' p, m, v (and first-order triple) in LDS and splits the
+// replay into single-element chains (E or E + 1 per row, each as long as its row's lag),
+// dealt to the 64 lanes in descending-lag order, snake-wise (round i: chains 64i..64i+63,
+// reversed on odd rounds): lanes that took a long chain take short ones after it.  Each
+// chain is the same sequence of rec_adam calls as before, so the results are unchanged.
 template <int E>
 __global__ __launch_bounds__(256) void rec_gather_kernel(const float* __restrict__ rec, RecCfg c, int64_t n_rows,
                                                          int n_rep, int64_t rep_base,
@@ -47,27 +56,90 @@ __global__ __launch_bounds__(256) void rec_gather_kernel(const float* __restrict
                                                          float* __restrict__ out, float* __restrict__ out1,
                                                          float* __restrict__ mv) {
   rec_load_hyper(c, opt);
-  constexpr int LPR = E / 4;
+  __shared__ float hw[kHistWin];
+  const RingW ring = load_hist_window(hw, hist, (int)opt[7], c);
+  constexpr int LPR = E / 4, RPW = 64 / LPR, PITCH = 3 * E + 3;
+  __shared__ float st_all[4][RPW * PITCH];           // per wave: p | m | v | w wm wv of each row
+  __shared__ int from_all[4][RPW], order_all[4][RPW];
+  const int lane = threadIdx.x & 63, wv_ = threadIdx.x >> 6;
+  float* st = st_all[wv_];
+  int* from_s = from_all[wv_];
+  int* order = order_all[wv_];
   const long long gt = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-  const int q = (int)(gt % LPR);
-  const long long group0 = gt / LPR, ngroups = (long long)gridDim.x * blockDim.x / LPR;
+  const int q = lane % LPR, rw = lane / LPR;
+  const long long wave_id = gt >> 6, nwaves = ((long long)gridDim.x * blockDim.x) >> 6;
   const long long total = n_rep + (n_uniq ? (long long)clamp_uniq(n_uniq, max_u) : max_u);
   const int target = (int)opt[7] - lag;
-  for (long long i = group0; i < total; i += ngroups) {
-    const int64_t row = i < n_rep ? rep_base + i : decode_key(uniq[i - n_rep], world);
+  const int nch = E + (c.has_first ? 1 : 0);          // element chains per row
+  const int T = RPW * nch;
+  for (long long base = wave_id * RPW; base < total; base += nwaves * RPW) {
+    const long long i = base + rw;
+    const bool valid = i < total;
+    const int64_t row = !valid ? -1 : i < n_rep ? rep_base + i : decode_key(uniq[i - n_rep], world);
     const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
     float4 p = z, m = z, v = z;
     float w = 0.f, wm = 0.f, wv = 0.f;
+    int from = target;
     if (row >= 0 && row < n_rows) {
       const float* r = rec + row * c.ld;
       p = *reinterpret_cast<const float4*>(r + 4 * q);
       m = *reinterpret_cast<const float4*>(r + E + 4 + 4 * q);
       v = *reinterpret_cast<const float4*>(r + 2 * E + 4 + 4 * q);
       const float4 tail = *reinterpret_cast<const float4*>(r + E);
-      const int stamp = __float_as_int(tail.w);
       w = tail.x; wm = tail.y; wv = tail.z;
-      if (stamp < target) catch_up4(p, m, v, w, wm, wv, c.has_first && q == 0, stamp, target, hist, c);
+      const int stamp = __float_as_int(tail.w);
+      if (stamp < target) from = catch_up_from(stamp, target, c);
     }
+    if (__any(from < target)) {
+      // stage the rows
+      float* sr = st + rw * PITCH;
+      sr[4 * q + 0] = p.x; sr[4 * q + 1] = p.y; sr[4 * q + 2] = p.z; sr[4 * q + 3] = p.w;
+      sr[E + 4 * q + 0] = m.x; sr[E + 4 * q + 1] = m.y; sr[E + 4 * q + 2] = m.z; sr[E + 4 * q + 3] = m.w;
+      sr[2 * E + 4 * q + 0] = v.x; sr[2 * E + 4 * q + 1] = v.y; sr[2 * E + 4 * q + 2] = v.z;
+      sr[2 * E + 4 * q + 3] = v.w;
+      const int mylag = target - from;
+      int rank = 0;   // rows with a longer lag (ties: lower row first)
+#pragma unroll
+      for (int o = 0; o < RPW; ++o) {
+        const int lo = __shfl(mylag, o * LPR, 64);
+        rank += (lo > mylag || (lo == mylag && o < rw)) ? 1 : 0;
+      }
+      if (q == 0) {
+        sr[3 * E] = w; sr[3 * E + 1] = wm; sr[3 * E + 2] = wv;
+        from_s[rw] = from;
+        order[rank] = rw;
+      }
+      __builtin_amdgcn_s_waitcnt(0xc07f);           // lgkmcnt(0): this wave's LDS writes landed
+      __builtin_amdgcn_wave_barrier();
+      for (int k0 = 0; k0 < T; k0 += 64) {
+        const int k = k0 + (((k0 >> 6) & 1) ? 63 - lane : lane);
+        if (k < T) {
+          const int r = order[k / nch], e = k % nch;
+          float* sr2 = st + r * PITCH;
+          const int f = from_s[r];
+          if (e < E) {
+            float pe = sr2[e], me = sr2[E + e], ve = sr2[2 * E + e];
+            float d0 = 0.f, d1 = 0.f, d2 = 0.f;
+            catch_up1(pe, me, ve, d0, d1, d2, false, f, target, ring, c);
+            sr2[e] = pe; sr2[E + e] = me; sr2[2 * E + e] = ve;
+          } else {
+            float pe = sr2[3 * E], me = sr2[3 * E + 1], ve = sr2[3 * E + 2];
+            float d0 = 0.f, d1 = 0.f, d2 = 0.f;
+            catch_up1(pe, me, ve, d0, d1, d2, false, f, target, ring, c);
+            sr2[3 * E] = pe; sr2[3 * E + 1] = me; sr2[3 * E + 2] = ve;
+          }
+        }
+      }
+      __builtin_amdgcn_s_waitcnt(0xc07f);
+      __builtin_amdgcn_wave_barrier();
+      p = make_float4(sr[4 * q], sr[4 * q + 1], sr[4 * q + 2], sr[4 * q + 3]);
+      m = make_float4(sr[E + 4 * q], sr[E + 4 * q + 1], sr[E + 4 * q + 2], sr[E + 4 * q + 3]);
+      v = make_float4(sr[2 * E + 4 * q], sr[2 * E + 4 * q + 1], sr[2 * E + 4 * q + 2], sr[2 * E + 4 * q + 3]);
+      w = sr[3 * E]; wm = sr[3 * E + 1]; wv = sr[3 * E + 2];
+      __builtin_amdgcn_s_waitcnt(0xc07f);            // reads done before the next rows are staged
+      __builtin_amdgcn_wave_barrier();
+    }
+    if (!valid) continue;
     *reinterpret_cast<float4*>(out + i * E + 4 * q) = p;
     if (out1 && q == 0) out1[i] = w;
     if (mv) {   // caught-up moments for the backward's update: [m(E) | v(E) | m1 v1 0 0]
@@ -83,13 +155,13 @@ __global__ __launch_bounds__(256) void rec_gather_kernel(const float* __restrict
 // Lane d of an E-lane group owns dim d; lane 0 also owns the first-order triple and
 // the stamp (every lane reads the stamp before lane 0 rewrites it: same wave).
 __device__ __forceinline__ void rec_update(float* __restrict__ r, int E, int d, float g, float g1, int t,
-                                           float alpha_t, const float* __restrict__ hist, const RecCfg& c) {
+                                           float alpha_t, const RingW& ring, const RecCfg& c) {
   const int stamp = __float_as_int(r[E + 3]);
   float p = r[d], m = r[E + 4 + d], v = r[2 * E + 4 + d];
   const bool first = c.has_first && d == 0;
   float w = 0.f, wm = 0.f, wv = 0.f;
   if (first) { w = r[E]; wm = r[E + 1]; wv = r[E + 2]; }
-  if (stamp < t - 1) catch_up1(p, m, v, w, wm, wv, first, stamp, t - 1, hist, c);
+  if (stamp < t - 1) catch_up1(p, m, v, w, wm, wv, first, stamp, t - 1, ring, c);
   rec_adam(p, m, v, g, alpha_t, c);
   r[d] = p; r[E + 4 + d] = m; r[2 * E + 4 + d] = v;
   if (first) {
@@ -159,6 +231,8 @@ __global__ __launch_bounds__(256) void rec_bwd_adam_kernel(SegGradIn sg, float* 
                                                            const float* __restrict__ opt) {
   if (step_poisoned(opt)) return;   // the batch failed validation: no update (common.h)
   rec_load_hyper(c, opt);
+  __shared__ float hw[kHistWin];
+  const RingW ring = load_hist_window(hw, hist, (int)opt[7], c);
   constexpr int LPR = E / 4;
   const dl_emb_layout& L = sg.L;
   const long long gt = (long long)blockIdx.x * blockDim.x + threadIdx.x;
@@ -212,7 +286,7 @@ __global__ __launch_bounds__(256) void rec_bwd_adam_kernel(SegGradIn sg, float* 
       const float4 tail = *reinterpret_cast<const float4*>(r + E);
       w = tail.x; wm = tail.y; wv = tail.z;
       const int stamp = __float_as_int(tail.w);
-      if (stamp < t - 1) catch_up4(p, m, v, w, wm, wv, first, stamp, t - 1, hist, c);
+      if (stamp < t - 1) catch_up4(p, m, v, w, wm, wv, first, stamp, t - 1, ring, c);
     }
     const SegGrad4 s = segment_grad4_range<E>(sg, cr.e0, cr.e1, kc, q, nrefs, wsec);
     if (!row_ok) continue;
@@ -249,6 +323,8 @@ __global__ __launch_bounds__(256) void rec_apply_rows_kernel(float* __restrict__
                                                              float* __restrict__ g1, const float* __restrict__ hist,
                                                              const float* __restrict__ opt) {
   rec_load_hyper(c, opt);
+  __shared__ float hw[kHistWin];
+  const RingW ring = load_hist_window(hw, hist, (int)opt[7], c);
   const int E = c.E;
   const int t = (int)opt[7];
   const float alpha_t = opt[3];
@@ -259,7 +335,7 @@ __global__ __launch_bounds__(256) void rec_apply_rows_kernel(float* __restrict__
     const int d = (int)(k % E);
     const float gi = g[k];
     const float g1i = (g1 && d == 0) ? g1[i] : 0.f;
-    if (!skip) rec_update(rec + (row0 + i) * c.ld, E, d, gi, g1i, t, alpha_t, hist, c);
+    if (!skip) rec_update(rec + (row0 + i) * c.ld, E, d, gi, g1i, t, alpha_t, ring, c);
     g[k] = 0.f;
     if (g1 && d == 0) g1[i] = 0.f;
   }
@@ -271,6 +347,8 @@ __global__ __launch_bounds__(256) void rec_flush_kernel(float* __restrict__ rec,
                                                         const float* __restrict__ hist,
                                                         const float* __restrict__ opt) {
   rec_load_hyper(c, opt);
+  __shared__ float hw[kHistWin];
+  const RingW ring = load_hist_window(hw, hist, (int)opt[7], c);
   constexpr int LPR = E / 4;
   const long long gt = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   const int q = (int)(gt % LPR);
@@ -285,7 +363,7 @@ __global__ __launch_bounds__(256) void rec_flush_kernel(float* __restrict__ rec,
     float4 v = *reinterpret_cast<const float4*>(r + 2 * E + 4 + 4 * q);
     float w = tail.x, wm = tail.y, wv = tail.z;
     const bool first = c.has_first && q == 0;
-    catch_up4(p, m, v, w, wm, wv, first, stamp, target, hist, c);
+    catch_up4(p, m, v, w, wm, wv, first, stamp, target, ring, c);
     *reinterpret_cast<float4*>(r + 4 * q) = p;
     *reinterpret_cast<float4*>(r + E + 4 + 4 * q) = m;
     *reinterpret_cast<float4*>(r + 2 * E + 4 + 4 * q) = v;
@@ -309,6 +387,8 @@ __global__ __launch_bounds__(256) void rec_apply_segments_kernel(float* __restri
                                                                  const float* __restrict__ opt) {
   if (step_poisoned(opt)) return;
   rec_load_hyper(c, opt);
+  __shared__ float hw[kHistWin];
+  const RingW ring = load_hist_window(hw, hist, (int)opt[7], c);
   constexpr int LPR = E / 4;
   const long long gt = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   const int q = (int)(gt % LPR);
@@ -336,7 +416,7 @@ __global__ __launch_bounds__(256) void rec_apply_segments_kernel(float* __restri
       if (first) g1s += g1[k];
     }
     const int stamp = __float_as_int(tail.w);
-    if (stamp < t - 1) catch_up4(p, m, v, w, wm, wv, first, stamp, t - 1, hist, c);
+    if (stamp < t - 1) catch_up4(p, m, v, w, wm, wv, first, stamp, t - 1, ring, c);
     rec_adam(p.x, m.x, v.x, gs.x, alpha, c);
     rec_adam(p.y, m.y, v.y, gs.y, alpha, c);
     rec_adam(p.z, m.z, v.z, gs.z, alpha, c);
@@ -376,6 +456,8 @@ __global__ __launch_bounds__(256) void rec_apply_chain_kernel(float* __restrict_
                                                               const float* __restrict__ opt) {
   if (step_poisoned(opt)) return;
   rec_load_hyper(c, opt);
+  __shared__ float hw[kHistWin];
+  const RingW ring = load_hist_window(hw, hist, (int)opt[7], c);
   constexpr int LPR = E / 4;
   const long long gt = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   const int q = (int)(gt % LPR);
@@ -413,7 +495,7 @@ __global__ __launch_bounds__(256) void rec_apply_chain_kernel(float* __restrict_
       }
     }
     const int stamp = __float_as_int(tail.w);
-    if (stamp < t - 1) catch_up4(p, m, v, w, wm, wv, first, stamp, t - 1, hist, c);
+    if (stamp < t - 1) catch_up4(p, m, v, w, wm, wv, first, stamp, t - 1, ring, c);
     rec_adam(p.x, m.x, v.x, gs.x, alpha, c);
     rec_adam(p.y, m.y, v.y, gs.y, alpha, c);
     rec_adam(p.z, m.z, v.z, gs.z, alpha, c);

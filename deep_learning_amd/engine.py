@@ -206,7 +206,7 @@ class ModelSpec:
 
 class CTREngine:
     def __init__(self, spec, max_batch, device="cuda", seed=2019, init="device", bwd="atomic",
-                 table_rows=None, adam="dense", hist_len=4096, rec_stash=False, fwd_rec=False):
+                 table_rows=None, adam="dense", hist_len=4096, rec_stash=True, fwd_rec=False):
         if not torch.cuda.is_available():
             raise _lib.DLError("CTREngine needs a HIP device (no CPU fallback)")
         _lib.lib()
@@ -514,9 +514,24 @@ class CTREngine:
             P = {sp.table_key: self.table[:N].cpu().numpy()}
             if self.first is not None:
                 P[sp.first_key] = self.first[:N].cpu().numpy()[:, None]
+        P.update(self._export_dense(self.W, self.w_head, getattr(self, "ww", None), getattr(self, "wb", None)))
+        return P
+
+    def dense_state(self):
+        """Adam moments of the dense parameters (hidden layers, head / wdl weights) in the
+        reference layout: {"m": {key: array}, "v": {key: array}} (tests; the table's are in
+        adam_state())."""
+        return {"m": self._export_dense(self.Wm, self.hm, getattr(self, "wm", None), getattr(self, "wbm", None)),
+                "v": self._export_dense(self.Wv, self.hv, getattr(self, "wv", None), getattr(self, "wbv", None))}
+
+    def _export_dense(self, Ws, head, ww, wb):
+        """Augmented hidden-layer matrices (bias row, x0 column order), the permuted head
+        vector and the wdl weights -> reference keys and layouts."""
+        sp = self.spec
+        P = {}
         dims = [self.D0] + sp.hidden
         for l in range(len(sp.hidden)):
-            Wi = self.W[l].cpu().numpy()
+            Wi = Ws[l].cpu().numpy()
             W = Wi[: dims[l], : dims[l + 1]]
             if l == 0:
                 Wr = np.zeros_like(W)
@@ -525,10 +540,10 @@ class CTREngine:
             P["deep_%d" % l] = W.copy()
             P["deep_bias_%d" % l] = Wi[dims[l], : dims[l + 1]][None, :].copy()
         if self.wdl:
-            P["wdl_weights"] = self.ww[: self.w_rows].cpu().numpy()[:, None].copy()
-            P["wdl_bias"] = self.wb[:1].cpu().numpy().copy()
+            P["wdl_weights"] = ww[: self.w_rows].cpu().numpy()[:, None].copy()
+            P["wdl_bias"] = wb[:1].cpu().numpy().copy()
             return P
-        wi = self.w_head[: self.head_n].cpu().numpy()
+        wi = head[: self.head_n].cpu().numpy()
         w = np.empty_like(wi)
         w[sp.head_ref_index()] = wi
         if sp.fm:

@@ -246,6 +246,28 @@ int dl_gemm_bf16(int32_t ta, int32_t tb, int32_t M, int32_t N, int32_t K, const 
                  int32_t c_bf16, int32_t epi, const void* mask, int32_t ldm, int32_t splits,
                  int64_t c_split_stride, void* stream);
 
+/* fp32 tower products on the bf16 matrix cores, three-plane split (gemm_s3.hip):
+ * every f32 operand splits exactly into bf16 planes hi + mid + lo and a product takes the
+ * six significant plane products (hi.hi, hi.mid, mid.hi, mid.mid, hi.lo, lo.hi) in f32
+ * accumulation: f32 accuracy (dropped terms <= 2^-25 |a.b|) at up to 2.7x the f32 MFMA rate.
+ * Replaces dl_gemm_f32 for deepfm_pipeline.py:150-152 and its gradients.
+ *
+ * dl_split3: planes of src [rows][cols] (ld lds) at dst + q * plane_stride (q = 0 hi,
+ *   1 mid, 2 lo), [r][c] with ld ldd, or [c][r] when `transpose`.
+ * dl_gemm_s3_nt: C[M][N] = A[M][K] . B[N][K]^T (+ epilogue: 0 store, 1 ReLU, 2 mask
+ *   (C = mask[i][j] > 0 ? C : 0, mask f32 with ld ldm)); A f32 (lda % 4 == 0, 16-B
+ *   aligned), B as planes from dl_split3 (ldb % 8 == 0, plane stride b_plane); K % 8 == 0.
+ * dl_gemm_s3_tn: split-K weight gradient, slab z of C (at C + z * c_split_stride, ld ldc)
+ *   = sum over k in split z of X[k][m] Y[k][n]; X [K][lda], Y [K][ldb] f32, N <= 416;
+ *   splits of ceil(K / splits) rounded up to 64 rows (ceil(K / that) slabs). */
+int dl_split3(const float* src, int32_t rows, int32_t cols, int32_t lds, int32_t transpose, uint16_t* dst,
+              int32_t ldd, int64_t plane_stride, void* stream);
+int dl_gemm_s3_nt(int32_t M, int32_t N, int32_t K, const float* A, int32_t lda, const uint16_t* B,
+                  int32_t ldb, int64_t b_plane, float* C, int32_t ldc, int32_t epi, const float* mask,
+                  int32_t ldm, void* stream);
+int dl_gemm_s3_tn(int32_t M, int32_t N, int32_t K, const float* X, int32_t lda, const float* Y, int32_t ldb,
+                  float* C, int32_t ldc, int32_t splits, int64_t c_split_stride, void* stream);
+
 /* ------------------------------------------------------------------------
  * Output layer + sigmoid + eps-log-loss, forward and backward fused
  * (deepfm_pipeline.py:157-183, dnn_pipeline.py:119-131):

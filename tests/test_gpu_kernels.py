@@ -292,7 +292,7 @@ def test_chain_apply_equals_sorted_segment_apply(hip_lib):
     gr = torch.randn(n, E, generator=g)
     g1 = torch.randn(n, generator=g)
     hist = torch.rand(hist_len, generator=g) * 1e-3
-    opt = torch.zeros(16)
+    opt = torch.zeros(32)   # DL_OPT_LEN: Adam scalars, sums, status word
     opt[3], opt[4], opt[5], opt[6], opt[7] = 1e-3, 0.9, 0.999, 1e-8, 10   # alpha, b1, b2, eps, step
     ids_d, gr_d, g1_d, hist_d, opt_d = ids.cuda(), gr.cuda(), g1.cuda(), hist.cuda(), opt.cuda()
     # sort + segments

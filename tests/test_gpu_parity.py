@@ -151,7 +151,7 @@ def test_record_forward_bit_identical_to_gather(hip_lib, name):
     bit-identical (8-entry alpha ring: lagging rows and flushes included)."""
     kw = dict(CASES[name], cate_index_size=50000)
     spec = ModelSpec(_model(name), **kw)
-    a = CTREngine(spec, max_batch=128, seed=3, adam="lazy", hist_len=8, fwd_rec=True)
+    a = CTREngine(spec, max_batch=128, seed=3, adam="lazy", hist_len=8, fwd_rec=True, rec_stash=False)
     b = CTREngine(spec, max_batch=128, seed=3, adam="lazy", hist_len=8, fwd_rec=False)
     assert a.fwd_rec and not b.fwd_rec
     bs = _batches(name, kw, 128, 15, seed=11)

@@ -218,3 +218,23 @@ def test_auc_matches_sklearn():
     s2 = rng.random(777)
     y2 = (rng.random(777) < s2).astype(np.float32)
     assert abs(R.auc(y2, s2) - roc_auc_score(y2, s2)) < 1e-12
+
+
+def test_torch_cpu_restatement_matches_numpy_oracle():
+    """bench.py's cpu_baseline times oracle/torch_cpu.py: it must compute what the numpy
+    oracle computes (same deepfm_pipeline graph, dense TF1 Adam) — 3 steps, logits, loss
+    and every parameter."""
+    from oracle.torch_cpu import DeepFMPipelineCPU
+    kw = dict(C=13, V=0, S=26, E=16, cate_index_size=3000, hidden=[48, 32])
+    cfg = R.make_cfg("deepfm_pipeline", **kw)
+    P = R.init_params(cfg, np.random.default_rng(3))
+    m = DeepFMPipelineCPU(13, 26, 16, 3000, [48, 32], P)
+    opt = R.AdamTF1(cfg, P)
+    for i in range(3):
+        b = make_batch(256, cate_index_size=3000, seed=50 + i)
+        fw = R.train_step(cfg, P, opt, b)
+        z, loss = m.train_step(b)
+        np.testing.assert_allclose(z.numpy(), fw["z"], atol=1e-5, rtol=0)
+        assert abs(loss - fw["loss"]) < 1e-5
+    for k in P:
+        np.testing.assert_allclose(m.params[k].detach().numpy(), P[k], atol=1e-5, rtol=0, err_msg=k)
