@@ -95,65 +95,72 @@ enum { S3_STORE = 0, S3_RELU = 1, S3_MASK = 2 };
 #endif
 
 // ---------------------------------------------------------------------------- NT
-constexpr int kNtBM = 256, kNtBN = 208, kNtNF = 13, kNtKP = 40;   // LDS row pitch 40 bf16 = 80 B
-constexpr int kNtPlane = kNtBN * kNtKP;                          // elements of one plane image
+// B chunk images: per plane 208 rows x 32 k (64 B), 16-B piece kq of row j at slot
+// kq ^ ((j >> 2) & 2): conflict-free fragment reads for ds_read_b128's four lane groups
+// ({0-3,12-15,20-27}, {4-11,16-19,28-31}, ... MI355X_MICROARCH.md §LDS; found by exhaustive
+// search over per-row slot permutations), filled by LDS-DMA
+// (global_load_lds_dwordx4: one instruction = 16 rows) two chunks ahead into a ring of three
+// buffers, so no chunk waits a full memory round trip for its weights.
+constexpr int kNtBM = 256, kNtBN = 208, kNtNF = 13;
+constexpr int kNtPlane = kNtBN * 32;                             // bf16 elements of one plane image
 constexpr int kNtBuf = 3 * kNtPlane;
-constexpr int kNtQB = 3 * kNtBN * 4;                             // 16-B pieces of a B chunk
-constexpr int kNtQPT = (kNtQB + 511) / 512;
-constexpr size_t kNtLds = 2 * kNtBuf * sizeof(unsigned short);
+constexpr int kNtDma = 3 * kNtBN / 16;                           // DMA instructions per chunk (39)
+constexpr size_t kNtLds = 3 * kNtBuf * sizeof(unsigned short);  // 119,808 B
+constexpr int kNtEP = kNtBN + 4;                                 // epilogue tile pitch (floats)
+static_assert(8 * 16 * kNtEP * sizeof(float) <= kNtLds, "epilogue tiles fit the ring");
+
+__device__ __forceinline__ int nt_slot(int j, int kq) { return kq ^ ((j >> 2) & 2); }   // an involution in kq
+
+// s_waitcnt vmcnt(n) (n < 64), other counters untouched
+#define DL_WAIT_VMCNT(n) __builtin_amdgcn_s_waitcnt(((n) & 0xF) | (((n) >> 4) << 14) | (0x7 << 4) | (0xF << 8))
 
 template <int EPI>
 __global__ __launch_bounds__(512) void gemm_s3_nt_kernel(S3Params p) {
-  extern __shared__ __attribute__((aligned(16))) unsigned short lds[];   // [2][3][BN][KP]
+  extern __shared__ __attribute__((aligned(16))) unsigned short lds[];   // [3 bufs][3 planes][BN][32]
   const unsigned short* __restrict__ Bp = reinterpret_cast<const unsigned short*>(p.B);
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int ntm = (p.M + kNtBM - 1) / kNtBM, ntn = (p.N + kNtBN - 1) / kNtBN;
   const int t = s3_xcd_tile(blockIdx.x, ntm * ntn);
   const int i0 = (t / ntn) * kNtBM, j0 = (t % ntn) * kNtBN;
   const int cl = lane & 15, kq = lane >> 4;
   const int r0 = i0 + wid * 32;
   const bool ok0 = r0 + cl < p.M, ok1 = r0 + 16 + cl < p.M;
-  const float* a0 = p.A + (long long)min(r0 + cl, p.M - 1) * p.lda + 8 * kq;
-  const float* a1 = p.A + (long long)min(r0 + 16 + cl, p.M - 1) * p.lda + 8 * kq;
+  // rows as float4 arrays (16-B aligned: A is, and lda % 4 == 0); loads are unconditional from
+  // clamped addresses, and out-of-range pieces are zeroed afterwards (no exec-masked loads)
+  const float4* a0 = reinterpret_cast<const float4*>(p.A + (long long)min(r0 + cl, p.M - 1) * p.lda);
+  const float4* a1 = reinterpret_cast<const float4*>(p.A + (long long)min(r0 + 16 + cl, p.M - 1) * p.lda);
   const int KC = (p.K + 31) / 32;
   const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
-  const uint4 zu = make_uint4(0u, 0u, 0u, 0u);
   const int nf_live = min(kNtNF, (p.N - j0 + 15) / 16);   // column fragments inside N (wave-uniform)
 
-  uint4 rb[kNtQPT];
-  auto load_b = [&](int c) {
+  // LDS-DMA of chunk c into buffer `buf`: instruction g (g = wid, wid + 8, ...) fills plane
+  // g / 13, rows 16 (g % 13) .. +16; lane L writes slot L & 3 of row L >> 2 and so fetches
+  // the piece that belongs there.  Rows past N / k past K read clamped in-range data (their
+  // products are discarded / multiplied by A's zeros).
+  auto dma_b = [&](int c, int buf) {
 #pragma unroll
-    for (int u = 0; u < kNtQPT; ++u) {
-      const int q = tid + u * 512;
-      uint4 v = zu;
-      if (q < kNtQB) {
-        const int pl = q / (kNtBN * 4), rem = q % (kNtBN * 4);
-        const int j = rem >> 2, c4 = rem & 3;
-        const int gj = j0 + j, gk = 32 * c + 8 * c4;
-        if (gj < p.N && gk < p.K)
-          v = *reinterpret_cast<const uint4*>(Bp + pl * p.b_plane + (long long)gj * p.ldb + gk);
-      }
-      rb[u] = v;
-    }
-  };
-  auto store_b = [&](int buf) {
-#pragma unroll
-    for (int u = 0; u < kNtQPT; ++u) {
-      const int q = tid + u * 512;
-      if (q < kNtQB) {
-        const int pl = q / (kNtBN * 4), rem = q % (kNtBN * 4);
-        const int j = rem >> 2, c4 = rem & 3;
-        *reinterpret_cast<uint4*>(&lds[buf * kNtBuf + pl * kNtPlane + j * kNtKP + 8 * c4]) = rb[u];
-      }
+    for (int g = wid; g < kNtDma; g += 8) {
+      const int pl = g / 13, rb = 16 * (g % 13);
+      const int j = rb + (lane >> 2);
+      const int kpc = nt_slot(j, lane & 3);        // the piece that belongs in slot lane & 3
+      const int gj = min(j0 + j, p.N - 1);
+      const int gk = min(32 * c + 8 * kpc, p.K - 8);
+      const unsigned short* src = Bp + pl * p.b_plane + (long long)gj * p.ldb + gk;
+      __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)&lds[buf * kNtBuf + pl * kNtPlane + rb * 32],
+                                       16, 0, 0);
     }
   };
   // A: this lane's 8 floats of rows r0 + cl, r0 + 16 + cl at k = 32c + 8kq
   auto load_a = [&](int c, float4 (&ra)[4]) {
-    const bool kin = 32 * c + 8 * kq < p.K;
-    ra[0] = (ok0 && kin) ? *reinterpret_cast<const float4*>(a0 + 32 * c) : z4;
-    ra[1] = (ok0 && kin) ? *reinterpret_cast<const float4*>(a0 + 32 * c + 4) : z4;
-    ra[2] = (ok1 && kin) ? *reinterpret_cast<const float4*>(a1 + 32 * c) : z4;
-    ra[3] = (ok1 && kin) ? *reinterpret_cast<const float4*>(a1 + 32 * c + 4) : z4;
+    const int k = 32 * c + 8 * kq;
+    const int kc = min(k, p.K - 8) >> 2;
+    ra[0] = a0[kc];
+    ra[1] = a0[kc + 1];
+    ra[2] = a1[kc];
+    ra[3] = a1[kc + 1];
+    const bool kin = k < p.K;
+    if (!(ok0 && kin)) { ra[0] = z4; ra[1] = z4; }
+    if (!(ok1 && kin)) { ra[2] = z4; ra[3] = z4; }
   };
 
   floatx4 acc[2][kNtNF];
@@ -163,25 +170,28 @@ __global__ __launch_bounds__(512) void gemm_s3_nt_kernel(S3Params p) {
     for (int f = 0; f < kNtNF; ++f) acc[a][f] = floatx4{0.f, 0.f, 0.f, 0.f};
 
   float4 raA[4], raB[4];
-  load_b(0);
-  store_b(0);
+  // prologue: B chunks 0 and 1 in flight, A chunks 0 and 1
+  dma_b(0, 0);
   load_a(0, raA);
+  if (KC > 1) dma_b(1, 1);
   if (KC > 1) load_a(1, raB);
+  // chunk 0's B must have landed (the <= 4 + 5 + 4 younger ops may stay in flight)
+  if (KC > 1) DL_WAIT_VMCNT(8); else DL_WAIT_VMCNT(0);
   __syncthreads();
 
   auto step = [&](int c, float4 (&ra)[4]) {
     shortx8 ah[2], am[2], al[2];
     split8(ra[0], ra[1], ah[0], am[0], al[0]);
     split8(ra[2], ra[3], ah[1], am[1], al[1]);
-    // B of the next chunk first, then A two chunks ahead: store_b at the end of this step
-    // waits only for the B loads (vmcnt leaves the younger A loads in flight)
-    if (c + 1 < KC) load_b(c + 1);
-    if (c + 2 < KC) load_a(c + 2, ra);          // the registers are free again
-    const unsigned short* Bs = lds + (c & 1) * kNtBuf;
+    // chunk c + 2: B into the buffer chunk c - 1 used (free since the last barrier), then A
+    if (c + 2 < KC) dma_b(c + 2, (c + 2) % 3);
+    if (c + 2 < KC) load_a(c + 2, ra);
+    const unsigned short* Bs = lds + (c % 3) * kNtBuf;
 #pragma unroll
     for (int f = 0; f < kNtNF; ++f) {
       if (f < nf_live) {
-        const int o = (16 * f + cl) * kNtKP + 8 * kq;
+        const int j = 16 * f + cl;
+        const int o = j * 32 + 8 * nt_slot(j, kq);
         const shortx8 bh = *reinterpret_cast<const shortx8*>(&Bs[o]);
         const shortx8 bm = *reinterpret_cast<const shortx8*>(&Bs[kNtPlane + o]);
         const shortx8 bl = *reinterpret_cast<const shortx8*>(&Bs[2 * kNtPlane + o]);
@@ -194,7 +204,9 @@ __global__ __launch_bounds__(512) void gemm_s3_nt_kernel(S3Params p) {
         }
       }
     }
-    if (c + 1 < KC) store_b((c + 1) & 1);
+    // chunk c + 1's B must have landed before the barrier publishes it: outstanding younger
+    // ops are at most chunk c + 2's (<= 5 DMA + 4 A loads); waiting to 8 is conservative
+    if (c + 2 < KC) DL_WAIT_VMCNT(8); else DL_WAIT_VMCNT(0);
     __syncthreads();
   };
   for (int c = 0; c < KC; c += 2) {
@@ -202,32 +214,57 @@ __global__ __launch_bounds__(512) void gemm_s3_nt_kernel(S3Params p) {
     if (c + 1 < KC) step(c + 1, raB);
   }
 
-  const float* __restrict__ Mk = p.mask;
   if (DL_S3_DIAG) {   // keep the loop's results live without storing them
-    float t = 0.f;
+    float tt = 0.f;
 #pragma unroll
     for (int a = 0; a < 2; ++a)
 #pragma unroll
-      for (int f = 0; f < kNtNF; ++f) t += acc[a][f][0] + acc[a][f][3];
-    if (t == 12345.f) p.C[0] = t;
+      for (int f = 0; f < kNtNF; ++f) tt += acc[a][f][0] + acc[a][f][3];
+    if (tt == 12345.f) p.C[0] = tt;
     return;
   }
+  // Epilogue through LDS (the ring is free after the last barrier): per wave and per half
+  // (rows 16h .. 16h+15 of its 32), the 16 x 208 tile is written from the MFMA layout, then
+  // each lane moves whole 16-B row pieces: ReLU / mask reads and stores as full row segments.
+  float* tile = reinterpret_cast<float*>(lds) + wid * 16 * kNtEP;
+  const float* __restrict__ Mk = p.mask;
 #pragma unroll
-  for (int a = 0; a < 2; ++a)
+  for (int h = 0; h < 2; ++h) {
 #pragma unroll
-    for (int f = 0; f < kNtNF; ++f) {
-      const int col = j0 + 16 * f + cl;
+    for (int f = 0; f < kNtNF; ++f)
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int row = r0 + 16 * a + 4 * kq + j;
-        if (row < p.M && col < p.N) {
-          float v = acc[a][f][j];
-          if (EPI == S3_RELU) v = fmaxf(v, 0.f);
-          if (EPI == S3_MASK) v = Mk[(long long)row * p.ldm + col] > 0.f ? v : 0.f;
-          p.C[(long long)row * p.ldc + col] = v;
+      for (int j = 0; j < 4; ++j) tile[(4 * kq + j) * kNtEP + 16 * f + cl] = acc[h][f][j];
+    __builtin_amdgcn_s_waitcnt(0xc07f);             // lgkmcnt(0): this wave's tile writes landed
+    __builtin_amdgcn_wave_barrier();
+    constexpr int VPR = kNtBN / 4;                  // 52 float4 pieces per row
+    for (int q = lane; q < 16 * VPR; q += 64) {
+      const int rl = q / VPR, pc = q % VPR;
+      const int row = r0 + 16 * h + rl, col = j0 + 4 * pc;
+      if (row >= p.M || col >= p.N) continue;
+      float4 v = *reinterpret_cast<const float4*>(tile + rl * kNtEP + 4 * pc);
+      if (EPI == S3_RELU) {
+        v.x = fmaxf(v.x, 0.f); v.y = fmaxf(v.y, 0.f); v.z = fmaxf(v.z, 0.f); v.w = fmaxf(v.w, 0.f);
+      }
+      float* dst = p.C + (long long)row * p.ldc + col;
+      const float* mk = Mk + (long long)row * p.ldm + col;
+      if (col + 4 <= p.N && ((reinterpret_cast<uintptr_t>(dst) | reinterpret_cast<uintptr_t>(mk)) & 15) == 0) {
+        if (EPI == S3_MASK) {
+          const float4 m4 = *reinterpret_cast<const float4*>(mk);
+          v.x = m4.x > 0.f ? v.x : 0.f; v.y = m4.y > 0.f ? v.y : 0.f;
+          v.z = m4.z > 0.f ? v.z : 0.f; v.w = m4.w > 0.f ? v.w : 0.f;
+        }
+        *reinterpret_cast<float4*>(dst) = v;
+      } else {
+        const float e4[4] = {v.x, v.y, v.z, v.w};
+        for (int e = 0; e < 4 && col + e < p.N; ++e) {
+          float x = e4[e];
+          if (EPI == S3_MASK) x = mk[e] > 0.f ? x : 0.f;
+          dst[e] = x;
         }
       }
     }
+    __builtin_amdgcn_wave_barrier();
+  }
 }
 
 // ---------------------------------------------------------------------------- TN
@@ -243,6 +280,7 @@ constexpr int kTnAE = kTnKS * kTnPA, kTnBE = kTnKS * kTnPB;          // elements
 constexpr int kTnQA = kTnKS * kTnBM / 4, kTnQB = kTnKS * kTnBN / 4;  // float4 pieces per step
 constexpr int kTnQ = (kTnQA + kTnQB + 511) / 512;
 constexpr size_t kTnLds = 3 * (kTnAE + kTnBE) * sizeof(unsigned short);
+static_assert(kTnQA == 2 * 512 && kTnQB == 6 * 512 + 256 && kTnQ == 9, "the TN piece mapping below");
 
 __device__ __forceinline__ uint2 s3_lds_tr16(const unsigned short* ptr_) {
   auto lp = (__attribute__((address_space(3))) unsigned short*)(const_cast<unsigned short*>(ptr_));
@@ -263,7 +301,7 @@ __global__ __launch_bounds__(512) void gemm_s3_tn_kernel(S3Params p) {
   unsigned short* Bs = lds + 3 * kTnAE;
   const float* __restrict__ X = p.A;
   const float* __restrict__ Y = reinterpret_cast<const float*>(p.B);
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int mtiles = (p.M + kTnBM - 1) / kTnBM;
   const int t = s3_xcd_tile(blockIdx.x, gridDim.x);
   const int m0 = (t % mtiles) * kTnBM, z = t / mtiles;
@@ -271,40 +309,51 @@ __global__ __launch_bounds__(512) void gemm_s3_tn_kernel(S3Params p) {
   const int kend = min(p.K, kbeg + p.k_per_split);
   const int nk = (kend - kbeg + kTnKS - 1) / kTnKS;
   const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
+  // Pieces of a step: 1024 A pieces (32 rows x 32 float4 of X) are u = 0, 1; then 3328 B pieces
+  // (32 rows x 104 float4 of Y) are u = 2..8 (u = 8: threads < 256 only).  Each thread's pieces
+  // sit at fixed offsets: loads go unconditionally to clamped addresses and out-of-range
+  // pieces are zeroed afterwards (no exec-masked loads).
   float4 rs[kTnQ];
+  const int qa_r0 = tid >> 5, qa_c = 4 * (tid & 31);                 // u = 0: row qa_r0, u = 1: row qa_r0 + 16
+  const bool qa_ok = m0 + qa_c < p.M;
+  const float* xa = X + min(m0 + qa_c, p.M - 4);
+  int qb_r[7], qb_c[7];
+  bool qb_ok[7];
+#pragma unroll
+  for (int u = 0; u < 7; ++u) {
+    const int qq = tid + 512 * u;
+    qb_r[u] = qq / 104;
+    qb_c[u] = 4 * (qq % 104);
+    qb_ok[u] = qb_c[u] < p.N && (u < 6 || tid < 256);
+  }
   auto load = [&](int k0) {
 #pragma unroll
-    for (int u = 0; u < kTnQ; ++u) {
-      const int q = tid + u * 512;
-      float4 v = z4;
-      if (q < kTnQA) {
-        const int r = q / (kTnBM / 4), c4 = q % (kTnBM / 4);
-        const int gk = k0 + r, gm = m0 + 4 * c4;
-        if (gk < kend && gm < p.M) v = *reinterpret_cast<const float4*>(X + (long long)gk * p.lda + gm);
-      } else if (q < kTnQA + kTnQB) {
-        const int qq = q - kTnQA, r = qq / (kTnBN / 4), c4 = qq % (kTnBN / 4);
-        const int gk = k0 + r, gn = 4 * c4;
-        if (gk < kend && gn < p.N) v = *reinterpret_cast<const float4*>(Y + (long long)gk * p.ldb + gn);
-      }
-      rs[u] = v;
+    for (int u = 0; u < 2; ++u) {
+      const int gk = k0 + qa_r0 + 16 * u;
+      const float4 v = *reinterpret_cast<const float4*>(xa + (long long)min(gk, kend - 1) * p.lda);
+      rs[u] = (qa_ok && gk < kend) ? v : z4;
+    }
+#pragma unroll
+    for (int u = 0; u < 7; ++u) {
+      const int gk = k0 + min(qb_r[u], kTnKS - 1);
+      const float4 v = *reinterpret_cast<const float4*>(Y + (long long)min(gk, kend - 1) * p.ldb +
+                                                          min(qb_c[u], p.N - 4));
+      rs[2 + u] = (qb_ok[u] && gk < kend) ? v : z4;
     }
   };
   auto store = [&]() {
 #pragma unroll
     for (int u = 0; u < kTnQ; ++u) {
-      const int q = tid + u * 512;
       uint32_t h0, m0_, l0, h1, m1_, l1;
       split2(rs[u].x, rs[u].y, h0, m0_, l0);
       split2(rs[u].z, rs[u].w, h1, m1_, l1);
-      if (q < kTnQA) {
-        const int r = q / (kTnBM / 4), c4 = q % (kTnBM / 4);
-        const int o = r * kTnPA + 4 * c4;
+      if (u < 2) {
+        const int o = (qa_r0 + 16 * u) * kTnPA + qa_c;
         *reinterpret_cast<uint2*>(&As[o]) = make_uint2(h0, h1);
         *reinterpret_cast<uint2*>(&As[kTnAE + o]) = make_uint2(m0_, m1_);
         *reinterpret_cast<uint2*>(&As[2 * kTnAE + o]) = make_uint2(l0, l1);
-      } else if (q < kTnQA + kTnQB) {
-        const int qq = q - kTnQA, r = qq / (kTnBN / 4), c4 = qq % (kTnBN / 4);
-        const int o = r * kTnPB + 4 * c4;
+      } else if (u < 8 || tid < 256) {
+        const int o = qb_r[u - 2] * kTnPB + qb_c[u - 2];
         *reinterpret_cast<uint2*>(&Bs[o]) = make_uint2(h0, h1);
         *reinterpret_cast<uint2*>(&Bs[kTnBE + o]) = make_uint2(m0_, m1_);
         *reinterpret_cast<uint2*>(&Bs[2 * kTnBE + o]) = make_uint2(l0, l1);
@@ -411,7 +460,7 @@ extern "C" int dl_gemm_s3_nt(int32_t M, int32_t N, int32_t K, const float* A, in
                              int32_t ldm, void* stream) {
   DL_CHECK_ARG(M >= 0 && N >= 0 && K >= 0, "negative dims");
   DL_CHECK_ARG(A && Bp && C, "NULL operand");
-  DL_CHECK_ARG(K % 8 == 0, "K %d must be a multiple of 8", K);
+  DL_CHECK_ARG(K % 8 == 0 && K >= 8, "K %d must be a positive multiple of 8", K);
   DL_CHECK_ARG(lda % 4 == 0 && lda >= K && ldb % 8 == 0 && ldb >= K && ldc >= N, "bad leading dims");
   DL_CHECK_ARG(((uintptr_t)A % 16) == 0 && ((uintptr_t)Bp % 16) == 0 && b_plane % 8 == 0,
                "A / B planes must be 16-byte aligned");
@@ -436,6 +485,7 @@ extern "C" int dl_gemm_s3_tn(int32_t M, int32_t N, int32_t K, const float* X, in
   DL_CHECK_ARG(M >= 0 && N >= 0 && K >= 0, "negative dims");
   DL_CHECK_ARG(X && Y && C, "NULL operand");
   DL_CHECK_ARG(N <= kTnBN, "N %d > %d", N, kTnBN);
+  DL_CHECK_ARG(M % 4 == 0 && N % 4 == 0 && (M == 0 || M >= 4) && (N == 0 || N >= 4), "M, N must be multiples of 4");
   DL_CHECK_ARG(lda % 4 == 0 && ldb % 4 == 0 && lda >= (M + 3) / 4 * 4 && ldb >= (N + 3) / 4 * 4 && ldc >= N,
                "bad leading dims");
   DL_CHECK_ARG(((uintptr_t)X % 16) == 0 && ((uintptr_t)Y % 16) == 0, "X / Y must be 16-byte aligned");

@@ -206,7 +206,7 @@ class ModelSpec:
 
 class CTREngine:
     def __init__(self, spec, max_batch, device="cuda", seed=2019, init="device", bwd="atomic",
-                 table_rows=None, adam="dense", hist_len=4096, rec_stash=True, fwd_rec=False):
+                 table_rows=None, adam="dense", hist_len=4096, rec_stash=True, fwd_rec=False, gemm="s3"):
         if not torch.cuda.is_available():
             raise _lib.DLError("CTREngine needs a HIP device (no CPU fallback)")
         _lib.lib()
@@ -265,6 +265,16 @@ class CTREngine:
         self.Wm = [torch.zeros_like(w) for w in self.W]
         self.Wv = [torch.zeros_like(w) for w in self.W]
         self.Wt = z(max(o * i for o, i in zip(self.out_ld, self.in_ld)))   # W_l^T scratch for dX
+        # fp32 tower products on the bf16 matrix cores through the exact three-plane split
+        # (gemm_s3.hip, f32 accuracy): bf16 planes of W (the dX operand, [in][out]) and of W^T
+        # (the forward operand, [out][in]), refreshed after every update of W
+        if gemm not in ("s3", "f32"):
+            raise ValueError("gemm must be 's3' or 'f32'")
+        self.s3 = gemm == "s3" and sp.tower == "f32"
+        if self.s3:
+            zp = lambda n: torch.zeros(n, dtype=torch.int16, device=dev)
+            self.Wp = [zp(3 * self.in_ld[l] * self.out_ld[l]) for l in range(len(sp.hidden))]
+            self.WTp = [zp(3 * self.out_ld[l] * self.in_ld[l]) for l in range(len(sp.hidden))]
         H = sp.hidden[-1]
         self.head_n = sp.fm_cols + H + 1
         self.w_head = z(_ru(self.head_n, 4))
@@ -459,7 +469,13 @@ class CTREngine:
         self._refresh_wb(l)
 
     def _refresh_wb(self, l, s=None):
-        """bf16 tower: the bf16 operand copy of the fp32 master weights W_l."""
+        """The tower's operand copies of the fp32 master weights W_l: bf16 tower, bf16 W and
+        W^T; split (s3) GEMMs, the three bf16 planes of W and of W^T."""
+        if getattr(self, "s3", False):
+            s = s if s is not None else _lib.stream_handle()
+            i, o = self.in_ld[l], self.out_ld[l]
+            call("dl_split3", ptr(self.W[l]), i, o, o, 0, ptr(self.Wp[l]), o, i * o, s)
+            call("dl_split3", ptr(self.W[l]), i, o, o, 1, ptr(self.WTp[l]), i, i * o, s)
         if self.bf:
             s = s if s is not None else _lib.stream_handle()
             call("dl_cast_bf16", ptr(self.W[l]), self.in_ld[l], self.out_ld[l], self.out_ld[l], ptr(self.Wb[l]),
@@ -694,6 +710,13 @@ class CTREngine:
                         0, s)
                 if not last:
                     xb = self.hb[l]
+        elif self.s3:
+            x = self.x0
+            for l, hdim in enumerate(sp.hidden):
+                self._c("gemm_fwd_l%d" % l, "dl_gemm_s3_nt", B, hdim, self.in_ld[l], ptr(x), self.in_ld[l],
+                        ptr(self.WTp[l]), self.in_ld[l], self.in_ld[l] * self.out_ld[l], ptr(self.h[l]),
+                        self.h_ld[l], 1, None, 0, s)
+                x = self.h[l]
         else:
             x = self.x0
             for l, hdim in enumerate(sp.hidden):
@@ -754,7 +777,7 @@ class CTREngine:
         for l in reversed(range(nl)):
             hdim = sp.hidden[l]
             stride = self.in_ld[l] * self.out_ld[l]
-            nsplit = _num_splits(B, splits, 64 if self.bf else 16)
+            nsplit = _num_splits(B, splits, 64 if (self.bf or self.s3) else 16)
             if self.bf:
                 # dW = X^T dY straight from the batch-major bf16 activations and gradients
                 # (transposing LDS reads inside the kernel: no X^T / dY^T copies)
@@ -770,6 +793,19 @@ class CTREngine:
                     self._c("gemm_dx_l0", "dl_gemm_bf16", 0, 1, B, self.dx_cols, self.out_ld[0], ptr(self.dhb[0]),
                             self.h_ld[0], ptr(self.Wb[0]), self.out_ld[0], ptr(self.dx0), self.dx_ld, 0, 0, None, 0,
                             1, 0, s)
+            elif self.s3:
+                # dW = X^T dY (split-K slabs over the batch), dX = dY W^T with ReluGrad
+                xin = self.x0 if l == 0 else self.h[l - 1]
+                i, o = self.in_ld[l], self.out_ld[l]
+                self._c("gemm_dw_l%d" % l, "dl_gemm_s3_tn", i, hdim, B, ptr(xin), i, ptr(self.dh[l]), self.h_ld[l],
+                        ptr(self.w_slab), o, splits, stride, s)
+                if l > 0:
+                    self._c("gemm_dx_l%d" % l, "dl_gemm_s3_nt", B, sp.hidden[l - 1], o, ptr(self.dh[l]),
+                            self.h_ld[l], ptr(self.Wp[l]), o, i * o, ptr(self.dh[l - 1]), self.h_ld[l - 1], 2,
+                            ptr(self.h[l - 1]), self.h_ld[l - 1], s)
+                else:
+                    self._c("gemm_dx_l0", "dl_gemm_s3_nt", B, self.dx_cols, o, ptr(self.dh[0]), self.h_ld[0],
+                            ptr(self.Wp[0]), o, i * o, ptr(self.dx0), self.dx_ld, 0, None, 0, s)
             else:
                 xin = self.x0 if l == 0 else self.h[l - 1]
                 self._c("gemm_dw_l%d" % l, "dl_gemm_f32", 1, 0, self.in_ld[l], hdim, B, ptr(xin), self.in_ld[l],

@@ -358,8 +358,13 @@ class ShardedCTREngine(CTREngine):
                 ptr(self.fm_sum), s)
         x = self.x0
         for l, hdim in enumerate(sp.hidden):
-            self._c("gemm_fwd_l%d" % l, "dl_gemm_f32", 0, 0, B, hdim, self.in_ld[l], ptr(x), self.in_ld[l],
-                    ptr(self.W[l]), self.out_ld[l], ptr(self.h[l]), self.h_ld[l], 1, None, 0, 1, 0, s)
+            if self.s3:
+                self._c("gemm_fwd_l%d" % l, "dl_gemm_s3_nt", B, hdim, self.in_ld[l], ptr(x), self.in_ld[l],
+                        ptr(self.WTp[l]), self.in_ld[l], self.in_ld[l] * self.out_ld[l], ptr(self.h[l]),
+                        self.h_ld[l], 1, None, 0, s)
+            else:
+                self._c("gemm_fwd_l%d" % l, "dl_gemm_f32", 0, 0, B, hdim, self.in_ld[l], ptr(x), self.in_ld[l],
+                        ptr(self.W[l]), self.out_ld[l], ptr(self.h[l]), self.h_ld[l], 1, None, 0, 1, 0, s)
             x = self.h[l]
         H = sp.hidden[-1]
         inv_b = 1.0 / (B * W)
@@ -369,6 +374,16 @@ class ShardedCTREngine(CTREngine):
         # 6a. input gradients, top layer down
         nl = len(sp.hidden)
         for l in reversed(range(nl)):
+            if self.s3:
+                i, o = self.in_ld[l], self.out_ld[l]
+                if l > 0:
+                    self._c("gemm_dx_l%d" % l, "dl_gemm_s3_nt", B, sp.hidden[l - 1], o, ptr(self.dh[l]),
+                            self.h_ld[l], ptr(self.Wp[l]), o, i * o, ptr(self.dh[l - 1]), self.h_ld[l - 1], 2,
+                            ptr(self.h[l - 1]), self.h_ld[l - 1], s)
+                else:
+                    self._c("gemm_dx_l0", "dl_gemm_s3_nt", B, self.dx_cols, o, ptr(self.dh[0]), self.h_ld[0],
+                            ptr(self.Wp[0]), o, i * o, ptr(self.dx0), self.dx_ld, 0, None, 0, s)
+                continue
             self._c("transpose_l%d" % l, "dl_transpose_f32", ptr(self.W[l]), self.in_ld[l], self.out_ld[l],
                     self.out_ld[l], ptr(self.Wt), self.in_ld[l], s)
             if l > 0:
@@ -394,9 +409,14 @@ class ShardedCTREngine(CTREngine):
             xin = self.x0 if l == 0 else self.h[l - 1]
             hdim = sp.hidden[l]
             stride = self.in_ld[l] * self.out_ld[l]
-            self._c("gemm_dw_l%d" % l, "dl_gemm_f32", 1, 0, self.in_ld[l], hdim, B, ptr(xin), self.in_ld[l],
-                    ptr(self.dh[l]), self.h_ld[l], ptr(self.w_slab), self.out_ld[l], 3, None, 0, splits, stride, s)
-            call("dl_slab_sum", ptr(self.w_slab), _num_splits(B, splits), stride, stride,
+            if self.s3:
+                self._c("gemm_dw_l%d" % l, "dl_gemm_s3_tn", self.in_ld[l], hdim, B, ptr(xin), self.in_ld[l],
+                        ptr(self.dh[l]), self.h_ld[l], ptr(self.w_slab), self.out_ld[l], splits, stride, s)
+            else:
+                self._c("gemm_dw_l%d" % l, "dl_gemm_f32", 1, 0, self.in_ld[l], hdim, B, ptr(xin), self.in_ld[l],
+                        ptr(self.dh[l]), self.h_ld[l], ptr(self.w_slab), self.out_ld[l], 3, None, 0, splits, stride,
+                        s)
+            call("dl_slab_sum", ptr(self.w_slab), _num_splits(B, splits, 64 if self.s3 else 16), stride, stride,
                  ptr(self.flat[self.seg[l][1]:]), s)
         hoff = self.seg[nl][1]
         call("dl_slab_sum", ptr(self.head_slab), call_int("dl_head_grid", B), self.head_w, self.head_w,
@@ -611,6 +631,7 @@ class ShardedCTREngine(CTREngine):
             off, sz = self.seg[l][1], self.seg[l][2]
             self._c("adam_dense_l%d" % l, "dl_adam_dense", ptr(self.W[l]), ptr(self.Wm[l]), ptr(self.Wv[l]),
                     ptr(self.flat[off:]), 1, sz, sz, 0.0, 0, ptr(self.opt), None, None, s)
+            self._refresh_wb(l, s)
         self._c("adam_head", "dl_adam_dense", ptr(self.w_head), ptr(self.hm), ptr(self.hv), ptr(self.flat[hoff:]),
                 1, self.head_w, self.head_n, sp.l2, self.head_n - 1, ptr(self.opt), ptr(self.w_head_prev), None, s)
         if rep:

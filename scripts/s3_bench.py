@@ -9,6 +9,7 @@ from deep_learning_amd import _lib  # noqa: E402
 from deep_learning_amd._lib import call, ptr  # noqa: E402
 
 reps = int(sys.argv[1]) if len(sys.argv) > 1 else 20
+only = sys.argv[2] if len(sys.argv) > 2 else None   # run one case (profiling)
 B = 65536
 s = _lib.stream_handle()
 g = torch.Generator(device="cuda").manual_seed(0)
@@ -89,6 +90,13 @@ cases.append(("dw_l1", 2 * B * 416 * 400,
               lambda: (rel(slab[:64 * 416 * 400].view(64, 416, 400).sum(0), refw1),
                        rel(slab2[:64 * 416 * 400].view(64, 416, 400).sum(0), refw1))))
 for name, fl, f_s3, f_f32, err in cases:
+    if only:
+        if name == only:
+            for _ in range(reps):
+                f_s3()
+            torch.cuda.synchronize()
+            print(name, "done")
+        continue
     f_s3()
     f_f32()
     torch.cuda.synchronize()
@@ -96,7 +104,7 @@ for name, fl, f_s3, f_f32, err in cases:
     t_s3, t_f32 = timeit(f_s3), timeit(f_f32)
     print("%-7s s3 %7.1f us %6.1f TF/s err %.2e | f32 %7.1f us %6.1f TF/s err %.2e" %
           (name, t_s3, fl / t_s3 / 1e6, e_s3, t_f32, fl / t_f32 / 1e6, e_f32), flush=True)
-for sp in (32, 48, 64, 96, 128):
+for sp in (() if only else (32, 48, 64, 96, 128)):
     fn = lambda: call("dl_gemm_s3_tn", 416, 400, B, ptr(h), 416, ptr(dy), 416, ptr(slab), 400, sp, 416 * 400, s)
     t = timeit(fn)
     print("dw_l1 s3 splits %3d %7.1f us %6.1f TF/s" % (sp, t, 2 * B * 416 * 400 / t / 1e6), flush=True)

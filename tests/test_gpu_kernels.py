@@ -93,6 +93,82 @@ def test_gemm_f32_tall_split_tiles(hip_lib, M, N, K, splits):
     assert ((got - ref).abs() / scale).max().item() < 2e-6
 
 
+def _planes(W, transpose):
+    """dl_split3 planes of the f32 matrix W [rows][cols] (or of W^T) as int16 [3][..]."""
+    rows, cols = W.shape
+    ld = rows if transpose else cols
+    n = rows * cols
+    P = torch.zeros(3 * n, dtype=torch.int16, device="cuda")
+    call("dl_split3", ptr(W), rows, cols, cols, 1 if transpose else 0, ptr(P), ld, n, _s())
+    return P
+
+
+def test_split3_is_exact(hip_lib):
+    """hi + mid + lo reconstructs every (normal) f32 exactly, each plane a bf16 rounding."""
+    g = torch.Generator().manual_seed(3)
+    W = (torch.randn(37, 24, generator=g) * torch.logspace(-20, 20, 24)).cuda()
+    P = _planes(W, False).view(3, 37, 24)
+    f = lambda t: (t.to(torch.int32) << 16).view(torch.float32)
+    back = (f(P[0]) + f(P[1])) + f(P[2])
+    assert torch.equal(back, W)
+    assert torch.equal(f(P[0]), W.bfloat16().float())
+    PT = _planes(W, True).view(3, 24, 37)
+    assert torch.equal(PT[0], P[0].t())
+
+
+@pytest.mark.parametrize("epi", [0, 1, 2])
+@pytest.mark.parametrize("M,N,K", [(65536, 400, 432), (300, 400, 416), (257, 416, 400), (1000, 80, 64),
+                                   (513, 16, 8), (100, 213, 40)])
+def test_gemm_s3_nt_matches_fp64(hip_lib, epi, M, N, K):
+    """C = A . B^T (+ ReLU / ReluGrad mask) on the three-plane split, against fp64: the same
+    2e-6 relative bound as the f32 kernel; columns past N untouched."""
+    if M == 65536 and epi == 2:
+        pytest.skip("one full-size case per epilogue pair is enough")
+    g = torch.Generator().manual_seed(M + 3 * N + K + epi)
+    lda = K + 4
+    A = torch.zeros(M, lda)
+    A[:, :K] = torch.randn(M, K, generator=g)
+    Bm = torch.randn(N, K, generator=g) * 0.05
+    ref = A[:, :K].double() @ Bm.double().t()
+    scale = (A[:, :K].abs().double() @ Bm.abs().double().t()).clamp(min=1e-3)
+    mask = torch.randn(M, N + 5, generator=g)
+    if epi == 1:
+        ref = ref.clamp(min=0)
+    elif epi == 2:
+        ref = torch.where(mask[:, :N] > 0, ref, torch.zeros_like(ref))
+    Ad, mk = A.cuda(), mask.cuda()
+    Bp = _planes(Bm.cuda(), False)     # B given as [N][K]: planes with ld K
+    ldb = K
+    ldc = N + 3
+    C = torch.full((M, ldc), 7.0, device="cuda")
+    call("dl_gemm_s3_nt", M, N, K, ptr(Ad), lda, ptr(Bp), ldb, N * K, ptr(C), ldc, epi,
+         ptr(mk) if epi == 2 else None, N + 5, _s())
+    torch.cuda.synchronize()
+    out = C[:, :N].double().cpu()
+    assert ((out - ref).abs() / scale).max().item() < 2e-6
+    assert (C[:, N:].cpu() == 7.0).all()
+
+
+@pytest.mark.parametrize("M,N,K,splits", [(432, 400, 65536, 64), (416, 400, 8192, 8), (428, 396, 5000, 3),
+                                            (64, 16, 100, 1), (16, 416, 4096, 16)])
+def test_gemm_s3_tn_split_slabs(hip_lib, M, N, K, splits):
+    """Weight gradients X^T . dY as split-K slabs (K chunks rounded to 64): slab sums against
+    fp64, slabs past the used count untouched."""
+    g = torch.Generator().manual_seed(M + N + K)
+    X = torch.randn(K, M, generator=g).cuda()
+    Y = (torch.randn(K, N, generator=g) * 1e-3).cuda()
+    ref = (X.t().double() @ Y.double()).cpu()
+    from deep_learning_amd.engine import _num_splits
+    used = _num_splits(K, splits, 64)
+    slab = torch.full((used + 1, M, N), 7.0, device="cuda")
+    call("dl_gemm_s3_tn", M, N, K, ptr(X), M, ptr(Y), N, ptr(slab), N, splits, M * N, _s())
+    torch.cuda.synchronize()
+    got = slab[:used].double().sum(0).cpu()
+    scale = (X.abs().t().double() @ Y.abs().double()).cpu().clamp(min=1e-6)
+    assert ((got - ref).abs() / scale).max().item() < 2e-6
+    assert (slab[used].cpu() == 7.0).all()
+
+
 def test_gemm_bf16(hip_lib):
     g = torch.Generator().manual_seed(2)
     M, N, K = 300, 200, 256
