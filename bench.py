@@ -38,7 +38,7 @@ def log(*a):
     print("[bench %s]" % time.strftime("%H:%M:%S"), *a, file=sys.stderr, flush=True)
 
 
-def kernel_work(spec, B, touched_rows, rows=None, uniq=None, shard=None, wide_rows=None):
+def kernel_work(spec, B, touched_rows, rows=None, uniq=None, shard=None, wide_rows=None, stash=False):
     """Algorithmic bytes / flops per launch."""
     E, S, C = spec.E, spec.S, spec.C
     N = rows if rows is not None else spec.n_rows
@@ -61,12 +61,16 @@ def kernel_work(spec, B, touched_rows, rows=None, uniq=None, shard=None, wide_ro
         rec_b = (3 * E + 4) * 4
         refs = 2 * S if spec.fm else S            # FM + deep references per sample (wdl/dnn: deep only)
         xb = 2 if spec.tower == "bf16" else 4      # x0 element bytes (the bf16 tower's x0 is written as bf16)
-        # gather: read U records, write the compact rows (E + 1 floats) + keys
-        w["rec_gather"] = ("hbm", uniq * (rec_b + (E + 1) * 4 + 4))
+        # gather: read U records, write the compact rows (E + 1 floats) + keys; with the moment
+        # stash (default) also the caught-up m, v (+ first-order m1, v1) for the backward
+        stash_b = (2 * E + 4) * 4 if stash else 0
+        w["rec_gather"] = ("hbm", uniq * (rec_b + (E + 1) * 4 + 4 + stash_b))
         # indexed x0 assembly: refs/sample x (compact row + inv) + first-order (FM) + x0 cat write
         w["embed_fwd"] = ("hbm", B * (refs * (E * 4 + 4) + (S * 4 if spec.fm else 0) + S * E * xb))
-        # fused backward + Adam: U records read + written, per ref: ref id + dx0/fm_sum row + dz
-        w["embed_bwd"] = ("hbm", uniq * (2 * rec_b + 4 + 8) + B * refs * (4 + E * 4 + 4))
+        # fused backward + Adam: U records written and read back (stash: the compact row and
+        # stashed moments read instead), per ref: ref id + dx0/fm_sum row + dz
+        rd_b = ((E + 1) * 4 + stash_b) if stash else rec_b
+        w["embed_bwd"] = ("hbm", uniq * (rec_b + rd_b + 4 + 8) + B * refs * (4 + E * 4 + 4))
     if shard is not None:
         # row-sharded engine (shard.py): this rank's batch needs U = nsend + nrep unique rows;
         # as an owner it serves nrecv of them (gather) and updates nrecv arrivals (rec_apply)
@@ -88,10 +92,10 @@ def kernel_work(spec, B, touched_rows, rows=None, uniq=None, shard=None, wide_ro
         # wdl cross logit: per sample Fw ids + weights + gradient atomics + touched bytes, the h row,
         # the dY row (bf16 tower: bf16), label/score/z/dz
         dyb = 2 if spec.tower == "bf16" else 4
-        w["head"] = ("hbm", B * (Fw * (8 + 4 + 4 + 1) + H * 4 + H * dyb + 16))
+        w["head"] = ("hbm", B * (Fw * (8 + 4 + 8 + 1) + H * 4 + H * dyb + 16))
         # wide Adam (L2 on every row: a dense sweep): p, m, v read + written, touched flag read;
-        # gradient read + reset where touched (at most B * Fw rows)
-        w["adam_wide"] = ("hbm", (wide_rows or 0) * (12 * 2 + 1) + B * Fw * 8)
+        # int64 fixed-point gradient read + reset where touched (at most B * Fw rows)
+        w["adam_wide"] = ("hbm", (wide_rows or 0) * (12 * 2 + 1) + B * Fw * 16)
     return w
 
 
@@ -337,7 +341,8 @@ def main():
     uniq = int(eng.idx_n[0].item()) if getattr(eng, "lazy", False) and not sharded else None
     ww = getattr(eng, "ww", None)
     work = kernel_work(spec, B, touched_rows, rows=getattr(eng, "local_rows", spec.n_rows), uniq=uniq,
-                       shard=shard_counts, wide_rows=int(ww.shape[0]) if ww is not None else None)
+                       shard=shard_counts, wide_rows=int(ww.shape[0]) if ww is not None else None,
+                       stash=getattr(eng, "mv_u", None) is not None)
     kernels = {}
     for label, ts in times.items():
         us = float(np.mean(ts))

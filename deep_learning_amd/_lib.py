@@ -42,7 +42,8 @@ class PoolDesc(C.Structure):
 OPT_LEN, OPT_STATUS = 32, 16
 STATUS_BAD_ID, STATUS_LAG = 1, 2
 REC_FIRST, REC_SPARSE_ADAM = 1, 2
-ROWS_CLEAR_TOUCHED, ROWS_SPARSE_ADAM = 1, 2
+ROWS_CLEAR_TOUCHED, ROWS_SPARSE_ADAM, ROWS_GRAD_FIXED = 1, 2, 4
+WIDE_GRAD_SCALE = 2.0 ** 48
 
 P = C.c_void_p
 I32, I64, U64, F = C.c_int32, C.c_int64, C.c_uint64, C.c_float

@@ -137,6 +137,12 @@ __device__ __forceinline__ int64_t decode_key(uint32_t k, int world) {
 
 inline int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }
 
+// The wdl wide-weight gradient as 64-bit fixed point (include/dlamd.h DL_WIDE_GRAD_SCALE):
+// deterministic integer accumulation of the per-sample dz terms, read back as f32 by the
+// wide Adam sweep (DL_ROWS_GRAD_FIXED).
+__device__ __forceinline__ long long wide_fixed(float g) { return __double2ll_rn((double)g * DL_WIDE_GRAD_SCALE); }
+__device__ __forceinline__ float wide_float(long long q) { return (float)((double)q * (1.0 / DL_WIDE_GRAD_SCALE)); }
+
 // bf16 <-> f32 (bf16 tower): round-to-nearest-even; NaN kept NaN
 __device__ __forceinline__ float bf2f(unsigned short h) { return __uint_as_float(((unsigned)h) << 16); }
 __device__ __forceinline__ unsigned short f2bf(float f) {

@@ -131,8 +131,12 @@ __global__ __launch_bounds__(256) void head_kernel(int B, int fm_cols, int H, co
 // Wide&Deep cross logit (models/wdl.py:225-264):
 //   z = sum_f w[wide_f] + sum_j w[Fw + j] * h_j + bias    (w = wdl_weights [N + H])
 // The deep-output weights are rows Fw..Fw+H of the same vector, aliasing wide ids
-// in that range.  Wide rows get dz by f32 atomics into g_w (+ touched flag); the
-// dense part leaves per-block partials slab[block][0..H) = sum dz*h_j,
+// in that range.  Wide rows get dz added into g_w (+ touched flag) as 64-bit fixed point
+// (units of 2^-48, DL_WIDE_GRAD_SCALE): integer atomics are associative, so the wide gradient
+// — a segment sum over the batch's wide ids, TF's UnsortedSegmentSum — is the same bits
+// whatever order the waves add in (f32 atomics were not: run-to-run ulp differences),
+// and at |sum| << 2^15 every term keeps ~2^-48 absolute precision, finer than an f32 sum.
+// The dense part leaves per-block partials slab[block][0..H) = sum dz*h_j,
 // [H] = sum dz (bias), [H+1] = sum loss_b.
 //
 // One wave per sample, samples strided over the grid.  The wide lookups are two
@@ -147,7 +151,7 @@ __global__ __launch_bounds__(256) void wdl_head_kernel(int B, int Fw, int H, con
                                                        long long w_rows, const float* __restrict__ label, float eps,
                                                        float inv_batch, float* __restrict__ score,
                                                        float* __restrict__ z_out, float* __restrict__ dz,
-                                                       void* __restrict__ dh_out, float* __restrict__ g_w,
+                                                       void* __restrict__ dh_out, long long* __restrict__ g_w,
                                                        uint8_t* __restrict__ touched, float* __restrict__ slab,
                                                        int32_t* err) {
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
@@ -202,7 +206,7 @@ __global__ __launch_bounds__(256) void wdl_head_kernel(int B, int Fw, int H, con
       lsum += -y * logf(p + eps) - (1.f - y) * logf(1.f - p + eps);
     }
     if (wr >= 0 && g_w) {
-      atomicAdd(g_w + wr, g);
+      atomicAdd(reinterpret_cast<unsigned long long*>(g_w + wr), (unsigned long long)wide_fixed(g));
       if (touched) touched[wr] = 1;
     }
 #pragma unroll
@@ -254,10 +258,11 @@ __global__ __launch_bounds__(256) void wdl_head_kernel(int B, int Fw, int H, con
     slab[(long long)blockIdx.x * width + c] = red[c] + red[width + c] + red[2 * width + c] + red[3 * width + c];
 }
 
-// g[row0 + j] += sum_blocks slab[blk*width + col0 + j]; touched[row0 + j] = 1
+// g[row0 + j] += sum_blocks slab[blk*width + col0 + j] (fixed point, as the head's wide
+// gradient); touched[row0 + j] = 1
 __global__ __launch_bounds__(256) void slab_fold_rows_kernel(const float* __restrict__ slab, int blocks, int width,
-                                                             int col0, int n, float* __restrict__ g, long long row0,
-                                                             uint8_t* __restrict__ touched) {
+                                                             int col0, int n, long long* __restrict__ g,
+                                                             long long row0, uint8_t* __restrict__ touched) {
   const int j = blockIdx.x;
   if (j >= n) return;
   float acc = 0.f;
@@ -267,7 +272,7 @@ __global__ __launch_bounds__(256) void slab_fold_rows_kernel(const float* __rest
   if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = acc;
   __syncthreads();
   if (threadIdx.x == 0) {
-    g[row0 + j] += part[0] + part[1] + part[2] + part[3];
+    g[row0 + j] += wide_fixed(part[0] + part[1] + part[2] + part[3]);
     if (touched) touched[row0 + j] = 1;
   }
 }
@@ -279,7 +284,7 @@ using namespace dl;
 template <bool DHB>
 static int wdl_head(int32_t B, int32_t Fw, int32_t H, const int64_t* wide, int32_t wide_ld, const float* h,
                     int32_t ldh, const float* w, const float* bias, int64_t w_rows, const float* label, float eps,
-                    float inv_batch, float* score, float* z_out, float* dz, void* dh, float* g_w, uint8_t* touched,
+                    float inv_batch, float* score, float* z_out, float* dz, void* dh, int64_t* g_w, uint8_t* touched,
                     float* slab, int32_t slab_blocks, int32_t* err, void* stream) {
   DL_CHECK_ARG(Fw >= 0 && Fw <= 64, "Fw %d not in [0, 64]", Fw);
   DL_CHECK_ARG(H > 0 && H <= 4 * 64 * kHeadMaxH4, "H %d too large", H);
@@ -292,7 +297,8 @@ static int wdl_head(int32_t B, int32_t Fw, int32_t H, const int64_t* wide, int32
   if (B == 0) return 0;
   const size_t lds = 4 * (size_t)(H + 2) * sizeof(float);
   hipLaunchKernelGGL(wdl_head_kernel<DHB>, dim3(grid), dim3(256), lds, as_stream(stream), B, Fw, H, wide, wide_ld,
-                     h, ldh, w, bias, (long long)w_rows, label, eps, inv_batch, score, z_out, dz, dh, g_w, touched,
+                     h, ldh, w, bias, (long long)w_rows, label, eps, inv_batch, score, z_out, dz, dh,
+                     reinterpret_cast<long long*>(g_w), touched,
                      slab, err);
   DL_RETURN_LAUNCH(DHB ? "dl_wdl_head_fwd_bwd_bf16" : "dl_wdl_head_fwd_bwd");
 }
@@ -300,7 +306,7 @@ static int wdl_head(int32_t B, int32_t Fw, int32_t H, const int64_t* wide, int32
 extern "C" int dl_wdl_head_fwd_bwd(int32_t B, int32_t Fw, int32_t H, const int64_t* wide, int32_t wide_ld,
                                    const float* h, int32_t ldh, const float* w, const float* bias, int64_t w_rows,
                                    const float* label, float eps, float inv_batch, float* score, float* z_out,
-                                   float* dz, float* dh, float* g_w, uint8_t* touched, float* slab,
+                                   float* dz, float* dh, int64_t* g_w, uint8_t* touched, float* slab,
                                    int32_t slab_blocks, int32_t* err, void* stream) {
   return wdl_head<false>(B, Fw, H, wide, wide_ld, h, ldh, w, bias, w_rows, label, eps, inv_batch, score, z_out, dz,
                          dh, g_w, touched, slab, slab_blocks, err, stream);
@@ -309,18 +315,18 @@ extern "C" int dl_wdl_head_fwd_bwd(int32_t B, int32_t Fw, int32_t H, const int64
 extern "C" int dl_wdl_head_fwd_bwd_bf16(int32_t B, int32_t Fw, int32_t H, const int64_t* wide, int32_t wide_ld,
                                         const float* h, int32_t ldh, const float* w, const float* bias,
                                         int64_t w_rows, const float* label, float eps, float inv_batch, float* score,
-                                        float* z_out, float* dz, uint16_t* dh, float* g_w, uint8_t* touched,
+                                        float* z_out, float* dz, uint16_t* dh, int64_t* g_w, uint8_t* touched,
                                         float* slab, int32_t slab_blocks, int32_t* err, void* stream) {
   return wdl_head<true>(B, Fw, H, wide, wide_ld, h, ldh, w, bias, w_rows, label, eps, inv_batch, score, z_out, dz,
                         dh, g_w, touched, slab, slab_blocks, err, stream);
 }
 
 extern "C" int dl_slab_fold_rows(const float* slab, int32_t blocks, int32_t width, int32_t col0, int32_t n,
-                                 float* g, int64_t row0, uint8_t* touched, void* stream) {
+                                 int64_t* g, int64_t row0, uint8_t* touched, void* stream) {
   DL_CHECK_ARG(slab && g && blocks >= 1 && col0 + n <= width, "bad args");
   if (n <= 0) return 0;
   hipLaunchKernelGGL(slab_fold_rows_kernel, dim3(n), dim3(256), 0, as_stream(stream), slab, blocks, width, col0, n,
-                     g, (long long)row0, touched);
+                     reinterpret_cast<long long*>(g), (long long)row0, touched);
   DL_RETURN_LAUNCH("dl_slab_fold_rows");
 }
 

@@ -154,9 +154,9 @@ __global__ __launch_bounds__(256) void adam_rows4_kernel(float4* __restrict__ p,
 }
 
 // Width-1 tables (first-order weights): one thread per 4 rows.
-template <bool SPARSE>
+template <bool SPARSE, bool FIXED>
 __global__ __launch_bounds__(256) void adam_rows1_kernel(float* __restrict__ p, float* __restrict__ m,
-                                                         float* __restrict__ v, float* __restrict__ g,
+                                                         float* __restrict__ v, void* __restrict__ g_,
                                                          uint8_t* __restrict__ touched, long long n,
                                                          float l2, int clear, const float* __restrict__ opt,
                                                          float* __restrict__ sq_out) {
@@ -172,10 +172,16 @@ __global__ __launch_bounds__(256) void adam_rows1_kernel(float* __restrict__ p, 
              vi = reinterpret_cast<float4*>(v)[i];
       const uchar4 t = reinterpret_cast<const uchar4*>(touched)[i];
       float4 gi = make_float4(0.f, 0.f, 0.f, 0.f);
-      float4* g4 = reinterpret_cast<float4*>(g) + i;
       if (t.x | t.y | t.z | t.w) {
-        gi = *g4;
-        *g4 = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (FIXED) {   // 64-bit fixed-point gradient (the wdl wide weights)
+          long long* q = reinterpret_cast<long long*>(g_) + 4 * i;
+          gi = make_float4(wide_float(q[0]), wide_float(q[1]), wide_float(q[2]), wide_float(q[3]));
+          q[0] = 0; q[1] = 0; q[2] = 0; q[3] = 0;
+        } else {
+          float4* g4 = reinterpret_cast<float4*>(g_) + i;
+          gi = *g4;
+          *g4 = make_float4(0.f, 0.f, 0.f, 0.f);
+        }
         if (!t.x) gi.x = 0.f; if (!t.y) gi.y = 0.f; if (!t.z) gi.z = 0.f; if (!t.w) gi.w = 0.f;
         if (clear) reinterpret_cast<uchar4*>(touched)[i] = make_uchar4(0, 0, 0, 0);
       }
@@ -191,7 +197,16 @@ __global__ __launch_bounds__(256) void adam_rows1_kernel(float* __restrict__ p, 
     } else {
       for (long long r = 4 * i; r < n; ++r) {
         float gi = 0.f;
-        if (touched[r]) { gi = g[r]; g[r] = 0.f; if (clear) touched[r] = 0; }
+        if (touched[r]) {
+          if (FIXED) {
+            gi = wide_float(reinterpret_cast<long long*>(g_)[r]);
+            reinterpret_cast<long long*>(g_)[r] = 0;
+          } else {
+            gi = reinterpret_cast<float*>(g_)[r];
+            reinterpret_cast<float*>(g_)[r] = 0.f;
+          }
+          if (clear) touched[r] = 0;
+        }
         if (skip) continue;
         float pi = p[r], mi = m[r], vi = v[r];
         if (l2 != 0.f) gi += l2 * pi;
@@ -302,11 +317,13 @@ extern "C" int dl_adam_dense(float* p, float* m, float* v, const float* slab, in
   return dl_adam_dense_reg(p, m, v, slab, nslab, slab_stride, n, l2, l2_count, 0, opt, p_prev, sq_out, stream);
 }
 
-extern "C" int dl_adam_rows(float* p, float* m, float* v, float* g, uint8_t* touched, int64_t n_rows,
+extern "C" int dl_adam_rows(float* p, float* m, float* v, void* g, uint8_t* touched, int64_t n_rows,
                             int32_t width, float l2, int32_t rows_flags, const float* opt, float* sq_out,
                             void* stream) {
   const int clear_touched = rows_flags & DL_ROWS_CLEAR_TOUCHED;
   const bool sparse = (rows_flags & DL_ROWS_SPARSE_ADAM) != 0;
+  const bool fixed = (rows_flags & DL_ROWS_GRAD_FIXED) != 0;
+  DL_CHECK_ARG(!fixed || width == 1, "the fixed-point gradient form is for width-1 rows");
   DL_CHECK_ARG(p && m && v && g && touched && opt, "NULL pointer");
   DL_CHECK_ARG(width == 1 || width % 4 == 0, "width must be 1 or a multiple of 4");
   DL_CHECK_ARG(((uintptr_t)p | (uintptr_t)m | (uintptr_t)v | (uintptr_t)g) % 16 == 0, "16-B alignment");
@@ -314,8 +331,10 @@ extern "C" int dl_adam_rows(float* p, float* m, float* v, float* g, uint8_t* tou
   hipStream_t s = as_stream(stream);
   if (width == 1) {
     DL_CHECK_ARG(((uintptr_t)touched % 4) == 0, "touched must be 4-B aligned");
-    hipLaunchKernelGGL(sparse ? adam_rows1_kernel<true> : adam_rows1_kernel<false>, dim3(grid_for(n_rows, 4)),
-                       dim3(256), 0, s, p, m, v, g, touched, (long long)n_rows, l2, clear_touched, opt, sq_out);
+    auto k = fixed ? (sparse ? adam_rows1_kernel<true, true> : adam_rows1_kernel<false, true>)
+                   : (sparse ? adam_rows1_kernel<true, false> : adam_rows1_kernel<false, false>);
+    hipLaunchKernelGGL(k, dim3(grid_for(n_rows, 4)), dim3(256), 0, s, p, m, v, g, touched, (long long)n_rows, l2,
+                       clear_touched, opt, sq_out);
   } else {
     const long long n4 = n_rows * (width / 4);
     hipLaunchKernelGGL(sparse ? adam_rows4_kernel<true> : adam_rows4_kernel<false>, dim3(grid_for(n4)), dim3(256),

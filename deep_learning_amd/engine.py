@@ -286,7 +286,9 @@ class CTREngine:
         if self.wdl:   # wdl_weights [N + H] (deep-output rows alias wide ids, wdl.py:241-248) + bias
             self.w_rows = N + sp.hidden[-1]
             wr = _ru(self.w_rows, 16)
-            self.ww, self.wm, self.wv, self.wg = z(wr), z(wr), z(wr), z(wr)
+            self.ww, self.wm, self.wv = z(wr), z(wr), z(wr)
+            # wide gradient: int64 fixed point (deterministic integer atomics, head.hip)
+            self.wg = z(wr, dt=torch.int64)
             self.w_touched = z(wr, dt=torch.uint8)
             self.wb, self.wbm, self.wbv = z(4), z(4), z(4)
         self.err = z(4, dt=torch.int32)       # the batch's id-validation word (per buffer set)
@@ -874,7 +876,8 @@ class CTREngine:
             self._c("adam_bias", "dl_adam_dense", ptr(self.wb), ptr(self.wbm), ptr(self.wbv),
                     ptr(self.head_slab[:, H:]), hb, H + 2, 1, 0.0, 0, ptr(self.opt), None, None, s)
             self._c("adam_wide", "dl_adam_rows", ptr(self.ww), ptr(self.wm), ptr(self.wv), ptr(self.wg),
-                    ptr(self.w_touched), self.ww.shape[0], 1, sp.l2, 1, ptr(self.opt), ptr(self.opt[8:]), s)
+                    ptr(self.w_touched), self.ww.shape[0], 1, sp.l2, 1 | _lib.ROWS_GRAD_FIXED, ptr(self.opt),
+                    ptr(self.opt[8:]), s)
             if self.lazy:
                 return
             self._c("adam_table", "dl_adam_rows", ptr(self.table), ptr(self.tm), ptr(self.tv), ptr(self.tg),

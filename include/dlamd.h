@@ -287,24 +287,26 @@ int dl_wdl_head_grid(int32_t B);
 /* Wide&Deep cross logit, forward and backward fused (models/wdl.py:225-275):
  * z = sum_f w[wide_f] + sum_j w[Fw+j] h_j + bias[0] (w = wdl_weights [w_rows]; the
  * deep-output rows Fw..Fw+H alias wide ids); sigmoid + eps-log-loss as dl_head_fwd_bwd.
- * Wide-row gradients dz go to g_w by f32 atomics (+ touched); the dense part leaves
+ * Wide-row gradients dz are added to g_w (int64 fixed point, units 1/DL_WIDE_GRAD_SCALE:
+ * integer atomics, so the segment sum is deterministic) (+ touched); the dense part leaves
  * slab[block][0..H) = sum dz*h, [H] = sum dz, [H+1] = sum loss (fold with
  * dl_slab_fold_rows into g_w rows Fw..Fw+H).  g_w = NULL: forward only (predict). */
 int dl_wdl_head_fwd_bwd(int32_t B, int32_t Fw, int32_t H, const int64_t* wide, int32_t wide_ld,
                         const float* h, int32_t ldh, const float* w, const float* bias, int64_t w_rows,
                         const float* label, float eps, float inv_batch, float* score, float* z_out,
-                        float* dz, float* dh, float* g_w, uint8_t* touched, float* slab,
+                        float* dz, float* dh, int64_t* g_w, uint8_t* touched, float* slab,
                         int32_t slab_blocks, int32_t* err, void* stream);
 /* As dl_wdl_head_fwd_bwd with dh written as bf16 (round-to-nearest-even): the bf16
  * tower's dY operand (config C5), 8-B aligned, same leading dimension ldh as h. */
 int dl_wdl_head_fwd_bwd_bf16(int32_t B, int32_t Fw, int32_t H, const int64_t* wide, int32_t wide_ld,
                              const float* h, int32_t ldh, const float* w, const float* bias, int64_t w_rows,
                              const float* label, float eps, float inv_batch, float* score, float* z_out,
-                             float* dz, uint16_t* dh, float* g_w, uint8_t* touched, float* slab,
+                             float* dz, uint16_t* dh, int64_t* g_w, uint8_t* touched, float* slab,
                              int32_t slab_blocks, int32_t* err, void* stream);
-/* g[row0+j] += sum over `blocks` slab rows of slab[blk*width + col0 + j], j < n. */
+/* g[row0+j] += sum over `blocks` slab rows of slab[blk*width + col0 + j], j < n, as int64
+ * fixed point (units 1/DL_WIDE_GRAD_SCALE, the wide gradient's form). */
 int dl_slab_fold_rows(const float* slab, int32_t blocks, int32_t width, int32_t col0, int32_t n,
-                      float* g, int64_t row0, uint8_t* touched, void* stream);
+                      int64_t* g, int64_t row0, uint8_t* touched, void* stream);
 
 /* ------------------------------------------------------------------------
  * TF1 Adam (training_ops.cc ApplyAdam, dense semantics: every element's m, v
@@ -353,10 +355,14 @@ int dl_adam_dense_reg(float* p, float* m, float* v, const float* slab, int32_t n
  * m = m*b1 + g*(1-b1), v = v*b2 + (g*g)*(1-b2), p -= lr*m/(sqrt(v)+eps); wdl.py:44-47,132,
  * deepfm.py:57-60, dnn.py:49-54), else ApplyAdam's (the pipeline models' tables, whose
  * gradient is densified by the row-0 concat, deepfm_pipeline.py:83-86).
- * width = E (table) or 1 (first-order). */
+ * width = E (table) or 1 (first-order).  DL_ROWS_GRAD_FIXED (width 1): g is int64 fixed
+ * point in units of 1/DL_WIDE_GRAD_SCALE (the wdl wide-weight gradient of
+ * dl_wdl_head_fwd_bwd / dl_slab_fold_rows). */
 #define DL_ROWS_CLEAR_TOUCHED 1
 #define DL_ROWS_SPARSE_ADAM 2
-int dl_adam_rows(float* p, float* m, float* v, float* g, uint8_t* touched, int64_t n_rows,
+#define DL_ROWS_GRAD_FIXED 4
+#define DL_WIDE_GRAD_SCALE 281474976710656.0 /* 2^48 */
+int dl_adam_rows(float* p, float* m, float* v, void* g, uint8_t* touched, int64_t n_rows,
                  int32_t width, float l2, int32_t rows_flags, const float* opt, float* sq_out,
                  void* stream);
 

@@ -574,7 +574,7 @@ def test_wdl_head_bf16_dy_is_rounded_f32_dy(hip_lib, B):
     for bf in (0, 1):
         score, z, dz = (torch.zeros(B, device="cuda") for _ in range(3))
         dh = torch.zeros(B, ldh, device="cuda", dtype=torch.bfloat16 if bf else torch.float32)
-        gw = torch.zeros(rows, device="cuda")
+        gw = torch.zeros(rows, device="cuda", dtype=torch.int64)   # fixed point, 2^-48 units
         touched = torch.zeros(rows, device="cuda", dtype=torch.uint8)
         slab = torch.zeros(grid * (H + 2), device="cuda")
         err = torch.zeros(4, device="cuda", dtype=torch.int32)
@@ -585,9 +585,11 @@ def test_wdl_head_bf16_dy_is_rounded_f32_dy(hip_lib, B):
         assert err.cpu().sum().item() == 0
         outs.append((score.cpu(), z.cpu(), dz.cpu(), dh[:, :H].cpu(), gw.cpu(), touched.cpu(), slab.cpu()))
     f, b = outs
-    for i in (0, 1, 2, 5, 6):
+    for i in (0, 1, 2, 4, 5, 6):   # wide gradient too: integer atomics, order-independent
         assert torch.equal(f[i], b[i])
     assert torch.equal(b[3], f[3].bfloat16())
-    np.testing.assert_allclose(b[4].numpy(), f[4].numpy(), rtol=1e-5, atol=1e-9)   # atomics: order differs
+    # the wide segment sum against fp64 (every dz term quantised to 2^-48)
+    gref = torch.zeros(rows, dtype=torch.float64).index_add_(0, wide.reshape(-1), f[2].double().repeat_interleave(Fw))
+    np.testing.assert_allclose(f[4].double().numpy() / 2.0 ** 48, gref.numpy(), rtol=0, atol=1e-12)
     z_ref = w.double()[wide].sum(1) + h[:, :H].double() @ w.double()[Fw:Fw + H] + 0.1
     np.testing.assert_allclose(f[1].double().numpy(), z_ref.numpy(), rtol=0, atol=1e-4)

@@ -112,17 +112,10 @@ def test_lazy_adam_bit_identical_to_dense(hip_lib, name, stash):
     """Row records + lazy catch-up (rec.hip) against the dense sweep with the same
     (sorted, deterministic) gradients: parameters, Adam moments, logits and
     predictions must be bit-identical.  A large table, a small batch and an 8-entry
-    alpha ring make rows lag many steps and force periodic flushes.
-
-    wdl: the wide-weight gradient (wdl_weights rows hit by wide ids) is accumulated by
-    f32 atomics in the head in both modes — order-dependent, like TF's GPU
-    UnsortedSegmentSum — so two runs may differ by an ulp there and through it in
-    everything downstream; that case is held to 1e-6 relative instead."""
+    alpha ring make rows lag many steps and force periodic flushes.  (wdl included: its
+    wide-weight gradient is an integer fixed-point segment sum, order-independent.)"""
     kw = dict(CASES[name], cate_index_size=50000)
-    if name == "wdl":
-        same = lambda a, b, err_msg="": np.testing.assert_allclose(a, b, rtol=1e-6, atol=1e-9, err_msg=err_msg)
-    else:
-        same = np.testing.assert_array_equal
+    same = np.testing.assert_array_equal
     model = _model(name)
     spec = ModelSpec(model, **kw)
     dense = CTREngine(spec, max_batch=128, seed=3, bwd="sorted")
