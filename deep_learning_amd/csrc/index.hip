@@ -9,107 +9,18 @@
 //
 // Key of a reference to row r (owner = r % world, local = r / world):
 //   (owner << 27) | local     (replicated rows r < replicated_below: owner = world)
-// so a sort by key groups rows by owner, then by local row.  Invalid refs
-// (row 0 under the zero-row rule, out-of-range ids) get key 0xFFFFFFFF and sort last.
-#include <hipcub/hipcub.hpp>
-
+// so a sort by key groups rows by owner, then by local row.  References without a key
+// (row 0 under the zero-row rule, out-of-range ids) are dropped by the sort's first pass.
+//
+// The sort is the hand-written stable LSD radix sort of rsort.hip (no library kernels, no
+// host synchronisation: the number of valid references stays on the device), so the whole
+// index build can run inside a captured hipGraph.
 #include "common.h"
+#include "rsort.h"
 
 namespace dl {
 
 constexpr int kLocalBits = 27;
-
-__device__ __forceinline__ bool row_ok_i(int64_t row, int zero_row0) {
-  return row > 0 || (row == 0 && !zero_row0);
-}
-
-__global__ __launch_bounds__(256) void make_refs_kernel(dl_emb_layout L, const int64_t* __restrict__ cate, int world,
-                                                        int rep_below, uint32_t kInvalidKey,
-                                                        uint32_t* __restrict__ keys,
-                                                        int32_t* __restrict__ refs, int32_t* err) {
-  const int S = L.cate_fields;
-  const int ns = index_slots(L);
-  const long long n = (long long)L.batch * ns;
-  for (long long k = (long long)blockIdx.x * blockDim.x + threadIdx.x; k < n; k += (long long)gridDim.x * blockDim.x) {
-    const int b = (int)(k / ns), s = (int)(k % ns);
-    int64_t row;
-    const int mb = index_multi_base(L);
-    if (L.use_fm && s < S) row = cate[(long long)b * L.cate_ld + s] + L.fm_cate_offset;
-    else if (s < mb) row = cate[(long long)b * L.cate_ld + (L.use_fm ? s - S : s)] + L.deep_cate_offset;
-    else row = cate[(long long)b * L.cate_ld + S + (s - mb)] + L.deep_cate_offset;   // multi-hot id
-    uint32_t key = kInvalidKey;
-    if (row < 0 || row >= L.n_rows) {
-      if (err) atomicOr(err, 1);
-    } else if (row_ok_i(row, L.zero_row0)) {
-      if (row < rep_below) key = ((uint32_t)world << kLocalBits) | (uint32_t)row;
-      else key = ((uint32_t)(row % world) << kLocalBits) | (uint32_t)(row / world);
-    }
-    keys[k] = key;
-    refs[k] = (int32_t)k;
-  }
-}
-
-// Multi-hot batches are mostly padding (id 0 -> invalid key): the valid (key, ref) pairs are
-// compacted in ref order before the sort, and inv starts at -1 for every reference.
-__global__ __launch_bounds__(256) void valid_flags_kernel(const uint32_t* __restrict__ keys, int n, uint32_t kInvalidKey,
-                                                          int32_t* __restrict__ flags, int32_t* __restrict__ inv) {
-  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
-    flags[i] = keys[i] != kInvalidKey ? 1 : 0;
-    if (inv) inv[i] = -1;
-  }
-}
-
-__global__ __launch_bounds__(256) void compact_kernel(const uint32_t* __restrict__ keys, const int32_t* __restrict__ pos1,
-                                                      int n, uint32_t kInvalidKey, uint32_t* __restrict__ kout,
-                                                      int32_t* __restrict__ rout, int32_t* __restrict__ n_valid) {
-  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
-    if (keys[i] != kInvalidKey) {
-      const int p = pos1[i] - 1;
-      kout[p] = keys[i];
-      rout[p] = i;
-    }
-    if (i + 1 == n) n_valid[0] = pos1[i];
-  }
-}
-
-__global__ __launch_bounds__(256) void head_flags_kernel(const uint32_t* __restrict__ keys, int n, uint32_t kInvalidKey,
-                                                         int32_t* __restrict__ flags) {
-  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
-    const uint32_t k = keys[i];
-    flags[i] = (k != kInvalidKey && (i == 0 || keys[i - 1] != k)) ? 1 : 0;
-  }
-}
-
-__global__ __launch_bounds__(256) void scatter_index_kernel(const uint32_t* __restrict__ keys, const int32_t* __restrict__ refs,
-                                                            const int32_t* __restrict__ uid1, int n, int world,
-                                                            uint32_t kInvalidKey,
-                                                            uint32_t* __restrict__ uniq, int32_t* __restrict__ seg_off,
-                                                            int32_t* __restrict__ n_uniq, int32_t* __restrict__ inv,
-                                                            int32_t* __restrict__ owner_counts) {
-  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
-    const uint32_t k = keys[i];
-    if (k == kInvalidKey) {
-      if (inv) inv[refs[i]] = -1;
-      continue;
-    }
-    const int u = uid1[i] - 1;
-    const bool head = (i == 0 || keys[i - 1] != k);
-    if (head) {
-      uniq[u] = k;
-      seg_off[u] = i;
-      // first unique row of an owner group (keys are sorted by owner): its start index.
-      // Counts follow from the starts (owner_counts_kernel) — no per-row atomics on the
-      // world+1 counters, which serialised 3.2 M updates (38 ms at one rank).
-      if (owner_counts && (i == 0 || (keys[i - 1] >> kLocalBits) != (k >> kLocalBits)))
-        owner_counts[k >> kLocalBits] = u;
-    }
-    if (i + 1 == n || keys[i + 1] == kInvalidKey) {
-      seg_off[u + 1] = i + 1;
-      n_uniq[0] = u + 1;
-    }
-    if (inv) inv[refs[i]] = u;
-  }
-}
 
 // ---------------------------------------------------------------------------
 // Segmented unique over the sorted keys in two passes (replaces head flags + a device
@@ -128,8 +39,9 @@ __device__ __forceinline__ bool uq_head(const uint32_t* __restrict__ keys, int i
   return k != invalid && (i == 0 || keys[i - 1] != k);
 }
 
-__global__ __launch_bounds__(256) void unique_count_kernel(const uint32_t* __restrict__ keys, int n, uint32_t invalid,
-                                                           int32_t* __restrict__ chunk_cnt) {
+__global__ __launch_bounds__(256) void unique_count_kernel(const uint32_t* __restrict__ keys, const int32_t* n_dev,
+                                                           int n_max, uint32_t invalid, int32_t* __restrict__ chunk_cnt) {
+  const int n = min(*n_dev, n_max);
   const int base = blockIdx.x * kUqChunk;
   int c = 0;
 #pragma unroll
@@ -145,12 +57,15 @@ __global__ __launch_bounds__(256) void unique_count_kernel(const uint32_t* __res
 }
 
 __global__ __launch_bounds__(256) void unique_emit_kernel(const uint32_t* __restrict__ keys, const int32_t* __restrict__ refs,
-                                                          int n, uint32_t invalid, const int32_t* __restrict__ chunk_cnt,
+                                                          const int32_t* n_dev, int n_max, uint32_t invalid,
+                                                          const int32_t* __restrict__ chunk_cnt,
                                                           uint32_t* __restrict__ uniq, int32_t* __restrict__ seg_off,
                                                           int32_t* __restrict__ n_uniq, int32_t* __restrict__ inv,
                                                           int32_t* __restrict__ owner_counts) {
   __shared__ int wsum[4];
   __shared__ int base_s;
+  const int n = min(*n_dev, n_max);
+  if ((long long)blockIdx.x * kUqChunk >= n) return;   // whole block past the valid keys
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   // exclusive offset of this chunk: sum of the earlier chunks' head counts
   int off = 0;
@@ -235,22 +150,13 @@ __global__ __launch_bounds__(256) void unique_emit_kernel(const uint32_t* __rest
   }
 }
 
-static void unique_from_sorted(const uint32_t* keys, const int32_t* refs, int n, uint32_t invalid, int32_t* chunk_cnt,
-                               uint32_t* uniq, int32_t* seg_off, int32_t* n_uniq, int32_t* inv,
-                               int32_t* owner_counts, hipStream_t s) {
-  const int chunks = (n + kUqChunk - 1) / kUqChunk;
-  hipLaunchKernelGGL(unique_count_kernel, dim3(chunks), dim3(256), 0, s, keys, n, invalid, chunk_cnt);
-  hipLaunchKernelGGL(unique_emit_kernel, dim3(chunks), dim3(256), 0, s, keys, refs, n, invalid, chunk_cnt, uniq,
-                     seg_off, n_uniq, inv, owner_counts);
-}
-
-// copies the compacted pairs back into the sort's input arrays
-__global__ __launch_bounds__(256) void iota_refs_copy_kernel(const uint32_t* __restrict__ kin, const int32_t* __restrict__ rin,
-                                                             int n, uint32_t* __restrict__ kout, int32_t* __restrict__ rout) {
-  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
-    kout[i] = kin[i];
-    rout[i] = rin[i];
-  }
+static void unique_from_sorted(const uint32_t* keys, const int32_t* refs, const int32_t* n_dev, int n_max,
+                               uint32_t invalid, int32_t* chunk_cnt, uint32_t* uniq, int32_t* seg_off,
+                               int32_t* n_uniq, int32_t* inv, int32_t* owner_counts, hipStream_t s) {
+  const int chunks = (n_max + kUqChunk - 1) / kUqChunk;
+  hipLaunchKernelGGL(unique_count_kernel, dim3(chunks), dim3(256), 0, s, keys, n_dev, n_max, invalid, chunk_cnt);
+  hipLaunchKernelGGL(unique_emit_kernel, dim3(chunks), dim3(256), 0, s, keys, refs, n_dev, n_max, invalid, chunk_cnt,
+                     uniq, seg_off, n_uniq, inv, owner_counts);
 }
 
 __global__ void index_init_kernel(int32_t* n_uniq, int32_t* seg_off, int32_t* owner_counts, int n_owner) {
@@ -260,7 +166,7 @@ __global__ void index_init_kernel(int32_t* n_uniq, int32_t* seg_off, int32_t* ow
     for (int i = t; i < n_owner; i += blockDim.x) owner_counts[i] = -1;   // group starts, -1 = absent
 }
 
-// owner group starts (scatter_index_kernel) -> counts, in owner order.
+// owner group starts (unique_emit_kernel) -> counts, in owner order.
 __global__ void owner_counts_kernel(int32_t* owner_counts, int n_owner, const int32_t* n_uniq) {
   if (threadIdx.x != 0 || blockIdx.x != 0) return;
   int end = n_uniq[0];
@@ -275,52 +181,35 @@ __global__ void owner_counts_kernel(int32_t* owner_counts, int n_owner, const in
   }
 }
 
-struct IndexWs {
-  uint32_t* keys_in;
-  int32_t* refs_in;
-  int32_t* flags;
-  int32_t* uid1;
-  void* temp;
-  size_t temp_bytes;
-};
-
 static size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
 
-// Onesweep radix sort over the key's significant bits only (25 for a 26M-row table).
-// (11-bit digits would save a pass, but rocPRIM's match-rank variant that fits them
-// in LDS ran 3x slower on gfx950 — measured; the default 8-bit digits stay.)
-static hipError_t sort_pairs(void* temp, size_t& bytes, const uint32_t* kin, uint32_t* kout, const int32_t* vin,
-                             int32_t* vout, int n, int end_bit, hipStream_t s) {
-  return hipcub::DeviceRadixSort::SortPairs(temp, bytes, kin, kout, vin, vout, n, 0, end_bit, s);
-}
+// workspace: the sort's, then the unique step's per-chunk head counts and the valid count
+struct IndexWs {
+  void* sort;
+  size_t sort_bytes;
+  int32_t* chunk_cnt;
+  int32_t* n_valid;
+};
 
-static size_t cub_temp_bytes(int n) {
-  size_t a = 0, b = 0;
-  sort_pairs(nullptr, a, nullptr, nullptr, nullptr, nullptr, n, 32, 0);
-  hipcub::DeviceScan::InclusiveSum(nullptr, b, (int32_t*)nullptr, (int32_t*)nullptr, n);
-  return a > b ? a : b;
-}
-
-// Bits of the sorted key range: keys are < 2^end_bit, the all-ones value marks invalid refs.
-static int key_bits(int64_t n_rows, int world, int rep_below) {
-  uint64_t max_key;
-  if (world == 1 && rep_below == 0) max_key = (uint64_t)n_rows;            // row; n_rows itself = headroom
-  else max_key = ((uint64_t)(rep_below > 0 ? world : world - 1) << kLocalBits) | ((1u << kLocalBits) - 1);
-  int b = 1;
-  while (b < 32 && (max_key + 1) > (1ull << b) - 1) ++b;
-  return b;
-}
-
-static IndexWs carve(void* ws, int n) {
+static IndexWs carve(void* ws, int64_t n) {
   char* p = reinterpret_cast<char*>(ws);
   IndexWs w;
-  w.keys_in = reinterpret_cast<uint32_t*>(p); p += align256((size_t)n * 4);
-  w.refs_in = reinterpret_cast<int32_t*>(p); p += align256((size_t)n * 4);
-  w.flags = reinterpret_cast<int32_t*>(p); p += align256((size_t)n * 4);
-  w.uid1 = reinterpret_cast<int32_t*>(p); p += align256((size_t)n * 4);
-  w.temp = p;
-  w.temp_bytes = cub_temp_bytes(n);
+  w.sort = p;
+  w.sort_bytes = rsort_workspace_bytes(n);
+  p += align256(w.sort_bytes);
+  w.chunk_cnt = reinterpret_cast<int32_t*>(p);
+  p += align256((size_t)((n + kUqChunk - 1) / kUqChunk + 1) * 4);
+  w.n_valid = reinterpret_cast<int32_t*>(p);
   return w;
+}
+
+// Bits of the compressed key range (rsort.h): owner-major, lrange rows per owner.
+static int compressed_bits(int64_t n_rows, int world, int rep_below, uint32_t& lrange) {
+  lrange = (uint32_t)((n_rows + world - 1) / world);
+  const uint64_t max_excl = rep_below > 0 ? (uint64_t)world * lrange + (uint64_t)rep_below : (uint64_t)world * lrange;
+  int b = 1;
+  while (b < 32 && (1ull << b) < max_excl) ++b;
+  return b;
 }
 
 }  // namespace dl
@@ -329,8 +218,8 @@ using namespace dl;
 
 extern "C" int64_t dl_index_workspace_bytes(int64_t n_refs) {
   if (n_refs <= 0 || n_refs > (1LL << 30)) return -1;
-  const int n = (int)n_refs;
-  return (int64_t)(4 * align256((size_t)n * 4) + align256(cub_temp_bytes(n)));
+  return (int64_t)(align256(rsort_workspace_bytes(n_refs)) + align256((size_t)((n_refs + kUqChunk - 1) / kUqChunk + 1) * 4) +
+                   256);
 }
 
 extern "C" int dl_index_build(const dl_emb_layout* L, const int64_t* cate, int32_t world,
@@ -341,70 +230,36 @@ extern "C" int dl_index_build(const dl_emb_layout* L, const int64_t* cate, int32
   DL_CHECK_ARG(L && cate && ws && sorted_keys && sorted_refs && uniq_keys && seg_off && n_uniq, "NULL argument");
   DL_CHECK_ARG(world >= 1 && world < 32, "world %d out of range", world);
   DL_CHECK_ARG(L->n_rows / world < (1LL << kLocalBits), "too many rows per shard for the 27-bit local key");
-  const int S = L->cate_fields;
+  DL_CHECK_ARG(replicated_below >= 0 && replicated_below < (1 << kLocalBits), "bad replicated_below");
   const long long n_ll = (long long)L->batch * index_slots(*L);
   DL_CHECK_ARG(n_ll < (1LL << 30), "too many references");
-  int n = (int)n_ll;
+  const int n = (int)n_ll;
   DL_CHECK_ARG(ws_bytes >= dl_index_workspace_bytes(n > 0 ? n : 1), "workspace too small");
   hipStream_t s = as_stream(stream);
   // zeroing by a kernel (not a memset node): keeps every node of a captured step a kernel
   hipLaunchKernelGGL(index_init_kernel, dim3(1), dim3(64), 0, s, n_uniq, seg_off, owner_counts, world + 1);
   if (n == 0) return 0;
   IndexWs w = carve(ws, n);
-  const int grid = (int)((n + 255) / 256 < 8192 ? (n + 255) / 256 : 8192);
-  const int end_bit = key_bits(L->n_rows, world, replicated_below);
-  const uint32_t invalid = end_bit >= 32 ? 0xFFFFFFFFu : (uint32_t)((1ull << end_bit) - 1);
-  hipLaunchKernelGGL(make_refs_kernel, dim3(grid), dim3(256), 0, s, *L, cate, world, replicated_below, invalid,
-                     w.keys_in, w.refs_in, err);
-  size_t tb = w.temp_bytes;
-  const uint32_t* sort_keys = w.keys_in;
-  const int32_t* sort_refs = w.refs_in;
-  int ns_sort = n;
-  if (L->multi_width > 0) {
-    // compact the valid references (ref order kept), then sort only those; the sorted
-    // arrays hold them first.  One stream sync to learn the count (the sort's size).
-    hipLaunchKernelGGL(valid_flags_kernel, dim3(grid), dim3(256), 0, s, w.keys_in, n, invalid, w.flags, inv);
-    if (hipcub::DeviceScan::InclusiveSum(w.temp, tb, w.flags, w.uid1, n, s) != hipSuccess) {
-      set_error("dl_index_build: scan failed");
-      return 3;
-    }
-    // compacted pairs go to the sorted_* arrays (free until the sort), then sort into place
-    uint32_t* ck = reinterpret_cast<uint32_t*>(w.flags);   // flags are consumed by the scan
-    hipLaunchKernelGGL(compact_kernel, dim3(grid), dim3(256), 0, s, w.keys_in, w.uid1, n, invalid, ck, sorted_refs,
-                       n_uniq);
-    int32_t nv = 0;
-    if (hipMemcpyAsync(&nv, n_uniq, sizeof(int32_t), hipMemcpyDeviceToHost, s) != hipSuccess ||
-        hipStreamSynchronize(s) != hipSuccess) {
-      set_error("dl_index_build: count readback failed");
-      return 4;
-    }
-    hipLaunchKernelGGL(iota_refs_copy_kernel, dim3(grid), dim3(256), 0, s, ck, sorted_refs, nv, w.keys_in, w.refs_in);
-    hipLaunchKernelGGL(index_init_kernel, dim3(1), dim3(64), 0, s, n_uniq, seg_off, owner_counts, world + 1);
-    ns_sort = nv;
-    tb = w.temp_bytes;
-  }
-  if (ns_sort > 0 &&
-      sort_pairs(w.temp, tb, sort_keys, sorted_keys, sort_refs, sorted_refs, ns_sort, end_bit, s) != hipSuccess) {
-    set_error("dl_index_build: radix sort failed");
+  uint32_t lrange;
+  const int bits = compressed_bits(L->n_rows, world, replicated_below, lrange);
+  RsSource src{};
+  src.kind = 1;
+  src.L = *L;
+  src.cate = cate;
+  src.world = world;
+  src.rep_below = replicated_below;
+  src.err = err;
+  src.inv = inv;
+  if (int rc = rsort_pairs(src, n, lrange, bits, w.sort, w.sort_bytes, sorted_keys, sorted_refs, w.n_valid, s)) {
+    set_error("dl_index_build: radix sort failed (%d)", rc);
     return 2;
   }
-  n = ns_sort;
-  if (n == 0) DL_RETURN_LAUNCH("dl_index_build");
-  unique_from_sorted(sorted_keys, sorted_refs, n, invalid, w.flags, uniq_keys, seg_off, n_uniq, inv, owner_counts, s);
+  unique_from_sorted(sorted_keys, sorted_refs, w.n_valid, n, 0xFFFFFFFFu, w.chunk_cnt, uniq_keys, seg_off, n_uniq, inv,
+                     owner_counts, s);
   if (owner_counts)
     hipLaunchKernelGGL(owner_counts_kernel, dim3(1), dim3(64), 0, s, owner_counts, world + 1, n_uniq);
   DL_RETURN_LAUNCH("dl_index_build");
 }
-
-namespace dl {
-__global__ __launch_bounds__(256) void iota_copy_kernel(const int32_t* __restrict__ keys, int n, int32_t* __restrict__ kout,
-                                                        int32_t* __restrict__ pos) {
-  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
-    kout[i] = keys[i];
-    pos[i] = i;
-  }
-}
-}  // namespace dl
 
 extern "C" int dl_sort_unique(const int32_t* keys, int64_t n_keys, int32_t key_bits, void* ws, int64_t ws_bytes,
                               int32_t* sorted_keys, int32_t* sorted_pos, int32_t* uniq_keys, int32_t* seg_off,
@@ -418,16 +273,16 @@ extern "C" int dl_sort_unique(const int32_t* keys, int64_t n_keys, int32_t key_b
   hipLaunchKernelGGL(index_init_kernel, dim3(1), dim3(64), 0, s, n_uniq, seg_off, (int32_t*)nullptr, 0);
   if (n == 0) return 0;
   IndexWs w = carve(ws, n);
-  const int grid = (int)((n + 255) / 256 < 8192 ? (n + 255) / 256 : 8192);
-  const uint32_t invalid = 0xFFFFFFFFu;   // keys are non-negative (< 2^key_bits): never equal
-  hipLaunchKernelGGL(iota_copy_kernel, dim3(grid), dim3(256), 0, s, keys, n, (int32_t*)w.keys_in, w.refs_in);
-  size_t tb = w.temp_bytes;
-  if (sort_pairs(w.temp, tb, w.keys_in, (uint32_t*)sorted_keys, w.refs_in, sorted_pos, n, key_bits, s) !=
-      hipSuccess) {
-    set_error("dl_sort_unique: radix sort failed");
+  RsSource src{};
+  src.kind = 0;
+  src.keys = reinterpret_cast<const uint32_t*>(keys);
+  if (int rc = rsort_pairs(src, n, 0u, key_bits, w.sort, w.sort_bytes, reinterpret_cast<uint32_t*>(sorted_keys),
+                           sorted_pos, w.n_valid, s)) {
+    set_error("dl_sort_unique: radix sort failed (%d)", rc);
     return 2;
   }
-  unique_from_sorted((const uint32_t*)sorted_keys, sorted_pos, n, invalid, w.flags, (uint32_t*)uniq_keys, seg_off,
-                     n_uniq, inv, (int32_t*)nullptr, s);
+  // keys are non-negative (< 2^key_bits): never equal to the 0xFFFFFFFF marker
+  unique_from_sorted(reinterpret_cast<const uint32_t*>(sorted_keys), sorted_pos, w.n_valid, n, 0xFFFFFFFFu,
+                     w.chunk_cnt, reinterpret_cast<uint32_t*>(uniq_keys), seg_off, n_uniq, inv, (int32_t*)nullptr, s);
   DL_RETURN_LAUNCH("dl_sort_unique");
 }

@@ -741,10 +741,9 @@ class CTREngine:
              self.head_blocks, s)
 
     def _pre(self, B):
-        """Work that must stay OUTSIDE a captured hipGraph: the batch index build
-        (rocPRIM onesweep radix sort faulted under hipGraph replay on this stack —
-        DESIGN.md §Known issues); it runs eagerly on the same stream before the
-        graph replay of the rest of the step."""
+        """The batch index build (dl_index_build: the hand-written radix sort + segmented
+        unique of index.hip, no host synchronisation).  Runs on the current stream — inside
+        the step's hipGraph (graph=True), or on the side stream when prefetched."""
         if self.bwd != "sorted":
             return
         s = _lib.stream_handle()
@@ -925,10 +924,11 @@ class CTREngine:
         self._slot_free = [None, None]    # event: the compute stream is done with a set
         self._pf = None                   # (set, B, ready event, batch) of a prefetched batch
 
-    def prefetch(self, batch):
+    def prefetch(self, batch, graph=False):
         """Stage `batch` and build its index into the idle buffer set on the side stream;
         train_step(batch) then starts from it.  Issued before the current step's work, so
-        the index build (memory bound) overlaps that step's GEMMs."""
+        the index build (memory bound) overlaps that step's GEMMs.  graph=True replays the
+        index build as a captured hipGraph (one per buffer set and batch size)."""
         self._enable_slots()
         if self._pf is not None:
             torch.cuda.current_stream().wait_event(self._pf[2])
@@ -943,7 +943,14 @@ class CTREngine:
         try:
             with torch.cuda.stream(side):
                 B = self.stage(batch)
-                self._pre(B)
+                if graph:
+                    key = (k, B, "pre")
+                    g = self.graphs.get(key)
+                    if g is None:
+                        g = self.graphs[key] = self._capture(B, pre_only=True)
+                    g.replay()
+                else:
+                    self._pre(B)
                 ev = torch.cuda.Event()
                 ev.record(side)
         finally:
@@ -980,15 +987,16 @@ class CTREngine:
             if self.since_flush >= self.hist_len - 2:
                 self.flush()
             self.since_flush += 1
-        if not indexed:
+        if not indexed and not graph:
             self._pre(B)
         if next_batch is not None:
-            self.prefetch(next_batch)
+            self.prefetch(next_batch, graph=graph)
         if graph:
-            key = (getattr(self, "_cur", 0), B)
+            # one graph per (buffer set, batch size, index built inside or prefetched)
+            key = (getattr(self, "_cur", 0), B, not indexed)
             g = self.graphs.get(key)
             if g is None:
-                g = self.graphs[key] = self._capture(B)
+                g = self.graphs[key] = self._capture(B, with_pre=not indexed)
             g.replay()
         else:
             self._train(B)
@@ -998,13 +1006,17 @@ class CTREngine:
         self.last_batch = B
         return B
 
-    def _capture(self, B):
-        # warm up allocations on a side stream, then capture the whole step
+    def _capture(self, B, with_pre=False, pre_only=False):
+        """Capture the step (with its index build when `with_pre`), or only the index build
+        (`pre_only`: the prefetch graph), on a capture stream; replayed on the caller's."""
         s = torch.cuda.Stream()
         s.wait_stream(torch.cuda.current_stream())
         g = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g, stream=s):
-            self._train(B)
+            if with_pre or pre_only:
+                self._pre(B)
+            if not pre_only:
+                self._train(B)
         torch.cuda.current_stream().wait_stream(s)
         return g
 
