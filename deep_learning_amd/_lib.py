@@ -40,7 +40,7 @@ class PoolDesc(C.Structure):
 
 # include/dlamd.h constants
 OPT_LEN, OPT_STATUS = 32, 16
-STATUS_BAD_ID, STATUS_LAG = 1, 2
+STATUS_BAD_ID, STATUS_LAG, STATUS_INDEX = 1, 2, 4
 REC_FIRST, REC_SPARSE_ADAM = 1, 2
 ROWS_CLEAR_TOUCHED, ROWS_SPARSE_ADAM, ROWS_GRAD_FIXED = 1, 2, 4
 WIDE_GRAD_SCALE = 2.0 ** 48

@@ -68,7 +68,7 @@ __global__ __launch_bounds__(256) void rec_gather_kernel(const float* __restrict
   const long long gt = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   const int q = lane % LPR, rw = lane / LPR;
   const long long wave_id = gt >> 6, nwaves = ((long long)gridDim.x * blockDim.x) >> 6;
-  const long long total = n_rep + (n_uniq ? (long long)clamp_uniq(n_uniq, max_u) : max_u);
+  const long long total = n_rep + (n_uniq ? (long long)clamp_uniq(n_uniq, max_u, c.status) : max_u);
   const int target = (int)opt[7] - lag;
   const int nch = E + (c.has_first ? 1 : 0);          // element chains per row
   const int T = RPW * nch;
@@ -243,7 +243,7 @@ __global__ __launch_bounds__(256) void rec_bwd_adam_kernel(SegGradIn sg, float* 
   const int Cf = (L.use_fm && L.fm_cont) ? L.cont_fields : 0;
   const int F = Cf + S + L.fm_extra;
   const long long nrefs = (long long)L.batch * ns;
-  const int nu = clamp_uniq(n_uniq, nrefs);
+  const int nu = clamp_uniq(n_uniq, nrefs, sg.status);
   // head weights of the FM second-order outputs (offset F: not 16-B aligned)
   const float* ws = sg.w_head + F + 4 * q;
   const float4 wsec = L.use_fm ? make_float4(ws[0], ws[1], ws[2], ws[3]) : make_float4(0.f, 0.f, 0.f, 0.f);
@@ -394,7 +394,7 @@ __global__ __launch_bounds__(256) void rec_apply_segments_kernel(float* __restri
   const int q = (int)(gt % LPR);
   const int t = (int)opt[7];
   const float alpha = opt[3];
-  const long long nu = n_uniq ? (long long)clamp_uniq(n_uniq, cap) : cap;
+  const long long nu = n_uniq ? (long long)clamp_uniq(n_uniq, cap, c.status) : cap;
   const bool first = c.has_first && q == 0;
   for (long long u = gt / LPR; u < nu; u += (long long)gridDim.x * blockDim.x / LPR) {
     const long long row = uniq[u];
@@ -594,6 +594,7 @@ extern "C" int dl_rec_bwd_adam(const dl_emb_layout* L, float* rec, int32_t rec_l
   DL_CHECK_ARG(!multi || (pool->dx0_pool_col % 4 == 0 && L->x0_pool_col % 4 == 0),
                "pool columns not float4 aligned");
   SegGradIn sg{*L, seg_off, sorted_refs, dz, w_head, fm_sum, dx0};
+  sg.status = opt_status(opt);
   const bool g1p = multi && L->use_fm && has_first;
   if (multi) {
     sg.slot_start = pool->slot_start; sg.slot_end = pool->slot_end; sg.n_slots = pool->n_slots;

@@ -28,7 +28,14 @@ struct SegGradIn {
   int n_slots;
   const float* g_pool;
   const float* g1_pool;
+  // opt's status word: an index entry out of range (a corrupt batch index) sets
+  // DL_STATUS_INDEX there and the host raises, instead of the entry being skipped silently
+  int* status;
 };
+
+__device__ __forceinline__ void index_fault(int* status) {
+  if (status) atomicOr(status, DL_STATUS_INDEX);
+}
 
 struct SegGrad {
   float s, dsum, x, g1;   // sum dsec*fm_sum, sum dsec, sum dx0, first-order gradient
@@ -43,13 +50,18 @@ __device__ __forceinline__ SegGrad segment_grad(const SegGradIn& a, long long u,
   const int S = L.cate_fields;
   const int ns = index_slots(L);
   const int Cf = (L.use_fm && L.fm_cont) ? L.cont_fields : 0;
-  const int e0 = max(0, a.seg_off[u]);
-  const int e1 = (int)min(nrefs, (long long)a.seg_off[u + 1]);
+  const int o0 = a.seg_off[u], o1 = a.seg_off[u + 1];
+  if (o0 < 0 || o1 > nrefs || o0 > o1) index_fault(a.status);
+  const int e0 = max(0, o0);
+  const int e1 = (int)min(nrefs, (long long)o1);
   SegGrad r{0.f, 0.f, 0.f, 0.f};
   const int mb = index_multi_base(L);   // multi-hot refs exist only with records (segment_grad4)
   for (int e = e0; e < e1; ++e) {
     const int k = a.refs[e];
-    if (k < 0 || k >= nrefs) continue;
+    if (k < 0 || k >= nrefs) {
+      index_fault(a.status);
+      continue;
+    }
     const int b = k / ns, sl = k % ns;
     if (sl >= mb) continue;
     if (L.use_fm && sl < S) {
@@ -82,7 +94,9 @@ struct SegGrad4 {
 struct SegRange { int e0, e1; };
 __device__ __forceinline__ SegRange seg_range(const SegGradIn& a, long long u, long long nu, long long nrefs) {
   if (u >= nu) return SegRange{0, 0};
-  return SegRange{max(0, a.seg_off[u]), (int)min(nrefs, (long long)a.seg_off[u + 1])};
+  const int o0 = a.seg_off[u], o1 = a.seg_off[u + 1];
+  if (o0 < 0 || o1 > nrefs || o0 > o1) index_fault(a.status);
+  return SegRange{max(0, o0), (int)min(nrefs, (long long)o1)};
 }
 
 // Sums over the references e0..e1 of one row; k_first = refs[e0] when the caller has
@@ -99,7 +113,10 @@ __device__ __forceinline__ SegGrad4 segment_grad4_range(const SegGradIn& a, int 
   const int mb = index_multi_base(L);
   for (int e = e0; e < e1; ++e) {
     const int k = (e == e0 && k_first != -2) ? k_first : a.refs[e];
-    if (k < 0 || k >= nrefs) continue;
+    if (k < 0 || k >= nrefs) {
+      index_fault(a.status);
+      continue;
+    }
     const int b = k / ns, sl = k % ns;
     if (sl >= mb) {
       // pooled slot m of multi position l: every member row gets the slot's gradient
@@ -131,13 +148,14 @@ __device__ __forceinline__ SegGrad4 segment_grad4_range(const SegGradIn& a, int 
 template <int E>
 __device__ __forceinline__ SegGrad4 segment_grad4(const SegGradIn& a, long long u, int q, long long nrefs,
                                                   float4 wsec) {
-  const int e0 = max(0, a.seg_off[u]);
-  const int e1 = (int)min(nrefs, (long long)a.seg_off[u + 1]);
-  return segment_grad4_range<E>(a, e0, e1, -2, q, nrefs, wsec);
+  const int o0 = a.seg_off[u], o1 = a.seg_off[u + 1];
+  if (o0 < 0 || o1 > nrefs || o0 > o1) index_fault(a.status);
+  return segment_grad4_range<E>(a, max(0, o0), (int)min(nrefs, (long long)o1), -2, q, nrefs, wsec);
 }
 
-__device__ __forceinline__ int clamp_uniq(const int32_t* n_uniq, long long cap) {
+__device__ __forceinline__ int clamp_uniq(const int32_t* n_uniq, long long cap, int* status = nullptr) {
   const int nu = n_uniq[0];
+  if (nu < 0 || nu > cap) index_fault(status);
   return nu < 0 ? 0 : (nu > cap ? (int)cap : nu);
 }
 

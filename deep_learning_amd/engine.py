@@ -1092,6 +1092,8 @@ class CTREngine:
         self._status_q.clear()
         if status & _lib.STATUS_LAG:
             raise _lib.DLError("internal: a row record lagged past the alpha ring (flush schedule)")
+        if status & _lib.STATUS_INDEX:
+            raise _lib.DLError("internal: batch index entry out of range (corrupt index)")
         raise _lib.DLError("InvalidArgumentError: categorical id out of range [0, %d) — the step of the "
                            "offending batch applied no update" % self.N)
 

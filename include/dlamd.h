@@ -329,6 +329,7 @@ int dl_slab_fold_rows(const float* slab, int32_t blocks, int32_t width, int32_t 
 #define DL_OPT_STATUS 16
 #define DL_STATUS_BAD_ID 1   /* a categorical / wide id outside [0, N) */
 #define DL_STATUS_LAG 2      /* a row record lagged past the alpha ring (flush schedule broken) */
+#define DL_STATUS_INDEX 4    /* a batch-index entry out of range (index consumers report, never skip silently) */
 int dl_adam_begin_step(float* opt, float decay_rate, float decay_steps, void* stream);
 /* opt[DL_OPT_STATUS] |= batch_err[0] (the batch's id-validation word, written by
  * dl_index_build / the forward kernels): issued before dl_adam_begin_step so the
