@@ -106,6 +106,13 @@ SIGNATURES = {
     "dl_rec_apply_chain": (I32, [P, I32, I32, I32, P, I64, P, P, P, P, P, I32, P, P]),
     "dl_auc_workspace_bytes": (I64, [I64]),
     "dl_auc": (I32, [P, I64, P, I64, I64, P, I64, P, P]),
+    "dl_comm_unique_id_bytes": (I32, []),
+    "dl_comm_get_unique_id": (I32, [P]),
+    "dl_comm_init": (I32, [P, I32, I32, P]),
+    "dl_comm_destroy": (I32, [P]),
+    "dl_all_to_allv": (I32, [P, P, P, P, P, I64, P]),
+    "dl_all_reduce_f32": (I32, [P, P, P, I64, P]),
+    "dl_all_gather": (I32, [P, P, P, I64, P]),
 }
 
 _LIB = None

@@ -594,7 +594,7 @@ extern "C" int dl_rec_bwd_adam(const dl_emb_layout* L, float* rec, int32_t rec_l
   DL_CHECK_ARG(!multi || (pool->dx0_pool_col % 4 == 0 && L->x0_pool_col % 4 == 0),
                "pool columns not float4 aligned");
   SegGradIn sg{*L, seg_off, sorted_refs, dz, w_head, fm_sum, dx0};
-  sg.status = opt_status(opt);
+  sg.status = reinterpret_cast<int*>(const_cast<float*>(opt) + DL_OPT_STATUS);   // opt_status(opt), host side
   const bool g1p = multi && L->use_fm && has_first;
   if (multi) {
     sg.slot_start = pool->slot_start; sg.slot_end = pool->slot_end; sg.n_slots = pool->n_slots;

@@ -52,3 +52,35 @@ class AucAccumulator:
         if not self.scores:
             raise ValueError(_SINGLE_CLASS)
         return roc_auc(torch.cat(self.labels), torch.cat(self.scores))
+
+
+class ShardedAucAccumulator(AucAccumulator):
+    """AUC over every rank's scores (row-sharded eval, shard.py): the local device scores and
+    labels are all-gathered (padded to the largest rank's count) and dl_auc runs on the global
+    concatenation, so every rank gets the single-GPU value of the whole set."""
+
+    def __init__(self, exch):
+        super().__init__()
+        self.exch = exch
+
+    def result(self):
+        import torch.distributed as dist
+        ex = self.exch
+        s = torch.cat(self.scores) if self.scores else torch.empty(0, device="cuda")
+        y = torch.cat(self.labels) if self.labels else torch.empty(0, device="cuda")
+        dev = "cpu" if ex.staged else "cuda"
+        n = torch.tensor([s.numel()], dtype=torch.int64, device=dev)
+        ns = [torch.empty_like(n) for _ in range(ex.world)]
+        dist.all_gather(ns, n, group=ex.group)
+        counts = [int(c.item()) for c in ns]
+        cap = max(counts)
+        if cap == 0:
+            raise ValueError(_SINGLE_CLASS)
+        pad = torch.zeros(2, cap, dtype=torch.float32, device=dev)
+        pad[0, : s.numel()] = s.to(dev)
+        pad[1, : y.numel()] = y.to(dev)
+        parts = [torch.empty_like(pad) for _ in range(ex.world)]
+        dist.all_gather(parts, pad, group=ex.group)
+        scores = torch.cat([p[0, :c] for p, c in zip(parts, counts)])
+        labels = torch.cat([p[1, :c] for p, c in zip(parts, counts)])
+        return roc_auc(labels, scores)

@@ -680,6 +680,85 @@ class ShardedCTREngine(CTREngine):
         self.last_loss_sum = None
         return B
 
+    # ------------------------------------------------------------ predict / eval
+    def predict(self, batch, logits=False, device=False):
+        """Forward only on this rank's batch (reference eval/predict, deepfm_pipeline.py:294-311):
+        the same index, id exchange and owner gather as a training step, rows caught up to the
+        last completed step (records are only read), no gradients, no update.  Every rank must
+        call it together (collectives).  Returns the sigmoid scores [B] (or logits) as host
+        numpy, or a device tensor copy with device=True."""
+        sp = self.spec
+        ex = self.exch
+        E = sp.E
+        pf = getattr(self, "_pf", None)
+        if pf is not None:   # a pending prefetch: let it land, drop it
+            torch.cuda.current_stream().wait_event(pf[2])
+            ex.resolve_counts(pf[4])
+            self._pf = None
+        B = self.stage(batch)
+        self._join_side()            # the last step's record update (side stream) has landed
+        s = _lib.stream_handle()
+        L = self.layout
+        L.batch = B
+        W = self.world
+        self._index(B)
+        cm = ex.count_matrix(self.owner_counts)
+        send = cm[self.rank][:W]
+        nsend, nrep = sum(send), cm[self.rank][W]
+        recv = [cm[r][self.rank] for r in range(W)]
+        nrecv = sum(recv)
+        recv_ids = ex.all_to_all(self.send_ids[:nsend], send, recv)
+        out_v = torch.empty(max(nrecv, 1), E, device=self.dev)
+        out_1 = torch.empty(max(nrecv, 1), device=self.dev)
+        if nrecv and self.lazy:   # lag 0: caught up to the last completed step, read only
+            call("dl_rec_gather", C_ref(L), ptr(self.rec), self.rec_ld, self.rec_flags, 0, ptr(recv_ids), None,
+                 nrecv, 1, ptr(self.hist), self.hist_len, ptr(self.opt), 0, ptr(out_v),
+                 ptr(out_1) if sp.fm else None, None, s)
+        elif nrecv:
+            call("dl_shard_gather", ptr(self.table), ptr(self.first), ptr(recv_ids), nrecv, E, ptr(out_v),
+                 ptr(out_1) if self.first is not None else None, s)
+        rep = self.rep
+        ex.all_to_all(out_v[:nrecv], recv, send, out=self.rows_u[rep: rep + nsend])
+        if sp.fm:
+            ex.all_to_all(out_1[:nrecv], recv, send, out=self.rows_u1[rep: rep + nsend])
+        if rep:
+            self.rows_u[:rep].copy_(self.rep_t[:rep])
+            if sp.fm:
+                self.rows_u1[:rep].copy_(self.rep_f[:rep])
+        if nrep:
+            call("dl_shard_gather", ptr(self.rep_t), ptr(self.rep_f) if sp.fm else None,
+                 ptr(self.send_ids[nsend:nsend + nrep]), nrep, E, ptr(self.rows_u[rep + nsend:]),
+                 ptr(self.rows_u1[rep + nsend:]) if sp.fm else None, s)
+        call("dl_embed_fwd_indexed", C_ref(L), ptr(self.rows_u), ptr(self.rows_u1) if sp.fm else None, ptr(self.inv),
+             rep, ptr(self.in_cont), ptr(self.in_vec), ptr(self.x0), ptr(self.fm_out), ptr(self.fm_sum), s)
+        x = self.x0
+        for l, hdim in enumerate(sp.hidden):
+            if self.s3:
+                call("dl_gemm_s3_nt", B, hdim, self.in_ld[l], ptr(x), self.in_ld[l], ptr(self.WTp[l]), self.in_ld[l],
+                     self.in_ld[l] * self.out_ld[l], ptr(self.h[l]), self.h_ld[l], 1, None, 0, s)
+            else:
+                call("dl_gemm_f32", 0, 0, B, hdim, self.in_ld[l], ptr(x), self.in_ld[l], ptr(self.W[l]),
+                     self.out_ld[l], ptr(self.h[l]), self.h_ld[l], 1, None, 0, 1, 0, s)
+            x = self.h[l]
+        H = sp.hidden[-1]
+        call("dl_head_fwd_bwd", B, sp.fm_cols, H, ptr(self.fm_out), self.fm_ld, ptr(self.h[-1]), self.h_ld[-1],
+             ptr(self.w_head), ptr(self.in_label), sp.logloss_eps, 1.0 / B, ptr(self.score), ptr(self.z),
+             ptr(self.dz), ptr(self.dh[-1]), ptr(self.head_slab), self.head_blocks, s)
+        self._release()
+        self.check_error()
+        out = (self.z if logits else self.score)[:B]
+        return out.clone() if device else out.cpu().numpy()
+
+    def evaluate(self, batches):
+        """Global ROC-AUC over every rank's batches (the reference's eval: sklearn roc_auc_score
+        over the whole validation set): scores stay on the device, one all-gather, then the
+        exact dl_auc on the concatenation — the same value on every rank."""
+        from .metrics import ShardedAucAccumulator
+        acc = ShardedAucAccumulator(self.exch)
+        for b in batches:
+            acc.add(b["label"], self.predict(b, device=True))
+        return acc.result()
+
     def loss(self):
         """Global loss of the last step: the all-reduced loss column + L2 on the head weights."""
         sp = self.spec

@@ -467,6 +467,27 @@ int dl_keys_to_local(const uint32_t* keys, const int32_t* n_uniq, int64_t cap, i
                      void* stream);
 
 /* ------------------------------------------------------------------------
+ * RCCL collectives of the row-sharded step (comm.cpp; SURVEY.md §8(b)3
+ * comm_init / all_to_allv / all_reduce), for a host that binds this library
+ * directly.  One communicator per rank (one GPU each); calls are stream-ordered.
+ * RCCL errors return 2000 + ncclResult_t.  The Python engine (shard.py) reaches the
+ * same RCCL through torch.distributed (backend "nccl").
+ *   dl_comm_get_unique_id: rank 0 creates the id (dl_comm_unique_id_bytes() bytes)
+ *     and ships it to the other ranks out of band (the reference-side launcher's job);
+ *   dl_all_to_allv: rows of row_bytes each, grouped by peer in rank order; counts are
+ *     host arrays of nranks row counts (the step's owner-count all-gather gives them);
+ *   dl_all_reduce_f32: sum, in place when send == recv;
+ *   dl_all_gather: `bytes` per rank into recv[nranks][bytes]. */
+int dl_comm_unique_id_bytes(void);
+int dl_comm_get_unique_id(void* id_out);
+int dl_comm_init(const void* unique_id, int32_t nranks, int32_t rank, void** comm_out);
+int dl_comm_destroy(void* comm);
+int dl_all_to_allv(void* comm, const void* send, const int64_t* send_counts, void* recv,
+                   const int64_t* recv_counts, int64_t row_bytes, void* stream);
+int dl_all_reduce_f32(void* comm, const float* send, float* recv, int64_t n, void* stream);
+int dl_all_gather(void* comm, const void* send, void* recv, int64_t bytes, void* stream);
+
+/* ------------------------------------------------------------------------
  * Utilities. */
 /* Counter-based (Philox-4x32-10) init: dist 0 normal(mean, scale), 1 uniform[mean, mean+scale). */
 int dl_init_random(float* p, int64_t n, int32_t dist, float mean, float scale, uint64_t seed,

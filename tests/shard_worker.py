@@ -150,6 +150,12 @@ def run_gpu(rank, world, steps, Bl, out_dir, adam="dense", prefetch=False, owner
         torch.cuda.synchronize()
         np.savez(os.path.join(out_dir, "rank%d_step%d.npz" % (rank, step)), z=eng.z[:Bl].cpu().numpy(),
                  loss=eng.loss())
+    # sharded eval (reference eval: predict every rank's half of two unseen global batches,
+    # one AUC over all of them)
+    evb = [local(bg, rank, world) for bg in global_batches(Bl * world, steps + 2)[steps:]]
+    scores = [eng.predict(b) for b in evb]
+    auc = eng.evaluate(evb)
+    np.savez(os.path.join(out_dir, "rank%d_eval.npz" % rank), s0=scores[0], s1=scores[1], auc=auc)
     rows, t, f = eng.shard_state()
     dense = {"W%d" % l: eng.W[l].cpu().numpy() for l in range(len(KW["hidden"]))}
     np.savez(os.path.join(out_dir, "rank%d.npz" % rank), rows=rows, table=t, first=f,
