@@ -106,6 +106,11 @@ SIGNATURES = {
     "dl_rec_apply_chain": (I32, [P, I32, I32, I32, P, I64, P, P, P, P, P, I32, P, P]),
     "dl_auc_workspace_bytes": (I64, [I64]),
     "dl_auc": (I32, [P, I64, P, I64, I64, P, I64, P, P]),
+    "dl_shard_gather_scalar": (I32, [P, P, I64, P, P]),
+    "dl_shard_add_fixed": (I32, [P, P, I64, P, P, P]),
+    "dl_wide_fold_owned": (I32, [P, I32, I64, I32, I32, P, P, P]),
+    "dl_wide_owned_values": (I32, [P, I32, I64, I32, I32, P, P]),
+    "dl_wide_local_ids": (I32, [P, I64, I64, P, P]),
     "dl_comm_unique_id_bytes": (I32, []),
     "dl_comm_get_unique_id": (I32, [P]),
     "dl_comm_init": (I32, [P, I32, I32, P]),

@@ -72,6 +72,60 @@ __global__ void keys_to_local_kernel(const uint32_t* __restrict__ keys, const in
     out[i] = (int32_t)(keys[i] & ((1u << 27) - 1));
 }
 
+// ---------------------------------------------------------------------------
+// Row-sharded wdl_weights (wdl.py:241-285; the wide / deep cross-logit weights, sharded like
+// the table: row r on rank r % world at local row r / world).
+__global__ __launch_bounds__(256) void shard_gather_scalar_kernel(const float* __restrict__ w,
+                                                                  const int32_t* __restrict__ ids, long long n,
+                                                                  float* __restrict__ out) {
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x)
+    out[i] = w[ids[i]];
+}
+
+// Arrived per-row wide gradients (int64 fixed point, the sender's segment sums) added to the
+// owner's gradient: integer atomics, so the sum does not depend on arrival order.
+__global__ __launch_bounds__(256) void shard_add_fixed_kernel(const int64_t* __restrict__ g,
+                                                              const int32_t* __restrict__ ids, long long n,
+                                                              int64_t* __restrict__ G, uint8_t* __restrict__ touched) {
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x) {
+    const int r = ids[i];
+    atomicAdd(reinterpret_cast<unsigned long long*>(G + r), (unsigned long long)g[i]);
+    if (touched) touched[r] = 1;
+  }
+}
+
+// The deep-output rows row0 + j (j < H; the all-reduced batch sums of dz*h) that this rank owns,
+// folded into its fixed-point gradient.
+__global__ void wide_fold_owned_kernel(const float* __restrict__ gdeep, int H, long long row0, int world, int rank,
+                                       int64_t* __restrict__ G, uint8_t* __restrict__ touched) {
+  for (int j = blockIdx.x * blockDim.x + threadIdx.x; j < H; j += gridDim.x * blockDim.x) {
+    const long long r = row0 + j;
+    if (r % world != rank) continue;
+    const long long lr = r / world;
+    atomicAdd(reinterpret_cast<unsigned long long*>(G + lr), (unsigned long long)wide_fixed(gdeep[j]));
+    if (touched) touched[lr] = 1;
+  }
+}
+
+// out[j] = this rank's value of row row0 + j if it owns it, else 0 (summed over ranks: the
+// replicated copy of the deep-output rows every rank's cross logit reads).
+__global__ void wide_owned_values_kernel(const float* __restrict__ w, int H, long long row0, int world, int rank,
+                                         float* __restrict__ out) {
+  for (int j = blockIdx.x * blockDim.x + threadIdx.x; j < H; j += gridDim.x * blockDim.x) {
+    const long long r = row0 + j;
+    out[j] = (r % world == rank) ? w[r / world] : 0.f;
+  }
+}
+
+// ids of the local wide table: out[k] = offset + inv[k] (-1 for a reference without a row)
+__global__ __launch_bounds__(256) void wide_local_ids_kernel(const int32_t* __restrict__ inv, long long n,
+                                                             long long offset, int64_t* __restrict__ out) {
+  for (long long k = (long long)blockIdx.x * blockDim.x + threadIdx.x; k < n; k += (long long)gridDim.x * blockDim.x) {
+    const int u = inv[k];
+    out[k] = u < 0 ? -1 : offset + u;
+  }
+}
+
 static int grid_of(long long n) {
   long long g = (n + 255) / 256;
   if (g > 8192) g = 8192;
@@ -120,4 +174,47 @@ extern "C" int dl_keys_to_local(const uint32_t* keys, const int32_t* n_uniq, int
   hipLaunchKernelGGL(keys_to_local_kernel, dim3(grid_of(cap)), dim3(256), 0, as_stream(stream), keys, n_uniq,
                      (long long)cap, out);
   DL_RETURN_LAUNCH("dl_keys_to_local");
+}
+
+extern "C" int dl_shard_gather_scalar(const float* w, const int32_t* ids, int64_t n, float* out, void* stream) {
+  DL_CHECK_ARG(w && ids && out, "NULL argument");
+  if (n <= 0) return 0;
+  hipLaunchKernelGGL(shard_gather_scalar_kernel, dim3(grid_of(n)), dim3(256), 0, as_stream(stream), w, ids,
+                     (long long)n, out);
+  DL_RETURN_LAUNCH("dl_shard_gather_scalar");
+}
+
+extern "C" int dl_shard_add_fixed(const int64_t* g, const int32_t* ids, int64_t n, int64_t* G, uint8_t* touched,
+                                  void* stream) {
+  DL_CHECK_ARG(g && ids && G, "NULL argument");
+  if (n <= 0) return 0;
+  hipLaunchKernelGGL(shard_add_fixed_kernel, dim3(grid_of(n)), dim3(256), 0, as_stream(stream), g, ids, (long long)n,
+                     G, touched);
+  DL_RETURN_LAUNCH("dl_shard_add_fixed");
+}
+
+extern "C" int dl_wide_fold_owned(const float* gdeep, int32_t H, int64_t row0, int32_t world, int32_t rank, int64_t* G,
+                                  uint8_t* touched, void* stream) {
+  DL_CHECK_ARG(gdeep && G && H >= 0 && world >= 1 && rank >= 0 && rank < world, "bad args");
+  if (H == 0) return 0;
+  hipLaunchKernelGGL(wide_fold_owned_kernel, dim3(1), dim3(256), 0, as_stream(stream), gdeep, H, (long long)row0, world,
+                     rank, G, touched);
+  DL_RETURN_LAUNCH("dl_wide_fold_owned");
+}
+
+extern "C" int dl_wide_owned_values(const float* w, int32_t H, int64_t row0, int32_t world, int32_t rank, float* out,
+                                    void* stream) {
+  DL_CHECK_ARG(w && out && H >= 0 && world >= 1 && rank >= 0 && rank < world, "bad args");
+  if (H == 0) return 0;
+  hipLaunchKernelGGL(wide_owned_values_kernel, dim3(1), dim3(256), 0, as_stream(stream), w, H, (long long)row0, world,
+                     rank, out);
+  DL_RETURN_LAUNCH("dl_wide_owned_values");
+}
+
+extern "C" int dl_wide_local_ids(const int32_t* inv, int64_t n, int64_t offset, int64_t* out, void* stream) {
+  DL_CHECK_ARG(inv && out, "NULL argument");
+  if (n <= 0) return 0;
+  hipLaunchKernelGGL(wide_local_ids_kernel, dim3(grid_of(n)), dim3(256), 0, as_stream(stream), inv, (long long)n,
+                     (long long)offset, out);
+  DL_RETURN_LAUNCH("dl_wide_local_ids");
 }

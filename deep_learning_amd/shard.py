@@ -143,8 +143,8 @@ class ShardedCTREngine(CTREngine):
 
     def __init__(self, spec, max_batch, exch, device="cuda", seed=2019, adam="dense", hist_len=4096,
                  owner_update=None):
-        if spec.model not in ("deepfm_pipeline", "dnn_pipeline"):
-            raise ValueError("sharded path supports deepfm_pipeline / dnn_pipeline")
+        if spec.model not in ("deepfm_pipeline", "dnn_pipeline", "wdl"):
+            raise ValueError("sharded path supports deepfm_pipeline / dnn_pipeline / wdl")
         self.exch = exch
         self.world, self.rank = exch.world, exch.rank
         N = spec.n_rows
@@ -208,6 +208,50 @@ class ShardedCTREngine(CTREngine):
         self.flat = z(off)
         if self.rep:
             self.rep_touched[: self.rep] = 1
+        if self.wdl:
+            self._init_wide(max_batch)
+
+    def _init_wide(self, B):
+        """wdl_weights sharded like the table (row r on rank r % world), plus the per-rank local
+        wide table the cross logit reads: wloc = [unused (Fw) | deep-output rows Fw..Fw+H,
+        replicated | this batch's exchanged unique wide rows].  The head (dl_wdl_head_fwd_bwd)
+        then runs unchanged on local ids and leaves each unique row's gradient in wgloc."""
+        sp = self.spec
+        W = self.world
+        z = lambda *sh, dt=torch.float32: torch.zeros(*sh, dtype=dt, device=self.dev)
+        Fw, H = sp.Fw, sp.hidden[-1]
+        self.w_local = -(-self.w_rows // W)
+        wl = _ru(self.w_local, 16)
+        self.ww, self.wm, self.wv = z(wl), z(wl), z(wl)
+        self.wg = z(wl, dt=torch.int64)
+        self.w_touched = z(wl, dt=torch.uint8)
+        self.wide_reg = z(4)
+        nw = B * Fw
+        self.n_wrefs = nw
+        self.wloc_off = Fw + H
+        self.wloc_rows = Fw + H + nw
+        self.wloc = z(_ru(self.wloc_rows, 4))
+        self.wgloc = z(self.wloc_rows, dt=torch.int64)
+        self.in_wide_loc = z(B, Fw, dt=torch.int64)
+        self.deep_buf = z(_ru(H, 4))
+        # the wide ids' batch index (owner-grouped unique rows, inverse map), per buffer set
+        wsb = _lib.lib().dl_index_workspace_bytes(max(1, nw))
+        self.widx_ws = z(wsb, dt=torch.uint8)
+        self.widx_keys, self.widx_refs, self.widx_uniq = (z(nw, dt=torch.int32) for _ in range(3))
+        self.widx_off = z(nw + 1, dt=torch.int32)
+        self.widx_n = z(4, dt=torch.int32)
+        self.winv = z(nw, dt=torch.int32)
+        self.wowner_counts = z(W + 1, dt=torch.int32)
+        self.wsend_ids = z(nw, dt=torch.int32)
+        WL = _lib.EmbLayout()
+        WL.n_rows = self.w_rows
+        WL.batch = B
+        WL.emb_dim = sp.E
+        WL.cate_fields = Fw
+        WL.cate_ld = self.in_wide.shape[1]
+        WL.use_fm = 0
+        WL.zero_row0 = 0
+        self.wlayout = WL
 
     def _owner_buffers(self, n):
         """(Re)size the owner-side arrival-chain buffer for n received ids."""
@@ -239,7 +283,22 @@ class ShardedCTREngine(CTREngine):
         rows = self.owned_rows()
         ok = rows < N
         t = np.zeros((self.rows_pad, sp.E), np.float32)
-        t[: self.local_rows][ok] = P["feats_emb"][rows[ok]]
+        t[: self.local_rows][ok] = P[sp.table_key][rows[ok]]
+        if self.wdl:
+            self._pack(torch.from_numpy(t).to(self.dev), None) if self.lazy else self.table.copy_(torch.from_numpy(t))
+            for l in range(len(sp.hidden)):
+                self._set_layer(l, P["deep_%d" % l], P["deep_bias_%d" % l])
+            wrows = np.arange(self.w_local) * self.world + self.rank
+            wok = wrows < self.w_rows
+            w = np.zeros(self.ww.shape[0], np.float32)
+            w[: self.w_local][wok] = np.asarray(P["wdl_weights"], np.float32)[wrows[wok], 0]
+            self.ww.copy_(torch.from_numpy(w))
+            self.wb.zero_()
+            self.wb[:1].copy_(torch.from_numpy(np.asarray(P["wdl_bias"], np.float32).reshape(-1)))
+            H = sp.hidden[-1]
+            self.wloc[sp.Fw: sp.Fw + H].copy_(torch.from_numpy(np.asarray(P["wdl_weights"], np.float32)[sp.Fw: sp.Fw + H, 0]))
+            torch.cuda.synchronize()
+            return
         f = None
         if sp.fm:
             f = np.zeros(self.rows_pad, np.float32)
@@ -271,8 +330,21 @@ class ShardedCTREngine(CTREngine):
         if self.lazy:
             self.table = torch.zeros(self.rows_pad, sp.E, device=self.dev)
             self.first = torch.zeros(self.rows_pad, device=self.dev) if sp.fm else None
-        call("dl_init_random", ptr(self.table), self.table.numel(), 0, 0.0, 0.01, seed,
-             self.rank * self.table.numel() * 4, s)
+        if sp.xavier_table:   # wdl.py:44-47: glorot-uniform weight_mat
+            import math
+            lim = math.sqrt(6.0 / (self.N + sp.E))
+            call("dl_init_random", ptr(self.table), self.table.numel(), 1, -lim, 2 * lim, seed,
+                 self.rank * self.table.numel() * 4, s)
+        else:
+            call("dl_init_random", ptr(self.table), self.table.numel(), 0, 0.0, 0.01, seed,
+                 self.rank * self.table.numel() * 4, s)
+        if self.wdl:   # wdl.py:241-244, the shard's rows; the deep-output rows from their owners
+            import math
+            call("dl_init_random", ptr(self.ww), _ru(self.ww.numel(), 4), 0, 0.0, math.sqrt(2.0 / self.w_rows),
+                 seed + 3, self.rank * self.ww.numel(), s)
+            self.ww[self.w_local:].zero_()
+            self.wb[0] = float(np.random.default_rng(seed).standard_normal())
+            self._wide_refresh()
         if self.first is not None:
             call("dl_init_random", ptr(self.first), _ru(self.first.numel(), 4), 1, 0.0, 1.0, seed + 1,
                  self.rank * _ru(self.first.numel(), 4), s)
@@ -305,10 +377,10 @@ class ShardedCTREngine(CTREngine):
         sp = self.spec
         g1 = ptr(g1b) if sp.fm else None
         if self.owner_update == "chain":
-            return ("dl_rec_apply_chain", ptr(self.rec), self.rec_ld, sp.E, int(sp.fm), ptr(recv_ids), nrecv,
+            return ("dl_rec_apply_chain", ptr(self.rec), self.rec_ld, sp.E, self.rec_flags, ptr(recv_ids), nrecv,
                     ptr(self.own_head), ptr(self.own_next), ptr(gb), g1, ptr(self.hist), self.hist_len, ptr(opt),
                     stream)
-        return ("dl_rec_apply_segments", ptr(self.rec), self.rec_ld, sp.E, int(sp.fm), ptr(self.own_uniq),
+        return ("dl_rec_apply_segments", ptr(self.rec), self.rec_ld, sp.E, self.rec_flags, ptr(self.own_uniq),
                 ptr(self.own_off), ptr(self.own_n), nrecv, nrecv, ptr(self.own_pos), ptr(gb), g1, ptr(self.hist),
                 self.hist_len, ptr(opt), stream)
 
@@ -340,6 +412,87 @@ class ShardedCTREngine(CTREngine):
         f = self.first[: self.local_rows].cpu().numpy()[ok] if self.first is not None else None
         return rows[ok], t, f
 
+    def _wide_exchange(self, B, cmw):
+        """The wide lookup: unique wide rows' ids to their owners, the owners' current values
+        back into the local wide table, local ids for the head.  Returns (send, recv, recv_ids)
+        for the gradient return."""
+        ex = self.exch
+        W = self.world
+        s = _lib.stream_handle()
+        wsend = cmw[self.rank][:W]
+        nwsend = sum(wsend)
+        wrecv = [cmw[r][self.rank] for r in range(W)]
+        nwrecv = sum(wrecv)
+        wrecv_ids = ex.all_to_all(self.wsend_ids[:nwsend], wsend, wrecv)
+        wout = torch.empty(max(nwrecv, 1), device=self.dev)
+        if nwrecv:
+            call("dl_shard_gather_scalar", ptr(self.ww), ptr(wrecv_ids), nwrecv, ptr(wout), s)
+        off = self.wloc_off
+        ex.all_to_all(wout[:nwrecv], wrecv, wsend, out=self.wloc[off: off + nwsend])
+        call("dl_wide_local_ids", ptr(self.winv), B * self.spec.Fw, off, ptr(self.in_wide_loc), s)
+        return wsend, wrecv, wrecv_ids
+
+    def _wide_refresh(self):
+        """Every rank's copy of the deep-output rows Fw..Fw+H of wdl_weights (read by the cross
+        logit) from their owners: one [H] sum all-reduce."""
+        sp = self.spec
+        H = sp.hidden[-1]
+        call("dl_wide_owned_values", ptr(self.ww), H, sp.Fw, self.world, self.rank, ptr(self.deep_buf),
+             _lib.stream_handle())
+        self.exch.all_reduce(self.deep_buf)
+        self.wloc[sp.Fw: sp.Fw + H].copy_(self.deep_buf[:H])
+
+    def _tower_fwd(self, B, s):
+        """Deep tower forward from x0 (f32 / three-plane split on bf16 MFMA / bf16 tower)."""
+        sp = self.spec
+        nl = len(sp.hidden)
+        if self.bf:
+            xb = self.x0b
+            for l, hdim in enumerate(sp.hidden):
+                last = l == nl - 1
+                out = self.h[l] if last else self.hb[l]
+                self._c("gemm_fwd_l%d" % l, "dl_gemm_bf16", 0, 1, B, hdim, self.in_ld[l], ptr(xb), self.in_ld[l],
+                        ptr(self.WbT[l]), self.in_ld[l], ptr(out), self.h_ld[l], 0 if last else 1, 1, None, 0, 1,
+                        0, s)
+                if not last:
+                    xb = self.hb[l]
+            return
+        x = self.x0
+        for l, hdim in enumerate(sp.hidden):
+            if self.s3:
+                self._c("gemm_fwd_l%d" % l, "dl_gemm_s3_nt", B, hdim, self.in_ld[l], ptr(x), self.in_ld[l],
+                        ptr(self.WTp[l]), self.in_ld[l], self.in_ld[l] * self.out_ld[l], ptr(self.h[l]),
+                        self.h_ld[l], 1, None, 0, s)
+            else:
+                self._c("gemm_fwd_l%d" % l, "dl_gemm_f32", 0, 0, B, hdim, self.in_ld[l], ptr(x), self.in_ld[l],
+                        ptr(self.W[l]), self.out_ld[l], ptr(self.h[l]), self.h_ld[l], 1, None, 0, 1, 0, s)
+            x = self.h[l]
+
+    def _head(self, B, s, train=True):
+        """Output layer + loss: the FM / deep_res head, or the wdl cross logit on the local
+        wide table (gradients of the exchanged wide rows left in wgloc)."""
+        sp = self.spec
+        H = sp.hidden[-1]
+        inv_b = 1.0 / (B * self.world)
+        if self.wdl:
+            if train:
+                self.wgloc.zero_()
+            fn, dh_last = ("dl_wdl_head_fwd_bwd_bf16", self.dhb[-1]) if self.bf else ("dl_wdl_head_fwd_bwd", self.dh[-1])
+            self._c("head", fn, B, sp.Fw, H, ptr(self.in_wide_loc), sp.Fw, ptr(self.h[-1]), self.h_ld[-1],
+                    ptr(self.wloc), ptr(self.wb), self.wloc_rows, ptr(self.in_label), sp.logloss_eps, inv_b,
+                    ptr(self.score), ptr(self.z), ptr(self.dz), ptr(dh_last), ptr(self.wgloc) if train else None,
+                    None, ptr(self.head_slab), self.head_blocks, ptr(self.err), s)
+            return
+        self._c("head", "dl_head_fwd_bwd", B, sp.fm_cols, H, ptr(self.fm_out), self.fm_ld, ptr(self.h[-1]),
+                self.h_ld[-1], ptr(self.w_head), ptr(self.in_label), sp.logloss_eps, inv_b, ptr(self.score),
+                ptr(self.z), ptr(self.dz), ptr(self.dh[-1]), ptr(self.head_slab), self.head_blocks, s)
+
+    def wide_state(self):
+        """(global rows, wdl_weights values) of this rank's shard of wdl_weights (host numpy)."""
+        rows = np.arange(self.w_local) * self.world + self.rank
+        ok = rows < self.w_rows
+        return rows[ok], self.ww[: self.w_local].cpu().numpy()[ok]
+
     def _mid_a(self, B):
         """Steps 5-6a: forward, head, the input-gradient chain down to dx0 and the per-row
         embedding gradients — fixed buffers and sizes for a batch size, so
@@ -354,26 +507,29 @@ class ShardedCTREngine(CTREngine):
         rep = self.rep
         # 5. forward
         self._c("embed_fwd", "dl_embed_fwd_indexed", C_ref(L), ptr(self.rows_u), ptr(self.rows_u1) if sp.fm else None,
-                ptr(self.inv), rep, ptr(self.in_cont), ptr(self.in_vec), ptr(self.x0), ptr(self.fm_out),
-                ptr(self.fm_sum), s)
-        x = self.x0
-        for l, hdim in enumerate(sp.hidden):
-            if self.s3:
-                self._c("gemm_fwd_l%d" % l, "dl_gemm_s3_nt", B, hdim, self.in_ld[l], ptr(x), self.in_ld[l],
-                        ptr(self.WTp[l]), self.in_ld[l], self.in_ld[l] * self.out_ld[l], ptr(self.h[l]),
-                        self.h_ld[l], 1, None, 0, s)
-            else:
-                self._c("gemm_fwd_l%d" % l, "dl_gemm_f32", 0, 0, B, hdim, self.in_ld[l], ptr(x), self.in_ld[l],
-                        ptr(self.W[l]), self.out_ld[l], ptr(self.h[l]), self.h_ld[l], 1, None, 0, 1, 0, s)
-            x = self.h[l]
-        H = sp.hidden[-1]
-        inv_b = 1.0 / (B * W)
-        self._c("head", "dl_head_fwd_bwd", B, sp.fm_cols, H, ptr(self.fm_out), self.fm_ld, ptr(self.h[-1]),
-                self.h_ld[-1], ptr(self.w_head), ptr(self.in_label), sp.logloss_eps, inv_b, ptr(self.score),
-                ptr(self.z), ptr(self.dz), ptr(self.dh[-1]), ptr(self.head_slab), self.head_blocks, s)
+                ptr(self.inv), rep, ptr(self.in_cont), ptr(self.in_vec), ptr(self.x0b if self.x0_direct else self.x0),
+                ptr(self.fm_out), ptr(self.fm_sum), s)
+        if self.bf and not self.x0_direct:
+            self._c("cast_x0", "dl_cast_bf16", ptr(self.x0), B, self.in_ld[0], self.in_ld[0], ptr(self.x0b),
+                    self.in_ld[0], s)
+        self._tower_fwd(B, s)
+        self._head(B, s)
         # 6a. input gradients, top layer down
         nl = len(sp.hidden)
+        if self.bf and not self.wdl:
+            self._c("cast_dh", "dl_cast_bf16", ptr(self.dh[-1]), B, self.h_ld[-1], self.h_ld[-1], ptr(self.dhb[-1]),
+                    self.h_ld[-1], s)
         for l in reversed(range(nl)):
+            if self.bf:
+                if l > 0:   # dX = dY . W^T, ReluGrad by the bf16 activations, bf16 out
+                    self._c("gemm_dx_l%d" % l, "dl_gemm_bf16", 0, 1, B, sp.hidden[l - 1], self.out_ld[l],
+                            ptr(self.dhb[l]), self.h_ld[l], ptr(self.Wb[l]), self.out_ld[l], ptr(self.dhb[l - 1]),
+                            self.h_ld[l - 1], 1, 2, ptr(self.hb[l - 1]), self.h_ld[l - 1], 1, 0, s)
+                else:       # dx0 stays fp32 for the embedding backward
+                    self._c("gemm_dx_l0", "dl_gemm_bf16", 0, 1, B, self.dx_cols, self.out_ld[0], ptr(self.dhb[0]),
+                            self.h_ld[0], ptr(self.Wb[0]), self.out_ld[0], ptr(self.dx0), self.dx_ld, 0, 0, None, 0,
+                            1, 0, s)
+                continue
             if self.s3:
                 i, o = self.in_ld[l], self.out_ld[l]
                 if l > 0:
@@ -409,17 +565,22 @@ class ShardedCTREngine(CTREngine):
             xin = self.x0 if l == 0 else self.h[l - 1]
             hdim = sp.hidden[l]
             stride = self.in_ld[l] * self.out_ld[l]
-            if self.s3:
+            if self.bf:
+                xl = self.x0b if l == 0 else self.hb[l - 1]
+                self._c("gemm_dw_l%d" % l, "dl_gemm_bf16", 1, 0, self.in_ld[l], hdim, B, ptr(xl), self.in_ld[l],
+                        ptr(self.dhb[l]), self.h_ld[l], ptr(self.w_slab), self.out_ld[l], 0, 3, None, 0, splits,
+                        stride, s)
+            elif self.s3:
                 self._c("gemm_dw_l%d" % l, "dl_gemm_s3_tn", self.in_ld[l], hdim, B, ptr(xin), self.in_ld[l],
                         ptr(self.dh[l]), self.h_ld[l], ptr(self.w_slab), self.out_ld[l], splits, stride, s)
             else:
                 self._c("gemm_dw_l%d" % l, "dl_gemm_f32", 1, 0, self.in_ld[l], hdim, B, ptr(xin), self.in_ld[l],
                         ptr(self.dh[l]), self.h_ld[l], ptr(self.w_slab), self.out_ld[l], 3, None, 0, splits, stride,
                         s)
-            call("dl_slab_sum", ptr(self.w_slab), _num_splits(B, splits, 64 if self.s3 else 16), stride, stride,
-                 ptr(self.flat[self.seg[l][1]:]), s)
+            call("dl_slab_sum", ptr(self.w_slab), _num_splits(B, splits, 64 if (self.s3 or self.bf) else 16), stride,
+                 stride, ptr(self.flat[self.seg[l][1]:]), s)
         hoff = self.seg[nl][1]
-        call("dl_slab_sum", ptr(self.head_slab), call_int("dl_head_grid", B), self.head_w, self.head_w,
+        call("dl_slab_sum", ptr(self.head_slab), call_int(self.head_grid, B), self.head_w, self.head_w,
              ptr(self.flat[hoff:]), s)
 
     def _mid(self, B):
@@ -441,7 +602,8 @@ class ShardedCTREngine(CTREngine):
         g[0].replay()
 
     # ------------------------------------------------------------ step
-    SLOT_ATTRS = CTREngine.SLOT_ATTRS + ("inv", "owner_counts", "send_ids")
+    SLOT_ATTRS = CTREngine.SLOT_ATTRS + ("inv", "owner_counts", "send_ids", "widx_ws", "widx_keys", "widx_refs",
+                                         "widx_uniq", "widx_off", "widx_n", "winv", "wowner_counts", "wsend_ids")
 
     def _index(self, B):
         """Step 1 on the current stream: the batch index (rows grouped by owner, replicated rows
@@ -453,6 +615,21 @@ class ShardedCTREngine(CTREngine):
                 ptr(self.idx_ws), self.idx_ws.numel(), ptr(self.idx_keys), ptr(self.idx_refs), ptr(self.idx_uniq),
                 ptr(self.idx_off), ptr(self.idx_n), ptr(self.inv), ptr(self.owner_counts), ptr(self.err), s)
         call("dl_keys_to_local", ptr(self.idx_uniq), ptr(self.idx_n), self.n_refs, ptr(self.send_ids), s)
+        if self.wdl:   # the wide ids: unique wdl_weights rows grouped by owner, inverse map
+            WL = self.wlayout
+            WL.batch = B
+            self._c("index_build_wide", "dl_index_build", C_ref(WL), ptr(self.in_wide), self.world, 0,
+                    ptr(self.widx_ws), self.widx_ws.numel(), ptr(self.widx_keys), ptr(self.widx_refs),
+                    ptr(self.widx_uniq), ptr(self.widx_off), ptr(self.widx_n), ptr(self.winv),
+                    ptr(self.wowner_counts), ptr(self.err), s)
+            call("dl_keys_to_local", ptr(self.widx_uniq), ptr(self.widx_n), self.n_wrefs, ptr(self.wsend_ids), s)
+
+    def _count_vec(self):
+        """The per-owner counts every rank all-gathers: table rows (+ replicated), and for wdl
+        the wide rows too (one collective for both)."""
+        if self.wdl:
+            return torch.cat([self.owner_counts, self.wowner_counts])
+        return self.owner_counts
 
     def prefetch(self, batch):
         """Stage the next batch, build its index and exchange its counts on the side stream
@@ -473,7 +650,7 @@ class ShardedCTREngine(CTREngine):
             with torch.cuda.stream(side):
                 B = self.stage(batch)
                 self._index(B)
-                counts = self.exch.count_matrix_async(self.owner_counts)
+                counts = self.exch.count_matrix_async(self._count_vec())
                 ev = torch.cuda.Event()
                 ev.record(side)
         finally:
@@ -513,9 +690,10 @@ class ShardedCTREngine(CTREngine):
         if counts is None:
             # 1. index + 2. counts: every rank's per-owner counts in one all-gather (host waits)
             self._index(B)
-            cm = ex.count_matrix(self.owner_counts)
+            cm = ex.count_matrix(self._count_vec())
         else:
             cm = ex.resolve_counts(counts)
+        cmw = [row[W + 1:] for row in cm] if self.wdl else None
         self._mark("index_launched")
         send = cm[self.rank][:W]
         nsend, nrep = sum(send), cm[self.rank][W]
@@ -538,7 +716,7 @@ class ShardedCTREngine(CTREngine):
         if nrecv and lazy:   # rows caught up to the previous step (read only)
             if self.apply_done is not None:   # the previous step's record update (side stream)
                 torch.cuda.current_stream().wait_event(self.apply_done)
-            self._c("rec_gather", "dl_rec_gather", C_ref(L), ptr(self.rec), self.rec_ld, int(sp.fm), 0,
+            self._c("rec_gather", "dl_rec_gather", C_ref(L), ptr(self.rec), self.rec_ld, self.rec_flags, 0,
                     ptr(recv_ids), None, nrecv, 1, ptr(self.hist), self.hist_len, ptr(self.opt), 1, ptr(out_v),
                     ptr(out_1) if sp.fm else None, None, s)
         elif nrecv:
@@ -577,6 +755,7 @@ class ShardedCTREngine(CTREngine):
             call("dl_shard_gather", ptr(self.rep_t), ptr(self.rep_f) if sp.fm else None,
                  ptr(self.send_ids[nsend:U]), nrep, E, ptr(self.rows_u[rep + nsend:]),
                  ptr(self.rows_u1[rep + nsend:]) if sp.fm else None, s)
+        wx = self._wide_exchange(B, cmw) if self.wdl else None
         self._mark("rows_a2a")
         if next_batch is not None:
             # after this step's row exchange is queued: the count all-gather it issues sits
@@ -592,6 +771,9 @@ class ShardedCTREngine(CTREngine):
         # embedding gradients to their owners, in flight while the weight gradients run
         gb, w_g = ex.all_to_all(self.gU[:nsend], send, recv, async_op=True)
         g1b, w_g1 = ex.all_to_all(self.g1U[:nsend], send, recv, async_op=True) if sp.fm else (None, None)
+        if self.wdl:   # the exchanged wide rows' gradients (int64 fixed point) back to their owners
+            off = self.wloc_off
+            wg_in, w_gw = ex.all_to_all(self.wgloc[off: off + sum(wx[0])], wx[0], wx[1], async_op=True)
         if replay:
             self._replay("graph_b%d" % slot, self._mid_b, B)
         else:
@@ -627,13 +809,35 @@ class ShardedCTREngine(CTREngine):
         ex.all_reduce(self.flat)
         self._mark("all_reduce")
         # 8. TF1 Adam
+        reg = sp.hidden_reg   # wdl: L2 on every hidden weight matrix (wdl.py:272-275), bias row excluded
         for l in range(nl):
             off, sz = self.seg[l][1], self.seg[l][2]
-            self._c("adam_dense_l%d" % l, "dl_adam_dense", ptr(self.W[l]), ptr(self.Wm[l]), ptr(self.Wv[l]),
-                    ptr(self.flat[off:]), 1, sz, sz, 0.0, 0, ptr(self.opt), None, None, s)
+            l2, l2n = (sp.l2, ([self.D0] + sp.hidden)[l] * self.out_ld[l]) if reg else (0.0, 0)
+            self._c("adam_dense_l%d" % l, "dl_adam_dense_reg", ptr(self.W[l]), ptr(self.Wm[l]), ptr(self.Wv[l]),
+                    ptr(self.flat[off:]), 1, sz, sz, l2, l2n, 1 if reg == "l1" else 0, ptr(self.opt), None,
+                    ptr(self.opt[8:]) if reg else None, s)
             self._refresh_wb(l, s)
-        self._c("adam_head", "dl_adam_dense", ptr(self.w_head), ptr(self.hm), ptr(self.hv), ptr(self.flat[hoff:]),
-                1, self.head_w, self.head_n, sp.l2, self.head_n - 1, ptr(self.opt), ptr(self.w_head_prev), None, s)
+        if self.wdl:
+            H = sp.hidden[-1]
+            self._c("adam_bias", "dl_adam_dense", ptr(self.wb), ptr(self.wbm), ptr(self.wbv), ptr(self.flat[hoff + H:]),
+                    1, 1, 1, 0.0, 0, ptr(self.opt), None, None, s)
+            # owners: arrived wide-row gradients + the deep-output rows they own, then the dense
+            # L2 Adam sweep over the shard of wdl_weights (wdl.py:270-271)
+            if w_gw is not None:
+                w_gw.wait()
+            nwrecv = sum(wx[1])
+            call("dl_shard_add_fixed", ptr(wg_in), ptr(wx[2]), nwrecv, ptr(self.wg), ptr(self.w_touched), s)
+            call("dl_wide_fold_owned", ptr(self.flat[hoff:]), H, sp.Fw, W, self.rank, ptr(self.wg),
+                 ptr(self.w_touched), s)
+            self.wide_reg.zero_()
+            self._c("adam_wide", "dl_adam_rows", ptr(self.ww), ptr(self.wm), ptr(self.wv), ptr(self.wg),
+                    ptr(self.w_touched), self.ww.shape[0], 1, sp.l2, 1 | _lib.ROWS_GRAD_FIXED, ptr(self.opt),
+                    ptr(self.wide_reg), s)
+            self._wide_refresh()
+        else:
+            self._c("adam_head", "dl_adam_dense", ptr(self.w_head), ptr(self.hm), ptr(self.hv), ptr(self.flat[hoff:]),
+                    1, self.head_w, self.head_n, sp.l2, self.head_n - 1, ptr(self.opt), ptr(self.w_head_prev), None,
+                    s)
         if rep:
             self.rep_g.view(-1)[: rg.numel()].copy_(rg.reshape(-1))
             self.rep_fg[: rg1.numel()].copy_(rg1)
@@ -672,7 +876,7 @@ class ShardedCTREngine(CTREngine):
                     ptr(self.touched), self.first.shape[0], 1, 0.0, 1, ptr(self.opt), None, s)
         else:
             self._c("adam_table", "dl_adam_rows", ptr(self.table), ptr(self.tm), ptr(self.tv), ptr(self.tg),
-                    ptr(self.touched), self.table.shape[0], E, 0.0, 1, ptr(self.opt), None, s)
+                    ptr(self.touched), self.table.shape[0], E, 0.0, 1 | self.rows_sparse, ptr(self.opt), None, s)
         self._release()
         self._mark("end")
         self.steps += 1
@@ -702,7 +906,8 @@ class ShardedCTREngine(CTREngine):
         L.batch = B
         W = self.world
         self._index(B)
-        cm = ex.count_matrix(self.owner_counts)
+        cm = ex.count_matrix(self._count_vec())
+        cmw = [row[W + 1:] for row in cm] if self.wdl else None
         send = cm[self.rank][:W]
         nsend, nrep = sum(send), cm[self.rank][W]
         recv = [cm[r][self.rank] for r in range(W)]
@@ -729,21 +934,15 @@ class ShardedCTREngine(CTREngine):
             call("dl_shard_gather", ptr(self.rep_t), ptr(self.rep_f) if sp.fm else None,
                  ptr(self.send_ids[nsend:nsend + nrep]), nrep, E, ptr(self.rows_u[rep + nsend:]),
                  ptr(self.rows_u1[rep + nsend:]) if sp.fm else None, s)
+        if self.wdl:
+            self._wide_exchange(B, cmw)
         call("dl_embed_fwd_indexed", C_ref(L), ptr(self.rows_u), ptr(self.rows_u1) if sp.fm else None, ptr(self.inv),
-             rep, ptr(self.in_cont), ptr(self.in_vec), ptr(self.x0), ptr(self.fm_out), ptr(self.fm_sum), s)
-        x = self.x0
-        for l, hdim in enumerate(sp.hidden):
-            if self.s3:
-                call("dl_gemm_s3_nt", B, hdim, self.in_ld[l], ptr(x), self.in_ld[l], ptr(self.WTp[l]), self.in_ld[l],
-                     self.in_ld[l] * self.out_ld[l], ptr(self.h[l]), self.h_ld[l], 1, None, 0, s)
-            else:
-                call("dl_gemm_f32", 0, 0, B, hdim, self.in_ld[l], ptr(x), self.in_ld[l], ptr(self.W[l]),
-                     self.out_ld[l], ptr(self.h[l]), self.h_ld[l], 1, None, 0, 1, 0, s)
-            x = self.h[l]
-        H = sp.hidden[-1]
-        call("dl_head_fwd_bwd", B, sp.fm_cols, H, ptr(self.fm_out), self.fm_ld, ptr(self.h[-1]), self.h_ld[-1],
-             ptr(self.w_head), ptr(self.in_label), sp.logloss_eps, 1.0 / B, ptr(self.score), ptr(self.z),
-             ptr(self.dz), ptr(self.dh[-1]), ptr(self.head_slab), self.head_blocks, s)
+             rep, ptr(self.in_cont), ptr(self.in_vec), ptr(self.x0b if self.x0_direct else self.x0), ptr(self.fm_out),
+             ptr(self.fm_sum), s)
+        if self.bf and not self.x0_direct:
+            call("dl_cast_bf16", ptr(self.x0), B, self.in_ld[0], self.in_ld[0], ptr(self.x0b), self.in_ld[0], s)
+        self._tower_fwd(B, s)
+        self._head(B, s, train=False)
         self._release()
         self.check_error()
         out = (self.z if logits else self.score)[:B]
@@ -760,9 +959,18 @@ class ShardedCTREngine(CTREngine):
         return acc.result()
 
     def loss(self):
-        """Global loss of the last step: the all-reduced loss column + L2 on the head weights."""
+        """Global loss of the last step: the all-reduced loss column + L2 on the head weights
+        (wdl: + L2 on every hidden weight matrix and on all of wdl_weights, whose shard sums are
+        all-reduced here — every rank calls it)."""
         sp = self.spec
         hoff = self.seg[len(sp.hidden)][1]
+        if self.wdl:
+            H = sp.hidden[-1]
+            data = float(self.flat[hoff + H + 1].item())
+            wr = self.wide_reg.clone()
+            self.exch.all_reduce(wr)
+            return data / (self.last_batch * self.world) + sp.l2 * 0.5 * (float(self.opt[8].item()) +
+                                                                           float(wr[0].item()))
         data = float(self.flat[hoff + self.head_w - 1].item())
         w = self.w_head_prev[: self.head_n - 1].double()
         return data / (self.last_batch * self.world) + sp.l2 * 0.5 * float((w * w).sum().item())

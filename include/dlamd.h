@@ -466,6 +466,24 @@ int dl_slab_sum(const float* slab, int32_t nslab, int64_t stride, int64_t n, flo
 int dl_keys_to_local(const uint32_t* keys, const int32_t* n_uniq, int64_t cap, int32_t* out,
                      void* stream);
 
+/* Row-sharded wdl_weights (wdl.py:241-285): row r on rank r % world, local r / world.
+ * dl_shard_gather_scalar: out[i] = w[ids[i]] (owner side of the wide lookup);
+ * dl_shard_add_fixed: G[ids[i]] += g[i] (int64 fixed point, integer atomics: order-free);
+ * dl_wide_fold_owned: the deep-output rows row0 + j (j < H) this rank owns get
+ *   G[(row0+j)/world] += fixed(gdeep[j]) (gdeep: the all-reduced sums of dz*h);
+ * dl_wide_owned_values: out[j] = w[(row0+j)/world] if owned here, else 0 (sum over ranks =
+ *   the replicated deep-output rows);
+ * dl_wide_local_ids: out[k] = offset + inv[k] (-1 where inv < 0): wide ids into the
+ *   rank's local wide table (exchanged rows). */
+int dl_shard_gather_scalar(const float* w, const int32_t* ids, int64_t n, float* out, void* stream);
+int dl_shard_add_fixed(const int64_t* g, const int32_t* ids, int64_t n, int64_t* G, uint8_t* touched,
+                       void* stream);
+int dl_wide_fold_owned(const float* gdeep, int32_t H, int64_t row0, int32_t world, int32_t rank, int64_t* G,
+                       uint8_t* touched, void* stream);
+int dl_wide_owned_values(const float* w, int32_t H, int64_t row0, int32_t world, int32_t rank, float* out,
+                         void* stream);
+int dl_wide_local_ids(const int32_t* inv, int64_t n, int64_t offset, int64_t* out, void* stream);
+
 /* ------------------------------------------------------------------------
  * RCCL collectives of the row-sharded step (comm.cpp; SURVEY.md §8(b)3
  * comm_init / all_to_allv / all_reduce), for a host that binds this library

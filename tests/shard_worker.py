@@ -162,12 +162,55 @@ def run_gpu(rank, world, steps, Bl, out_dir, adam="dense", prefetch=False, owner
              rep=eng.rep_t[:KW["C"]].cpu().numpy(), head=eng.w_head.cpu().numpy(), **dense)
 
 
+WKW = dict(C=13, S=26, E=16, cate_index_size=8000, hidden=[32, 24], Fw=26)
+
+
+def wdl_batches(Bg, steps):
+    out = []
+    for i in range(steps):
+        b = make_batch(Bg, cont=WKW["C"], cate_fields=WKW["S"], cate_index_size=WKW["cate_index_size"], seed=300 + i,
+                       wide_fields=WKW["Fw"])
+        b["wide_feats"][0, :3] = [WKW["Fw"], WKW["Fw"] + 1, 3]   # wide ids aliasing deep-output rows
+        out.append(b)
+    return out
+
+
+def run_gpu_wdl(rank, world, steps, Bl, out_dir, adam, tower, prefetch):
+    """Row-sharded Wide&Deep (table and wdl_weights sharded, bf16 or fp32 tower)."""
+    from deep_learning_amd.engine import ModelSpec
+    from deep_learning_amd.shard import Exchange, ShardedCTREngine
+    torch.cuda.set_device(0)
+    ex = Exchange()
+    cfg = R.make_cfg("wdl", **WKW)
+    P = R.init_params(cfg, np.random.default_rng(42))
+    eng = ShardedCTREngine(ModelSpec("wdl", tower=tower, **WKW), Bl, ex, adam=adam, hist_len=4)
+    eng.load_params(P)
+    batches = [local(bg, rank, world) for bg in wdl_batches(Bl * world, steps)]
+    for step, b in enumerate(batches):
+        nxt = batches[step + 1] if prefetch and step + 1 < len(batches) else None
+        eng.train_step(b, graph=step >= 2, next_batch=nxt)
+        torch.cuda.synchronize()
+        np.savez(os.path.join(out_dir, "rank%d_step%d.npz" % (rank, step)), z=eng.z[:Bl].cpu().numpy(),
+                 loss=eng.loss())
+    evb = [local(bg, rank, world) for bg in wdl_batches(Bl * world, steps + 2)[steps:]]
+    scores = [eng.predict(b) for b in evb]
+    auc = eng.evaluate(evb)
+    rows, t, _ = eng.shard_state()
+    wrows, wv = eng.wide_state()
+    np.savez(os.path.join(out_dir, "rank%d.npz" % rank), rows=rows, table=t, wrows=wrows, ww=wv,
+             wb=eng.wb[:1].cpu().numpy(), s0=scores[0], s1=scores[1], auc=auc,
+             **{"W%d" % l: eng.W[l].cpu().numpy() for l in range(len(WKW["hidden"]))})
+
+
 if __name__ == "__main__":
     mode, steps, Bl, out_dir = sys.argv[1], int(sys.argv[2]), int(sys.argv[3]), sys.argv[4]
     dist.init_process_group("gloo")
     rank, world = dist.get_rank(), dist.get_world_size()
     if mode == "sim":
         run_sim(rank, world, steps, Bl, out_dir)
+    elif mode.startswith("gpu_wdl"):
+        run_gpu_wdl(rank, world, steps, Bl, out_dir, adam="lazy" if "lazy" in mode else "dense",
+                    tower="bf16" if "bf16" in mode else "f32", prefetch=mode.endswith("_pf"))
     else:
         run_gpu(rank, world, steps, Bl, out_dir, adam="lazy" if mode.startswith("gpu_lazy") else "dense",
                 prefetch=mode.endswith("_pf"), owner_update="chain" if "_chain" in mode else None)

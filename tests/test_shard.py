@@ -15,7 +15,7 @@ import pytest
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 from oracle import ctr_ref as R  # noqa: E402
-from tests.shard_worker import KW, global_batches  # noqa: E402
+from tests.shard_worker import KW, WKW, global_batches, wdl_batches  # noqa: E402
 
 STEPS, BL, WORLD = 5, 96, 2
 
@@ -98,3 +98,46 @@ def test_sharded_engine_two_ranks_equals_global_batch(tmp_path, mode):
     want_auc = R.auc(np.concatenate(all_y), np.concatenate(all_s))
     assert float(ev[0]["auc"]) == float(ev[1]["auc"])
     assert abs(float(ev[0]["auc"]) - want_auc) < 1e-4
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mode", ["gpu_wdl", "gpu_wdl_lazy_pf", "gpu_wdl_bf16_lazy"])
+def test_sharded_wdl_two_ranks_equals_global_batch(tmp_path, mode):
+    """Wide&Deep row-sharded (BASELINE C5 at N GPUs): weight_mat and wdl_weights split by rows
+    (r % world), the wide lookup and its fixed-point gradients exchanged, the deep-output rows
+    of wdl_weights (aliasing wide ids Fw..Fw+H) updated by their owners and re-broadcast.
+    Against the fp32 oracle on the global batch: 1e-5 for the fp32 tower, the bf16 tower's
+    stated tolerance (test_gpu_parity.py::test_wdl_bf16_tower_tracks_oracle) for bf16."""
+    _launch(mode, tmp_path)
+    bf = "bf16" in mode
+    ztol, ptol = (3e-2, 5e-3) if bf else (1e-5, 1e-5)
+    cfg = R.make_cfg("wdl", **WKW)
+    P = R.init_params(cfg, np.random.default_rng(42))
+    opt = R.AdamTF1(cfg, P)
+    for step, b in enumerate(wdl_batches(BL * WORLD, STEPS)):
+        fw = R.train_step(cfg, P, opt, b)
+        z = np.concatenate([np.load(tmp_path / ("rank%d_step%d.npz" % (r, step)))["z"] for r in range(WORLD)])
+        np.testing.assert_allclose(z, fw["z"], atol=ztol, rtol=0, err_msg="logits step %d" % step)
+        loss = float(np.load(tmp_path / ("rank0_step%d.npz" % step))["loss"])
+        assert abs(loss - fw["loss"]) < (5e-3 if bf else 1e-5), (step, loss, fw["loss"])
+    d = [np.load(tmp_path / ("rank%d.npz" % r)) for r in range(WORLD)]
+    table = np.zeros_like(P["weight_mat"])
+    ww = np.zeros_like(P["wdl_weights"][:, 0])
+    for e in d:
+        table[e["rows"]] = e["table"]
+        ww[e["wrows"]] = e["ww"]
+    np.testing.assert_allclose(table, P["weight_mat"], atol=ptol, rtol=0)
+    np.testing.assert_allclose(ww, P["wdl_weights"][:, 0], atol=ptol, rtol=0)
+    np.testing.assert_allclose(d[0]["wb"], P["wdl_bias"], atol=ptol, rtol=0)
+    np.testing.assert_array_equal(d[0]["W0"], d[1]["W0"])      # replicated dense state identical
+    # sharded eval on two unseen global batches
+    evb = wdl_batches(BL * WORLD, STEPS + 2)[STEPS:]
+    all_s, all_y = [], []
+    for j, b in enumerate(evb):
+        want = 1.0 / (1.0 + np.exp(-R.forward(cfg, P, b)["z"].astype(np.float64)))
+        got = np.concatenate([e["s%d" % j] for e in d])
+        np.testing.assert_allclose(got, want, atol=ztol, rtol=0, err_msg="eval batch %d" % j)
+        all_s.append(want)
+        all_y.append(b["label"].reshape(-1))
+    assert float(d[0]["auc"]) == float(d[1]["auc"])
+    assert abs(float(d[0]["auc"]) - R.auc(np.concatenate(all_y), np.concatenate(all_s))) < (2e-3 if bf else 1e-4)
