@@ -185,7 +185,7 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--workload", default="c2", choices=["c2", "c3", "c5"],
                     help="c2 DeepFM (the headline, default); c3 deepfm_multi_cate 6 multi-hot slots x 60; "
-                         "c5 Wide&Deep with the bf16 tower (single GPU)")
+                         "c5 Wide&Deep with the bf16 tower (single GPU, or row-sharded at N>1 / --sharded)")
     ap.add_argument("--no-graph", action="store_true", help="eager launches instead of hipGraph replay")
     ap.add_argument("--owner-update", default=None, choices=["sort", "chain"],
                     help="sharded owners: group arriving rows by a sort (default) or by arrival chains")
@@ -233,11 +233,12 @@ def main():
             dist.barrier()
 
     B = args.batch
-    if not args.vocab:
-        args.vocab = C2["per_field_vocab"] if not sharded else 100_000_000 // C2["S"]
     wl = args.workload
-    if wl != "c2" and world > 1:
-        raise SystemExit("--workload %s is single-GPU here; the multi-GPU path is C4 (default)" % wl)
+    if not args.vocab:
+        # C4 (the default multi-GPU workload): a 100M-row table; C5 keeps its 26 x 1M vocab at every N
+        args.vocab = C2["per_field_vocab"] if (not sharded or wl == "c5") else 100_000_000 // C2["S"]
+    if wl == "c3" and sharded:
+        raise SystemExit("--workload c3 is single-GPU here; the multi-GPU workloads are C4 (default) and C5")
     if wl == "c3":
         spec = ModelSpec("deepfm_multi_cate", C=0, V=0, S=C2["S"], E=C2["E"], cate_index_size=C2["S"] * args.vocab,
                          hidden=C2["hidden"], multi_ranges=[[60 * i, 60 * (i + 1), "slot%d" % i] for i in range(6)])
