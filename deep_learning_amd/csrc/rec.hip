@@ -29,6 +29,10 @@
 #include "rec.h"
 #include "segment.h"
 
+#ifndef DL_REC_FULL_LINES
+#define DL_REC_FULL_LINES 0
+#endif
+
 namespace dl {
 
 // ---------------------------------------------------------------------------
@@ -314,6 +318,11 @@ __global__ __launch_bounds__(256) void rec_bwd_adam_kernel(SegGradIn sg, float* 
       if (first) rec_adam(w, wm, wv, s.g1, alpha, c);
       *reinterpret_cast<float4*>(r + E) = make_float4(w, wm, wv, __int_as_float(t));
     }
+#if DL_REC_FULL_LINES
+    // the record's pad too (zeros): the row's last 128-B line is written whole, so no
+    // partially dirty line has to be merged with its old bytes below the L2
+    for (int o = 3 * E + 4 + 4 * q; o < c.ld; o += E) *reinterpret_cast<float4*>(r + o) = make_float4(0.f, 0.f, 0.f, 0.f);
+#endif
   }
 }
 

@@ -454,6 +454,49 @@ def test_pool_weighted_matches_oracle(hip_lib, E):
     np.testing.assert_array_equal(touched.cpu().numpy(), want_touched)
 
 
+@pytest.mark.gpu
+def test_textline_pooling_frozen_tag_slot(hip_lib):
+    """deep_learning_amd.textline (dnn_multi_textline.py:69-103): slots 'a', 'b' pooled from the
+    trainable table (row 0 zeroed), slot 'tag' from the frozen word2vec table (:45-47,85-88: read
+    directly, row 0 not zeroed, no gradient); counts bit-exact, pooled vectors and the table
+    gradient (non-tag slots only) against oracle.pool_weighted / pool_weighted_bwd."""
+    from oracle import ctr_ref as R
+    from deep_learning_amd.textline import TextlinePooling
+    rng = np.random.default_rng(5)
+    B, N, Nw, E = 257, 3000, 2000, 16
+    ranges = [[0, 20, "a"], [20, 50, "tag"], [50, 64, "b"]]
+    W = 64
+    V = (rng.standard_normal((N, E)) * 0.1).astype(np.float32)
+    w2v = (rng.standard_normal((Nw, E)) * 0.1).astype(np.float32)   # row 0 nonzero: tag padding counts
+    ids = rng.integers(1, Nw, (B, W))
+    ids[rng.random((B, W)) < 0.4] = 0
+    vals = (rng.random((B, W)) * 2).astype(np.float32)
+    Vz = V.copy()
+    Vz[0] = 0
+    ref, ref_cnt = [], []
+    for r in ranges:
+        tab = w2v if r[2] == "tag" else Vz
+        p, c = R.pool_weighted(tab, ids, vals, [r])
+        ref.append(p)
+        ref_cnt.append(c)
+    ref, ref_cnt = np.concatenate(ref, 1), np.concatenate(ref_cnt, 1)
+    dev = lambda a: torch.from_numpy(np.ascontiguousarray(a)).cuda()
+    tp = TextlinePooling(ranges, E, N, w2v=dev(w2v))
+    pooled, cnt = tp.forward(dev(V), dev(ids), dev(vals))
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(cnt.cpu().numpy(), ref_cnt)
+    np.testing.assert_allclose(pooled.cpu().numpy().reshape(B, 3, E), ref, rtol=1e-5, atol=1e-6)
+    d = rng.standard_normal((B, 3, E)).astype(np.float32)
+    g = torch.zeros(N, E, device="cuda")
+    touched = torch.zeros(N, dtype=torch.uint8, device="cuda")
+    tp.backward(dev(d.reshape(B, -1)), dev(ids), dev(vals), g, touched)
+    torch.cuda.synchronize()
+    keep = [0, 2]
+    G = R.pool_weighted_bwd(N, ids, vals.astype(np.float64), [ranges[m] for m in keep],
+                            ref_cnt[:, keep].astype(np.float64), d[:, keep].astype(np.float64))
+    np.testing.assert_allclose(g.cpu().numpy(), G, rtol=1e-5, atol=1e-6)
+
+
 def test_auc_gpu_matches_sklearn_goldens_and_oracle(hip_lib):
     """dl_auc (metrics.hip) against the committed sklearn goldens and the oracle on a
     tie-heavy 2M-sample set (float32 scores, as the reference's score tensor)."""
