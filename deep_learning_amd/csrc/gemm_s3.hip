@@ -228,19 +228,34 @@ __global__ __launch_bounds__(512) void gemm_s3_nt_kernel(S3Params p) {
   // each lane moves whole 16-B row pieces: ReLU / mask reads and stores as full row segments.
   float* tile = reinterpret_cast<float*>(lds) + wid * 16 * kNtEP;
   const float* __restrict__ Mk = p.mask;
+  constexpr int VPR = kNtBN / 4;                    // 52 float4 pieces per row
+  constexpr int NIT = (16 * VPR + 63) / 64;         // pieces per lane per half
 #pragma unroll
   for (int h = 0; h < 2; ++h) {
+    // the ReluGrad mask's pieces for this half are loaded first (all in flight together,
+    // under the tile's LDS writes), not one dependent round trip per piece
+    float4 mk4[EPI == S3_MASK ? NIT : 1];
+    if (EPI == S3_MASK) {
+#pragma unroll
+      for (int it = 0; it < NIT; ++it) {
+        const int q = lane + 64 * it;
+        const int rl = q / VPR, pc = q % VPR;
+        const int row = min(r0 + 16 * h + rl, p.M - 1), col = max(0, min(j0 + 4 * pc, p.N - 4));
+        mk4[it] = *reinterpret_cast<const float4*>(Mk + (long long)row * p.ldm + (col & ~3));
+      }
+    }
 #pragma unroll
     for (int f = 0; f < kNtNF; ++f)
 #pragma unroll
       for (int j = 0; j < 4; ++j) tile[(4 * kq + j) * kNtEP + 16 * f + cl] = acc[h][f][j];
     __builtin_amdgcn_s_waitcnt(0xc07f);             // lgkmcnt(0): this wave's tile writes landed
     __builtin_amdgcn_wave_barrier();
-    constexpr int VPR = kNtBN / 4;                  // 52 float4 pieces per row
-    for (int q = lane; q < 16 * VPR; q += 64) {
+#pragma unroll
+    for (int it = 0; it < NIT; ++it) {
+      const int q = lane + 64 * it;
       const int rl = q / VPR, pc = q % VPR;
       const int row = r0 + 16 * h + rl, col = j0 + 4 * pc;
-      if (row >= p.M || col >= p.N) continue;
+      if (q >= 16 * VPR || row >= p.M || col >= p.N) continue;
       float4 v = *reinterpret_cast<const float4*>(tile + rl * kNtEP + 4 * pc);
       if (EPI == S3_RELU) {
         v.x = fmaxf(v.x, 0.f); v.y = fmaxf(v.y, 0.f); v.z = fmaxf(v.z, 0.f); v.w = fmaxf(v.w, 0.f);
@@ -249,7 +264,7 @@ __global__ __launch_bounds__(512) void gemm_s3_nt_kernel(S3Params p) {
       const float* mk = Mk + (long long)row * p.ldm + col;
       if (col + 4 <= p.N && ((reinterpret_cast<uintptr_t>(dst) | reinterpret_cast<uintptr_t>(mk)) & 15) == 0) {
         if (EPI == S3_MASK) {
-          const float4 m4 = *reinterpret_cast<const float4*>(mk);
+          const float4 m4 = mk4[EPI == S3_MASK ? it : 0];
           v.x = m4.x > 0.f ? v.x : 0.f; v.y = m4.y > 0.f ? v.y : 0.f;
           v.z = m4.z > 0.f ? v.z : 0.f; v.w = m4.w > 0.f ? v.w : 0.f;
         }
