@@ -608,8 +608,27 @@ __global__ __launch_bounds__(512) void gemm_bf16_bres_kernel(GemmParams p) {
   constexpr int EPP = 16 / ES;                      // elements per 16-B piece
   constexpr int VPR = BN / EPP;                     // pieces per row (10 or 20)
   unsigned char* tile = reinterpret_cast<unsigned char*>(Bs) + (size_t)wid * HR * TP * ES;
+  constexpr int NIT = (HR * VPR + 63) / 64;         // pieces per lane per pass
 #pragma unroll
   for (int h = 0; h < 32 / HR; ++h) {
+    // the ReluGrad mask's pieces of this pass, loaded before the tile's LDS writes: all in
+    // flight together instead of one dependent round trip per piece
+    uint4 mkr[EPI == EPI_MASK ? NIT : 1];
+    if (EPI == EPI_MASK) {
+#pragma unroll
+      for (int it = 0; it < NIT; ++it) {
+        const int q = min(lane + 64 * it, HR * VPR - 1);
+        const int rl = q / VPR, pc = q % VPR;
+        const int row = min(r0 + HR * h + rl, p.M - 1), col = max(0, min(j0 + pc * EPP, p.N - EPP));
+        const unsigned short* mk = reinterpret_cast<const unsigned short*>(p.mask) + (long long)row * p.ldm + col;
+        if (CBF16) {
+          mkr[it] = *reinterpret_cast<const uint4*>(mk);
+        } else {
+          const uint2 m2 = *reinterpret_cast<const uint2*>(mk);
+          mkr[it] = make_uint4(m2.x, m2.y, 0u, 0u);
+        }
+      }
+    }
 #pragma unroll
     for (int a = 0; a < 2; ++a) {
       if (16 * a < HR * h || 16 * a >= HR * (h + 1)) continue;
@@ -626,23 +645,20 @@ __global__ __launch_bounds__(512) void gemm_bf16_bres_kernel(GemmParams p) {
     }
     __builtin_amdgcn_s_waitcnt(0xc07f);             // lgkmcnt(0): this wave's tile writes landed
     __builtin_amdgcn_wave_barrier();
-    for (int q = lane; q < HR * VPR; q += 64) {
+#pragma unroll
+    for (int it = 0; it < NIT; ++it) {
+      const int q = lane + 64 * it;
       const int rl = q / VPR, pc = q % VPR;
       const int row = r0 + HR * h + rl, col = j0 + pc * EPP;
-      if (row >= p.M || col >= p.N) continue;
+      if (q >= HR * VPR || row >= p.M || col >= p.N) continue;
       uint4 v = *reinterpret_cast<const uint4*>(tile + ((size_t)rl * TP * ES + pc * 16));
       const int nv = min(EPP, p.N - col);           // elements of this piece inside N
       if (EPI == EPI_MASK) {
         const unsigned short* mk = reinterpret_cast<const unsigned short*>(p.mask) + (long long)row * p.ldm + col;
         unsigned short mv[8] = {0, 0, 0, 0, 0, 0, 0, 0};
         if (nv == EPP && (reinterpret_cast<uintptr_t>(mk) & (2 * EPP - 1)) == 0) {
-          if (CBF16) {
-            const uint4 m4 = *reinterpret_cast<const uint4*>(mk);
-            memcpy(mv, &m4, 16);
-          } else {
-            const uint2 m2 = *reinterpret_cast<const uint2*>(mk);
-            memcpy(mv, &m2, 8);
-          }
+          const uint4 m4 = mkr[EPI == EPI_MASK ? it : 0];
+          memcpy(mv, &m4, CBF16 ? 16 : 8);
         } else {
           for (int e = 0; e < nv; ++e) mv[e] = mk[e];
         }
