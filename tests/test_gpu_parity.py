@@ -233,10 +233,8 @@ def test_prefetch_matches_inline_index(hip_lib, name, adam):
                 zs.append(eng.predict(bs[6]))
         p = eng.params()
         runs.append((zs, p))
-    # wdl's wide-weight gradients are scattered with float atomics (order-dependent in the
-    # last bit), so that model is held to 1e-6 instead of bit equality
-    eq = (lambda a, b, **k: np.testing.assert_allclose(a, b, atol=1e-6, rtol=0, **k)) if model == "wdl" \
-        else np.testing.assert_array_equal
+    # (wdl's wide-weight gradient is int64 fixed point with integer atomics: order-free, exact)
+    eq = np.testing.assert_array_equal
     for a, b in zip(runs[0][0], runs[1][0]):
         eq(a, b)
     for k in runs[0][1]:
