@@ -425,7 +425,8 @@ def main():
             "vs_baseline": None,
             "dtype": "bf16+f32" if wl == "c5" else "f32",
             "data": "synthetic (seeded Criteo-shaped batches, %s ids, resident in HBM)" % args.dist,
-            "config": {"workload": {"c2": "C2 deepfm_pipeline: 13 dense + 26 cat x %d vocab (table %d x 16 f32), "
+            "config": {"workload": {"c2": ("C4 deepfm_pipeline, table row-sharded over the ranks" if sharded else "C2 deepfm_pipeline")
+                                          + ": 13 dense + 26 cat x %d vocab (table %d x 16 f32), "
                                           "MLP [400,400,400], TF1-dense Adam",
                                     "c3": "C3 deepfm_multi_cate: 26 cat + 6 multi-hot slots x 60 over %d vocab "
                                           "(table %d x 16 f32), MLP [400,400,400], TF1-dense Adam",
@@ -433,7 +434,7 @@ def main():
                                           "bf16 MLP [400,400,400] (fp32 master), fp32 wide logit, TF1-dense Adam",
                                     }[wl] % (args.vocab, spec.n_rows),
                        "global_batch": B * world, "per_gpu_batch": B,
-                       "parallelism": "dp%d" % world if world == 1 else
+                       "parallelism": "dp%d" % world if not sharded else
                        "dp%d + row-sharded table (RCCL all-to-all lookup, all-reduce dense grads)" % world,
                        "id_dist": args.dist, "table_adam": args.adam},
             "roofline": roof,
