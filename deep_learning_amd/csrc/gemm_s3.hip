@@ -91,7 +91,9 @@ struct S3Params {
 enum { S3_STORE = 0, S3_RELU = 1, S3_MASK = 2 };
 
 #ifndef DL_S3_DIAG
-#define DL_S3_DIAG 0   // diagnostics builds: 1 = no epilogue stores, 2 = no MFMAs either
+#define DL_S3_DIAG 0   // diagnostics builds: 1 = no epilogue stores, 2 = no MFMAs either;
+                       // 3 = no stores, no A loads (constant A); 4 = no stores, no B LDS reads;
+                       // 5 = no stores, no per-chunk barrier (results wrong: timing only)
 #endif
 
 // ---------------------------------------------------------------------------- NT
@@ -152,6 +154,10 @@ __global__ __launch_bounds__(512) void gemm_s3_nt_kernel(S3Params p) {
   };
   // A: this lane's 8 floats of rows r0 + cl, r0 + 16 + cl at k = 32c + 8kq
   auto load_a = [&](int c, float4 (&ra)[4]) {
+    if (DL_S3_DIAG == 3) {
+      ra[0] = ra[1] = ra[2] = ra[3] = make_float4(1.f + c, 2.f, 3.f, 4.f);
+      return;
+    }
     const int k = 32 * c + 8 * kq;
     const int kc = min(k, p.K - 8) >> 2;
     ra[0] = a0[kc];
@@ -192,10 +198,15 @@ __global__ __launch_bounds__(512) void gemm_s3_nt_kernel(S3Params p) {
       if (f < nf_live) {
         const int j = 16 * f + cl;
         const int o = j * 32 + 8 * nt_slot(j, kq);
-        const shortx8 bh = *reinterpret_cast<const shortx8*>(&Bs[o]);
-        const shortx8 bm = *reinterpret_cast<const shortx8*>(&Bs[kNtPlane + o]);
-        const shortx8 bl = *reinterpret_cast<const shortx8*>(&Bs[2 * kNtPlane + o]);
-        if (DL_S3_DIAG >= 2) {
+        shortx8 bh, bm, bl;
+        if (DL_S3_DIAG == 4) {
+          bh = am[0]; bm = al[1]; bl = ah[1];
+        } else {
+          bh = *reinterpret_cast<const shortx8*>(&Bs[o]);
+          bm = *reinterpret_cast<const shortx8*>(&Bs[kNtPlane + o]);
+          bl = *reinterpret_cast<const shortx8*>(&Bs[2 * kNtPlane + o]);
+        }
+        if (DL_S3_DIAG == 2) {
           acc[0][f][0] += (float)(bh[0] ^ ah[0][1] ^ bm[2] ^ bl[3] ^ am[0][0] ^ al[0][2]);
           acc[1][f][0] += (float)(bh[1] ^ ah[1][1] ^ bm[3] ^ bl[4] ^ am[1][0] ^ al[1][2]);
         } else {
@@ -207,7 +218,7 @@ __global__ __launch_bounds__(512) void gemm_s3_nt_kernel(S3Params p) {
     // chunk c + 1's B must have landed before the barrier publishes it: outstanding younger
     // ops are at most chunk c + 2's (<= 5 DMA + 4 A loads); waiting to 8 is conservative
     if (c + 2 < KC) DL_WAIT_VMCNT(8); else DL_WAIT_VMCNT(0);
-    __syncthreads();
+    if (DL_S3_DIAG != 5) __syncthreads();
   };
   for (int c = 0; c < KC; c += 2) {
     step(c, raA);
