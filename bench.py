@@ -103,7 +103,9 @@ def kernel_work(spec, B, touched_rows, rows=None, uniq=None, shard=None, wide_ro
 PMC_KERNEL = {"adam_table": "adam_rows4_kernel", "adam_first": "adam_rows1_kernel",
               "embed_fwd": "embed_fwd_kernel<16, 5>", "embed_bwd": "embed_bwd_kernel<16, false>",
               "head": "head_kernel"}
-PMC_KERNEL_LAZY = {"rec_gather": "rec_gather_kernel<16>", "embed_bwd": "rec_bwd_adam_kernel<16>",
+PMC_KERNEL_LAZY = {"rec_gather": ("rec_gather_kernel<16, false>", "rec_gather_kernel<16, true>",
+                                  "rec_gather_kernel<16>"),     # the last: summaries before the SPARSE template
+                   "embed_bwd": "rec_bwd_adam_kernel<16>",
                    "head": "head_kernel"}
 
 
@@ -120,9 +122,11 @@ def pmc_traffic(label, world, lazy=False, workload="c2"):
         d = json.load(open(f))
         if d.get("workload", "c2") != workload:
             continue
-        k = d["kernels"].get(names[label])
-        if k and "hbm_bytes" in k:
-            return {"hbm_bytes": int(k["hbm_bytes"]), "source": os.path.relpath(f, ROOT)}
+        want = names[label] if isinstance(names[label], tuple) else (names[label],)
+        for n in want:
+            k = d["kernels"].get(n)
+            if k and "hbm_bytes" in k:
+                return {"hbm_bytes": int(k["hbm_bytes"]), "source": os.path.relpath(f, ROOT)}
     return None
 
 

@@ -106,6 +106,34 @@ __device__ __forceinline__ void catch_up1_loop(float& p, float& m, float& v, flo
   }
 }
 
+// One zero-gradient step of the catch-up replay.  Bitwise the same as rec_adam(..., g = 0, ...):
+// with g = 0 the dense form's (g - m) * omb1 is (-m) * omb1 = m * (-omb1) exactly (0 - m and -m
+// differ only at m = +0, where both products are zeros that m + . maps to the same +0), and
+// the sparse form's g * omb1 is the constant 0 * omb1, hoisted (Zero0).
+struct Zero0 {   // per-launch constants of the zero-gradient step
+  float b1, b2, nomb1, nomb2, z1, z2, eps;
+  __device__ __forceinline__ explicit Zero0(const RecCfg& c) {
+#pragma clang fp contract(off)
+    b1 = c.b1; b2 = c.b2; nomb1 = -c.omb1; nomb2 = -c.omb2; eps = c.eps;
+    const float g = 0.f;
+    z1 = g * c.omb1;
+    z2 = (g * g) * c.omb2;
+  }
+};
+
+template <bool SPARSE>
+__device__ __forceinline__ void rec_adam0_x1(float& p, float& m, float& v, float alpha, const Zero0& k) {
+#pragma clang fp contract(off)
+  if (SPARSE) {
+    m = m * k.b1 + k.z1;
+    v = v * k.b2 + k.z2;
+  } else {
+    m = m + m * k.nomb1;
+    v = v + v * k.nomb2;
+  }
+  p = p - adam_step_size(m, v, alpha, k.eps);
+}
+
 // LDS-only reads of the alpha window
 struct RingWin {
   const float* sh;

@@ -50,7 +50,56 @@ namespace dl {
 // dealt to the 64 lanes in descending-lag order, snake-wise (round i: chains 64i..64i+63,
 // reversed on odd rounds): lanes that took a long chain take short ones after it.  Each
 // chain is the same sequence of rec_adam calls as before, so the results are unchanged.
-template <int E>
+#ifndef DL_GATHER_REPLAY   // 1: rank-dealt units, wave-uniform step loop; 0: per-lane chains (round-2 v1)
+#define DL_GATHER_REPLAY 1
+#endif
+
+// The replay loop of rec_gather_kernel's staged rows: one wave-uniform loop over the steps
+// k = top .. 1 (step target - k + 1), a lane stepping its unit (one element's p / m / v, or
+// the first-order triple) while the unit's lag `mine` covers k.  The alphas of
+// the last 64 steps sit one per lane in `alv` (lane l: step target - l, loaded once per
+// kernel) and are read with v_readlane: no LDS round trip inside the loop; older steps (a lag
+// beyond 64, rare) read the ring.
+template <bool SPARSE>
+__device__ __forceinline__ void replay_steps(float& p, float& m, float& v, int mine, int top, int target,
+                                             const RingW& ring, const Zero0& z, float alv) {
+  int k = top;
+  for (; k > 64; --k) {
+    const float al = ring(target - k + 1);
+    if (mine >= k) rec_adam0_x1<SPARSE>(p, m, v, al, z);
+  }
+  for (; k >= 1; --k) {
+    const float al = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(alv), k - 1));
+    if (mine >= k) rec_adam0_x1<SPARSE>(p, m, v, al, z);
+  }
+}
+
+// The staged rows' replay: E element units + the first-order triple per row, dealt in rank
+// order (most-lagging rows first) 64 to a round, so a round's uniform loop runs as long as its
+// first row's lag and the later, less-lagging rounds stop early.
+template <int E, bool SPARSE>
+__device__ __forceinline__ void replay_elems(float* st, const int* from_s, const int* order, int pitch, int target,
+                                             int nch, const RingW& ring, const RecCfg& c, float alv) {
+  constexpr int LPR = E / 4, RPW = 64 / LPR;
+  const int lane = threadIdx.x & 63;
+  const Zero0 z(c);
+  const int T = RPW * nch;
+  for (int r0 = 0; r0 < T; r0 += 64) {
+    const int top = __builtin_amdgcn_readfirstlane(target - from_s[order[r0 / nch]]);
+    if (top <= 0) break;                             // rank order: every later round is caught up too
+    const int k = r0 + lane;
+    const int r = order[min(k, T - 1) / nch], e = k % nch;
+    float* sr = st + r * pitch;
+    const int mine = k < T ? target - from_s[r] : 0;
+    float* x = e < E ? sr + e : sr + 3 * E;
+    const int s1 = e < E ? E : 1;
+    float P = x[0], M = x[s1], V = x[2 * s1];
+    replay_steps<SPARSE>(P, M, V, mine, top, target, ring, z, alv);
+    if (k < T) { x[0] = P; x[s1] = M; x[2 * s1] = V; }
+  }
+}
+
+template <int E, bool SPARSE>
 __global__ __launch_bounds__(256) void rec_gather_kernel(const float* __restrict__ rec, RecCfg c, int64_t n_rows,
                                                          int n_rep, int64_t rep_base,
                                                          const uint32_t* __restrict__ uniq,
@@ -74,6 +123,7 @@ __global__ __launch_bounds__(256) void rec_gather_kernel(const float* __restrict
   const long long wave_id = gt >> 6, nwaves = ((long long)gridDim.x * blockDim.x) >> 6;
   const long long total = n_rep + (n_uniq ? (long long)clamp_uniq(n_uniq, max_u, c.status) : max_u);
   const int target = (int)opt[7] - lag;
+  const float alv = ring(target - lane);               // lane l: alpha of step target - l
   const int nch = E + (c.has_first ? 1 : 0);          // element chains per row
   const int T = RPW * nch;
   for (long long base = wave_id * RPW; base < total; base += nwaves * RPW) {
@@ -115,6 +165,9 @@ __global__ __launch_bounds__(256) void rec_gather_kernel(const float* __restrict
       }
       __builtin_amdgcn_s_waitcnt(0xc07f);           // lgkmcnt(0): this wave's LDS writes landed
       __builtin_amdgcn_wave_barrier();
+#if DL_GATHER_REPLAY
+      replay_elems<E, SPARSE>(st, from_s, order, PITCH, target, nch, ring, c, alv);
+#else
       for (int k0 = 0; k0 < T; k0 += 64) {
         const int k = k0 + (((k0 >> 6) & 1) ? 63 - lane : lane);
         if (k < T) {
@@ -134,6 +187,7 @@ __global__ __launch_bounds__(256) void rec_gather_kernel(const float* __restrict
           }
         }
       }
+#endif
       __builtin_amdgcn_s_waitcnt(0xc07f);
       __builtin_amdgcn_wave_barrier();
       p = make_float4(sr[4 * q], sr[4 * q + 1], sr[4 * q + 2], sr[4 * q + 3]);
@@ -567,7 +621,8 @@ extern "C" int dl_rec_gather(const dl_emb_layout* L, const float* rec, int32_t r
   if (total == 0) return 0;
   DL_DISPATCH_E(L->emb_dim, {
     const unsigned grid = grid_cap(total * (kE / 4));
-    hipLaunchKernelGGL(rec_gather_kernel<kE>, dim3(grid), dim3(256), 0, as_stream(stream), rec,
+    auto kern = (rec_flags & DL_REC_SPARSE_ADAM) ? rec_gather_kernel<kE, true> : rec_gather_kernel<kE, false>;
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(256), 0, as_stream(stream), rec,
                        make_rec_cfg(kE, rec_ld, rec_flags, hist_len), (int64_t)L->n_rows, n_rep,
                        n_rep ? (int64_t)L->fm_cont_offset : (int64_t)0, uniq_keys, n_uniq, (long long)max_uniq,
                        world, hist, opt, lag, rows_u,
