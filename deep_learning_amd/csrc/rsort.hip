@@ -66,16 +66,19 @@ __device__ __forceinline__ bool rs_get(const RsSource& src, const RsPass& p, lon
   }
   const dl_emb_layout& L = src.L;
   const int S = L.cate_fields, ns = index_slots(L), mb = index_multi_base(L);
-  const long long b = ec / ns;
-  const int s = (int)(ec - b * ns);
+  // 32-bit division (a reference index is an int32): the 64-bit one is a long subroutine,
+  // and this runs per element in both the upsweep and the downsweep
+  const uint32_t ecu = (uint32_t)ec, b = ecu / (uint32_t)ns;
+  const int s = (int)(ecu - b * (uint32_t)ns);
   const int col = (L.use_fm && s < S) ? s : s < mb ? (L.use_fm ? s - S : s) : S + (s - mb);
   const int64_t off = (L.use_fm && s < S) ? L.fm_cate_offset : L.deep_cate_offset;
-  const int64_t row = src.cate[b * L.cate_ld + col] + off;
+  const int64_t row = src.cate[(long long)b * L.cate_ld + col] + off;
   const bool range_ok = row >= 0 && row < L.n_rows;
   if (in && !range_ok && flag_err && src.err) atomicOr(src.err, 1);
   const int w = src.world;
   const uint32_t r32 = (uint32_t)row;
-  key = row < src.rep_below ? (((uint32_t)w << kLocal) | r32) : (((r32 % (uint32_t)w) << kLocal) | (r32 / (uint32_t)w));
+  const uint32_t qw = w == 1 ? r32 : r32 / (uint32_t)w;   // w is uniform: one rank divides by nothing
+  key = row < src.rep_below ? (((uint32_t)w << kLocal) | r32) : (((r32 - qw * (uint32_t)w) << kLocal) | qw);
   return in && range_ok && !(row == 0 && L.zero_row0);
 }
 
