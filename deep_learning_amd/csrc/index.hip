@@ -62,91 +62,76 @@ __global__ __launch_bounds__(256) void unique_emit_kernel(const uint32_t* __rest
                                                           uint32_t* __restrict__ uniq, int32_t* __restrict__ seg_off,
                                                           int32_t* __restrict__ n_uniq, int32_t* __restrict__ inv,
                                                           int32_t* __restrict__ owner_counts) {
+  // Element i = chunk base + r * 256 + tid (round r): every load and every uniq / seg_off
+  // store of a round is one coalesced run (a round's heads take consecutive unique ids).
   __shared__ int wsum[4];
+  __shared__ int rw[kUqIpt * 4];   // heads per (round, wave), then their exclusive prefix
   __shared__ int base_s;
   const int n = min(*n_dev, n_max);
   if ((long long)blockIdx.x * kUqChunk >= n) return;   // whole block past the valid keys
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int c0 = blockIdx.x * kUqChunk;
   // exclusive offset of this chunk: sum of the earlier chunks' head counts
   int off = 0;
   for (int c = tid; c < (int)blockIdx.x; c += 256) off += chunk_cnt[c];
   off = __reduce_add_sync(~0ull, off);
   if (lane == 0) wsum[wid] = off;
+  uint32_t k[kUqIpt];
+  int32_t rf[kUqIpt];
+  uint64_t hm[kUqIpt];
+#pragma unroll
+  for (int r = 0; r < kUqIpt; ++r) {
+    const int i = c0 + r * 256 + tid;
+    k[r] = i < n ? keys[i] : invalid;
+    if (inv) rf[r] = i < n ? refs[i] : 0;
+  }
+#pragma unroll
+  for (int r = 0; r < kUqIpt; ++r) {
+    const int i = c0 + r * 256 + tid;
+    uint32_t pk = __shfl_up(k[r], 1, 64);
+    if (lane == 0) pk = i > 0 && i - 1 < n ? keys[i - 1] : invalid;
+    const bool hd = i < n && k[r] != invalid && (i == 0 || pk != k[r]);
+    hm[r] = __ballot(hd);
+    if (lane == 0) rw[r * 4 + wid] = __popcll(hm[r]);
+  }
   __syncthreads();
-  if (tid == 0) base_s = wsum[0] + wsum[1] + wsum[2] + wsum[3];
+  if (tid < 64) {   // exclusive scan over (round, wave) in element order
+    const int x = rw[tid];
+    int inc = x;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const int y = __shfl_up(inc, o, 64);
+      if (lane >= o) inc += y;
+    }
+    rw[tid] = inc - x;
+    if (tid == 0) base_s = wsum[0] + wsum[1] + wsum[2] + wsum[3];
+  }
   __syncthreads();
   const int base = base_s;
-  // this thread's kUqIpt consecutive keys
-  const int i0 = blockIdx.x * kUqChunk + tid * kUqIpt;
-  uint32_t k[kUqIpt];
-  int h = 0;
-  uint32_t prev = (i0 > 0 && i0 - 1 < n) ? keys[i0 - 1] : 0u;
-  if (i0 + kUqIpt <= n) {   // 64-B aligned run: four 16-B loads
+  const uint64_t le = lane == 63 ? ~0ull : (2ull << lane) - 1;   // lanes <= this one
 #pragma unroll
-    for (int q = 0; q < kUqIpt / 4; ++q) {
-      const uint4 v = reinterpret_cast<const uint4*>(keys + i0)[q];
-      k[4 * q] = v.x; k[4 * q + 1] = v.y; k[4 * q + 2] = v.z; k[4 * q + 3] = v.w;
-    }
-  } else {
-#pragma unroll
-    for (int u = 0; u < kUqIpt; ++u) k[u] = i0 + u < n ? keys[i0 + u] : invalid;
-  }
-#pragma unroll
-  for (int u = 0; u < kUqIpt; ++u) {
-    const int i = i0 + u;
-    const bool hd = i < n && k[u] != invalid && (i == 0 || (u == 0 ? prev : k[u - 1]) != k[u]);
-    h += hd ? 1 : 0;
-  }
-  // block exclusive scan of the per-thread head counts (wave scan + wave totals)
-  int x = h;
-#pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    const int y = __shfl_up(x, o, 64);
-    if (lane >= o) x += y;
-  }
-  __syncthreads();
-  if (lane == 63) wsum[wid] = x;
-  __syncthreads();
-  int wbase = 0;
-  for (int w = 0; w < wid; ++w) wbase += wsum[w];
-  int run = base + wbase + x - h;   // heads before this thread's first key
-  // the key after this thread's run and the refs of the run (16-B loads when whole);
-  // the loop below is fully unrolled (no break/continue: k[] stays in registers)
-  const uint32_t after = i0 + kUqIpt < n ? keys[i0 + kUqIpt] : invalid;
-  int32_t rf[kUqIpt];
-  if (inv) {
-    if (i0 + kUqIpt <= n) {
-#pragma unroll
-      for (int q = 0; q < kUqIpt / 4; ++q) {
-        const int4 v = reinterpret_cast<const int4*>(refs + i0)[q];
-        rf[4 * q] = v.x; rf[4 * q + 1] = v.y; rf[4 * q + 2] = v.z; rf[4 * q + 3] = v.w;
-      }
-    } else {
-#pragma unroll
-      for (int u = 0; u < kUqIpt; ++u) rf[u] = i0 + u < n ? refs[i0 + u] : 0;
-    }
-  }
-#pragma unroll
-  for (int u = 0; u < kUqIpt; ++u) {
-    const int i = i0 + u;
-    const uint32_t kk = k[u];
-    const uint32_t pk = u == 0 ? prev : k[u - 1];
-    const uint32_t nk = u + 1 < kUqIpt ? k[u + 1] : after;
+  for (int r = 0; r < kUqIpt; ++r) {
+    const int i = c0 + r * 256 + tid;
+    const uint32_t kk = k[r];
     const bool valid = i < n && kk != invalid;
-    const bool hd = valid && (i == 0 || pk != kk);
-    run += hd ? 1 : 0;
-    const int uu = run - 1;
+    const bool hd = (hm[r] >> lane) & 1;
+    const int uu = base + rw[r * 4 + wid] + __popcll(hm[r] & le) - 1;   // heads at or before i, minus one
+    uint32_t nk = __shfl_down(kk, 1, 64);
+    if (lane == 63) nk = i + 1 < n ? keys[i + 1] : invalid;
     if (hd) {
       uniq[uu] = kk;
       seg_off[uu] = i;
       // first unique row of an owner group (keys sorted by owner): counts follow from the starts
-      if (owner_counts && (i == 0 || (pk >> kLocalBits) != (kk >> kLocalBits))) owner_counts[kk >> kLocalBits] = uu;
+      if (owner_counts) {
+        const uint32_t pk = i > 0 ? keys[i - 1] : 0u;
+        if (i == 0 || (pk >> kLocalBits) != (kk >> kLocalBits)) owner_counts[kk >> kLocalBits] = uu;
+      }
     }
     if (valid && (i + 1 == n || nk == invalid)) {
       seg_off[uu + 1] = i + 1;
       n_uniq[0] = uu + 1;
     }
-    if (inv && i < n) inv[rf[u]] = valid ? uu : -1;
+    if (inv && i < n) inv[rf[r]] = valid ? uu : -1;
   }
 }
 
