@@ -107,6 +107,7 @@ constexpr int kNtBM = 256, kNtBN = 208, kNtNF = 13;
 constexpr int kNtPlane = kNtBN * 32;                             // bf16 elements of one plane image
 constexpr int kNtBuf = 3 * kNtPlane;
 constexpr int kNtDma = 3 * kNtBN / 16;                           // DMA instructions per chunk (39)
+constexpr int kNtDmaW = (kNtDma + 7) / 8;                        // per wave (5)
 constexpr size_t kNtLds = 3 * kNtBuf * sizeof(unsigned short);  // 119,808 B
 constexpr int kNtEP = kNtBN + 4;                                 // epilogue tile pitch (floats)
 static_assert(8 * 16 * kNtEP * sizeof(float) <= kNtLds, "epilogue tiles fit the ring");
@@ -129,44 +130,58 @@ __global__ __launch_bounds__(512) void gemm_s3_nt_kernel(S3Params p) {
   const bool ok0 = r0 + cl < p.M, ok1 = r0 + 16 + cl < p.M;
   // rows as float4 arrays (16-B aligned: A is, and lda % 4 == 0); loads are unconditional from
   // clamped addresses, and out-of-range pieces are zeroed afterwards (no exec-masked loads)
-  const float4* a0 = reinterpret_cast<const float4*>(p.A + (long long)min(r0 + cl, p.M - 1) * p.lda);
-  const float4* a1 = reinterpret_cast<const float4*>(p.A + (long long)min(r0 + 16 + cl, p.M - 1) * p.lda);
+  // byte offsets of this lane's rows (the host checks M * lda * 4 < 2^31)
+  const uint32_t a_off0 = 4u * (uint32_t)(min(r0 + cl, p.M - 1) * p.lda);
+  const uint32_t a_off1 = 4u * (uint32_t)(min(r0 + 16 + cl, p.M - 1) * p.lda);
+  const auto a_rsrc = __builtin_amdgcn_make_buffer_rsrc((void*)p.A, (short)0, p.M * p.lda * 4, 0x00020000);
   const int KC = (p.K + 31) / 32;
-  const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
   const int nf_live = min(kNtNF, (p.N - j0 + 15) / 16);   // column fragments inside N (wave-uniform)
 
   // LDS-DMA of chunk c into buffer `buf`: instruction g (g = wid, wid + 8, ...) fills plane
   // g / 13, rows 16 (g % 13) .. +16; lane L writes slot L & 3 of row L >> 2 and so fetches
   // the piece that belongs there.  Rows past N / k past K read clamped in-range data (their
   // products are discarded / multiplied by A's zeros).
+  // The DMA is inline asm: hipcc tracks a builtin LDS-DMA as a pending LDS write and then
+  // waits vmcnt(0) before the first use of any load it tracks (the A loads), draining the
+  // whole prefetch every chunk.  Invisible to its bookkeeping, the DMA is counted by hand in
+  // publish() below; hipcc's own waits for the A loads count only those (over-waiting, safe).
+  const uint32_t lds_base = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) unsigned short*)lds;
+  // Every wave issues exactly kNtDmaW instructions (the last one clamped: wave 7 repeats
+  // instruction kNtDma - 1, the same bytes to the same place), so the vmcnt bookkeeping below
+  // is one straight-line count for every wave and the compiler's own waits can count too.
   auto dma_b = [&](int c, int buf) {
 #pragma unroll
-    for (int g = wid; g < kNtDma; g += 8) {
+    for (int i = 0; i < kNtDmaW; ++i) {
+      const int g = min(wid + 8 * i, kNtDma - 1);
       const int pl = g / 13, rb = 16 * (g % 13);
       const int j = rb + (lane >> 2);
       const int kpc = nt_slot(j, lane & 3);        // the piece that belongs in slot lane & 3
       const int gj = min(j0 + j, p.N - 1);
       const int gk = min(32 * c + 8 * kpc, p.K - 8);
       const unsigned short* src = Bp + pl * p.b_plane + (long long)gj * p.ldb + gk;
-      __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)&lds[buf * kNtBuf + pl * kNtPlane + rb * 32],
-                                       16, 0, 0);
+      const uint32_t dst = lds_base + 2u * (uint32_t)(buf * kNtBuf + pl * kNtPlane + rb * 32);
+      unsigned keep;
+      asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+                   : "=&s"(keep) : "v"(src), "s"(__builtin_amdgcn_readfirstlane(dst)) : "memory");
     }
   };
   // A: this lane's 8 floats of rows r0 + cl, r0 + 16 + cl at k = 32c + 8kq
+  // A through a buffer descriptor: a piece outside M or K gets an offset past the descriptor's
+  // range and reads as zeros, so no fixup follows a load (overwriting a register whose load
+  // is in flight would cost a wait for it).
   auto load_a = [&](int c, float4 (&ra)[4]) {
     if (DL_S3_DIAG == 3) {
       ra[0] = ra[1] = ra[2] = ra[3] = make_float4(1.f + c, 2.f, 3.f, 4.f);
       return;
     }
     const int k = 32 * c + 8 * kq;
-    const int kc = min(k, p.K - 8) >> 2;
-    ra[0] = a0[kc];
-    ra[1] = a0[kc + 1];
-    ra[2] = a1[kc];
-    ra[3] = a1[kc + 1];
     const bool kin = k < p.K;
-    if (!(ok0 && kin)) { ra[0] = z4; ra[1] = z4; }
-    if (!(ok1 && kin)) { ra[2] = z4; ra[3] = z4; }
+    const uint32_t o0 = ok0 && kin ? a_off0 + 4u * k : 0x80000000u;
+    const uint32_t o1 = ok1 && kin ? a_off1 + 4u * k : 0x80000000u;
+    ra[0] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(a_rsrc, (int)o0, 0, 0));
+    ra[1] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(a_rsrc, (int)(o0 + 16u), 0, 0));
+    ra[2] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(a_rsrc, (int)o1, 0, 0));
+    ra[3] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(a_rsrc, (int)(o1 + 16u), 0, 0));
   };
 
   floatx4 acc[2][kNtNF];
@@ -179,19 +194,36 @@ __global__ __launch_bounds__(512) void gemm_s3_nt_kernel(S3Params p) {
   // prologue: B chunks 0 and 1 in flight, A chunks 0 and 1
   dma_b(0, 0);
   load_a(0, raA);
-  if (KC > 1) dma_b(1, 1);
-  if (KC > 1) load_a(1, raB);
-  // chunk 0's B must have landed (the <= 4 + 5 + 4 younger ops may stay in flight)
-  if (KC > 1) DL_WAIT_VMCNT(8); else DL_WAIT_VMCNT(0);
-  __syncthreads();
+  dma_b(1, 1);     // unconditional, like every prefetch below: chunks past KC read clamped
+  load_a(1, raB);  // weights into a free buffer and zeros for A
+
+  // The per-chunk barrier is a bare s_barrier after explicit counter waits: __syncthreads()
+  // carries a workgroup release fence, which the compiler lowers to vmcnt(0) — a wait for
+  // every load in flight, including the A loads and weight DMA issued for two chunks ahead,
+  // so each chunk paid a full memory round trip.  Here a wave waits only for the batches
+  // older than the one it just issued (vmcnt counts in issue order), which include its DMA of
+  // the chunk the barrier publishes.
+  auto publish = [&](int c) {           // chunk c + 1's weights -> every wave
+    if (c + 1 < KC) DL_WAIT_VMCNT(kNtDmaW + 4);   // every batch but chunk c + 2's: chunk c + 1's DMA too
+    else DL_WAIT_VMCNT(0);                // the epilogue reuses the ring: nothing may still land
+
+    __builtin_amdgcn_s_waitcnt(0xc07f);   // lgkmcnt(0): this wave's fragment reads are done
+    __builtin_amdgcn_s_barrier();
+  };
+  // chunk 0's B must have landed
+  publish(-1);
 
   auto step = [&](int c, float4 (&ra)[4]) {
     shortx8 ah[2], am[2], al[2];
     split8(ra[0], ra[1], ah[0], am[0], al[0]);
     split8(ra[2], ra[3], ah[1], am[1], al[1]);
+    // hipcc's wait for chunk c's A counts only its own loads (4 a batch), so it must come
+    // before the next batch is issued or it would also wait for part of that batch: the empty
+    // statement pins the split (and its wait) ahead of the batch's DMA statements
+    asm volatile("" : "+v"(ah[0]), "+v"(am[0]), "+v"(al[0]), "+v"(ah[1]), "+v"(am[1]), "+v"(al[1]));
     // chunk c + 2: B into the buffer chunk c - 1 used (free since the last barrier), then A
-    if (c + 2 < KC) dma_b(c + 2, (c + 2) % 3);
-    if (c + 2 < KC) load_a(c + 2, ra);
+    dma_b(c + 2, (c + 2) % 3);
+    load_a(c + 2, ra);
     const unsigned short* Bs = lds + (c % 3) * kNtBuf;
 #pragma unroll
     for (int f = 0; f < kNtNF; ++f) {
@@ -215,15 +247,16 @@ __global__ __launch_bounds__(512) void gemm_s3_nt_kernel(S3Params p) {
         }
       }
     }
-    // chunk c + 1's B must have landed before the barrier publishes it: outstanding younger
-    // ops are at most chunk c + 2's (<= 5 DMA + 4 A loads); waiting to 8 is conservative
-    if (c + 2 < KC) DL_WAIT_VMCNT(8); else DL_WAIT_VMCNT(0);
-    if (DL_S3_DIAG != 5) __syncthreads();
+    if (DL_S3_DIAG != 5) publish(c);
   };
-  for (int c = 0; c < KC; c += 2) {
+  // pairs of unconditional steps (an odd last chunk after the loop): at the loop head the
+  // latest batch is always raB's, so hipcc's own wait for raA leaves that batch in flight
+  int c = 0;
+  for (; c + 1 < KC; c += 2) {
     step(c, raA);
-    if (c + 1 < KC) step(c + 1, raB);
+    step(c + 1, raB);
   }
+  if (c < KC) step(c, raA);
 
   if (DL_S3_DIAG) {   // keep the loop's results live without storing them
     float tt = 0.f;
@@ -493,6 +526,8 @@ extern "C" int dl_gemm_s3_nt(int32_t M, int32_t N, int32_t K, const float* A, in
   DL_CHECK_ARG(b_plane >= (long long)ldb * N, "plane stride too small");
   DL_CHECK_ARG(epi >= 0 && epi <= 2, "bad epilogue %d", epi);
   DL_CHECK_ARG(epi != S3_MASK || mask, "mask epilogue needs mask");
+  DL_CHECK_ARG((long long)M * lda * 4 < (1LL << 31), "A spans %lld bytes: past the 31-bit buffer range",
+               (long long)M * lda * 4);
   if (M == 0 || N == 0) return 0;
   S3Params p{};
   p.A = A; p.B = Bp; p.C = C; p.mask = mask;
