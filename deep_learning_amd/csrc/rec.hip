@@ -446,6 +446,9 @@ __global__ __launch_bounds__(256) void rec_apply_segments_kernel(float* __restri
                                                                  long long n, const int32_t* __restrict__ pos,
                                                                  const float* __restrict__ g,
                                                                  const float* __restrict__ g1,
+                                                                 const float* __restrict__ rows,
+                                                                 const float* __restrict__ rows1,
+                                                                 const float* __restrict__ mv,
                                                                  const float* __restrict__ hist,
                                                                  const float* __restrict__ opt) {
   if (step_poisoned(opt)) return;
@@ -462,13 +465,32 @@ __global__ __launch_bounds__(256) void rec_apply_segments_kernel(float* __restri
   for (long long u = gt / LPR; u < nu; u += (long long)gridDim.x * blockDim.x / LPR) {
     const long long row = uniq[u];
     float* r = rec + row * c.ld;
-    float4 p = *reinterpret_cast<const float4*>(r + 4 * q);
-    float4 m = *reinterpret_cast<const float4*>(r + E + 4 + 4 * q);
-    float4 v = *reinterpret_cast<const float4*>(r + 2 * E + 4 + 4 * q);
-    const float4 tail = *reinterpret_cast<const float4*>(r + E);
-    float w = tail.x, wm = tail.y, wv = tail.z;
     const int e0 = max(0, seg_off[u]);
     const int e1 = (int)min(n, (long long)seg_off[u + 1]);
+    float4 p, m, v;
+    float w = 0.f, wm = 0.f, wv = 0.f;
+    int stamp = t - 1;
+    if (mv) {
+      // the owner gather's caught-up state at the row's first arrival (every arrival of a row
+      // was gathered from the same record to the same step): no record read, no replay
+      const int k0 = e0 < e1 ? pos[e0] : -1;
+      if (k0 < 0 || k0 >= n) {
+        index_fault(c.status);
+        continue;
+      }
+      p = *reinterpret_cast<const float4*>(rows + (long long)k0 * E + 4 * q);
+      const float* o = mv + (long long)k0 * (2 * E + 4);
+      m = *reinterpret_cast<const float4*>(o + 4 * q);
+      v = *reinterpret_cast<const float4*>(o + E + 4 * q);
+      if (first) { w = rows1[k0]; wm = o[2 * E]; wv = o[2 * E + 1]; }
+    } else {
+      p = *reinterpret_cast<const float4*>(r + 4 * q);
+      m = *reinterpret_cast<const float4*>(r + E + 4 + 4 * q);
+      v = *reinterpret_cast<const float4*>(r + 2 * E + 4 + 4 * q);
+      const float4 tail = *reinterpret_cast<const float4*>(r + E);
+      w = tail.x; wm = tail.y; wv = tail.z;
+      stamp = __float_as_int(tail.w);
+    }
     float4 gs = make_float4(0.f, 0.f, 0.f, 0.f);
     float g1s = 0.f;
     for (int e = e0; e < e1; ++e) {
@@ -478,7 +500,6 @@ __global__ __launch_bounds__(256) void rec_apply_segments_kernel(float* __restri
       gs.x += gk.x; gs.y += gk.y; gs.z += gk.z; gs.w += gk.w;
       if (first) g1s += g1[k];
     }
-    const int stamp = __float_as_int(tail.w);
     if (stamp < t - 1) catch_up4(p, m, v, w, wm, wv, first, stamp, t - 1, ring, c);
     rec_adam(p.x, m.x, v.x, gs.x, alpha, c);
     rec_adam(p.y, m.y, v.y, gs.y, alpha, c);
@@ -711,18 +732,19 @@ extern "C" int dl_rec_flush(float* rec, int32_t rec_ld, int32_t emb_dim, int32_t
 extern "C" int dl_rec_apply_segments(float* rec, int32_t rec_ld, int32_t emb_dim, int32_t rec_flags,
                                      const int32_t* uniq, const int32_t* seg_off, const int32_t* n_uniq,
                                      int64_t max_uniq, int64_t n, const int32_t* sorted_pos, const float* g,
-                                     const float* g1, const float* hist, int32_t hist_len, const float* opt,
-                                     void* stream) {
+                                     const float* g1, const float* rows, const float* rows1, const float* mv,
+                                     const float* hist, int32_t hist_len, const float* opt, void* stream) {
   const int32_t has_first = rec_flags & DL_REC_FIRST;
   DL_CHECK_ARG(rec && uniq && seg_off && sorted_pos && g && hist && opt, "NULL argument");
   if (int rc = rec_check(emb_dim, rec_ld, hist_len)) return rc;
   DL_CHECK_ARG(!has_first || g1, "g1 required with first-order weights");
+  DL_CHECK_ARG(!mv || (rows && (!has_first || rows1)), "the stash needs the gathered rows (and rows1)");
   if (max_uniq <= 0 || n <= 0) return 0;
   DL_DISPATCH_E(emb_dim, {
     hipLaunchKernelGGL(rec_apply_segments_kernel<kE>, dim3(grid_cap(max_uniq * (kE / 4))), dim3(256), 0,
                        as_stream(stream), rec, make_rec_cfg(kE, rec_ld, rec_flags, hist_len), uniq,
                        seg_off, n_uniq, (long long)max_uniq, (long long)n, sorted_pos, g, has_first ? g1 : nullptr,
-                       hist, opt);
+                       rows, has_first ? rows1 : nullptr, mv, hist, opt);
   });
   DL_RETURN_LAUNCH("dl_rec_apply_segments");
 }

@@ -269,6 +269,8 @@ class ShardedCTREngine(CTREngine):
             self.own_ws = e(_lib.lib().dl_index_workspace_bytes(cap), torch.uint8)
             self.own_keys, self.own_pos, self.own_uniq = e(cap), e(cap), e(cap)
             self.own_off, self.own_n = e(cap + 1), e(4)
+            # the owner gather's moment stash [cap][2E+4], read back by the update
+            self.own_mv = e(cap * (2 * self.spec.E + 4), torch.float32)
         self.own_cap = cap
 
     # ------------------------------------------------------------ parameters
@@ -380,9 +382,11 @@ class ShardedCTREngine(CTREngine):
             return ("dl_rec_apply_chain", ptr(self.rec), self.rec_ld, sp.E, self.rec_flags, ptr(recv_ids), nrecv,
                     ptr(self.own_head), ptr(self.own_next), ptr(gb), g1, ptr(self.hist), self.hist_len, ptr(opt),
                     stream)
+        # the owner gather's outputs at every arrival: the caught-up state (no second replay)
+        rows, rows1 = self.own_rows
         return ("dl_rec_apply_segments", ptr(self.rec), self.rec_ld, sp.E, self.rec_flags, ptr(self.own_uniq),
-                ptr(self.own_off), ptr(self.own_n), nrecv, nrecv, ptr(self.own_pos), ptr(gb), g1, ptr(self.hist),
-                self.hist_len, ptr(opt), stream)
+                ptr(self.own_off), ptr(self.own_n), nrecv, nrecv, ptr(self.own_pos), ptr(gb), g1, ptr(rows),
+                ptr(rows1) if sp.fm else None, ptr(self.own_mv), ptr(self.hist), self.hist_len, ptr(opt), stream)
 
     def _mark(self, name):
         if self.host_marks is not None:
@@ -716,9 +720,12 @@ class ShardedCTREngine(CTREngine):
         if nrecv and lazy:   # rows caught up to the previous step (read only)
             if self.apply_done is not None:   # the previous step's record update (side stream)
                 torch.cuda.current_stream().wait_event(self.apply_done)
+            self._owner_buffers(nrecv)
+            stash = self.owner_update == "sort"   # the update reads the caught-up state back
             self._c("rec_gather", "dl_rec_gather", C_ref(L), ptr(self.rec), self.rec_ld, self.rec_flags, 0,
                     ptr(recv_ids), None, nrecv, 1, ptr(self.hist), self.hist_len, ptr(self.opt), 1, ptr(out_v),
-                    ptr(out_1) if sp.fm else None, None, s)
+                    ptr(out_1) if sp.fm else None, ptr(self.own_mv) if stash else None, s)
+            self.own_rows = (out_v, out_1)
         elif nrecv:
             call("dl_shard_gather", ptr(self.table), ptr(self.first), ptr(recv_ids), nrecv, E, ptr(out_v),
                  ptr(out_1) if self.first is not None else None, s)
@@ -869,6 +876,8 @@ class ShardedCTREngine(CTREngine):
                 gb.record_stream(self.side)
                 if g1b is not None:
                     g1b.record_stream(self.side)
+                out_v.record_stream(self.side)   # the update reads the gathered rows (stash form)
+                out_1.record_stream(self.side)
         elif sp.fm:
             self._c("adam_table", "dl_adam_rows", ptr(self.table), ptr(self.tm), ptr(self.tv), ptr(self.tg),
                     ptr(self.touched), self.table.shape[0], E, 0.0, 0, ptr(self.opt), None, s)

@@ -442,11 +442,15 @@ int dl_rec_apply_rows(float* rec, int32_t rec_ld, int32_t emb_dim, int32_t rec_f
                       int64_t n, float* g, float* g1, const float* hist, int32_t hist_len,
                       const float* opt, void* stream);
 /* Sharded owners, deterministic: per unique received row (dl_sort_unique over the received
- * ids) the ordered sum of its arrivals g[pos][E], g1[pos] is applied (catch-up + step opt[7]). */
+ * ids) the ordered sum of its arrivals g[pos][E], g1[pos] is applied (step opt[7]).  With
+ * mv (the owner gather's moment stash, [n][2E+4]) the row's caught-up state is taken from
+ * rows[pos][E] / rows1[pos] / mv[pos] at its first arrival — the owner gather's outputs —
+ * and the record is only written; without it the record is read and caught up again. */
 int dl_rec_apply_segments(float* rec, int32_t rec_ld, int32_t emb_dim, int32_t rec_flags, const int32_t* uniq,
                           const int32_t* seg_off, const int32_t* n_uniq, int64_t max_uniq, int64_t n,
-                          const int32_t* sorted_pos, const float* g, const float* g1, const float* hist,
-                          int32_t hist_len, const float* opt, void* stream);
+                          const int32_t* sorted_pos, const float* g, const float* g1, const float* rows,
+                          const float* rows1, const float* mv, const float* hist, int32_t hist_len,
+                          const float* opt, void* stream);
 /* Every row caught up to step opt[7] (before export/checkpoint, and every hist_len steps). */
 int dl_rec_flush(float* rec, int32_t rec_ld, int32_t emb_dim, int32_t rec_flags, int64_t n_rows,
                  const float* hist, int32_t hist_len, const float* opt, void* stream);

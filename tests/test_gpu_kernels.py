@@ -352,8 +352,8 @@ def test_sorted_backward_equals_atomic(hip_lib, model):
 
 def test_chain_apply_equals_sorted_segment_apply(hip_lib):
     """Owner update of the sharded path: arrival chains (dl_rec_chain_link +
-    dl_rec_apply_chain) against the sort + segment form (dl_sort_unique +
-    dl_rec_apply_segments) on the same arrivals — 8 senders with unique ids each, so
+    dl_rec_apply_chain) and the stash form (dl_rec_gather's moments at every arrival) against
+    the sort + segment form (dl_sort_unique + dl_rec_apply_segments) on the same arrivals — 8 senders with unique ids each, so
     rows arrive up to 8 times, some rows lagging several steps: records bit-identical,
     chain heads back to -1."""
     E, ld, rows, W, per, hist_len = 16, 64, 5000, 8, 900, 8
@@ -379,7 +379,18 @@ def test_chain_apply_equals_sorted_segment_apply(hip_lib):
     call("dl_sort_unique", ptr(ids_d), n, 13, ptr(ws), ws.numel(), ptr(keys), ptr(pos), ptr(uniq), ptr(off),
          ptr(nu), None, _s())
     call("dl_rec_apply_segments", ptr(recA), ld, E, 1, ptr(uniq), ptr(off), ptr(nu), n, n, ptr(pos), ptr(gr_d),
-         ptr(g1_d), ptr(hist_d), hist_len, ptr(opt_d), _s())
+         ptr(g1_d), None, None, None, ptr(hist_d), hist_len, ptr(opt_d), _s())
+    # with the owner gather's stash (rows + moments caught up to step 9 at every arrival
+    # position): the record is only written, and must come out the same
+    recC = rec0.clone().cuda()
+    L = _lib.EmbLayout()
+    L.n_rows, L.batch, L.emb_dim = rows, 1, E
+    rows_u, rows_u1 = torch.empty(n, E, device="cuda"), torch.empty(n, device="cuda")
+    mv = torch.empty(n, 2 * E + 4, device="cuda")
+    call("dl_rec_gather", C.byref(L), ptr(recC), ld, 1, 0, ptr(ids_d), None, n, 1, ptr(hist_d), hist_len,
+         ptr(opt_d), 1, ptr(rows_u), ptr(rows_u1), ptr(mv), _s())
+    call("dl_rec_apply_segments", ptr(recC), ld, E, 1, ptr(uniq), ptr(off), ptr(nu), n, n, ptr(pos), ptr(gr_d),
+         ptr(g1_d), ptr(rows_u), ptr(rows_u1), ptr(mv), ptr(hist_d), hist_len, ptr(opt_d), _s())
     # chains
     recB = rec0.clone().cuda()
     head = torch.full((rows,), -1, dtype=torch.int32, device="cuda")
@@ -390,6 +401,8 @@ def test_chain_apply_equals_sorted_segment_apply(hip_lib):
     torch.cuda.synchronize()
     assert int(nu[0]) == len(np.unique(ids.numpy()))
     np.testing.assert_array_equal(recB.cpu().numpy().view(np.int32), recA.cpu().numpy().view(np.int32))
+    np.testing.assert_array_equal(recC.cpu().numpy().view(np.int32)[:, :3 * E + 4],
+                                  recA.cpu().numpy().view(np.int32)[:, :3 * E + 4])
     assert bool((head == -1).all())
     touched = np.unique(ids.numpy())
     assert (recB.view(torch.int32)[:, E + 3].cpu().numpy()[touched] == 10).all()
