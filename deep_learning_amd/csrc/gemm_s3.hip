@@ -90,6 +90,10 @@ struct S3Params {
 
 enum { S3_STORE = 0, S3_RELU = 1, S3_MASK = 2 };
 
+#ifndef DL_S3_TN2
+#define DL_S3_TN2 1   // weight gradients: the double-buffered TN kernel (0: the single-buffer one)
+#endif
+
 #ifndef DL_S3_DIAG
 #define DL_S3_DIAG 0   // diagnostics builds: 1 = no epilogue stores, 2 = no MFMAs either;
                        // 3 = no stores, no A loads (constant A); 4 = no stores, no B LDS reads;
@@ -477,6 +481,143 @@ __global__ __launch_bounds__(512) void gemm_s3_tn_kernel(S3Params p) {
     }
 }
 
+// ---------------------------------------------------------------------------- TN, double-buffered
+// The weight gradients again, with two LDS buffers so a step's MFMAs never wait for the next
+// step's staging: per 32-deep batch step a wave computes from buffer kt & 1 while the next
+// step's tiles (loaded into registers at the step's start) are split and written into the
+// other buffer, and one barrier per step publishes them.  Two 73.7 KB buffers fit the 160 KB
+// LDS at a 128 x 224 block (8 waves: rows 32 (w & 3) .. +32 = 2 fragments, columns 112 (w >> 2)
+// .. +112 = 7 fragments); N takes ceil(N / 224) column tiles (N = 400: 2).  Pitches 144 and
+// 240 bf16 (8 x odd words: conflict-free transposed reads, as above).  Out-of-range pieces
+// are loaded through buffer descriptors with an offset past the range: zeros, no fixup.
+constexpr int kT2BM = 128, kT2BN = 224, kT2KS = 32, kT2PA = 144, kT2PB = 240, kT2NF = 7;
+constexpr int kT2AE = kT2KS * kT2PA, kT2BE = kT2KS * kT2PB;           // bf16 elements per plane image
+constexpr int kT2Buf = 3 * (kT2AE + kT2BE);                           // one buffer: A planes, B planes
+constexpr size_t kT2Lds = 2 * kT2Buf * sizeof(unsigned short);       // 147,456 B
+constexpr int kT2QA = kT2KS * kT2BM / 4, kT2QB = kT2KS * kT2BN / 4;   // float4 pieces per step
+constexpr int kT2Q = (kT2QA + kT2QB + 511) / 512;
+static_assert(kT2QA == 2 * 512 && kT2QB == 3 * 512 + 256 && kT2Q == 6, "the piece mapping below");
+
+__global__ __launch_bounds__(512) void gemm_s3_tn2_kernel(S3Params p) {
+  extern __shared__ __attribute__((aligned(16))) unsigned short lds[];   // [2][3 A planes | 3 B planes]
+  const int tid = threadIdx.x, lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int mtiles = (p.M + kT2BM - 1) / kT2BM, ntiles = (p.N + kT2BN - 1) / kT2BN;
+  const int t = s3_xcd_tile(blockIdx.x, gridDim.x);   // the column tiles of one (m, slab) adjacent: X shared in L2
+  const int n0 = (t % ntiles) * kT2BN, m0 = ((t / ntiles) % mtiles) * kT2BM, z = t / (ntiles * mtiles);
+  const int kbeg = z * p.k_per_split;
+  const int kend = min(p.K, kbeg + p.k_per_split);
+  const int nk = (kend - kbeg + kT2KS - 1) / kT2KS;
+  const auto xr = __builtin_amdgcn_make_buffer_rsrc((void*)p.A, (short)0, p.K * p.lda * 4, 0x00020000);
+  const auto yr = __builtin_amdgcn_make_buffer_rsrc((void*)p.B, (short)0, p.K * p.ldb * 4, 0x00020000);
+  // this thread's pieces: u = 0, 1 -> X rows (tid >> 5) + 16u, columns 4 (tid & 31); u = 2..5 ->
+  // Y piece tid + 512 (u - 2) = row / 56, column 4 (piece % 56) (u = 5: threads < 256 only)
+  int pr[kT2Q], pc[kT2Q];
+  bool pok[kT2Q];
+#pragma unroll
+  for (int u = 0; u < kT2Q; ++u) {
+    if (u < 2) {
+      pr[u] = (tid >> 5) + 16 * u;
+      pc[u] = 4 * (tid & 31);
+      pok[u] = m0 + pc[u] < p.M;
+    } else {
+      const int qb = tid + 512 * (u - 2);
+      pr[u] = qb / (kT2BN / 4);
+      pc[u] = 4 * (qb % (kT2BN / 4));
+      pok[u] = n0 + pc[u] < p.N && (u < 5 || tid < 256);
+    }
+  }
+  float4 rs[kT2Q];
+  auto load = [&](int k0) {
+#pragma unroll
+    for (int u = 0; u < kT2Q; ++u) {
+      const int gk = k0 + pr[u];
+      const bool ok = pok[u] & (gk < kend);   // no short circuit: a select, not a branch
+      if (u < 2) {
+        const uint32_t o = 4u * (uint32_t)(gk * p.lda + m0 + pc[u]);
+        rs[u] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(xr, (int)(ok ? o : 0x80000000u), 0, 0));
+      } else {
+        const uint32_t o = 4u * (uint32_t)(gk * p.ldb + n0 + pc[u]);
+        rs[u] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(yr, (int)(ok ? o : 0x80000000u), 0, 0));
+      }
+    }
+  };
+  auto store = [&](int buf) {
+    unsigned short* As = lds + buf * kT2Buf;
+    unsigned short* Bs = As + 3 * kT2AE;
+#pragma unroll
+    for (int u = 0; u < kT2Q; ++u) {
+      if (u == 5 && tid >= 256) continue;
+      uint32_t h0, m0_, l0, h1, m1_, l1;
+      split2(rs[u].x, rs[u].y, h0, m0_, l0);
+      split2(rs[u].z, rs[u].w, h1, m1_, l1);
+      unsigned short* img = u < 2 ? As : Bs;
+      const int pe = u < 2 ? kT2AE : kT2BE;
+      const int o = pr[u] * (u < 2 ? kT2PA : kT2PB) + pc[u];
+      *reinterpret_cast<uint2*>(&img[o]) = make_uint2(h0, h1);
+      *reinterpret_cast<uint2*>(&img[pe + o]) = make_uint2(m0_, m1_);
+      *reinterpret_cast<uint2*>(&img[2 * pe + o]) = make_uint2(l0, l1);
+    }
+  };
+  floatx4 acc[2][kT2NF];
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < kT2NF; ++b) acc[a][b] = floatx4{0.f, 0.f, 0.f, 0.f};
+  const int wm = wid & 3, wn = wid >> 2;
+  const int cl = lane & 15, kq = lane >> 4, rq = cl >> 2, cp = cl & 3;
+  const int ra = 4 * kq + rq, rb = 16 + 4 * kq + rq;
+  const int ma_live = min(2, max(0, (p.M - (m0 + 32 * wm) + 15) / 16));
+  const int nb_live = min(kT2NF, max(0, (p.N - (n0 + 112 * wn) + 15) / 16));
+  auto compute = [&](int buf) {
+    const unsigned short* As = lds + buf * kT2Buf;
+    const unsigned short* Bs = As + 3 * kT2AE;
+    shortx8 ah[2], am[2], al[2];
+#pragma unroll
+    for (int a = 0; a < 2; ++a) {
+      const int col = 32 * wm + 16 * a + 4 * cp;
+      ah[a] = s3_tr_frag(As, kT2PA, ra, rb, col);
+      am[a] = s3_tr_frag(As + kT2AE, kT2PA, ra, rb, col);
+      al[a] = s3_tr_frag(As + 2 * kT2AE, kT2PA, ra, rb, col);
+    }
+#pragma unroll
+    for (int b = 0; b < kT2NF; ++b) {
+      if (b < nb_live) {
+        const int col = 112 * wn + 16 * b + 4 * cp;
+        const shortx8 bh = s3_tr_frag(Bs, kT2PB, ra, rb, col);
+        const shortx8 bm = s3_tr_frag(Bs + kT2BE, kT2PB, ra, rb, col);
+        const shortx8 bl = s3_tr_frag(Bs + 2 * kT2BE, kT2PB, ra, rb, col);
+#pragma unroll
+        for (int a = 0; a < 2; ++a)
+          if (a < ma_live) acc[a][b] = mfma_s3(ah[a], am[a], al[a], bh, bm, bl, acc[a][b]);
+      }
+    }
+  };
+  if (nk > 0) {
+    load(kbeg);
+    store(0);
+  }
+  __syncthreads();
+  for (int kt = 0; kt < nk; ++kt) {
+    const bool more = kt + 1 < nk;
+    if (more) load(kbeg + (kt + 1) * kT2KS);
+    compute(kt & 1);
+    if (more) store((kt + 1) & 1);   // the other buffer: its last readers passed the previous barrier
+    __syncthreads();
+  }
+  float* __restrict__ C = p.C + (long long)z * p.c_split_stride;
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < kT2NF; ++b) {
+      const int col = n0 + 112 * wn + 16 * b + cl;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int row = m0 + 32 * wm + 16 * a + 4 * kq + j;
+        if (row < p.M && col < p.N) C[(long long)row * p.ldc + col] = acc[a][b][j];
+      }
+    }
+}
+
 // ---------------------------------------------------------------------------- split
 // dst plane q (q = 0 hi, 1 mid, 2 lo) at dst + q * plane: element (r, c) of src [rows][cols]
 // (ld lds) goes to [r][c] (ldd), or to [c][r] when transposed.
@@ -545,8 +686,10 @@ extern "C" int dl_gemm_s3_tn(int32_t M, int32_t N, int32_t K, const float* X, in
                              void* stream) {
   DL_CHECK_ARG(M >= 0 && N >= 0 && K >= 0, "negative dims");
   DL_CHECK_ARG(X && Y && C, "NULL operand");
-  DL_CHECK_ARG(N <= kTnBN, "N %d > %d", N, kTnBN);
+  DL_CHECK_ARG(DL_S3_TN2 || N <= kTnBN, "N %d > %d", N, kTnBN);
   DL_CHECK_ARG(M % 4 == 0 && N % 4 == 0 && (M == 0 || M >= 4) && (N == 0 || N >= 4), "M, N must be multiples of 4");
+  DL_CHECK_ARG(!DL_S3_TN2 || ((long long)K * lda * 4 < (1LL << 31) && (long long)K * ldb * 4 < (1LL << 31)),
+               "X / Y past the 31-bit buffer range");
   DL_CHECK_ARG(lda % 4 == 0 && ldb % 4 == 0 && lda >= (M + 3) / 4 * 4 && ldb >= (N + 3) / 4 * 4 && ldc >= N,
                "bad leading dims");
   DL_CHECK_ARG(((uintptr_t)X % 16) == 0 && ((uintptr_t)Y % 16) == 0, "X / Y must be 16-byte aligned");
@@ -561,7 +704,12 @@ extern "C" int dl_gemm_s3_tn(int32_t M, int32_t N, int32_t K, const float* X, in
   p.k_per_split = kps;
   p.c_split_stride = c_split_stride;
   splits = (int)ceil_div(K > 0 ? K : 1, kps);
-  const int mtiles = (int)ceil_div(M, kTnBM);
-  hipLaunchKernelGGL(gemm_s3_tn_kernel, dim3((unsigned)(mtiles * splits)), dim3(512), kTnLds, as_stream(stream), p);
+  if (DL_S3_TN2) {
+    const int tiles = (int)(ceil_div(M, kT2BM) * ceil_div(N, kT2BN));
+    hipLaunchKernelGGL(gemm_s3_tn2_kernel, dim3((unsigned)(tiles * splits)), dim3(512), kT2Lds, as_stream(stream), p);
+  } else {
+    const int mtiles = (int)ceil_div(M, kTnBM);
+    hipLaunchKernelGGL(gemm_s3_tn_kernel, dim3((unsigned)(mtiles * splits)), dim3(512), kTnLds, as_stream(stream), p);
+  }
   DL_RETURN_LAUNCH("dl_gemm_s3_tn");
 }

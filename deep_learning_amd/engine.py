@@ -20,6 +20,7 @@ Internal layouts (import/export map to the reference's):
   head w = [first (F) | second (E) | deep (H) | bias]   (deepfm; dnn: [H | bias])
 """
 import math
+import os
 
 import numpy as np
 import torch
@@ -334,7 +335,9 @@ class CTREngine:
         self.head_blocks = call_int(self.head_grid, B)
         self.head_slab = z(self.head_blocks, sp.fm_cols + H + 2)
         self.in_wide = z(B, max(sp.Fw, 1), dt=torch.int64)
-        self.splits = max(1, min(64, B // 1024))
+        # split-K slabs of the weight gradients: the double-buffered s3 TN kernel (one block per
+        # CU, 2 column tiles) runs best at 32 (scripts/s3_bench.py: 147 vs 152 us at 64)
+        self.splits = max(1, min(int(os.environ.get("DLAMD_DW_SPLITS", 32 if self.s3 else 64)), B // 1024))
         self.w_slab = z(self.splits * max(i * o for i, o in zip(self.in_ld, self.out_ld)))
         self.layout = self._layout(B)
         self.bwd_blocks = _lib.lib().dl_embed_bwd_grid(C_ref(self.layout))
