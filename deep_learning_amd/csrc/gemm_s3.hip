@@ -90,6 +90,10 @@ struct S3Params {
 
 enum { S3_STORE = 0, S3_RELU = 1, S3_MASK = 2 };
 
+#ifndef DL_S3_BPF
+#define DL_S3_BPF 0   // 1: NT pins the next fragment's weight reads ahead of this one's MFMAs
+#endif                // (sched_barrier; measured slower than leaving the order to the scheduler)
+
 #ifndef DL_S3_TN2
 #define DL_S3_TN2 1   // weight gradients: the double-buffered TN kernel (0: the single-buffer one)
 #endif
@@ -139,7 +143,6 @@ __global__ __launch_bounds__(512) void gemm_s3_nt_kernel(S3Params p) {
   const uint32_t a_off1 = 4u * (uint32_t)(min(r0 + 16 + cl, p.M - 1) * p.lda);
   const auto a_rsrc = __builtin_amdgcn_make_buffer_rsrc((void*)p.A, (short)0, p.M * p.lda * 4, 0x00020000);
   const int KC = (p.K + 31) / 32;
-  const int nf_live = min(kNtNF, (p.N - j0 + 15) / 16);   // column fragments inside N (wave-uniform)
 
   // LDS-DMA of chunk c into buffer `buf`: instruction g (g = wid, wid + 8, ...) fills plane
   // g / 13, rows 16 (g % 13) .. +16; lane L writes slot L & 3 of row L >> 2 and so fetches
@@ -229,19 +232,28 @@ __global__ __launch_bounds__(512) void gemm_s3_nt_kernel(S3Params p) {
     dma_b(c + 2, (c + 2) % 3);
     load_a(c + 2, ra);
     const unsigned short* Bs = lds + (c % 3) * kNtBuf;
+    auto rd_b = [&](int f, shortx8& bh, shortx8& bm, shortx8& bl) {
+      const int j = 16 * f + cl;
+      const int o = j * 32 + 8 * nt_slot(j, kq);
+      if (DL_S3_DIAG == 4) {
+        bh = am[0]; bm = al[1]; bl = ah[1];
+      } else {
+        bh = *reinterpret_cast<const shortx8*>(&Bs[o]);
+        bm = *reinterpret_cast<const shortx8*>(&Bs[kNtPlane + o]);
+        bl = *reinterpret_cast<const shortx8*>(&Bs[2 * kNtPlane + o]);
+      }
+    };
+    // every fragment, also those past N (clamped weight rows, products discarded by the
+    // epilogue): no per-fragment branch, so the scheduler hoists fragment f + 1's reads over
+    // fragment f's MFMAs instead of each fragment waiting out its own LDS latency
+    shortx8 nh, nm, nl;
+    rd_b(0, nh, nm, nl);
 #pragma unroll
     for (int f = 0; f < kNtNF; ++f) {
-      if (f < nf_live) {
-        const int j = 16 * f + cl;
-        const int o = j * 32 + 8 * nt_slot(j, kq);
-        shortx8 bh, bm, bl;
-        if (DL_S3_DIAG == 4) {
-          bh = am[0]; bm = al[1]; bl = ah[1];
-        } else {
-          bh = *reinterpret_cast<const shortx8*>(&Bs[o]);
-          bm = *reinterpret_cast<const shortx8*>(&Bs[kNtPlane + o]);
-          bl = *reinterpret_cast<const shortx8*>(&Bs[2 * kNtPlane + o]);
-        }
+      {
+        const shortx8 bh = nh, bm = nm, bl = nl;
+        if (f + 1 < kNtNF) rd_b(f + 1, nh, nm, nl);
+        if (DL_S3_BPF) __builtin_amdgcn_sched_barrier(0);   // keep them there
         if (DL_S3_DIAG == 2) {
           acc[0][f][0] += (float)(bh[0] ^ ah[0][1] ^ bm[2] ^ bl[3] ^ am[0][0] ^ al[0][2]);
           acc[1][f][0] += (float)(bh[1] ^ ah[1][1] ^ bm[3] ^ bl[4] ^ am[1][0] ^ al[1][2]);
@@ -566,9 +578,7 @@ __global__ __launch_bounds__(512) void gemm_s3_tn2_kernel(S3Params p) {
   const int wm = wid & 3, wn = wid >> 2;
   const int cl = lane & 15, kq = lane >> 4, rq = cl >> 2, cp = cl & 3;
   const int ra = 4 * kq + rq, rb = 16 + 4 * kq + rq;
-  const int ma_live = min(2, max(0, (p.M - (m0 + 32 * wm) + 15) / 16));
-  const int nb_live = min(kT2NF, max(0, (p.N - (n0 + 112 * wn) + 15) / 16));
-  auto compute = [&](int buf) {
+  auto compute = [&](int buf) {   // every fragment (zeros past M / N): no branches between them
     const unsigned short* As = lds + buf * kT2Buf;
     const unsigned short* Bs = As + 3 * kT2AE;
     shortx8 ah[2], am[2], al[2];
@@ -581,15 +591,12 @@ __global__ __launch_bounds__(512) void gemm_s3_tn2_kernel(S3Params p) {
     }
 #pragma unroll
     for (int b = 0; b < kT2NF; ++b) {
-      if (b < nb_live) {
-        const int col = 112 * wn + 16 * b + 4 * cp;
-        const shortx8 bh = s3_tr_frag(Bs, kT2PB, ra, rb, col);
-        const shortx8 bm = s3_tr_frag(Bs + kT2BE, kT2PB, ra, rb, col);
-        const shortx8 bl = s3_tr_frag(Bs + 2 * kT2BE, kT2PB, ra, rb, col);
+      const int col = 112 * wn + 16 * b + 4 * cp;
+      const shortx8 bh = s3_tr_frag(Bs, kT2PB, ra, rb, col);
+      const shortx8 bm = s3_tr_frag(Bs + kT2BE, kT2PB, ra, rb, col);
+      const shortx8 bl = s3_tr_frag(Bs + 2 * kT2BE, kT2PB, ra, rb, col);
 #pragma unroll
-        for (int a = 0; a < 2; ++a)
-          if (a < ma_live) acc[a][b] = mfma_s3(ah[a], am[a], al[a], bh, bm, bl, acc[a][b]);
-      }
+      for (int a = 0; a < 2; ++a) acc[a][b] = mfma_s3(ah[a], am[a], al[a], bh, bm, bl, acc[a][b]);
     }
   };
   if (nk > 0) {
