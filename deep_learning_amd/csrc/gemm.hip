@@ -554,16 +554,21 @@ __global__ __launch_bounds__(512) void gemm_bf16_bres_kernel(GemmParams p) {
   const uint4 z4 = make_uint4(0u, 0u, 0u, 0u);
   // A fragments of this wave: rows r0 + cl and r0 + 16 + cl, k = 32c + 8kq .. +7
   const int r0 = i0 + wid * 32;
-  const unsigned short* a0 = A + (long long)min(r0 + cl, p.M - 1) * p.lda + 8 * kq;
-  const unsigned short* a1 = A + (long long)min(r0 + 16 + cl, p.M - 1) * p.lda + 8 * kq;
+  // A through a buffer descriptor (the host checks M * lda * 2 < 2^31): a piece past M or K
+  // gets an offset past the range and reads as zeros — no select on a loaded value, which
+  // made hipcc wait for each load where it was issued
+  const auto a_rsrc = __builtin_amdgcn_make_buffer_rsrc((void*)p.A, (short)0, p.M * p.lda * 2, 0x00020000);
+  const uint32_t o0 = 2u * (uint32_t)(min(r0 + cl, p.M - 1) * p.lda + 8 * kq);
+  const uint32_t o1 = 2u * (uint32_t)(min(r0 + 16 + cl, p.M - 1) * p.lda + 8 * kq);
   const bool ok0 = r0 + cl < p.M, ok1 = r0 + 16 + cl < p.M;
+  auto lda_ = [&](int c, uint4 (&r)[2]) {
+    const bool kin = 32 * c + 8 * kq < p.K;
+    r[0] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(a_rsrc, (int)((ok0 & kin) ? o0 + 64u * c : 0x80000000u), 0, 0));
+    r[1] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(a_rsrc, (int)((ok1 & kin) ? o1 + 64u * c : 0x80000000u), 0, 0));
+  };
   uint4 ra[KC][2];
 #pragma unroll
-  for (int c = 0; c < DEPTH && c < KC; ++c) {
-    const bool kin = 32 * c + 8 * kq < p.K;
-    ra[c][0] = (ok0 && kin) ? *reinterpret_cast<const uint4*>(a0 + 32 * c) : z4;
-    ra[c][1] = (ok1 && kin) ? *reinterpret_cast<const uint4*>(a1 + 32 * c) : z4;
-  }
+  for (int c = 0; c < DEPTH && c < KC; ++c) lda_(c, ra[c]);
   // B slab -> LDS: row j (column j0 + j of the product), k contiguous, zero past N and K
   for (int q = tid; q < BN * KC * 4; q += 512) {
     const int j = q / (KC * 4), k8 = q % (KC * 4);
@@ -577,23 +582,18 @@ __global__ __launch_bounds__(512) void gemm_bf16_bres_kernel(GemmParams p) {
   for (int a = 0; a < 2; ++a)
 #pragma unroll
     for (int f = 0; f < NF; ++f) acc[a][f] = floatx4{0.f, 0.f, 0.f, 0.f};
-  const int nf_live = min(NF, (p.N - j0 + 15) / 16);   // column fragments inside N (wave-uniform)
+  // every fragment (the slab is zero past N): no per-fragment branch to stop the scheduler
+  // from overlapping the next fragment's read with this one's MFMAs
 #pragma unroll
   for (int c = 0; c < KC; ++c) {
-    if (c + DEPTH < KC) {
-      const bool kin = 32 * (c + DEPTH) + 8 * kq < p.K;
-      ra[c + DEPTH][0] = (ok0 && kin) ? *reinterpret_cast<const uint4*>(a0 + 32 * (c + DEPTH)) : z4;
-      ra[c + DEPTH][1] = (ok1 && kin) ? *reinterpret_cast<const uint4*>(a1 + 32 * (c + DEPTH)) : z4;
-    }
+    if (c + DEPTH < KC) lda_(c + DEPTH, ra[c + DEPTH]);
     const shortx8 av0 = __builtin_bit_cast(shortx8, ra[c][0]);
     const shortx8 av1 = __builtin_bit_cast(shortx8, ra[c][1]);
 #pragma unroll
     for (int f = 0; f < NF; ++f) {
-      if (f < nf_live) {
-        const shortx8 bv = *reinterpret_cast<const shortx8*>(&Bs[(16 * f + cl) * KP + 32 * c + 8 * kq]);
-        acc[0][f] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av0, bv, acc[0][f], 0, 0, 0);
-        acc[1][f] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av1, bv, acc[1][f], 0, 0, 0);
-      }
+      const shortx8 bv = *reinterpret_cast<const shortx8*>(&Bs[(16 * f + cl) * KP + 32 * c + 8 * kq]);
+      acc[0][f] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av0, bv, acc[0][f], 0, 0, 0);
+      acc[1][f] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av1, bv, acc[1][f], 0, 0, 0);
     }
   }
   // Epilogue through LDS (the B slab is dead now): each wave writes its 32 x 80 tile row-major
@@ -708,7 +708,9 @@ static void launch_bf16_bres_kc(const GemmParams& gp, int epi, bool cb, hipStrea
 
 // true if the B-resident kernel takes the product (and launches it)
 static bool launch_bf16_bres(const GemmParams& gp, int epi, bool cb, hipStream_t s) {
-  if (epi == EPI_SPLIT || gp.K <= 0 || gp.K > 448 || gp.K % 8 || gp.lda % 8 || gp.ldb % 8 || gp.M < 256) return false;
+  if (epi == EPI_SPLIT || gp.K <= 0 || gp.K > 448 || gp.K % 8 || gp.lda % 8 || gp.ldb % 8 || gp.M < 256 ||
+      (long long)gp.M * gp.lda * 2 >= (1LL << 31))
+    return false;
   const int kc = (gp.K + 31) / 32;
   if (kc <= 13) launch_bf16_bres_kc<13>(gp, epi, cb, s);
   else launch_bf16_bres_kc<14>(gp, epi, cb, s);
@@ -750,23 +752,29 @@ __global__ __launch_bounds__(320) void gemm_bf16_dw_kernel(GemmParams p) {
   const int kbeg = z * p.k_per_split;
   const int kend = min(p.K, kbeg + p.k_per_split);
   const int nk = (kend - kbeg + KS - 1) / KS;
-  const uint4 z4 = make_uint4(0u, 0u, 0u, 0u);
+  // both operands through buffer descriptors (the host checks K * ld * 2 < 2^31): a piece
+  // past K, M or N gets an offset past the range and reads as zeros, so every load is issued
+  // unconditionally (a branch around each load made hipcc wait for it in place)
+  const auto xr = __builtin_amdgcn_make_buffer_rsrc((void*)p.A, (short)0, p.K * p.lda * 2, 0x00020000);
+  const auto yr = __builtin_amdgcn_make_buffer_rsrc((void*)p.B, (short)0, p.K * p.ldb * 2, 0x00020000);
   uint4 rs[Q];
   auto load = [&](int k0) {
 #pragma unroll
     for (int u = 0; u < Q; ++u) {
       const int q = tid + u * NT;
-      uint4 v = z4;
-      if (q < QA_N) {
+      if (q < QA_N) {   // (u, tid) ranges: wave-uniform for this mapping except at the boundary
         const int r = q / (BM / 8), c8 = q % (BM / 8);
         const int gk = k0 + r, gm = m0 + 8 * c8;
-        if (gk < kend && gm < p.M) v = *reinterpret_cast<const uint4*>(X + (long long)gk * p.lda + gm);
-      } else if (q < QA_N + QB_N) {
+        const uint32_t o = 2u * (uint32_t)(gk * p.lda + gm);
+        rs[u] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(
+                                              xr, (int)(((gk < kend) & (gm < p.M)) ? o : 0x80000000u), 0, 0));
+      } else {
         const int qq = q - QA_N, r = qq / (BN / 8), c8 = qq % (BN / 8);
         const int gk = k0 + r, gn = 8 * c8;
-        if (gk < kend && gn < p.N) v = *reinterpret_cast<const uint4*>(Y + (long long)gk * p.ldb + gn);
+        const uint32_t o = 2u * (uint32_t)(gk * p.ldb + gn);
+        const bool ok = (q < QA_N + QB_N) & (gk < kend) & (gn < p.N);
+        rs[u] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(yr, (int)(ok ? o : 0x80000000u), 0, 0));
       }
-      rs[u] = v;
     }
   };
   auto store = [&](int buf) {
@@ -837,7 +845,8 @@ __global__ __launch_bounds__(320) void gemm_bf16_dw_kernel(GemmParams p) {
 // true if the transposed-read kernel takes the product (ta = 1, tb = 0, split slabs)
 static bool launch_bf16_dw(const GemmParams& gp0, int splits_req, hipStream_t s) {
   if (gp0.N > 400 || gp0.N % 8 || gp0.M % 8 || gp0.lda % 8 || gp0.ldb % 8 || gp0.lda < gp0.M ||
-      gp0.ldb < gp0.N || (reinterpret_cast<uintptr_t>(gp0.A) & 15) || (reinterpret_cast<uintptr_t>(gp0.B) & 15))
+      gp0.ldb < gp0.N || (reinterpret_cast<uintptr_t>(gp0.A) & 15) || (reinterpret_cast<uintptr_t>(gp0.B) & 15) ||
+      (long long)gp0.K * gp0.lda * 2 >= (1LL << 31) || (long long)gp0.K * gp0.ldb * 2 >= (1LL << 31))
     return false;
   GemmParams gp = gp0;
   int kps = (int)ceil_div(gp.K > 0 ? gp.K : 1, splits_req);
