@@ -42,6 +42,20 @@ from ._lib import call, ptr
 from .engine import CTREngine, C_ref, _num_splits, _ru, call_int
 
 
+class _Works:
+    """The works of one grouped point-to-point exchange, waited together, and the event
+    after the rank's own segment's copy (queued on the issuing stream: a waiter on another
+    stream must order after it too)."""
+
+    def __init__(self, works, copied):
+        self.works, self.copied = works, copied
+
+    def wait(self):
+        torch.cuda.current_stream().wait_event(self.copied)
+        for w in self.works:
+            w.wait()
+
+
 class Exchange:
     """Thin wrapper over torch.distributed collectives for the sharded step."""
 
@@ -102,6 +116,28 @@ class Exchange:
         ev.synchronize()
         return host.view(-1, n).tolist()
 
+    def _exchange_p2p(self, res, src, send_splits, recv_splits):
+        """RCCL all-to-all as grouped point-to-point transfers with the rank's own segment
+        copied on the current stream (a device copy at HBM speed instead of RCCL's few-CU
+        self-transfer: all of the data at one rank, half of it at two).  Returns the works."""
+        so = [0] * (self.world + 1)
+        ro = [0] * (self.world + 1)
+        for p in range(self.world):
+            so[p + 1] = so[p] + send_splits[p]
+            ro[p + 1] = ro[p] + recv_splits[p]
+        me = self.rank
+        if send_splits[me]:
+            res[ro[me]: ro[me + 1]].copy_(src[so[me]: so[me + 1]])
+        ops = []
+        for p in range(self.world):
+            if p == me:
+                continue
+            if send_splits[p]:
+                ops.append(dist.P2POp(dist.isend, src[so[p]: so[p + 1]], p, self.group))
+            if recv_splits[p]:
+                ops.append(dist.P2POp(dist.irecv, res[ro[p]: ro[p + 1]], p, self.group))
+        return dist.batch_isend_irecv(ops) if ops else []
+
     def all_to_all(self, send, send_splits, recv_splits, out=None, async_op=False):
         """Variable all-to-all along dim 0 (splits in rows).  `out` (device, contiguous,
         sum(recv_splits) rows) receives in place — RCCL writes straight into it.
@@ -111,6 +147,20 @@ class Exchange:
         src = self._dev(send.contiguous())
         direct = out is not None and not self.staged and out.is_contiguous()
         res = out if direct else torch.empty(shape, dtype=send.dtype, device=src.device)
+        if not self.staged:
+            works = self._exchange_p2p(res, src, list(send_splits), list(recv_splits))
+            if async_op:
+                copied = torch.cuda.Event()
+                copied.record()
+                return res, _Works(works, copied)
+            for w in works:
+                w.wait()
+            if direct:
+                return out
+            if out is not None:
+                out.copy_(res)
+                return out
+            return res
         if async_op and not self.staged:
             work = dist.all_to_all_single(res, src, output_split_sizes=list(recv_splits),
                                           input_split_sizes=list(send_splits), group=self.group, async_op=True)
