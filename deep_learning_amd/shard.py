@@ -179,6 +179,8 @@ class Exchange:
         return res
 
     def all_reduce(self, t):
+        if self.world == 1:   # the sum over one rank is the input
+            return t
         if self.staged and t.is_cuda:
             c = t.cpu()
             dist.all_reduce(c, group=self.group)
