@@ -778,10 +778,8 @@ class CTREngine:
         if self.bf and not self.wdl:      # the wdl head writes its bf16 dY itself
             self._c("cast_dh", "dl_cast_bf16", ptr(self.dh[-1]), B, self.h_ld[-1], self.h_ld[-1], ptr(self.dhb[-1]),
                     self.h_ld[-1], s)
-        for l in reversed(range(nl)):
-            hdim = sp.hidden[l]
-            stride = self.in_ld[l] * self.out_ld[l]
-            nsplit = _num_splits(B, splits, 64 if (self.bf or self.s3) else 16)
+        def dw(l):   # the weight gradient of layer l (split-K slabs into w_slab)
+            hdim, stride = sp.hidden[l], self.in_ld[l] * self.out_ld[l]
             if self.bf:
                 # dW = X^T dY straight from the batch-major bf16 activations and gradients
                 # (transposing LDS reads inside the kernel: no X^T / dY^T copies)
@@ -789,6 +787,18 @@ class CTREngine:
                 self._c("gemm_dw_l%d" % l, "dl_gemm_bf16", 1, 0, self.in_ld[l], hdim, B, ptr(xl), self.in_ld[l],
                         ptr(self.dhb[l]), self.h_ld[l], ptr(self.w_slab), self.out_ld[l], 0, 3, None, 0, splits,
                         stride, s)
+            elif self.s3:   # dW = X^T dY (split-K slabs over the batch)
+                xin = self.x0 if l == 0 else self.h[l - 1]
+                i, o = self.in_ld[l], self.out_ld[l]
+                self._c("gemm_dw_l%d" % l, "dl_gemm_s3_tn", i, hdim, B, ptr(xin), i, ptr(self.dh[l]), self.h_ld[l],
+                        ptr(self.w_slab), o, splits, stride, s)
+            else:
+                xin = self.x0 if l == 0 else self.h[l - 1]
+                self._c("gemm_dw_l%d" % l, "dl_gemm_f32", 1, 0, self.in_ld[l], hdim, B, ptr(xin), self.in_ld[l],
+                        ptr(self.dh[l]), self.h_ld[l], ptr(self.w_slab), self.out_ld[l], 3, None, 0, splits, stride, s)
+
+        def dx(l):   # the input gradient of layer l (ReluGrad by the layer below; l = 0: dx0 in f32)
+            if self.bf:
                 if l > 0:   # dX = dY . W^T, ReluGrad by the bf16 activations, bf16 out
                     self._c("gemm_dx_l%d" % l, "dl_gemm_bf16", 0, 1, B, sp.hidden[l - 1], self.out_ld[l],
                             ptr(self.dhb[l]), self.h_ld[l], ptr(self.Wb[l]), self.out_ld[l], ptr(self.dhb[l - 1]),
@@ -797,12 +807,8 @@ class CTREngine:
                     self._c("gemm_dx_l0", "dl_gemm_bf16", 0, 1, B, self.dx_cols, self.out_ld[0], ptr(self.dhb[0]),
                             self.h_ld[0], ptr(self.Wb[0]), self.out_ld[0], ptr(self.dx0), self.dx_ld, 0, 0, None, 0,
                             1, 0, s)
-            elif self.s3:
-                # dW = X^T dY (split-K slabs over the batch), dX = dY W^T with ReluGrad
-                xin = self.x0 if l == 0 else self.h[l - 1]
+            elif self.s3:   # dX = dY W^T with ReluGrad
                 i, o = self.in_ld[l], self.out_ld[l]
-                self._c("gemm_dw_l%d" % l, "dl_gemm_s3_tn", i, hdim, B, ptr(xin), i, ptr(self.dh[l]), self.h_ld[l],
-                        ptr(self.w_slab), o, splits, stride, s)
                 if l > 0:
                     self._c("gemm_dx_l%d" % l, "dl_gemm_s3_nt", B, sp.hidden[l - 1], o, ptr(self.dh[l]),
                             self.h_ld[l], ptr(self.Wp[l]), o, i * o, ptr(self.dh[l - 1]), self.h_ld[l - 1], 2,
@@ -811,9 +817,6 @@ class CTREngine:
                     self._c("gemm_dx_l0", "dl_gemm_s3_nt", B, self.dx_cols, o, ptr(self.dh[0]), self.h_ld[0],
                             ptr(self.Wp[0]), o, i * o, ptr(self.dx0), self.dx_ld, 0, None, 0, s)
             else:
-                xin = self.x0 if l == 0 else self.h[l - 1]
-                self._c("gemm_dw_l%d" % l, "dl_gemm_f32", 1, 0, self.in_ld[l], hdim, B, ptr(xin), self.in_ld[l],
-                        ptr(self.dh[l]), self.h_ld[l], ptr(self.w_slab), self.out_ld[l], 3, None, 0, splits, stride, s)
                 self._c("transpose_l%d" % l, "dl_transpose_f32", ptr(self.W[l]), self.in_ld[l], self.out_ld[l],
                         self.out_ld[l], ptr(self.Wt), self.in_ld[l], s)
                 if l > 0:
@@ -823,32 +826,27 @@ class CTREngine:
                 else:
                     self._c("gemm_dx_l0", "dl_gemm_f32", 0, 0, B, self.dx_cols, self.out_ld[0], ptr(self.dh[0]),
                             self.h_ld[0], ptr(self.Wt), self.in_ld[0], ptr(self.dx0), self.dx_ld, 0, None, 0, 1, 0, s)
-            # L2 on every hidden weight matrix only for wdl (wdl.py:272-275); bias row excluded
+
+        def adam(l):
             # regulariser on every hidden weight matrix: wdl L2 (wdl.py:272-275), dnn L1 (dnn.py:88-90);
             # bias row excluded
+            stride = self.in_ld[l] * self.out_ld[l]
+            nsplit = _num_splits(B, splits, 64 if (self.bf or self.s3) else 16)
             reg = sp.hidden_reg
             l2, l2n = (sp.l2, ([self.D0] + sp.hidden)[l] * self.out_ld[l]) if reg else (0.0, 0)
             self._c("adam_dense_l%d" % l, "dl_adam_dense_reg", ptr(self.W[l]), ptr(self.Wm[l]), ptr(self.Wv[l]),
                     ptr(self.w_slab), nsplit, stride, stride, l2, l2n, 1 if reg == "l1" else 0, ptr(self.opt),
                     None, ptr(self.opt[8:]) if reg else None, s)
             self._refresh_wb(l, s)
+
+        for l in reversed(range(nl)):
+            dw(l)
+            dx(l)
+            adam(l)
         # embedding backward (uses pre-update table and head weights)
         bwd_blocks = call_int("dl_embed_bwd_grid", C_ref(L))
         if self.lazy:
-            E, R = sp.E, self.n_rep
-            self._c("embed_bwd", "dl_rec_bwd_adam", C_ref(L), ptr(self.rec), self.rec_ld, self.rec_flags, R,
-                    ptr(self.rows_u), ptr(self.rows_u1), ptr(self.mv_u), ptr(self.idx_uniq), ptr(self.idx_off),
-                    ptr(self.idx_n), ptr(self.idx_refs), 1, B * self.n_slot, ptr(self.dz), ptr(self.w_head),
-                    ptr(self.fm_sum), ptr(self.dx0), ptr(self.g_rep), ptr(self.g1_rep), ptr(self.hist),
-                    self.hist_len, ptr(self.opt), C_ref(self.pool_desc) if sp.M else None, s)
-            if R:
-                # FM cont-field rows: per-block register partials, folded into g_rep, then updated
-                self._c("cont_bwd", "dl_embed_cont_bwd", C_ref(L), ptr(self.rows_u), ptr(self._cont()),
-                        ptr(self.dz), ptr(self.w_head), ptr(self.fm_sum), ptr(self.cont_slab), self.bwd_blocks, s)
-                self._c("cont_reduce", "dl_embed_cont_reduce", C_ref(L), ptr(self.cont_slab), bwd_blocks,
-                        ptr(self.g_rep), ptr(self.g1_rep), ptr(self.rep_touched), s)
-                self._c("adam_rep", "dl_rec_apply_rows", ptr(self.rec), self.rec_ld, E, self.rec_flags, sp.fm_cont_offset, R,
-                        ptr(self.g_rep), ptr(self.g1_rep), ptr(self.hist), self.hist_len, ptr(self.opt), s)
+            self._embed_bwd_lazy(B, L, s)
         elif self.bwd == "sorted":
             self._c("embed_bwd", "dl_embed_bwd_sorted", C_ref(L), ptr(self.table), None, ptr(self.idx_uniq),
                     ptr(self.idx_off), ptr(self.idx_n), ptr(self.idx_refs), 1, B * self.n_slot, ptr(self.dz),
@@ -1008,6 +1006,26 @@ class CTREngine:
         self.steps += 1
         self.last_batch = B
         return B
+
+    def _embed_bwd_lazy(self, B, L, s):
+        """The lazy-record embedding backward on stream s: every unique row's ordered
+        segment sum and TF1 Adam step (dl_rec_bwd_adam), then the FM cont-field rows."""
+        sp = self.spec
+        bwd_blocks = call_int("dl_embed_bwd_grid", C_ref(L))
+        E, R = sp.E, self.n_rep
+        self._c("embed_bwd", "dl_rec_bwd_adam", C_ref(L), ptr(self.rec), self.rec_ld, self.rec_flags, R,
+                ptr(self.rows_u), ptr(self.rows_u1), ptr(self.mv_u), ptr(self.idx_uniq), ptr(self.idx_off),
+                ptr(self.idx_n), ptr(self.idx_refs), 1, B * self.n_slot, ptr(self.dz), ptr(self.w_head),
+                ptr(self.fm_sum), ptr(self.dx0), ptr(self.g_rep), ptr(self.g1_rep), ptr(self.hist),
+                self.hist_len, ptr(self.opt), C_ref(self.pool_desc) if sp.M else None, s)
+        if R:
+            # FM cont-field rows: per-block register partials, folded into g_rep, then updated
+            self._c("cont_bwd", "dl_embed_cont_bwd", C_ref(L), ptr(self.rows_u), ptr(self._cont()),
+                    ptr(self.dz), ptr(self.w_head), ptr(self.fm_sum), ptr(self.cont_slab), self.bwd_blocks, s)
+            self._c("cont_reduce", "dl_embed_cont_reduce", C_ref(L), ptr(self.cont_slab), bwd_blocks,
+                    ptr(self.g_rep), ptr(self.g1_rep), ptr(self.rep_touched), s)
+            self._c("adam_rep", "dl_rec_apply_rows", ptr(self.rec), self.rec_ld, E, self.rec_flags, sp.fm_cont_offset, R,
+                    ptr(self.g_rep), ptr(self.g1_rep), ptr(self.hist), self.hist_len, ptr(self.opt), s)
 
     def _capture(self, B, with_pre=False, pre_only=False):
         """Capture the step (with its index build when `with_pre`), or only the index build
