@@ -851,8 +851,14 @@ __global__ __launch_bounds__(256) void embed_bwd_sorted_kernel(BwdSortedArgs a) 
   const float* ws = a.w_head + F + 4 * q;   // not 16-B aligned
   const float4 wsec = L.use_fm ? make_float4(ws[0], ws[1], ws[2], ws[3]) : make_float4(0.f, 0.f, 0.f, 0.f);
   const SegGradIn sg{L, a.seg_off, a.refs, a.dz, a.w_head, a.fm_sum, a.dx0};
-  for (long long u = group0; u < nu; u += ngroups) {
-    const SegGrad4 sgr = segment_grad4<E>(sg, u, q, nrefs, wsec);
+  // wave-uniform trip count: a hot row's long segment is summed by the whole wave (segment.h)
+  for (long long u = group0; __any(u < nu); u += ngroups) {
+    const bool active = u < nu;
+    const SegRange cr = seg_range(sg, u, nu, nrefs);   // empty past nu
+    const bool lng = cr.e1 - cr.e0 > kSegLong;
+    SegGrad4 sgr = segment_grad4_range<E>(sg, cr.e0, lng ? cr.e0 : cr.e1, -2, q, nrefs, wsec);
+    segment_grad4_long<E>(sg, cr.e0, cr.e1, lng, nrefs, wsec, sgr);
+    if (!active) continue;
     const int64_t row = decode_key(a.uniq[u], a.world);
     if (row < 0 || row >= L.n_rows) continue;
     float4 v = make_float4(0.f, 0.f, 0.f, 0.f);

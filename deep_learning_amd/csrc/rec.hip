@@ -316,7 +316,10 @@ __global__ __launch_bounds__(256) void rec_bwd_adam_kernel(SegGradIn sg, float* 
   int kx = nx.e0 < nx.e1 ? sg.refs[nx.e0] : -1;
   SegRange nn = seg_range(sg, group0 + ngroups, nu, nrefs);
   uint32_t key_n = group0 < nu ? uniq[group0] : 0u;   // the row key too (the record load waits on it)
-  for (long long u = group0; u < nu; u += ngroups) {
+  // wave-uniform trip count (a wave's groups hold consecutive rows): the long-segment sums
+  // below need every lane of the wave; a group past the last row idles through its trips
+  for (long long u = group0; __any(u < nu); u += ngroups) {
+    const bool active = u < nu;
     const SegRange cr = nx;
     const int kc = kx;
     const uint32_t key = key_n;
@@ -327,10 +330,11 @@ __global__ __launch_bounds__(256) void rec_bwd_adam_kernel(SegGradIn sg, float* 
     const int64_t row = decode_key(key, world);
     // the row's caught-up state (independent of the segment walk: issued first)
     const long long iu = n_rep + u;
-    float4 p, m, v;
+    float4 p = make_float4(0.f, 0.f, 0.f, 0.f), m = p, v = p;
     float w = 0.f, wm = 0.f, wv = 0.f;
-    const bool row_ok = row >= 0 && row < L.n_rows;
-    if (mv) {
+    const bool row_ok = active && row >= 0 && row < L.n_rows;
+    if (!active) {
+    } else if (mv) {
       p = *reinterpret_cast<const float4*>(rows_u + iu * E + 4 * q);
       const float* o = mv + iu * (2 * E + 4);
       m = *reinterpret_cast<const float4*>(o + 4 * q);
@@ -346,7 +350,10 @@ __global__ __launch_bounds__(256) void rec_bwd_adam_kernel(SegGradIn sg, float* 
       const int stamp = __float_as_int(tail.w);
       if (stamp < t - 1) catch_up4(p, m, v, w, wm, wv, first, stamp, t - 1, ring, c);
     }
-    const SegGrad4 s = segment_grad4_range<E>(sg, cr.e0, cr.e1, kc, q, nrefs, wsec);
+    // a hot row's long segment is summed by the whole wave (segment.h), the rest by their group
+    const bool lng = cr.e1 - cr.e0 > kSegLong;
+    SegGrad4 s = segment_grad4_range<E>(sg, cr.e0, lng ? cr.e0 : cr.e1, kc, q, nrefs, wsec);
+    segment_grad4_long<E>(sg, cr.e0, cr.e1, lng, nrefs, wsec, s);
     if (!row_ok) continue;
     float4 g;
     g.x = seg_row_grad(s.s.x, s.dsum.x, s.x.x, s.dsum.x != 0.f ? p.x : 0.f);

@@ -103,7 +103,7 @@ __device__ __forceinline__ SegRange seg_range(const SegGradIn& a, long long u, l
 // already loaded it (software pipelining across rows), -2 to load it here.
 template <int E>
 __device__ __forceinline__ SegGrad4 segment_grad4_range(const SegGradIn& a, int e0, int e1, int k_first, int q,
-                                                        long long nrefs, float4 wsec) {
+                                                        long long nrefs, float4 wsec, int stride = 1) {
   const dl_emb_layout& L = a.L;
   const int S = L.cate_fields;
   const int ns = index_slots(L);
@@ -111,7 +111,7 @@ __device__ __forceinline__ SegGrad4 segment_grad4_range(const SegGradIn& a, int 
   const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
   SegGrad4 r{z, z, z, 0.f};
   const int mb = index_multi_base(L);
-  for (int e = e0; e < e1; ++e) {
+  for (int e = e0; e < e1; e += stride) {
     const int k = (e == e0 && k_first != -2) ? k_first : a.refs[e];
     if (k < 0 || k >= nrefs) {
       index_fault(a.status);
@@ -143,6 +143,60 @@ __device__ __forceinline__ SegGrad4 segment_grad4_range(const SegGradIn& a, int 
     }
   }
   return r;
+}
+
+// Hot rows (Zipf ids): a segment longer than kSegLong references is not walked by its own
+// lane group, one reference after another, but by the whole wave: 64 / (E/4) slots of E/4
+// lanes each take the references slot, slot + NS, ... in order, and the slot sums are
+// combined by a fixed butterfly (lane xor E/4, 2E/4, ... 32).  Every lane of the wave must
+// call this, with the same (e0, e1); every lane gets the total for its dims 4q..4q+3.  The
+// order is fixed, so the sums are deterministic, and every kernel using it (the lazy
+// record update, the dense sorted backward, the sharded senders) sums a row alike.
+constexpr int kSegLong = 32;
+
+__device__ __forceinline__ float4 seg_xor4(float4 v, int m) {
+  return make_float4(__shfl_xor(v.x, m, 64), __shfl_xor(v.y, m, 64), __shfl_xor(v.z, m, 64), __shfl_xor(v.w, m, 64));
+}
+
+template <int E>
+__device__ __forceinline__ SegGrad4 segment_grad4_wave(const SegGradIn& a, int e0, int e1, long long nrefs,
+                                                       float4 wsec) {
+  constexpr int LPR = E / 4, NS = 64 / LPR;
+  const int lane = threadIdx.x & 63, q = lane % LPR, slot = lane / LPR;
+  SegGrad4 r = segment_grad4_range<E>(a, e0 + slot, e1, -2, q, nrefs, wsec, NS);
+#pragma unroll
+  for (int m = LPR; m < 64; m <<= 1) {
+    const float4 s2 = seg_xor4(r.s, m), x2 = seg_xor4(r.x, m), d2 = seg_xor4(r.dsum, m);
+    const float g2 = __shfl_xor(r.g1, m, 64);
+    // lower slot first, so both partners form the same sum
+    const bool lo = (lane & m) == 0;
+    r.s = lo ? make_float4(r.s.x + s2.x, r.s.y + s2.y, r.s.z + s2.z, r.s.w + s2.w)
+             : make_float4(s2.x + r.s.x, s2.y + r.s.y, s2.z + r.s.z, s2.w + r.s.w);
+    r.x = lo ? make_float4(r.x.x + x2.x, r.x.y + x2.y, r.x.z + x2.z, r.x.w + x2.w)
+             : make_float4(x2.x + r.x.x, x2.y + r.x.y, x2.z + r.x.z, x2.w + r.x.w);
+    r.dsum = lo ? make_float4(r.dsum.x + d2.x, r.dsum.y + d2.y, r.dsum.z + d2.z, r.dsum.w + d2.w)
+                : make_float4(d2.x + r.dsum.x, d2.y + r.dsum.y, d2.z + r.dsum.z, d2.w + r.dsum.w);
+    r.g1 = lo ? r.g1 + g2 : g2 + r.g1;
+  }
+  return r;
+}
+
+// The wave's long segments, one after another (wave-uniform loop): a lane group whose
+// segment [e0, e1) is longer than kSegLong gets its sums here; the others keep theirs.
+// Every lane of the wave must call this.
+template <int E>
+__device__ __forceinline__ void segment_grad4_long(const SegGradIn& a, int e0, int e1, bool mine_long,
+                                                   long long nrefs, float4 wsec, SegGrad4& out) {
+  constexpr int LPR = E / 4;
+  const int lane = threadIdx.x & 63;
+  uint64_t todo = __ballot(mine_long && (lane % LPR) == 0);
+  while (todo) {
+    const int leader = __builtin_ctzll(todo);
+    todo &= todo - 1;
+    const int le0 = __shfl(e0, leader, 64), le1 = __shfl(e1, leader, 64);
+    const SegGrad4 t = segment_grad4_wave<E>(a, le0, le1, nrefs, wsec);
+    if (lane / LPR == leader / LPR) out = t;
+  }
 }
 
 template <int E>

@@ -275,3 +275,64 @@ def test_bad_id_step_applies_nothing_and_raises(hip_lib, name):
     torch.cuda.synchronize()
     eng.check_error()
     assert float(eng.opt[7].item()) == step0 + 1
+
+
+def _hot(bs, seed=5):
+    """Zipf-like hot rows: one field all one id, one field over five ids, 10 % of every
+    other entry one shared id — segments of hundreds of references (the wave-cooperative
+    long-segment sums of segment.h), beside ordinary short ones."""
+    rng = np.random.default_rng(seed)
+    for b in bs:
+        c = b["cate_feats"]
+        c[:, 3] = 77
+        c[:, 5] = 100 + rng.integers(0, 5, size=c.shape[0])
+        m = rng.random(c.shape) < 0.1
+        m[:, 3] = m[:, 5] = False
+        c[m] = 9
+    return bs
+
+
+@pytest.mark.parametrize("name", ["deepfm_pipeline", "wdl", "dnn_pipeline"])
+def test_hot_rows_lazy_bit_identical_to_dense(hip_lib, name):
+    """Hot rows: the lazy record update and the dense sorted backward sum every long
+    segment by the same wave-cooperative order — bit-identical parameters and moments."""
+    kw = dict(CASES[name], cate_index_size=50000)
+    same = np.testing.assert_array_equal
+    spec = ModelSpec(_model(name), **kw)
+    dense = CTREngine(spec, max_batch=1024, seed=3, bwd="sorted")
+    lazy = CTREngine(spec, max_batch=1024, seed=3, adam="lazy", hist_len=8)
+    bs = _hot(_batches(name, kw, 1024, 6, seed=9))
+    for i, b in enumerate(bs):
+        dense.train_step(b, graph=i >= 2)
+        lazy.train_step(b, graph=i >= 2)
+        torch.cuda.synchronize()
+        same(lazy.z[:1024].cpu().numpy(), dense.z[:1024].cpu().numpy(), err_msg="logits step %d" % i)
+    pd, pl = dense.params(), lazy.params()
+    for k in pd:
+        same(pl[k], pd[k], err_msg=k)
+
+
+@pytest.mark.parametrize("bwd", ["sorted", "lazy"])
+@pytest.mark.parametrize("name", ["deepfm_pipeline", "deepfm_multi_cate"])
+def test_hot_rows_match_oracle(hip_lib, name, bwd):
+    """Hot rows against the oracle (its segment sums run in reference order; the long
+    segments here are summed in the wave's fixed order): logits, loss, parameters 1e-5."""
+    kw = CASES[name]
+    model = _model(name)
+    cfg = R.make_cfg(model, **kw)
+    spec = ModelSpec(model, **kw)
+    P = R.init_params(cfg, np.random.default_rng(42))
+    B = 1536
+    eng = (CTREngine(spec, max_batch=B, init="none", adam="lazy") if bwd == "lazy"
+           else CTREngine(spec, max_batch=B, init="none", bwd=bwd))
+    eng.load_params(P)
+    opt = R.AdamTF1(cfg, P)
+    for step, b in enumerate(_hot(_batches(name, kw, B, 3))):
+        fw = R.train_step(cfg, P, opt, b)
+        eng.train_step(b, graph=(step >= 1))
+        torch.cuda.synchronize()
+        np.testing.assert_allclose(eng.z[:B].cpu().numpy(), fw["z"], atol=TOL, rtol=0, err_msg="logits %d" % step)
+        assert abs(eng.loss() - fw["loss"]) < TOL
+    got = eng.params()
+    for k in P:
+        np.testing.assert_allclose(got[k], P[k], atol=TOL, rtol=0, err_msg=k)
