@@ -833,6 +833,28 @@ struct BwdSortedArgs {
 };
 
 
+// One unique row's gradient from its segment sums, to g_out (compact: by unique index).
+template <int E>
+__device__ __forceinline__ void embed_bwd_sorted_row(const BwdSortedArgs& a, long long u, int q, const SegGrad4& sgr) {
+  const dl_emb_layout& L = a.L;
+  const int64_t row = decode_key(a.uniq[u], a.world);
+  if (row < 0 || row >= L.n_rows) return;
+  float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (sgr.dsum.x != 0.f || sgr.dsum.y != 0.f || sgr.dsum.z != 0.f || sgr.dsum.w != 0.f)
+    v = *reinterpret_cast<const float4*>((a.rows_u ? a.rows_u + u * E : a.table + row * E) + 4 * q);
+  float4 g;
+  g.x = seg_row_grad(sgr.s.x, sgr.dsum.x, sgr.x.x, sgr.dsum.x != 0.f ? v.x : 0.f);
+  g.y = seg_row_grad(sgr.s.y, sgr.dsum.y, sgr.x.y, sgr.dsum.y != 0.f ? v.y : 0.f);
+  g.z = seg_row_grad(sgr.s.z, sgr.dsum.z, sgr.x.z, sgr.dsum.z != 0.f ? v.z : 0.f);
+  g.w = seg_row_grad(sgr.s.w, sgr.dsum.w, sgr.x.w, sgr.dsum.w != 0.f ? v.w : 0.f);
+  const long long o = a.compact ? u : row;
+  *reinterpret_cast<float4*>(a.g_out + o * E + 4 * q) = g;
+  if (q == 0) {
+    if (a.g1_out && (a.compact || L.use_fm)) a.g1_out[o] = sgr.g1;
+    if (!a.compact) a.touched[row] = 1;
+  }
+}
+
 // float4 lanes (E/4 per unique row, as rec_bwd_adam_kernel): a wave keeps 64/(E/4)
 // rows' segment walks in flight; sums are bit-identical to the per-dim form.
 template <int E>
@@ -851,31 +873,28 @@ __global__ __launch_bounds__(256) void embed_bwd_sorted_kernel(BwdSortedArgs a) 
   const float* ws = a.w_head + F + 4 * q;   // not 16-B aligned
   const float4 wsec = L.use_fm ? make_float4(ws[0], ws[1], ws[2], ws[3]) : make_float4(0.f, 0.f, 0.f, 0.f);
   const SegGradIn sg{L, a.seg_off, a.refs, a.dz, a.w_head, a.fm_sum, a.dx0};
-  // wave-uniform trip count: a hot row's long segment is summed by the whole wave (segment.h)
-  for (long long u = group0; __any(u < nu); u += ngroups) {
-    const bool active = u < nu;
-    const SegRange cr = seg_range(sg, u, nu, nrefs);   // empty past nu
-    const bool lng = cr.e1 - cr.e0 > kSegLong;
-    SegGrad4 sgr = segment_grad4_range<E>(sg, cr.e0, lng ? cr.e0 : cr.e1, -2, q, nrefs, wsec);
-    segment_grad4_long<E>(sg, cr.e0, cr.e1, lng, nrefs, wsec, sgr);
-    if (!active) continue;
-    const int64_t row = decode_key(a.uniq[u], a.world);
-    if (row < 0 || row >= L.n_rows) continue;
-    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (sgr.dsum.x != 0.f || sgr.dsum.y != 0.f || sgr.dsum.z != 0.f || sgr.dsum.w != 0.f)
-      v = *reinterpret_cast<const float4*>((a.rows_u ? a.rows_u + u * E : a.table + row * E) + 4 * q);
-    float4 g;
-    g.x = seg_row_grad(sgr.s.x, sgr.dsum.x, sgr.x.x, sgr.dsum.x != 0.f ? v.x : 0.f);
-    g.y = seg_row_grad(sgr.s.y, sgr.dsum.y, sgr.x.y, sgr.dsum.y != 0.f ? v.y : 0.f);
-    g.z = seg_row_grad(sgr.s.z, sgr.dsum.z, sgr.x.z, sgr.dsum.z != 0.f ? v.z : 0.f);
-    g.w = seg_row_grad(sgr.s.w, sgr.dsum.w, sgr.x.w, sgr.dsum.w != 0.f ? v.w : 0.f);
-    const long long o = a.compact ? u : row;
-    *reinterpret_cast<float4*>(a.g_out + o * E + 4 * q) = g;
-    if (q == 0) {
-      if (a.g1_out && (a.compact || L.use_fm)) a.g1_out[o] = sgr.g1;
-      if (!a.compact) a.touched[row] = 1;
-    }
+  for (long long u = group0; u < nu; u += ngroups) {
+    const SegRange cr = seg_range(sg, u, nu, nrefs);
+    if (cr.e1 - cr.e0 > kSegLong) continue;   // a hot row: embed_bwd_long_kernel
+    const SegGrad4 sgr = segment_grad4_range<E>(sg, cr.e0, cr.e1, -2, q, nrefs, wsec);
+    embed_bwd_sorted_row<E>(a, u, q, sgr);
   }
+}
+
+template <int E>
+__global__ __launch_bounds__(256) void embed_bwd_long_kernel(BwdSortedArgs a) {
+  __shared__ SegLongLds sh;
+  const dl_emb_layout& L = a.L;
+  const int q = threadIdx.x % (E / 4);
+  const int S = L.cate_fields, ns = index_slots(L);
+  const int Cf = (L.use_fm && L.fm_cont) ? L.cont_fields : 0;
+  const int F = Cf + S + L.fm_extra;
+  const long long nrefs = (long long)L.batch * ns;
+  const int nu = clamp_uniq(a.n_uniq, nrefs);
+  const float* ws = a.w_head + F + 4 * q;
+  const float4 wsec = L.use_fm ? make_float4(ws[0], ws[1], ws[2], ws[3]) : make_float4(0.f, 0.f, 0.f, 0.f);
+  const SegGradIn sg{L, a.seg_off, a.refs, a.dz, a.w_head, a.fm_sum, a.dx0};
+  for_long_segments<E>(sg, nu, nrefs, wsec, sh, [&](long long u, const SegGrad4& s) { embed_bwd_sorted_row<E>(a, u, q, s); });
 }
 
 }  // namespace dl
@@ -897,8 +916,10 @@ extern "C" int dl_embed_bwd_sorted(const dl_emb_layout* L, const float* table, c
   if (blocks > 8192) blocks = 8192;
   BwdSortedArgs a{*L, table, rows_u, uniq_keys, seg_off, n_uniq, sorted_refs, world, dz, w_head, fm_sum, dx0,
                   g_out, g1_out, touched, compact};
-  DL_DISPATCH_E(L->emb_dim, hipLaunchKernelGGL(embed_bwd_sorted_kernel<kE>, dim3((unsigned)blocks), dim3(256), 0,
-                                               as_stream(stream), a));
+  DL_DISPATCH_E(L->emb_dim, {
+    hipLaunchKernelGGL(embed_bwd_sorted_kernel<kE>, dim3((unsigned)blocks), dim3(256), 0, as_stream(stream), a);
+    hipLaunchKernelGGL(embed_bwd_long_kernel<kE>, dim3(1024), dim3(256), 0, as_stream(stream), a);
+  });
   DL_RETURN_LAUNCH("dl_embed_bwd_sorted");
 }
 

@@ -277,16 +277,81 @@ __global__ __launch_bounds__(256) void pool_grad_kernel(dl_emb_layout L, dl_pool
   }
 }
 
+// The backward's per-row state: the caught-up p, m, v (and first-order triple) of unique
+// row u — from the gather's stash, or the record caught up again without one.
 template <int E>
-__global__ __launch_bounds__(256) void rec_bwd_adam_kernel(SegGradIn sg, float* __restrict__ rec, RecCfg c,
-                                                           int n_rep, const float* __restrict__ rows_u,
-                                                           const float* __restrict__ rows_u1,
-                                                           const float* __restrict__ mv,
-                                                           const uint32_t* __restrict__ uniq,
-                                                           const int32_t* __restrict__ n_uniq, int world,
-                                                           float* __restrict__ g_rep, float* __restrict__ g1_rep,
-                                                           const float* __restrict__ hist,
-                                                           const float* __restrict__ opt) {
+__device__ __forceinline__ void rec_bwd_state(int64_t row, long long iu, int q, bool first, bool row_ok,
+                                              const float* __restrict__ rec, const float* __restrict__ rows_u,
+                                              const float* __restrict__ rows_u1, const float* __restrict__ mv,
+                                              const RecCfg& c, int t, const RingW& ring, float4& p, float4& m,
+                                              float4& v, float& w, float& wm, float& wv) {
+  if (mv) {
+    p = *reinterpret_cast<const float4*>(rows_u + iu * E + 4 * q);
+    const float* o = mv + iu * (2 * E + 4);
+    m = *reinterpret_cast<const float4*>(o + 4 * q);
+    v = *reinterpret_cast<const float4*>(o + E + 4 * q);
+    if (first) { w = rows_u1[iu]; wm = o[2 * E]; wv = o[2 * E + 1]; }
+  } else if (row_ok) {   // no stash: re-read the record and replay its catch-up
+    const float* r = rec + row * c.ld;
+    p = *reinterpret_cast<const float4*>(r + 4 * q);
+    m = *reinterpret_cast<const float4*>(r + E + 4 + 4 * q);
+    v = *reinterpret_cast<const float4*>(r + 2 * E + 4 + 4 * q);
+    const float4 tail = *reinterpret_cast<const float4*>(r + E);
+    w = tail.x; wm = tail.y; wv = tail.z;
+    const int stamp = __float_as_int(tail.w);
+    if (stamp < t - 1) catch_up4(p, m, v, w, wm, wv, first, stamp, t - 1, ring, c);
+  }
+}
+
+// The row's gradient from its segment sums, then the TF1 Adam step on the record (or the
+// replicated rows' accumulation for the later dense update).
+template <int E>
+__device__ __forceinline__ void rec_bwd_apply(const SegGrad4& s, int64_t row, int q, bool first, float4 p, float4 m,
+                                              float4 v, float w, float wm, float wv, float* __restrict__ rec,
+                                              const RecCfg& c, const dl_emb_layout& L, int n_rep,
+                                              float* __restrict__ g_rep, float* __restrict__ g1_rep, float alpha,
+                                              int t) {
+  float4 g;
+  g.x = seg_row_grad(s.s.x, s.dsum.x, s.x.x, s.dsum.x != 0.f ? p.x : 0.f);
+  g.y = seg_row_grad(s.s.y, s.dsum.y, s.x.y, s.dsum.y != 0.f ? p.y : 0.f);
+  g.z = seg_row_grad(s.s.z, s.dsum.z, s.x.z, s.dsum.z != 0.f ? p.z : 0.f);
+  g.w = seg_row_grad(s.s.w, s.dsum.w, s.x.w, s.dsum.w != 0.f ? p.w : 0.f);
+  const int64_t rrow = row - L.fm_cont_offset;   // replicated rows: [fm_cont_offset, + n_rep)
+  if (rrow >= 0 && rrow < n_rep) {
+    float* gr = g_rep + rrow * E + 4 * q;
+    gr[0] += g.x; gr[1] += g.y; gr[2] += g.z; gr[3] += g.w;
+    if (g1_rep && q == 0) g1_rep[rrow] += s.g1;
+    return;
+  }
+  rec_adam(p.x, m.x, v.x, g.x, alpha, c);
+  rec_adam(p.y, m.y, v.y, g.y, alpha, c);
+  rec_adam(p.z, m.z, v.z, g.z, alpha, c);
+  rec_adam(p.w, m.w, v.w, g.w, alpha, c);
+  float* r = rec + row * c.ld;
+  *reinterpret_cast<float4*>(r + 4 * q) = p;
+  *reinterpret_cast<float4*>(r + E + 4 + 4 * q) = m;
+  *reinterpret_cast<float4*>(r + 2 * E + 4 + 4 * q) = v;
+  if (q == 0) {
+    if (first) rec_adam(w, wm, wv, s.g1, alpha, c);
+    *reinterpret_cast<float4*>(r + E) = make_float4(w, wm, wv, __int_as_float(t));
+  }
+#if DL_REC_FULL_LINES
+  // the record's pad too (zeros): the row's last 128-B line is written whole, so no
+  // partially dirty line has to be merged with its old bytes below the L2
+  for (int o = 3 * E + 4 + 4 * q; o < c.ld; o += E) *reinterpret_cast<float4*>(r + o) = make_float4(0.f, 0.f, 0.f, 0.f);
+#endif
+}
+
+#define DL_REC_BWD_PARAMS                                                                                    \
+  SegGradIn sg, float *__restrict__ rec, RecCfg c, int n_rep, const float *__restrict__ rows_u,              \
+      const float *__restrict__ rows_u1, const float *__restrict__ mv, const uint32_t *__restrict__ uniq,   \
+      const int32_t *__restrict__ n_uniq, int world, float *__restrict__ g_rep, float *__restrict__ g1_rep, \
+      const float *__restrict__ hist, const float *__restrict__ opt
+
+// Pass 1: every unique row but the hot ones (more than kSegLong references: pass 2), E/4
+// lanes per row.
+template <int E>
+__global__ __launch_bounds__(256) void rec_bwd_adam_kernel(DL_REC_BWD_PARAMS) {
   if (step_poisoned(opt)) return;   // the batch failed validation: no update (common.h)
   rec_load_hyper(c, opt);
   __shared__ float hw[kHistWin];
@@ -316,10 +381,7 @@ __global__ __launch_bounds__(256) void rec_bwd_adam_kernel(SegGradIn sg, float* 
   int kx = nx.e0 < nx.e1 ? sg.refs[nx.e0] : -1;
   SegRange nn = seg_range(sg, group0 + ngroups, nu, nrefs);
   uint32_t key_n = group0 < nu ? uniq[group0] : 0u;   // the row key too (the record load waits on it)
-  // wave-uniform trip count (a wave's groups hold consecutive rows): the long-segment sums
-  // below need every lane of the wave; a group past the last row idles through its trips
-  for (long long u = group0; __any(u < nu); u += ngroups) {
-    const bool active = u < nu;
+  for (long long u = group0; u < nu; u += ngroups) {
     const SegRange cr = nx;
     const int kc = kx;
     const uint32_t key = key_n;
@@ -327,64 +389,47 @@ __global__ __launch_bounds__(256) void rec_bwd_adam_kernel(SegGradIn sg, float* 
     kx = nx.e0 < nx.e1 ? sg.refs[nx.e0] : -1;
     nn = seg_range(sg, u + 2 * ngroups, nu, nrefs);
     key_n = u + ngroups < nu ? uniq[u + ngroups] : 0u;
+    if (cr.e1 - cr.e0 > kSegLong) continue;   // a hot row: pass 2 (rec_bwd_long_kernel)
     const int64_t row = decode_key(key, world);
+    const bool row_ok = row >= 0 && row < L.n_rows;
     // the row's caught-up state (independent of the segment walk: issued first)
-    const long long iu = n_rep + u;
     float4 p = make_float4(0.f, 0.f, 0.f, 0.f), m = p, v = p;
     float w = 0.f, wm = 0.f, wv = 0.f;
-    const bool row_ok = active && row >= 0 && row < L.n_rows;
-    if (!active) {
-    } else if (mv) {
-      p = *reinterpret_cast<const float4*>(rows_u + iu * E + 4 * q);
-      const float* o = mv + iu * (2 * E + 4);
-      m = *reinterpret_cast<const float4*>(o + 4 * q);
-      v = *reinterpret_cast<const float4*>(o + E + 4 * q);
-      if (first) { w = rows_u1[iu]; wm = o[2 * E]; wv = o[2 * E + 1]; }
-    } else if (row_ok) {   // no stash: re-read the record and replay its catch-up
-      const float* r = rec + row * c.ld;
-      p = *reinterpret_cast<const float4*>(r + 4 * q);
-      m = *reinterpret_cast<const float4*>(r + E + 4 + 4 * q);
-      v = *reinterpret_cast<const float4*>(r + 2 * E + 4 + 4 * q);
-      const float4 tail = *reinterpret_cast<const float4*>(r + E);
-      w = tail.x; wm = tail.y; wv = tail.z;
-      const int stamp = __float_as_int(tail.w);
-      if (stamp < t - 1) catch_up4(p, m, v, w, wm, wv, first, stamp, t - 1, ring, c);
-    }
-    // a hot row's long segment is summed by the whole wave (segment.h), the rest by their group
-    const bool lng = cr.e1 - cr.e0 > kSegLong;
-    SegGrad4 s = segment_grad4_range<E>(sg, cr.e0, lng ? cr.e0 : cr.e1, kc, q, nrefs, wsec);
-    segment_grad4_long<E>(sg, cr.e0, cr.e1, lng, nrefs, wsec, s);
+    rec_bwd_state<E>(row, n_rep + u, q, first, row_ok, rec, rows_u, rows_u1, mv, c, t, ring, p, m, v, w, wm, wv);
+    const SegGrad4 s = segment_grad4_range<E>(sg, cr.e0, cr.e1, kc, q, nrefs, wsec);
     if (!row_ok) continue;
-    float4 g;
-    g.x = seg_row_grad(s.s.x, s.dsum.x, s.x.x, s.dsum.x != 0.f ? p.x : 0.f);
-    g.y = seg_row_grad(s.s.y, s.dsum.y, s.x.y, s.dsum.y != 0.f ? p.y : 0.f);
-    g.z = seg_row_grad(s.s.z, s.dsum.z, s.x.z, s.dsum.z != 0.f ? p.z : 0.f);
-    g.w = seg_row_grad(s.s.w, s.dsum.w, s.x.w, s.dsum.w != 0.f ? p.w : 0.f);
-    const int64_t rrow = row - L.fm_cont_offset;   // replicated rows: [fm_cont_offset, + n_rep)
-    if (rrow >= 0 && rrow < n_rep) {
-      float* gr = g_rep + rrow * E + 4 * q;
-      gr[0] += g.x; gr[1] += g.y; gr[2] += g.z; gr[3] += g.w;
-      if (g1_rep && q == 0) g1_rep[rrow] += s.g1;
-      continue;
-    }
-    rec_adam(p.x, m.x, v.x, g.x, alpha, c);
-    rec_adam(p.y, m.y, v.y, g.y, alpha, c);
-    rec_adam(p.z, m.z, v.z, g.z, alpha, c);
-    rec_adam(p.w, m.w, v.w, g.w, alpha, c);
-    float* r = rec + row * c.ld;
-    *reinterpret_cast<float4*>(r + 4 * q) = p;
-    *reinterpret_cast<float4*>(r + E + 4 + 4 * q) = m;
-    *reinterpret_cast<float4*>(r + 2 * E + 4 + 4 * q) = v;
-    if (q == 0) {
-      if (first) rec_adam(w, wm, wv, s.g1, alpha, c);
-      *reinterpret_cast<float4*>(r + E) = make_float4(w, wm, wv, __int_as_float(t));
-    }
-#if DL_REC_FULL_LINES
-    // the record's pad too (zeros): the row's last 128-B line is written whole, so no
-    // partially dirty line has to be merged with its old bytes below the L2
-    for (int o = 3 * E + 4 + 4 * q; o < c.ld; o += E) *reinterpret_cast<float4*>(r + o) = make_float4(0.f, 0.f, 0.f, 0.f);
-#endif
+    rec_bwd_apply<E>(s, row, q, first, p, m, v, w, wm, wv, rec, c, L, n_rep, g_rep, g1_rep, alpha, t);
   }
+}
+
+// Pass 2: the rows whose segments have more than kSegLong references, one whole block each.
+template <int E>
+__global__ __launch_bounds__(256) void rec_bwd_long_kernel(DL_REC_BWD_PARAMS) {
+  if (step_poisoned(opt)) return;
+  rec_load_hyper(c, opt);
+  __shared__ float hw[kHistWin];
+  const RingW ring = load_hist_window(hw, hist, (int)opt[7], c);
+  __shared__ SegLongLds sh;
+  const dl_emb_layout& L = sg.L;
+  const int q = threadIdx.x % (E / 4);
+  const int S = L.cate_fields, ns = index_slots(L);
+  const int Cf = (L.use_fm && L.fm_cont) ? L.cont_fields : 0;
+  const int F = Cf + S + L.fm_extra;
+  const long long nrefs = (long long)L.batch * ns;
+  const int nu = clamp_uniq(n_uniq, nrefs, sg.status);
+  const float* ws = sg.w_head + F + 4 * q;
+  const float4 wsec = L.use_fm ? make_float4(ws[0], ws[1], ws[2], ws[3]) : make_float4(0.f, 0.f, 0.f, 0.f);
+  const int t = (int)opt[7];
+  const float alpha = opt[3];
+  const bool first = c.has_first && q == 0;
+  for_long_segments<E>(sg, nu, nrefs, wsec, sh, [&](long long u, const SegGrad4& s) {
+    const int64_t row = decode_key(uniq[u], world);
+    const bool row_ok = row >= 0 && row < L.n_rows;
+    float4 p = make_float4(0.f, 0.f, 0.f, 0.f), m = p, v = p;
+    float w = 0.f, wm = 0.f, wv = 0.f;
+    rec_bwd_state<E>(row, n_rep + u, q, first, row_ok, rec, rows_u, rows_u1, mv, c, t, ring, p, m, v, w, wm, wv);
+    if (row_ok) rec_bwd_apply<E>(s, row, q, first, p, m, v, w, wm, wv, rec, c, L, n_rep, g_rep, g1_rep, alpha, t);
+  });
 }
 
 // Rows [row0, row0 + n) updated with dense gradients g [n][E], g1 [n] (then zeroed).
@@ -700,6 +745,11 @@ extern "C" int dl_rec_bwd_adam(const dl_emb_layout* L, float* rec, int32_t rec_l
   DL_DISPATCH_E(L->emb_dim, {
     const unsigned grid = grid_cap(max_uniq * (kE / 4));
     hipLaunchKernelGGL(rec_bwd_adam_kernel<kE>, dim3(grid), dim3(256), 0, as_stream(stream), sg, rec,
+                       make_rec_cfg(kE, rec_ld, rec_flags, (mv_u ? 2 : hist_len)), n_rep, rows_u,
+                       has_first ? rows_u1 : nullptr, mv_u, uniq_keys, n_uniq, world, g_rep,
+                       has_first ? g1_rep : nullptr, hist, opt);
+    // the hot rows' long segments (none at uniform ids: one scan of the segment offsets)
+    hipLaunchKernelGGL(rec_bwd_long_kernel<kE>, dim3(1024), dim3(256), 0, as_stream(stream), sg, rec,
                        make_rec_cfg(kE, rec_ld, rec_flags, (mv_u ? 2 : hist_len)), n_rep, rows_u,
                        has_first ? rows_u1 : nullptr, mv_u, uniq_keys, n_uniq, world, g_rep,
                        has_first ? g1_rep : nullptr, hist, opt);

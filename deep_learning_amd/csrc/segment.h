@@ -145,57 +145,170 @@ __device__ __forceinline__ SegGrad4 segment_grad4_range(const SegGradIn& a, int 
   return r;
 }
 
-// Hot rows (Zipf ids): a segment longer than kSegLong references is not walked by its own
-// lane group, one reference after another, but by the whole wave: 64 / (E/4) slots of E/4
-// lanes each take the references slot, slot + NS, ... in order, and the slot sums are
-// combined by a fixed butterfly (lane xor E/4, 2E/4, ... 32).  Every lane of the wave must
-// call this, with the same (e0, e1); every lane gets the total for its dims 4q..4q+3.  The
-// order is fixed, so the sums are deterministic, and every kernel using it (the lazy
-// record update, the dense sorted backward, the sharded senders) sums a row alike.
+// One reference's contribution, loaded (fetch) apart from its accumulation (acc), so that
+// several references' loads can be in flight before the first is added; acc in reference
+// order performs exactly the operations of segment_grad4_range.
+struct SegRef {
+  int kind;     // 0 none, 1 pooled slot, 2 FM second order, 3 deep embedding
+  float4 v;     // g_pool row / fm_sum row / dx0 row
+  float dzb, w; // FM: dz[b], w_head[Cf + sl]; pooled: g1_pool (when present)
+};
+
+template <int E>
+__device__ __forceinline__ SegRef seg_fetch(const SegGradIn& a, bool in, int k, int q, long long nrefs) {
+  const dl_emb_layout& L = a.L;
+  const int S = L.cate_fields, ns = index_slots(L), mb = index_multi_base(L);
+  const int Cf = (L.use_fm && L.fm_cont) ? L.cont_fields : 0;
+  SegRef f{0, make_float4(0.f, 0.f, 0.f, 0.f), 0.f, 0.f};
+  if (!in) return f;
+  if (k < 0 || k >= nrefs) {
+    index_fault(a.status);
+    return f;
+  }
+  const int b = k / ns, sl = k % ns;
+  if (sl >= mb) {
+    const int l = sl - mb;
+    int m = 0;
+    while (m < a.n_slots && !(l >= a.slot_start[m] && l < a.slot_end[m])) ++m;
+    if (m == a.n_slots) return f;
+    const long long bm = (long long)b * a.n_slots + m;
+    f.kind = 1;
+    f.v = *reinterpret_cast<const float4*>(a.g_pool + bm * E + 4 * q);
+    f.w = a.g1_pool ? a.g1_pool[bm] : 0.f;
+  } else if (L.use_fm && sl < S) {
+    f.kind = 2;
+    f.dzb = a.dz[b];
+    f.v = *reinterpret_cast<const float4*>(a.fm_sum + (long long)b * E + 4 * q);
+    f.w = a.w_head[Cf + sl];
+  } else {
+    const int fi = L.use_fm ? sl - S : sl;
+    f.kind = 3;
+    f.v = *reinterpret_cast<const float4*>(a.dx0 + (long long)b * L.dx0_ld + L.dx0_cat_col + fi * E + 4 * q);
+  }
+  return f;
+}
+
+__device__ __forceinline__ void seg_acc(SegGrad4& r, const SegRef& f, float4 wsec, bool g1pool) {
+  if (f.kind == 1 || f.kind == 3) {
+    r.x.x += f.v.x; r.x.y += f.v.y; r.x.z += f.v.z; r.x.w += f.v.w;
+    if (f.kind == 1 && g1pool) r.g1 += f.w;
+  } else if (f.kind == 2) {
+    const float4 ds = make_float4(f.dzb * wsec.x, f.dzb * wsec.y, f.dzb * wsec.z, f.dzb * wsec.w);
+    r.s.x = fmaf(ds.x, f.v.x, r.s.x); r.s.y = fmaf(ds.y, f.v.y, r.s.y);
+    r.s.z = fmaf(ds.z, f.v.z, r.s.z); r.s.w = fmaf(ds.w, f.v.w, r.s.w);
+    r.dsum.x += ds.x; r.dsum.y += ds.y; r.dsum.z += ds.z; r.dsum.w += ds.w;
+    r.g1 = fmaf(f.dzb, f.w, r.g1);
+  }
+}
+
+// segment_grad4_range over e0, e0 + stride, ... < e1 with four references' loads in flight
+// at a time (same sums, same order)
+template <int E>
+__device__ __forceinline__ SegGrad4 segment_grad4_strided(const SegGradIn& a, int e0, int e1, int stride, int q,
+                                                          long long nrefs, float4 wsec) {
+  const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
+  SegGrad4 r{z, z, z, 0.f};
+  const bool g1pool = a.g1_pool != nullptr;
+  for (int e = e0; e < e1; e += 4 * stride) {
+    int k[4];
+    bool in[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      in[i] = e + i * stride < e1;
+      k[i] = in[i] ? a.refs[e + i * stride] : -1;
+    }
+    SegRef f[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) f[i] = seg_fetch<E>(a, in[i], k[i], q, nrefs);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) seg_acc(r, f[i], wsec, g1pool);
+  }
+  return r;
+}
+
+// Hot rows (Zipf ids; a Zipf batch's hottest rows have ~15 k references, where one lane
+// group used to take ~15 k dependent loads).  A segment of more than kSegLong references is
+// left out of the per-row pass and summed in a second pass by a whole 256-thread block:
+// 256 / (E/4) slots of E/4 lanes each take the references slot, slot + NS, ... in order
+// (four loads in flight); a wave's slot sums are combined by a fixed butterfly (lane xor E/4,
+// 2E/4, ... 32), the block's four wave sums in wave order.  The order is fixed, so the sums
+// are deterministic, and every kernel using it (the lazy record update, the dense sorted
+// backward, the sharded senders) sums a row alike.  The per-row pass keeps its registers
+// (and occupancy): a long segment costs it one length test.
 constexpr int kSegLong = 32;
 
 __device__ __forceinline__ float4 seg_xor4(float4 v, int m) {
   return make_float4(__shfl_xor(v.x, m, 64), __shfl_xor(v.y, m, 64), __shfl_xor(v.z, m, 64), __shfl_xor(v.w, m, 64));
 }
+__device__ __forceinline__ float4 f4add(float4 a, float4 b) { return make_float4(a.x + b.x, a.y + b.y, a.z + b.z, a.w + b.w); }
 
-template <int E>
-__device__ __forceinline__ SegGrad4 segment_grad4_wave(const SegGradIn& a, int e0, int e1, long long nrefs,
-                                                       float4 wsec) {
-  constexpr int LPR = E / 4, NS = 64 / LPR;
-  const int lane = threadIdx.x & 63, q = lane % LPR, slot = lane / LPR;
-  SegGrad4 r = segment_grad4_range<E>(a, e0 + slot, e1, -2, q, nrefs, wsec, NS);
+template <int LPR>
+__device__ __forceinline__ void seg_wave_butterfly(SegGrad4& r) {
 #pragma unroll
   for (int m = LPR; m < 64; m <<= 1) {
-    const float4 s2 = seg_xor4(r.s, m), x2 = seg_xor4(r.x, m), d2 = seg_xor4(r.dsum, m);
-    const float g2 = __shfl_xor(r.g1, m, 64);
-    // lower slot first, so both partners form the same sum
-    const bool lo = (lane & m) == 0;
-    r.s = lo ? make_float4(r.s.x + s2.x, r.s.y + s2.y, r.s.z + s2.z, r.s.w + s2.w)
-             : make_float4(s2.x + r.s.x, s2.y + r.s.y, s2.z + r.s.z, s2.w + r.s.w);
-    r.x = lo ? make_float4(r.x.x + x2.x, r.x.y + x2.y, r.x.z + x2.z, r.x.w + x2.w)
-             : make_float4(x2.x + r.x.x, x2.y + r.x.y, x2.z + r.x.z, x2.w + r.x.w);
-    r.dsum = lo ? make_float4(r.dsum.x + d2.x, r.dsum.y + d2.y, r.dsum.z + d2.z, r.dsum.w + d2.w)
-                : make_float4(d2.x + r.dsum.x, d2.y + r.dsum.y, d2.z + r.dsum.z, d2.w + r.dsum.w);
-    r.g1 = lo ? r.g1 + g2 : g2 + r.g1;
+    r.s = f4add(r.s, seg_xor4(r.s, m));
+    r.x = f4add(r.x, seg_xor4(r.x, m));
+    r.dsum = f4add(r.dsum, seg_xor4(r.dsum, m));
+    r.g1 += __shfl_xor(r.g1, m, 64);
   }
-  return r;
 }
 
-// The wave's long segments, one after another (wave-uniform loop): a lane group whose
-// segment [e0, e1) is longer than kSegLong gets its sums here; the others keep theirs.
-// Every lane of the wave must call this.
+struct SegLongLds {   // per block
+  int n;
+  int u[256];
+  float4 s[4][16], x[4][16], d[4][16];   // per wave, per q (E/4 <= 16)
+  float g1[4];
+};
+
+// One long segment summed by the whole block (every thread calls it); the total lands in
+// threads 0 .. E/4 - 1 (lane q = thread).
 template <int E>
-__device__ __forceinline__ void segment_grad4_long(const SegGradIn& a, int e0, int e1, bool mine_long,
-                                                   long long nrefs, float4 wsec, SegGrad4& out) {
-  constexpr int LPR = E / 4;
-  const int lane = threadIdx.x & 63;
-  uint64_t todo = __ballot(mine_long && (lane % LPR) == 0);
-  while (todo) {
-    const int leader = __builtin_ctzll(todo);
-    todo &= todo - 1;
-    const int le0 = __shfl(e0, leader, 64), le1 = __shfl(e1, leader, 64);
-    const SegGrad4 t = segment_grad4_wave<E>(a, le0, le1, nrefs, wsec);
-    if (lane / LPR == leader / LPR) out = t;
+__device__ __forceinline__ SegGrad4 segment_grad4_block(const SegGradIn& a, int e0, int e1, long long nrefs,
+                                                        float4 wsec, SegLongLds& sh) {
+  constexpr int LPR = E / 4, NS = 256 / LPR;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, q = tid % LPR;
+  SegGrad4 r = segment_grad4_strided<E>(a, e0 + tid / LPR, e1, NS, q, nrefs, wsec);
+  seg_wave_butterfly<LPR>(r);
+  if (lane < LPR) {
+    sh.s[wv][lane] = r.s; sh.x[wv][lane] = r.x; sh.d[wv][lane] = r.dsum;
+    if (lane == 0) sh.g1[wv] = r.g1;
+  }
+  __syncthreads();
+  SegGrad4 t = {sh.s[0][q], sh.x[0][q], sh.d[0][q], sh.g1[0]};
+#pragma unroll
+  for (int w = 1; w < 4; ++w) {
+    t.s = f4add(t.s, sh.s[w][q]); t.x = f4add(t.x, sh.x[w][q]); t.dsum = f4add(t.dsum, sh.d[w][q]);
+    t.g1 += sh.g1[w];
+  }
+  __syncthreads();   // the partials are re-used by the next segment
+  return t;
+}
+
+// Second pass over the long segments: block b scans its share of the unique rows for
+// segments of more than kSegLong references and calls fn(u, sums) for each, in threads
+// 0 .. E/4 - 1, after the whole block summed it.  Block-uniform; one barrier per 256 rows.
+template <int E, class Fn>
+__device__ __forceinline__ void for_long_segments(const SegGradIn& a, long long nu, long long nrefs, float4 wsec,
+                                                  SegLongLds& sh, Fn&& fn) {
+  const int tid = threadIdx.x;
+  const long long per = (nu + gridDim.x - 1) / gridDim.x;
+  const long long u0 = (long long)blockIdx.x * per, u1 = min(nu, u0 + per);
+  for (long long base = u0; base < u1; base += 256) {
+    const long long u = base + tid;
+    const SegRange cr = seg_range(a, u < u1 ? u : nu, nu, nrefs);
+    const bool lng = cr.e1 - cr.e0 > kSegLong;
+    if (tid == 0) sh.n = 0;
+    if (!__syncthreads_or(lng)) continue;
+    if (lng) sh.u[atomicAdd(&sh.n, 1)] = (int)(u - base);
+    __syncthreads();
+    const int n = sh.n;
+    for (int k = 0; k < n; ++k) {
+      const long long uu = base + sh.u[k];
+      const SegRange r = seg_range(a, uu, nu, nrefs);
+      const SegGrad4 t = segment_grad4_block<E>(a, r.e0, r.e1, nrefs, wsec, sh);
+      if (tid < E / 4) fn(uu, t);
+    }
+    __syncthreads();   // sh.n / sh.u before the next chunk
   }
 }
 
