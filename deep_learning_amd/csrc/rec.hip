@@ -30,7 +30,7 @@
 #include "segment.h"
 
 #ifndef DL_REC_FULL_LINES
-#define DL_REC_FULL_LINES 0
+#define DL_REC_FULL_LINES 1   // record updates also write the pad (see rec_write_pad)
 #endif
 
 namespace dl {
@@ -277,6 +277,17 @@ __global__ __launch_bounds__(256) void pool_grad_kernel(dl_emb_layout L, dl_pool
   }
 }
 
+// A record update writes p, the tail, m and v — 208 of the 256 B at E = 16, so the record's
+// second 128-B line would be left partly dirty and merged with its old bytes below the L2
+// (a read of the line per update).  Writing the pad (zeros) too makes both lines whole:
+// same-box C2, rec_bwd_adam 531 -> 452 us, step 2.49 -> 2.39 ms.
+template <int E>
+__device__ __forceinline__ void rec_write_pad(float* __restrict__ r, int q, int ld) {
+#if DL_REC_FULL_LINES
+  for (int o = 3 * E + 4 + 4 * q; o < ld; o += E) *reinterpret_cast<float4*>(r + o) = make_float4(0.f, 0.f, 0.f, 0.f);
+#endif
+}
+
 // The backward's per-row state: the caught-up p, m, v (and first-order triple) of unique
 // row u — from the gather's stash, or the record caught up again without one.
 template <int E>
@@ -335,11 +346,7 @@ __device__ __forceinline__ void rec_bwd_apply(const SegGrad4& s, int64_t row, in
     if (first) rec_adam(w, wm, wv, s.g1, alpha, c);
     *reinterpret_cast<float4*>(r + E) = make_float4(w, wm, wv, __int_as_float(t));
   }
-#if DL_REC_FULL_LINES
-  // the record's pad too (zeros): the row's last 128-B line is written whole, so no
-  // partially dirty line has to be merged with its old bytes below the L2
-  for (int o = 3 * E + 4 + 4 * q; o < c.ld; o += E) *reinterpret_cast<float4*>(r + o) = make_float4(0.f, 0.f, 0.f, 0.f);
-#endif
+  rec_write_pad<E>(r, q, c.ld);
 }
 
 #define DL_REC_BWD_PARAMS                                                                                    \
@@ -564,6 +571,7 @@ __global__ __launch_bounds__(256) void rec_apply_segments_kernel(float* __restri
       if (first) rec_adam(w, wm, wv, g1s, alpha, c);
       *reinterpret_cast<float4*>(r + E) = make_float4(w, wm, wv, __int_as_float(t));
     }
+    rec_write_pad<E>(r, q, c.ld);
   }
 }
 
@@ -643,6 +651,7 @@ __global__ __launch_bounds__(256) void rec_apply_chain_kernel(float* __restrict_
       if (first) rec_adam(w, wm, wv, g1s, alpha, c);
       *reinterpret_cast<float4*>(r + E) = make_float4(w, wm, wv, __int_as_float(t));
     }
+    rec_write_pad<E>(r, q, c.ld);
   }
 }
 
