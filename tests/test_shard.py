@@ -141,3 +141,15 @@ def test_sharded_wdl_two_ranks_equals_global_batch(tmp_path, mode):
         all_y.append(b["label"].reshape(-1))
     assert float(d[0]["auc"]) == float(d[1]["auc"])
     assert abs(float(d[0]["auc"]) - R.auc(np.concatenate(all_y), np.concatenate(all_s))) < (2e-3 if bf else 1e-4)
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_exchange_p2p_matches_all_to_all(world):
+    """Exchange's grouped point-to-point all-to-all (the RCCL path: own segment copied on
+    the device) equals all_to_all_single on uneven splits with zero-size transfers (gloo)."""
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", OMP_NUM_THREADS="1")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(world),
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
+           os.path.join(ROOT, "tests", "exchange_worker.py")]
+    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=300, cwd=ROOT)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
