@@ -63,12 +63,15 @@ __global__ __launch_bounds__(256) void adam_dense_thread_kernel(float* __restric
   float sq = 0.f;
   for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n;
        i += (long long)gridDim.x * blockDim.x) {
+    // the slab column: 16 loads in flight per round trip, added in slab order (the same sum)
     float g = 0.f;
     int s = 0;
-    for (; s + 4 <= nslab; s += 4) {
-      const float a0 = slab[(s + 0) * stride + i], a1 = slab[(s + 1) * stride + i];
-      const float a2 = slab[(s + 2) * stride + i], a3 = slab[(s + 3) * stride + i];
-      g += a0; g += a1; g += a2; g += a3;
+    for (; s + 16 <= nslab; s += 16) {
+      float a[16];
+#pragma unroll
+      for (int j = 0; j < 16; ++j) a[j] = slab[(s + j) * stride + i];
+#pragma unroll
+      for (int j = 0; j < 16; ++j) g += a[j];
     }
     for (; s < nslab; ++s) g += slab[s * stride + i];
     float pi = p[i], mi = m[i], vi = v[i];
