@@ -362,7 +362,7 @@ __global__ __launch_bounds__(256) void embed_bwd_kernel(EmbBwdArgs a) {
 
   if (Cf > 0) {
     // block reduction of the hot rows -> cont_slab[block][Cf*(E+1)]
-    __shared__ float red[4][kMaxHotCont * 65];
+    __shared__ float red[4][kMaxHotCont * (E + 1)];   // 8.7 KB at E = 16: LDS does not cap the occupancy
     const int width = Cf * (E + 1);
 #pragma unroll
     for (int p = 0; p < NCP; ++p) {
@@ -374,6 +374,84 @@ __global__ __launch_bounds__(256) void embed_bwd_kernel(EmbBwdArgs a) {
     for (int k = threadIdx.x; k < width; k += blockDim.x)
       a.cont_slab[(int64_t)blockIdx.x * width + k] = red[0][k] + red[1][k] + red[2][k] + red[3][k];
   }
+}
+
+// The FM cont-field rows every sample hits, alone (the sorted / lazy backward does the
+// rest): E / 4 lanes per sample, one float4 of the dims each, every field of the sample in
+// the lane's registers, so a wave covers 64 / (E / 4) samples per load round trip instead
+// of one.  Per-element terms as embed_bwd_kernel's; block partials to cont_slab[block].
+template <int E, int NC>
+__global__ __launch_bounds__(256) void cont_bwd_kernel(EmbBwdArgs a) {
+  constexpr int QPR = E / 4, SPW = 64 / QPR;
+  const dl_emb_layout& L = a.L;
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int q = lane % QPR;
+  const int Cf = L.cont_fields;
+  const int F = Cf + L.cate_fields + L.fm_extra;
+  const float w0 = a.w_head[F + 4 * q], w1 = a.w_head[F + 4 * q + 1];
+  const float w2 = a.w_head[F + 4 * q + 2], w3 = a.w_head[F + 4 * q + 3];
+  float4 gc[NC];
+  float g1[NC / QPR];
+#pragma unroll
+  for (int f = 0; f < NC; ++f) gc[f] = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+  for (int j = 0; j < NC / QPR; ++j) g1[j] = 0.f;
+  // the butterfly below is the costly part (ds_bpermute), so the samples are dealt to the
+  // first `active` blocks, four wave iterations each; the rest write zero slabs
+  const int active = min((int)gridDim.x, max(1, (L.batch + 16 * SPW - 1) / (16 * SPW)));
+  const int nw = active * (blockDim.x >> 6);
+  for (int b = blockIdx.x < active ? ((blockIdx.x * blockDim.x + threadIdx.x) >> 6) * SPW + lane / QPR : L.batch;
+       b < L.batch; b += nw * SPW) {
+    const float dzb = a.dz[b];
+    const float4 sd = *reinterpret_cast<const float4*>(a.fm_sum + (int64_t)b * E + 4 * q);
+    const float* cb = a.cont + (int64_t)b * Cf;
+    const float d0 = dzb * w0, d1 = dzb * w1, d2 = dzb * w2, d3 = dzb * w3;
+#pragma unroll
+    for (int f = 0; f < NC; ++f) {
+      if (f < Cf) {
+        const int64_t row = L.fm_cont_offset + f;
+        const float val = cb[f];
+        float4 e = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (row_ok(row, L.zero_row0)) {
+          e = *reinterpret_cast<const float4*>(a.table + (L.cont_rows_compact ? f : row) * E + 4 * q);
+          e.x *= val; e.y *= val; e.z *= val; e.w *= val;
+        }
+        gc[f].x += val * d0 * (sd.x - e.x); gc[f].y += val * d1 * (sd.y - e.y);
+        gc[f].z += val * d2 * (sd.z - e.z); gc[f].w += val * d3 * (sd.w - e.w);
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < NC / QPR; ++j) {
+      const int f = q + QPR * j;
+      if (f < Cf) g1[j] += dzb * a.w_head[f] * cb[f];
+    }
+  }
+  // the wave's SPW samples (lanes with the same q) summed by butterfly
+#pragma unroll
+  for (int o = QPR; o < 64; o <<= 1) {
+#pragma unroll
+    for (int f = 0; f < NC; ++f) {
+      if (f < Cf) {
+        gc[f].x += __shfl_xor(gc[f].x, o, 64); gc[f].y += __shfl_xor(gc[f].y, o, 64);
+        gc[f].z += __shfl_xor(gc[f].z, o, 64); gc[f].w += __shfl_xor(gc[f].w, o, 64);
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < NC / QPR; ++j) g1[j] += __shfl_xor(g1[j], o, 64);
+  }
+  __shared__ __align__(16) float red[4][NC * (E + 1)];
+  if (lane < QPR) {
+#pragma unroll
+    for (int f = 0; f < NC; ++f)
+      if (f < Cf) *reinterpret_cast<float4*>(&red[wid][f * E + 4 * q]) = gc[f];
+#pragma unroll
+    for (int j = 0; j < NC / QPR; ++j)
+      if (q + QPR * j < Cf) red[wid][Cf * E + q + QPR * j] = g1[j];
+  }
+  __syncthreads();
+  const int width = Cf * (E + 1);
+  for (int k = threadIdx.x; k < width; k += blockDim.x)
+    a.cont_slab[(int64_t)blockIdx.x * width + k] = red[0][k] + red[1][k] + red[2][k] + red[3][k];
 }
 
 // Folds the cont-field partial slabs into the dense gradient tables.
@@ -931,7 +1009,11 @@ extern "C" int dl_embed_cont_bwd(const dl_emb_layout* L, const float* table, con
   const int grid = dl_embed_bwd_grid(L);
   DL_CHECK_ARG(cont_slab && cont_slab_blocks >= grid, "cont_slab needs %d blocks", grid);
   EmbBwdArgs a{*L, table, nullptr, cont, dz, w_head, fm_sum, nullptr, nullptr, nullptr, nullptr, cont_slab};
-  DL_DISPATCH_E(L->emb_dim, hipLaunchKernelGGL((embed_bwd_kernel<kE, true>), dim3(grid), dim3(256), 0,
-                                               as_stream(stream), a));
+  DL_DISPATCH_E(L->emb_dim, {
+    if (L->cont_fields <= 16)
+      hipLaunchKernelGGL((cont_bwd_kernel<kE, 16>), dim3(grid), dim3(256), 0, as_stream(stream), a);
+    else
+      hipLaunchKernelGGL((cont_bwd_kernel<kE, kMaxHotCont>), dim3(grid), dim3(256), 0, as_stream(stream), a);
+  });
   DL_RETURN_LAUNCH("dl_embed_cont_bwd");
 }

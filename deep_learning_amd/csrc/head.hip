@@ -49,54 +49,73 @@ __global__ __launch_bounds__(256) void head_kernel(int B, int fm_cols, int H, co
   for (int k = 0; k < kHeadMaxH4; ++k) gh[k] = make_float4(0.f, 0.f, 0.f, 0.f);
   float gb = 0.f, lsum = 0.f;
 
-  for (int b = wave; b < B; b += nwaves) {
-    float ff[kHeadMaxFm / 64];
-    float4 hh[kHeadMaxH4];
-    float part = 0.f;
+  // Four samples per round: their rows are loaded together (four round trips in flight
+  // per wave instead of one), then reduced in the same sample order as a one-sample loop.
+  constexpr int kAhead = 4;
+  for (int b0 = wave; b0 < B; b0 += kAhead * nwaves) {
+    float ff[kAhead][kHeadMaxFm / 64];
+    float4 hh[kAhead][kHeadMaxH4];
+    float yy[kAhead];
 #pragma unroll
-    for (int k = 0; k < kHeadMaxFm / 64; ++k) {
-      const int c = lane + 64 * k;
-      ff[k] = c < fm_cols ? fm_out[(long long)b * fm_ld + c] : 0.f;
-      part += ff[k] * wf[k];
-    }
-    const float* hb = h + (long long)b * ldh;
+    for (int i = 0; i < kAhead; ++i) {
+      const int b = b0 + i * nwaves;
+      const bool ok = b < B;
 #pragma unroll
-    for (int k = 0; k < kHeadMaxH4; ++k) {
-      const int c4 = lane + 64 * k;
-      hh[k] = c4 < H4 ? *reinterpret_cast<const float4*>(hb + 4 * c4) : make_float4(0.f, 0.f, 0.f, 0.f);
-      part += hh[k].x * wh[k].x + hh[k].y * wh[k].y + hh[k].z * wh[k].z + hh[k].w * wh[k].w;
-    }
-    const float z = wave_sum(part) + bias;
-    const float p = 1.f / (1.f + expf(-z));
-    const float y = label[b];
-    const float dp = (-y / (p + eps) + (1.f - y) / (1.f - p + eps)) * inv_batch;
-    const float g = dp * p * (1.f - p);   // SigmoidGrad
-    if (lane == 0) {
-      score[b] = p;
-      if (z_out) z_out[b] = z;
-      dz[b] = g;
-      gb += g;
-      lsum += -y * logf(p + eps) - (1.f - y) * logf(1.f - p + eps);
+      for (int k = 0; k < kHeadMaxFm / 64; ++k) {
+        const int c = lane + 64 * k;
+        ff[i][k] = ok && c < fm_cols ? fm_out[(long long)b * fm_ld + c] : 0.f;
+      }
+      const float* hb = h + (long long)b * ldh;
+#pragma unroll
+      for (int k = 0; k < kHeadMaxH4; ++k) {
+        const int c4 = lane + 64 * k;
+        hh[i][k] = ok && c4 < H4 ? *reinterpret_cast<const float4*>(hb + 4 * c4) : make_float4(0.f, 0.f, 0.f, 0.f);
+      }
+      yy[i] = ok ? label[b] : 0.f;
     }
 #pragma unroll
-    for (int k = 0; k < kHeadMaxFm / 64; ++k) gf[k] += g * ff[k];
-    float* dhb = dh + (long long)b * ldh;
+    for (int i = 0; i < kAhead; ++i) {
+      const int b = b0 + i * nwaves;
+      if (b >= B) break;   // wave-uniform
+      float part = 0.f;
 #pragma unroll
-    for (int k = 0; k < kHeadMaxH4; ++k) {
-      const int c4 = lane + 64 * k;
-      gh[k].x += g * hh[k].x; gh[k].y += g * hh[k].y; gh[k].z += g * hh[k].z; gh[k].w += g * hh[k].w;
-      if (c4 < H4) {
-        const int c = 4 * c4;
-        float4 o;
-        o.x = hh[k].x > 0.f ? g * wh[k].x : 0.f;
-        o.y = hh[k].y > 0.f ? g * wh[k].y : 0.f;
-        o.z = hh[k].z > 0.f ? g * wh[k].z : 0.f;
-        o.w = hh[k].w > 0.f ? g * wh[k].w : 0.f;
-        if (c + 3 < H) *reinterpret_cast<float4*>(dhb + c) = o;
-        else {
-          if (c + 0 < H) dhb[c + 0] = o.x;
-          if (c + 1 < H) dhb[c + 1] = o.y;
-          if (c + 2 < H) dhb[c + 2] = o.z;
+      for (int k = 0; k < kHeadMaxFm / 64; ++k) part += ff[i][k] * wf[k];
+#pragma unroll
+      for (int k = 0; k < kHeadMaxH4; ++k)
+        part += hh[i][k].x * wh[k].x + hh[i][k].y * wh[k].y + hh[i][k].z * wh[k].z + hh[i][k].w * wh[k].w;
+      const float z = wave_sum(part) + bias;
+      const float p = 1.f / (1.f + expf(-z));
+      const float y = yy[i];
+      const float dp = (-y / (p + eps) + (1.f - y) / (1.f - p + eps)) * inv_batch;
+      const float g = dp * p * (1.f - p);   // SigmoidGrad
+      if (lane == 0) {
+        score[b] = p;
+        if (z_out) z_out[b] = z;
+        dz[b] = g;
+        gb += g;
+        lsum += -y * logf(p + eps) - (1.f - y) * logf(1.f - p + eps);
+      }
+#pragma unroll
+      for (int k = 0; k < kHeadMaxFm / 64; ++k) gf[k] += g * ff[i][k];
+      float* dhb = dh + (long long)b * ldh;
+#pragma unroll
+      for (int k = 0; k < kHeadMaxH4; ++k) {
+        const int c4 = lane + 64 * k;
+        gh[k].x += g * hh[i][k].x; gh[k].y += g * hh[i][k].y;
+        gh[k].z += g * hh[i][k].z; gh[k].w += g * hh[i][k].w;
+        if (c4 < H4) {
+          const int c = 4 * c4;
+          float4 o;
+          o.x = hh[i][k].x > 0.f ? g * wh[k].x : 0.f;
+          o.y = hh[i][k].y > 0.f ? g * wh[k].y : 0.f;
+          o.z = hh[i][k].z > 0.f ? g * wh[k].z : 0.f;
+          o.w = hh[i][k].w > 0.f ? g * wh[k].w : 0.f;
+          if (c + 3 < H) *reinterpret_cast<float4*>(dhb + c) = o;
+          else {
+            if (c + 0 < H) dhb[c + 0] = o.x;
+            if (c + 1 < H) dhb[c + 1] = o.y;
+            if (c + 2 < H) dhb[c + 2] = o.z;
+          }
         }
       }
     }
