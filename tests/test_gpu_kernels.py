@@ -649,3 +649,57 @@ def test_wdl_head_bf16_dy_is_rounded_f32_dy(hip_lib, B):
     np.testing.assert_allclose(f[4].double().numpy() / 2.0 ** 48, gref.numpy(), rtol=0, atol=1e-12)
     z_ref = w.double()[wide].sum(1) + h[:, :H].double() @ w.double()[Fw:Fw + H] + 0.1
     np.testing.assert_allclose(f[1].double().numpy(), z_ref.numpy(), rtol=0, atol=1e-4)
+
+
+@pytest.mark.parametrize("n", [1003, 4096 * 256 * 4 * 2 + 4 * 100 + 3])
+@pytest.mark.parametrize("flags", [0, _lib.ROWS_SPARSE_ADAM, _lib.ROWS_GRAD_FIXED,
+                                   _lib.ROWS_GRAD_FIXED | _lib.ROWS_SPARSE_ADAM])
+def test_adam_rows_width1_sweep(hip_lib, n, flags):
+    """dl_adam_rows at width 1 (first-order / wdl wide weights, optim.hip adam_rows1_kernel):
+    every row steps (touched rows with their gradient, the rest with g = l2*p), the consumed
+    gradients and flags are reset, sq = sum p^2; n with a 3-row tail, and large enough that
+    each thread takes two groups per round.  p
+    goes through the hardware reciprocal; all three are held to f32-rounding tolerances."""
+    rng = np.random.default_rng(n + flags)
+    p = rng.standard_normal(n).astype(np.float32)
+    m = (rng.standard_normal(n) * 1e-2).astype(np.float32)
+    v = (rng.random(n) * 1e-3).astype(np.float32)
+    touched = (rng.random(n) < 0.3).astype(np.uint8)
+    fixed = bool(flags & _lib.ROWS_GRAD_FIXED)
+    # the gradient table's invariant: zero outside the touched rows
+    gf = np.where(touched == 1, rng.standard_normal(n) * 1e-2, 0).astype(np.float32)
+    if fixed:
+        gq = np.round(gf.astype(np.float64) * 2.0 ** 48).astype(np.int64)
+        g_d = torch.from_numpy(gq).cuda()
+        g_eff = (gq.astype(np.float64) * 2.0 ** -48).astype(np.float32)
+    else:
+        g_d = torch.from_numpy(gf).cuda()
+        g_eff = gf
+    g_eff = np.where(touched == 1, g_eff, np.float32(0))
+    l2 = np.float32(1e-3)
+    b1, b2, eps, alpha = np.float32(0.9), np.float32(0.999), np.float32(1e-8), np.float32(1e-3)
+    opt = torch.zeros(_lib.OPT_LEN, dtype=torch.float32)
+    opt[3], opt[4], opt[5], opt[6] = float(alpha), float(b1), float(b2), float(eps)
+    opt = opt.cuda()
+    sq = torch.zeros(1, dtype=torch.float32, device="cuda")
+    pd, md, vd = (torch.from_numpy(a.copy()).cuda() for a in (p, m, v))
+    td = torch.from_numpy(touched.copy()).cuda()
+    call("dl_adam_rows", ptr(pd), ptr(md), ptr(vd), ptr(g_d), ptr(td), n, 1, float(l2),
+         flags | _lib.ROWS_CLEAR_TOUCHED, ptr(opt), ptr(sq), _s())
+    torch.cuda.synchronize()
+    g = (g_eff + l2 * p).astype(np.float32)
+    omb1, omb2 = np.float32(1) - b1, np.float32(1) - b2
+    if flags & _lib.ROWS_SPARSE_ADAM:
+        m1 = (m * b1 + g * omb1).astype(np.float32)
+        v1 = (v * b2 + (g * g) * omb2).astype(np.float32)
+    else:
+        m1 = (m + (g - m) * omb1).astype(np.float32)
+        v1 = (v + (g * g - v) * omb2).astype(np.float32)
+    p1 = (p - (m1 * alpha) / (np.sqrt(v1) + eps)).astype(np.float32)
+    # g + l2*p may contract to an fma on the device: m, v within f32 rounding, not bit-equal
+    np.testing.assert_allclose(md.cpu().numpy(), m1, rtol=2e-6, atol=2e-9)
+    np.testing.assert_allclose(vd.cpu().numpy(), v1, rtol=2e-6, atol=2e-11)
+    np.testing.assert_allclose(pd.cpu().numpy(), p1, rtol=1e-6, atol=1e-7)
+    assert int(td.sum()) == 0
+    assert not torch.any(g_d != 0)
+    np.testing.assert_allclose(float(sq.item()), float(np.sum(p.astype(np.float64) ** 2)), rtol=1e-4)
