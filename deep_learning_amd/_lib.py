@@ -87,6 +87,7 @@ SIGNATURES = {
     "dl_slab_fold_rows": (I32, [P, I32, I32, I32, I32, P, I64, P, P]),
     "dl_adam_begin_step": (I32, [P, F, F, P]),
     "dl_step_guard": (I32, [P, P, P]),
+    "dl_step_begin": (I32, [P, P, F, F, P, I32, P]),
     "dl_adam_dense": (I32, [P, P, P, P, I32, I64, I64, F, I64, P, P, P, P]),
     "dl_adam_dense_reg": (I32, [P, P, P, P, I32, I64, I64, F, I64, I32, P, P, P, P]),
     "dl_adam_rows": (I32, [P, P, P, P, P, I64, I32, F, I32, P, P, P]),

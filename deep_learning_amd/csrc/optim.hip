@@ -28,7 +28,7 @@ __device__ __forceinline__ void block_atomic_add(float x, float* out) {
 }
 
 // opt: [0] b1p [1] b2p [2] lr [3] alpha [4] b1 [5] b2 [6] eps [7] step
-__global__ void adam_begin_kernel(float* opt, float decay_rate, float decay_steps) {
+__device__ __forceinline__ void adam_begin_body(float* opt, float decay_rate, float decay_steps) {
   if (step_poisoned(opt)) return;   // a failed batch: the step does not begin (common.h)
   const float step = opt[7];
   const float pw = floorf(step / decay_steps);                   // staircase=True
@@ -41,12 +41,29 @@ __global__ void adam_begin_kernel(float* opt, float decay_rate, float decay_step
   for (int i = 8; i < 16; ++i) opt[i] = 0.f;                     // per-step L2 accumulators
 }
 
+__global__ void adam_begin_kernel(float* opt, float decay_rate, float decay_steps) {
+  adam_begin_body(opt, decay_rate, decay_steps);
+}
+
 // The batch's id validation (dl_index_build / the forward's err word) poisons the step it
 // belongs to: opt's sticky status word gets the batch's error bits before the step begins.
-__global__ void step_guard_kernel(const int32_t* batch_err, float* opt) {
+__device__ __forceinline__ void step_guard_kernel_body(const int32_t* batch_err, float* opt) {
   const int e = batch_err[0];
   if (e) opt_status(opt)[0] |= (e & DL_STATUS_BAD_ID) ? DL_STATUS_BAD_ID : e;
 }
+
+__global__ void step_guard_kernel(const int32_t* batch_err, float* opt) { step_guard_kernel_body(batch_err, opt); }
+
+// The three scalar updates that open a training step, in one launch (one graph node instead
+// of three): the guard (dl_step_guard), the Adam step begin (dl_adam_begin_step) and, for the
+// lazy tables, the alpha ring entry (dl_adam_hist_record) — the same operations in the same order.
+__global__ void step_begin_kernel(const int32_t* batch_err, float* opt, float decay_rate, float decay_steps,
+                                  float* hist, int mask) {
+  step_guard_kernel_body(batch_err, opt);
+  adam_begin_body(opt, decay_rate, decay_steps);
+  if (hist) hist[(int)opt[7] & mask] = opt[3];
+}
+
 
 // Dense parameter, gradient = sum of partial slabs (+ l2 * p for i < l2_count).
 // REG: 0 = L2 (g += l2 * p, sq_out += p^2: tf.contrib.layers.l2_regularizer), 1 = L1
@@ -289,6 +306,15 @@ extern "C" int dl_step_guard(const int32_t* batch_err, float* opt, void* stream)
   DL_CHECK_ARG(batch_err && opt, "NULL pointer");
   hipLaunchKernelGGL(step_guard_kernel, dim3(1), dim3(1), 0, as_stream(stream), batch_err, opt);
   DL_RETURN_LAUNCH("dl_step_guard");
+}
+
+extern "C" int dl_step_begin(const int32_t* batch_err, float* opt, float decay_rate, float decay_steps, float* hist,
+                             int32_t hist_len, void* stream) {
+  DL_CHECK_ARG(batch_err && opt, "NULL pointer");
+  DL_CHECK_ARG(!hist || (hist_len >= 2 && (hist_len & (hist_len - 1)) == 0), "bad hist");
+  hipLaunchKernelGGL(step_begin_kernel, dim3(1), dim3(1), 0, as_stream(stream), batch_err, opt, decay_rate,
+                     decay_steps, hist, hist ? hist_len - 1 : 0);
+  DL_RETURN_LAUNCH("dl_step_begin");
 }
 
 extern "C" int dl_adam_dense_reg(float* p, float* m, float* v, const float* slab, int32_t nslab,

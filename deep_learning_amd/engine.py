@@ -764,10 +764,9 @@ class CTREngine:
         s = _lib.stream_handle()
         L = self.layout
         # a batch whose ids failed validation (index build) poisons the step: nothing is applied
-        self._c("step_guard", "dl_step_guard", ptr(self.err), ptr(self.opt), s)
-        self._c("adam_begin", "dl_adam_begin_step", ptr(self.opt), sp.decay_rate, float(sp.decay_steps), s)
-        if self.lazy:
-            self._c("adam_hist", "dl_adam_hist_record", ptr(self.opt), ptr(self.hist), self.hist_len, s)
+        # (dl_step_begin: the guard, the Adam step begin and the lazy tables' alpha ring entry)
+        self._c("step_begin", "dl_step_begin", ptr(self.err), ptr(self.opt), sp.decay_rate, float(sp.decay_steps),
+                ptr(self.hist) if self.lazy else None, self.hist_len if self.lazy else 0, s)
         self._forward(B, s, train=True)
         if not self.lazy or self.wdl:
             # ids validated inside the forward (dense-layout gather, wdl wide ids): the updates

@@ -682,10 +682,31 @@ class ShardedCTREngine(CTREngine):
 
     def _count_vec(self):
         """The per-owner counts every rank all-gathers: table rows (+ replicated), and for wdl
-        the wide rows too (one collective for both)."""
-        if self.wdl:
-            return torch.cat([self.owner_counts, self.wowner_counts])
-        return self.owner_counts
+        the wide rows too (one collective for both), then the batch's id-validation word, so
+        every rank learns from the same collective whether any rank's batch holds a bad id."""
+        parts = [self.owner_counts] + ([self.wowner_counts] if self.wdl else []) + [self.err[:1]]
+        return torch.cat(parts)
+
+    def _split_counts(self, cm):
+        """Strip the id-validation column off the all-gathered counts.  A bad id on any rank
+        raises on every rank before the step begins (TF's InvalidArgumentError in the failing
+        sess.run, deepfm_pipeline.py:219-221): nothing is exchanged or applied, the optimizer
+        step does not advance, and the replicas stay identical."""
+        bad = [r for r, row in enumerate(cm) if int(row[-1]) != 0]
+        if bad:
+            for w in self._error_words():
+                w.zero_()
+            raise _lib.DLError("InvalidArgumentError: categorical id out of range [0, %d) in the batch of rank(s) "
+                               "%s — the step applied no update" % (self.N, bad))
+        return [row[:-1] for row in cm]
+
+    def _drop_prefetch(self, pf):
+        """A prefetched batch that will not be trained: its counts are consumed and a bad id
+        it carried is forgotten with it (its buffer set's validation word cleared)."""
+        cm = self.exch.resolve_counts(pf[4])
+        if any(int(row[-1]) != 0 for row in cm):
+            self._slots[pf[0]]["err"].zero_()
+        self._pf = None
 
     def prefetch(self, batch):
         """Stage the next batch, build its index and exchange its counts on the side stream
@@ -727,8 +748,7 @@ class ShardedCTREngine(CTREngine):
         else:
             if pf is not None:   # a different batch came: drop the prefetch (after it lands)
                 torch.cuda.current_stream().wait_event(pf[2])
-                ex.resolve_counts(pf[4])
-                self._pf = None
+                self._drop_prefetch(pf)
             B = self.stage(batch) if batch is not None else self.B
         s = _lib.stream_handle()
         L = self.layout
@@ -740,15 +760,17 @@ class ShardedCTREngine(CTREngine):
             if self.since_flush >= self.hist_len - 2:   # bound every row's lag below the alpha ring
                 self.flush()
             self.since_flush += 1
-        call("dl_adam_begin_step", ptr(self.opt), sp.decay_rate, float(sp.decay_steps), s)
-        if lazy:
-            call("dl_adam_hist_record", ptr(self.opt), ptr(self.hist), self.hist_len, s)
         if counts is None:
             # 1. index + 2. counts: every rank's per-owner counts in one all-gather (host waits)
             self._index(B)
             cm = ex.count_matrix(self._count_vec())
         else:
             cm = ex.resolve_counts(counts)
+        cm = self._split_counts(cm)   # raises on every rank if any rank's batch has a bad id
+        # the step begins once every rank's ids are known to be valid
+        call("dl_adam_begin_step", ptr(self.opt), sp.decay_rate, float(sp.decay_steps), s)
+        if lazy:
+            call("dl_adam_hist_record", ptr(self.opt), ptr(self.hist), self.hist_len, s)
         cmw = [row[W + 1:] for row in cm] if self.wdl else None
         self._mark("index_launched")
         send = cm[self.rank][:W]
@@ -958,8 +980,7 @@ class ShardedCTREngine(CTREngine):
         pf = getattr(self, "_pf", None)
         if pf is not None:   # a pending prefetch: let it land, drop it
             torch.cuda.current_stream().wait_event(pf[2])
-            ex.resolve_counts(pf[4])
-            self._pf = None
+            self._drop_prefetch(pf)
         B = self.stage(batch)
         self._join_side()            # the last step's record update (side stream) has landed
         s = _lib.stream_handle()
@@ -967,7 +988,7 @@ class ShardedCTREngine(CTREngine):
         L.batch = B
         W = self.world
         self._index(B)
-        cm = ex.count_matrix(self._count_vec())
+        cm = self._split_counts(ex.count_matrix(self._count_vec()))
         cmw = [row[W + 1:] for row in cm] if self.wdl else None
         send = cm[self.rank][:W]
         nsend, nrep = sum(send), cm[self.rank][W]

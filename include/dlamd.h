@@ -335,6 +335,10 @@ int dl_adam_begin_step(float* opt, float decay_rate, float decay_steps, void* st
  * dl_index_build / the forward kernels): issued before dl_adam_begin_step so the
  * step of a bad batch is poisoned from its start. */
 int dl_step_guard(const int32_t* batch_err, float* opt, void* stream);
+/* dl_step_guard, dl_adam_begin_step and (hist non-NULL) dl_adam_hist_record in one
+ * launch, same operations in the same order: the step's opening graph node. */
+int dl_step_begin(const int32_t* batch_err, float* opt, float decay_rate, float decay_steps, float* hist,
+                  int32_t hist_len, void* stream);
 /* Dense parameter whose gradient is the sum of `nslab` partial slabs
  * (g = sum_s slab[s*slab_stride + i]); l2 * p is added for i < l2_count;
  * p_prev (may be NULL) receives the pre-update values; sq_out (may be NULL) gets

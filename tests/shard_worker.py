@@ -162,6 +162,41 @@ def run_gpu(rank, world, steps, Bl, out_dir, adam="dense", prefetch=False, owner
              rep=eng.rep_t[:KW["C"]].cpu().numpy(), head=eng.w_head.cpu().numpy(), **dense)
 
 
+def run_gpu_badid(rank, world, steps, Bl, out_dir):
+    """Lazy + prefetch; global batch 1 carries an out-of-range id on rank 1 only.  Every rank
+    must raise at that step (one collective decides) with nothing applied, then train on."""
+    from deep_learning_amd import _lib
+    from deep_learning_amd.engine import ModelSpec
+    from deep_learning_amd.shard import Exchange, ShardedCTREngine
+    torch.cuda.set_device(0)
+    ex = Exchange()
+    cfg = R.make_cfg("deepfm_pipeline", **KW)
+    P = R.init_params(cfg, np.random.default_rng(42))
+    eng = ShardedCTREngine(ModelSpec("deepfm_pipeline", **KW), Bl, ex, adam="lazy", hist_len=4)
+    eng.load_params(P)
+    batches = [local(bg, rank, world) for bg in global_batches(Bl * world, steps)]
+    if rank == 1:
+        batches[1]["cate_feats"][3, 5] = KW["cate_index_size"] + 7
+    raised, trained = [], 0
+    for step, b in enumerate(batches):
+        nxt = batches[step + 1] if step + 1 < len(batches) else None
+        step_before = float(eng.opt[7].item())
+        try:
+            eng.train_step(b, graph=step >= 2, next_batch=nxt)
+        except _lib.DLError as e:
+            assert "out of range" in str(e), str(e)
+            assert float(eng.opt[7].item()) == step_before   # the optimizer step did not begin
+            raised.append(step)
+            continue
+        torch.cuda.synchronize()
+        np.savez(os.path.join(out_dir, "rank%d_step%d.npz" % (rank, trained)), z=eng.z[:Bl].cpu().numpy())
+        trained += 1
+    eng.check_error()
+    rows, t, f = eng.shard_state()
+    np.savez(os.path.join(out_dir, "rank%d.npz" % rank), rows=rows, table=t, first=f, raised=np.array(raised),
+             rep=eng.rep_t[:KW["C"]].cpu().numpy(), head=eng.w_head.cpu().numpy())
+
+
 WKW = dict(C=13, S=26, E=16, cate_index_size=8000, hidden=[32, 24], Fw=26)
 
 
@@ -208,6 +243,8 @@ if __name__ == "__main__":
     rank, world = dist.get_rank(), dist.get_world_size()
     if mode == "sim":
         run_sim(rank, world, steps, Bl, out_dir)
+    elif mode == "gpu_badid":
+        run_gpu_badid(rank, world, steps, Bl, out_dir)
     elif mode.startswith("gpu_wdl"):
         run_gpu_wdl(rank, world, steps, Bl, out_dir, adam="lazy" if "lazy" in mode else "dense",
                     tower="bf16" if "bf16" in mode else "f32", prefetch=mode.endswith("_pf"))

@@ -101,6 +101,33 @@ def test_sharded_engine_two_ranks_equals_global_batch(tmp_path, mode):
 
 
 @pytest.mark.gpu
+def test_sharded_bad_id_on_one_rank_raises_everywhere(tmp_path):
+    """A bad id in one rank's batch (here rank 1's half of global batch 1, prefetched during
+    step 0): its id-validation word travels in the count all-gather, so every rank raises TF's
+    InvalidArgumentError at that step before the optimizer step begins (deepfm_pipeline.py:219-221),
+    nothing is applied anywhere, and training continues — equal to the oracle trained on the
+    global batches without batch 1, with the replicated state identical on both ranks."""
+    _launch("gpu_badid", tmp_path)
+    cfg = R.make_cfg("deepfm_pipeline", **KW)
+    P = R.init_params(cfg, np.random.default_rng(42))
+    opt = R.AdamTF1(cfg, P)
+    good = [b for i, b in enumerate(global_batches(BL * WORLD, STEPS)) if i != 1]
+    for step, b in enumerate(good):
+        z = np.concatenate([np.load(tmp_path / ("rank%d_step%d.npz" % (r, step)))["z"] for r in range(WORLD)])
+        np.testing.assert_allclose(z, R.train_step(cfg, P, opt, b)["z"], atol=1e-5, rtol=0,
+                                   err_msg="logits step %d" % step)
+    d = [np.load(tmp_path / ("rank%d.npz" % r)) for r in range(WORLD)]
+    for e in d:
+        assert e["raised"].tolist() == [1]
+    table = np.zeros_like(P["feats_emb"])
+    for e in d:
+        table[e["rows"]] = e["table"]
+    C = KW["C"]
+    np.testing.assert_allclose(table[C:], P["feats_emb"][C:], atol=1e-5, rtol=0)
+    np.testing.assert_array_equal(d[0]["head"], d[1]["head"])
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("mode", ["gpu_wdl", "gpu_wdl_lazy_pf", "gpu_wdl_bf16_lazy"])
 def test_sharded_wdl_two_ranks_equals_global_batch(tmp_path, mode):
     """Wide&Deep row-sharded (BASELINE C5 at N GPUs): weight_mat and wdl_weights split by rows
