@@ -112,12 +112,13 @@ PMC_KERNEL_LAZY = {"rec_gather": ("rec_gather_kernel<16, false>", "rec_gather_ke
 def pmc_traffic(label, world, lazy=False, workload="c2"):
     """HBM bytes per launch of `label` from the newest committed PMC summary of the same
     workload (scripts/pmc_summary.py: (2*FETCH_SIZE + WRITE_SIZE)*1024, gfx950 correction;
-    a summary without a "workload" key was collected on C2)."""
+    a summary without a "workload" key was collected on C2).  Newest = the latest round tag
+    (profiles/r02s > r02q > r01r): file times do not survive a checkout or a copy."""
     import glob
     names = PMC_KERNEL_LAZY if lazy else PMC_KERNEL
     if world != 1 or label not in names:
         return None
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*", "pmc_summary.json")), key=os.path.getmtime)
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*", "pmc_summary.json")))
     for f in reversed(files):
         d = json.load(open(f))
         if d.get("workload", "c2") != workload:
