@@ -105,7 +105,7 @@ PMC_KERNEL = {"adam_table": "adam_rows4_kernel", "adam_first": "adam_rows1_kerne
               "head": "head_kernel"}
 PMC_KERNEL_LAZY = {"rec_gather": ("rec_gather_kernel<16, false>", "rec_gather_kernel<16, true>",
                                   "rec_gather_kernel<16>"),     # the last: summaries before the SPARSE template
-                   "embed_bwd": "rec_bwd_adam_kernel<16>",
+                   "embed_bwd": ("rec_bwd_adam_kernel<16, true>", "rec_bwd_adam_kernel<16>"),
                    "head": "head_kernel"}
 
 

@@ -290,19 +290,19 @@ __device__ __forceinline__ void rec_write_pad(float* __restrict__ r, int q, int 
 
 // The backward's per-row state: the caught-up p, m, v (and first-order triple) of unique
 // row u — from the gather's stash, or the record caught up again without one.
-template <int E>
+template <int E, bool STASH = false>   // STASH: the stash is known present (no catch-up code)
 __device__ __forceinline__ void rec_bwd_state(int64_t row, long long iu, int q, bool first, bool row_ok,
                                               const float* __restrict__ rec, const float* __restrict__ rows_u,
                                               const float* __restrict__ rows_u1, const float* __restrict__ mv,
                                               const RecCfg& c, int t, const RingW& ring, float4& p, float4& m,
                                               float4& v, float& w, float& wm, float& wv) {
-  if (mv) {
+  if (STASH || mv) {
     p = *reinterpret_cast<const float4*>(rows_u + iu * E + 4 * q);
     const float* o = mv + iu * (2 * E + 4);
     m = *reinterpret_cast<const float4*>(o + 4 * q);
     v = *reinterpret_cast<const float4*>(o + E + 4 * q);
     if (first) { w = rows_u1[iu]; wm = o[2 * E]; wv = o[2 * E + 1]; }
-  } else if (row_ok) {   // no stash: re-read the record and replay its catch-up
+  } else if (!STASH && row_ok) {   // no stash: re-read the record and replay its catch-up
     const float* r = rec + row * c.ld;
     p = *reinterpret_cast<const float4*>(r + 4 * q);
     m = *reinterpret_cast<const float4*>(r + E + 4 + 4 * q);
@@ -356,13 +356,21 @@ __device__ __forceinline__ void rec_bwd_apply(const SegGrad4& s, int64_t row, in
       const float *__restrict__ hist, const float *__restrict__ opt
 
 // Pass 1: every unique row but the hot ones (more than kSegLong references: pass 2), E/4
-// lanes per row.
-template <int E>
-__global__ __launch_bounds__(256) void rec_bwd_adam_kernel(DL_REC_BWD_PARAMS) {
+// lanes per row.  STASH (the gather's moment stash is given, the engine's default): the
+// catch-up path and its alpha window are compiled out — 96 -> fewer VGPRs, no LDS window.
+template <int E, bool STASH>
+#ifndef DL_BWD_MIN_WAVES
+#define DL_BWD_MIN_WAVES 1
+#endif
+#ifndef DL_BWD_STASH_SPECIAL
+#define DL_BWD_STASH_SPECIAL 1
+#endif
+__global__ __launch_bounds__(256, STASH ? DL_BWD_MIN_WAVES : 1) void rec_bwd_adam_kernel(DL_REC_BWD_PARAMS) {
   if (step_poisoned(opt)) return;   // the batch failed validation: no update (common.h)
   rec_load_hyper(c, opt);
-  __shared__ float hw[kHistWin];
-  const RingW ring = load_hist_window(hw, hist, (int)opt[7], c);
+  __shared__ float hw[STASH ? 1 : kHistWin];
+  RingW ring{hw, hist, c.hist_mask, (int)opt[7]};
+  if (!STASH) ring = load_hist_window(hw, hist, (int)opt[7], c);
   constexpr int LPR = E / 4;
   const dl_emb_layout& L = sg.L;
   const long long gt = (long long)blockIdx.x * blockDim.x + threadIdx.x;
@@ -402,7 +410,8 @@ __global__ __launch_bounds__(256) void rec_bwd_adam_kernel(DL_REC_BWD_PARAMS) {
     // the row's caught-up state (independent of the segment walk: issued first)
     float4 p = make_float4(0.f, 0.f, 0.f, 0.f), m = p, v = p;
     float w = 0.f, wm = 0.f, wv = 0.f;
-    rec_bwd_state<E>(row, n_rep + u, q, first, row_ok, rec, rows_u, rows_u1, mv, c, t, ring, p, m, v, w, wm, wv);
+    rec_bwd_state<E, STASH>(row, n_rep + u, q, first, row_ok, rec, rows_u, rows_u1, mv, c, t, ring, p, m, v, w, wm,
+                            wv);
     const SegGrad4 s = segment_grad4_range<E>(sg, cr.e0, cr.e1, kc, q, nrefs, wsec);
     if (!row_ok) continue;
     rec_bwd_apply<E>(s, row, q, first, p, m, v, w, wm, wv, rec, c, L, n_rep, g_rep, g1_rep, alpha, t);
@@ -753,7 +762,8 @@ extern "C" int dl_rec_bwd_adam(const dl_emb_layout* L, float* rec, int32_t rec_l
   }
   DL_DISPATCH_E(L->emb_dim, {
     const unsigned grid = grid_cap(max_uniq * (kE / 4));
-    hipLaunchKernelGGL(rec_bwd_adam_kernel<kE>, dim3(grid), dim3(256), 0, as_stream(stream), sg, rec,
+    auto bwd = (DL_BWD_STASH_SPECIAL && mv_u) ? rec_bwd_adam_kernel<kE, true> : rec_bwd_adam_kernel<kE, false>;
+    hipLaunchKernelGGL(bwd, dim3(grid), dim3(256), 0, as_stream(stream), sg, rec,
                        make_rec_cfg(kE, rec_ld, rec_flags, (mv_u ? 2 : hist_len)), n_rep, rows_u,
                        has_first ? rows_u1 : nullptr, mv_u, uniq_keys, n_uniq, world, g_rep,
                        has_first ? g1_rep : nullptr, hist, opt);
