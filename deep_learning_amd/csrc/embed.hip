@@ -54,8 +54,13 @@ constexpr int kMaxHotContFwd = 32;
 constexpr int kTileSamples = 16;   // samples staged per block iteration
 constexpr int kMaxSlots = 128;     // FM slots + deep slots per sample
 
+#ifndef DL_FWD_MIN_WAVES
+#define DL_FWD_MIN_WAVES 5
+#endif
+// Occupancy: the gathered-rows form (C2: E = 16, NPS = 5) needs 97 VGPRs unbounded — one past
+// the 5-waves-per-SIMD line; the bound keeps it at 96 (no spill; NPS > 5 would spill: unbounded).
 template <int E, int NPS, bool REC = false>
-__global__ __launch_bounds__(256) void embed_fwd_kernel(EmbArgs a) {
+__global__ __launch_bounds__(256, (REC || NPS > 5) ? 1 : DL_FWD_MIN_WAVES) void embed_fwd_kernel(EmbArgs a) {
   // Per block iteration a tile of 16 samples is staged: every (sample, slot)
   // row index is resolved once into LDS by a coalesced pass over the id matrix
   // (slot = FM field f < Fs, or deep field Fs + f).  Each wave then owns 4
