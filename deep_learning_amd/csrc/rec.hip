@@ -761,7 +761,10 @@ extern "C" int dl_rec_bwd_adam(const dl_emb_layout* L, float* rec, int32_t rec_l
       });
   }
   DL_DISPATCH_E(L->emb_dim, {
-    const unsigned grid = grid_cap(max_uniq * (kE / 4));
+    unsigned grid = grid_cap(max_uniq * (kE / 4));
+#ifdef DL_BWD_GRID_CAP
+    if (grid > DL_BWD_GRID_CAP) grid = DL_BWD_GRID_CAP;
+#endif
     auto bwd = (DL_BWD_STASH_SPECIAL && mv_u) ? rec_bwd_adam_kernel<kE, true> : rec_bwd_adam_kernel<kE, false>;
     hipLaunchKernelGGL(bwd, dim3(grid), dim3(256), 0, as_stream(stream), sg, rec,
                        make_rec_cfg(kE, rec_ld, rec_flags, (mv_u ? 2 : hist_len)), n_rep, rows_u,
