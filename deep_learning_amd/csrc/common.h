@@ -52,12 +52,20 @@ __device__ __forceinline__ int64_t checked_row(int64_t id, int64_t off, int64_t 
 }
 
 // Optimizer state block (include/dlamd.h, DL_OPT_*): [0..7] Adam scalars, [8..15] per-step
-// regulariser sums, [16] the sticky status word (int32 bits).  A set status word poisons the
-// step: every kernel that writes parameters or optimizer state returns without doing so (the
-// gradients it would have consumed are still reset), so a batch with an out-of-range id
-// changes nothing — as TF's failing sess.run applies nothing before raising.
+// regulariser sums, [16] the sticky status word (int32 bits, the host's report), [17] the
+// step's skip word.  A set skip word poisons the step: every kernel that writes parameters or
+// optimizer state returns without doing so (the gradients it would have consumed are still
+// reset), so a batch with an out-of-range id changes nothing — as TF's failing sess.run
+// applies nothing before raising — and the next batch applies normally.
 __device__ __forceinline__ bool step_poisoned(const float* opt) {
-  return __float_as_int(opt[DL_OPT_STATUS]) != 0;
+  return __float_as_int(opt[DL_OPT_SKIP]) != 0;
+}
+// An internal fault (DL_STATUS_LAG / DL_STATUS_INDEX) seen mid-step: reported to the host
+// (status) and poisoning the rest of this step and every later one (skip, re-derived from the
+// status at each step begin).  `status` points at opt[DL_OPT_STATUS]; the skip word follows it.
+__device__ __forceinline__ void raise_fault(int* status, int bits) {
+  atomicOr(status, bits);
+  atomicOr(status + (DL_OPT_SKIP - DL_OPT_STATUS), bits);
 }
 __device__ __forceinline__ int* opt_status(const float* opt) {
   return const_cast<int*>(reinterpret_cast<const int*>(opt + DL_OPT_STATUS));

@@ -197,9 +197,59 @@ static int compressed_bits(int64_t n_rows, int world, int rep_below, uint32_t& l
   return b;
 }
 
+__global__ void batch_err_reset_kernel(int32_t* err) { err[0] = 0; }
+
+// The batch's ids against the rows they address (the checks the forward kernels make, done
+// before the step begins): single cate column c < S reads deep row id + deep_cate_offset and,
+// with FM, FM row id + fm_cate_offset; multi-hot columns read row id + deep_cate_offset; wide
+// ids address wdl_weights rows [0, wide_rows).
+__global__ __launch_bounds__(256) void validate_batch_kernel(dl_emb_layout L, const int64_t* __restrict__ cate,
+                                                             const int64_t* __restrict__ wide, int wide_cols,
+                                                             int wide_ld, int64_t wide_rows,
+                                                             int32_t* __restrict__ err) {
+  const long long nc = cate ? (long long)L.batch * L.cate_ld : 0;
+  const long long nw = wide ? (long long)L.batch * wide_cols : 0;
+  bool bad = false;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < nc + nw;
+       i += (long long)gridDim.x * blockDim.x) {
+    if (i < nc) {
+      const int c = (int)(i % L.cate_ld);
+      const int64_t id = cate[i];
+      const int64_t d = id + L.deep_cate_offset;
+      bad |= d < 0 || d >= L.n_rows;
+      if (c < L.cate_fields && L.use_fm) {
+        const int64_t f = id + L.fm_cate_offset;
+        bad |= f < 0 || f >= L.n_rows;
+      }
+    } else {
+      const long long k = i - nc;
+      const int64_t id = wide[(k / wide_cols) * wide_ld + k % wide_cols];
+      bad |= id < 0 || id >= wide_rows;
+    }
+  }
+  if (__any(bad) && (threadIdx.x & 63) == 0) atomicOr(err, DL_STATUS_BAD_ID);
+}
+
 }  // namespace dl
 
 using namespace dl;
+
+extern "C" int dl_validate_batch(const dl_emb_layout* L, const int64_t* cate, const int64_t* wide, int32_t wide_cols,
+                                 int32_t wide_ld, int64_t wide_rows, int32_t reset, int32_t* err, void* stream) {
+  DL_CHECK_ARG(L && err, "NULL argument");
+  DL_CHECK_ARG(!wide || (wide_cols > 0 && wide_ld >= wide_cols && wide_rows > 0), "bad wide shape");
+  DL_CHECK_ARG(!cate || L->cate_ld > 0, "bad cate shape");
+  hipStream_t s = as_stream(stream);
+  if (reset) hipLaunchKernelGGL(batch_err_reset_kernel, dim3(1), dim3(1), 0, s, err);
+  const long long n = (cate ? (long long)L->batch * L->cate_ld : 0) + (wide ? (long long)L->batch * wide_cols : 0);
+  if (n > 0) {
+    long long blocks = (n + 255) / 256;
+    if (blocks > 2048) blocks = 2048;
+    hipLaunchKernelGGL(validate_batch_kernel, dim3((unsigned)blocks), dim3(256), 0, s, *L, cate, wide, wide_cols,
+                       wide_ld, wide_rows, err);
+  }
+  DL_RETURN_LAUNCH("dl_validate_batch");
+}
 
 extern "C" int64_t dl_index_workspace_bytes(int64_t n_refs) {
   if (n_refs <= 0 || n_refs > (1LL << 30)) return -1;

@@ -1,57 +1,69 @@
 // Exact tie-aware ROC-AUC on the GPU — the evaluation metric of the reference
 // (sklearn.metrics.roc_auc_score at models/deepfm_pipeline.py:311,344, wdl.py:343-358).
+// No library kernels: the sort is the hand-written stable radix sort of rsort.hip (the one
+// the batch index build uses), the scan below is this file's own.
 //
-// AUC = sum over positives of (#negatives scored below + 0.5 * #negatives tied) / (P * N).
-// The scores are sorted as 33-bit keys (order-preserving float bits << 1 | label), so
-// within a tie group the negatives come first.  For a positive at sorted position i in a
-// tie group starting at s (cpos = exclusive count of positives):
-//     negatives at positions < i  = i - cpos[i]   (= below + tied: all tied negatives precede it)
-//     negatives below the group   = s - cpos[s]
-// and twice its contribution is their sum — an integer.  The numerator is therefore an
-// exact int64 sum (order-free, deterministic), divided once in double at the end.
-#include <hipcub/hipcub.hpp>
-
+// AUC = sum over tie groups g of pos_g * (neg_below_g + 0.5 * neg_g) / (P * N)
+// (a positive counts every negative scored below it and half of each negative tied with it).
+// Steps:
+//   1. keys[i] = order-preserving bits of score i; rsort_pairs sorts (key, i) stably
+//   2. per sorted position j: label bit of the sample it holds, head bit (first of a tie group)
+//      packed as one int64 v[j] = label + (head << 32); exclusive scan of v gives, at every
+//      position, the positives before it (low word) and the number of groups that started
+//      before it (high word)
+//   3. at every group head j (group g = high word): start[g] = j, cpos[g] = positives before j
+//   4. per group: e = next group's start (or n), pos_g = cpos[g+1] - cpos[g], neg_g = e - s - pos_g,
+//      neg_below = s - cpos[g]; 2 * numerator += pos_g * (2 * neg_below + neg_g) — an exact
+//      int64 sum (order-free, deterministic), divided once in double at the end.
 #include "common.h"
+#include "rsort.h"
 
 namespace dl {
 namespace {
 
+constexpr int kScanThreads = 256;
+constexpr int kScanPer = 16;                            // elements per thread
+constexpr int kScanTile = kScanThreads * kScanPer;      // 4096
+
 struct AucWs {
-  uint64_t* keys;
-  uint64_t* keys_sorted;
-  int32_t* cpos;         // exclusive count of positives before i
-  int32_t* start;        // first position of i's tie group
-  unsigned long long* acc;  // [0] = 2 * numerator, [1] = P
-  void* temp;
-  size_t temp_bytes;
+  uint32_t* keys;        // float keys (input order)
+  uint32_t* skeys;       // sorted keys
+  int32_t* sidx;         // sorted sample indices
+  uint64_t* v;           // packed label / head bits, then their exclusive scan (in place)
+  uint64_t* tsum;        // per-tile sums, then their exclusive scan
+  int32_t* gstart;       // start position of group g
+  int32_t* gcpos;        // positives before group g
+  int32_t* n_valid;      // rsort's count (every key is valid)
+  unsigned long long* acc;   // [0] = 2 * numerator, [1] = P, [2] = groups
+  void* sort_ws;
+  size_t sort_ws_bytes;
 };
 
 size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
-
-// max-scan functor over group-head positions
-struct MaxOp {
-  __device__ __forceinline__ int32_t operator()(int32_t a, int32_t b) const { return a > b ? a : b; }
-};
-
-size_t cub_bytes(int n) {
-  size_t a = 0, b = 0, c = 0;
-  hipcub::DeviceRadixSort::SortKeys(nullptr, a, (const uint64_t*)nullptr, (uint64_t*)nullptr, n, 0, 33);
-  hipcub::DeviceScan::ExclusiveSum(nullptr, b, (const int32_t*)nullptr, (int32_t*)nullptr, n);
-  hipcub::DeviceScan::InclusiveScan(nullptr, c, (const int32_t*)nullptr, (int32_t*)nullptr, MaxOp(), n);
-  return std::max(a, std::max(b, c));
-}
+int scan_tiles(int n) { return (n + kScanTile - 1) / kScanTile; }
 
 AucWs carve(void* ws, int n) {
   char* p = static_cast<char*>(ws);
   AucWs w;
-  w.keys = reinterpret_cast<uint64_t*>(p); p += align256(8ull * n);
-  w.keys_sorted = reinterpret_cast<uint64_t*>(p); p += align256(8ull * n);
-  w.cpos = reinterpret_cast<int32_t*>(p); p += align256(4ull * n);
-  w.start = reinterpret_cast<int32_t*>(p); p += align256(4ull * n);
+  const int T = scan_tiles(n);
+  w.keys = reinterpret_cast<uint32_t*>(p); p += align256(4ull * n);
+  w.skeys = reinterpret_cast<uint32_t*>(p); p += align256(4ull * n);
+  w.sidx = reinterpret_cast<int32_t*>(p); p += align256(4ull * n);
+  w.v = reinterpret_cast<uint64_t*>(p); p += align256(8ull * n);
+  w.tsum = reinterpret_cast<uint64_t*>(p); p += align256(8ull * (T + 1));
+  w.gstart = reinterpret_cast<int32_t*>(p); p += align256(4ull * (n + 1));
+  w.gcpos = reinterpret_cast<int32_t*>(p); p += align256(4ull * (n + 1));
+  w.n_valid = reinterpret_cast<int32_t*>(p); p += 256;
   w.acc = reinterpret_cast<unsigned long long*>(p); p += 256;
-  w.temp = p;
-  w.temp_bytes = cub_bytes(n);
+  w.sort_ws = p;
+  w.sort_ws_bytes = rsort_workspace_bytes(n);
   return w;
+}
+
+size_t ws_bytes(int n) {
+  const int T = scan_tiles(n);
+  return 3 * align256(4ull * n) + align256(8ull * n) + align256(8ull * (T + 1)) + 2 * align256(4ull * (n + 1)) +
+         512 + rsort_workspace_bytes(n);
 }
 
 // order-preserving map of a float to uint32 (-0.0 folded onto +0.0: they tie, as np.diff says)
@@ -60,47 +72,138 @@ __device__ __forceinline__ uint32_t float_key(float x) {
   return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
 }
 
-__global__ __launch_bounds__(256) void auc_keys_kernel(const float* __restrict__ scores, int64_t s_stride,
-                                                       const float* __restrict__ labels, int64_t l_stride,
-                                                       int n, uint64_t* __restrict__ keys,
-                                                       unsigned long long* acc) {
+__global__ __launch_bounds__(256) void auc_keys_kernel(const float* __restrict__ scores, int64_t s_stride, int n,
+                                                       uint32_t* __restrict__ keys, unsigned long long* acc) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < 2 && blockIdx.x == 0) acc[i] = 0;
-  if (i >= n) return;
-  const uint64_t lab = labels[(int64_t)i * l_stride] > 0.5f ? 1u : 0u;
-  keys[i] = ((uint64_t)float_key(scores[(int64_t)i * s_stride]) << 1) | lab;
+  if (blockIdx.x == 0 && threadIdx.x < 4) acc[threadIdx.x] = 0;
+  if (i < n) keys[i] = float_key(scores[(int64_t)i * s_stride]);
 }
 
-// label bits of the sorted keys (for the scan) and the group-head positions (for the max-scan)
-__global__ __launch_bounds__(256) void auc_flags_kernel(const uint64_t* __restrict__ k, int n,
-                                                        int32_t* __restrict__ lab, int32_t* __restrict__ head) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  const uint64_t ki = k[i];
-  lab[i] = (int32_t)(ki & 1u);
-  head[i] = (i == 0 || (k[i - 1] >> 1) != (ki >> 1)) ? i : 0;
+// v[j] = label of the sample at sorted position j + (j starts a tie group) << 32
+__global__ __launch_bounds__(256) void auc_flags_kernel(const uint32_t* __restrict__ sk, const int32_t* __restrict__ si,
+                                                        const float* __restrict__ labels, int64_t l_stride, int n,
+                                                        uint64_t* __restrict__ v) {
+  const int j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= n) return;
+  const uint32_t k = sk[j];
+  const int idx = min(max(si[j], 0), n - 1);
+  const uint64_t lab = labels[(int64_t)idx * l_stride] > 0.5f ? 1u : 0u;
+  const uint64_t head = (j == 0 || sk[j - 1] != k) ? 1u : 0u;
+  v[j] = lab | (head << 32);
 }
 
-__global__ __launch_bounds__(256) void auc_sum_kernel(const uint64_t* __restrict__ k, const int32_t* __restrict__ cpos,
-                                                      const int32_t* __restrict__ start, int n,
-                                                      unsigned long long* acc) {
-  unsigned long long num = 0, pos = 0;
-  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
-    if (k[i] & 1u) {
-      const int s = start[i];
-      num += (unsigned long long)(i - cpos[i]) + (unsigned long long)(s - cpos[s]);
-      pos += 1;
-    }
-  }
-  // wave reduce, then one atomic per wave (integer: the order does not matter)
+// Block-wide exclusive scan of one uint64 per thread; *total = the block's sum.
+__device__ __forceinline__ uint64_t block_exscan(uint64_t x, uint64_t* wsum, uint64_t* total) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  uint64_t inc = x;
 #pragma unroll
-  for (int o = 32; o >= 1; o >>= 1) {
-    num += __shfl_xor(num, o, 64);
-    pos += __shfl_xor(pos, o, 64);
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint64_t y = __shfl_up(inc, o, 64);
+    if (lane >= o) inc += y;
   }
-  if ((threadIdx.x & 63) == 0 && pos) {
-    atomicAdd(acc, num);
-    atomicAdd(acc + 1, pos);
+  __syncthreads();
+  if (lane == 63) wsum[w] = inc;
+  __syncthreads();
+  uint64_t base = 0, all = 0;
+#pragma unroll
+  for (int i = 0; i < kScanThreads / 64; ++i) {
+    base += i < w ? wsum[i] : 0;
+    all += wsum[i];
+  }
+  *total = all;
+  return base + inc - x;
+}
+
+// Pass 1: the sum of each 4096-element tile.
+__global__ __launch_bounds__(kScanThreads) void scan_tile_sums(const uint64_t* __restrict__ v, int n,
+                                                               uint64_t* __restrict__ tsum) {
+  __shared__ uint64_t wsum[kScanThreads / 64];
+  const long long t0 = (long long)blockIdx.x * kScanTile;
+  uint64_t s = 0;
+#pragma unroll
+  for (int r = 0; r < kScanPer; ++r) {
+    const long long e = t0 + r * kScanThreads + threadIdx.x;
+    s += e < n ? v[e] : 0;
+  }
+  uint64_t all;
+  block_exscan(s, wsum, &all);
+  if (threadIdx.x == 0) tsum[blockIdx.x] = all;
+}
+
+// Pass 2 (one block): exclusive scan of the tile sums in place; tsum[T] = the grand total.
+__global__ __launch_bounds__(kScanThreads) void scan_tile_prefix(uint64_t* __restrict__ tsum, int T) {
+  __shared__ uint64_t wsum[kScanThreads / 64];
+  const int per = (T + kScanThreads - 1) / kScanThreads;
+  const int a = threadIdx.x * per, b = min(T, a + per);
+  uint64_t s = 0;
+  for (int i = a; i < b; ++i) s += tsum[i];
+  uint64_t all;
+  uint64_t run = block_exscan(s, wsum, &all);
+  for (int i = a; i < b; ++i) {
+    const uint64_t c = tsum[i];
+    tsum[i] = run;
+    run += c;
+  }
+  if (threadIdx.x == 0) tsum[T] = all;
+}
+
+// Pass 3: each tile's exclusive scan (thread-contiguous runs of kScanPer elements), offset by
+// the tile's prefix; at every group head j: gstart[g] = j, gcpos[g] = positives before j.
+__global__ __launch_bounds__(kScanThreads) void scan_tile_apply(uint64_t* __restrict__ v, int n,
+                                                                const uint64_t* __restrict__ tsum,
+                                                                int32_t* __restrict__ gstart,
+                                                                int32_t* __restrict__ gcpos) {
+  __shared__ uint64_t wsum[kScanThreads / 64];
+  const long long e0 = (long long)blockIdx.x * kScanTile + (long long)threadIdx.x * kScanPer;
+  uint64_t x[kScanPer];
+  uint64_t s = 0;
+#pragma unroll
+  for (int r = 0; r < kScanPer; ++r) {
+    x[r] = e0 + r < n ? v[e0 + r] : 0;
+    s += x[r];
+  }
+  uint64_t all;
+  uint64_t run = block_exscan(s, wsum, &all) + tsum[blockIdx.x];
+#pragma unroll
+  for (int r = 0; r < kScanPer; ++r) {
+    const long long e = e0 + r;
+    if (e < n) {
+      v[e] = run;
+      if (x[r] >> 32) {   // a group head: run's high word = groups before it = its group index
+        const uint32_t g = (uint32_t)(run >> 32);
+        gstart[g] = (int32_t)e;
+        gcpos[g] = (int32_t)(run & 0xffffffffu);
+      }
+    }
+    run += x[r];
+  }
+}
+
+// Per group g: its positives times (2 x negatives below it + its own negatives).
+__global__ __launch_bounds__(256) void auc_groups_kernel(const int32_t* __restrict__ gstart,
+                                                         const int32_t* __restrict__ gcpos,
+                                                         const uint64_t* __restrict__ tsum, int T, int n,
+                                                         unsigned long long* acc) {
+  const uint64_t tot = tsum[T];
+  const long long G = (long long)(tot >> 32);
+  const long long P = (long long)(tot & 0xffffffffu);
+  unsigned long long num = 0;
+  for (long long g = (long long)blockIdx.x * blockDim.x + threadIdx.x; g < G; g += (long long)gridDim.x * blockDim.x) {
+    const long long s = gstart[g];
+    const long long e = g + 1 < G ? gstart[g + 1] : n;
+    const long long c0 = gcpos[g];
+    const long long c1 = g + 1 < G ? gcpos[g + 1] : P;
+    const long long pos = c1 - c0;
+    const long long neg = (e - s) - pos;
+    const long long below = s - c0;
+    num += (unsigned long long)(pos * (2 * below + neg));
+  }
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) num += __shfl_xor(num, o, 64);
+  if ((threadIdx.x & 63) == 0 && num) atomicAdd(acc, num);
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    acc[1] = (unsigned long long)P;
+    acc[2] = (unsigned long long)G;
   }
 }
 
@@ -116,43 +219,34 @@ using namespace dl;
 
 extern "C" int64_t dl_auc_workspace_bytes(int64_t n) {
   if (n <= 0 || n > 0x7fffffff) return -1;
-  const int m = (int)n;
-  return (int64_t)(2 * align256(8ull * m) + 2 * align256(4ull * m) + 256 + cub_bytes(m));
+  return (int64_t)ws_bytes((int)n);
 }
 
 extern "C" int dl_auc(const float* scores, int64_t s_stride, const float* labels, int64_t l_stride, int64_t n,
-                      void* ws, int64_t ws_bytes, double* out, void* stream) {
+                      void* ws, int64_t ws_bytes_, double* out, void* stream) {
   DL_CHECK_ARG(scores && labels && out && ws, "NULL argument");
   DL_CHECK_ARG(n > 0 && n <= 0x7fffffff, "n = %lld out of range", (long long)n);
-  DL_CHECK_ARG(ws_bytes >= dl_auc_workspace_bytes(n), "workspace too small (%lld < %lld)", (long long)ws_bytes,
+  DL_CHECK_ARG(ws_bytes_ >= dl_auc_workspace_bytes(n), "workspace too small (%lld < %lld)", (long long)ws_bytes_,
                (long long)dl_auc_workspace_bytes(n));
   const int m = (int)n;
   hipStream_t s = as_stream(stream);
   AucWs w = carve(ws, m);
   const int g = (m + 255) / 256;
-  hipLaunchKernelGGL(auc_keys_kernel, dim3(g), dim3(256), 0, s, scores, s_stride, labels, l_stride, m, w.keys,
+  hipLaunchKernelGGL(auc_keys_kernel, dim3(g), dim3(256), 0, s, scores, s_stride, m, w.keys, w.acc);
+  RsSource src{};
+  src.kind = 0;
+  src.keys = w.keys;
+  if (int rc = rsort_pairs(src, m, 0, 32, w.sort_ws, w.sort_ws_bytes, w.skeys, w.sidx, w.n_valid, s)) {
+    set_error("dl_auc: radix sort failed (%d)", rc);
+    return rc;
+  }
+  hipLaunchKernelGGL(auc_flags_kernel, dim3(g), dim3(256), 0, s, w.skeys, w.sidx, labels, l_stride, m, w.v);
+  const int T = scan_tiles(m);
+  hipLaunchKernelGGL(scan_tile_sums, dim3(T), dim3(kScanThreads), 0, s, w.v, m, w.tsum);
+  hipLaunchKernelGGL(scan_tile_prefix, dim3(1), dim3(kScanThreads), 0, s, w.tsum, T);
+  hipLaunchKernelGGL(scan_tile_apply, dim3(T), dim3(kScanThreads), 0, s, w.v, m, w.tsum, w.gstart, w.gcpos);
+  hipLaunchKernelGGL(auc_groups_kernel, dim3(std::min(g, 2048)), dim3(256), 0, s, w.gstart, w.gcpos, w.tsum, T, m,
                      w.acc);
-  size_t tb = w.temp_bytes;
-  if (hipcub::DeviceRadixSort::SortKeys(w.temp, tb, w.keys, w.keys_sorted, m, 0, 33, s) != hipSuccess) {
-    set_error("dl_auc: radix sort failed");
-    return 1001;
-  }
-  // the key buffer is free after the sort: reuse it for the label bits and head positions
-  int32_t* lab = reinterpret_cast<int32_t*>(w.keys);
-  int32_t* head = lab + m;
-  hipLaunchKernelGGL(auc_flags_kernel, dim3(g), dim3(256), 0, s, w.keys_sorted, m, lab, head);
-  tb = w.temp_bytes;
-  if (hipcub::DeviceScan::ExclusiveSum(w.temp, tb, lab, w.cpos, m, s) != hipSuccess) {
-    set_error("dl_auc: scan failed");
-    return 1001;
-  }
-  tb = w.temp_bytes;
-  if (hipcub::DeviceScan::InclusiveScan(w.temp, tb, head, w.start, MaxOp(), m, s) != hipSuccess) {
-    set_error("dl_auc: max-scan failed");
-    return 1001;
-  }
-  const int gs = std::min(g, 2048);
-  hipLaunchKernelGGL(auc_sum_kernel, dim3(gs), dim3(256), 0, s, w.keys_sorted, w.cpos, w.start, m, w.acc);
   hipLaunchKernelGGL(auc_final_kernel, dim3(1), dim3(1), 0, s, w.acc, m, out);
   DL_RETURN_LAUNCH("dl_auc");
 }

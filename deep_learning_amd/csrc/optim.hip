@@ -49,7 +49,15 @@ __global__ void adam_begin_kernel(float* opt, float decay_rate, float decay_step
 // belongs to: opt's sticky status word gets the batch's error bits before the step begins.
 __device__ __forceinline__ void step_guard_kernel_body(const int32_t* batch_err, float* opt) {
   const int e = batch_err[0];
-  if (e) opt_status(opt)[0] |= (e & DL_STATUS_BAD_ID) ? DL_STATUS_BAD_ID : e;
+  int* st = opt_status(opt);
+  const int bad = e ? ((e & DL_STATUS_BAD_ID) ? DL_STATUS_BAD_ID : e) : 0;
+  // this step's skip word: the batch's own bits + any sticky internal fault
+  st[DL_OPT_SKIP - DL_OPT_STATUS] = bad | (st[0] & (DL_STATUS_LAG | DL_STATUS_INDEX));
+  if (bad) {
+    st[0] |= bad;
+    opt[DL_OPT_BAD_STEP] = opt[7];            // global_step the bad batch would have advanced from
+    opt[DL_OPT_BAD_COUNT] += 1.f;
+  }
 }
 
 __global__ void step_guard_kernel(const int32_t* batch_err, float* opt) { step_guard_kernel_body(batch_err, opt); }

@@ -44,7 +44,7 @@ __device__ __forceinline__ void rec_adam(float& p, float& m, float& v, float g, 
 // raises) and the replay covers the ring's steps only.
 __device__ __forceinline__ int catch_up_from(int from, int to, const RecCfg& c) {
   if (to - from > c.hist_mask + 1) {
-    atomicOr(c.status, DL_STATUS_LAG);
+    raise_fault(c.status, DL_STATUS_LAG);
     return to - (c.hist_mask + 1);
   }
   return from;

@@ -34,7 +34,7 @@ struct SegGradIn {
 };
 
 __device__ __forceinline__ void index_fault(int* status) {
-  if (status) atomicOr(status, DL_STATUS_INDEX);
+  if (status) raise_fault(status, DL_STATUS_INDEX);
 }
 
 struct SegGrad {

@@ -744,14 +744,22 @@ class CTREngine:
              self.head_blocks, s)
 
     def _pre(self, B):
-        """The batch index build (dl_index_build: the hand-written radix sort + segmented
-        unique of index.hip, no host synchronisation).  Runs on the current stream — inside
-        the step's hipGraph (graph=True), or on the side stream when prefetched."""
-        if self.bwd != "sorted":
-            return
+        """The batch's validation and index build, before its step begins: the batch's
+        validation word is reset, then set by dl_validate_batch for every id no index build
+        checks (the dense-layout gathers' cate ids, wdl's wide ids) and by dl_index_build (the
+        hand-written radix sort + segmented unique of index.hip, no host synchronisation).
+        Runs on the current stream — inside the step's hipGraph (graph=True), or on the side
+        stream when prefetched — so a bad batch is known before dl_step_begin opens its step."""
         s = _lib.stream_handle()
         L = self.layout
         L.batch = B
+        sp = self.spec
+        cate = self.in_cate if self.bwd != "sorted" else None
+        wide = self.in_wide if self.wdl else None
+        self._c("validate", "dl_validate_batch", C_ref(L), ptr(cate), ptr(wide), sp.Fw if wide is not None else 0,
+                self.in_wide.shape[1], getattr(self, "w_rows", 0), 1, ptr(self.err), s)
+        if self.bwd != "sorted":
+            return
         # single GPU: keys are the rows themselves (replicated rows need no owner group;
         # the record kernels recognise them by row < n_rep) — the narrowest sort range
         self._c("index_build", "dl_index_build", C_ref(L), ptr(self.in_cate), 1, 0, ptr(self.idx_ws),
@@ -768,10 +776,6 @@ class CTREngine:
         self._c("step_begin", "dl_step_begin", ptr(self.err), ptr(self.opt), sp.decay_rate, float(sp.decay_steps),
                 ptr(self.hist) if self.lazy else None, self.hist_len if self.lazy else 0, s)
         self._forward(B, s, train=True)
-        if not self.lazy or self.wdl:
-            # ids validated inside the forward (dense-layout gather, wdl wide ids): the updates
-            # after it are skipped (the step counter has already advanced)
-            self._c("step_guard2", "dl_step_guard", ptr(self.err), ptr(self.opt), s)
         nl = len(sp.hidden)
         splits = max(1, min(self.splits, B // 1024))
         if self.bf and not self.wdl:      # the wdl head writes its bf16 dY itself
@@ -1103,19 +1107,28 @@ class CTREngine:
         or the optimizer's status word."""
         st = self.opt.view(torch.int32)[_lib.OPT_STATUS:_lib.OPT_STATUS + 1]
         status = int(st.item())
-        bad = any(int(w[0].item()) != 0 for w in self._error_words())
+        # the current buffer set's validation word: a batch validated whose step has not begun
+        # (predict); a trained batch's word is consumed by its step (dl_step_begin -> status),
+        # and every batch's own validation resets its word (no other set's word is touched:
+        # a prefetched bad batch must still be skipped by its own step)
+        bad = int(self.err[0].item()) != 0 and not status
         if not status and not bad:
             return
-        for w in self._error_words():
-            w.zero_()
-        st.zero_()
+        bad_step, n_bad = (int(x) for x in self.opt[_lib.OPT_BAD_STEP:_lib.OPT_BAD_COUNT + 1].tolist())
+        if bad:
+            self.err.zero_()
+        self.opt[_lib.OPT_STATUS:_lib.OPT_BAD_COUNT + 1].zero_()   # status, skip, bad step, count
         self._status_q.clear()
         if status & _lib.STATUS_LAG:
             raise _lib.DLError("internal: a row record lagged past the alpha ring (flush schedule)")
         if status & _lib.STATUS_INDEX:
             raise _lib.DLError("internal: batch index entry out of range (corrupt index)")
-        raise _lib.DLError("InvalidArgumentError: categorical id out of range [0, %d) — the step of the "
-                           "offending batch applied no update" % self.N)
+        if not status:   # a validated batch whose step has not begun yet (predict, or queued)
+            raise _lib.DLError("InvalidArgumentError: categorical id out of range [0, %d) in the current "
+                               "batch — no update applied" % self.N)
+        raise _lib.DLError("InvalidArgumentError: categorical id out of range [0, %d) — %d batch(es) skipped "
+                           "with no update, the last at global_step %d; the batches around them applied "
+                           "normally" % (self.N, n_bad, bad_step))
 
 
 def default_adam(spec):

@@ -314,27 +314,48 @@ int dl_slab_fold_rows(const float* slab, int32_t blocks, int32_t width, int32_t 
  * [0] beta1_power [1] beta2_power [2] lr [3] alpha [4] beta1 [5] beta2
  * [6] epsilon [7] step (as float, exact < 2^24), [8..15] per-step accumulators
  * (zeroed by dl_adam_begin_step; sq_out targets), [16] the status word (int32
- * bits, sticky until the host clears it); DL_OPT_LEN floats in all.
+ * bits, sticky until the host clears it: what the host reports), [17] the skip
+ * word (int32 bits of the CURRENT step only, rewritten by dl_step_guard /
+ * dl_step_begin), [18] the global step at which the last bad batch was skipped,
+ * [19] how many batches were skipped since the host last cleared the status;
+ * DL_OPT_LEN floats in all.
  * dl_adam_begin_step computes alpha = lr_t*sqrt(1-b2p)/(1-b1p) with
  * lr_t = lr*rate^floor(step/decay_steps) and then advances b1p*=b1, b2p*=b2,
  * step+=1 (TF's _finish + global_step).
  *
- * A nonzero status word POISONS the step: dl_adam_begin_step and every call that
+ * A nonzero SKIP word poisons the step: dl_adam_begin_step and every call that
  * writes parameters or Adam state (dl_adam_*, dl_rec_bwd_adam, dl_rec_apply_*)
  * return without writing them; gradient buffers they would consume are still
  * reset.  A batch whose ids fail validation therefore changes nothing, as TF's
  * failing sess.run applies nothing before raising InvalidArgumentError
- * (deepfm_pipeline.py:219-221); the host reads the word back and raises. */
+ * (deepfm_pipeline.py:219-221), and the next batch applies normally (the skip word
+ * belongs to one step); the host reads the sticky status word back and raises.
+ * Internal faults (DL_STATUS_LAG / DL_STATUS_INDEX) set both words and keep every
+ * later step skipped until the host clears the status. */
 #define DL_OPT_LEN 32
 #define DL_OPT_STATUS 16
+#define DL_OPT_SKIP 17
+#define DL_OPT_BAD_STEP 18
+#define DL_OPT_BAD_COUNT 19
 #define DL_STATUS_BAD_ID 1   /* a categorical / wide id outside [0, N) */
 #define DL_STATUS_LAG 2      /* a row record lagged past the alpha ring (flush schedule broken) */
 #define DL_STATUS_INDEX 4    /* a batch-index entry out of range (index consumers report, never skip silently) */
 int dl_adam_begin_step(float* opt, float decay_rate, float decay_steps, void* stream);
-/* opt[DL_OPT_STATUS] |= batch_err[0] (the batch's id-validation word, written by
- * dl_index_build / the forward kernels): issued before dl_adam_begin_step so the
- * step of a bad batch is poisoned from its start. */
+/* The step's skip word := the batch's validation bits (batch_err[0], written by
+ * dl_index_build / dl_validate_batch) | the sticky internal-fault bits; a bad batch
+ * also sets opt[DL_OPT_STATUS], records the global step it was skipped at and counts
+ * itself.  Issued before dl_adam_begin_step so the step of a bad batch is poisoned
+ * from its start. */
 int dl_step_guard(const int32_t* batch_err, float* opt, void* stream);
+/* The batch's id-validation word, before its step begins: reset != 0 zeroes err[0] first
+ * (one word per batch, not sticky); then every cate id (cate non-NULL, [L->batch][L->cate_ld]:
+ * single columns against their deep row id + deep_cate_offset and, with FM, their FM row
+ * id + fm_cate_offset; multi-hot columns against id + deep_cate_offset, all in [0, n_rows))
+ * and every wide id (wide non-NULL, [batch][wide_ld], first wide_cols: [0, wide_rows)) sets
+ * DL_STATUS_BAD_ID in err[0] if out of range.  For the batches no dl_index_build validates
+ * (dense-layout gathers) and wdl's wide ids (models/wdl.py:225-228). */
+int dl_validate_batch(const dl_emb_layout* L, const int64_t* cate, const int64_t* wide, int32_t wide_cols,
+                      int32_t wide_ld, int64_t wide_rows, int32_t reset, int32_t* err, void* stream);
 /* dl_step_guard, dl_adam_begin_step and (hist non-NULL) dl_adam_hist_record in one
  * launch, same operations in the same order: the step's opening graph node. */
 int dl_step_begin(const int32_t* batch_err, float* opt, float decay_rate, float decay_steps, float* hist,

@@ -1,30 +1,35 @@
-"""Parity at the BASELINE configurations' own sizes (SURVEY.md §8 config keys C2, C3, C5).
+"""Parity at the BASELINE configurations' own sizes (SURVEY.md §8 config keys C2-C5).
 
 The per-model parity tests (test_gpu_parity.py) run at B <= 1536 and small tables; these
-run the product path (row records, lazy-exact Adam, hipGraph replay) at full size against
-the numpy oracle fed the same injected initial parameters and the same batches:
+run the product path (row records, lazy-exact Adam, hipGraph replay) at full size:
 
-  C2  deepfm_pipeline, 26,000,013 x 16 table, MLP [400]x3, B = 65,536        (fp32, TOL 1e-5)
+  C2  deepfm_pipeline, 26,000,013 x 16 table, MLP [400]x3, B = 65,536          (fp32, TOL 1e-5)
   C3  deepfm_multi_cate, 26 single + 6 multi-hot slots x 60, 26M rows, B = 65,536 (fp32)
+  C4  deepfm_pipeline, 100,000,013-row table in the row-sharded engine (RCCL, one rank)
+      against the single-GPU engine on the same table and batches
   C5  wdl, bf16 deep tower, 26M rows + 26 wide ids, B = 65,536  (stated bf16 tolerance)
 
-Each of 2 training steps is checked from identical state: before step t the oracle takes
-the GPU's parameters and Adam moments (step 0: the injected parameters, zero moments), so
-every comparison is one step of the reference math against one step of the HIP path:
-every logit and the loss (fp32 tolerance 1e-5), then the updated table rows (values and both
-Adam moments) of a sample of rows the batch touched plus a sample of rows it did not, and
-every dense parameter.
+C2 / C3 / C5 follow a 3-step TRAJECTORY against the numpy oracle fed the same injected
+initial parameters and batches, with no re-synchronisation between steps: every logit and
+the loss at every step; the updated table rows (values and both Adam moments) of a sample of
+rows the batch touched plus a sample it did not, and every dense parameter, after the first
+step and after the last.
 
 Sign flips of near-zero gradient sums: the first Adam steps move an element by ~±alpha
 whatever the gradient's size (m/sqrt(v) saturates), so an element whose summed gradient is
 within fp32 rounding of 0 can move the other way when the summation order differs from
 numpy's (a [400, 400] weight gradient sums 65,536 products per element).  Parameters are
-therefore held to 1e-5 except for at most 1e-4 of the elements (at least one for small
-arrays), which must still be within 2*FLIP*alpha (the size of such a flip).  Re-syncing before
-each step keeps flips of one step from feeding the next step's gradients (a flipped hidden
-weight moves the next step's embedding gradients by ~0.2 %, enough to flip ~1e-3 of the
-near-zero ones: measured, and the reason the comparison is per step).
+held to TOL except for a small stated fraction of elements, which must still be within
+2*FLIP*alpha per step taken (the size of such a flip): 1e-4 after the first step; after the
+third, 2e-3 (flips of one step move the next steps' gradients slightly, so a few more
+near-zero sums flip).  The logits carry no such allowance: 1e-5 at every step.
+
+DLAMD_TEST_STATS=<dir>: each test appends its measured maxima / flip fractions there (json).
 """
+import json
+import os
+import socket
+
 import numpy as np
 import pytest
 import torch
@@ -39,42 +44,45 @@ TOL = 1e-5
 N_CATE = 26 * 1_000_000
 B = 65536
 HIDDEN = [400, 400, 400]
-
+STEPS = 3
 
 # |m / sqrt(v)| <= (1 - b1) / sqrt(1 - b2) for TF1 Adam's moments (b1^2 < b2), so one update
 # moves an element by at most FLIP * alpha and a sign flip of it by twice that
 FLIP = (1 - 0.9) / np.sqrt(1 - 0.999)
 
+# bf16 tower (C5): the tower's gradients carry bf16 operand rounding (relative ~2^-9 per
+# product), so the table's gradients, and through Adam's sign-saturated first steps the
+# updates, differ from the fp32 oracle's by a sign flip wherever the fp32 gradient is within
+# that rounding of zero.  Stated bf16 bounds: elements within BF16_ATOL except at most
+# BF16_FRAC of them (measured ~0.3-0.6 %, profiles/r03*/fullsize_stats.json), and every
+# element within the flip size; Adam moments within BF16_MRTOL relative (+ a floor) except
+# the same fraction.
+BF16_ATOL = 1e-5
+BF16_FRAC = 0.02
+BF16_MRTOL = 0.05
 
-def _check_table(got, want, alpha, what, loose=False):
-    d = np.abs(got.astype(np.float64) - want.astype(np.float64))
-    bound = 2 * FLIP * alpha + TOL
-    if loose:   # bf16 tower: every element within the size of a sign flip of its update
-        assert d.max() <= bound, "%s: max error %g > 2*FLIP*alpha" % (what, d.max())
+
+def _stat(name, **kw):
+    d = os.environ.get("DLAMD_TEST_STATS")
+    if not d:
         return
-    bad = d > TOL
-    assert bad.sum() <= max(1, 1e-4 * d.size), "%s: %d of %d elements off by > %g (max %g)" % (what, bad.sum(), d.size, TOL, d.max())
-    assert d.max() <= bound, "%s: max error %g > 2*FLIP*alpha" % (what, d.max())
+    os.makedirs(d, exist_ok=True)
+    with open(os.path.join(d, "fullsize_stats.jsonl"), "a") as f:
+        f.write(json.dumps(dict(test=name, **{k: float(v) for k, v in kw.items()})) + "\n")
 
 
-def _sync_oracle(eng, cfg, opt):
-    """Oracle state := the GPU's parameters and Adam moments (beta powers and step already
-    advance in lockstep)."""
-    P = eng.params()
-    st = eng.adam_state()
-    ds = eng.dense_state()
-    spec = eng.spec
-    tk = spec.table_key
-    opt.m[tk], opt.v[tk] = st["m"], st["v"]
-    if spec.fm:
-        opt.m[spec.first_key], opt.v[spec.first_key] = st["m1"][:, None], st["v1"][:, None]
-    for k in ds["m"]:
-        opt.m[k] = ds["m"][k].reshape(opt.m[k].shape)
-        opt.v[k] = ds["v"][k].reshape(opt.v[k].shape)
-    return P
+def _check(got, want, bound, what, frac, atol=TOL, rtol=0.0, name=""):
+    """All elements within `bound`; at most `frac` of them (at least one) beyond atol + rtol|want|."""
+    g64, w64 = got.astype(np.float64), want.astype(np.float64)
+    d = np.abs(g64 - w64)
+    bad = d > atol + rtol * np.abs(w64)
+    _stat(name or what, max_err=d.max() if d.size else 0.0, frac_bad=bad.mean() if d.size else 0.0)
+    assert bad.sum() <= max(1, frac * d.size), "%s: %d of %d elements off by > %g (max %g)" % (
+        what, bad.sum(), d.size, atol, d.max())
+    assert d.max() <= bound, "%s: max error %g > %g" % (what, d.max(), bound)
 
 
-def _run(model, kw, batches, tower="f32", z_tol=TOL, loss_tol=TOL, auc_tol=None, seed=42):
+def _run(name, model, kw, batches, tower="f32", z_tol=TOL, loss_tol=TOL, auc_tol=None, seed=42):
     cfg = R.make_cfg(model, **kw)
     P = R.init_params(cfg, np.random.default_rng(seed))
     eng = CTREngine(ModelSpec(model, tower=tower, **kw), max_batch=B, init="none", adam="lazy")
@@ -82,65 +90,152 @@ def _run(model, kw, batches, tower="f32", z_tol=TOL, loss_tol=TOL, auc_tol=None,
     opt = R.AdamTF1(cfg, P)
     spec = eng.spec
     tk = spec.table_key
-    loose = tower == "bf16"
+    bf = tower == "bf16"
     rng = np.random.default_rng(1)
+    alphas = []
+    touched_all = []
     for step, b in enumerate(batches):
-        if step:
-            P = _sync_oracle(eng, cfg, opt)
-        alpha = float(opt.alpha())           # this step's alpha (before the oracle advances it)
+        alphas.append(float(opt.alpha()))          # this step's alpha (before the oracle advances it)
         fw = R.train_step(cfg, P, opt, b)
         eng.train_step(b, graph=step >= 1)
         torch.cuda.synchronize()
         eng.check_error()
         z = eng.z[:B].cpu().numpy()
+        dz = np.abs(z.astype(np.float64) - fw["z"])
+        _stat("%s step %d" % (name, step), z_max_err=dz.max(), loss_err=abs(eng.loss() - fw["loss"]))
         np.testing.assert_allclose(z, fw["z"], atol=z_tol, rtol=0, err_msg="logits step %d" % step)
         assert abs(eng.loss() - fw["loss"]) < loss_tol, (eng.loss(), fw["loss"])
         if auc_tol is not None:
             s = eng.score[:B].cpu().numpy()
             assert abs(R.auc(b["label"], s) - R.auc(b["label"], fw["p"])) < auc_tol
-        # the step's update: touched rows (FM rows id + offset, deep rows id, multi-hot ids) and others
+        # rows the step touched (FM rows id + offset, deep rows id, multi-hot ids)
         ids = b["cate_feats"].reshape(-1).astype(np.int64)
-        touched = np.unique(np.concatenate([ids + spec.fm_cate_offset, ids]))
-        touched = touched[touched < spec.n_rows]
-        pick = np.concatenate([rng.choice(touched, 20000, replace=False), rng.integers(0, spec.n_rows, 20000)])
+        t = np.unique(np.concatenate([ids + spec.fm_cate_offset, ids]))
+        touched_all.append(t[t < spec.n_rows])
+        if step not in (0, len(batches) - 1):
+            continue
+        # parameters: after the first step (same state before it) and at the end of the trajectory
+        k = step + 1
+        bound = k * 2 * FLIP * max(alphas) + TOL
+        frac = 1e-4 if step == 0 else 2e-3
+        pick = np.concatenate([rng.choice(touched_all[-1], 20000, replace=False),
+                               rng.choice(touched_all[0], 5000, replace=False),
+                               rng.integers(0, spec.n_rows, 20000)])
         got = eng.params()
         st = eng.adam_state()
-        what = lambda k: "%s (step %d)" % (k, step)
-        _check_table(got[tk][pick], P[tk][pick], alpha, what(tk), loose)
-        if loose:   # moments: the bf16 gradients' relative error
-            np.testing.assert_allclose(st["m"][pick], opt.m[tk][pick], rtol=0.1, atol=1e-7)
-            np.testing.assert_allclose(st["v"][pick], opt.v[tk][pick], rtol=0.2, atol=1e-10)
+        what = lambda key: "%s (step %d)" % (key, step)
+        nm = lambda key: "%s %s step %d" % (name, key, step)
+        if bf:
+            _check(got[tk][pick], P[tk][pick], bound, what(tk), BF16_FRAC, BF16_ATOL, name=nm(tk))
+            _check(st["m"][pick], opt.m[tk][pick], np.inf, what("m"), BF16_FRAC, 1e-7, BF16_MRTOL, name=nm("m"))
+            _check(st["v"][pick], opt.v[tk][pick], np.inf, what("v"), BF16_FRAC, 1e-10, 2 * BF16_MRTOL, name=nm("v"))
         else:
-            _check_table(st["m"][pick], opt.m[tk][pick], alpha, what("m"))
-            _check_table(st["v"][pick], opt.v[tk][pick], alpha, what("v"))
+            _check(got[tk][pick], P[tk][pick], bound, what(tk), frac, name=nm(tk))
+            _check(st["m"][pick], opt.m[tk][pick], bound, what("m"), frac, name=nm("m"))
+            _check(st["v"][pick], opt.v[tk][pick], bound, what("v"), frac, name=nm("v"))
         if spec.fm:
             fk = spec.first_key
-            _check_table(got[fk][pick], P[fk][pick], alpha, what(fk))
-        for k in P:
-            if k in (tk, spec.first_key):
+            _check(got[fk][pick], P[fk][pick], bound, what(fk), frac, name=nm(fk))
+        for key in P:
+            if key in (tk, spec.first_key):
                 continue
-            _check_table(got[k], P[k], alpha, what(k), loose)
+            if bf:
+                _check(got[key], P[key], bound, what(key), BF16_FRAC, BF16_ATOL, name=nm(key))
+            else:
+                _check(got[key], P[key], bound, what(key), frac, name=nm(key))
         del got, st
     return eng
 
 
-def test_c2_deepfm_pipeline_full_size(hip_lib):
+def test_c2_deepfm_pipeline_full_size_trajectory(hip_lib):
     kw = dict(C=13, V=0, S=26, E=16, cate_index_size=N_CATE, hidden=HIDDEN)
-    bs = [make_batch(B, cate_index_size=N_CATE, seed=100 + i) for i in range(2)]
-    _run("deepfm_pipeline", kw, bs)
+    bs = [make_batch(B, cate_index_size=N_CATE, seed=100 + i) for i in range(STEPS)]
+    _run("c2", "deepfm_pipeline", kw, bs)
 
 
-def test_c3_deepfm_multi_cate_full_size(hip_lib):
+def test_c3_deepfm_multi_cate_full_size_trajectory(hip_lib):
     ranges = [[60 * i, 60 * (i + 1), "slot%d" % i] for i in range(6)]
     kw = dict(C=0, V=0, S=26, E=16, cate_index_size=N_CATE, hidden=HIDDEN, multi_ranges=ranges)
     bs = [make_batch(B, cont=0, cate_fields=26, cate_index_size=N_CATE, multi_slots=6, multi_width=60,
-                     seed=200 + i, cate_only=True) for i in range(2)]
-    _run("deepfm_multi_cate", kw, bs)
+                     seed=200 + i, cate_only=True) for i in range(STEPS)]
+    _run("c3", "deepfm_multi_cate", kw, bs)
 
 
-def test_c5_wdl_bf16_full_size(hip_lib):
+def test_c5_wdl_bf16_full_size_trajectory(hip_lib):
     """C5 with the bf16 tower against the fp32 oracle, at the bf16 tolerance stated in
-    test_gpu_parity.py::test_wdl_bf16_tower_tracks_oracle (logits 3e-2, loss 5e-3, AUC 2e-3)."""
+    test_gpu_parity.py::test_wdl_bf16_tower_tracks_oracle (logits 3e-2, loss 5e-3, AUC 2e-3)
+    and the BF16_* parameter bounds above."""
     kw = dict(C=13, S=26, E=16, cate_index_size=N_CATE, hidden=HIDDEN, Fw=26)
-    bs = [make_batch(B, cate_index_size=N_CATE, seed=300 + i, wide_fields=26) for i in range(2)]
-    _run("wdl", kw, bs, tower="bf16", z_tol=3e-2, loss_tol=5e-3, auc_tol=2e-3)
+    bs = [make_batch(B, cate_index_size=N_CATE, seed=300 + i, wide_fields=26) for i in range(STEPS)]
+    _run("c5", "wdl", kw, bs, tower="bf16", z_tol=3e-2, loss_tol=5e-3, auc_tol=2e-3)
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def test_c4_sharded_100m_rows_equals_single_gpu(hip_lib):
+    """C4's workload at one rank: the 100,000,013-row table (25.6 GB of row records) in the
+    row-sharded engine (shard.py: index, count all-gather, RCCL id / row / gradient exchanges,
+    owner gather and update, flat all-reduce) against the single-GPU engine on the same table,
+    parameters and batches (B = 65,536, 3 steps): logits and loss every step, then the records
+    (p, both moments, first-order triple) of sampled touched rows, the replicated FM cont rows
+    and every dense parameter.  At one rank both engines sum every gradient in the same order,
+    so the bar is bit-identity, with 1e-5 allowed for the replicated rows' dense update."""
+    import torch.distributed as dist
+    from deep_learning_amd.shard import Exchange, ShardedCTREngine
+    n_cate = 100_000_000
+    spec = ModelSpec("deepfm_pipeline", C=13, V=0, S=26, E=16, cate_index_size=n_cate, hidden=HIDDEN)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()), RANK="0", WORLD_SIZE="1")
+    dist.init_process_group("nccl", device_id=torch.device("cuda", 0))
+    try:
+        one = CTREngine(spec, max_batch=B, seed=2019, adam="lazy")
+        sh = ShardedCTREngine(spec, B, Exchange(), seed=2019, adam="lazy")
+        # the same state: records copied (local row i == global row i at one rank), the
+        # replicated FM cont rows taken from the same records, the dense parameters copied
+        assert sh.rec.shape == one.rec.shape
+        sh.rec.copy_(one.rec)
+        E, rep = spec.E, sh.rep
+        sh.rep_t[:rep].copy_(one.rec[:rep, :E])
+        sh.rep_f[:rep].copy_(one.rec[:rep, E])
+        for l in range(len(HIDDEN)):
+            sh.W[l].copy_(one.W[l])
+            sh._refresh_wb(l)
+        sh.w_head.copy_(one.w_head)
+        sh.opt.copy_(one.opt)
+        torch.cuda.synchronize()
+        bs = [make_batch(B, cate_index_size=n_cate, seed=400 + i) for i in range(STEPS)]
+        dev = [{k: torch.from_numpy(v).cuda() for k, v in b.items()} for b in bs]
+        for step, b in enumerate(dev):
+            one.train_step(b, graph=step >= 1)
+            sh.train_step(b, graph=step >= 1)
+            torch.cuda.synchronize()
+            one.check_error()
+            za, zb = one.z[:B].cpu().numpy(), sh.z[:B].cpu().numpy()
+            _stat("c4 step %d" % step, z_max_err=np.abs(za - zb).max(), z_bit_equal=(za == zb).mean())
+            np.testing.assert_allclose(zb, za, atol=TOL, rtol=0, err_msg="logits step %d" % step)
+            assert abs(sh.loss() - one.loss()) < TOL
+        one.flush()
+        sh.flush()
+        torch.cuda.synchronize()
+        ids = np.concatenate([b["cate_feats"].reshape(-1) for b in bs]).astype(np.int64)
+        rows = np.unique(np.concatenate([ids + 13, ids]))
+        rows = rows[rows >= rep]        # rows < 13 are the replicated FM cont rows (checked below)
+        rng = np.random.default_rng(5)
+        pick = torch.from_numpy(np.concatenate([rng.choice(rows, 200_000, replace=False),
+                                                rng.integers(rep, spec.n_rows, 50_000)])).cuda()
+        ra, rb = one.rec[pick, : 3 * E + 4], sh.rec[pick, : 3 * E + 4]
+        _stat("c4 records", max_err=(ra - rb).abs().max().item(), bit_equal=(ra == rb).float().mean().item())
+        assert torch.equal(ra, rb), "records differ: max %g" % (ra - rb).abs().max().item()
+        # replicated FM cont-field rows (dense Adam on the replica) against the single-GPU records
+        np.testing.assert_allclose(sh.rep_t[:rep].cpu().numpy(), one.rec[:rep, :E].cpu().numpy(), atol=TOL, rtol=0)
+        np.testing.assert_allclose(sh.rep_f[:rep].cpu().numpy(), one.rec[:rep, E].cpu().numpy(), atol=TOL, rtol=0)
+        for l in range(len(HIDDEN)):
+            np.testing.assert_allclose(sh.W[l].cpu().numpy(), one.W[l].cpu().numpy(), atol=TOL, rtol=0)
+        np.testing.assert_allclose(sh.w_head.cpu().numpy(), one.w_head.cpu().numpy(), atol=TOL, rtol=0)
+        del one, sh
+        torch.cuda.empty_cache()
+    finally:
+        dist.destroy_process_group()

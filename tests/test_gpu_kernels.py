@@ -531,8 +531,16 @@ def test_auc_gpu_matches_sklearn_goldens_and_oracle(hip_lib):
     for a in range(0, n, 700_001):                                        # ragged batches
         acc.add(torch.from_numpy(y[a:a + 700_001]).cuda(), torch.from_numpy(s[a:a + 700_001]).cuda())
     assert abs(acc.result() - R.auc(y, s)) < 1e-12
+    # tiny sets: one positive and one negative (either order, tied), a tie group holding every class
+    assert roc_auc(np.array([0, 1]), np.array([0.1, 0.2])) == 1.0
+    assert roc_auc(np.array([1, 0]), np.array([0.1, 0.2])) == 0.0
+    assert roc_auc(np.array([1, 0]), np.array([0.3, 0.3])) == 0.5
+    y3, s3 = np.array([1, 0, 1, 0, 0]), np.array([0.5, 0.5, 0.9, -1.0, 0.5], np.float32)
+    assert abs(roc_auc(y3, s3) - R.auc(y3, s3)) < 1e-12
     with pytest.raises(ValueError, match="one class"):
         roc_auc(np.ones(10), np.arange(10.0))
+    with pytest.raises(ValueError, match="one class"):
+        roc_auc(np.zeros(1), np.zeros(1))
 
 
 @pytest.mark.parametrize("n,distinct", [(1, 1), (4096 * 3, 5), (100_003, 50), (262_147, 200_000), (5000, 4999)])

@@ -241,40 +241,58 @@ def test_prefetch_matches_inline_index(hip_lib, name, adam):
         eq(runs[0][1][k], runs[1][1][k], err_msg=k)
 
 
-@pytest.mark.parametrize("name", ["deepfm_pipeline", "wdl", "deepfm_multi_cate"])
-def test_bad_id_step_applies_nothing_and_raises(hip_lib, name):
+@pytest.mark.parametrize("name,adam,where", [
+    ("deepfm_pipeline", "lazy", "cate"), ("deepfm_pipeline", "dense", "cate"),
+    ("wdl", "lazy", "cate"), ("wdl", "lazy", "wide"), ("wdl", "dense", "wide"),
+    ("deepfm_multi_cate", "lazy", "multi"), ("deepfm_multi_cate", "dense", "multi")])
+def test_bad_id_batch_skipped_alone_and_raises(hip_lib, name, adam, where):
     """TF raises InvalidArgumentError inside the failing sess.run, before anything is applied
-    (deepfm_pipeline.py:219-221).  Here the batch index validates the ids and poisons the step
-    (include/dlamd.h, status word): the bad step and any step issued before the host notices
-    apply nothing, and train_step raises within two calls.  Parameters, Adam moments and the
-    step counter are then exactly those of the last good step, and training continues."""
+    (deepfm_pipeline.py:219-221), and the next sess.run applies normally.  Here every id is
+    validated before its step begins (dl_index_build, dl_validate_batch for the dense-layout
+    gathers and wdl's wide ids), the step of the bad batch is skipped whole (the per-step skip
+    word, include/dlamd.h), the batches after it apply, and train_step raises within two calls
+    naming the global step skipped.  The final state is bit-identical to an engine that never
+    saw the bad batch: parameters, Adam moments, the step counter (adam='dense' runs the
+    dense-layout gather and the float-atomic backward, whose summation order varies: 1e-5)."""
     from deep_learning_amd import _lib
     kw = CASES[name]
     spec = ModelSpec(_model(name), **kw)
-    eng = CTREngine(spec, max_batch=256, seed=4, adam="lazy")
-    bs = _batches(name, kw, 256, 5, seed=13)
-    for i, b in enumerate(bs[:3]):
-        eng.train_step(b, graph=i >= 1)
-    p0, s0 = eng.params(), eng.adam_state()
-    step0 = float(eng.opt[7].item())
+    mk = lambda: CTREngine(spec, max_batch=256, seed=4, adam=adam)
+    eng, twin = mk(), mk()
+    bs = _batches(name, kw, 256, 6, seed=13)
     bad = {k: v.copy() for k, v in bs[3].items()}
-    bad["cate_feats"][5, 3] = kw["cate_index_size"] + 7
-    with pytest.raises(_lib.DLError, match="out of range"):
-        eng.train_step(bad, graph=True)
-        for b in bs[:3]:
-            eng.train_step(b, graph=True)
-        torch.cuda.synchronize()
-        eng.check_error()
-    assert float(eng.opt[7].item()) == step0
-    p1, s1 = eng.params(), eng.adam_state()
-    for k in p0:
-        np.testing.assert_array_equal(p1[k], p0[k], err_msg=k)
-    for k in s0:
-        np.testing.assert_array_equal(s1[k], s0[k], err_msg=k)
-    eng.train_step(bs[4], graph=True)        # the engine trains on after the error
+    if where == "cate":
+        bad["cate_feats"][5, 3] = kw["cate_index_size"] + 7
+    elif where == "multi":
+        bad["cate_feats"][7, -2] = kw["cate_index_size"] + 3
+    else:
+        bad["wide_feats"][9, 1] = kw["cate_index_size"] + kw["hidden"][-1] + 1
+    seq = bs[:3] + [bad] + bs[4:]
+    raised = []
+    for i, b in enumerate(seq):
+        try:
+            eng.train_step(b, graph=i >= 1)        # the batch's step is issued even if this raises
+        except _lib.DLError as e:
+            raised.append(str(e))
     torch.cuda.synchronize()
-    eng.check_error()
-    assert float(eng.opt[7].item()) == step0 + 1
+    try:
+        eng.check_error()
+    except _lib.DLError as e:
+        raised.append(str(e))
+    assert len(raised) == 1 and "out of range" in raised[0] and "global_step 3" in raised[0], raised
+    for i, b in enumerate(bs[:3] + bs[4:]):
+        twin.train_step(b, graph=i >= 1)
+    torch.cuda.synchronize()
+    twin.check_error()
+    assert float(eng.opt[7].item()) == float(twin.opt[7].item()) == 5
+    same = (np.testing.assert_array_equal if adam == "lazy" else
+            lambda a, b, err_msg: np.testing.assert_allclose(a, b, atol=TOL, rtol=0, err_msg=err_msg))
+    pe, pt = eng.params(), twin.params()
+    for k in pt:
+        same(pe[k], pt[k], err_msg=k)
+    se, st = eng.adam_state(), twin.adam_state()
+    for k in st:
+        same(se[k], st[k], err_msg=k)
 
 
 def _hot(bs, seed=5):
