@@ -77,9 +77,17 @@ extern "C" int dl_all_to_allv(void* comm, const void* send, const int64_t* send_
       dl::set_error("dl_all_to_allv: negative count for peer %d", p);
       return 22;
     }
-    // bytes as ncclChar: no element-size constraint on the rows
-    if (send_counts[p]) DL_NCCL(ncclSend(s + so * row_bytes, (size_t)(send_counts[p] * row_bytes), ncclChar, p, c, st));
-    if (recv_counts[p]) DL_NCCL(ncclRecv(r + ro * row_bytes, (size_t)(recv_counts[p] * row_bytes), ncclChar, p, c, st));
+    // bytes as ncclChar: no element-size constraint on the rows.  A failed send/recv closes
+    // the group before returning, so no later RCCL call of the thread is left grouped.
+    ncclResult_t e = ncclSuccess;
+    if (send_counts[p]) e = ncclSend(s + so * row_bytes, (size_t)(send_counts[p] * row_bytes), ncclChar, p, c, st);
+    if (e == ncclSuccess && recv_counts[p])
+      e = ncclRecv(r + ro * row_bytes, (size_t)(recv_counts[p] * row_bytes), ncclChar, p, c, st);
+    if (e != ncclSuccess) {
+      ncclGroupEnd();
+      dl::set_error("dl_all_to_allv: peer %d: %s", p, ncclGetErrorString(e));
+      return 2000 + (int)e;
+    }
     so += send_counts[p];
     ro += recv_counts[p];
   }

@@ -161,10 +161,6 @@ class Exchange:
                 out.copy_(res)
                 return out
             return res
-        if async_op and not self.staged:
-            work = dist.all_to_all_single(res, src, output_split_sizes=list(recv_splits),
-                                          input_split_sizes=list(send_splits), group=self.group, async_op=True)
-            return res, work
         dist.all_to_all_single(res, src, output_split_sizes=list(recv_splits),
                                input_split_sizes=list(send_splits), group=self.group)
         if async_op:
@@ -321,7 +317,8 @@ class ShardedCTREngine(CTREngine):
             self.own_ws = e(_lib.lib().dl_index_workspace_bytes(cap), torch.uint8)
             self.own_keys, self.own_pos, self.own_uniq = e(cap), e(cap), e(cap)
             self.own_off, self.own_n = e(cap + 1), e(4)
-            # the owner gather's moment stash [cap][2E+4], read back by the update
+            # the owner gather's moment stash [cap][2E+4], read back by the sorted update
+            # (the arrival-chain update re-reads the record instead: no stash)
             self.own_mv = e(cap * (2 * self.spec.E + 4), torch.float32)
         self.own_cap = cap
 
