@@ -94,6 +94,17 @@ enum { S3_STORE = 0, S3_RELU = 1, S3_MASK = 2 };
 #define DL_S3_BPF 0   // 1: NT pins the next fragment's weight reads ahead of this one's MFMAs
 #endif                // (sched_barrier; measured slower than leaving the order to the scheduler)
 
+#ifndef DL_S3_PF
+#define DL_S3_PF 1    // NT: weight fragments read this many fragments ahead of their MFMAs
+#endif
+#ifndef DL_S3_SGB
+#define DL_S3_SGB 0   // NT: pin the order (fragment f + PF's LDS reads, then fragment f's 12 MFMAs)
+#endif                // with sched_group_barrier, so the reads are not sunk next to their use
+
+#ifndef DL_S3_ASMB
+#define DL_S3_ASMB 0  // NT: the weight fragments' LDS reads as inline asm, DL_S3_PF fragments ahead,
+#endif                // each fragment's MFMAs behind a hand-counted lgkmcnt wait tied to its registers
+
 #ifndef DL_S3_TN2
 #define DL_S3_TN2 1   // weight gradients: the double-buffered TN kernel (0: the single-buffer one)
 #endif
@@ -121,6 +132,18 @@ constexpr int kNtEP = kNtBN + 4;                                 // epilogue til
 static_assert(8 * 16 * kNtEP * sizeof(float) <= kNtLds, "epilogue tiles fit the ring");
 
 __device__ __forceinline__ int nt_slot(int j, int kq) { return kq ^ ((j >> 2) & 2); }   // an involution in kq
+
+// One weight fragment's three plane reads (planes kNtPlane apart = 13,312 B), issued as asm
+// so the compiler cannot sink them next to their MFMAs; lds_wait<N> then waits until at most
+// N LDS reads are outstanding (LDS reads complete in order) and ties the fragment's registers
+// to that wait, so its MFMAs cannot be scheduled above it.
+__device__ __forceinline__ void nt_rd3(uint32_t a, shortx8& h, shortx8& m, shortx8& l) {
+  asm volatile("ds_read_b128 %0, %3\n\tds_read_b128 %1, %3 offset:13312\n\tds_read_b128 %2, %3 offset:26624"
+               : "=&v"(h), "=&v"(m), "=&v"(l)
+               : "v"(a)
+               : "memory");
+}
+#define DL_LDS_WAIT(N, h, m, l) asm volatile("s_waitcnt lgkmcnt(" #N ")" : "+v"(h), "+v"(m), "+v"(l))
 
 // s_waitcnt vmcnt(n) (n < 64), other counters untouched
 #define DL_WAIT_VMCNT(n) __builtin_amdgcn_s_waitcnt(((n) & 0xF) | (((n) >> 4) << 14) | (0x7 << 4) | (0xF << 8))
@@ -244,15 +267,39 @@ __global__ __launch_bounds__(512) void gemm_s3_nt_kernel(S3Params p) {
       }
     };
     // every fragment, also those past N (clamped weight rows, products discarded by the
-    // epilogue): no per-fragment branch, so the scheduler hoists fragment f + 1's reads over
+    // epilogue): no per-fragment branch, so the scheduler hoists fragment f + PF's reads over
     // fragment f's MFMAs instead of each fragment waiting out its own LDS latency
-    shortx8 nh, nm, nl;
-    rd_b(0, nh, nm, nl);
+    constexpr int PF = DL_S3_PF;
+    shortx8 bb[PF + 1][3];
+    // the fragments' LDS byte address: fragment f's rows 16f + cl sit 1,024 B apart (the
+    // swizzle slot depends only on cl and kq), planes 13,312 B apart
+    const uint32_t b_addr = lds_base + 2u * (uint32_t)((c % 3) * kNtBuf + cl * 32 + 8 * nt_slot(cl, kq));
+#pragma unroll
+    for (int i = 0; i < PF; ++i) {
+      if (DL_S3_ASMB) nt_rd3(b_addr + 1024u * i, bb[i][0], bb[i][1], bb[i][2]);
+      else rd_b(i, bb[i][0], bb[i][1], bb[i][2]);
+    }
 #pragma unroll
     for (int f = 0; f < kNtNF; ++f) {
       {
-        const shortx8 bh = nh, bm = nm, bl = nl;
-        if (f + 1 < kNtNF) rd_b(f + 1, nh, nm, nl);
+        constexpr int NB = PF + 1;
+        if (f + PF < kNtNF) {
+          if (DL_S3_ASMB) nt_rd3(b_addr + 1024u * (f + PF), bb[(f + PF) % NB][0], bb[(f + PF) % NB][1], bb[(f + PF) % NB][2]);
+          else rd_b(f + PF, bb[(f + PF) % NB][0], bb[(f + PF) % NB][1], bb[(f + PF) % NB][2]);
+        }
+        if (DL_S3_ASMB) {
+          shortx8 &h = bb[f % NB][0], &m = bb[f % NB][1], &l = bb[f % NB][2];
+          if (f + PF < kNtNF) {           // fragments f + 1 .. f + PF may stay in flight
+            if (PF == 1) DL_LDS_WAIT(3, h, m, l);
+            else if (PF == 2) DL_LDS_WAIT(6, h, m, l);
+            else DL_LDS_WAIT(9, h, m, l);
+          } else if (f + 1 < kNtNF) {     // the tail: only fragment f + 1's reads remain younger
+            DL_LDS_WAIT(3, h, m, l);
+          } else {
+            DL_LDS_WAIT(0, h, m, l);
+          }
+        }
+        const shortx8 bh = bb[f % NB][0], bm = bb[f % NB][1], bl = bb[f % NB][2];
         if (DL_S3_BPF) __builtin_amdgcn_sched_barrier(0);   // keep them there
         if (DL_S3_DIAG == 2) {
           acc[0][f][0] += (float)(bh[0] ^ ah[0][1] ^ bm[2] ^ bl[3] ^ am[0][0] ^ al[0][2]);
@@ -260,6 +307,10 @@ __global__ __launch_bounds__(512) void gemm_s3_nt_kernel(S3Params p) {
         } else {
           acc[0][f] = mfma_s3(ah[0], am[0], al[0], bh, bm, bl, acc[0][f]);
           acc[1][f] = mfma_s3(ah[1], am[1], al[1], bh, bm, bl, acc[1][f]);
+        }
+        if (DL_S3_SGB) {
+          if (f + PF < kNtNF) __builtin_amdgcn_sched_group_barrier(0x100, 3, 0);   // 3 DS reads
+          __builtin_amdgcn_sched_group_barrier(0x008, 12, 0);                     // then 12 MFMAs
         }
       }
     }

@@ -64,3 +64,46 @@ def make_batch(B, cont=13, vector=0, cate_fields=26, cate_index_size=26_000_000,
         out["wide_feats"] = np.stack(
             [_field_ids(rng, B, f % max(S, 1), per_field, dist, alpha, perm) for f in range(wide_fields)], 1)
     return out
+
+
+def make_batch_device(B, cont=13, vector=0, cate_fields=26, cate_index_size=26_000_000, multi_slots=0,
+                      multi_width=60, wide_fields=0, seed=2019, cate_only=False, device="cuda"):
+    """The same distributions as make_batch (uniform ids only), drawn on the device with a
+    seeded torch generator: fresh batches every bench step cost no host time (a host draw of
+    one C3 batch takes ~0.3 s).  Values differ from make_batch's for the same seed; keys,
+    dtypes and shapes are the reference loader's (utils/data_loader.py:12-24)."""
+    import torch
+    g = torch.Generator(device=device)
+    g.manual_seed(int(seed))
+    S = cate_fields
+    per_field = max(2, cate_index_size // max(1, S + multi_slots))
+    span = per_field - 1
+    out = {}
+    dense = None
+    if cont > 0 and not cate_only:
+        c = torch.empty(B, cont, device=device).exponential_(0.1, generator=g).log1p_()
+        out["cont_feats"] = c
+        dense = c / 4.0
+    elif not cate_only:
+        out["cont_feats"] = torch.zeros(B, 0, device=device)
+    out["vector_feats"] = torch.randn(B, vector, device=device, generator=g) * 0.1
+    lo = torch.arange(S, device=device, dtype=torch.int64) * per_field + 1
+    cols = [lo + torch.randint(0, span, (B, S), device=device, generator=g)]
+    for m in range(multi_slots):
+        ids = (S + m) * per_field + 1 + torch.randint(0, span, (B, multi_width), device=device, generator=g)
+        ln = torch.randint(1, multi_width, (B, 1), device=device, generator=g)
+        ids[torch.arange(multi_width, device=device)[None, :] >= ln] = 0
+        cols.append(ids)
+    cate = torch.cat(cols, 1).contiguous()
+    out["cate_feats"] = cate
+    tw = ((cate[:, :S] * 2654435761) % 1000).double() / 1000.0 - 0.5
+    logit = tw.sum(1) * 0.6 - 1.1
+    if dense is not None:
+        logit = logit + dense.double() @ torch.linspace(-0.5, 0.5, dense.shape[1], device=device, dtype=torch.float64)
+    p = torch.sigmoid(logit)
+    out["label"] = (torch.rand(B, device=device, generator=g, dtype=torch.float64) < p).float().reshape(B, 1)
+    if wide_fields:
+        f = torch.arange(wide_fields, device=device, dtype=torch.int64) % max(S, 1)
+        out["wide_feats"] = (f * per_field + 1 + torch.randint(0, span, (B, wide_fields), device=device,
+                                                                generator=g)).contiguous()
+    return out

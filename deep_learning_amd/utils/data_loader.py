@@ -24,7 +24,7 @@ import os
 import numpy as np
 
 from . import tfrecord
-from .native_reader import NativeReader
+from .native_reader import DeviceBatches, NativeReader
 
 CATE_ALGS = ("deepfm_cate", "dnn_cate", "dnn_multi_cate", "deepfm_multi_cate")
 
@@ -53,11 +53,13 @@ def parse_example(data, spec):
 
 
 class BatchStream:
-    """Re-iterable stream of batches (dicts of numpy arrays).  Each ``iter()`` opens the
-    native reader (libdlio.so: framing + CRC-32C, shuffle buffer, FixedLenFeature parse on
+    """Re-iterable stream of batches (dicts of numpy arrays; with ``device`` set — or
+    ``mp.device_batches`` — dicts of device tensors with the same keys, dtypes and shapes,
+    uploaded one batch ahead through pinned buffers: DeviceBatches).  Each ``iter()`` opens
+    the native reader (libdlio.so: framing + CRC-32C, shuffle buffer, FixedLenFeature parse on
     ``threads`` C++ threads — num_parallel_calls=10 at data_loader.py:31 — and batching)."""
 
-    def __init__(self, mp, files, action_type, threads=10, depth=4):
+    def __init__(self, mp, files, action_type, threads=10, depth=4, device=None):
         self.mp = mp
         self.files = list(files)
         self.repeat = int(mp.epochs) if action_type == "train" else 1
@@ -67,12 +69,14 @@ class BatchStream:
         self.seed = getattr(mp, "shuffle_seed", None)
         self.threads = int(getattr(mp, "reader_threads", threads))
         self.depth = depth
+        self.device = device if device is not None else getattr(mp, "device_batches", None)
 
     def __iter__(self):
         spec = [(k, kind, size) for k, (kind, size) in self.spec.items()]
-        return NativeReader(self.files, spec, self.bsz, repeat=self.repeat,
-                            shuffle_buf=self.bsz * 10 if self.shuffle else 0,   # shuffle(bsz*10), :34
-                            seed=self.seed, threads=self.threads, depth=self.depth)
+        r = NativeReader(self.files, spec, self.bsz, repeat=self.repeat,
+                         shuffle_buf=self.bsz * 10 if self.shuffle else 0,   # shuffle(bsz*10), :34
+                         seed=self.seed, threads=self.threads, depth=self.depth)
+        return DeviceBatches(r, self.device, self.depth) if self.device else r
 
 
 def get_file_list(input_path):
@@ -81,12 +85,14 @@ def get_file_list(input_path):
     return [input_path + f for f in files if f[:4] == "part"]
 
 
-def pipeline_process(mp, file_dir_list, action_type):
-    return BatchStream(mp, file_dir_list, action_type)
+def pipeline_process(mp, file_dir_list, action_type, device=None):
+    return BatchStream(mp, file_dir_list, action_type, device=device)
 
 
-def load_input_file(mp, input_path, action_type):
-    return pipeline_process(mp, get_file_list(input_path), action_type)
+def load_input_file(mp, input_path, action_type, device=None):
+    """device="cuda": batches as device tensors (the reference's get_next() tensors,
+    data_loader.py:43-46); default host numpy batches (the model stages them itself)."""
+    return pipeline_process(mp, get_file_list(input_path), action_type, device=device)
 
 
 def write_tfrecord_part(path, batch):

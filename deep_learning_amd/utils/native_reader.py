@@ -89,6 +89,48 @@ class PinnedFeed:
             self.events[batch["_slot"]] = event
 
 
+class DeviceBatches:
+    """Iterator of batches as DEVICE tensors (the reference's loader hands its graph
+    `get_next()` tensors, utils/data_loader.py:29-46): the native reader decodes into pinned
+    host buffers (PinnedFeed), each batch is uploaded on a copy stream of its own one batch
+    ahead of the consumer, and a yielded batch is ordered after its upload on the consumer's
+    current stream (keys, dtypes and shapes as the host batches: label [B,1] f32, cont_feats
+    [B,C] f32, vector_feats [B,V] f32, cate_feats [B,S+M] int64)."""
+
+    def __init__(self, reader, device="cuda", depth=4):
+        import torch
+        self.torch = torch
+        self.device = torch.device(device)
+        self.feed = PinnedFeed(reader, depth)
+        self.stream = torch.cuda.Stream(self.device)
+        self.pending = self._upload(self.feed.next())
+
+    def _upload(self, hb):
+        if hb is None:
+            return None
+        torch = self.torch
+        with torch.cuda.stream(self.stream):
+            d = {k: v.to(self.device, non_blocking=True) for k, v in hb.items() if k != "_slot"}
+            ev = torch.cuda.Event()
+            ev.record(self.stream)
+        self.feed.mark(hb, ev)          # the pinned set is reused once this copy has landed
+        return d, ev
+
+    def __iter__(self):
+        return self
+
+    def __next__(self):
+        if self.pending is None:
+            raise StopIteration
+        d, ev = self.pending
+        self.pending = self._upload(self.feed.next())   # the next upload overlaps this batch's use
+        cur = self.torch.cuda.current_stream(self.device)
+        cur.wait_event(ev)
+        for t in d.values():
+            t.record_stream(cur)        # allocated on the copy stream, used on the consumer's
+        return d
+
+
 class NativeReader:
     """Iterator of batches: dict name -> array [batch, size] (float32 / int64).
 

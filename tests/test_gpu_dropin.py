@@ -248,3 +248,49 @@ def test_tfrecord_two_epoch_trajectory_matches_oracle(hip_lib, tmp_path):
     got = eng.params()
     for k in P:
         np.testing.assert_allclose(got[k], P[k], atol=1e-5, rtol=0, err_msg=k)
+
+
+def test_device_batch_iterator_matches_host_batches(hip_lib, tmp_path):
+    """load_input_file(..., device="cuda") yields DEVICE tensors (the reference's get_next()
+    tensors, utils/data_loader.py:29-46) with the host iterator's keys, dtypes, shapes and
+    values, epoch by epoch (shuffle off, drop_remainder, repeat 2), and trains the drop-in
+    model exactly as the host batches do (logits of every step equal)."""
+    from deep_learning_amd.local_run import ModelParams
+    from deep_learning_amd.models import deepfm_pipeline as M
+    from deep_learning_amd.synthetic import make_batch
+    from deep_learning_amd.utils import data_loader
+    from oracle import ctr_ref as R
+    conf, tr = tmp_path / "conf", tmp_path / "train"
+    for p in (conf, tr):
+        p.mkdir()
+    _conf(str(conf))
+    V, Bsz = 3000, 64
+    for i, n in enumerate((70, 90, 50)):
+        data_loader.write_tfrecord_part(str(tr / ("part-%d" % i)), make_batch(n, cate_index_size=V, seed=i + 1))
+    argv = ["local_run.py", "deepfm_pipeline", "train", "2", "8", str(V), "1000", str(conf), str(tr) + "/",
+            str(tr) + "/", str(tmp_path / "model_pb"), str(tmp_path / "ckpt"), "0", str(tmp_path / "ckpt"),
+            "batch_size=%d" % Bsz, "hidden_units=32,16", "shuffle=0"]
+    mp = ModelParams(argv)
+    host = list(data_loader.load_input_file(mp, mp.train_path, "train"))
+    dev = list(data_loader.load_input_file(mp, mp.train_path, "train", device="cuda"))
+    assert len(host) == len(dev) == 6     # 3 batches per epoch (210 records // 64), 2 epochs
+    for h, d in zip(host, dev):
+        assert set(h) == set(d)
+        for k in h:
+            assert d[k].is_cuda and d[k].dtype == torch.from_numpy(h[k]).dtype and tuple(d[k].shape) == h[k].shape
+            np.testing.assert_array_equal(d[k].cpu().numpy(), h[k], err_msg=k)
+    cfg = R.make_cfg("deepfm_pipeline", C=13, V=0, S=26, E=8, cate_index_size=V, hidden=[32, 16])
+    zs = []
+    for batches in (host, dev):
+        m = M.DeepModel(mp, batches)
+        m.model_optimizer()
+        eng = m.engine
+        eng.load_params(R.init_params(cfg, np.random.default_rng(3)))
+        out = []
+        for b in batches:
+            eng.train_step(b)
+            torch.cuda.synchronize()
+            out.append(eng.z[:Bsz].cpu().numpy().copy())
+        zs.append(out)
+    for a, b in zip(*zs):
+        np.testing.assert_array_equal(a, b)
