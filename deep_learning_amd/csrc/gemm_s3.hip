@@ -105,6 +105,10 @@ enum { S3_STORE = 0, S3_RELU = 1, S3_MASK = 2 };
 #define DL_S3_ASMB 0  // NT: the weight fragments' LDS reads as inline asm, DL_S3_PF fragments ahead,
 #endif                // each fragment's MFMAs behind a hand-counted lgkmcnt wait tied to its registers
 
+#ifndef DL_S3_TNSTAG
+#define DL_S3_TNSTAG 0   // TN2: waves 4-7 split + store the next step's tiles BEFORE their MFMAs
+#endif                   // (waves 0-3 after), so the two waves of a SIMD overlap VALU/LDS with MFMA
+
 #ifndef DL_S3_TN2
 #define DL_S3_TN2 1   // weight gradients: the double-buffered TN kernel (0: the single-buffer one)
 #endif
@@ -650,17 +654,45 @@ __global__ __launch_bounds__(512) void gemm_s3_tn2_kernel(S3Params p) {
       for (int a = 0; a < 2; ++a) acc[a][b] = mfma_s3(ah[a], am[a], al[a], bh, bm, bl, acc[a][b]);
     }
   };
-  if (nk > 0) {
-    load(kbeg);
-    store(0);
-  }
-  __syncthreads();
-  for (int kt = 0; kt < nk; ++kt) {
-    const bool more = kt + 1 < nk;
-    if (more) load(kbeg + (kt + 1) * kT2KS);
-    compute(kt & 1);
-    if (more) store((kt + 1) & 1);   // the other buffer: its last readers passed the previous barrier
+  if (DL_S3_TNSTAG) {
+    // Staggered roles (MI355X_MICROARCH.md, two waves per SIMD: waves w and w + 4 share one):
+    // waves 0-3 run [MFMAs of step kt][split + store of step kt + 1], waves 4-7 the reverse, so
+    // on every SIMD one wave's VALU/LDS work runs beside the other's MFMAs.  The registers
+    // hold step kt + 1's tiles from the load issued after the previous store; the barrier
+    // waits only for this wave's LDS writes (a __syncthreads would also drain the loads in
+    // flight, vmcnt(0)).
+    if (nk > 0) {
+      load(kbeg);
+      store(0);
+      if (nk > 1) load(kbeg + kT2KS);
+    }
+    __builtin_amdgcn_s_waitcnt(0xc07f);   // lgkmcnt(0)
+    __builtin_amdgcn_s_barrier();
+    const bool late = wid >= 4;
+    for (int kt = 0; kt < nk; ++kt) {
+      const bool more = kt + 1 < nk;
+      if (!late) compute(kt & 1);
+      if (more) {
+        store((kt + 1) & 1);            // the other buffer: its last readers passed the previous barrier
+        if (kt + 2 < nk) load(kbeg + (kt + 2) * kT2KS);
+      }
+      if (late) compute(kt & 1);
+      __builtin_amdgcn_s_waitcnt(0xc07f);
+      __builtin_amdgcn_s_barrier();
+    }
+  } else {
+    if (nk > 0) {
+      load(kbeg);
+      store(0);
+    }
     __syncthreads();
+    for (int kt = 0; kt < nk; ++kt) {
+      const bool more = kt + 1 < nk;
+      if (more) load(kbeg + (kt + 1) * kT2KS);
+      compute(kt & 1);
+      if (more) store((kt + 1) & 1);   // the other buffer: its last readers passed the previous barrier
+      __syncthreads();
+    }
   }
   float* __restrict__ C = p.C + (long long)z * p.c_split_stride;
 #pragma unroll

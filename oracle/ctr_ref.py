@@ -362,7 +362,10 @@ def dlogit(cfg, p, lab, dtype=F32):
     return (dp * p * (1 - p)).astype(dtype)
 
 
-def backward(cfg, P, batch, fw, dtype=F32):
+def backward(cfg, P, batch, fw, dtype=F32, trace=None):
+    """Analytic gradients of every parameter.  trace (a dict, tests only) receives each dense
+    layer's input X_i and output gradient g_i (G[deep_i] = X_i^T g_i) and dz, so a test can
+    measure how ill-conditioned a gradient sum is (sum_b |X_i[b, r]| |g_i[b, c]| against |G|)."""
     E, S, C = cfg.E, cfg.S, cfg.C
     B = fw["z"].shape[0]
     G = {k: np.zeros_like(v, dtype=dtype) for k, v in P.items()}
@@ -393,8 +396,12 @@ def backward(cfg, P, batch, fw, dtype=F32):
     # MLP backward
     xs = [fw["x0"]] + fw["hs"][:-1]
     g = (dh * (fw["hs"][-1] > 0)).astype(dtype)
+    if trace is not None:
+        trace.update(dz=dz, xs=xs, g={})
     for i in reversed(range(len(H))):
         Wi = P["deep_%d" % i].astype(dtype)
+        if trace is not None:
+            trace["g"][i] = g
         G["deep_%d" % i] = (xs[i].T @ g).astype(dtype)
         if cfg.model == "wdl":
             G["deep_%d" % i] += l2 * Wi

@@ -10,19 +10,23 @@ run the product path (row records, lazy-exact Adam, hipGraph replay) at full siz
   C5  wdl, bf16 deep tower, 26M rows + 26 wide ids, B = 65,536  (stated bf16 tolerance)
 
 C2 / C3 / C5 follow a 3-step TRAJECTORY against the numpy oracle fed the same injected
-initial parameters and batches, with no re-synchronisation between steps: every logit and
-the loss at every step; the updated table rows (values and both Adam moments) of a sample of
-rows the batch touched plus a sample it did not, and every dense parameter, after the first
-step and after the last.
+initial parameters and batches: every logit and the loss at every step; every dense
+parameter and its Adam moments after every step; the updated table rows (values and both
+Adam moments) of a sample of rows the batches touched plus a sample they did not, after the
+first step and after the last.
 
-Sign flips of near-zero gradient sums: the first Adam steps move an element by ~±alpha
+Ill-conditioned gradient sums: the first Adam steps move an element by up to FLIP * alpha
 whatever the gradient's size (m/sqrt(v) saturates), so an element whose summed gradient is
-within fp32 rounding of 0 can move the other way when the summation order differs from
-numpy's (a [400, 400] weight gradient sums 65,536 products per element).  Parameters are
-held to TOL except for a small stated fraction of elements, which must still be within
-2*FLIP*alpha per step taken (the size of such a flip): 1e-4 after the first step; after the
-third, 2e-3 (flips of one step move the next steps' gradients slightly, so a few more
-near-zero sums flip).  The logits carry no such allowance: 1e-5 at every step.
+within fp32 rounding of zero can move differently when the summation order differs from
+numpy's (a [400, 400] weight gradient sums 65,536 products per element).  After each step a
+dense element off by more than TOL must (a) be one of at most 1e-4 of the layer's elements,
+(b) be within one step's flip size, and (c) have an ill-conditioned gradient: |G| <= 1e-3 *
+sum_b |terms| (measured from the oracle's own operands: X_i^T g_i for hidden weights).  Only
+such elements — typically a dozen of the ~500 k dense parameters per step — take the GPU's
+value (and moments) in the oracle before the next step; everything else runs on unsynced, so
+a flip cannot hide a real error and cannot leak into the next step's logits either, which are
+then held to 1e-5.  Table rows are never re-synced: sampled rows within TOL except 1e-4 of
+the elements after the first step and 5e-4 after the last (their gradients are short sums).
 
 DLAMD_TEST_STATS=<dir>: each test appends its measured maxima / flip fractions there (json).
 """
@@ -53,12 +57,13 @@ FLIP = (1 - 0.9) / np.sqrt(1 - 0.999)
 # bf16 tower (C5): the tower's gradients carry bf16 operand rounding (relative ~2^-9 per
 # product), so the table's gradients, and through Adam's sign-saturated first steps the
 # updates, differ from the fp32 oracle's by a sign flip wherever the fp32 gradient is within
-# that rounding of zero.  Stated bf16 bounds: elements within BF16_ATOL except at most
-# BF16_FRAC of them (measured ~0.3-0.6 %, profiles/r03*/fullsize_stats.json), and every
-# element within the flip size; Adam moments within BF16_MRTOL relative (+ a floor) except
-# the same fraction.
-BF16_ATOL = 1e-5
-BF16_FRAC = 0.02
+# that rounding of zero (and move by a different amount where it is near Adam's epsilon).
+# Stated bf16 bounds: elements within BF16_ATOL except at most BF16_FRAC of them (measured
+# after one step: hidden weights 0.1 % beyond 1e-5, max 8.7e-4; biases 3.75 % beyond 1e-5,
+# max 8.8e-5 — profiles/r03b/fullsize_stats.jsonl), every element within the flip size;
+# Adam moments within BF16_MRTOL relative (+ a floor) except the same fraction.
+BF16_ATOL = 1e-4
+BF16_FRAC = 0.01
 BF16_MRTOL = 0.05
 
 
@@ -71,15 +76,23 @@ def _stat(name, **kw):
         f.write(json.dumps(dict(test=name, **{k: float(v) for k, v in kw.items()})) + "\n")
 
 
-def _check(got, want, bound, what, frac, atol=TOL, rtol=0.0, name=""):
-    """All elements within `bound`; at most `frac` of them (at least one) beyond atol + rtol|want|."""
-    g64, w64 = got.astype(np.float64), want.astype(np.float64)
-    d = np.abs(g64 - w64)
-    bad = d > atol + rtol * np.abs(w64)
-    _stat(name or what, max_err=d.max() if d.size else 0.0, frac_bad=bad.mean() if d.size else 0.0)
-    assert bad.sum() <= max(1, frac * d.size), "%s: %d of %d elements off by > %g (max %g)" % (
-        what, bad.sum(), d.size, atol, d.max())
-    assert d.max() <= bound, "%s: max error %g > %g" % (what, d.max(), bound)
+def _terms(key, idx, trace, fw):
+    """sum_b |terms| of the gradient sums of dense parameter `key` at flat indices idx (the
+    scale the sums' f32 rounding lives on): hidden weights X_i^T g_i, biases sum_b g_i, the
+    FM / deep_res head weights feats^T dz (hs[-1]^T dz), its bias sum_b dz."""
+    dz = np.abs(trace["dz"]).astype(np.float64)
+    if key.startswith("deep_bias_"):
+        g = np.abs(trace["g"][int(key.rsplit("_", 1)[1])]).astype(np.float64)
+        return g.sum(0)[idx]
+    if key.startswith("deep_") and key[5:].isdigit():
+        i = int(key[5:])
+        X, g = np.abs(trace["xs"][i]), np.abs(trace["g"][i])
+        r, c = np.unravel_index(idx, (X.shape[1], g.shape[1]))
+        return np.array([float(np.dot(X[:, a].astype(np.float64), g[:, b].astype(np.float64))) for a, b in zip(r, c)])
+    if key in ("deep_fm_weight", "deep_res"):
+        F = np.abs(fw["feats"] if key == "deep_fm_weight" else fw["hs"][-1]).astype(np.float64)
+        return (F[:, idx] * dz[:, None]).sum(0)
+    return np.full(len(idx), dz.sum())
 
 
 def _run(name, model, kw, batches, tower="f32", z_tol=TOL, loss_tol=TOL, auc_tol=None, seed=42):
@@ -92,58 +105,93 @@ def _run(name, model, kw, batches, tower="f32", z_tol=TOL, loss_tol=TOL, auc_tol
     tk = spec.table_key
     bf = tower == "bf16"
     rng = np.random.default_rng(1)
-    alphas = []
     touched_all = []
+    fails = []
+
+    def check(cond, msg):
+        if not cond:
+            fails.append(msg)
+
+    def compare(got, want, bound, what, frac, atol=TOL, rtol=0.0):
+        g64, w64 = got.astype(np.float64), want.astype(np.float64)
+        d = np.abs(g64 - w64)
+        bad = d > atol + rtol * np.abs(w64)
+        _stat("%s %s" % (name, what), max_err=d.max() if d.size else 0.0, frac_bad=bad.mean() if d.size else 0.0)
+        check(bad.sum() <= max(1, frac * d.size), "%s: %d of %d elements off by > %g (max %g)" % (
+            what, bad.sum(), d.size, atol, d.max()))
+        check(d.max() <= bound, "%s: max error %g > %g" % (what, d.max(), bound))
+        return bad
+
     for step, b in enumerate(batches):
-        alphas.append(float(opt.alpha()))          # this step's alpha (before the oracle advances it)
-        fw = R.train_step(cfg, P, opt, b)
+        alpha = float(opt.alpha())           # this step's alpha (before the oracle advances it)
+        trace = {}
+        fw = R.forward(cfg, P, b)
+        G, _ = R.backward(cfg, P, b, fw, trace=trace)
+        opt.apply(P, G)
         eng.train_step(b, graph=step >= 1)
         torch.cuda.synchronize()
         eng.check_error()
         z = eng.z[:B].cpu().numpy()
         dz = np.abs(z.astype(np.float64) - fw["z"])
-        _stat("%s step %d" % (name, step), z_max_err=dz.max(), loss_err=abs(eng.loss() - fw["loss"]))
-        np.testing.assert_allclose(z, fw["z"], atol=z_tol, rtol=0, err_msg="logits step %d" % step)
-        assert abs(eng.loss() - fw["loss"]) < loss_tol, (eng.loss(), fw["loss"])
+        _stat("%s step %d" % (name, step), z_max_err=dz.max(), z_frac_bad=(dz > z_tol).mean(),
+              loss_err=abs(eng.loss() - fw["loss"]))
+        check(dz.max() <= z_tol, "logits step %d: max error %g > %g (%d samples)" % (step, dz.max(), z_tol,
+                                                                                      (dz > z_tol).sum()))
+        check(abs(eng.loss() - fw["loss"]) < loss_tol, "loss step %d: %r vs %r" % (step, eng.loss(), fw["loss"]))
         if auc_tol is not None:
             s = eng.score[:B].cpu().numpy()
-            assert abs(R.auc(b["label"], s) - R.auc(b["label"], fw["p"])) < auc_tol
+            check(abs(R.auc(b["label"], s) - R.auc(b["label"], fw["p"])) < auc_tol, "AUC step %d" % step)
         # rows the step touched (FM rows id + offset, deep rows id, multi-hot ids)
         ids = b["cate_feats"].reshape(-1).astype(np.int64)
         t = np.unique(np.concatenate([ids + spec.fm_cate_offset, ids]))
         touched_all.append(t[t < spec.n_rows])
+        # dense parameters and moments after every step
+        bound = 2 * FLIP * alpha + TOL
+        got = eng._export_dense(eng.W, eng.w_head, getattr(eng, "ww", None), getattr(eng, "wb", None))
+        ds = eng.dense_state()
+        for key in got:
+            what = "%s (step %d)" % (key, step)
+            if bf:
+                compare(got[key], P[key], bound, what, BF16_FRAC, BF16_ATOL)
+                continue
+            bad = compare(got[key], P[key], bound, what, 1e-4).reshape(-1)
+            if not bad.any() or key == "wdl_weights":
+                continue
+            # the elements off: ill-conditioned sums only, then the oracle takes the GPU's state
+            idx = np.flatnonzero(bad)
+            gabs = np.abs(G[key].reshape(-1)[idx].astype(np.float64))
+            terms = _terms(key, idx, trace, fw)
+            ratio = (gabs / np.maximum(terms, 1e-300)).max()
+            _stat("%s %s cond" % (name, what), repaired=len(idx), max_g_over_terms=ratio)
+            check(ratio <= 1e-3, "%s: an element off by > %g has a well-conditioned gradient (|G|/sum|terms| %g)"
+                  % (what, TOL, ratio))
+            for arr, src in ((P[key], got[key]), (opt.m[key], ds["m"][key]), (opt.v[key], ds["v"][key])):
+                arr.reshape(-1)[idx] = np.asarray(src).reshape(-1)[idx]
         if step not in (0, len(batches) - 1):
             continue
-        # parameters: after the first step (same state before it) and at the end of the trajectory
+        # the table: after the first step and at the end of the trajectory (never re-synced)
         k = step + 1
-        bound = k * 2 * FLIP * max(alphas) + TOL
-        frac = 1e-4 if step == 0 else 2e-3
+        tbound = k * 2 * FLIP * alpha + TOL
+        frac = 1e-4 if step == 0 else 5e-4
         pick = np.concatenate([rng.choice(touched_all[-1], 20000, replace=False),
                                rng.choice(touched_all[0], 5000, replace=False),
                                rng.integers(0, spec.n_rows, 20000)])
-        got = eng.params()
+        gp = eng.params()
         st = eng.adam_state()
         what = lambda key: "%s (step %d)" % (key, step)
-        nm = lambda key: "%s %s step %d" % (name, key, step)
         if bf:
-            _check(got[tk][pick], P[tk][pick], bound, what(tk), BF16_FRAC, BF16_ATOL, name=nm(tk))
-            _check(st["m"][pick], opt.m[tk][pick], np.inf, what("m"), BF16_FRAC, 1e-7, BF16_MRTOL, name=nm("m"))
-            _check(st["v"][pick], opt.v[tk][pick], np.inf, what("v"), BF16_FRAC, 1e-10, 2 * BF16_MRTOL, name=nm("v"))
+            compare(gp[tk][pick], P[tk][pick], tbound, what(tk), BF16_FRAC, BF16_ATOL)
+            compare(st["m"][pick], opt.m[tk][pick], np.inf, what("m"), BF16_FRAC, 1e-7, BF16_MRTOL)
+            compare(st["v"][pick], opt.v[tk][pick], np.inf, what("v"), BF16_FRAC, 1e-10, 2 * BF16_MRTOL)
         else:
-            _check(got[tk][pick], P[tk][pick], bound, what(tk), frac, name=nm(tk))
-            _check(st["m"][pick], opt.m[tk][pick], bound, what("m"), frac, name=nm("m"))
-            _check(st["v"][pick], opt.v[tk][pick], bound, what("v"), frac, name=nm("v"))
+            compare(gp[tk][pick], P[tk][pick], tbound, what(tk), frac)
+            compare(st["m"][pick], opt.m[tk][pick], tbound, what("m"), frac)
+            compare(st["v"][pick], opt.v[tk][pick], tbound, what("v"), frac)
         if spec.fm:
             fk = spec.first_key
-            _check(got[fk][pick], P[fk][pick], bound, what(fk), frac, name=nm(fk))
-        for key in P:
-            if key in (tk, spec.first_key):
-                continue
-            if bf:
-                _check(got[key], P[key], bound, what(key), BF16_FRAC, BF16_ATOL, name=nm(key))
-            else:
-                _check(got[key], P[key], bound, what(key), frac, name=nm(key))
-        del got, st
+            compare(gp[fk][pick], P[fk][pick], tbound, what(fk), frac)
+        del gp, st
+    assert not fails, "; ".join(fails)
     return eng
 
 
