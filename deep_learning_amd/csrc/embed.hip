@@ -41,6 +41,11 @@ struct EmbArgs {
   const float* hist;
   const float* opt;
   int lag;
+  // staged mode (with inv; the lazy single-GPU forward after dl_rec_gather_scatter): the FM
+  // reference (b, f) reads table row inv_base + b*S + f (the FM staging rows), its first-order
+  // output and the deep references' x0 columns are already written — only references whose
+  // row has no key (inv < 0: the zero row) are written here, as zeros
+  int staged;
 };
 
 __device__ __forceinline__ bool row_ok(int64_t row, int zero_row0) {
@@ -108,10 +113,10 @@ __global__ __launch_bounds__(256, (REC || NPS > 5) ? 1 : DL_FWD_MIN_WAVES) void 
           const int j = k / S, f = k % S;
           const int64_t rb = (int64_t)(b0 + j) * ns;
           const int di = a.inv[rb + (L.use_fm ? S : 0) + f];
-          rows_s[j][Fs + f] = di < 0 ? -1 : a.inv_base + di;
+          rows_s[j][Fs + f] = di < 0 ? -1 : (a.staged ? -2 : a.inv_base + di);   // -2: written by the gather
           if (L.use_fm) {
             const int fi = a.inv[rb + f];
-            rows_s[j][Cf + f] = fi < 0 ? -1 : a.inv_base + fi;
+            rows_s[j][Cf + f] = fi < 0 ? -1 : a.inv_base + (a.staged ? (b0 + j) * S + f : fi);
           }
         }
       } else {
@@ -196,10 +201,13 @@ __global__ __launch_bounds__(256, (REC || NPS > 5) ? 1 : DL_FWD_MIN_WAVES) void 
       // first-order terms (one lane per FM field; record mode: the cont fields only)
       float w1 = 0.f, val = 0.f;
       int frow = -1;
+      // staged: the FM cate fields' first-order outputs were written by the gather (their rows
+      // index the staging rows, not first_order) — only the zero rows' are written here
+      const bool w1_done = a.staged && lane >= Cf && lane < Fs && rows_s[j][lane] >= 0;
       if (lane < (REC ? Cf : Fs)) {
         frow = rows_s[j][lane];
         val = lane < Cf ? vals_s[j][lane] : 1.f;
-        w1 = a.first_order[frow < 0 ? 0 : frow];
+        w1 = a.first_order[(frow < 0 || w1_done) ? 0 : frow];
       }
       float4 s = z4, ss = z4;
 #pragma unroll
@@ -216,7 +224,7 @@ __global__ __launch_bounds__(256, (REC || NPS > 5) ? 1 : DL_FWD_MIN_WAVES) void 
             s.x += ev.x; s.y += ev.y; s.z += ev.z; s.w += ev.w;
             ss.x = fmaf(ev.x, ev.x, ss.x); ss.y = fmaf(ev.y, ev.y, ss.y);
             ss.z = fmaf(ev.z, ev.z, ss.z); ss.w = fmaf(ev.w, ev.w, ss.w);
-          } else if (sl < nslot) {
+          } else if (sl < nslot && rw[p] != -2) {
             const int col = L.x0_cat_col + (sl - Fs) * E + 4 * q;
             if (L.x0_bf16)
               *reinterpret_cast<uint2*>(xbb + col) = make_uint2(f2bf(t4.x) | ((unsigned)f2bf(t4.y) << 16),
@@ -226,9 +234,10 @@ __global__ __launch_bounds__(256, (REC || NPS > 5) ? 1 : DL_FWD_MIN_WAVES) void 
           }
         }
       }
-      if (lane < (REC ? Cf : Fs)) a.fm_out[(int64_t)b * L.fm_ld + lane] = frow < 0 ? 0.f : w1 * val;
+      if (lane < (REC ? Cf : Fs) && !w1_done) a.fm_out[(int64_t)b * L.fm_ld + lane] = frow < 0 ? 0.f : w1 * val;
       for (int f = 64 + lane; f < (REC ? 0 : Fs); f += 64) {   // > 64 FM fields (rare; record mode: <= 64)
         const int fr = rows_s[j][f];
+        if (a.staged && f >= Cf && fr >= 0) continue;
         const float vv = f < Cf ? vals_s[j][f] : 1.f;
         a.fm_out[(int64_t)b * L.fm_ld + f] = fr < 0 ? 0.f : a.first_order[fr] * vv;
       }
@@ -718,6 +727,19 @@ extern "C" int dl_embed_fwd_indexed(const dl_emb_layout* L, const float* rows, c
   DL_CHECK_ARG(!L->use_fm || (rows_first && fm_out && fm_sum), "FM outputs required");
   if (L->batch == 0) return 0;
   EmbArgs a{*L, inv, inv_base, rows, rows_first, nullptr, cont, vector, x0, fm_out, fm_sum, nullptr};
+  return launch_embed_fwd<false>(L, a, stream);
+}
+
+extern "C" int dl_embed_fwd_staged(const dl_emb_layout* L, const float* fmst, const float* rows_first,
+                                   const int32_t* inv, int32_t n_rep, const float* cont, const float* vector,
+                                   float* x0, float* fm_out, float* fm_sum, void* stream) {
+  if (int rc = check_layout(L)) return rc;
+  DL_CHECK_ARG(inv && x0, "NULL inv/x0");
+  DL_CHECK_ARG(!L->use_fm || (fmst && rows_first && fm_out && fm_sum), "FM inputs / outputs required");
+  DL_CHECK_ARG(!L->use_fm || !L->fm_cont || L->cont_rows_compact, "the FM cont-field rows come compact");
+  if (L->batch == 0) return 0;
+  EmbArgs a{*L, inv, n_rep, fmst ? fmst : x0, rows_first, nullptr, cont, vector, x0, fm_out, fm_sum, nullptr};
+  a.staged = 1;
   return launch_embed_fwd<false>(L, a, stream);
 }
 

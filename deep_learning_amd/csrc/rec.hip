@@ -99,7 +99,50 @@ __device__ __forceinline__ void replay_elems(float* st, const int* from_s, const
   }
 }
 
-template <int E, bool SPARSE>
+// Forward scatter (the lazy single-GPU forward, dl_rec_gather_scatter): each caught-up row is
+// also written straight to the references that read it, through the batch index's sorted
+// segments, instead of only compactly for embed_fwd to re-read at random through the inverse
+// map — random 64-B writes run at the HBM write rate, random 64-B reads at about half of it
+// (profiles/r03b/ubench_scatter.txt: 6.0 vs 3.3 TB/s):
+//   FM reference (b, f)    -> fmst[n_rep + b*S + f] (the rows embed_fwd's staged mode sums per
+//                             sample) and fm_out[b][Cf + f] = w1 (the first-order output)
+//   deep reference (b, f)  -> x0[b][x0_cat_col + f*E] (f32, or bf16 for the bf16 tower)
+// Multi-hot references are pooled from the compact rows as before; the replicated rows go to
+// fmst[0, n_rep).  Rows with more than kSegLong references are left to gather_scatter_long.
+struct GatherScatter {
+  const int32_t* seg_off;
+  const int32_t* refs;
+  float* fmst;
+  float* x0;
+  float* fm_out;
+  long long nrefs;
+  int ns, S, mb, use_fm, Cf, x0_ld, x0_cat_col, x0_bf16, fm_ld, n_rep;
+  int* status;
+};
+
+template <int E>
+__device__ __forceinline__ void scatter_ref(const GatherScatter& s, int k, int q, float4 p, float w, bool first) {
+  if (k < 0 || k >= s.nrefs) {
+    index_fault(s.status);
+    return;
+  }
+  const int b = k / s.ns, sl = k - b * s.ns;
+  if (sl >= s.mb) return;   // multi-hot: pooled from the compact rows
+  if (s.use_fm && sl < s.S) {
+    *reinterpret_cast<float4*>(s.fmst + ((long long)s.n_rep + (long long)b * s.S + sl) * E + 4 * q) = p;
+    if (first && q == 0) s.fm_out[(long long)b * s.fm_ld + s.Cf + sl] = w * 1.f;
+  } else {
+    const int f = s.use_fm ? sl - s.S : sl;
+    const long long o = (long long)b * s.x0_ld + s.x0_cat_col + f * E + 4 * q;
+    if (s.x0_bf16)
+      *reinterpret_cast<uint2*>(reinterpret_cast<unsigned short*>(s.x0) + o) =
+          make_uint2(f2bf(p.x) | ((unsigned)f2bf(p.y) << 16), f2bf(p.z) | ((unsigned)f2bf(p.w) << 16));
+    else
+      *reinterpret_cast<float4*>(s.x0 + o) = p;
+  }
+}
+
+template <int E, bool SPARSE, bool SCAT = false>
 __global__ __launch_bounds__(256) void rec_gather_kernel(const float* __restrict__ rec, RecCfg c, int64_t n_rows,
                                                          int n_rep, int64_t rep_base,
                                                          const uint32_t* __restrict__ uniq,
@@ -107,7 +150,7 @@ __global__ __launch_bounds__(256) void rec_gather_kernel(const float* __restrict
                                                          int world, const float* __restrict__ hist,
                                                          const float* __restrict__ opt, int lag,
                                                          float* __restrict__ out, float* __restrict__ out1,
-                                                         float* __restrict__ mv) {
+                                                         float* __restrict__ mv, GatherScatter sc = {}) {
   rec_load_hyper(c, opt);
   __shared__ float hw[kHistWin];
   const RingW ring = load_hist_window(hw, hist, (int)opt[7], c);
@@ -130,6 +173,17 @@ __global__ __launch_bounds__(256) void rec_gather_kernel(const float* __restrict
     const long long i = base + rw;
     const bool valid = i < total;
     const int64_t row = !valid ? -1 : i < n_rep ? rep_base + i : decode_key(uniq[i - n_rep], world);
+    // the row's reference segment (scatter form), loaded beside the record
+    int so0 = 0, so1 = 0, k0 = -1;
+    if (SCAT && valid && i >= n_rep) {
+      so0 = sc.seg_off[i - n_rep];
+      so1 = sc.seg_off[i - n_rep + 1];
+      if (so0 < 0 || so1 > sc.nrefs || so0 > so1) {
+        index_fault(sc.status);
+        so0 = so1 = 0;
+      }
+      k0 = so0 < so1 ? sc.refs[so0] : -1;
+    }
     const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
     float4 p = z, m = z, v = z;
     float w = 0.f, wm = 0.f, wv = 0.f;
@@ -198,6 +252,14 @@ __global__ __launch_bounds__(256) void rec_gather_kernel(const float* __restrict
       __builtin_amdgcn_wave_barrier();
     }
     if (!valid) continue;
+    if (SCAT) {
+      if (i < n_rep) {
+        *reinterpret_cast<float4*>(sc.fmst + i * E + 4 * q) = p;
+      } else if (so1 - so0 <= kSegLong) {   // longer segments: gather_scatter_long_kernel
+        if (so0 < so1) scatter_ref<E>(sc, k0, q, p, w, c.has_first);
+        for (int e = so0 + 1; e < so1; ++e) scatter_ref<E>(sc, sc.refs[e], q, p, w, c.has_first);
+      }
+    }
     *reinterpret_cast<float4*>(out + i * E + 4 * q) = p;
     if (out1 && q == 0) out1[i] = w;
     if (mv) {   // caught-up moments for the backward's update: [m(E) | v(E) | m1 v1 0 0]
@@ -206,6 +268,45 @@ __global__ __launch_bounds__(256) void rec_gather_kernel(const float* __restrict
       *reinterpret_cast<float4*>(o + E + 4 * q) = v;
       if (q == 0) *reinterpret_cast<float4*>(o + 2 * E) = make_float4(wm, wv, 0.f, 0.f);
     }
+  }
+}
+
+// The scatter form's second pass: the rows with more than kSegLong references (hot ids), one
+// whole block each, from the compact rows the gather wrote (the write order is immaterial:
+// every reference has its own destination).
+template <int E>
+__global__ __launch_bounds__(256) void gather_scatter_long_kernel(GatherScatter s, const int32_t* __restrict__ n_uniq,
+                                                                  long long max_u, const float* __restrict__ rows,
+                                                                  const float* __restrict__ rows1, int has_first) {
+  __shared__ int n_long;
+  __shared__ int long_u[256];
+  constexpr int LPR = E / 4, NS = 256 / LPR;
+  const int tid = threadIdx.x, q = tid % LPR;
+  const long long nu = clamp_uniq(n_uniq, max_u, s.status);
+  const long long per = (nu + gridDim.x - 1) / gridDim.x;
+  const long long u0 = (long long)blockIdx.x * per, u1 = min(nu, u0 + per);
+  for (long long base = u0; base < u1; base += 256) {
+    const long long u = base + tid;
+    int o0 = 0, o1 = 0;
+    if (u < u1) {
+      o0 = max(0, s.seg_off[u]);
+      o1 = (int)min(s.nrefs, (long long)s.seg_off[u + 1]);
+    }
+    const bool lng = o1 - o0 > kSegLong;
+    if (tid == 0) n_long = 0;
+    if (!__syncthreads_or(lng)) continue;
+    if (lng) long_u[atomicAdd(&n_long, 1)] = (int)(u - base);
+    __syncthreads();
+    const int n = n_long;
+    for (int t = 0; t < n; ++t) {
+      const long long uu = base + long_u[t];
+      const int e0 = max(0, s.seg_off[uu]), e1 = (int)min(s.nrefs, (long long)s.seg_off[uu + 1]);
+      const long long iu = s.n_rep + uu;
+      const float4 p = *reinterpret_cast<const float4*>(rows + iu * E + 4 * q);
+      const float w = has_first ? rows1[iu] : 0.f;
+      for (int e = e0 + tid / LPR; e < e1; e += NS) scatter_ref<E>(s, s.refs[e], q, p, w, has_first);
+    }
+    __syncthreads();
   }
 }
 
@@ -717,9 +818,57 @@ extern "C" int dl_rec_gather(const dl_emb_layout* L, const float* rec, int32_t r
                        make_rec_cfg(kE, rec_ld, rec_flags, hist_len), (int64_t)L->n_rows, n_rep,
                        n_rep ? (int64_t)L->fm_cont_offset : (int64_t)0, uniq_keys, n_uniq, (long long)max_uniq,
                        world, hist, opt, lag, rows_u,
-                       has_first ? rows_u1 : nullptr, mv_u);
+                       has_first ? rows_u1 : nullptr, mv_u, GatherScatter{});
   });
   DL_RETURN_LAUNCH("dl_rec_gather");
+}
+
+extern "C" int dl_rec_gather_scatter(const dl_emb_layout* L, const float* rec, int32_t rec_ld, int32_t rec_flags,
+                                     int32_t n_rep, const uint32_t* uniq_keys, const int32_t* n_uniq,
+                                     int64_t max_uniq, const int32_t* seg_off, const int32_t* sorted_refs,
+                                     const float* hist, int32_t hist_len, const float* opt, int32_t lag,
+                                     float* rows_u, float* rows_u1, float* mv_u, float* fmst, void* x0,
+                                     float* fm_out, void* stream) {
+  const int32_t has_first = rec_flags & DL_REC_FIRST;
+  DL_CHECK_ARG(L && rec && hist && opt && rows_u && uniq_keys && n_uniq && seg_off && sorted_refs && x0,
+               "NULL argument");
+  if (int rc = rec_check(L->emb_dim, rec_ld, hist_len)) return rc;
+  DL_CHECK_ARG(n_rep >= 0 && n_rep <= L->n_rows, "bad n_rep");
+  DL_CHECK_ARG(!has_first || rows_u1, "rows_u1 required with first-order weights");
+  DL_CHECK_ARG(!L->use_fm || (fmst && fm_out), "FM staging rows and fm_out required");
+  DL_CHECK_ARG(L->x0_ld % 4 == 0 && L->x0_cat_col % 4 == 0, "x0 must be float4 aligned");
+  const long long total = n_rep + (max_uniq > 0 ? max_uniq : 0);
+  if (total == 0) return 0;
+  GatherScatter sc{};
+  sc.seg_off = seg_off;
+  sc.refs = sorted_refs;
+  sc.fmst = fmst;
+  sc.x0 = reinterpret_cast<float*>(x0);
+  sc.fm_out = fm_out;
+  sc.nrefs = (long long)L->batch * index_slots(*L);
+  sc.ns = index_slots(*L);
+  sc.S = L->cate_fields;
+  sc.mb = index_multi_base(*L);
+  sc.use_fm = L->use_fm;
+  sc.Cf = (L->use_fm && L->fm_cont) ? L->cont_fields : 0;
+  sc.x0_ld = L->x0_ld;
+  sc.x0_cat_col = L->x0_cat_col;
+  sc.x0_bf16 = L->x0_bf16;
+  sc.fm_ld = L->fm_ld;
+  sc.n_rep = n_rep;
+  sc.status = reinterpret_cast<int*>(const_cast<float*>(opt) + DL_OPT_STATUS);
+  DL_DISPATCH_E(L->emb_dim, {
+    const unsigned grid = grid_cap(total * (kE / 4));
+    auto kern = (rec_flags & DL_REC_SPARSE_ADAM) ? rec_gather_kernel<kE, true, true> : rec_gather_kernel<kE, false, true>;
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(256), 0, as_stream(stream), rec,
+                       make_rec_cfg(kE, rec_ld, rec_flags, hist_len), (int64_t)L->n_rows, n_rep,
+                       n_rep ? (int64_t)L->fm_cont_offset : (int64_t)0, uniq_keys, n_uniq, (long long)max_uniq, 1,
+                       hist, opt, lag, rows_u, has_first ? rows_u1 : nullptr, mv_u, sc);
+    if (max_uniq > 0)
+      hipLaunchKernelGGL(gather_scatter_long_kernel<kE>, dim3(1024), dim3(256), 0, as_stream(stream), sc, n_uniq,
+                         (long long)max_uniq, rows_u, has_first ? rows_u1 : nullptr, has_first);
+  });
+  DL_RETURN_LAUNCH("dl_rec_gather_scatter");
 }
 
 extern "C" int dl_rec_bwd_adam(const dl_emb_layout* L, float* rec, int32_t rec_ld, int32_t rec_flags, int32_t n_rep,

@@ -207,7 +207,8 @@ class ModelSpec:
 
 class CTREngine:
     def __init__(self, spec, max_batch, device="cuda", seed=2019, init="device", bwd="atomic",
-                 table_rows=None, adam="dense", hist_len=4096, rec_stash=True, fwd_rec=False, gemm="s3"):
+                 table_rows=None, adam="dense", hist_len=4096, rec_stash=True, fwd_rec=False, gemm="s3",
+                 fwd_scatter=None):
         if not torch.cuda.is_available():
             raise _lib.DLError("CTREngine needs a HIP device (no CPU fallback)")
         _lib.lib()
@@ -382,6 +383,15 @@ class CTREngine:
         # waves/SIMD (169 VGPRs) costs ~190 us that the gather's catch-up hides (253 us with
         # no rows lagging; scripts/catchup_cost.py).
         self.fwd_rec = bool(fwd_rec and self.lazy and not M and not rec_stash)
+        # fwd_scatter (the lazy default): the gather writes each caught-up row straight to the
+        # references reading it (dl_rec_gather_scatter: FM staging rows, first-order outputs,
+        # x0's deep columns) and dl_embed_fwd_staged sums the FM terms per sample from the
+        # staging rows — random 64-B writes in place of the indexed forward's random 64-B reads
+        # through the inverse map.  DLAMD_FWD_SCATTER=0 keeps the indexed forward.
+        if fwd_scatter is None:
+            fwd_scatter = os.environ.get("DLAMD_FWD_SCATTER", "1") != "0"
+        self.fwd_scatter = bool(fwd_scatter and self.lazy and not self.fwd_rec and type(self) is CTREngine)
+        self.fmst = z(self.n_rep + B * S, E) if (self.fwd_scatter and sp.fm) else None
         # static input slots (graph capture reads from these)
         self.in_label = z(B)
         self.in_cont = z(B, max(sp.C, 1))
@@ -681,6 +691,22 @@ class CTREngine:
                     ptr(self.rows_u), ptr(self.rows_u1) if sp.fm else None, ptr(self.in_cate), ptr(self.in_cont),
                     ptr(self.in_vec), ptr(self.hist), self.hist_len, ptr(self.opt), 1 if train else 0,
                     ptr(x0), ptr(self.fm_out), ptr(self.fm_sum), ptr(self.err), s)
+        elif self.fwd_scatter:
+            # rows of the batch (index built by _pre), caught up to the step being taken and
+            # scattered to the references reading them; then the FM sums per sample
+            self._c("rec_gather", "dl_rec_gather_scatter", C_ref(L), ptr(self.rec), self.rec_ld, self.rec_flags,
+                    self.n_rep, ptr(self.idx_uniq), ptr(self.idx_n), B * self.n_slot, ptr(self.idx_off),
+                    ptr(self.idx_refs), ptr(self.hist), self.hist_len, ptr(self.opt), 1 if train else 0,
+                    ptr(self.rows_u), ptr(self.rows_u1), ptr(self.mv_u) if (train and self.mv_u is not None) else None,
+                    ptr(self.fmst), ptr(x0), ptr(self.fm_out), s)
+            if sp.M:
+                self._c("pool_fwd", "dl_pool_fwd_indexed", C_ref(L), ptr(self.rows_u),
+                        ptr(self.rows_u1) if sp.fm else None, ptr(self.idx_inv), self.n_rep, ptr(self.slot_start),
+                        ptr(self.slot_end), sp.M, self.fm_pool_col, ptr(self.x0), ptr(self.fm_out), ptr(self.cnt_emb),
+                        ptr(self.cnt_first), s)
+            self._c("embed_fwd", "dl_embed_fwd_staged", C_ref(L), ptr(self.fmst), ptr(self.rows_u1) if sp.fm else None,
+                    ptr(self.idx_inv), self.n_rep, ptr(self.in_cont), ptr(self.in_vec), ptr(x0), ptr(self.fm_out),
+                    ptr(self.fm_sum), s)
         elif self.lazy:
             # rows of the batch (index built by _pre), caught up to the step being taken
             self._c("rec_gather", "dl_rec_gather", C_ref(L), ptr(self.rec), self.rec_ld, self.rec_flags, self.n_rep,

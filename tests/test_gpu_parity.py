@@ -354,3 +354,34 @@ def test_hot_rows_match_oracle(hip_lib, name, bwd):
     got = eng.params()
     for k in P:
         np.testing.assert_allclose(got[k], P[k], atol=TOL, rtol=0, err_msg=k)
+
+
+@pytest.mark.parametrize("name,tower", [("deepfm_pipeline", "f32"), ("wdl", "f32"), ("wdl", "bf16"),
+                                        ("deepfm_multi_cate", "f32"), ("dnn_pipeline", "f32")])
+def test_scatter_forward_bit_identical_to_indexed(hip_lib, name, tower):
+    """The lazy forward's scatter form (dl_rec_gather_scatter + dl_embed_fwd_staged: rows
+    written to their references' FM staging rows / first-order outputs / x0 columns) against
+    the indexed form (compact rows read back through the inverse map): logits, x0 (bf16 for
+    the bf16 tower), the FM outputs and the trained parameters bit for bit, on batches with
+    hot rows (segments far past the 32-reference per-row limit: the block-per-row pass),
+    padding id 0 (no row: zeros written by the staged forward) and ids aliasing cont rows."""
+    kw = CASES[name]
+    spec = ModelSpec(_model(name), tower=tower, **kw)
+    a = CTREngine(spec, max_batch=1024, seed=5, adam="lazy", fwd_scatter=True)
+    b = CTREngine(spec, max_batch=1024, seed=5, adam="lazy", fwd_scatter=False)
+    assert a.fwd_scatter and not b.fwd_scatter
+    same = np.testing.assert_array_equal
+    for i, bt in enumerate(_hot(_batches(name, kw, 1024, 4, seed=21))):
+        a.train_step(bt, graph=i >= 1)
+        b.train_step(bt, graph=i >= 1)
+        torch.cuda.synchronize()
+        same(a.z[:1024].cpu().numpy(), b.z[:1024].cpu().numpy(), err_msg="logits step %d" % i)
+        xa, xb = (a.x0b, b.x0b) if a.x0_direct else (a.x0, b.x0)
+        same(xa[:1024].float().cpu().numpy(), xb[:1024].float().cpu().numpy(), err_msg="x0 step %d" % i)
+        if spec.fm:
+            same(a.fm_out[:1024].cpu().numpy(), b.fm_out[:1024].cpu().numpy(), err_msg="fm_out step %d" % i)
+    pa, pb = a.params(), b.params()
+    for k in pa:
+        same(pa[k], pb[k], err_msg=k)
+    # predict (lag 0, no stash) through both forms
+    same(a.predict(bt), b.predict(bt))
