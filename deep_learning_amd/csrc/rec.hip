@@ -459,7 +459,10 @@ __device__ __forceinline__ void rec_bwd_apply(const SegGrad4& s, int64_t row, in
 // Pass 1: every unique row but the hot ones (more than kSegLong references: pass 2), E/4
 // lanes per row.  STASH (the gather's moment stash is given, the engine's default): the
 // catch-up path and its alpha window are compiled out — 96 -> fewer VGPRs, no LDS window.
-template <int E, bool STASH>
+// MULTI (multi-hot references present, C3): the pooled slot of a position from an LDS table,
+// and each row's references fetched four at a time (their loads in flight together: a
+// multi-hot row has ~2-3 references, each a dependent refs -> g_pool round trip); same sums.
+template <int E, bool STASH, bool MULTI = false>
 #ifndef DL_BWD_MIN_WAVES
 #define DL_BWD_MIN_WAVES 1
 #endif
@@ -469,6 +472,8 @@ template <int E, bool STASH>
 __global__ __launch_bounds__(256, STASH ? DL_BWD_MIN_WAVES : 1) void rec_bwd_adam_kernel(DL_REC_BWD_PARAMS) {
   if (step_poisoned(opt)) return;   // the batch failed validation: no update (common.h)
   rec_load_hyper(c, opt);
+  __shared__ unsigned char slot_lut[MULTI ? kSlotLutMax : 1];
+  if (MULTI) build_slot_lut(sg, slot_lut, sg.L.multi_width);
   __shared__ float hw[STASH ? 1 : kHistWin];
   RingW ring{hw, hist, c.hist_mask, (int)opt[7]};
   if (!STASH) ring = load_hist_window(hw, hist, (int)opt[7], c);
@@ -513,7 +518,8 @@ __global__ __launch_bounds__(256, STASH ? DL_BWD_MIN_WAVES : 1) void rec_bwd_ada
     float w = 0.f, wm = 0.f, wv = 0.f;
     rec_bwd_state<E, STASH>(row, n_rep + u, q, first, row_ok, rec, rows_u, rows_u1, mv, c, t, ring, p, m, v, w, wm,
                             wv);
-    const SegGrad4 s = segment_grad4_range<E>(sg, cr.e0, cr.e1, kc, q, nrefs, wsec);
+    const SegGrad4 s = MULTI ? segment_grad4_range_pf<E>(sg, cr.e0, cr.e1, kc, q, nrefs, wsec)
+                             : segment_grad4_range<E>(sg, cr.e0, cr.e1, kc, q, nrefs, wsec);
     if (!row_ok) continue;
     rec_bwd_apply<E>(s, row, q, first, p, m, v, w, wm, wv, rec, c, L, n_rep, g_rep, g1_rep, alpha, t);
   }
@@ -524,6 +530,8 @@ template <int E>
 __global__ __launch_bounds__(256) void rec_bwd_long_kernel(DL_REC_BWD_PARAMS) {
   if (step_poisoned(opt)) return;
   rec_load_hyper(c, opt);
+  __shared__ unsigned char slot_lut[kSlotLutMax];
+  build_slot_lut(sg, slot_lut, sg.L.multi_width);
   __shared__ float hw[kHistWin];
   const RingW ring = load_hist_window(hw, hist, (int)opt[7], c);
   __shared__ SegLongLds sh;
@@ -914,7 +922,8 @@ extern "C" int dl_rec_bwd_adam(const dl_emb_layout* L, float* rec, int32_t rec_l
 #ifdef DL_BWD_GRID_CAP
     if (grid > DL_BWD_GRID_CAP) grid = DL_BWD_GRID_CAP;
 #endif
-    auto bwd = (DL_BWD_STASH_SPECIAL && mv_u) ? rec_bwd_adam_kernel<kE, true> : rec_bwd_adam_kernel<kE, false>;
+    auto bwd = (DL_BWD_STASH_SPECIAL && mv_u) ? (multi ? rec_bwd_adam_kernel<kE, true, true> : rec_bwd_adam_kernel<kE, true>)
+                                              : rec_bwd_adam_kernel<kE, false>;
     hipLaunchKernelGGL(bwd, dim3(grid), dim3(256), 0, as_stream(stream), sg, rec,
                        make_rec_cfg(kE, rec_ld, rec_flags, (mv_u ? 2 : hist_len)), n_rep, rows_u,
                        has_first ? rows_u1 : nullptr, mv_u, uniq_keys, n_uniq, world, g_rep,

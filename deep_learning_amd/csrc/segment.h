@@ -31,7 +31,31 @@ struct SegGradIn {
   // opt's status word: an index entry out of range (a corrupt batch index) sets
   // DL_STATUS_INDEX there and the host raises, instead of the entry being skipped silently
   int* status;
+  // optional: the pooled slot of every multi-hot position (slot_lut[l], n_slots = none), an LDS
+  // table built by the kernel in place of the per-reference search over the slot ranges
+  const unsigned char* slot_lut;
 };
+
+// The pooled slot of multi-hot position l (n_slots when l lies in no slot).
+__device__ __forceinline__ int seg_slot_of(const SegGradIn& a, int l) {
+  if (a.slot_lut) return a.slot_lut[l];
+  int m = 0;
+  while (m < a.n_slots && !(l >= a.slot_start[m] && l < a.slot_end[m])) ++m;
+  return m;
+}
+
+// Fills an LDS slot table for positions [0, width) (every thread of the block calls it).
+constexpr int kSlotLutMax = 2048;
+__device__ __forceinline__ void build_slot_lut(SegGradIn& a, unsigned char* lut, int width) {
+  if (a.n_slots <= 0 || width <= 0 || width > kSlotLutMax || a.n_slots > 255) return;
+  for (int l = threadIdx.x; l < width; l += blockDim.x) {
+    int m = 0;
+    while (m < a.n_slots && !(l >= a.slot_start[m] && l < a.slot_end[m])) ++m;
+    lut[l] = (unsigned char)m;
+  }
+  __syncthreads();
+  a.slot_lut = lut;
+}
 
 __device__ __forceinline__ void index_fault(int* status) {
   if (status) raise_fault(status, DL_STATUS_INDEX);
@@ -120,9 +144,7 @@ __device__ __forceinline__ SegGrad4 segment_grad4_range(const SegGradIn& a, int 
     const int b = k / ns, sl = k % ns;
     if (sl >= mb) {
       // pooled slot m of multi position l: every member row gets the slot's gradient
-      const int l = sl - mb;
-      int m = 0;
-      while (m < a.n_slots && !(l >= a.slot_start[m] && l < a.slot_end[m])) ++m;
+      const int m = seg_slot_of(a, sl - mb);
       if (m == a.n_slots) continue;
       const long long bm = (long long)b * a.n_slots + m;
       const float4 gp = *reinterpret_cast<const float4*>(a.g_pool + bm * E + 4 * q);
@@ -167,9 +189,7 @@ __device__ __forceinline__ SegRef seg_fetch(const SegGradIn& a, bool in, int k, 
   }
   const int b = k / ns, sl = k % ns;
   if (sl >= mb) {
-    const int l = sl - mb;
-    int m = 0;
-    while (m < a.n_slots && !(l >= a.slot_start[m] && l < a.slot_end[m])) ++m;
+    const int m = seg_slot_of(a, sl - mb);
     if (m == a.n_slots) return f;
     const long long bm = (long long)b * a.n_slots + m;
     f.kind = 1;
@@ -199,6 +219,31 @@ __device__ __forceinline__ void seg_acc(SegGrad4& r, const SegRef& f, float4 wse
     r.dsum.x += ds.x; r.dsum.y += ds.y; r.dsum.z += ds.z; r.dsum.w += ds.w;
     r.g1 = fmaf(f.dzb, f.w, r.g1);
   }
+}
+
+// segment_grad4_range with four references' loads in flight at a time (same sums, same
+// order): k_first = refs[e0] already loaded by the caller, or -2
+template <int E>
+__device__ __forceinline__ SegGrad4 segment_grad4_range_pf(const SegGradIn& a, int e0, int e1, int k_first, int q,
+                                                           long long nrefs, float4 wsec) {
+  const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
+  SegGrad4 r{z, z, z, 0.f};
+  const bool g1pool = a.g1_pool != nullptr;
+  for (int e = e0; e < e1; e += 4) {
+    int k[4];
+    bool in[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      in[i] = e + i < e1;
+      k[i] = !in[i] ? -1 : (e + i == e0 && k_first != -2) ? k_first : a.refs[e + i];
+    }
+    SegRef f[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) f[i] = seg_fetch<E>(a, in[i], k[i], q, nrefs);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) seg_acc(r, f[i], wsec, g1pool);
+  }
+  return r;
 }
 
 // segment_grad4_range over e0, e0 + stride, ... < e1 with four references' loads in flight
