@@ -214,7 +214,8 @@ __global__ __launch_bounds__(256) void adam_rows1_kernel(float* __restrict__ p, 
         if (clear) reinterpret_cast<uchar4*>(touched)[i] = make_uchar4(0, 0, 0, 0);
       }
       if (skip) continue;
-      if (l2 != 0.f) { gi.x += l2 * pi.x; gi.y += l2 * pi.y; gi.z += l2 * pi.z; gi.w += l2 * pi.w; }
+      // the L2 term as one fma (wide.hip's lazy replay uses the same expression: bit-identical)
+      if (l2 != 0.f) { gi.x = fmaf(l2, pi.x, gi.x); gi.y = fmaf(l2, pi.y, gi.y); gi.z = fmaf(l2, pi.z, gi.z); gi.w = fmaf(l2, pi.w, gi.w); }
       sq += pi.x * pi.x + pi.y * pi.y + pi.z * pi.z + pi.w * pi.w;
       table_adam<SPARSE>(pi.x, mi.x, vi.x, gi.x, alpha, b1, b2, omb1, omb2, eps);
       table_adam<SPARSE>(pi.y, mi.y, vi.y, gi.y, alpha, b1, b2, omb1, omb2, eps);
@@ -237,7 +238,7 @@ __global__ __launch_bounds__(256) void adam_rows1_kernel(float* __restrict__ p, 
         }
         if (skip) continue;
         float pi = p[r], mi = m[r], vi = v[r];
-        if (l2 != 0.f) gi += l2 * pi;
+        if (l2 != 0.f) gi = fmaf(l2, pi, gi);
         sq += pi * pi;
         table_adam<SPARSE>(pi, mi, vi, gi, alpha, b1, b2, omb1, omb2, eps);
         p[r] = pi; m[r] = mi; v[r] = vi;

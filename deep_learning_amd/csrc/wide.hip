@@ -1,0 +1,228 @@
+// Lazy-exact TF1 Adam for Wide&Deep's wide weights (models/wdl.py:241-285).
+//
+// wdl_weights [N + H, 1] carries an L2 penalty on every row (wdl.py:270-271), so TF's
+// gradient is dense: each step every row r gets g_r = (batch term) + l2 * w_r and every row's
+// w, m, v move — a 26 M-row sweep of p, m, v per step (the dense form, dl_adam_rows).  Here a
+// row the batch does not reference is left alone and its skipped steps are replayed when it is
+// next read: for each skipped step j, g = l2 * w (the dense sweep's gradient of an untouched
+// row), then the same adam_elem — bit-identical to the sweep, only computed later.
+//
+// Record per row: float4 {w, m, v, stamp} (stamp = int32 bits of the last step applied).
+// One step (single GPU, the batch's wide ids indexed by dl_index_build):
+//   dl_wide_rec_gather   unique wide rows + the H deep-output rows caught up to t - lag, into
+//                        the head's compact local table wloc = [— (Fw) | deep rows Fw..Fw+H |
+//                        unique wide rows]; the unique rows' caught-up state stashed
+//   (dl_wdl_head_fwd_bwd on local ids: int64 fixed-point gradients per local row in gloc)
+//   dl_wide_rec_update   the TF1 Adam step t of every touched row (the batch's unique wide rows
+//                        and the H deep-output rows; a row that is both gets both gradient
+//                        parts summed exactly in fixed point first), written with stamp t; the
+//                        L2 loss term of these rows (pre-update w^2) into sq_out
+//   dl_wide_rec_flush    every row caught up to step t (the flush schedule, exports); the L2
+//                        loss term of the rows the last step did not touch comes with it
+#include "common.h"
+
+namespace dl {
+
+struct WideHyper {
+  float b1, b2, omb1, omb2, eps, l2;
+  int mask;
+};
+
+__device__ __forceinline__ WideHyper wide_hyper(const float* opt, float l2, int hist_len) {
+  return WideHyper{opt[4], opt[5], 1.f - opt[4], 1.f - opt[5], opt[6], l2, hist_len - 1};
+}
+
+// the dense sweep's gradient of a row: batch term + l2 * w (adam_rows1_kernel, the same fma)
+__device__ __forceinline__ float wide_l2_grad(float g, float l2, float w) { return fmaf(l2, w, g); }
+
+// steps from+1 .. to with a zero batch term (rows the batch did not touch)
+__device__ __forceinline__ void wide_catch_up(float& w, float& m, float& v, int from, int to, const float* __restrict__ hist,
+                                              const WideHyper& h) {
+  for (int j = from + 1; j <= to; ++j)
+    adam_elem(w, m, v, wide_l2_grad(0.f, h.l2, w), hist[j & h.mask], h.omb1, h.omb2, h.eps);
+}
+
+__device__ __forceinline__ int wide_from(float stamp_bits, int target, int hist_len, int* status) {
+  const int st = __float_as_int(stamp_bits);
+  if (target - st >= hist_len - 1) {   // lagged past the alpha ring: report, never truncate silently
+    raise_fault(status, DL_STATUS_LAG);
+    return target;
+  }
+  return st;
+}
+
+// Unique wide rows u < n_uniq (rows uniq[u]) and the H deep-output rows Fw + j, caught up to
+// step opt[7] - lag: wloc[Fw + j] / wloc[Fw + H + u] = w; stash[u] = (w, m, v, row bits).
+__global__ __launch_bounds__(256) void wide_rec_gather_kernel(const float4* __restrict__ rec, long long w_rows,
+                                                              const uint32_t* __restrict__ uniq,
+                                                              const int32_t* __restrict__ n_uniq, long long max_u,
+                                                              int Fw, int H, const float* __restrict__ hist,
+                                                              int hist_len, const float* __restrict__ opt, float l2,
+                                                              int lag, float* __restrict__ wloc,
+                                                              float4* __restrict__ stash) {
+  const WideHyper h = wide_hyper(opt, l2, hist_len);
+  int* status = opt_status(opt);
+  const int target = (int)opt[7] - lag;
+  const long long nu = n_uniq ? (long long)min((long long)max(n_uniq[0], 0), max_u) : max_u;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < H + nu;
+       i += (long long)gridDim.x * blockDim.x) {
+    const long long row = i < H ? Fw + i : (long long)uniq[i - H];
+    if (row < 0 || row >= w_rows) {
+      raise_fault(status, DL_STATUS_INDEX);
+      continue;
+    }
+    float4 r = rec[row];
+    const int from = wide_from(r.w, target, hist_len, status);
+    if (from < target) wide_catch_up(r.x, r.y, r.z, from, target, hist, h);
+    wloc[Fw + i] = r.x;   // i < H: the deep-output row Fw + i; else local row Fw + H + u
+    if (i >= H && stash) stash[i - H] = make_float4(r.x, r.y, r.z, __int_as_float((int)row));
+  }
+}
+
+// Pass A: the batch's unique wide rows.  g = (its wide terms + its deep-output term when the row
+// is one of Fw..Fw+H: exact int64 sum) + l2 * w, TF1 Adam step t from the stashed caught-up
+// state, record written with stamp t.  Deep-output rows it covered are marked for pass B.
+__global__ __launch_bounds__(256) void wide_rec_update_kernel(float4* __restrict__ rec, const int32_t* __restrict__ n_uniq,
+                                                              long long max_u, const float4* __restrict__ stash,
+                                                              long long* __restrict__ gloc, int Fw, int H, float l2,
+                                                              int hist_len, const float* __restrict__ opt,
+                                                              uint8_t* __restrict__ dmark, float* __restrict__ sq_out) {
+  const WideHyper h = wide_hyper(opt, l2, hist_len);
+  const bool skip = step_poisoned(opt);
+  const int t = (int)opt[7];
+  const float alpha = opt[3];
+  const long long nu = (long long)min((long long)max(n_uniq[0], 0), max_u);
+  float sq = 0.f;
+  for (long long u = (long long)blockIdx.x * blockDim.x + threadIdx.x; u < nu; u += (long long)gridDim.x * blockDim.x) {
+    const float4 s = stash[u];
+    const long long row = (long long)__float_as_int(s.w);
+    long long q = gloc[Fw + H + u];
+    gloc[Fw + H + u] = 0;
+    const bool deep = row >= Fw && row < Fw + H;
+    if (deep) {
+      q += gloc[row];   // the deep-output term of the same row (pass B resets it)
+      dmark[row - Fw] = 1;
+    }
+    if (skip) continue;
+    float w = s.x, m = s.y, v = s.z;
+    sq += w * w;
+    adam_elem(w, m, v, wide_l2_grad(wide_float(q), h.l2, w), alpha, h.omb1, h.omb2, h.eps);
+    rec[row] = make_float4(w, m, v, __int_as_float(t));
+  }
+  if (sq_out) {
+    sq = wave_sum(sq);
+    if ((threadIdx.x & 63) == 0 && sq != 0.f) atomicAdd(sq_out, sq);
+  }
+}
+
+// Pass B: the H deep-output rows pass A did not cover (their gradient: the deep term alone).
+__global__ __launch_bounds__(256) void wide_rec_update_deep_kernel(float4* __restrict__ rec, long long* __restrict__ gloc,
+                                                                   int Fw, int H, float l2, const float* __restrict__ hist,
+                                                                   int hist_len, const float* __restrict__ opt,
+                                                                   uint8_t* __restrict__ dmark,
+                                                                   float* __restrict__ sq_out) {
+  const WideHyper h = wide_hyper(opt, l2, hist_len);
+  const bool skip = step_poisoned(opt);
+  const int t = (int)opt[7];
+  const float alpha = opt[3];
+  float sq = 0.f;
+  for (int j = blockIdx.x * blockDim.x + threadIdx.x; j < H; j += gridDim.x * blockDim.x) {
+    const long long row = Fw + j;
+    const long long q = gloc[row];
+    gloc[row] = 0;
+    if (dmark[j]) {   // updated in pass A with the batch's wide terms
+      dmark[j] = 0;
+      continue;
+    }
+    if (skip) continue;
+    float4 r = rec[row];
+    const int from = wide_from(r.w, t - 1, hist_len, opt_status(opt));
+    if (from < t - 1) wide_catch_up(r.x, r.y, r.z, from, t - 1, hist, h);
+    sq += r.x * r.x;
+    adam_elem(r.x, r.y, r.z, wide_l2_grad(wide_float(q), h.l2, r.x), alpha, h.omb1, h.omb2, h.eps);
+    rec[row] = make_float4(r.x, r.y, r.z, __int_as_float(t));
+  }
+  if (sq_out) {
+    sq = wave_sum(sq);
+    if ((threadIdx.x & 63) == 0 && sq != 0.f) atomicAdd(sq_out, sq);
+  }
+}
+
+// Every row caught up to step opt[7].  Rows the last step did not touch (stamp < t) pass
+// through their step t - 1 state on the way: its w^2 — the L2 loss term of step t's pre-update
+// weights for those rows — is summed into sq_untouched.
+__global__ __launch_bounds__(256) void wide_rec_flush_kernel(float4* __restrict__ rec, long long w_rows, float l2,
+                                                             const float* __restrict__ hist, int hist_len,
+                                                             const float* __restrict__ opt,
+                                                             float* __restrict__ sq_untouched) {
+  const WideHyper h = wide_hyper(opt, l2, hist_len);
+  const int t = (int)opt[7];
+  float sq = 0.f;
+  for (long long row = (long long)blockIdx.x * blockDim.x + threadIdx.x; row < w_rows;
+       row += (long long)gridDim.x * blockDim.x) {
+    float4 r = rec[row];
+    const int from = wide_from(r.w, t, hist_len, opt_status(opt));
+    if (from >= t) continue;
+    if (from < t - 1) wide_catch_up(r.x, r.y, r.z, from, t - 1, hist, h);
+    sq += r.x * r.x;
+    wide_catch_up(r.x, r.y, r.z, t - 1, t, hist, h);
+    rec[row] = make_float4(r.x, r.y, r.z, __int_as_float(t));
+  }
+  if (sq_untouched) {
+    sq = wave_sum(sq);
+    if ((threadIdx.x & 63) == 0 && sq != 0.f) atomicAdd(sq_untouched, sq);
+  }
+}
+
+static unsigned wide_grid(long long n) {
+  long long b = (n + 255) / 256;
+  if (b > 8192) b = 8192;
+  return (unsigned)(b < 1 ? 1 : b);
+}
+
+}  // namespace dl
+
+using namespace dl;
+
+extern "C" int dl_wide_rec_gather(const float* rec, int64_t w_rows, const uint32_t* uniq_rows, const int32_t* n_uniq,
+                                  int64_t max_uniq, int32_t Fw, int32_t H, const float* hist, int32_t hist_len,
+                                  const float* opt, float l2, int32_t lag, float* wloc, float* stash, void* stream) {
+  DL_CHECK_ARG(rec && hist && opt && wloc && (max_uniq == 0 || uniq_rows), "NULL argument");
+  DL_CHECK_ARG(hist_len >= 2 && (hist_len & (hist_len - 1)) == 0, "hist_len must be a power of two");
+  DL_CHECK_ARG(Fw >= 0 && H >= 0 && (long long)Fw + H <= w_rows, "bad Fw / H");
+  DL_CHECK_ARG(((uintptr_t)rec % 16) == 0 && ((uintptr_t)stash % 16) == 0, "rec / stash must be 16-B aligned");
+  const long long n = H + (max_uniq > 0 ? max_uniq : 0);
+  if (n == 0) return 0;
+  hipLaunchKernelGGL(wide_rec_gather_kernel, dim3(wide_grid(n)), dim3(256), 0, as_stream(stream),
+                     reinterpret_cast<const float4*>(rec), (long long)w_rows, uniq_rows, n_uniq, (long long)max_uniq,
+                     Fw, H, hist, hist_len, opt, l2, lag, wloc, reinterpret_cast<float4*>(stash));
+  DL_RETURN_LAUNCH("dl_wide_rec_gather");
+}
+
+extern "C" int dl_wide_rec_update(float* rec, const int32_t* n_uniq, int64_t max_uniq, const float* stash, int64_t* gloc,
+                                  int32_t Fw, int32_t H, float l2, const float* hist, int32_t hist_len,
+                                  const float* opt, uint8_t* dmark, float* sq_out, void* stream) {
+  DL_CHECK_ARG(rec && n_uniq && stash && gloc && hist && opt && dmark, "NULL argument");
+  DL_CHECK_ARG(hist_len >= 2 && (hist_len & (hist_len - 1)) == 0, "hist_len must be a power of two");
+  DL_CHECK_ARG(Fw >= 0 && H >= 0, "bad Fw / H");
+  hipStream_t s = as_stream(stream);
+  if (max_uniq > 0)
+    hipLaunchKernelGGL(wide_rec_update_kernel, dim3(wide_grid(max_uniq)), dim3(256), 0, s,
+                       reinterpret_cast<float4*>(rec), n_uniq, (long long)max_uniq,
+                       reinterpret_cast<const float4*>(stash), reinterpret_cast<long long*>(gloc), Fw, H, l2, hist_len,
+                       opt, dmark, sq_out);
+  if (H > 0)
+    hipLaunchKernelGGL(wide_rec_update_deep_kernel, dim3(wide_grid(H)), dim3(256), 0, s, reinterpret_cast<float4*>(rec),
+                       reinterpret_cast<long long*>(gloc), Fw, H, l2, hist, hist_len, opt, dmark, sq_out);
+  DL_RETURN_LAUNCH("dl_wide_rec_update");
+}
+
+extern "C" int dl_wide_rec_flush(float* rec, int64_t w_rows, float l2, const float* hist, int32_t hist_len,
+                                 const float* opt, float* sq_untouched, void* stream) {
+  DL_CHECK_ARG(rec && hist && opt, "NULL argument");
+  DL_CHECK_ARG(hist_len >= 2 && (hist_len & (hist_len - 1)) == 0, "hist_len must be a power of two");
+  if (w_rows <= 0) return 0;
+  hipLaunchKernelGGL(wide_rec_flush_kernel, dim3(wide_grid(w_rows)), dim3(256), 0, as_stream(stream),
+                     reinterpret_cast<float4*>(rec), (long long)w_rows, l2, hist, hist_len, opt, sq_untouched);
+  DL_RETURN_LAUNCH("dl_wide_rec_flush");
+}

@@ -293,6 +293,39 @@ class CTREngine:
             self.wg = z(wr, dt=torch.int64)
             self.w_touched = z(wr, dt=torch.uint8)
             self.wb, self.wbm, self.wbv = z(4), z(4), z(4)
+        # wide_lazy (single-GPU wdl with lazy tables): wdl_weights as {w, m, v, stamp} records
+        # with lazy-exact Adam (wide.hip): the batch's unique wide ids indexed, gathered caught
+        # up into the head's compact local table [— (Fw) | deep-output rows | unique rows], and
+        # only those rows (and the H deep-output rows) updated — in place of the dense L2 sweep
+        # over all N + H rows (wdl.py:270-271); bit-identical to it.  DLAMD_WIDE_LAZY=0: dense.
+        self.wide_lazy = bool(self.wdl and self.lazy and type(self) is CTREngine
+                              and os.environ.get("DLAMD_WIDE_LAZY", "1") != "0")
+        if self.wide_lazy:
+            Fw, Hh, Bm = sp.Fw, sp.hidden[-1], max_batch
+            nw = Bm * Fw
+            self.wrec = z(_ru(self.w_rows, 16), 4)
+            self.wloc = z(_ru(Fw + Hh + nw, 4))
+            self.wgloc = z(Fw + Hh + nw, dt=torch.int64)
+            self.wstash = z(max(nw, 1), 4)
+            self.wdmark = z(_ru(Hh, 16), dt=torch.uint8)
+            self.wsq = z(4)                      # L2 term of the rows the last step left (from a flush)
+            self._wsq_step = -1
+            self.in_wide_loc = z(Bm, Fw, dt=torch.int64)
+            wsb = _lib.lib().dl_index_workspace_bytes(max(1, nw))
+            self.widx_ws = z(wsb, dt=torch.uint8)
+            self.widx_keys, self.widx_refs, self.widx_uniq = (z(max(nw, 1), dt=torch.int32) for _ in range(3))
+            self.widx_off = z(nw + 1, dt=torch.int32)
+            self.widx_n = z(4, dt=torch.int32)
+            self.winv = z(max(nw, 1), dt=torch.int32)
+            WL = _lib.EmbLayout()
+            WL.n_rows = self.w_rows
+            WL.batch = Bm
+            WL.emb_dim = sp.E
+            WL.cate_fields = Fw
+            WL.cate_ld = max(Fw, 1)
+            WL.use_fm = 0
+            WL.zero_row0 = 0
+            self.wlayout = WL
         self.err = z(4, dt=torch.int32)       # the batch's id-validation word (per buffer set)
         # table update form (TF: ApplyAdam, or the sparse-apply form for direct lookups)
         self.rec_flags = (_lib.REC_FIRST if sp.fm else 0) | (_lib.REC_SPARSE_ADAM if sp.sparse_table else 0)
@@ -470,6 +503,8 @@ class CTREngine:
         w[:-1] = rng.standard_normal(self.head_n - 1) * g
         w[-1] = rng.standard_normal()
         self.w_head[: self.head_n].copy_(torch.from_numpy(w))
+        if getattr(self, "wide_lazy", False):
+            self._wide_pack()
         torch.cuda.synchronize()
 
     def _set_layer(self, l, W, b, ref_order=True):
@@ -520,6 +555,10 @@ class CTREngine:
             self.ww[: self.w_rows].copy_(torch.from_numpy(np.ascontiguousarray(P["wdl_weights"][:, 0], np.float32)))
             self.wb.zero_()
             self.wb[:1].copy_(torch.from_numpy(np.asarray(P["wdl_bias"], np.float32).reshape(-1)))
+            if self.wide_lazy:
+                self.wm.zero_()
+                self.wv.zero_()
+                self._wide_pack()
             torch.cuda.synchronize()
             return
         if sp.fm:
@@ -545,15 +584,46 @@ class CTREngine:
             P = {sp.table_key: self.table[:N].cpu().numpy()}
             if self.first is not None:
                 P[sp.first_key] = self.first[:N].cpu().numpy()[:, None]
-        P.update(self._export_dense(self.W, self.w_head, getattr(self, "ww", None), getattr(self, "wb", None)))
+        P.update(self._export_dense(self.W, self.w_head, self._wide_state()[0], getattr(self, "wb", None)))
         return P
 
     def dense_state(self):
         """Adam moments of the dense parameters (hidden layers, head / wdl weights) in the
         reference layout: {"m": {key: array}, "v": {key: array}} (tests; the table's are in
         adam_state())."""
-        return {"m": self._export_dense(self.Wm, self.hm, getattr(self, "wm", None), getattr(self, "wbm", None)),
-                "v": self._export_dense(self.Wv, self.hv, getattr(self, "wv", None), getattr(self, "wbv", None))}
+        _, wm, wv = self._wide_state()
+        return {"m": self._export_dense(self.Wm, self.hm, wm, getattr(self, "wbm", None)),
+                "v": self._export_dense(self.Wv, self.hv, wv, getattr(self, "wbv", None))}
+
+    # ------------------------------------------------------------------ wide records (wdl)
+    def _wide_pack(self):
+        """Dense wdl_weights (+ moments) -> records {w, m, v, stamp = current step}."""
+        n = self.ww.shape[0]
+        self.wrec.zero_()
+        self.wrec[:n, 0].copy_(self.ww)
+        self.wrec[:n, 1].copy_(self.wm)
+        self.wrec[:n, 2].copy_(self.wv)
+        self.wrec.view(torch.int32)[:, 3] = int(self.opt[7].item())
+        self._wsq_step = -1
+
+    def _wide_state(self):
+        """(w, m, v) of wdl_weights as device tensors (records: caught up first), or Nones."""
+        if not getattr(self, "wdl", False):
+            return None, None, None
+        if not self.wide_lazy:
+            return self.ww, self.wm, self.wv
+        self._wide_flush()
+        return self.wrec[:, 0], self.wrec[:, 1], self.wrec[:, 2]
+
+    def _wide_flush(self):
+        """Every wide record caught up to the current step; the L2 term of the rows the last
+        step did not touch (their pre-update w^2) is left in wsq for loss()."""
+        if self._wsq_step == self.steps:
+            return
+        self.wsq.zero_()
+        call("dl_wide_rec_flush", ptr(self.wrec), self.w_rows, self.spec.l2, ptr(self.hist), self.hist_len,
+             ptr(self.opt), ptr(self.wsq), _lib.stream_handle())
+        self._wsq_step = self.steps
 
     def _export_dense(self, Ws, head, ww, wb):
         """Augmented hidden-layer matrices (bias row, x0 column order), the permuted head
@@ -603,6 +673,8 @@ class CTREngine:
             return
         self._c("rec_flush", "dl_rec_flush", ptr(self.rec), self.rec_ld, self.spec.E, self.rec_flags,
                 self.rec.shape[0], ptr(self.hist), self.hist_len, ptr(self.opt), _lib.stream_handle())
+        if getattr(self, "wide_lazy", False):
+            self._wide_flush()
         self.since_flush = 0
 
     def adam_state(self):
@@ -755,6 +827,18 @@ class CTREngine:
                         ptr(self.W[l]), self.out_ld[l], ptr(self.h[l]), self.h_ld[l], 1, None, 0, 1, 0, s)
                 x = self.h[l]
         H = sp.hidden[-1]
+        if self.wdl and self.wide_lazy:
+            # the batch's wide rows caught up into the compact local table, the head on local ids
+            fn, dh_last = ("dl_wdl_head_fwd_bwd_bf16", self.dhb[-1]) if self.bf else ("dl_wdl_head_fwd_bwd", self.dh[-1])
+            nw = B * sp.Fw
+            self._c("wide_gather", "dl_wide_rec_gather", ptr(self.wrec), self.w_rows, ptr(self.widx_uniq),
+                    ptr(self.widx_n), nw, sp.Fw, H, ptr(self.hist), self.hist_len, ptr(self.opt), sp.l2,
+                    1 if train else 0, ptr(self.wloc), ptr(self.wstash) if train else None, s)
+            self._c("head", fn, B, sp.Fw, H, ptr(self.in_wide_loc), sp.Fw, ptr(self.h[-1]), self.h_ld[-1],
+                    ptr(self.wloc), ptr(self.wb), sp.Fw + H + nw, ptr(self.in_label), sp.logloss_eps, 1.0 / B,
+                    ptr(self.score), ptr(self.z), ptr(self.dz), ptr(dh_last), ptr(self.wgloc) if train else None, None,
+                    ptr(self.head_slab), self.head_blocks, ptr(self.err), s)
+            return
         if self.wdl:
             # bf16 tower: dY of the last layer written as bf16 by the head itself (no cast pass)
             fn, dh_last = ("dl_wdl_head_fwd_bwd_bf16", self.dhb[-1]) if self.bf else ("dl_wdl_head_fwd_bwd", self.dh[-1])
@@ -792,6 +876,15 @@ class CTREngine:
                 self.idx_ws.numel(), ptr(self.idx_keys), ptr(self.idx_refs), ptr(self.idx_uniq),
                 ptr(self.idx_off), ptr(self.idx_n), ptr(self.idx_inv) if self.lazy else None, None,
                 ptr(self.err), s)
+        if getattr(self, "wide_lazy", False):
+            # the wide ids' index (unique wdl_weights rows, inverse map) and the head's local ids
+            WL = self.wlayout
+            WL.batch = B
+            Fw, H = sp.Fw, sp.hidden[-1]
+            self._c("index_build_wide", "dl_index_build", C_ref(WL), ptr(self.in_wide), 1, 0, ptr(self.widx_ws),
+                    self.widx_ws.numel(), ptr(self.widx_keys), ptr(self.widx_refs), ptr(self.widx_uniq),
+                    ptr(self.widx_off), ptr(self.widx_n), ptr(self.winv), None, ptr(self.err), s)
+            call("dl_wide_local_ids", ptr(self.winv), B * Fw, Fw + H, ptr(self.in_wide_loc), s)
 
     def _train(self, B):
         sp = self.spec
@@ -897,6 +990,18 @@ class CTREngine:
                  ptr(self.touched), s)
         H = sp.hidden[-1]
         hb = call_int(self.head_grid, B)
+        if self.wdl and self.wide_lazy:
+            # wdl_weights, lazy: the deep-output rows' batch sums folded into the local gradient,
+            # then TF1 Adam (L2 on every row, wdl.py:270-271) on the batch's unique wide rows and
+            # the deep-output rows only; the untouched rows' L2 steps are replayed when read
+            self._c("wdl_fold", "dl_slab_fold_rows", ptr(self.head_slab), hb, H + 2, 0, H, ptr(self.wgloc), sp.Fw,
+                    None, s)
+            self._c("adam_bias", "dl_adam_dense", ptr(self.wb), ptr(self.wbm), ptr(self.wbv),
+                    ptr(self.head_slab[:, H:]), hb, H + 2, 1, 0.0, 0, ptr(self.opt), None, None, s)
+            self._c("adam_wide", "dl_wide_rec_update", ptr(self.wrec), ptr(self.widx_n), B * sp.Fw, ptr(self.wstash),
+                    ptr(self.wgloc), sp.Fw, H, sp.l2, ptr(self.hist), self.hist_len, ptr(self.opt), ptr(self.wdmark),
+                    ptr(self.opt[8:]), s)
+            return
         if self.wdl:
             # wdl_weights: dense Adam with L2 on every row (wdl.py:270-271); the deep-output
             # rows get their batch sums folded in from the head slab first
@@ -931,7 +1036,8 @@ class CTREngine:
     # buffered — the next batch is staged and indexed into the other set on a side stream
     # while the current step runs.
     SLOT_ATTRS = ("in_label", "in_cont", "in_vec", "in_cate", "in_wide", "idx_ws", "idx_keys", "idx_refs",
-                  "idx_uniq", "idx_off", "idx_n", "idx_inv", "err")
+                  "idx_uniq", "idx_off", "idx_n", "idx_inv", "err", "widx_ws", "widx_keys", "widx_refs", "widx_uniq",
+                  "widx_off", "widx_n", "winv", "in_wide_loc")
 
     def _side_stream(self):
         if getattr(self, "side", None) is None:
@@ -1094,7 +1200,12 @@ class CTREngine:
         data = self.head_slab[:rows, width - 1].double().sum().item() / B
         if sp.hidden_reg == "l1":   # l1_regularizer: scale * sum |W| (dnn.py:88-90)
             return data + sp.l2 * float(self.opt[8].item())
-        return data + sp.l2 * 0.5 * float(self.opt[8].item())
+        reg = float(self.opt[8].item())
+        if getattr(self, "wide_lazy", False):
+            # the wide rows the step left untouched: their L2 term from a flush (wide.hip)
+            self._wide_flush()
+            reg += float(self.wsq[0].item())
+        return data + sp.l2 * 0.5 * reg
 
     # ------------------------------------------------------------------ errors
     def _queue_status(self):

@@ -113,7 +113,9 @@ def test_lazy_adam_bit_identical_to_dense(hip_lib, name, stash):
     (sorted, deterministic) gradients: parameters, Adam moments, logits and
     predictions must be bit-identical.  A large table, a small batch and an 8-entry
     alpha ring make rows lag many steps and force periodic flushes.  (wdl included: its
-    wide-weight gradient is an integer fixed-point segment sum, order-independent.)"""
+    wide-weight gradient is an integer fixed-point segment sum, order-independent, and its
+    wide weights are lazy records too (wide.hip) against the dense L2 sweep — wide ids
+    aliasing the deep-output rows included; the loss's L2 term within 1e-6 relative.)"""
     kw = dict(CASES[name], cate_index_size=50000)
     same = np.testing.assert_array_equal
     model = _model(name)
@@ -122,6 +124,11 @@ def test_lazy_adam_bit_identical_to_dense(hip_lib, name, stash):
     lazy = CTREngine(spec, max_batch=128, seed=3, adam="lazy", hist_len=8, rec_stash=stash)
     np.testing.assert_array_equal(lazy.params()[spec.table_key], dense.params()[spec.table_key])
     bs = _batches(name, kw, 128, 21, seed=7)
+    if "wide_feats" in bs[0]:   # wide ids on the deep-output rows Fw .. Fw+H (wdl.py:225-228 aliasing)
+        Fw, H = kw["Fw"], kw["hidden"][-1]
+        for j, b in enumerate(bs):
+            b["wide_feats"][j % 7, :3] = [Fw + j % H, Fw + H - 1, Fw]
+    assert lazy.wide_lazy == (name == "wdl")
     for i, b in enumerate(bs):
         dense.train_step(b, graph=i >= 3)
         lazy.train_step(b, graph=i >= 3)
@@ -129,12 +136,17 @@ def test_lazy_adam_bit_identical_to_dense(hip_lib, name, stash):
         same(lazy.z[:128].cpu().numpy(), dense.z[:128].cpu().numpy(), err_msg="logits step %d" % i)
         if i == 10:
             same(lazy.predict(bs[0]), dense.predict(bs[0]))
+    np.testing.assert_allclose(lazy.loss(), dense.loss(), rtol=1e-6)
     pd, pl = dense.params(), lazy.params()
     for k in pd:
         same(pl[k], pd[k], err_msg=k)
     sd, sl = dense.adam_state(), lazy.adam_state()
     for k in sd:
         same(sl[k], sd[k], err_msg=k)
+    dd, dl = dense.dense_state(), lazy.dense_state()
+    for mv in ("m", "v"):
+        for k in dd[mv]:
+            same(dl[mv][k], dd[mv][k], err_msg="%s %s" % (mv, k))
 
 
 @pytest.mark.parametrize("name", ["deepfm_pipeline", "dnn_pipeline", "wdl"])
