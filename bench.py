@@ -41,7 +41,8 @@ def log(*a):
     print("[bench %s]" % time.strftime("%H:%M:%S"), *a, file=sys.stderr, flush=True)
 
 
-def kernel_work(spec, B, touched_rows, rows=None, uniq=None, shard=None, wide_rows=None, stash=False):
+def kernel_work(spec, B, touched_rows, rows=None, uniq=None, shard=None, wide_rows=None, stash=False, scatter=False,
+                wide_uniq=None):
     """Algorithmic bytes / flops per launch."""
     E, S, C = spec.E, spec.S, spec.C
     N = rows if rows is not None else spec.n_rows
@@ -70,6 +71,14 @@ def kernel_work(spec, B, touched_rows, rows=None, uniq=None, shard=None, wide_ro
         w["rec_gather"] = ("hbm", uniq * (rec_b + (E + 1) * 4 + 4 + stash_b))
         # indexed x0 assembly: refs/sample x (compact row + inv) + first-order (FM) + x0 cat write
         w["embed_fwd"] = ("hbm", B * (refs * (E * 4 + 4) + (S * 4 if spec.fm else 0) + S * E * xb))
+        if scatter:
+            # scatter form: the gather also writes every reference's row (64 B) and the FM
+            # references' first-order outputs, reading the index's segments and references;
+            # the staged forward reads the FM staging rows and the inverse map in order
+            w["rec_gather"] = ("hbm", uniq * (rec_b + (E + 1) * 4 + 4 + stash_b + 8) + B * refs * (4 + E * 4) +
+                               (B * S * 4 if spec.fm else 0))
+            w["embed_fwd"] = ("hbm", B * ((S * E * 4 + S * 4 + C * 4 + spec.fm_cols * 4 + E * 4) if spec.fm else 0) +
+                              B * refs * 4 + B * C * xb)
         # fused backward + Adam: U records written and read back (stash: the compact row and
         # stashed moments read instead), per ref: ref id + dx0/fm_sum row + dz
         rd_b = ((E + 1) * 4 + stash_b) if stash else rec_b
@@ -99,6 +108,11 @@ def kernel_work(spec, B, touched_rows, rows=None, uniq=None, shard=None, wide_ro
         # wide Adam (L2 on every row: a dense sweep): p, m, v read + written, touched flag read;
         # int64 fixed-point gradient read + reset where touched (at most B * Fw rows)
         w["adam_wide"] = ("hbm", (wide_rows or 0) * (12 * 2 + 1) + B * Fw * 16)
+        if wide_uniq is not None:
+            # lazy wide records: the unique wide rows' stash read, record written, gradient read +
+            # reset; the deep-output rows' records; the wide gather: record read, stash + local w written
+            w["adam_wide"] = ("hbm", wide_uniq * (16 + 16 + 16) + H * 40)
+            w["wide_gather"] = ("hbm", wide_uniq * (4 + 16 + 16 + 4) + H * 20)
     return w
 
 
@@ -286,9 +300,11 @@ def run_workload(wl, args, world, rank, sharded, steps, warmup, age, ksteps, bar
     shard_counts = getattr(eng, "last_counts", None) if sharded and getattr(eng, "lazy", False) else None
     uniq = int(eng.idx_n[0].item()) if getattr(eng, "lazy", False) and not sharded else None
     ww = getattr(eng, "ww", None)
+    wide_uniq = int(eng.widx_n[0].item()) if getattr(eng, "wide_lazy", False) else None
     work = kernel_work(spec, B, touched_rows, rows=getattr(eng, "local_rows", spec.n_rows), uniq=uniq,
                        shard=shard_counts, wide_rows=int(ww.shape[0]) if ww is not None else None,
-                       stash=getattr(eng, "mv_u", None) is not None)
+                       stash=getattr(eng, "mv_u", None) is not None, scatter=getattr(eng, "fwd_scatter", False),
+                       wide_uniq=wide_uniq)
     s3 = getattr(eng, "s3", False)
     # the tower GEMMs' own peak: f32 products as six bf16 plane products (gemm_s3.hip) run at
     # 1/6 of the bf16 MFMA peak; the bf16 tower at the bf16 peak; f32 MFMA otherwise

@@ -523,6 +523,10 @@ struct PoolArgs {
   int32_t* err;
   const float* vals;       // weighted mode: value of multi position l of sample b = vals[b*vals_ld + l]
   int vals_ld;
+  // staged mode (IDX; after dl_rec_gather_scatter with multi-hot staging): the row of multi
+  // position l of sample b is table row b * multi_width + l (written there by the gather),
+  // a position without a row (inv < 0: padding) none
+  int staged;
 };
 
 // One wave per sample.  A slot's positions are resolved 64 at a time, one per lane (ids or
@@ -560,7 +564,7 @@ __global__ __launch_bounds__(256) void pool_fwd_kernel(PoolArgs a) {
         if (lane < nl) {
           if (IDX) {
             const int ri = invb[c0 + lane];
-            src = ri >= 0 ? (long long)a.inv_base + ri : -1;
+            src = ri < 0 ? -1 : a.staged ? (long long)b * L.multi_width + c0 + lane : (long long)a.inv_base + ri;
           } else {
             const int64_t row = checked_row(ids[c0 + lane], 0, L.n_rows, a.err);
             src = row_ok(row, L.zero_row0) ? row : -1;
@@ -859,6 +863,22 @@ extern "C" int dl_pool_fwd_indexed(const dl_emb_layout* L, const float* rows, co
   DL_DISPATCH_E(L->emb_dim, hipLaunchKernelGGL((pool_fwd_kernel<kE, true>), dim3(emb_grid(L->batch)),
                                                dim3(256), 0, as_stream(stream), a));
   DL_RETURN_LAUNCH("dl_pool_fwd_indexed");
+}
+
+extern "C" int dl_pool_fwd_staged(const dl_emb_layout* L, const float* mst, const float* mst1, const int32_t* inv,
+                                  const int32_t* slot_start, const int32_t* slot_end, int32_t n_slots, int32_t fm_col,
+                                  float* x0, float* fm_out, float* cnt_emb, float* cnt_first, void* stream) {
+  if (int rc = check_layout(L)) return rc;
+  DL_CHECK_ARG(mst && inv && x0 && cnt_emb && slot_start && slot_end && n_slots >= 0, "NULL argument");
+  DL_CHECK_ARG(L->multi_width > 0, "staged pooling needs the multi-hot refs in the index (multi_width)");
+  DL_CHECK_ARG(!mst1 || (fm_out && cnt_first), "first-order pooling needs fm_out/cnt_first");
+  if (L->batch == 0 || n_slots == 0) return 0;
+  PoolArgs a{*L, inv, 0, mst, mst1, nullptr, 0, slot_start, slot_end, n_slots, fm_col,
+             x0, fm_out, cnt_emb, cnt_first, nullptr, nullptr, 0};
+  a.staged = 1;
+  DL_DISPATCH_E(L->emb_dim, hipLaunchKernelGGL((pool_fwd_kernel<kE, true>), dim3(emb_grid(L->batch)),
+                                               dim3(256), 0, as_stream(stream), a));
+  DL_RETURN_LAUNCH("dl_pool_fwd_staged");
 }
 
 extern "C" int dl_pool_bwd(const dl_emb_layout* L, const int64_t* ids, int32_t ids_col,

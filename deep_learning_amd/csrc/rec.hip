@@ -115,8 +115,10 @@ struct GatherScatter {
   float* fmst;
   float* x0;
   float* fm_out;
+  float* mst;      // multi-hot staging (may be NULL): position l of sample b -> mst[b*mw + l][E], mst1
+  float* mst1;
   long long nrefs;
-  int ns, S, mb, use_fm, Cf, x0_ld, x0_cat_col, x0_bf16, fm_ld, n_rep;
+  int ns, S, mb, use_fm, Cf, x0_ld, x0_cat_col, x0_bf16, fm_ld, n_rep, mw;
   int* status;
 };
 
@@ -127,7 +129,14 @@ __device__ __forceinline__ void scatter_ref(const GatherScatter& s, int k, int q
     return;
   }
   const int b = k / s.ns, sl = k - b * s.ns;
-  if (sl >= s.mb) return;   // multi-hot: pooled from the compact rows
+  if (sl >= s.mb) {   // multi-hot: into the staging rows the pooling reads per sample (or left)
+    if (s.mst) {
+      const long long o = (long long)b * s.mw + (sl - s.mb);
+      *reinterpret_cast<float4*>(s.mst + o * E + 4 * q) = p;
+      if (s.mst1 && q == 0) s.mst1[o] = w;
+    }
+    return;
+  }
   if (s.use_fm && sl < s.S) {
     *reinterpret_cast<float4*>(s.fmst + ((long long)s.n_rep + (long long)b * s.S + sl) * E + 4 * q) = p;
     if (first && q == 0) s.fm_out[(long long)b * s.fm_ld + s.Cf + sl] = w * 1.f;
@@ -836,7 +845,7 @@ extern "C" int dl_rec_gather_scatter(const dl_emb_layout* L, const float* rec, i
                                      int64_t max_uniq, const int32_t* seg_off, const int32_t* sorted_refs,
                                      const float* hist, int32_t hist_len, const float* opt, int32_t lag,
                                      float* rows_u, float* rows_u1, float* mv_u, float* fmst, void* x0,
-                                     float* fm_out, void* stream) {
+                                     float* fm_out, float* mst, float* mst1, void* stream) {
   const int32_t has_first = rec_flags & DL_REC_FIRST;
   DL_CHECK_ARG(L && rec && hist && opt && rows_u && uniq_keys && n_uniq && seg_off && sorted_refs && x0,
                "NULL argument");
@@ -864,6 +873,9 @@ extern "C" int dl_rec_gather_scatter(const dl_emb_layout* L, const float* rec, i
   sc.x0_bf16 = L->x0_bf16;
   sc.fm_ld = L->fm_ld;
   sc.n_rep = n_rep;
+  sc.mst = L->multi_width > 0 ? mst : nullptr;
+  sc.mst1 = (L->multi_width > 0 && mst && has_first) ? mst1 : nullptr;
+  sc.mw = L->multi_width;
   sc.status = reinterpret_cast<int*>(const_cast<float*>(opt) + DL_OPT_STATUS);
   DL_DISPATCH_E(L->emb_dim, {
     const unsigned grid = grid_cap(total * (kE / 4));

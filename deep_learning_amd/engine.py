@@ -425,6 +425,10 @@ class CTREngine:
             fwd_scatter = os.environ.get("DLAMD_FWD_SCATTER", "1") != "0"
         self.fwd_scatter = bool(fwd_scatter and self.lazy and not self.fwd_rec and type(self) is CTREngine)
         self.fmst = z(self.n_rep + B * S, E) if (self.fwd_scatter and sp.fm) else None
+        # multi-hot staging (scatter form): position l of sample b at row b * multi_width + l
+        mw = sp.multi_width
+        self.mst = z(B * mw, E) if (self.fwd_scatter and M) else None
+        self.mst1 = z(B * mw) if (self.fwd_scatter and M and sp.fm) else None
         # static input slots (graph capture reads from these)
         self.in_label = z(B)
         self.in_cont = z(B, max(sp.C, 1))
@@ -770,12 +774,11 @@ class CTREngine:
                     self.n_rep, ptr(self.idx_uniq), ptr(self.idx_n), B * self.n_slot, ptr(self.idx_off),
                     ptr(self.idx_refs), ptr(self.hist), self.hist_len, ptr(self.opt), 1 if train else 0,
                     ptr(self.rows_u), ptr(self.rows_u1), ptr(self.mv_u) if (train and self.mv_u is not None) else None,
-                    ptr(self.fmst), ptr(x0), ptr(self.fm_out), s)
+                    ptr(self.fmst), ptr(x0), ptr(self.fm_out), ptr(self.mst), ptr(self.mst1), s)
             if sp.M:
-                self._c("pool_fwd", "dl_pool_fwd_indexed", C_ref(L), ptr(self.rows_u),
-                        ptr(self.rows_u1) if sp.fm else None, ptr(self.idx_inv), self.n_rep, ptr(self.slot_start),
-                        ptr(self.slot_end), sp.M, self.fm_pool_col, ptr(self.x0), ptr(self.fm_out), ptr(self.cnt_emb),
-                        ptr(self.cnt_first), s)
+                self._c("pool_fwd", "dl_pool_fwd_staged", C_ref(L), ptr(self.mst), ptr(self.mst1), ptr(self.idx_inv),
+                        ptr(self.slot_start), ptr(self.slot_end), sp.M, self.fm_pool_col, ptr(self.x0),
+                        ptr(self.fm_out), ptr(self.cnt_emb), ptr(self.cnt_first), s)
             self._c("embed_fwd", "dl_embed_fwd_staged", C_ref(L), ptr(self.fmst), ptr(self.rows_u1) if sp.fm else None,
                     ptr(self.idx_inv), self.n_rep, ptr(self.in_cont), ptr(self.in_vec), ptr(x0), ptr(self.fm_out),
                     ptr(self.fm_sum), s)

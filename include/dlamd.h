@@ -123,6 +123,12 @@ int dl_embed_fwd_indexed(const dl_emb_layout* L, const float* rows, const float*
  * n_rep + b*S + f), the cont fields' first-order outputs from rows_first[0, C), x0's cont /
  * vector columns, and zeros for every reference without a row (inv < 0: the zero row) —
  * its FM row, first-order output or x0 columns; everything the gather scattered is left. */
+int dl_pool_fwd_staged(const dl_emb_layout* L, const float* mst, const float* mst1, const int32_t* inv,
+                       const int32_t* slot_start, const int32_t* slot_end, int32_t n_slots, int32_t fm_col,
+                       float* x0, float* fm_out, float* cnt_emb, float* cnt_first, void* stream);
+/* dl_pool_fwd_indexed with multi position l of sample b read from the gather's multi-hot
+ * staging rows mst[b * multi_width + l] (mst1 the first-order weights); positions without a
+ * row (inv < 0: padding) count as none.  Same sums, same order. */
 int dl_embed_fwd_staged(const dl_emb_layout* L, const float* fmst, const float* rows_first, const int32_t* inv,
                         int32_t n_rep, const float* cont, const float* vector, float* x0, float* fm_out,
                         float* fm_sum, void* stream);
@@ -433,7 +439,9 @@ int dl_rec_gather(const dl_emb_layout* L, const float* rec, int32_t rec_ld, int3
  * references reading it, through the batch index's sorted segments (seg_off, sorted_refs of
  * dl_index_build): FM reference (b, f) -> fmst[n_rep + b*S + f][E] and fm_out[b][Cf + f] =
  * w1; deep reference (b, f) -> x0[b][x0_cat_col + f*E] (bf16 when L->x0_bf16); the
- * replicated rows -> fmst[0, n_rep).  Multi-hot references are left to the pooling kernels.
+ * replicated rows -> fmst[0, n_rep).  Multi-hot reference (b, l) -> mst[b * multi_width + l][E]
+ * and mst1[...] = w1 when mst is given (then dl_pool_fwd_staged pools them), else left to
+ * the pooling kernels.
  * Random 64-B writes in place of dl_embed_fwd_indexed's random 64-B reads through the
  * inverse map (the forward of models/deepfm_pipeline.py:89-123 reorganised around the
  * batch's unique rows); follow with dl_embed_fwd_staged.  fmst: [n_rep + B*S][E]. */
@@ -441,7 +449,7 @@ int dl_rec_gather_scatter(const dl_emb_layout* L, const float* rec, int32_t rec_
                           int32_t n_rep, const uint32_t* uniq_keys, const int32_t* n_uniq, int64_t max_uniq,
                           const int32_t* seg_off, const int32_t* sorted_refs, const float* hist, int32_t hist_len,
                           const float* opt, int32_t lag, float* rows_u, float* rows_u1, float* mv_u, float* fmst,
-                          void* x0, float* fm_out, void* stream);
+                          void* x0, float* fm_out, float* mst, float* mst1, void* stream);
 /* Fused backward + Adam: per unique row the ordered segment sum of its references
  * (as dl_embed_bwd_sorted) is applied with step opt[7]'s alpha to the caught-up
  * state of dl_rec_gather (rows_u, rows_u1, mv_u — full arrays, replicated rows
