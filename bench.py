@@ -122,7 +122,8 @@ PMC_KERNEL = {"adam_table": "adam_rows4_kernel", "adam_first": "adam_rows1_kerne
               "head": "head_kernel"}
 PMC_KERNEL_LAZY = {"rec_gather": ("rec_gather_kernel<16, false>", "rec_gather_kernel<16, true>",
                                   "rec_gather_kernel<16>"),     # the last: summaries before the SPARSE template
-                   "embed_bwd": ("rec_bwd_adam_kernel<16, true>", "rec_bwd_adam_kernel<16>"),
+                   "embed_bwd": ("rec_bwd_adam_kernel<16, true, false>", "rec_bwd_adam_kernel<16, true, true>",
+                                 "rec_bwd_adam_kernel<16, true>", "rec_bwd_adam_kernel<16>"),
                    "head": "head_kernel"}
 
 
@@ -135,7 +136,7 @@ def pmc_traffic(label, world, lazy=False, workload="c2"):
     names = PMC_KERNEL_LAZY if lazy else PMC_KERNEL
     if world != 1 or label not in names:
         return None
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*", "pmc_summary.json")))
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*", "pmc_summary*.json")))
     for f in reversed(files):
         d = json.load(open(f))
         if d.get("workload", "c2") != workload:

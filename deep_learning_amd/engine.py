@@ -416,13 +416,16 @@ class CTREngine:
         # waves/SIMD (169 VGPRs) costs ~190 us that the gather's catch-up hides (253 us with
         # no rows lagging; scripts/catchup_cost.py).
         self.fwd_rec = bool(fwd_rec and self.lazy and not M and not rec_stash)
-        # fwd_scatter (the lazy default): the gather writes each caught-up row straight to the
-        # references reading it (dl_rec_gather_scatter: FM staging rows, first-order outputs,
-        # x0's deep columns) and dl_embed_fwd_staged sums the FM terms per sample from the
-        # staging rows — random 64-B writes in place of the indexed forward's random 64-B reads
-        # through the inverse map.  DLAMD_FWD_SCATTER=0 keeps the indexed forward.
+        # fwd_scatter (opt-in, DLAMD_FWD_SCATTER=1): the gather writes each caught-up row
+        # straight to the references reading it (dl_rec_gather_scatter: FM staging rows,
+        # first-order outputs, x0's deep columns, multi-hot staging rows) and
+        # dl_embed_fwd_staged sums the FM terms per sample from the staging rows — random
+        # 64-B writes in place of the indexed forward's random 64-B reads through the inverse
+        # map.  Measured slower end to end (profiles/r03d: C2 2.45 vs 2.32 ms, the gather
+        # +170 us for the forward's -58 us; C3 gather +830 us for pooling's -95 us): the
+        # per-reference segment walk serialises dependent loads in the gather's waves.
         if fwd_scatter is None:
-            fwd_scatter = os.environ.get("DLAMD_FWD_SCATTER", "1") != "0"
+            fwd_scatter = os.environ.get("DLAMD_FWD_SCATTER", "0") != "0"
         self.fwd_scatter = bool(fwd_scatter and self.lazy and not self.fwd_rec and type(self) is CTREngine)
         self.fmst = z(self.n_rep + B * S, E) if (self.fwd_scatter and sp.fm) else None
         # multi-hot staging (scatter form): position l of sample b at row b * multi_width + l
@@ -588,8 +591,13 @@ class CTREngine:
             P = {sp.table_key: self.table[:N].cpu().numpy()}
             if self.first is not None:
                 P[sp.first_key] = self.first[:N].cpu().numpy()[:, None]
-        P.update(self._export_dense(self.W, self.w_head, self._wide_state()[0], getattr(self, "wb", None)))
+        P.update(self.dense_params())
         return P
+
+    def dense_params(self):
+        """The dense parameters (hidden layers, head or wdl weights + bias) in the reference
+        layout (numpy); the wide records are caught up first."""
+        return self._export_dense(self.W, self.w_head, self._wide_state()[0], getattr(self, "wb", None))
 
     def dense_state(self):
         """Adam moments of the dense parameters (hidden layers, head / wdl weights) in the

@@ -27,7 +27,10 @@ TOL must be one of at most 1e-4 of its array after the first step (dense: 1e-3, 
 after the others) and within one step's
 flip size, and those elements alone take the GPU's value and moments in the oracle before the
 next step (their count and |G| / sum|terms| are recorded in the stats); the rest of the state
-is never re-synced, and the logits are held to 1e-5 at every step.
+is never re-synced.  Logits: 1e-5 at step 0 (identical state); at later steps 1e-5 against the
+oracle's forward of the GPU's own state after the previous step (identical state again), and
+along the trajectory against the never-re-synced oracle within 1e-5 for all but 1e-3 of the
+samples, every one within Z_DRIFT (measured: 9 of 65,536 samples at 1.2e-5, C2 step 2, r03d).
 
 DLAMD_TEST_STATS=<dir>: each test appends its measured maxima / flip fractions there (json).
 """
@@ -64,6 +67,8 @@ FLIP = (1 - 0.9) / np.sqrt(1 - 0.999)
 # max 8.8e-5 — profiles/r03b/fullsize_stats.jsonl), every element within the flip size;
 # Adam moments within BF16_MRTOL relative (+ a floor) except the same fraction.
 BF16_ATOL = 1e-4
+# logits along the fp32 trajectory (steps >= 1) against the never-re-synced oracle state
+Z_DRIFT = 5 * TOL
 BF16_FRAC = 0.01
 BF16_MRTOL = 0.05
 
@@ -136,8 +141,22 @@ def _run(name, model, kw, batches, tower="f32", z_tol=TOL, loss_tol=TOL, auc_tol
         dz = np.abs(z.astype(np.float64) - fw["z"])
         _stat("%s step %d" % (name, step), z_max_err=dz.max(), z_frac_bad=(dz > z_tol).mean(),
               loss_err=abs(eng.loss() - fw["loss"]))
-        check(dz.max() <= z_tol, "logits step %d: max error %g > %g (%d samples)" % (step, dz.max(), z_tol,
-                                                                                      (dz > z_tol).sum()))
+        if step == 0 or bf:
+            check(dz.max() <= z_tol, "logits step %d: max error %g > %g (%d samples)" % (
+                step, dz.max(), z_tol, (dz > z_tol).sum()))
+        else:
+            # from identical state (the GPU's own state after the last step, through the
+            # oracle's forward): the reference's 1e-5 on every logit
+            z1 = R.forward(cfg, prev, b)["z"]
+            d1 = np.abs(z.astype(np.float64) - z1)
+            _stat("%s step %d same-state" % (name, step), z_max_err=d1.max())
+            check(d1.max() <= z_tol, "logits step %d from the GPU's state: max error %g > %g" % (
+                step, d1.max(), z_tol))
+            # along the trajectory the oracle's state carries its own sub-TOL summation-order
+            # differences (never re-synced): within TOL but for at most 1e-3 of the samples,
+            # every one within Z_DRIFT
+            check((dz > z_tol).mean() <= 1e-3 and dz.max() <= Z_DRIFT,
+                  "logits step %d: max error %g, %d samples > %g" % (step, dz.max(), (dz > z_tol).sum(), z_tol))
         check(abs(eng.loss() - fw["loss"]) < loss_tol, "loss step %d: %r vs %r" % (step, eng.loss(), fw["loss"]))
         if auc_tol is not None:
             s = eng.score[:B].cpu().numpy()
@@ -148,7 +167,7 @@ def _run(name, model, kw, batches, tower="f32", z_tol=TOL, loss_tol=TOL, auc_tol
         touched_all.append(t[t < spec.n_rows])
         # dense parameters and moments after every step
         bound = 2 * FLIP * alpha + TOL
-        got = eng._export_dense(eng.W, eng.w_head, getattr(eng, "ww", None), getattr(eng, "wb", None))
+        got = eng.dense_params()
         ds = eng.dense_state()
         for key in got:
             what = "%s (step %d)" % (key, step)
@@ -189,6 +208,7 @@ def _run(name, model, kw, batches, tower="f32", z_tol=TOL, loss_tol=TOL, auc_tol
             continue
         gp = eng.params()
         st = eng.adam_state()
+        prev = gp
         keys = [(tk, "m", "v")] + ([(spec.first_key, "m1", "v1")] if spec.fm else [])
         for key, mk, vk in keys:
             bad = compare(gp[key], P[key], tbound, what(key), frac if not last else 5e-4)
@@ -198,7 +218,7 @@ def _run(name, model, kw, batches, tower="f32", z_tol=TOL, loss_tol=TOL, auc_tol
                 _stat("%s %s repaired" % (name, what(key)), n=len(idx))
                 for arr, src in ((P[key], gp[key]), (opt.m[key], st[mk]), (opt.v[key], st[vk])):
                     arr.reshape(-1)[idx] = np.asarray(src).reshape(-1)[idx]
-        del gp, st
+        del st
     assert not fails, "; ".join(fails)
     return eng
 
