@@ -12,21 +12,6 @@
 
 namespace dl {
 
-// One atomic per block for the per-step regulariser sums: device-scope atomics on one
-// address serialise across the XCDs (~12 ns each measured: a per-wave atomic cost the
-// 26 M-row wide-weight sweep ~100 us and each 400x400 layer ~30 us).
-__device__ __forceinline__ void block_atomic_add(float x, float* out) {
-  __shared__ float part[16];
-  x = wave_sum(x);
-  if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = x;
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    float t = 0.f;
-    for (int w = 0; w < (int)(blockDim.x >> 6); ++w) t += part[w];
-    atomicAdd(out, t);
-  }
-}
-
 // opt: [0] b1p [1] b2p [2] lr [3] alpha [4] b1 [5] b2 [6] eps [7] step
 __device__ __forceinline__ void adam_begin_body(float* opt, float decay_rate, float decay_steps) {
   if (step_poisoned(opt)) return;   // a failed batch: the step does not begin (common.h)

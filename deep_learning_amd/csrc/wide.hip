@@ -109,10 +109,7 @@ __global__ __launch_bounds__(256) void wide_rec_update_kernel(float4* __restrict
     adam_elem(w, m, v, wide_l2_grad(wide_float(q), h.l2, w), alpha, h.omb1, h.omb2, h.eps);
     rec[row] = make_float4(w, m, v, __int_as_float(t));
   }
-  if (sq_out) {
-    sq = wave_sum(sq);
-    if ((threadIdx.x & 63) == 0 && sq != 0.f) atomicAdd(sq_out, sq);
-  }
+  if (sq_out) block_atomic_add(sq, sq_out);
 }
 
 // Pass B: the H deep-output rows pass A did not cover (their gradient: the deep term alone).
@@ -142,10 +139,7 @@ __global__ __launch_bounds__(256) void wide_rec_update_deep_kernel(float4* __res
     adam_elem(r.x, r.y, r.z, wide_l2_grad(wide_float(q), h.l2, r.x), alpha, h.omb1, h.omb2, h.eps);
     rec[row] = make_float4(r.x, r.y, r.z, __int_as_float(t));
   }
-  if (sq_out) {
-    sq = wave_sum(sq);
-    if ((threadIdx.x & 63) == 0 && sq != 0.f) atomicAdd(sq_out, sq);
-  }
+  if (sq_out) block_atomic_add(sq, sq_out);
 }
 
 // Every row caught up to step opt[7].  Rows the last step did not touch (stamp < t) pass
@@ -168,15 +162,12 @@ __global__ __launch_bounds__(256) void wide_rec_flush_kernel(float4* __restrict_
     wide_catch_up(r.x, r.y, r.z, t - 1, t, hist, h);
     rec[row] = make_float4(r.x, r.y, r.z, __int_as_float(t));
   }
-  if (sq_untouched) {
-    sq = wave_sum(sq);
-    if ((threadIdx.x & 63) == 0 && sq != 0.f) atomicAdd(sq_untouched, sq);
-  }
+  if (sq_untouched) block_atomic_add(sq, sq_untouched);
 }
 
-static unsigned wide_grid(long long n) {
+static unsigned wide_grid(long long n) {   // grid-stride kernels, one regulariser atomic per block
   long long b = (n + 255) / 256;
-  if (b > 8192) b = 8192;
+  if (b > kSumGrid) b = kSumGrid;
   return (unsigned)(b < 1 ? 1 : b);
 }
 
