@@ -120,7 +120,8 @@ def kernel_work(spec, B, touched_rows, rows=None, uniq=None, shard=None, wide_ro
 PMC_KERNEL = {"adam_table": "adam_rows4_kernel", "adam_first": "adam_rows1_kernel",
               "embed_fwd": "embed_fwd_kernel<16, 5>", "embed_bwd": "embed_bwd_kernel<16, false>",
               "head": "head_kernel"}
-PMC_KERNEL_LAZY = {"rec_gather": ("rec_gather_kernel<16, false>", "rec_gather_kernel<16, true>",
+PMC_KERNEL_LAZY = {"rec_gather": ("rec_gather_kernel<16, false, false>", "rec_gather_kernel<16, true, false>",
+                                  "rec_gather_kernel<16, false>", "rec_gather_kernel<16, true>",
                                   "rec_gather_kernel<16>"),     # the last: summaries before the SPARSE template
                    "embed_bwd": ("rec_bwd_adam_kernel<16, true, false>", "rec_bwd_adam_kernel<16, true, true>",
                                  "rec_bwd_adam_kernel<16, true>", "rec_bwd_adam_kernel<16>"),

@@ -717,6 +717,227 @@ static bool launch_bf16_bres(const GemmParams& gp, int epi, bool cb, hipStream_t
   return true;
 }
 
+// ---------------------------------------------------------------------------
+// Tall-skinny bf16 product with the weights streamed through an LDS ring (the C5 tower's
+// forward and dX: M = batch rows, both operands k-contiguous bf16).  The structure of the
+// s3 NT kernel (gemm_s3.hip) on one plane: block 256 x 208 (8 waves x 32 rows x 13 column
+// fragments), A streamed from HBM straight into MFMA fragments (one 16-B load per lane and
+// row fragment per 32-deep chunk), each chunk's [208][32] weight image (conflict-free slot
+// swizzle) filled by LDS-DMA two chunks ahead into a ring of three.  Against the B-resident
+// kernel above (256 x 80 blocks: A fetched once per 80 columns, five times for N = 400) a
+// block covers 208 columns, so A is fetched twice; the weight chunks come from L2.
+constexpr int kBnBM = 256, kBnBN = 208, kBnNF = 13;
+constexpr int kBnPlane = kBnBN * 32;                         // bf16 elements of one chunk image (13,312 B)
+constexpr int kBnDma = kBnBN / 16;                           // DMA instructions per chunk (13)
+constexpr int kBnDmaW = (kBnDma + 7) / 8;                    // per wave (2; the last clamped)
+constexpr int kBnEP = kBnBN + 4;                             // epilogue tile pitch (floats)
+constexpr size_t kBnLds = 8 * 16 * kBnEP * sizeof(float);    // the epilogue tiles: 108,544 B
+static_assert(3 * kBnPlane * sizeof(unsigned short) <= kBnLds, "the ring fits in the epilogue's LDS");
+#ifndef DL_BN_PF
+#define DL_BN_PF 4   // weight fragments read this many fragments ahead of their MFMAs
+#endif
+
+__device__ __forceinline__ int bn_slot(int j, int kq) { return kq ^ ((j >> 2) & 2); }   // an involution in kq
+
+// s_waitcnt vmcnt(n) (n < 64), other counters untouched
+#define DL_BN_VMCNT(n) __builtin_amdgcn_s_waitcnt(((n) & 0xF) | (((n) >> 4) << 14) | (0x7 << 4) | (0xF << 8))
+
+template <int EPI, bool CBF16>
+__global__ __launch_bounds__(512) void gemm_bf16_nt_kernel(GemmParams p) {
+  extern __shared__ __attribute__((aligned(16))) unsigned short lds[];   // [3 bufs][BN][32], then the epilogue
+  const unsigned short* __restrict__ Bm = reinterpret_cast<const unsigned short*>(p.B);
+  const int tid = threadIdx.x, lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int ntm = (p.M + kBnBM - 1) / kBnBM, ntn = (p.N + kBnBN - 1) / kBnBN;
+  const int t = xcd_tile(blockIdx.x, ntm * ntn);     // the column tiles of a row tile on one XCD: A from L2
+  const int i0 = (t / ntn) * kBnBM, j0 = (t % ntn) * kBnBN;
+  const int cl = lane & 15, kq = lane >> 4;
+  const int r0 = i0 + wid * 32;
+  const bool ok0 = r0 + cl < p.M, ok1 = r0 + 16 + cl < p.M;
+  // A through a buffer descriptor (the host checks M * lda * 2 < 2^31): a piece past M or K
+  // gets an offset past the range and reads as zeros (no fixup after a load)
+  const uint32_t a_off0 = 2u * (uint32_t)(min(r0 + cl, p.M - 1) * p.lda + 8 * kq);
+  const uint32_t a_off1 = 2u * (uint32_t)(min(r0 + 16 + cl, p.M - 1) * p.lda + 8 * kq);
+  const auto a_rsrc = __builtin_amdgcn_make_buffer_rsrc((void*)p.A, (short)0, p.M * p.lda * 2, 0x00020000);
+  const int KC = (p.K + 31) / 32;
+  const uint32_t lds_base = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) unsigned short*)lds;
+  // LDS-DMA of chunk c into buffer `buf`: instruction g fills rows 16g .. 16g + 15; lane L writes
+  // slot L & 3 of row L >> 2 and fetches the piece that belongs there.  Rows past N / k past K
+  // read clamped in-range data (discarded by the epilogue / multiplied by A's zeros).  Inline
+  // asm, as in gemm_s3.hip: a builtin LDS-DMA makes hipcc wait vmcnt(0) before the first use of
+  // any A load; every wave issues exactly kBnDmaW instructions, so the counts below are
+  // straight-line.
+  auto dma_b = [&](int c, int buf) {
+#pragma unroll
+    for (int i = 0; i < kBnDmaW; ++i) {
+      const int g = min(wid + 8 * i, kBnDma - 1);
+      const int rb = 16 * g;
+      const int j = rb + (lane >> 2);
+      const int kpc = bn_slot(j, lane & 3);
+      const int gj = min(j0 + j, p.N - 1);
+      const int gk = min(32 * c + 8 * kpc, p.K - 8);
+      const unsigned short* src = Bm + (long long)gj * p.ldb + gk;
+      const uint32_t dst = lds_base + 2u * (uint32_t)(buf * kBnPlane + rb * 32);
+      unsigned keep;
+      asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+                   : "=&s"(keep) : "v"(src), "s"(__builtin_amdgcn_readfirstlane(dst)) : "memory");
+    }
+  };
+  auto load_a = [&](int c, uint4 (&ra)[2]) {
+    const bool kin = 32 * c + 8 * kq < p.K;
+    ra[0] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(
+                                          a_rsrc, (int)((ok0 & kin) ? a_off0 + 64u * c : 0x80000000u), 0, 0));
+    ra[1] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(
+                                          a_rsrc, (int)((ok1 & kin) ? a_off1 + 64u * c : 0x80000000u), 0, 0));
+  };
+  floatx4 acc[2][kBnNF];
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int f = 0; f < kBnNF; ++f) acc[a][f] = floatx4{0.f, 0.f, 0.f, 0.f};
+  uint4 raA[2], raB[2];
+  dma_b(0, 0);
+  load_a(0, raA);
+  dma_b(1, 1);     // unconditional, like every prefetch below: chunks past KC read clamped
+  load_a(1, raB);  // weights into a free buffer and zeros for A
+  // chunk c + 1's weights -> every wave: wait for every batch but the newest (chunk c + 2's),
+  // then a bare s_barrier (a __syncthreads would drain the prefetch: vmcnt(0))
+  auto publish = [&](int c) {
+    if (c + 1 < KC) DL_BN_VMCNT(kBnDmaW + 2);
+    else DL_BN_VMCNT(0);                  // the epilogue reuses the LDS: nothing may still land
+    __builtin_amdgcn_s_waitcnt(0xc07f);   // lgkmcnt(0): this wave's fragment reads are done
+    __builtin_amdgcn_s_barrier();
+  };
+  publish(-1);
+  auto step = [&](int c, uint4 (&ra)[2]) {
+    shortx8 a0 = __builtin_bit_cast(shortx8, ra[0]), a1 = __builtin_bit_cast(shortx8, ra[1]);
+    // chunk c's A in registers of their own before the next batch reuses ra (hipcc's wait for
+    // it counts only its own loads)
+    asm volatile("" : "+v"(a0), "+v"(a1));
+    dma_b(c + 2, (c + 2) % 3);
+    load_a(c + 2, ra);
+    const unsigned short* Bs = lds + (c % 3) * kBnPlane + cl * 32 + 8 * bn_slot(cl, kq);
+    constexpr int PF = DL_BN_PF, NB = PF + 1;
+    shortx8 bb[NB];
+#pragma unroll
+    for (int i = 0; i < PF; ++i) bb[i] = *reinterpret_cast<const shortx8*>(Bs + 512 * i);   // fragment rows 16i + cl
+#pragma unroll
+    for (int f = 0; f < kBnNF; ++f) {
+      if (f + PF < kBnNF) bb[(f + PF) % NB] = *reinterpret_cast<const shortx8*>(Bs + 512 * (f + PF));
+      const shortx8 bv = bb[f % NB];
+      acc[0][f] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0, bv, acc[0][f], 0, 0, 0);
+      acc[1][f] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1, bv, acc[1][f], 0, 0, 0);
+    }
+    publish(c);
+  };
+  int c = 0;
+  for (; c + 1 < KC; c += 2) {
+    step(c, raA);
+    step(c + 1, raB);
+  }
+  if (c < KC) step(c, raA);
+
+  // Epilogue through LDS (free after the last barrier): per wave and half (rows 16h .. 16h + 15
+  // of its 32) the 16 x 208 f32 tile is written from the MFMA layout, then each lane moves
+  // whole row pieces (8 bf16 or 4 f32 = 16 B), ReLU / ReluGrad mask applied there.
+  float* tile = reinterpret_cast<float*>(lds) + wid * 16 * kBnEP;
+  const unsigned short* __restrict__ Mk = reinterpret_cast<const unsigned short*>(p.mask);
+  constexpr int EPP = CBF16 ? 8 : 4;                // output elements per 16-B piece
+  constexpr int VPR = kBnBN / EPP;                  // pieces per row (26 or 52)
+  constexpr int NIT = (16 * VPR + 63) / 64;         // pieces per lane per half
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    // the mask's pieces of this half first (all in flight together, under the tile writes)
+    uint4 mk4[EPI == EPI_MASK ? NIT : 1];
+    if (EPI == EPI_MASK) {
+#pragma unroll
+      for (int it = 0; it < NIT; ++it) {
+        const int q = min(lane + 64 * it, 16 * VPR - 1);
+        const int rl = q / VPR, pc = q % VPR;
+        const int row = min(r0 + 16 * h + rl, p.M - 1), col = max(0, min(j0 + EPP * pc, p.N - EPP));
+        const unsigned short* mk = Mk + (long long)row * p.ldm + col;
+        if (CBF16) {
+          mk4[it] = *reinterpret_cast<const uint4*>(mk);
+        } else {
+          const uint2 m2 = *reinterpret_cast<const uint2*>(mk);
+          mk4[it] = make_uint4(m2.x, m2.y, 0u, 0u);
+        }
+      }
+    }
+#pragma unroll
+    for (int f = 0; f < kBnNF; ++f)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) tile[(4 * kq + j) * kBnEP + 16 * f + cl] = acc[h][f][j];
+    __builtin_amdgcn_s_waitcnt(0xc07f);             // lgkmcnt(0): this wave's tile writes landed
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int it = 0; it < NIT; ++it) {
+      const int q = lane + 64 * it;
+      const int rl = q / VPR, pc = q % VPR;
+      const int row = r0 + 16 * h + rl, col = j0 + EPP * pc;
+      if (q >= 16 * VPR || row >= p.M || col >= p.N) continue;
+      float x[8];
+      const float4 v0 = *reinterpret_cast<const float4*>(tile + rl * kBnEP + EPP * pc);
+      x[0] = v0.x; x[1] = v0.y; x[2] = v0.z; x[3] = v0.w;
+      if (CBF16) {
+        const float4 v1 = *reinterpret_cast<const float4*>(tile + rl * kBnEP + EPP * pc + 4);
+        x[4] = v1.x; x[5] = v1.y; x[6] = v1.z; x[7] = v1.w;
+      }
+      const int nv = min(EPP, p.N - col);
+      const unsigned short* mk = Mk + (long long)row * p.ldm + col;
+      const bool whole_mask = EPI == EPI_MASK && nv == EPP && (reinterpret_cast<uintptr_t>(mk) & (2 * EPP - 1)) == 0;
+      unsigned short mv[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+      if (EPI == EPI_MASK) {
+        if (whole_mask) memcpy(mv, &mk4[EPI == EPI_MASK ? it : 0], 2 * EPP);
+        else for (int e = 0; e < nv; ++e) mv[e] = mk[e];
+      }
+#pragma unroll
+      for (int e = 0; e < EPP; ++e) {
+        if (EPI == EPI_RELU) x[e] = fmaxf(x[e], 0.f);
+        if (EPI == EPI_MASK) x[e] = bf2f(mv[e]) > 0.f ? x[e] : 0.f;
+      }
+      unsigned char* dst = reinterpret_cast<unsigned char*>(p.C) + ((long long)row * p.ldc + col) * (CBF16 ? 2 : 4);
+      if (nv == EPP && (reinterpret_cast<uintptr_t>(dst) & 15) == 0) {
+        if (CBF16)
+          *reinterpret_cast<uint4*>(dst) = make_uint4(f2bf(x[0]) | ((unsigned)f2bf(x[1]) << 16),
+                                                      f2bf(x[2]) | ((unsigned)f2bf(x[3]) << 16),
+                                                      f2bf(x[4]) | ((unsigned)f2bf(x[5]) << 16),
+                                                      f2bf(x[6]) | ((unsigned)f2bf(x[7]) << 16));
+        else
+          *reinterpret_cast<float4*>(dst) = make_float4(x[0], x[1], x[2], x[3]);
+      } else {
+        for (int e = 0; e < nv; ++e) {
+          if (CBF16) reinterpret_cast<unsigned short*>(dst)[e] = f2bf(x[e]);
+          else reinterpret_cast<float*>(dst)[e] = x[e];
+        }
+      }
+    }
+    __builtin_amdgcn_wave_barrier();
+  }
+}
+
+#ifndef DL_BF16_NT
+#define DL_BF16_NT 1   // forward / dX products on gemm_bf16_nt_kernel (0: the B-resident kernel)
+#endif
+
+// true if the streamed-weight kernel takes the product (and launches it)
+static bool launch_bf16_nt(const GemmParams& gp, int epi, bool cb, hipStream_t s) {
+  if (!DL_BF16_NT || epi == EPI_SPLIT || gp.K < 8 || gp.K % 8 || gp.lda % 8 || gp.ldb % 8 || gp.lda < gp.K ||
+      gp.ldb < gp.K || (epi == EPI_MASK && gp.ldm % 8) || (reinterpret_cast<uintptr_t>(gp.A) & 15) ||
+      (reinterpret_cast<uintptr_t>(gp.B) & 15) || (long long)gp.M * gp.lda * 2 >= (1LL << 31))
+    return false;
+  const dim3 grid((unsigned)(ceil_div(gp.M, kBnBM) * ceil_div(gp.N, kBnBN))), block(512);
+#define DL_BNT(E_, C_) hipLaunchKernelGGL((gemm_bf16_nt_kernel<E_, C_>), grid, block, kBnLds, s, gp)
+  if (epi == EPI_STORE) {
+    if (cb) DL_BNT(EPI_STORE, true); else DL_BNT(EPI_STORE, false);
+  } else if (epi == EPI_RELU) {
+    if (cb) DL_BNT(EPI_RELU, true); else DL_BNT(EPI_RELU, false);
+  } else {
+    if (cb) DL_BNT(EPI_MASK, true); else DL_BNT(EPI_MASK, false);
+  }
+#undef DL_BNT
+  return true;
+}
+
 // Weight gradients of the bf16 tower without transposed operand copies (ta = 1, tb = 0,
 // split-K slabs): slab z of C = sum over the batch rows k of split z of X[k][m] dY[k][n], with
 // X [K][lda] bf16 (m contiguous: the activations as the forward wrote them) and dY [K][ldb]
@@ -1073,6 +1294,7 @@ extern "C" int dl_gemm_bf16(int32_t ta, int32_t tb, int32_t M, int32_t N, int32_
     if (kps2 == 0) kps2 = 64;
     gp.k_per_split = kps2;
     const int sp2 = (int)ceil_div(K > 0 ? K : 1, kps2);
+    if (sp2 == 1 && launch_bf16_nt(gp, epi, c_bf16 != 0, s)) DL_RETURN_LAUNCH("dl_gemm_bf16");
     if (sp2 == 1 && launch_bf16_bres(gp, epi, c_bf16 != 0, s)) DL_RETURN_LAUNCH("dl_gemm_bf16");
     const int bn = (N + 79) / 80 * 80 <= (N + 207) / 208 * 208 ? 80 : 208;
     dispatch_bf16_kc(gp, epi, sp2, c_bf16 != 0, bn, s);

@@ -116,7 +116,8 @@ enum { S3_STORE = 0, S3_RELU = 1, S3_MASK = 2 };
 #ifndef DL_S3_DIAG
 #define DL_S3_DIAG 0   // diagnostics builds: 1 = no epilogue stores, 2 = no MFMAs either;
                        // 3 = no stores, no A loads (constant A); 4 = no stores, no B LDS reads;
-                       // 5 = no stores, no per-chunk barrier (results wrong: timing only)
+                       // 5 = no stores, no per-chunk barrier; 6 = no plane split (A in NT, both
+                       // operands in TN2: the f32 bits taken as planes) (results wrong: timing only)
 #endif
 
 // ---------------------------------------------------------------------------- NT
@@ -249,8 +250,13 @@ __global__ __launch_bounds__(512) void gemm_s3_nt_kernel(S3Params p) {
 
   auto step = [&](int c, float4 (&ra)[4]) {
     shortx8 ah[2], am[2], al[2];
-    split8(ra[0], ra[1], ah[0], am[0], al[0]);
-    split8(ra[2], ra[3], ah[1], am[1], al[1]);
+    if (DL_S3_DIAG == 6) {   // timing only: the f32 bits taken as planes, no split
+      ah[0] = __builtin_bit_cast(shortx8, ra[0]); am[0] = __builtin_bit_cast(shortx8, ra[1]); al[0] = ah[0];
+      ah[1] = __builtin_bit_cast(shortx8, ra[2]); am[1] = __builtin_bit_cast(shortx8, ra[3]); al[1] = ah[1];
+    } else {
+      split8(ra[0], ra[1], ah[0], am[0], al[0]);
+      split8(ra[2], ra[3], ah[1], am[1], al[1]);
+    }
     // hipcc's wait for chunk c's A counts only its own loads (4 a batch), so it must come
     // before the next batch is issued or it would also wait for part of that batch: the empty
     // statement pins the split (and its wait) ahead of the batch's DMA statements
@@ -329,7 +335,7 @@ __global__ __launch_bounds__(512) void gemm_s3_nt_kernel(S3Params p) {
   }
   if (c < KC) step(c, raA);
 
-  if (DL_S3_DIAG) {   // keep the loop's results live without storing them
+  if (DL_S3_DIAG && DL_S3_DIAG != 6) {   // keep the loop's results live without storing them
     float tt = 0.f;
 #pragma unroll
     for (int a = 0; a < 2; ++a)
@@ -615,8 +621,13 @@ __global__ __launch_bounds__(512) void gemm_s3_tn2_kernel(S3Params p) {
     for (int u = 0; u < kT2Q; ++u) {
       if (u == 5 && tid >= 256) continue;
       uint32_t h0, m0_, l0, h1, m1_, l1;
-      split2(rs[u].x, rs[u].y, h0, m0_, l0);
-      split2(rs[u].z, rs[u].w, h1, m1_, l1);
+      if (DL_S3_DIAG == 6) {   // timing only: no split
+        h0 = __float_as_uint(rs[u].x); m0_ = __float_as_uint(rs[u].y); l0 = h0;
+        h1 = __float_as_uint(rs[u].z); m1_ = __float_as_uint(rs[u].w); l1 = h1;
+      } else {
+        split2(rs[u].x, rs[u].y, h0, m0_, l0);
+        split2(rs[u].z, rs[u].w, h1, m1_, l1);
+      }
       unsigned short* img = u < 2 ? As : Bs;
       const int pe = u < 2 ? kT2AE : kT2BE;
       const int o = pr[u] * (u < 2 ? kT2PA : kT2PB) + pc[u];

@@ -372,7 +372,8 @@ class CTREngine:
         # split-K slabs of the weight gradients: the double-buffered s3 TN kernel (one block per
         # CU, 2 column tiles) runs best at 32 (scripts/s3_bench.py: 147 vs 152 us at 64)
         self.splits = max(1, min(int(os.environ.get("DLAMD_DW_SPLITS", 32 if self.s3 else 64)), B // 1024))
-        self.w_slab = z(self.splits * max(i * o for i, o in zip(self.in_ld, self.out_ld)))
+        self.dw_splits = self._dw_splits(B, fixed="DLAMD_DW_SPLITS" in os.environ)
+        self.w_slab = z(max(k * i * o for k, i, o in zip(self.dw_splits, self.in_ld, self.out_ld)))
         self.layout = self._layout(B)
         self.bwd_blocks = _lib.lib().dl_embed_bwd_grid(C_ref(self.layout))
         self.cont_slab = z(max(1, self.bwd_blocks * sp.C * (E + 1)))
@@ -593,6 +594,13 @@ class CTREngine:
                 P[sp.first_key] = self.first[:N].cpu().numpy()[:, None]
         P.update(self.dense_params())
         return P
+
+    def _dw_splits(self, B, fixed=False):
+        """Per-layer split-K slab counts of the weight gradients (fixed: self.splits for all)."""
+        base = max(1, min(self.splits, B // 1024))
+        if fixed or not self.s3:
+            return [base] * len(self.spec.hidden)
+        return [_s3_dw_splits(i, o, B, base) for i, o in zip(self.in_ld, self.spec.hidden)]
 
     def dense_params(self):
         """The dense parameters (hidden layers, head or wdl weights + bias) in the reference
@@ -907,12 +915,13 @@ class CTREngine:
                 ptr(self.hist) if self.lazy else None, self.hist_len if self.lazy else 0, s)
         self._forward(B, s, train=True)
         nl = len(sp.hidden)
-        splits = max(1, min(self.splits, B // 1024))
+        dws = self._dw_splits(B, fixed="DLAMD_DW_SPLITS" in os.environ)
         if self.bf and not self.wdl:      # the wdl head writes its bf16 dY itself
             self._c("cast_dh", "dl_cast_bf16", ptr(self.dh[-1]), B, self.h_ld[-1], self.h_ld[-1], ptr(self.dhb[-1]),
                     self.h_ld[-1], s)
         def dw(l):   # the weight gradient of layer l (split-K slabs into w_slab)
             hdim, stride = sp.hidden[l], self.in_ld[l] * self.out_ld[l]
+            splits = dws[l]
             if self.bf:
                 # dW = X^T dY straight from the batch-major bf16 activations and gradients
                 # (transposing LDS reads inside the kernel: no X^T / dY^T copies)
@@ -964,7 +973,7 @@ class CTREngine:
             # regulariser on every hidden weight matrix: wdl L2 (wdl.py:272-275), dnn L1 (dnn.py:88-90);
             # bias row excluded
             stride = self.in_ld[l] * self.out_ld[l]
-            nsplit = _num_splits(B, splits, 64 if (self.bf or self.s3) else 16)
+            nsplit = _num_splits(B, dws[l], 64 if (self.bf or self.s3) else 16)
             reg = sp.hidden_reg
             l2, l2n = (sp.l2, ([self.D0] + sp.hidden)[l] * self.out_ld[l]) if reg else (0.0, 0)
             self._c("adam_dense_l%d" % l, "dl_adam_dense_reg", ptr(self.W[l]), ptr(self.Wm[l]), ptr(self.Wv[l]),
@@ -1283,6 +1292,19 @@ def default_adam(spec):
     """Table Adam used by the drop-in model classes: row records with lazy-exact
     catch-up (bit-identical to the dense sweep, rec.hip) wherever supported."""
     return "lazy"
+
+
+def _s3_dw_splits(M, N, B, base, cus=256):
+    """Split-K slab count of one s3 weight gradient (dl_gemm_s3_tn: one 128 x 224 block per CU,
+    (M / 128) x (N / 224) tiles per slab).  The blocks run in ceil(tiles x s / cus) rounds of
+    ceil(B / s) batch rows (rounded to 64) each; the s <= base minimising rounds x rows, the
+    largest on ties.  C2's layers (8 tiles) keep 32; C3's layer 0 (M = 528: 10 tiles) takes 25
+    — one round of 250 blocks instead of two rounds for 320."""
+    tiles = -(-M // 128) * -(-N // 224)
+
+    def cost(s):
+        return -(-tiles * s // cus) * (-(-(-(-B // s)) // 64) * 64)
+    return min(range(base, 0, -1), key=cost)
 
 
 def _num_splits(K, splits, align=16):

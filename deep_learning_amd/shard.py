@@ -613,8 +613,9 @@ class ShardedCTREngine(CTREngine):
         sp = self.spec
         s = _lib.stream_handle()
         nl = len(sp.hidden)
-        splits = max(1, min(self.splits, B // 1024))
+        dws = self._dw_splits(B, fixed="DLAMD_DW_SPLITS" in os.environ)
         for l in reversed(range(nl)):
+            splits = dws[l]
             xin = self.x0 if l == 0 else self.h[l - 1]
             hdim = sp.hidden[l]
             stride = self.in_ld[l] * self.out_ld[l]

@@ -569,28 +569,31 @@ def test_sort_unique_matches_numpy(hip_lib, n, distinct):
 
 
 @pytest.mark.parametrize("M,N,K,epi,cbf", [(65536, 400, 432, 1, 1), (9000, 400, 400, 2, 1), (5000, 416, 400, 0, 0),
-                                           (4100, 37, 200, 1, 0), (8192, 400, 416, 1, 0)])
+                                           (4100, 37, 200, 1, 0), (8192, 400, 416, 1, 0), (300, 209, 40, 2, 1),
+                                           (777, 208, 8, 1, 1), (1000, 100, 1000, 2, 0), (257, 400, 432, 0, 1)])
 def test_gemm_bf16_b_resident(hip_lib, M, N, K, epi, cbf):
-    """The tall-skinny bf16 path (B slab resident in LDS, A streamed to fragments; ta=0,
-    tb=1, M >= 4096, K <= 448): relu / ReluGrad-mask / store epilogues, bf16 or f32
-    output, ragged M, N and K chunks, against an fp64 product of the same bf16 operands."""
+    """The tall-skinny bf16 path (ta=0, tb=1: the streamed-weight kernel gemm_bf16_nt_kernel,
+    the B-resident kernel where it declines): relu / ReluGrad-mask / store epilogues, bf16 or
+    f32 output, ragged M, N and K chunks (K past one chunk, not a multiple of 32, beyond the
+    B-resident limit), against an fp64 product of the same bf16 operands."""
     g = torch.Generator().manual_seed(M + N + K)
     lda = (K + 7) // 8 * 8 + 8
     A = torch.randn(M, lda, generator=g).bfloat16()
     A[:, K:] = 7.0                                  # pad past K must not be read
     Bt = torch.randn(N, lda, generator=g).bfloat16()
     Bt[:, K:] = -3.0
-    mask = torch.randn(M, N, generator=g).bfloat16()
+    ldm = (N + 7) // 8 * 8
+    mask = torch.randn(M, ldm, generator=g).bfloat16()
     ref = A[:, :K].double() @ Bt[:, :K].double().t()
     if epi == 1:
         ref = ref.clamp(min=0)
     elif epi == 2:
-        ref = torch.where(mask.double() > 0, ref, torch.zeros_like(ref))
+        ref = torch.where(mask[:, :N].double() > 0, ref, torch.zeros_like(ref))
     ldc = N + 3
     C = torch.full((M, ldc), 5.0, device="cuda", dtype=torch.bfloat16 if cbf else torch.float32)
     md, Ad, Bd = mask.cuda(), A.cuda(), Bt.cuda()    # held for the launch (no freed temporaries)
     call("dl_gemm_bf16", 0, 1, M, N, K, ptr(Ad), lda, ptr(Bd), lda, ptr(C), ldc, cbf, epi,
-         ptr(md) if epi == 2 else None, N, 1, 0, _s())
+         ptr(md) if epi == 2 else None, ldm, 1, 0, _s())
     torch.cuda.synchronize()
     out = C[:, :N].double().cpu()
     scale = (A[:, :K].double().abs() @ Bt[:, :K].double().abs().t()).clamp(min=1.0)
