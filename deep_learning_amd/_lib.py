@@ -77,6 +77,7 @@ SIGNATURES = {
     "dl_gemm_bf16": (I32, [I32, I32, I32, I32, I32, P, I32, P, I32, P, I32, I32, I32, P, I32, I32, I64, P]),
     "dl_split3": (I32, [P, I32, I32, I32, I32, P, I32, I64, P]),
     "dl_gemm_s3_nt": (I32, [I32, I32, I32, P, I32, P, I32, I64, P, I32, I32, P, I32, P]),
+    "dl_gemm_s3_nt_bits": (I32, [I32, I32, I32, P, I32, P, I32, I64, P, I32, I32, P, I32, P, I32, P]),
     "dl_gemm_s3_tn": (I32, [I32, I32, I32, P, I32, P, I32, P, I32, I32, I64, P]),
     "dl_head_fwd_bwd": (I32, [I32, I32, I32, P, I32, P, I32, P, P, F, F, P, P, P, P, P, I32, P]),
     "dl_head_grid": (I32, [I32]),

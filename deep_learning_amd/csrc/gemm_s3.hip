@@ -86,9 +86,13 @@ struct S3Params {
   long long b_plane;         // NT: elements between the planes of B
   int k_per_split;           // TN
   long long c_split_stride;  // TN
+  uint16_t* bits;            // NT: the ReLU sign bitmask [M][ldbits] (written by S3_RELU, read by S3_MASKBITS)
+  int ldbits;
 };
 
-enum { S3_STORE = 0, S3_RELU = 1, S3_MASK = 2 };
+// S3_MASKBITS: the ReluGrad mask from the forward's bitmask (bit c & 15 of halfword
+// [row][c >> 4] = h[row][c] > 0) instead of the f32 activations — 1/32 of the mask bytes
+enum { S3_STORE = 0, S3_RELU = 1, S3_MASK = 2, S3_MASKBITS = 3 };
 
 #ifndef DL_S3_BPF
 #define DL_S3_BPF 0   // 1: NT pins the next fragment's weight reads ahead of this one's MFMAs
@@ -353,6 +357,31 @@ __global__ __launch_bounds__(512) void gemm_s3_nt_kernel(S3Params p) {
   constexpr int NIT = (16 * VPR + 63) / 64;         // pieces per lane per half
 #pragma unroll
   for (int h = 0; h < 2; ++h) {
+    // the forward's sign bitmask, straight from the accumulators: ballot j of fragment f holds
+    // rows 4kq + j (kq = bit / 16) x columns 16f + (bit % 16); lane r < 16 stores row r's halfword
+    if (EPI == S3_RELU && p.bits) {
+#pragma unroll
+      for (int f = 0; f < kNtNF; ++f) {
+        const uint64_t b0 = __ballot(acc[h][f][0] > 0.f), b1 = __ballot(acc[h][f][1] > 0.f);
+        const uint64_t b2 = __ballot(acc[h][f][2] > 0.f), b3 = __ballot(acc[h][f][3] > 0.f);
+        const int hw = (j0 >> 4) + f, row = r0 + 16 * h + lane;
+        if (lane < 16 && row < p.M && 16 * hw < p.N) {
+          const int jj = lane & 3;
+          const uint64_t b = jj == 0 ? b0 : jj == 1 ? b1 : jj == 2 ? b2 : b3;
+          p.bits[(long long)row * p.ldbits + hw] = (uint16_t)(b >> (16 * (lane >> 2)));
+        }
+      }
+    }
+    uint32_t mb[EPI == S3_MASKBITS ? NIT : 1];
+    if (EPI == S3_MASKBITS) {
+#pragma unroll
+      for (int it = 0; it < NIT; ++it) {
+        const int q = lane + 64 * it;
+        const int rl = q / VPR, pc = q % VPR;
+        const int row = min(r0 + 16 * h + rl, p.M - 1), col = min(j0 + 4 * pc, p.N - 1);
+        mb[it] = (uint32_t)p.bits[(long long)row * p.ldbits + (col >> 4)] >> (col & 15);
+      }
+    }
     // the ReluGrad mask's pieces for this half are loaded first (all in flight together,
     // under the tile's LDS writes), not one dependent round trip per piece
     float4 mk4[EPI == S3_MASK ? NIT : 1];
@@ -380,6 +409,10 @@ __global__ __launch_bounds__(512) void gemm_s3_nt_kernel(S3Params p) {
       float4 v = *reinterpret_cast<const float4*>(tile + rl * kNtEP + 4 * pc);
       if (EPI == S3_RELU) {
         v.x = fmaxf(v.x, 0.f); v.y = fmaxf(v.y, 0.f); v.z = fmaxf(v.z, 0.f); v.w = fmaxf(v.w, 0.f);
+      }
+      if (EPI == S3_MASKBITS) {   // col % 4 == 0: the piece's four bits sit in one halfword
+        const uint32_t m = mb[EPI == S3_MASKBITS ? it : 0];
+        v.x = (m & 1u) ? v.x : 0.f; v.y = (m & 2u) ? v.y : 0.f; v.z = (m & 4u) ? v.z : 0.f; v.w = (m & 8u) ? v.w : 0.f;
       }
       float* dst = p.C + (long long)row * p.ldc + col;
       const float* mk = Mk + (long long)row * p.ldm + col;
@@ -756,9 +789,9 @@ extern "C" int dl_split3(const float* src, int32_t rows, int32_t cols, int32_t l
   DL_RETURN_LAUNCH("dl_split3");
 }
 
-extern "C" int dl_gemm_s3_nt(int32_t M, int32_t N, int32_t K, const float* A, int32_t lda, const uint16_t* Bp,
-                             int32_t ldb, int64_t b_plane, float* C, int32_t ldc, int32_t epi, const float* mask,
-                             int32_t ldm, void* stream) {
+extern "C" int dl_gemm_s3_nt_bits(int32_t M, int32_t N, int32_t K, const float* A, int32_t lda, const uint16_t* Bp,
+                                  int32_t ldb, int64_t b_plane, float* C, int32_t ldc, int32_t epi, const float* mask,
+                                  int32_t ldm, uint16_t* bits, int32_t ldbits, void* stream) {
   DL_CHECK_ARG(M >= 0 && N >= 0 && K >= 0, "negative dims");
   DL_CHECK_ARG(A && Bp && C, "NULL operand");
   DL_CHECK_ARG(K % 8 == 0 && K >= 8, "K %d must be a positive multiple of 8", K);
@@ -766,20 +799,32 @@ extern "C" int dl_gemm_s3_nt(int32_t M, int32_t N, int32_t K, const float* A, in
   DL_CHECK_ARG(((uintptr_t)A % 16) == 0 && ((uintptr_t)Bp % 16) == 0 && b_plane % 8 == 0,
                "A / B planes must be 16-byte aligned");
   DL_CHECK_ARG(b_plane >= (long long)ldb * N, "plane stride too small");
-  DL_CHECK_ARG(epi >= 0 && epi <= 2, "bad epilogue %d", epi);
+  DL_CHECK_ARG(epi >= 0 && epi <= 3, "bad epilogue %d", epi);
   DL_CHECK_ARG(epi != S3_MASK || mask, "mask epilogue needs mask");
+  DL_CHECK_ARG(epi != S3_MASKBITS || bits, "bitmask epilogue needs the bitmask");
+  DL_CHECK_ARG(!bits || ldbits >= (N + 15) / 16, "ldbits %d < %d halfwords", ldbits, (N + 15) / 16);
+  DL_CHECK_ARG(!bits || epi == S3_RELU || epi == S3_MASKBITS, "a bitmask goes with the relu / bitmask epilogues");
   DL_CHECK_ARG((long long)M * lda * 4 < (1LL << 31), "A spans %lld bytes: past the 31-bit buffer range",
                (long long)M * lda * 4);
   if (M == 0 || N == 0) return 0;
   S3Params p{};
   p.A = A; p.B = Bp; p.C = C; p.mask = mask;
   p.M = M; p.N = N; p.K = K; p.lda = lda; p.ldb = ldb; p.ldc = ldc; p.ldm = ldm; p.b_plane = b_plane;
+  p.bits = bits; p.ldbits = ldbits;
   const int tiles = (int)(ceil_div(M, kNtBM) * ceil_div(N, kNtBN));
   hipStream_t s = as_stream(stream);
   if (epi == S3_STORE) hipLaunchKernelGGL(gemm_s3_nt_kernel<S3_STORE>, dim3(tiles), dim3(512), kNtLds, s, p);
   else if (epi == S3_RELU) hipLaunchKernelGGL(gemm_s3_nt_kernel<S3_RELU>, dim3(tiles), dim3(512), kNtLds, s, p);
-  else hipLaunchKernelGGL(gemm_s3_nt_kernel<S3_MASK>, dim3(tiles), dim3(512), kNtLds, s, p);
+  else if (epi == S3_MASK) hipLaunchKernelGGL(gemm_s3_nt_kernel<S3_MASK>, dim3(tiles), dim3(512), kNtLds, s, p);
+  else hipLaunchKernelGGL(gemm_s3_nt_kernel<S3_MASKBITS>, dim3(tiles), dim3(512), kNtLds, s, p);
   DL_RETURN_LAUNCH("dl_gemm_s3_nt");
+}
+
+extern "C" int dl_gemm_s3_nt(int32_t M, int32_t N, int32_t K, const float* A, int32_t lda, const uint16_t* Bp,
+                             int32_t ldb, int64_t b_plane, float* C, int32_t ldc, int32_t epi, const float* mask,
+                             int32_t ldm, void* stream) {
+  DL_CHECK_ARG(epi >= 0 && epi <= 2, "bad epilogue %d", epi);
+  return dl_gemm_s3_nt_bits(M, N, K, A, lda, Bp, ldb, b_plane, C, ldc, epi, mask, ldm, nullptr, 0, stream);
 }
 
 extern "C" int dl_gemm_s3_tn(int32_t M, int32_t N, int32_t K, const float* X, int32_t lda, const float* Y,

@@ -342,6 +342,12 @@ class CTREngine:
             t[:, hdim] = 1.0
             self.h.append(t)
         self.dh = [z(B, self.h_ld[l]) for l in range(len(sp.hidden))]
+        # the forward's ReLU sign bitmasks (s3 tower; dl_gemm_s3_nt_bits): the dX ReluGrad
+        # epilogue reads 2 bytes per 16 columns instead of the f32 activations.
+        # DLAMD_RELU_BITS=0 keeps the f32 mask.
+        self.relu_bits = bool(self.s3 and os.environ.get("DLAMD_RELU_BITS", "1") != "0")
+        self.hbits_ld = [_ru(-(-h // 16), 32) for h in sp.hidden]
+        self.hbits = [z(B, self.hbits_ld[l], dt=torch.int16) for l in range(len(sp.hidden) - 1)] if self.relu_bits else []
         self.bf = sp.tower == "bf16"
         # bf16 tower without pooled fields: the embedding forward writes the bf16 x0 itself
         self.x0_direct = self.bf and not sp.M
@@ -835,9 +841,10 @@ class CTREngine:
         elif self.s3:
             x = self.x0
             for l, hdim in enumerate(sp.hidden):
-                self._c("gemm_fwd_l%d" % l, "dl_gemm_s3_nt", B, hdim, self.in_ld[l], ptr(x), self.in_ld[l],
+                bits = (ptr(self.hbits[l]), self.hbits_ld[l]) if l < len(self.hbits) else (None, 0)
+                self._c("gemm_fwd_l%d" % l, "dl_gemm_s3_nt_bits", B, hdim, self.in_ld[l], ptr(x), self.in_ld[l],
                         ptr(self.WTp[l]), self.in_ld[l], self.in_ld[l] * self.out_ld[l], ptr(self.h[l]),
-                        self.h_ld[l], 1, None, 0, s)
+                        self.h_ld[l], 1, None, 0, *bits, s)
                 x = self.h[l]
         else:
             x = self.x0
@@ -951,7 +958,11 @@ class CTREngine:
                             1, 0, s)
             elif self.s3:   # dX = dY W^T with ReluGrad
                 i, o = self.in_ld[l], self.out_ld[l]
-                if l > 0:
+                if l > 0 and self.relu_bits:   # ReluGrad from the forward's sign bitmask
+                    self._c("gemm_dx_l%d" % l, "dl_gemm_s3_nt_bits", B, sp.hidden[l - 1], o, ptr(self.dh[l]),
+                            self.h_ld[l], ptr(self.Wp[l]), o, i * o, ptr(self.dh[l - 1]), self.h_ld[l - 1], 3,
+                            None, 0, ptr(self.hbits[l - 1]), self.hbits_ld[l - 1], s)
+                elif l > 0:
                     self._c("gemm_dx_l%d" % l, "dl_gemm_s3_nt", B, sp.hidden[l - 1], o, ptr(self.dh[l]),
                             self.h_ld[l], ptr(self.Wp[l]), o, i * o, ptr(self.dh[l - 1]), self.h_ld[l - 1], 2,
                             ptr(self.h[l - 1]), self.h_ld[l - 1], s)

@@ -513,9 +513,10 @@ class ShardedCTREngine(CTREngine):
         x = self.x0
         for l, hdim in enumerate(sp.hidden):
             if self.s3:
-                self._c("gemm_fwd_l%d" % l, "dl_gemm_s3_nt", B, hdim, self.in_ld[l], ptr(x), self.in_ld[l],
+                bits = (ptr(self.hbits[l]), self.hbits_ld[l]) if l < len(self.hbits) else (None, 0)
+                self._c("gemm_fwd_l%d" % l, "dl_gemm_s3_nt_bits", B, hdim, self.in_ld[l], ptr(x), self.in_ld[l],
                         ptr(self.WTp[l]), self.in_ld[l], self.in_ld[l] * self.out_ld[l], ptr(self.h[l]),
-                        self.h_ld[l], 1, None, 0, s)
+                        self.h_ld[l], 1, None, 0, *bits, s)
             else:
                 self._c("gemm_fwd_l%d" % l, "dl_gemm_f32", 0, 0, B, hdim, self.in_ld[l], ptr(x), self.in_ld[l],
                         ptr(self.W[l]), self.out_ld[l], ptr(self.h[l]), self.h_ld[l], 1, None, 0, 1, 0, s)
@@ -585,7 +586,11 @@ class ShardedCTREngine(CTREngine):
                 continue
             if self.s3:
                 i, o = self.in_ld[l], self.out_ld[l]
-                if l > 0:
+                if l > 0 and self.relu_bits:   # ReluGrad from the forward's sign bitmask
+                    self._c("gemm_dx_l%d" % l, "dl_gemm_s3_nt_bits", B, sp.hidden[l - 1], o, ptr(self.dh[l]),
+                            self.h_ld[l], ptr(self.Wp[l]), o, i * o, ptr(self.dh[l - 1]), self.h_ld[l - 1], 3,
+                            None, 0, ptr(self.hbits[l - 1]), self.hbits_ld[l - 1], s)
+                elif l > 0:
                     self._c("gemm_dx_l%d" % l, "dl_gemm_s3_nt", B, sp.hidden[l - 1], o, ptr(self.dh[l]),
                             self.h_ld[l], ptr(self.Wp[l]), o, i * o, ptr(self.dh[l - 1]), self.h_ld[l - 1], 2,
                             ptr(self.h[l - 1]), self.h_ld[l - 1], s)

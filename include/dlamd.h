@@ -281,6 +281,14 @@ int dl_gemm_s3_nt(int32_t M, int32_t N, int32_t K, const float* A, int32_t lda, 
                   int32_t ldm, void* stream);
 int dl_gemm_s3_tn(int32_t M, int32_t N, int32_t K, const float* X, int32_t lda, const float* Y, int32_t ldb,
                   float* C, int32_t ldc, int32_t splits, int64_t c_split_stride, void* stream);
+/* dl_gemm_s3_nt_bits: dl_gemm_s3_nt with the ReLU sign bitmask — bits [M][ldbits] uint16,
+ * bit (c & 15) of halfword [i][c >> 4] = (C[i][c] > 0), ldbits >= ceil(N / 16).  epi 1 (ReLU)
+ * also writes the bitmask when bits != NULL; epi 3 applies the ReluGrad mask from it
+ * (C = bit ? C : 0) in place of epi 2's f32 mask rows: 2 bytes per 16 columns read instead of
+ * 64 (the tower's dX, deepfm_pipeline.py:150-152 gradients). */
+int dl_gemm_s3_nt_bits(int32_t M, int32_t N, int32_t K, const float* A, int32_t lda, const uint16_t* B,
+                       int32_t ldb, int64_t b_plane, float* C, int32_t ldc, int32_t epi, const float* mask,
+                       int32_t ldm, uint16_t* bits, int32_t ldbits, void* stream);
 
 /* ------------------------------------------------------------------------
  * Output layer + sigmoid + eps-log-loss, forward and backward fused

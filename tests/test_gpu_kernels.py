@@ -149,6 +149,38 @@ def test_gemm_s3_nt_matches_fp64(hip_lib, epi, M, N, K):
     assert (C[:, N:].cpu() == 7.0).all()
 
 
+@pytest.mark.parametrize("M,N,K", [(65536, 400, 416), (300, 400, 416), (257, 213, 40), (513, 16, 8)])
+def test_gemm_s3_relu_bitmask_round_trip(hip_lib, M, N, K):
+    """dl_gemm_s3_nt_bits: the ReLU forward writes bit (c & 15) of halfword [i][c >> 4] =
+    (h[i][c] > 0) (checked against the f32 output it writes beside it, every bit of every
+    row, padding halfwords untouched), and the bitmask ReluGrad epilogue (epi 3) gives exactly
+    the f32-mask epilogue's output (epi 2 with the same activations as the mask)."""
+    g = torch.Generator().manual_seed(M + N + K)
+    A = torch.randn(M, K + 4, generator=g).cuda()
+    Bm = (torch.randn(N, K, generator=g) * 0.05).cuda()
+    Bp = _planes(Bm, False)
+    ldc, ldb16 = N + 3, (N + 15) // 16 + 2
+    h = torch.full((M, ldc), 7.0, device="cuda")
+    bits = torch.full((M, ldb16), -1, dtype=torch.int16, device="cuda")
+    call("dl_gemm_s3_nt_bits", M, N, K, ptr(A), K + 4, ptr(Bp), K, N * K, ptr(h), ldc, 1, None, 0,
+         ptr(bits), ldb16, _s())
+    torch.cuda.synchronize()
+    nh = (N + 15) // 16
+    words = bits[:, :nh].to(torch.int32) & 0xFFFF
+    got = ((words[:, :, None] >> torch.arange(16, device="cuda")) & 1).reshape(M, nh * 16)[:, :N].bool()
+    assert torch.equal(got, h[:, :N] > 0)
+    assert (bits[:, nh:] == -1).all()
+    # dX-shaped use: the same bitmask against the f32 mask it encodes
+    dY = torch.randn(M, K + 4, generator=g).cuda()
+    c2 = torch.full((M, ldc), 5.0, device="cuda")
+    c3 = torch.full((M, ldc), 5.0, device="cuda")
+    call("dl_gemm_s3_nt", M, N, K, ptr(dY), K + 4, ptr(Bp), K, N * K, ptr(c2), ldc, 2, ptr(h), ldc, _s())
+    call("dl_gemm_s3_nt_bits", M, N, K, ptr(dY), K + 4, ptr(Bp), K, N * K, ptr(c3), ldc, 3, None, 0,
+         ptr(bits), ldb16, _s())
+    torch.cuda.synchronize()
+    assert torch.equal(c2, c3)
+
+
 @pytest.mark.parametrize("M,N,K,splits", [(432, 400, 65536, 64), (416, 400, 8192, 8), (428, 396, 5000, 3),
                                             (64, 16, 100, 1), (16, 416, 4096, 16)])
 def test_gemm_s3_tn_split_slabs(hip_lib, M, N, K, splits):
