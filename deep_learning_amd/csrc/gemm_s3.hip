@@ -357,21 +357,6 @@ __global__ __launch_bounds__(512) void gemm_s3_nt_kernel(S3Params p) {
   constexpr int NIT = (16 * VPR + 63) / 64;         // pieces per lane per half
 #pragma unroll
   for (int h = 0; h < 2; ++h) {
-    // the forward's sign bitmask, straight from the accumulators: ballot j of fragment f holds
-    // rows 4kq + j (kq = bit / 16) x columns 16f + (bit % 16); lane r < 16 stores row r's halfword
-    if (EPI == S3_RELU && p.bits) {
-#pragma unroll
-      for (int f = 0; f < kNtNF; ++f) {
-        const uint64_t b0 = __ballot(acc[h][f][0] > 0.f), b1 = __ballot(acc[h][f][1] > 0.f);
-        const uint64_t b2 = __ballot(acc[h][f][2] > 0.f), b3 = __ballot(acc[h][f][3] > 0.f);
-        const int hw = (j0 >> 4) + f, row = r0 + 16 * h + lane;
-        if (lane < 16 && row < p.M && 16 * hw < p.N) {
-          const int jj = lane & 3;
-          const uint64_t b = jj == 0 ? b0 : jj == 1 ? b1 : jj == 2 ? b2 : b3;
-          p.bits[(long long)row * p.ldbits + hw] = (uint16_t)(b >> (16 * (lane >> 2)));
-        }
-      }
-    }
     uint32_t mb[EPI == S3_MASKBITS ? NIT : 1];
     if (EPI == S3_MASKBITS) {
 #pragma unroll
@@ -429,6 +414,22 @@ __global__ __launch_bounds__(512) void gemm_s3_nt_kernel(S3Params p) {
           float x = e4[e];
           if (EPI == S3_MASK) x = mk[e] > 0.f ? x : 0.f;
           dst[e] = x;
+        }
+      }
+    }
+    // the forward's sign bitmask, straight from the accumulators (after the half's stores are
+    // issued, so the ballots run while they drain): ballot j of fragment f holds
+    // rows 4kq + j (kq = bit / 16) x columns 16f + (bit % 16); lane r < 16 stores row r's halfword
+    if (EPI == S3_RELU && p.bits) {
+#pragma unroll
+      for (int f = 0; f < kNtNF; ++f) {
+        const uint64_t b0 = __ballot(acc[h][f][0] > 0.f), b1 = __ballot(acc[h][f][1] > 0.f);
+        const uint64_t b2 = __ballot(acc[h][f][2] > 0.f), b3 = __ballot(acc[h][f][3] > 0.f);
+        const int hw = (j0 >> 4) + f, row = r0 + 16 * h + lane;
+        if (lane < 16 && row < p.M && 16 * hw < p.N) {
+          const int jj = lane & 3;
+          const uint64_t b = jj == 0 ? b0 : jj == 1 ? b1 : jj == 2 ? b2 : b3;
+          p.bits[(long long)row * p.ldbits + hw] = (uint16_t)(b >> (16 * (lane >> 2)));
         }
       }
     }

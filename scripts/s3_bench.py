@@ -76,7 +76,7 @@ cases.append(("dx_l1", 2 * B * 400 * 416,
               lambda: (rel(out, refd), rel(out2, refd))))
 # dX l1 with the ReluGrad mask from the forward's sign bitmask (dl_gemm_s3_nt_bits, epi 3)
 hbits = torch.zeros(B, 32, dtype=torch.int16, device="cuda")
-call("dl_gemm_s3_nt_bits", B, 416, 416, ptr(h), 416, ptr(W1T_p), 416, 400 * 416, ptr(out2), 416, 1, None, 0,
+call("dl_gemm_s3_nt_bits", B, 400, 416, ptr(h), 416, ptr(W1T_p), 416, 400 * 416, ptr(out2), 416, 1, None, 0,
      ptr(hbits), 32, s)   # any ReLU output will do as the bitmask source for timing
 cases.append(("dx_l1 bits", 2 * B * 400 * 416,
               lambda: call("dl_gemm_s3_nt_bits", B, 416, 400, ptr(dy), 416, ptr(W1_p), 400, 416 * 400, ptr(out), 416,
