@@ -1074,7 +1074,7 @@ class CTREngine:
         if getattr(self, "side", None) is None:
             # high priority: a hardware queue of its own (a default-priority stream can share
             # the compute stream's queue, which serialises the two)
-            self.side = torch.cuda.Stream(priority=-1)
+            self.side = torch.cuda.Stream(priority=int(os.environ.get("DLAMD_SIDE_PRIORITY", "-1")))
         return self.side
 
     def _use_slot(self, k):

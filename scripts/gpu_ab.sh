@@ -11,15 +11,13 @@ run() {   # run NAME ENV... -- bench args
   local envs=()
   while [ "$1" != "--" ]; do envs+=("$1"); shift; done; shift
   env "${envs[@]}" timeout -k 10 300 python bench.py --no-cpu-baseline --no-extra "$@" > $OUT/bench_$name.json 2> $OUT/bench_$name.err || { tail -5 $OUT/bench_$name.err; return 1; }
-  echo "== $name"; python scripts/bench_brief.py $OUT/bench_$name.json
+  echo "== $name $(python -c "import json;d=json.loads(open('$OUT/bench_$name.json').read().strip().splitlines()[-1]);print(d['ms_per_step'])")"
 }
-run c2_side DLAMD_PF_FUSED=0 -- --steps 20 --warmup 5 || exit 1
-run c2_fused DLAMD_PF_FUSED=1 -- --steps 20 --warmup 5 || exit 1
-run c2_fused_rs8 DLAMD_PF_FUSED=1 DLAMD_VARIANT=rs8 -- --steps 20 --warmup 5 || exit 1
-run c2_side2 DLAMD_PF_FUSED=0 -- --steps 20 --warmup 5 || exit 1
-run c2_fused2 DLAMD_PF_FUSED=1 -- --steps 20 --warmup 5 || exit 1
-run c3_side DLAMD_PF_FUSED=0 -- --workload c3 --steps 10 --warmup 3 || exit 1
-run c3_fused DLAMD_PF_FUSED=1 -- --workload c3 --steps 10 --warmup 3 || exit 1
-run c3_fused_rs8 DLAMD_PF_FUSED=1 DLAMD_VARIANT=rs8 -- --workload c3 --steps 10 --warmup 3 || exit 1
-run c5_side DLAMD_PF_FUSED=0 -- --workload c5 --steps 10 --warmup 3 || exit 1
-run c5_fused DLAMD_PF_FUSED=1 -- --workload c5 --steps 10 --warmup 3 || exit 1
+for i in 1 2; do
+  run c2_nofork$i DLAMD_DW_FORK=0 -- --steps 30 --warmup 5 || exit 1
+  run c2_fork$i DLAMD_DW_FORK=1 -- --steps 30 --warmup 5 || exit 1
+done
+run c3_nofork DLAMD_DW_FORK=0 -- --workload c3 --steps 10 --warmup 3 || exit 1
+run c3_fork DLAMD_DW_FORK=1 -- --workload c3 --steps 10 --warmup 3 || exit 1
+run c5_nofork DLAMD_DW_FORK=0 -- --workload c5 --steps 10 --warmup 3 || exit 1
+run c5_fork DLAMD_DW_FORK=1 -- --workload c5 --steps 10 --warmup 3 || exit 1
