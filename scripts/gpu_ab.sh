@@ -11,13 +11,11 @@ run() {   # run NAME ENV... -- bench args
   local envs=()
   while [ "$1" != "--" ]; do envs+=("$1"); shift; done; shift
   env "${envs[@]}" timeout -k 10 300 python bench.py --no-cpu-baseline --no-extra "$@" > $OUT/bench_$name.json 2> $OUT/bench_$name.err || { tail -5 $OUT/bench_$name.err; return 1; }
-  echo "== $name $(python -c "import json;d=json.loads(open('$OUT/bench_$name.json').read().strip().splitlines()[-1]);print(d['ms_per_step'])")"
+  echo "== $name $(python -c "import json;d=json.loads(open('$OUT/bench_$name.json').read().strip().splitlines()[-1]);print(d['ms_per_step'], {k: v['us'] for k, v in d['kernels'].items() if k.startswith('gemm')})")"
 }
-for i in 1 2; do
-  run c2_nofork$i DLAMD_DW_FORK=0 -- --steps 30 --warmup 5 || exit 1
-  run c2_fork$i DLAMD_DW_FORK=1 -- --steps 30 --warmup 5 || exit 1
+for v in "" bnd2; do
+  DLAMD_VARIANT=$v timeout -k 10 120 python scripts/gemm_bf16_bench.py 20 > $OUT/bf16bench_${v:-d4}.txt 2>&1 || exit 1
+  echo "== bf16 ${v:-d4}"; grep -v amdgpu.ids $OUT/bf16bench_${v:-d4}.txt | head -3
 done
-run c3_nofork DLAMD_DW_FORK=0 -- --workload c3 --steps 10 --warmup 3 || exit 1
-run c3_fork DLAMD_DW_FORK=1 -- --workload c3 --steps 10 --warmup 3 || exit 1
-run c5_nofork DLAMD_DW_FORK=0 -- --workload c5 --steps 10 --warmup 3 || exit 1
-run c5_fork DLAMD_DW_FORK=1 -- --workload c5 --steps 10 --warmup 3 || exit 1
+run c5_d4 DLAMD_VARIANT= -- --workload c5 --steps 20 --warmup 5 || exit 1
+run c5_d2 DLAMD_VARIANT=bnd2 -- --workload c5 --steps 20 --warmup 5 || exit 1
