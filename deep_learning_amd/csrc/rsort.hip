@@ -23,7 +23,10 @@ constexpr int kRsWaves = kRsThreads / 64;
 constexpr int kRsRounds = DL_RS_ROUNDS;                      // elements per lane
 constexpr int kRsTile = kRsThreads * kRsRounds;              // 4096 elements per tile
 constexpr int kRsWaveSpan = 64 * kRsRounds;                  // consecutive elements per wave
-constexpr int kRsMaxBits = 9;
+#ifndef DL_RS_MAXBITS
+#define DL_RS_MAXBITS 9
+#endif
+constexpr int kRsMaxBits = DL_RS_MAXBITS;                    // digit bits per pass at most
 constexpr int kRsMaxRadix = 1 << kRsMaxBits;
 constexpr int kLocal = 27;
 

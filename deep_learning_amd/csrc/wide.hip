@@ -165,6 +165,64 @@ __global__ __launch_bounds__(256) void wide_rec_flush_kernel(float4* __restrict_
   if (sq_untouched) block_atomic_add(sq, sq_untouched);
 }
 
+// The batch's wide gradient per unique wide row, from the wide index instead of atomics:
+// q[u] = sum over the row's references e (sorted positions off[u] .. off[u + 1]) of
+// wide_fixed(dz[e / Fw]) — TF's UnsortedSegmentSum of the cross logit's gradient (wdl.py:
+// 241-264).  Int64 fixed point adds associatively, so the sum is the same bits as the head's
+// per-reference atomics it replaces, in any order.  Pass 1: one thread per unique row for
+// segments up to kWideSegShort references, longer ones (hot ids) appended to a list; pass 2:
+// one block per listed row, the block's threads striding the segment.
+constexpr int kWideSegShort = 64;
+
+__global__ __launch_bounds__(256) void wide_seg_sum_kernel(const float* __restrict__ dz, int Fw,
+                                                           const int32_t* __restrict__ refs,
+                                                           const int32_t* __restrict__ off,
+                                                           const int32_t* __restrict__ n_uniq, long long max_u,
+                                                           long long nrefs, long long* __restrict__ q,
+                                                           int32_t* __restrict__ lng, const float* __restrict__ opt) {
+  int* status = opt_status(opt);
+  const long long nu = min((long long)max(n_uniq[0], 0), max_u);
+  for (long long u = (long long)blockIdx.x * blockDim.x + threadIdx.x; u < nu; u += (long long)gridDim.x * blockDim.x) {
+    const int e0 = off[u], e1 = off[u + 1];
+    if (e0 < 0 || e1 > nrefs || e0 > e1) {
+      raise_fault(status, DL_STATUS_INDEX);
+      q[u] = 0;
+      continue;
+    }
+    if (e1 - e0 > kWideSegShort) {
+      lng[1 + atomicAdd(lng, 1)] = (int32_t)u;
+      continue;
+    }
+    long long acc = 0;
+    for (int e = e0; e < e1; ++e) acc += wide_fixed(dz[refs[e] / Fw]);
+    q[u] = acc;
+  }
+}
+
+__global__ void wide_seg_reset_kernel(int32_t* __restrict__ lng) {
+  if (threadIdx.x == 0) lng[0] = 0;
+}
+
+__global__ __launch_bounds__(256) void wide_seg_long_kernel(const float* __restrict__ dz, int Fw,
+                                                            const int32_t* __restrict__ refs,
+                                                            const int32_t* __restrict__ off,
+                                                            const int32_t* __restrict__ lng, long long* __restrict__ q) {
+  __shared__ long long part[4];
+  const int n = lng[0];
+  for (int i = blockIdx.x; i < n; i += gridDim.x) {
+    const int u = lng[1 + i];
+    const int e0 = off[u], e1 = off[u + 1];
+    long long acc = 0;
+    for (int e = e0 + threadIdx.x; e < e1; e += blockDim.x) acc += wide_fixed(dz[refs[e] / Fw]);
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) acc += __shfl_xor(acc, o, 64);
+    if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = acc;
+    __syncthreads();
+    if (threadIdx.x == 0) q[u] = part[0] + part[1] + part[2] + part[3];
+    __syncthreads();
+  }
+}
+
 static unsigned wide_grid(long long n) {   // grid-stride kernels, one regulariser atomic per block
   long long b = (n + 255) / 256;
   if (b > kSumGrid) b = kSumGrid;
@@ -188,6 +246,21 @@ extern "C" int dl_wide_rec_gather(const float* rec, int64_t w_rows, const uint32
                      reinterpret_cast<const float4*>(rec), (long long)w_rows, uniq_rows, n_uniq, (long long)max_uniq,
                      Fw, H, hist, hist_len, opt, l2, lag, wloc, reinterpret_cast<float4*>(stash));
   DL_RETURN_LAUNCH("dl_wide_rec_gather");
+}
+
+extern "C" int dl_wide_seg_grad(const float* dz, int32_t Fw, const int32_t* refs, const int32_t* seg_off,
+                                const int32_t* n_uniq, int64_t max_uniq, int64_t nrefs, int64_t* q, int32_t* long_ws,
+                                const float* opt, void* stream) {
+  DL_CHECK_ARG(dz && refs && seg_off && n_uniq && q && long_ws && opt, "NULL argument");
+  DL_CHECK_ARG(Fw > 0, "Fw must be positive");
+  if (max_uniq <= 0) return 0;
+  hipStream_t s = as_stream(stream);
+  hipLaunchKernelGGL(wide_seg_reset_kernel, dim3(1), dim3(64), 0, s, long_ws);   // (no memset node in the graph)
+  hipLaunchKernelGGL(wide_seg_sum_kernel, dim3(wide_grid(max_uniq)), dim3(256), 0, s, dz, Fw, refs, seg_off, n_uniq,
+                     (long long)max_uniq, (long long)nrefs, reinterpret_cast<long long*>(q), long_ws, opt);
+  hipLaunchKernelGGL(wide_seg_long_kernel, dim3(256), dim3(256), 0, s, dz, Fw, refs, seg_off, long_ws,
+                     reinterpret_cast<long long*>(q));
+  DL_RETURN_LAUNCH("dl_wide_seg_grad");
 }
 
 extern "C" int dl_wide_rec_update(float* rec, const int32_t* n_uniq, int64_t max_uniq, const float* stash, int64_t* gloc,

@@ -308,6 +308,7 @@ class CTREngine:
             self.wgloc = z(Fw + Hh + nw, dt=torch.int64)
             self.wstash = z(max(nw, 1), 4)
             self.wdmark = z(_ru(Hh, 16), dt=torch.uint8)
+            self.wlong = z(nw + 1, dt=torch.int32)   # dl_wide_seg_grad's hot-row list
             self.wsq = z(4)                      # L2 term of the rows the last step left (from a flush)
             self._wsq_step = -1
             self.in_wide_loc = z(Bm, Fw, dt=torch.int64)
@@ -862,8 +863,11 @@ class CTREngine:
                     1 if train else 0, ptr(self.wloc), ptr(self.wstash) if train else None, s)
             self._c("head", fn, B, sp.Fw, H, ptr(self.in_wide_loc), sp.Fw, ptr(self.h[-1]), self.h_ld[-1],
                     ptr(self.wloc), ptr(self.wb), sp.Fw + H + nw, ptr(self.in_label), sp.logloss_eps, 1.0 / B,
-                    ptr(self.score), ptr(self.z), ptr(self.dz), ptr(dh_last), ptr(self.wgloc) if train else None, None,
+                    ptr(self.score), ptr(self.z), ptr(self.dz), ptr(dh_last), None, None,
                     ptr(self.head_slab), self.head_blocks, ptr(self.err), s)
+            if train:   # the wide rows' gradient: segment sums over the wide index (no atomics)
+                self._c("wide_grad", "dl_wide_seg_grad", ptr(self.dz), sp.Fw, ptr(self.widx_refs), ptr(self.widx_off),
+                        ptr(self.widx_n), nw, nw, ptr(self.wgloc[sp.Fw + H:]), ptr(self.wlong), ptr(self.opt), s)
             return
         if self.wdl:
             # bf16 tower: dY of the last layer written as bf16 by the head itself (no cast pass)

@@ -556,6 +556,11 @@ int dl_wide_local_ids(const int32_t* inv, int64_t n, int64_t offset, int64_t* ou
  * dl_wide_rec_gather: the deep-output rows Fw..Fw+H and the unique wide rows uniq_rows[u]
  * (dl_index_build keys, world 1) caught up to step opt[7] - lag into the head's local table
  * wloc = [— (Fw) | deep rows (H) | unique rows]; stash[u] (may be NULL) = {w, m, v, row bits}.
+ * dl_wide_seg_grad: the batch's wide-weight gradient per unique wide row from the wide index
+ *   (dl_index_build over the wide ids: sorted references `refs`, segment offsets `seg_off`, count
+ *   n_uniq on the device): q[u] = sum over the row's references e of wide_fixed(dz[e / Fw]), int64
+ *   fixed point (DL_WIDE_GRAD_SCALE) — the same bits as the head's per-reference atomics, without
+ *   them (the head then runs with g_w = NULL).  long_ws: int32 [max_uniq + 1] scratch (hot rows).
  * dl_wide_rec_update: step opt[7] on the unique rows (gradient gloc[Fw + H + u] + the deep
  * term gloc[row] of a row in Fw..Fw+H, exact int64, + l2 w) from the stash, then on the deep
  * rows not covered; gloc reset; sum of pre-update w^2 added to sq_out (may be NULL).
@@ -564,6 +569,8 @@ int dl_wide_local_ids(const int32_t* inv, int64_t n, int64_t offset, int64_t* ou
 int dl_wide_rec_gather(const float* rec, int64_t w_rows, const uint32_t* uniq_rows, const int32_t* n_uniq,
                        int64_t max_uniq, int32_t Fw, int32_t H, const float* hist, int32_t hist_len,
                        const float* opt, float l2, int32_t lag, float* wloc, float* stash, void* stream);
+int dl_wide_seg_grad(const float* dz, int32_t Fw, const int32_t* refs, const int32_t* seg_off, const int32_t* n_uniq,
+                     int64_t max_uniq, int64_t nrefs, int64_t* q, int32_t* long_ws, const float* opt, void* stream);
 int dl_wide_rec_update(float* rec, const int32_t* n_uniq, int64_t max_uniq, const float* stash, int64_t* gloc,
                        int32_t Fw, int32_t H, float l2, const float* hist, int32_t hist_len,
                        const float* opt, uint8_t* dmark, float* sq_out, void* stream);
