@@ -7,7 +7,10 @@
 // next read: for each skipped step j, g = l2 * w (the dense sweep's gradient of an untouched
 // row), then the same adam_elem — bit-identical to the sweep, only computed later.
 //
-// Record per row: float4 {w, m, v, stamp} (stamp = int32 bits of the last step applied).
+// Record per row: float4 {w, m, v, stamp} (stamp = int32 bits of the last step applied) at the
+// start of a 128-B slot (kWideRecF4 float4s, the rest zero): an update writes the whole slot, so
+// no partly written line is merged with its old bytes below the L2 (a random 16-B record write
+// would cost a line read besides the write).
 // One step (single GPU, the batch's wide ids indexed by dl_index_build):
 //   dl_wide_rec_gather   unique wide rows + the H deep-output rows caught up to t - lag, into
 //                        the head's compact local table wloc = [— (Fw) | deep rows Fw..Fw+H |
@@ -22,6 +25,17 @@
 #include "common.h"
 
 namespace dl {
+
+constexpr int kWideRecF4 = 8;   // float4s per record slot (128 B)
+
+// the whole slot: the record, then zeros
+__device__ __forceinline__ void wide_rec_store(float4* __restrict__ rec, long long row, float4 r) {
+  float4* q = rec + row * kWideRecF4;
+  q[0] = r;
+  const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+  for (int i = 1; i < kWideRecF4; ++i) q[i] = z;
+}
 
 struct WideHyper {
   float b1, b2, omb1, omb2, eps, l2;
@@ -71,7 +85,7 @@ __global__ __launch_bounds__(256) void wide_rec_gather_kernel(const float4* __re
       raise_fault(status, DL_STATUS_INDEX);
       continue;
     }
-    float4 r = rec[row];
+    float4 r = rec[row * kWideRecF4];
     const int from = wide_from(r.w, target, hist_len, status);
     if (from < target) wide_catch_up(r.x, r.y, r.z, from, target, hist, h);
     wloc[Fw + i] = r.x;   // i < H: the deep-output row Fw + i; else local row Fw + H + u
@@ -107,7 +121,7 @@ __global__ __launch_bounds__(256) void wide_rec_update_kernel(float4* __restrict
     float w = s.x, m = s.y, v = s.z;
     sq += w * w;
     adam_elem(w, m, v, wide_l2_grad(wide_float(q), h.l2, w), alpha, h.omb1, h.omb2, h.eps);
-    rec[row] = make_float4(w, m, v, __int_as_float(t));
+    wide_rec_store(rec, row, make_float4(w, m, v, __int_as_float(t)));
   }
   if (sq_out) block_atomic_add(sq, sq_out);
 }
@@ -132,12 +146,12 @@ __global__ __launch_bounds__(256) void wide_rec_update_deep_kernel(float4* __res
       continue;
     }
     if (skip) continue;
-    float4 r = rec[row];
+    float4 r = rec[row * kWideRecF4];
     const int from = wide_from(r.w, t - 1, hist_len, opt_status(opt));
     if (from < t - 1) wide_catch_up(r.x, r.y, r.z, from, t - 1, hist, h);
     sq += r.x * r.x;
     adam_elem(r.x, r.y, r.z, wide_l2_grad(wide_float(q), h.l2, r.x), alpha, h.omb1, h.omb2, h.eps);
-    rec[row] = make_float4(r.x, r.y, r.z, __int_as_float(t));
+    wide_rec_store(rec, row, make_float4(r.x, r.y, r.z, __int_as_float(t)));
   }
   if (sq_out) block_atomic_add(sq, sq_out);
 }
@@ -154,13 +168,13 @@ __global__ __launch_bounds__(256) void wide_rec_flush_kernel(float4* __restrict_
   float sq = 0.f;
   for (long long row = (long long)blockIdx.x * blockDim.x + threadIdx.x; row < w_rows;
        row += (long long)gridDim.x * blockDim.x) {
-    float4 r = rec[row];
+    float4 r = rec[row * kWideRecF4];   // (the sweep reads every slot's line: the record alone is written back)
     const int from = wide_from(r.w, t, hist_len, opt_status(opt));
     if (from >= t) continue;
     if (from < t - 1) wide_catch_up(r.x, r.y, r.z, from, t - 1, hist, h);
     sq += r.x * r.x;
     wide_catch_up(r.x, r.y, r.z, t - 1, t, hist, h);
-    rec[row] = make_float4(r.x, r.y, r.z, __int_as_float(t));
+    rec[row * kWideRecF4] = make_float4(r.x, r.y, r.z, __int_as_float(t));
   }
   if (sq_untouched) block_atomic_add(sq, sq_untouched);
 }

@@ -303,7 +303,7 @@ class CTREngine:
         if self.wide_lazy:
             Fw, Hh, Bm = sp.Fw, sp.hidden[-1], max_batch
             nw = Bm * Fw
-            self.wrec = z(_ru(self.w_rows, 16), 4)
+            self.wrec = z(_ru(self.w_rows, 16), 32)   # 128-B slots: {w, m, v, stamp} + zeros (wide.hip)
             self.wloc = z(_ru(Fw + Hh + nw, 4))
             self.wgloc = z(Fw + Hh + nw, dt=torch.int64)
             self.wstash = z(max(nw, 1), 4)

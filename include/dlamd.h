@@ -550,8 +550,9 @@ int dl_wide_owned_values(const float* w, int32_t H, int64_t row0, int32_t world,
                          void* stream);
 int dl_wide_local_ids(const int32_t* inv, int64_t n, int64_t offset, int64_t* out, void* stream);
 /* Lazy-exact TF1 Adam for Wide&Deep's wide weights (wide.hip; models/wdl.py:241-285, L2 on
- * every row: TF's dense gradient l2 * w reaches every row each step).  rec [w_rows][4] =
- * {w, m, v, stamp}; a row's skipped steps are replayed on read (g = l2 * w, adam_elem),
+ * every row: TF's dense gradient l2 * w reaches every row each step).  rec [w_rows][32] f32:
+ * 128-B slots {w, m, v, stamp, 0 ...} (an update writes the whole slot: no partial-line
+ * merge); a row's skipped steps are replayed on read (g = l2 * w, adam_elem),
  * bit-identical to the dense dl_adam_rows sweep.
  * dl_wide_rec_gather: the deep-output rows Fw..Fw+H and the unique wide rows uniq_rows[u]
  * (dl_index_build keys, world 1) caught up to step opt[7] - lag into the head's local table

@@ -287,3 +287,19 @@ def test_native_reader_wire_variants(tmp_path):
     np.testing.assert_array_equal(b["cont"], [[1.5, -2.0]] * 3)
     np.testing.assert_array_equal(b["ids"], [[7, -3]] * 3)
     np.testing.assert_array_equal(b["label"], [[1.0]] * 3)
+
+
+def test_s3_dw_split_counts():
+    """engine._s3_dw_splits: the split-K count of an s3 weight gradient fills the CUs in as few
+    rounds of 128 x 224 blocks as possible (C2's 8-tile layers keep 32 slabs; C3's layer 0,
+    M = 528 = 10 tiles, takes 25 — one round of 250 blocks, not two of 320), never more than
+    the cap, at least one."""
+    from deep_learning_amd.engine import _s3_dw_splits
+    assert _s3_dw_splits(432, 400, 65536, 32) == 32
+    assert _s3_dw_splits(416, 400, 65536, 32) == 32
+    assert _s3_dw_splits(528, 400, 65536, 32) == 25
+    assert _s3_dw_splits(432, 400, 1536, 1) == 1
+    for M in (16, 100, 432, 528, 1000):
+        for base in (1, 7, 32, 64):
+            s = _s3_dw_splits(M, 400, 65536, base)
+            assert 1 <= s <= base
