@@ -118,6 +118,7 @@ SIGNATURES = {
     "dl_wide_owned_values": (I32, [P, I32, I64, I32, I32, P, P]),
     "dl_wide_local_ids": (I32, [P, I64, I64, P, P]),
     "dl_wide_rec_gather": (I32, [P, I64, P, P, I64, I32, I32, P, I32, P, F, I32, P, P, P]),
+    "dl_wide_update_blocks": (I64, [I64, I32]),
     "dl_wide_seg_grad": (I32, [P, I32, P, P, P, I64, I64, P, P, P, P]),
     "dl_wide_rec_update": (I32, [P, P, I64, P, P, I32, I32, F, P, I32, P, P, P, P]),
     "dl_wide_rec_flush": (I32, [P, I64, F, P, I32, P, P, P]),

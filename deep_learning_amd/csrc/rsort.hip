@@ -279,7 +279,12 @@ int rsort_pairs(const RsSource& src, int64_t n, uint32_t lrange, int bits, void*
   int32_t* tv = reinterpret_cast<int32_t*>(w); w += rs_align((size_t)n * 4);
   int32_t* counts = reinterpret_cast<int32_t*>(w); w += rs_align((size_t)kRsMaxRadix * tiles * 4);
   int32_t* total = reinterpret_cast<int32_t*>(w);
-  const int passes = (bits + kRsMaxBits - 1) / kRsMaxBits;
+  // digit width: up to 9 bits a pass; for large sorts (C3's 51 M candidate references) at
+  // most 8 — one more pass, but longer runs per digit in each tile's scatter (25-bit keys:
+  // 7/6/6/6 instead of 9/8/8; C3 index 1,033 -> 871 us, step 4.48 -> 4.39 ms), while C2's
+  // 3.4 M-pair sort measured slower as a step with the extra pass (profiles/r03t/)
+  const int maxb = n >= (int64_t)(8 << 20) ? min(8, kRsMaxBits) : kRsMaxBits;
+  const int passes = (bits + maxb - 1) / maxb;
   int shift = 0;
   const uint32_t* kin = nullptr;
   const int32_t* vin = nullptr;

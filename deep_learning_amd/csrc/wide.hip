@@ -7,10 +7,10 @@
 // next read: for each skipped step j, g = l2 * w (the dense sweep's gradient of an untouched
 // row), then the same adam_elem — bit-identical to the sweep, only computed later.
 //
-// Record per row: float4 {w, m, v, stamp} (stamp = int32 bits of the last step applied) at the
-// start of a 128-B slot (kWideRecF4 float4s, the rest zero): an update writes the whole slot, so
-// no partly written line is merged with its old bytes below the L2 (a random 16-B record write
-// would cost a line read besides the write).
+// Record per row: float4 {w, m, v, stamp} (stamp = int32 bits of the last step applied).
+// (128-B slots written whole, to spare the partial-line merges of the random updates, measured
+// slower: update 70 -> 92 us, gather 58 -> 69 us at C5 — 8x the table's span for the random
+// accesses; profiles/r03t/.)
 // One step (single GPU, the batch's wide ids indexed by dl_index_build):
 //   dl_wide_rec_gather   unique wide rows + the H deep-output rows caught up to t - lag, into
 //                        the head's compact local table wloc = [— (Fw) | deep rows Fw..Fw+H |
@@ -26,7 +26,7 @@
 
 namespace dl {
 
-constexpr int kWideRecF4 = 8;   // float4s per record slot (128 B)
+constexpr int kWideRecF4 = 1;   // float4s per record slot
 
 // the whole slot: the record, then zeros
 __device__ __forceinline__ void wide_rec_store(float4* __restrict__ rec, long long row, float4 r) {
@@ -35,6 +35,27 @@ __device__ __forceinline__ void wide_rec_store(float4* __restrict__ rec, long lo
   const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
   for (int i = 1; i < kWideRecF4; ++i) q[i] = z;
+}
+
+// per-block partial sums of the L2 term (every thread of the block calls it): written, not
+// added, so the update kernels need no grid cap for atomics; the host sums the partials
+__device__ __forceinline__ void block_sum_store(float x, float* out) {
+  __shared__ float part[16];
+  x = wave_sum(x);
+  if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = x;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float t = 0.f;
+    for (int w = 0; w < (int)(blockDim.x >> 6); ++w) t += part[w];
+    *out = t;
+  }
+}
+
+// uncapped grid of a one-thread-per-row kernel (the chains of dependent loads want every row in flight)
+static unsigned wide_rows_grid(long long n) {
+  long long b = (n + 255) / 256;
+  if (b > 65535) b = 65535;
+  return (unsigned)(b < 1 ? 1 : b);
 }
 
 struct WideHyper {
@@ -123,7 +144,7 @@ __global__ __launch_bounds__(256) void wide_rec_update_kernel(float4* __restrict
     adam_elem(w, m, v, wide_l2_grad(wide_float(q), h.l2, w), alpha, h.omb1, h.omb2, h.eps);
     wide_rec_store(rec, row, make_float4(w, m, v, __int_as_float(t)));
   }
-  if (sq_out) block_atomic_add(sq, sq_out);
+  if (sq_out) block_sum_store(sq, sq_out + blockIdx.x);
 }
 
 // Pass B: the H deep-output rows pass A did not cover (their gradient: the deep term alone).
@@ -153,7 +174,7 @@ __global__ __launch_bounds__(256) void wide_rec_update_deep_kernel(float4* __res
     adam_elem(r.x, r.y, r.z, wide_l2_grad(wide_float(q), h.l2, r.x), alpha, h.omb1, h.omb2, h.eps);
     wide_rec_store(rec, row, make_float4(r.x, r.y, r.z, __int_as_float(t)));
   }
-  if (sq_out) block_atomic_add(sq, sq_out);
+  if (sq_out) block_sum_store(sq, sq_out + blockIdx.x);
 }
 
 // Every row caught up to step opt[7].  Rows the last step did not touch (stamp < t) pass
@@ -256,10 +277,14 @@ extern "C" int dl_wide_rec_gather(const float* rec, int64_t w_rows, const uint32
   DL_CHECK_ARG(((uintptr_t)rec % 16) == 0 && ((uintptr_t)stash % 16) == 0, "rec / stash must be 16-B aligned");
   const long long n = H + (max_uniq > 0 ? max_uniq : 0);
   if (n == 0) return 0;
-  hipLaunchKernelGGL(wide_rec_gather_kernel, dim3(wide_grid(n)), dim3(256), 0, as_stream(stream),
+  hipLaunchKernelGGL(wide_rec_gather_kernel, dim3(wide_rows_grid(n)), dim3(256), 0, as_stream(stream),
                      reinterpret_cast<const float4*>(rec), (long long)w_rows, uniq_rows, n_uniq, (long long)max_uniq,
                      Fw, H, hist, hist_len, opt, l2, lag, wloc, reinterpret_cast<float4*>(stash));
   DL_RETURN_LAUNCH("dl_wide_rec_gather");
+}
+
+extern "C" int64_t dl_wide_update_blocks(int64_t max_uniq, int32_t H) {
+  return (max_uniq > 0 ? wide_rows_grid(max_uniq) : 0) + (H > 0 ? wide_rows_grid(H) : 0);
 }
 
 extern "C" int dl_wide_seg_grad(const float* dz, int32_t Fw, const int32_t* refs, const int32_t* seg_off,
@@ -270,7 +295,9 @@ extern "C" int dl_wide_seg_grad(const float* dz, int32_t Fw, const int32_t* refs
   if (max_uniq <= 0) return 0;
   hipStream_t s = as_stream(stream);
   hipLaunchKernelGGL(wide_seg_reset_kernel, dim3(1), dim3(64), 0, s, long_ws);   // (no memset node in the graph)
-  hipLaunchKernelGGL(wide_seg_sum_kernel, dim3(wide_grid(max_uniq)), dim3(256), 0, s, dz, Fw, refs, seg_off, n_uniq,
+  // one thread per unique row (no regulariser atomic here, so no grid cap: the chain
+  // offsets -> references -> dz is latency-bound and wants every row in flight at once)
+  hipLaunchKernelGGL(wide_seg_sum_kernel, dim3(wide_rows_grid(max_uniq)), dim3(256), 0, s, dz, Fw, refs, seg_off, n_uniq,
                      (long long)max_uniq, (long long)nrefs, reinterpret_cast<long long*>(q), long_ws, opt);
   hipLaunchKernelGGL(wide_seg_long_kernel, dim3(256), dim3(256), 0, s, dz, Fw, refs, seg_off, long_ws,
                      reinterpret_cast<long long*>(q));
@@ -285,13 +312,14 @@ extern "C" int dl_wide_rec_update(float* rec, const int32_t* n_uniq, int64_t max
   DL_CHECK_ARG(Fw >= 0 && H >= 0, "bad Fw / H");
   hipStream_t s = as_stream(stream);
   if (max_uniq > 0)
-    hipLaunchKernelGGL(wide_rec_update_kernel, dim3(wide_grid(max_uniq)), dim3(256), 0, s,
+    hipLaunchKernelGGL(wide_rec_update_kernel, dim3(wide_rows_grid(max_uniq)), dim3(256), 0, s,
                        reinterpret_cast<float4*>(rec), n_uniq, (long long)max_uniq,
                        reinterpret_cast<const float4*>(stash), reinterpret_cast<long long*>(gloc), Fw, H, l2, hist_len,
-                       opt, dmark, sq_out);
+                       opt, dmark, sq_out);   // partials [0, wide_rows_grid(max_uniq))
   if (H > 0)
-    hipLaunchKernelGGL(wide_rec_update_deep_kernel, dim3(wide_grid(H)), dim3(256), 0, s, reinterpret_cast<float4*>(rec),
-                       reinterpret_cast<long long*>(gloc), Fw, H, l2, hist, hist_len, opt, dmark, sq_out);
+    hipLaunchKernelGGL(wide_rec_update_deep_kernel, dim3(wide_rows_grid(H)), dim3(256), 0, s, reinterpret_cast<float4*>(rec),
+                       reinterpret_cast<long long*>(gloc), Fw, H, l2, hist, hist_len, opt, dmark,
+                       sq_out ? sq_out + (max_uniq > 0 ? wide_rows_grid(max_uniq) : 0) : nullptr);
   DL_RETURN_LAUNCH("dl_wide_rec_update");
 }
 

@@ -303,12 +303,14 @@ class CTREngine:
         if self.wide_lazy:
             Fw, Hh, Bm = sp.Fw, sp.hidden[-1], max_batch
             nw = Bm * Fw
-            self.wrec = z(_ru(self.w_rows, 16), 32)   # 128-B slots: {w, m, v, stamp} + zeros (wide.hip)
+            self.wrec = z(_ru(self.w_rows, 16), 4)    # {w, m, v, stamp} (wide.hip)
             self.wloc = z(_ru(Fw + Hh + nw, 4))
             self.wgloc = z(Fw + Hh + nw, dt=torch.int64)
             self.wstash = z(max(nw, 1), 4)
             self.wdmark = z(_ru(Hh, 16), dt=torch.uint8)
             self.wlong = z(nw + 1, dt=torch.int32)   # dl_wide_seg_grad's hot-row list
+            # the update kernels' per-block partial sums of the touched rows' L2 term
+            self.wsq_part = z(max(1, int(_lib.lib().dl_wide_update_blocks(nw, Hh))))
             self.wsq = z(4)                      # L2 term of the rows the last step left (from a flush)
             self._wsq_step = -1
             self.in_wide_loc = z(Bm, Fw, dt=torch.int64)
@@ -1035,7 +1037,7 @@ class CTREngine:
                     ptr(self.head_slab[:, H:]), hb, H + 2, 1, 0.0, 0, ptr(self.opt), None, None, s)
             self._c("adam_wide", "dl_wide_rec_update", ptr(self.wrec), ptr(self.widx_n), B * sp.Fw, ptr(self.wstash),
                     ptr(self.wgloc), sp.Fw, H, sp.l2, ptr(self.hist), self.hist_len, ptr(self.opt), ptr(self.wdmark),
-                    ptr(self.opt[8:]), s)
+                    ptr(self.wsq_part), s)
             return
         if self.wdl:
             # wdl_weights: dense Adam with L2 on every row (wdl.py:270-271); the deep-output
@@ -1239,7 +1241,7 @@ class CTREngine:
         if getattr(self, "wide_lazy", False):
             # the wide rows the step left untouched: their L2 term from a flush (wide.hip)
             self._wide_flush()
-            reg += float(self.wsq[0].item())
+            reg += float(self.wsq[0].item()) + float(self.wsq_part.double().sum().item())
         return data + sp.l2 * 0.5 * reg
 
     # ------------------------------------------------------------------ errors

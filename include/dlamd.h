@@ -550,9 +550,8 @@ int dl_wide_owned_values(const float* w, int32_t H, int64_t row0, int32_t world,
                          void* stream);
 int dl_wide_local_ids(const int32_t* inv, int64_t n, int64_t offset, int64_t* out, void* stream);
 /* Lazy-exact TF1 Adam for Wide&Deep's wide weights (wide.hip; models/wdl.py:241-285, L2 on
- * every row: TF's dense gradient l2 * w reaches every row each step).  rec [w_rows][32] f32:
- * 128-B slots {w, m, v, stamp, 0 ...} (an update writes the whole slot: no partial-line
- * merge); a row's skipped steps are replayed on read (g = l2 * w, adam_elem),
+ * every row: TF's dense gradient l2 * w reaches every row each step).  rec [w_rows][4] =
+ * {w, m, v, stamp}; a row's skipped steps are replayed on read (g = l2 * w, adam_elem),
  * bit-identical to the dense dl_adam_rows sweep.
  * dl_wide_rec_gather: the deep-output rows Fw..Fw+H and the unique wide rows uniq_rows[u]
  * (dl_index_build keys, world 1) caught up to step opt[7] - lag into the head's local table
@@ -564,12 +563,14 @@ int dl_wide_local_ids(const int32_t* inv, int64_t n, int64_t offset, int64_t* ou
  *   them (the head then runs with g_w = NULL).  long_ws: int32 [max_uniq + 1] scratch (hot rows).
  * dl_wide_rec_update: step opt[7] on the unique rows (gradient gloc[Fw + H + u] + the deep
  * term gloc[row] of a row in Fw..Fw+H, exact int64, + l2 w) from the stash, then on the deep
- * rows not covered; gloc reset; sum of pre-update w^2 added to sq_out (may be NULL).
+ * rows not covered; gloc reset; the pre-update w^2 of those rows as per-block partial sums
+ * written to sq_out[0 .. dl_wide_update_blocks(max_uniq, H)) (may be NULL; the caller sums).
  * dl_wide_rec_flush: every row caught up to step opt[7]; the pre-update w^2 of the rows the
  * last step left untouched (the loss's L2 term for them) added to sq_untouched. */
 int dl_wide_rec_gather(const float* rec, int64_t w_rows, const uint32_t* uniq_rows, const int32_t* n_uniq,
                        int64_t max_uniq, int32_t Fw, int32_t H, const float* hist, int32_t hist_len,
                        const float* opt, float l2, int32_t lag, float* wloc, float* stash, void* stream);
+int64_t dl_wide_update_blocks(int64_t max_uniq, int32_t H);
 int dl_wide_seg_grad(const float* dz, int32_t Fw, const int32_t* refs, const int32_t* seg_off, const int32_t* n_uniq,
                      int64_t max_uniq, int64_t nrefs, int64_t* q, int32_t* long_ws, const float* opt, void* stream);
 int dl_wide_rec_update(float* rec, const int32_t* n_uniq, int64_t max_uniq, const float* stash, int64_t* gloc,

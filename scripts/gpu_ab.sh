@@ -13,13 +13,6 @@ run() {   # run NAME ENV... -- bench args
   env "${envs[@]}" timeout -k 10 300 python bench.py --no-cpu-baseline --no-extra "$@" > $OUT/bench_$name.json 2> $OUT/bench_$name.err || { tail -5 $OUT/bench_$name.err; return 1; }
   echo "== $name $(python -c "import json;d=json.loads(open('$OUT/bench_$name.json').read().strip().splitlines()[-1]);k=d['kernels'];print(d['ms_per_step'], {n: k[n]['us'] for n in ('head', 'wide_grad', 'adam_wide', 'index_build', 'index_build_wide') if n in k})")"
 }
-for i in 1 2; do
-  run c2_base$i -- --steps 30 --warmup 5 || exit 1
-  run c2_rsb8_$i DLAMD_VARIANT=rsb8 -- --steps 30 --warmup 5 || exit 1
-done
-for i in 1 2; do
-  run c3_base$i -- --workload c3 --steps 10 --warmup 3 || exit 1
-  run c3_rsb8_$i DLAMD_VARIANT=rsb8 -- --workload c3 --steps 10 --warmup 3 || exit 1
-done
-run c5_base -- --workload c5 --steps 20 --warmup 5 || exit 1
-run c5_rsb8 DLAMD_VARIANT=rsb8 -- --workload c5 --steps 20 --warmup 5 || exit 1
+run c5 -- --workload c5 --steps 20 --warmup 5 || exit 1
+run c3 -- --workload c3 --steps 10 --warmup 3 || exit 1
+run c2 -- --steps 30 --warmup 5 || exit 1
