@@ -91,6 +91,7 @@ SIGNATURES = {
     "dl_step_begin": (I32, [P, P, F, F, P, I32, P]),
     "dl_validate_batch": (I32, [LP, P, P, I32, I32, I64, I32, P, P]),
     "dl_adam_dense": (I32, [P, P, P, P, I32, I64, I64, F, I64, P, P, P, P]),
+    "dl_adam_dense_split3": (I32, [P, P, P, P, I32, I64, I32, I32, F, I64, I32, P, P, P, P, P]),
     "dl_adam_dense_reg": (I32, [P, P, P, P, I32, I64, I64, F, I64, I32, P, P, P, P]),
     "dl_adam_rows": (I32, [P, P, P, P, P, I64, I32, F, I32, P, P, P]),
     "dl_init_random": (I32, [P, I64, I32, F, F, U64, U64, P]),

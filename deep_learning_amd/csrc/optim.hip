@@ -58,18 +58,46 @@ __global__ void step_begin_kernel(const int32_t* batch_err, float* opt, float de
 }
 
 
+// One f32 -> its three exact bf16 planes, as gemm_s3.hip's split (v_cvt_pk_bf16_f32, round to
+// nearest even): x = hi + mid + lo.
+typedef __bf16 dl_optim_bf16x2 __attribute__((ext_vector_type(2)));
+typedef float dl_optim_f32x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ unsigned short bf16_rne_hw(float x) {
+  return (unsigned short)(__builtin_bit_cast(uint32_t, __builtin_convertvector((dl_optim_f32x2){x, 0.f}, dl_optim_bf16x2)) &
+                          0xffffu);
+}
+__device__ __forceinline__ void split3_one(float x, unsigned short& h, unsigned short& m, unsigned short& l) {
+#pragma clang fp contract(off)
+  h = bf16_rne_hw(x);
+  const float r = x - __uint_as_float((uint32_t)h << 16);
+  m = bf16_rne_hw(r);
+  const float t = r - __uint_as_float((uint32_t)m << 16);
+  l = bf16_rne_hw(t);
+}
+
+// The s3 tower's operand planes of an updated weight W [rows][cols] (dl_split3's two layouts):
+// wp[q][r][c] and wtp[q][c][r], q = hi, mid, lo; plane stride rows * cols.
+struct Split3Out {
+  unsigned short* wp;
+  unsigned short* wtp;
+  int rows, cols;
+};
+
 // Dense parameter, gradient = sum of partial slabs (+ l2 * p for i < l2_count).
 // REG: 0 = L2 (g += l2 * p, sq_out += p^2: tf.contrib.layers.l2_regularizer), 1 = L1
 // (g += l1 * sign(p), sq_out += |p|: l1_regularizer, models/dnn.py:88-90).
-template <int REG>
+// SPLIT: also writes the updated element's s3 planes (in place of two dl_split3 launches).
+template <int REG, bool SPLIT = false>
 __global__ __launch_bounds__(256) void adam_dense_thread_kernel(float* __restrict__ p, float* __restrict__ m,
                                                                 float* __restrict__ v,
                                                                 const float* __restrict__ slab, int nslab,
                                                                 long long stride, long long n, float l2,
                                                                 long long l2_count, const float* __restrict__ opt,
-                                                                float* __restrict__ p_prev, float* __restrict__ sq_out) {
+                                                                float* __restrict__ p_prev, float* __restrict__ sq_out,
+                                                                Split3Out so = {}) {
   if (step_poisoned(opt)) return;
   const float alpha = opt[3], omb1 = 1.f - opt[4], omb2 = 1.f - opt[5], eps = opt[6];
+  const long long plane = SPLIT ? (long long)so.rows * so.cols : 0;
   float sq = 0.f;
   for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n;
        i += (long long)gridDim.x * blockDim.x) {
@@ -92,6 +120,14 @@ __global__ __launch_bounds__(256) void adam_dense_thread_kernel(float* __restric
     }
     adam_elem(pi, mi, vi, g, alpha, omb1, omb2, eps);
     p[i] = pi; m[i] = mi; v[i] = vi;
+    if (SPLIT) {
+      unsigned short h, mm, l;
+      split3_one(pi, h, mm, l);
+      const int r = (int)(i / so.cols), c = (int)(i - (long long)r * so.cols);
+      so.wp[i] = h; so.wp[plane + i] = mm; so.wp[2 * plane + i] = l;
+      const long long t = (long long)c * so.rows + r;
+      so.wtp[t] = h; so.wtp[plane + t] = mm; so.wtp[2 * plane + t] = l;
+    }
   }
   if (sq_out) block_atomic_add(sq, sq_out);
 }
@@ -327,11 +363,29 @@ extern "C" int dl_adam_dense_reg(float* p, float* m, float* v, const float* slab
   } else {                                                                                                    \
     hipLaunchKernelGGL(adam_dense_thread_kernel<R>, dim3(grid_for(n)), dim3(256), 0, as_stream(stream), p, m, \
                        v, slab, nslab, (long long)slab_stride, (long long)n, reg, (long long)reg_count, opt,    \
-                       p_prev, acc_out);                                                                      \
+                       p_prev, acc_out, Split3Out{});                                                         \
   }
   if (reg_kind == 0) { DL_ADAM_DENSE(0) } else { DL_ADAM_DENSE(1) }
 #undef DL_ADAM_DENSE
   DL_RETURN_LAUNCH("dl_adam_dense_reg");
+}
+
+extern "C" int dl_adam_dense_split3(float* p, float* m, float* v, const float* slab, int32_t nslab,
+                                    int64_t slab_stride, int32_t rows, int32_t cols, float reg, int64_t reg_count,
+                                    int32_t reg_kind, const float* opt, float* acc_out, uint16_t* wp, uint16_t* wtp,
+                                    void* stream) {
+  DL_CHECK_ARG(p && m && v && slab && opt && wp && wtp, "NULL pointer");
+  const long long n = (long long)rows * cols;
+  DL_CHECK_ARG(rows > 0 && cols > 0 && nslab >= 1 && slab_stride >= n, "bad shape / slabs");
+  DL_CHECK_ARG(reg_kind == 0 || reg_kind == 1, "reg_kind must be 0 (L2) or 1 (L1)");
+  const Split3Out so{reinterpret_cast<unsigned short*>(wp), reinterpret_cast<unsigned short*>(wtp), rows, cols};
+  if (reg_kind == 0)
+    hipLaunchKernelGGL((adam_dense_thread_kernel<0, true>), dim3(grid_for(n)), dim3(256), 0, as_stream(stream), p, m, v,
+                       slab, nslab, (long long)slab_stride, n, reg, (long long)reg_count, opt, nullptr, acc_out, so);
+  else
+    hipLaunchKernelGGL((adam_dense_thread_kernel<1, true>), dim3(grid_for(n)), dim3(256), 0, as_stream(stream), p, m, v,
+                       slab, nslab, (long long)slab_stride, n, reg, (long long)reg_count, opt, nullptr, acc_out, so);
+  DL_RETURN_LAUNCH("dl_adam_dense_split3");
 }
 
 extern "C" int dl_adam_dense(float* p, float* m, float* v, const float* slab, int32_t nslab,

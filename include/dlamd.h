@@ -387,6 +387,13 @@ int dl_step_begin(const int32_t* batch_err, float* opt, float decay_rate, float 
  * p_prev (may be NULL) receives the pre-update values; sq_out (may be NULL) gets
  * sum p_pre^2 over the L2-regularised elements added (atomically) — the loss's
  * l2_regularizer term of the step, read back without copying the parameters. */
+/* dl_adam_dense_split3: dl_adam_dense_reg on a tower weight W [rows][cols] (n = rows * cols,
+ * no p_prev) that also writes the updated W's three bf16 planes in dl_split3's two layouts —
+ * wp[q][r][c] and wtp[q][c][r], plane stride rows * cols — in place of two dl_split3 launches
+ * after the update (the s3 GEMMs' operands; deepfm_pipeline.py:184-188 ApplyAdam on W). */
+int dl_adam_dense_split3(float* p, float* m, float* v, const float* slab, int32_t nslab, int64_t slab_stride,
+                         int32_t rows, int32_t cols, float reg, int64_t reg_count, int32_t reg_kind, const float* opt,
+                         float* acc_out, uint16_t* wp, uint16_t* wtp, void* stream);
 int dl_adam_dense(float* p, float* m, float* v, const float* slab, int32_t nslab,
                   int64_t slab_stride, int64_t n, float l2, int64_t l2_count, const float* opt,
                   float* p_prev, float* sq_out, void* stream);

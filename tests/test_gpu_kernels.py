@@ -103,6 +103,53 @@ def _planes(W, transpose):
     return P
 
 
+@pytest.mark.parametrize("rows,cols,reg_kind", [(432, 400, 0), (416, 400, 1), (37, 24, 0)])
+def test_adam_dense_split3_equals_adam_then_split(hip_lib, rows, cols, reg_kind):
+    """dl_adam_dense_split3 (the tower weight's Adam update writing its own s3 planes) against
+    dl_adam_dense_reg followed by the two dl_split3 launches it replaces: W, m, v and both plane
+    layouts bit-identical, the regulariser sum (block atomics) within 1e-5 relative; a poisoned
+    step leaves all unchanged."""
+    g = torch.Generator().manual_seed(rows + cols + reg_kind)
+    n = rows * cols
+    nslab = 5
+    W0 = (torch.randn(rows, cols, generator=g) * 0.05).cuda()
+    m0 = (torch.randn(rows, cols, generator=g) * 1e-3).cuda()
+    v0 = (torch.rand(rows, cols, generator=g) * 1e-6).cuda()
+    slab = (torch.randn(nslab, n, generator=g) * 1e-3).cuda()
+    opt = torch.zeros(_lib.OPT_LEN)
+    opt[3], opt[4], opt[5], opt[6], opt[7] = 1e-3, 0.9, 0.999, 1e-8, 10
+    out = []
+    for fused in (False, True):
+        W, m, v, o = W0.clone(), m0.clone(), v0.clone(), opt.clone().cuda()
+        wp = torch.zeros(3 * n, dtype=torch.int16, device="cuda")
+        wtp = torch.zeros(3 * n, dtype=torch.int16, device="cuda")
+        if fused:
+            call("dl_adam_dense_split3", ptr(W), ptr(m), ptr(v), ptr(slab), nslab, n, rows, cols, 1e-4, n - cols,
+                 reg_kind, ptr(o), ptr(o[8:]), ptr(wp), ptr(wtp), _s())
+        else:
+            call("dl_adam_dense_reg", ptr(W), ptr(m), ptr(v), ptr(slab), nslab, n, n, 1e-4, n - cols, reg_kind,
+                 ptr(o), None, ptr(o[8:]), _s())
+            call("dl_split3", ptr(W), rows, cols, cols, 0, ptr(wp), cols, n, _s())
+            call("dl_split3", ptr(W), rows, cols, cols, 1, ptr(wtp), rows, n, _s())
+        torch.cuda.synchronize()
+        out.append((W, m, v, o[8].item(), wp, wtp))
+    for a, b in zip(out[0], out[1]):
+        if isinstance(a, float):   # the regulariser sum: one float atomic per block, in any order
+            assert abs(a - b) <= 1e-5 * abs(a)
+        else:
+            assert torch.equal(a, b)
+    # a poisoned step (the step guard's skip word) applies nothing and writes no plane
+    W, m, v, o = W0.clone(), m0.clone(), v0.clone(), opt.clone()
+    o[_lib.OPT_SKIP] = 1
+    o = o.cuda()
+    wp = torch.full((3 * n,), 7, dtype=torch.int16, device="cuda")
+    wtp = torch.full((3 * n,), 7, dtype=torch.int16, device="cuda")
+    call("dl_adam_dense_split3", ptr(W), ptr(m), ptr(v), ptr(slab), nslab, n, rows, cols, 1e-4, n - cols,
+         reg_kind, ptr(o), ptr(o[8:]), ptr(wp), ptr(wtp), _s())
+    torch.cuda.synchronize()
+    assert torch.equal(W, W0) and torch.equal(m, m0) and (wp == 7).all() and (wtp == 7).all()
+
+
 def test_split3_is_exact(hip_lib):
     """hi + mid + lo reconstructs every (normal) f32 exactly, each plane a bf16 rounding."""
     g = torch.Generator().manual_seed(3)
