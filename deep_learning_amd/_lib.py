@@ -92,6 +92,7 @@ SIGNATURES = {
     "dl_validate_batch": (I32, [LP, P, P, I32, I32, I64, I32, P, P]),
     "dl_adam_dense": (I32, [P, P, P, P, I32, I64, I64, F, I64, P, P, P, P]),
     "dl_adam_dense_split3": (I32, [P, P, P, P, I32, I64, I32, I32, F, I64, I32, P, P, P, P, P]),
+    "dl_adam_dense_bf16": (I32, [P, P, P, P, I32, I64, I32, I32, F, I64, I32, P, P, P, P, P]),
     "dl_adam_dense_reg": (I32, [P, P, P, P, I32, I64, I64, F, I64, I32, P, P, P, P]),
     "dl_adam_rows": (I32, [P, P, P, P, P, I64, I32, F, I32, P, P, P]),
     "dl_init_random": (I32, [P, I64, I32, F, F, U64, U64, P]),

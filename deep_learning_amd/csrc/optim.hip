@@ -86,8 +86,10 @@ struct Split3Out {
 // Dense parameter, gradient = sum of partial slabs (+ l2 * p for i < l2_count).
 // REG: 0 = L2 (g += l2 * p, sq_out += p^2: tf.contrib.layers.l2_regularizer), 1 = L1
 // (g += l1 * sign(p), sq_out += |p|: l1_regularizer, models/dnn.py:88-90).
-// SPLIT: also writes the updated element's s3 planes (in place of two dl_split3 launches).
-template <int REG, bool SPLIT = false>
+// NPL: also writes the updated element's operand copies (in place of separate launches after
+// the update): 3 = the s3 planes (dl_split3's rounding), 1 = the bf16 copy (dl_cast_bf16 /
+// dl_transpose_bf16's rounding, f2bf), 0 = none.
+template <int REG, int NPL = 0>
 __global__ __launch_bounds__(256) void adam_dense_thread_kernel(float* __restrict__ p, float* __restrict__ m,
                                                                 float* __restrict__ v,
                                                                 const float* __restrict__ slab, int nslab,
@@ -97,7 +99,7 @@ __global__ __launch_bounds__(256) void adam_dense_thread_kernel(float* __restric
                                                                 Split3Out so = {}) {
   if (step_poisoned(opt)) return;
   const float alpha = opt[3], omb1 = 1.f - opt[4], omb2 = 1.f - opt[5], eps = opt[6];
-  const long long plane = SPLIT ? (long long)so.rows * so.cols : 0;
+  const long long plane = NPL ? (long long)so.rows * so.cols : 0;
   float sq = 0.f;
   for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n;
        i += (long long)gridDim.x * blockDim.x) {
@@ -120,13 +122,18 @@ __global__ __launch_bounds__(256) void adam_dense_thread_kernel(float* __restric
     }
     adam_elem(pi, mi, vi, g, alpha, omb1, omb2, eps);
     p[i] = pi; m[i] = mi; v[i] = vi;
-    if (SPLIT) {
+    if (NPL == 3) {
       unsigned short h, mm, l;
       split3_one(pi, h, mm, l);
       const int r = (int)(i / so.cols), c = (int)(i - (long long)r * so.cols);
       so.wp[i] = h; so.wp[plane + i] = mm; so.wp[2 * plane + i] = l;
       const long long t = (long long)c * so.rows + r;
       so.wtp[t] = h; so.wtp[plane + t] = mm; so.wtp[2 * plane + t] = l;
+    } else if (NPL == 1) {
+      const unsigned short h = f2bf(pi);
+      const int r = (int)(i / so.cols), c = (int)(i - (long long)r * so.cols);
+      so.wp[i] = h;
+      so.wtp[(long long)c * so.rows + r] = h;
     }
   }
   if (sq_out) block_atomic_add(sq, sq_out);
@@ -370,22 +377,38 @@ extern "C" int dl_adam_dense_reg(float* p, float* m, float* v, const float* slab
   DL_RETURN_LAUNCH("dl_adam_dense_reg");
 }
 
-extern "C" int dl_adam_dense_split3(float* p, float* m, float* v, const float* slab, int32_t nslab,
-                                    int64_t slab_stride, int32_t rows, int32_t cols, float reg, int64_t reg_count,
-                                    int32_t reg_kind, const float* opt, float* acc_out, uint16_t* wp, uint16_t* wtp,
-                                    void* stream) {
+template <int NPL>
+static int adam_dense_copies(float* p, float* m, float* v, const float* slab, int32_t nslab, int64_t slab_stride,
+                             int32_t rows, int32_t cols, float reg, int64_t reg_count, int32_t reg_kind,
+                             const float* opt, float* acc_out, uint16_t* wp, uint16_t* wtp, void* stream) {
   DL_CHECK_ARG(p && m && v && slab && opt && wp && wtp, "NULL pointer");
   const long long n = (long long)rows * cols;
   DL_CHECK_ARG(rows > 0 && cols > 0 && nslab >= 1 && slab_stride >= n, "bad shape / slabs");
   DL_CHECK_ARG(reg_kind == 0 || reg_kind == 1, "reg_kind must be 0 (L2) or 1 (L1)");
   const Split3Out so{reinterpret_cast<unsigned short*>(wp), reinterpret_cast<unsigned short*>(wtp), rows, cols};
   if (reg_kind == 0)
-    hipLaunchKernelGGL((adam_dense_thread_kernel<0, true>), dim3(grid_for(n)), dim3(256), 0, as_stream(stream), p, m, v,
+    hipLaunchKernelGGL((adam_dense_thread_kernel<0, NPL>), dim3(grid_for(n)), dim3(256), 0, as_stream(stream), p, m, v,
                        slab, nslab, (long long)slab_stride, n, reg, (long long)reg_count, opt, nullptr, acc_out, so);
   else
-    hipLaunchKernelGGL((adam_dense_thread_kernel<1, true>), dim3(grid_for(n)), dim3(256), 0, as_stream(stream), p, m, v,
+    hipLaunchKernelGGL((adam_dense_thread_kernel<1, NPL>), dim3(grid_for(n)), dim3(256), 0, as_stream(stream), p, m, v,
                        slab, nslab, (long long)slab_stride, n, reg, (long long)reg_count, opt, nullptr, acc_out, so);
-  DL_RETURN_LAUNCH("dl_adam_dense_split3");
+  DL_RETURN_LAUNCH(NPL == 3 ? "dl_adam_dense_split3" : "dl_adam_dense_bf16");
+}
+
+extern "C" int dl_adam_dense_split3(float* p, float* m, float* v, const float* slab, int32_t nslab,
+                                    int64_t slab_stride, int32_t rows, int32_t cols, float reg, int64_t reg_count,
+                                    int32_t reg_kind, const float* opt, float* acc_out, uint16_t* wp, uint16_t* wtp,
+                                    void* stream) {
+  return adam_dense_copies<3>(p, m, v, slab, nslab, slab_stride, rows, cols, reg, reg_count, reg_kind, opt, acc_out,
+                              wp, wtp, stream);
+}
+
+extern "C" int dl_adam_dense_bf16(float* p, float* m, float* v, const float* slab, int32_t nslab,
+                                  int64_t slab_stride, int32_t rows, int32_t cols, float reg, int64_t reg_count,
+                                  int32_t reg_kind, const float* opt, float* acc_out, uint16_t* wb, uint16_t* wbt,
+                                  void* stream) {
+  return adam_dense_copies<1>(p, m, v, slab, nslab, slab_stride, rows, cols, reg, reg_count, reg_kind, opt, acc_out,
+                              wb, wbt, stream);
 }
 
 extern "C" int dl_adam_dense(float* p, float* m, float* v, const float* slab, int32_t nslab,

@@ -993,11 +993,11 @@ class CTREngine:
             nsplit = _num_splits(B, dws[l], 64 if (self.bf or self.s3) else 16)
             reg = sp.hidden_reg
             l2, l2n = (sp.l2, ([self.D0] + sp.hidden)[l] * self.out_ld[l]) if reg else (0.0, 0)
-            if self.s3:   # the update writes the s3 planes of W and W^T itself
-                self._c("adam_dense_l%d" % l, "dl_adam_dense_split3", ptr(self.W[l]), ptr(self.Wm[l]), ptr(self.Wv[l]),
+            if self.s3 or self.bf:   # the update writes the GEMM operand copies of W and W^T itself
+                self._c("adam_dense_l%d" % l, "dl_adam_dense_split3" if self.s3 else "dl_adam_dense_bf16", ptr(self.W[l]), ptr(self.Wm[l]), ptr(self.Wv[l]),
                         ptr(self.w_slab), nsplit, stride, self.in_ld[l], self.out_ld[l], l2, l2n,
                         1 if reg == "l1" else 0, ptr(self.opt), ptr(self.opt[8:]) if reg else None,
-                        ptr(self.Wp[l]), ptr(self.WTp[l]), s)
+                        ptr(self.Wp[l] if self.s3 else self.Wb[l]), ptr(self.WTp[l] if self.s3 else self.WbT[l]), s)
                 return
             self._c("adam_dense_l%d" % l, "dl_adam_dense_reg", ptr(self.W[l]), ptr(self.Wm[l]), ptr(self.Wv[l]),
                     ptr(self.w_slab), nsplit, stride, stride, l2, l2n, 1 if reg == "l1" else 0, ptr(self.opt),

@@ -394,6 +394,11 @@ int dl_step_begin(const int32_t* batch_err, float* opt, float decay_rate, float 
 int dl_adam_dense_split3(float* p, float* m, float* v, const float* slab, int32_t nslab, int64_t slab_stride,
                          int32_t rows, int32_t cols, float reg, int64_t reg_count, int32_t reg_kind, const float* opt,
                          float* acc_out, uint16_t* wp, uint16_t* wtp, void* stream);
+/* dl_adam_dense_bf16: the same for the bf16 tower (C5): the updated W's bf16 copy wb [rows][cols]
+ * and its transpose wbt [cols][rows] (dl_cast_bf16 / dl_transpose_bf16's rounding). */
+int dl_adam_dense_bf16(float* p, float* m, float* v, const float* slab, int32_t nslab, int64_t slab_stride,
+                       int32_t rows, int32_t cols, float reg, int64_t reg_count, int32_t reg_kind, const float* opt,
+                       float* acc_out, uint16_t* wb, uint16_t* wbt, void* stream);
 int dl_adam_dense(float* p, float* m, float* v, const float* slab, int32_t nslab,
                   int64_t slab_stride, int64_t n, float l2, int64_t l2_count, const float* opt,
                   float* p_prev, float* sq_out, void* stream);

@@ -103,8 +103,9 @@ def _planes(W, transpose):
     return P
 
 
+@pytest.mark.parametrize("kind", ["s3", "bf16"])
 @pytest.mark.parametrize("rows,cols,reg_kind", [(432, 400, 0), (416, 400, 1), (37, 24, 0)])
-def test_adam_dense_split3_equals_adam_then_split(hip_lib, rows, cols, reg_kind):
+def test_adam_dense_split3_equals_adam_then_split(hip_lib, rows, cols, reg_kind, kind):
     """dl_adam_dense_split3 (the tower weight's Adam update writing its own s3 planes) against
     dl_adam_dense_reg followed by the two dl_split3 launches it replaces: W, m, v and both plane
     layouts bit-identical, the regulariser sum (block atomics) within 1e-5 relative; a poisoned
@@ -124,13 +125,17 @@ def test_adam_dense_split3_equals_adam_then_split(hip_lib, rows, cols, reg_kind)
         wp = torch.zeros(3 * n, dtype=torch.int16, device="cuda")
         wtp = torch.zeros(3 * n, dtype=torch.int16, device="cuda")
         if fused:
-            call("dl_adam_dense_split3", ptr(W), ptr(m), ptr(v), ptr(slab), nslab, n, rows, cols, 1e-4, n - cols,
-                 reg_kind, ptr(o), ptr(o[8:]), ptr(wp), ptr(wtp), _s())
+            call("dl_adam_dense_split3" if kind == "s3" else "dl_adam_dense_bf16", ptr(W), ptr(m), ptr(v), ptr(slab),
+                 nslab, n, rows, cols, 1e-4, n - cols, reg_kind, ptr(o), ptr(o[8:]), ptr(wp), ptr(wtp), _s())
         else:
             call("dl_adam_dense_reg", ptr(W), ptr(m), ptr(v), ptr(slab), nslab, n, n, 1e-4, n - cols, reg_kind,
                  ptr(o), None, ptr(o[8:]), _s())
-            call("dl_split3", ptr(W), rows, cols, cols, 0, ptr(wp), cols, n, _s())
-            call("dl_split3", ptr(W), rows, cols, cols, 1, ptr(wtp), rows, n, _s())
+            if kind == "s3":
+                call("dl_split3", ptr(W), rows, cols, cols, 0, ptr(wp), cols, n, _s())
+                call("dl_split3", ptr(W), rows, cols, cols, 1, ptr(wtp), rows, n, _s())
+            else:   # the bf16 tower's refresh (engine._refresh_wb)
+                call("dl_cast_bf16", ptr(W), rows, cols, cols, ptr(wp), cols, _s())
+                call("dl_transpose_bf16", ptr(W), 1, rows, cols, cols, ptr(wtp), rows, _s())
         torch.cuda.synchronize()
         out.append((W, m, v, o[8].item(), wp, wtp))
     for a, b in zip(out[0], out[1]):
@@ -144,8 +149,8 @@ def test_adam_dense_split3_equals_adam_then_split(hip_lib, rows, cols, reg_kind)
     o = o.cuda()
     wp = torch.full((3 * n,), 7, dtype=torch.int16, device="cuda")
     wtp = torch.full((3 * n,), 7, dtype=torch.int16, device="cuda")
-    call("dl_adam_dense_split3", ptr(W), ptr(m), ptr(v), ptr(slab), nslab, n, rows, cols, 1e-4, n - cols,
-         reg_kind, ptr(o), ptr(o[8:]), ptr(wp), ptr(wtp), _s())
+    call("dl_adam_dense_split3" if kind == "s3" else "dl_adam_dense_bf16", ptr(W), ptr(m), ptr(v), ptr(slab), nslab,
+         n, rows, cols, 1e-4, n - cols, reg_kind, ptr(o), ptr(o[8:]), ptr(wp), ptr(wtp), _s())
     torch.cuda.synchronize()
     assert torch.equal(W, W0) and torch.equal(m, m0) and (wp == 7).all() and (wtp == 7).all()
 
