@@ -1063,6 +1063,134 @@ __global__ __launch_bounds__(320) void gemm_bf16_dw_kernel(GemmParams p) {
     }
 }
 
+// The same weight gradients with a deeper pipeline and fewer operand re-reads: block 144 (m) x
+// 400 (n) — three m tiles for the tower's M = 416 / 432, so each dY slice is read three times
+// (from L2) instead of seven — and 15 waves (3 m groups of 48 rows x 5 n groups of 80 columns,
+// 3 x 5 fragments each).  Per 32-deep batch step the X [32][144] and dY [32][400] bf16 rows land
+// in LDS by LDS-DMA (global_load_lds_dwordx4, 34 one-KB instructions per step) into a ring of four
+// stages issued three steps ahead, so a step waits on no memory round trip (the two-buffer kernel
+// above, with its register-staged next step, paid one per 32 rows: 77 us for a C5 layer).  The
+// images are the operands' plain rows (pitches 144 and 400 bf16 = 8 x odd words: conflict-free
+// transposed reads, as above), so every DMA lane moves one 16-B piece of one row.  Needs whole
+// 32-row steps in every split (K % 32 == 0; the split size is a multiple of 64); pieces past M
+// or N read clamped in-range data whose products only reach discarded outputs.
+constexpr int kD3BM = 144, kD3BN = 400, kD3KS = 32, kD3R = 4, kD3W = 15;
+constexpr int kD3AB = kD3KS * kD3BM * 2, kD3BB = kD3KS * kD3BN * 2;   // image bytes per stage
+constexpr int kD3SB = kD3AB + kD3BB;                                   // 34,816 B
+constexpr int kD3DA = kD3AB / 1024, kD3D = kD3DA + kD3BB / 1024;      // 9 + 25 DMA instructions
+constexpr size_t kD3Lds = (size_t)kD3R * kD3SB;                        // 139,264 B
+static_assert(kD3AB % 1024 == 0 && kD3BB % 1024 == 0 && kD3D == 34, "whole DMA instructions per image");
+static_assert(kD3D <= 3 * kD3W, "at most three DMA instructions per wave and step");
+#ifndef DL_BF16_DW3
+#define DL_BF16_DW3 1   // 0: the two-buffer kernel above for every weight gradient
+#endif
+
+__global__ __launch_bounds__(960) void gemm_bf16_dw3_kernel(GemmParams p) {
+  extern __shared__ __attribute__((aligned(16))) unsigned short lds[];   // [R stages][A image | B image]
+  const unsigned short* __restrict__ X = reinterpret_cast<const unsigned short*>(p.A);
+  const unsigned short* __restrict__ Y = reinterpret_cast<const unsigned short*>(p.B);
+  const int tid = threadIdx.x, lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int mtiles = (p.M + kD3BM - 1) / kD3BM;
+  const int t = xcd_tile(blockIdx.x, gridDim.x);   // the m tiles of one split adjacent: dY's slice shared in L2
+  const int m0 = (t % mtiles) * kD3BM, z = t / mtiles;
+  const int kbeg = z * p.k_per_split;
+  const int kend = min(p.K, kbeg + p.k_per_split);
+  const int nk = (kend - kbeg) / kD3KS;            // whole steps (the host checks K % 32 == 0)
+  const uint32_t lds_base = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) unsigned short*)lds;
+  // This wave's DMA instructions (wave-uniform): waves 0-3 issue three per step, the others two
+  // (34 = 4 x 3 + 11 x 2).  Instruction g < 9 fills A image bytes 1024 g .. +1023 (row o / 288,
+  // piece (o % 288) / 16), g >= 9 the B image's (row o / 800, piece (o % 800) / 16).  The source
+  // row and piece of this lane are fixed per instruction; a step adds 32 rows.
+  const int ndma = wid < 4 ? 3 : 2;
+  const unsigned short* src[3];
+  uint32_t dst[3];
+  int ld[3];
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    const int g = wid < 4 ? 3 * wid + i : 12 + 2 * (wid - 4) + min(i, 1);
+    if (g < kD3DA) {
+      const int o = 1024 * g + 16 * lane, r = o / (2 * kD3BM), m = m0 + ((o % (2 * kD3BM)) >> 1);
+      src[i] = X + (long long)(kbeg + r) * p.lda + (m < p.M ? m : 0);
+      dst[i] = 1024u * g;
+      ld[i] = p.lda;
+    } else {
+      const int o = 1024 * (g - kD3DA) + 16 * lane, r = o / (2 * kD3BN), n = (o % (2 * kD3BN)) >> 1;
+      src[i] = Y + (long long)(kbeg + r) * p.ldb + (n < p.N ? n : 0);
+      dst[i] = (uint32_t)kD3AB + 1024u * (g - kD3DA);
+      ld[i] = p.ldb;
+    }
+  }
+  // step c's rows into stage c % R; steps past this split's range re-read its last step (the
+  // stage is never computed on), so every wave issues the same count every step
+  auto dma = [&](int c) {
+    const long long dk = (long long)min(c, nk - 1) * kD3KS;
+    const uint32_t sb = lds_base + (uint32_t)((c % kD3R) * kD3SB);
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+      if (i < ndma) {
+        const unsigned short* sp = src[i] + dk * ld[i];
+        unsigned keep;
+        asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+                     : "=&s"(keep) : "v"(sp), "s"(__builtin_amdgcn_readfirstlane(sb + dst[i])) : "memory");
+      }
+    }
+  };
+  floatx4 acc[3][5];
+#pragma unroll
+  for (int a = 0; a < 3; ++a)
+#pragma unroll
+    for (int b = 0; b < 5; ++b) acc[a][b] = floatx4{0.f, 0.f, 0.f, 0.f};
+  const int wm = wid / 5, wn = wid % 5;
+  const int cl = lane & 15, kq = lane >> 4, rq = cl >> 2, cp = cl & 3;
+  const int ra = 4 * kq + rq, rb = 16 + 4 * kq + rq;   // this lane's rows of the two transposed reads
+  if (nk > 0) {
+#pragma unroll
+    for (int c = 0; c < kD3R - 1; ++c) dma(c);
+    for (int kt = 0; kt < nk; ++kt) {
+      // this wave's DMA of step kt has landed once only the younger R - 2 steps' are in flight;
+      // then the barrier publishes every wave's (a bare s_barrier: __syncthreads' fence would
+      // wait for the whole prefetch)
+      if (ndma == 3) DL_BN_VMCNT(3 * (kD3R - 2));
+      else DL_BN_VMCNT(2 * (kD3R - 2));
+      __builtin_amdgcn_s_waitcnt(0xc07f);   // lgkmcnt(0): this wave's reads of step kt - 1 are done
+      __builtin_amdgcn_s_barrier();
+      dma(kt + kD3R - 1);                   // into the stage step kt - 1 used
+      const unsigned short* As = lds + (kt % kD3R) * (kD3SB / 2);
+      const unsigned short* Bs = As + kD3AB / 2;
+      shortx8 af[3];
+#pragma unroll
+      for (int a = 0; a < 3; ++a) {
+        const int col = 48 * wm + 16 * a + 4 * cp;
+        const uint2 lo = lds_tr16(&As[ra * kD3BM + col]);
+        const uint2 hi = lds_tr16(&As[rb * kD3BM + col]);
+        af[a] = __builtin_bit_cast(shortx8, make_uint4(lo.x, lo.y, hi.x, hi.y));
+      }
+#pragma unroll
+      for (int b = 0; b < 5; ++b) {
+        const int col = 80 * wn + 16 * b + 4 * cp;
+        const uint2 lo = lds_tr16(&Bs[ra * kD3BN + col]);
+        const uint2 hi = lds_tr16(&Bs[rb * kD3BN + col]);
+        const shortx8 bf = __builtin_bit_cast(shortx8, make_uint4(lo.x, lo.y, hi.x, hi.y));
+#pragma unroll
+        for (int a = 0; a < 3; ++a) acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[a], bf, acc[a][b], 0, 0, 0);
+      }
+    }
+    DL_BN_VMCNT(0);   // the trailing DMAs land before the workgroup's LDS is released
+  }
+  float* __restrict__ C = reinterpret_cast<float*>(p.C) + (long long)z * p.c_split_stride;
+#pragma unroll
+  for (int a = 0; a < 3; ++a)
+#pragma unroll
+    for (int b = 0; b < 5; ++b) {
+      const int col = 80 * wn + 16 * b + cl;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int row = m0 + 48 * wm + 16 * a + 4 * kq + j;
+        if (row < p.M && col < p.N) C[(long long)row * p.ldc + col] = acc[a][b][j];
+      }
+    }
+}
+
 // true if the transposed-read kernel takes the product (ta = 1, tb = 0, split slabs)
 static bool launch_bf16_dw(const GemmParams& gp0, int splits_req, hipStream_t s) {
   if (gp0.N > 400 || gp0.N % 8 || gp0.M % 8 || gp0.lda % 8 || gp0.ldb % 8 || gp0.lda < gp0.M ||
@@ -1074,6 +1202,11 @@ static bool launch_bf16_dw(const GemmParams& gp0, int splits_req, hipStream_t s)
   kps = (kps + 63) / 64 * 64;                 // the engine sums ceil(K / kps) slabs at this rounding
   gp.k_per_split = kps;
   const int splits = (int)ceil_div(gp.K > 0 ? gp.K : 1, kps);
+  if (DL_BF16_DW3 && gp.K % kD3KS == 0) {
+    const int mtiles = (int)ceil_div(gp.M, kD3BM);
+    hipLaunchKernelGGL(gemm_bf16_dw3_kernel, dim3((unsigned)(mtiles * splits)), dim3(64 * kD3W), kD3Lds, s, gp);
+    return true;
+  }
   const int mtiles = (int)ceil_div(gp.M, 64);
   hipLaunchKernelGGL(gemm_bf16_dw_kernel, dim3((unsigned)(mtiles * splits)), dim3(320), 0, s, gp);
   return true;

@@ -103,9 +103,17 @@ __global__ __launch_bounds__(256) void adam_dense_thread_kernel(float* __restric
   float sq = 0.f;
   for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n;
        i += (long long)gridDim.x * blockDim.x) {
-    // the slab column: 16 loads in flight per round trip, added in slab order (the same sum)
+    // the slab column: 32 (then 16) loads in flight per round trip, added in slab order (the
+    // same sum for any grouping)
     float g = 0.f;
     int s = 0;
+    for (; s + 32 <= nslab; s += 32) {
+      float a[32];
+#pragma unroll
+      for (int j = 0; j < 32; ++j) a[j] = slab[(s + j) * stride + i];
+#pragma unroll
+      for (int j = 0; j < 32; ++j) g += a[j];
+    }
     for (; s + 16 <= nslab; s += 16) {
       float a[16];
 #pragma unroll

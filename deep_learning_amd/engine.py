@@ -380,9 +380,12 @@ class CTREngine:
         self.in_wide = z(B, max(sp.Fw, 1), dt=torch.int64)
         # split-K slabs of the weight gradients: the double-buffered s3 TN kernel (one block per
         # CU, 2 column tiles) runs best at 32 (scripts/s3_bench.py: 147 vs 152 us at 64)
-        self.splits = max(1, min(int(os.environ.get("DLAMD_DW_SPLITS", 32 if self.s3 else 64)), B // 1024))
+        # (the bf16 tower's ring kernel, one 144 x 400 block per CU, takes up to 96: _bf16_dw_splits)
+        dflt = 32 if self.s3 else 96 if self.bf else 64
+        self.splits = max(1, min(int(os.environ.get("DLAMD_DW_SPLITS", dflt)), B // (512 if self.bf else 1024)))
         self.dw_splits = self._dw_splits(B, fixed="DLAMD_DW_SPLITS" in os.environ)
-        self.w_slab = z(max(k * i * o for k, i, o in zip(self.dw_splits, self.in_ld, self.out_ld)))
+        # sized for the cap: a smaller batch may choose more splits than the largest one did
+        self.w_slab = z(max(self.splits * i * o for i, o in zip(self.in_ld, self.out_ld)))
         self.layout = self._layout(B)
         self.bwd_blocks = _lib.lib().dl_embed_bwd_grid(C_ref(self.layout))
         self.cont_slab = z(max(1, self.bwd_blocks * sp.C * (E + 1)))
@@ -606,9 +609,11 @@ class CTREngine:
 
     def _dw_splits(self, B, fixed=False):
         """Per-layer split-K slab counts of the weight gradients (fixed: self.splits for all)."""
-        base = max(1, min(self.splits, B // 1024))
-        if fixed or not self.s3:
+        base = max(1, min(self.splits, B // (512 if self.bf else 1024)))
+        if fixed or not (self.s3 or self.bf):
             return [base] * len(self.spec.hidden)
+        if self.bf:
+            return [_bf16_dw_splits(i, B, base) for i in self.in_ld]
         return [_s3_dw_splits(i, o, B, base) for i, o in zip(self.in_ld, self.spec.hidden)]
 
     def dense_params(self):
@@ -1324,6 +1329,21 @@ def _s3_dw_splits(M, N, B, base, cus=256):
     largest on ties.  C2's layers (8 tiles) keep 32; C3's layer 0 (M = 528: 10 tiles) takes 25
     — one round of 250 blocks instead of two rounds for 320."""
     tiles = -(-M // 128) * -(-N // 224)
+
+    def cost(s):
+        return -(-tiles * s // cus) * (-(-(-(-B // s)) // 64) * 64)
+    return min(range(base, 0, -1), key=cost)
+
+
+def _bf16_dw_splits(M, B, base, cus=256):
+    """Split-K slab count of one bf16 weight gradient.  With whole 32-row batch steps
+    (B % 32 == 0) dl_gemm_bf16 runs the LDS-DMA ring kernel: one 144 x 400 block per CU,
+    ceil(M / 144) tiles per slab; the s <= base minimising rounds x rows per block, the largest
+    on ties (C5: M = 432 / 416 -> 3 tiles, 79 slabs of 832 rows, 237 blocks in one round).
+    Otherwise the two-buffer kernel (64-row tiles, two blocks per CU) takes `base`."""
+    if B % 32:
+        return base
+    tiles = -(-M // 144)
 
     def cost(s):
         return -(-tiles * s // cus) * (-(-(-(-B // s)) // 64) * 64)

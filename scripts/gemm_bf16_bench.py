@@ -20,7 +20,7 @@ WT = bf(400, 432)          # W^T, k-contiguous
 W1 = bf(416, 400)
 out_b = torch.zeros(B, 416, device="cuda", dtype=torch.bfloat16)
 out_f = torch.zeros(B, 416, device="cuda")
-slab = torch.zeros(64 * 432 * 416, device="cuda")
+slab = torch.zeros(96 * 432 * 416, device="cuda")
 u16 = lambda t: ptr(t)
 cases = {
     "fwd_l0 bf16 out relu": (lambda: call("dl_gemm_bf16", 0, 1, B, 400, 432, u16(x0), 432, u16(WT), 432, ptr(out_b), 416, 1, 1,
@@ -33,6 +33,10 @@ cases = {
                                    64, 416 * 400, s), 2 * B * 417 * 400),
     "dw_l1 direct (ta=1) split64": (lambda: call("dl_gemm_bf16", 1, 0, 416, 400, B, u16(h), 416, u16(out_b), 416,
                                                  ptr(slab), 400, 0, 3, None, 0, 64, 416 * 400, s), 2 * B * 417 * 400),
+    "dw_l0 direct (ta=1) split85": (lambda: call("dl_gemm_bf16", 1, 0, 432, 400, B, u16(x0), 432, u16(out_b), 416,
+                                                 ptr(slab), 400, 0, 3, None, 0, 85, 432 * 400, s), 2 * B * 433 * 400),
+    "dw_l1 direct (ta=1) split85": (lambda: call("dl_gemm_bf16", 1, 0, 416, 400, B, u16(h), 416, u16(out_b), 416,
+                                                 ptr(slab), 400, 0, 3, None, 0, 85, 416 * 400, s), 2 * B * 417 * 400),
     "transpose_bf16 [B,416]": (lambda: call("dl_transpose_bf16", u16(h), 0, B, 416, 416, u16(hT), B, s), 0),
     "cast_bf16 [B,416]": (lambda: call("dl_cast_bf16", ptr(out_f), B, 416, 416, u16(out_b), 416, s), 0),
 }

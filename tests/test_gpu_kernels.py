@@ -687,11 +687,13 @@ def test_gemm_bf16_b_resident(hip_lib, M, N, K, epi, cbf):
 
 
 @pytest.mark.parametrize("M,N,K,splits", [(432, 400, 65536, 64), (416, 400, 40000, 7), (264, 208, 1000, 3),
-                                          (64, 16, 96, 1)])
+                                          (64, 16, 96, 1), (432, 400, 65536, 85), (416, 400, 65536, 85),
+                                          (136, 120, 4096, 5), (288, 392, 2048, 1)])
 def test_gemm_bf16_dw_transposed_reads(hip_lib, M, N, K, splits):
     """Weight gradients of the bf16 tower from batch-major operands (ta=1, tb=0, split slabs):
-    the transposing-LDS-read kernel against an fp64 product of the same bf16 inputs, with
-    ragged M tiles, K steps and splits."""
+    the transposing-LDS-read kernels against an fp64 product of the same bf16 inputs, with
+    ragged M tiles, K steps and splits (K % 32 == 0: the LDS-DMA ring kernel, 144 x 400 blocks;
+    K = 1000: the two-buffer kernel)."""
     g = torch.Generator().manual_seed(M + N + K)
     X = torch.randn(K, M, generator=g).bfloat16()
     Y = torch.randn(K, N, generator=g).bfloat16()

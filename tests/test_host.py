@@ -303,3 +303,19 @@ def test_s3_dw_split_counts():
         for base in (1, 7, 32, 64):
             s = _s3_dw_splits(M, 400, 65536, base)
             assert 1 <= s <= base
+
+
+def test_bf16_dw_split_counts():
+    """engine._bf16_dw_splits: the bf16 ring kernel's split count (144 x 400 blocks, one per CU):
+    C5's layers (M = 432 / 416: 3 tiles) take 85 requested = 79 slabs of 832 rows in one round
+    of 237 blocks; a batch without whole 32-row steps keeps the cap (two-buffer kernel)."""
+    from deep_learning_amd.engine import _bf16_dw_splits, _num_splits
+    assert _bf16_dw_splits(432, 65536, 96) == 85
+    assert _bf16_dw_splits(416, 65536, 96) == 85
+    assert _num_splits(65536, 85, 64) == 79
+    assert _bf16_dw_splits(432, 1000, 1) == 1
+    assert _bf16_dw_splits(432, 65540, 96) == 96
+    for M in (16, 144, 432, 1000):
+        for base in (1, 7, 64, 96):
+            s = _bf16_dw_splits(M, 65536, base)
+            assert 1 <= s <= base and -(-M // 144) * s <= max(256, -(-M // 144))
