@@ -753,6 +753,153 @@ __global__ __launch_bounds__(512) void gemm_s3_tn2_kernel(S3Params p) {
     }
 }
 
+// ---------------------------------------------------------------------------- TN, interleaved
+// The double-buffered TN kernel with its staging moved under the MFMAs: the f32 tiles are
+// loaded two steps ahead (two register sets), and step kt + 1's six pieces per thread are split
+// and written to the other LDS buffer between step kt's fragment groups (piece b after fragment
+// b's twelve MFMAs), so each wave's VALU split and LDS stores issue while its MFMAs execute
+// instead of in a phase of their own between barriers (tn2: MFMA busy about half the loop).
+// Same tiles, images, fragment reads and k order as tn2: the same sums bit for bit.
+#ifndef DL_S3_TN3
+#define DL_S3_TN3 1   // weight gradients: the interleaved kernel (0: tn2)
+#endif
+
+__global__ __launch_bounds__(512) void gemm_s3_tn3_kernel(S3Params p) {
+  extern __shared__ __attribute__((aligned(16))) unsigned short lds[];   // [2][3 A planes | 3 B planes]
+  const int tid = threadIdx.x, lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int mtiles = (p.M + kT2BM - 1) / kT2BM, ntiles = (p.N + kT2BN - 1) / kT2BN;
+  const int t = s3_xcd_tile(blockIdx.x, gridDim.x);
+  const int n0 = (t % ntiles) * kT2BN, m0 = ((t / ntiles) % mtiles) * kT2BM, z = t / (ntiles * mtiles);
+  const int kbeg = z * p.k_per_split;
+  const int kend = min(p.K, kbeg + p.k_per_split);
+  const int nk = (kend - kbeg + kT2KS - 1) / kT2KS;
+  const auto xr = __builtin_amdgcn_make_buffer_rsrc((void*)p.A, (short)0, p.K * p.lda * 4, 0x00020000);
+  const auto yr = __builtin_amdgcn_make_buffer_rsrc((void*)p.B, (short)0, p.K * p.ldb * 4, 0x00020000);
+  int pr[kT2Q], pc[kT2Q];
+  bool pok[kT2Q];
+#pragma unroll
+  for (int u = 0; u < kT2Q; ++u) {
+    if (u < 2) {
+      pr[u] = (tid >> 5) + 16 * u;
+      pc[u] = 4 * (tid & 31);
+      pok[u] = m0 + pc[u] < p.M;
+    } else {
+      const int qb = tid + 512 * (u - 2);
+      pr[u] = qb / (kT2BN / 4);
+      pc[u] = 4 * (qb % (kT2BN / 4));
+      pok[u] = n0 + pc[u] < p.N && (u < 5 || tid < 256);
+    }
+  }
+  auto load = [&](int k0, float4 (&rs)[kT2Q]) {
+#pragma unroll
+    for (int u = 0; u < kT2Q; ++u) {
+      const int gk = k0 + pr[u];
+      const bool ok = pok[u] & (gk < kend);
+      if (u < 2) {
+        const uint32_t o = 4u * (uint32_t)(gk * p.lda + m0 + pc[u]);
+        rs[u] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(xr, (int)(ok ? o : 0x80000000u), 0, 0));
+      } else {
+        const uint32_t o = 4u * (uint32_t)(gk * p.ldb + n0 + pc[u]);
+        rs[u] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(yr, (int)(ok ? o : 0x80000000u), 0, 0));
+      }
+    }
+  };
+  auto store_piece = [&](int buf, int u, const float4& r) {
+    if (u == 5 && tid >= 256) return;
+    unsigned short* As = lds + buf * kT2Buf;
+    unsigned short* Bs = As + 3 * kT2AE;
+    uint32_t h0, m0_, l0, h1, m1_, l1;
+    split2(r.x, r.y, h0, m0_, l0);
+    split2(r.z, r.w, h1, m1_, l1);
+    unsigned short* img = u < 2 ? As : Bs;
+    const int pe = u < 2 ? kT2AE : kT2BE;
+    const int o = pr[u] * (u < 2 ? kT2PA : kT2PB) + pc[u];
+    *reinterpret_cast<uint2*>(&img[o]) = make_uint2(h0, h1);
+    *reinterpret_cast<uint2*>(&img[pe + o]) = make_uint2(m0_, m1_);
+    *reinterpret_cast<uint2*>(&img[2 * pe + o]) = make_uint2(l0, l1);
+  };
+  floatx4 acc[2][kT2NF];
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < kT2NF; ++b) acc[a][b] = floatx4{0.f, 0.f, 0.f, 0.f};
+  const int wm = wid & 3, wn = wid >> 2;
+  const int cl = lane & 15, kq = lane >> 4, rq = cl >> 2, cp = cl & 3;
+  const int ra = 4 * kq + rq, rb = 16 + 4 * kq + rq;
+  // step kt from buffer kt & 1; `nx` (step kt + 1's tiles) split into buffer (kt + 1) & 1 piece by
+  // piece between the fragment groups (skipped past the last step: nothing left to stage)
+  auto step = [&](int kt, const float4 (&nx)[kT2Q]) {
+    const int buf = kt & 1;
+    const bool more = kt + 1 < nk;
+    const unsigned short* As = lds + buf * kT2Buf;
+    const unsigned short* Bs = As + 3 * kT2AE;
+    shortx8 ah[2], am[2], al[2];
+#pragma unroll
+    for (int a = 0; a < 2; ++a) {
+      const int col = 32 * wm + 16 * a + 4 * cp;
+      ah[a] = s3_tr_frag(As, kT2PA, ra, rb, col);
+      am[a] = s3_tr_frag(As + kT2AE, kT2PA, ra, rb, col);
+      al[a] = s3_tr_frag(As + 2 * kT2AE, kT2PA, ra, rb, col);
+    }
+    shortx8 bb[2][3];
+    {
+      const int col = 112 * wn + 4 * cp;
+      bb[0][0] = s3_tr_frag(Bs, kT2PB, ra, rb, col);
+      bb[0][1] = s3_tr_frag(Bs + kT2BE, kT2PB, ra, rb, col);
+      bb[0][2] = s3_tr_frag(Bs + 2 * kT2BE, kT2PB, ra, rb, col);
+    }
+#pragma unroll
+    for (int b = 0; b < kT2NF; ++b) {
+      if (b + 1 < kT2NF) {   // fragment b + 1's reads ahead of fragment b's MFMAs
+        const int col = 112 * wn + 16 * (b + 1) + 4 * cp;
+        bb[(b + 1) & 1][0] = s3_tr_frag(Bs, kT2PB, ra, rb, col);
+        bb[(b + 1) & 1][1] = s3_tr_frag(Bs + kT2BE, kT2PB, ra, rb, col);
+        bb[(b + 1) & 1][2] = s3_tr_frag(Bs + 2 * kT2BE, kT2PB, ra, rb, col);
+      }
+#pragma unroll
+      for (int a = 0; a < 2; ++a)
+        acc[a][b] = mfma_s3(ah[a], am[a], al[a], bb[b & 1][0], bb[b & 1][1], bb[b & 1][2], acc[a][b]);
+      if (b < kT2Q && more) store_piece(buf ^ 1, b, nx[b]);
+    }
+  };
+  float4 rA[kT2Q], rB[kT2Q];
+  if (nk > 0) {
+    load(kbeg, rA);
+    load(kbeg + kT2KS, rB);   // past kend: zeros (never stored)
+#pragma unroll
+    for (int u = 0; u < kT2Q; ++u) store_piece(0, u, rA[u]);
+  }
+  __syncthreads();
+  // pairs of steps: at step kt the registers of kt + 1 are stored and those of kt (already in
+  // LDS) take step kt + 2's loads
+  // (a bare s_barrier after lgkmcnt(0): __syncthreads' fence would also wait for the loads of
+  // two steps ahead)
+  int kt = 0;
+  for (; kt + 1 < nk; kt += 2) {
+    load(kbeg + (kt + 2) * kT2KS, rA);
+    step(kt, rB);
+    __builtin_amdgcn_s_waitcnt(0xc07f);
+    __builtin_amdgcn_s_barrier();
+    load(kbeg + (kt + 3) * kT2KS, rB);
+    step(kt + 1, rA);
+    __builtin_amdgcn_s_waitcnt(0xc07f);
+    __builtin_amdgcn_s_barrier();
+  }
+  if (kt < nk) step(kt, rB);
+  float* __restrict__ C = p.C + (long long)z * p.c_split_stride;
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < kT2NF; ++b) {
+      const int col = n0 + 112 * wn + 16 * b + cl;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int row = m0 + 32 * wm + 16 * a + 4 * kq + j;
+        if (row < p.M && col < p.N) C[(long long)row * p.ldc + col] = acc[a][b][j];
+      }
+    }
+}
+
 // ---------------------------------------------------------------------------- split
 // dst plane q (q = 0 hi, 1 mid, 2 lo) at dst + q * plane: element (r, c) of src [rows][cols]
 // (ld lds) goes to [r][c] (ldd), or to [c][r] when transposed.
@@ -851,7 +998,10 @@ extern "C" int dl_gemm_s3_tn(int32_t M, int32_t N, int32_t K, const float* X, in
   p.k_per_split = kps;
   p.c_split_stride = c_split_stride;
   splits = (int)ceil_div(K > 0 ? K : 1, kps);
-  if (DL_S3_TN2) {
+  if (DL_S3_TN2 && DL_S3_TN3) {
+    const int tiles = (int)(ceil_div(M, kT2BM) * ceil_div(N, kT2BN));
+    hipLaunchKernelGGL(gemm_s3_tn3_kernel, dim3((unsigned)(tiles * splits)), dim3(512), kT2Lds, as_stream(stream), p);
+  } else if (DL_S3_TN2) {
     const int tiles = (int)(ceil_div(M, kT2BM) * ceil_div(N, kT2BN));
     hipLaunchKernelGGL(gemm_s3_tn2_kernel, dim3((unsigned)(tiles * splits)), dim3(512), kT2Lds, as_stream(stream), p);
   } else {
