@@ -764,6 +764,7 @@ __global__ __launch_bounds__(512) void gemm_s3_tn2_kernel(S3Params p) {
 #define DL_S3_TN3 1   // weight gradients: the interleaved kernel (0: tn2)
 #endif
 
+
 __global__ __launch_bounds__(512) void gemm_s3_tn3_kernel(S3Params p) {
   extern __shared__ __attribute__((aligned(16))) unsigned short lds[];   // [2][3 A planes | 3 B planes]
   const int tid = threadIdx.x, lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);

@@ -9,7 +9,10 @@ from deep_learning_amd import _lib  # noqa: E402
 from deep_learning_amd._lib import call, ptr  # noqa: E402
 
 reps = int(sys.argv[1]) if len(sys.argv) > 1 else 20
-only = sys.argv[2] if len(sys.argv) > 2 else None   # run one case (profiling)
+only = sys.argv[2] if len(sys.argv) > 2 else None   # run one case (profiling); "t:<case>": time just it
+timed = None
+if only and only.startswith("t:"):
+    timed, only = only[2:], None
 B = 65536
 s = _lib.stream_handle()
 g = torch.Generator(device="cuda").manual_seed(0)
@@ -106,14 +109,16 @@ for name, fl, f_s3, f_f32, err in cases:
             torch.cuda.synchronize()
             print(name, "done")
         continue
+    if timed and name != timed:
+        continue
     f_s3()
     f_f32()
     torch.cuda.synchronize()
     e_s3, e_f32 = err()
-    t_s3, t_f32 = timeit(f_s3), timeit(f_f32)
+    t_s3, t_f32 = timeit(f_s3), (timeit(f_f32) if not timed else 1.0)
     print("%-7s s3 %7.1f us %6.1f TF/s err %.2e | f32 %7.1f us %6.1f TF/s err %.2e" %
           (name, t_s3, fl / t_s3 / 1e6, e_s3, t_f32, fl / t_f32 / 1e6, e_f32), flush=True)
-for sp in (() if only else (32, 48, 64, 96, 128)):
+for sp in (() if (only or timed) else (32, 48, 64, 96, 128)):
     fn = lambda: call("dl_gemm_s3_tn", 416, 400, B, ptr(h), 416, ptr(dy), 416, ptr(slab), 400, sp, 416 * 400, s)
     t = timeit(fn)
     print("dw_l1 s3 splits %3d %7.1f us %6.1f TF/s" % (sp, t, 2 * B * 416 * 400 / t / 1e6), flush=True)
