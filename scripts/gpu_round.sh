@@ -44,6 +44,7 @@ if [ "$MODE" = prof ]; then
     python scripts/pmc_summary.py $W $OUT/pmc_summary_$wl.json $wl > $W/summary.txt && head -12 $W/summary.txt
   done
   bash scripts/pmc_s3.sh $OUT/s3pmc fwd_l1 dw_l1 || exit $?
+  python scripts/sq_summary.py $OUT/s3pmc $OUT/s3_sq_counters.json fwd_l1 dw_l1
   exit 0
 fi
 echo "usage: gpu_round.sh suite|prof TAG"; exit 2
