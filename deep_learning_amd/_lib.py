@@ -33,7 +33,7 @@ class PoolDesc(C.Structure):
     """Mirror of ``dl_pool_desc`` (include/dlamd.h)."""
     _fields_ = [
         ("slot_start", C.c_void_p), ("slot_end", C.c_void_p), ("n_slots", C.c_int32), ("fm_col", C.c_int32),
-        ("dx0_pool_col", C.c_int32), ("pad_", C.c_int32), ("x0", C.c_void_p), ("cnt_emb", C.c_void_p),
+        ("dx0_pool_col", C.c_int32), ("g_pitch", C.c_int32), ("x0", C.c_void_p), ("cnt_emb", C.c_void_p),
         ("cnt_first", C.c_void_p), ("g_pool", C.c_void_p), ("g1_pool", C.c_void_p),
     ]
 

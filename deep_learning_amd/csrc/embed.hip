@@ -64,6 +64,9 @@ constexpr int kMaxSlots = 128;     // FM slots + deep slots per sample
 #endif
 // Occupancy: the gathered-rows form (C2: E = 16, NPS = 5) needs 97 VGPRs unbounded — one past
 // the 5-waves-per-SIMD line; the bound keeps it at 96 (no spill; NPS > 5 would spill: unbounded).
+#ifndef DL_POOL_DIAG_NO_W1
+#define DL_POOL_DIAG_NO_W1 0   // diagnostics build: first-order weights not read by the forward / pooling (wrong fm_out)
+#endif
 template <int E, int NPS, bool REC = false>
 __global__ __launch_bounds__(256, (REC || NPS > 5) ? 1 : DL_FWD_MIN_WAVES) void embed_fwd_kernel(EmbArgs a) {
   // Per block iteration a tile of 16 samples is staged: every (sample, slot)
@@ -207,7 +210,7 @@ __global__ __launch_bounds__(256, (REC || NPS > 5) ? 1 : DL_FWD_MIN_WAVES) void 
       if (lane < (REC ? Cf : Fs)) {
         frow = rows_s[j][lane];
         val = lane < Cf ? vals_s[j][lane] : 1.f;
-        w1 = a.first_order[(frow < 0 || w1_done) ? 0 : frow];
+        w1 = DL_POOL_DIAG_NO_W1 ? 1.f : a.first_order[(frow < 0 || w1_done) ? 0 : frow];
       }
       float4 s = z4, ss = z4;
 #pragma unroll
@@ -571,7 +574,7 @@ __global__ __launch_bounds__(256) void pool_fwd_kernel(PoolArgs a) {
           }
         }
         if (a.first_order) {
-          const float w = src >= 0 ? a.first_order[src] : 0.f;
+          const float w = src >= 0 ? (DL_POOL_DIAG_NO_W1 ? 1.f : a.first_order[src]) : 0.f;
           s1v += w;
           c1 += (w != 0.f) ? 1.f : 0.f;
         }

@@ -379,10 +379,11 @@ __global__ __launch_bounds__(256) void pool_grad_kernel(dl_emb_layout L, dl_pool
       }
       gv = make_float4(dp.x / c, dp.y / c, dp.z / c, dp.w / c);
     }
-    *reinterpret_cast<float4*>(p.g_pool + bm * E + 4 * q) = gv;
+    const int gp = p.g_pitch > 0 ? p.g_pitch : E;
+    *reinterpret_cast<float4*>(p.g_pool + bm * gp + 4 * q) = gv;
     if (g1 && q == 0) {
       const float c1 = p.cnt_first[bm];
-      p.g1_pool[bm] = c1 > 0.f ? dzb * w_head[p.fm_col + m] / c1 : 0.f;
+      p.g1_pool[bm * (p.g_pitch > 0 ? p.g_pitch : 1)] = c1 > 0.f ? dzb * w_head[p.fm_col + m] / c1 : 0.f;
     }
   }
 }
@@ -917,12 +918,16 @@ extern "C" int dl_rec_bwd_adam(const dl_emb_layout* L, float* rec, int32_t rec_l
                "cnt_first / g1_pool required");
   DL_CHECK_ARG(!multi || (pool->dx0_pool_col % 4 == 0 && L->x0_pool_col % 4 == 0),
                "pool columns not float4 aligned");
+  DL_CHECK_ARG(!multi || pool->g_pitch == 0 || (pool->g_pitch >= L->emb_dim + 1 && pool->g_pitch % 4 == 0),
+               "g_pitch %d: 0 or >= E + 1 and a multiple of 4", multi ? pool->g_pitch : 0);
   SegGradIn sg{*L, seg_off, sorted_refs, dz, w_head, fm_sum, dx0};
   sg.status = reinterpret_cast<int*>(const_cast<float*>(opt) + DL_OPT_STATUS);   // opt_status(opt), host side
   const bool g1p = multi && L->use_fm && has_first;
   if (multi) {
     sg.slot_start = pool->slot_start; sg.slot_end = pool->slot_end; sg.n_slots = pool->n_slots;
     sg.g_pool = pool->g_pool; sg.g1_pool = g1p ? pool->g1_pool : nullptr;
+    sg.g_pitch = pool->g_pitch > 0 ? pool->g_pitch : L->emb_dim;
+    sg.g1_stride = pool->g_pitch > 0 ? pool->g_pitch : 1;
     if (L->batch > 0)
       DL_DISPATCH_E(L->emb_dim, {
         hipLaunchKernelGGL(pool_grad_kernel<kE>, dim3(grid_cap((long long)L->batch * pool->n_slots * (kE / 4))),

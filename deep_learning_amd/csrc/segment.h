@@ -28,6 +28,8 @@ struct SegGradIn {
   int n_slots;
   const float* g_pool;
   const float* g1_pool;
+  int g_pitch;    // floats between (sample, slot) rows of g_pool (E: packed)
+  int g1_stride;  // ... and between their g1_pool entries (1: packed; g_pitch: interleaved)
   // opt's status word: an index entry out of range (a corrupt batch index) sets
   // DL_STATUS_INDEX there and the host raises, instead of the entry being skipped silently
   int* status;
@@ -147,9 +149,9 @@ __device__ __forceinline__ SegGrad4 segment_grad4_range(const SegGradIn& a, int 
       const int m = seg_slot_of(a, sl - mb);
       if (m == a.n_slots) continue;
       const long long bm = (long long)b * a.n_slots + m;
-      const float4 gp = *reinterpret_cast<const float4*>(a.g_pool + bm * E + 4 * q);
+      const float4 gp = *reinterpret_cast<const float4*>(a.g_pool + bm * a.g_pitch + 4 * q);
       r.x.x += gp.x; r.x.y += gp.y; r.x.z += gp.z; r.x.w += gp.w;
-      if (a.g1_pool) r.g1 += a.g1_pool[bm];
+      if (a.g1_pool) r.g1 += a.g1_pool[bm * a.g1_stride];
     } else if (L.use_fm && sl < S) {
       const float dzb = a.dz[b];
       const float4 fs = *reinterpret_cast<const float4*>(a.fm_sum + (long long)b * E + 4 * q);
@@ -193,8 +195,8 @@ __device__ __forceinline__ SegRef seg_fetch(const SegGradIn& a, bool in, int k, 
     if (m == a.n_slots) return f;
     const long long bm = (long long)b * a.n_slots + m;
     f.kind = 1;
-    f.v = *reinterpret_cast<const float4*>(a.g_pool + bm * E + 4 * q);
-    f.w = a.g1_pool ? a.g1_pool[bm] : 0.f;
+    f.v = *reinterpret_cast<const float4*>(a.g_pool + bm * a.g_pitch + 4 * q);
+    f.w = a.g1_pool ? a.g1_pool[bm * a.g1_stride] : 0.f;
   } else if (L.use_fm && sl < S) {
     f.kind = 2;
     f.dzb = a.dz[b];

@@ -395,12 +395,17 @@ class CTREngine:
             self.slot_end = torch.tensor([r[1] for r in sp.multi_ranges], dtype=torch.int32, device=dev)
             self.cnt_emb, self.cnt_first = z(B, M), z(B, M)
             if self.lazy:
-                self.g_pool, self.g1_pool = z(B, M, E), z(B, M)
+                # per (sample, slot): the slot gradient (E floats) and the first-order one at
+                # column E of a row padded to whole 128-B lines (one line fetch per multi-hot
+                # reference in the backward instead of two: dl_pool_desc.g_pitch)
+                gp = 0 if os.environ.get("DLAMD_GPOOL_PACKED") else _ru(E + 1, 32)   # env: A/B only
+                self.g_pool = z(B, M, gp or E)
+                self.g1_pool = self.g_pool.view(-1)[E:] if gp else z(B, M)
                 self.pool_desc = _lib.PoolDesc(
                     slot_start=self.slot_start.data_ptr(), slot_end=self.slot_end.data_ptr(), n_slots=M,
-                    fm_col=self.fm_pool_col, dx0_pool_col=S * E, x0=self.x0.data_ptr(), cnt_emb=self.cnt_emb.data_ptr(),
-                    cnt_first=self.cnt_first.data_ptr(), g_pool=self.g_pool.data_ptr(),
-                    g1_pool=self.g1_pool.data_ptr())
+                    fm_col=self.fm_pool_col, dx0_pool_col=S * E, g_pitch=gp, x0=self.x0.data_ptr(),
+                    cnt_emb=self.cnt_emb.data_ptr(), cnt_first=self.cnt_first.data_ptr(),
+                    g_pool=self.g_pool.data_ptr(), g1_pool=self.g1_pool.data_ptr())
         # batch reference index (deterministic backward)
         self.bwd = bwd
         self.n_slot = (S if sp.fm else 0) + S + (sp.multi_width if self.lazy else 0)

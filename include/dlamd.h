@@ -480,14 +480,18 @@ int dl_rec_gather_scatter(const dl_emb_layout* L, const float* rec, int32_t rec_
 /* Multi-hot pooling state for dl_rec_bwd_adam (deepfm_multi_cate.py:71-111): slot ranges
  * within the multi block, the head column of the pooled first-order outputs, dx0's pooled
  * columns, the pooled x0 (L->x0_pool_col), the nonzero counts of dl_pool_fwd_indexed and
- * scratch g_pool [B][n_slots][E], g1_pool [B][n_slots] for the per-slot gradients. */
+ * scratch g_pool [B][n_slots][E], g1_pool [B][n_slots] for the per-slot gradients.
+ * g_pitch > 0 (>= E + 1, a multiple of 4): row (b, m) of g_pool at g_pool + (b*n_slots + m)*g_pitch
+ * and its first-order gradient at g1_pool[(b*n_slots + m)*g_pitch] — with g1_pool = g_pool + E
+ * and g_pitch = 32 (E = 16) both sit in one 128-B line, so a multi-hot reference's gradient
+ * costs one line fetch instead of two; g_pitch = 0: the packed layouts above. */
 typedef struct dl_pool_desc {
   const int32_t* slot_start;
   const int32_t* slot_end;
   int32_t n_slots;
   int32_t fm_col;
   int32_t dx0_pool_col;
-  int32_t pad_;
+  int32_t g_pitch;
   const float* x0;
   const float* cnt_emb;
   const float* cnt_first;
