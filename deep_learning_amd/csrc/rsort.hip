@@ -29,6 +29,10 @@ constexpr int kRsWaveSpan = 64 * kRsRounds;                  // consecutive elem
 constexpr int kRsMaxBits = DL_RS_MAXBITS;                    // digit bits per pass at most
 constexpr int kRsMaxRadix = 1 << kRsMaxBits;
 constexpr int kLocal = 27;
+constexpr uint32_t kRsNoKey = 0xFFFFFFFFu;   // rs_keys_kernel: a reference without a key
+#ifndef DL_RS_PREKEYS
+#define DL_RS_PREKEYS 0   // 1: the index build's keys materialised first by rs_keys_kernel (alone C3 956 -> 886 us,
+#endif                    // C2 257 -> 246 us; in the step slower by 7-20 us: profiles/r03pk/)
 
 struct RsPass {
   int shift, bits;
@@ -49,7 +53,8 @@ __device__ __forceinline__ int rs_digit(uint32_t key, const RsPass& p) {
 }
 
 // The pair at element e of the pass's input; false when e has no key (or lies past the end).
-// MODE 0: the previous pass's arrays; 1: the source's key array; 2: the batch's references.
+// MODE 0: the previous pass's arrays; 1: the source's key array; 2: the batch's references;
+// 3: the batch references' keys from rs_keys_kernel (value = the reference).
 // Loads are unconditional (clamped index) and validity is computed after, so a tile's loads
 // can all be in flight at once.
 template <int MODE>
@@ -67,6 +72,10 @@ __device__ __forceinline__ bool rs_get(const RsSource& src, const RsPass& p, lon
     key = src.keys[ec];
     return in;
   }
+  if (MODE == 3) {   // keys materialised by rs_keys_kernel (kRsNoKey: no key)
+    key = p.kin[ec];
+    return in && key != kRsNoKey;
+  }
   const dl_emb_layout& L = src.L;
   const int S = L.cate_fields, ns = index_slots(L), mb = index_multi_base(L);
   // 32-bit division (a reference index is an int32): the 64-bit one is a long subroutine,
@@ -83,6 +92,21 @@ __device__ __forceinline__ bool rs_get(const RsSource& src, const RsPass& p, lon
   const uint32_t qw = w == 1 ? r32 : r32 / (uint32_t)w;   // w is uniform: one rank divides by nothing
   key = row < src.rep_below ? (((uint32_t)w << kLocal) | r32) : (((r32 - qw * (uint32_t)w) << kLocal) | qw);
   return in && range_ok && !(row == 0 && L.zero_row0);
+}
+
+// The batch references' keys, one streaming pass (MODE 3's input): the first sort pass then
+// reads 4 B per candidate instead of gathering its int64 id and deriving the key twice (in the
+// upsweep and again in the downsweep).  A reference without a key gets kRsNoKey, its inverse
+// entry -1, and an out-of-range id flags the batch, as MODE 2's upsweep did.
+__global__ __launch_bounds__(kRsThreads) void rs_keys_kernel(RsSource src, long long n, uint32_t* __restrict__ keys) {
+  const RsPass p{};
+  for (long long e = (long long)blockIdx.x * kRsThreads + threadIdx.x; e < n; e += (long long)gridDim.x * kRsThreads) {
+    uint32_t key;
+    int32_t val;
+    const bool ok = rs_get<2>(src, p, e, n, true, key, val);
+    keys[e] = ok ? key : kRsNoKey;
+    if (!ok && src.inv) src.inv[e] = -1;
+  }
 }
 
 __device__ __forceinline__ long long rs_count(const RsPass& p) {
@@ -295,17 +319,30 @@ int rsort_pairs(const RsSource& src, int64_t n, uint32_t lrange, int bits, void*
     uint32_t* ko = to_out ? out_keys : tk;
     int32_t* vo = to_out ? out_vals : tv;
     RsPass p{shift, pb, lrange, kin, vin, n_valid, n, i == 0 ? 1 : 0};
-    const int mode = i > 0 ? 0 : src.kind == 0 ? 1 : 2;
+    int mode = i > 0 ? 0 : src.kind == 0 ? 1 : 2;
+    if (mode == 2 && DL_RS_PREKEYS) {
+      // the keys into a buffer pass 0 does not write: out_keys when pass 0 lands in the
+      // temporaries, else the temporary keys (the first pass's output is the outputs)
+      uint32_t* pre = to_out ? tk : out_keys;
+      long long g = ((long long)n + kRsThreads - 1) / kRsThreads;
+      if (g > 8192) g = 8192;
+      hipLaunchKernelGGL(rs_keys_kernel, dim3((unsigned)g), dim3(kRsThreads), 0, s, src, (long long)n, pre);
+      p.kin = pre;
+      mode = 3;
+    }
     if (mode == 0) hipLaunchKernelGGL(rs_upsweep<0>, dim3(tiles), dim3(kRsThreads), 0, s, src, p, counts, tiles);
     else if (mode == 1) hipLaunchKernelGGL(rs_upsweep<1>, dim3(tiles), dim3(kRsThreads), 0, s, src, p, counts, tiles);
-    else hipLaunchKernelGGL(rs_upsweep<2>, dim3(tiles), dim3(kRsThreads), 0, s, src, p, counts, tiles);
+    else if (mode == 2) hipLaunchKernelGGL(rs_upsweep<2>, dim3(tiles), dim3(kRsThreads), 0, s, src, p, counts, tiles);
+    else hipLaunchKernelGGL(rs_upsweep<3>, dim3(tiles), dim3(kRsThreads), 0, s, src, p, counts, tiles);
     hipLaunchKernelGGL(rs_rowscan, dim3(1 << pb), dim3(kRsThreads), 0, s, counts, tiles, total);
     if (mode == 0)
       hipLaunchKernelGGL(rs_downsweep<0>, dim3(tiles), dim3(kRsThreads), 0, s, src, p, counts, tiles, total, ko, vo, n_valid);
     else if (mode == 1)
       hipLaunchKernelGGL(rs_downsweep<1>, dim3(tiles), dim3(kRsThreads), 0, s, src, p, counts, tiles, total, ko, vo, n_valid);
-    else
+    else if (mode == 2)
       hipLaunchKernelGGL(rs_downsweep<2>, dim3(tiles), dim3(kRsThreads), 0, s, src, p, counts, tiles, total, ko, vo, n_valid);
+    else
+      hipLaunchKernelGGL(rs_downsweep<3>, dim3(tiles), dim3(kRsThreads), 0, s, src, p, counts, tiles, total, ko, vo, n_valid);
     kin = ko;
     vin = vo;
     shift += pb;
