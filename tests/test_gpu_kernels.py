@@ -654,7 +654,8 @@ def test_sort_unique_matches_numpy(hip_lib, n, distinct):
 
 @pytest.mark.parametrize("M,N,K,epi,cbf", [(65536, 400, 432, 1, 1), (9000, 400, 400, 2, 1), (5000, 416, 400, 0, 0),
                                            (4100, 37, 200, 1, 0), (8192, 400, 416, 1, 0), (300, 209, 40, 2, 1),
-                                           (777, 208, 8, 1, 1), (1000, 100, 1000, 2, 0), (257, 400, 432, 0, 1)])
+                                           (777, 208, 8, 1, 1), (1000, 100, 1000, 2, 0), (257, 400, 432, 0, 1),
+                                           (1000, 300, 72, 2, 0), (129, 416, 48, 1, 1), (65536, 416, 400, 0, 0)])
 def test_gemm_bf16_b_resident(hip_lib, M, N, K, epi, cbf):
     """The tall-skinny bf16 path (ta=0, tb=1: the streamed-weight kernel gemm_bf16_nt_kernel,
     the B-resident kernel where it declines): relu / ReluGrad-mask / store epilogues, bf16 or
