@@ -216,6 +216,49 @@ def workload_name(wl, vocab, n_rows, sharded):
             }[wl] % (vocab, n_rows)
 
 
+def lookup_alone(eng, batch, B, per_sample, reps=20):
+    """SURVEY §8(d)'s embedding gather as a lookup kernel alone: right after a flush (every row
+    caught up, so no zero-gradient steps to replay) the flat record lookup dl_embed_fwd_rec_flat
+    that CTREngine.predict runs on a flushed table — each reference's row and first-order weight
+    read from its record's first line, the FM sums and x0 assembled; bit-identical to the
+    rec_gather + embed_fwd pair at lag 0 by test — preceded by the 13 replicated FM cont-field
+    rows' compact gather, both timed with HIP events on the launch stream."""
+    import torch
+    from deep_learning_amd import _lib
+    from deep_learning_amd._lib import call, ptr
+    from deep_learning_amd.engine import C_ref
+    sp = eng.spec
+    eng.stage(batch)
+    L = eng.layout
+    L.batch = B
+    s = _lib.stream_handle()
+    x0 = eng.x0b if eng.x0_direct else eng.x0
+
+    def run():
+        if eng.n_rep:
+            call("dl_rec_gather", C_ref(L), ptr(eng.rec), eng.rec_ld, eng.rec_flags, eng.n_rep, ptr(eng.idx_uniq), None,
+                 0, 1, ptr(eng.hist), eng.hist_len, ptr(eng.opt), 0, ptr(eng.rows_u), ptr(eng.rows_u1), None, s)
+        call("dl_embed_fwd_rec_flat", C_ref(L), ptr(eng.rec), eng.rec_ld, eng.rec_flags, ptr(eng.rows_u),
+             ptr(eng.rows_u1) if sp.fm else None, ptr(eng.in_cate), ptr(eng.in_cont), ptr(eng.in_vec), ptr(eng.opt),
+             ptr(x0), ptr(eng.fm_out), ptr(eng.fm_sum), ptr(eng.err), s)
+    run()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        run()
+    e1.record()
+    torch.cuda.synchronize()
+    eng.check_error()
+    us = e0.elapsed_time(e1) * 1e3 / reps
+    gb = B * per_sample / (us * 1e-6) / 1e9
+    return {"kernels": ["rec_gather (13 cont rows)", "embed_fwd_rec_flat"], "us": round(us, 1),
+            "GB/s": round(gb, 1), "frac": round(gb / HBM_PEAK_GBS, 3),
+            "note": "flushed table: the lookup without lazy Adam's catch-up (dl_embed_fwd_rec_flat, predict's "
+                    "forward on a flushed table); the training step's gather above also replays each row's "
+                    "pending zero-gradient Adam steps and stashes its moments"}
+
+
 def run_workload(wl, args, world, rank, sharded, steps, warmup, age, ksteps, barrier):
     """Build the engine of workload `wl`, age its table, time `steps` steps (hipGraph replay,
     next batch prefetched), then `ksteps` eager steps bracketed per kernel by HIP events.
@@ -365,6 +408,10 @@ def run_workload(wl, args, world, rank, sharded, steps, warmup, age, ksteps, bar
         fus = (time.perf_counter() - t0) * 1e6
         flush = {"us": round(fus, 1), "every_steps": eng.hist_len - 2,
                  "us_per_step_amortised": round(fus / (eng.hist_len - 2), 2)}
+        if per_sample and not spec.M:
+            gather_lookup = lookup_alone(eng, batches[base % nb], B, per_sample)
+            if gather is not None:
+                gather["lookup_alone"] = gather_lookup
     out = dict(spec=spec, value=value, ms=ms, loss=loss, roofline=roof, gather=gather, flush=flush, kernels=kernels,
                kernel_sum=sum(k["us"] for k in kernels.values()), nb=nb, gemm_peak=gemm_peak)
     del eng, batches

@@ -60,6 +60,7 @@ SIGNATURES = {
     "dl_embed_cont_reduce": (I32, [LP, P, I32, P, P, P, P]),
     "dl_embed_fwd_indexed": (I32, [LP, P, P, P, I32, P, P, P, P, P, P]),
     "dl_embed_fwd_rec": (I32, [LP, P, I32, I32, P, P, P, P, P, P, I32, P, I32, P, P, P, P, P]),
+    "dl_embed_fwd_rec_flat": (I32, [LP, P, I32, I32, P, P, P, P, P, P, P, P, P, P, P]),
     "dl_shard_gather": (I32, [P, P, P, I64, I32, P, P, P]),
     "dl_shard_scatter_add": (I32, [P, P, P, I64, I32, P, P, P, P]),
     "dl_slab_sum": (I32, [P, I32, I64, I64, P, P]),

@@ -67,8 +67,11 @@ constexpr int kMaxSlots = 128;     // FM slots + deep slots per sample
 #ifndef DL_POOL_DIAG_NO_W1
 #define DL_POOL_DIAG_NO_W1 0   // diagnostics build: first-order weights not read by the forward / pooling (wrong fm_out)
 #endif
-template <int E, int NPS, bool REC = false>
-__global__ __launch_bounds__(256, (REC || NPS > 5) ? 1 : DL_FWD_MIN_WAVES) void embed_fwd_kernel(EmbArgs a) {
+// REC: 0 dense table; 1 row records caught up in registers (lazy training); 2 row records
+// already caught up (a flushed table: predict after dl_rec_flush) — only each record's first
+// 128-B line is read (p and the first-order triple + stamp), a stale row faults (DL_STATUS_LAG).
+template <int E, int NPS, int REC = 0>
+__global__ __launch_bounds__(256, (REC == 1 || NPS > 5) ? 1 : DL_FWD_MIN_WAVES) void embed_fwd_kernel(EmbArgs a) {
   // Per block iteration a tile of 16 samples is staged: every (sample, slot)
   // row index is resolved once into LDS by a coalesced pass over the id matrix
   // (slot = FM field f < Fs, or deep field Fs + f).  Each wave then owns 4
@@ -95,7 +98,11 @@ __global__ __launch_bounds__(256, (REC || NPS > 5) ? 1 : DL_FWD_MIN_WAVES) void 
   int target = 0;
   extern __shared__ float hist_s[];   // record mode: the alpha ring, so the catch-up loop's
                                       // per-step reads are LDS hits, not L2 round trips
-  if (REC) {
+  if (REC == 2) {
+    target = (int)a.opt[7] - a.lag;
+    rc.status = opt_status(a.opt);
+  }
+  if (REC == 1) {
     rec_load_hyper(rc, a.opt);
     target = (int)a.opt[7] - a.lag;
     for (int k = threadIdx.x; k <= rc.hist_mask; k += blockDim.x) hist_s[k] = a.hist[k];
@@ -167,9 +174,30 @@ __global__ __launch_bounds__(256, (REC || NPS > 5) ? 1 : DL_FWD_MIN_WAVES) void 
         rw[p] = rows_s[j][sl < nslot ? sl : 0];
         if (sl >= nslot) rw[p] = -1;
       }
-      if (!REC) {
+      if (REC == 0) {
 #pragma unroll
         for (int p = 0; p < NPS; ++p) v[p] = tab4[(rw[p] < 0 ? 0 : rw[p]) * LPR + q];
+      } else if (REC == 2) {
+        float4 t4[NPS];
+#pragma unroll
+        for (int p = 0; p < NPS; ++p) {
+          const int sl = p * RPI + r;
+          if (sl < Cf) {
+            v[p] = tab4[(rw[p] < 0 ? 0 : rw[p]) * LPR + q];
+          } else {
+            const float* rr = a.rec + (int64_t)(rw[p] < 0 ? 0 : rw[p]) * rc.ld;
+            v[p] = *reinterpret_cast<const float4*>(rr + 4 * q);
+            t4[p] = *reinterpret_cast<const float4*>(rr + E);
+          }
+        }
+#pragma unroll
+        for (int p = 0; p < NPS; ++p) {
+          const int sl = p * RPI + r;
+          if (sl >= Cf && sl < nslot) {
+            if (rw[p] >= 0 && __float_as_int(t4[p].w) != target) raise_fault(rc.status, DL_STATUS_LAG);
+            if (sl < Fs && rc.has_first && q == 0) a.fm_out[(int64_t)b * L.fm_ld + sl] = rw[p] < 0 ? 0.f : t4[p].x * 1.f;
+          }
+        }
       } else {
         // slots >= Cf: the whole record (p, m, v, first-order triple + stamp) is loaded for
         // every pass before any is consumed, then caught up exactly as dl_rec_gather does
@@ -207,7 +235,7 @@ __global__ __launch_bounds__(256, (REC || NPS > 5) ? 1 : DL_FWD_MIN_WAVES) void 
       // staged: the FM cate fields' first-order outputs were written by the gather (their rows
       // index the staging rows, not first_order) — only the zero rows' are written here
       const bool w1_done = a.staged && lane >= Cf && lane < Fs && rows_s[j][lane] >= 0;
-      if (lane < (REC ? Cf : Fs)) {
+      if (lane < (REC != 0 ? Cf : Fs)) {
         frow = rows_s[j][lane];
         val = lane < Cf ? vals_s[j][lane] : 1.f;
         w1 = DL_POOL_DIAG_NO_W1 ? 1.f : a.first_order[(frow < 0 || w1_done) ? 0 : frow];
@@ -237,8 +265,8 @@ __global__ __launch_bounds__(256, (REC || NPS > 5) ? 1 : DL_FWD_MIN_WAVES) void 
           }
         }
       }
-      if (lane < (REC ? Cf : Fs) && !w1_done) a.fm_out[(int64_t)b * L.fm_ld + lane] = frow < 0 ? 0.f : w1 * val;
-      for (int f = 64 + lane; f < (REC ? 0 : Fs); f += 64) {   // > 64 FM fields (rare; record mode: <= 64)
+      if (lane < (REC != 0 ? Cf : Fs) && !w1_done) a.fm_out[(int64_t)b * L.fm_ld + lane] = frow < 0 ? 0.f : w1 * val;
+      for (int f = 64 + lane; f < (REC != 0 ? 0 : Fs); f += 64) {   // > 64 FM fields (rare; record mode: <= 64)
         const int fr = rows_s[j][f];
         if (a.staged && f >= Cf && fr >= 0) continue;
         const float vv = f < Cf ? vals_s[j][f] : 1.f;
@@ -712,7 +740,7 @@ static int emb_grid(int B) {
 
 using namespace dl;
 
-template <bool REC>
+template <int REC>
 static int launch_embed_fwd(const dl_emb_layout* L, const EmbArgs& a, void* stream);
 
 extern "C" int dl_embed_fwd(const dl_emb_layout* L, const float* table, const float* first_order,
@@ -723,7 +751,7 @@ extern "C" int dl_embed_fwd(const dl_emb_layout* L, const float* table, const fl
   DL_CHECK_ARG(!L->use_fm || (first_order && fm_out && fm_sum), "FM outputs required");
   if (L->batch == 0) return 0;
   EmbArgs a{*L, nullptr, 0, table, first_order, cate, cont, vector, x0, fm_out, fm_sum, err};
-  return launch_embed_fwd<false>(L, a, stream);
+  return launch_embed_fwd<0>(L, a, stream);
 }
 
 extern "C" int dl_embed_fwd_indexed(const dl_emb_layout* L, const float* rows, const float* rows_first,
@@ -734,7 +762,7 @@ extern "C" int dl_embed_fwd_indexed(const dl_emb_layout* L, const float* rows, c
   DL_CHECK_ARG(!L->use_fm || (rows_first && fm_out && fm_sum), "FM outputs required");
   if (L->batch == 0) return 0;
   EmbArgs a{*L, inv, inv_base, rows, rows_first, nullptr, cont, vector, x0, fm_out, fm_sum, nullptr};
-  return launch_embed_fwd<false>(L, a, stream);
+  return launch_embed_fwd<0>(L, a, stream);
 }
 
 extern "C" int dl_embed_fwd_staged(const dl_emb_layout* L, const float* fmst, const float* rows_first,
@@ -747,7 +775,7 @@ extern "C" int dl_embed_fwd_staged(const dl_emb_layout* L, const float* fmst, co
   if (L->batch == 0) return 0;
   EmbArgs a{*L, inv, n_rep, fmst ? fmst : x0, rows_first, nullptr, cont, vector, x0, fm_out, fm_sum, nullptr};
   a.staged = 1;
-  return launch_embed_fwd<false>(L, a, stream);
+  return launch_embed_fwd<0>(L, a, stream);
 }
 
 extern "C" int dl_embed_fwd_rec(const dl_emb_layout* L, const float* rec, int32_t rec_ld, int32_t rec_flags,
@@ -769,20 +797,39 @@ extern "C" int dl_embed_fwd_rec(const dl_emb_layout* L, const float* rec, int32_
   if (L->batch == 0) return 0;
   EmbArgs a{*L, nullptr, 0, rows_rep, rows_rep1, cate, cont, vector, x0, fm_out, fm_sum, err,
             rec, make_rec_cfg(L->emb_dim, rec_ld, rec_flags, hist_len), hist, opt, lag};
-  return launch_embed_fwd<true>(L, a, stream);
+  return launch_embed_fwd<1>(L, a, stream);
 }
 
-template <bool REC>
+extern "C" int dl_embed_fwd_rec_flat(const dl_emb_layout* L, const float* rec, int32_t rec_ld, int32_t rec_flags,
+                                     const float* rows_rep, const float* rows_rep1, const int64_t* cate,
+                                     const float* cont, const float* vector, const float* opt, float* x0,
+                                     float* fm_out, float* fm_sum, int32_t* err, void* stream) {
+  const int32_t has_first = rec_flags & DL_REC_FIRST;
+  if (int rc = check_layout(L)) return rc;
+  DL_CHECK_ARG(rec && cate && x0 && opt, "NULL argument");
+  DL_CHECK_ARG(rec_ld % 4 == 0 && rec_ld >= 3 * L->emb_dim + 4, "rec_ld %d too small", rec_ld);
+  DL_CHECK_ARG(L->multi_width == 0 && L->fm_extra == 0, "record forward: single-valued fields only");
+  const int Cf = (L->use_fm && L->fm_cont) ? L->cont_fields : 0;
+  DL_CHECK_ARG(Cf == 0 || (L->cont_rows_compact && rows_rep && (!has_first || rows_rep1)),
+               "the FM cont-field rows come compact in rows_rep / rows_rep1");
+  DL_CHECK_ARG(!L->use_fm || (fm_out && fm_sum && Cf + L->cate_fields <= 64), "FM outputs required (<= 64 fields)");
+  if (L->batch == 0) return 0;
+  EmbArgs a{*L, nullptr, 0, rows_rep, rows_rep1, cate, cont, vector, x0, fm_out, fm_sum, err,
+            rec, make_rec_cfg(L->emb_dim, rec_ld, rec_flags, 2), nullptr, opt, 0};
+  return launch_embed_fwd<2>(L, a, stream);
+}
+
+template <int REC>
 static int launch_embed_fwd(const dl_emb_layout* L, const EmbArgs& a, void* stream) {
   DL_CHECK_ARG((L->use_fm ? (L->fm_cont ? L->cont_fields : 0) + 2 * L->cate_fields : L->cate_fields) <= kMaxSlots,
                "too many fields per sample for the gather kernel (max %d slots)", kMaxSlots);
   const int tiles = (L->batch + kTileSamples - 1) / kTileSamples;
-  const int gmax = REC ? 1024 : 8192;   // record mode: each block stages the alpha ring once
+  const int gmax = REC == 1 ? 1024 : 8192;   // record mode: each block stages the alpha ring once
   const dim3 grid(tiles < gmax ? tiles : gmax), block(256);
   const int nslot = (L->use_fm ? (L->fm_cont ? L->cont_fields : 0) + L->cate_fields : 0) + L->cate_fields;
   const int rpi = 64 / (L->emb_dim / 4);
   const int nps = (nslot + rpi - 1) / rpi;
-  const size_t lds = REC ? (size_t)(a.rc.hist_mask + 1) * sizeof(float) : 0;
+  const size_t lds = REC == 1 ? (size_t)(a.rc.hist_mask + 1) * sizeof(float) : 0;
   hipStream_t st = as_stream(stream);
 #define DL_FWD(E_, N_) hipLaunchKernelGGL((embed_fwd_kernel<E_, N_, REC>), grid, block, lds, st, a)
   switch (L->emb_dim) {

@@ -793,7 +793,17 @@ class CTREngine:
             self._c("pool_fwd", "dl_pool_fwd", C_ref(L), ptr(self.table), ptr(self.first) if sp.fm else None,
                  ptr(self.in_cate), sp.S, ptr(self.slot_start), ptr(self.slot_end), sp.M, self.fm_pool_col,
                  ptr(self.x0), ptr(self.fm_out), ptr(self.cnt_emb), ptr(self.cnt_first), ptr(self.err), s)
-        if self.fwd_rec:
+        if not train and self.lazy and not sp.M and self.since_flush == 0 and type(self) is CTREngine:
+            # predict on a flushed table (every record caught up to the current step): the plain
+            # lookup, each reference reading its record's first line (dl_embed_fwd_rec_flat)
+            if self.n_rep:   # the replicated FM cont-field rows, compact
+                self._c("rec_gather", "dl_rec_gather", C_ref(L), ptr(self.rec), self.rec_ld, self.rec_flags, self.n_rep,
+                        ptr(self.idx_uniq), None, 0, 1, ptr(self.hist), self.hist_len, ptr(self.opt), 0,
+                        ptr(self.rows_u), ptr(self.rows_u1), None, s)
+            self._c("embed_fwd", "dl_embed_fwd_rec_flat", C_ref(L), ptr(self.rec), self.rec_ld, self.rec_flags,
+                    ptr(self.rows_u), ptr(self.rows_u1) if sp.fm else None, ptr(self.in_cate), ptr(self.in_cont),
+                    ptr(self.in_vec), ptr(self.opt), ptr(x0), ptr(self.fm_out), ptr(self.fm_sum), ptr(self.err), s)
+        elif self.fwd_rec:
             if self.n_rep:   # the replicated FM cont-field rows, caught up, compact
                 self._c("rec_gather", "dl_rec_gather", C_ref(L), ptr(self.rec), self.rec_ld, self.rec_flags, self.n_rep,
                         ptr(self.idx_uniq), None, 0, 1, ptr(self.hist), self.hist_len, ptr(self.opt),

@@ -145,6 +145,15 @@ int dl_embed_fwd_rec(const dl_emb_layout* L, const float* rec, int32_t rec_ld, i
                      const float* cont, const float* vector, const float* hist, int32_t hist_len,
                      const float* opt, int32_t lag, float* x0, float* fm_out, float* fm_sum,
                      int32_t* err, void* stream);
+/* The record forward on a flushed table (every row caught up to step opt[7]: after
+ * dl_rec_flush, before any further update): the plain lookup — each reference reads only its
+ * record's first 128-B line (p, and the first-order weight beside it); a row whose stamp is not
+ * opt[7] sets DL_STATUS_LAG (the host raises) instead of being read stale.  Same outputs as
+ * dl_embed_fwd_rec at lag 0.  rows_rep / rows_rep1: the C FM cont-field rows, compact. */
+int dl_embed_fwd_rec_flat(const dl_emb_layout* L, const float* rec, int32_t rec_ld, int32_t rec_flags,
+                          const float* rows_rep, const float* rows_rep1, const int64_t* cate,
+                          const float* cont, const float* vector, const float* opt, float* x0,
+                          float* fm_out, float* fm_sum, int32_t* err, void* stream);
 
 /* Hot cont-field rows only (the FM cont part of dl_embed_bwd): per-block
  * partials into cont_slab, folded in by dl_embed_cont_reduce. */

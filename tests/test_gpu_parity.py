@@ -9,6 +9,7 @@ import torch
 
 pytestmark = pytest.mark.gpu
 
+from deep_learning_amd import _lib  # noqa: E402
 from deep_learning_amd.engine import CTREngine, ModelSpec  # noqa: E402
 from deep_learning_amd.synthetic import make_batch  # noqa: E402
 from oracle import ctr_ref as R  # noqa: E402
@@ -170,6 +171,36 @@ def test_record_forward_bit_identical_to_gather(hip_lib, name):
     pa, pb = a.params(), b.params()
     for k in pa:
         np.testing.assert_array_equal(pa[k], pb[k], err_msg=k)
+
+
+@pytest.mark.parametrize("name", ["deepfm_pipeline", "dnn_pipeline", "wdl"])
+def test_flat_lookup_after_flush_bit_identical(hip_lib, name):
+    """predict() on a flushed table reads each reference's record first line only
+    (dl_embed_fwd_rec_flat) — the same scores and forward outputs as the gather + indexed
+    forward at lag 0 on the same table; after a further training step predict() leaves the flat
+    path; and the flat lookup on a table that is not caught up raises (DL_STATUS_LAG) instead of
+    reading stale rows."""
+    kw = dict(CASES[name], cate_index_size=50000)
+    spec = ModelSpec(_model(name), **kw)
+    e = CTREngine(spec, max_batch=128, seed=3, adam="lazy", hist_len=8)
+    bs = _batches(name, kw, 128, 6, seed=13)
+    for i, bt in enumerate(bs[:5]):
+        e.train_step(bt, graph=i >= 2)
+    ref = e.predict(bs[5], logits=True)           # gather + indexed forward, lag 0
+    ref_fm = e.fm_out[:128].cpu().numpy().copy()
+    e.flush()
+    assert e.since_flush == 0
+    got = e.predict(bs[5], logits=True)           # flat lookup
+    np.testing.assert_array_equal(got, ref)
+    np.testing.assert_array_equal(e.fm_out[:128].cpu().numpy(), ref_fm)
+    e.train_step(bs[0])
+    assert e.since_flush == 1
+    np.testing.assert_array_equal(e.predict(bs[5], logits=True), e.predict(bs[5], logits=True))
+    # forced onto a table whose touched rows lag: the status word, then the host raise
+    e.train_step(bs[1])
+    e.since_flush = 0
+    with pytest.raises(_lib.DLError, match="lagged"):
+        e.predict(bs[5])
 
 
 def test_lazy_multi_hot_tracks_oracle(hip_lib):
