@@ -19,6 +19,8 @@ Internal layouts (import/export map to the reference's):
   W_l = [in_ld, out_ld] row-major; row in_dim holds the bias, pads are zero
   head w = [first (F) | second (E) | deep (H) | bias]   (deepfm; dnn: [H | bias])
 """
+import contextlib
+import gc
 import math
 import os
 
@@ -1231,7 +1233,7 @@ class CTREngine:
         s = torch.cuda.Stream()
         s.wait_stream(torch.cuda.current_stream())
         g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g, stream=s):
+        with capture_guard(), torch.cuda.graph(g, stream=s):
             if with_pre or pre_only:
                 self._pre(B)
             if not pre_only:
@@ -1348,6 +1350,22 @@ def _s3_dw_splits(M, N, B, base, cus=256):
     def cost(s):
         return -(-tiles * s // cus) * (-(-(-(-B // s)) // 64) * 64)
     return min(range(base, 0, -1), key=cost)
+
+
+@contextlib.contextmanager
+def capture_guard():
+    """No Python garbage collection while a hipGraph is being captured: a collection that
+    frees an unreachable object holding a HIP resource (a torch.cuda.Event of an engine a
+    caller dropped) would call hipEventDestroy inside the capture, which HIP refuses (the
+    process aborts).  Garbage is collected before the capture instead."""
+    enabled = gc.isenabled()
+    gc.collect()
+    gc.disable()
+    try:
+        yield
+    finally:
+        if enabled:
+            gc.enable()
 
 
 def _bf16_dw_splits(M, B, base, cus=256):

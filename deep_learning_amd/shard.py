@@ -39,7 +39,7 @@ import torch.distributed as dist
 
 from . import _lib
 from ._lib import call, ptr
-from .engine import CTREngine, C_ref, _num_splits, _ru, call_int
+from .engine import CTREngine, C_ref, _num_splits, _ru, call_int, capture_guard
 
 
 class _Works:
@@ -653,7 +653,7 @@ class ShardedCTREngine(CTREngine):
             st = torch.cuda.Stream()
             st.wait_stream(torch.cuda.current_stream())
             cg = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(cg, stream=st):
+            with capture_guard(), torch.cuda.graph(cg, stream=st):
                 fn(B)
             torch.cuda.current_stream().wait_stream(st)
             g = (cg, B)
