@@ -248,27 +248,42 @@ __device__ __forceinline__ SegGrad4 segment_grad4_range_pf(const SegGradIn& a, i
   return r;
 }
 
-// segment_grad4_range over e0, e0 + stride, ... < e1 with four references' loads in flight
-// at a time (same sums, same order)
+// segment_grad4_range over e0, e0 + stride, ... < e1 (same sums, same order) for the long
+// segments of hot rows (Zipf: a C3 batch's hottest multi-hot row has ~10^5 references, ~3 k per
+// lane group): kSegUnroll references' data loads in flight at a time, and the next group's
+// reference indices loaded while this group's data is in flight — one memory round trip per
+// kSegUnroll references instead of two per four.
+#ifndef DL_SEG_UNROLL
+#define DL_SEG_UNROLL 16
+#endif
+constexpr int kSegUnroll = DL_SEG_UNROLL;
+
 template <int E>
 __device__ __forceinline__ SegGrad4 segment_grad4_strided(const SegGradIn& a, int e0, int e1, int stride, int q,
                                                           long long nrefs, float4 wsec) {
+  constexpr int U = kSegUnroll;
   const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
   SegGrad4 r{z, z, z, 0.f};
   const bool g1pool = a.g1_pool != nullptr;
-  for (int e = e0; e < e1; e += 4 * stride) {
-    int k[4];
-    bool in[4];
+  int kn[U];
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
+  for (int i = 0; i < U; ++i) kn[i] = e0 + i * stride < e1 ? a.refs[e0 + i * stride] : -1;
+  for (int e = e0; e < e1; e += U * stride) {
+    int k[U];
+    bool in[U];
+#pragma unroll
+    for (int i = 0; i < U; ++i) {
       in[i] = e + i * stride < e1;
-      k[i] = in[i] ? a.refs[e + i * stride] : -1;
+      k[i] = kn[i];
     }
-    SegRef f[4];
+    SegRef f[U];
 #pragma unroll
-    for (int i = 0; i < 4; ++i) f[i] = seg_fetch<E>(a, in[i], k[i], q, nrefs);
+    for (int i = 0; i < U; ++i) f[i] = seg_fetch<E>(a, in[i], k[i], q, nrefs);
+    const int en = e + U * stride;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) seg_acc(r, f[i], wsec, g1pool);
+    for (int i = 0; i < U; ++i) kn[i] = en + i * stride < e1 ? a.refs[en + i * stride] : -1;
+#pragma unroll
+    for (int i = 0; i < U; ++i) seg_acc(r, f[i], wsec, g1pool);
   }
   return r;
 }
