@@ -252,9 +252,10 @@ __device__ __forceinline__ SegGrad4 segment_grad4_range_pf(const SegGradIn& a, i
 // segments of hot rows (Zipf: a C3 batch's hottest multi-hot row has ~10^5 references, ~3 k per
 // lane group): kSegUnroll references' data loads in flight at a time, and the next group's
 // reference indices loaded while this group's data is in flight — one memory round trip per
-// kSegUnroll references instead of two per four.
+// kSegUnroll references instead of two.  (16 in flight: 198 VGPRs, the long kernel's 1,024
+// blocks in two rounds, and no faster on hot rows; 4 keeps 4 waves per SIMD: profiles/r03u4/.)
 #ifndef DL_SEG_UNROLL
-#define DL_SEG_UNROLL 16
+#define DL_SEG_UNROLL 4
 #endif
 constexpr int kSegUnroll = DL_SEG_UNROLL;
 
