@@ -128,10 +128,11 @@ PMC_KERNEL_LAZY = {"rec_gather": ("rec_gather_kernel<16, false, false>", "rec_ga
                    "head": "head_kernel"}
 
 
-def pmc_traffic(label, world, lazy=False, workload="c2"):
+def pmc_traffic(label, world, lazy=False, workload="c2", id_dist="uniform"):
     """HBM bytes per launch of `label` from the newest committed PMC summary of the same
     workload (scripts/pmc_summary.py: (2*FETCH_SIZE + WRITE_SIZE)*1024, gfx950 correction;
-    a summary without a "workload" key was collected on C2).  Newest = the latest round tag
+    a summary without a "workload" key was collected on C2; one without "id_dist" on uniform ids,
+    and a workload's zipf traffic is only taken from a zipf summary).  Newest = the latest round tag
     (profiles/r02s > r02q > r01r): file times do not survive a checkout or a copy."""
     import glob
     names = PMC_KERNEL_LAZY if lazy else PMC_KERNEL
@@ -140,7 +141,7 @@ def pmc_traffic(label, world, lazy=False, workload="c2"):
     files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*", "pmc_summary*.json")))
     for f in reversed(files):
         d = json.load(open(f))
-        if d.get("workload", "c2") != workload:
+        if d.get("workload", "c2") != workload or d.get("id_dist", "uniform") != id_dist:
             continue
         want = names[label] if isinstance(names[label], tuple) else (names[label],)
         for n in want:
@@ -150,15 +151,14 @@ def pmc_traffic(label, world, lazy=False, workload="c2"):
     return None
 
 
-def cpu_baseline(spec_kw, B, steps_big=20, steps_small=50, warm=2):
+def cpu_baseline(spec_kw, B, steps_big=12, warm_big=2, steps_small=50, warm_small=10):
     """The CPU baseline of BASELINE.md §2: the torch-CPU restatement of
     models/deepfm_pipeline.py (oracle/torch_cpu.py; the reference's TF-CPU path cannot run
     without TensorFlow) timed on this host's cores at the full C2 table (26M rows, dense TF1
-    Adam over every row), at the headline batch (65,536: `value`) and at the reference's
-    default batch (1,024).  Median step time of `steps_big` / `steps_small` steps after
-    `warm` warmup steps each (BASELINE.md asks >= 50 after 10: at B = 65,536 a step takes
-    ~3.4 s, so 20 keep the default bench inside its time budget; the count is in the label).
-    """
+    Adam over every row), at the reference's default batch (1,024: SURVEY §8(d)'s >= 50 steps
+    after 10 warmups) and at the headline batch (65,536: `value`, as many steps as the
+    default bench's time budget allows — each sweeps the 26M-row table, ~2.5-3.4 s).
+    Median step time; the counts are in the label."""
     import torch
     from oracle import ctr_ref as R
     from oracle.torch_cpu import DeepFMPipelineCPU
@@ -172,7 +172,7 @@ def cpu_baseline(spec_kw, B, steps_big=20, steps_small=50, warm=2):
     m = DeepFMPipelineCPU(spec_kw["C"], spec_kw["S"], spec_kw["E"], N, spec_kw["hidden"],
                           R.init_params(cfg, np.random.default_rng(0)))
     res = {}
-    for bsz, n in ((B, steps_big), (1024, steps_small)):
+    for bsz, n, warm in ((1024, steps_small, warm_small), (B, steps_big, warm_big)):
         bs = [make_batch(bsz, cate_index_size=N, seed=7 + i) for i in range(4)]
         for i in range(warm):
             m.train_step(bs[i % 4])
@@ -181,17 +181,25 @@ def cpu_baseline(spec_kw, B, steps_big=20, steps_small=50, warm=2):
             t0 = time.perf_counter()
             m.train_step(bs[i % 4])
             ts.append(time.perf_counter() - t0)
-        res[bsz] = (float(np.median(ts)), len(ts))
-        log("cpu baseline B=%d: median %.3f s over %d steps" % (bsz, res[bsz][0], n))
-    med, n = res[B]
-    med1, n1 = res[1024]
+        res[bsz] = (float(np.median(ts)), len(ts), warm)
+        log("cpu baseline B=%d: median %.3f s over %d steps after %d warmup" % (bsz, res[bsz][0], n, warm))
+    med, n, w = res[B]
+    med1, n1, w1 = res[1024]
     return {"value": B / med, "unit": "samples/s", "cores": threads, "kind": "port",
             "sample": "torch-CPU restatement of deepfm_pipeline.py (oracle/torch_cpu.py), full C2 table "
                       "(26M rows, dense TF1 Adam over every row, autograd backward), %d intra-op threads; "
-                      "median of %d steps at B=%d (%.2f s/step) after %d warmup steps (BASELINE.md asks 50 "
-                      "after 10; 20 fit the bench's time budget at ~3.4 s/step); B=1024: median of %d steps "
-                      "after %d warmup" % (threads, n, B, med, warm, n1, warm),
-            "b1024": {"value": 1024 / med1, "median_s": round(med1, 3), "steps": n1}}
+                      "value: median of %d steps at B=%d (%.2f s/step) after %d warmup steps (the bench's time "
+                      "budget); B=1024: median of %d steps after %d warmup (SURVEY §8(d))"
+                      % (threads, n, B, med, w, n1, w1),
+            "b1024": {"value": 1024 / med1, "median_s": round(med1, 3), "steps": n1, "warmup": w1}}
+
+
+def vocab_for(wl, args, sharded):
+    """Per-field vocab of a workload: --vocab, else 1M (C2, C3, C5 at every N) or, for the
+    sharded DeepFM (C4), 100M rows over the 26 fields."""
+    if args.vocab:
+        return args.vocab
+    return C2["per_field_vocab"] if (not sharded or wl != "c2") else -(-100_000_000 // C2["S"])
 
 
 def make_spec(wl, vocab):
@@ -269,7 +277,7 @@ def run_workload(wl, args, world, rank, sharded, steps, warmup, age, ksteps, bar
     from deep_learning_amd.engine import CTREngine
     from deep_learning_amd.synthetic import make_batch, make_batch_device
     B = args.batch
-    spec = make_spec(wl, args.vocab)
+    spec = make_spec(wl, vocab_for(wl, args, sharded))
     log("%s rank %d/%d: building engine, table rows %d" % (wl, rank, world, spec.n_rows))
     use_graph = not args.no_graph
     prefetch = not args.no_prefetch
@@ -381,7 +389,7 @@ def run_workload(wl, args, world, rank, sharded, steps, warmup, age, ksteps, bar
         roof = {"kernel": dom, "bound": "mfma", "achieved": round(ach, 2), "peak": round(gemm_peak, 1),
                 "unit": "TFLOP/s", "frac": round(ach / gemm_peak, 3), "traffic": None,
                 "algorithmic_flops": amount}
-    pmc = pmc_traffic(dom, world, lazy=uniq is not None, workload=wl)
+    pmc = pmc_traffic(dom, world, lazy=uniq is not None, workload=wl, id_dist=args.dist)
     if pmc is not None:
         roof["traffic"] = pmc["hbm_bytes"]
         roof["traffic_source"] = pmc["source"]
@@ -418,6 +426,52 @@ def run_workload(wl, args, world, rank, sharded, steps, warmup, age, ksteps, bar
     torch.cuda.synchronize()
     torch.cuda.empty_cache()
     return out
+
+
+def free_port():
+    """A free TCP port on 127.0.0.1 for the ranks' rendezvous."""
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_command(n, argv, port, script=None):
+    """The command that runs this bench as `n` ranks, one process per GPU (the driver's own
+    form: torch.distributed.run on one node, rendezvous on 127.0.0.1).  `argv` is this
+    process's argument list; every rank parses the same arguments."""
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(n),
+            "--master-addr", "127.0.0.1", "--master-port", str(port),
+            script or os.path.abspath(__file__)] + list(argv)
+
+
+def world_check(gpus, env):
+    """(world, need_launch): under a launcher (WORLD_SIZE set) the world must be --gpus;
+    without one, --gpus N > 1 means this process starts the N ranks itself."""
+    ws = env.get("WORLD_SIZE")
+    if ws is None:
+        return 1, gpus > 1
+    if int(ws) != gpus:
+        raise SystemExit("bench.py: WORLD_SIZE=%s from the launcher but --gpus %d: the line would misreport "
+                         "n_gpus; launch --nproc-per-node %d or pass --gpus %s" % (ws, gpus, gpus, ws))
+    return int(ws), False
+
+
+def relay_ranks(n, argv, json_fd, script=None):
+    """Run the bench as n rank processes (started before this process touches the GPU: it
+    never initialises HIP, so no exec or fork of a GPU-holding process happens), relay rank
+    0's JSON line to our stdout and return the launcher's exit code."""
+    import subprocess
+    cmd = launch_command(n, argv, free_port(), script)
+    log("launching %d ranks: %s" % (n, " ".join(cmd)))
+    p = subprocess.run(cmd, stdout=subprocess.PIPE, stderr=None, env=dict(os.environ))
+    lines = [l for l in p.stdout.decode(errors="replace").splitlines() if l.startswith("{")]
+    for l in lines[-1:]:
+        os.write(json_fd, (l + "\n").encode())
+    if p.returncode == 0 and not lines:
+        log("the ranks exited 0 without a result line")
+        return 1
+    return p.returncode
 
 
 def main():
@@ -458,10 +512,14 @@ def main():
                     help="table Adam: dense sweep, or row records with lazy-exact catch-up (same result)")
     args = ap.parse_args()
 
+    # --gpus N without a launcher: start the N ranks now, before anything touches the GPU
+    world, need_launch = world_check(args.gpus, os.environ)
+    if need_launch:
+        sys.exit(relay_ranks(args.gpus, sys.argv[1:], json_fd))
+
     import torch
     import torch.distributed as dist
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     # DLAMD_BENCH_BACKEND=gloo: rehearsal of the multi-rank flow with ranks sharing one GPU
@@ -486,9 +544,6 @@ def main():
             dist.barrier()
 
     wl = args.workload
-    if not args.vocab:
-        # C4 (the default multi-GPU workload): a 100M-row table; C5 keeps its 26 x 1M vocab at every N
-        args.vocab = C2["per_field_vocab"] if (not sharded or wl == "c5") else 100_000_000 // C2["S"]
     if wl == "c3" and sharded:
         raise SystemExit("--workload c3 is single-GPU here; the multi-GPU workloads are C4 (default) and C5")
     r = run_workload(wl, args, world, rank, sharded, args.steps, args.warmup, args.age_steps,
@@ -497,22 +552,29 @@ def main():
     B = args.batch
     # the other single-GPU BASELINE configurations, timed the same way with fewer steps, so the
     # driver's run covers every single-GPU config (BASELINE.json configs[2], configs[4])
+    # (N > 1: the sharded Wide&Deep, C5 at N GPUs, after the sharded DeepFM C4)
     extra = {}
-    if world == 1 and not sharded and not args.no_extra:
-        for w2 in ("c2", "c3", "c5"):
-            if w2 == wl:
-                continue
-            try:
-                e = run_workload(w2, args, world, rank, False, args.extra_steps, min(args.warmup, 3),
-                                 args.age_steps, 5, barrier)
-            except Exception as ex:   # reported, never fatal for the headline number
-                extra[w2] = {"error": repr(ex)}
-                continue
-            extra[w2] = {"workload": workload_name(w2, args.vocab, e["spec"].n_rows, False),
-                         "ms_per_step": round(e["ms"], 4), "samples_per_s": round(e["value"], 1),
-                         "steps": args.extra_steps, "roofline": e["roofline"], "gather_north_star": e["gather"],
-                         "kernel_sum_us_per_step": round(e["kernel_sum"], 1), "loss": round(e["loss"], 6),
-                         "kernels": e["kernels"]}
+    others = ()
+    if not args.no_extra:
+        if world == 1 and not sharded:
+            others = tuple(w2 for w2 in ("c2", "c3", "c5") if w2 != wl)
+        elif world > 1 and wl == "c2":
+            others = ("c5",)
+    for w2 in others:
+        try:
+            e = run_workload(w2, args, world, rank, sharded, args.extra_steps, min(args.warmup, 3),
+                             args.age_steps, 5, barrier)
+        except Exception as ex:   # reported, never fatal for the headline number
+            if world > 1:         # a rank that failed alone would leave the others in a collective
+                raise
+            extra[w2] = {"error": repr(ex)}
+            continue
+        extra[w2] = {"workload": workload_name(w2, vocab_for(w2, args, sharded), e["spec"].n_rows, sharded),
+                     "global_batch": B * world,
+                     "ms_per_step": round(e["ms"], 4), "samples_per_s": round(e["value"], 1),
+                     "steps": args.extra_steps, "roofline": e["roofline"], "gather_north_star": e["gather"],
+                     "kernel_sum_us_per_step": round(e["kernel_sum"], 1), "loss": round(e["loss"], 6),
+                     "kernels": e["kernels"]}
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         log("cpu baseline (torch-CPU restatement)")
@@ -539,7 +601,10 @@ def main():
                      "every step, resident in HBM before the timed region)" if args.dist == "uniform" else
                      "synthetic (seeded Criteo-shaped batches, zipf ids, %d batches cycled, resident in HBM)"
                      % r["nb"]),
-            "config": {"workload": workload_name(wl, args.vocab, spec.n_rows, sharded),
+            "world": {"torch_distributed": dist.get_world_size() if sharded else 1,
+                      "backend": dist.get_backend() if sharded else None,
+                      "ranks": world, "device_per_rank": backend == "nccl"},
+            "config": {"workload": workload_name(wl, vocab_for(wl, args, sharded), spec.n_rows, sharded),
                        "global_batch": B * world, "per_gpu_batch": B,
                        "parallelism": "dp%d" % world if not sharded else
                        "dp%d + row-sharded table (RCCL all-to-all lookup, all-reduce dense grads)" % world,

@@ -44,6 +44,7 @@ STATUS_BAD_ID, STATUS_LAG, STATUS_INDEX = 1, 2, 4
 REC_FIRST, REC_SPARSE_ADAM = 1, 2
 ROWS_CLEAR_TOUCHED, ROWS_SPARSE_ADAM, ROWS_GRAD_FIXED = 1, 2, 4
 WIDE_GRAD_SCALE = 2.0 ** 48
+LOSS_ACC_SLOTS = 65536
 
 P = C.c_void_p
 I32, I64, U64, F = C.c_int32, C.c_int64, C.c_uint64, C.c_float
@@ -90,6 +91,7 @@ SIGNATURES = {
     "dl_adam_begin_step": (I32, [P, F, F, P]),
     "dl_step_guard": (I32, [P, P, P]),
     "dl_step_begin": (I32, [P, P, F, F, P, I32, P]),
+    "dl_loss_accumulate": (I32, [P, I32, I32, I32, C.c_double, P, F, P, P]),
     "dl_validate_batch": (I32, [LP, P, P, I32, I32, I64, I32, P, P]),
     "dl_adam_dense": (I32, [P, P, P, P, I32, I64, I64, F, I64, P, P, P, P]),
     "dl_adam_dense_split3": (I32, [P, P, P, P, I32, I64, I32, I32, F, I64, I32, P, P, P, P, P]),
@@ -120,11 +122,11 @@ SIGNATURES = {
     "dl_wide_fold_owned": (I32, [P, I32, I64, I32, I32, P, P, P]),
     "dl_wide_owned_values": (I32, [P, I32, I64, I32, I32, P, P]),
     "dl_wide_local_ids": (I32, [P, I64, I64, P, P]),
-    "dl_wide_rec_gather": (I32, [P, I64, P, P, I64, I32, I32, P, I32, P, F, I32, P, P, P]),
+    "dl_wide_rec_gather": (I32, [P, I64, P, P, I64, I32, I32, P, I32, P, F, I32, P, P, P, P]),
     "dl_wide_update_blocks": (I64, [I64, I32]),
     "dl_wide_seg_grad": (I32, [P, I32, P, P, P, I64, I64, P, P, P, P]),
-    "dl_wide_rec_update": (I32, [P, P, I64, P, P, I32, I32, F, P, I32, P, P, P, P]),
-    "dl_wide_rec_flush": (I32, [P, I64, F, P, I32, P, P, P]),
+    "dl_wide_rec_update": (I32, [P, P, I64, P, P, I32, I32, F, P, I32, P, P, P, P, P, P]),
+    "dl_wide_rec_flush": (I32, [P, I64, F, P, I32, P, P, P, P]),
     "dl_comm_unique_id_bytes": (I32, []),
     "dl_comm_get_unique_id": (I32, [P]),
     "dl_comm_init": (I32, [P, I32, I32, P]),

@@ -47,6 +47,32 @@ __device__ __forceinline__ void step_guard_kernel_body(const int32_t* batch_err,
 
 __global__ void step_guard_kernel(const int32_t* batch_err, float* opt) { step_guard_kernel_body(batch_err, opt); }
 
+// The running loss of a training loop — the load-style fit's epoch mean of the per-step loss
+// (wdl.py:305-313, deepfm.py:172-190, dnn.py:111-127 sum loss_t * batch_size over the epoch):
+// acc[0] += the step's data term (the head slab's loss column summed in a fixed order, in
+// double, times inv_b); acc[1] += reg_coef * opt[8] (the step's regulariser sum, accumulated by
+// the Adam kernels); acc[2] += 1.  A skipped step (bad batch) adds nothing.  One block, so the
+// step needs no host read; the host reads acc once per epoch.
+__global__ __launch_bounds__(256) void loss_accumulate_kernel(const float* __restrict__ slab, int rows, int pitch,
+                                                              int col, double inv_b, const float* __restrict__ opt,
+                                                              float reg_coef, double* __restrict__ acc) {
+  __shared__ double part[256];
+  if (step_poisoned(opt)) return;
+  double s = 0.0;
+  for (int r = threadIdx.x; r < rows; r += blockDim.x) s += (double)slab[(long long)r * pitch + col];
+  part[threadIdx.x] = s;
+  __syncthreads();
+  for (int o = 128; o >= 1; o >>= 1) {
+    if ((int)threadIdx.x < o) part[threadIdx.x] += part[threadIdx.x + o];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    acc[0] += part[0] * inv_b;
+    acc[1] += (double)reg_coef * (double)opt[8];
+    acc[2] += 1.0;
+  }
+}
+
 // The three scalar updates that open a training step, in one launch (one graph node instead
 // of three): the guard (dl_step_guard), the Adam step begin (dl_adam_begin_step) and, for the
 // lazy tables, the alpha ring entry (dl_adam_hist_record) — the same operations in the same order.
@@ -351,6 +377,15 @@ extern "C" int dl_step_guard(const int32_t* batch_err, float* opt, void* stream)
   DL_CHECK_ARG(batch_err && opt, "NULL pointer");
   hipLaunchKernelGGL(step_guard_kernel, dim3(1), dim3(1), 0, as_stream(stream), batch_err, opt);
   DL_RETURN_LAUNCH("dl_step_guard");
+}
+
+extern "C" int dl_loss_accumulate(const float* slab, int32_t rows, int32_t pitch, int32_t col, double inv_b,
+                                  const float* opt, float reg_coef, double* acc, void* stream) {
+  DL_CHECK_ARG(slab && opt && acc, "NULL pointer");
+  DL_CHECK_ARG(rows >= 0 && pitch > col && col >= 0, "bad slab shape");
+  hipLaunchKernelGGL(loss_accumulate_kernel, dim3(1), dim3(256), 0, as_stream(stream), slab, rows, pitch, col, inv_b,
+                     opt, reg_coef, acc);
+  DL_RETURN_LAUNCH("dl_loss_accumulate");
 }
 
 extern "C" int dl_step_begin(const int32_t* batch_err, float* opt, float decay_rate, float decay_steps, float* hist,

@@ -77,6 +77,32 @@ __device__ __forceinline__ void wide_catch_up(float& w, float& m, float& v, int 
     adam_elem(w, m, v, wide_l2_grad(0.f, h.l2, w), hist[j & h.mask], h.omb1, h.omb2, h.eps);
 }
 
+// the same, summing w^2 of each replayed step's pre-update state (the loss's L2 term of that
+// step for this row: wdl.py:270-271) into sq
+__device__ __forceinline__ void wide_catch_up_sq(float& w, float& m, float& v, int from, int to,
+                                                 const float* __restrict__ hist, const WideHyper& h, float& sq) {
+  for (int j = from + 1; j <= to; ++j) {
+    sq = fmaf(w, w, sq);
+    adam_elem(w, m, v, wide_l2_grad(0.f, h.l2, w), hist[j & h.mask], h.omb1, h.omb2, h.eps);
+  }
+}
+
+// A kernel's running-loss contribution: the block's sum added to its own slot of acc (double;
+// slots are per block index, and the kernels that add to them run in stream order, so no
+// atomics).  The host sums the slots when it reads the running loss (engine.loss_sum_end).
+__device__ __forceinline__ void block_sum_accumulate(float x, double* acc) {
+  __shared__ float part[16];
+  x = wave_sum(x);
+  if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = x;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float t = 0.f;
+    for (int w = 0; w < (int)(blockDim.x >> 6); ++w) t += part[w];
+    acc[blockIdx.x] += (double)t;
+  }
+  __syncthreads();
+}
+
 __device__ __forceinline__ int wide_from(float stamp_bits, int target, int hist_len, int* status) {
   const int st = __float_as_int(stamp_bits);
   if (target - st >= hist_len - 1) {   // lagged past the alpha ring: report, never truncate silently
@@ -94,7 +120,7 @@ __global__ __launch_bounds__(256) void wide_rec_gather_kernel(const float4* __re
                                                               int Fw, int H, const float* __restrict__ hist,
                                                               int hist_len, const float* __restrict__ opt, float l2,
                                                               int lag, float* __restrict__ wloc,
-                                                              float4* __restrict__ stash) {
+                                                              float4* __restrict__ stash, float* __restrict__ rep_sq) {
   const WideHyper h = wide_hyper(opt, l2, hist_len);
   int* status = opt_status(opt);
   const int target = (int)opt[7] - lag;
@@ -108,9 +134,14 @@ __global__ __launch_bounds__(256) void wide_rec_gather_kernel(const float4* __re
     }
     float4 r = rec[row * kWideRecF4];
     const int from = wide_from(r.w, target, hist_len, status);
-    if (from < target) wide_catch_up(r.x, r.y, r.z, from, target, hist, h);
+    float sq = 0.f;
+    if (from < target) {
+      if (rep_sq && i >= H) wide_catch_up_sq(r.x, r.y, r.z, from, target, hist, h, sq);
+      else wide_catch_up(r.x, r.y, r.z, from, target, hist, h);
+    }
     wloc[Fw + i] = r.x;   // i < H: the deep-output row Fw + i; else local row Fw + H + u
     if (i >= H && stash) stash[i - H] = make_float4(r.x, r.y, r.z, __int_as_float((int)row));
+    if (i >= H && rep_sq) rep_sq[i - H] = sq;   // the replayed steps' L2 terms, counted once the update lands
   }
 }
 
@@ -121,13 +152,14 @@ __global__ __launch_bounds__(256) void wide_rec_update_kernel(float4* __restrict
                                                               long long max_u, const float4* __restrict__ stash,
                                                               long long* __restrict__ gloc, int Fw, int H, float l2,
                                                               int hist_len, const float* __restrict__ opt,
-                                                              uint8_t* __restrict__ dmark, float* __restrict__ sq_out) {
+                                                              uint8_t* __restrict__ dmark, float* __restrict__ sq_out,
+                                                              const float* __restrict__ rep_sq, double* __restrict__ acc) {
   const WideHyper h = wide_hyper(opt, l2, hist_len);
   const bool skip = step_poisoned(opt);
   const int t = (int)opt[7];
   const float alpha = opt[3];
   const long long nu = (long long)min((long long)max(n_uniq[0], 0), max_u);
-  float sq = 0.f;
+  float sq = 0.f, run = 0.f;
   for (long long u = (long long)blockIdx.x * blockDim.x + threadIdx.x; u < nu; u += (long long)gridDim.x * blockDim.x) {
     const float4 s = stash[u];
     const long long row = (long long)__float_as_int(s.w);
@@ -141,10 +173,12 @@ __global__ __launch_bounds__(256) void wide_rec_update_kernel(float4* __restrict
     if (skip) continue;
     float w = s.x, m = s.y, v = s.z;
     sq += w * w;
+    if (acc) run += (rep_sq ? rep_sq[u] : 0.f) + w * w;
     adam_elem(w, m, v, wide_l2_grad(wide_float(q), h.l2, w), alpha, h.omb1, h.omb2, h.eps);
     wide_rec_store(rec, row, make_float4(w, m, v, __int_as_float(t)));
   }
   if (sq_out) block_sum_store(sq, sq_out + blockIdx.x);
+  if (acc) block_sum_accumulate(run, acc);
 }
 
 // Pass B: the H deep-output rows pass A did not cover (their gradient: the deep term alone).
@@ -152,12 +186,12 @@ __global__ __launch_bounds__(256) void wide_rec_update_deep_kernel(float4* __res
                                                                    int Fw, int H, float l2, const float* __restrict__ hist,
                                                                    int hist_len, const float* __restrict__ opt,
                                                                    uint8_t* __restrict__ dmark,
-                                                                   float* __restrict__ sq_out) {
+                                                                   float* __restrict__ sq_out, double* __restrict__ acc) {
   const WideHyper h = wide_hyper(opt, l2, hist_len);
   const bool skip = step_poisoned(opt);
   const int t = (int)opt[7];
   const float alpha = opt[3];
-  float sq = 0.f;
+  float sq = 0.f, run = 0.f;
   for (int j = blockIdx.x * blockDim.x + threadIdx.x; j < H; j += gridDim.x * blockDim.x) {
     const long long row = Fw + j;
     const long long q = gloc[row];
@@ -169,12 +203,14 @@ __global__ __launch_bounds__(256) void wide_rec_update_deep_kernel(float4* __res
     if (skip) continue;
     float4 r = rec[row * kWideRecF4];
     const int from = wide_from(r.w, t - 1, hist_len, opt_status(opt));
-    if (from < t - 1) wide_catch_up(r.x, r.y, r.z, from, t - 1, hist, h);
+    if (from < t - 1) wide_catch_up_sq(r.x, r.y, r.z, from, t - 1, hist, h, run);
     sq += r.x * r.x;
+    run += r.x * r.x;
     adam_elem(r.x, r.y, r.z, wide_l2_grad(wide_float(q), h.l2, r.x), alpha, h.omb1, h.omb2, h.eps);
     wide_rec_store(rec, row, make_float4(r.x, r.y, r.z, __int_as_float(t)));
   }
   if (sq_out) block_sum_store(sq, sq_out + blockIdx.x);
+  if (acc) block_sum_accumulate(run, acc);
 }
 
 // Every row caught up to step opt[7].  Rows the last step did not touch (stamp < t) pass
@@ -183,21 +219,23 @@ __global__ __launch_bounds__(256) void wide_rec_update_deep_kernel(float4* __res
 __global__ __launch_bounds__(256) void wide_rec_flush_kernel(float4* __restrict__ rec, long long w_rows, float l2,
                                                              const float* __restrict__ hist, int hist_len,
                                                              const float* __restrict__ opt,
-                                                             float* __restrict__ sq_untouched) {
+                                                             float* __restrict__ sq_untouched, double* __restrict__ acc) {
   const WideHyper h = wide_hyper(opt, l2, hist_len);
   const int t = (int)opt[7];
-  float sq = 0.f;
+  float sq = 0.f, run = 0.f;
   for (long long row = (long long)blockIdx.x * blockDim.x + threadIdx.x; row < w_rows;
        row += (long long)gridDim.x * blockDim.x) {
     float4 r = rec[row * kWideRecF4];   // (the sweep reads every slot's line: the record alone is written back)
     const int from = wide_from(r.w, t, hist_len, opt_status(opt));
     if (from >= t) continue;
-    if (from < t - 1) wide_catch_up(r.x, r.y, r.z, from, t - 1, hist, h);
+    if (from < t - 1) wide_catch_up_sq(r.x, r.y, r.z, from, t - 1, hist, h, run);
     sq += r.x * r.x;
+    run += r.x * r.x;
     wide_catch_up(r.x, r.y, r.z, t - 1, t, hist, h);
     rec[row * kWideRecF4] = make_float4(r.x, r.y, r.z, __int_as_float(t));
   }
   if (sq_untouched) block_atomic_add(sq, sq_untouched);
+  if (acc) block_sum_accumulate(run, acc);
 }
 
 // The batch's wide gradient per unique wide row, from the wide index instead of atomics:
@@ -270,7 +308,8 @@ using namespace dl;
 
 extern "C" int dl_wide_rec_gather(const float* rec, int64_t w_rows, const uint32_t* uniq_rows, const int32_t* n_uniq,
                                   int64_t max_uniq, int32_t Fw, int32_t H, const float* hist, int32_t hist_len,
-                                  const float* opt, float l2, int32_t lag, float* wloc, float* stash, void* stream) {
+                                  const float* opt, float l2, int32_t lag, float* wloc, float* stash, float* rep_sq,
+                                  void* stream) {
   DL_CHECK_ARG(rec && hist && opt && wloc && (max_uniq == 0 || uniq_rows), "NULL argument");
   DL_CHECK_ARG(hist_len >= 2 && (hist_len & (hist_len - 1)) == 0, "hist_len must be a power of two");
   DL_CHECK_ARG(Fw >= 0 && H >= 0 && (long long)Fw + H <= w_rows, "bad Fw / H");
@@ -279,7 +318,7 @@ extern "C" int dl_wide_rec_gather(const float* rec, int64_t w_rows, const uint32
   if (n == 0) return 0;
   hipLaunchKernelGGL(wide_rec_gather_kernel, dim3(wide_rows_grid(n)), dim3(256), 0, as_stream(stream),
                      reinterpret_cast<const float4*>(rec), (long long)w_rows, uniq_rows, n_uniq, (long long)max_uniq,
-                     Fw, H, hist, hist_len, opt, l2, lag, wloc, reinterpret_cast<float4*>(stash));
+                     Fw, H, hist, hist_len, opt, l2, lag, wloc, reinterpret_cast<float4*>(stash), rep_sq);
   DL_RETURN_LAUNCH("dl_wide_rec_gather");
 }
 
@@ -306,7 +345,8 @@ extern "C" int dl_wide_seg_grad(const float* dz, int32_t Fw, const int32_t* refs
 
 extern "C" int dl_wide_rec_update(float* rec, const int32_t* n_uniq, int64_t max_uniq, const float* stash, int64_t* gloc,
                                   int32_t Fw, int32_t H, float l2, const float* hist, int32_t hist_len,
-                                  const float* opt, uint8_t* dmark, float* sq_out, void* stream) {
+                                  const float* opt, uint8_t* dmark, float* sq_out, const float* rep_sq, double* acc,
+                                  void* stream) {
   DL_CHECK_ARG(rec && n_uniq && stash && gloc && hist && opt && dmark, "NULL argument");
   DL_CHECK_ARG(hist_len >= 2 && (hist_len & (hist_len - 1)) == 0, "hist_len must be a power of two");
   DL_CHECK_ARG(Fw >= 0 && H >= 0, "bad Fw / H");
@@ -315,20 +355,20 @@ extern "C" int dl_wide_rec_update(float* rec, const int32_t* n_uniq, int64_t max
     hipLaunchKernelGGL(wide_rec_update_kernel, dim3(wide_rows_grid(max_uniq)), dim3(256), 0, s,
                        reinterpret_cast<float4*>(rec), n_uniq, (long long)max_uniq,
                        reinterpret_cast<const float4*>(stash), reinterpret_cast<long long*>(gloc), Fw, H, l2, hist_len,
-                       opt, dmark, sq_out);   // partials [0, wide_rows_grid(max_uniq))
+                       opt, dmark, sq_out, rep_sq, acc);   // partials [0, wide_rows_grid(max_uniq))
   if (H > 0)
     hipLaunchKernelGGL(wide_rec_update_deep_kernel, dim3(wide_rows_grid(H)), dim3(256), 0, s, reinterpret_cast<float4*>(rec),
                        reinterpret_cast<long long*>(gloc), Fw, H, l2, hist, hist_len, opt, dmark,
-                       sq_out ? sq_out + (max_uniq > 0 ? wide_rows_grid(max_uniq) : 0) : nullptr);
+                       sq_out ? sq_out + (max_uniq > 0 ? wide_rows_grid(max_uniq) : 0) : nullptr, acc);
   DL_RETURN_LAUNCH("dl_wide_rec_update");
 }
 
 extern "C" int dl_wide_rec_flush(float* rec, int64_t w_rows, float l2, const float* hist, int32_t hist_len,
-                                 const float* opt, float* sq_untouched, void* stream) {
+                                 const float* opt, float* sq_untouched, double* acc, void* stream) {
   DL_CHECK_ARG(rec && hist && opt, "NULL argument");
   DL_CHECK_ARG(hist_len >= 2 && (hist_len & (hist_len - 1)) == 0, "hist_len must be a power of two");
   if (w_rows <= 0) return 0;
   hipLaunchKernelGGL(wide_rec_flush_kernel, dim3(wide_grid(w_rows)), dim3(256), 0, as_stream(stream),
-                     reinterpret_cast<float4*>(rec), (long long)w_rows, l2, hist, hist_len, opt, sq_untouched);
+                     reinterpret_cast<float4*>(rec), (long long)w_rows, l2, hist, hist_len, opt, sq_untouched, acc);
   DL_RETURN_LAUNCH("dl_wide_rec_flush");
 }

@@ -315,6 +315,10 @@ class CTREngine:
             self.wsq_part = z(max(1, int(_lib.lib().dl_wide_update_blocks(nw, Hh))))
             self.wsq = z(4)                      # L2 term of the rows the last step left (from a flush)
             self._wsq_step = -1
+            # the running loss's wide L2 term (loss_sum_begin / loss_sum_end): per-block slots the
+            # update and flush kernels add to, and each unique row's replayed steps' w^2 (gather)
+            self.wacc = z(_lib.LOSS_ACC_SLOTS, dt=torch.float64)
+            self.wrep = z(max(nw, 1))
             self.in_wide_loc = z(Bm, Fw, dt=torch.int64)
             wsb = _lib.lib().dl_index_workspace_bytes(max(1, nw))
             self.widx_ws = z(wsb, dt=torch.uint8)
@@ -332,6 +336,9 @@ class CTREngine:
             WL.zero_row0 = 0
             self.wlayout = WL
         self.err = z(4, dt=torch.int32)       # the batch's id-validation word (per buffer set)
+        # running loss of a training loop (dl_loss_accumulate, every step inside its graph):
+        # [sum of data terms, sum of regulariser terms, steps]
+        self.loss_acc = z(4, dt=torch.float64)
         # table update form (TF: ApplyAdam, or the sparse-apply form for direct lookups)
         self.rec_flags = (_lib.REC_FIRST if sp.fm else 0) | (_lib.REC_SPARSE_ADAM if sp.sparse_table else 0)
         self.rows_sparse = _lib.ROWS_SPARSE_ADAM if sp.sparse_table else 0
@@ -663,7 +670,7 @@ class CTREngine:
             return
         self.wsq.zero_()
         call("dl_wide_rec_flush", ptr(self.wrec), self.w_rows, self.spec.l2, ptr(self.hist), self.hist_len,
-             ptr(self.opt), ptr(self.wsq), _lib.stream_handle())
+             ptr(self.opt), ptr(self.wsq), ptr(self.wacc), _lib.stream_handle())
         self._wsq_step = self.steps
 
     def _export_dense(self, Ws, head, ww, wb):
@@ -884,7 +891,8 @@ class CTREngine:
             nw = B * sp.Fw
             self._c("wide_gather", "dl_wide_rec_gather", ptr(self.wrec), self.w_rows, ptr(self.widx_uniq),
                     ptr(self.widx_n), nw, sp.Fw, H, ptr(self.hist), self.hist_len, ptr(self.opt), sp.l2,
-                    1 if train else 0, ptr(self.wloc), ptr(self.wstash) if train else None, s)
+                    1 if train else 0, ptr(self.wloc), ptr(self.wstash) if train else None,
+                    ptr(self.wrep) if train else None, s)
             self._c("head", fn, B, sp.Fw, H, ptr(self.in_wide_loc), sp.Fw, ptr(self.h[-1]), self.h_ld[-1],
                     ptr(self.wloc), ptr(self.wb), sp.Fw + H + nw, ptr(self.in_label), sp.logloss_eps, 1.0 / B,
                     ptr(self.score), ptr(self.z), ptr(self.dz), ptr(dh_last), None, None,
@@ -941,6 +949,15 @@ class CTREngine:
             call("dl_wide_local_ids", ptr(self.winv), B * Fw, Fw + H, ptr(self.in_wide_loc), s)
 
     def _train(self, B):
+        self._train_body(B)
+        # the step's loss into the running sum (read once per epoch: loss_sum_end)
+        sp = self.spec
+        width = self.head_slab.shape[1]
+        coef = sp.l2 if sp.hidden_reg == "l1" else 0.5 * sp.l2
+        self._c("loss_acc", "dl_loss_accumulate", ptr(self.head_slab), call_int(self.head_grid, B), width, width - 1,
+                1.0 / B, ptr(self.opt), coef, ptr(self.loss_acc), _lib.stream_handle())
+
+    def _train_body(self, B):
         sp = self.spec
         s = _lib.stream_handle()
         L = self.layout
@@ -1065,7 +1082,7 @@ class CTREngine:
                     ptr(self.head_slab[:, H:]), hb, H + 2, 1, 0.0, 0, ptr(self.opt), None, None, s)
             self._c("adam_wide", "dl_wide_rec_update", ptr(self.wrec), ptr(self.widx_n), B * sp.Fw, ptr(self.wstash),
                     ptr(self.wgloc), sp.Fw, H, sp.l2, ptr(self.hist), self.hist_len, ptr(self.opt), ptr(self.wdmark),
-                    ptr(self.wsq_part), s)
+                    ptr(self.wsq_part), ptr(self.wrep), ptr(self.wacc), s)
             return
         if self.wdl:
             # wdl_weights: dense Adam with L2 on every row (wdl.py:270-271); the deep-output
@@ -1267,10 +1284,35 @@ class CTREngine:
             return data + sp.l2 * float(self.opt[8].item())
         reg = float(self.opt[8].item())
         if getattr(self, "wide_lazy", False):
-            # the wide rows the step left untouched: their L2 term from a flush (wide.hip)
+            # the wide rows the step left untouched: their L2 term from a flush (wide.hip); the
+            # touched rows' from the update's block partials — only the blocks this batch size
+            # launched (a smaller last batch leaves an earlier batch's partials beyond them)
             self._wide_flush()
-            reg += float(self.wsq[0].item()) + float(self.wsq_part.double().sum().item())
+            nparts = int(_lib.lib().dl_wide_update_blocks(B * sp.Fw, H))
+            reg += float(self.wsq[0].item()) + float(self.wsq_part[:nparts].double().sum().item())
         return data + sp.l2 * 0.5 * reg
+
+    def loss_sum_begin(self):
+        """Start a running loss sum over the following training steps (the load-style fit's
+        epoch loss, wdl.py:305-313): no host read per step — each step's graph adds its data and
+        regulariser terms on the device (dl_loss_accumulate), and with lazy wide records their
+        L2 term arrives as the records are applied (the wide table is flushed first, so every
+        replayed step from here on belongs to the sum)."""
+        if getattr(self, "wide_lazy", False):
+            self._wide_flush()
+            self.wacc.zero_()
+        self.loss_acc.zero_()
+
+    def loss_sum_end(self):
+        """(sum of the per-step losses since loss_sum_begin, steps): every wide record is caught
+        up first, which adds the L2 terms of the steps it left untouched."""
+        sp = self.spec
+        acc = self.loss_acc.tolist()
+        total = acc[0] + acc[1]
+        if getattr(self, "wide_lazy", False):
+            self._wide_flush()
+            total = (self.loss_acc[0] + self.loss_acc[1] + 0.5 * sp.l2 * self.wacc.sum()).item()
+        return float(total), int(round(acc[2]))
 
     # ------------------------------------------------------------------ errors
     def _queue_status(self):

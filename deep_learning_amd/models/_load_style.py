@@ -64,11 +64,28 @@ class LoadStyleModel:
         num_samples = 0
         for epoch in range(self.epochs):
             st = time.time()
-            for item in train_data:
-                b = self.batch(item)
-                eng.train_step(b, graph=b["label"].shape[0] == eng.B)
-                losses.append(eng.loss() * self.batch_size)
+            # sess.run([loss, optimizer]) per batch (wdl.py:305-309): the step's loss is summed on
+            # the device (no host read per step, no wide-table flush); the epoch's mean is the
+            # reference's sum(loss_t * batch_size) / num_samples (num_samples counts batch_size
+            # per batch, the last partial batch included)
+            eng.loss_sum_begin()
+            steps = 0
+            items = iter(train_data)
+            b = next(items, None)
+            b = self.batch(b) if b is not None else None
+            while b is not None:
+                # the next batch is unpickled, staged and indexed while this step runs
+                nxt = next(items, None)
+                nxt = self.batch(nxt) if nxt is not None else None
+                eng.train_step(b, graph=b["label"].shape[0] == eng.B,
+                               **({"next_batch": nxt} if nxt is not None else {}))
+                steps += 1
                 num_samples += self.batch_size
+                b = nxt
+            loss_sum, counted = eng.loss_sum_end()
+            if counted != steps:
+                eng.check_error()   # a skipped (bad) batch raises here, as its sess.run did
+            losses.append(loss_sum * self.batch_size)
             end_time = time.time()
             total_loss = float(np.sum(losses) / num_samples)
             valid_metric = self.evaluate(None, val_data)

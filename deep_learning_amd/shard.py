@@ -1043,6 +1043,11 @@ class ShardedCTREngine(CTREngine):
             acc.add(b["label"], self.predict(b, device=True))
         return acc.result()
 
+    def loss_sum_begin(self):
+        raise NotImplementedError("the sharded engine reads the loss per step: loss()")
+
+    loss_sum_end = loss_sum_begin
+
     def loss(self):
         """Global loss of the last step: the all-reduced loss column + L2 on the head weights
         (wdl: + L2 on every hidden weight matrix and on all of wdl_weights, whose shard sums are

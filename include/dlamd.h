@@ -391,6 +391,13 @@ int dl_validate_batch(const dl_emb_layout* L, const int64_t* cate, const int64_t
  * launch, same operations in the same order: the step's opening graph node. */
 int dl_step_begin(const int32_t* batch_err, float* opt, float decay_rate, float decay_steps, float* hist,
                   int32_t hist_len, void* stream);
+/* The running loss of a training loop (the load-style fit's per-epoch mean, wdl.py:305-313):
+ * acc[0] += sum_r slab[r * pitch + col] * inv_b (the step's data term; double, fixed order),
+ * acc[1] += reg_coef * opt[8] (the step's regulariser sum), acc[2] += 1; nothing for a skipped
+ * step.  acc: double[3] on the device, read by the host once per epoch.  (Wide&Deep with lazy
+ * wide records adds the wide L2 term per record step through dl_wide_rec_update / _flush acc.) */
+int dl_loss_accumulate(const float* slab, int32_t rows, int32_t pitch, int32_t col, double inv_b, const float* opt,
+                       float reg_coef, double* acc, void* stream);
 /* Dense parameter whose gradient is the sum of `nslab` partial slabs
  * (g = sum_s slab[s*slab_stride + i]); l2 * p is added for i < l2_count;
  * p_prev (may be NULL) receives the pre-update values; sq_out (may be NULL) gets
@@ -580,7 +587,9 @@ int dl_wide_local_ids(const int32_t* inv, int64_t n, int64_t offset, int64_t* ou
  * bit-identical to the dense dl_adam_rows sweep.
  * dl_wide_rec_gather: the deep-output rows Fw..Fw+H and the unique wide rows uniq_rows[u]
  * (dl_index_build keys, world 1) caught up to step opt[7] - lag into the head's local table
- * wloc = [— (Fw) | deep rows (H) | unique rows]; stash[u] (may be NULL) = {w, m, v, row bits}.
+ * wloc = [— (Fw) | deep rows (H) | unique rows]; stash[u] (may be NULL) = {w, m, v, row bits};
+ * rep_sq[u] (may be NULL) = the sum of w^2 over the steps replayed for unique row u (each
+ * step's pre-update state: that step's L2 loss term for the row), counted by the update.
  * dl_wide_seg_grad: the batch's wide-weight gradient per unique wide row from the wide index
  *   (dl_index_build over the wide ids: sorted references `refs`, segment offsets `seg_off`, count
  *   n_uniq on the device): q[u] = sum over the row's references e of wide_fixed(dz[e / Fw]), int64
@@ -590,19 +599,27 @@ int dl_wide_local_ids(const int32_t* inv, int64_t n, int64_t offset, int64_t* ou
  * term gloc[row] of a row in Fw..Fw+H, exact int64, + l2 w) from the stash, then on the deep
  * rows not covered; gloc reset; the pre-update w^2 of those rows as per-block partial sums
  * written to sq_out[0 .. dl_wide_update_blocks(max_uniq, H)) (may be NULL; the caller sums).
+ * acc (may be NULL; double[65536], one slot per block index): the running loss's wide L2
+ * term — every pre-update w^2 of the rows this step applies, and of the steps replayed for
+ * them (rep_sq, or the deep rows' own replay) — added per block.
  * dl_wide_rec_flush: every row caught up to step opt[7]; the pre-update w^2 of the rows the
- * last step left untouched (the loss's L2 term for them) added to sq_untouched. */
+ * last step left untouched (the loss's L2 term for them) added to sq_untouched; every replayed
+ * step's pre-update w^2 added to acc's slots (may be NULL).  Summed over acc after a flush, the
+ * slots hold sum_t sum_r w_r(t-1)^2 over the steps since acc was zeroed on a flushed table. */
 int dl_wide_rec_gather(const float* rec, int64_t w_rows, const uint32_t* uniq_rows, const int32_t* n_uniq,
                        int64_t max_uniq, int32_t Fw, int32_t H, const float* hist, int32_t hist_len,
-                       const float* opt, float l2, int32_t lag, float* wloc, float* stash, void* stream);
+                       const float* opt, float l2, int32_t lag, float* wloc, float* stash, float* rep_sq,
+                       void* stream);
 int64_t dl_wide_update_blocks(int64_t max_uniq, int32_t H);
 int dl_wide_seg_grad(const float* dz, int32_t Fw, const int32_t* refs, const int32_t* seg_off, const int32_t* n_uniq,
                      int64_t max_uniq, int64_t nrefs, int64_t* q, int32_t* long_ws, const float* opt, void* stream);
 int dl_wide_rec_update(float* rec, const int32_t* n_uniq, int64_t max_uniq, const float* stash, int64_t* gloc,
                        int32_t Fw, int32_t H, float l2, const float* hist, int32_t hist_len,
-                       const float* opt, uint8_t* dmark, float* sq_out, void* stream);
+                       const float* opt, uint8_t* dmark, float* sq_out, const float* rep_sq, double* acc,
+                       void* stream);
 int dl_wide_rec_flush(float* rec, int64_t w_rows, float l2, const float* hist, int32_t hist_len,
-                      const float* opt, float* sq_untouched, void* stream);
+                      const float* opt, float* sq_untouched, double* acc, void* stream);
+#define DL_LOSS_ACC_SLOTS 65536   /* slots of the wide running-loss accumulator (>= any grid above) */
 
 /* ------------------------------------------------------------------------
  * RCCL collectives of the row-sharded step (comm.cpp; SURVEY.md §8(b)3

@@ -11,7 +11,8 @@ def kernels(k, n=8):
 
 def main(path):
     d = json.loads(open(path).read().strip().splitlines()[-1])
-    print("%s: %.4f ms/step, %.3g samples/s" % (d["config"]["workload"], d["ms_per_step"], d["value"]))
+    print("%s: %.4f ms/step, %.3g samples/s, n_gpus %s, %s, world %s" % (
+        d["config"]["workload"], d["ms_per_step"], d["value"], d["n_gpus"], d["config"]["parallelism"], d.get("world")))
     r = d["roofline"]
     print("  roofline %s %s: %.4g %s = %.3f of peak, traffic %s" % (
         r.get("kernel"), r["bound"], r["achieved"], r["unit"], r["frac"], r.get("traffic")))

@@ -47,4 +47,13 @@ if [ "$MODE" = prof ]; then
   python scripts/sq_summary.py $OUT/s3pmc $OUT/s3_sq_counters.json fwd_l1 dw_l1
   exit 0
 fi
-echo "usage: gpu_round.sh suite|prof TAG"; exit 2
+if [ "$MODE" = rehearse ]; then
+  # the multi-rank bench flow on one GPU: bench.py --gpus 2 starts its two ranks itself
+  # (gloo-staged exchange, both ranks on device 0), then the same under the driver's launcher form
+  DLAMD_BENCH_BACKEND=gloo timeout -k 10 600 python bench.py --gpus 2 --steps 5 --warmup 2 --age-steps 8 \
+    --extra-steps 3 > $OUT/bench_gpus2.json 2> $OUT/bench_gpus2.err
+  rc=$?; echo "bench --gpus 2 rc=$rc"; [ $rc -eq 0 ] || { tail -20 $OUT/bench_gpus2.err; exit $rc; }
+  python scripts/bench_brief.py $OUT/bench_gpus2.json
+  exit 0
+fi
+echo "usage: gpu_round.sh suite|prof|rehearse TAG"; exit 2

@@ -9,7 +9,7 @@
                   streaming read (16 B/lane); exact for the streaming Adam sweep, an
                   upper-bound-style estimate for other access widths (uncalibrated).
 
-usage: python scripts/pmc_summary.py gpurun_out/r01e profiles/r01e/pmc_summary.json
+usage: python scripts/pmc_summary.py gpurun_out/r01e profiles/r01e/pmc_summary.json [workload] [id_dist]
 """
 import csv
 import json
@@ -25,7 +25,7 @@ def short(name):
     return name.replace("dl::", "")
 
 
-def main(src, dst, workload="c2"):
+def main(src, dst, workload="c2", id_dist="uniform"):
     stats = {}
     p = os.path.join(src, "prof_trace", "trace_kernel_stats.csv")
     for r in csv.DictReader(open(p)):
@@ -42,11 +42,11 @@ def main(src, dst, workload="c2"):
         if "fetch_kb" in v and "write_kb" in v:
             v["hbm_bytes"] = (2 * v["fetch_kb"] + v["write_kb"]) * 1024
     os.makedirs(os.path.dirname(dst), exist_ok=True)
-    json.dump({"source": src, "workload": workload, "kernels": stats}, open(dst, "w"), indent=1, sort_keys=True)
+    json.dump({"source": src, "workload": workload, "id_dist": id_dist, "kernels": stats}, open(dst, "w"), indent=1, sort_keys=True)
     for k, v in sorted(stats.items(), key=lambda kv: -kv[1].get("avg_us", 0))[:14]:
         print("%-60s %10.1f us  hbm %s" % (k[:60], v.get("avg_us", 0), "%.3g GB" % (v["hbm_bytes"] / 1e9)
                                           if "hbm_bytes" in v else "-"))
 
 
 if __name__ == "__main__":
-    main(sys.argv[1], sys.argv[2], *sys.argv[3:4])
+    main(sys.argv[1], sys.argv[2], *sys.argv[3:5])

@@ -428,3 +428,40 @@ def test_scatter_forward_bit_identical_to_indexed(hip_lib, name, tower):
         same(pa[k], pb[k], err_msg=k)
     # predict (lag 0, no stash) through both forms
     same(a.predict(bt), b.predict(bt))
+
+
+@pytest.mark.parametrize("name", ["wdl", "deepfm_pipeline", "dnn"])
+def test_running_loss_sum_and_partial_last_batch(hip_lib, name):
+    """The load-style fit's epoch loss (wdl.py:305-313: sum of loss_t * batch_size) summed on
+    the device (loss_sum_begin / loss_sum_end: no host read, no wide-table flush per step)
+    against the oracle's per-step losses; an 8-entry alpha ring forces lagging wide rows and
+    flushes mid-sum.  The last batch is smaller than the others: the per-step loss() of that
+    step (lazy wide records: only the update blocks that batch launched) must match too."""
+    kw = dict(CASES[name], cate_index_size=30000)
+    model = _model(name)
+    cfg = R.make_cfg(model, **kw)
+    P = R.init_params(cfg, np.random.default_rng(17))
+    spec = ModelSpec(model, **kw)
+    run = CTREngine(spec, max_batch=256, init="none", adam="lazy", hist_len=8)
+    step = CTREngine(spec, max_batch=256, init="none", adam="lazy", hist_len=8)
+    run.load_params(P)
+    step.load_params(P)
+    opt = R.AdamTF1(cfg, P)
+    bs = _batches(name, kw, 256, 13, seed=31)
+    last = _batches(name, kw, 96, 1, seed=77)[0]
+    bs.append(last)
+    run.loss_sum_begin()
+    ref = []
+    for i, b in enumerate(bs):
+        fw = R.train_step(cfg, P, opt, b)
+        ref.append(fw["loss"])
+        full = b["label"].shape[0] == 256
+        nxt = bs[i + 1] if i + 1 < len(bs) else None
+        run.train_step(b, graph=full and i >= 2, **({"next_batch": nxt} if nxt is not None else {}))
+        step.train_step(b, graph=full and i >= 2)
+        assert abs(step.loss() - fw["loss"]) < TOL, "per-step loss at step %d (B=%d)" % (i, b["label"].shape[0])
+    total, n = run.loss_sum_end()
+    assert n == len(bs)
+    np.testing.assert_allclose(total, float(np.sum(ref)), rtol=0, atol=TOL * len(bs))
+    # the running sum and the exact per-step sum agree far below the oracle bar
+    np.testing.assert_allclose(run.params()[spec.table_key], step.params()[spec.table_key], rtol=0, atol=0)
