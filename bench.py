@@ -225,46 +225,101 @@ def workload_name(wl, vocab, n_rows, sharded):
 
 
 def lookup_alone(eng, batch, B, per_sample, reps=20):
-    """SURVEY §8(d)'s embedding gather as a lookup kernel alone: right after a flush (every row
-    caught up, so no zero-gradient steps to replay) the flat record lookup dl_embed_fwd_rec_flat
-    that CTREngine.predict runs on a flushed table — each reference's row and first-order weight
-    read from its record's first line, the FM sums and x0 assembled; bit-identical to the
-    rec_gather + embed_fwd pair at lag 0 by test — preceded by the 13 replicated FM cont-field
-    rows' compact gather, both timed with HIP events on the launch stream."""
+    """SURVEY §8(d)'s embedding gather as a lookup kernel alone, the one CTREngine.predict runs
+    on a flushed table: the flush writes every row's p and first-order weight out as dense planes
+    (dl_rec_flush with planes) and the lookup reads 64-B rows from them (dl_embed_fwd: the FM
+    sums and x0 assembled) — bit-identical to the rec_gather + embed_fwd pair at lag 0 by test.
+    Also timed: the same lookup reading each record's first 128-B line (dl_embed_fwd_rec_flat,
+    the form without planes).  HIP events on the launch stream."""
     import torch
     from deep_learning_amd import _lib
     from deep_learning_amd._lib import call, ptr
     from deep_learning_amd.engine import C_ref
     sp = eng.spec
+    eng.flush(planes=True)
     eng.stage(batch)
     L = eng.layout
     L.batch = B
+    FL = eng._flat_layout(B)
     s = _lib.stream_handle()
     x0 = eng.x0b if eng.x0_direct else eng.x0
 
-    def run():
+    def planes():
+        call("dl_embed_fwd", C_ref(FL), ptr(eng.p_plane), ptr(eng.w1_plane), ptr(eng.in_cate), ptr(eng.in_cont),
+             ptr(eng.in_vec), ptr(x0), ptr(eng.fm_out), ptr(eng.fm_sum), ptr(eng.err), s)
+
+    def records():
         if eng.n_rep:
             call("dl_rec_gather", C_ref(L), ptr(eng.rec), eng.rec_ld, eng.rec_flags, eng.n_rep, ptr(eng.idx_uniq), None,
                  0, 1, ptr(eng.hist), eng.hist_len, ptr(eng.opt), 0, ptr(eng.rows_u), ptr(eng.rows_u1), None, s)
         call("dl_embed_fwd_rec_flat", C_ref(L), ptr(eng.rec), eng.rec_ld, eng.rec_flags, ptr(eng.rows_u),
              ptr(eng.rows_u1) if sp.fm else None, ptr(eng.in_cate), ptr(eng.in_cont), ptr(eng.in_vec), ptr(eng.opt),
              ptr(x0), ptr(eng.fm_out), ptr(eng.fm_sum), ptr(eng.err), s)
-    run()
+
+    def timed(fn):
+        fn()
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(reps):
+            fn()
+        e1.record()
+        torch.cuda.synchronize()
+        eng.check_error()
+        us = e0.elapsed_time(e1) * 1e3 / reps
+        gb = B * per_sample / (us * 1e-6) / 1e9
+        return round(us, 1), round(gb, 1), round(gb / HBM_PEAK_GBS, 3)
+
+    us, gb, fr = timed(planes)
+    rus, rgb, rfr = timed(records)
+    return {"kernels": ["embed_fwd (dense planes)"], "us": us, "GB/s": gb, "frac": fr,
+            "records": {"kernels": ["rec_gather (13 cont rows)", "embed_fwd_rec_flat"], "us": rus, "GB/s": rgb,
+                        "frac": rfr},
+            "note": "flushed table: the lookup without lazy Adam's catch-up, as predict runs it (the flush writes "
+                    "dense p / first-order planes; 'records' reads each record's first line instead); the "
+                    "training step's gather above also replays each row's pending zero-gradient Adam steps and "
+                    "stashes its moments"}
+
+
+def dropin_fit(args, n_batches=12, warm=3):
+    """The Wide&Deep drop-in's own training loop at C5 shapes: models/wdl.DeepModel (the
+    load-style surface of /root/reference/models/wdl.py:287-316) trained over pickled host
+    batches (utils/data_loader_load.py's format: a dict of arrays per batch, unpickled each
+    step as wdl.py:296 does) — unpickle, host-to-device staging of the next batch during the
+    current step, the step, and the per-step loss summed on the device (read once per epoch).
+    Timed over one pass of n_batches after a warmup pass of `warm`."""
+    import pickle
+    import torch
+    from deep_learning_amd.models import wdl
+    from deep_learning_amd.synthetic import make_batch
+
+    class A:
+        hidden_units, epochs, batch_size, learning_rate = list(C2["hidden"]), 1, args.batch, 0.001
+        model_pb, learning_rate_decay_steps, learning_rate_decay_rate, l2_reg = "", 10000000, 0.9, 1e-5
+        cont_field_size, cate_field_size, embedding_size, wide_field_size = C2["C"], C2["S"], C2["E"], 26
+        cate_index_size = C2["S"] * C2["per_field_vocab"]
+        alg_name, vector_field_size, tower_dtype = "wdl", 0, "bf16"
+    items = []
+    for i in range(n_batches):
+        b = make_batch(args.batch, cate_index_size=A.cate_index_size, seed=500 + i, wide_fields=26)
+        items.append(pickle.dumps({"labels": b["label"], "cont_feats": b["cont_feats"], "cate_feats": b["cate_feats"],
+                                   "wide_feats": b["wide_feats"]}, protocol=pickle.HIGHEST_PROTOCOL))
+    m = wdl.DeepModel(A)
+    m.train_epoch(items[:warm])
     torch.cuda.synchronize()
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    e0.record()
-    for _ in range(reps):
-        run()
-    e1.record()
+    t0 = time.perf_counter()
+    loss_sum, steps = m.train_epoch(items)
     torch.cuda.synchronize()
-    eng.check_error()
-    us = e0.elapsed_time(e1) * 1e3 / reps
-    gb = B * per_sample / (us * 1e-6) / 1e9
-    return {"kernels": ["rec_gather (13 cont rows)", "embed_fwd_rec_flat"], "us": round(us, 1),
-            "GB/s": round(gb, 1), "frac": round(gb / HBM_PEAK_GBS, 3),
-            "note": "flushed table: the lookup without lazy Adam's catch-up (dl_embed_fwd_rec_flat, predict's "
-                    "forward on a flushed table); the training step's gather above also replays each row's "
-                    "pending zero-gradient Adam steps and stashes its moments"}
+    dt = time.perf_counter() - t0
+    out = {"ms_per_step": round(dt / steps * 1e3, 4), "steps": steps, "samples_per_s": round(steps * args.batch / dt, 1),
+           "epoch_mean_loss": round(loss_sum / steps, 6),
+           "note": "wdl.DeepModel.train_epoch over %d pickled C5 batches (B=%d, 26M-row table, bf16 tower): "
+                   "unpickle + staging + step + device-summed loss per step; after a %d-batch warmup pass"
+                   % (n_batches, args.batch, warm)}
+    del m
+    torch.cuda.synchronize()
+    torch.cuda.empty_cache()
+    return out
 
 
 def run_workload(wl, args, world, rank, sharded, steps, warmup, age, ksteps, barrier):
@@ -575,6 +630,13 @@ def main():
                      "steps": args.extra_steps, "roofline": e["roofline"], "gather_north_star": e["gather"],
                      "kernel_sum_us_per_step": round(e["kernel_sum"], 1), "loss": round(e["loss"], 6),
                      "kernels": e["kernels"]}
+    if "c5" in extra and "error" not in extra["c5"] and world == 1:
+        try:
+            extra["c5"]["dropin_fit"] = dropin_fit(args)
+            extra["c5"]["dropin_fit"]["vs_engine_step"] = round(extra["c5"]["dropin_fit"]["ms_per_step"] /
+                                                                extra["c5"]["ms_per_step"], 3)
+        except Exception as ex:   # reported, never fatal
+            extra["c5"]["dropin_fit"] = {"error": repr(ex)}
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         log("cpu baseline (torch-CPU restatement)")

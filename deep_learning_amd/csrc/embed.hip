@@ -648,6 +648,175 @@ __global__ __launch_bounds__(256) void pool_fwd_kernel(PoolArgs a) {
   }
 }
 
+// Ballot-compacted pooling (the default; pool_fwd_kernel above serves more than kPoolMaxSlots
+// slots or a multi block wider than kSlotLutMax).  One wave per sample walks the sample's whole
+// multi block 64 positions at a time: each lane resolves its position's slot (an LDS table) and
+// source row, a __ballot of the valid ones (a row present, not padding, not the zero row) and
+// the lane's prefix popcount (mbcnt) give every valid position a compacted queue index, and the
+// wave appends (row, slot, value) there in LDS.  Each full queue of 64 is drained 16 rows per
+// round with all four rounds' row and first-order loads in flight together: the wave loads only
+// the rows the sample references — padding costs no iteration and no predicated-off lanes —
+// and every slot's rows are in flight at once instead of slot after slot.  Per-slot sums stay in
+// registers (a lane's rows in queue order, then the xor tree over the 16 row groups): the
+// order depends only on the positions, so the dense, indexed and staged modes pool identically.
+// deepfm_multi_cate.py:73-78: cnt = count_nonzero(reduce_sum(V[ids], axis=2)) per slot,
+// out = div_no_nan(reduce_sum(V[ids], axis=1), cnt); the first-order weights likewise.
+constexpr int kPoolMaxSlots = 8;
+constexpr int kPoolQ = 64;   // compacted rows per drain
+
+template <int E, bool IDX, bool WT>
+__global__ __launch_bounds__(256) void pool_fwd_compact_kernel(PoolArgs a) {
+  constexpr int LPR = E / 4, RPI = 64 / LPR, NIT = kPoolQ / RPI;
+  const dl_emb_layout& L = a.L;
+  __shared__ unsigned char lut[kSlotLutMax];
+  __shared__ int q_src[4][2 * kPoolQ];
+  __shared__ unsigned char q_slot[4][2 * kPoolQ];
+  __shared__ float q_val[4][WT ? 2 * kPoolQ : 1];
+  const int M = a.n_slots;
+  int W = 0;
+  for (int m = 0; m < M; ++m) W = max(W, a.slot_end[m]);
+  const bool use_lut = W <= kSlotLutMax;
+  for (int l = threadIdx.x; use_lut && l < W; l += blockDim.x) {
+    int m = 0;
+    while (m < M && !(l >= a.slot_start[m] && l < a.slot_end[m])) ++m;
+    lut[l] = (unsigned char)m;
+  }
+  __syncthreads();
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int r = lane / LPR, q = lane % LPR;
+  int* qs = q_src[wv];
+  unsigned char* qm = q_slot[wv];
+  float* qv = q_val[wv];
+  const int wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int nwaves = (gridDim.x * blockDim.x) >> 6;
+  const float4* tab4 = reinterpret_cast<const float4*>(a.table);
+  const int ns = index_slots(L), mb = index_multi_base(L);
+  const uint64_t below = lane ? (~0ull >> (64 - lane)) : 0ull;
+  for (int b = wave; b < L.batch; b += nwaves) {
+    const int64_t* ids = IDX ? nullptr : a.ids + (int64_t)b * L.cate_ld + a.ids_col;
+    const int32_t* invb = IDX ? a.inv + (int64_t)b * ns + mb : nullptr;
+    const float* valb = WT ? a.vals + (int64_t)b * a.vals_ld : nullptr;
+    float4 s[kPoolMaxSlots];
+    float cnt[kPoolMaxSlots], s1[kPoolMaxSlots], c1[kPoolMaxSlots];
+#pragma unroll
+    for (int m = 0; m < kPoolMaxSlots; ++m) { s[m] = f4_zero(); cnt[m] = s1[m] = c1[m] = 0.f; }
+    int qn = 0;
+    // one drain: queue entries [0, n) (n <= kPoolQ), four rounds of RPI rows, loads first
+    auto drain = [&](int n) {
+      float4 e[NIT];
+      float w[NIT];
+      int mm[NIT];
+#pragma unroll
+      for (int it = 0; it < NIT; ++it) {
+        const int j = it * RPI + r;
+        const bool in = j < n;
+        const int src = in ? qs[j] : -1;
+        mm[it] = in ? qm[j] : kPoolMaxSlots;
+        e[it] = src >= 0 ? tab4[(long long)src * LPR + q] : f4_zero();
+        w[it] = (a.first_order && src >= 0 && q == 0) ? a.first_order[src] : 0.f;
+      }
+#pragma unroll
+      for (int it = 0; it < NIT; ++it) {
+        float4 x = e[it];
+        float rs = (x.x + x.y) + (x.z + x.w);   // tf.reduce_sum(emb, axis=2): the count's test
+#pragma unroll
+        for (int o = 1; o < LPR; o <<= 1) rs += __shfl_xor(rs, o, 64);
+        if (WT) {
+          const float vv = (it * RPI + r) < n ? qv[it * RPI + r] : 0.f;
+          x.x *= vv; x.y *= vv; x.z *= vv; x.w *= vv;   // tf.multiply(emb, value), then the sum
+        }
+#pragma unroll
+        for (int m = 0; m < kPoolMaxSlots; ++m) {
+          if (mm[it] == m) {
+            s[m].x += x.x; s[m].y += x.y; s[m].z += x.z; s[m].w += x.w;
+            if (q == 0) {
+              cnt[m] += rs != 0.f ? 1.f : 0.f;
+              s1[m] += w[it];
+              c1[m] += w[it] != 0.f ? 1.f : 0.f;
+            }
+          }
+        }
+      }
+    };
+    for (int p0 = 0; p0 < W; p0 += 64) {
+      const int pos = p0 + lane;
+      int src = -1, m = M;
+      float vv = 0.f;
+      if (pos < W) {
+        if (use_lut) {
+          m = lut[pos];
+        } else {
+          m = 0;
+          while (m < M && !(pos >= a.slot_start[m] && pos < a.slot_end[m])) ++m;
+        }
+        if (m < M) {
+          if (IDX) {
+            const int ri = invb[pos];
+            src = ri < 0 ? -1 : a.staged ? b * L.multi_width + pos : a.inv_base + ri;
+          } else {
+            const int64_t row = checked_row(ids[pos], 0, L.n_rows, a.err);
+            src = row_ok(row, L.zero_row0) ? (int)row : -1;
+          }
+          if (WT) vv = valb[pos];
+        }
+      }
+      const uint64_t vm = __ballot(src >= 0);
+      if (src >= 0) {
+        const int c = qn + __popcll(vm & below);
+        qs[c] = src;
+        qm[c] = (unsigned char)m;
+        if (WT) qv[c] = vv;
+      }
+      qn += __popcll(vm);
+      __builtin_amdgcn_s_waitcnt(0xc07f);   // lgkmcnt(0): the queue writes landed for the wave
+      __builtin_amdgcn_wave_barrier();
+      if (qn >= kPoolQ) {
+        drain(kPoolQ);
+        qn -= kPoolQ;
+        __builtin_amdgcn_wave_barrier();
+        if (lane < qn) {   // carry the overflow to the queue's front
+          qs[lane] = qs[kPoolQ + lane];
+          qm[lane] = qm[kPoolQ + lane];
+          if (WT) qv[lane] = qv[kPoolQ + lane];
+        }
+        __builtin_amdgcn_s_waitcnt(0xc07f);
+        __builtin_amdgcn_wave_barrier();
+      }
+    }
+    if (qn > 0) drain(qn);
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int m = 0; m < kPoolMaxSlots; ++m) {
+      if (m >= M) break;
+      float4 t = s[m];
+#pragma unroll
+      for (int o = LPR; o < 64; o <<= 1) {
+        t.x += __shfl_xor(t.x, o, 64); t.y += __shfl_xor(t.y, o, 64);
+        t.z += __shfl_xor(t.z, o, 64); t.w += __shfl_xor(t.w, o, 64);
+      }
+      const float cn = wave_sum(cnt[m]);
+      if (r == 0) {
+        float4 o4 = f4_zero();
+        if (cn > 0.f) { o4.x = t.x / cn; o4.y = t.y / cn; o4.z = t.z / cn; o4.w = t.w / cn; }
+        *reinterpret_cast<float4*>(a.x0 + (int64_t)b * L.x0_ld + L.x0_pool_col + m * E + 4 * q) = o4;
+      }
+      if (lane == 0) a.cnt_emb[(int64_t)b * M + m] = cn;
+      if (a.first_order) {
+        const float sv = wave_sum(s1[m]), cc = wave_sum(c1[m]);
+        if (lane == 0) {
+          a.fm_out[(int64_t)b * L.fm_ld + a.fm_col + m] = cc > 0.f ? sv / cc : 0.f;
+          a.cnt_first[(int64_t)b * M + m] = cc;
+        }
+      }
+    }
+  }
+}
+
+// compacted pooling when the slots fit (n_slots <= kPoolMaxSlots; width checked on the host)
+#ifndef DL_POOL_COMPACT
+#define DL_POOL_COMPACT 1
+#endif
+
 struct PoolBwdArgs {
   dl_emb_layout L;
   const int64_t* ids;
@@ -894,7 +1063,10 @@ extern "C" int dl_pool_fwd(const dl_emb_layout* L, const float* table, const flo
   if (L->batch == 0 || n_slots == 0) return 0;
   PoolArgs a{*L, nullptr, 0, table, first_order, ids, ids_col, slot_start, slot_end, n_slots, fm_col,
              x0, fm_out, cnt_emb, cnt_first, err, nullptr, 0};
-  DL_DISPATCH_E(L->emb_dim, hipLaunchKernelGGL((pool_fwd_kernel<kE, false>), dim3(emb_grid(L->batch)),
+  if (DL_POOL_COMPACT && n_slots <= kPoolMaxSlots)
+    DL_DISPATCH_E(L->emb_dim, hipLaunchKernelGGL((pool_fwd_compact_kernel<kE, false, false>), dim3(emb_grid(L->batch)),
+                                                 dim3(256), 0, as_stream(stream), a))
+  else DL_DISPATCH_E(L->emb_dim, hipLaunchKernelGGL((pool_fwd_kernel<kE, false>), dim3(emb_grid(L->batch)),
                                                dim3(256), 0, as_stream(stream), a));
   DL_RETURN_LAUNCH("dl_pool_fwd");
 }
@@ -910,7 +1082,10 @@ extern "C" int dl_pool_fwd_indexed(const dl_emb_layout* L, const float* rows, co
   if (L->batch == 0 || n_slots == 0) return 0;
   PoolArgs a{*L, inv, inv_base, rows, rows_first, nullptr, 0, slot_start, slot_end, n_slots, fm_col,
              x0, fm_out, cnt_emb, cnt_first, nullptr, nullptr, 0};
-  DL_DISPATCH_E(L->emb_dim, hipLaunchKernelGGL((pool_fwd_kernel<kE, true>), dim3(emb_grid(L->batch)),
+  if (DL_POOL_COMPACT && n_slots <= kPoolMaxSlots)
+    DL_DISPATCH_E(L->emb_dim, hipLaunchKernelGGL((pool_fwd_compact_kernel<kE, true, false>), dim3(emb_grid(L->batch)),
+                                                 dim3(256), 0, as_stream(stream), a))
+  else DL_DISPATCH_E(L->emb_dim, hipLaunchKernelGGL((pool_fwd_kernel<kE, true>), dim3(emb_grid(L->batch)),
                                                dim3(256), 0, as_stream(stream), a));
   DL_RETURN_LAUNCH("dl_pool_fwd_indexed");
 }
@@ -926,7 +1101,10 @@ extern "C" int dl_pool_fwd_staged(const dl_emb_layout* L, const float* mst, cons
   PoolArgs a{*L, inv, 0, mst, mst1, nullptr, 0, slot_start, slot_end, n_slots, fm_col,
              x0, fm_out, cnt_emb, cnt_first, nullptr, nullptr, 0};
   a.staged = 1;
-  DL_DISPATCH_E(L->emb_dim, hipLaunchKernelGGL((pool_fwd_kernel<kE, true>), dim3(emb_grid(L->batch)),
+  if (DL_POOL_COMPACT && n_slots <= kPoolMaxSlots)
+    DL_DISPATCH_E(L->emb_dim, hipLaunchKernelGGL((pool_fwd_compact_kernel<kE, true, false>), dim3(emb_grid(L->batch)),
+                                                 dim3(256), 0, as_stream(stream), a))
+  else DL_DISPATCH_E(L->emb_dim, hipLaunchKernelGGL((pool_fwd_kernel<kE, true>), dim3(emb_grid(L->batch)),
                                                dim3(256), 0, as_stream(stream), a));
   DL_RETURN_LAUNCH("dl_pool_fwd_staged");
 }
@@ -958,7 +1136,10 @@ extern "C" int dl_pool_fwd_weighted(const dl_emb_layout* L, const float* table, 
   if (L->batch == 0 || n_slots == 0) return 0;
   PoolArgs a{*L, nullptr, 0, table, nullptr, ids, ids_col, slot_start, slot_end, n_slots, 0,
              x0, nullptr, cnt_emb, nullptr, err, values, values_ld};
-  DL_DISPATCH_E(L->emb_dim, hipLaunchKernelGGL((pool_fwd_kernel<kE, false, true>), dim3(emb_grid(L->batch)),
+  if (DL_POOL_COMPACT && n_slots <= kPoolMaxSlots)
+    DL_DISPATCH_E(L->emb_dim, hipLaunchKernelGGL((pool_fwd_compact_kernel<kE, false, true>), dim3(emb_grid(L->batch)),
+                                                 dim3(256), 0, as_stream(stream), a))
+  else DL_DISPATCH_E(L->emb_dim, hipLaunchKernelGGL((pool_fwd_kernel<kE, false, true>), dim3(emb_grid(L->batch)),
                                                dim3(256), 0, as_stream(stream), a));
   DL_RETURN_LAUNCH("dl_pool_fwd_weighted");
 }

@@ -464,7 +464,44 @@ __device__ __forceinline__ void rec_bwd_apply(const SegGrad4& s, int64_t row, in
   SegGradIn sg, float *__restrict__ rec, RecCfg c, int n_rep, const float *__restrict__ rows_u,              \
       const float *__restrict__ rows_u1, const float *__restrict__ mv, const uint32_t *__restrict__ uniq,   \
       const int32_t *__restrict__ n_uniq, int world, float *__restrict__ g_rep, float *__restrict__ g1_rep, \
-      const float *__restrict__ hist, const float *__restrict__ opt
+      const float *__restrict__ hist, const float *__restrict__ opt, int32_t *__restrict__ hot
+
+// The hot rows' workspace (dl_rec_bwd_workspace_bytes): int32 header [kHotN] the number of
+// hot rows, [kHotT] their chunks; then the hot rows' unique indices (appended by pass 1 in any
+// order), their first chunk (exclusive prefix over ceil(refs / kSegChunk), plus the total), the
+// owner of every chunk, and one partial sum per chunk (E/4 x {s, x, dsum} float4 + g1).
+constexpr int kHotN = 0, kHotT = 1, kHotList = 4;
+struct HotWs {
+  int32_t* hdr;
+  int32_t* list;
+  int32_t* off;
+  int32_t* map;
+  float* part;
+  long long cap_list, cap_chunks;
+};
+__host__ __device__ inline long long hot_cap_list(long long nrefs) { return nrefs / (kSegLong + 1) + 1; }
+__host__ __device__ inline long long hot_cap_chunks(long long nrefs) { return nrefs / kSegChunk + hot_cap_list(nrefs); }
+__host__ __device__ inline int hot_part_floats(int E) { return 3 * E + 4; }
+__host__ __device__ inline HotWs hot_ws(void* ws, long long nrefs, int E) {
+  HotWs h;
+  const long long cl = hot_cap_list(nrefs), cc = hot_cap_chunks(nrefs);
+  h.hdr = reinterpret_cast<int32_t*>(ws);
+  h.list = h.hdr + kHotList;
+  h.off = h.list + cl;
+  h.map = h.off + cl + 1;
+  long long o = (long long)kHotList + cl + (cl + 1) + cc;
+  o = (o + 3) / 4 * 4;   // 16-B aligned partials
+  h.part = reinterpret_cast<float*>(h.hdr + o);
+  h.cap_list = cl;
+  h.cap_chunks = cc;
+  return h;
+}
+__host__ __device__ inline long long hot_ws_bytes(long long nrefs, int E) {
+  const long long cl = hot_cap_list(nrefs), cc = hot_cap_chunks(nrefs);
+  long long o = (long long)kHotList + cl + (cl + 1) + cc;
+  o = (o + 3) / 4 * 4;
+  return 4 * o + 4 * cc * (long long)hot_part_floats(E);
+}
 
 // Pass 1: every unique row but the hot ones (more than kSegLong references: pass 2), E/4
 // lanes per row.  STASH (the gather's moment stash is given, the engine's default): the
@@ -520,7 +557,10 @@ __global__ __launch_bounds__(256, STASH ? DL_BWD_MIN_WAVES : 1) void rec_bwd_ada
     kx = nx.e0 < nx.e1 ? sg.refs[nx.e0] : -1;
     nn = seg_range(sg, u + 2 * ngroups, nu, nrefs);
     key_n = u + ngroups < nu ? uniq[u + ngroups] : 0u;
-    if (cr.e1 - cr.e0 > kSegLong) continue;   // a hot row: pass 2 (rec_bwd_long_kernel)
+    if (cr.e1 - cr.e0 > kSegLong) {   // a hot row: pass 2 (rec_bwd_long_kernel, or the chunked passes)
+      if (hot && q == 0) hot[kHotList + atomicAdd(&hot[kHotN], 1)] = (int32_t)u;
+      continue;
+    }
     const int64_t row = decode_key(key, world);
     const bool row_ok = row >= 0 && row < L.n_rows;
     // the row's caught-up state (independent of the segment walk: issued first)
@@ -567,6 +607,135 @@ __global__ __launch_bounds__(256) void rec_bwd_long_kernel(DL_REC_BWD_PARAMS) {
   });
 }
 
+// Hot rows over many blocks (Zipf: a C3 batch's hottest rows have ~10^5 references, which one
+// block summed alone while the rest of the chip idled).  Pass 1 lists the hot rows; then
+//   rec_hot_scan_kernel   (one block) each hot row's chunks of kSegChunk references: the
+//                         exclusive prefix of their counts and every chunk's owner
+//   rec_hot_chunk_kernel  one block per chunk (grid-stride): the chunk's block sum
+//                         (segment_grad4_block), written as the chunk's partial
+//   rec_hot_apply_kernel  E/4 lanes per hot row: its partials added in chunk order (the
+//                         canonical long-segment sum, segment.h) and the row's Adam step
+__global__ void rec_hot_reset_kernel(int32_t* __restrict__ hdr) {
+  if (threadIdx.x == 0) { hdr[kHotN] = 0; hdr[kHotT] = 0; }
+}
+
+__global__ __launch_bounds__(1024) void rec_hot_scan_kernel(SegGradIn sg, HotWs h, const int32_t* __restrict__ n_uniq,
+                                                           const float* __restrict__ opt) {
+  __shared__ int ws[16];
+  __shared__ int carry_s;
+  if (step_poisoned(opt)) return;
+  const long long nrefs = (long long)sg.L.batch * index_slots(sg.L);
+  const int nu = clamp_uniq(n_uniq, nrefs, sg.status);
+  const int n = (int)min((long long)h.hdr[kHotN], h.cap_list);
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  if (tid == 0) carry_s = 0;
+  __syncthreads();
+  for (int i0 = 0; i0 < n; i0 += 1024) {
+    const int i = i0 + tid;
+    int nch = 0;
+    if (i < n) {
+      const SegRange r = seg_range(sg, h.list[i], nu, nrefs);
+      nch = (r.e1 - r.e0 + kSegChunk - 1) / kSegChunk;
+    }
+    int inc = nch;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const int y = __shfl_up(inc, o, 64);
+      if (lane >= o) inc += y;
+    }
+    if (lane == 63) ws[wv] = inc;
+    __syncthreads();
+    int wbase = 0;
+    for (int w = 0; w < wv; ++w) wbase += ws[w];
+    const int carry = carry_s;
+    const int ex = carry + wbase + inc - nch;
+    if (i < n) {
+      h.off[i] = ex;
+      for (int c = 0; c < nch && ex + c < h.cap_chunks; ++c) h.map[ex + c] = i;
+    }
+    __syncthreads();
+    if (tid == 1023) carry_s = ex + nch;
+    __syncthreads();
+  }
+  if (tid == 0) {
+    const int total = (int)min((long long)carry_s, h.cap_chunks);
+    h.off[n] = total;
+    h.hdr[kHotT] = total;
+  }
+}
+
+template <int E>
+__global__ __launch_bounds__(256) void rec_hot_chunk_kernel(SegGradIn sg, HotWs h, const int32_t* __restrict__ n_uniq,
+                                                            const float* __restrict__ opt) {
+  if (step_poisoned(opt)) return;
+  __shared__ unsigned char slot_lut[kSlotLutMax];
+  build_slot_lut(sg, slot_lut, sg.L.multi_width);
+  __shared__ SegLongLds sh;
+  const dl_emb_layout& L = sg.L;
+  const int q = threadIdx.x % (E / 4);
+  const int Cf = (L.use_fm && L.fm_cont) ? L.cont_fields : 0;
+  const int F = Cf + L.cate_fields + L.fm_extra;
+  const long long nrefs = (long long)L.batch * index_slots(L);
+  const int nu = clamp_uniq(n_uniq, nrefs, sg.status);
+  const float* ws = sg.w_head + F + 4 * q;
+  const float4 wsec = L.use_fm ? make_float4(ws[0], ws[1], ws[2], ws[3]) : make_float4(0.f, 0.f, 0.f, 0.f);
+  const int T = h.hdr[kHotT];
+  const int PF = hot_part_floats(E);
+  for (int t = blockIdx.x; t < T; t += gridDim.x) {
+    const int i = h.map[t];
+    const int c = t - h.off[i];
+    const SegRange r = seg_range(sg, h.list[i], nu, nrefs);
+    const int c0 = r.e0 + c * kSegChunk;
+    const SegGrad4 p = segment_grad4_block<E>(sg, c0, min(r.e1, c0 + kSegChunk), nrefs, wsec, sh);
+    if (threadIdx.x < E / 4) {
+      float4* o = reinterpret_cast<float4*>(h.part + (long long)t * PF) + 3 * q;
+      o[0] = p.s; o[1] = p.x; o[2] = p.dsum;
+      if (q == 0) h.part[(long long)t * PF + 3 * E] = p.g1;
+    }
+  }
+}
+
+template <int E>
+__global__ __launch_bounds__(256) void rec_hot_apply_kernel(SegGradIn sg, float* __restrict__ rec, RecCfg c, int n_rep,
+                                                            const float* __restrict__ rows_u,
+                                                            const float* __restrict__ rows_u1,
+                                                            const float* __restrict__ mv,
+                                                            const uint32_t* __restrict__ uniq, int world,
+                                                            float* __restrict__ g_rep, float* __restrict__ g1_rep,
+                                                            const float* __restrict__ hist,
+                                                            const float* __restrict__ opt, HotWs h) {
+  if (step_poisoned(opt)) return;
+  rec_load_hyper(c, opt);
+  __shared__ float hw[kHistWin];
+  const RingW ring = load_hist_window(hw, hist, (int)opt[7], c);
+  constexpr int LPR = E / 4;
+  const dl_emb_layout& L = sg.L;
+  const long long gt = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  const int q = (int)(gt % LPR);
+  const long long g0 = gt / LPR, ng = (long long)gridDim.x * blockDim.x / LPR;
+  const int n = (int)min((long long)h.hdr[kHotN], h.cap_list);
+  const int t = (int)opt[7];
+  const float alpha = opt[3];
+  const bool first = c.has_first && q == 0;
+  const int PF = hot_part_floats(E);
+  for (long long i = g0; i < n; i += ng) {
+    const long long u = h.list[i];
+    const int t0 = h.off[i], t1 = h.off[i + 1];
+    auto load = [&](int k) {
+      const float4* o = reinterpret_cast<const float4*>(h.part + (long long)k * PF) + 3 * q;
+      return SegGrad4{o[0], o[1], o[2], h.part[(long long)k * PF + 3 * E]};
+    };
+    SegGrad4 s = load(t0);
+    for (int k = t0 + 1; k < t1; ++k) seg_add(s, load(k));
+    const int64_t row = decode_key(uniq[u], world);
+    const bool row_ok = row >= 0 && row < L.n_rows;
+    float4 p = make_float4(0.f, 0.f, 0.f, 0.f), m = p, v = p;
+    float w = 0.f, wm = 0.f, wv = 0.f;
+    rec_bwd_state<E>(row, n_rep + u, q, first, row_ok, rec, rows_u, rows_u1, mv, c, t, ring, p, m, v, w, wm, wv);
+    if (row_ok) rec_bwd_apply<E>(s, row, q, first, p, m, v, w, wm, wv, rec, c, L, n_rep, g_rep, g1_rep, alpha, t);
+  }
+}
+
 // Rows [row0, row0 + n) updated with dense gradients g [n][E], g1 [n] (then zeroed).
 __global__ __launch_bounds__(256) void rec_apply_rows_kernel(float* __restrict__ rec, RecCfg c, long long row0,
                                                              long long n, float* __restrict__ g,
@@ -595,7 +764,8 @@ __global__ __launch_bounds__(256) void rec_apply_rows_kernel(float* __restrict__
 template <int E>
 __global__ __launch_bounds__(256) void rec_flush_kernel(float* __restrict__ rec, RecCfg c, long long n_rows,
                                                         const float* __restrict__ hist,
-                                                        const float* __restrict__ opt) {
+                                                        const float* __restrict__ opt, float* __restrict__ p_plane,
+                                                        float* __restrict__ w1_plane) {
   rec_load_hyper(c, opt);
   __shared__ float hw[kHistWin];
   const RingW ring = load_hist_window(hw, hist, (int)opt[7], c);
@@ -607,13 +777,23 @@ __global__ __launch_bounds__(256) void rec_flush_kernel(float* __restrict__ rec,
     float* r = rec + row * c.ld;
     const float4 tail = *reinterpret_cast<const float4*>(r + E);
     const int stamp = __float_as_int(tail.w);
-    if (stamp >= target) continue;
+    if (stamp >= target) {
+      if (p_plane) {   // caught up already: its p (and first-order weight) into the planes
+        *reinterpret_cast<float4*>(p_plane + row * E + 4 * q) = *reinterpret_cast<const float4*>(r + 4 * q);
+        if (w1_plane && q == 0) w1_plane[row] = tail.x;
+      }
+      continue;
+    }
     float4 p = *reinterpret_cast<const float4*>(r + 4 * q);
     float4 m = *reinterpret_cast<const float4*>(r + E + 4 + 4 * q);
     float4 v = *reinterpret_cast<const float4*>(r + 2 * E + 4 + 4 * q);
     float w = tail.x, wm = tail.y, wv = tail.z;
     const bool first = c.has_first && q == 0;
     catch_up4(p, m, v, w, wm, wv, first, stamp, target, ring, c);
+    if (p_plane) {
+      *reinterpret_cast<float4*>(p_plane + row * E + 4 * q) = p;
+      if (w1_plane && q == 0) w1_plane[row] = w;
+    }
     *reinterpret_cast<float4*>(r + 4 * q) = p;
     *reinterpret_cast<float4*>(r + E + 4 + 4 * q) = m;
     *reinterpret_cast<float4*>(r + 2 * E + 4 + 4 * q) = v;
@@ -892,16 +1072,24 @@ extern "C" int dl_rec_gather_scatter(const dl_emb_layout* L, const float* rec, i
   DL_RETURN_LAUNCH("dl_rec_gather_scatter");
 }
 
+extern "C" int64_t dl_rec_bwd_workspace_bytes(int64_t nrefs, int32_t emb_dim) {
+  return nrefs > 0 && emb_dim > 0 ? hot_ws_bytes(nrefs, emb_dim) : 0;
+}
+
 extern "C" int dl_rec_bwd_adam(const dl_emb_layout* L, float* rec, int32_t rec_ld, int32_t rec_flags, int32_t n_rep,
                                const float* rows_u, const float* rows_u1, const float* mv_u,
                                const uint32_t* uniq_keys, const int32_t* seg_off, const int32_t* n_uniq,
                                const int32_t* sorted_refs, int32_t world, int64_t max_uniq, const float* dz,
                                const float* w_head, const float* fm_sum, const float* dx0, float* g_rep,
                                float* g1_rep, const float* hist, int32_t hist_len, const float* opt,
-                               const dl_pool_desc* pool, void* stream) {
+                               const dl_pool_desc* pool, void* hot_ws_ptr, int64_t hot_ws_size, void* stream) {
   const int32_t has_first = rec_flags & DL_REC_FIRST;
   DL_CHECK_ARG(L && rec && rows_u && uniq_keys && seg_off && n_uniq && sorted_refs && dx0 && opt,
                "NULL argument");
+  const long long nrefs_all = (long long)L->batch * index_slots(*L);
+  DL_CHECK_ARG(!hot_ws_ptr || (hot_ws_size >= hot_ws_bytes(nrefs_all, L->emb_dim) && (uintptr_t)hot_ws_ptr % 16 == 0),
+               "hot-row workspace: %lld bytes needed (dl_rec_bwd_workspace_bytes), 16-B aligned",
+               (long long)hot_ws_bytes(nrefs_all, L->emb_dim));
   DL_CHECK_ARG(mv_u || hist, "without the moment stash the alpha ring is required");
   if (int rc = rec_check(L->emb_dim, rec_ld, mv_u ? 2 : hist_len)) return rc;
   DL_CHECK_ARG(!L->use_fm || (dz && w_head && fm_sum), "FM backward inputs required");
@@ -941,15 +1129,27 @@ extern "C" int dl_rec_bwd_adam(const dl_emb_layout* L, float* rec, int32_t rec_l
 #endif
     auto bwd = (DL_BWD_STASH_SPECIAL && mv_u) ? (multi ? rec_bwd_adam_kernel<kE, true, true> : rec_bwd_adam_kernel<kE, true>)
                                               : rec_bwd_adam_kernel<kE, false>;
-    hipLaunchKernelGGL(bwd, dim3(grid), dim3(256), 0, as_stream(stream), sg, rec,
-                       make_rec_cfg(kE, rec_ld, rec_flags, (mv_u ? 2 : hist_len)), n_rep, rows_u,
-                       has_first ? rows_u1 : nullptr, mv_u, uniq_keys, n_uniq, world, g_rep,
-                       has_first ? g1_rep : nullptr, hist, opt);
-    // the hot rows' long segments (none at uniform ids: one scan of the segment offsets)
-    hipLaunchKernelGGL(rec_bwd_long_kernel<kE>, dim3(1024), dim3(256), 0, as_stream(stream), sg, rec,
-                       make_rec_cfg(kE, rec_ld, rec_flags, (mv_u ? 2 : hist_len)), n_rep, rows_u,
-                       has_first ? rows_u1 : nullptr, mv_u, uniq_keys, n_uniq, world, g_rep,
-                       has_first ? g1_rep : nullptr, hist, opt);
+    hipStream_t st = as_stream(stream);
+    const RecCfg rc = make_rec_cfg(kE, rec_ld, rec_flags, (mv_u ? 2 : hist_len));
+    if (hot_ws_ptr) {
+      const HotWs h = hot_ws(hot_ws_ptr, nrefs_all, kE);
+      hipLaunchKernelGGL(rec_hot_reset_kernel, dim3(1), dim3(64), 0, st, h.hdr);   // (no memset node in the graph)
+      hipLaunchKernelGGL(bwd, dim3(grid), dim3(256), 0, st, sg, rec, rc, n_rep, rows_u, has_first ? rows_u1 : nullptr,
+                         mv_u, uniq_keys, n_uniq, world, g_rep, has_first ? g1_rep : nullptr, hist, opt, h.hdr);
+      // the hot rows (none at uniform ids): chunks over the whole grid, then their updates
+      hipLaunchKernelGGL(rec_hot_scan_kernel, dim3(1), dim3(1024), 0, st, sg, h, n_uniq, opt);
+      hipLaunchKernelGGL(rec_hot_chunk_kernel<kE>, dim3(1024), dim3(256), 0, st, sg, h, n_uniq, opt);
+      hipLaunchKernelGGL(rec_hot_apply_kernel<kE>, dim3(64), dim3(256), 0, st, sg, rec, rc, n_rep, rows_u,
+                         has_first ? rows_u1 : nullptr, mv_u, uniq_keys, world, g_rep, has_first ? g1_rep : nullptr,
+                         hist, opt, h);
+    } else {
+      hipLaunchKernelGGL(bwd, dim3(grid), dim3(256), 0, st, sg, rec, rc, n_rep, rows_u, has_first ? rows_u1 : nullptr,
+                         mv_u, uniq_keys, n_uniq, world, g_rep, has_first ? g1_rep : nullptr, hist, opt, nullptr);
+      // the hot rows' long segments (none at uniform ids: one scan of the segment offsets)
+      hipLaunchKernelGGL(rec_bwd_long_kernel<kE>, dim3(1024), dim3(256), 0, st, sg, rec, rc, n_rep, rows_u,
+                         has_first ? rows_u1 : nullptr, mv_u, uniq_keys, n_uniq, world, g_rep,
+                         has_first ? g1_rep : nullptr, hist, opt, nullptr);
+    }
   });
   DL_RETURN_LAUNCH("dl_rec_bwd_adam");
 }
@@ -970,15 +1170,17 @@ extern "C" int dl_rec_apply_rows(float* rec, int32_t rec_ld, int32_t emb_dim, in
 }
 
 extern "C" int dl_rec_flush(float* rec, int32_t rec_ld, int32_t emb_dim, int32_t rec_flags, int64_t n_rows,
-                            const float* hist, int32_t hist_len, const float* opt, void* stream) {
+                            const float* hist, int32_t hist_len, const float* opt, float* p_plane, float* w1_plane,
+                            void* stream) {
   const int32_t has_first = rec_flags & DL_REC_FIRST;
   DL_CHECK_ARG(rec && hist && opt, "NULL argument");
   if (int rc = rec_check(emb_dim, rec_ld, hist_len)) return rc;
+  DL_CHECK_ARG(!p_plane || (uintptr_t)p_plane % 16 == 0, "p_plane must be 16-B aligned");
   if (n_rows <= 0) return 0;
   DL_DISPATCH_E(emb_dim, {
     hipLaunchKernelGGL(rec_flush_kernel<kE>, dim3(grid_cap(n_rows * (kE / 4))), dim3(256), 0, as_stream(stream),
                        rec, make_rec_cfg(kE, rec_ld, rec_flags, hist_len), (long long)n_rows, hist,
-                       opt);
+                       opt, p_plane, has_first ? w1_plane : nullptr);
   });
   DL_RETURN_LAUNCH("dl_rec_flush");
 }

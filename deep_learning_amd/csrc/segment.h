@@ -347,6 +347,27 @@ __device__ __forceinline__ SegGrad4 segment_grad4_block(const SegGradIn& a, int 
   return t;
 }
 
+// The canonical sum of a long segment: chunks of kSegChunk references, each summed by
+// segment_grad4_block from its own start, and the chunk sums added in chunk order
+// (total = c0; total += c1; ...).  One block computes it chunk after chunk here; the lazy
+// record backward spreads the chunks of its hot rows over many blocks (rec.hip,
+// rec_bwd_chunk_kernel) and adds their partials in the same order — the same sums either way.
+constexpr int kSegChunk = 1024;
+
+__device__ __forceinline__ void seg_add(SegGrad4& t, const SegGrad4& c) {
+  t.s = f4add(t.s, c.s); t.x = f4add(t.x, c.x); t.dsum = f4add(t.dsum, c.dsum);
+  t.g1 += c.g1;
+}
+
+template <int E>
+__device__ __forceinline__ SegGrad4 segment_grad4_chunked(const SegGradIn& a, int e0, int e1, long long nrefs,
+                                                          float4 wsec, SegLongLds& sh) {
+  SegGrad4 t = segment_grad4_block<E>(a, e0, min(e1, e0 + kSegChunk), nrefs, wsec, sh);
+  for (int c0 = e0 + kSegChunk; c0 < e1; c0 += kSegChunk)
+    seg_add(t, segment_grad4_block<E>(a, c0, min(e1, c0 + kSegChunk), nrefs, wsec, sh));
+  return t;
+}
+
 // Second pass over the long segments: block b scans its share of the unique rows for
 // segments of more than kSegLong references and calls fn(u, sums) for each, in threads
 // 0 .. E/4 - 1, after the whole block summed it.  Block-uniform; one barrier per 256 rows.
@@ -368,7 +389,7 @@ __device__ __forceinline__ void for_long_segments(const SegGradIn& a, long long 
     for (int k = 0; k < n; ++k) {
       const long long uu = base + sh.u[k];
       const SegRange r = seg_range(a, uu, nu, nrefs);
-      const SegGrad4 t = segment_grad4_block<E>(a, r.e0, r.e1, nrefs, wsec, sh);
+      const SegGrad4 t = segment_grad4_chunked<E>(a, r.e0, r.e1, nrefs, wsec, sh);
       if (tid < E / 4) fn(uu, t);
     }
     __syncthreads();   // sh.n / sh.u before the next chunk

@@ -435,6 +435,8 @@ class CTREngine:
             # Off by default — re-reading the record in the backward measured faster on both
             # kernels (gather 328 -> 232 us, backward 505 -> 447 us at C2; profiles/r01l).
             self.mv_u = z(self.n_rep + self.n_refs, 2 * E + 4) if rec_stash else None
+            # hot rows' chunked segment sums (dl_rec_bwd_adam: Zipf rows over many blocks)
+            self.hot_ws = z(int(_lib.lib().dl_rec_bwd_workspace_bytes(self.n_refs, E)), dt=torch.uint8)
         # fwd_rec: the forward reads the cate rows straight from the records (dl_embed_fwd_rec)
         # instead of gathering the batch's unique rows and reading them back through the
         # inverse map; only the C replicated cont rows are gathered.  Single-valued fields.
@@ -465,6 +467,9 @@ class CTREngine:
         self.in_vec = z(B, max(sp.V, 1))
         self.in_cate = z(B, max(sp.cate_ld, 1), dt=torch.int64)
         self.graphs = {}        # (buffer set, batch) -> captured step
+        # predict on a flushed table reads dense p / first-order planes written by the flush
+        # (DLAMD_FLAT_PLANES=0: each reference reads its record's first line instead)
+        self.flat_planes = os.environ.get("DLAMD_FLAT_PLANES", "1") != "0"
         self.prof = None
         self.steps = 0
         if init == "device":
@@ -499,6 +504,14 @@ class CTREngine:
         L.multi_width = sp.multi_width if self.lazy else 0
         L.cont_rows_compact = 1 if self.lazy else 0     # records: cont rows gathered first into rows_u
         L.x0_bf16 = 1 if self.x0_direct else 0           # bf16 tower: the forward writes x0 as bf16
+        return L
+
+    def _flat_layout(self, B):
+        """The layout of the dense-table forward over the flushed planes (the replicated FM
+        cont rows read from the planes in place, no batch index)."""
+        L = self._layout(B)
+        L.cont_rows_compact = 0
+        L.multi_width = 0
         return L
 
     # ------------------------------------------------------------------ params
@@ -713,14 +726,25 @@ class CTREngine:
             self.rec[: first.shape[0], E].copy_(first)
         self.rec.view(torch.int32)[:, E + 3] = int(self.opt[7].item())
         self.since_flush = 0
+        self.planes_step = -1   # the planes (if any) no longer match the records
         torch.cuda.synchronize()
 
-    def flush(self):
-        """Catch every row record up to the current step (no-op for the dense engine)."""
+    def flush(self, planes=False):
+        """Catch every row record up to the current step (no-op for the dense engine).
+        planes=True also writes every row's p and first-order weight out as dense planes
+        (the table predict's plain lookup reads, _forward)."""
         if not self.lazy:
             return
+        pp = w1 = None
+        if planes:
+            if getattr(self, "p_plane", None) is None:
+                self.p_plane = torch.empty(self.rec.shape[0], self.spec.E, device=self.dev)
+                self.w1_plane = torch.empty(self.rec.shape[0], device=self.dev) if self.spec.fm else None
+            pp, w1 = self.p_plane, self.w1_plane
         self._c("rec_flush", "dl_rec_flush", ptr(self.rec), self.rec_ld, self.spec.E, self.rec_flags,
-                self.rec.shape[0], ptr(self.hist), self.hist_len, ptr(self.opt), _lib.stream_handle())
+                self.rec.shape[0], ptr(self.hist), self.hist_len, ptr(self.opt), ptr(pp), ptr(w1),
+                _lib.stream_handle())
+        self.planes_step = self.steps if planes else getattr(self, "planes_step", -1)
         if getattr(self, "wide_lazy", False):
             self._wide_flush()
         self.since_flush = 0
@@ -758,6 +782,7 @@ class CTREngine:
             self.rec[:N, E + 2].copy_(t("v1"))
         self.rec.view(torch.int32)[:, E + 3] = int(self.opt[7].item())
         self.since_flush = 0
+        self.planes_step = -1
 
     # ------------------------------------------------------------------ inputs
     def stage(self, batch):
@@ -802,7 +827,14 @@ class CTREngine:
             self._c("pool_fwd", "dl_pool_fwd", C_ref(L), ptr(self.table), ptr(self.first) if sp.fm else None,
                  ptr(self.in_cate), sp.S, ptr(self.slot_start), ptr(self.slot_end), sp.M, self.fm_pool_col,
                  ptr(self.x0), ptr(self.fm_out), ptr(self.cnt_emb), ptr(self.cnt_first), ptr(self.err), s)
-        if not train and self.lazy and not sp.M and self.since_flush == 0 and type(self) is CTREngine:
+        if (not train and self.lazy and not sp.M and self.since_flush == 0 and type(self) is CTREngine
+                and getattr(self, "planes_step", -1) == self.steps):
+            # predict on a flushed table whose p / first-order planes are current (flush(planes=
+            # True) at this step): the plain lookup of the dense layout, 64-B rows (dl_embed_fwd)
+            self._c("embed_fwd", "dl_embed_fwd", C_ref(self._flat_layout(B)), ptr(self.p_plane), ptr(self.w1_plane),
+                    ptr(self.in_cate), ptr(self.in_cont), ptr(self.in_vec), ptr(x0), ptr(self.fm_out),
+                    ptr(self.fm_sum), ptr(self.err), s)
+        elif not train and self.lazy and not sp.M and self.since_flush == 0 and type(self) is CTREngine:
             # predict on a flushed table (every record caught up to the current step): the plain
             # lookup, each reference reading its record's first line (dl_embed_fwd_rec_flat)
             if self.n_rep:   # the replicated FM cont-field rows, compact
@@ -1234,7 +1266,8 @@ class CTREngine:
                 ptr(self.rows_u), ptr(self.rows_u1), ptr(self.mv_u), ptr(self.idx_uniq), ptr(self.idx_off),
                 ptr(self.idx_n), ptr(self.idx_refs), 1, B * self.n_slot, ptr(self.dz), ptr(self.w_head),
                 ptr(self.fm_sum), ptr(self.dx0), ptr(self.g_rep), ptr(self.g1_rep), ptr(self.hist),
-                self.hist_len, ptr(self.opt), C_ref(self.pool_desc) if sp.M else None, s)
+                self.hist_len, ptr(self.opt), C_ref(self.pool_desc) if sp.M else None, ptr(self.hot_ws),
+                self.hot_ws.numel(), s)
         if R:
             # FM cont-field rows: per-block register partials, folded into g_rep, then updated
             self._c("cont_bwd", "dl_embed_cont_bwd", C_ref(L), ptr(self.rows_u), ptr(self._cont()),
@@ -1260,7 +1293,12 @@ class CTREngine:
 
     def predict(self, batch, logits=False, device=False):
         """Forward only: returns sigmoid scores [B] (or the logits) as host numpy, or as a
-        device tensor (a copy) with device=True."""
+        device tensor (a copy) with device=True.  On a flushed table (no training step since
+        the last flush) the first predict writes the p / first-order planes once (a flush
+        that only copies: every row is caught up) and every later one reads them."""
+        if (self.lazy and not self.spec.M and self.since_flush == 0 and type(self) is CTREngine
+                and getattr(self, "planes_step", -1) != self.steps and self.flat_planes):
+            self.flush(planes=True)
         B, indexed = self._begin(batch)
         s = _lib.stream_handle()
         if not indexed:

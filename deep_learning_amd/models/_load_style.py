@@ -58,33 +58,38 @@ class LoadStyleModel:
                                     adam=default_adam(self.spec))
         return self.engine
 
+    def train_epoch(self, train_data):
+        """One pass over the pickled batches: sess.run([loss, optimizer]) per batch (wdl.py:
+        305-309).  The step's loss is summed on the device (no host read per step, no wide-table
+        flush) and read once at the end; the next batch is unpickled, staged and indexed while
+        the current step runs.  Returns (sum of the per-step losses, steps)."""
+        eng = self.model_optimizer()
+        eng.loss_sum_begin()
+        steps = 0
+        items = iter(train_data)
+        b = next(items, None)
+        b = self.batch(b) if b is not None else None
+        while b is not None:
+            nxt = next(items, None)
+            nxt = self.batch(nxt) if nxt is not None else None
+            eng.train_step(b, graph=b["label"].shape[0] == eng.B, **({"next_batch": nxt} if nxt is not None else {}))
+            steps += 1
+            b = nxt
+        loss_sum, counted = eng.loss_sum_end()
+        if counted != steps:
+            eng.check_error()   # a skipped (bad) batch raises here, as its sess.run did
+        return loss_sum, steps
+
     def fit(self, train_data, val_data):
         eng = self.model_optimizer()
         losses = []
         num_samples = 0
         for epoch in range(self.epochs):
             st = time.time()
-            # sess.run([loss, optimizer]) per batch (wdl.py:305-309): the step's loss is summed on
-            # the device (no host read per step, no wide-table flush); the epoch's mean is the
-            # reference's sum(loss_t * batch_size) / num_samples (num_samples counts batch_size
-            # per batch, the last partial batch included)
-            eng.loss_sum_begin()
-            steps = 0
-            items = iter(train_data)
-            b = next(items, None)
-            b = self.batch(b) if b is not None else None
-            while b is not None:
-                # the next batch is unpickled, staged and indexed while this step runs
-                nxt = next(items, None)
-                nxt = self.batch(nxt) if nxt is not None else None
-                eng.train_step(b, graph=b["label"].shape[0] == eng.B,
-                               **({"next_batch": nxt} if nxt is not None else {}))
-                steps += 1
-                num_samples += self.batch_size
-                b = nxt
-            loss_sum, counted = eng.loss_sum_end()
-            if counted != steps:
-                eng.check_error()   # a skipped (bad) batch raises here, as its sess.run did
+            # the epoch's mean is the reference's sum(loss_t * batch_size) / num_samples
+            # (num_samples counts batch_size per batch, the last partial batch included)
+            loss_sum, steps = self.train_epoch(train_data)
+            num_samples += self.batch_size * steps
             losses.append(loss_sum * self.batch_size)
             end_time = time.time()
             total_loss = float(np.sum(losses) / num_samples)

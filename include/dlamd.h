@@ -515,14 +515,19 @@ typedef struct dl_pool_desc {
   float* g1_pool;
 } dl_pool_desc;
 /* pool: required when L->multi_width > 0 (multi refs add (dp/cnt) to the row gradient
- * and dz*w_head[fm_col+m]/cnt_first to the first-order one), else may be NULL. */
+ * and dz*w_head[fm_col+m]/cnt_first to the first-order one), else may be NULL.
+ * hot_ws (may be NULL; dl_rec_bwd_workspace_bytes(batch * index slots, E) bytes, 16-B aligned):
+ * the rows with more than 32 references (Zipf-hot ids) are summed in chunks of 1,024
+ * references spread over the whole grid, the chunk sums added in chunk order — the same
+ * canonical sum as the single-block pass used without it (and by dl_embed_bwd_sorted). */
 int dl_rec_bwd_adam(const dl_emb_layout* L, float* rec, int32_t rec_ld, int32_t rec_flags, int32_t n_rep,
                     const float* rows_u, const float* rows_u1, const float* mv_u,
                     const uint32_t* uniq_keys, const int32_t* seg_off, const int32_t* n_uniq,
                     const int32_t* sorted_refs, int32_t world, int64_t max_uniq, const float* dz,
                     const float* w_head, const float* fm_sum, const float* dx0, float* g_rep,
                     float* g1_rep, const float* hist, int32_t hist_len, const float* opt,
-                    const dl_pool_desc* pool, void* stream);
+                    const dl_pool_desc* pool, void* hot_ws, int64_t hot_ws_bytes, void* stream);
+int64_t dl_rec_bwd_workspace_bytes(int64_t nrefs, int32_t emb_dim);
 /* Sharded owners without a sort: link every received position into its row's arrival
  * chain (head[local_rows] starts at -1; next[n]).  Then apply: one leader per row sums its
  * arrivals g[pos][E], g1[pos] in ascending position order (as dl_rec_apply_segments over a
@@ -545,9 +550,13 @@ int dl_rec_apply_segments(float* rec, int32_t rec_ld, int32_t emb_dim, int32_t r
                           const int32_t* sorted_pos, const float* g, const float* g1, const float* rows,
                           const float* rows1, const float* mv, const float* hist, int32_t hist_len,
                           const float* opt, void* stream);
-/* Every row caught up to step opt[7] (before export/checkpoint, and every hist_len steps). */
+/* Every row caught up to step opt[7] (before export/checkpoint, and every hist_len steps).
+ * p_plane [n_rows][E] / w1_plane [n_rows] (may be NULL): every row's caught-up p and first-order
+ * weight written out densely — the table predict's plain lookup then reads (dl_embed_fwd on the
+ * planes: 64-B rows instead of the records' 128-B first lines). */
 int dl_rec_flush(float* rec, int32_t rec_ld, int32_t emb_dim, int32_t rec_flags, int64_t n_rows,
-                 const float* hist, int32_t hist_len, const float* opt, void* stream);
+                 const float* hist, int32_t hist_len, const float* opt, float* p_plane, float* w1_plane,
+                 void* stream);
 
 /* ------------------------------------------------------------------------
  * Row-sharded tables (shard.hip).  Owner side of the all-to-all lookup:

@@ -1,0 +1,36 @@
+#!/bin/bash
+# Round-4 GPU steps: bash scripts/gpu_r4.sh MODE TAG
+#   quick   the GPU suite without the full-size trajectories, then C3 uniform and Zipf benches
+#   full    the full-size trajectories (C2, C3 10 steps with the fp64 audit; C5; C4)
+#   bench   the default bench line
+MODE=$1
+TAG=${2:-r4}
+cd "$GRAFT_REPO_ROOT"
+OUT=gpurun_out/$TAG
+mkdir -p $OUT
+export TMPDIR=/tmp
+if [ "$MODE" = quick ]; then
+  timeout -k 10 600 python -u -m pytest tests -m gpu -x -q -rf -p no:cacheprovider --timeout 300 --timeout-method thread \
+    --deselect tests/test_gpu_fullsize.py --durations=10 > $OUT/pytest_quick.log 2>&1
+  rc=$?; echo "pytest rc=$rc"; tail -15 $OUT/pytest_quick.log; [ $rc -eq 0 ] || exit $rc
+  timeout -k 10 300 python bench.py --workload c3 --no-extra --no-cpu-baseline --steps 10 > $OUT/c3.json 2> $OUT/c3.err
+  rc=$?; echo "c3 rc=$rc"; [ $rc -eq 0 ] || { tail -5 $OUT/c3.err; exit $rc; }
+  python scripts/bench_brief.py $OUT/c3.json
+  timeout -k 10 300 python bench.py --workload c3 --dist zipf --no-extra --no-cpu-baseline --steps 10 > $OUT/c3z.json 2> $OUT/c3z.err
+  rc=$?; echo "c3 zipf rc=$rc"; [ $rc -eq 0 ] || { tail -5 $OUT/c3z.err; exit $rc; }
+  python scripts/bench_brief.py $OUT/c3z.json
+  exit 0
+fi
+if [ "$MODE" = full ]; then
+  export DLAMD_TEST_STATS=$OUT
+  timeout -k 10 1100 python -u -m pytest tests/test_gpu_fullsize.py -x -v -rf -p no:cacheprovider --timeout 1000 \
+    --timeout-method thread --durations=6 > $OUT/pytest_full.log 2>&1
+  rc=$?; echo "pytest rc=$rc"; tail -15 $OUT/pytest_full.log; exit $rc
+fi
+if [ "$MODE" = bench ]; then
+  timeout -k 10 600 python bench.py > $OUT/bench_default.json 2> $OUT/bench_default.err
+  rc=$?; echo "bench rc=$rc"; [ $rc -eq 0 ] || { tail -5 $OUT/bench_default.err; exit $rc; }
+  python scripts/bench_brief.py $OUT/bench_default.json
+  exit 0
+fi
+echo "usage: gpu_r4.sh quick|full|bench TAG"; exit 2

@@ -132,6 +132,7 @@ def test_local_run_family_models_end_to_end(hip_lib, tmp_path, alg):
 
 
 def test_wdl_load_style_fit_evaluate_predict(hip_lib, tmp_path):
+    from oracle import ctr_ref as R
     from deep_learning_amd.models import wdl
     from deep_learning_amd.synthetic import make_batch
     from deep_learning_amd.utils import data_loader_load as dll
@@ -148,6 +149,21 @@ def test_wdl_load_style_fit_evaluate_predict(hip_lib, tmp_path):
     tr = dll.load_input_file(Args, str(tmp_path / "tr"))
     va = dll.load_input_file(Args, str(tmp_path / "va"))
     m = wdl.DeepModel(Args)
+    # the training trajectory against the oracle: the epoch losses the fit prints (the
+    # device-summed per-step losses, wdl.py:305-313) over two epochs of the same pickled
+    # batches (the last one partial: 300 = 4 x 64 + 44) from the engine's own initial state
+    eng = m.model_optimizer()
+    P = eng.params()
+    cfg = R.make_cfg("wdl", C=13, S=26, E=8, cate_index_size=4000, hidden=[32, 16], Fw=26)
+    opt = R.AdamTF1(cfg, P)
+    for epoch in range(2):
+        ref = [R.train_step(cfg, P, opt, m.batch(item))["loss"] for item in tr]
+        got, steps = m.train_epoch(tr)
+        assert steps == len(ref) == 5
+        np.testing.assert_allclose(got, float(np.sum(ref)), rtol=1e-5, err_msg="epoch %d loss sum" % epoch)
+    Pg = eng.params()
+    for k in P:
+        np.testing.assert_allclose(Pg[k], P[k], atol=1e-5, rtol=0, err_msg=k)
     m.fit(tr, va)
     auc_eval = m.evaluate(None, va)
     auc_pred = m.predict(va)

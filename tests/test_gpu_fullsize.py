@@ -9,28 +9,34 @@ run the product path (row records, lazy-exact Adam, hipGraph replay) at full siz
       against the single-GPU engine on the same table and batches
   C5  wdl, bf16 deep tower, 26M rows + 26 wide ids, B = 65,536  (stated bf16 tolerance)
 
-C2 / C3 / C5 follow a 3-step TRAJECTORY against the numpy oracle fed the same injected
-initial parameters and batches: every logit and the loss at every step; every dense
-parameter and its Adam moments after every step; the whole table (values, first-order
-weights, Adam moments) after every step (fp32), or a sample of the rows the batches touched
-plus rows they did not after the first and the last step (the bf16 tower, which is held to
-its stated bf16 bounds and never repaired).
+C2 / C3 run 10 steps (logits within 1e-5 at steps 0-10) in two tracks against
+the numpy oracle, from the same injected initial parameters and the same batches:
 
-Ill-conditioned sums: an element whose summed gradient is within fp32 rounding of zero, or
-whose few terms switch on or off with a ReLU pre-activation within rounding of zero, can move
-differently when the summation order differs from numpy's (a [400, 400] weight gradient sums
-65,536 products per element) — by up to FLIP * alpha in Adam's sign-saturated first steps,
-and by ~1e-4 in its epsilon regime (|g| ~ 1e-8, where d(update)/dg = 0.1 alpha / eps = 1e4).
-Measured at C2 (profiles/r03b, r03c): ~15 of the ~560 k dense parameters per step, which then
-move the next step's logits by up to 5e-5.  So after each step every element off by more than
-TOL must be one of at most 1e-4 of its array after the first step (dense: 1e-3, table: 5e-4
-after the others) and within one step's
-flip size, and those elements alone take the GPU's value and moments in the oracle before the
-next step (their count and |G| / sum|terms| are recorded in the stats); the rest of the state
-is never re-synced.  Logits: 1e-5 at step 0 (identical state); at later steps 1e-5 against the
-oracle's forward of the GPU's own state after the previous step (identical state again), and
-along the trajectory against the never-re-synced oracle within 1e-5 for all but 1e-3 of the
-samples, every one within Z_DRIFT (measured: 9 of 65,536 samples at 1.2e-5, C2 step 2, r03d).
+  same-state (all 10 steps): before every step the oracle takes the GPU's whole state
+    (parameters and Adam moments, exported), takes the f32 TF1 step, and the GPU's step must
+    agree: every logit and the loss within 1e-5, every parameter element within 1e-5 —
+    or else the element is AUDITED in fp64 (tests/_fp64_audit.py): the gradient the GPU
+    applied (read back from its Adam moments) must equal the element's gradient of the GPU's
+    own pre-step state recomputed in float64 within the a-priori f32 error bound
+    K u S (S the element's running-error scale, K = K_SUM the summation depth) plus the
+    envelope of ReLU pre-activations within rounding of zero, and its v and p must have moved
+    by TF1 Adam on that gradient.  An element that fails the audit fails the test; the
+    audited elements' count and conditioning (min |G| / S, max |g' - G| / (u S)) go to the
+    stats, table and dense alike.
+  trajectory (first TRAJ_STEPS steps): the oracle is never re-synced except for the elements
+    off by more than 1e-5 (ill-conditioned sums, counted and bounded: at most 1e-4 of an
+    array after the first step, 1e-3 / 5e-4 later, each within one step's flip size), and
+    the logits along it must stay within 1e-5 for all but 1e-3 of the samples, every one
+    within Z_DRIFT — the drift of two f32 evaluation orders, which the same-state track
+    shows is not an error of either step.
+
+Why the same-state track and not a longer trajectory: the elements whose summed gradient is
+within f32 rounding of zero (a [400, 400] weight gradient sums 65,536 products per element)
+move by up to 2 * FLIP * alpha in Adam's sign-saturated first steps whichever way the sum
+rounds, so two correct f32 implementations drift apart step by step (measured: 770, 3,827,
+13,644 such table elements at steps 0-2 of the never-re-synced C2 run, profiles/r03zl).
+
+C5 (bf16 tower) follows the TRAJ_STEPS trajectory at its stated bf16 bounds, never repaired.
 
 DLAMD_TEST_STATS=<dir>: each test appends its measured maxima / flip fractions there (json).
 """
@@ -47,12 +53,15 @@ pytestmark = [pytest.mark.gpu, pytest.mark.timeout(900)]
 from deep_learning_amd.engine import CTREngine, ModelSpec  # noqa: E402
 from deep_learning_amd.synthetic import make_batch  # noqa: E402
 from oracle import ctr_ref as R  # noqa: E402
+from tests import _fp64_audit as A  # noqa: E402
 
 TOL = 1e-5
 N_CATE = 26 * 1_000_000
 B = 65536
 HIDDEN = [400, 400, 400]
-STEPS = 3
+STEPS = 10           # fp32 C2 / C3, same-state track
+TRAJ_STEPS = 3       # the never-re-synced trajectory (fp32) and the C5 bf16 run
+K_SUM = 2048         # summation-depth bound of the fp64 audit (|g' - G64| <= K_SUM u S + U)
 
 # |m / sqrt(v)| <= (1 - b1) / sqrt(1 - b2) for TF1 Adam's moments (b1^2 < b2), so one update
 # moves an element by at most FLIP * alpha and a sign flip of it by twice that
@@ -223,10 +232,131 @@ def _run(name, model, kw, batches, tower="f32", z_tol=TOL, loss_tol=TOL, auc_tol
     return eng
 
 
+def _run_fp32(name, model, kw, batches, seed=42):
+    """The fp32 configs (C2, C3): the same-state track over every batch with the fp64 audit of
+    every element off by more than TOL, and the never-re-synced trajectory over the first
+    TRAJ_STEPS batches (module docstring)."""
+    cfg = R.make_cfg(model, **kw)
+    P0 = R.init_params(cfg, np.random.default_rng(seed))
+    eng = CTREngine(ModelSpec(model, **kw), max_batch=B, init="none", adam="lazy")
+    eng.load_params(P0)
+    spec = eng.spec
+    tk, fk = spec.table_key, spec.first_key
+    tab_moments = {tk: ("m", "v"), fk: ("m1", "v1")}
+    fails = []
+
+    def check(cond, msg):
+        if not cond:
+            fails.append(msg)
+
+    # the GPU's state before the next step, in the reference layout
+    gpu_p = {k: v.copy() for k, v in P0.items()}
+    gpu_m = {k: np.zeros_like(v) for k, v in P0.items()}
+    gpu_v = {k: np.zeros_like(v) for k, v in P0.items()}
+    opt_s = R.AdamTF1(cfg, gpu_p)
+    Pt = {k: v.copy() for k, v in P0.items()}          # the never-re-synced trajectory
+    opt_t = R.AdamTF1(cfg, Pt)
+    b1, b2, eps = cfg.beta1, cfg.beta2, cfg.eps
+    for step, b in enumerate(batches):
+        alpha = float(opt_s.alpha())
+        # ---- the same-state oracle step: from the GPU's whole state after the previous step
+        Ps = {k: v.copy() for k, v in gpu_p.items()}
+        opt_s.m = {k: v.copy() for k, v in gpu_m.items()}
+        opt_s.v = {k: v.copy() for k, v in gpu_v.items()}
+        fw = R.forward(cfg, Ps, b)
+        G, _ = R.backward(cfg, Ps, b, fw)
+        opt_s.apply(Ps, G)
+        del G
+        traj = step < TRAJ_STEPS
+        if traj:
+            trace = {}
+            fwt = R.forward(cfg, Pt, b)
+            Gt, _ = R.backward(cfg, Pt, b, fwt, trace=trace)
+            opt_t.apply(Pt, Gt)
+        eng.train_step(b, graph=step >= 1)
+        torch.cuda.synchronize()
+        eng.check_error()
+        gpu_mid = A.read_gpu(eng, B)
+        z = eng.z[:B].cpu().numpy().astype(np.float64)
+        loss = eng.loss()
+        d = np.abs(z - fw["z"])
+        _stat("%s step %d same-state" % (name, step), z_max_err=d.max(), loss_err=abs(loss - fw["loss"]))
+        check(d.max() <= TOL, "logits step %d from the GPU's state: max error %g (%d samples > %g)" % (
+            step, d.max(), (d > TOL).sum(), TOL))
+        check(abs(loss - fw["loss"]) < TOL, "loss step %d: %r vs %r" % (step, loss, fw["loss"]))
+        gp = eng.params()
+        ds = eng.dense_state()
+        st = eng.adam_state()
+        new_m = {k: (st[tab_moments[k][0]].reshape(P0[k].shape) if k in tab_moments else ds["m"][k]) for k in gp}
+        new_v = {k: (st[tab_moments[k][1]].reshape(P0[k].shape) if k in tab_moments else ds["v"][k]) for k in gp}
+        del st, ds
+        # ---- every stage of the GPU's step against fp64 of its own inputs (tests/_fp64_audit.py)
+        audit = A.StepAudit(cfg, gpu_p, b, gpu_mid)
+        for what, st_ in audit.stats.items():
+            _stat("%s step %d stage %s" % (name, step, what), **st_)
+        fails += ["step %d: %s" % (step, f) for f in audit.fails]
+        # ---- every element of the GPU's step against the oracle's step from the same state;
+        # the elements off by more than TOL are audited in fp64
+        for key in P0:
+            diff = np.abs(gp[key].astype(np.float64) - Ps[key])
+            idx = np.flatnonzero(diff.reshape(-1) > TOL)
+            what = "%s (step %d)" % (key, step)
+            _stat("%s %s same-state" % (name, what), max_err=diff.max(), n_off=len(idx))
+            if not len(idx):
+                continue
+            check(len(idx) <= max(1, 1e-3 * diff.size), "%s: %d of %d elements off by > %g" % (
+                what, len(idx), diff.size, TOL))
+            fl = lambda a: np.asarray(a).reshape(-1)[idx]
+            ok, st_, (g, G64, S) = A.audit_elements(audit, key, idx, P0[key].shape, fl(gpu_m[key]), fl(new_m[key]),
+                                                    fl(gpu_v[key]), fl(new_v[key]), fl(gpu_p[key]), fl(gp[key]),
+                                                    alpha, b1, b2, eps)
+            _stat("%s %s audited" % (name, what), **st_)
+            if not ok.all():
+                j = int(np.flatnonzero(~ok)[0])
+                fails.append("%s: %d of %d audited elements fail the fp64 audit (e.g. flat %d: GPU gradient %r, "
+                             "fp64 %r, scale %r)" % (what, (~ok).sum(), len(idx), idx[j], g[j], G64[j], S[j]))
+        del audit
+        # ---- the never-re-synced trajectory (first TRAJ_STEPS steps)
+        if traj:
+            dz = np.abs(z - fwt["z"])
+            _stat("%s step %d" % (name, step), z_max_err=dz.max(), z_frac_bad=(dz > TOL).mean(),
+                  loss_err=abs(loss - fwt["loss"]))
+            check((dz > TOL).mean() <= 1e-3 and dz.max() <= Z_DRIFT,
+                  "trajectory logits step %d: max error %g, %d samples > %g" % (step, dz.max(), (dz > TOL).sum(), TOL))
+            bound = 2 * FLIP * alpha + TOL
+            tbound = (step + 1) * 2 * FLIP * alpha + TOL
+            for key in P0:
+                tab = key in tab_moments
+                diff = np.abs(gp[key].astype(np.float64) - Pt[key])
+                bad = diff > TOL
+                frac = 1e-4 if step == 0 else (5e-4 if tab else 1e-3)
+                _stat("%s %s (step %d) trajectory" % (name, key, step), max_err=diff.max(), frac_bad=bad.mean())
+                check(bad.sum() <= max(1, frac * diff.size) and diff.max() <= (tbound if tab else bound),
+                      "trajectory %s step %d: %d elements off by > %g (max %g)" % (key, step, bad.sum(), TOL,
+                                                                                    diff.max()))
+                if not bad.any():
+                    continue
+                idx = np.flatnonzero(bad.reshape(-1))
+                rec = dict(n=len(idx))
+                if not tab:
+                    gabs = np.abs(Gt[key].reshape(-1)[idx].astype(np.float64))
+                    terms = _terms(key, idx, trace, fwt)
+                    rec.update(min_g_over_terms=(gabs / np.maximum(terms, 1e-300)).min(), max_abs_g=gabs.max())
+                _stat("%s %s (step %d) repaired" % (name, key, step), **rec)
+                # those elements take the GPU's value and moments; the rest is never re-synced
+                for arr, src in ((Pt[key], gp[key]), (opt_t.m[key], new_m[key]), (opt_t.v[key], new_v[key])):
+                    arr.reshape(-1)[idx] = np.asarray(src).reshape(-1)[idx]
+            del Gt, trace
+        gpu_p, gpu_m, gpu_v = gp, new_m, new_v
+        del Ps
+    assert not fails, "; ".join(fails[:8])
+    return eng
+
+
 def test_c2_deepfm_pipeline_full_size_trajectory(hip_lib):
     kw = dict(C=13, V=0, S=26, E=16, cate_index_size=N_CATE, hidden=HIDDEN)
     bs = [make_batch(B, cate_index_size=N_CATE, seed=100 + i) for i in range(STEPS)]
-    _run("c2", "deepfm_pipeline", kw, bs)
+    _run_fp32("c2", "deepfm_pipeline", kw, bs)
 
 
 def test_c3_deepfm_multi_cate_full_size_trajectory(hip_lib):
@@ -234,7 +364,7 @@ def test_c3_deepfm_multi_cate_full_size_trajectory(hip_lib):
     kw = dict(C=0, V=0, S=26, E=16, cate_index_size=N_CATE, hidden=HIDDEN, multi_ranges=ranges)
     bs = [make_batch(B, cont=0, cate_fields=26, cate_index_size=N_CATE, multi_slots=6, multi_width=60,
                      seed=200 + i, cate_only=True) for i in range(STEPS)]
-    _run("c3", "deepfm_multi_cate", kw, bs)
+    _run_fp32("c3", "deepfm_multi_cate", kw, bs)
 
 
 def test_c5_wdl_bf16_full_size_trajectory(hip_lib):
@@ -242,7 +372,7 @@ def test_c5_wdl_bf16_full_size_trajectory(hip_lib):
     test_gpu_parity.py::test_wdl_bf16_tower_tracks_oracle (logits 3e-2, loss 5e-3, AUC 2e-3)
     and the BF16_* parameter bounds above."""
     kw = dict(C=13, S=26, E=16, cate_index_size=N_CATE, hidden=HIDDEN, Fw=26)
-    bs = [make_batch(B, cate_index_size=N_CATE, seed=300 + i, wide_fields=26) for i in range(STEPS)]
+    bs = [make_batch(B, cate_index_size=N_CATE, seed=300 + i, wide_fields=26) for i in range(TRAJ_STEPS)]
     _run("c5", "wdl", kw, bs, tower="bf16", z_tol=3e-2, loss_tol=5e-3, auc_tol=2e-3)
 
 
@@ -282,7 +412,7 @@ def test_c4_sharded_100m_rows_equals_single_gpu(hip_lib):
         sh.w_head.copy_(one.w_head)
         sh.opt.copy_(one.opt)
         torch.cuda.synchronize()
-        bs = [make_batch(B, cate_index_size=n_cate, seed=400 + i) for i in range(STEPS)]
+        bs = [make_batch(B, cate_index_size=n_cate, seed=400 + i) for i in range(TRAJ_STEPS)]
         dev = [{k: torch.from_numpy(v).cuda() for k, v in b.items()} for b in bs]
         for step, b in enumerate(dev):
             one.train_step(b, graph=step >= 1)

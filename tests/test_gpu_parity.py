@@ -190,15 +190,23 @@ def test_flat_lookup_after_flush_bit_identical(hip_lib, name):
     ref_fm = e.fm_out[:128].cpu().numpy().copy()
     e.flush()
     assert e.since_flush == 0
-    got = e.predict(bs[5], logits=True)           # flat lookup
+    got = e.predict(bs[5], logits=True)           # flat lookup on the flushed planes
+    assert e.planes_step == e.steps
     np.testing.assert_array_equal(got, ref)
     np.testing.assert_array_equal(e.fm_out[:128].cpu().numpy(), ref_fm)
+    e.flat_planes = False                         # the record form of the flat lookup
+    e.planes_step = -1
+    np.testing.assert_array_equal(e.predict(bs[5], logits=True), ref)
+    np.testing.assert_array_equal(e.fm_out[:128].cpu().numpy(), ref_fm)
+    e.flat_planes = True
     e.train_step(bs[0])
     assert e.since_flush == 1
     np.testing.assert_array_equal(e.predict(bs[5], logits=True), e.predict(bs[5], logits=True))
-    # forced onto a table whose touched rows lag: the status word, then the host raise
+    # the record form of the flat lookup (without planes) forced onto a table whose touched
+    # rows lag: the status word, then the host raise
     e.train_step(bs[1])
     e.since_flush = 0
+    e.flat_planes = False
     with pytest.raises(_lib.DLError, match="lagged"):
         e.predict(bs[5])
 
