@@ -33,6 +33,30 @@
 #define DL_REC_FULL_LINES 1   // record updates also write the pad (see rec_write_pad)
 #endif
 
+// DL_REC_NT=1 (experiment): the once-touched streams of the gather and the backward — the
+// gather's record reads and moment-stash writes, the backward's stash reads and record writes —
+// as non-temporal accesses, so the random per-reference reads (dx0, fm_sum, g_pool rows) may
+// stay cached instead of being evicted by them.
+#ifndef DL_REC_NT
+#define DL_REC_NT 0
+#endif
+typedef float rec_f4v __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ float4 rec_ld4(const float* p) {
+#if DL_REC_NT
+  const rec_f4v x = __builtin_nontemporal_load(reinterpret_cast<const rec_f4v*>(p));
+  return make_float4(x[0], x[1], x[2], x[3]);
+#else
+  return *reinterpret_cast<const float4*>(p);
+#endif
+}
+__device__ __forceinline__ void rec_st4(float* p, float4 v) {
+#if DL_REC_NT
+  __builtin_nontemporal_store(rec_f4v{v.x, v.y, v.z, v.w}, reinterpret_cast<rec_f4v*>(p));
+#else
+  *reinterpret_cast<float4*>(p) = v;
+#endif
+}
+
 namespace dl {
 
 // ---------------------------------------------------------------------------
@@ -199,10 +223,10 @@ __global__ __launch_bounds__(256) void rec_gather_kernel(const float* __restrict
     int from = target;
     if (row >= 0 && row < n_rows) {
       const float* r = rec + row * c.ld;
-      p = *reinterpret_cast<const float4*>(r + 4 * q);
-      m = *reinterpret_cast<const float4*>(r + E + 4 + 4 * q);
-      v = *reinterpret_cast<const float4*>(r + 2 * E + 4 + 4 * q);
-      const float4 tail = *reinterpret_cast<const float4*>(r + E);
+      p = rec_ld4(r + 4 * q);
+      m = rec_ld4(r + E + 4 + 4 * q);
+      v = rec_ld4(r + 2 * E + 4 + 4 * q);
+      const float4 tail = rec_ld4(r + E);
       w = tail.x; wm = tail.y; wv = tail.z;
       const int stamp = __float_as_int(tail.w);
       if (stamp < target) from = catch_up_from(stamp, target, c);
@@ -273,9 +297,9 @@ __global__ __launch_bounds__(256) void rec_gather_kernel(const float* __restrict
     if (out1 && q == 0) out1[i] = w;
     if (mv) {   // caught-up moments for the backward's update: [m(E) | v(E) | m1 v1 0 0]
       float* o = mv + i * (2 * E + 4);
-      *reinterpret_cast<float4*>(o + 4 * q) = m;
-      *reinterpret_cast<float4*>(o + E + 4 * q) = v;
-      if (q == 0) *reinterpret_cast<float4*>(o + 2 * E) = make_float4(wm, wv, 0.f, 0.f);
+      rec_st4(o + 4 * q, m);
+      rec_st4(o + E + 4 * q, v);
+      if (q == 0) rec_st4(o + 2 * E, make_float4(wm, wv, 0.f, 0.f));
     }
   }
 }
@@ -395,7 +419,7 @@ __global__ __launch_bounds__(256) void pool_grad_kernel(dl_emb_layout L, dl_pool
 template <int E>
 __device__ __forceinline__ void rec_write_pad(float* __restrict__ r, int q, int ld) {
 #if DL_REC_FULL_LINES
-  for (int o = 3 * E + 4 + 4 * q; o < ld; o += E) *reinterpret_cast<float4*>(r + o) = make_float4(0.f, 0.f, 0.f, 0.f);
+  for (int o = 3 * E + 4 + 4 * q; o < ld; o += E) rec_st4(r + o, make_float4(0.f, 0.f, 0.f, 0.f));
 #endif
 }
 
@@ -408,10 +432,10 @@ __device__ __forceinline__ void rec_bwd_state(int64_t row, long long iu, int q, 
                                               const RecCfg& c, int t, const RingW& ring, float4& p, float4& m,
                                               float4& v, float& w, float& wm, float& wv) {
   if (STASH || mv) {
-    p = *reinterpret_cast<const float4*>(rows_u + iu * E + 4 * q);
+    p = rec_ld4(rows_u + iu * E + 4 * q);
     const float* o = mv + iu * (2 * E + 4);
-    m = *reinterpret_cast<const float4*>(o + 4 * q);
-    v = *reinterpret_cast<const float4*>(o + E + 4 * q);
+    m = rec_ld4(o + 4 * q);
+    v = rec_ld4(o + E + 4 * q);
     if (first) { w = rows_u1[iu]; wm = o[2 * E]; wv = o[2 * E + 1]; }
   } else if (!STASH && row_ok) {   // no stash: re-read the record and replay its catch-up
     const float* r = rec + row * c.ld;
@@ -450,12 +474,12 @@ __device__ __forceinline__ void rec_bwd_apply(const SegGrad4& s, int64_t row, in
   rec_adam(p.z, m.z, v.z, g.z, alpha, c);
   rec_adam(p.w, m.w, v.w, g.w, alpha, c);
   float* r = rec + row * c.ld;
-  *reinterpret_cast<float4*>(r + 4 * q) = p;
-  *reinterpret_cast<float4*>(r + E + 4 + 4 * q) = m;
-  *reinterpret_cast<float4*>(r + 2 * E + 4 + 4 * q) = v;
+  rec_st4(r + 4 * q, p);
+  rec_st4(r + E + 4 + 4 * q, m);
+  rec_st4(r + 2 * E + 4 + 4 * q, v);
   if (q == 0) {
     if (first) rec_adam(w, wm, wv, s.g1, alpha, c);
-    *reinterpret_cast<float4*>(r + E) = make_float4(w, wm, wv, __int_as_float(t));
+    rec_st4(r + E, make_float4(w, wm, wv, __int_as_float(t)));
   }
   rec_write_pad<E>(r, q, c.ld);
 }

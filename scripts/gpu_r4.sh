@@ -33,4 +33,22 @@ if [ "$MODE" = bench ]; then
   python scripts/bench_brief.py $OUT/bench_default.json
   exit 0
 fi
-echo "usage: gpu_r4.sh quick|full|bench TAG"; exit 2
+if [ "$MODE" = trace ]; then
+  # kernel timeline of the hipGraph steps (workload $3, default c2)
+  WL=${3:-c2}
+  timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d $OUT/trace_$WL -o trace -- \
+    python bench.py --no-extra --no-cpu-baseline --workload $WL --steps 10 --warmup 3 --age-steps 16 \
+    > $OUT/trace_$WL.log 2>&1
+  rc=$?; echo "trace rc=$rc"; [ $rc -eq 0 ] || { tail -5 $OUT/trace_$WL.log; exit $rc; }
+  f=$(ls $OUT/trace_$WL/*kernel_trace.csv 2>/dev/null | head -1)
+  [ -n "$f" ] || f=$(find $OUT/trace_$WL -name "*kernel_trace.csv" | head -1)
+  python scripts/step_timeline.py "$f" > $OUT/timeline_$WL.txt && head -40 $OUT/timeline_$WL.txt
+  exit 0
+fi
+if [ "$MODE" = combo ]; then
+  # quick, then an A/B of a library variant ($3) on C2 and C3
+  bash scripts/gpu_r4.sh quick $TAG || exit $?
+  bash scripts/gpu_ab_variant.sh ${TAG}_ab $3 "" "" "c2 c3"
+  exit $?
+fi
+echo "usage: gpu_r4.sh quick|full|bench|combo TAG [variant]"; exit 2
