@@ -69,6 +69,7 @@ SIGNATURES = {
     "dl_embed_cont_bwd": (I32, [LP, P, P, P, P, P, P, I32, P]),
     "dl_index_workspace_bytes": (I64, [I64]),
     "dl_index_build": (I32, [LP, P, I32, I32, P, I64, P, P, P, P, P, P, P, P, P]),
+    "dl_index_build_pair": (I32, [LP, P, LP, P, P, I64, P, P, P, P, P, P, P, P, P, P, P, P, P]),
     "dl_embed_bwd_sorted": (I32, [LP, P, P, P, P, P, P, I32, I64, P, P, P, P, P, P, P, I32, P]),
     "dl_pool_fwd": (I32, [LP, P, P, P, I32, P, P, I32, I32, P, P, P, P, P, P]),
     "dl_pool_fwd_indexed": (I32, [LP, P, P, P, I32, P, P, I32, I32, P, P, P, P, P]),

@@ -136,6 +136,86 @@ __device__ __forceinline__ void adam_elem_sparse(float& p, float& m, float& v, f
   p = p - adam_step_size(m, v, alpha, eps);
 }
 
+// ---------------------------------------------------------------------------
+// Embedding-table Adam state in the root form: the table keeps s = sqrt(v) in place of v
+// (records, the dense table sweep, the gather's moment stash; the host converts at the
+// boundary: adam_state() exports fl(s*s), set_adam_state() imports fl(sqrt(v))).
+//
+// Why: a row the batch does not touch takes g = 0 steps — every replayed catch-up step and
+// almost every element of the dense sweep.  With g = 0, v' = v * b2 exactly in real
+// arithmetic, so s' = s * sqrt(b2): the step needs one reciprocal instead of a square root and
+// a reciprocal (the two quarter-rate transcendentals bounded the lazy replay).  sqrt(b2) is
+// applied as a two-term product fma(s, c_hi, s * c_lo) (c_hi + c_lo = sqrt(b2) to ~2^-48),
+// so an idle row's s drifts by rounding only (random, ~0.5 ulp a step), not by a constant
+// ~0.4 ulp a step that a single rounded c would compound over long idle runs.
+// A g != 0 step forms v = s * s, applies TF's v update and takes s' = sqrt(v'): the same
+// operations as before plus one multiply.  TF parity: v differs from TF's by a few ulp, p by
+// a few ulp of its update — far inside the 1e-5 bar.  Lazy / dense bit-identity holds by
+// construction: every path applies this one function of (p, m, s, g), and g == 0 selects
+// the zero form wherever it arises (a replayed step, an untouched row of the sweep, a touched
+// row whose summed gradient is exactly 0).
+struct RootDecay {   // c_hi + c_lo = sqrt(b2)
+  float hi, lo;
+};
+__device__ __forceinline__ RootDecay root_decay(float b2) {
+  const double c = sqrt((double)b2);   // 1 - (1 - b2) == b2 exactly for b2 in [0.5, 1]
+  RootDecay r;
+  r.hi = (float)c;
+  r.lo = (float)(c - (double)r.hi);
+  return r;
+}
+
+__device__ __forceinline__ float root_step_size(float m, float s, float alpha, float eps) {
+#pragma clang fp contract(off)
+#if DL_ADAM_IEEE
+  return (m * alpha) / (s + eps);
+#else
+  return (m * alpha) * __builtin_amdgcn_rcpf(s + eps);
+#endif
+}
+
+__device__ __forceinline__ float root_sqrt(float v) {
+#if DL_ADAM_IEEE
+  return sqrtf(v);
+#else
+  return __builtin_amdgcn_sqrtf(v);
+#endif
+}
+
+// the g = 0 step of both forms' s
+__device__ __forceinline__ float root_decay_step(float s, RootDecay c) { return __builtin_fmaf(s, c.hi, s * c.lo); }
+
+// TF1 ApplyAdam (dense form, adam_elem) on the root state
+__device__ __forceinline__ void adam_elem_root(float& p, float& m, float& s, float g, float alpha, float omb1,
+                                               float omb2, RootDecay c, float eps) {
+#pragma clang fp contract(off)
+  if (g == 0.f) {
+    m = m + m * (-omb1);
+    s = root_decay_step(s, c);
+  } else {
+    m = m + (g - m) * omb1;
+    float v = s * s;
+    v = v + (g * g - v) * omb2;
+    s = root_sqrt(v);
+  }
+  p = p - root_step_size(m, s, alpha, eps);
+}
+
+// TF1 sparse-apply form (adam_elem_sparse) on the root state
+__device__ __forceinline__ void adam_elem_sparse_root(float& p, float& m, float& s, float g, float alpha, float b1,
+                                                      float b2, float omb1, float omb2, RootDecay c, float eps) {
+#pragma clang fp contract(off)
+  if (g == 0.f) {
+    m = m * b1;
+    s = root_decay_step(s, c);
+  } else {
+    m = m * b1 + g * omb1;
+    const float v = (s * s) * b2 + (g * g) * omb2;
+    s = root_sqrt(v);
+  }
+  p = p - root_step_size(m, s, alpha, eps);
+}
+
 #define DL_DISPATCH_E(E, ...)                    \
   switch (E) {                                   \
     case 4: { constexpr int kE = 4; __VA_ARGS__; break; }   \

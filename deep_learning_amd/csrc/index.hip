@@ -17,6 +17,7 @@
 // index build can run inside a captured hipGraph.
 #include "common.h"
 #include "rsort.h"
+#include <algorithm>
 
 namespace dl {
 
@@ -166,6 +167,39 @@ __global__ void owner_counts_kernel(int32_t* owner_counts, int n_owner, const in
   }
 }
 
+// dl_index_build_pair: the combined index (owner group 0 = the first id set, group 1 = the
+// second; owner_counts already turned into counts) split into the two sets' own index arrays:
+// the first set's stay in place as a prefix (its n_uniq becomes its own count; its segments,
+// inverse entries and sorted references are already right), the second set's are copied out
+// with its unique ids, reference numbers and segment offsets rebased to start at 0.
+__global__ __launch_bounds__(256) void index_split_kernel(const int32_t* __restrict__ counts, long long n1, long long n2,
+                                                          const uint32_t* __restrict__ uniq,
+                                                          const int32_t* __restrict__ seg_off,
+                                                          const int32_t* __restrict__ refs,
+                                                          const int32_t* __restrict__ inv, int32_t* __restrict__ n_uniq,
+                                                          uint32_t* __restrict__ uniq2, int32_t* __restrict__ seg2,
+                                                          int32_t* __restrict__ refs2, int32_t* __restrict__ n_uniq2,
+                                                          int32_t* __restrict__ inv2) {
+  const int nt = counts[0], nw = counts[1];
+  const int r0 = seg_off[nt];             // the second set's first sorted reference
+  const int nr = seg_off[nt + nw] - r0;   // its valid references
+  const long long span = max((long long)nw + 1, max((long long)nr, n2));
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < span;
+       i += (long long)gridDim.x * blockDim.x) {
+    if (i < nw) uniq2[i] = uniq[nt + i] & ((1u << kLocalBits) - 1);
+    if (i <= nw) seg2[i] = seg_off[nt + i] - r0;
+    if (i < nr) refs2[i] = refs[r0 + i] - (int32_t)n1;
+    if (i < n2) {
+      const int u = inv[n1 + i];
+      inv2[i] = u >= 0 ? u - nt : -1;
+    }
+  }
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    n_uniq[0] = nt;
+    n_uniq2[0] = nw;
+  }
+}
+
 static size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
 
 // workspace: the sort's, then the unique step's per-chunk head counts and the valid count
@@ -174,6 +208,7 @@ struct IndexWs {
   size_t sort_bytes;
   int32_t* chunk_cnt;
   int32_t* n_valid;
+  int32_t* pair_counts;   // dl_index_build_pair: the two id sets' unique counts
 };
 
 static IndexWs carve(void* ws, int64_t n) {
@@ -185,6 +220,7 @@ static IndexWs carve(void* ws, int64_t n) {
   w.chunk_cnt = reinterpret_cast<int32_t*>(p);
   p += align256((size_t)((n + kUqChunk - 1) / kUqChunk + 1) * 4);
   w.n_valid = reinterpret_cast<int32_t*>(p);
+  w.pair_counts = w.n_valid + 4;
   return w;
 }
 
@@ -294,6 +330,51 @@ extern "C" int dl_index_build(const dl_emb_layout* L, const int64_t* cate, int32
   if (owner_counts)
     hipLaunchKernelGGL(owner_counts_kernel, dim3(1), dim3(64), 0, s, owner_counts, world + 1, n_uniq);
   DL_RETURN_LAUNCH("dl_index_build");
+}
+
+extern "C" int dl_index_build_pair(const dl_emb_layout* L, const int64_t* cate, const dl_emb_layout* L2,
+                                   const int64_t* cate2, void* ws, int64_t ws_bytes, uint32_t* sorted_keys,
+                                   int32_t* sorted_refs, uint32_t* uniq_keys, int32_t* seg_off, int32_t* n_uniq,
+                                   int32_t* inv, uint32_t* uniq2, int32_t* sorted_refs2, int32_t* seg_off2,
+                                   int32_t* n_uniq2, int32_t* inv2, int32_t* err, void* stream) {
+  DL_CHECK_ARG(L && cate && L2 && cate2 && ws && sorted_keys && sorted_refs && uniq_keys && seg_off && n_uniq && inv &&
+                   uniq2 && sorted_refs2 && seg_off2 && n_uniq2 && inv2,
+               "NULL argument");
+  DL_CHECK_ARG(L->n_rows < (1LL << kLocalBits) && L2->n_rows < (1LL << kLocalBits), "too many rows for the 27-bit key");
+  const long long n1 = (long long)L->batch * index_slots(*L), n2 = (long long)L2->batch * index_slots(*L2);
+  DL_CHECK_ARG(n1 > 0 && n2 > 0 && n1 + n2 < (1LL << 30), "bad reference counts");
+  const int n = (int)(n1 + n2);
+  DL_CHECK_ARG(ws_bytes >= dl_index_workspace_bytes(n), "workspace too small");
+  hipStream_t s = as_stream(stream);
+  IndexWs w = carve(ws, n);
+  hipLaunchKernelGGL(index_init_kernel, dim3(1), dim3(64), 0, s, n_uniq, seg_off, w.pair_counts, 2);
+  // owner-major compressed keys: group 0 = [0, lrange), group 1 = [lrange, 2 lrange)
+  const uint32_t lrange = (uint32_t)std::max(L->n_rows, L2->n_rows);
+  int bits = 1;
+  while (bits < 32 && (1ull << bits) < 2ull * lrange) ++bits;
+  RsSource src{};
+  src.kind = 1;
+  src.L = *L;
+  src.cate = cate;
+  src.world = 1;
+  src.rep_below = 0;
+  src.err = err;
+  src.inv = inv;
+  src.n1 = n1;
+  src.L2 = *L2;
+  src.cate2 = cate2;
+  if (int rc = rsort_pairs(src, n, lrange, bits, w.sort, w.sort_bytes, sorted_keys, sorted_refs, w.n_valid, s)) {
+    set_error("dl_index_build_pair: radix sort failed (%d)", rc);
+    return 2;
+  }
+  unique_from_sorted(sorted_keys, sorted_refs, w.n_valid, n, 0xFFFFFFFFu, w.chunk_cnt, uniq_keys, seg_off, n_uniq, inv,
+                     w.pair_counts, s);
+  hipLaunchKernelGGL(owner_counts_kernel, dim3(1), dim3(64), 0, s, w.pair_counts, 2, n_uniq);
+  long long g = (std::max(n1, n2) + 255) / 256;
+  if (g > 4096) g = 4096;
+  hipLaunchKernelGGL(index_split_kernel, dim3((unsigned)g), dim3(256), 0, s, w.pair_counts, n1, n2, uniq_keys, seg_off,
+                     sorted_refs, inv, n_uniq, uniq2, seg_off2, sorted_refs2, n_uniq2, inv2);
+  DL_RETURN_LAUNCH("dl_index_build_pair");
 }
 
 extern "C" int dl_sort_unique(const int32_t* keys, int64_t n_keys, int32_t key_bits, void* ws, int64_t ws_bytes,

@@ -204,12 +204,19 @@ __global__ __launch_bounds__(256) void adam_dense_wave_kernel(float* __restrict_
 }
 
 // Table element update in the reference's form for the table: ApplyAdam (dense) or the
-// sparse-apply form of Variables read by embedding_lookup directly (common.h).
-template <bool SPARSE>
+// sparse-apply form of Variables read by embedding_lookup directly (common.h).  ROOT: the
+// embedding tables' root state (v holds s = sqrt(v): common.h adam_elem_root, the form the
+// lazy records replay); the wdl wide weights (fixed-point gradients) keep v.
+template <bool SPARSE, bool ROOT>
 __device__ __forceinline__ void table_adam(float& p, float& m, float& v, float g, float alpha, float b1, float b2,
-                                           float omb1, float omb2, float eps) {
-  if (SPARSE) adam_elem_sparse(p, m, v, g, alpha, b1, b2, omb1, omb2, eps);
-  else adam_elem(p, m, v, g, alpha, omb1, omb2, eps);
+                                           float omb1, float omb2, RootDecay rd, float eps) {
+  if (ROOT) {
+    if (SPARSE) adam_elem_sparse_root(p, m, v, g, alpha, b1, b2, omb1, omb2, rd, eps);
+    else adam_elem_root(p, m, v, g, alpha, omb1, omb2, rd, eps);
+  } else {
+    if (SPARSE) adam_elem_sparse(p, m, v, g, alpha, b1, b2, omb1, omb2, eps);
+    else adam_elem(p, m, v, g, alpha, omb1, omb2, eps);
+  }
 }
 
 // Embedding table rows of width W (multiple of 4): one thread per float4.
@@ -220,6 +227,7 @@ __global__ __launch_bounds__(256) void adam_rows4_kernel(float4* __restrict__ p,
                                                          int lpr, float l2, const float* __restrict__ opt,
                                                          float* __restrict__ sq_out) {
   const float alpha = opt[3], b1 = opt[4], b2 = opt[5], omb1 = 1.f - opt[4], omb2 = 1.f - opt[5], eps = opt[6];
+  const RootDecay rd = root_decay(b2);
   const bool skip = step_poisoned(opt);   // consume the gradients, apply nothing
   float sq = 0.f;
   for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n4;
@@ -234,10 +242,10 @@ __global__ __launch_bounds__(256) void adam_rows4_kernel(float4* __restrict__ p,
     if (skip) continue;
     if (l2 != 0.f) { gi.x += l2 * pi.x; gi.y += l2 * pi.y; gi.z += l2 * pi.z; gi.w += l2 * pi.w; }
     if (sq_out) sq += pi.x * pi.x + pi.y * pi.y + pi.z * pi.z + pi.w * pi.w;
-    table_adam<SPARSE>(pi.x, mi.x, vi.x, gi.x, alpha, b1, b2, omb1, omb2, eps);
-    table_adam<SPARSE>(pi.y, mi.y, vi.y, gi.y, alpha, b1, b2, omb1, omb2, eps);
-    table_adam<SPARSE>(pi.z, mi.z, vi.z, gi.z, alpha, b1, b2, omb1, omb2, eps);
-    table_adam<SPARSE>(pi.w, mi.w, vi.w, gi.w, alpha, b1, b2, omb1, omb2, eps);
+    table_adam<SPARSE, true>(pi.x, mi.x, vi.x, gi.x, alpha, b1, b2, omb1, omb2, rd, eps);
+    table_adam<SPARSE, true>(pi.y, mi.y, vi.y, gi.y, alpha, b1, b2, omb1, omb2, rd, eps);
+    table_adam<SPARSE, true>(pi.z, mi.z, vi.z, gi.z, alpha, b1, b2, omb1, omb2, rd, eps);
+    table_adam<SPARSE, true>(pi.w, mi.w, vi.w, gi.w, alpha, b1, b2, omb1, omb2, rd, eps);
     p[i] = pi; m[i] = mi; v[i] = vi;
   }
   if (sq_out) block_atomic_add(sq, sq_out);
@@ -251,6 +259,7 @@ __global__ __launch_bounds__(256) void adam_rows1_kernel(float* __restrict__ p, 
                                                          float l2, int clear, const float* __restrict__ opt,
                                                          float* __restrict__ sq_out) {
   const float alpha = opt[3], b1 = opt[4], b2 = opt[5], omb1 = 1.f - opt[4], omb2 = 1.f - opt[5], eps = opt[6];
+  const RootDecay rd = root_decay(b2);
   const bool skip = step_poisoned(opt);
   const long long n4 = n / 4;
   float sq = 0.f;
@@ -279,10 +288,10 @@ __global__ __launch_bounds__(256) void adam_rows1_kernel(float* __restrict__ p, 
       // the L2 term as one fma (wide.hip's lazy replay uses the same expression: bit-identical)
       if (l2 != 0.f) { gi.x = fmaf(l2, pi.x, gi.x); gi.y = fmaf(l2, pi.y, gi.y); gi.z = fmaf(l2, pi.z, gi.z); gi.w = fmaf(l2, pi.w, gi.w); }
       sq += pi.x * pi.x + pi.y * pi.y + pi.z * pi.z + pi.w * pi.w;
-      table_adam<SPARSE>(pi.x, mi.x, vi.x, gi.x, alpha, b1, b2, omb1, omb2, eps);
-      table_adam<SPARSE>(pi.y, mi.y, vi.y, gi.y, alpha, b1, b2, omb1, omb2, eps);
-      table_adam<SPARSE>(pi.z, mi.z, vi.z, gi.z, alpha, b1, b2, omb1, omb2, eps);
-      table_adam<SPARSE>(pi.w, mi.w, vi.w, gi.w, alpha, b1, b2, omb1, omb2, eps);
+      table_adam<SPARSE, !FIXED>(pi.x, mi.x, vi.x, gi.x, alpha, b1, b2, omb1, omb2, rd, eps);
+      table_adam<SPARSE, !FIXED>(pi.y, mi.y, vi.y, gi.y, alpha, b1, b2, omb1, omb2, rd, eps);
+      table_adam<SPARSE, !FIXED>(pi.z, mi.z, vi.z, gi.z, alpha, b1, b2, omb1, omb2, rd, eps);
+      table_adam<SPARSE, !FIXED>(pi.w, mi.w, vi.w, gi.w, alpha, b1, b2, omb1, omb2, rd, eps);
       reinterpret_cast<float4*>(p)[i] = pi; reinterpret_cast<float4*>(m)[i] = mi;
       reinterpret_cast<float4*>(v)[i] = vi;
     } else {
@@ -302,7 +311,7 @@ __global__ __launch_bounds__(256) void adam_rows1_kernel(float* __restrict__ p, 
         float pi = p[r], mi = m[r], vi = v[r];
         if (l2 != 0.f) gi = fmaf(l2, pi, gi);
         sq += pi * pi;
-        table_adam<SPARSE>(pi, mi, vi, gi, alpha, b1, b2, omb1, omb2, eps);
+        table_adam<SPARSE, !FIXED>(pi, mi, vi, gi, alpha, b1, b2, omb1, omb2, rd, eps);
         p[r] = pi; m[r] = mi; v[r] = vi;
       }
     }

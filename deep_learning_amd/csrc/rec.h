@@ -10,6 +10,7 @@ struct RecCfg {
   int E, ld, has_first, hist_mask;
   int sparse;                          // TF's sparse-apply Adam form (DL_REC_SPARSE_ADAM)
   float b1, b2, omb1, omb2, eps;       // filled on the device from opt (rec_load_hyper)
+  RootDecay rd;                        // sqrt(b2) for the root state's zero steps (common.h)
   int* status;                         // opt's status word (lag overflow is reported there)
 };
 
@@ -30,13 +31,15 @@ __device__ __forceinline__ void rec_load_hyper(RecCfg& c, const float* opt) {
   c.omb1 = 1.f - opt[4];
   c.omb2 = 1.f - opt[5];
   c.eps = opt[6];
+  c.rd = root_decay(opt[5]);
   c.status = opt_status(opt);
 }
 
-// The table's TF1 Adam element update in the form the reference applies to it.
+// The table's TF1 Adam element update in the form the reference applies to it, on the root
+// state (s = sqrt(v): common.h adam_elem_root).  `v` below is that s throughout.
 __device__ __forceinline__ void rec_adam(float& p, float& m, float& v, float g, float alpha, const RecCfg& c) {
-  if (c.sparse) adam_elem_sparse(p, m, v, g, alpha, c.b1, c.b2, c.omb1, c.omb2, c.eps);
-  else adam_elem(p, m, v, g, alpha, c.omb1, c.omb2, c.eps);
+  if (c.sparse) adam_elem_sparse_root(p, m, v, g, alpha, c.b1, c.b2, c.omb1, c.omb2, c.rd, c.eps);
+  else adam_elem_root(p, m, v, g, alpha, c.omb1, c.omb2, c.rd, c.eps);
 }
 
 // A row lagging more steps than the alpha ring holds cannot be caught up exactly: the host
@@ -106,32 +109,46 @@ __device__ __forceinline__ void catch_up1_loop(float& p, float& m, float& v, flo
   }
 }
 
-// One zero-gradient step of the catch-up replay.  Bitwise the same as rec_adam(..., g = 0, ...):
-// with g = 0 the dense form's (g - m) * omb1 is (-m) * omb1 = m * (-omb1) exactly (0 - m and -m
-// differ only at m = +0, where both products are zeros that m + . maps to the same +0), and
-// the sparse form's g * omb1 is the constant 0 * omb1, hoisted (Zero0).
+// One zero-gradient step of the catch-up replay: rec_adam(..., g = 0, ...) written out (the
+// g == 0 branch of adam_elem_root / adam_elem_sparse_root), with its constants hoisted.
 struct Zero0 {   // per-launch constants of the zero-gradient step
-  float b1, b2, nomb1, nomb2, z1, z2, eps;
+  float b1, nomb1, eps;
+  RootDecay rd;
   __device__ __forceinline__ explicit Zero0(const RecCfg& c) {
-#pragma clang fp contract(off)
-    b1 = c.b1; b2 = c.b2; nomb1 = -c.omb1; nomb2 = -c.omb2; eps = c.eps;
-    const float g = 0.f;
-    z1 = g * c.omb1;
-    z2 = (g * g) * c.omb2;
+    b1 = c.b1; nomb1 = -c.omb1; eps = c.eps; rd = c.rd;
   }
 };
 
 template <bool SPARSE>
-__device__ __forceinline__ void rec_adam0_x1(float& p, float& m, float& v, float alpha, const Zero0& k) {
+__device__ __forceinline__ void rec_adam0_x1(float& p, float& m, float& s, float alpha, const Zero0& k) {
 #pragma clang fp contract(off)
-  if (SPARSE) {
-    m = m * k.b1 + k.z1;
-    v = v * k.b2 + k.z2;
-  } else {
-    m = m + m * k.nomb1;
-    v = v + v * k.nomb2;
-  }
-  p = p - adam_step_size(m, v, alpha, k.eps);
+  if (SPARSE) m = m * k.b1;
+  else m = m + m * k.nomb1;
+  s = root_decay_step(s, k.rd);
+  p = p - root_step_size(m, s, alpha, k.eps);
+}
+
+// Two elements of one row stepped together: the same float operations per half as
+// rec_adam0_x1 (the packed multiplies, fmas and adds round each half exactly as the scalar
+// ones do), so the halves stay bit-identical to the dense sweep; the packed form issues the
+// decays, the alpha product and the update once for both elements.
+typedef float rec_f2v __attribute__((ext_vector_type(2)));
+template <bool SPARSE>
+__device__ __forceinline__ void rec_adam0_x2(rec_f2v& p, rec_f2v& m, rec_f2v& s, float alpha, const Zero0& k) {
+#pragma clang fp contract(off)
+#if DL_ADAM_IEEE
+  rec_adam0_x1<SPARSE>(p.x, m.x, s.x, alpha, k);
+  rec_adam0_x1<SPARSE>(p.y, m.y, s.y, alpha, k);
+#else
+  if (SPARSE) m = m * k.b1;
+  else m = m + m * k.nomb1;
+  s = __builtin_elementwise_fma(s, rec_f2v{k.rd.hi, k.rd.hi}, s * k.rd.lo);
+  const rec_f2v d = s + k.eps;
+  rec_f2v r;
+  r.x = __builtin_amdgcn_rcpf(d.x);
+  r.y = __builtin_amdgcn_rcpf(d.y);
+  p = p - (m * alpha) * r;
+#endif
 }
 
 // LDS-only reads of the alpha window

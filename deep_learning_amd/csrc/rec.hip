@@ -18,10 +18,11 @@
 //
 // Row record (rec_ld floats, rec_ld % 32 == 0 so a record starts a 128-B line):
 //   [0, E)        p                   (the embedding row)
-//   E .. E+2      w1, m(w1), v(w1)    (FM first-order weight of the row, if any)
+//   E .. E+2      w1, m(w1), s(w1)    (FM first-order weight of the row, if any)
 //   E+3           stamp               (int32 bits: last step applied to the row)
 //   [E+4, 2E+4)   m
-//   [2E+4, 3E+4)  v
+//   [2E+4, 3E+4)  s = sqrt(v)         (the root state, common.h adam_elem_root: a replayed
+//                                      zero-gradient step costs one reciprocal)
 // p and w1 share the first 128-B line: the forward's useful bytes sit together,
 // and one record is two lines for E = 16.
 #include "common.h"
@@ -74,8 +75,10 @@ namespace dl {
 // dealt to the 64 lanes in descending-lag order, snake-wise (round i: chains 64i..64i+63,
 // reversed on odd rounds): lanes that took a long chain take short ones after it.  Each
 // chain is the same sequence of rec_adam calls as before, so the results are unchanged.
-#ifndef DL_GATHER_REPLAY   // 1: rank-dealt units, wave-uniform step loop; 0: per-lane chains (round-2 v1)
-#define DL_GATHER_REPLAY 1
+// 2: rank-dealt element pairs, wave-uniform step loop; 1: the same with single elements
+// (round 3); 0: per-lane chains (round-2 v1)
+#ifndef DL_GATHER_REPLAY
+#define DL_GATHER_REPLAY 2
 #endif
 
 // The replay loop of rec_gather_kernel's staged rows: one wave-uniform loop over the steps
@@ -120,6 +123,63 @@ __device__ __forceinline__ void replay_elems(float* st, const int* from_s, const
     float P = x[0], M = x[s1], V = x[2 * s1];
     replay_steps<SPARSE>(P, M, V, mine, top, target, ring, z, alv);
     if (k < T) { x[0] = P; x[s1] = M; x[2 * s1] = V; }
+  }
+}
+
+// The paired form: a unit is two adjacent elements of a row (same lag, one rec_adam0_x2 chain)
+// or the row's first-order triple (its second half idle: zeros in, nothing written back).
+// E / 2 + 1 units per row instead of E + 1: half the rounds, and the packed decay / update.
+template <bool SPARSE>
+__device__ __forceinline__ void replay_steps2(rec_f2v& p, rec_f2v& m, rec_f2v& v, int mine, int top, int target,
+                                              const RingW& ring, const Zero0& z, float alv) {
+  int k = top;
+  for (; k > 64; --k) {
+    const float al = ring(target - k + 1);
+    if (mine >= k) rec_adam0_x2<SPARSE>(p, m, v, al, z);
+  }
+  for (; k >= 1; --k) {
+    const float al = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(alv), k - 1));
+    if (mine >= k) rec_adam0_x2<SPARSE>(p, m, v, al, z);
+  }
+}
+
+template <int E, bool SPARSE>
+__device__ __forceinline__ void replay_pairs(float* st, const int* from_s, const int* order, int pitch, int target,
+                                             int has_first, const RingW& ring, const RecCfg& c, float alv) {
+  constexpr int LPR = E / 4, RPW = 64 / LPR, NP = E / 2;
+  const int lane = threadIdx.x & 63;
+  const Zero0 z(c);
+  const int nu = NP + has_first;
+  const int T = RPW * nu;
+  for (int r0 = 0; r0 < T; r0 += 64) {
+    const int top = __builtin_amdgcn_readfirstlane(target - from_s[order[r0 / nu]]);
+    if (top <= 0) break;                             // rank order: every later round is caught up too
+    const int k = r0 + lane;
+    const int r = order[min(k, T - 1) / nu], e = k % nu;
+    float* sr = st + r * pitch;
+    const int mine = k < T ? target - from_s[r] : 0;
+    rec_f2v P, M, V;
+    if (e < NP) {
+      float* x = sr + 2 * e;
+      P = rec_f2v{x[0], x[1]};
+      M = rec_f2v{x[E], x[E + 1]};
+      V = rec_f2v{x[2 * E], x[2 * E + 1]};
+    } else {
+      float* x = sr + 3 * E;
+      P = rec_f2v{x[0], 0.f};
+      M = rec_f2v{x[1], 0.f};
+      V = rec_f2v{x[2], 0.f};
+    }
+    replay_steps2<SPARSE>(P, M, V, mine, top, target, ring, z, alv);
+    if (k < T) {
+      if (e < NP) {
+        float* x = sr + 2 * e;
+        x[0] = P.x; x[1] = P.y; x[E] = M.x; x[E + 1] = M.y; x[2 * E] = V.x; x[2 * E + 1] = V.y;
+      } else {
+        float* x = sr + 3 * E;
+        x[0] = P.x; x[1] = M.x; x[2] = V.x;
+      }
+    }
   }
 }
 
@@ -252,7 +312,9 @@ __global__ __launch_bounds__(256) void rec_gather_kernel(const float* __restrict
       }
       __builtin_amdgcn_s_waitcnt(0xc07f);           // lgkmcnt(0): this wave's LDS writes landed
       __builtin_amdgcn_wave_barrier();
-#if DL_GATHER_REPLAY
+#if DL_GATHER_REPLAY == 2
+      replay_pairs<E, SPARSE>(st, from_s, order, PITCH, target, c.has_first, ring, c, alv);
+#elif DL_GATHER_REPLAY
       replay_elems<E, SPARSE>(st, from_s, order, PITCH, target, nch, ring, c, alv);
 #else
       for (int k0 = 0; k0 < T; k0 += 64) {

@@ -21,6 +21,12 @@ struct RsSource {
   int world, rep_below;
   int32_t* err;
   int32_t* inv;
+  // kind 1 with n1 > 0 (dl_index_build_pair): references e >= n1 are a second id set — the
+  // references of (L2, cate2) numbered from n1, keyed (1 << 27) | row in owner group 1 (the
+  // first set keeps owner 0: world must be 1)
+  long long n1;
+  dl_emb_layout L2;
+  const int64_t* cate2;
 };
 
 // Bytes of workspace rsort_pairs needs for n pairs (16-B aligned pieces).

@@ -76,22 +76,35 @@ __device__ __forceinline__ bool rs_get(const RsSource& src, const RsPass& p, lon
     key = p.kin[ec];
     return in && key != kRsNoKey;
   }
-  const dl_emb_layout& L = src.L;
-  const int S = L.cate_fields, ns = index_slots(L), mb = index_multi_base(L);
+  // the pair build's second id set: its layout's fields selected one by one (a selected
+  // reference to a whole kernel-argument struct would be copied to scratch)
+  const bool second = src.n1 > 0 && ec >= src.n1;
+  const dl_emb_layout& L1 = src.L;
+  const dl_emb_layout& L2 = src.L2;
+  const int64_t* __restrict__ cate = second ? src.cate2 : src.cate;
+  const int S = second ? L2.cate_fields : L1.cate_fields;
+  const int use_fm = second ? L2.use_fm : L1.use_fm;
+  const int ns = second ? index_slots(L2) : index_slots(L1);
+  const int mb = second ? index_multi_base(L2) : index_multi_base(L1);
+  const int cate_ld = second ? L2.cate_ld : L1.cate_ld;
+  const int64_t n_rows = second ? L2.n_rows : L1.n_rows;
+  const bool zero_row0 = second ? L2.zero_row0 : L1.zero_row0;
   // 32-bit division (a reference index is an int32): the 64-bit one is a long subroutine,
   // and this runs per element in both the upsweep and the downsweep
-  const uint32_t ecu = (uint32_t)ec, b = ecu / (uint32_t)ns;
+  const uint32_t ecu = (uint32_t)(second ? ec - src.n1 : ec), b = ecu / (uint32_t)ns;
   const int s = (int)(ecu - b * (uint32_t)ns);
-  const int col = (L.use_fm && s < S) ? s : s < mb ? (L.use_fm ? s - S : s) : S + (s - mb);
-  const int64_t off = (L.use_fm && s < S) ? L.fm_cate_offset : L.deep_cate_offset;
-  const int64_t row = src.cate[(long long)b * L.cate_ld + col] + off;
-  const bool range_ok = row >= 0 && row < L.n_rows;
+  const int col = (use_fm && s < S) ? s : s < mb ? (use_fm ? s - S : s) : S + (s - mb);
+  const int64_t off = (use_fm && s < S) ? (second ? L2.fm_cate_offset : L1.fm_cate_offset)
+                                        : (second ? L2.deep_cate_offset : L1.deep_cate_offset);
+  const int64_t row = cate[(long long)b * cate_ld + col] + off;
+  const bool range_ok = row >= 0 && row < n_rows;
   if (in && !range_ok && flag_err && src.err) atomicOr(src.err, 1);
   const int w = src.world;
   const uint32_t r32 = (uint32_t)row;
   const uint32_t qw = w == 1 ? r32 : r32 / (uint32_t)w;   // w is uniform: one rank divides by nothing
-  key = row < src.rep_below ? (((uint32_t)w << kLocal) | r32) : (((r32 - qw * (uint32_t)w) << kLocal) | qw);
-  return in && range_ok && !(row == 0 && L.zero_row0);
+  key = second ? ((1u << kLocal) | r32)
+               : row < src.rep_below ? (((uint32_t)w << kLocal) | r32) : (((r32 - qw * (uint32_t)w) << kLocal) | qw);
+  return in && range_ok && !(row == 0 && zero_row0);
 }
 
 // The batch references' keys, one streaming pass (MODE 3's input): the first sort pass then

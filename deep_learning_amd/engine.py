@@ -207,6 +207,17 @@ class ModelSpec:
         return np.concatenate([cat, pool, cont, vec])
 
 
+
+def _root_to_v(s):
+    """Device root state s = sqrt(v) (a tensor) -> TF's v, fl(s * s), as host numpy."""
+    a = s.cpu().numpy().astype(np.float64)
+    return (a * a).astype(np.float32)
+
+
+def _v_to_root(v):
+    """TF's v (array-like) -> the root state fl(sqrt(v)), host numpy f32."""
+    return np.sqrt(np.ascontiguousarray(v, np.float64)).astype(np.float32)
+
 class CTREngine:
     def __init__(self, spec, max_batch, device="cuda", seed=2019, init="device", bwd="atomic",
                  table_rows=None, adam="dense", hist_len=4096, rec_stash=True, fwd_rec=False, gemm="s3",
@@ -419,15 +430,24 @@ class CTREngine:
         self.bwd = bwd
         self.n_slot = (S if sp.fm else 0) + S + (sp.multi_width if self.lazy else 0)
         self.n_refs = B * self.n_slot
+        # wide_lazy: the table ids and the wide ids in ONE index build (dl_index_build_pair): the
+        # table's index arrays hold both sets' sorted references and unique rows, the wide set's
+        # own arrays (widx_*) are split out of them.  DLAMD_INDEX_PAIR=0: two builds.
+        self.index_pair = bool(getattr(self, "wide_lazy", False) and bwd == "sorted"
+                               and os.environ.get("DLAMD_INDEX_PAIR", "1") != "0")
         if bwd == "sorted":
-            wsb = _lib.lib().dl_index_workspace_bytes(max(1, self.n_refs))
+            cap = self.n_refs + (B * sp.Fw if self.index_pair else 0)
+            wsb = _lib.lib().dl_index_workspace_bytes(max(1, cap))
             self.idx_ws = z(wsb, dt=torch.uint8)
-            self.idx_keys = z(self.n_refs, dt=torch.int32)
-            self.idx_refs = z(self.n_refs, dt=torch.int32)
-            self.idx_uniq = z(self.n_refs, dt=torch.int32)
-            self.idx_off = z(self.n_refs + 1, dt=torch.int32)
+            self.idx_keys = z(cap, dt=torch.int32)
+            self.idx_refs = z(cap, dt=torch.int32)
+            self.idx_uniq = z(cap, dt=torch.int32)
+            self.idx_off = z(cap + 1, dt=torch.int32)
             self.idx_n = z(4, dt=torch.int32)
-            self.idx_inv = z(self.n_refs, dt=torch.int32) if self.lazy else None
+            self.idx_inv = z(cap, dt=torch.int32) if self.lazy else None
+            if self.index_pair:   # the second build's workspace and key array are not needed
+                self.widx_ws = z(256, dt=torch.uint8)
+                self.widx_keys = z(1, dt=torch.int32)
         if self.lazy:
             self.rows_u = z(self.n_rep + self.n_refs, E)
             self.rows_u1 = z(self.n_rep + self.n_refs)
@@ -750,36 +770,40 @@ class CTREngine:
         self.since_flush = 0
 
     def adam_state(self):
-        """Table Adam state in the dense layout (tests): dict of m, v (+ m1, v1) as numpy."""
+        """Table Adam state in the dense layout (tests, checkpoints): dict of m, v (+ m1, v1) as
+        numpy.  The device keeps the root state s = sqrt(v) (csrc/common.h adam_elem_root);
+        v is exported as fl(s * s)."""
         E, N = self.spec.E, self.N
         if not self.lazy:
-            d = {"m": self.tm[:N].cpu().numpy(), "v": self.tv[:N].cpu().numpy()}
+            d = {"m": self.tm[:N].cpu().numpy(), "v": _root_to_v(self.tv[:N])}
             if self.first is not None:
-                d["m1"], d["v1"] = self.fmm[:N].cpu().numpy(), self.fmv[:N].cpu().numpy()
+                d["m1"], d["v1"] = self.fmm[:N].cpu().numpy(), _root_to_v(self.fmv[:N])
             return d
         self.flush()
         r = self.rec[:N]
-        d = {"m": r[:, E + 4: 2 * E + 4].cpu().numpy(), "v": r[:, 2 * E + 4: 3 * E + 4].cpu().numpy()}
+        d = {"m": r[:, E + 4: 2 * E + 4].cpu().numpy(), "v": _root_to_v(r[:, 2 * E + 4: 3 * E + 4])}
         if self.spec.fm:
-            d["m1"], d["v1"] = r[:, E + 1].cpu().numpy(), r[:, E + 2].cpu().numpy()
+            d["m1"], d["v1"] = r[:, E + 1].cpu().numpy(), _root_to_v(r[:, E + 2])
         return d
 
     def set_adam_state(self, d):
-        """Inverse of adam_state(); for records, stamps the rows with the current step."""
+        """Inverse of adam_state() (v imported as s = fl(sqrt(v))); for records, stamps the rows
+        with the current step."""
         E, N = self.spec.E, self.N
         t = lambda k: torch.from_numpy(np.ascontiguousarray(d[k], np.float32)).to(self.dev)
+        s = lambda k: torch.from_numpy(_v_to_root(d[k])).to(self.dev)
         if not self.lazy:
             self.tm[:N].copy_(t("m"))
-            self.tv[:N].copy_(t("v"))
+            self.tv[:N].copy_(s("v"))
             if self.first is not None and "m1" in d:
                 self.fmm[:N].copy_(t("m1"))
-                self.fmv[:N].copy_(t("v1"))
+                self.fmv[:N].copy_(s("v1"))
             return
         self.rec[:N, E + 4: 2 * E + 4].copy_(t("m"))
-        self.rec[:N, 2 * E + 4: 3 * E + 4].copy_(t("v"))
+        self.rec[:N, 2 * E + 4: 3 * E + 4].copy_(s("v"))
         if self.spec.fm and "m1" in d:
             self.rec[:N, E + 1].copy_(t("m1"))
-            self.rec[:N, E + 2].copy_(t("v1"))
+            self.rec[:N, E + 2].copy_(s("v1"))
         self.rec.view(torch.int32)[:, E + 3] = int(self.opt[7].item())
         self.since_flush = 0
         self.planes_step = -1
@@ -963,6 +987,15 @@ class CTREngine:
         self._c("validate", "dl_validate_batch", C_ref(L), ptr(cate), ptr(wide), sp.Fw if wide is not None else 0,
                 self.in_wide.shape[1], getattr(self, "w_rows", 0), 1, ptr(self.err), s)
         if self.bwd != "sorted":
+            return
+        if self.index_pair:
+            WL = self.wlayout
+            WL.batch = B
+            self._c("index_build", "dl_index_build_pair", C_ref(L), ptr(self.in_cate), C_ref(WL), ptr(self.in_wide),
+                    ptr(self.idx_ws), self.idx_ws.numel(), ptr(self.idx_keys), ptr(self.idx_refs),
+                    ptr(self.idx_uniq), ptr(self.idx_off), ptr(self.idx_n), ptr(self.idx_inv), ptr(self.widx_uniq),
+                    ptr(self.widx_refs), ptr(self.widx_off), ptr(self.widx_n), ptr(self.winv), ptr(self.err), s)
+            call("dl_wide_local_ids", ptr(self.winv), B * sp.Fw, sp.Fw + sp.hidden[-1], ptr(self.in_wide_loc), s)
             return
         # single GPU: keys are the rows themselves (replicated rows need no owner group;
         # the record kernels recognise them by row < n_rep) — the narrowest sort range

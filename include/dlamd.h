@@ -174,6 +174,20 @@ int dl_index_build(const dl_emb_layout* L, const int64_t* cate, int32_t world,
                    int32_t replicated_below, void* ws, int64_t ws_bytes, uint32_t* sorted_keys,
                    int32_t* sorted_refs, uint32_t* uniq_keys, int32_t* seg_off, int32_t* n_uniq,
                    int32_t* inv, int32_t* owner_counts, int32_t* err, void* stream);
+/* Two id sets indexed by ONE sort (single GPU, world 1): the table references of (L, cate) and
+ * a second set (L2, cate2: the wdl wide ids, wdl.py:44-47 / :132 read wdl_weights through
+ * embedding_lookup) keyed into owner groups 0 and 1 of one radix sort + segmented unique —
+ * one launch sequence over n1 + n2 references in place of two builds over n1 and n2.
+ * Outputs are exactly dl_index_build(L, cate, 1, 0, ...)'s for the first set (uniq_keys,
+ * seg_off, n_uniq, inv; sorted_refs within its segments) and dl_index_build(L2, cate2, ...)'s
+ * for the second (uniq2, seg_off2, n_uniq2, inv2, sorted_refs2), references numbered per set.
+ * sorted_keys / sorted_refs / inv / uniq_keys / seg_off hold n1 + n2 (+1) entries; the second
+ * set's arrays n2 (+1).  Workspace: dl_index_workspace_bytes(n1 + n2). */
+int dl_index_build_pair(const dl_emb_layout* L, const int64_t* cate, const dl_emb_layout* L2,
+                        const int64_t* cate2, void* ws, int64_t ws_bytes, uint32_t* sorted_keys,
+                        int32_t* sorted_refs, uint32_t* uniq_keys, int32_t* seg_off, int32_t* n_uniq,
+                        int32_t* inv, uint32_t* uniq2, int32_t* sorted_refs2, int32_t* seg_off2,
+                        int32_t* n_uniq2, int32_t* inv2, int32_t* err, void* stream);
 /* Generic form for the sharded owners: sort n non-negative int32 keys (< 2^key_bits) with
  * their positions, dedup: uniq_keys [n_uniq], seg_off [n_uniq+1] into sorted_pos, and
  * inv[i] = unique id of keys[i] (may be NULL).  Workspace: dl_index_workspace_bytes(n). */
@@ -433,7 +447,12 @@ int dl_adam_dense_reg(float* p, float* m, float* v, const float* slab, int32_t n
  * gradient is densified by the row-0 concat, deepfm_pipeline.py:83-86).
  * width = E (table) or 1 (first-order).  DL_ROWS_GRAD_FIXED (width 1): g is int64 fixed
  * point in units of 1/DL_WIDE_GRAD_SCALE (the wdl wide-weight gradient of
- * dl_wdl_head_fwd_bwd / dl_slab_fold_rows). */
+ * dl_wdl_head_fwd_bwd / dl_slab_fold_rows).
+ * State form: `v` holds the ROOT state s = sqrt(v) for the embedding tables (every call
+ * without DL_ROWS_GRAD_FIXED) — the form the row records keep, so the g = 0 step is
+ * s' = s*sqrt(b2) (one reciprocal, no square root); a g != 0 step forms v = s*s, applies
+ * the update above and stores sqrt(v').  With DL_ROWS_GRAD_FIXED (the wdl wide weights)
+ * `v` is TF's v.  Callers convert at the boundary (engine.py adam_state / set_adam_state). */
 #define DL_ROWS_CLEAR_TOUCHED 1
 #define DL_ROWS_SPARSE_ADAM 2
 #define DL_ROWS_GRAD_FIXED 4
@@ -447,8 +466,8 @@ int dl_adam_rows(float* p, float* m, float* v, void* g, uint8_t* touched, int64_
  * dense sweep of dl_adam_rows (bit-identical: the skipped zero-gradient steps
  * are replayed with the same float operations when a row is next read), but a
  * step only touches the rows its batch references.  Record of rec_ld floats
- * (rec_ld >= 3E+4, multiple of 32): [p(E) | w1 m1 v1 stamp | m(E) | v(E) | pad];
- * stamp = int32 bits of the last step applied.  hist = ring of hist_len (power
+ * (rec_ld >= 3E+4, multiple of 32): [p(E) | w1 m1 s1 stamp | m(E) | s(E) | pad],
+ * s = sqrt(v) (the root state of dl_adam_rows); stamp = int32 bits of the last step applied.  hist = ring of hist_len (power
  * of two) per-step alphas; the caller keeps every row's lag < hist_len by
  * calling dl_rec_flush at least once per hist_len steps.
  * Replaces, for the table and first-order Variables, the dense ApplyAdam of
@@ -465,7 +484,7 @@ int dl_adam_hist_record(const float* opt, float* hist, int32_t hist_len, void* s
  * L->fm_cont_offset + i for i < n_rep (the replicated FM cont-field rows) else the row of uniq_keys[i-n_rep] (batch index,
  * dl_index_build keys; n_uniq = NULL: max_uniq keys, e.g. an owner's received local
  * rows with world = 1).  Records are only read.  mv_u (may be NULL) receives the
- * caught-up moments [i][2E+4] = m(E) | v(E) | m1 v1 0 0 for dl_rec_bwd_adam.
+ * caught-up moments [i][2E+4] = m(E) | s(E) | m1 s1 0 0 for dl_rec_bwd_adam.
  * lag = 1 inside a training step, 0 for predict. */
 int dl_rec_gather(const dl_emb_layout* L, const float* rec, int32_t rec_ld, int32_t rec_flags,
                   int32_t n_rep, const uint32_t* uniq_keys, const int32_t* n_uniq, int64_t max_uniq,

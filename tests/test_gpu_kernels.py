@@ -418,6 +418,59 @@ def test_index_build_matches_numpy(hip_lib):
     np.testing.assert_array_equal(oc.cpu().numpy(), np.bincount(own_u, minlength=world + 1))
 
 
+@pytest.mark.parametrize("B", [300, 2048])
+def test_index_build_pair_equals_two_builds(hip_lib, B):
+    """dl_index_build_pair (the wdl table ids and wide ids in one sort, index.hip) against
+    dl_index_build run once per id set: unique rows, counts, segment offsets, the sorted
+    references inside every segment and both inverse maps bit-identical — row-0 references
+    (dropped when the layout's zero-row rule applies), repeated ids and wide ids on the
+    deep-output rows included."""
+    import ctypes
+    from deep_learning_amd.engine import CTREngine, ModelSpec
+    from deep_learning_amd.synthetic import make_batch
+    Fw, H = 26, 32
+    spec = ModelSpec("wdl", C=13, S=26, E=16, cate_index_size=8000, hidden=[64, H], Fw=Fw)
+    eng = CTREngine(spec, max_batch=B, init="none", adam="lazy")
+    assert eng.index_pair
+    b = make_batch(B, cate_index_size=8000, wide_fields=Fw, seed=B)
+    b["cate_feats"][0, :4] = [0, 0, 5, 5]
+    b["wide_feats"][1, :3] = [Fw, Fw + H - 1, Fw]
+    eng.stage(b)
+    eng._pre(B)
+    torch.cuda.synchronize()
+    nt, nw = int(eng.idx_n[0].item()), int(eng.widx_n[0].item())
+    got = dict(u=eng.idx_uniq[:nt].cpu().numpy(), off=eng.idx_off[:nt + 1].cpu().numpy(),
+               inv=eng.idx_inv[:eng.n_refs].cpu().numpy(), refs=eng.idx_refs.cpu().numpy(),
+               wu=eng.widx_uniq[:nw].cpu().numpy(), woff=eng.widx_off[:nw + 1].cpu().numpy(),
+               winv=eng.winv[:B * Fw].cpu().numpy(), wrefs=eng.widx_refs.cpu().numpy())
+
+    def one(L, cate, n):
+        ws = torch.zeros(hip_lib.dl_index_workspace_bytes(n), dtype=torch.uint8, device="cuda")
+        t = [torch.zeros(n + 1, dtype=torch.int32, device="cuda") for _ in range(6)]
+        call("dl_index_build", ctypes.byref(L), ptr(cate), 1, 0, ptr(ws), ws.numel(), ptr(t[0]), ptr(t[1]), ptr(t[2]),
+             ptr(t[3]), ptr(t[4]), ptr(t[5]), None, ptr(eng.err), _s())
+        torch.cuda.synchronize()
+        k = int(t[4][0].item())
+        return k, t[2][:k].cpu().numpy(), t[3][:k + 1].cpu().numpy(), t[5][:n].cpu().numpy(), t[1].cpu().numpy()
+
+    L = eng.layout
+    L.batch = B
+    k1, u1, off1, inv1, refs1 = one(L, eng.in_cate, eng.n_refs)
+    WL = eng.wlayout
+    WL.batch = B
+    k2, u2, off2, inv2, refs2 = one(WL, eng.in_wide, B * Fw)
+    assert (nt, nw) == (k1, k2)
+    same = np.testing.assert_array_equal
+    same(got["u"], u1)
+    same(got["off"], off1)
+    same(got["inv"], inv1)
+    same(got["refs"][:off1[-1]], refs1[:off1[-1]])
+    same(got["wu"], u2)
+    same(got["woff"], off2)
+    same(got["winv"], inv2)
+    same(got["wrefs"][:off2[-1]], refs2[:off2[-1]])
+
+
 @pytest.mark.parametrize("model", ["deepfm_pipeline", "dnn_pipeline"])
 def test_sorted_backward_equals_atomic(hip_lib, model):
     from deep_learning_amd.engine import CTREngine, ModelSpec
@@ -787,16 +840,20 @@ def test_adam_rows_width1_sweep(hip_lib, n, flags):
     torch.cuda.synchronize()
     g = (g_eff + l2 * p).astype(np.float32)
     omb1, omb2 = np.float32(1) - b1, np.float32(1) - b2
+    # first-order tables keep the root state s = sqrt(v) (common.h adam_elem_root): the input
+    # array is s, the output is s'; the wide weights (fixed-point form) keep v
+    v_in = v if fixed else (v * v).astype(np.float32)
     if flags & _lib.ROWS_SPARSE_ADAM:
         m1 = (m * b1 + g * omb1).astype(np.float32)
-        v1 = (v * b2 + (g * g) * omb2).astype(np.float32)
+        v1 = (v_in * b2 + (g * g) * omb2).astype(np.float32)
     else:
         m1 = (m + (g - m) * omb1).astype(np.float32)
-        v1 = (v + (g * g - v) * omb2).astype(np.float32)
+        v1 = (v_in + (g * g - v_in) * omb2).astype(np.float32)
     p1 = (p - (m1 * alpha) / (np.sqrt(v1) + eps)).astype(np.float32)
     # g + l2*p may contract to an fma on the device: m, v within f32 rounding, not bit-equal
     np.testing.assert_allclose(md.cpu().numpy(), m1, rtol=2e-6, atol=2e-9)
-    np.testing.assert_allclose(vd.cpu().numpy(), v1, rtol=2e-6, atol=2e-11)
+    v_out = vd.cpu().numpy().astype(np.float64)
+    np.testing.assert_allclose(v_out if fixed else v_out * v_out, v1, rtol=4e-6, atol=2e-11)
     np.testing.assert_allclose(pd.cpu().numpy(), p1, rtol=1e-6, atol=1e-7)
     assert int(td.sum()) == 0
     assert not torch.any(g_d != 0)
