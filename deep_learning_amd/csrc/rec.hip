@@ -535,6 +535,10 @@ __device__ __forceinline__ void rec_bwd_apply(const SegGrad4& s, int64_t row, in
   rec_adam(p.y, m.y, v.y, g.y, alpha, c);
   rec_adam(p.z, m.z, v.z, g.z, alpha, c);
   rec_adam(p.w, m.w, v.w, g.w, alpha, c);
+  if (DL_BWD_DIAG & 8) {   // diagnostics: no record writes (one lane keeps the result live)
+    if (p.x == 1234.5f) rec[q] = p.y + m.x + v.x;
+    return;
+  }
   float* r = rec + row * c.ld;
   rec_st4(r + 4 * q, p);
   rec_st4(r + E + 4 + 4 * q, m);

@@ -8,6 +8,14 @@
 // deep references (:120) contribute the dx0 columns of their slot.  Lane d of an
 // E-lane group owns dim d.
 #pragma once
+
+// Diagnostics builds only (wrong results): DL_BWD_DIAG bits redirect one of the backward's
+// access streams to a cache-resident address, so PMC bytes and time split by stream —
+// 1: the dx0 slices, 2: the fm_sum rows (segment_grad4_range), 4: the stash rows,
+// 8: the record writes (rec.hip rec_bwd_state / rec_bwd_apply).
+#ifndef DL_BWD_DIAG
+#define DL_BWD_DIAG 0
+#endif
 #include "common.h"
 
 namespace dl {
@@ -154,7 +162,7 @@ __device__ __forceinline__ SegGrad4 segment_grad4_range(const SegGradIn& a, int 
       if (a.g1_pool) r.g1 += a.g1_pool[bm * a.g1_stride];
     } else if (L.use_fm && sl < S) {
       const float dzb = a.dz[b];
-      const float4 fs = *reinterpret_cast<const float4*>(a.fm_sum + (long long)b * E + 4 * q);
+      const float4 fs = *reinterpret_cast<const float4*>(a.fm_sum + (long long)((DL_BWD_DIAG & 2) ? 0 : b) * E + 4 * q);
       const float4 ds = make_float4(dzb * wsec.x, dzb * wsec.y, dzb * wsec.z, dzb * wsec.w);
       r.s.x = fmaf(ds.x, fs.x, r.s.x); r.s.y = fmaf(ds.y, fs.y, r.s.y);
       r.s.z = fmaf(ds.z, fs.z, r.s.z); r.s.w = fmaf(ds.w, fs.w, r.s.w);
@@ -162,7 +170,8 @@ __device__ __forceinline__ SegGrad4 segment_grad4_range(const SegGradIn& a, int 
       r.g1 = fmaf(dzb, a.w_head[Cf + sl], r.g1);
     } else {
       const int f = L.use_fm ? sl - S : sl;
-      const float4 gx = *reinterpret_cast<const float4*>(a.dx0 + (long long)b * L.dx0_ld + L.dx0_cat_col + f * E + 4 * q);
+      const float4 gx = *reinterpret_cast<const float4*>(a.dx0 + (long long)((DL_BWD_DIAG & 1) ? 0 : b) * L.dx0_ld +
+                                                         L.dx0_cat_col + f * E + 4 * q);
       r.x.x += gx.x; r.x.y += gx.y; r.x.z += gx.z; r.x.w += gx.w;
     }
   }

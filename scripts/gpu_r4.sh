@@ -10,7 +10,7 @@ OUT=gpurun_out/$TAG
 mkdir -p $OUT
 export TMPDIR=/tmp
 if [ "$MODE" = quick ]; then
-  timeout -k 10 600 python -u -m pytest tests -m gpu -x -q -rf -p no:cacheprovider --timeout 300 --timeout-method thread \
+  timeout -k 10 600 python -u -m pytest tests -m gpu --maxfail=8 -q -rf -p no:cacheprovider --timeout 300 --timeout-method thread \
     --deselect tests/test_gpu_fullsize.py --durations=10 > $OUT/pytest_quick.log 2>&1
   rc=$?; echo "pytest rc=$rc"; tail -15 $OUT/pytest_quick.log; [ $rc -eq 0 ] || exit $rc
   timeout -k 10 300 python bench.py --workload c3 --no-extra --no-cpu-baseline --steps 10 > $OUT/c3.json 2> $OUT/c3.err
@@ -51,4 +51,22 @@ if [ "$MODE" = combo ]; then
   bash scripts/gpu_ab_variant.sh ${TAG}_ab $3 "" "" "c2 c3"
   exit $?
 fi
-echo "usage: gpu_r4.sh quick|full|bench|combo TAG [variant]"; exit 2
+if [ "$MODE" = bwddiag ]; then
+  # the backward's excess line fetches split by access stream: C2 FETCH_SIZE / WRITE_SIZE passes
+  # for the default build and the DL_BWD_DIAG builds (d1: dx0 slices, d2: fm_sum rows, d8: no
+  # record writes — each redirected to a cache-resident address; wrong results, bytes only)
+  for V in new d1 d2 d8; do
+    W=$OUT/bwd_$V; mkdir -p $W
+    if [ $V = new ]; then VV=""; else VV=$V; fi
+    args="--no-cpu-baseline --no-extra --workload c2"
+    DLAMD_VARIANT=$VV timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $W/prof_fetch -o fetch -- \
+      python bench.py --steps 3 --warmup 1 $args > $W/prof_fetch.log 2>&1
+    rc=$?; echo "$V fetch rc=$rc"; [ $rc -eq 0 ] || exit $rc
+    DLAMD_VARIANT=$VV timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $W/prof_write -o write -- \
+      python bench.py --steps 3 --warmup 1 $args > $W/prof_write.log 2>&1
+    rc=$?; echo "$V write rc=$rc"; [ $rc -eq 0 ] || exit $rc
+    python scripts/pmc_summary.py $W $W/pmc_summary.json c2 > $W/summary.txt && grep -i "bwd\|gather" $W/summary.txt | head -6
+  done
+  exit 0
+fi
+echo "usage: gpu_r4.sh quick|full|bench|trace|combo|bwddiag TAG [variant]"; exit 2

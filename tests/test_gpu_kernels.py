@@ -817,6 +817,8 @@ def test_adam_rows_width1_sweep(hip_lib, n, flags):
     v = (rng.random(n) * 1e-3).astype(np.float32)
     touched = (rng.random(n) < 0.3).astype(np.uint8)
     fixed = bool(flags & _lib.ROWS_GRAD_FIXED)
+    if not fixed:   # the first-order tables' root state s = sqrt(v) (common.h adam_elem_root)
+        v = np.sqrt(v.astype(np.float64)).astype(np.float32)
     # the gradient table's invariant: zero outside the touched rows
     gf = np.where(touched == 1, rng.standard_normal(n) * 1e-2, 0).astype(np.float32)
     if fixed:
