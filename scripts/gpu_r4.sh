@@ -51,6 +51,14 @@ if [ "$MODE" = combo ]; then
   bash scripts/gpu_ab_variant.sh ${TAG}_ab $3 "" "" "c2 c3"
   exit $?
 fi
+if [ "$MODE" = perf ]; then
+  # step timelines of C2 and C5, then the replay A/B (paired vs single-element units)
+  bash scripts/gpu_r4.sh trace $TAG c2 || exit $?
+  bash scripts/gpu_r4.sh trace $TAG c5 || exit $?
+  bash scripts/gpu_ab_variant.sh ${TAG}_rp rp1 "" "" "c2 c5" || exit $?
+  bash scripts/gpu_ab_variant.sh ${TAG}_nt nt "" "" "c2 c3"
+  exit $?
+fi
 if [ "$MODE" = bwddiag ]; then
   # the backward's excess line fetches split by access stream: C2 FETCH_SIZE / WRITE_SIZE passes
   # for the default build and the DL_BWD_DIAG builds (d1: dx0 slices, d2: fm_sum rows, d8: no
