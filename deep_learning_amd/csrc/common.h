@@ -154,6 +154,11 @@ __device__ __forceinline__ void adam_elem_sparse(float& p, float& m, float& v, f
 // construction: every path applies this one function of (p, m, s, g), and g == 0 selects
 // the zero form wherever it arises (a replayed step, an untouched row of the sweep, a touched
 // row whose summed gradient is exactly 0).
+// DL_ROOT_STATE=0 (A/B builds only: the host's adam_state conversions assume the root form)
+// keeps TF's v in the tables as before.
+#ifndef DL_ROOT_STATE
+#define DL_ROOT_STATE 1
+#endif
 struct RootDecay {   // c_hi + c_lo = sqrt(b2)
   float hi, lo;
 };

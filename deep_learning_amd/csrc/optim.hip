@@ -210,7 +210,7 @@ __global__ __launch_bounds__(256) void adam_dense_wave_kernel(float* __restrict_
 template <bool SPARSE, bool ROOT>
 __device__ __forceinline__ void table_adam(float& p, float& m, float& v, float g, float alpha, float b1, float b2,
                                            float omb1, float omb2, RootDecay rd, float eps) {
-  if (ROOT) {
+  if (ROOT && DL_ROOT_STATE) {
     if (SPARSE) adam_elem_sparse_root(p, m, v, g, alpha, b1, b2, omb1, omb2, rd, eps);
     else adam_elem_root(p, m, v, g, alpha, omb1, omb2, rd, eps);
   } else {

@@ -38,8 +38,13 @@ __device__ __forceinline__ void rec_load_hyper(RecCfg& c, const float* opt) {
 // The table's TF1 Adam element update in the form the reference applies to it, on the root
 // state (s = sqrt(v): common.h adam_elem_root).  `v` below is that s throughout.
 __device__ __forceinline__ void rec_adam(float& p, float& m, float& v, float g, float alpha, const RecCfg& c) {
+#if DL_ROOT_STATE
   if (c.sparse) adam_elem_sparse_root(p, m, v, g, alpha, c.b1, c.b2, c.omb1, c.omb2, c.rd, c.eps);
   else adam_elem_root(p, m, v, g, alpha, c.omb1, c.omb2, c.rd, c.eps);
+#else
+  if (c.sparse) adam_elem_sparse(p, m, v, g, alpha, c.b1, c.b2, c.omb1, c.omb2, c.eps);
+  else adam_elem(p, m, v, g, alpha, c.omb1, c.omb2, c.eps);
+#endif
 }
 
 // A row lagging more steps than the alpha ring holds cannot be caught up exactly: the host
@@ -114,18 +119,35 @@ __device__ __forceinline__ void catch_up1_loop(float& p, float& m, float& v, flo
 struct Zero0 {   // per-launch constants of the zero-gradient step
   float b1, nomb1, eps;
   RootDecay rd;
+  float b2, nomb2, z1, z2;   // the v form (DL_ROOT_STATE=0)
   __device__ __forceinline__ explicit Zero0(const RecCfg& c) {
+#pragma clang fp contract(off)
     b1 = c.b1; nomb1 = -c.omb1; eps = c.eps; rd = c.rd;
+    b2 = c.b2; nomb2 = -c.omb2;
+    const float g = 0.f;
+    z1 = g * c.omb1;
+    z2 = (g * g) * c.omb2;
   }
 };
 
 template <bool SPARSE>
 __device__ __forceinline__ void rec_adam0_x1(float& p, float& m, float& s, float alpha, const Zero0& k) {
 #pragma clang fp contract(off)
+#if DL_ROOT_STATE
   if (SPARSE) m = m * k.b1;
   else m = m + m * k.nomb1;
   s = root_decay_step(s, k.rd);
   p = p - root_step_size(m, s, alpha, k.eps);
+#else   // s is TF's v here: the round-3 zero step
+  if (SPARSE) {
+    m = m * k.b1 + k.z1;
+    s = s * k.b2 + k.z2;
+  } else {
+    m = m + m * k.nomb1;
+    s = s + s * k.nomb2;
+  }
+  p = p - adam_step_size(m, s, alpha, k.eps);
+#endif
 }
 
 // Two elements of one row stepped together: the same float operations per half as
@@ -136,7 +158,7 @@ typedef float rec_f2v __attribute__((ext_vector_type(2)));
 template <bool SPARSE>
 __device__ __forceinline__ void rec_adam0_x2(rec_f2v& p, rec_f2v& m, rec_f2v& s, float alpha, const Zero0& k) {
 #pragma clang fp contract(off)
-#if DL_ADAM_IEEE
+#if DL_ADAM_IEEE || !DL_ROOT_STATE
   rec_adam0_x1<SPARSE>(p.x, m.x, s.x, alpha, k);
   rec_adam0_x1<SPARSE>(p.y, m.y, s.y, alpha, k);
 #else

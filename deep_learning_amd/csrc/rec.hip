@@ -34,29 +34,11 @@
 #define DL_REC_FULL_LINES 1   // record updates also write the pad (see rec_write_pad)
 #endif
 
-// DL_REC_NT=1 (experiment): the once-touched streams of the gather and the backward — the
-// gather's record reads and moment-stash writes, the backward's stash reads and record writes —
-// as non-temporal accesses, so the random per-reference reads (dx0, fm_sum, g_pool rows) may
-// stay cached instead of being evicted by them.
-#ifndef DL_REC_NT
-#define DL_REC_NT 0
-#endif
-typedef float rec_f4v __attribute__((ext_vector_type(4)));
-__device__ __forceinline__ float4 rec_ld4(const float* p) {
-#if DL_REC_NT
-  const rec_f4v x = __builtin_nontemporal_load(reinterpret_cast<const rec_f4v*>(p));
-  return make_float4(x[0], x[1], x[2], x[3]);
-#else
-  return *reinterpret_cast<const float4*>(p);
-#endif
-}
-__device__ __forceinline__ void rec_st4(float* p, float4 v) {
-#if DL_REC_NT
-  __builtin_nontemporal_store(rec_f4v{v.x, v.y, v.z, v.w}, reinterpret_cast<rec_f4v*>(p));
-#else
-  *reinterpret_cast<float4*>(p) = v;
-#endif
-}
+// The record / stash streams' float4 accesses (round 4 tried them non-temporal, so the random
+// per-reference reads might stay cached: gather 328 -> 410 us, backward 439 -> 723 us at C2,
+// profiles/r04f_nt/ — removed).
+__device__ __forceinline__ float4 rec_ld4(const float* p) { return *reinterpret_cast<const float4*>(p); }
+__device__ __forceinline__ void rec_st4(float* p, float4 v) { *reinterpret_cast<float4*>(p) = v; }
 
 namespace dl {
 
@@ -75,10 +57,10 @@ namespace dl {
 // dealt to the 64 lanes in descending-lag order, snake-wise (round i: chains 64i..64i+63,
 // reversed on odd rounds): lanes that took a long chain take short ones after it.  Each
 // chain is the same sequence of rec_adam calls as before, so the results are unchanged.
-// 2: rank-dealt element pairs, wave-uniform step loop; 1: the same with single elements
-// (round 3); 0: per-lane chains (round-2 v1)
+// 1: rank-dealt single elements, wave-uniform step loop; 2: the same with element pairs
+// (packed math; measured no faster: profiles/r04f_rp/); 0: per-lane chains (round-2 v1)
 #ifndef DL_GATHER_REPLAY
-#define DL_GATHER_REPLAY 2
+#define DL_GATHER_REPLAY 1
 #endif
 
 // The replay loop of rec_gather_kernel's staged rows: one wave-uniform loop over the steps

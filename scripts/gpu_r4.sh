@@ -59,6 +59,12 @@ if [ "$MODE" = perf ]; then
   bash scripts/gpu_ab_variant.sh ${TAG}_nt nt "" "" "c2 c3"
   exit $?
 fi
+if [ "$MODE" = abdiag ]; then
+  # the root Adam state against TF's v (libdlamd_vst), then the backward's byte split
+  bash scripts/gpu_ab_variant.sh ${TAG}_vst vst "" "" "c2 c5" || exit $?
+  bash scripts/gpu_r4.sh bwddiag $TAG
+  exit $?
+fi
 if [ "$MODE" = bwddiag ]; then
   # the backward's excess line fetches split by access stream: C2 FETCH_SIZE / WRITE_SIZE passes
   # for the default build and the DL_BWD_DIAG builds (d1: dx0 slices, d2: fm_sum rows, d8: no
