@@ -354,10 +354,13 @@ def run_workload(wl, args, world, rank, sharded, steps, warmup, age, ksteps, bar
                     make_batch(B, seed=1000 * rank + i, dist=args.dist, **kw).items()} for i in range(nb)]
     torch.cuda.synchronize()
 
+    depth = getattr(eng, "pf_depth", 1)
+
     def step(i, graph=use_graph, pf=prefetch):
-        # the batch after step i is prefetched during it (each step still builds exactly one
-        # index: the last timed step builds the one after the timed region)
-        eng.train_step(batches[i % nb], graph=graph, **({"next_batch": batches[(i + 1) % nb]} if pf else {}))
+        # the batches after step i are prefetched during it (pf_depth of them in flight; each
+        # step still builds exactly one index: the last timed step builds one after the region)
+        ahead = [batches[(i + j) % nb] for j in range(1, depth + 1)]
+        eng.train_step(batches[i % nb], graph=graph, **({"next_batch": ahead if depth > 1 else ahead[0]} if pf else {}))
 
     # table age: untimed steps before the warmup, so the rows the timed steps reference carry
     # the steady-state lag of lazy Adam (the zero-gradient steps a row replays when next
@@ -377,8 +380,12 @@ def run_workload(wl, args, world, rank, sharded, steps, warmup, age, ksteps, bar
     barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
+    w0 = getattr(eng, "host_wait", 0.0)
     for i in range(base, base + steps):
         step(i)
+    # the host's own submission time per step (the time train_step spent waiting for the GPU to
+    # catch up excluded): close to ms_per_step would mean the host, not the GPU, sets the pace
+    host_ms = (time.perf_counter() - t0 - (getattr(eng, "host_wait", 0.0) - w0)) / steps * 1e3
     torch.cuda.synchronize()
     barrier()
     dt = time.perf_counter() - t0
@@ -476,7 +483,7 @@ def run_workload(wl, args, world, rank, sharded, steps, warmup, age, ksteps, bar
             if gather is not None:
                 gather["lookup_alone"] = gather_lookup
     out = dict(spec=spec, value=value, ms=ms, loss=loss, roofline=roof, gather=gather, flush=flush, kernels=kernels,
-               kernel_sum=sum(k["us"] for k in kernels.values()), nb=nb, gemm_peak=gemm_peak)
+               kernel_sum=sum(k["us"] for k in kernels.values()), nb=nb, gemm_peak=gemm_peak, host_ms=host_ms)
     del eng, batches
     torch.cuda.synchronize()
     torch.cuda.empty_cache()
@@ -629,6 +636,7 @@ def main():
                      "ms_per_step": round(e["ms"], 4), "samples_per_s": round(e["value"], 1),
                      "steps": args.extra_steps, "roofline": e["roofline"], "gather_north_star": e["gather"],
                      "kernel_sum_us_per_step": round(e["kernel_sum"], 1), "loss": round(e["loss"], 6),
+                     "host_submit_ms_per_step": round(e["host_ms"], 4),
                      "kernels": e["kernels"]}
     if "c5" in extra and "error" not in extra["c5"] and world == 1:
         try:
@@ -680,6 +688,7 @@ def main():
             "gemm_peak_tflops": round(r["gemm_peak"], 1),
             "kernels": r["kernels"],
             "kernel_sum_us_per_step": round(r["kernel_sum"], 1),
+            "host_submit_ms_per_step": round(r["host_ms"], 4),
             "loss": round(r["loss"], 6),
             "extra_workloads": extra or None,
         }

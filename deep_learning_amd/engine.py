@@ -23,6 +23,7 @@ import contextlib
 import gc
 import math
 import os
+import time
 
 import numpy as np
 import torch
@@ -347,6 +348,8 @@ class CTREngine:
             WL.zero_row0 = 0
             self.wlayout = WL
         self.err = z(4, dt=torch.int32)       # the batch's id-validation word (per buffer set)
+        # batches prefetched ahead (train_step(next_batch=[...])): buffer sets = pf_depth + 1
+        self.pf_depth = int(os.environ.get("DLAMD_PF_DEPTH", "1")) if type(self) is CTREngine else 1
         # running loss of a training loop (dl_loss_accumulate, every step inside its graph):
         # [sum of data terms, sum of regulariser terms, steps]
         self.loss_acc = z(4, dt=torch.float64)
@@ -355,6 +358,7 @@ class CTREngine:
         self.rows_sparse = _lib.ROWS_SPARSE_ADAM if sp.sparse_table else 0
         self._status_q = []
         self._status_host = None
+        self.host_wait = 0.0
         # ---- activations / workspaces
         B = max_batch
         self.x0 = z(B, self.in_ld[0])
@@ -1202,21 +1206,24 @@ class CTREngine:
         if getattr(self, "_slots", None) is not None:
             return
         a = {n: getattr(self, n) for n in self.SLOT_ATTRS if getattr(self, n, None) is not None}
-        self._slots = [a, {n: torch.zeros_like(t) for n, t in a.items()}]
+        depth = max(1, getattr(self, "pf_depth", 1))
+        self._slots = [a] + [{n: torch.zeros_like(t) for n, t in a.items()} for _ in range(depth)]
         self._cur = 0
-        self._slot_free = [None, None]    # event: the compute stream is done with a set
-        self._pf = None                   # (set, B, ready event, batch) of a prefetched batch
+        self._slot_free = [None] * len(self._slots)   # event: the compute stream is done with a set
+        self._pfq = []                    # pending prefetches, oldest first: (set, B, ready event, batch)
+        self._pf = None                   # the oldest pending prefetch (_pfq[0])
 
     def prefetch(self, batch, graph=False):
-        """Stage `batch` and build its index into the idle buffer set on the side stream;
-        train_step(batch) then starts from it.  Issued before the current step's work, so
-        the index build (memory bound) overlaps that step's GEMMs.  graph=True replays the
-        index build as a captured hipGraph (one per buffer set and batch size)."""
+        """Stage `batch` and build its index into an idle buffer set on the side stream;
+        train_step(batch) then starts from it.  Up to pf_depth batches may be pending (buffer
+        sets: pf_depth + 1), consumed in order.  graph=True replays the index build as a
+        captured hipGraph (one per buffer set and batch size)."""
         self._enable_slots()
-        if self._pf is not None:
-            torch.cuda.current_stream().wait_event(self._pf[2])
+        if any(p[3] is batch for p in self._pfq) or len(self._pfq) >= len(self._slots) - 1:
+            return
         cur = self._cur
-        k = 1 - cur
+        used = {cur} | {p[0] for p in self._pfq}
+        k = next(i for i in range(len(self._slots)) if i not in used)
         side = self._side_stream()
         if self._slot_free[k] is not None:
             side.wait_event(self._slot_free[k])
@@ -1238,19 +1245,24 @@ class CTREngine:
                 ev.record(side)
         finally:
             self._use_slot(cur)
-        self._pf = (k, B, ev, batch)
+        self._pfq.append((k, B, ev, batch))
+        self._pf = self._pfq[0]
 
     def _begin(self, batch):
-        """Buffers of this step's batch: the prefetched set if `batch` is the one prefetched,
-        else staged and indexed now on the compute stream."""
-        pf = getattr(self, "_pf", None)
-        if pf is not None and batch is not None and batch is pf[3]:
-            self._pf = None
-            self._use_slot(pf[0])
-            torch.cuda.current_stream().wait_event(pf[2])
-            return pf[1], True
-        if pf is not None:      # a different batch came: drop the prefetch (after it lands)
-            torch.cuda.current_stream().wait_event(pf[2])
+        """Buffers of this step's batch: the prefetched set if `batch` is the oldest one
+        prefetched, else (every pending prefetch dropped once it lands) staged and indexed now
+        on the compute stream."""
+        q = getattr(self, "_pfq", None) or []
+        if q and batch is not None and batch is q[0][3]:
+            k, B, ev, _ = q.pop(0)
+            self._pf = q[0] if q else None
+            self._use_slot(k)
+            torch.cuda.current_stream().wait_event(ev)
+            return B, True
+        for p in q:      # other batches came: drop the prefetches (after they land)
+            torch.cuda.current_stream().wait_event(p[2])
+        if q:
+            q.clear()
             self._pf = None
         return (self.stage(batch) if batch is not None else self.B), False
 
@@ -1272,8 +1284,14 @@ class CTREngine:
             self.since_flush += 1
         if not indexed and not graph:
             self._pre(B)
-        if next_batch is not None:
-            self.prefetch(next_batch, graph=graph)
+        # next_batch: the batch after this one, or a list of the next ones (up to pf_depth are
+        # kept in flight); prefetched before this step's graph is submitted, or after it
+        # (DLAMD_PF_AFTER=1)
+        ahead = [] if next_batch is None else list(next_batch) if isinstance(next_batch, (list, tuple)) else [next_batch]
+        pf_after = os.environ.get("DLAMD_PF_AFTER", "0") == "1"
+        if not pf_after:
+            for nb in ahead:
+                self.prefetch(nb, graph=graph)
         if graph:
             # one graph per (buffer set, batch size, index built inside or prefetched)
             key = (getattr(self, "_cur", 0), B, not indexed)
@@ -1284,6 +1302,9 @@ class CTREngine:
         else:
             self._train(B)
         self._release()
+        if pf_after:
+            for nb in ahead:
+                self.prefetch(nb, graph=graph)
         self._queue_status()
         self.steps += 1
         self.last_batch = B
@@ -1402,7 +1423,9 @@ class CTREngine:
         while self._status_q:
             k0, e0 = self._status_q[0]
             if len(self._status_q) > 2:
+                t0 = time.perf_counter()
                 e0.synchronize()
+                self.host_wait += time.perf_counter() - t0   # bench.py: host time spent ahead of the GPU
             elif not e0.query():
                 break
             self._status_q.pop(0)

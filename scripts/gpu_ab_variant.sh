@@ -18,6 +18,6 @@ for wl in $5; do
     env $E timeout -k 10 300 python bench.py --no-cpu-baseline --no-extra --workload $wl --steps 20 --warmup 5 > $OUT/bench_${wl}_$arm.json 2> $OUT/bench_${wl}_$arm.err || { tail -5 $OUT/bench_${wl}_$arm.err; exit 1; }
     python -c "
 import json;d=json.loads(open('$OUT/bench_${wl}_$arm.json').read().strip().splitlines()[-1]);k=d['kernels']
-print('$wl $arm', d['ms_per_step'], {n: k[n]['us'] for n in k if k[n]['us'] >= 30})"
+print('$wl $arm', d['ms_per_step'], 'host', d.get('host_submit_ms_per_step'), {n: k[n]['us'] for n in k if k[n]['us'] >= 30})"
   done
 done

@@ -59,6 +59,38 @@ if [ "$MODE" = perf ]; then
   bash scripts/gpu_ab_variant.sh ${TAG}_nt nt "" "" "c2 c3"
   exit $?
 fi
+if [ "$MODE" = pfdepth ]; then
+  # prefetch depth (batches in flight on the side stream) x submission order, then a C5 trace
+  timeout -k 10 300 python -u -m pytest tests/test_gpu_parity.py -m gpu -q -rf -k prefetch -p no:cacheprovider \
+    --timeout 120 --timeout-method thread > $OUT/pytest_pf.log 2>&1
+  rc=$?; echo "pytest rc=$rc: $(tail -1 $OUT/pytest_pf.log)"; [ $rc -eq 0 ] || { grep -E "^(FAILED|ERROR)" $OUT/pytest_pf.log; exit $rc; }
+  for rep in 1 2; do
+    for cfg in c5:1:0 c5:2:0 c5:2:1 c2:1:0 c2:2:0; do
+      IFS=: read wl d a <<< "$cfg"
+      DLAMD_PF_DEPTH=$d DLAMD_PF_AFTER=$a timeout -k 10 300 python bench.py --no-cpu-baseline --no-extra --workload $wl \
+        --steps 20 --warmup 5 > $OUT/pf_${wl}_${d}_${a}.json 2> $OUT/pf_${wl}_${d}_${a}.err || { tail -5 $OUT/pf_${wl}_${d}_${a}.err; exit 1; }
+      python -c "
+import json;d=json.loads(open('$OUT/pf_${wl}_${d}_${a}.json').read().strip().splitlines()[-1])
+print('$wl depth=$d after=$a', d['ms_per_step'], 'host', d.get('host_submit_ms_per_step'))"
+    done
+  done
+  DLAMD_PF_DEPTH=2 bash scripts/gpu_r4.sh trace ${TAG}_d2 c5
+  exit $?
+fi
+if [ "$MODE" = pfab ]; then
+  # the next batch's prefetch submitted before (0) or after (1) the step's own graph
+  for wl in c5 c2; do
+    for a in 0 1 0 1; do
+      DLAMD_PF_AFTER=$a timeout -k 10 300 python bench.py --no-cpu-baseline --no-extra --workload $wl --steps 20 \
+        --warmup 5 > $OUT/pf_${wl}_$a.json 2> $OUT/pf_${wl}_$a.err || { tail -5 $OUT/pf_${wl}_$a.err; exit 1; }
+      python -c "
+import json;d=json.loads(open('$OUT/pf_${wl}_$a.json').read().strip().splitlines()[-1])
+print('$wl pf_after=$a', d['ms_per_step'], 'host', d.get('host_submit_ms_per_step'))"
+    done
+  done
+  DLAMD_PF_AFTER=1 bash scripts/gpu_r4.sh trace ${TAG}_pf1 c5
+  exit $?
+fi
 if [ "$MODE" = abdiag ]; then
   # the root Adam state against TF's v (libdlamd_vst), then the backward's byte split
   bash scripts/gpu_ab_variant.sh ${TAG}_vst vst "" "" "c2 c5" || exit $?

@@ -261,22 +261,27 @@ def test_wdl_bf16_tower_tracks_oracle(hip_lib, adam):
     assert worst < 3e-2, worst
 
 
-@pytest.mark.parametrize("name,adam", [("deepfm_pipeline", "lazy"), ("deepfm_pipeline", "dense"),
-                                       ("deepfm_multi_cate", "lazy"), ("wdl", "lazy")])
-def test_prefetch_matches_inline_index(hip_lib, name, adam):
-    """train_step(next_batch=...) stages and indexes the next batch into the other buffer
-    set on the side stream during the current step: results are bit-identical to building
-    each index at the start of its own step (graph and eager replays, a predict between)."""
+@pytest.mark.parametrize("name,adam,depth", [("deepfm_pipeline", "lazy", 1), ("deepfm_pipeline", "dense", 1),
+                                             ("deepfm_multi_cate", "lazy", 1), ("wdl", "lazy", 1),
+                                             ("deepfm_pipeline", "lazy", 2), ("wdl", "lazy", 2)])
+def test_prefetch_matches_inline_index(hip_lib, name, adam, depth, monkeypatch):
+    """train_step(next_batch=...) stages and indexes the next batch (depth 2: the next two,
+    three buffer sets) into idle buffer sets on the side stream during the current step:
+    results are bit-identical to building each index at the start of its own step (graph and
+    eager replays, a predict between, a step that prefetches nothing)."""
+    monkeypatch.setenv("DLAMD_PF_DEPTH", str(depth))
     kw = CASES[name]
     model = _model(name)
     spec = ModelSpec(model, **kw)
-    bs = _batches(name, kw, 256, 7, seed=3)
+    bs = _batches(name, kw, 256, 8, seed=3)
     runs = []
     for pf in (False, True):
         eng = CTREngine(spec, max_batch=256, seed=9, adam=adam, **({} if adam == "lazy" else {"bwd": "sorted"}))
+        assert eng.pf_depth == depth
         zs = []
         for i, b in enumerate(bs[:6]):
-            nxt = bs[i + 1] if pf and i != 3 else None      # step 3: no prefetch, step 4 indexes inline
+            # step 3: no prefetch (depth 1: step 4 indexes inline)
+            nxt = (bs[i + 1] if depth == 1 else bs[i + 1: i + 1 + depth]) if pf and i != 3 else None
             eng.train_step(b, graph=i >= 2, next_batch=nxt)
             torch.cuda.synchronize()
             zs.append(eng.z[:256].cpu().numpy().copy())
