@@ -1289,9 +1289,10 @@ class CTREngine:
         # (DLAMD_PF_AFTER=1)
         ahead = [] if next_batch is None else list(next_batch) if isinstance(next_batch, (list, tuple)) else [next_batch]
         pf_after = os.environ.get("DLAMD_PF_AFTER", "0") == "1"
+        pf_graph = graph and os.environ.get("DLAMD_PF_EAGER", "0") != "1"
         if not pf_after:
             for nb in ahead:
-                self.prefetch(nb, graph=graph)
+                self.prefetch(nb, graph=pf_graph)
         if graph:
             # one graph per (buffer set, batch size, index built inside or prefetched)
             key = (getattr(self, "_cur", 0), B, not indexed)
@@ -1304,7 +1305,7 @@ class CTREngine:
         self._release()
         if pf_after:
             for nb in ahead:
-                self.prefetch(nb, graph=graph)
+                self.prefetch(nb, graph=pf_graph)
         self._queue_status()
         self.steps += 1
         self.last_batch = B

@@ -59,6 +59,27 @@ if [ "$MODE" = perf ]; then
   bash scripts/gpu_ab_variant.sh ${TAG}_nt nt "" "" "c2 c3"
   exit $?
 fi
+if [ "$MODE" = pfeager ]; then
+  # the prefetch's index build as a graph replay (0) or eager launches (1) on the side stream;
+  # and no prefetch at all
+  for rep in 1 2; do
+    for cfg in c5:0 c5:1 c2:0 c2:1; do
+      IFS=: read wl e <<< "$cfg"
+      DLAMD_PF_EAGER=$e timeout -k 10 300 python bench.py --no-cpu-baseline --no-extra --workload $wl \
+        --steps 20 --warmup 5 > $OUT/pe_${wl}_$e.json 2> $OUT/pe_${wl}_$e.err || { tail -5 $OUT/pe_${wl}_$e.err; exit 1; }
+      python -c "
+import json;d=json.loads(open('$OUT/pe_${wl}_$e.json').read().strip().splitlines()[-1])
+print('$wl pf_eager=$e', d['ms_per_step'], 'host', d.get('host_submit_ms_per_step'))"
+    done
+    timeout -k 10 300 python bench.py --no-cpu-baseline --no-extra --workload c5 --no-prefetch --steps 20 --warmup 5 \
+      > $OUT/pe_c5_nopf.json 2> $OUT/pe_c5_nopf.err || exit 1
+    python -c "
+import json;d=json.loads(open('$OUT/pe_c5_nopf.json').read().strip().splitlines()[-1])
+print('c5 no prefetch', d['ms_per_step'], 'host', d.get('host_submit_ms_per_step'))"
+  done
+  DLAMD_PF_EAGER=1 bash scripts/gpu_r4.sh trace ${TAG}_e1 c5
+  exit $?
+fi
 if [ "$MODE" = pfdepth ]; then
   # prefetch depth (batches in flight on the side stream) x submission order, then a C5 trace
   timeout -k 10 300 python -u -m pytest tests/test_gpu_parity.py -m gpu -q -rf -k prefetch -p no:cacheprovider \
