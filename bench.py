@@ -323,6 +323,21 @@ def dropin_fit(args, n_batches=12, warm=3):
 
 
 def run_workload(wl, args, world, rank, sharded, steps, warmup, age, ksteps, barrier):
+    """The workload on the default stream, or (DLAMD_MAIN_PRIORITY set, an A/B switch) on a
+    compute stream of that priority."""
+    import torch
+    pr = os.environ.get("DLAMD_MAIN_PRIORITY")
+    if pr is None:
+        return _run_workload(wl, args, world, rank, sharded, steps, warmup, age, ksteps, barrier)
+    st = torch.cuda.Stream(priority=int(pr))
+    st.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(st):
+        r = _run_workload(wl, args, world, rank, sharded, steps, warmup, age, ksteps, barrier)
+    torch.cuda.current_stream().wait_stream(st)
+    return r
+
+
+def _run_workload(wl, args, world, rank, sharded, steps, warmup, age, ksteps, barrier):
     """Build the engine of workload `wl`, age its table, time `steps` steps (hipGraph replay,
     next batch prefetched), then `ksteps` eager steps bracketed per kernel by HIP events.
     Uniform ids: a fresh device-drawn batch every step (no batch repeats, so the model never

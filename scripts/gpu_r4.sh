@@ -59,6 +59,22 @@ if [ "$MODE" = perf ]; then
   bash scripts/gpu_ab_variant.sh ${TAG}_nt nt "" "" "c2 c3"
   exit $?
 fi
+if [ "$MODE" = prio ]; then
+  # stream priorities: side (index prefetch) / main (the step) — default -1 / 0
+  for rep in 1 2; do
+    for cfg in c5:-1:x c5:-1:-1 c5:0:x c2:-1:x c2:-1:-1; do
+      IFS=: read wl sp mp <<< "$cfg"
+      if [ $mp = x ]; then MP=""; else MP="DLAMD_MAIN_PRIORITY=$mp"; fi
+      env DLAMD_SIDE_PRIORITY=$sp $MP timeout -k 10 300 python bench.py --no-cpu-baseline --no-extra --workload $wl \
+        --steps 20 --warmup 5 > $OUT/pr_${wl}_${sp}_$mp.json 2> $OUT/pr_${wl}_${sp}_$mp.err || { tail -5 $OUT/pr_${wl}_${sp}_$mp.err; exit 1; }
+      python -c "
+import json;d=json.loads(open('$OUT/pr_${wl}_${sp}_$mp.json').read().strip().splitlines()[-1])
+print('$wl side=$sp main=$mp', d['ms_per_step'], 'host', d.get('host_submit_ms_per_step'))"
+    done
+  done
+  DLAMD_MAIN_PRIORITY=-1 bash scripts/gpu_r4.sh trace ${TAG}_mp c5
+  exit $?
+fi
 if [ "$MODE" = pfeager ]; then
   # the prefetch's index build as a graph replay (0) or eager launches (1) on the side stream;
   # and no prefetch at all
