@@ -1243,10 +1243,6 @@ class CTREngine:
                     self._pre(B)
                 ev = torch.cuda.Event()
                 ev.record(side)
-                if os.environ.get("DLAMD_PF_MARKER", "0") == "1":   # A/B: one tiny op after the record
-                    if getattr(self, "_pf_mark", None) is None:
-                        self._pf_mark = torch.zeros(1, device=self.dev)
-                    self._pf_mark.add_(1)
         finally:
             self._use_slot(cur)
         self._pfq.append((k, B, ev, batch))

@@ -59,20 +59,6 @@ if [ "$MODE" = perf ]; then
   bash scripts/gpu_ab_variant.sh ${TAG}_nt nt "" "" "c2 c3"
   exit $?
 fi
-if [ "$MODE" = pfmark ]; then
-  for rep in 1 2; do
-    for cfg in c5:0 c5:1; do
-      IFS=: read wl e <<< "$cfg"
-      DLAMD_PF_MARKER=$e timeout -k 10 300 python bench.py --no-cpu-baseline --no-extra --workload $wl \
-        --steps 20 --warmup 5 > $OUT/pm_${wl}_$e.json 2> $OUT/pm_${wl}_$e.err || { tail -5 $OUT/pm_${wl}_$e.err; exit 1; }
-      python -c "
-import json;d=json.loads(open('$OUT/pm_${wl}_$e.json').read().strip().splitlines()[-1])
-print('$wl pf_marker=$e', d['ms_per_step'], 'host', d.get('host_submit_ms_per_step'))"
-    done
-  done
-  DLAMD_PF_MARKER=1 bash scripts/gpu_r4.sh trace ${TAG}_m1 c5
-  exit $?
-fi
 if [ "$MODE" = prio ]; then
   # stream priorities: side (index prefetch) / main (the step) — default -1 / 0
   for rep in 1 2; do
