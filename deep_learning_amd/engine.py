@@ -1413,6 +1413,9 @@ class CTREngine:
         memory.  Completed read-backs are checked at the next steps without waiting; at most
         two may be outstanding, so a bad batch raises within two train_step calls (TF raises
         in the failing sess.run; here the failing step itself has applied nothing)."""
+        every = int(os.environ.get("DLAMD_STATUS_EVERY", "1"))   # A/B: read back every N steps
+        if every > 1 and self.steps % every:
+            return
         if self._status_host is None:
             self._status_host = torch.zeros(4, dtype=torch.int32, pin_memory=True)
         k = self.steps % 4

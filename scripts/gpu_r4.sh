@@ -59,6 +59,21 @@ if [ "$MODE" = perf ]; then
   bash scripts/gpu_ab_variant.sh ${TAG}_nt nt "" "" "c2 c3"
   exit $?
 fi
+if [ "$MODE" = status ]; then
+  # the per-step status read-back (a D2H copy into pinned memory after every step) every 1 / 16 steps
+  for rep in 1 2; do
+    for cfg in c5:1 c5:16 c2:1 c2:16; do
+      IFS=: read wl e <<< "$cfg"
+      DLAMD_STATUS_EVERY=$e timeout -k 10 300 python bench.py --no-cpu-baseline --no-extra --workload $wl \
+        --steps 20 --warmup 5 > $OUT/st_${wl}_$e.json 2> $OUT/st_${wl}_$e.err || { tail -5 $OUT/st_${wl}_$e.err; exit 1; }
+      python -c "
+import json;d=json.loads(open('$OUT/st_${wl}_$e.json').read().strip().splitlines()[-1])
+print('$wl status_every=$e', d['ms_per_step'], 'host', d.get('host_submit_ms_per_step'))"
+    done
+  done
+  DLAMD_STATUS_EVERY=16 bash scripts/gpu_r4.sh trace ${TAG}_s16 c5
+  exit $?
+fi
 if [ "$MODE" = prio ]; then
   # stream priorities: side (index prefetch) / main (the step) — default -1 / 0
   for rep in 1 2; do
