@@ -542,7 +542,7 @@ __device__ __forceinline__ void rec_bwd_apply(const SegGrad4& s, int64_t row, in
 // hot rows, [kHotT] their chunks; then the hot rows' unique indices (appended by pass 1 in any
 // order), their first chunk (exclusive prefix over ceil(refs / kSegChunk), plus the total), the
 // owner of every chunk, and one partial sum per chunk (E/4 x {s, x, dsum} float4 + g1).
-constexpr int kHotN = 0, kHotT = 1, kHotList = 4;
+constexpr int kHotN = 0, kHotT = 1, kHotDone = 2, kHotList = 4;
 struct HotWs {
   int32_t* hdr;
   int32_t* list;
@@ -687,10 +687,6 @@ __global__ __launch_bounds__(256) void rec_bwd_long_kernel(DL_REC_BWD_PARAMS) {
 //                         (segment_grad4_block), written as the chunk's partial
 //   rec_hot_apply_kernel  E/4 lanes per hot row: its partials added in chunk order (the
 //                         canonical long-segment sum, segment.h) and the row's Adam step
-__global__ void rec_hot_reset_kernel(int32_t* __restrict__ hdr) {
-  if (threadIdx.x == 0) { hdr[kHotN] = 0; hdr[kHotT] = 0; }
-}
-
 __global__ __launch_bounds__(1024) void rec_hot_scan_kernel(SegGradIn sg, HotWs h, const int32_t* __restrict__ n_uniq,
                                                            const float* __restrict__ opt) {
   __shared__ int ws[16];
@@ -776,7 +772,7 @@ __global__ __launch_bounds__(256) void rec_hot_apply_kernel(SegGradIn sg, float*
                                                             float* __restrict__ g_rep, float* __restrict__ g1_rep,
                                                             const float* __restrict__ hist,
                                                             const float* __restrict__ opt, HotWs h) {
-  if (step_poisoned(opt)) return;
+  const bool live = !step_poisoned(opt);
   rec_load_hyper(c, opt);
   __shared__ float hw[kHistWin];
   const RingW ring = load_hist_window(hw, hist, (int)opt[7], c);
@@ -785,7 +781,7 @@ __global__ __launch_bounds__(256) void rec_hot_apply_kernel(SegGradIn sg, float*
   const long long gt = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   const int q = (int)(gt % LPR);
   const long long g0 = gt / LPR, ng = (long long)gridDim.x * blockDim.x / LPR;
-  const int n = (int)min((long long)h.hdr[kHotN], h.cap_list);
+  const int n = live ? (int)min((long long)h.hdr[kHotN], h.cap_list) : 0;
   const int t = (int)opt[7];
   const float alpha = opt[3];
   const bool first = c.has_first && q == 0;
@@ -805,6 +801,18 @@ __global__ __launch_bounds__(256) void rec_hot_apply_kernel(SegGradIn sg, float*
     float w = 0.f, wm = 0.f, wv = 0.f;
     rec_bwd_state<E>(row, n_rep + u, q, first, row_ok, rec, rows_u, rows_u1, mv, c, t, ring, p, m, v, w, wm, wv);
     if (row_ok) rec_bwd_apply<E>(s, row, q, first, p, m, v, w, wm, wv, rec, c, L, n_rep, g_rep, g1_rep, alpha, t);
+  }
+  // the last block to finish resets the header for the next step's pass 1 (in place of a
+  // reset launch before it): every block has read it by then
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __threadfence();
+    if (atomicAdd(&h.hdr[kHotDone], 1) == (int)gridDim.x - 1) {
+      h.hdr[kHotN] = 0;
+      h.hdr[kHotT] = 0;
+      h.hdr[kHotDone] = 0;
+      __threadfence();
+    }
   }
 }
 
@@ -828,6 +836,52 @@ __global__ __launch_bounds__(256) void rec_apply_rows_kernel(float* __restrict__
     const float g1i = (g1 && d == 0) ? g1[i] : 0.f;
     if (!skip) rec_update(rec + (row0 + i) * c.ld, E, d, gi, g1i, t, alpha_t, ring, c);
     g[k] = 0.f;
+    if (g1 && d == 0) g1[i] = 0.f;
+  }
+}
+
+// dl_rec_apply_rows with the FM cont-field rows' slab partials (dl_embed_cont_bwd) folded in
+// first: each column summed exactly as dl_embed_cont_reduce sums it (strided per thread, then
+// wave_sum, then the four waves), added to g after the rows' own reference gradients, as
+// cont_reduce's += did — one launch instead of two, the same bits.  One block per row.
+__global__ __launch_bounds__(256) void rec_apply_rows_slab_kernel(float* __restrict__ rec, RecCfg c, long long row0,
+                                                                  int n, float* __restrict__ g, float* __restrict__ g1,
+                                                                  const float* __restrict__ hist,
+                                                                  const float* __restrict__ opt,
+                                                                  const float* __restrict__ slab, int blocks,
+                                                                  int zero_row0) {
+  rec_load_hyper(c, opt);
+  __shared__ float hw[kHistWin];
+  const RingW ring = load_hist_window(hw, hist, (int)opt[7], c);
+  const int E = c.E, i = blockIdx.x;
+  if (i >= n) return;   // whole block
+  const int width = n * (E + 1);
+  __shared__ float tot[65];
+  __shared__ float part[4];
+  for (int j = 0; j <= E; ++j) {
+    const int k = j < E ? i * E + j : n * E + i;
+    float acc = 0.f;
+    for (int t = threadIdx.x; t < blocks; t += blockDim.x) acc += slab[(long long)t * width + k];
+    acc = wave_sum(acc);
+    if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = acc;
+    __syncthreads();
+    if (threadIdx.x == 0) tot[j] = part[0] + part[1] + part[2] + part[3];
+    __syncthreads();
+  }
+  const bool ok = !(zero_row0 && row0 + i == 0);   // the zero row takes no gradient (cont_reduce's row_ok)
+  const int t = (int)opt[7];
+  const float alpha_t = opt[3];
+  const bool skip = step_poisoned(opt);
+  for (int d = threadIdx.x; d < E; d += blockDim.x) {
+    float gi = g[(long long)i * E + d];
+    if (ok) gi += tot[d];
+    float g1i = 0.f;
+    if (g1 && d == 0) {
+      g1i = g1[i];
+      if (ok) g1i += tot[E];
+    }
+    if (!skip) rec_update(rec + (row0 + i) * c.ld, E, d, gi, g1i, t, alpha_t, ring, c);
+    g[(long long)i * E + d] = 0.f;
     if (g1 && d == 0) g1[i] = 0.f;
   }
 }
@@ -1205,7 +1259,7 @@ extern "C" int dl_rec_bwd_adam(const dl_emb_layout* L, float* rec, int32_t rec_l
     const RecCfg rc = make_rec_cfg(kE, rec_ld, rec_flags, (mv_u ? 2 : hist_len));
     if (hot_ws_ptr) {
       const HotWs h = hot_ws(hot_ws_ptr, nrefs_all, kE);
-      hipLaunchKernelGGL(rec_hot_reset_kernel, dim3(1), dim3(64), 0, st, h.hdr);   // (no memset node in the graph)
+      // the header is zero here: zeroed at allocation, reset by the previous step's apply
       hipLaunchKernelGGL(bwd, dim3(grid), dim3(256), 0, st, sg, rec, rc, n_rep, rows_u, has_first ? rows_u1 : nullptr,
                          mv_u, uniq_keys, n_uniq, world, g_rep, has_first ? g1_rep : nullptr, hist, opt, h.hdr);
       // the hot rows (none at uniform ids): chunks over the whole grid, then their updates
@@ -1239,6 +1293,22 @@ extern "C" int dl_rec_apply_rows(float* rec, int32_t rec_ld, int32_t emb_dim, in
                      make_rec_cfg(emb_dim, rec_ld, rec_flags, hist_len), (long long)row0,
                      (long long)n, g, has_first ? g1 : nullptr, hist, opt);
   DL_RETURN_LAUNCH("dl_rec_apply_rows");
+}
+
+extern "C" int dl_rec_apply_rows_slab(float* rec, int32_t rec_ld, int32_t emb_dim, int32_t rec_flags, int64_t row0,
+                                      int32_t n, float* g, float* g1, const float* hist, int32_t hist_len,
+                                      const float* opt, const float* slab, int32_t slab_blocks, int32_t zero_row0,
+                                      void* stream) {
+  const int32_t has_first = rec_flags & DL_REC_FIRST;
+  DL_CHECK_ARG(rec && g && hist && opt && slab, "NULL argument");
+  if (int rc = rec_check(emb_dim, rec_ld, hist_len)) return rc;
+  DL_CHECK_ARG(!has_first || g1, "g1 required with first-order weights");
+  DL_CHECK_ARG(row0 >= 0 && n >= 0 && slab_blocks > 0 && emb_dim <= 64, "bad arguments");
+  if (n == 0) return 0;
+  hipLaunchKernelGGL(rec_apply_rows_slab_kernel, dim3(n), dim3(256), 0, as_stream(stream), rec,
+                     make_rec_cfg(emb_dim, rec_ld, rec_flags, hist_len), (long long)row0, n, g,
+                     has_first ? g1 : nullptr, hist, opt, slab, slab_blocks, zero_row0);
+  DL_RETURN_LAUNCH("dl_rec_apply_rows_slab");
 }
 
 extern "C" int dl_rec_flush(float* rec, int32_t rec_ld, int32_t emb_dim, int32_t rec_flags, int64_t n_rows,

@@ -1324,13 +1324,20 @@ class CTREngine:
                 self.hist_len, ptr(self.opt), C_ref(self.pool_desc) if sp.M else None, ptr(self.hot_ws),
                 self.hot_ws.numel(), s)
         if R:
-            # FM cont-field rows: per-block register partials, folded into g_rep, then updated
+            # FM cont-field rows: per-block register partials (on the blocks that have samples),
+            # then folded into g_rep and the rows updated in one launch
+            cb = self._cont_blocks(B, bwd_blocks)
             self._c("cont_bwd", "dl_embed_cont_bwd", C_ref(L), ptr(self.rows_u), ptr(self._cont()),
-                    ptr(self.dz), ptr(self.w_head), ptr(self.fm_sum), ptr(self.cont_slab), self.bwd_blocks, s)
-            self._c("cont_reduce", "dl_embed_cont_reduce", C_ref(L), ptr(self.cont_slab), bwd_blocks,
-                    ptr(self.g_rep), ptr(self.g1_rep), ptr(self.rep_touched), s)
-            self._c("adam_rep", "dl_rec_apply_rows", ptr(self.rec), self.rec_ld, E, self.rec_flags, sp.fm_cont_offset, R,
-                    ptr(self.g_rep), ptr(self.g1_rep), ptr(self.hist), self.hist_len, ptr(self.opt), s)
+                    ptr(self.dz), ptr(self.w_head), ptr(self.fm_sum), ptr(self.cont_slab), cb, s)
+            self._c("adam_rep", "dl_rec_apply_rows_slab", ptr(self.rec), self.rec_ld, E, self.rec_flags,
+                    sp.fm_cont_offset, R, ptr(self.g_rep), ptr(self.g1_rep), ptr(self.hist), self.hist_len,
+                    ptr(self.opt), ptr(self.cont_slab), cb, int(L.zero_row0), s)
+
+    def _cont_blocks(self, B, bwd_blocks):
+        """dl_embed_cont_bwd's blocks that hold samples (embed.hip cont_bwd_kernel: 16 samples a
+        lane group, 64 / (E / 4) per wave, four waves): the rest would write zero partials."""
+        spw = 64 // (self.spec.E // 4)
+        return max(1, min(bwd_blocks, (B + 16 * spw - 1) // (16 * spw)))
 
     def _capture(self, B, with_pre=False, pre_only=False):
         """Capture the step (with its index build when `with_pre`), or only the index build
