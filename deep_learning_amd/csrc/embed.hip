@@ -1284,8 +1284,10 @@ extern "C" int dl_embed_cont_bwd(const dl_emb_layout* L, const float* table, con
                                  int32_t cont_slab_blocks, void* stream) {
   if (int rc = check_layout(L)) return rc;
   if (L->batch == 0 || !(L->use_fm && L->fm_cont && L->cont_fields > 0)) return 0;
-  const int grid = dl_embed_bwd_grid(L);
-  DL_CHECK_ARG(cont_slab && cont_slab_blocks >= grid, "cont_slab needs %d blocks", grid);
+  // blocks: cont_slab_blocks, at most dl_embed_bwd_grid (blocks past the samples' share write
+  // zero partials, so a caller may pass just the blocks that hold samples: same partials)
+  const int grid = min(dl_embed_bwd_grid(L), (int)cont_slab_blocks);
+  DL_CHECK_ARG(cont_slab && cont_slab_blocks >= 1, "cont_slab needs at least one block");
   EmbBwdArgs a{*L, table, nullptr, cont, dz, w_head, fm_sum, nullptr, nullptr, nullptr, nullptr, cont_slab};
   DL_DISPATCH_E(L->emb_dim, {
     if (L->cont_fields <= 16)

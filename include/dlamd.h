@@ -156,7 +156,9 @@ int dl_embed_fwd_rec_flat(const dl_emb_layout* L, const float* rec, int32_t rec_
                           float* fm_out, float* fm_sum, int32_t* err, void* stream);
 
 /* Hot cont-field rows only (the FM cont part of dl_embed_bwd): per-block
- * partials into cont_slab, folded in by dl_embed_cont_reduce. */
+ * partials into cont_slab[0 .. min(cont_slab_blocks, dl_embed_bwd_grid)), folded in by
+ * dl_embed_cont_reduce or dl_rec_apply_rows_slab (blocks beyond the samples' share hold zeros,
+ * so passing only the blocks that hold samples gives the same partials). */
 int dl_embed_cont_bwd(const dl_emb_layout* L, const float* table, const float* cont,
                       const float* dz, const float* w_head, const float* fm_sum, float* cont_slab,
                       int32_t cont_slab_blocks, void* stream);

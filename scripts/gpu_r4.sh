@@ -59,6 +59,17 @@ if [ "$MODE" = perf ]; then
   bash scripts/gpu_ab_variant.sh ${TAG}_nt nt "" "" "c2 c3"
   exit $?
 fi
+if [ "$MODE" = check ]; then
+  # the GPU suite without the full-size tests, then C2 / C5 benches and a C2 trace
+  bash scripts/gpu_r4.sh quick $TAG || exit $?
+  for wl in c2 c5; do
+    timeout -k 10 300 python bench.py --no-cpu-baseline --no-extra --workload $wl --steps 20 --warmup 5 \
+      > $OUT/b_$wl.json 2> $OUT/b_$wl.err || { tail -5 $OUT/b_$wl.err; exit 1; }
+    python scripts/bench_brief.py $OUT/b_$wl.json
+  done
+  bash scripts/gpu_r4.sh trace $TAG c2
+  exit $?
+fi
 if [ "$MODE" = status ]; then
   # the per-step status read-back (a D2H copy into pinned memory after every step) every 1 / 16 steps
   for rep in 1 2; do
