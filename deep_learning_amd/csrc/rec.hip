@@ -857,17 +857,22 @@ __global__ __launch_bounds__(256) void rec_apply_rows_slab_kernel(float* __restr
   if (i >= n) return;   // whole block
   const int width = n * (E + 1);
   __shared__ float tot[65];
-  __shared__ float part[4];
-  for (int j = 0; j <= E; ++j) {
+  // each wave takes whole columns; per column its lane l plays cont_reduce's threads
+  // 64 w + l (w = 0..3) in turn — the strided per-thread sums, wave_sum, then the four
+  // waves' sums in order: cont_reduce's exact operations, the columns in parallel
+  const int lane = threadIdx.x & 63;
+  for (int j = threadIdx.x >> 6; j <= E; j += blockDim.x >> 6) {
     const int k = j < E ? i * E + j : n * E + i;
-    float acc = 0.f;
-    for (int t = threadIdx.x; t < blocks; t += blockDim.x) acc += slab[(long long)t * width + k];
-    acc = wave_sum(acc);
-    if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = acc;
-    __syncthreads();
-    if (threadIdx.x == 0) tot[j] = part[0] + part[1] + part[2] + part[3];
-    __syncthreads();
+    float ws[4];
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {
+      float acc = 0.f;
+      for (int tt = 64 * w + lane; tt < blocks; tt += 256) acc += slab[(long long)tt * width + k];
+      ws[w] = wave_sum(acc);
+    }
+    if (lane == 0) tot[j] = ws[0] + ws[1] + ws[2] + ws[3];
   }
+  __syncthreads();
   const bool ok = !(zero_row0 && row0 + i == 0);   // the zero row takes no gradient (cont_reduce's row_ok)
   const int t = (int)opt[7];
   const float alpha_t = opt[3];
