@@ -151,6 +151,21 @@ def pmc_traffic(label, world, lazy=False, workload="c2", id_dist="uniform"):
     return None
 
 
+def bwd_calibrated(label, world, lazy=False, workload="c2", id_dist="uniform"):
+    """The lazy backward's HBM bytes with the x2 FETCH_SIZE correction applied only to its
+    coalesced streams (scripts/bwd_split.py: diagnostic builds show each random 64-B slice read
+    is one 64-B request, already counted at its size) — C2 uniform only, where it was measured."""
+    import glob
+    if label != "embed_bwd" or not lazy or world != 1 or workload != "c2" or id_dist != "uniform":
+        return None
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*", "bwd_split.json")))
+    if not files:
+        return None
+    d = json.load(open(files[-1]))
+    return {"traffic_calibrated": int(d["hbm_bytes_calibrated"]),
+            "traffic_calibrated_source": os.path.relpath(files[-1], ROOT)}
+
+
 def cpu_baseline(spec_kw, B, steps_big=12, warm_big=2, steps_small=50, warm_small=10):
     """The CPU baseline of BASELINE.md §2: the torch-CPU restatement of
     models/deepfm_pipeline.py (oracle/torch_cpu.py; the reference's TF-CPU path cannot run
@@ -470,6 +485,9 @@ def _run_workload(wl, args, world, rank, sharded, steps, warmup, age, ksteps, ba
     if pmc is not None:
         roof["traffic"] = pmc["hbm_bytes"]
         roof["traffic_source"] = pmc["source"]
+        cal = bwd_calibrated(dom, world, lazy=uniq is not None, workload=wl, id_dist=args.dist)
+        if cal is not None:
+            roof.update(cal)
     # the embedding lookup by SURVEY §8(d)'s own byte count (C2: 26 FM + 26 deep rows x 64 B +
     # 26 first-order x 4 B + 26 ids x 8 B = 3,640 B/sample; C3: 17,096 B/sample) over the
     # kernels that do it here (record gather + indexed forward); the per-kernel figures above

@@ -59,6 +59,33 @@ if [ "$MODE" = perf ]; then
   bash scripts/gpu_ab_variant.sh ${TAG}_nt nt "" "" "c2 c3"
   exit $?
 fi
+if [ "$MODE" = dropin ]; then
+  # the wdl drop-in fit (load-style train_epoch) at C5 shapes: its tests, then bench's dropin_fit
+  timeout -k 10 300 python -u -m pytest tests/test_gpu_dropin.py tests/test_gpu_parity.py -m gpu -q -rf -k "wdl or load_style or running_loss" \
+    -p no:cacheprovider --timeout 200 --timeout-method thread > $OUT/pytest_dropin.log 2>&1
+  rc=$?; echo "pytest rc=$rc: $(tail -1 $OUT/pytest_dropin.log)"; [ $rc -eq 0 ] || { grep -E "^(FAILED|ERROR)" $OUT/pytest_dropin.log; exit $rc; }
+  timeout -k 10 300 python -c "
+import bench, json, argparse
+a = argparse.Namespace(batch=65536)
+print(json.dumps(bench.dropin_fit(a)))" > $OUT/dropin.json 2> $OUT/dropin.err || { tail -5 $OUT/dropin.err; exit 1; }
+  cat $OUT/dropin.json
+  exit 0
+fi
+if [ "$MODE" = nowait ]; then
+  # probe: the compute stream's cross-stream wait on the prefetch replaced by a host wait
+  for rep in 1 2; do
+    for cfg in c5:0 c5:1 c2:0 c2:1; do
+      IFS=: read wl e <<< "$cfg"
+      DLAMD_PF_NOWAIT=$e timeout -k 10 300 python bench.py --no-cpu-baseline --no-extra --workload $wl \
+        --steps 20 --warmup 5 > $OUT/nw_${wl}_$e.json 2> $OUT/nw_${wl}_$e.err || { tail -5 $OUT/nw_${wl}_$e.err; exit 1; }
+      python -c "
+import json;d=json.loads(open('$OUT/nw_${wl}_$e.json').read().strip().splitlines()[-1])
+print('$wl pf_nowait=$e', d['ms_per_step'], 'host', d.get('host_submit_ms_per_step'))"
+    done
+  done
+  DLAMD_PF_NOWAIT=1 bash scripts/gpu_r4.sh trace ${TAG}_nw c5
+  exit $?
+fi
 if [ "$MODE" = check ]; then
   # the GPU suite without the full-size tests, then C2 / C5 benches and a C2 trace
   bash scripts/gpu_r4.sh quick $TAG || exit $?
