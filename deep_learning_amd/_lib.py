@@ -112,7 +112,6 @@ SIGNATURES = {
                               P, P, I64, P]),
     "dl_rec_bwd_workspace_bytes": (I64, [I64, I32]),
     "dl_rec_apply_rows": (I32, [P, I32, I32, I32, I64, I64, P, P, P, I32, P, P]),
-    "dl_rec_apply_rows_slab": (I32, [P, I32, I32, I32, I64, I32, P, P, P, I32, P, P, I32, I32, P]),
     "dl_sort_unique": (I32, [P, I64, I32, P, I64, P, P, P, P, P, P, P]),
     "dl_rec_apply_segments": (I32, [P, I32, I32, I32, P, P, P, I64, I64, P, P, P, P, P, P, P, I32, P, P]),
     "dl_rec_flush": (I32, [P, I32, I32, I32, I64, P, I32, P, P, P, P]),

@@ -840,57 +840,6 @@ __global__ __launch_bounds__(256) void rec_apply_rows_kernel(float* __restrict__
   }
 }
 
-// dl_rec_apply_rows with the FM cont-field rows' slab partials (dl_embed_cont_bwd) folded in
-// first: each column summed exactly as dl_embed_cont_reduce sums it (strided per thread, then
-// wave_sum, then the four waves), added to g after the rows' own reference gradients, as
-// cont_reduce's += did — one launch instead of two, the same bits.  One block per row.
-__global__ __launch_bounds__(256) void rec_apply_rows_slab_kernel(float* __restrict__ rec, RecCfg c, long long row0,
-                                                                  int n, float* __restrict__ g, float* __restrict__ g1,
-                                                                  const float* __restrict__ hist,
-                                                                  const float* __restrict__ opt,
-                                                                  const float* __restrict__ slab, int blocks,
-                                                                  int zero_row0) {
-  rec_load_hyper(c, opt);
-  __shared__ float hw[kHistWin];
-  const RingW ring = load_hist_window(hw, hist, (int)opt[7], c);
-  const int E = c.E, i = blockIdx.x;
-  if (i >= n) return;   // whole block
-  const int width = n * (E + 1);
-  __shared__ float tot[65];
-  // each wave takes whole columns; per column its lane l plays cont_reduce's threads
-  // 64 w + l (w = 0..3) in turn — the strided per-thread sums, wave_sum, then the four
-  // waves' sums in order: cont_reduce's exact operations, the columns in parallel
-  const int lane = threadIdx.x & 63;
-  for (int j = threadIdx.x >> 6; j <= E; j += blockDim.x >> 6) {
-    const int k = j < E ? i * E + j : n * E + i;
-    float ws[4];
-#pragma unroll
-    for (int w = 0; w < 4; ++w) {
-      float acc = 0.f;
-      for (int tt = 64 * w + lane; tt < blocks; tt += 256) acc += slab[(long long)tt * width + k];
-      ws[w] = wave_sum(acc);
-    }
-    if (lane == 0) tot[j] = ws[0] + ws[1] + ws[2] + ws[3];
-  }
-  __syncthreads();
-  const bool ok = !(zero_row0 && row0 + i == 0);   // the zero row takes no gradient (cont_reduce's row_ok)
-  const int t = (int)opt[7];
-  const float alpha_t = opt[3];
-  const bool skip = step_poisoned(opt);
-  for (int d = threadIdx.x; d < E; d += blockDim.x) {
-    float gi = g[(long long)i * E + d];
-    if (ok) gi += tot[d];
-    float g1i = 0.f;
-    if (g1 && d == 0) {
-      g1i = g1[i];
-      if (ok) g1i += tot[E];
-    }
-    if (!skip) rec_update(rec + (row0 + i) * c.ld, E, d, gi, g1i, t, alpha_t, ring, c);
-    g[(long long)i * E + d] = 0.f;
-    if (g1 && d == 0) g1[i] = 0.f;
-  }
-}
-
 // Every row caught up to step opt[7] (zero-gradient steps only).
 template <int E>
 __global__ __launch_bounds__(256) void rec_flush_kernel(float* __restrict__ rec, RecCfg c, long long n_rows,
@@ -1298,22 +1247,6 @@ extern "C" int dl_rec_apply_rows(float* rec, int32_t rec_ld, int32_t emb_dim, in
                      make_rec_cfg(emb_dim, rec_ld, rec_flags, hist_len), (long long)row0,
                      (long long)n, g, has_first ? g1 : nullptr, hist, opt);
   DL_RETURN_LAUNCH("dl_rec_apply_rows");
-}
-
-extern "C" int dl_rec_apply_rows_slab(float* rec, int32_t rec_ld, int32_t emb_dim, int32_t rec_flags, int64_t row0,
-                                      int32_t n, float* g, float* g1, const float* hist, int32_t hist_len,
-                                      const float* opt, const float* slab, int32_t slab_blocks, int32_t zero_row0,
-                                      void* stream) {
-  const int32_t has_first = rec_flags & DL_REC_FIRST;
-  DL_CHECK_ARG(rec && g && hist && opt && slab, "NULL argument");
-  if (int rc = rec_check(emb_dim, rec_ld, hist_len)) return rc;
-  DL_CHECK_ARG(!has_first || g1, "g1 required with first-order weights");
-  DL_CHECK_ARG(row0 >= 0 && n >= 0 && slab_blocks > 0 && emb_dim <= 64, "bad arguments");
-  if (n == 0) return 0;
-  hipLaunchKernelGGL(rec_apply_rows_slab_kernel, dim3(n), dim3(256), 0, as_stream(stream), rec,
-                     make_rec_cfg(emb_dim, rec_ld, rec_flags, hist_len), (long long)row0, n, g,
-                     has_first ? g1 : nullptr, hist, opt, slab, slab_blocks, zero_row0);
-  DL_RETURN_LAUNCH("dl_rec_apply_rows_slab");
 }
 
 extern "C" int dl_rec_flush(float* rec, int32_t rec_ld, int32_t emb_dim, int32_t rec_flags, int64_t n_rows,

@@ -1329,14 +1329,15 @@ class CTREngine:
                 self.hist_len, ptr(self.opt), C_ref(self.pool_desc) if sp.M else None, ptr(self.hot_ws),
                 self.hot_ws.numel(), s)
         if R:
-            # FM cont-field rows: per-block register partials (on the blocks that have samples),
-            # then folded into g_rep and the rows updated in one launch
+            # FM cont-field rows: per-block register partials (on the blocks that hold samples),
+            # folded into g_rep, then the rows updated
             cb = self._cont_blocks(B, bwd_blocks)
             self._c("cont_bwd", "dl_embed_cont_bwd", C_ref(L), ptr(self.rows_u), ptr(self._cont()),
                     ptr(self.dz), ptr(self.w_head), ptr(self.fm_sum), ptr(self.cont_slab), cb, s)
-            self._c("adam_rep", "dl_rec_apply_rows_slab", ptr(self.rec), self.rec_ld, E, self.rec_flags,
-                    sp.fm_cont_offset, R, ptr(self.g_rep), ptr(self.g1_rep), ptr(self.hist), self.hist_len,
-                    ptr(self.opt), ptr(self.cont_slab), cb, int(L.zero_row0), s)
+            self._c("cont_reduce", "dl_embed_cont_reduce", C_ref(L), ptr(self.cont_slab), cb,
+                    ptr(self.g_rep), ptr(self.g1_rep), ptr(self.rep_touched), s)
+            self._c("adam_rep", "dl_rec_apply_rows", ptr(self.rec), self.rec_ld, E, self.rec_flags, sp.fm_cont_offset, R,
+                    ptr(self.g_rep), ptr(self.g1_rep), ptr(self.hist), self.hist_len, ptr(self.opt), s)
 
     def _cont_blocks(self, B, bwd_blocks):
         """dl_embed_cont_bwd's blocks that hold samples (embed.hip cont_bwd_kernel: 16 samples a

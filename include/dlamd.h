@@ -157,8 +157,8 @@ int dl_embed_fwd_rec_flat(const dl_emb_layout* L, const float* rec, int32_t rec_
 
 /* Hot cont-field rows only (the FM cont part of dl_embed_bwd): per-block
  * partials into cont_slab[0 .. min(cont_slab_blocks, dl_embed_bwd_grid)), folded in by
- * dl_embed_cont_reduce or dl_rec_apply_rows_slab (blocks beyond the samples' share hold zeros,
- * so passing only the blocks that hold samples gives the same partials). */
+ * dl_embed_cont_reduce (blocks beyond the samples' share hold zeros, so passing only the
+ * blocks that hold samples gives the same partials). */
 int dl_embed_cont_bwd(const dl_emb_layout* L, const float* table, const float* cont,
                       const float* dz, const float* w_head, const float* fm_sum, float* cont_slab,
                       int32_t cont_slab_blocks, void* stream);
@@ -561,14 +561,6 @@ int dl_rec_apply_chain(float* rec, int32_t rec_ld, int32_t emb_dim, int32_t rec_
 int dl_rec_apply_rows(float* rec, int32_t rec_ld, int32_t emb_dim, int32_t rec_flags, int64_t row0,
                       int64_t n, float* g, float* g1, const float* hist, int32_t hist_len,
                       const float* opt, void* stream);
-/* dl_rec_apply_rows for the FM cont-field rows with dl_embed_cont_bwd's slab partials folded in
- * first (cont_slab [slab_blocks][n * (E + 1)]: each column summed as dl_embed_cont_reduce sums
- * it and added to g / g1 as its += does; rows with zero_row0 and row 0 take none) — the
- * cont_reduce + apply_rows pair in one launch, the same bits.  n <= 65535, E <= 64. */
-int dl_rec_apply_rows_slab(float* rec, int32_t rec_ld, int32_t emb_dim, int32_t rec_flags, int64_t row0,
-                           int32_t n, float* g, float* g1, const float* hist, int32_t hist_len,
-                           const float* opt, const float* slab, int32_t slab_blocks, int32_t zero_row0,
-                           void* stream);
 /* Sharded owners, deterministic: per unique received row (dl_sort_unique over the received
  * ids) the ordered sum of its arrivals g[pos][E], g1[pos] is applied (step opt[7]).  With
  * mv (the owner gather's moment stash, [n][2E+4]) the row's caught-up state is taken from
