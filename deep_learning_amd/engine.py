@@ -1257,12 +1257,7 @@ class CTREngine:
             k, B, ev, _ = q.pop(0)
             self._pf = q[0] if q else None
             self._use_slot(k)
-            if os.environ.get("DLAMD_PF_NOWAIT", "0") == "1":
-                # A/B: the host waits for the index instead of the compute stream (the step is
-                # submitted once its index is built; no cross-queue wait packet)
-                ev.synchronize()
-            else:
-                torch.cuda.current_stream().wait_event(ev)
+            torch.cuda.current_stream().wait_event(ev)
             return B, True
         for p in q:      # other batches came: drop the prefetches (after they land)
             torch.cuda.current_stream().wait_event(p[2])

@@ -70,14 +70,10 @@ class LoadStyleModel:
         b = next(items, None)
         b = self.batch(b) if b is not None else None
         while b is not None:
-            # the step is submitted first, so the next batch's unpickling and host-to-device
-            # staging (host work) overlap it; its index build then runs on the side stream
-            eng.train_step(b, graph=b["label"].shape[0] == eng.B)
-            steps += 1
             nxt = next(items, None)
             nxt = self.batch(nxt) if nxt is not None else None
-            if nxt is not None:
-                eng.prefetch(nxt, graph=nxt["label"].shape[0] == eng.B)
+            eng.train_step(b, graph=b["label"].shape[0] == eng.B, **({"next_batch": nxt} if nxt is not None else {}))
+            steps += 1
             b = nxt
         loss_sum, counted = eng.loss_sum_end()
         if counted != steps:
