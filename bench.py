@@ -513,6 +513,14 @@ def _run_workload(wl, args, world, rank, sharded, steps, warmup, age, ksteps, ba
                  "us_per_step_amortised": round(fus / (eng.hist_len - 2), 2)}
         if per_sample and not spec.M:
             gather_lookup = lookup_alone(eng, batches[base % nb], B, per_sample)
+            if args.dist == "uniform":
+                # the same lookup over a Zipf batch (SURVEY §8(d)'s realistic ids: hot rows re-read)
+                zb = {k: torch.from_numpy(v).cuda() for k, v in
+                      make_batch(B, seed=4242, dist="zipf", **kw).items()}
+                z = lookup_alone(eng, zb, B, per_sample)
+                gather_lookup["zipf"] = {k: z[k] for k in ("us", "GB/s", "frac")}
+                gather_lookup["zipf"]["records"] = z["records"]
+                del zb
             if gather is not None:
                 gather["lookup_alone"] = gather_lookup
     out = dict(spec=spec, value=value, ms=ms, loss=loss, roofline=roof, gather=gather, flush=flush, kernels=kernels,
