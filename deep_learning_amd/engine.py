@@ -1225,22 +1225,14 @@ class CTREngine:
         used = {cur} | {p[0] for p in self._pfq}
         k = next(i for i in range(len(self._slots)) if i not in used)
         side = self._side_stream()
-        stage_main = os.environ.get("DLAMD_PF_STAGE_MAIN", "0") == "1"   # A/B: the copies on the compute stream
-        if stage_main:
-            self._use_slot(k)
-            try:
-                Bm = self.stage(batch)
-            finally:
-                self._use_slot(cur)
-            side.wait_stream(torch.cuda.current_stream())
-        elif self._slot_free[k] is not None:
+        if self._slot_free[k] is not None:
             side.wait_event(self._slot_free[k])
         else:
             side.wait_stream(torch.cuda.current_stream())
         self._use_slot(k)
         try:
             with torch.cuda.stream(side):
-                B = Bm if stage_main else self.stage(batch)
+                B = self.stage(batch)
                 if graph:
                     key = (k, B, "pre")
                     g = self.graphs.get(key)

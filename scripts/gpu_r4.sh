@@ -59,20 +59,6 @@ if [ "$MODE" = perf ]; then
   bash scripts/gpu_ab_variant.sh ${TAG}_nt nt "" "" "c2 c3"
   exit $?
 fi
-if [ "$MODE" = stagemain ]; then
-  for rep in 1 2; do
-    for cfg in c5:0 c5:1 c2:0 c2:1; do
-      IFS=: read wl e <<< "$cfg"
-      DLAMD_PF_STAGE_MAIN=$e timeout -k 10 300 python bench.py --no-cpu-baseline --no-extra --workload $wl \
-        --steps 20 --warmup 5 > $OUT/sm_${wl}_$e.json 2> $OUT/sm_${wl}_$e.err || { tail -5 $OUT/sm_${wl}_$e.err; exit 1; }
-      python -c "
-import json;d=json.loads(open('$OUT/sm_${wl}_$e.json').read().strip().splitlines()[-1])
-print('$wl stage_main=$e', d['ms_per_step'], 'host', d.get('host_submit_ms_per_step'))"
-    done
-  done
-  DLAMD_PF_STAGE_MAIN=1 bash scripts/gpu_r4.sh trace ${TAG}_sm c5
-  exit $?
-fi
 if [ "$MODE" = dropin ]; then
   # the wdl drop-in fit (load-style train_epoch) at C5 shapes: its tests, then bench's dropin_fit
   timeout -k 10 300 python -u -m pytest tests/test_gpu_dropin.py tests/test_gpu_parity.py -m gpu -q -rf -k "wdl or load_style or running_loss" \
