@@ -1017,8 +1017,12 @@ class CTREngine:
                     ptr(self.widx_off), ptr(self.widx_n), ptr(self.winv), None, ptr(self.err), s)
             call("dl_wide_local_ids", ptr(self.winv), B * Fw, Fw + H, ptr(self.in_wide_loc), s)
 
-    def _train(self, B):
-        self._train_body(B)
+    def _train(self, B, part="all"):
+        """The step's launches; part "front" = through the tower's backward and dense Adam,
+        "back" = the embedding backward onwards (train_step's DLAMD_PF_MID split)."""
+        self._train_body(B, part)
+        if part == "front":
+            return
         # the step's loss into the running sum (read once per epoch: loss_sum_end)
         sp = self.spec
         width = self.head_slab.shape[1]
@@ -1026,10 +1030,12 @@ class CTREngine:
         self._c("loss_acc", "dl_loss_accumulate", ptr(self.head_slab), call_int(self.head_grid, B), width, width - 1,
                 1.0 / B, ptr(self.opt), coef, ptr(self.loss_acc), _lib.stream_handle())
 
-    def _train_body(self, B):
+    def _train_body(self, B, part="all"):
         sp = self.spec
         s = _lib.stream_handle()
         L = self.layout
+        if part == "back":
+            return self._train_back(B, s, L)
         # a batch whose ids failed validation (index build) poisons the step: nothing is applied
         # (dl_step_begin: the guard, the Adam step begin and the lazy tables' alpha ring entry)
         self._c("step_begin", "dl_step_begin", ptr(self.err), ptr(self.opt), sp.decay_rate, float(sp.decay_steps),
@@ -1116,6 +1122,11 @@ class CTREngine:
             dw(l)
             dx(l)
             adam(l)
+        if part == "all":
+            self._train_back(B, s, L)
+
+    def _train_back(self, B, s, L):
+        sp = self.spec
         # embedding backward (uses pre-update table and head weights)
         bwd_blocks = call_int("dl_embed_bwd_grid", C_ref(L))
         if self.lazy:
@@ -1213,11 +1224,13 @@ class CTREngine:
         self._pfq = []                    # pending prefetches, oldest first: (set, B, ready event, batch)
         self._pf = None                   # the oldest pending prefetch (_pfq[0])
 
-    def prefetch(self, batch, graph=False):
+    def prefetch(self, batch, graph=False, after=None):
         """Stage `batch` and build its index into an idle buffer set on the side stream;
         train_step(batch) then starts from it.  Up to pf_depth batches may be pending (buffer
         sets: pf_depth + 1), consumed in order.  graph=True replays the index build as a
-        captured hipGraph (one per buffer set and batch size)."""
+        captured hipGraph (one per buffer set and batch size).  after: an event on the compute
+        stream recorded after every earlier step; the side stream starts from it (instead of
+        from the moment the chosen buffer set is free)."""
         self._enable_slots()
         if any(p[3] is batch for p in self._pfq) or len(self._pfq) >= len(self._slots) - 1:
             return
@@ -1225,7 +1238,9 @@ class CTREngine:
         used = {cur} | {p[0] for p in self._pfq}
         k = next(i for i in range(len(self._slots)) if i not in used)
         side = self._side_stream()
-        if self._slot_free[k] is not None:
+        if after is not None:
+            side.wait_event(after)
+        elif self._slot_free[k] is not None:
             side.wait_event(self._slot_free[k])
         else:
             side.wait_stream(torch.cuda.current_stream())
@@ -1290,6 +1305,29 @@ class CTREngine:
         ahead = [] if next_batch is None else list(next_batch) if isinstance(next_batch, (list, tuple)) else [next_batch]
         pf_after = os.environ.get("DLAMD_PF_AFTER", "0") == "1"
         pf_graph = graph and os.environ.get("DLAMD_PF_EAGER", "0") != "1"
+        # DLAMD_PF_MID=1: the step in two launches, the prefetch's staging and index build
+        # released between them — beside the embedding backward, not the tower GEMMs
+        pf_mid = bool(ahead) and not pf_after and os.environ.get("DLAMD_PF_MID", "0") == "1"
+        if pf_mid:
+            for part in ("front", "back"):
+                if graph:
+                    key = (getattr(self, "_cur", 0), B, not indexed, part)
+                    g = self.graphs.get(key)
+                    if g is None:
+                        g = self.graphs[key] = self._capture(B, with_pre=not indexed, part=part)
+                    g.replay()
+                else:
+                    self._train(B, part)
+                if part == "front":
+                    mid = torch.cuda.Event()
+                    mid.record()
+                    for nb in ahead:
+                        self.prefetch(nb, graph=pf_graph, after=mid)
+            self._release()
+            self._queue_status()
+            self.steps += 1
+            self.last_batch = B
+            return B
         if not pf_after:
             for nb in ahead:
                 self.prefetch(nb, graph=pf_graph)
@@ -1340,17 +1378,18 @@ class CTREngine:
         spw = 64 // (self.spec.E // 4)
         return max(1, min(bwd_blocks, (B + 16 * spw - 1) // (16 * spw)))
 
-    def _capture(self, B, with_pre=False, pre_only=False):
+    def _capture(self, B, with_pre=False, pre_only=False, part="all"):
         """Capture the step (with its index build when `with_pre`), or only the index build
-        (`pre_only`: the prefetch graph), on a capture stream; replayed on the caller's."""
+        (`pre_only`: the prefetch graph), on a capture stream; replayed on the caller's.
+        part: the whole step, or its front / back half (see _train)."""
         s = torch.cuda.Stream()
         s.wait_stream(torch.cuda.current_stream())
         g = torch.cuda.CUDAGraph()
         with capture_guard(), torch.cuda.graph(g, stream=s):
-            if with_pre or pre_only:
+            if (with_pre and part != "back") or pre_only:
                 self._pre(B)
             if not pre_only:
-                self._train(B)
+                self._train(B, part)
         torch.cuda.current_stream().wait_stream(s)
         return g
 

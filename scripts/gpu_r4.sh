@@ -45,6 +45,36 @@ if [ "$MODE" = trace ]; then
   python scripts/step_timeline.py "$f" > $OUT/timeline_$WL.txt && head -40 $OUT/timeline_$WL.txt
   exit 0
 fi
+if [ "$MODE" = hosttrace ]; then
+  # kernels and HIP API calls of the hipGraph steps: host submission against the GPU at the boundary
+  WL=${3:-c5}
+  timeout -k 10 300 rocprofv3 --kernel-trace --hip-runtime-trace --output-format csv -d $OUT/htrace_$WL -o trace -- \
+    python bench.py --no-extra --no-cpu-baseline --workload $WL --steps 10 --warmup 3 --age-steps 16 \
+    > $OUT/htrace_$WL.log 2>&1
+  rc=$?; echo "htrace rc=$rc"; [ $rc -eq 0 ] || { tail -5 $OUT/htrace_$WL.log; exit $rc; }
+  k=$(find $OUT/htrace_$WL -name "*kernel_trace.csv" | head -1)
+  a=$(find $OUT/htrace_$WL -name "*hip_api_trace.csv" | head -1)
+  python scripts/host_timeline.py "$k" "$a" > $OUT/host_timeline_$WL.txt; rc=$?
+  head -30 $OUT/host_timeline_$WL.txt; exit $rc
+fi
+if [ "$MODE" = pfmid ]; then
+  # the step in two launches with the prefetch released between them: bit-identity, A/B, trace
+  timeout -k 10 300 python -u -m pytest tests/test_gpu_parity.py -m gpu -q -rf -k prefetch_matches \
+    -p no:cacheprovider --timeout 200 --timeout-method thread > $OUT/pytest_pfmid.log 2>&1
+  rc=$?; echo "pytest rc=$rc: $(tail -1 $OUT/pytest_pfmid.log)"; [ $rc -eq 0 ] || { grep -E "^(FAILED|ERROR)" $OUT/pytest_pfmid.log; exit $rc; }
+  for rep in 1 2; do
+    for cfg in c5:0 c5:1 c2:0 c2:1; do
+      IFS=: read wl e <<< "$cfg"
+      DLAMD_PF_MID=$e timeout -k 10 300 python bench.py --no-cpu-baseline --no-extra --workload $wl \
+        --steps 20 --warmup 5 > $OUT/mid_${wl}_$e.json 2> $OUT/mid_${wl}_$e.err || { tail -5 $OUT/mid_${wl}_$e.err; exit 1; }
+      python -c "
+import json;d=json.loads(open('$OUT/mid_${wl}_$e.json').read().strip().splitlines()[-1])
+print('$wl pf_mid=$e', d['ms_per_step'], 'host', d.get('host_submit_ms_per_step'))"
+    done
+  done
+  DLAMD_PF_MID=1 bash scripts/gpu_r4.sh trace ${TAG}_mid c5 && DLAMD_PF_MID=1 bash scripts/gpu_r4.sh trace ${TAG}_mid c2
+  exit $?
+fi
 if [ "$MODE" = combo ]; then
   # quick, then an A/B of a library variant ($3) on C2 and C3
   bash scripts/gpu_r4.sh quick $TAG || exit $?

@@ -261,15 +261,19 @@ def test_wdl_bf16_tower_tracks_oracle(hip_lib, adam):
     assert worst < 3e-2, worst
 
 
-@pytest.mark.parametrize("name,adam,depth", [("deepfm_pipeline", "lazy", 1), ("deepfm_pipeline", "dense", 1),
-                                             ("deepfm_multi_cate", "lazy", 1), ("wdl", "lazy", 1),
-                                             ("deepfm_pipeline", "lazy", 2), ("wdl", "lazy", 2)])
-def test_prefetch_matches_inline_index(hip_lib, name, adam, depth, monkeypatch):
+@pytest.mark.parametrize("name,adam,depth,mid", [("deepfm_pipeline", "lazy", 1, 0), ("deepfm_pipeline", "dense", 1, 0),
+                                                 ("deepfm_multi_cate", "lazy", 1, 0), ("wdl", "lazy", 1, 0),
+                                                 ("deepfm_pipeline", "lazy", 2, 0), ("wdl", "lazy", 2, 0),
+                                                 ("deepfm_pipeline", "lazy", 1, 1), ("wdl", "lazy", 1, 1),
+                                                 ("deepfm_multi_cate", "dense", 2, 1)])
+def test_prefetch_matches_inline_index(hip_lib, name, adam, depth, mid, monkeypatch):
     """train_step(next_batch=...) stages and indexes the next batch (depth 2: the next two,
     three buffer sets) into idle buffer sets on the side stream during the current step:
     results are bit-identical to building each index at the start of its own step (graph and
-    eager replays, a predict between, a step that prefetches nothing)."""
+    eager replays, a predict between, a step that prefetches nothing).  mid=1: the step in two
+    launches with the prefetch released between them (DLAMD_PF_MID)."""
     monkeypatch.setenv("DLAMD_PF_DEPTH", str(depth))
+    monkeypatch.setenv("DLAMD_PF_MID", str(mid))
     kw = CASES[name]
     model = _model(name)
     spec = ModelSpec(model, **kw)
