@@ -121,7 +121,8 @@ enum { S3_STORE = 0, S3_RELU = 1, S3_MASK = 2, S3_MASKBITS = 3 };
 #define DL_S3_DIAG 0   // diagnostics builds: 1 = no epilogue stores, 2 = no MFMAs either;
                        // 3 = no stores, no A loads (constant A); 4 = no stores, no B LDS reads;
                        // 5 = no stores, no per-chunk barrier; 6 = no plane split (A in NT, both
-                       // operands in TN2: the f32 bits taken as planes) (results wrong: timing only)
+                       // operands in TN2: the f32 bits taken as planes); 7 = NT A pieces at k = 32c + 4kq
+                       // and + 16 (results wrong: timing only)
 #endif
 
 // ---------------------------------------------------------------------------- NT
@@ -213,14 +214,17 @@ __global__ __launch_bounds__(512) void gemm_s3_nt_kernel(S3Params p) {
       ra[0] = ra[1] = ra[2] = ra[3] = make_float4(1.f + c, 2.f, 3.f, 4.f);
       return;
     }
-    const int k = 32 * c + 8 * kq;
+    // DL_S3_DIAG 7 (timing only): the pieces at k = 32c + 4kq and + 16, so each instruction
+    // reads one contiguous 64-B half line per row instead of four 16-B pieces of a whole line
+    const int k = DL_S3_DIAG == 7 ? 32 * c + 4 * kq : 32 * c + 8 * kq;
+    const uint32_t d2 = DL_S3_DIAG == 7 ? 64u : 16u;
     const bool kin = k < p.K;
     const uint32_t o0 = ok0 && kin ? a_off0 + 4u * k : 0x80000000u;
     const uint32_t o1 = ok1 && kin ? a_off1 + 4u * k : 0x80000000u;
     ra[0] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(a_rsrc, (int)o0, 0, 0));
-    ra[1] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(a_rsrc, (int)(o0 + 16u), 0, 0));
+    ra[1] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(a_rsrc, (int)(o0 + d2), 0, 0));
     ra[2] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(a_rsrc, (int)o1, 0, 0));
-    ra[3] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(a_rsrc, (int)(o1 + 16u), 0, 0));
+    ra[3] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(a_rsrc, (int)(o1 + d2), 0, 0));
   };
 
   floatx4 acc[2][kNtNF];
@@ -339,7 +343,7 @@ __global__ __launch_bounds__(512) void gemm_s3_nt_kernel(S3Params p) {
   }
   if (c < KC) step(c, raA);
 
-  if (DL_S3_DIAG && DL_S3_DIAG != 6) {   // keep the loop's results live without storing them
+  if (DL_S3_DIAG && DL_S3_DIAG != 6 && DL_S3_DIAG != 7) {   // keep the loop's results live without storing them
     float tt = 0.f;
 #pragma unroll
     for (int a = 0; a < 2; ++a)

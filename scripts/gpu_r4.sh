@@ -57,13 +57,25 @@ if [ "$MODE" = hosttrace ]; then
   python scripts/host_timeline.py "$k" "$a" > $OUT/host_timeline_$WL.txt; rc=$?
   head -30 $OUT/host_timeline_$WL.txt; exit $rc
 fi
+if [ "$MODE" = s3d7 ]; then
+  # the NT kernels' A pieces as contiguous 64-B half lines (diag 7, timing only) against the default
+  for rep in 1 2; do
+    for v in "" diag7; do
+      for c in fwd_l0 fwd_l1 dx_l1; do
+        DLAMD_VARIANT=$v timeout -k 10 120 python scripts/s3_bench.py 30 t:$c 2>&1 | grep -v amdgpu.ids | sed "s/^/[${v:-default}] /" | tee -a $OUT/d7.txt || exit 1
+      done
+    done
+  done
+  exit 0
+fi
 if [ "$MODE" = pfmid ]; then
   # the step in two launches with the prefetch released between them: bit-identity, A/B, trace
   timeout -k 10 300 python -u -m pytest tests/test_gpu_parity.py -m gpu -q -rf -k prefetch_matches \
     -p no:cacheprovider --timeout 200 --timeout-method thread > $OUT/pytest_pfmid.log 2>&1
   rc=$?; echo "pytest rc=$rc: $(tail -1 $OUT/pytest_pfmid.log)"; [ $rc -eq 0 ] || { grep -E "^(FAILED|ERROR)" $OUT/pytest_pfmid.log; exit $rc; }
-  for rep in 1 2; do
-    for cfg in c5:0 c5:1 c2:0 c2:1; do
+  for rep in 1 2 3; do
+    cfgs="c5:0 c5:1 c2:0 c2:1"; [ $rep -eq 3 ] && cfgs="c3:0 c3:1"
+    for cfg in $cfgs; do
       IFS=: read wl e <<< "$cfg"
       DLAMD_PF_MID=$e timeout -k 10 300 python bench.py --no-cpu-baseline --no-extra --workload $wl \
         --steps 20 --warmup 5 > $OUT/mid_${wl}_$e.json 2> $OUT/mid_${wl}_$e.err || { tail -5 $OUT/mid_${wl}_$e.err; exit 1; }
