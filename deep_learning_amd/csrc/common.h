@@ -154,6 +154,21 @@ __device__ __forceinline__ void adam_elem_sparse(float& p, float& m, float& v, f
 // construction: every path applies this one function of (p, m, s, g), and g == 0 selects
 // the zero form wherever it arises (a replayed step, an untouched row of the sweep, a touched
 // row whose summed gradient is exactly 0).
+// s3 weight planes (gemm_s3.hip NT kernels; written by dl_split3 and dl_adam_dense_split3):
+// with DL_S3_KPERM the k index of every whole 32-deep chunk is stored permuted, so that lane
+// group kq's eight bf16 (positions 8kq .. 8kq+7) hold k = 4kq .. 4kq+3 and 16+4kq .. 16+4kq+3:
+// the NT kernel then reads A as two contiguous 64-B half lines per row per chunk (four lane
+// groups x 16 B) instead of one whole line in four 16-B pieces per instruction.  A trailing
+// partial chunk (K % 32 != 0) stays in natural order.  K = the planes' row length.
+#ifndef DL_S3_KPERM
+#define DL_S3_KPERM 0
+#endif
+__host__ __device__ __forceinline__ int s3_kpos(int k, int K) {
+  if (!DL_S3_KPERM || (k | 31) >= K) return k;
+  const int kk = k & 31;
+  return (k & ~31) | (kk < 16 ? 8 * (kk >> 2) + (kk & 3) : 8 * ((kk - 16) >> 2) + 4 + (kk & 3));
+}
+
 // DL_ROOT_STATE=0 (A/B builds only: the host's adam_state conversions assume the root form)
 // keeps TF's v in the tables as before.
 #ifndef DL_ROOT_STATE

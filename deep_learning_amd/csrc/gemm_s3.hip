@@ -214,10 +214,12 @@ __global__ __launch_bounds__(512) void gemm_s3_nt_kernel(S3Params p) {
       ra[0] = ra[1] = ra[2] = ra[3] = make_float4(1.f + c, 2.f, 3.f, 4.f);
       return;
     }
-    // DL_S3_DIAG 7 (timing only): the pieces at k = 32c + 4kq and + 16, so each instruction
-    // reads one contiguous 64-B half line per row instead of four 16-B pieces of a whole line
-    const int k = DL_S3_DIAG == 7 ? 32 * c + 4 * kq : 32 * c + 8 * kq;
-    const uint32_t d2 = DL_S3_DIAG == 7 ? 64u : 16u;
+    // DL_S3_KPERM (common.h s3_kpos): a whole chunk's pieces at k = 32c + 4kq and + 16, so
+    // each instruction reads one contiguous 64-B half line per row instead of four 16-B pieces
+    // of a whole line (DL_S3_DIAG 7: the same loads against natural-order planes, timing only)
+    const bool perm = (DL_S3_KPERM || DL_S3_DIAG == 7) && 32 * c + 32 <= p.K;
+    const int k = perm ? 32 * c + 4 * kq : 32 * c + 8 * kq;
+    const uint32_t d2 = perm ? 64u : 16u;
     const bool kin = k < p.K;
     const uint32_t o0 = ok0 && kin ? a_off0 + 4u * k : 0x80000000u;
     const uint32_t o1 = ok1 && kin ? a_off1 + 4u * k : 0x80000000u;
@@ -916,7 +918,8 @@ __global__ __launch_bounds__(256) void split3_kernel(const float* __restrict__ s
     const int r = (int)(i / cols), c = (int)(i % cols);
     uint32_t h, m, l;
     split2(src[(long long)r * lds + c], 0.f, h, m, l);
-    const long long o = transpose ? (long long)c * ldd + r : (long long)r * ldd + c;
+    // the k index (the planes' row position) in the NT kernels' order (common.h s3_kpos)
+    const long long o = transpose ? (long long)c * ldd + s3_kpos(r, rows) : (long long)r * ldd + s3_kpos(c, cols);
     dst[o] = (unsigned short)h;
     dst[plane + o] = (unsigned short)m;
     dst[2 * plane + o] = (unsigned short)l;
@@ -926,6 +929,8 @@ __global__ __launch_bounds__(256) void split3_kernel(const float* __restrict__ s
 }  // namespace dl
 
 using namespace dl;
+
+extern "C" int32_t dl_s3_kperm(void) { return DL_S3_KPERM; }
 
 extern "C" int dl_split3(const float* src, int32_t rows, int32_t cols, int32_t lds, int32_t transpose,
                          uint16_t* dst, int32_t ldd, int64_t plane_stride, void* stream) {

@@ -160,8 +160,9 @@ __global__ __launch_bounds__(256) void adam_dense_thread_kernel(float* __restric
       unsigned short h, mm, l;
       split3_one(pi, h, mm, l);
       const int r = (int)(i / so.cols), c = (int)(i - (long long)r * so.cols);
-      so.wp[i] = h; so.wp[plane + i] = mm; so.wp[2 * plane + i] = l;
-      const long long t = (long long)c * so.rows + r;
+      const long long w = (long long)r * so.cols + s3_kpos(c, so.cols);   // dl_split3's layouts
+      so.wp[w] = h; so.wp[plane + w] = mm; so.wp[2 * plane + w] = l;
+      const long long t = (long long)c * so.rows + s3_kpos(r, so.rows);
       so.wtp[t] = h; so.wtp[plane + t] = mm; so.wtp[2 * plane + t] = l;
     } else if (NPL == 1) {
       const unsigned short h = f2bf(pi);

@@ -292,7 +292,11 @@ int dl_gemm_bf16(int32_t ta, int32_t tb, int32_t M, int32_t N, int32_t K, const 
  * Replaces dl_gemm_f32 for deepfm_pipeline.py:150-152 and its gradients.
  *
  * dl_split3: planes of src [rows][cols] (ld lds) at dst + q * plane_stride (q = 0 hi,
- *   1 mid, 2 lo), [r][c] with ld ldd, or [c][r] when `transpose`.
+ *   1 mid, 2 lo), [r][c] with ld ldd, or [c][r] when `transpose`.  In a library built with
+ *   DL_S3_KPERM (dl_s3_kperm() == 1) the k index (the row position: c, or r when transposed;
+ *   K = cols, or rows) of every whole 32-deep chunk is stored permuted — position
+ *   8q + j (j < 4) holds k = 4q + j, position 8q + 4 + j holds k = 16 + 4q + j — the order
+ *   dl_gemm_s3_nt reads; a trailing partial chunk keeps natural order.
  * dl_gemm_s3_nt: C[M][N] = A[M][K] . B[N][K]^T (+ epilogue: 0 store, 1 ReLU, 2 mask
  *   (C = mask[i][j] > 0 ? C : 0, mask f32 with ld ldm)); A f32 (lda % 4 == 0, 16-B
  *   aligned), B as planes from dl_split3 (ldb % 8 == 0, plane stride b_plane); K % 8 == 0.
@@ -301,6 +305,7 @@ int dl_gemm_bf16(int32_t ta, int32_t tb, int32_t M, int32_t N, int32_t K, const 
  *   splits of ceil(K / splits) rounded up to 64 rows (ceil(K / that) slabs). */
 int dl_split3(const float* src, int32_t rows, int32_t cols, int32_t lds, int32_t transpose, uint16_t* dst,
               int32_t ldd, int64_t plane_stride, void* stream);
+int32_t dl_s3_kperm(void);
 int dl_gemm_s3_nt(int32_t M, int32_t N, int32_t K, const float* A, int32_t lda, const uint16_t* B,
                   int32_t ldb, int64_t b_plane, float* C, int32_t ldc, int32_t epi, const float* mask,
                   int32_t ldm, void* stream);

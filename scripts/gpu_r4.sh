@@ -58,15 +58,21 @@ if [ "$MODE" = hosttrace ]; then
   head -30 $OUT/host_timeline_$WL.txt; exit $rc
 fi
 if [ "$MODE" = s3d7 ]; then
-  # the NT kernels' A pieces as contiguous 64-B half lines (diag 7, timing only) against the default
+  # the NT kernels' A pieces as contiguous 64-B half lines: the k-permuted planes (variant kp,
+  # DL_S3_KPERM=1) through the s3 kernel and tower tests, then kernel times default / diag 7
+  # (timing only) / kp, then C2 and C3 step A/B
+  DLAMD_VARIANT=kp timeout -k 10 400 python -u -m pytest tests/test_gpu_kernels.py tests/test_gpu_parity.py -m gpu -q -rf \
+    -k "s3 or split3 or deepfm_pipeline" -p no:cacheprovider --timeout 200 --timeout-method thread > $OUT/pytest_kp.log 2>&1
+  rc=$?; echo "pytest kp rc=$rc: $(tail -1 $OUT/pytest_kp.log)"; [ $rc -eq 0 ] || { grep -E "^(FAILED|ERROR)" $OUT/pytest_kp.log; exit $rc; }
   for rep in 1 2; do
-    for v in "" diag7; do
+    for v in "" diag7 kp; do
       for c in fwd_l0 fwd_l1 dx_l1; do
         DLAMD_VARIANT=$v timeout -k 10 120 python scripts/s3_bench.py 30 t:$c 2>&1 | grep -v amdgpu.ids | sed "s/^/[${v:-default}] /" | tee -a $OUT/d7.txt || exit 1
       done
     done
   done
-  exit 0
+  bash scripts/gpu_ab_variant.sh ${TAG}_kp kp "" "" "c2 c3"
+  exit $?
 fi
 if [ "$MODE" = pfmid ]; then
   # the step in two launches with the prefetch released between them: bit-identity, A/B, trace

@@ -165,7 +165,25 @@ def test_split3_is_exact(hip_lib):
     assert torch.equal(back, W)
     assert torch.equal(f(P[0]), W.bfloat16().float())
     PT = _planes(W, True).view(3, 24, 37)
-    assert torch.equal(PT[0], P[0].t())
+    # the transposed layout's rows have K = 37 (one whole 32-deep chunk): natural order back
+    pos = torch.tensor([_s3_kpos(k, 37) for k in range(37)], device="cuda")
+    assert torch.equal(PT[0][:, pos], P[0].t())
+    # a whole-chunk row length in both layouts: K = 64 (W^T rows) and 96 (W rows)
+    W2 = (torch.randn(64, 96, generator=g)).cuda()
+    P2 = _planes(W2, False).view(3, 64, 96)
+    PT2 = _planes(W2, True).view(3, 96, 64)
+    p96 = torch.tensor([_s3_kpos(k, 96) for k in range(96)], device="cuda")
+    p64 = torch.tensor([_s3_kpos(k, 64) for k in range(64)], device="cuda")
+    assert torch.equal(P2[:, :, p96][0], PT2[:, :, p64][0].t())
+    assert torch.equal(f(P2[0][:, p96]), W2.bfloat16().float())
+
+
+def _s3_kpos(k, K):
+    """Position of k in a plane row of length K (include/dlamd.h dl_split3, DL_S3_KPERM)."""
+    if not _lib.lib().dl_s3_kperm() or (k | 31) >= K:
+        return k
+    kk = k & 31
+    return (k & ~31) | (8 * (kk >> 2) + (kk & 3) if kk < 16 else 8 * ((kk - 16) >> 2) + 4 + (kk & 3))
 
 
 @pytest.mark.parametrize("epi", [0, 1, 2])
