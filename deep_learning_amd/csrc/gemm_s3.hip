@@ -930,7 +930,7 @@ __global__ __launch_bounds__(256) void split3_kernel(const float* __restrict__ s
 
 using namespace dl;
 
-extern "C" int32_t dl_s3_kperm(void) { return DL_S3_KPERM; }
+extern "C" int dl_s3_kperm(void) { return DL_S3_KPERM; }
 
 extern "C" int dl_split3(const float* src, int32_t rows, int32_t cols, int32_t lds, int32_t transpose,
                          uint16_t* dst, int32_t ldd, int64_t plane_stride, void* stream) {

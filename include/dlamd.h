@@ -305,7 +305,7 @@ int dl_gemm_bf16(int32_t ta, int32_t tb, int32_t M, int32_t N, int32_t K, const 
  *   splits of ceil(K / splits) rounded up to 64 rows (ceil(K / that) slabs). */
 int dl_split3(const float* src, int32_t rows, int32_t cols, int32_t lds, int32_t transpose, uint16_t* dst,
               int32_t ldd, int64_t plane_stride, void* stream);
-int32_t dl_s3_kperm(void);
+int dl_s3_kperm(void);
 int dl_gemm_s3_nt(int32_t M, int32_t N, int32_t K, const float* A, int32_t lda, const uint16_t* B,
                   int32_t ldb, int64_t b_plane, float* C, int32_t ldc, int32_t epi, const float* mask,
                   int32_t ldm, void* stream);
