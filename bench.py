@@ -409,6 +409,8 @@ def _run_workload(wl, args, world, rank, sharded, steps, warmup, age, ksteps, ba
     log("%s: timed %d steps" % (wl, steps))
     barrier()
     torch.cuda.synchronize()
+    if os.environ.get("DLAMD_STEP_EVENTS", "0") == "1":   # the compute stream's span / gap per step
+        eng.step_events = []
     t0 = time.perf_counter()
     w0 = getattr(eng, "host_wait", 0.0)
     for i in range(base, base + steps):
@@ -420,6 +422,16 @@ def _run_workload(wl, args, world, rank, sharded, steps, warmup, age, ksteps, ba
     barrier()
     dt = time.perf_counter() - t0
     base += steps
+    step_ev = None
+    if getattr(eng, "step_events", None):
+        ev, eng.step_events = eng.step_events, None
+        starts = [e for k, e in ev if k == 0]
+        ends = [e for k, e in ev if k == 1]
+        span = [a.elapsed_time(b) for a, b in zip(starts, ends)]
+        gap = [b.elapsed_time(a) for b, a in zip(ends, starts[1:])]
+        step_ev = {"span_ms": round(sum(span) / len(span), 4), "gap_ms": round(sum(gap) / max(1, len(gap)), 4),
+                   "gap_max_ms": round(max(gap, default=0.0), 4)}
+        log("%s: step span %.4f ms, gap to the next step %.4f ms" % (wl, step_ev["span_ms"], step_ev["gap_ms"]))
     if world > 1:
         import torch.distributed as dist
         tt = torch.tensor([dt], device="cuda", dtype=torch.float64)
@@ -524,7 +536,8 @@ def _run_workload(wl, args, world, rank, sharded, steps, warmup, age, ksteps, ba
             if gather is not None:
                 gather["lookup_alone"] = gather_lookup
     out = dict(spec=spec, value=value, ms=ms, loss=loss, roofline=roof, gather=gather, flush=flush, kernels=kernels,
-               kernel_sum=sum(k["us"] for k in kernels.values()), nb=nb, gemm_peak=gemm_peak, host_ms=host_ms)
+               kernel_sum=sum(k["us"] for k in kernels.values()), nb=nb, gemm_peak=gemm_peak, host_ms=host_ms,
+               step_events=step_ev)
     del eng, batches
     torch.cuda.synchronize()
     torch.cuda.empty_cache()
@@ -730,6 +743,7 @@ def main():
             "kernels": r["kernels"],
             "kernel_sum_us_per_step": round(r["kernel_sum"], 1),
             "host_submit_ms_per_step": round(r["host_ms"], 4),
+            **({"step_events": r["step_events"]} if r.get("step_events") else {}),
             "loss": round(r["loss"], 6),
             "extra_workloads": extra or None,
         }

@@ -1281,6 +1281,15 @@ class CTREngine:
             self._pf = None
         return (self.stage(batch) if batch is not None else self.B), False
 
+    def _step_mark(self, end):
+        """bench.py (DLAMD_STEP_EVENTS=1): timing events on the compute stream around each step's
+        launches — the step's own span, and the gap to the next step's start (waits included)."""
+        ev = getattr(self, "step_events", None)
+        if ev is not None:
+            e = torch.cuda.Event(enable_timing=True)
+            e.record()
+            ev.append((end, e))
+
     def _release(self):
         """Mark the current buffer set free once the compute stream's queued work is done."""
         if getattr(self, "_slots", None) is not None:
@@ -1309,6 +1318,7 @@ class CTREngine:
         # released between them — beside the embedding backward, not the tower GEMMs
         pf_mid = bool(ahead) and not pf_after and os.environ.get("DLAMD_PF_MID", "0") == "1"
         if pf_mid:
+            self._step_mark(0)
             for part in ("front", "back"):
                 if graph:
                     key = (getattr(self, "_cur", 0), B, not indexed, part)
@@ -1323,6 +1333,7 @@ class CTREngine:
                     mid.record()
                     for nb in ahead:
                         self.prefetch(nb, graph=pf_graph, after=mid)
+            self._step_mark(1)
             self._release()
             self._queue_status()
             self.steps += 1
@@ -1331,6 +1342,7 @@ class CTREngine:
         if not pf_after:
             for nb in ahead:
                 self.prefetch(nb, graph=pf_graph)
+        self._step_mark(0)
         if graph:
             # one graph per (buffer set, batch size, index built inside or prefetched)
             key = (getattr(self, "_cur", 0), B, not indexed)
@@ -1340,6 +1352,7 @@ class CTREngine:
             g.replay()
         else:
             self._train(B)
+        self._step_mark(1)
         self._release()
         if pf_after:
             for nb in ahead:

@@ -83,11 +83,11 @@ if [ "$MODE" = pfmid ]; then
     cfgs="c5:0 c5:1 c2:0 c2:1"; [ $rep -eq 3 ] && cfgs="c3:0 c3:1"
     for cfg in $cfgs; do
       IFS=: read wl e <<< "$cfg"
-      DLAMD_PF_MID=$e timeout -k 10 300 python bench.py --no-cpu-baseline --no-extra --workload $wl \
+      DLAMD_STEP_EVENTS=1 DLAMD_PF_MID=$e timeout -k 10 300 python bench.py --no-cpu-baseline --no-extra --workload $wl \
         --steps 20 --warmup 5 > $OUT/mid_${wl}_$e.json 2> $OUT/mid_${wl}_$e.err || { tail -5 $OUT/mid_${wl}_$e.err; exit 1; }
       python -c "
 import json;d=json.loads(open('$OUT/mid_${wl}_$e.json').read().strip().splitlines()[-1])
-print('$wl pf_mid=$e', d['ms_per_step'], 'host', d.get('host_submit_ms_per_step'))"
+print('$wl pf_mid=$e', d['ms_per_step'], 'host', d.get('host_submit_ms_per_step'), 'events', d.get('step_events'))"
     done
   done
   DLAMD_PF_MID=1 bash scripts/gpu_r4.sh trace ${TAG}_mid c5 && DLAMD_PF_MID=1 bash scripts/gpu_r4.sh trace ${TAG}_mid c2

@@ -265,7 +265,7 @@ def test_wdl_bf16_tower_tracks_oracle(hip_lib, adam):
                                                  ("deepfm_multi_cate", "lazy", 1, 0), ("wdl", "lazy", 1, 0),
                                                  ("deepfm_pipeline", "lazy", 2, 0), ("wdl", "lazy", 2, 0),
                                                  ("deepfm_pipeline", "lazy", 1, 1), ("wdl", "lazy", 1, 1),
-                                                 ("deepfm_multi_cate", "dense", 2, 1)])
+                                                 ("deepfm_multi_cate", "lazy", 2, 1)])
 def test_prefetch_matches_inline_index(hip_lib, name, adam, depth, mid, monkeypatch):
     """train_step(next_batch=...) stages and indexes the next batch (depth 2: the next two,
     three buffer sets) into idle buffer sets on the side stream during the current step:
