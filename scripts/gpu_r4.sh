@@ -93,6 +93,23 @@ print('$wl pf_mid=$e', d['ms_per_step'], 'host', d.get('host_submit_ms_per_step'
   DLAMD_PF_MID=1 bash scripts/gpu_r4.sh trace ${TAG}_mid c5 && DLAMD_PF_MID=1 bash scripts/gpu_r4.sh trace ${TAG}_mid c2
   exit $?
 fi
+if [ "$MODE" = pfmid2 ]; then
+  # prefetch depth x release point (d1m0 = the default): step time and the event span / gap
+  for rep in 1 2 3; do
+    wls="c5 c2"; [ $rep -eq 3 ] && wls="c3"
+    for wl in $wls; do
+      for cfg in 1:0 2:1 2:0; do
+        IFS=: read dp e <<< "$cfg"
+        DLAMD_STEP_EVENTS=1 DLAMD_PF_DEPTH=$dp DLAMD_PF_MID=$e timeout -k 10 300 python bench.py --no-cpu-baseline --no-extra \
+          --workload $wl --steps 30 --warmup 5 > $OUT/m2_${wl}_$dp$e.json 2> $OUT/m2_${wl}_$dp$e.err || { tail -5 $OUT/m2_${wl}_$dp$e.err; exit 1; }
+        python -c "
+import json;d=json.loads(open('$OUT/m2_${wl}_$dp$e.json').read().strip().splitlines()[-1])
+print('$wl depth=$dp mid=$e', d['ms_per_step'], 'host', d.get('host_submit_ms_per_step'), 'events', d.get('step_events'))"
+      done
+    done
+  done
+  exit 0
+fi
 if [ "$MODE" = combo ]; then
   # quick, then an A/B of a library variant ($3) on C2 and C3
   bash scripts/gpu_r4.sh quick $TAG || exit $?
