@@ -93,6 +93,20 @@ print('$wl pf_mid=$e', d['ms_per_step'], 'host', d.get('host_submit_ms_per_step'
   DLAMD_PF_MID=1 bash scripts/gpu_r4.sh trace ${TAG}_mid c5 && DLAMD_PF_MID=1 bash scripts/gpu_r4.sh trace ${TAG}_mid c2
   exit $?
 fi
+if [ "$MODE" = cores ]; then
+  # the index build's kernels sized to share a CU with the forward NT GEMM block (LDS <= 43 KB,
+  # VGPR <= 112): radix tiles of 14 / 12 rounds (and pre-materialised keys); sort tests per
+  # variant, then step A/B on C2, C3, C5
+  for v in r14 r12 r12pk; do
+    DLAMD_VARIANT=$v timeout -k 10 300 python -u -m pytest tests/test_gpu_kernels.py tests/test_gpu_parity.py -m gpu -q -rf \
+      -k "index or sort_unique or prefetch_matches" -p no:cacheprovider --timeout 200 --timeout-method thread > $OUT/pytest_$v.log 2>&1
+    rc=$?; echo "pytest $v rc=$rc: $(tail -1 $OUT/pytest_$v.log)"; [ $rc -eq 0 ] || { grep -E "^(FAILED|ERROR)" $OUT/pytest_$v.log; exit $rc; }
+  done
+  for v in r14 r12 r12pk; do
+    bash scripts/gpu_ab_variant.sh ${TAG}_$v $v "" "" "c2 c5 c3" || exit $?
+  done
+  exit 0
+fi
 if [ "$MODE" = pfmid2 ]; then
   # prefetch depth x release point (d1m0 = the default): step time and the event span / gap
   for rep in 1 2 3; do
