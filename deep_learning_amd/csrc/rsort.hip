@@ -20,9 +20,18 @@ constexpr int kRsWaves = kRsThreads / 64;
 #ifndef DL_RS_ROUNDS
 #define DL_RS_ROUNDS 16
 #endif
-constexpr int kRsRounds = DL_RS_ROUNDS;                      // elements per lane
-constexpr int kRsTile = kRsThreads * kRsRounds;              // 4096 elements per tile
-constexpr int kRsWaveSpan = 64 * kRsRounds;                  // consecutive elements per wave
+// Elements per lane (a tile = 256 R elements).  Sorts of at least kRsBigN references use
+// R = 12 with the keys materialised first (rs_keys_kernel): the downsweep then takes 36.9 KB of
+// LDS and 68 VGPRs, so its blocks fit beside a forward s3 GEMM block on a CU (120 KB LDS,
+// 2 x 200 VGPRs a SIMD) instead of holding CUs the GEMM's second round waits for
+// (C3 4.43 -> 4.30 ms, C5 1.44 -> 1.41 ms; C2's 1.7 M-reference sort keeps R = 16:
+// profiles/r04z/).
+constexpr int kRsRounds = DL_RS_ROUNDS;
+constexpr int kRsRoundsBig = 12;
+#ifndef DL_RS_BIGN
+#define DL_RS_BIGN (2LL << 20)
+#endif
+constexpr int64_t kRsBigN = DL_RS_BIGN;
 #ifndef DL_RS_MAXBITS
 #define DL_RS_MAXBITS 9
 #endif
@@ -31,8 +40,8 @@ constexpr int kRsMaxRadix = 1 << kRsMaxBits;
 constexpr int kLocal = 27;
 constexpr uint32_t kRsNoKey = 0xFFFFFFFFu;   // rs_keys_kernel: a reference without a key
 #ifndef DL_RS_PREKEYS
-#define DL_RS_PREKEYS 0   // 1: the index build's keys materialised first by rs_keys_kernel (alone C3 956 -> 886 us,
-#endif                    // C2 257 -> 246 us; in the step slower by 7-20 us: profiles/r03pk/)
+#define DL_RS_PREKEYS 0   // 1: keys materialised first by rs_keys_kernel at every size (always done from kRsBigN
+#endif                    // on; below it, C2: alone 257 -> 246 us, in the step 7-20 us slower: profiles/r03pk/)
 
 struct RsPass {
   int shift, bits;
@@ -126,9 +135,10 @@ __device__ __forceinline__ long long rs_count(const RsPass& p) {
   return p.first ? p.n_max : (long long)min((long long)*p.n_dev, p.n_max);
 }
 
-template <int MODE>
+template <int MODE, int R>
 __global__ __launch_bounds__(kRsThreads) void rs_upsweep(RsSource src, RsPass p, int32_t* __restrict__ counts,
                                                          int tiles) {
+  constexpr int kRsTile = kRsThreads * R;
   __shared__ int hist[kRsMaxRadix];
   const int radix = 1 << p.bits;
   for (int d = threadIdx.x; d < radix; d += kRsThreads) hist[d] = 0;
@@ -136,17 +146,17 @@ __global__ __launch_bounds__(kRsThreads) void rs_upsweep(RsSource src, RsPass p,
   const long long n = rs_count(p);
   const long long t0 = (long long)blockIdx.x * kRsTile;
   // every load of the tile first (one memory round trip), then the histogram
-  uint32_t key[kRsRounds];
-  bool ok[kRsRounds];
+  uint32_t key[R];
+  bool ok[R];
 #pragma unroll
-  for (int r = 0; r < kRsRounds; ++r) {
+  for (int r = 0; r < R; ++r) {
     const long long e = t0 + r * kRsThreads + threadIdx.x;   // coalesced: counting needs no order
     int32_t val;
     ok[r] = rs_get<MODE>(src, p, e, n, true, key[r], val);
     if (MODE == 2 && !ok[r] && e < n && src.inv) src.inv[e] = -1;
   }
 #pragma unroll
-  for (int r = 0; r < kRsRounds; ++r)
+  for (int r = 0; r < R; ++r)
     if (ok[r]) atomicAdd(&hist[rs_digit(key[r], p)], 1);
   __syncthreads();
   for (int d = threadIdx.x; d < radix; d += kRsThreads) counts[(long long)d * tiles + blockIdx.x] = hist[d];
@@ -193,11 +203,12 @@ __global__ __launch_bounds__(kRsThreads) void rs_rowscan(int32_t* __restrict__ c
   if (threadIdx.x == 0) total[blockIdx.x] = all;
 }
 
-template <int MODE>
+template <int MODE, int R>
 __global__ __launch_bounds__(kRsThreads) void rs_downsweep(RsSource src, RsPass p, const int32_t* __restrict__ counts,
                                                            int tiles, const int32_t* __restrict__ total,
                                                            uint32_t* __restrict__ kout, int32_t* __restrict__ vout,
                                                            int32_t* __restrict__ n_valid) {
+  constexpr int kRsTile = kRsThreads * R, kRsWaveSpan = 64 * R;   // tile; consecutive elements per wave
   __shared__ int cnt[kRsWaves][kRsMaxRadix];   // per-wave running counts, then per-wave prefixes
   __shared__ int tstart[kRsMaxRadix];          // the tile's digit starts (exclusive scan over digits)
   __shared__ int gbase[kRsMaxRadix];           // global position of the tile's first element of each digit
@@ -209,14 +220,14 @@ __global__ __launch_bounds__(kRsThreads) void rs_downsweep(RsSource src, RsPass 
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const long long n = rs_count(p);
   const long long e0 = (long long)blockIdx.x * kRsTile + (long long)w * kRsWaveSpan;
-  uint32_t key[kRsRounds];
-  int32_t val[kRsRounds];
-  int rank[kRsRounds];
+  uint32_t key[R];
+  int32_t val[R];
+  int rank[R];
   const uint64_t lt = (1ull << lane) - 1;
   // every load of the wave's 1024 elements first (one memory round trip)
   uint32_t okm = 0;
 #pragma unroll
-  for (int r = 0; r < kRsRounds; ++r)
+  for (int r = 0; r < R; ++r)
     okm |= rs_get<MODE>(src, p, e0 + r * 64 + lane, n, false, key[r], val[r]) ? (1u << r) : 0u;
   for (int i = tid; i < kRsWaves * kRsMaxRadix; i += kRsThreads) (&cnt[0][0])[i] = 0;
   // digit starts from the totals (each thread scans two digits' worth)
@@ -233,7 +244,7 @@ __global__ __launch_bounds__(kRsThreads) void rs_downsweep(RsSource src, RsPass 
   for (int d = tid; d < radix; d += kRsThreads) gbase[d] += counts[(long long)d * tiles + blockIdx.x];
   // per-wave stable ranks: rounds in element order, lanes in element order within a round
 #pragma unroll
-  for (int r = 0; r < kRsRounds; ++r) {
+  for (int r = 0; r < R; ++r) {
     const bool ok = (okm >> r) & 1;
     const int d = ok ? rs_digit(key[r], p) : 0;
     uint64_t peers = __ballot(ok);
@@ -276,7 +287,7 @@ __global__ __launch_bounds__(kRsThreads) void rs_downsweep(RsSource src, RsPass 
   __syncthreads();
   // stage the tile in digit order
 #pragma unroll
-  for (int r = 0; r < kRsRounds; ++r) {
+  for (int r = 0; r < R; ++r) {
     if (rank[r] >= 0) {
       const int d = rs_digit(key[r], p);
       const int lp = tstart[d] + cnt[w][d] + rank[r];
@@ -298,12 +309,32 @@ __global__ __launch_bounds__(kRsThreads) void rs_downsweep(RsSource src, RsPass 
 
 static size_t rs_align(size_t x) { return (x + 255) & ~(size_t)255; }
 
-static int rs_tiles(int64_t n) { return (int)((n + kRsTile - 1) / kRsTile); }
+static int rs_rounds(int64_t n) { return n >= kRsBigN ? kRsRoundsBig : kRsRounds; }
+static int rs_tiles(int64_t n) { return (int)((n + kRsThreads * rs_rounds(n) - 1) / (kRsThreads * rs_rounds(n))); }
 
 size_t rsort_workspace_bytes(int64_t n) {
   if (n < 1) n = 1;
   const int tiles = rs_tiles(n);
   return 2 * rs_align((size_t)n * 4) + rs_align((size_t)kRsMaxRadix * tiles * 4) + rs_align(kRsMaxRadix * 4);
+}
+
+// one pass: tile histograms, their scan per digit, the stable scatter
+template <int R>
+static void rs_pass(int mode, const RsSource& src, const RsPass& p, int32_t* counts, int tiles, int32_t* total, int pb,
+                    uint32_t* ko, int32_t* vo, int32_t* n_valid, hipStream_t s) {
+  if (mode == 0) hipLaunchKernelGGL((rs_upsweep<0, R>), dim3(tiles), dim3(kRsThreads), 0, s, src, p, counts, tiles);
+  else if (mode == 1) hipLaunchKernelGGL((rs_upsweep<1, R>), dim3(tiles), dim3(kRsThreads), 0, s, src, p, counts, tiles);
+  else if (mode == 2) hipLaunchKernelGGL((rs_upsweep<2, R>), dim3(tiles), dim3(kRsThreads), 0, s, src, p, counts, tiles);
+  else hipLaunchKernelGGL((rs_upsweep<3, R>), dim3(tiles), dim3(kRsThreads), 0, s, src, p, counts, tiles);
+  hipLaunchKernelGGL(rs_rowscan, dim3(1 << pb), dim3(kRsThreads), 0, s, counts, tiles, total);
+  if (mode == 0)
+    hipLaunchKernelGGL((rs_downsweep<0, R>), dim3(tiles), dim3(kRsThreads), 0, s, src, p, counts, tiles, total, ko, vo, n_valid);
+  else if (mode == 1)
+    hipLaunchKernelGGL((rs_downsweep<1, R>), dim3(tiles), dim3(kRsThreads), 0, s, src, p, counts, tiles, total, ko, vo, n_valid);
+  else if (mode == 2)
+    hipLaunchKernelGGL((rs_downsweep<2, R>), dim3(tiles), dim3(kRsThreads), 0, s, src, p, counts, tiles, total, ko, vo, n_valid);
+  else
+    hipLaunchKernelGGL((rs_downsweep<3, R>), dim3(tiles), dim3(kRsThreads), 0, s, src, p, counts, tiles, total, ko, vo, n_valid);
 }
 
 int rsort_pairs(const RsSource& src, int64_t n, uint32_t lrange, int bits, void* ws, size_t ws_bytes,
@@ -333,7 +364,7 @@ int rsort_pairs(const RsSource& src, int64_t n, uint32_t lrange, int bits, void*
     int32_t* vo = to_out ? out_vals : tv;
     RsPass p{shift, pb, lrange, kin, vin, n_valid, n, i == 0 ? 1 : 0};
     int mode = i > 0 ? 0 : src.kind == 0 ? 1 : 2;
-    if (mode == 2 && DL_RS_PREKEYS) {
+    if (mode == 2 && (DL_RS_PREKEYS || n >= kRsBigN)) {
       // the keys into a buffer pass 0 does not write: out_keys when pass 0 lands in the
       // temporaries, else the temporary keys (the first pass's output is the outputs)
       uint32_t* pre = to_out ? tk : out_keys;
@@ -343,19 +374,10 @@ int rsort_pairs(const RsSource& src, int64_t n, uint32_t lrange, int bits, void*
       p.kin = pre;
       mode = 3;
     }
-    if (mode == 0) hipLaunchKernelGGL(rs_upsweep<0>, dim3(tiles), dim3(kRsThreads), 0, s, src, p, counts, tiles);
-    else if (mode == 1) hipLaunchKernelGGL(rs_upsweep<1>, dim3(tiles), dim3(kRsThreads), 0, s, src, p, counts, tiles);
-    else if (mode == 2) hipLaunchKernelGGL(rs_upsweep<2>, dim3(tiles), dim3(kRsThreads), 0, s, src, p, counts, tiles);
-    else hipLaunchKernelGGL(rs_upsweep<3>, dim3(tiles), dim3(kRsThreads), 0, s, src, p, counts, tiles);
-    hipLaunchKernelGGL(rs_rowscan, dim3(1 << pb), dim3(kRsThreads), 0, s, counts, tiles, total);
-    if (mode == 0)
-      hipLaunchKernelGGL(rs_downsweep<0>, dim3(tiles), dim3(kRsThreads), 0, s, src, p, counts, tiles, total, ko, vo, n_valid);
-    else if (mode == 1)
-      hipLaunchKernelGGL(rs_downsweep<1>, dim3(tiles), dim3(kRsThreads), 0, s, src, p, counts, tiles, total, ko, vo, n_valid);
-    else if (mode == 2)
-      hipLaunchKernelGGL(rs_downsweep<2>, dim3(tiles), dim3(kRsThreads), 0, s, src, p, counts, tiles, total, ko, vo, n_valid);
+    if (rs_rounds(n) == kRsRoundsBig)
+      rs_pass<kRsRoundsBig>(mode, src, p, counts, tiles, total, pb, ko, vo, n_valid, s);
     else
-      hipLaunchKernelGGL(rs_downsweep<3>, dim3(tiles), dim3(kRsThreads), 0, s, src, p, counts, tiles, total, ko, vo, n_valid);
+      rs_pass<kRsRounds>(mode, src, p, counts, tiles, total, pb, ko, vo, n_valid, s);
     kin = ko;
     vin = vo;
     shift += pb;

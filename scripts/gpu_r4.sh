@@ -107,6 +107,15 @@ if [ "$MODE" = cores ]; then
   done
   exit 0
 fi
+if [ "$MODE" = rsbig ]; then
+  # the size-chosen radix tile (12 rounds + pre-materialised keys from 2 M references) against the
+  # previous single configuration (variant old): index / sort / prefetch / wdl tests, then A/B
+  timeout -k 10 400 python -u -m pytest tests/test_gpu_kernels.py tests/test_gpu_parity.py tests/test_gpu_dropin.py -m gpu -q -rf \
+    -k "index or sort_unique or prefetch or hot or wdl or multi_cate" -p no:cacheprovider --timeout 200 --timeout-method thread > $OUT/pytest_rs.log 2>&1
+  rc=$?; echo "pytest rc=$rc: $(tail -1 $OUT/pytest_rs.log)"; [ $rc -eq 0 ] || { grep -E "^(FAILED|ERROR)" $OUT/pytest_rs.log; exit $rc; }
+  bash scripts/gpu_ab_variant.sh ${TAG}_ab old "" "" "c5 c3 c2"
+  exit $?
+fi
 if [ "$MODE" = pfmid2 ]; then
   # prefetch depth x release point (d1m0 = the default): step time and the event span / gap
   for rep in 1 2 3; do
