@@ -39,7 +39,7 @@ class PoolDesc(C.Structure):
 
 
 # include/dlamd.h constants
-OPT_LEN, OPT_STATUS, OPT_SKIP, OPT_BAD_STEP, OPT_BAD_COUNT = 32, 16, 17, 18, 19
+OPT_LEN, OPT_STATUS, OPT_SKIP, OPT_BAD_STEP, OPT_BAD_COUNT, OPT_SEQ = 32, 16, 17, 18, 19, 20
 STATUS_BAD_ID, STATUS_LAG, STATUS_INDEX = 1, 2, 4
 REC_FIRST, REC_SPARSE_ADAM = 1, 2
 ROWS_CLEAR_TOUCHED, ROWS_SPARSE_ADAM, ROWS_GRAD_FIXED = 1, 2, 4
@@ -93,7 +93,7 @@ SIGNATURES = {
     "dl_adam_begin_step": (I32, [P, F, F, P]),
     "dl_step_guard": (I32, [P, P, P]),
     "dl_step_begin": (I32, [P, P, F, F, P, I32, P]),
-    "dl_loss_accumulate": (I32, [P, I32, I32, I32, C.c_double, P, F, P, P]),
+    "dl_loss_accumulate": (I32, [P, I32, I32, I32, C.c_double, P, F, P, P, P]),
     "dl_validate_batch": (I32, [LP, P, P, I32, I32, I64, I32, P, P]),
     "dl_adam_dense": (I32, [P, P, P, P, I32, I64, I64, F, I64, P, P, P, P]),
     "dl_adam_dense_split3": (I32, [P, P, P, P, I32, I64, I32, I32, F, I64, I32, P, P, P, P, P]),

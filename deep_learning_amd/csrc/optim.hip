@@ -53,10 +53,24 @@ __global__ void step_guard_kernel(const int32_t* batch_err, float* opt) { step_g
 // double, times inv_b); acc[1] += reg_coef * opt[8] (the step's regulariser sum, accumulated by
 // the Adam kernels); acc[2] += 1.  A skipped step (bad batch) adds nothing.  One block, so the
 // step needs no host read; the host reads acc once per epoch.
+// ring (may be NULL): the step's status report into pinned host memory, in place of a
+// device-to-host copy after the step — every step (skipped ones too) advances the sequence
+// opt[DL_OPT_SEQ] to k and writes slot k & 3: [2s + 1] = the status word, then (after a
+// system-scope fence) [2s] = k, so a host that reads k there reads this step's status.
 __global__ __launch_bounds__(256) void loss_accumulate_kernel(const float* __restrict__ slab, int rows, int pitch,
-                                                              int col, double inv_b, const float* __restrict__ opt,
-                                                              float reg_coef, double* __restrict__ acc) {
+                                                              int col, double inv_b, float* __restrict__ opt,
+                                                              float reg_coef, double* __restrict__ acc,
+                                                              int32_t* __restrict__ ring) {
   __shared__ double part[256];
+  if (ring && threadIdx.x == 0) {
+    const int k = __float_as_int(opt[DL_OPT_SEQ]) + 1;
+    opt[DL_OPT_SEQ] = __int_as_float(k);
+    volatile int32_t* r = ring + 2 * (k & 3);
+    r[1] = *opt_status(opt);
+    __threadfence_system();
+    r[0] = k;
+    __threadfence_system();
+  }
   if (step_poisoned(opt)) return;
   double s = 0.0;
   for (int r = threadIdx.x; r < rows; r += blockDim.x) s += (double)slab[(long long)r * pitch + col];
@@ -390,11 +404,11 @@ extern "C" int dl_step_guard(const int32_t* batch_err, float* opt, void* stream)
 }
 
 extern "C" int dl_loss_accumulate(const float* slab, int32_t rows, int32_t pitch, int32_t col, double inv_b,
-                                  const float* opt, float reg_coef, double* acc, void* stream) {
+                                  float* opt, float reg_coef, double* acc, int32_t* status_ring, void* stream) {
   DL_CHECK_ARG(slab && opt && acc, "NULL pointer");
   DL_CHECK_ARG(rows >= 0 && pitch > col && col >= 0, "bad slab shape");
   hipLaunchKernelGGL(loss_accumulate_kernel, dim3(1), dim3(256), 0, as_stream(stream), slab, rows, pitch, col, inv_b,
-                     opt, reg_coef, acc);
+                     opt, reg_coef, acc, status_ring);
   DL_RETURN_LAUNCH("dl_loss_accumulate");
 }
 

@@ -359,6 +359,13 @@ class CTREngine:
         self._status_q = []
         self._status_host = None
         self.host_wait = 0.0
+        # DLAMD_STATUS_RING=1: the step's last kernel writes its status into pinned host memory
+        # (dl_loss_accumulate's ring) instead of a device-to-host copy after each step
+        self._ring = None
+        if os.environ.get("DLAMD_STATUS_RING", "0") == "1" and type(self) is CTREngine:
+            self._ring = torch.zeros(8, dtype=torch.int32, pin_memory=True)
+            self._ring_np = self._ring.numpy()
+            self._ring_sent = None
         # ---- activations / workspaces
         B = max_batch
         self.x0 = z(B, self.in_ld[0])
@@ -1028,7 +1035,7 @@ class CTREngine:
         width = self.head_slab.shape[1]
         coef = sp.l2 if sp.hidden_reg == "l1" else 0.5 * sp.l2
         self._c("loss_acc", "dl_loss_accumulate", ptr(self.head_slab), call_int(self.head_grid, B), width, width - 1,
-                1.0 / B, ptr(self.opt), coef, ptr(self.loss_acc), _lib.stream_handle())
+                1.0 / B, ptr(self.opt), coef, ptr(self.loss_acc), ptr(self._ring), _lib.stream_handle())
 
     def _train_body(self, B, part="all"):
         sp = self.spec
@@ -1473,6 +1480,8 @@ class CTREngine:
         memory.  Completed read-backs are checked at the next steps without waiting; at most
         two may be outstanding, so a bad batch raises within two train_step calls (TF raises
         in the failing sess.run; here the failing step itself has applied nothing)."""
+        if self._ring is not None:
+            return self._ring_status()
         every = int(os.environ.get("DLAMD_STATUS_EVERY", "1"))   # A/B: read back every N steps
         if every > 1 and self.steps % every:
             return
@@ -1495,6 +1504,35 @@ class CTREngine:
             self._status_q.pop(0)
             if int(self._status_host[k0]) != 0:
                 self._status_q.clear()
+                self.check_error()
+
+    def _ring_status(self):
+        """_queue_status from the status ring the step's last kernel writes (slot k & 3: the
+        step sequence k and its status word): reports already written are checked without
+        waiting; with more than two steps outstanding the oldest is waited for."""
+        r = self._ring_np
+        if self._ring_sent is None:   # first step: the device's sequence (this read waits for it)
+            self._ring_sent = int(self.opt.view(torch.int32)[_lib.OPT_SEQ].item())
+            self._ring_checked = self._ring_sent - 1
+        else:
+            self._ring_sent += 1
+        while self._ring_checked < self._ring_sent:
+            k = self._ring_checked + 1
+            j = 2 * (k & 3)
+            if int(r[j]) != k:
+                if self._ring_sent - self._ring_checked <= 2:
+                    break
+                t0 = time.perf_counter()
+                while int(r[j]) != k:
+                    if time.perf_counter() - t0 > 10.0:   # the sequence went out of step: resynchronise
+                        torch.cuda.synchronize()
+                        if int(r[j]) != k:
+                            self._ring_sent = None
+                            self.check_error()
+                            return
+                self.host_wait += time.perf_counter() - t0   # bench.py: host time spent ahead of the GPU
+            self._ring_checked = k
+            if int(r[j + 1]) != 0:
                 self.check_error()
 
     def _error_words(self):

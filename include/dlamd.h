@@ -389,6 +389,7 @@ int dl_slab_fold_rows(const float* slab, int32_t blocks, int32_t width, int32_t 
 #define DL_OPT_SKIP 17
 #define DL_OPT_BAD_STEP 18
 #define DL_OPT_BAD_COUNT 19
+#define DL_OPT_SEQ 20       /* int32 bits: steps reported through dl_loss_accumulate's status ring */
 #define DL_STATUS_BAD_ID 1   /* a categorical / wide id outside [0, N) */
 #define DL_STATUS_LAG 2      /* a row record lagged past the alpha ring (flush schedule broken) */
 #define DL_STATUS_INDEX 4    /* a batch-index entry out of range (index consumers report, never skip silently) */
@@ -416,9 +417,13 @@ int dl_step_begin(const int32_t* batch_err, float* opt, float decay_rate, float 
  * acc[0] += sum_r slab[r * pitch + col] * inv_b (the step's data term; double, fixed order),
  * acc[1] += reg_coef * opt[8] (the step's regulariser sum), acc[2] += 1; nothing for a skipped
  * step.  acc: double[3] on the device, read by the host once per epoch.  (Wide&Deep with lazy
- * wide records adds the wide L2 term per record step through dl_wide_rec_update / _flush acc.) */
-int dl_loss_accumulate(const float* slab, int32_t rows, int32_t pitch, int32_t col, double inv_b, const float* opt,
-                       float reg_coef, double* acc, void* stream);
+ * wide records adds the wide L2 term per record step through dl_wide_rec_update / _flush acc.)
+ * status_ring (may be NULL): int32[8] of pinned host memory; every call (skipped steps too)
+ * advances the step sequence opt[DL_OPT_SEQ] to k and writes the status word to ring[2(k & 3) + 1],
+ * then k to ring[2(k & 3)] (system-scope fence between): the host's per-step status report
+ * without a device-to-host copy. */
+int dl_loss_accumulate(const float* slab, int32_t rows, int32_t pitch, int32_t col, double inv_b, float* opt,
+                       float reg_coef, double* acc, int32_t* status_ring, void* stream);
 /* Dense parameter whose gradient is the sum of `nslab` partial slabs
  * (g = sum_s slab[s*slab_stride + i]); l2 * p is added for i < l2_count;
  * p_prev (may be NULL) receives the pre-update values; sq_out (may be NULL) gets

@@ -116,6 +116,26 @@ if [ "$MODE" = rsbig ]; then
   bash scripts/gpu_ab_variant.sh ${TAG}_ab old "" "" "c5 c3 c2"
   exit $?
 fi
+if [ "$MODE" = stgap ]; then
+  # what the per-step status read-back costs the boundary: read back every step vs (almost) never
+  # (ring: the status written by the step's last kernel into pinned memory, DLAMD_STATUS_RING)
+  timeout -k 10 300 python -u -m pytest tests/test_gpu_parity.py -m gpu -q -rf -k "bad_id" \
+    -p no:cacheprovider --timeout 200 --timeout-method thread > $OUT/pytest_ring.log 2>&1
+  rc=$?; echo "pytest rc=$rc: $(tail -1 $OUT/pytest_ring.log)"; [ $rc -eq 0 ] || { grep -E "^(FAILED|ERROR)" $OUT/pytest_ring.log; exit $rc; }
+  for rep in 1 2; do
+    for wl in c5 c2; do
+      for cfg in 1:0 1000:0 1:1; do
+        IFS=: read ev rg <<< "$cfg"
+        DLAMD_STEP_EVENTS=1 DLAMD_STATUS_EVERY=$ev DLAMD_STATUS_RING=$rg timeout -k 10 300 python bench.py --no-cpu-baseline --no-extra \
+          --workload $wl --steps 30 --warmup 5 > $OUT/st_${wl}_$ev$rg.json 2> $OUT/st_${wl}_$ev$rg.err || { tail -5 $OUT/st_${wl}_$ev$rg.err; exit 1; }
+        python -c "
+import json;d=json.loads(open('$OUT/st_${wl}_$ev$rg.json').read().strip().splitlines()[-1])
+print('$wl status_every=$ev ring=$rg', d['ms_per_step'], 'host', d.get('host_submit_ms_per_step'), 'events', d.get('step_events'))"
+      done
+    done
+  done
+  exit 0
+fi
 if [ "$MODE" = pfmid2 ]; then
   # prefetch depth x release point (d1m0 = the default): step time and the event span / gap
   for rep in 1 2 3; do

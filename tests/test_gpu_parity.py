@@ -301,11 +301,12 @@ def test_prefetch_matches_inline_index(hip_lib, name, adam, depth, mid, monkeypa
         eq(runs[0][1][k], runs[1][1][k], err_msg=k)
 
 
-@pytest.mark.parametrize("name,adam,where", [
-    ("deepfm_pipeline", "lazy", "cate"), ("deepfm_pipeline", "dense", "cate"),
-    ("wdl", "lazy", "cate"), ("wdl", "lazy", "wide"), ("wdl", "dense", "wide"),
-    ("deepfm_multi_cate", "lazy", "multi"), ("deepfm_multi_cate", "dense", "multi")])
-def test_bad_id_batch_skipped_alone_and_raises(hip_lib, name, adam, where):
+@pytest.mark.parametrize("name,adam,where,ring", [
+    ("deepfm_pipeline", "lazy", "cate", 0), ("deepfm_pipeline", "dense", "cate", 0),
+    ("wdl", "lazy", "cate", 0), ("wdl", "lazy", "wide", 0), ("wdl", "dense", "wide", 0),
+    ("deepfm_multi_cate", "lazy", "multi", 0), ("deepfm_multi_cate", "dense", "multi", 0),
+    ("deepfm_pipeline", "lazy", "cate", 1), ("wdl", "lazy", "wide", 1)])
+def test_bad_id_batch_skipped_alone_and_raises(hip_lib, name, adam, where, ring, monkeypatch):
     """TF raises InvalidArgumentError inside the failing sess.run, before anything is applied
     (deepfm_pipeline.py:219-221), and the next sess.run applies normally.  Here every id is
     validated before its step begins (dl_index_build, dl_validate_batch for the dense-layout
@@ -313,8 +314,10 @@ def test_bad_id_batch_skipped_alone_and_raises(hip_lib, name, adam, where):
     word, include/dlamd.h), the batches after it apply, and train_step raises within two calls
     naming the global step skipped.  The final state is bit-identical to an engine that never
     saw the bad batch: parameters, Adam moments, the step counter (adam='dense' runs the
-    dense-layout gather and the float-atomic backward, whose summation order varies: 1e-5)."""
+    dense-layout gather and the float-atomic backward, whose summation order varies: 1e-5).
+    ring=1: the status reported by the step's last kernel into pinned memory (DLAMD_STATUS_RING)."""
     from deep_learning_amd import _lib
+    monkeypatch.setenv("DLAMD_STATUS_RING", str(ring))
     kw = CASES[name]
     spec = ModelSpec(_model(name), **kw)
     mk = lambda: CTREngine(spec, max_batch=256, seed=4, adam=adam)
