@@ -362,7 +362,7 @@ class CTREngine:
         # DLAMD_STATUS_RING=1: the step's last kernel writes its status into pinned host memory
         # (dl_loss_accumulate's ring) instead of a device-to-host copy after each step
         self._ring = None
-        if os.environ.get("DLAMD_STATUS_RING", "0") == "1" and type(self) is CTREngine:
+        if os.environ.get("DLAMD_STATUS_RING", "1") == "1" and type(self) is CTREngine:
             self._ring = torch.zeros(8, dtype=torch.int32, pin_memory=True)
             self._ring_np = self._ring.numpy()
             self._ring_sent = None
