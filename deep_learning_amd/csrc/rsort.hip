@@ -24,8 +24,8 @@ constexpr int kRsWaves = kRsThreads / 64;
 // R = 12 with the keys materialised first (rs_keys_kernel): the downsweep then takes 36.9 KB of
 // LDS and 68 VGPRs, so its blocks fit beside a forward s3 GEMM block on a CU (120 KB LDS,
 // 2 x 200 VGPRs a SIMD) instead of holding CUs the GEMM's second round waits for
-// (C3 4.43 -> 4.30 ms, C5 1.44 -> 1.41 ms; C2's 1.7 M-reference sort keeps R = 16:
-// profiles/r04z/).
+// (C3 4.43 -> 4.31 ms, C5 1.447 -> 1.437 ms; C2's 3.4 M candidate references: unchanged within
+// the box's noise; profiles/r04z/, profiles/r04za/).
 constexpr int kRsRounds = DL_RS_ROUNDS;
 constexpr int kRsRoundsBig = 12;
 #ifndef DL_RS_BIGN
