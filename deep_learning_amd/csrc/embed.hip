@@ -445,30 +445,64 @@ __global__ __launch_bounds__(256) void cont_bwd_kernel(EmbBwdArgs a) {
   // first `active` blocks, four wave iterations each; the rest write zero slabs
   const int active = min((int)gridDim.x, max(1, (L.batch + 16 * SPW - 1) / (16 * SPW)));
   const int nw = active * (blockDim.x >> 6);
-  for (int b = blockIdx.x < active ? ((blockIdx.x * blockDim.x + threadIdx.x) >> 6) * SPW + lane / QPR : L.batch;
-       b < L.batch; b += nw * SPW) {
-    const float dzb = a.dz[b];
-    const float4 sd = *reinterpret_cast<const float4*>(a.fm_sum + (int64_t)b * E + 4 * q);
-    const float* cb = a.cont + (int64_t)b * Cf;
-    const float d0 = dzb * w0, d1 = dzb * w1, d2 = dzb * w2, d3 = dzb * w3;
+  // the cont rows (the same for every sample) and their first-order head weights, once
+  float4 er[NC];
+  float wf[NC / QPR];
 #pragma unroll
-    for (int f = 0; f < NC; ++f) {
-      if (f < Cf) {
-        const int64_t row = L.fm_cont_offset + f;
-        const float val = cb[f];
-        float4 e = make_float4(0.f, 0.f, 0.f, 0.f);
-        if (row_ok(row, L.zero_row0)) {
-          e = *reinterpret_cast<const float4*>(a.table + (L.cont_rows_compact ? f : row) * E + 4 * q);
-          e.x *= val; e.y *= val; e.z *= val; e.w *= val;
-        }
-        gc[f].x += val * d0 * (sd.x - e.x); gc[f].y += val * d1 * (sd.y - e.y);
-        gc[f].z += val * d2 * (sd.z - e.z); gc[f].w += val * d3 * (sd.w - e.w);
-      }
+  for (int f = 0; f < NC; ++f) {
+    const int64_t row = L.fm_cont_offset + f;
+    er[f] = (f < Cf && row_ok(row, L.zero_row0))
+                ? *reinterpret_cast<const float4*>(a.table + (L.cont_rows_compact ? f : row) * E + 4 * q)
+                : make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+#pragma unroll
+  for (int j = 0; j < NC / QPR; ++j) wf[j] = q + QPR * j < Cf ? a.w_head[q + QPR * j] : 0.f;
+  // kIt of the wave's samples loaded together (one memory round trip: at one wave a SIMD the
+  // loop is latency-bound), then summed in the same sample order as one at a time
+  constexpr int kIt = NC > 16 ? 1 : 4;   // (32 cont rows: one at a time, or the registers spill)
+  const int stride = nw * SPW;
+  for (int b0 = blockIdx.x < active ? ((blockIdx.x * blockDim.x + threadIdx.x) >> 6) * SPW + lane / QPR : L.batch;
+       b0 < L.batch; b0 += kIt * stride) {
+    float dzv[kIt], cv[kIt][NC];
+    float4 sdv[kIt];
+#pragma unroll
+    for (int i = 0; i < kIt; ++i) {
+      const int b = b0 + i * stride;
+      const int bc = b < L.batch ? b : b0;
+      dzv[i] = a.dz[bc];
+      sdv[i] = *reinterpret_cast<const float4*>(a.fm_sum + (int64_t)bc * E + 4 * q);
+#pragma unroll
+      for (int f = 0; f < NC; ++f) cv[i][f] = f < Cf ? a.cont[(int64_t)bc * Cf + f] : 0.f;
     }
 #pragma unroll
-    for (int j = 0; j < NC / QPR; ++j) {
-      const int f = q + QPR * j;
-      if (f < Cf) g1[j] += dzb * a.w_head[f] * cb[f];
+    for (int i = 0; i < kIt; ++i) {
+      if (b0 + i * stride >= L.batch) break;
+      const float dzb = dzv[i];
+      const float4 sd = sdv[i];
+      const float d0 = dzb * w0, d1 = dzb * w1, d2 = dzb * w2, d3 = dzb * w3;
+#pragma unroll
+      for (int f = 0; f < NC; ++f) {
+        if (f < Cf) {
+          const int64_t row = L.fm_cont_offset + f;
+          const float val = cv[i][f];
+          float4 e = make_float4(0.f, 0.f, 0.f, 0.f);
+          if (row_ok(row, L.zero_row0)) {
+            e = er[f];
+            e.x *= val; e.y *= val; e.z *= val; e.w *= val;
+          }
+          gc[f].x += val * d0 * (sd.x - e.x); gc[f].y += val * d1 * (sd.y - e.y);
+          gc[f].z += val * d2 * (sd.z - e.z); gc[f].w += val * d3 * (sd.w - e.w);
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < NC / QPR; ++j) {
+        const int f = q + QPR * j;
+        float cf = cv[i][QPR * j];   // cv[i][f] by constant indices (q selects): no scratch
+#pragma unroll
+        for (int t = 1; t < QPR; ++t)
+          if (q == t) cf = cv[i][QPR * j + t];
+        if (f < Cf) g1[j] += dzb * wf[j] * cf;
+      }
     }
   }
   // the wave's SPW samples (lanes with the same q) summed by butterfly
