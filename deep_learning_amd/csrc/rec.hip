@@ -542,7 +542,7 @@ __device__ __forceinline__ void rec_bwd_apply(const SegGrad4& s, int64_t row, in
 // hot rows, [kHotT] their chunks; then the hot rows' unique indices (appended by pass 1 in any
 // order), their first chunk (exclusive prefix over ceil(refs / kSegChunk), plus the total), the
 // owner of every chunk, and one partial sum per chunk (E/4 x {s, x, dsum} float4 + g1).
-constexpr int kHotN = 0, kHotT = 1, kHotDone = 2, kHotList = 4;
+constexpr int kHotN = 0, kHotT = 1, kHotDone = 2, kHotTicket = 3, kHotList = 4;
 struct HotWs {
   int32_t* hdr;
   int32_t* list;
@@ -573,6 +573,52 @@ __host__ __device__ inline long long hot_ws_bytes(long long nrefs, int E) {
   long long o = (long long)kHotList + cl + (cl + 1) + cc;
   o = (o + 3) / 4 * 4;
   return 4 * o + 4 * cc * (long long)hot_part_floats(E);
+}
+
+#ifndef DL_HOT_SCAN_FOLD
+#define DL_HOT_SCAN_FOLD 1   // 0 (A/B): the scan as its own launch after pass 1
+#endif
+// The scan, by one block of any size (a multiple of 64, at most 1024 threads): run by the
+// last block of pass 1 to finish (rec_bwd_adam_kernel), or by rec_hot_scan_kernel.
+__device__ __forceinline__ void hot_scan_block(const SegGradIn& sg, const HotWs& h, int nu, long long nrefs) {
+  __shared__ int ws[16];
+  __shared__ int carry_s;
+  const int n = (int)min((long long)h.hdr[kHotN], h.cap_list);
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, nt = blockDim.x;
+  if (tid == 0) carry_s = 0;
+  __syncthreads();
+  for (int i0 = 0; i0 < n; i0 += nt) {
+    const int i = i0 + tid;
+    int nch = 0;
+    if (i < n) {
+      const SegRange r = seg_range(sg, h.list[i], nu, nrefs);
+      nch = (r.e1 - r.e0 + kSegChunk - 1) / kSegChunk;
+    }
+    int inc = nch;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const int y = __shfl_up(inc, o, 64);
+      if (lane >= o) inc += y;
+    }
+    if (lane == 63) ws[wv] = inc;
+    __syncthreads();
+    int wbase = 0;
+    for (int w = 0; w < wv; ++w) wbase += ws[w];
+    const int carry = carry_s;
+    const int ex = carry + wbase + inc - nch;
+    if (i < n) {
+      h.off[i] = ex;
+      for (int c = 0; c < nch && ex + c < h.cap_chunks; ++c) h.map[ex + c] = i;
+    }
+    __syncthreads();
+    if (tid == nt - 1) carry_s = ex + nch;
+    __syncthreads();
+  }
+  if (tid == 0) {
+    const int total = (int)min((long long)carry_s, h.cap_chunks);
+    h.off[n] = total;
+    h.hdr[kHotT] = total;
+  }
 }
 
 // Pass 1: every unique row but the hot ones (more than kSegLong references: pass 2), E/4
@@ -645,6 +691,20 @@ __global__ __launch_bounds__(256, STASH ? DL_BWD_MIN_WAVES : 1) void rec_bwd_ada
     if (!row_ok) continue;
     rec_bwd_apply<E>(s, row, q, first, p, m, v, w, wm, wv, rec, c, L, n_rep, g_rep, g1_rep, alpha, t);
   }
+  if (DL_HOT_SCAN_FOLD && hot) {
+    // the last block to finish lists the hot rows' chunks (in place of a scan launch): every
+    // block's appends are published before its ticket
+    __shared__ int last_s;
+    __threadfence();
+    __syncthreads();
+    if (threadIdx.x == 0) last_s = atomicAdd(&hot[kHotTicket], 1) == (int)gridDim.x - 1;
+    __syncthreads();
+    if (last_s) {
+      __threadfence();
+      hot_scan_block(sg, hot_ws(hot, nrefs, E), nu, nrefs);
+      if (threadIdx.x == 0) hot[kHotTicket] = 0;
+    }
+  }
 }
 
 // Pass 2: the rows whose segments have more than kSegLong references, one whole block each.
@@ -689,53 +749,17 @@ __global__ __launch_bounds__(256) void rec_bwd_long_kernel(DL_REC_BWD_PARAMS) {
 //                         canonical long-segment sum, segment.h) and the row's Adam step
 __global__ __launch_bounds__(1024) void rec_hot_scan_kernel(SegGradIn sg, HotWs h, const int32_t* __restrict__ n_uniq,
                                                            const float* __restrict__ opt) {
-  __shared__ int ws[16];
-  __shared__ int carry_s;
   if (step_poisoned(opt)) return;
   const long long nrefs = (long long)sg.L.batch * index_slots(sg.L);
-  const int nu = clamp_uniq(n_uniq, nrefs, sg.status);
-  const int n = (int)min((long long)h.hdr[kHotN], h.cap_list);
-  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  if (tid == 0) carry_s = 0;
-  __syncthreads();
-  for (int i0 = 0; i0 < n; i0 += 1024) {
-    const int i = i0 + tid;
-    int nch = 0;
-    if (i < n) {
-      const SegRange r = seg_range(sg, h.list[i], nu, nrefs);
-      nch = (r.e1 - r.e0 + kSegChunk - 1) / kSegChunk;
-    }
-    int inc = nch;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-      const int y = __shfl_up(inc, o, 64);
-      if (lane >= o) inc += y;
-    }
-    if (lane == 63) ws[wv] = inc;
-    __syncthreads();
-    int wbase = 0;
-    for (int w = 0; w < wv; ++w) wbase += ws[w];
-    const int carry = carry_s;
-    const int ex = carry + wbase + inc - nch;
-    if (i < n) {
-      h.off[i] = ex;
-      for (int c = 0; c < nch && ex + c < h.cap_chunks; ++c) h.map[ex + c] = i;
-    }
-    __syncthreads();
-    if (tid == 1023) carry_s = ex + nch;
-    __syncthreads();
-  }
-  if (tid == 0) {
-    const int total = (int)min((long long)carry_s, h.cap_chunks);
-    h.off[n] = total;
-    h.hdr[kHotT] = total;
-  }
+  hot_scan_block(sg, h, clamp_uniq(n_uniq, nrefs, sg.status), nrefs);
 }
 
 template <int E>
 __global__ __launch_bounds__(256) void rec_hot_chunk_kernel(SegGradIn sg, HotWs h, const int32_t* __restrict__ n_uniq,
                                                             const float* __restrict__ opt) {
   if (step_poisoned(opt)) return;
+  const int T = h.hdr[kHotT];
+  if ((int)blockIdx.x >= T) return;   // (uniform ids: no hot chunk, every block leaves here)
   __shared__ unsigned char slot_lut[kSlotLutMax];
   build_slot_lut(sg, slot_lut, sg.L.multi_width);
   __shared__ SegLongLds sh;
@@ -747,7 +771,6 @@ __global__ __launch_bounds__(256) void rec_hot_chunk_kernel(SegGradIn sg, HotWs 
   const int nu = clamp_uniq(n_uniq, nrefs, sg.status);
   const float* ws = sg.w_head + F + 4 * q;
   const float4 wsec = L.use_fm ? make_float4(ws[0], ws[1], ws[2], ws[3]) : make_float4(0.f, 0.f, 0.f, 0.f);
-  const int T = h.hdr[kHotT];
   const int PF = hot_part_floats(E);
   for (int t = blockIdx.x; t < T; t += gridDim.x) {
     const int i = h.map[t];
@@ -1216,8 +1239,9 @@ extern "C" int dl_rec_bwd_adam(const dl_emb_layout* L, float* rec, int32_t rec_l
       // the header is zero here: zeroed at allocation, reset by the previous step's apply
       hipLaunchKernelGGL(bwd, dim3(grid), dim3(256), 0, st, sg, rec, rc, n_rep, rows_u, has_first ? rows_u1 : nullptr,
                          mv_u, uniq_keys, n_uniq, world, g_rep, has_first ? g1_rep : nullptr, hist, opt, h.hdr);
-      // the hot rows (none at uniform ids): chunks over the whole grid, then their updates
-      hipLaunchKernelGGL(rec_hot_scan_kernel, dim3(1), dim3(1024), 0, st, sg, h, n_uniq, opt);
+      // the hot rows (none at uniform ids; listed by pass 1's last block): chunks over the
+      // whole grid, then their updates
+      if (!DL_HOT_SCAN_FOLD) hipLaunchKernelGGL(rec_hot_scan_kernel, dim3(1), dim3(1024), 0, st, sg, h, n_uniq, opt);
       hipLaunchKernelGGL(rec_hot_chunk_kernel<kE>, dim3(1024), dim3(256), 0, st, sg, h, n_uniq, opt);
       hipLaunchKernelGGL(rec_hot_apply_kernel<kE>, dim3(64), dim3(256), 0, st, sg, rec, rc, n_rep, rows_u,
                          has_first ? rows_u1 : nullptr, mv_u, uniq_keys, world, g_rep, has_first ? g1_rep : nullptr,

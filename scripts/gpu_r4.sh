@@ -136,6 +136,16 @@ print('$wl status_every=$ev ring=$rg', d['ms_per_step'], 'host', d.get('host_sub
   done
   exit 0
 fi
+if [ "$MODE" = hotfold ]; then
+  # the hot-row chunk scan folded into pass 1's last block (variant nofold: its own launch)
+  timeout -k 10 400 python -u -m pytest tests -m gpu -q -rf -k "hot or determin or lazy or prefetch or bad_id or zipf" \
+    --deselect tests/test_gpu_fullsize.py -p no:cacheprovider --timeout 200 --timeout-method thread > $OUT/pytest_hot.log 2>&1
+  rc=$?; echo "pytest rc=$rc: $(tail -1 $OUT/pytest_hot.log)"; [ $rc -eq 0 ] || { grep -E "^(FAILED|ERROR)" $OUT/pytest_hot.log; exit $rc; }
+  timeout -k 10 300 python bench.py --workload c3 --dist zipf --no-extra --no-cpu-baseline --steps 10 > $OUT/c3z.json 2> $OUT/c3z.err || { tail -5 $OUT/c3z.err; exit 1; }
+  python scripts/bench_brief.py $OUT/c3z.json
+  bash scripts/gpu_ab_variant.sh ${TAG}_ab nofold "" "" "c2 c5"
+  exit $?
+fi
 if [ "$MODE" = pfmid2 ]; then
   # prefetch depth x release point (d1m0 = the default): step time and the event span / gap
   for rep in 1 2 3; do
