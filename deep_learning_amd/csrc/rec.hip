@@ -542,7 +542,7 @@ __device__ __forceinline__ void rec_bwd_apply(const SegGrad4& s, int64_t row, in
 // hot rows, [kHotT] their chunks; then the hot rows' unique indices (appended by pass 1 in any
 // order), their first chunk (exclusive prefix over ceil(refs / kSegChunk), plus the total), the
 // owner of every chunk, and one partial sum per chunk (E/4 x {s, x, dsum} float4 + g1).
-constexpr int kHotN = 0, kHotT = 1, kHotDone = 2, kHotTicket = 3, kHotList = 4;
+constexpr int kHotN = 0, kHotT = 1, kHotDone = 2, kHotList = 4;
 struct HotWs {
   int32_t* hdr;
   int32_t* list;
@@ -575,11 +575,9 @@ __host__ __device__ inline long long hot_ws_bytes(long long nrefs, int E) {
   return 4 * o + 4 * cc * (long long)hot_part_floats(E);
 }
 
-#ifndef DL_HOT_SCAN_FOLD
-#define DL_HOT_SCAN_FOLD 1   // 0 (A/B): the scan as its own launch after pass 1
-#endif
-// The scan, by one block of any size (a multiple of 64, at most 1024 threads): run by the
-// last block of pass 1 to finish (rec_bwd_adam_kernel), or by rec_hot_scan_kernel.
+// The scan, by one block of any size (a multiple of 64, at most 1024 threads).  (Run instead
+// by pass 1's last block to finish, it cost every block a device-scope release fence — an L2
+// write-back each on this chip: C2 2.25 -> 4.26 ms, profiles/r04zg/.)
 __device__ __forceinline__ void hot_scan_block(const SegGradIn& sg, const HotWs& h, int nu, long long nrefs) {
   __shared__ int ws[16];
   __shared__ int carry_s;
@@ -690,20 +688,6 @@ __global__ __launch_bounds__(256, STASH ? DL_BWD_MIN_WAVES : 1) void rec_bwd_ada
                              : segment_grad4_range<E>(sg, cr.e0, cr.e1, kc, q, nrefs, wsec);
     if (!row_ok) continue;
     rec_bwd_apply<E>(s, row, q, first, p, m, v, w, wm, wv, rec, c, L, n_rep, g_rep, g1_rep, alpha, t);
-  }
-  if (DL_HOT_SCAN_FOLD && hot) {
-    // the last block to finish lists the hot rows' chunks (in place of a scan launch): every
-    // block's appends are published before its ticket
-    __shared__ int last_s;
-    __threadfence();
-    __syncthreads();
-    if (threadIdx.x == 0) last_s = atomicAdd(&hot[kHotTicket], 1) == (int)gridDim.x - 1;
-    __syncthreads();
-    if (last_s) {
-      __threadfence();
-      hot_scan_block(sg, hot_ws(hot, nrefs, E), nu, nrefs);
-      if (threadIdx.x == 0) hot[kHotTicket] = 0;
-    }
   }
 }
 
@@ -1239,9 +1223,8 @@ extern "C" int dl_rec_bwd_adam(const dl_emb_layout* L, float* rec, int32_t rec_l
       // the header is zero here: zeroed at allocation, reset by the previous step's apply
       hipLaunchKernelGGL(bwd, dim3(grid), dim3(256), 0, st, sg, rec, rc, n_rep, rows_u, has_first ? rows_u1 : nullptr,
                          mv_u, uniq_keys, n_uniq, world, g_rep, has_first ? g1_rep : nullptr, hist, opt, h.hdr);
-      // the hot rows (none at uniform ids; listed by pass 1's last block): chunks over the
-      // whole grid, then their updates
-      if (!DL_HOT_SCAN_FOLD) hipLaunchKernelGGL(rec_hot_scan_kernel, dim3(1), dim3(1024), 0, st, sg, h, n_uniq, opt);
+      // the hot rows (none at uniform ids): chunks over the whole grid, then their updates
+      hipLaunchKernelGGL(rec_hot_scan_kernel, dim3(1), dim3(1024), 0, st, sg, h, n_uniq, opt);
       hipLaunchKernelGGL(rec_hot_chunk_kernel<kE>, dim3(1024), dim3(256), 0, st, sg, h, n_uniq, opt);
       hipLaunchKernelGGL(rec_hot_apply_kernel<kE>, dim3(64), dim3(256), 0, st, sg, rec, rc, n_rep, rows_u,
                          has_first ? rows_u1 : nullptr, mv_u, uniq_keys, world, g_rep, has_first ? g1_rep : nullptr,
