@@ -55,21 +55,21 @@ __global__ void step_guard_kernel(const int32_t* batch_err, float* opt) { step_g
 // step needs no host read; the host reads acc once per epoch.
 // ring (may be NULL): the step's status report into pinned host memory, in place of a
 // device-to-host copy after the step — every step (skipped ones too) advances the sequence
-// opt[DL_OPT_SEQ] to k and writes slot k & 3: [2s + 1] = the status word, then (after a
-// system-scope fence) [2s] = k, so a host that reads k there reads this step's status.
+// opt[DL_OPT_SEQ] to k and writes slot k & 3: [2s] = k and [2s + 1] = the status word in one
+// 8-byte store, so a host that reads k there reads this step's status.
 __global__ __launch_bounds__(256) void loss_accumulate_kernel(const float* __restrict__ slab, int rows, int pitch,
                                                               int col, double inv_b, float* __restrict__ opt,
                                                               float reg_coef, double* __restrict__ acc,
                                                               int32_t* __restrict__ ring) {
   __shared__ double part[256];
   if (ring && threadIdx.x == 0) {
+    // (k, status) as one 8-byte store: the host never sees a slot's k without its status; it
+    // lands with this kernel's end-of-kernel release (no system-scope fence, which would write
+    // back the L2)
     const int k = __float_as_int(opt[DL_OPT_SEQ]) + 1;
     opt[DL_OPT_SEQ] = __int_as_float(k);
-    volatile int32_t* r = ring + 2 * (k & 3);
-    r[1] = *opt_status(opt);
-    __threadfence_system();
-    r[0] = k;
-    __threadfence_system();
+    *reinterpret_cast<volatile unsigned long long*>(ring + 2 * (k & 3)) =
+        (unsigned long long)(uint32_t)k | ((unsigned long long)(uint32_t)*opt_status(opt) << 32);
   }
   if (step_poisoned(opt)) return;
   double s = 0.0;

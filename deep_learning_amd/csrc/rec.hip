@@ -810,16 +810,14 @@ __global__ __launch_bounds__(256) void rec_hot_apply_kernel(SegGradIn sg, float*
     if (row_ok) rec_bwd_apply<E>(s, row, q, first, p, m, v, w, wm, wv, rec, c, L, n_rep, g_rep, g1_rep, alpha, t);
   }
   // the last block to finish resets the header for the next step's pass 1 (in place of a
-  // reset launch before it): every block has read it by then
+  // reset launch before it): every block has read it by then (its loop bound came from it).
+  // No fences: the zeros reach the next kernel through this one's end-of-kernel release, and a
+  // device-scope fence here would write back the XCD's L2 in every block.
   __syncthreads();
-  if (threadIdx.x == 0) {
-    __threadfence();
-    if (atomicAdd(&h.hdr[kHotDone], 1) == (int)gridDim.x - 1) {
-      h.hdr[kHotN] = 0;
-      h.hdr[kHotT] = 0;
-      h.hdr[kHotDone] = 0;
-      __threadfence();
-    }
+  if (threadIdx.x == 0 && atomicAdd(&h.hdr[kHotDone], 1) == (int)gridDim.x - 1) {
+    h.hdr[kHotN] = 0;
+    h.hdr[kHotT] = 0;
+    h.hdr[kHotDone] = 0;
   }
 }
 

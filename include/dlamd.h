@@ -419,9 +419,9 @@ int dl_step_begin(const int32_t* batch_err, float* opt, float decay_rate, float 
  * step.  acc: double[3] on the device, read by the host once per epoch.  (Wide&Deep with lazy
  * wide records adds the wide L2 term per record step through dl_wide_rec_update / _flush acc.)
  * status_ring (may be NULL): int32[8] of pinned host memory; every call (skipped steps too)
- * advances the step sequence opt[DL_OPT_SEQ] to k and writes the status word to ring[2(k & 3) + 1],
- * then k to ring[2(k & 3)] (system-scope fence between): the host's per-step status report
- * without a device-to-host copy. */
+ * advances the step sequence opt[DL_OPT_SEQ] to k and writes k to ring[2(k & 3)] and the status
+ * word to ring[2(k & 3) + 1] in one 8-byte store: the host's per-step status report without a
+ * device-to-host copy. */
 int dl_loss_accumulate(const float* slab, int32_t rows, int32_t pitch, int32_t col, double inv_b, float* opt,
                        float reg_coef, double* acc, int32_t* status_ring, void* stream);
 /* Dense parameter whose gradient is the sum of `nslab` partial slabs
