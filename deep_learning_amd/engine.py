@@ -839,7 +839,7 @@ class CTREngine:
         # device-resident arrays of the buffers' shape: one dl_copy_many launch for all of them
         # (a runtime copy each otherwise)
         many = [(d, x) for d, x in todo if d.is_contiguous() and x.is_contiguous() and x.shape == d.shape
-                and x.data_ptr() % 16 == 0 and x.is_cuda and os.environ.get("DLAMD_STAGE_MANY", "1") == "1"]
+                and x.data_ptr() % 16 == 0]
         for d, x in todo:
             if not any(d is e for e, _ in many):
                 d.copy_(x)

@@ -146,24 +146,6 @@ if [ "$MODE" = hotfold ]; then
   bash scripts/gpu_ab_variant.sh ${TAG}_ab nofold "" "" "c2 c5"
   exit $?
 fi
-if [ "$MODE" = stage ]; then
-  # a batch's staging in one dl_copy_many launch against a runtime copy per array
-  timeout -k 10 400 python -u -m pytest tests/test_gpu_kernels.py tests/test_gpu_parity.py tests/test_gpu_dropin.py -m gpu -q -rf \
-    -k "copy_many or prefetch or dropin or load_style or bad_id" -p no:cacheprovider --timeout 200 --timeout-method thread > $OUT/pytest_stage.log 2>&1
-  rc=$?; echo "pytest rc=$rc: $(tail -1 $OUT/pytest_stage.log)"; [ $rc -eq 0 ] || { grep -E "^(FAILED|ERROR)" $OUT/pytest_stage.log; exit $rc; }
-  for rep in 1 2; do
-    for wl in c5 c2 c3; do
-      for m in 0 1; do
-        DLAMD_STEP_EVENTS=1 DLAMD_STAGE_MANY=$m timeout -k 10 300 python bench.py --no-cpu-baseline --no-extra \
-          --workload $wl --steps 20 --warmup 5 > $OUT/sg_${wl}_$m.json 2> $OUT/sg_${wl}_$m.err || { tail -5 $OUT/sg_${wl}_$m.err; exit 1; }
-        python -c "
-import json;d=json.loads(open('$OUT/sg_${wl}_$m.json').read().strip().splitlines()[-1])
-print('$wl stage_many=$m', d['ms_per_step'], 'host', d.get('host_submit_ms_per_step'), 'events', d.get('step_events'))"
-      done
-    done
-  done
-  exit 0
-fi
 if [ "$MODE" = pfmid2 ]; then
   # prefetch depth x release point (d1m0 = the default): step time and the event span / gap
   for rep in 1 2 3; do
