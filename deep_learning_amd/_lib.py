@@ -80,7 +80,6 @@ SIGNATURES = {
     "dl_gemm_bf16": (I32, [I32, I32, I32, I32, I32, P, I32, P, I32, P, I32, I32, I32, P, I32, I32, I64, P]),
     "dl_split3": (I32, [P, I32, I32, I32, I32, P, I32, I64, P]),
     "dl_s3_kperm": (I32, []),
-    "dl_copy_many": (I32, [I32, P, P, P, P]),
     "dl_gemm_s3_nt": (I32, [I32, I32, I32, P, I32, P, I32, I64, P, I32, I32, P, I32, P]),
     "dl_gemm_s3_nt_bits": (I32, [I32, I32, I32, P, I32, P, I32, I64, P, I32, I32, P, I32, P, I32, P]),
     "dl_gemm_s3_tn": (I32, [I32, I32, I32, P, I32, P, I32, P, I32, I32, I64, P]),

@@ -266,53 +266,9 @@ __global__ __launch_bounds__(256) void validate_batch_kernel(dl_emb_layout L, co
   if (__any(bad) && (threadIdx.x & 63) == 0) atomicOr(err, DL_STATUS_BAD_ID);
 }
 
-// A batch's staging copies (engine.stage: labels, cont, vector, cate and wide ids into the
-// static buffer set the step graphs were captured on) in one launch instead of one runtime
-// blit per array: 16-B pieces over the whole grid, the arrays' byte tails by the first block.
-constexpr int kCopyMax = 8;
-struct CopyMany {
-  const unsigned char* src[kCopyMax];
-  unsigned char* dst[kCopyMax];
-  long long bytes[kCopyMax];
-  int n;
-};
-
-__global__ __launch_bounds__(256) void copy_many_kernel(CopyMany a) {
-  const long long t0 = (long long)blockIdx.x * blockDim.x + threadIdx.x, nt = (long long)gridDim.x * blockDim.x;
-  for (int j = 0; j < a.n; ++j) {
-    const long long n16 = a.bytes[j] >> 4;
-    const uint4* __restrict__ s = reinterpret_cast<const uint4*>(a.src[j]);
-    uint4* __restrict__ d = reinterpret_cast<uint4*>(a.dst[j]);
-    for (long long i = t0; i < n16; i += nt) d[i] = s[i];
-    if (blockIdx.x == 0)
-      for (long long b = (n16 << 4) + threadIdx.x; b < a.bytes[j]; b += blockDim.x) a.dst[j][b] = a.src[j][b];
-  }
-}
-
 }  // namespace dl
 
 using namespace dl;
-
-extern "C" int dl_copy_many(int32_t n, const void* const* src, void* const* dst, const int64_t* bytes, void* stream) {
-  DL_CHECK_ARG(n >= 0 && n <= kCopyMax, "n %d out of range (at most %d arrays)", n, kCopyMax);
-  DL_CHECK_ARG(n == 0 || (src && dst && bytes), "NULL argument");
-  CopyMany a{};
-  long long most = 0;
-  for (int j = 0; j < n; ++j) {
-    DL_CHECK_ARG(bytes[j] >= 0 && (bytes[j] == 0 || (src[j] && dst[j])), "bad array %d", j);
-    DL_CHECK_ARG(((uintptr_t)src[j] | (uintptr_t)dst[j]) % 16 == 0, "array %d not 16-B aligned", j);
-    a.src[j] = static_cast<const unsigned char*>(src[j]);
-    a.dst[j] = static_cast<unsigned char*>(dst[j]);
-    a.bytes[j] = bytes[j];
-    most = std::max(most, (long long)bytes[j]);
-  }
-  a.n = n;
-  if (most == 0) return 0;
-  long long blocks = (most / 16 + 255) / 256;
-  blocks = std::min(std::max(blocks, 1LL), 2048LL);
-  hipLaunchKernelGGL(copy_many_kernel, dim3((unsigned)blocks), dim3(256), 0, as_stream(stream), a);
-  DL_RETURN_LAUNCH("dl_copy_many");
-}
 
 extern "C" int dl_validate_batch(const dl_emb_layout* L, const int64_t* cate, const int64_t* wide, int32_t wide_cols,
                                  int32_t wide_ld, int64_t wide_rows, int32_t reset, int32_t* err, void* stream) {

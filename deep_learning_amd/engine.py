@@ -20,7 +20,6 @@ Internal layouts (import/export map to the reference's):
   head w = [first (F) | second (E) | deep (H) | bias]   (deepfm; dnn: [H | bias])
 """
 import contextlib
-import ctypes
 import gc
 import math
 import os
@@ -828,28 +827,14 @@ class CTREngine:
         B = lab.shape[0]
         if B > self.B:
             raise ValueError("batch %d > engine max_batch %d" % (B, self.B))
-        todo = [(self.in_label[:B], lab)]
+        self.in_label[:B].copy_(lab)
         if sp.C:
-            todo.append((self.in_cont[:B, : sp.C], _as_dev(batch["cont_feats"], F32, self.dev)))
+            self.in_cont[:B, : sp.C].copy_(_as_dev(batch["cont_feats"], F32, self.dev))
         if sp.V:
-            todo.append((self.in_vec[:B, : sp.V], _as_dev(batch["vector_feats"], F32, self.dev)))
-        todo.append((self.in_cate[:B, : sp.cate_ld], _as_dev(batch["cate_feats"], torch.int64, self.dev)))
+            self.in_vec[:B, : sp.V].copy_(_as_dev(batch["vector_feats"], F32, self.dev))
+        self.in_cate[:B, : sp.cate_ld].copy_(_as_dev(batch["cate_feats"], torch.int64, self.dev))
         if sp.Fw:
-            todo.append((self.in_wide[:B, : sp.Fw], _as_dev(batch["wide_feats"], torch.int64, self.dev)))
-        # device-resident arrays of the buffers' shape: one dl_copy_many launch for all of them
-        # (a runtime copy each otherwise)
-        many = [(d, x) for d, x in todo if d.is_contiguous() and x.is_contiguous() and x.shape == d.shape
-                and x.data_ptr() % 16 == 0]
-        for d, x in todo:
-            if not any(d is e for e, _ in many):
-                d.copy_(x)
-        if many:
-            n = len(many)
-            src = (ctypes.c_void_p * n)(*[x.data_ptr() for _, x in many])
-            dst = (ctypes.c_void_p * n)(*[d.data_ptr() for d, _ in many])
-            nb = (ctypes.c_int64 * n)(*[d.numel() * d.element_size() for d, _ in many])
-            vp = lambda a: ctypes.cast(a, ctypes.c_void_p)
-            call("dl_copy_many", n, vp(src), vp(dst), vp(nb), _lib.stream_handle())
+            self.in_wide[:B, : sp.Fw].copy_(_as_dev(batch["wide_feats"], torch.int64, self.dev))
         return B
 
     # ------------------------------------------------------------------ step

@@ -400,10 +400,6 @@ int dl_adam_begin_step(float* opt, float decay_rate, float decay_steps, void* st
  * itself.  Issued before dl_adam_begin_step so the step of a bad batch is poisoned
  * from its start. */
 int dl_step_guard(const int32_t* batch_err, float* opt, void* stream);
-/* dl_copy_many: n (<= 8) device-to-device copies of bytes[j] from src[j] to dst[j] (16-B aligned
- * arrays, any byte count) in one launch — a batch's staging into the static buffers captured
- * step graphs read (in place of one runtime copy per array). */
-int dl_copy_many(int32_t n, const void* const* src, void* const* dst, const int64_t* bytes, void* stream);
 /* The batch's id-validation word, before its step begins: reset != 0 zeroes err[0] first
  * (one word per batch, not sticky); then every cate id (cate non-NULL, [L->batch][L->cate_ld]:
  * single columns against their deep row id + deep_cate_offset and, with FM, their FM row

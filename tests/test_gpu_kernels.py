@@ -878,23 +878,3 @@ def test_adam_rows_width1_sweep(hip_lib, n, flags):
     assert int(td.sum()) == 0
     assert not torch.any(g_d != 0)
     np.testing.assert_allclose(float(sq.item()), float(np.sum(p.astype(np.float64) ** 2)), rtol=1e-4)
-
-
-def test_copy_many_equals_torch_copies(hip_lib):
-    """dl_copy_many (a batch's staging in one launch): every array copied byte for byte, byte
-    counts that are not multiples of 16 included, the bytes past each destination untouched."""
-    import ctypes
-    g = torch.Generator(device="cuda").manual_seed(7)
-    sizes = [262144, 3407872, 13631488, 37, 1, 0, 1000003]
-    srcs = [torch.randint(0, 256, (n,), dtype=torch.uint8, device="cuda", generator=g) for n in sizes]
-    dsts = [torch.full((n + 64,), 0xAB, dtype=torch.uint8, device="cuda") for n in sizes]
-    k = len(sizes)
-    vp = lambda a: ctypes.cast(a, ctypes.c_void_p)
-    src = (ctypes.c_void_p * k)(*[t.data_ptr() for t in srcs])
-    dst = (ctypes.c_void_p * k)(*[t.data_ptr() for t in dsts])
-    nb = (ctypes.c_int64 * k)(*sizes)
-    call("dl_copy_many", k, vp(src), vp(dst), vp(nb), _s())
-    torch.cuda.synchronize()
-    for n, s_, d in zip(sizes, srcs, dsts):
-        assert torch.equal(d[:n], s_)
-        assert (d[n:] == 0xAB).all()
