@@ -411,6 +411,8 @@ def _run_workload(wl, args, world, rank, sharded, steps, warmup, age, ksteps, ba
     torch.cuda.synchronize()
     if os.environ.get("DLAMD_STEP_EVENTS", "0") == "1":   # the compute stream's span / gap per step
         eng.step_events = []
+    if getattr(eng, "host_marks", None) is not None:
+        eng.host_marks.clear()
     t0 = time.perf_counter()
     w0 = getattr(eng, "host_wait", 0.0)
     for i in range(base, base + steps):
@@ -422,6 +424,13 @@ def _run_workload(wl, args, world, rank, sharded, steps, warmup, age, ksteps, ba
     barrier()
     dt = time.perf_counter() - t0
     base += steps
+    marks = getattr(eng, "host_marks", None)
+    if marks:   # sharded engine, DLAMD_HOST_TIMING=1: host time per phase of the step (ms)
+        ph = {}
+        for (n0, t0_), (n1, t1_) in zip(marks[:-1], marks[1:]):
+            if n1 != "start":
+                ph.setdefault(n1, []).append((t1_ - t0_) * 1e3)
+        log("%s: host ms per phase %s" % (wl, {k: round(sum(v) / len(v), 4) for k, v in ph.items()}))
     step_ev = None
     if getattr(eng, "step_events", None):
         ev, eng.step_events = eng.step_events, None
