@@ -1405,7 +1405,7 @@ class CTREngine:
         s = torch.cuda.Stream()
         s.wait_stream(torch.cuda.current_stream())
         g = torch.cuda.CUDAGraph()
-        with capture_guard(), torch.cuda.graph(g, stream=s):
+        with capture_guard(), torch.cuda.graph(g, stream=s, capture_error_mode="thread_local"):
             if (with_pre and part != "back") or pre_only:
                 self._pre(B)
             if not pre_only:

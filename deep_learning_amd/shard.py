@@ -660,7 +660,7 @@ class ShardedCTREngine(CTREngine):
             st = torch.cuda.Stream()
             st.wait_stream(torch.cuda.current_stream())
             cg = torch.cuda.CUDAGraph()
-            with capture_guard(), torch.cuda.graph(cg, stream=st):
+            with capture_guard(), torch.cuda.graph(cg, stream=st, capture_error_mode="thread_local"):
                 fn(B)
             torch.cuda.current_stream().wait_stream(st)
             g = (cg, B)
