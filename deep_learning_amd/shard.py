@@ -65,13 +65,6 @@ class Exchange:
         self.rank = dist.get_rank(group)
         self.backend = dist.get_backend(group)
         self.staged = self.backend != "nccl"
-        # the prefetched batch's count all-gather on a communicator of its own (RCCL): on the
-        # step's communicator it queued in front of this step's gradient exchange, which then
-        # waited for the next batch's index build (DLAMD_COUNT_GROUP=0: one communicator)
-        self.count_group = group
-        if not self.staged and os.environ.get("DLAMD_COUNT_GROUP", "1") == "1":
-            ranks = dist.get_process_group_ranks(group) if group is not None else list(range(self.world))
-            self.count_group = dist.new_group(ranks, backend=self.backend)
 
     def _dev(self, t):
         return t.cpu() if self.staged and t.is_cuda else t
@@ -108,7 +101,7 @@ class Exchange:
             return self.count_matrix(owner_counts)
         c = owner_counts.to(torch.int64)
         out = torch.empty(self.world * c.numel(), dtype=torch.int64, device=c.device)
-        dist.all_gather_into_tensor(out, c, group=self.count_group)
+        dist.all_gather_into_tensor(out, c, group=self.group)
         host = torch.empty(out.numel(), dtype=torch.int64, pin_memory=True)
         host.copy_(out, non_blocking=True)
         ev = torch.cuda.Event()

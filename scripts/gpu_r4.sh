@@ -146,21 +146,6 @@ if [ "$MODE" = hotfold ]; then
   bash scripts/gpu_ab_variant.sh ${TAG}_ab nofold "" "" "c2 c5"
   exit $?
 fi
-if [ "$MODE" = cgroup ]; then
-  # the prefetched count all-gather on its own communicator (DLAMD_COUNT_GROUP): shard tests, then
-  # the one-rank sharded step A/B with the host time per phase
-  timeout -k 10 500 python -u -m pytest tests/test_shard.py tests/test_gpu_comm.py tests/test_gpu_fullsize.py -m gpu -q -rf \
-    -k "shard or comm or c4" -p no:cacheprovider --timeout 300 --timeout-method thread > $OUT/pytest_cg.log 2>&1
-  rc=$?; echo "pytest rc=$rc: $(tail -1 $OUT/pytest_cg.log)"; [ $rc -eq 0 ] || { grep -E "^(FAILED|ERROR)" $OUT/pytest_cg.log; exit $rc; }
-  for rep in 1 2; do
-    for cg in 0 1; do
-      DLAMD_HOST_TIMING=1 DLAMD_COUNT_GROUP=$cg timeout -k 10 300 python bench.py --no-cpu-baseline --no-extra --sharded \
-        --vocab 1000000 --steps 20 --warmup 5 > $OUT/cg_$cg.json 2> $OUT/cg_$cg.err || { tail -5 $OUT/cg_$cg.err; exit 1; }
-      echo "count_group=$cg $(grep -h 'ms/step\|per phase' $OUT/cg_$cg.err | tr '\n' ' ')"
-    done
-  done
-  exit 0
-fi
 if [ "$MODE" = pfmid2 ]; then
   # prefetch depth x release point (d1m0 = the default): step time and the event span / gap
   for rep in 1 2 3; do
