@@ -146,6 +146,23 @@ if [ "$MODE" = hotfold ]; then
   bash scripts/gpu_ab_variant.sh ${TAG}_ab nofold "" "" "c2 c5"
   exit $?
 fi
+if [ "$MODE" = s3pf ]; then
+  # the NT kernels' weight-fragment read distance (DL_S3_PF 1 default, variants pf2 / pf3)
+  for v in pf2 pf3; do
+    DLAMD_VARIANT=$v timeout -k 10 300 python -u -m pytest tests/test_gpu_kernels.py -m gpu -q -rf -k "s3" \
+      -p no:cacheprovider --timeout 200 --timeout-method thread > $OUT/pytest_$v.log 2>&1
+    rc=$?; echo "pytest $v rc=$rc: $(tail -1 $OUT/pytest_$v.log)"; [ $rc -eq 0 ] || exit $rc
+  done
+  for rep in 1 2; do
+    for v in "" pf2 pf3; do
+      for c in fwd_l1 dx_l1; do
+        DLAMD_VARIANT=$v timeout -k 10 120 python scripts/s3_bench.py 30 t:$c 2>&1 | grep -v amdgpu.ids | sed "s/^/[${v:-default}] /" | tee -a $OUT/pf.txt || exit 1
+      done
+    done
+  done
+  bash scripts/gpu_ab_variant.sh ${TAG}_pf2 pf2 "" "" "c2" && bash scripts/gpu_ab_variant.sh ${TAG}_pf3 pf3 "" "" "c2"
+  exit $?
+fi
 if [ "$MODE" = pfmid2 ]; then
   # prefetch depth x release point (d1m0 = the default): step time and the event span / gap
   for rep in 1 2 3; do
