@@ -547,6 +547,9 @@ def _run_workload(wl, args, world, rank, sharded, steps, warmup, age, ksteps, ba
     out = dict(spec=spec, value=value, ms=ms, loss=loss, roofline=roof, gather=gather, flush=flush, kernels=kernels,
                kernel_sum=sum(k["us"] for k in kernels.values()), nb=nb, gemm_peak=gemm_peak, host_ms=host_ms,
                step_events=step_ev)
+    if sharded:
+        out["shard"] = {"cap": eng.cap, "overflows": getattr(eng, "overflows", 0), "report_lag": eng.lag}
+        eng.exch.close()
     del eng, batches
     torch.cuda.synchronize()
     torch.cuda.empty_cache()
@@ -752,6 +755,7 @@ def main():
             "kernels": r["kernels"],
             "kernel_sum_us_per_step": round(r["kernel_sum"], 1),
             "host_submit_ms_per_step": round(r["host_ms"], 4),
+            **({"shard": r["shard"]} if r.get("shard") else {}),
             **({"step_events": r["step_events"]} if r.get("step_events") else {}),
             "loss": round(r["loss"], 6),
             "extra_workloads": extra or None,

@@ -39,8 +39,8 @@ class PoolDesc(C.Structure):
 
 
 # include/dlamd.h constants
-OPT_LEN, OPT_STATUS, OPT_SKIP, OPT_BAD_STEP, OPT_BAD_COUNT, OPT_SEQ = 32, 16, 17, 18, 19, 20
-STATUS_BAD_ID, STATUS_LAG, STATUS_INDEX = 1, 2, 4
+OPT_LEN, OPT_STATUS, OPT_SKIP, OPT_BAD_STEP, OPT_BAD_COUNT, OPT_SEQ, OPT_BAD_RANKS = 32, 16, 17, 18, 19, 20, 21
+STATUS_BAD_ID, STATUS_LAG, STATUS_INDEX, STATUS_OVERFLOW, STATUS_DESYNC = 1, 2, 4, 8, 16
 REC_FIRST, REC_SPARSE_ADAM = 1, 2
 ROWS_CLEAR_TOUCHED, ROWS_SPARSE_ADAM, ROWS_GRAD_FIXED = 1, 2, 4
 WIDE_GRAD_SCALE = 2.0 ** 48
@@ -64,13 +64,16 @@ SIGNATURES = {
     "dl_embed_fwd_rec_flat": (I32, [LP, P, I32, I32, P, P, P, P, P, P, P, P, P, P, P]),
     "dl_shard_gather": (I32, [P, P, P, I64, I32, P, P, P]),
     "dl_shard_scatter_add": (I32, [P, P, P, I64, I32, P, P, P, P]),
+    "dl_shard_route": (I32, [P, P, P, I32, I32, I64, I32, P, P, P, P, P, P, I64, I64, P]),
+    "dl_shard_stamp": (I32, [P, I32, I32, P, P]),
+    "dl_shard_step_begin": (I32, [P, P, I32, I64, I64, P, F, F, P, I32, P]),
     "dl_slab_sum": (I32, [P, I32, I64, I64, P, P]),
     "dl_keys_to_local": (I32, [P, P, I64, P, P]),
     "dl_embed_cont_bwd": (I32, [LP, P, P, P, P, P, P, I32, P]),
     "dl_index_workspace_bytes": (I64, [I64]),
     "dl_index_build": (I32, [LP, P, I32, I32, P, I64, P, P, P, P, P, P, P, P, P]),
     "dl_index_build_pair": (I32, [LP, P, LP, P, P, I64, P, P, P, P, P, P, P, P, P, P, P, P, P]),
-    "dl_embed_bwd_sorted": (I32, [LP, P, P, P, P, P, P, I32, I64, P, P, P, P, P, P, P, I32, P]),
+    "dl_embed_bwd_sorted": (I32, [LP, P, P, P, P, P, P, I32, I64, P, P, P, P, P, P, P, I32, P, P]),
     "dl_pool_fwd": (I32, [LP, P, P, P, I32, P, P, I32, I32, P, P, P, P, P, P]),
     "dl_pool_fwd_indexed": (I32, [LP, P, P, P, I32, P, P, I32, I32, P, P, P, P, P]),
     "dl_pool_bwd": (I32, [LP, P, I32, P, P, I32, I32, P, P, P, P, P, I32, P, P, P, P, P, P]),
@@ -137,6 +140,7 @@ SIGNATURES = {
     "dl_all_to_allv": (I32, [P, P, P, P, P, I64, P]),
     "dl_all_reduce_f32": (I32, [P, P, P, I64, P]),
     "dl_all_gather": (I32, [P, P, P, I64, P]),
+    "dl_shard_exchange": (I32, [P, I32, P, P, I32, P]),
 }
 
 _LIB = None

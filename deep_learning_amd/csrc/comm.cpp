@@ -95,6 +95,48 @@ extern "C" int dl_all_to_allv(void* comm, const void* send, const int64_t* send_
   return 0;
 }
 
+// The sharded step's fixed-capacity exchange (shard.hip's block layout): for every array a,
+// block_bytes[a] per block, 2W - 1 blocks from bases[a]; block p < W = what peer p sends this
+// rank, block W + p - (p > rank) = this rank's side of its traffic with peer p.  dir 0 (requests
+// and gradients to the owners): send the sender-side block to p, receive p's into block p;
+// dir 1 (rows back to the senders): send block p to p, receive into the sender-side block.
+// Every array's transfers with every peer in one group (one launch); this rank's own block
+// never moves.  Sizes are fixed, so the call is captured into the step's hipGraph unchanged.
+extern "C" int dl_shard_exchange(void* comm, int32_t n_arrays, void* const* bases, const int64_t* block_bytes,
+                                 int32_t dir, void* stream) {
+  if (!comm || n_arrays < 0 || (n_arrays && (!bases || !block_bytes)) || (dir != 0 && dir != 1)) {
+    dl::set_error("dl_shard_exchange: bad arguments");
+    return 22;
+  }
+  ncclComm_t c = reinterpret_cast<ncclComm_t>(comm);
+  int n = 0, me = 0;
+  DL_NCCL(ncclCommCount(c, &n));
+  DL_NCCL(ncclCommUserRank(c, &me));
+  if (n == 1 || n_arrays == 0) return 0;
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  DL_NCCL(ncclGroupStart());
+  for (int p = 0; p < n; ++p) {
+    if (p == me) continue;
+    const int64_t mine = n + p - (p > me ? 1 : 0);   // this rank's side of the traffic with p
+    for (int a = 0; a < n_arrays; ++a) {
+      char* base = reinterpret_cast<char*>(bases[a]);
+      const int64_t bb = block_bytes[a];
+      if (bb <= 0) continue;
+      char* snd = base + (dir == 0 ? mine : p) * bb;
+      char* rcv = base + (dir == 0 ? p : mine) * bb;
+      ncclResult_t e = ncclSend(snd, (size_t)bb, ncclChar, p, c, st);
+      if (e == ncclSuccess) e = ncclRecv(rcv, (size_t)bb, ncclChar, p, c, st);
+      if (e != ncclSuccess) {
+        ncclGroupEnd();
+        dl::set_error("dl_shard_exchange: peer %d: %s", p, ncclGetErrorString(e));
+        return 2000 + (int)e;
+      }
+    }
+  }
+  DL_NCCL(ncclGroupEnd());
+  return 0;
+}
+
 // Sum all-reduce of n floats (in place when send == recv): the step's flat dense-gradient buffer.
 extern "C" int dl_all_reduce_f32(void* comm, const float* send, float* recv, int64_t n, void* stream) {
   if (!comm || !send || !recv || n < 0) {

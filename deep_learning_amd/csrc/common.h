@@ -84,6 +84,9 @@ __device__ __forceinline__ void raise_fault(int* status, int bits) {
   atomicOr(status, bits);
   atomicOr(status + (DL_OPT_SKIP - DL_OPT_STATUS), bits);
 }
+// The status bits that poison every later step until the host clears them (internal faults,
+// and the sharded step's overflow / desynchronisation, decided identically on every rank).
+constexpr int kStickyFaults = DL_STATUS_LAG | DL_STATUS_INDEX | DL_STATUS_OVERFLOW | DL_STATUS_DESYNC;
 __device__ __forceinline__ int* opt_status(const float* opt) {
   return const_cast<int*>(reinterpret_cast<const int*>(opt + DL_OPT_STATUS));
 }

@@ -1220,6 +1220,8 @@ struct BwdSortedArgs {
   float* g1_out;
   uint8_t* touched;
   int compact;
+  const int32_t* upos;     // compact: the slot of unique row u in rows_u / g_out (sharded exchange
+                           // blocks, dl_shard_route; -1 = no slot), NULL = u itself
 };
 
 
@@ -1229,15 +1231,17 @@ __device__ __forceinline__ void embed_bwd_sorted_row(const BwdSortedArgs& a, lon
   const dl_emb_layout& L = a.L;
   const int64_t row = decode_key(a.uniq[u], a.world);
   if (row < 0 || row >= L.n_rows) return;
+  const long long slot = a.upos ? (long long)a.upos[u] : u;
+  if (slot < 0) return;
   float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
   if (sgr.dsum.x != 0.f || sgr.dsum.y != 0.f || sgr.dsum.z != 0.f || sgr.dsum.w != 0.f)
-    v = *reinterpret_cast<const float4*>((a.rows_u ? a.rows_u + u * E : a.table + row * E) + 4 * q);
+    v = *reinterpret_cast<const float4*>((a.rows_u ? a.rows_u + slot * E : a.table + row * E) + 4 * q);
   float4 g;
   g.x = seg_row_grad(sgr.s.x, sgr.dsum.x, sgr.x.x, sgr.dsum.x != 0.f ? v.x : 0.f);
   g.y = seg_row_grad(sgr.s.y, sgr.dsum.y, sgr.x.y, sgr.dsum.y != 0.f ? v.y : 0.f);
   g.z = seg_row_grad(sgr.s.z, sgr.dsum.z, sgr.x.z, sgr.dsum.z != 0.f ? v.z : 0.f);
   g.w = seg_row_grad(sgr.s.w, sgr.dsum.w, sgr.x.w, sgr.dsum.w != 0.f ? v.w : 0.f);
-  const long long o = a.compact ? u : row;
+  const long long o = a.compact ? slot : row;
   *reinterpret_cast<float4*>(a.g_out + o * E + 4 * q) = g;
   if (q == 0) {
     if (a.g1_out && (a.compact || L.use_fm)) a.g1_out[o] = sgr.g1;
@@ -1294,7 +1298,7 @@ extern "C" int dl_embed_bwd_sorted(const dl_emb_layout* L, const float* table, c
                                    const int32_t* sorted_refs, int32_t world, int64_t max_uniq,
                                    const float* dz, const float* w_head, const float* fm_sum,
                                    const float* dx0, float* g_out, float* g1_out, uint8_t* touched,
-                                   int32_t compact, void* stream) {
+                                   int32_t compact, const int32_t* upos, void* stream) {
   if (int rc = check_layout(L)) return rc;
   DL_CHECK_ARG(uniq_keys && seg_off && n_uniq && sorted_refs && dx0 && g_out, "NULL argument");
   DL_CHECK_ARG(table || rows_u, "need the table or the gathered rows");
@@ -1305,7 +1309,7 @@ extern "C" int dl_embed_bwd_sorted(const dl_emb_layout* L, const float* table, c
   long long blocks = (max_uniq * (L->emb_dim / 4) + 255) / 256;
   if (blocks > 8192) blocks = 8192;
   BwdSortedArgs a{*L, table, rows_u, uniq_keys, seg_off, n_uniq, sorted_refs, world, dz, w_head, fm_sum, dx0,
-                  g_out, g1_out, touched, compact};
+                  g_out, g1_out, touched, compact, compact ? upos : nullptr};
   DL_DISPATCH_E(L->emb_dim, {
     hipLaunchKernelGGL(embed_bwd_sorted_kernel<kE>, dim3((unsigned)blocks), dim3(256), 0, as_stream(stream), a);
     hipLaunchKernelGGL(embed_bwd_long_kernel<kE>, dim3(1024), dim3(256), 0, as_stream(stream), a);

@@ -37,7 +37,7 @@ __device__ __forceinline__ void step_guard_kernel_body(const int32_t* batch_err,
   int* st = opt_status(opt);
   const int bad = e ? ((e & DL_STATUS_BAD_ID) ? DL_STATUS_BAD_ID : e) : 0;
   // this step's skip word: the batch's own bits + any sticky internal fault
-  st[DL_OPT_SKIP - DL_OPT_STATUS] = bad | (st[0] & (DL_STATUS_LAG | DL_STATUS_INDEX));
+  st[DL_OPT_SKIP - DL_OPT_STATUS] = bad | (st[0] & kStickyFaults);
   if (bad) {
     st[0] |= bad;
     opt[DL_OPT_BAD_STEP] = opt[7];            // global_step the bad batch would have advanced from
@@ -68,8 +68,11 @@ __global__ __launch_bounds__(256) void loss_accumulate_kernel(const float* __res
     // back the L2)
     const int k = __float_as_int(opt[DL_OPT_SEQ]) + 1;
     opt[DL_OPT_SEQ] = __int_as_float(k);
+    // the status word: the sticky status bits (low half) and this step's own skip bits (high half)
+    const int* st = opt_status(opt);
+    const uint32_t word = ((uint32_t)st[0] & 0xffffu) | ((uint32_t)st[DL_OPT_SKIP - DL_OPT_STATUS] << 16);
     *reinterpret_cast<volatile unsigned long long*>(ring + 2 * (k & 3)) =
-        (unsigned long long)(uint32_t)k | ((unsigned long long)(uint32_t)*opt_status(opt) << 32);
+        (unsigned long long)(uint32_t)k | ((unsigned long long)word << 32);
   }
   if (step_poisoned(opt)) return;
   double s = 0.0;
@@ -93,6 +96,44 @@ __global__ __launch_bounds__(256) void loss_accumulate_kernel(const float* __res
 __global__ void step_begin_kernel(const int32_t* batch_err, float* opt, float decay_rate, float decay_steps,
                                   float* hist, int mask) {
   step_guard_kernel_body(batch_err, opt);
+  adam_begin_body(opt, decay_rate, decay_steps);
+  if (hist) hist[(int)opt[7] & mask] = opt[3];
+}
+
+// The sharded step's opening node, after the request exchange: one decision every rank takes
+// from the same data — the headers every rank sent this one (block p from rank p: its count,
+// its batch's validation bit, its overflow and sticky fault bits, its global step).  A bad id on
+// any rank skips the step everywhere (the batch's bit, not sticky); an overflowing block, an
+// internal fault on any rank or ranks at different steps poison this and every later step
+// everywhere until the host clears the status (it then replays the skipped steps).
+__global__ void shard_step_begin_kernel(const int32_t* __restrict__ hdr, const int32_t* __restrict__ hdr2, int world,
+                                        long long cap, long long cap2, float* opt, float decay_rate, float decay_steps,
+                                        float* hist, int mask) {
+  int fl = 0, bad_ranks = 0;
+  const int step = (int)opt[7];
+  for (int p = 0; p < world; ++p) {
+    const int* h = hdr + 4 * p;
+    if (h[0] < 0 || h[0] > cap) fl |= DL_STATUS_INDEX;
+    if (h[3] != step) fl |= DL_STATUS_DESYNC;
+    fl |= h[1];
+    if (h[1] & DL_STATUS_BAD_ID) bad_ranks |= 1 << p;
+    if (hdr2) {   // the second id set's blocks (wdl's wide ids): their counts and flags
+      const int* h2 = hdr2 + 4 * p;
+      if (h2[0] < 0 || h2[0] > cap2) fl |= DL_STATUS_INDEX;
+      fl |= h2[1];
+      if (h2[1] & DL_STATUS_BAD_ID) bad_ranks |= 1 << p;
+    }
+  }
+  int* st = opt_status(opt);
+  const int bad = fl & DL_STATUS_BAD_ID;
+  const int sticky = (fl | st[0]) & kStickyFaults;
+  st[DL_OPT_SKIP - DL_OPT_STATUS] = bad | sticky;
+  st[0] |= bad | sticky;
+  if (bad) {
+    opt[DL_OPT_BAD_STEP] = opt[7];
+    opt[DL_OPT_BAD_COUNT] += 1.f;
+    opt[DL_OPT_BAD_RANKS] = __int_as_float(__float_as_int(opt[DL_OPT_BAD_RANKS]) | bad_ranks);
+  }
   adam_begin_body(opt, decay_rate, decay_steps);
   if (hist) hist[(int)opt[7] & mask] = opt[3];
 }
@@ -410,6 +451,16 @@ extern "C" int dl_loss_accumulate(const float* slab, int32_t rows, int32_t pitch
   hipLaunchKernelGGL(loss_accumulate_kernel, dim3(1), dim3(256), 0, as_stream(stream), slab, rows, pitch, col, inv_b,
                      opt, reg_coef, acc, status_ring);
   DL_RETURN_LAUNCH("dl_loss_accumulate");
+}
+
+extern "C" int dl_shard_step_begin(const int32_t* hdr, const int32_t* hdr2, int32_t world, int64_t cap, int64_t cap2,
+                                   float* opt, float decay_rate, float decay_steps, float* hist, int32_t hist_len,
+                                   void* stream) {
+  DL_CHECK_ARG(hdr && opt && world >= 1 && world <= 31 && cap >= 1 && (!hdr2 || cap2 >= 1), "bad args");
+  DL_CHECK_ARG(!hist || (hist_len >= 2 && (hist_len & (hist_len - 1)) == 0), "bad hist");
+  hipLaunchKernelGGL(shard_step_begin_kernel, dim3(1), dim3(1), 0, as_stream(stream), hdr, hdr2, world, (long long)cap,
+                     (long long)cap2, opt, decay_rate, decay_steps, hist, hist ? hist_len - 1 : 0);
+  DL_RETURN_LAUNCH("dl_shard_step_begin");
 }
 
 extern "C" int dl_step_begin(const int32_t* batch_err, float* opt, float decay_rate, float decay_steps, float* hist,

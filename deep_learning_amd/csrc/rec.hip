@@ -674,7 +674,13 @@ __global__ __launch_bounds__(256, STASH ? DL_BWD_MIN_WAVES : 1) void rec_bwd_ada
     nn = seg_range(sg, u + 2 * ngroups, nu, nrefs);
     key_n = u + ngroups < nu ? uniq[u + ngroups] : 0u;
     if (cr.e1 - cr.e0 > kSegLong) {   // a hot row: pass 2 (rec_bwd_long_kernel, or the chunked passes)
-      if (hot && q == 0) hot[kHotList + atomicAdd(&hot[kHotN], 1)] = (int32_t)u;
+      if (hot && q == 0) {
+        // at most nrefs / (kSegLong + 1) rows can be hot; an index past that means a stale
+        // header (a step whose apply never ran): report it instead of writing past the list
+        const int k = atomicAdd(&hot[kHotN], 1);
+        if (k < hot_cap_list(nrefs)) hot[kHotList + k] = (int32_t)u;
+        else index_fault(sg.status);
+      }
       continue;
     }
     const int64_t row = decode_key(key, world);
@@ -979,7 +985,7 @@ constexpr int kMaxChain = 64;
 __global__ __launch_bounds__(256) void rec_chain_link_kernel(const int32_t* __restrict__ ids, long long n,
                                                              int32_t* __restrict__ head, int32_t* __restrict__ next) {
   for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x)
-    next[i] = atomicExch(head + ids[i], (int32_t)i);
+    if (ids[i] >= 0) next[i] = atomicExch(head + ids[i], (int32_t)i);   // -1: an empty exchange slot
 }
 
 template <int E>
@@ -1003,7 +1009,7 @@ __global__ __launch_bounds__(256) void rec_apply_chain_kernel(float* __restrict_
   const bool first = c.has_first && q == 0;
   for (long long i = gt / LPR; i < n; i += (long long)gridDim.x * blockDim.x / LPR) {
     const long long row = ids[i];
-    if (head[row] != (int32_t)i) continue;   // not the leader of this row's arrivals
+    if (row < 0 || head[row] != (int32_t)i) continue;   // an empty slot, or not the row's leader
     float* r = rec + row * c.ld;
     float4 p = *reinterpret_cast<const float4*>(r + 4 * q);
     float4 m = *reinterpret_cast<const float4*>(r + E + 4 + 4 * q);
@@ -1052,7 +1058,7 @@ __global__ __launch_bounds__(256) void rec_apply_chain_kernel(float* __restrict_
 __global__ __launch_bounds__(256) void rec_chain_reset_kernel(const int32_t* __restrict__ ids, long long n,
                                                               int32_t* __restrict__ head) {
   for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x)
-    head[ids[i]] = -1;
+    if (ids[i] >= 0) head[ids[i]] = -1;
 }
 
 __global__ void hist_record_kernel(const float* opt, float* hist, int mask) {

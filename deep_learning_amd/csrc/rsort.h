@@ -9,7 +9,7 @@ namespace dl {
 
 // Where the first pass reads its (key, value) pairs from.
 struct RsSource {
-  // kind 0: keys[e] (all valid), value e                                  (dl_sort_unique)
+  // kind 0: keys[e], value e; a key of 0xFFFFFFFF (-1) is dropped          (dl_sort_unique)
   // kind 1: the batch's table references, value e = sample * slots + slot (dl_index_build):
   //         key (owner << 27) | local of the referenced row, or no key (row 0 under the
   //         zero-row rule); out-of-range ids set *err and give no key; inv[e] = -1 for

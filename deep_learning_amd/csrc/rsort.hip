@@ -77,9 +77,9 @@ __device__ __forceinline__ bool rs_get(const RsSource& src, const RsPass& p, lon
     return in;
   }
   val = (int32_t)e;
-  if (MODE == 1) {
+  if (MODE == 1) {   // a negative int32 key (0xFFFFFFFF: a padding slot) is dropped
     key = src.keys[ec];
-    return in;
+    return in && key != kRsNoKey;
   }
   if (MODE == 3) {   // keys materialised by rs_keys_kernel (kRsNoKey: no key)
     key = p.kin[ec];

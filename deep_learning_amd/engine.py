@@ -767,10 +767,17 @@ class CTREngine:
         if not self.lazy:
             return
         pp = w1 = None
-        if planes:
-            if getattr(self, "p_plane", None) is None:
+        if planes and getattr(self, "p_plane", None) is None:
+            # rows x E f32 (+ rows f32): 1.7 GB at 26 M rows, E = 16 — dropped again when training
+            # resumes (train_step); without the memory, predict reads the records instead
+            try:
                 self.p_plane = torch.empty(self.rec.shape[0], self.spec.E, device=self.dev)
                 self.w1_plane = torch.empty(self.rec.shape[0], device=self.dev) if self.spec.fm else None
+            except torch.cuda.OutOfMemoryError:
+                self.p_plane = self.w1_plane = None
+                self.flat_planes = False
+                planes = False
+        if planes:
             pp, w1 = self.p_plane, self.w1_plane
         self._c("rec_flush", "dl_rec_flush", ptr(self.rec), self.rec_ld, self.spec.E, self.rec_flags,
                 self.rec.shape[0], ptr(self.hist), self.hist_len, ptr(self.opt), ptr(pp), ptr(w1),
@@ -1142,7 +1149,7 @@ class CTREngine:
             self._c("embed_bwd", "dl_embed_bwd_sorted", C_ref(L), ptr(self.table), None, ptr(self.idx_uniq),
                     ptr(self.idx_off), ptr(self.idx_n), ptr(self.idx_refs), 1, B * self.n_slot, ptr(self.dz),
                     ptr(self.w_head), ptr(self.fm_sum), ptr(self.dx0), ptr(self.tg), ptr(self.fmg),
-                    ptr(self.touched), 0, s)
+                    ptr(self.touched), 0, None, s)
             self._c("cont_bwd", "dl_embed_cont_bwd", C_ref(L), ptr(self.table), ptr(self._cont()), ptr(self.dz),
                     ptr(self.w_head), ptr(self.fm_sum), ptr(self.cont_slab), self.bwd_blocks, s)
         else:
@@ -1308,6 +1315,9 @@ class CTREngine:
         """One training step on `batch` (or on the already-staged slots if None).
         next_batch: prefetch it (stage + index build on the side stream) during this step."""
         B, indexed = self._begin(batch)
+        if getattr(self, "p_plane", None) is not None:   # predict's planes go stale: free them
+            self.p_plane = self.w1_plane = None
+            self.planes_step = -1
         if self.lazy:
             # every row's lag must stay below the alpha ring (rec.hip)
             if self.since_flush >= self.hist_len - 2:
@@ -1523,7 +1533,11 @@ class CTREngine:
                 if self._ring_sent - self._ring_checked <= 2:
                     break
                 t0 = time.perf_counter()
+                spins = 0
                 while int(r[j]) != k:
+                    spins += 1
+                    if spins > 1000:   # past ~1 ms: yield the core instead of spinning on it
+                        time.sleep(2e-5)
                     if time.perf_counter() - t0 > 10.0:   # the sequence went out of step: resynchronise
                         torch.cuda.synchronize()
                         if int(r[j]) != k:
@@ -1534,6 +1548,17 @@ class CTREngine:
             self._ring_checked = k
             if int(r[j + 1]) != 0:
                 self.check_error()
+
+    def set_opt(self, values):
+        """Restore the optimizer block (a checkpoint's opt array) mid-process.  The step sequence
+        of the status ring (opt[DL_OPT_SEQ]) belongs to this process's timeline, not the
+        checkpoint's: the device's current value is kept, and the host re-reads it at the next
+        step (otherwise the ring numbers the host expects would never arrive)."""
+        v = torch.as_tensor(values, dtype=torch.float32).to(self.dev).clone()
+        v[_lib.OPT_SEQ] = self.opt[_lib.OPT_SEQ]
+        self.opt.copy_(v)
+        if self._ring is not None:
+            self._ring_sent = None
 
     def _error_words(self):
         words = [self.err]

@@ -176,7 +176,7 @@ def _adam_state(eng):
 
 
 def _load_adam_state(eng, d):
-    eng.opt.copy_(torch.from_numpy(d["adam/opt"]))
+    eng.set_opt(torch.from_numpy(d["adam/opt"]))
     eng.steps = int(d["adam/steps"][0])
     eng.set_adam_state({k[len("adam/table_"):]: d[k] for k in d.files if k.startswith("adam/table_")})
     eng.hm.copy_(torch.from_numpy(d["adam/hm"]))

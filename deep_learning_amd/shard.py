@@ -1,34 +1,45 @@
-"""Row-sharded multi-GPU training (BASELINE config C4).
+"""Row-sharded multi-GPU training (BASELINE configs C4 and C5 at N GPUs).
 
-One process per GPU.  The embedding table (and its first-order column and TF1
-Adam state) is split by rows: row r lives on rank r % world at local row
-r // world (cyclic, so Zipf-hot low ids spread over all ranks).  The rows
-below ``replicated`` (deepfm_pipeline's 13 cont-field rows, hit by every
-sample) are replicated on every rank.  Dense parameters are replicated.
+One process per GPU.  The embedding table (and its first-order column and TF1 Adam state) is
+split by rows: row r lives on rank r % world at local row r // world (cyclic, so Zipf-hot low
+ids spread over all ranks).  The rows below ``replicated`` (deepfm_pipeline's 13 cont-field
+rows, hit by every sample) are replicated on every rank.  Dense parameters are replicated.
+The loop this replaces is the reference's session loop, models/deepfm_pipeline.py:219-234
+(and wdl.py:287-317), run at the global batch B * world.
 
-Step on every rank (local batch B, global batch B*world):
-  1. index: sort/dedup this batch's row references; unique rows grouped by owner
-  2. all-gather of the per-owner unique-row counts, all-to-all of the row ids
-  3. owners gather the requested rows (E floats + first-order weight)
-  4. all-to-all of the rows back; the forward expands them through the inverse map
-  5. MLP + head forward, input gradients down to the embeddings
-  6. per-unique-row gradient (deterministic segment sum), all-to-all to owners,
-     overlapping the weight gradients
-  7. one all-reduce (sum) of the dense gradients + replicated-row gradients
-  8. TF1 Adam: dense + replicated parameters identically everywhere; the shard rows
-     by their owners — row records with lazy-exact catch-up: each row's arrivals
-     (at most one per sender) summed in a fixed order and applied once
-The result equals single-GPU training on the concatenated global batch.
+A step is device-driven end to end, so it is one hipGraph: every exchange moves FIXED-SIZE
+blocks (dl_shard_route / dl_shard_exchange, shard.hip's layout), the true row counts travel in a
+header beside the data, and every decision that depends on them is taken on the device:
 
-Off the critical path, on a second (high-priority) stream: the owners' arrival
-chains and record update of a step, and — with train_step(next_batch=...) — the
-next batch's staging, index build and count all-gather, so a step starts at its
-id exchange with the counts already on the host.
+  prefetch (side stream, during the previous step): stage the batch; index it (sort/dedup, unique
+      rows grouped by owner); route it — each owner's unique rows into a block of `cap` slots,
+      the inverse map remapped to slots, a header per block {count, flags, rank, step}
+  1. request exchange (ids + headers, one RCCL group)
+  2. dl_shard_step_begin: from every rank's header, the same decision on every rank — a bad id
+     anywhere skips the step everywhere; an overflowing block (more unique rows for an owner
+     than `cap`), an internal fault or ranks at different steps poison it (and the next ones)
+  3. owners gather the requested rows (caught up to step t-1) into their answer blocks; the
+     owner sort that groups this step's arrivals by row runs on a branch meanwhile
+  4. answer exchange (rows + first-order weights, one group); the forward reads them through
+     the remapped inverse map
+  5. MLP + head, the input-gradient chain, per-unique-row gradients written into slots
+  6. gradient exchange to the owners (one group) on a branch, beside the weight gradients;
+     the flat all-reduce of the dense + replicated gradients on a second communicator and
+     stream, beside it
+  7. TF1 Adam: dense + replicated parameters identically everywhere; owners apply each row's
+     arrivals (at most one per sender, summed in rank order) once — lazy-exact row records
+  8. the step's loss and status into the pinned status ring (no host read in the step)
 
-Collectives go through torch.distributed: backend "nccl" is RCCL (xGMI) and
-exchanges device tensors directly; backend "gloo" (CPU tests, and several ranks
-sharing one GPU) stages them through host memory.
+The host waits only for the status report of the step submitted `lag` calls earlier.  A report
+naming an overflow (every rank sees the same one) makes every rank synchronise, grow its blocks
+and replay the skipped steps in order — the result is the same as if nothing had overflowed.
+
+Collectives: backend "nccl" uses two RCCL communicators of our own (comm.cpp: one for the block
+exchanges, one for the all-reduce), launched on our streams inside the step's graph; the torch
+process group only ships their ids.  Backend "gloo" (CPU tests, several ranks sharing one GPU)
+stages the same fixed blocks through host memory, eagerly.
 """
+import ctypes
 import os
 import time
 
@@ -41,23 +52,13 @@ from . import _lib
 from ._lib import call, ptr
 from .engine import CTREngine, C_ref, _num_splits, _ru, call_int, capture_guard
 
-
-class _Works:
-    """The works of one grouped point-to-point exchange, waited together, and the event
-    after the rank's own segment's copy (queued on the issuing stream: a waiter on another
-    stream must order after it too)."""
-
-    def __init__(self, works, copied):
-        self.works, self.copied = works, copied
-
-    def wait(self):
-        torch.cuda.current_stream().wait_event(self.copied)
-        for w in self.works:
-            w.wait()
+_STICKY = _lib.STATUS_LAG | _lib.STATUS_INDEX | _lib.STATUS_OVERFLOW | _lib.STATUS_DESYNC
 
 
 class Exchange:
-    """Thin wrapper over torch.distributed collectives for the sharded step."""
+    """The sharded step's collectives.  `blocks` moves whole blocks of 2W - 1-block arrays
+    (dl_shard_exchange's layout); `all_reduce` sums in place.  RCCL: our own communicators on
+    the caller's stream (capturable); gloo: staged through host memory."""
 
     def __init__(self, group=None):
         self.group = group
@@ -65,117 +66,77 @@ class Exchange:
         self.rank = dist.get_rank(group)
         self.backend = dist.get_backend(group)
         self.staged = self.backend != "nccl"
+        self._comm = self._comm_ar = None
 
-    def _dev(self, t):
-        return t.cpu() if self.staged and t.is_cuda else t
+    def _comms(self):
+        """Two RCCL communicators (the block exchanges; the all-reduce, so it can run beside
+        them on its own stream), created collectively on first use; their ids travel over the
+        torch process group."""
+        if self._comm is None:
+            nb = int(_lib.lib().dl_comm_unique_id_bytes())
+            ids = torch.zeros(2 * nb, dtype=torch.uint8)
+            if self.rank == 0:
+                for k in range(2):
+                    call("dl_comm_get_unique_id", ctypes.c_void_p(ids.data_ptr() + k * nb))
+            d = ids.cuda()
+            src = 0 if self.group is None else dist.get_global_rank(self.group, 0)
+            dist.broadcast(d, src, group=self.group)
+            ids = d.cpu()
+            comms = []
+            for k in range(2):
+                c = ctypes.c_void_p()
+                call("dl_comm_init", ctypes.c_void_p(ids.data_ptr() + k * nb), self.world, self.rank, ctypes.byref(c))
+                comms.append(c)
+            self._comm, self._comm_ar = comms
+        return self._comm, self._comm_ar
 
-    def counts(self, send_counts):
-        """All-to-all of one int per peer -> list of received counts."""
-        dev = "cpu" if self.staged else "cuda"
-        s = torch.tensor(send_counts, dtype=torch.int64, device=dev)
-        r = torch.empty_like(s)
-        dist.all_to_all_single(r, s, group=self.group)
-        return [int(x) for x in r.cpu().tolist()]
+    def block(self, p):
+        """This rank's block of its traffic with peer p (p == rank: its own, never moved)."""
+        return p if p == self.rank else self.world + p - (1 if p > self.rank else 0)
 
-    def count_matrix(self, owner_counts):
-        """All-gather of every rank's per-owner counts (device int32 [world+1]) -> host
-        [world][world+1] list: row r = what rank r sends to each owner (+ its replicated
-        count).  One collective and one device->host copy give both the send and the
-        receive splits."""
-        c = owner_counts.to(torch.int64)
-        if self.staged:
-            c = c.cpu()
-        if self.staged:
-            parts = [torch.empty_like(c) for _ in range(self.world)]
-            dist.all_gather(parts, c, group=self.group)
-            return torch.stack(parts).tolist()
-        out = torch.empty(self.world * c.numel(), dtype=torch.int64, device=c.device)
-        dist.all_gather_into_tensor(out, c, group=self.group)
-        return out.view(self.world, -1).cpu().tolist()
-
-    def count_matrix_async(self, owner_counts):
-        """count_matrix without blocking the host: the all-gather and a copy into pinned host
-        memory are queued behind the current stream's work; resolve_counts() waits only for
-        that copy.  (Host-staged backends resolve immediately.)"""
-        if self.staged:
-            return self.count_matrix(owner_counts)
-        c = owner_counts.to(torch.int64)
-        out = torch.empty(self.world * c.numel(), dtype=torch.int64, device=c.device)
-        dist.all_gather_into_tensor(out, c, group=self.group)
-        host = torch.empty(out.numel(), dtype=torch.int64, pin_memory=True)
-        host.copy_(out, non_blocking=True)
-        ev = torch.cuda.Event()
-        ev.record()
-        return (host, ev, c.numel())
-
-    @staticmethod
-    def resolve_counts(h):
-        if isinstance(h, list):
-            return h
-        host, ev, n = h
-        ev.synchronize()
-        return host.view(-1, n).tolist()
-
-    def _exchange_p2p(self, res, src, send_splits, recv_splits):
-        """RCCL all-to-all as grouped point-to-point transfers with the rank's own segment
-        copied on the current stream (a device copy at HBM speed instead of RCCL's few-CU
-        self-transfer: all of the data at one rank, half of it at two).  Returns the works."""
-        so = [0] * (self.world + 1)
-        ro = [0] * (self.world + 1)
-        for p in range(self.world):
-            so[p + 1] = so[p] + send_splits[p]
-            ro[p + 1] = ro[p] + recv_splits[p]
-        me = self.rank
-        if send_splits[me]:
-            res[ro[me]: ro[me + 1]].copy_(src[so[me]: so[me + 1]])
-        ops = []
-        for p in range(self.world):
-            if p == me:
-                continue
-            if send_splits[p]:
-                ops.append(dist.P2POp(dist.isend, src[so[p]: so[p + 1]], p, self.group))
-            if recv_splits[p]:
-                ops.append(dist.P2POp(dist.irecv, res[ro[p]: ro[p + 1]], p, self.group))
-        return dist.batch_isend_irecv(ops) if ops else []
-
-    def all_to_all(self, send, send_splits, recv_splits, out=None, async_op=False):
-        """Variable all-to-all along dim 0 (splits in rows).  `out` (device, contiguous,
-        sum(recv_splits) rows) receives in place — RCCL writes straight into it.
-        async_op (RCCL only): returns (result, work) with the collective running on
-        RCCL's stream; work.wait() orders the current stream after it."""
-        shape = (sum(recv_splits),) + tuple(send.shape[1:])
-        src = self._dev(send.contiguous())
-        direct = out is not None and not self.staged and out.is_contiguous()
-        res = out if direct else torch.empty(shape, dtype=send.dtype, device=src.device)
+    def blocks(self, arrays, direction, stream=None):
+        """arrays: [2W - 1, per-block elements] tensors.  direction 0 (to the owners): this rank's
+        block for peer p goes to p, p's arrives in block p; 1 (back): block p goes to p, p's
+        arrives in this rank's block for p."""
+        W, me = self.world, self.rank
+        if W == 1 or not arrays:
+            return
         if not self.staged:
-            works = self._exchange_p2p(res, src, list(send_splits), list(recv_splits))
-            if async_op:
-                copied = torch.cuda.Event()
-                copied.record()
-                return res, _Works(works, copied)
-            for w in works:
-                w.wait()
-            if direct:
-                return out
-            if out is not None:
-                out.copy_(res)
-                return out
-            return res
-        dist.all_to_all_single(res, src, output_split_sizes=list(recv_splits),
-                               input_split_sizes=list(send_splits), group=self.group)
-        if async_op:
-            res = res.to(send.device) if res.device != send.device else res
-            return res, None
-        if direct:
-            return out
-        res = res.to(send.device, non_blocking=False) if res.device != send.device else res
-        if out is not None:
-            out.copy_(res)
-            return out
-        return res
+            comm, _ = self._comms()
+            n = len(arrays)
+            bases = (ctypes.c_void_p * n)(*[a.data_ptr() for a in arrays])
+            bb = (ctypes.c_int64 * n)(*[a[0].numel() * a.element_size() for a in arrays])
+            call("dl_shard_exchange", comm, n, ctypes.cast(bases, ctypes.c_void_p), ctypes.cast(bb, ctypes.c_void_p),
+                 direction, _lib.stream_handle(stream))
+            return
+        for a in arrays:
+            h = a.cpu()
+            send = torch.zeros((W,) + tuple(h.shape[1:]), dtype=h.dtype)
+            for p in range(W):
+                if p != me:
+                    send[p] = h[self.block(p) if direction == 0 else p]
+            recv = torch.empty_like(send)
+            dist.all_to_all_single(recv, send, group=self.group)
+            for p in range(W):
+                if p != me:
+                    a[p if direction == 0 else self.block(p)].copy_(recv[p])
 
-    def all_reduce(self, t):
-        if self.world == 1:   # the sum over one rank is the input
+    def all_reduce(self, t, stream=None):
+        """Sum over the ranks, in place (inside the step: RCCL on `stream`)."""
+        if self.world == 1:
+            return t
+        if self.staged:
+            c = t.cpu()
+            dist.all_reduce(c, group=self.group)
+            t.copy_(c)
+            return t
+        _, comm_ar = self._comms()
+        call("dl_all_reduce_f32", comm_ar, ptr(t), ptr(t), t.numel(), _lib.stream_handle(stream))
+        return t
+
+    def host_sum(self, t):
+        """A sum outside the step (loss read-out): the torch process group."""
+        if self.world == 1:
             return t
         if self.staged and t.is_cuda:
             c = t.cpu()
@@ -185,12 +146,23 @@ class Exchange:
             dist.all_reduce(t, group=self.group)
         return t
 
+    def close(self):
+        """Release the RCCL communicators (after every rank's work is done)."""
+        for c in (self._comm, self._comm_ar):
+            if c is not None:
+                torch.cuda.synchronize()
+                call("dl_comm_destroy", c)
+        self._comm = self._comm_ar = None
+
 
 class ShardedCTREngine(CTREngine):
     """CTREngine whose embedding tables are row-sharded across the ranks of `exch`."""
 
+    # slack of a block over an even split of the batch's references (DLAMD_SHARD_SLACK)
+    SLACK = 0.25
+
     def __init__(self, spec, max_batch, exch, device="cuda", seed=2019, adam="dense", hist_len=4096,
-                 owner_update=None):
+                 owner_update=None, slack=None, lag=2):
         if spec.model not in ("deepfm_pipeline", "dnn_pipeline", "wdl"):
             raise ValueError("sharded path supports deepfm_pipeline / dnn_pipeline / wdl")
         self.exch = exch
@@ -200,47 +172,37 @@ class ShardedCTREngine(CTREngine):
         local_rows = -(-N // self.world)
         super().__init__(spec, max_batch, device=device, seed=seed, init="none", bwd="sorted",
                          table_rows=local_rows, adam=adam, hist_len=hist_len)
-        dev = self.dev
-        z = lambda *sh, dt=torch.float32: torch.zeros(*sh, dtype=dt, device=dev)
-        E = spec.E
+        z = lambda *sh, dt=torch.float32: torch.zeros(*sh, dtype=dt, device=self.dev)
+        E, W = spec.E, self.world
         self.local_rows = local_rows
-        # side stream (own hardware queue): the owner arrival chains and the record update of
-        # a step run there, the update overlapping the next step's start
         self.side = None
-        self.apply_done = None
-        # DLAMD_HOST_TIMING=1: host-side timestamps of the step's phases (diagnostics)
         self.host_marks = [] if os.environ.get("DLAMD_HOST_TIMING") else None
-        self.opt_snap = z(2, _lib.OPT_LEN)
+        self.slack = float(os.environ.get("DLAMD_SHARD_SLACK", self.SLACK)) if slack is None else float(slack)
+        self.lag = max(0, int(lag))
         if self.lazy:
-            # shard rows as records (rec.hip).  Owners group the ids they receive by row (a sort,
-            # or per-row arrival chains); the gradients come back in the same positions, so each
-            # row's arrivals are summed in ascending position order and applied once —
-            # deterministic, no dense gradient table.
-            # owner_update: "sort" (dl_sort_unique + dl_rec_apply_segments) or "chain"
-            # (dl_rec_chain_link + dl_rec_apply_chain: no sort; bit-identical records)
+            # owners group a step's arrivals by row with a sort (dl_sort_unique + apply_segments) or
+            # per-row arrival chains (dl_rec_chain_link + apply_chain); bit-identical records
             self.owner_update = owner_update or os.environ.get("DLAMD_OWNER_UPDATE", "sort")
             if self.owner_update not in ("sort", "chain"):
                 raise ValueError("owner_update must be 'sort' or 'chain'")
-            self.mv_u = None
-            self.own_cap = 0
             self.own_bits = max(1, int(self.rows_pad - 1).bit_length())
             if self.owner_update == "chain":
-                # arrival chains (rec.hip dl_rec_chain_link): head per local row, -1 = no arrival
                 self.own_head = torch.full((self.rows_pad,), -1, dtype=torch.int32, device=self.dev)
+        # the single-GPU engine's batch buffers this engine replaces (blocks, slots, its own stash)
+        self.mv_u = self.hot_ws = self.idx_inv = None
         R = max(self.rep, 1)
         rp = _ru(R, 16)
-        self.rep_t, self.rep_m, self.rep_v, self.rep_g = z(rp, E), z(rp, E), z(rp, E), z(rp, E)
-        self.rep_f, self.rep_fm, self.rep_fv, self.rep_fg = z(rp), z(rp), z(rp), z(rp)
-        self.rep_touched = z(rp, dt=torch.uint8)
+        self.rep_cap = rp if self.rep else 0
+        self.rep_t, self.rep_m, self.rep_v = z(rp, E), z(rp, E), z(rp, E)
+        self.rep_f, self.rep_fm, self.rep_fv = z(rp), z(rp), z(rp)
+        self.rep_all = torch.ones(rp, dtype=torch.uint8, device=self.dev)    # every replicated row steps
+        self.rep_scratch = z(rp, dt=torch.uint8)                               # touched flags nobody reads
+        self.rep_iota = torch.arange(rp, dtype=torch.int32, device=self.dev)
         n = self.n_refs
         self.inv = z(n, dt=torch.int32)
-        self.owner_counts = z(self.world + 1, dt=torch.int32)
-        self.send_ids = z(n, dt=torch.int32)
-        self.gU = z(n, E)
-        self.g1U = z(n)
-        self.rows_u = z(self.rep + n, E)
-        self.rows_u1 = z(self.rep + n)
-        # flat dense-gradient buffer: every layer's W_aug, the head, replicated rows
+        self.owner_counts = z(W + 1, dt=torch.int32)
+        self.upos = z(n, dt=torch.int32)
+        # flat dense-gradient buffer (one all-reduce): every layer's W_aug, the head, the replicated rows
         self.seg = []
         off = 0
         for l in range(len(spec.hidden)):
@@ -254,20 +216,95 @@ class ShardedCTREngine(CTREngine):
         self.rep_off = off
         off += rp * E + rp
         self.flat = z(off)
-        if self.rep:
-            self.rep_touched[: self.rep] = 1
+        self.opt[_lib.OPT_BAD_RANKS] = 0.0
         if self.wdl:
             self._init_wide(max_batch)
+        self.cap = self.wcap = 0
+        self._alloc_blocks(self._cap_for(self.n_refs), self._cap_for(getattr(self, "n_wrefs", 0)))
+        # the step's own streams: the gradient exchange and the owner sort (branches of the step
+        # graph), the all-reduce (second communicator); the ring of per-step status reports
+        self.x_stream = torch.cuda.Stream()
+        self.ar_stream = torch.cuda.Stream()
+        self.own_stream = torch.cuda.Stream()
+        self._ring = torch.zeros(8, dtype=torch.int32, pin_memory=True)
+        self._ring_np = self._ring.numpy()
+        self._ring_sent = None
+        self._hist_b = {}          # sequence -> batch of the steps not yet reported
+        self._steps_eager = 0
+
+    # ------------------------------------------------------------ block buffers
+    def _cap_for(self, n):
+        """Slots per block for n references a batch: all of them at one rank (no overflow
+        possible), else an even split plus the slack, rounded to 64."""
+        if n <= 0:
+            return 0
+        if self.world == 1:
+            return n
+        return min(n, _ru(int(np.ceil(n / self.world * (1.0 + self.slack))), 64))
+
+    def _alloc_blocks(self, cap, wcap):
+        """(Re)size everything whose shape follows the block capacity (first call, or growing
+        after an overflow: the graphs and any prefetch are dropped with it)."""
+        sp, E, W = self.spec, self.spec.E, self.world
+        z = lambda *sh, dt=torch.float32: torch.zeros(*sh, dtype=dt, device=self.dev)
+        nb = 2 * W - 1
+        self.cap, self.wcap, self.nb = cap, wcap, nb
+        rep, rc = self.rep, self.rep_cap
+        # rows: [replicated cont rows | 2W - 1 blocks | replicated group], gradients likewise
+        self.rows_u = z(rep + nb * cap + rc, E)
+        self.rows_u1 = z(rep + nb * cap + rc)
+        self.g_all = z(nb * cap + rc, E)
+        self.g1_all = z(nb * cap + rc)
+        per_batch = {"ids_all": z(nb * cap, dt=torch.int32), "hdr_all": z(nb * 4, dt=torch.int32),
+                     "rep_ids": z(max(rc, 1), dt=torch.int32)}
+        if self.wdl:
+            Fw, H = sp.Fw, sp.hidden[-1]
+            self.wloc_off = Fw + H
+            old = getattr(self, "wloc", None)
+            self.wloc = z(_ru(Fw + H + nb * wcap, 4))
+            if old is not None:   # the replicated deep-output rows carry over
+                self.wloc[Fw: Fw + H].copy_(old[Fw: Fw + H])
+            self.wgloc = z(Fw + H + nb * wcap, dt=torch.int64)
+            per_batch.update({"wids_all": z(nb * wcap, dt=torch.int32), "whdr_all": z(nb * 4, dt=torch.int32)})
+        for k, t in per_batch.items():
+            setattr(self, k, t)
+        if getattr(self, "_slots", None) is not None:
+            for sl in self._slots:
+                for k, t in per_batch.items():
+                    sl[k] = torch.zeros_like(t)
+            self._use_slot(self._cur)
+            self._pf = None
+            self._pfq = []
+            self._slot_free = [None] * len(self._slots)
+        if self.lazy:
+            self.own_mv = z(W * cap, 2 * E + 4) if self.owner_update == "sort" else None
+            if self.owner_update == "chain":
+                self.own_next = z(W * cap, dt=torch.int32)
+            elif W > 1:
+                ws = _lib.lib().dl_index_workspace_bytes(W * cap)
+                self.own_ws = z(ws, dt=torch.uint8)
+                self.own_keys, self.own_pos, self.own_uniq = (z(W * cap, dt=torch.int32) for _ in range(3))
+                self.own_off, self.own_n = z(W * cap + 1, dt=torch.int32), z(4, dt=torch.int32)
+            else:   # one sender: its block is already grouped by row (sorted, unique) — no sort
+                self.iota = torch.arange(cap + 1, dtype=torch.int32, device=self.dev)
+        self.graphs = {}
+
+    def _grow(self):
+        """After an overflow: every block twice as large (at most every reference a batch)."""
+        cap = min(self.n_refs, max(2 * self.cap, 64))
+        wcap = min(getattr(self, "n_wrefs", 0), max(2 * self.wcap, 64)) if self.wdl else 0
+        self._alloc_blocks(cap, wcap)
 
     def _init_wide(self, B):
         """wdl_weights sharded like the table (row r on rank r % world), plus the per-rank local
         wide table the cross logit reads: wloc = [unused (Fw) | deep-output rows Fw..Fw+H,
-        replicated | this batch's exchanged unique wide rows].  The head (dl_wdl_head_fwd_bwd)
-        then runs unchanged on local ids and leaves each unique row's gradient in wgloc."""
+        replicated | the exchange blocks of this batch's wide rows].  The head
+        (dl_wdl_head_fwd_bwd) runs unchanged on local ids and leaves each exchanged row's
+        gradient in wgloc at the same slot."""
         sp = self.spec
         W = self.world
         z = lambda *sh, dt=torch.float32: torch.zeros(*sh, dtype=dt, device=self.dev)
-        Fw, H = sp.Fw, sp.hidden[-1]
+        Fw = sp.Fw
         self.w_local = -(-self.w_rows // W)
         wl = _ru(self.w_local, 16)
         self.ww, self.wm, self.wv = z(wl), z(wl), z(wl)
@@ -276,13 +313,7 @@ class ShardedCTREngine(CTREngine):
         self.wide_reg = z(4)
         nw = B * Fw
         self.n_wrefs = nw
-        self.wloc_off = Fw + H
-        self.wloc_rows = Fw + H + nw
-        self.wloc = z(_ru(self.wloc_rows, 4))
-        self.wgloc = z(self.wloc_rows, dt=torch.int64)
         self.in_wide_loc = z(B, Fw, dt=torch.int64)
-        self.deep_buf = z(_ru(H, 4))
-        # the wide ids' batch index (owner-grouped unique rows, inverse map), per buffer set
         wsb = _lib.lib().dl_index_workspace_bytes(max(1, nw))
         self.widx_ws = z(wsb, dt=torch.uint8)
         self.widx_keys, self.widx_refs, self.widx_uniq = (z(nw, dt=torch.int32) for _ in range(3))
@@ -290,7 +321,6 @@ class ShardedCTREngine(CTREngine):
         self.widx_n = z(4, dt=torch.int32)
         self.winv = z(nw, dt=torch.int32)
         self.wowner_counts = z(W + 1, dt=torch.int32)
-        self.wsend_ids = z(nw, dt=torch.int32)
         WL = _lib.EmbLayout()
         WL.n_rows = self.w_rows
         WL.batch = B
@@ -300,27 +330,6 @@ class ShardedCTREngine(CTREngine):
         WL.use_fm = 0
         WL.zero_row0 = 0
         self.wlayout = WL
-
-    def _owner_buffers(self, n):
-        """(Re)size the owner-side arrival-chain buffer for n received ids."""
-        if n > self.own_cap:
-            self._join_side()   # the previous step's update on the side stream still reads them
-        if n <= self.own_cap:
-            return
-        cap = max(n, int(self.own_cap * 1.25), 1 << 16)
-        # empty, not zeros: a fill queued on the compute stream could land after the side
-        # stream has written them (the sort / the link write every entry later read)
-        e = lambda k, dt=torch.int32: torch.empty(k, dtype=dt, device=self.dev)
-        if self.owner_update == "chain":
-            self.own_next = e(cap)
-        else:
-            self.own_ws = e(_lib.lib().dl_index_workspace_bytes(cap), torch.uint8)
-            self.own_keys, self.own_pos, self.own_uniq = e(cap), e(cap), e(cap)
-            self.own_off, self.own_n = e(cap + 1), e(4)
-            # the owner gather's moment stash [cap][2E+4], read back by the sorted update
-            # (the arrival-chain update re-reads the record instead: no stash)
-            self.own_mv = e(cap * (2 * self.spec.E + 4), torch.float32)
-        self.own_cap = cap
 
     # ------------------------------------------------------------ parameters
     def owned_rows(self):
@@ -395,7 +404,7 @@ class ShardedCTREngine(CTREngine):
                  seed + 3, self.rank * self.ww.numel(), s)
             self.ww[self.w_local:].zero_()
             self.wb[0] = float(np.random.default_rng(seed).standard_normal())
-            self._wide_refresh()
+            self._wide_refresh(s)
         if self.first is not None:
             call("dl_init_random", ptr(self.first), _ru(self.first.numel(), 4), 1, 0.0, 1.0, seed + 1,
                  self.rank * _ru(self.first.numel(), 4), s)
@@ -423,33 +432,6 @@ class ShardedCTREngine(CTREngine):
     def params(self):
         raise NotImplementedError("gather shards with gather_params()")
 
-    def _owner_apply_args(self, recv_ids, nrecv, gb, g1b, opt, stream):
-        """Entry point + arguments of the owners' record update (one per arriving row)."""
-        sp = self.spec
-        g1 = ptr(g1b) if sp.fm else None
-        if self.owner_update == "chain":
-            return ("dl_rec_apply_chain", ptr(self.rec), self.rec_ld, sp.E, self.rec_flags, ptr(recv_ids), nrecv,
-                    ptr(self.own_head), ptr(self.own_next), ptr(gb), g1, ptr(self.hist), self.hist_len, ptr(opt),
-                    stream)
-        # the owner gather's outputs at every arrival: the caught-up state (no second replay)
-        rows, rows1 = self.own_rows
-        return ("dl_rec_apply_segments", ptr(self.rec), self.rec_ld, sp.E, self.rec_flags, ptr(self.own_uniq),
-                ptr(self.own_off), ptr(self.own_n), nrecv, nrecv, ptr(self.own_pos), ptr(gb), g1, ptr(rows),
-                ptr(rows1) if sp.fm else None, ptr(self.own_mv), ptr(self.hist), self.hist_len, ptr(opt), stream)
-
-    def _mark(self, name):
-        if self.host_marks is not None:
-            self.host_marks.append((name, time.perf_counter()))
-
-    def _join_side(self):
-        """Order the compute stream after everything queued on the side stream."""
-        if self.side is not None:
-            torch.cuda.current_stream().wait_stream(self.side)
-
-    def flush(self):
-        self._join_side()
-        super().flush()
-
     def shard_state(self):
         """(global rows, table rows, first-order) of this rank's shard (host numpy)."""
         rows = self.owned_rows()
@@ -465,35 +447,143 @@ class ShardedCTREngine(CTREngine):
         f = self.first[: self.local_rows].cpu().numpy()[ok] if self.first is not None else None
         return rows[ok], t, f
 
-    def _wide_exchange(self, B, cmw):
-        """The wide lookup: unique wide rows' ids to their owners, the owners' current values
-        back into the local wide table, local ids for the head.  Returns (send, recv, recv_ids)
-        for the gradient return."""
-        ex = self.exch
-        W = self.world
-        s = _lib.stream_handle()
-        wsend = cmw[self.rank][:W]
-        nwsend = sum(wsend)
-        wrecv = [cmw[r][self.rank] for r in range(W)]
-        nwrecv = sum(wrecv)
-        wrecv_ids = ex.all_to_all(self.wsend_ids[:nwsend], wsend, wrecv)
-        wout = torch.empty(max(nwrecv, 1), device=self.dev)
-        if nwrecv:
-            call("dl_shard_gather_scalar", ptr(self.ww), ptr(wrecv_ids), nwrecv, ptr(wout), s)
-        off = self.wloc_off
-        ex.all_to_all(wout[:nwrecv], wrecv, wsend, out=self.wloc[off: off + nwsend])
-        call("dl_wide_local_ids", ptr(self.winv), B * self.spec.Fw, off, ptr(self.in_wide_loc), s)
-        return wsend, wrecv, wrecv_ids
+    def wide_state(self):
+        """(global rows, wdl_weights values) of this rank's shard of wdl_weights (host numpy)."""
+        rows = np.arange(self.w_local) * self.world + self.rank
+        ok = rows < self.w_rows
+        return rows[ok], self.ww[: self.w_local].cpu().numpy()[ok]
 
-    def _wide_refresh(self):
-        """Every rank's copy of the deep-output rows Fw..Fw+H of wdl_weights (read by the cross
-        logit) from their owners: one [H] sum all-reduce."""
+    @property
+    def last_counts(self):
+        """(unique rows this rank's batch needs from owners, replicated rows, rows it served as an
+        owner) of the last step (bench.py prices the per-kernel work with them)."""
+        W = self.world
+        oc = self.owner_counts.tolist()
+        h = self.hdr_all[: 4 * W].view(W, 4)[:, 0].tolist()
+        return sum(oc[:W]), oc[W], sum(h)
+
+    # ------------------------------------------------------------ the step's pieces
+    def _mark(self, name):
+        if self.host_marks is not None:
+            self.host_marks.append((name, time.perf_counter()))
+
+    def _own_layout(self):
+        """The owner gather's layout: local rows (an empty slot's -1 decodes past them)."""
+        L = self._layout(self.B)
+        L.n_rows = self.local_rows
+        return L
+
+    # the per-batch buffers (double-buffered with prefetch): inputs, the index, the route
+    SLOT_ATTRS = CTREngine.SLOT_ATTRS + ("inv", "owner_counts", "upos", "ids_all", "hdr_all", "rep_ids", "widx_ws",
+                                         "widx_keys", "widx_refs", "widx_uniq", "widx_off", "widx_n", "winv",
+                                         "wowner_counts", "wids_all", "whdr_all", "in_wide_loc")
+
+    def _pre(self, B):
+        """Index + route the staged batch on the current stream (the prefetch's work): the
+        unique rows grouped by owner into this rank's blocks, the inverse map remapped to slots,
+        the headers; for wdl the wide ids likewise and the head's local wide ids."""
+        s = _lib.stream_handle()
+        L = self.layout
+        L.batch = B
+        W = self.world
+        # the batch's validation word starts clear (the index builds set it for a bad id)
+        call("dl_validate_batch", C_ref(L), None, None, 0, 1, 0, 1, ptr(self.err), s)
+        self._c("index_build", "dl_index_build", C_ref(L), ptr(self.in_cate), W, self.rep,
+                ptr(self.idx_ws), self.idx_ws.numel(), ptr(self.idx_keys), ptr(self.idx_refs), ptr(self.idx_uniq),
+                ptr(self.idx_off), ptr(self.idx_n), ptr(self.inv), ptr(self.owner_counts), ptr(self.err), s)
+        n = B * self.n_slot
+        self._c("route", "dl_shard_route", ptr(self.idx_uniq), ptr(self.idx_n), ptr(self.owner_counts), W, self.rank,
+                self.cap, self.rep_cap, ptr(self.err), ptr(self.ids_all), ptr(self.hdr_all),
+                ptr(self.rep_ids) if self.rep_cap else None, ptr(self.upos), ptr(self.inv), n, n, s)
+        if self.wdl:   # the wide ids (dl_index_build range-checks them against w_rows)
+            WL = self.wlayout
+            WL.batch = B
+            sp = self.spec
+            self._c("index_build_wide", "dl_index_build", C_ref(WL), ptr(self.in_wide), W, 0,
+                    ptr(self.widx_ws), self.widx_ws.numel(), ptr(self.widx_keys), ptr(self.widx_refs),
+                    ptr(self.widx_uniq), ptr(self.widx_off), ptr(self.widx_n), ptr(self.winv),
+                    ptr(self.wowner_counts), ptr(self.err), s)
+            nw = B * sp.Fw
+            self._c("route_wide", "dl_shard_route", ptr(self.widx_uniq), ptr(self.widx_n), ptr(self.wowner_counts), W,
+                    self.rank, self.wcap, 0, ptr(self.err), ptr(self.wids_all), ptr(self.whdr_all), None, None,
+                    ptr(self.winv), nw, 0, s)
+            call("dl_wide_local_ids", ptr(self.winv), nw, self.wloc_off, ptr(self.in_wide_loc), s)
+
+    def _requests(self, s):
+        """Step 1: the requests (ids + headers) to their owners, stamped with this rank's sticky
+        faults and step."""
+        W, me = self.world, self.rank
+        call("dl_shard_stamp", ptr(self.hdr_all), W, me, ptr(self.opt), s)
+        arrs = [self.ids_all.view(self.nb, self.cap), self.hdr_all.view(self.nb, 4)]
+        if self.wdl:
+            arrs += [self.wids_all.view(self.nb, self.wcap), self.whdr_all.view(self.nb, 4)]
+        self._c("x_requests", "exchange", lambda: self.exch.blocks(arrs, 0))
+
+    def _c(self, label, name, *args):
+        """_c of the engine; name 'exchange' runs a Python callable (a collective) timed alike."""
+        if name != "exchange":
+            return super()._c(label, name, *args)
+        fn = args[0]
+        if self.prof is None:
+            return fn()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        fn()
+        e1.record()
+        self.prof.append((label, e0, e1))
+
+    def _gather_owned(self, B, s, lag):
+        """Step 3: the owner side — every requested row (blocks [0, W) of ids_all) caught up to
+        step t - lag into this rank's answer blocks; the wide values likewise."""
         sp = self.spec
-        H = sp.hidden[-1]
-        call("dl_wide_owned_values", ptr(self.ww), H, sp.Fw, self.world, self.rank, ptr(self.deep_buf),
-             _lib.stream_handle())
-        self.exch.all_reduce(self.deep_buf)
-        self.wloc[sp.Fw: sp.Fw + H].copy_(self.deep_buf[:H])
+        E, W, rep, cap = sp.E, self.world, self.rep, self.cap
+        rows, rows1 = self.rows_u[rep:], self.rows_u1[rep:]
+        if self.lazy:
+            stash = lag == 1 and self.own_mv is not None
+            self._c("rec_gather", "dl_rec_gather", C_ref(self._own_layout()), ptr(self.rec), self.rec_ld,
+                    self.rec_flags, 0, ptr(self.ids_all), None, W * cap, 1, ptr(self.hist), self.hist_len,
+                    ptr(self.opt), lag, ptr(rows), ptr(rows1) if sp.fm else None, ptr(self.own_mv) if stash else None,
+                    s)
+        else:
+            self._c("rec_gather", "dl_shard_gather", ptr(self.table), ptr(self.first), ptr(self.ids_all), W * cap, E,
+                    ptr(rows), ptr(rows1) if self.first is not None else None, s)
+        if self.wdl:
+            self._c("wide_gather", "dl_shard_gather_scalar", ptr(self.ww), ptr(self.wids_all), W * self.wcap,
+                    ptr(self.wloc[self.wloc_off:]), s)
+
+    def _answers(self, s):
+        """Step 4: the answers back to the senders (rows + first-order weights + wide values, one
+        group), then the replicated rows (cont fields, and those cate ids reference) locally."""
+        sp = self.spec
+        E, rep, nb, cap = sp.E, self.rep, self.nb, self.cap
+        arrs = [self.rows_u[rep: rep + nb * cap].view(nb, cap * E)]
+        if sp.fm:
+            arrs.append(self.rows_u1[rep: rep + nb * cap].view(nb, cap))
+        if self.wdl:
+            o = self.wloc_off
+            arrs.append(self.wloc[o: o + nb * self.wcap].view(nb, self.wcap))
+        self._c("x_answers", "exchange", lambda: self.exch.blocks(arrs, 1))
+        if rep:
+            f = self.rep_f if sp.fm else None
+            call("dl_shard_gather", ptr(self.rep_t), ptr(f), ptr(self.rep_iota), rep, E, ptr(self.rows_u),
+                 ptr(self.rows_u1) if sp.fm else None, s)
+            o = rep + nb * cap
+            call("dl_shard_gather", ptr(self.rep_t), ptr(f), ptr(self.rep_ids), self.rep_cap, E, ptr(self.rows_u[o:]),
+                 ptr(self.rows_u1[o:]) if sp.fm else None, s)
+
+    def _forward_local(self, B, s, train):
+        """Step 5a: the forward on this rank's batch from the exchanged rows."""
+        sp = self.spec
+        L = self.layout
+        L.batch = B
+        self._c("embed_fwd", "dl_embed_fwd_indexed", C_ref(L), ptr(self.rows_u), ptr(self.rows_u1) if sp.fm else None,
+                ptr(self.inv), self.rep, ptr(self.in_cont), ptr(self.in_vec),
+                ptr(self.x0b if self.x0_direct else self.x0), ptr(self.fm_out), ptr(self.fm_sum), s)
+        if self.bf and not self.x0_direct:
+            self._c("cast_x0", "dl_cast_bf16", ptr(self.x0), B, self.in_ld[0], self.in_ld[0], ptr(self.x0b),
+                    self.in_ld[0], s)
+        self._tower_fwd(B, s)
+        self._head(B, s, train)
 
     def _tower_fwd(self, B, s):
         """Deep tower forward from x0 (f32 / three-plane split on bf16 MFMA / bf16 tower)."""
@@ -524,7 +614,7 @@ class ShardedCTREngine(CTREngine):
 
     def _head(self, B, s, train=True):
         """Output layer + loss: the FM / deep_res head, or the wdl cross logit on the local
-        wide table (gradients of the exchanged wide rows left in wgloc)."""
+        wide table (gradients of the exchanged wide rows left in wgloc at their slots)."""
         sp = self.spec
         H = sp.hidden[-1]
         inv_b = 1.0 / (B * self.world)
@@ -533,7 +623,7 @@ class ShardedCTREngine(CTREngine):
                 self.wgloc.zero_()
             fn, dh_last = ("dl_wdl_head_fwd_bwd_bf16", self.dhb[-1]) if self.bf else ("dl_wdl_head_fwd_bwd", self.dh[-1])
             self._c("head", fn, B, sp.Fw, H, ptr(self.in_wide_loc), sp.Fw, ptr(self.h[-1]), self.h_ld[-1],
-                    ptr(self.wloc), ptr(self.wb), self.wloc_rows, ptr(self.in_label), sp.logloss_eps, inv_b,
+                    ptr(self.wloc), ptr(self.wb), self.wgloc.numel(), ptr(self.in_label), sp.logloss_eps, inv_b,
                     ptr(self.score), ptr(self.z), ptr(self.dz), ptr(dh_last), ptr(self.wgloc) if train else None,
                     None, ptr(self.head_slab), self.head_blocks, ptr(self.err), s)
             return
@@ -541,34 +631,11 @@ class ShardedCTREngine(CTREngine):
                 self.h_ld[-1], ptr(self.w_head), ptr(self.in_label), sp.logloss_eps, inv_b, ptr(self.score),
                 ptr(self.z), ptr(self.dz), ptr(self.dh[-1]), ptr(self.head_slab), self.head_blocks, s)
 
-    def wide_state(self):
-        """(global rows, wdl_weights values) of this rank's shard of wdl_weights (host numpy)."""
-        rows = np.arange(self.w_local) * self.world + self.rank
-        ok = rows < self.w_rows
-        return rows[ok], self.ww[: self.w_local].cpu().numpy()[ok]
-
-    def _mid_a(self, B):
-        """Steps 5-6a: forward, head, the input-gradient chain down to dx0 and the per-row
-        embedding gradients — fixed buffers and sizes for a batch size, so
-        train_step(graph=True) replays it as one hipGraph (the exchanges around it need
-        host-known sizes and stay eager).  The weight gradients are left to _mid_b, which
-        runs while the embedding gradients are in flight to their owners."""
+    def _input_grads(self, B, s):
+        """Step 5b: the input-gradient chain, top layer down to dx0, then every unique row's
+        gradient into its slot (dl_embed_bwd_sorted with the route's slots)."""
         sp = self.spec
-        s = _lib.stream_handle()
         L = self.layout
-        L.batch = B
-        W = self.world
-        rep = self.rep
-        # 5. forward
-        self._c("embed_fwd", "dl_embed_fwd_indexed", C_ref(L), ptr(self.rows_u), ptr(self.rows_u1) if sp.fm else None,
-                ptr(self.inv), rep, ptr(self.in_cont), ptr(self.in_vec), ptr(self.x0b if self.x0_direct else self.x0),
-                ptr(self.fm_out), ptr(self.fm_sum), s)
-        if self.bf and not self.x0_direct:
-            self._c("cast_x0", "dl_cast_bf16", ptr(self.x0), B, self.in_ld[0], self.in_ld[0], ptr(self.x0b),
-                    self.in_ld[0], s)
-        self._tower_fwd(B, s)
-        self._head(B, s)
-        # 6a. input gradients, top layer down
         nl = len(sp.hidden)
         if self.bf and not self.wdl:
             self._c("cast_dh", "dl_cast_bf16", ptr(self.dh[-1]), B, self.h_ld[-1], self.h_ld[-1], ptr(self.dhb[-1]),
@@ -607,16 +674,16 @@ class ShardedCTREngine(CTREngine):
             else:
                 self._c("gemm_dx_l0", "dl_gemm_f32", 0, 0, B, self.dx_cols, self.out_ld[0], ptr(self.dh[0]),
                         self.h_ld[0], ptr(self.Wt), self.in_ld[0], ptr(self.dx0), self.dx_ld, 0, None, 0, 1, 0, s)
-        # embedding gradients per unique row -> owners
-        self._c("embed_bwd", "dl_embed_bwd_sorted", C_ref(L), None, ptr(self.rows_u[rep:]), ptr(self.idx_uniq),
-                ptr(self.idx_off), ptr(self.idx_n), ptr(self.idx_refs), W, self.n_refs, ptr(self.dz),
-                ptr(self.w_head), ptr(self.fm_sum), ptr(self.dx0), ptr(self.gU), ptr(self.g1U), None, 1, s)
+        self._c("embed_bwd", "dl_embed_bwd_sorted", C_ref(L), None, ptr(self.rows_u[self.rep:]), ptr(self.idx_uniq),
+                ptr(self.idx_off), ptr(self.idx_n), ptr(self.idx_refs), self.world, B * self.n_slot, ptr(self.dz),
+                ptr(self.w_head), ptr(self.fm_sum), ptr(self.dx0), ptr(self.g_all), ptr(self.g1_all), None, 1,
+                ptr(self.upos), s)
 
-    def _mid_b(self, B):
-        """Step 6b: weight gradients (split-K slabs summed into the flat all-reduce buffer)
-        and the head's column sums — overlaps the embedding-gradient all-to-all."""
+    def _weight_grads(self, B, s):
+        """Step 6 (main branch): weight gradients (split-K slabs summed into the flat buffer), the
+        head's column sums, the replicated rows' gradients — beside the gradient exchange."""
         sp = self.spec
-        s = _lib.stream_handle()
+        E, L = sp.E, self.layout
         nl = len(sp.hidden)
         dws = self._dw_splits(B, fixed="DLAMD_DW_SPLITS" in os.environ)
         for l in reversed(range(nl)):
@@ -636,400 +703,353 @@ class ShardedCTREngine(CTREngine):
                 self._c("gemm_dw_l%d" % l, "dl_gemm_f32", 1, 0, self.in_ld[l], hdim, B, ptr(xin), self.in_ld[l],
                         ptr(self.dh[l]), self.h_ld[l], ptr(self.w_slab), self.out_ld[l], 3, None, 0, splits, stride,
                         s)
-            call("dl_slab_sum", ptr(self.w_slab), _num_splits(B, splits, 64 if (self.s3 or self.bf) else 16), stride,
-                 stride, ptr(self.flat[self.seg[l][1]:]), s)
+            self._c("slab_sum_l%d" % l, "dl_slab_sum", ptr(self.w_slab),
+                    _num_splits(B, splits, 64 if (self.s3 or self.bf) else 16), stride, stride,
+                    ptr(self.flat[self.seg[l][1]:]), s)
         hoff = self.seg[nl][1]
-        call("dl_slab_sum", ptr(self.head_slab), call_int(self.head_grid, B), self.head_w, self.head_w,
-             ptr(self.flat[hoff:]), s)
-
-    def _mid(self, B):
-        self._mid_a(B)
-        self._mid_b(B)
-
-    def _replay(self, name, fn, B):
-        """Capture fn(B) once per batch size as a hipGraph, then replay it."""
-        g = getattr(self, name, None)
-        if g is None or g[1] != B:
-            st = torch.cuda.Stream()
-            st.wait_stream(torch.cuda.current_stream())
-            cg = torch.cuda.CUDAGraph()
-            with capture_guard(), torch.cuda.graph(cg, stream=st, capture_error_mode="thread_local"):
-                fn(B)
-            torch.cuda.current_stream().wait_stream(st)
-            g = (cg, B)
-            setattr(self, name, g)
-        g[0].replay()
-
-    # ------------------------------------------------------------ step
-    SLOT_ATTRS = CTREngine.SLOT_ATTRS + ("inv", "owner_counts", "send_ids", "widx_ws", "widx_keys", "widx_refs",
-                                         "widx_uniq", "widx_off", "widx_n", "winv", "wowner_counts", "wsend_ids")
-
-    def _index(self, B):
-        """Step 1 on the current stream: the batch index (rows grouped by owner, replicated rows
-        last) and the owner-local ids to send."""
-        s = _lib.stream_handle()
-        L = self.layout
-        L.batch = B
-        self._c("index_build", "dl_index_build", C_ref(L), ptr(self.in_cate), self.world, self.rep,
-                ptr(self.idx_ws), self.idx_ws.numel(), ptr(self.idx_keys), ptr(self.idx_refs), ptr(self.idx_uniq),
-                ptr(self.idx_off), ptr(self.idx_n), ptr(self.inv), ptr(self.owner_counts), ptr(self.err), s)
-        call("dl_keys_to_local", ptr(self.idx_uniq), ptr(self.idx_n), self.n_refs, ptr(self.send_ids), s)
-        if self.wdl:   # the wide ids: unique wdl_weights rows grouped by owner, inverse map
-            WL = self.wlayout
-            WL.batch = B
-            self._c("index_build_wide", "dl_index_build", C_ref(WL), ptr(self.in_wide), self.world, 0,
-                    ptr(self.widx_ws), self.widx_ws.numel(), ptr(self.widx_keys), ptr(self.widx_refs),
-                    ptr(self.widx_uniq), ptr(self.widx_off), ptr(self.widx_n), ptr(self.winv),
-                    ptr(self.wowner_counts), ptr(self.err), s)
-            call("dl_keys_to_local", ptr(self.widx_uniq), ptr(self.widx_n), self.n_wrefs, ptr(self.wsend_ids), s)
-
-    def _count_vec(self):
-        """The per-owner counts every rank all-gathers: table rows (+ replicated), and for wdl
-        the wide rows too (one collective for both), then the batch's id-validation word, so
-        every rank learns from the same collective whether any rank's batch holds a bad id."""
-        parts = [self.owner_counts] + ([self.wowner_counts] if self.wdl else []) + [self.err[:1]]
-        return torch.cat(parts)
-
-    def _split_counts(self, cm):
-        """Strip the id-validation column off the all-gathered counts.  A bad id on any rank
-        raises on every rank before the step begins (TF's InvalidArgumentError in the failing
-        sess.run, deepfm_pipeline.py:219-221): nothing is exchanged or applied, the optimizer
-        step does not advance, and the replicas stay identical."""
-        bad = [r for r, row in enumerate(cm) if int(row[-1]) != 0]
-        if bad:
-            for w in self._error_words():
-                w.zero_()
-            raise _lib.DLError("InvalidArgumentError: categorical id out of range [0, %d) in the batch of rank(s) "
-                               "%s — the step applied no update" % (self.N, bad))
-        return [row[:-1] for row in cm]
-
-    def _drop_prefetch(self, pf):
-        """A prefetched batch that will not be trained: its counts are consumed and a bad id
-        it carried is forgotten with it (its buffer set's validation word cleared)."""
-        cm = self.exch.resolve_counts(pf[4])
-        if any(int(row[-1]) != 0 for row in cm):
-            self._slots[pf[0]]["err"].zero_()
-        self._pf = None
-
-    def prefetch(self, batch):
-        """Stage the next batch, build its index and exchange its counts on the side stream
-        while the current step runs; the next train_step(batch) starts at its id exchange with
-        no host wait on the GPU (the counts are in pinned memory by then)."""
-        self._enable_slots()
-        if self._pf is not None:
-            torch.cuda.current_stream().wait_event(self._pf[2])
-        cur = self._cur
-        k = 1 - cur
-        side = self._side_stream()
-        if self._slot_free[k] is not None:
-            side.wait_event(self._slot_free[k])
-        else:
-            side.wait_stream(torch.cuda.current_stream())
-        self._use_slot(k)
-        try:
-            with torch.cuda.stream(side):
-                B = self.stage(batch)
-                self._index(B)
-                counts = self.exch.count_matrix_async(self._count_vec())
-                ev = torch.cuda.Event()
-                ev.record(side)
-        finally:
-            self._use_slot(cur)
-        self._pf = (k, B, ev, batch, counts)
-
-    def train_step(self, batch=None, graph=False, next_batch=None):
-        sp = self.spec
-        ex = self.exch
-        E = sp.E
-        pf = getattr(self, "_pf", None)
-        counts = None
-        if pf is not None and batch is not None and batch is pf[3]:
-            self._pf = None
-            self._use_slot(pf[0])
-            torch.cuda.current_stream().wait_event(pf[2])
-            B, counts = pf[1], pf[4]
-        else:
-            if pf is not None:   # a different batch came: drop the prefetch (after it lands)
-                torch.cuda.current_stream().wait_event(pf[2])
-                self._drop_prefetch(pf)
-            B = self.stage(batch) if batch is not None else self.B
-        s = _lib.stream_handle()
-        L = self.layout
-        L.batch = B
-        W = self.world
-        lazy = self.lazy
-        self._mark("start")
-        if lazy:
-            if self.since_flush >= self.hist_len - 2:   # bound every row's lag below the alpha ring
-                self.flush()
-            self.since_flush += 1
-        if counts is None:
-            # 1. index + 2. counts: every rank's per-owner counts in one all-gather (host waits)
-            self._index(B)
-            cm = ex.count_matrix(self._count_vec())
-        else:
-            cm = ex.resolve_counts(counts)
-        cm = self._split_counts(cm)   # raises on every rank if any rank's batch has a bad id
-        # the step begins once every rank's ids are known to be valid
-        call("dl_adam_begin_step", ptr(self.opt), sp.decay_rate, float(sp.decay_steps), s)
-        if lazy:
-            call("dl_adam_hist_record", ptr(self.opt), ptr(self.hist), self.hist_len, s)
-        cmw = [row[W + 1:] for row in cm] if self.wdl else None
-        self._mark("index_launched")
-        send = cm[self.rank][:W]
-        nsend, nrep = sum(send), cm[self.rank][W]
-        U = nsend + nrep
-        recv = [cm[r][self.rank] for r in range(W)]
-        nrecv = sum(recv)
-        self.last_counts = (nsend, nrep, nrecv)   # bench.py prices the per-kernel work with these
-        self._mark("counts")
-        recv_ids = ex.all_to_all(self.send_ids[:nsend], send, recv)
-        self._mark("ids_a2a")
-        # optimizer scalars of this step for the record update on the side stream (the next
-        # step's adam_begin advances opt; two buffers: the update of step t-1 may still read one)
-        snap = self.opt_snap[self.steps % 2]
-        snap.copy_(self.opt)
-        ids_ready = torch.cuda.Event()
-        ids_ready.record()
-        # 3. owners gather requested rows
-        out_v = torch.empty(max(nrecv, 1), E, device=self.dev)
-        out_1 = torch.empty(max(nrecv, 1), device=self.dev)
-        if nrecv and lazy:   # rows caught up to the previous step (read only)
-            if self.apply_done is not None:   # the previous step's record update (side stream)
-                torch.cuda.current_stream().wait_event(self.apply_done)
-            self._owner_buffers(nrecv)
-            stash = self.owner_update == "sort"   # the update reads the caught-up state back
-            self._c("rec_gather", "dl_rec_gather", C_ref(L), ptr(self.rec), self.rec_ld, self.rec_flags, 0,
-                    ptr(recv_ids), None, nrecv, 1, ptr(self.hist), self.hist_len, ptr(self.opt), 1, ptr(out_v),
-                    ptr(out_1) if sp.fm else None, ptr(self.own_mv) if stash else None, s)
-            self.own_rows = (out_v, out_1)
-        elif nrecv:
-            call("dl_shard_gather", ptr(self.table), ptr(self.first), ptr(recv_ids), nrecv, E, ptr(out_v),
-                 ptr(out_1) if self.first is not None else None, s)
-        self._mark("gather")
-        link_done = None
-        if nrecv and lazy:
-            # link this step's arrivals into per-row chains, for the update at the end of the
-            # step: on the side stream, after the previous update reset the chain heads
-            # (launched after the gather, so the host queues the critical path first)
-            self._owner_buffers(nrecv)
-            self._side_stream().wait_event(ids_ready)   # only the received ids, not the gather queued since
-            with torch.cuda.stream(self.side):
-                if self.owner_update == "chain":
-                    call("dl_rec_chain_link", ptr(recv_ids), nrecv, ptr(self.own_head), ptr(self.own_next),
-                         _lib.stream_handle(self.side))
-                else:
-                    call("dl_sort_unique", ptr(recv_ids), nrecv, self.own_bits, ptr(self.own_ws),
-                         self.own_ws.numel(), ptr(self.own_keys), ptr(self.own_pos), ptr(self.own_uniq),
-                         ptr(self.own_off), ptr(self.own_n), None, _lib.stream_handle(self.side))
-                link_done = torch.cuda.Event()
-                link_done.record(self.side)
-            recv_ids.record_stream(self.side)
-        self._mark("link")
-        # 4. rows back, in unique-id order
-        rep = self.rep
-        ex.all_to_all(out_v[:nrecv], recv, send, out=self.rows_u[rep: rep + nsend])
-        if sp.fm:
-            ex.all_to_all(out_1[:nrecv], recv, send, out=self.rows_u1[rep: rep + nsend])
-        if rep:
-            self.rows_u[:rep].copy_(self.rep_t[:rep])
-            if sp.fm:
-                self.rows_u1[:rep].copy_(self.rep_f[:rep])
-        if nrep:   # replicated rows referenced by cate ids: local rows of the replica
-            call("dl_shard_gather", ptr(self.rep_t), ptr(self.rep_f) if sp.fm else None,
-                 ptr(self.send_ids[nsend:U]), nrep, E, ptr(self.rows_u[rep + nsend:]),
-                 ptr(self.rows_u1[rep + nsend:]) if sp.fm else None, s)
-        wx = self._wide_exchange(B, cmw) if self.wdl else None
-        self._mark("rows_a2a")
-        if next_batch is not None:
-            # after this step's row exchange is queued: the count all-gather it issues sits
-            # behind it on RCCL's stream, and ahead of this step's gradient exchange
-            self.prefetch(next_batch)
-        replay = graph and self.prof is None
-        slot = getattr(self, "_cur", 0)
-        if replay:
-            self._replay("graph_a%d" % slot, self._mid_a, B)
-        else:
-            self._mid_a(B)
-        self._mark("mid_a")
-        # embedding gradients to their owners, in flight while the weight gradients run
-        gb, w_g = ex.all_to_all(self.gU[:nsend], send, recv, async_op=True)
-        g1b, w_g1 = ex.all_to_all(self.g1U[:nsend], send, recv, async_op=True) if sp.fm else (None, None)
-        if self.wdl:   # the exchanged wide rows' gradients (int64 fixed point) back to their owners
-            off = self.wloc_off
-            wg_in, w_gw = ex.all_to_all(self.wgloc[off: off + sum(wx[0])], wx[0], wx[1], async_op=True)
-        if replay:
-            self._replay("graph_b%d" % slot, self._mid_b, B)
-        else:
-            self._mid_b(B)
-        self._mark("mid_b")
-        side_apply = lazy and nrecv and self.prof is None
-        if not side_apply:
-            for w in (w_g, w_g1):
-                if w is not None:
-                    w.wait()
-        nl = len(sp.hidden)
-        hoff = self.seg[nl][1]
-        if nrecv and not lazy:
-            call("dl_shard_scatter_add", ptr(gb), ptr(g1b) if sp.fm else None, ptr(recv_ids), nrecv, E,
-                 ptr(self.tg), ptr(self.fmg) if sp.fm else None, ptr(self.touched), s)
-        # replicated rows: cate-id refs + the FM cont fields, into the flat buffer
-        rg = self.flat[self.rep_off: self.rep_off + self.rep_g.numel()].view(-1, E)
-        rg1 = self.flat[self.rep_off + self.rep_g.numel():]
+        self._c("slab_sum_head", "dl_slab_sum", ptr(self.head_slab), call_int(self.head_grid, B), self.head_w,
+                self.head_w, ptr(self.flat[hoff:]), s)
+        if not self.rep:
+            return
+        # replicated rows: the cate-id references' gradients (the replicated group's slots) and
+        # the FM cont fields', into the flat buffer (every rank adds its part; the all-reduce sums)
+        rg = self.flat[self.rep_off: self.rep_off + self.rep_t.numel()].view(-1, E)
+        rg1 = self.flat[self.rep_off + self.rep_t.numel():]
         rg.zero_()
         rg1.zero_()
-        tmp_touch = self.rep_touched.clone()
-        if nrep:
-            call("dl_shard_scatter_add", ptr(self.gU[nsend:U]), ptr(self.g1U[nsend:U]) if sp.fm else None,
-                 ptr(self.send_ids[nsend:U]), nrep, E, ptr(rg), ptr(rg1) if sp.fm else None, ptr(tmp_touch), s)
-        if rep and sp.fm:
+        o = self.nb * self.cap
+        call("dl_shard_scatter_add", ptr(self.g_all[o:]), ptr(self.g1_all[o:]) if sp.fm else None, ptr(self.rep_ids),
+             self.rep_cap, E, ptr(rg), ptr(rg1) if sp.fm else None, ptr(self.rep_scratch), s)
+        if sp.fm:
             bwd_blocks = call_int("dl_embed_bwd_grid", C_ref(L))
-            call("dl_embed_cont_bwd", C_ref(L), ptr(self.rows_u), ptr(self.in_cont), ptr(self.dz), ptr(self.w_head),
-                 ptr(self.fm_sum), ptr(self.cont_slab), self.bwd_blocks, s)
-            call("dl_embed_cont_reduce", C_ref(L), ptr(self.cont_slab), bwd_blocks, ptr(rg), ptr(rg1),
-                 ptr(tmp_touch), s)
-        # 7. one all-reduce of every replicated gradient
-        self._mark("rep_grads")
-        ex.all_reduce(self.flat)
-        self._mark("all_reduce")
-        # 8. TF1 Adam
+            cb = self._cont_blocks(B, bwd_blocks)
+            self._c("cont_bwd", "dl_embed_cont_bwd", C_ref(L), ptr(self.rows_u), ptr(self.in_cont), ptr(self.dz),
+                    ptr(self.w_head), ptr(self.fm_sum), ptr(self.cont_slab), cb, s)
+            self._c("cont_reduce", "dl_embed_cont_reduce", C_ref(L), ptr(self.cont_slab), cb, ptr(rg), ptr(rg1),
+                    ptr(self.rep_scratch), s)
+
+    def _dense_adam(self, B, s):
+        """Step 7a: TF1 Adam on the all-reduced dense and replicated gradients (identical on every
+        rank); the tower updates write their GEMM operand copies themselves."""
+        sp = self.spec
+        E = sp.E
+        nl = len(sp.hidden)
+        hoff = self.seg[nl][1]
         reg = sp.hidden_reg   # wdl: L2 on every hidden weight matrix (wdl.py:272-275), bias row excluded
         for l in range(nl):
             off, sz = self.seg[l][1], self.seg[l][2]
             l2, l2n = (sp.l2, ([self.D0] + sp.hidden)[l] * self.out_ld[l]) if reg else (0.0, 0)
-            self._c("adam_dense_l%d" % l, "dl_adam_dense_reg", ptr(self.W[l]), ptr(self.Wm[l]), ptr(self.Wv[l]),
-                    ptr(self.flat[off:]), 1, sz, sz, l2, l2n, 1 if reg == "l1" else 0, ptr(self.opt), None,
-                    ptr(self.opt[8:]) if reg else None, s)
-            self._refresh_wb(l, s)
+            if self.s3 or self.bf:
+                self._c("adam_dense_l%d" % l, "dl_adam_dense_split3" if self.s3 else "dl_adam_dense_bf16",
+                        ptr(self.W[l]), ptr(self.Wm[l]), ptr(self.Wv[l]), ptr(self.flat[off:]), 1, sz, self.in_ld[l],
+                        self.out_ld[l], l2, l2n, 1 if reg == "l1" else 0, ptr(self.opt),
+                        ptr(self.opt[8:]) if reg else None, ptr(self.Wp[l] if self.s3 else self.Wb[l]),
+                        ptr(self.WTp[l] if self.s3 else self.WbT[l]), s)
+            else:
+                self._c("adam_dense_l%d" % l, "dl_adam_dense_reg", ptr(self.W[l]), ptr(self.Wm[l]), ptr(self.Wv[l]),
+                        ptr(self.flat[off:]), 1, sz, sz, l2, l2n, 1 if reg == "l1" else 0, ptr(self.opt), None,
+                        ptr(self.opt[8:]) if reg else None, s)
         if self.wdl:
             H = sp.hidden[-1]
             self._c("adam_bias", "dl_adam_dense", ptr(self.wb), ptr(self.wbm), ptr(self.wbv), ptr(self.flat[hoff + H:]),
                     1, 1, 1, 0.0, 0, ptr(self.opt), None, None, s)
-            # owners: arrived wide-row gradients + the deep-output rows they own, then the dense
-            # L2 Adam sweep over the shard of wdl_weights (wdl.py:270-271)
-            if w_gw is not None:
-                w_gw.wait()
-            nwrecv = sum(wx[1])
-            call("dl_shard_add_fixed", ptr(wg_in), ptr(wx[2]), nwrecv, ptr(self.wg), ptr(self.w_touched), s)
-            call("dl_wide_fold_owned", ptr(self.flat[hoff:]), H, sp.Fw, W, self.rank, ptr(self.wg),
-                 ptr(self.w_touched), s)
-            self.wide_reg.zero_()
-            self._c("adam_wide", "dl_adam_rows", ptr(self.ww), ptr(self.wm), ptr(self.wv), ptr(self.wg),
-                    ptr(self.w_touched), self.ww.shape[0], 1, sp.l2, 1 | _lib.ROWS_GRAD_FIXED, ptr(self.opt),
-                    ptr(self.wide_reg), s)
-            self._wide_refresh()
         else:
             self._c("adam_head", "dl_adam_dense", ptr(self.w_head), ptr(self.hm), ptr(self.hv), ptr(self.flat[hoff:]),
                     1, self.head_w, self.head_n, sp.l2, self.head_n - 1, ptr(self.opt), ptr(self.w_head_prev), None,
                     s)
-        if rep:
-            self.rep_g.view(-1)[: rg.numel()].copy_(rg.reshape(-1))
-            self.rep_fg[: rg1.numel()].copy_(rg1)
-            self.rep_touched[: self.rep] = 1
-            call("dl_adam_rows", ptr(self.rep_t), ptr(self.rep_m), ptr(self.rep_v), ptr(self.rep_g),
-                 ptr(self.rep_touched), self.rep_t.shape[0], E, 0.0, 0, ptr(self.opt), None, s)
+        if self.rep:
+            rg = self.flat[self.rep_off: self.rep_off + self.rep_t.numel()]
+            rg1 = self.flat[self.rep_off + self.rep_t.numel():]
+            n = self.rep_t.shape[0]
+            call("dl_adam_rows", ptr(self.rep_t), ptr(self.rep_m), ptr(self.rep_v), ptr(rg), ptr(self.rep_all), n, E,
+                 0.0, 0, ptr(self.opt), None, s)
             if sp.fm:
-                call("dl_adam_rows", ptr(self.rep_f), ptr(self.rep_fm), ptr(self.rep_fv), ptr(self.rep_fg),
-                     ptr(self.rep_touched), self.rep_f.shape[0], 1, 0.0, 0, ptr(self.opt), None, s)
-        if lazy:
-            if nrecv and self.prof is not None:   # bench's per-kernel pass: timed on the compute stream
-                torch.cuda.current_stream().wait_event(link_done)
-                self._c("rec_apply", *self._owner_apply_args(recv_ids, nrecv, gb, g1b, self.opt, s))
-            elif nrecv:
-                # on the side stream (after the chain link queued there): overlaps the next step's
-                # start; that step's gather waits for it (apply_done).  The optimizer scalars
-                # are snapshotted — the next adam_begin advances them.
-                if ex.staged:   # host-staged exchange: the gradients were copied in on this stream
-                    self.side.wait_stream(torch.cuda.current_stream())
-                with torch.cuda.stream(self.side):
-                    # the side stream waits for the arrived gradients themselves: the update
-                    # starts as soon as they land, beside this step's weight gradients
-                    for w in (w_g, w_g1):
-                        if w is not None:
-                            w.wait()
-                    call(*self._owner_apply_args(recv_ids, nrecv, gb, g1b, snap, _lib.stream_handle(self.side)))
-                    self.apply_done = torch.cuda.Event()
-                    self.apply_done.record(self.side)
-                gb.record_stream(self.side)
-                if g1b is not None:
-                    g1b.record_stream(self.side)
-                out_v.record_stream(self.side)   # the update reads the gathered rows (stash form)
-                out_1.record_stream(self.side)
-        elif sp.fm:
-            self._c("adam_table", "dl_adam_rows", ptr(self.table), ptr(self.tm), ptr(self.tv), ptr(self.tg),
-                    ptr(self.touched), self.table.shape[0], E, 0.0, 0, ptr(self.opt), None, s)
-            self._c("adam_first", "dl_adam_rows", ptr(self.first), ptr(self.fmm), ptr(self.fmv), ptr(self.fmg),
-                    ptr(self.touched), self.first.shape[0], 1, 0.0, 1, ptr(self.opt), None, s)
+                call("dl_adam_rows", ptr(self.rep_f), ptr(self.rep_fm), ptr(self.rep_fv), ptr(rg1), ptr(self.rep_all),
+                     n, 1, 0.0, 0, ptr(self.opt), None, s)
+
+    def _owner_apply(self, s):
+        """Step 7b: the owners' update of every arriving row (blocks [0, W) of the gradients)."""
+        sp = self.spec
+        E, W, cap, rep = sp.E, self.world, self.cap, self.rep
+        g1 = ptr(self.g1_all) if sp.fm else None
+        if not self.lazy:
+            self._c("rec_apply", "dl_shard_scatter_add", ptr(self.g_all), g1, ptr(self.ids_all), W * cap, E,
+                    ptr(self.tg), ptr(self.fmg) if sp.fm else None, ptr(self.touched), s)
+            if sp.fm:
+                self._c("adam_table", "dl_adam_rows", ptr(self.table), ptr(self.tm), ptr(self.tv), ptr(self.tg),
+                        ptr(self.touched), self.table.shape[0], E, 0.0, 0, ptr(self.opt), None, s)
+                self._c("adam_first", "dl_adam_rows", ptr(self.first), ptr(self.fmm), ptr(self.fmv), ptr(self.fmg),
+                        ptr(self.touched), self.first.shape[0], 1, 0.0, 1, ptr(self.opt), None, s)
+            else:
+                self._c("adam_table", "dl_adam_rows", ptr(self.table), ptr(self.tm), ptr(self.tv), ptr(self.tg),
+                        ptr(self.touched), self.table.shape[0], E, 0.0, 1 | self.rows_sparse, ptr(self.opt), None, s)
+            return
+        if self.owner_update == "chain":
+            self._c("rec_apply", "dl_rec_apply_chain", ptr(self.rec), self.rec_ld, E, self.rec_flags,
+                    ptr(self.ids_all), W * cap, ptr(self.own_head), ptr(self.own_next), ptr(self.g_all), g1,
+                    ptr(self.hist), self.hist_len, ptr(self.opt), s)
+            return
+        rows, rows1 = self.rows_u[rep:], (self.rows_u1[rep:] if sp.fm else None)
+        if W == 1:   # one sender's block: rows already unique and in order — identity segments
+            uniq, off, nu, pos = self.ids_all, self.iota, self.hdr_all, self.iota
         else:
-            self._c("adam_table", "dl_adam_rows", ptr(self.table), ptr(self.tm), ptr(self.tv), ptr(self.tg),
-                    ptr(self.touched), self.table.shape[0], E, 0.0, 1 | self.rows_sparse, ptr(self.opt), None, s)
+            uniq, off, nu, pos = self.own_uniq, self.own_off, self.own_n, self.own_pos
+        self._c("rec_apply", "dl_rec_apply_segments", ptr(self.rec), self.rec_ld, E, self.rec_flags, ptr(uniq),
+                ptr(off), ptr(nu), W * cap, W * cap, ptr(pos), ptr(self.g_all), g1, ptr(rows), ptr(rows1),
+                ptr(self.own_mv), ptr(self.hist), self.hist_len, ptr(self.opt), s)
+
+    def _owner_group(self, s):
+        """The owner's grouping of this step's arrivals by row (a branch: it needs only the
+        received ids)."""
+        W, cap = self.world, self.cap
+        if not self.lazy:
+            return
+        if self.owner_update == "chain":
+            call("dl_rec_chain_link", ptr(self.ids_all), W * cap, ptr(self.own_head), ptr(self.own_next), s)
+        elif W > 1:
+            self._c("owner_sort", "dl_sort_unique", ptr(self.ids_all), W * cap, self.own_bits, ptr(self.own_ws),
+                    self.own_ws.numel(), ptr(self.own_keys), ptr(self.own_pos), ptr(self.own_uniq),
+                    ptr(self.own_off), ptr(self.own_n), None, s)
+
+    def _wide_update(self, s):
+        """wdl_weights: the arrived wide gradients + the deep-output rows this rank owns, then the
+        dense L2 Adam sweep over the shard (wdl.py:270-271), then every rank's copy of the
+        deep-output rows from their owners (an in-place all-reduce)."""
+        sp = self.spec
+        H = sp.hidden[-1]
+        hoff = self.seg[len(sp.hidden)][1]
+        o = self.wloc_off
+        call("dl_shard_add_fixed", ptr(self.wgloc[o:]), ptr(self.wids_all), self.world * self.wcap, ptr(self.wg),
+             ptr(self.w_touched), s)
+        call("dl_wide_fold_owned", ptr(self.flat[hoff:]), H, sp.Fw, self.world, self.rank, ptr(self.wg),
+             ptr(self.w_touched), s)
+        self.wide_reg.zero_()
+        self._c("adam_wide", "dl_adam_rows", ptr(self.ww), ptr(self.wm), ptr(self.wv), ptr(self.wg),
+                ptr(self.w_touched), self.ww.shape[0], 1, sp.l2, 1 | _lib.ROWS_GRAD_FIXED, ptr(self.opt),
+                ptr(self.wide_reg), s)
+        self._wide_refresh(s)
+
+    def _wide_refresh(self, s):
+        """Every rank's copy of the deep-output rows Fw..Fw+H of wdl_weights (read by the cross
+        logit) from their owners: one [H] sum all-reduce, in place."""
+        sp = self.spec
+        H = sp.hidden[-1]
+        d = self.wloc[sp.Fw: sp.Fw + H]
+        call("dl_wide_owned_values", ptr(self.ww), H, sp.Fw, self.world, self.rank, ptr(d), s)
+        self.exch.all_reduce(d, torch.cuda.current_stream())
+
+    def _step(self, B):
+        """One whole training step on the current stream (graph-captured, or eager), branches
+        forked to the engine's streams and joined."""
+        sp = self.spec
+        s = _lib.stream_handle()
+        main = torch.cuda.current_stream()
+        L = self.layout
+        L.batch = B
+        self._requests(s)
+        self._c("step_begin", "dl_shard_step_begin", ptr(self.hdr_all), ptr(self.whdr_all) if self.wdl else None,
+                self.world, self.cap, self.wcap, ptr(self.opt), sp.decay_rate, float(sp.decay_steps),
+                ptr(self.hist) if self.lazy else None, self.hist_len if self.lazy else 0, s)
+        own = self.lazy and (self.owner_update == "chain" or self.world > 1)
+        if own:   # the owner's grouping of the arrivals, beside the gather and the forward
+            self.own_stream.wait_stream(main)
+            with torch.cuda.stream(self.own_stream):
+                self._owner_group(_lib.stream_handle(self.own_stream))
+        self._gather_owned(B, s, 1)
+        self._answers(s)
+        self._forward_local(B, s, True)
+        self._input_grads(B, s)
+        # the gradients to their owners on a branch, beside the weight gradients
+        x = self.x_stream
+        x.wait_stream(main)
+        garrs = [self.g_all[: self.nb * self.cap].view(self.nb, self.cap * sp.E)]
+        if sp.fm:
+            garrs.append(self.g1_all[: self.nb * self.cap].view(self.nb, self.cap))
+        if self.wdl:
+            o = self.wloc_off
+            garrs.append(self.wgloc[o: o + self.nb * self.wcap].view(self.nb, self.wcap))
+        with torch.cuda.stream(x):
+            self._c("x_grads", "exchange", lambda: self.exch.blocks(garrs, 0, x))
+        self._weight_grads(B, s)
+        # the dense all-reduce on the second communicator's stream, beside the gradient exchange
+        a = self.ar_stream
+        a.wait_stream(main)
+        with torch.cuda.stream(a):
+            self._c("all_reduce", "exchange", lambda: self.exch.all_reduce(self.flat, a))
+        main.wait_stream(a)
+        self._dense_adam(B, s)
+        main.wait_stream(x)
+        if own:
+            main.wait_stream(self.own_stream)
+        if self.wdl:
+            self._wide_update(s)
+        self._owner_apply(s)
+        hoff = self.seg[len(sp.hidden)][1]
+        coef = sp.l2 if sp.hidden_reg == "l1" else 0.5 * sp.l2
+        self._c("loss_acc", "dl_loss_accumulate", ptr(self.flat[hoff:]), 1, self.head_w, self.head_w - 1,
+                1.0 / (B * self.world), ptr(self.opt), coef, ptr(self.loss_acc), ptr(self._ring), s)
+
+    def _capture_step(self, B):
+        st = torch.cuda.Stream()
+        st.wait_stream(torch.cuda.current_stream())
+        g = torch.cuda.CUDAGraph()
+        with capture_guard(), torch.cuda.graph(g, stream=st, capture_error_mode="thread_local"):
+            self._step(B)
+        torch.cuda.current_stream().wait_stream(st)
+        return g
+
+    # ------------------------------------------------------------ step
+    def prefetch(self, batch, graph=False, after=None):
+        """Stage the next batch, index and route it on the side stream while this step runs."""
+        super().prefetch(batch, graph=False, after=after)
+
+    def train_step(self, batch=None, graph=False, next_batch=None):
+        """One training step on this rank's batch (every rank calls it together).  Returns B.
+        Raises (on every rank at the same call, `lag` calls after the step) when a step was
+        skipped for a bad id on any rank; replays the steps an overflow skipped."""
+        B = self._submit(batch, graph, next_batch)
+        self._check_reports(self.lag)
+        return B
+
+    def _submit(self, batch, graph, next_batch):
+        B, indexed = self._begin(batch)
+        self._mark("start")
+        if not indexed:
+            self._pre(B)
+        if self.lazy:
+            if self.since_flush >= self.hist_len - 2:   # bound every row's lag below the alpha ring
+                self.flush()
+            self.since_flush += 1
+        if next_batch is not None:   # the next batch's staging, index and route, beside this step
+            self.prefetch(next_batch)
+        self._mark("prefetch")
+        if self._ring_sent is None:   # the device's step sequence (a read that waits, once)
+            self._ring_sent = int(self.opt.view(torch.int32)[_lib.OPT_SEQ].item())
+            self._ring_checked = self._ring_sent
+        # the first steps run eagerly: RCCL connects its peers then, not inside a capture
+        if graph and self.prof is None and self._steps_eager >= 1 and not self.exch.staged:
+            key = (getattr(self, "_cur", 0), B)
+            g = self.graphs.get(key)
+            if g is None:
+                g = self.graphs[key] = self._capture_step(B)
+            g.replay()
+        else:
+            self._step(B)
+            self._steps_eager += 1
+        self._mark("submitted")
+        self._ring_sent += 1
+        self._hist_b[self._ring_sent] = batch
         self._release()
-        self._mark("end")
         self.steps += 1
         self.last_batch = B
         self.last_loss_sum = None
         return B
 
+    def _clear_status(self):
+        """Status, skip, bad-step and bad-count words and the bad-rank mask (not the sequence)."""
+        self.opt[_lib.OPT_STATUS: _lib.OPT_BAD_COUNT + 1].zero_()
+        self.opt[_lib.OPT_BAD_RANKS] = 0.0
+
+    def _check_reports(self, lag):
+        """Read the status reports of every step submitted up to `lag` calls ago (waiting for the
+        oldest if needed: every rank reads the same reports at the same call).  A skipped step is
+        handled identically everywhere: bad ids raise, an overflow grows the blocks and replays."""
+        if self._ring_sent is None:   # no step submitted since the last resynchronisation
+            return
+        r = self._ring_np
+        bad = []
+        while self._ring_checked < self._ring_sent - lag:
+            k = self._ring_checked + 1
+            j = 2 * (k & 3)
+            t0 = time.perf_counter()
+            spins = 0
+            while int(r[j]) != k:
+                spins += 1
+                if spins > 1000:
+                    time.sleep(2e-5)
+                if time.perf_counter() - t0 > 60.0:
+                    raise _lib.DLError("sharded step %d reported no status within 60 s (a rank stopped?)" % k)
+            self.host_wait += time.perf_counter() - t0
+            word = int(r[j + 1]) & 0xffffffff
+            skip = word >> 16
+            self._ring_checked = k
+            batch = self._hist_b.pop(k, None)
+            if skip & _lib.STATUS_OVERFLOW:
+                return self._recover(k, batch)
+            if skip & (_lib.STATUS_LAG | _lib.STATUS_INDEX | _lib.STATUS_DESYNC):
+                self._hist_b.clear()
+                raise _lib.DLError("internal: sharded step %d faulted (status bits %#x: lag / index / desync)"
+                                   % (k, skip))
+            if skip & _lib.STATUS_BAD_ID:
+                bad.append(k)
+        if bad:
+            torch.cuda.synchronize()
+            ranks = int(self.opt.view(torch.int32)[_lib.OPT_BAD_RANKS].item())
+            step = int(self.opt[_lib.OPT_BAD_STEP].item())
+            self._clear_status()
+            for w in self._error_words():
+                w.zero_()
+            raise _lib.DLError("InvalidArgumentError: categorical id out of range [0, %d) in the batch of rank(s) %s "
+                               "— %d step(s) skipped on every rank with no update, the last at global_step %d"
+                               % (self.N, [p for p in range(self.world) if ranks >> p & 1], len(bad), step))
+
+    def _recover(self, k, batch):
+        """Step k overflowed a block on some rank, so it and every step after it were skipped on
+        every rank: wait for them, clear the fault, grow the blocks and replay them in order."""
+        torch.cuda.synchronize()
+        replay = [batch] + [self._hist_b[q] for q in sorted(self._hist_b)]
+        self._hist_b.clear()
+        self._clear_status()
+        self._grow()
+        self.steps -= len(replay)
+        self._ring_sent = None
+        self.overflows = getattr(self, "overflows", 0) + 1
+        for b in replay:
+            self._submit(b, False, None)
+            self._check_reports(0)
+
     # ------------------------------------------------------------ predict / eval
     def predict(self, batch, logits=False, device=False):
         """Forward only on this rank's batch (reference eval/predict, deepfm_pipeline.py:294-311):
-        the same index, id exchange and owner gather as a training step, rows caught up to the
-        last completed step (records are only read), no gradients, no update.  Every rank must
-        call it together (collectives).  Returns the sigmoid scores [B] (or logits) as host
-        numpy, or a device tensor copy with device=True."""
-        sp = self.spec
-        ex = self.exch
-        E = sp.E
-        pf = getattr(self, "_pf", None)
-        if pf is not None:   # a pending prefetch: let it land, drop it
-            torch.cuda.current_stream().wait_event(pf[2])
-            self._drop_prefetch(pf)
+        the same index, route, request and answer exchanges as a training step, rows caught up to
+        the last completed step (records are only read), no gradients, no update.  Every rank
+        must call it together.  Returns the sigmoid scores [B] (or logits) as host numpy, or a
+        device tensor copy with device=True."""
+        self._check_reports(0)
+        q = getattr(self, "_pfq", None) or []
+        for p in q:   # pending prefetches: let them land, drop them
+            torch.cuda.current_stream().wait_event(p[2])
+        if q:
+            q.clear()
+            self._pf = None
         B = self.stage(batch)
-        self._join_side()            # the last step's record update (side stream) has landed
         s = _lib.stream_handle()
-        L = self.layout
-        L.batch = B
         W = self.world
-        self._index(B)
-        cm = self._split_counts(ex.count_matrix(self._count_vec()))
-        cmw = [row[W + 1:] for row in cm] if self.wdl else None
-        send = cm[self.rank][:W]
-        nsend, nrep = sum(send), cm[self.rank][W]
-        recv = [cm[r][self.rank] for r in range(W)]
-        nrecv = sum(recv)
-        recv_ids = ex.all_to_all(self.send_ids[:nsend], send, recv)
-        out_v = torch.empty(max(nrecv, 1), E, device=self.dev)
-        out_1 = torch.empty(max(nrecv, 1), device=self.dev)
-        if nrecv and self.lazy:   # lag 0: caught up to the last completed step, read only
-            call("dl_rec_gather", C_ref(L), ptr(self.rec), self.rec_ld, self.rec_flags, 0, ptr(recv_ids), None,
-                 nrecv, 1, ptr(self.hist), self.hist_len, ptr(self.opt), 0, ptr(out_v),
-                 ptr(out_1) if sp.fm else None, None, s)
-        elif nrecv:
-            call("dl_shard_gather", ptr(self.table), ptr(self.first), ptr(recv_ids), nrecv, E, ptr(out_v),
-                 ptr(out_1) if self.first is not None else None, s)
-        rep = self.rep
-        ex.all_to_all(out_v[:nrecv], recv, send, out=self.rows_u[rep: rep + nsend])
-        if sp.fm:
-            ex.all_to_all(out_1[:nrecv], recv, send, out=self.rows_u1[rep: rep + nsend])
-        if rep:
-            self.rows_u[:rep].copy_(self.rep_t[:rep])
-            if sp.fm:
-                self.rows_u1[:rep].copy_(self.rep_f[:rep])
-        if nrep:
-            call("dl_shard_gather", ptr(self.rep_t), ptr(self.rep_f) if sp.fm else None,
-                 ptr(self.send_ids[nsend:nsend + nrep]), nrep, E, ptr(self.rows_u[rep + nsend:]),
-                 ptr(self.rows_u1[rep + nsend:]) if sp.fm else None, s)
+        self._pre(B)
+        call("dl_shard_stamp", ptr(self.hdr_all), W, self.rank, ptr(self.opt), s)
+        arrs = [self.ids_all.view(self.nb, self.cap), self.hdr_all.view(self.nb, 4)]
         if self.wdl:
-            self._wide_exchange(B, cmw)
-        call("dl_embed_fwd_indexed", C_ref(L), ptr(self.rows_u), ptr(self.rows_u1) if sp.fm else None, ptr(self.inv),
-             rep, ptr(self.in_cont), ptr(self.in_vec), ptr(self.x0b if self.x0_direct else self.x0), ptr(self.fm_out),
-             ptr(self.fm_sum), s)
-        if self.bf and not self.x0_direct:
-            call("dl_cast_bf16", ptr(self.x0), B, self.in_ld[0], self.in_ld[0], ptr(self.x0b), self.in_ld[0], s)
-        self._tower_fwd(B, s)
-        self._head(B, s, train=False)
+            arrs += [self.wids_all.view(self.nb, self.wcap), self.whdr_all.view(self.nb, 4)]
+        self.exch.blocks(arrs, 0)
+        # the same decision on every rank, from every rank's header
+        fl = 0
+        for h in (self.hdr_all, self.whdr_all if self.wdl else None):
+            if h is not None:
+                hv = h[: 4 * W].view(W, 4)
+                bad_rows = hv[:, 1].tolist()
+                for f in bad_rows:
+                    fl |= int(f)
+        if fl & _lib.STATUS_OVERFLOW:
+            self._grow()
+            return self.predict(batch, logits, device)
+        if fl & _lib.STATUS_BAD_ID:
+            for w in self._error_words():
+                w.zero_()
+            raise _lib.DLError("InvalidArgumentError: categorical id out of range [0, %d) in a predict batch" % self.N)
+        self._gather_owned(B, s, 0)
+        self._answers(s)
+        self._forward_local(B, s, False)
         self._release()
-        self.check_error()
         out = (self.z if logits else self.score)[:B]
         return out.clone() if device else out.cpu().numpy()
 
@@ -1052,15 +1072,21 @@ class ShardedCTREngine(CTREngine):
         """Global loss of the last step: the all-reduced loss column + L2 on the head weights
         (wdl: + L2 on every hidden weight matrix and on all of wdl_weights, whose shard sums are
         all-reduced here — every rank calls it)."""
+        self._check_reports(0)
         sp = self.spec
         hoff = self.seg[len(sp.hidden)][1]
         if self.wdl:
             H = sp.hidden[-1]
             data = float(self.flat[hoff + H + 1].item())
             wr = self.wide_reg.clone()
-            self.exch.all_reduce(wr)
+            self.exch.host_sum(wr)
             return data / (self.last_batch * self.world) + sp.l2 * 0.5 * (float(self.opt[8].item()) +
                                                                            float(wr[0].item()))
         data = float(self.flat[hoff + self.head_w - 1].item())
         w = self.w_head_prev[: self.head_n - 1].double()
         return data / (self.last_batch * self.world) + sp.l2 * 0.5 * float((w * w).sum().item())
+
+    def check_error(self):
+        """Every report read (raising as train_step would), then the engine's own check."""
+        self._check_reports(0)
+        super().check_error()

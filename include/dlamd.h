@@ -190,9 +190,10 @@ int dl_index_build_pair(const dl_emb_layout* L, const int64_t* cate, const dl_em
                         int32_t* sorted_refs, uint32_t* uniq_keys, int32_t* seg_off, int32_t* n_uniq,
                         int32_t* inv, uint32_t* uniq2, int32_t* sorted_refs2, int32_t* seg_off2,
                         int32_t* n_uniq2, int32_t* inv2, int32_t* err, void* stream);
-/* Generic form for the sharded owners: sort n non-negative int32 keys (< 2^key_bits) with
- * their positions, dedup: uniq_keys [n_uniq], seg_off [n_uniq+1] into sorted_pos, and
- * inv[i] = unique id of keys[i] (may be NULL).  Workspace: dl_index_workspace_bytes(n). */
+/* Generic form for the sharded owners: sort n int32 keys (< 2^key_bits; a key of -1 — an empty
+ * slot of a fixed-capacity exchange block — is dropped) with their positions, dedup:
+ * uniq_keys [n_uniq], seg_off [n_uniq+1] into sorted_pos, and inv[i] = unique id of keys[i]
+ * (may be NULL).  Workspace: dl_index_workspace_bytes(n). */
 int dl_sort_unique(const int32_t* keys, int64_t n_keys, int32_t key_bits, void* ws, int64_t ws_bytes,
                    int32_t* sorted_keys, int32_t* sorted_pos, int32_t* uniq_keys, int32_t* seg_off,
                    int32_t* n_uniq, int32_t* inv, void* stream);
@@ -201,13 +202,15 @@ int dl_sort_unique(const int32_t* keys, int64_t n_keys, int32_t key_bits, void* 
  * into the dense gradient tables g_out [n_rows, E] / g1_out [n_rows] + touched
  * flags (single GPU); compact=1: g_out [u][E], g1_out [u] per unique id (the
  * sharded path sends these to the owners).  rows_u: gathered rows per unique id
- * (sharded) or NULL to read `table`. */
+ * (sharded) or NULL to read `table`.  upos (compact only, may be NULL): unique row u's slot in
+ * rows_u / g_out / g1_out (the fixed-capacity exchange blocks of dl_shard_route; a slot of -1
+ * is skipped) in place of u. */
 int dl_embed_bwd_sorted(const dl_emb_layout* L, const float* table, const float* rows_u,
                         const uint32_t* uniq_keys, const int32_t* seg_off, const int32_t* n_uniq,
                         const int32_t* sorted_refs, int32_t world, int64_t max_uniq,
                         const float* dz, const float* w_head, const float* fm_sum,
                         const float* dx0, float* g_out, float* g1_out, uint8_t* touched,
-                        int32_t compact, void* stream);
+                        int32_t compact, const int32_t* upos, void* stream);
 
 /* Multi-hot nonzero-mean pooling (deepfm_multi_cate.py:71-111).
  * ids [B, ids_ld] int64 (padding id 0); slot m covers columns
@@ -390,9 +393,12 @@ int dl_slab_fold_rows(const float* slab, int32_t blocks, int32_t width, int32_t 
 #define DL_OPT_BAD_STEP 18
 #define DL_OPT_BAD_COUNT 19
 #define DL_OPT_SEQ 20       /* int32 bits: steps reported through dl_loss_accumulate's status ring */
+#define DL_OPT_BAD_RANKS 21 /* int32 bits: sharded step — bit p set when rank p's batch held a bad id */
 #define DL_STATUS_BAD_ID 1   /* a categorical / wide id outside [0, N) */
 #define DL_STATUS_LAG 2      /* a row record lagged past the alpha ring (flush schedule broken) */
 #define DL_STATUS_INDEX 4    /* a batch-index entry out of range (index consumers report, never skip silently) */
+#define DL_STATUS_OVERFLOW 8 /* sharded step: a rank had more unique rows for an owner than a block holds */
+#define DL_STATUS_DESYNC 16  /* sharded step: the ranks' headers named different global steps */
 int dl_adam_begin_step(float* opt, float decay_rate, float decay_steps, void* stream);
 /* The step's skip word := the batch's validation bits (batch_err[0], written by
  * dl_index_build / dl_validate_batch) | the sticky internal-fault bits; a bad batch
@@ -598,6 +604,33 @@ int dl_shard_gather(const float* table, const float* first, const int32_t* ids, 
                     int32_t emb_dim, float* out, float* out_first, void* stream);
 int dl_shard_scatter_add(const float* g, const float* g_first, const int32_t* ids, int64_t n,
                          int32_t emb_dim, float* G, float* G_first, uint8_t* touched, void* stream);
+/* Fixed-capacity exchange blocks of the sharded step (one hipGraph per step).
+ * Arrays of 2W - 1 blocks of `cap` slots: block p < W = what peer p sends this rank (block
+ * `rank`: this rank's own requests, in place), block W + p - (p > rank) = this rank's requests
+ * to / answers from peer p.  dl_shard_route, from the batch index (unique keys grouped by owner,
+ * owner_counts [W + 1] with the replicated group last): ids[block(p) cap + j] = the j-th unique
+ * row owned by p (local row), -1 past its count; hdr[block(p) * 4] = {count, flags, rank, 0}
+ * with flags = DL_STATUS_BAD_ID if err[0] and DL_STATUS_OVERFLOW if any owner's count exceeds
+ * cap (or the replicated group rep_cap); rep_ids[j] = the replicated rows (-1 past the count);
+ * upos[u] (may be NULL; u < n_max) = unique row u's slot block(p) cap + j, or
+ * (2W - 1) cap + j for the replicated group, -1 past a capacity; inv (may be NULL, n_refs
+ * entries) remapped in place from unique ids to slots.  The forward then reads rows_u[slot],
+ * the backward writes its gradients at slots (dl_embed_bwd_sorted upos), and the exchanges
+ * (dl_shard_exchange) move whole blocks.
+ * dl_shard_stamp: before the request exchange, every outgoing header gets this rank's sticky
+ * fault bits and its global step.
+ * dl_shard_step_begin (after it): the step's guard from every rank's header — a bad id on any
+ * rank skips the step everywhere (status DL_STATUS_BAD_ID, opt[DL_OPT_BAD_RANKS] |= the ranks),
+ * an overflow / sticky fault on any rank or different steps (DL_STATUS_DESYNC) poison this and
+ * every later step everywhere until the host clears the status — then dl_adam_begin_step and
+ * (hist non-NULL) dl_adam_hist_record, as dl_step_begin.  hdr2 (may be NULL; blocks of cap2
+ * slots): a second id set's headers (wdl's wide ids), counted and flagged alike. */
+int dl_shard_route(const uint32_t* uniq_keys, const int32_t* n_uniq, const int32_t* owner_counts, int32_t world,
+                   int32_t rank, int64_t cap, int32_t rep_cap, const int32_t* err, int32_t* ids, int32_t* hdr,
+                   int32_t* rep_ids, int32_t* upos, int32_t* inv, int64_t n_refs, int64_t n_max, void* stream);
+int dl_shard_stamp(int32_t* hdr, int32_t world, int32_t rank, const float* opt, void* stream);
+int dl_shard_step_begin(const int32_t* hdr, const int32_t* hdr2, int32_t world, int64_t cap, int64_t cap2, float* opt,
+                        float decay_rate, float decay_steps, float* hist, int32_t hist_len, void* stream);
 /* out[i] = sum_s slab[s*stride + i] (dense gradients before the all-reduce). */
 int dl_slab_sum(const float* slab, int32_t nslab, int64_t stride, int64_t n, float* out, void* stream);
 /* out[i] = local row of uniq key i (i < min(n_uniq, cap)): the id send list. */
@@ -681,6 +714,14 @@ int dl_all_to_allv(void* comm, const void* send, const int64_t* send_counts, voi
                    const int64_t* recv_counts, int64_t row_bytes, void* stream);
 int dl_all_reduce_f32(void* comm, const float* send, float* recv, int64_t n, void* stream);
 int dl_all_gather(void* comm, const void* send, void* recv, int64_t bytes, void* stream);
+/* The sharded step's exchanges (dl_shard_route's block layout; replaces the id / row / gradient
+ * all-to-alls of SURVEY §8(e) with fixed sizes, so the whole step is one hipGraph): for each of
+ * n_arrays device arrays of 2W - 1 blocks of block_bytes[a] bytes (host arrays), every block
+ * this rank sends to / receives from every other peer, in one RCCL group.  dir 0 (to the
+ * owners): send block W + p - (p > rank), receive peer p's into block p; dir 1 (back to the
+ * senders): send block p, receive into block W + p - (p > rank).  world 1: no-op. */
+int dl_shard_exchange(void* comm, int32_t n_arrays, void* const* bases, const int64_t* block_bytes, int32_t dir,
+                      void* stream);
 
 /* ------------------------------------------------------------------------
  * Utilities. */

@@ -35,7 +35,9 @@ U32 = 2.0 ** -24
 F64 = np.float64
 K_GEMM = 512        # forward / input-gradient products: 6 bf16 planes x <= 512 / 32 MFMA chunks + bias
 K_WGRAD = 2048      # weight gradients: 6 planes x (65,536 / 32 slabs) / 32 chunks + 32 slab sums, rounded up
-K_TABLE = 8192      # table rows: up to 65,536 references of the FM cont rows (block partials + reduce)
+K_TABLE = 512       # table rows: a row's references summed in fixed-order segments / chunks (segment.h) and
+                    # the FM cont rows' 65,536 references as block partials + a reduce (pairwise-like
+                    # depth); measured worst 92 u*S over 20 full-size C2/C3 steps (round 4: was 8,192)
 
 
 def read_gpu(eng, B):

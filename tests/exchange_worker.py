@@ -1,6 +1,7 @@
-"""Worker for test_exchange_p2p_matches_all_to_all (CPU, gloo): the grouped point-to-point
-all-to-all of shard.Exchange (own segment copied locally, one send / receive per peer,
-zero-size transfers skipped) against the all-to-all it replaces, on uneven splits."""
+"""Worker for test_block_exchange (CPU, gloo): shard.Exchange.blocks moves the fixed-capacity
+blocks of the sharded step (shard.hip's layout: 2W - 1 blocks, block p < W = what peer p sent
+this rank, block W + p - (p > rank) = this rank's side of its traffic with p) — checked against
+what every peer put there, in both directions, for several dtypes and block shapes."""
 import os
 import sys
 
@@ -11,24 +12,40 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from deep_learning_amd.shard import Exchange  # noqa: E402
 
 
+def val(src, dst, j, dt):
+    """What rank src puts in slot j of its block for rank dst."""
+    return torch.tensor(1000 * src + 100 * dst + j).to(dt)
+
+
 def main():
     dist.init_process_group("gloo")
     ex = Exchange()
     W, me = ex.world, ex.rank
-    g = torch.Generator().manual_seed(7)
-    # rows rank r sends to rank p: splits[r][p] (zeros included), 3 floats per row
-    splits = torch.randint(0, 5, (W, W), generator=g)
-    splits[0, W - 1] = 0
-    splits[W - 1, 0] = 0
-    send = list(splits[me].tolist())
-    recv = [int(splits[r][me]) for r in range(W)]
-    src = torch.arange(sum(send) * 3, dtype=torch.float32).view(-1, 3) + 1000 * me
-    res = torch.full((sum(recv), 3), float("nan"))
-    for w in ex._exchange_p2p(res, src, send, recv):
-        w.wait()
-    ref = torch.empty_like(res)
-    dist.all_to_all_single(ref, src, output_split_sizes=recv, input_split_sizes=send)
-    assert torch.equal(res, ref), (me, res, ref)
+    assert ex.staged
+    for dt, blk in ((torch.int32, 5), (torch.float32, 7), (torch.int64, 3)):
+        # direction 0: this rank's request block for peer p travels to p's block `me`
+        a = torch.full((2 * W - 1, blk), -7, dtype=dt)
+        for p in range(W):
+            for j in range(blk):
+                a[ex.block(p), j] = val(me, p, j, dt)
+        own = a[me].clone()
+        ex.blocks([a], 0)
+        for p in range(W):
+            for j in range(blk):
+                want = val(p, me, j, dt)       # block p: what p sent to this rank (own block unchanged)
+                assert a[p, j] == want, (me, p, j, a[p, j], want)
+        assert torch.equal(a[me], own)
+        # direction 1: the answers in block p go back to p's block for this rank
+        b = torch.full((2 * W - 1, blk), -7, dtype=dt)
+        for p in range(W):
+            for j in range(blk):
+                b[p, j] = val(me, p, j, dt)
+        ex.blocks([b], 1)
+        for p in range(W):
+            if p == me:
+                continue
+            for j in range(blk):
+                assert b[ex.block(p), j] == val(p, me, j, dt), (me, p, j)
     dist.barrier()
     dist.destroy_process_group()
 

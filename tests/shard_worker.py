@@ -41,7 +41,8 @@ def local(b, rank, world):
 
 
 def run_sim(rank, world, steps, Bl, out_dir):
-    """numpy sharded step using the real Exchange over gloo."""
+    """numpy sharded step over the real fixed-capacity block exchange (gloo): each owner's
+    unique rows routed into a block of `cap` slots with a header, blocks exchanged both ways."""
     from deep_learning_amd.shard import Exchange
     ex = Exchange()
     cfg = R.make_cfg("deepfm_pipeline", **KW)
@@ -49,7 +50,8 @@ def run_sim(rank, world, steps, Bl, out_dir):
     N = R.n_rows(cfg)
     C, E = cfg.C, cfg.E
     own = lambda r: r % world
-    mine = np.arange(N)[np.arange(N) % world == rank]
+    nb = 2 * world - 1
+    cap = -(-(Bl * 2 * KW["S"]) // world) * 2                # roomy: the sim never overflows
     # shard state: this rank's rows of the tables (+ Adam moments) keyed by global row
     opt = R.AdamTF1(cfg, P)
     for step, bg in enumerate(global_batches(Bl * world, steps)):
@@ -59,16 +61,25 @@ def run_sim(rank, world, steps, Bl, out_dir):
         rows = rows[rows >= C]                                  # replicated rows stay local
         owners = own(rows)
         send = [rows[owners == p] for p in range(world)]
-        counts = ex.counts([len(x) for x in send])
-        # the engine's single-collective form: all ranks' per-owner counts (+ a replicated count)
-        cm = ex.count_matrix(torch.tensor([len(x) for x in send] + [7], dtype=torch.int32))
-        assert [cm[r][rank] for r in range(world)] == counts and cm[rank][:world] == [len(x) for x in send]
-        assert all(row[world] == 7 for row in cm)
-        req = ex.all_to_all(torch.from_numpy(np.concatenate(send)), [len(x) for x in send], counts).numpy()
+        ids = torch.full((nb, cap), -1, dtype=torch.int32)
+        hdr = torch.zeros((nb, 4), dtype=torch.int32)
+        for p in range(world):
+            ids[ex.block(p), : len(send[p])] = torch.from_numpy((send[p] // world).astype(np.int32))
+            hdr[ex.block(p), 0] = len(send[p])
+        ex.blocks([ids, hdr], 0)
+        counts = [int(hdr[p, 0]) for p in range(world)]
+        req = np.concatenate([ids[p, : counts[p]].numpy().astype(np.int64) * world + rank for p in range(world)])
         # owner side: answer from its own rows only
         assert np.all(own(req) == rank)
-        ans = torch.from_numpy(np.concatenate([P["feats_emb"][req], P["fm_first_order_emb"][req]], 1))
-        back = ex.all_to_all(ans, counts, [len(x) for x in send]).numpy()
+        ans = torch.zeros((nb, cap, E + 1), dtype=torch.float32)
+        o = 0
+        for p in range(world):
+            r = req[o: o + counts[p]]
+            ans[p, : len(r)] = torch.from_numpy(np.concatenate([P["feats_emb"][r], P["fm_first_order_emb"][r]], 1))
+            o += counts[p]
+        ans_v = ans.view(nb, -1)
+        ex.blocks([ans_v], 1)
+        back = np.concatenate([ans[ex.block(p), : len(send[p])].numpy() for p in range(world)])
         # the local view of the table: own/exchanged rows + replicated rows; others poisoned
         view = {k: np.full_like(v, np.nan) for k, v in P.items() if k in ("feats_emb", "fm_first_order_emb")}
         got = np.concatenate(send)
@@ -88,8 +99,12 @@ def run_sim(rank, world, steps, Bl, out_dir):
         Gt = G["feats_emb"] / world
         G1 = G["fm_first_order_emb"] / world
         # embedding grads: requested rows go back to their owners
-        gsend = torch.from_numpy(np.concatenate([Gt[got], G1[got]], 1).astype(np.float32))
-        grecv = ex.all_to_all(gsend, [len(x) for x in send], counts).numpy()
+        gb = torch.zeros((nb, cap, E + 1), dtype=torch.float32)
+        for p in range(world):
+            gb[ex.block(p), : len(send[p])] = torch.from_numpy(
+                np.concatenate([Gt[send[p]], G1[send[p]]], 1).astype(np.float32))
+        ex.blocks([gb.view(nb, -1)], 0)
+        grecv = np.concatenate([gb[p, : counts[p]].numpy() for p in range(world)])
         full_t = np.zeros_like(P["feats_emb"])
         full_1 = np.zeros_like(P["fm_first_order_emb"])
         np.add.at(full_t, req, grecv[:, :E])
@@ -131,7 +146,9 @@ def run_sim(rank, world, steps, Bl, out_dir):
     np.savez(os.path.join(out_dir, "rank%d.npz" % rank), **P)
 
 
-def run_gpu(rank, world, steps, Bl, out_dir, adam="dense", prefetch=False, owner_update=None):
+def run_gpu(rank, world, steps, Bl, out_dir, adam="dense", prefetch=False, owner_update=None, slack=None):
+    """slack: the blocks' slack over an even split (-0.6: blocks too small for these batches, so
+    the first step overflows, every rank grows its blocks and replays the skipped steps)."""
     from deep_learning_amd.engine import ModelSpec
     from deep_learning_amd.shard import Exchange, ShardedCTREngine
     torch.cuda.set_device(0)
@@ -139,7 +156,8 @@ def run_gpu(rank, world, steps, Bl, out_dir, adam="dense", prefetch=False, owner
     cfg = R.make_cfg("deepfm_pipeline", **KW)
     P = R.init_params(cfg, np.random.default_rng(42))
     eng = ShardedCTREngine(ModelSpec("deepfm_pipeline", **KW), Bl, ex, adam=adam, hist_len=4,
-                           owner_update=owner_update)
+                           owner_update=owner_update, slack=slack)
+    cap0 = eng.cap
     eng.load_params(P)
     batches = [local(bg, rank, world) for bg in global_batches(Bl * world, steps)]
     for step, b in enumerate(batches):
@@ -159,7 +177,8 @@ def run_gpu(rank, world, steps, Bl, out_dir, adam="dense", prefetch=False, owner
     rows, t, f = eng.shard_state()
     dense = {"W%d" % l: eng.W[l].cpu().numpy() for l in range(len(KW["hidden"]))}
     np.savez(os.path.join(out_dir, "rank%d.npz" % rank), rows=rows, table=t, first=f,
-             rep=eng.rep_t[:KW["C"]].cpu().numpy(), head=eng.w_head.cpu().numpy(), **dense)
+             rep=eng.rep_t[:KW["C"]].cpu().numpy(), head=eng.w_head.cpu().numpy(),
+             overflows=getattr(eng, "overflows", 0), cap=np.array([cap0, eng.cap]), **dense)
 
 
 def run_gpu_badid(rank, world, steps, Bl, out_dir):
@@ -180,18 +199,20 @@ def run_gpu_badid(rank, world, steps, Bl, out_dir):
     raised, trained = [], 0
     for step, b in enumerate(batches):
         nxt = batches[step + 1] if step + 1 < len(batches) else None
-        step_before = float(eng.opt[7].item())
         try:
             eng.train_step(b, graph=step >= 2, next_batch=nxt)
         except _lib.DLError as e:
-            assert "out of range" in str(e), str(e)
-            assert float(eng.opt[7].item()) == step_before   # the optimizer step did not begin
+            # reported `lag` calls after the skipped step, on every rank at the same call; this
+            # call's own batch was trained
+            assert "out of range" in str(e) and "rank(s) [1]" in str(e), str(e)
             raised.append(step)
-            continue
         torch.cuda.synchronize()
+        if step == 1:            # the skipped step: nothing applied, its logits are not a result
+            continue
         np.savez(os.path.join(out_dir, "rank%d_step%d.npz" % (rank, trained)), z=eng.z[:Bl].cpu().numpy())
         trained += 1
     eng.check_error()
+    assert float(eng.opt[7].item()) == steps - 1   # the skipped step never advanced global_step
     rows, t, f = eng.shard_state()
     np.savez(os.path.join(out_dir, "rank%d.npz" % rank), rows=rows, table=t, first=f, raised=np.array(raised),
              rep=eng.rep_t[:KW["C"]].cpu().numpy(), head=eng.w_head.cpu().numpy())
@@ -250,6 +271,7 @@ if __name__ == "__main__":
                     tower="bf16" if "bf16" in mode else "f32", prefetch=mode.endswith("_pf"))
     else:
         run_gpu(rank, world, steps, Bl, out_dir, adam="lazy" if mode.startswith("gpu_lazy") else "dense",
-                prefetch=mode.endswith("_pf"), owner_update="chain" if "_chain" in mode else None)
+                prefetch=mode.endswith("_pf"), owner_update="chain" if "_chain" in mode else None,
+                slack=-0.6 if "_ovf" in mode else None)
     dist.barrier()
     dist.destroy_process_group()

@@ -1,8 +1,8 @@
 """The stage-wise fp64 audit of tests/_fp64_audit.py (used by the full-size GPU tests) on CPU:
 an f32 evaluation of the reference graph — the numpy oracle's own step, standing in for the
 GPU's intermediates — passes every stage and every element audit, so the audit never blames a
-correct f32 step; a gradient off by more than its error bound, or a stage tensor with a wrong
-element, fails it."""
+correct f32 step; a gradient off by more than its error bound (1 % on a dense weight, 1e-4 relative
+on the table rows), a dropped reference, or a stage tensor with a wrong element, fails it."""
 import numpy as np
 import pytest
 
@@ -98,3 +98,29 @@ def test_audit_rejects_wrong_gradients_and_stages():
     mid3 = dict(mid, x0=mid["x0"].copy())
     mid3["x0"][2, cfg.C + 4] = np.nextafter(mid3["x0"][2, cfg.C + 4], np.float32(1))
     assert any("x0 cate rows" in f for f in A.StepAudit(cfg, pre, b, mid3).fails)
+
+
+def test_audit_rejects_small_systematic_table_gradient_error():
+    """With the table bound at K = 512 (u = 2^-24), a systematic 1e-4-relative error in the
+    table rows' gradients fails the element audit for most of the batch's rows (those whose
+    gradient is not a near-cancelling sum, |g| > 0.31 S); the round-4 bound (K = 8,192) let it
+    pass everywhere."""
+    cfg, b, pre, m0, v0, G, P, opt, alpha, mid = _step("deepfm_pipeline")
+    audit = A.StepAudit(cfg, pre, b, mid)
+    E = cfg.E
+    ids = b["cate_feats"].reshape(-1)
+    rows = np.unique(np.concatenate([ids, ids + cfg.C]))
+    rows = rows[(rows >= cfg.C) & (rows < P["feats_emb"].shape[0])]
+    r_, c_ = np.repeat(rows, E), np.tile(np.arange(E), len(rows))
+    G64, S = audit.table_elements(False, r_, c_)
+    g = G["feats_emb"][r_, c_].astype(np.float64)
+    wrong = g * (1 + 1e-4)
+    caught = np.abs(wrong - G64) > A.K_TABLE * A.U32 * S
+    well = np.abs(G64) > 0.35 * S                 # not a near-cancelling sum
+    assert caught[well].mean() > 0.99 and well.mean() > 0.4, (caught[well].mean(), well.mean())
+    assert not (np.abs(wrong - G64) > 8192 * A.U32 * S).any()      # what the old bound allowed
+    # and the first-order column likewise
+    G1, S1 = audit.table_elements(True, rows, np.zeros(len(rows), np.int64))
+    w1 = G["fm_first_order_emb"][rows, 0].astype(np.float64) * (1 + 1e-4)
+    well1 = np.abs(G1) > 0.35 * S1
+    assert (np.abs(w1 - G1) > A.K_TABLE * A.U32 * S1)[well1].mean() > 0.99 and well1.mean() > 0.4

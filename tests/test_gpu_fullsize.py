@@ -110,7 +110,7 @@ def _terms(key, idx, trace, fw):
     return np.full(len(idx), dz.sum())
 
 
-def _run(name, model, kw, batches, tower="f32", z_tol=TOL, loss_tol=TOL, auc_tol=None, seed=42):
+def _run(name, model, kw, batches, tower="f32", z_tol=TOL, loss_tol=TOL, auc_tol=None, seed=42, heldout=()):
     cfg = R.make_cfg(model, **kw)
     P = R.init_params(cfg, np.random.default_rng(seed))
     eng = CTREngine(ModelSpec(model, tower=tower, **kw), max_batch=B, init="none", adam="lazy")
@@ -228,6 +228,24 @@ def _run(name, model, kw, batches, tower="f32", z_tol=TOL, loss_tol=TOL, auc_tol
                 for arr, src in ((P[key], gp[key]), (opt.m[key], st[mk]), (opt.v[key], st[vk])):
                     arr.reshape(-1)[idx] = np.asarray(src).reshape(-1)[idx]
         del st
+    if heldout:
+        # the reference's evaluate (wdl.py:343-358: sklearn roc_auc_score over the held-out
+        # batches' predictions) on the trained state, against the oracle's trained parameters
+        ys, sg, so, zerr = [], [], [], 0.0
+        for hb in heldout:
+            zg = eng.predict(hb, logits=True).astype(np.float64)
+            fo = R.forward(cfg, P, hb)
+            zerr = max(zerr, float(np.abs(zg - fo["z"]).max()))
+            ys.append(hb["label"].reshape(-1))
+            sg.append(1.0 / (1.0 + np.exp(-zg)))
+            so.append(fo["p"])
+        y = np.concatenate(ys)
+        a_gpu, a_ref = R.auc(y, np.concatenate(sg)), R.auc(y, np.concatenate(so))
+        _stat("%s heldout" % name, n=len(y), auc_gpu=a_gpu, auc_oracle=a_ref, auc_delta=abs(a_gpu - a_ref),
+              z_max_err=zerr)
+        check(zerr <= z_tol, "held-out logits: max error %g > %g" % (zerr, z_tol))
+        check(abs(a_gpu - a_ref) < auc_tol, "held-out AUC %r vs oracle %r (|d| %g >= %g)" % (
+            a_gpu, a_ref, abs(a_gpu - a_ref), auc_tol))
     assert not fails, "; ".join(fails)
     return eng
 
@@ -368,12 +386,14 @@ def test_c3_deepfm_multi_cate_full_size_trajectory(hip_lib):
 
 
 def test_c5_wdl_bf16_full_size_trajectory(hip_lib):
-    """C5 with the bf16 tower against the fp32 oracle, at the bf16 tolerance stated in
-    test_gpu_parity.py::test_wdl_bf16_tower_tracks_oracle (logits 3e-2, loss 5e-3, AUC 2e-3)
-    and the BF16_* parameter bounds above."""
+    """C5 with the bf16 tower against the fp32 oracle (never re-synced): every logit within 1e-3
+    (measured <= 2.9e-4 over these steps, profiles/r04zp), the loss within 1e-4, the per-step
+    AUC and — north star — the AUC of 4 held-out full-size batches predicted with the trained
+    state within 1e-4 of the oracle's (wdl.py:343-358), the BF16_* parameter bounds above."""
     kw = dict(C=13, S=26, E=16, cate_index_size=N_CATE, hidden=HIDDEN, Fw=26)
     bs = [make_batch(B, cate_index_size=N_CATE, seed=300 + i, wide_fields=26) for i in range(TRAJ_STEPS)]
-    _run("c5", "wdl", kw, bs, tower="bf16", z_tol=3e-2, loss_tol=5e-3, auc_tol=2e-3)
+    hb = [make_batch(B, cate_index_size=N_CATE, seed=900 + i, wide_fields=26) for i in range(4)]
+    _run("c5", "wdl", kw, bs, tower="bf16", z_tol=1e-3, loss_tol=1e-4, auc_tol=1e-4, heldout=hb)
 
 
 def _free_port():

@@ -20,6 +20,9 @@ CASES = {
     "deepfm_pipeline": dict(C=13, V=0, S=26, E=16, cate_index_size=20000, hidden=[64, 48, 32]),
     "deepfm_pipeline_e8_vec": dict(C=13, V=5, S=26, E=8, cate_index_size=3000, hidden=[40, 24]),
     "dnn_pipeline": dict(C=13, V=3, S=26, E=8, cate_index_size=10000, hidden=[64, 32, 16]),
+    # BASELINE config C1 at the reference's own defaults: hidden [512, 256, 128] (local_run.py:29),
+    # 13 dense + 26 cate over a 10k vocab, embedding 8
+    "dnn_pipeline_c1": dict(C=13, V=0, S=26, E=8, cate_index_size=10000, hidden=[512, 256, 128]),
     "deepfm_multi_cate": dict(V=4, S=8, E=16, cate_index_size=6000, hidden=[48, 32],
                               multi_ranges=[[0, 30, "a"], [30, 50, "b"]]),
     "wdl": dict(C=13, S=26, E=16, cate_index_size=8000, hidden=[64, 32], Fw=26),
@@ -36,8 +39,19 @@ CASES = {
 }
 
 
+def _stat(name, **kw):
+    """DLAMD_TEST_STATS=<dir>: measured maxima appended as json lines (as test_gpu_fullsize.py)."""
+    import json
+    import os
+    d = os.environ.get("DLAMD_TEST_STATS")
+    if d:
+        os.makedirs(d, exist_ok=True)
+        with open(os.path.join(d, "parity_stats.jsonl"), "a") as f:
+            f.write(json.dumps(dict(test=name, **{k: float(v) for k, v in kw.items()})) + "\n")
+
+
 def _model(name):
-    return name.split("_e8")[0]
+    return name.split("_e8")[0].split("_c1")[0]
 
 
 def _batches(name, kw, B, n, seed=11):
@@ -242,23 +256,26 @@ def test_lazy_multi_hot_tracks_oracle(hip_lib):
 def test_wdl_bf16_tower_tracks_oracle(hip_lib, adam):
     """Config C5: the deep tower on bf16 MFMA (fp32 master weights, fp32 wide cross logit).
     Stated bf16 tolerance: logits within 3e-2 absolute of the fp32 oracle over
-    4 steps, loss within 5e-3, and the AUC of the scores within 2e-3."""
+    4 steps (the bf16 operand rounding of a small, fast-moving tower), loss within 5e-3, and the
+    AUC of the scores within 1e-4 (north star).  The measured maxima are recorded
+    (DLAMD_TEST_STATS)."""
     kw = CASES["wdl"]
     cfg = R.make_cfg("wdl", **kw)
     P = R.init_params(cfg, np.random.default_rng(42))
     eng = CTREngine(ModelSpec("wdl", tower="bf16", **kw), max_batch=1536, init="none", adam=adam)
     eng.load_params(P)
     opt = R.AdamTF1(cfg, P)
-    worst = 0.0
+    worst, worst_loss, worst_auc = 0.0, 0.0, 0.0
     for step, b in enumerate(_batches("wdl", kw, 1536, 4)):
         fw = R.train_step(cfg, P, opt, b)
         eng.train_step(b, graph=(step >= 2))
         torch.cuda.synchronize()
         z = eng.z[:1536].cpu().numpy()
         worst = max(worst, float(np.abs(z - fw["z"]).max()))
-        assert abs(eng.loss() - fw["loss"]) < 5e-3
-        assert abs(R.auc(b["label"], eng.score[:1536].cpu().numpy()) - R.auc(b["label"], fw["p"])) < 2e-3
-    assert worst < 3e-2, worst
+        worst_loss = max(worst_loss, abs(eng.loss() - fw["loss"]))
+        worst_auc = max(worst_auc, abs(R.auc(b["label"], eng.score[:1536].cpu().numpy()) - R.auc(b["label"], fw["p"])))
+    _stat("wdl bf16 B=1536 %s" % adam, z_max_err=worst, loss_err=worst_loss, auc_delta=worst_auc)
+    assert worst < 3e-2 and worst_loss < 5e-3 and worst_auc < 1e-4, (worst, worst_loss, worst_auc)
 
 
 @pytest.mark.parametrize("name,adam,depth,mid", [("deepfm_pipeline", "lazy", 1, 0), ("deepfm_pipeline", "dense", 1, 0),
