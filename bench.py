@@ -337,22 +337,22 @@ def dropin_fit(args, n_batches=12, warm=3):
     return out
 
 
-def run_workload(wl, args, world, rank, sharded, steps, warmup, age, ksteps, barrier):
+def run_workload(wl, args, world, rank, sharded, steps, warmup, age, ksteps, barrier, dist_ids=None):
     """The workload on the default stream, or (DLAMD_MAIN_PRIORITY set, an A/B switch) on a
-    compute stream of that priority."""
+    compute stream of that priority.  dist_ids: the id distribution (default --dist)."""
     import torch
     pr = os.environ.get("DLAMD_MAIN_PRIORITY")
     if pr is None:
-        return _run_workload(wl, args, world, rank, sharded, steps, warmup, age, ksteps, barrier)
+        return _run_workload(wl, args, world, rank, sharded, steps, warmup, age, ksteps, barrier, dist_ids)
     st = torch.cuda.Stream(priority=int(pr))
     st.wait_stream(torch.cuda.current_stream())
     with torch.cuda.stream(st):
-        r = _run_workload(wl, args, world, rank, sharded, steps, warmup, age, ksteps, barrier)
+        r = _run_workload(wl, args, world, rank, sharded, steps, warmup, age, ksteps, barrier, dist_ids)
     torch.cuda.current_stream().wait_stream(st)
     return r
 
 
-def _run_workload(wl, args, world, rank, sharded, steps, warmup, age, ksteps, barrier):
+def _run_workload(wl, args, world, rank, sharded, steps, warmup, age, ksteps, barrier, dist_ids=None):
     """Build the engine of workload `wl`, age its table, time `steps` steps (hipGraph replay,
     next batch prefetched), then `ksteps` eager steps bracketed per kernel by HIP events.
     Uniform ids: a fresh device-drawn batch every step (no batch repeats, so the model never
@@ -362,6 +362,7 @@ def _run_workload(wl, args, world, rank, sharded, steps, warmup, age, ksteps, ba
     from deep_learning_amd.engine import CTREngine
     from deep_learning_amd.synthetic import make_batch, make_batch_device
     B = args.batch
+    id_dist = dist_ids or args.dist
     spec = make_spec(wl, vocab_for(wl, args, sharded))
     log("%s rank %d/%d: building engine, table rows %d" % (wl, rank, world, spec.n_rows))
     use_graph = not args.no_graph
@@ -375,13 +376,13 @@ def _run_workload(wl, args, world, rank, sharded, steps, warmup, age, ksteps, ba
     kw = dict(cont=0, cate_fields=C2["S"], cate_index_size=spec.cate_index_size, multi_slots=6, multi_width=60,
               cate_only=True) if wl == "c3" else dict(cate_index_size=spec.cate_index_size, wide_fields=spec.Fw)
     total = age + warmup + steps + ksteps + 1
-    if args.dist == "uniform":
+    if id_dist == "uniform":
         nb = total
         batches = [make_batch_device(B, seed=100_000 * rank + i, **kw) for i in range(nb)]
     else:
         nb = 16 if wl == "c3" else 32
         batches = [{k: torch.from_numpy(v).cuda() for k, v in
-                    make_batch(B, seed=1000 * rank + i, dist=args.dist, **kw).items()} for i in range(nb)]
+                    make_batch(B, seed=1000 * rank + i, dist=id_dist, **kw).items()} for i in range(nb)]
     torch.cuda.synchronize()
 
     depth = getattr(eng, "pf_depth", 1)
@@ -502,11 +503,11 @@ def _run_workload(wl, args, world, rank, sharded, steps, warmup, age, ksteps, ba
         roof = {"kernel": dom, "bound": "mfma", "achieved": round(ach, 2), "peak": round(gemm_peak, 1),
                 "unit": "TFLOP/s", "frac": round(ach / gemm_peak, 3), "traffic": None,
                 "algorithmic_flops": amount}
-    pmc = pmc_traffic(dom, world, lazy=uniq is not None, workload=wl, id_dist=args.dist)
+    pmc = pmc_traffic(dom, world, lazy=uniq is not None, workload=wl, id_dist=id_dist)
     if pmc is not None:
         roof["traffic"] = pmc["hbm_bytes"]
         roof["traffic_source"] = pmc["source"]
-        cal = bwd_calibrated(dom, world, lazy=uniq is not None, workload=wl, id_dist=args.dist)
+        cal = bwd_calibrated(dom, world, lazy=uniq is not None, workload=wl, id_dist=id_dist)
         if cal is not None:
             roof.update(cal)
     # the embedding lookup by SURVEY §8(d)'s own byte count (C2: 26 FM + 26 deep rows x 64 B +
@@ -534,7 +535,7 @@ def _run_workload(wl, args, world, rank, sharded, steps, warmup, age, ksteps, ba
                  "us_per_step_amortised": round(fus / (eng.hist_len - 2), 2)}
         if per_sample and not spec.M:
             gather_lookup = lookup_alone(eng, batches[base % nb], B, per_sample)
-            if args.dist == "uniform":
+            if id_dist == "uniform":
                 # the same lookup over a Zipf batch (SURVEY §8(d)'s realistic ids: hot rows re-read)
                 zb = {k: torch.from_numpy(v).cuda() for k, v in
                       make_batch(B, seed=4242, dist="zipf", **kw).items()}
@@ -685,25 +686,29 @@ def main():
     others = ()
     if not args.no_extra:
         if world == 1 and not sharded:
-            others = tuple(w2 for w2 in ("c2", "c3", "c5") if w2 != wl)
+            others = tuple((w2, None) for w2 in ("c2", "c3", "c5") if w2 != wl)
+            if args.dist == "uniform":   # both id distributions for the training step
+                others += (("c2", "zipf"), ("c5", "zipf"))
         elif world > 1 and wl == "c2":
-            others = ("c5",)
-    for w2 in others:
+            others = (("c5", None),)
+    for w2, d2 in others:
+        key = w2 + ("_" + d2 if d2 else "")
         try:
             e = run_workload(w2, args, world, rank, sharded, args.extra_steps, min(args.warmup, 3),
-                             args.age_steps, 5, barrier)
+                             args.age_steps, 5, barrier, dist_ids=d2)
         except Exception as ex:   # reported, never fatal for the headline number
             if world > 1:         # a rank that failed alone would leave the others in a collective
                 raise
-            extra[w2] = {"error": repr(ex)}
+            extra[key] = {"error": repr(ex)}
             continue
-        extra[w2] = {"workload": workload_name(w2, vocab_for(w2, args, sharded), e["spec"].n_rows, sharded),
-                     "global_batch": B * world,
-                     "ms_per_step": round(e["ms"], 4), "samples_per_s": round(e["value"], 1),
-                     "steps": args.extra_steps, "roofline": e["roofline"], "gather_north_star": e["gather"],
-                     "kernel_sum_us_per_step": round(e["kernel_sum"], 1), "loss": round(e["loss"], 6),
-                     "host_submit_ms_per_step": round(e["host_ms"], 4),
-                     "kernels": e["kernels"]}
+        extra[key] = {"id_dist": d2 or args.dist,
+                      "workload": workload_name(w2, vocab_for(w2, args, sharded), e["spec"].n_rows, sharded),
+                      "global_batch": B * world,
+                      "ms_per_step": round(e["ms"], 4), "samples_per_s": round(e["value"], 1),
+                      "steps": args.extra_steps, "roofline": e["roofline"], "gather_north_star": e["gather"],
+                      "kernel_sum_us_per_step": round(e["kernel_sum"], 1), "loss": round(e["loss"], 6),
+                      "host_submit_ms_per_step": round(e["host_ms"], 4),
+                      "kernels": e["kernels"]}
     if "c5" in extra and "error" not in extra["c5"] and world == 1:
         try:
             extra["c5"]["dropin_fit"] = dropin_fit(args)

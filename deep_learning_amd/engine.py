@@ -830,18 +830,18 @@ class CTREngine:
     def stage(self, batch):
         """Copy one batch (dict of tensors/arrays, reference keys) into the static slots."""
         sp = self.spec
-        lab = _as_dev(batch["label"], F32, self.dev).reshape(-1)
-        B = lab.shape[0]
+        lab = batch["label"]
+        B = int(np.prod(lab.shape))
         if B > self.B:
             raise ValueError("batch %d > engine max_batch %d" % (B, self.B))
-        self.in_label[:B].copy_(lab)
+        _copy_in(self.in_label[:B], lab, F32, self.dev)
         if sp.C:
-            self.in_cont[:B, : sp.C].copy_(_as_dev(batch["cont_feats"], F32, self.dev))
+            _copy_in(self.in_cont[:B, : sp.C], batch["cont_feats"], F32, self.dev)
         if sp.V:
-            self.in_vec[:B, : sp.V].copy_(_as_dev(batch["vector_feats"], F32, self.dev))
-        self.in_cate[:B, : sp.cate_ld].copy_(_as_dev(batch["cate_feats"], torch.int64, self.dev))
+            _copy_in(self.in_vec[:B, : sp.V], batch["vector_feats"], F32, self.dev)
+        _copy_in(self.in_cate[:B, : sp.cate_ld], batch["cate_feats"], torch.int64, self.dev)
         if sp.Fw:
-            self.in_wide[:B, : sp.Fw].copy_(_as_dev(batch["wide_feats"], torch.int64, self.dev))
+            _copy_in(self.in_wide[:B, : sp.Fw], batch["wide_feats"], torch.int64, self.dev)
         return B
 
     # ------------------------------------------------------------------ step
@@ -1661,6 +1661,16 @@ def call_int(name, *args):
 def C_ref(L):
     import ctypes
     return ctypes.byref(L)
+
+
+def _copy_in(dst, x, dtype, dev):
+    """One input array into its static device slot: a pinned host tensor of the slot's dtype is
+    copied straight in, asynchronously on the current stream (no host wait); anything else goes
+    through _as_dev."""
+    if isinstance(x, torch.Tensor) and not x.is_cuda and x.dtype == dtype and x.is_pinned():
+        dst.copy_(x.view(dst.shape), non_blocking=True)
+    else:
+        dst.copy_(_as_dev(x, dtype, dev).reshape(dst.shape))
 
 
 def _as_dev(x, dtype, dev):

@@ -13,11 +13,15 @@ averaged over the epoch's batches (each weighted by batch_size), then exports th
 predict prints 'val of auc:%.5f'.  The engine runs the step as one hipGraph replay for
 full batches.
 """
+import concurrent.futures as cf
+import os
 import pickle
 import sys
+import threading
 import time
 
 import numpy as np
+import torch
 
 from ..engine import CTREngine, default_adam
 from ..metrics import AucAccumulator
@@ -26,6 +30,83 @@ from ._ctr_model import _predict_batches, export_model, load_model
 
 def unpickle(item):
     return pickle.loads(item) if isinstance(item, (bytes, bytearray)) else item
+
+
+class PinnedFeed:
+    """The load-style batches (pickled dicts, wdl.py:296) unpickled and converted on worker
+    threads into a ring of pinned host buffers, in order, ahead of the training loop: the engine
+    then stages each one with an asynchronous host-to-device copy on its side stream
+    (engine._copy_in) instead of the loop unpickling and copying 31 MB of pageable memory a C5
+    batch between steps.  A ring slot is refilled only after the step that consumed it has run
+    (release(): an event on the compute stream after that step)."""
+
+    def __init__(self, model, items, workers=None, depth=None):
+        self.model = model
+        self.items = iter(items)
+        self.workers = workers or int(os.environ.get("DLAMD_FEED_WORKERS", "2"))
+        self.depth = depth or self.workers + 2
+        self.bufs = [dict() for _ in range(self.depth)]
+        self.events = [None] * self.depth
+        self.free = [threading.Event() for _ in range(self.depth)]
+        for f in self.free:
+            f.set()
+        self.pool = cf.ThreadPoolExecutor(max_workers=self.workers)
+        self.pending = []
+        self.k = 0
+        self.lock = threading.Lock()
+        self.done = False
+        for _ in range(self.depth):
+            self._submit()
+
+    def _submit(self):
+        with self.lock:
+            if self.done:
+                return
+            item = next(self.items, None)
+            if item is None:
+                self.done = True
+                return
+            k = self.k
+            self.k += 1
+        self.pending.append(self.pool.submit(self._prepare, k, item))
+
+    def _prepare(self, k, item):
+        s = k % self.depth
+        self.free[s].wait()       # the slot's previous batch has been released (one claimant a slot:
+        self.free[s].clear()      # batch k + depth is submitted only once batch k was taken)
+        ev = self.events[s]
+        if ev is not None:
+            ev.synchronize()
+        d = self.model.batch(item)
+        out = {}
+        for key, a in d.items():
+            a = np.ascontiguousarray(a)
+            buf = self.bufs[s].get(key)
+            if buf is None or buf.numel() < a.size or buf.dtype != torch.from_numpy(a[:0]).dtype:
+                buf = self.bufs[s][key] = torch.empty(a.size, dtype=torch.from_numpy(a[:0]).dtype).pin_memory()
+            v = buf[: a.size].view(a.shape)
+            v.copy_(torch.from_numpy(a))
+            out[key] = v
+        out["_slot"] = s
+        return out
+
+    def __iter__(self):
+        while self.pending:
+            fut = self.pending.pop(0)
+            b = fut.result()
+            self._submit()
+            yield b
+
+    def release(self, b):
+        """b's step has been submitted: its slot may be refilled once the compute stream is past it."""
+        s = b["_slot"]
+        ev = torch.cuda.Event()
+        ev.record()
+        self.events[s] = ev
+        self.free[s].set()
+
+    def close(self):
+        self.pool.shutdown(wait=True)
 
 
 class LoadStyleModel:
@@ -66,15 +147,18 @@ class LoadStyleModel:
         eng = self.model_optimizer()
         eng.loss_sum_begin()
         steps = 0
-        items = iter(train_data)
-        b = next(items, None)
-        b = self.batch(b) if b is not None else None
-        while b is not None:
-            nxt = next(items, None)
-            nxt = self.batch(nxt) if nxt is not None else None
-            eng.train_step(b, graph=b["label"].shape[0] == eng.B, **({"next_batch": nxt} if nxt is not None else {}))
-            steps += 1
-            b = nxt
+        feed = PinnedFeed(self, train_data)
+        try:
+            items = iter(feed)
+            b = next(items, None)
+            while b is not None:
+                nxt = next(items, None)
+                eng.train_step(b, graph=b["label"].shape[0] == eng.B, **({"next_batch": nxt} if nxt is not None else {}))
+                feed.release(b)
+                steps += 1
+                b = nxt
+        finally:
+            feed.close()
         loss_sum, counted = eng.loss_sum_end()
         if counted != steps:
             eng.check_error()   # a skipped (bad) batch raises here, as its sess.run did
