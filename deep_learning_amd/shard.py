@@ -213,6 +213,7 @@ class ShardedCTREngine(CTREngine):
         self.head_w = spec.fm_cols + H + 2          # weights + bias + loss sum
         self.seg.append(("head", off, self.head_w))
         off += self.head_w
+        off = _ru(off, 4)                           # the replicated rows' gradients 16-B aligned (dl_adam_rows)
         self.rep_off = off
         off += rp * E + rp
         self.flat = z(off)

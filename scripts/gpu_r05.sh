@@ -1,0 +1,37 @@
+#!/bin/bash
+# Round-5 GPU session: steps named on the command line, each under its own time limit; a
+# step that times out, aborts or faults (rc >= 124) ends the session, a failing test does not.
+#   bash scripts/gpu_r05.sh TAG step [step ...]
+#   steps: shard | gemm_epd | kernels | parity | fullsize | bench | benchsh | smoke | all_gpu
+cd "$GRAFT_REPO_ROOT"; export TMPDIR=/tmp; OUT=gpurun_out/$1; shift; mkdir -p $OUT
+run() {   # run NAME LIMIT CMD...
+  local name=$1 lim=$2; shift 2
+  timeout -k 10 $lim "$@" > $OUT/$name.log 2>&1; local rc=$?
+  echo "[$name] rc=$rc $(grep -v amdgpu.ids $OUT/$name.log | tail -1)"
+  if [ $rc -ge 124 ]; then echo "[$name] stopping the session (rc $rc)"; exit $rc; fi
+  return 0
+}
+PYT="python -u -m pytest -v --timeout 300 --timeout-method thread -p no:cacheprovider"
+for step in "$@"; do
+  case $step in
+    shard) run shard 700 $PYT tests/test_gpu_shard.py tests/test_shard.py -m gpu ;;
+    kernels) run kernels 900 $PYT tests/test_gpu_kernels.py tests/test_gpu_comm.py -m gpu ;;
+    parity) run parity 1100 env DLAMD_TEST_STATS=$OUT $PYT tests/test_gpu_parity.py tests/test_gpu_dropin.py -m gpu ;;
+    fullsize) run fullsize 1150 env DLAMD_TEST_STATS=$OUT $PYT tests/test_gpu_fullsize.py -m gpu ;;
+    all_gpu) run all_gpu 1150 env DLAMD_TEST_STATS=$OUT $PYT tests -m gpu ;;
+    gemm_epd)
+      run epd_tests 600 env DLAMD_VARIANT=epd $PYT tests/test_gpu_kernels.py -m gpu -k "s3 or gemm"
+      for v in base epd base epd; do
+        if [ $v = base ]; then E=""; else E=$v; fi
+        run s3_$v 200 env DLAMD_VARIANT=$E python scripts/s3_bench.py 20
+        cat $OUT/s3_$v.log | grep -v amdgpu.ids >> $OUT/s3_ab.txt
+      done ;;
+    bench) run bench 900 python bench.py ;;
+    benchsh) run benchsh 600 python bench.py --sharded --no-extra --no-cpu-baseline --steps 20 ;;
+    benchsh_c2) run benchsh_c2 600 python bench.py --sharded --no-extra --no-cpu-baseline --steps 20 --vocab 1000000 ;;
+    benchc2) run benchc2 600 python bench.py --no-extra --no-cpu-baseline --steps 20 ;;
+    benchc4single) run benchc4single 600 python bench.py --no-extra --no-cpu-baseline --steps 20 --vocab 3846154 ;;
+    smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
+    *) echo "unknown step $step" ;;
+  esac
+done

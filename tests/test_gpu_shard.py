@@ -95,7 +95,8 @@ def test_shard_route_matches_numpy(hip_lib, world, rank, room):
     np.testing.assert_array_equal(ids.cpu().numpy(), e_ids)
     h = hdr.cpu().numpy().reshape(nb, 4)
     np.testing.assert_array_equal(h[:, [0, 2, 3]], e_hdr[:, [0, 2, 3]])
-    assert (h[:, 1] == (_lib.STATUS_OVERFLOW if ovf else 0)).all(), h[:, 1]
+    sent = [p if p == rank else world + p - (1 if p > rank else 0) for p in range(world)]   # the route's blocks
+    assert (h[sent, 1] == (_lib.STATUS_OVERFLOW if ovf else 0)).all(), h[:, 1]
     np.testing.assert_array_equal(rep.cpu().numpy(), e_rep[:rep_cap])
     np.testing.assert_array_equal(upos[:nuv].cpu().numpy(), e_upos)
     np.testing.assert_array_equal(inv.cpu().numpy(), e_inv)
