@@ -109,6 +109,10 @@ enum { S3_STORE = 0, S3_RELU = 1, S3_MASK = 2, S3_MASKBITS = 3 };
 #define DL_S3_ASMB 0  // NT: the weight fragments' LDS reads as inline asm, DL_S3_PF fragments ahead,
 #endif                // each fragment's MFMAs behind a hand-counted lgkmcnt wait tied to its registers
 
+#ifndef DL_S3_ESPLIT
+#define DL_S3_ESPLIT 0   // NT: chunk c + 1's A planes split in the middle of chunk c's MFMAs
+#endif
+
 #ifndef DL_S3_TNSTAG
 #define DL_S3_TNSTAG 0   // TN2: waves 4-7 split + store the next step's tiles BEFORE their MFMAs
 #endif                   // (waves 0-3 after), so the two waves of a SIMD overlap VALU/LDS with MFMA
@@ -258,6 +262,59 @@ __global__ __launch_bounds__(512) void gemm_s3_nt_kernel(S3Params p) {
   // chunk 0's B must have landed
   publish(-1);
 
+#if DL_S3_ESPLIT
+  if constexpr (EPI != S3_MASK) {
+    // Early split: chunk c + 1's A planes are split in the middle of chunk c's fragments (its
+    // MFMAs issue beside the VALU work), so after each barrier the waves start on MFMAs instead of
+    // on the split.  Per step c: A(c + 2) into the raw registers chunk c came in (split during
+    // step c - 1), fragments 0..kNtEsAt, the split of chunk c + 1 (its wait covers only loads older
+    // than A(c + 2)), B(c + 2) by LDS-DMA, the other fragments, the barrier (every batch but
+    // A(c + 2) + B(c + 2) landed: chunk c + 1's weights).  Same products in the same order.
+    constexpr int kNtEsAt = 6;
+    shortx8 pA[6], pB[6];
+    auto splitp = [&](float4 (&ra)[4], shortx8 (&P)[6]) {
+      split8(ra[0], ra[1], P[0], P[1], P[2]);
+      split8(ra[2], ra[3], P[3], P[4], P[5]);
+      asm volatile("" : "+v"(P[0]), "+v"(P[1]), "+v"(P[2]), "+v"(P[3]), "+v"(P[4]), "+v"(P[5]));
+    };
+    splitp(raA, pA);
+    auto step_es = [&](int c, shortx8 (&P)[6], shortx8 (&Pn)[6], float4 (&R)[4], float4 (&F)[4]) {
+      load_a(c + 2, F);
+      asm volatile("" ::: "memory");   // the loads issue here, not sunk to the mid-step split
+      const uint32_t b_addr = lds_base + 2u * (uint32_t)((c % 3) * kNtBuf + cl * 32 + 8 * nt_slot(cl, kq));
+      const unsigned short* Bs = lds + (c % 3) * kNtBuf;
+      auto rd_b = [&](int f, shortx8& bh, shortx8& bm, shortx8& bl) {
+        const int j = 16 * f + cl;
+        const int o = j * 32 + 8 * nt_slot(j, kq);
+        bh = *reinterpret_cast<const shortx8*>(&Bs[o]);
+        bm = *reinterpret_cast<const shortx8*>(&Bs[kNtPlane + o]);
+        bl = *reinterpret_cast<const shortx8*>(&Bs[2 * kNtPlane + o]);
+      };
+      (void)b_addr;
+      shortx8 bb[2][3];
+      rd_b(0, bb[0][0], bb[0][1], bb[0][2]);
+#pragma unroll
+      for (int f = 0; f < kNtNF; ++f) {
+        if (f + 1 < kNtNF) rd_b(f + 1, bb[(f + 1) & 1][0], bb[(f + 1) & 1][1], bb[(f + 1) & 1][2]);
+        const shortx8 bh = bb[f & 1][0], bm = bb[f & 1][1], bl = bb[f & 1][2];
+        acc[0][f] = mfma_s3(P[0], P[1], P[2], bh, bm, bl, acc[0][f]);
+        acc[1][f] = mfma_s3(P[3], P[4], P[5], bh, bm, bl, acc[1][f]);
+        if (f == kNtEsAt) {
+          if (c + 1 < KC) splitp(R, Pn);
+          dma_b(c + 2, (c + 2) % 3);
+        }
+      }
+      publish(c);
+    };
+    int c = 0;
+    for (; c + 1 < KC; c += 2) {
+      step_es(c, pA, pB, raB, raA);
+      step_es(c + 1, pB, pA, raA, raB);
+    }
+    if (c < KC) step_es(c, pA, pB, raB, raA);
+  } else
+#endif
+  {
   auto step = [&](int c, float4 (&ra)[4]) {
     shortx8 ah[2], am[2], al[2];
     if (DL_S3_DIAG == 6) {   // timing only: the f32 bits taken as planes, no split
@@ -344,6 +401,7 @@ __global__ __launch_bounds__(512) void gemm_s3_nt_kernel(S3Params p) {
     step(c + 1, raB);
   }
   if (c < KC) step(c, raA);
+  }
 
   if (DL_S3_DIAG && DL_S3_DIAG != 6 && DL_S3_DIAG != 7) {   // keep the loop's results live without storing them
     float tt = 0.f;

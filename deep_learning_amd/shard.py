@@ -158,8 +158,10 @@ class Exchange:
 class ShardedCTREngine(CTREngine):
     """CTREngine whose embedding tables are row-sharded across the ranks of `exch`."""
 
-    # slack of a block over an even split of the batch's references (DLAMD_SHARD_SLACK)
-    SLACK = 0.25
+    # slack of a block over an even split of the batch's references (DLAMD_SHARD_SLACK): at C4
+    # (8 ranks, 3.4 M references a batch) a block holds 468 k rows against ~419 k unique rows per
+    # owner for uniform ids (binomial spread ~0.7 k), fewer under Zipf; an overflow is replayed
+    SLACK = 0.10
 
     def __init__(self, spec, max_batch, exch, device="cuda", seed=2019, adam="dense", hist_len=4096,
                  owner_update=None, slack=None, lag=2):
@@ -928,12 +930,22 @@ class ShardedCTREngine(CTREngine):
             self._ring_sent = int(self.opt.view(torch.int32)[_lib.OPT_SEQ].item())
             self._ring_checked = self._ring_sent
         # the first steps run eagerly: RCCL connects its peers then, not inside a capture
-        if graph and self.prof is None and self._steps_eager >= 1 and not self.exch.staged:
+        if (graph and self.prof is None and self._steps_eager >= 1 and not self.exch.staged
+                and os.environ.get("DLAMD_SHARD_GRAPH", "1") != "0" and not getattr(self, "_graph_failed", False)):
             key = (getattr(self, "_cur", 0), B)
             g = self.graphs.get(key)
             if g is None:
-                g = self.graphs[key] = self._capture_step(B)
-            g.replay()
+                try:
+                    g = self.graphs[key] = self._capture_step(B)
+                except Exception as ex:   # a runtime that cannot capture the step's RCCL group: eager
+                    import sys
+                    print("[shard] step capture failed (%r): the step runs eagerly" % (ex,), file=sys.stderr)
+                    self._graph_failed = True
+                    g = None
+            if g is not None:
+                g.replay()
+            else:
+                self._step(B)
         else:
             self._step(B)
             self._steps_eager += 1

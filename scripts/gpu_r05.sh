@@ -19,12 +19,22 @@ for step in "$@"; do
     parity) run parity 1100 env DLAMD_TEST_STATS=$OUT $PYT tests/test_gpu_parity.py tests/test_gpu_dropin.py -m gpu ;;
     fullsize) run fullsize 1150 env DLAMD_TEST_STATS=$OUT $PYT tests/test_gpu_fullsize.py -m gpu ;;
     all_gpu) run all_gpu 1150 env DLAMD_TEST_STATS=$OUT $PYT tests -m gpu ;;
-    gemm_epd)
-      run epd_tests 600 env DLAMD_VARIANT=epd $PYT tests/test_gpu_kernels.py -m gpu -k "s3 or gemm"
-      for v in base epd base epd; do
-        if [ $v = base ]; then E=""; else E=$v; fi
-        run s3_$v 200 env DLAMD_VARIANT=$E python scripts/s3_bench.py 20
-        cat $OUT/s3_$v.log | grep -v amdgpu.ids >> $OUT/s3_ab.txt
+    c1) run c1 600 env DLAMD_TEST_STATS=$OUT $PYT tests/test_gpu_parity.py -m gpu -k "c1_defaults or bf16_tower" ;;
+    suite) run suite 1100 env DLAMD_TEST_STATS=$OUT $PYT tests -m gpu --ignore=tests/test_gpu_fullsize.py ;;
+    gemm_ab_*)   # gemm_ab_<variant>: GEMM tests on the variant, s3_bench and C2 A/B
+      v=${step#gemm_ab_}
+      run ${v}_tests 600 env DLAMD_VARIANT=$v $PYT tests/test_gpu_kernels.py -m gpu -k "s3 or gemm"
+      for a in base $v base $v; do
+        if [ $a = base ]; then E=""; else E=$a; fi
+        run s3_$a 200 env DLAMD_VARIANT=$E python scripts/s3_bench.py 20
+        grep -v amdgpu.ids $OUT/s3_$a.log | sed "s/^/[$a] /" >> $OUT/s3_ab.txt
+      done
+      for a in base $v base $v; do
+        if [ $a = base ]; then E=""; else E=$a; fi
+        run c2_$a 300 env DLAMD_VARIANT=$E python bench.py --no-cpu-baseline --no-extra --steps 20
+        grep '^{' $OUT/c2_$a.log | python -c "
+import json,sys;d=json.loads(sys.stdin.read().strip().splitlines()[-1]);k=d['kernels']
+print('$a', d['ms_per_step'], {n: k[n]['us'] for n in k if n.startswith('gemm')})" >> $OUT/c2_ab.txt
       done ;;
     bench) run bench 900 python bench.py ;;
     benchsh) run benchsh 600 python bench.py --sharded --no-extra --no-cpu-baseline --steps 20 ;;
