@@ -21,10 +21,12 @@
 //       MFMA fragments by CDNA4's transposing ds_read_b64_tr_b16.  Block 128 x 416
 //       (8 waves x 32 rows x 13 column fragments).
 #include "common.h"
+#include <cstdlib>
 
 namespace dl {
 
 typedef float floatx4 __attribute__((ext_vector_type(4)));
+typedef unsigned int s3_u32x4_t __attribute__((__vector_size__(4 * sizeof(unsigned int))));
 typedef short shortx8 __attribute__((ext_vector_type(8)));
 typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
 typedef float floatx2_t __attribute__((ext_vector_type(2)));
@@ -70,6 +72,21 @@ __device__ __forceinline__ floatx4 mfma_s3(const shortx8& ah, const shortx8& am,
   return acc;
 }
 
+// The same six products, each with the operands' roles swapped (B's planes as the MFMA's src A):
+// the accumulator then holds C^T's 16 x 16 block — lane (kq, cl) has row cl, columns 4kq .. 4kq + 3
+// — so the NT epilogue stores a float4 of one output row per lane straight from registers.
+__device__ __forceinline__ floatx4 mfma_s3_t(const shortx8& ah, const shortx8& am, const shortx8& al,
+                                             const shortx8& bh, const shortx8& bm, const shortx8& bl,
+                                             floatx4 acc) {
+  acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bh, al, acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bl, ah, acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bm, am, acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bh, am, acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bm, ah, acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bh, ah, acc, 0, 0, 0);
+  return acc;
+}
+
 __device__ __forceinline__ int s3_xcd_tile(int bid, int T) {
   const int x = bid & 7;
   const int q = T >> 3, rm = T & 7;
@@ -110,7 +127,8 @@ enum { S3_STORE = 0, S3_RELU = 1, S3_MASK = 2, S3_MASKBITS = 3 };
 #endif                // each fragment's MFMAs behind a hand-counted lgkmcnt wait tied to its registers
 
 #ifndef DL_S3_ESPLIT
-#define DL_S3_ESPLIT 0   // NT: chunk c + 1's A planes split in the middle of chunk c's MFMAs
+#define DL_S3_ESPLIT 1   // NT: chunk c + 1's A planes split in the middle of chunk c's MFMAs
+                         // (fwd_l1 114.7 -> 110.9 us alone, profiles/r05f/s3_ab.txt)
 #endif
 
 #ifndef DL_S3_TNSTAG
@@ -162,7 +180,12 @@ __device__ __forceinline__ void nt_rd3(uint32_t a, shortx8& h, shortx8& m, short
 // s_waitcnt vmcnt(n) (n < 64), other counters untouched
 #define DL_WAIT_VMCNT(n) __builtin_amdgcn_s_waitcnt(((n) & 0xF) | (((n) >> 4) << 14) | (0x7 << 4) | (0xF << 8))
 
-template <int EPI>
+// DIRECT: the transposed accumulator layout (mfma_s3_t) and the epilogue straight from registers
+// — one 16-B store of four consecutive columns per lane and fragment (a wave instruction writes
+// 16 rows x 64 B), ReLU / ReluGrad bitmask in registers — instead of the transpose through the
+// LDS ring; the bitmask words the dX epilogue needs are loaded before the main loop.  Needs
+// N % 4 == 0, ldc % 4 == 0 and an even ldbits (the host picks it then; otherwise the LDS form).
+template <int EPI, bool DIRECT = false>
 __global__ __launch_bounds__(512) void gemm_s3_nt_kernel(S3Params p) {
   extern __shared__ __attribute__((aligned(16))) unsigned short lds[];   // [3 bufs][3 planes][BN][32]
   const unsigned short* __restrict__ Bp = reinterpret_cast<const unsigned short*>(p.B);
@@ -239,6 +262,20 @@ __global__ __launch_bounds__(512) void gemm_s3_nt_kernel(S3Params p) {
 #pragma unroll
     for (int f = 0; f < kNtNF; ++f) acc[a][f] = floatx4{0.f, 0.f, 0.f, 0.f};
 
+  // DIRECT ReluGrad: this lane's rows' bitmask words for the tile's 13 halfwords (j0 / 16 ..
+  // + 12), 7 dwords from the dword holding the first (ldbits even: rows are dword aligned),
+  // loaded here so the epilogue does not wait a memory round trip for them
+  uint32_t mw[DIRECT && EPI == S3_MASKBITS ? 2 : 1][7];
+  if constexpr (DIRECT && EPI == S3_MASKBITS) {
+#pragma unroll
+    for (int a = 0; a < 2; ++a) {
+      const int row = min(r0 + 16 * a + cl, p.M - 1);
+      const uint32_t* wp = reinterpret_cast<const uint32_t*>(p.bits + (long long)row * p.ldbits) + (j0 >> 5);
+#pragma unroll
+      for (int i = 0; i < 7; ++i) mw[a][i] = wp[i];
+    }
+  }
+
   float4 raA[4], raB[4];
   // prologue: B chunks 0 and 1 in flight, A chunks 0 and 1
   dma_b(0, 0);
@@ -297,8 +334,13 @@ __global__ __launch_bounds__(512) void gemm_s3_nt_kernel(S3Params p) {
       for (int f = 0; f < kNtNF; ++f) {
         if (f + 1 < kNtNF) rd_b(f + 1, bb[(f + 1) & 1][0], bb[(f + 1) & 1][1], bb[(f + 1) & 1][2]);
         const shortx8 bh = bb[f & 1][0], bm = bb[f & 1][1], bl = bb[f & 1][2];
-        acc[0][f] = mfma_s3(P[0], P[1], P[2], bh, bm, bl, acc[0][f]);
-        acc[1][f] = mfma_s3(P[3], P[4], P[5], bh, bm, bl, acc[1][f]);
+        if (DIRECT) {
+          acc[0][f] = mfma_s3_t(P[0], P[1], P[2], bh, bm, bl, acc[0][f]);
+          acc[1][f] = mfma_s3_t(P[3], P[4], P[5], bh, bm, bl, acc[1][f]);
+        } else {
+          acc[0][f] = mfma_s3(P[0], P[1], P[2], bh, bm, bl, acc[0][f]);
+          acc[1][f] = mfma_s3(P[3], P[4], P[5], bh, bm, bl, acc[1][f]);
+        }
         if (f == kNtEsAt) {
           if (c + 1 < KC) splitp(R, Pn);
           dma_b(c + 2, (c + 2) % 3);
@@ -381,6 +423,9 @@ __global__ __launch_bounds__(512) void gemm_s3_nt_kernel(S3Params p) {
         if (DL_S3_DIAG == 2) {
           acc[0][f][0] += (float)(bh[0] ^ ah[0][1] ^ bm[2] ^ bl[3] ^ am[0][0] ^ al[0][2]);
           acc[1][f][0] += (float)(bh[1] ^ ah[1][1] ^ bm[3] ^ bl[4] ^ am[1][0] ^ al[1][2]);
+        } else if (DIRECT) {
+          acc[0][f] = mfma_s3_t(ah[0], am[0], al[0], bh, bm, bl, acc[0][f]);
+          acc[1][f] = mfma_s3_t(ah[1], am[1], al[1], bh, bm, bl, acc[1][f]);
         } else {
           acc[0][f] = mfma_s3(ah[0], am[0], al[0], bh, bm, bl, acc[0][f]);
           acc[1][f] = mfma_s3(ah[1], am[1], al[1], bh, bm, bl, acc[1][f]);
@@ -410,6 +455,41 @@ __global__ __launch_bounds__(512) void gemm_s3_nt_kernel(S3Params p) {
 #pragma unroll
       for (int f = 0; f < kNtNF; ++f) tt += acc[a][f][0] + acc[a][f][3];
     if (tt == 12345.f) p.C[0] = tt;
+    return;
+  }
+  if constexpr (DIRECT) {
+    // lane (kq, cl): acc[a][f][j] = C[r0 + 16a + cl][j0 + 16f + 4kq + j].  Stores go through a
+    // buffer descriptor: a piece past M or N gets an offset past its range and is dropped.
+    const auto c_rsrc = __builtin_amdgcn_make_buffer_rsrc((void*)p.C, (short)0, p.M * p.ldc * 4, 0x00020000);
+#pragma unroll
+    for (int a = 0; a < 2; ++a) {
+      const int row = r0 + 16 * a + cl;
+#pragma unroll
+      for (int f = 0; f < kNtNF; ++f) {
+        const int col = j0 + 16 * f + 4 * kq;
+        floatx4 v = acc[a][f];
+        if (EPI == S3_RELU) {
+          v[0] = fmaxf(v[0], 0.f); v[1] = fmaxf(v[1], 0.f); v[2] = fmaxf(v[2], 0.f); v[3] = fmaxf(v[3], 0.f);
+        }
+        if constexpr (EPI == S3_MASKBITS) {   // halfword (j0 >> 4) + f of the row, bits 4kq .. 4kq + 3
+          const int hi = (j0 >> 4) + f - 2 * (j0 >> 5);
+          const uint32_t m = (mw[a][hi >> 1] >> (16 * (hi & 1) + 4 * kq)) & 0xFu;
+          v[0] = (m & 1u) ? v[0] : 0.f; v[1] = (m & 2u) ? v[1] : 0.f;
+          v[2] = (m & 4u) ? v[2] : 0.f; v[3] = (m & 8u) ? v[3] : 0.f;
+        }
+        const bool ok = row < p.M && col + 4 <= p.N;
+        const uint32_t off = ok ? 4u * (uint32_t)(row * p.ldc + col) : 0x80000000u;
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(s3_u32x4_t, v), c_rsrc, (int)off, 0, 0);
+        if (EPI == S3_RELU && p.bits) {   // the sign bitmask: row's 16 bits of fragment f from 4 lanes
+          uint32_t hw = (uint32_t)((acc[a][f][0] > 0.f) | ((acc[a][f][1] > 0.f) << 1) | ((acc[a][f][2] > 0.f) << 2) |
+                                   ((acc[a][f][3] > 0.f) << 3)) << (4 * kq);
+          hw |= (uint32_t)__shfl_xor((int)hw, 16, 64);
+          hw |= (uint32_t)__shfl_xor((int)hw, 32, 64);
+          const int h = (j0 >> 4) + f;
+          if (kq == 0 && row < p.M && 16 * h < p.N) p.bits[(long long)row * p.ldbits + h] = (uint16_t)hw;
+        }
+      }
+    }
     return;
   }
   // Epilogue through LDS (the ring is free after the last barrier): per wave and per half
@@ -990,6 +1070,15 @@ using namespace dl;
 
 extern "C" int dl_s3_kperm(void) { return DL_S3_KPERM; }
 
+// DL_S3_DIRECT=0 in the environment: the NT epilogue through LDS (A/B measurements)
+static bool s3_direct_enabled() {
+  static const bool on = [] {
+    const char* e = getenv("DL_S3_DIRECT");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
 extern "C" int dl_split3(const float* src, int32_t rows, int32_t cols, int32_t lds, int32_t transpose,
                          uint16_t* dst, int32_t ldd, int64_t plane_stride, void* stream) {
   DL_CHECK_ARG(src && dst, "NULL pointer");
@@ -1029,7 +1118,14 @@ extern "C" int dl_gemm_s3_nt_bits(int32_t M, int32_t N, int32_t K, const float* 
   p.bits = bits; p.ldbits = ldbits;
   const int tiles = (int)(ceil_div(M, kNtBM) * ceil_div(N, kNtBN));
   hipStream_t s = as_stream(stream);
-  if (epi == S3_STORE) hipLaunchKernelGGL(gemm_s3_nt_kernel<S3_STORE>, dim3(tiles), dim3(512), kNtLds, s, p);
+  const bool direct = s3_direct_enabled() && N % 4 == 0 && ldc % 4 == 0 && (!bits || ldbits % 2 == 0) &&
+                      epi != S3_MASK && (long long)M * ldc * 4 < (1LL << 31) &&
+                      (epi != S3_MASKBITS || ldbits >= 2 * ((((int)ceil_div(N, kNtBN) - 1) * kNtBN >> 5) + 7));
+  if (direct) {
+    if (epi == S3_STORE) hipLaunchKernelGGL((gemm_s3_nt_kernel<S3_STORE, true>), dim3(tiles), dim3(512), kNtLds, s, p);
+    else if (epi == S3_RELU) hipLaunchKernelGGL((gemm_s3_nt_kernel<S3_RELU, true>), dim3(tiles), dim3(512), kNtLds, s, p);
+    else hipLaunchKernelGGL((gemm_s3_nt_kernel<S3_MASKBITS, true>), dim3(tiles), dim3(512), kNtLds, s, p);
+  } else if (epi == S3_STORE) hipLaunchKernelGGL(gemm_s3_nt_kernel<S3_STORE>, dim3(tiles), dim3(512), kNtLds, s, p);
   else if (epi == S3_RELU) hipLaunchKernelGGL(gemm_s3_nt_kernel<S3_RELU>, dim3(tiles), dim3(512), kNtLds, s, p);
   else if (epi == S3_MASK) hipLaunchKernelGGL(gemm_s3_nt_kernel<S3_MASK>, dim3(tiles), dim3(512), kNtLds, s, p);
   else hipLaunchKernelGGL(gemm_s3_nt_kernel<S3_MASKBITS>, dim3(tiles), dim3(512), kNtLds, s, p);

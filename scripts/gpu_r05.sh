@@ -36,6 +36,17 @@ for step in "$@"; do
 import json,sys;d=json.loads(sys.stdin.read().strip().splitlines()[-1]);k=d['kernels']
 print('$a', d['ms_per_step'], {n: k[n]['us'] for n in k if n.startswith('gemm')})" >> $OUT/c2_ab.txt
       done ;;
+    envab_*)   # envab_<VAR>_<workload>[_<dist>]: bench arms VAR=0 / 1 / 0 / 1 on one box
+      rest=${step#envab_}; var=${rest%%__*}; wl=${rest#*__}; dist=uniform
+      case $wl in *_zipf) dist=zipf; wl=${wl%_zipf} ;; esac
+      for a in 0 1 0 1; do
+        run ${var}_${wl}_${dist}_$a 300 env $var=$a python bench.py --workload $wl --dist $dist --no-cpu-baseline --no-extra --steps 20
+        grep '^{' $OUT/${var}_${wl}_${dist}_$a.log | python -c "
+import json,sys;d=json.loads(sys.stdin.read().strip().splitlines()[-1]);k=d['kernels']
+print('$var=$a $wl $dist', d['ms_per_step'], {n: k[n]['us'] for n in k})" >> $OUT/envab.txt
+      done ;;
+    tests_*)   # tests_<pattern>: the GPU tests whose names match
+      run tests_sel 900 $PYT tests -m gpu -k "${step#tests_}" ;;
     bench) run bench 900 python bench.py ;;
     benchsh) run benchsh 600 python bench.py --sharded --no-extra --no-cpu-baseline --steps 20 ;;
     benchsh_c2) run benchsh_c2 600 python bench.py --sharded --no-extra --no-cpu-baseline --steps 20 --vocab 1000000 ;;

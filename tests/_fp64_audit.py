@@ -24,8 +24,9 @@ own bound; its v and p must have moved by TF1 Adam on that gradient.  Together: 
 the GPU's step is an f32 evaluation of the reference graph, so an element whose value differs
 from the f32 oracle's (numpy's evaluation order) is ill-conditioned, not wrong.
 
-Supported: the FM pipeline models with a zero row 0 (deepfm_pipeline, deepfm_multi_cate —
-BASELINE configs C2, C3).
+Supported: the pipeline models with a zero row 0 — the FM ones (deepfm_pipeline,
+deepfm_multi_cate: BASELINE configs C2, C3) and the DNN ones (dnn_pipeline: C1, whose head is
+deep_res on the last hidden layer, dnn_pipeline.py).
 """
 import numpy as np
 
@@ -54,14 +55,16 @@ def read_gpu(eng, B):
              fm_sum=eng.fm_sum[:B, :sp.E].cpu().numpy(), w_head=eng.w_head_prev[:eng.head_n].cpu().numpy())
     if sp.M:
         d["cnt_emb"] = eng.cnt_emb[:B].cpu().numpy()
-        d["cnt_first"] = eng.cnt_first[:B].cpu().numpy()
+        if sp.fm:
+            d["cnt_first"] = eng.cnt_first[:B].cpu().numpy()
     return d
 
 
 class StepAudit:
     def __init__(self, cfg, P, batch, gpu):
         """P: the GPU's pre-step parameters (reference layout); gpu: read_gpu() after the step."""
-        assert R.is_fm(cfg) and R.zero_row0(cfg), "the audit covers the FM pipeline models"
+        assert R.zero_row0(cfg) and cfg.model not in ("wdl", "deepfm", "dnn"), "the audit covers the pipeline models"
+        fm = self.fm = R.is_fm(cfg)
         self.cfg, self.gpu = cfg, gpu
         self.fails, self.stats = [], {}
         E, S, C = cfg.E, cfg.S, cfg.C
@@ -93,7 +96,7 @@ class StepAudit:
         idx = np.concatenate([cidx, single + (C if fam == "first" else 0)], 1)
         val = np.concatenate([cont[:, :Cf], np.ones((B, S))], 1)
         nI = idx.shape[1]
-        nF = R.fm_fields(cfg)
+        nF = R.fm_fields(cfg) if fm else 0
         # ---- x0: the deep lookups bit-exact, the pooled means within their bound
         x0g = gpu["x0"].astype(F64)
         col = C + cfg.V
@@ -105,11 +108,12 @@ class StepAudit:
             ids = multi[:, a:b_]
             v32 = rows32(ids)
             n = (v32.sum(axis=2) != 0).sum(1)
-            f32 = np.where(ids == 0, 0, P[t1][ids, 0])
+            f32 = np.where(ids == 0, 0, P[t1][ids, 0]) if fm else np.zeros(ids.shape, np.float32)
             n1 = (f32 != 0).sum(1)
             # the counts are integers: bit-exact
             self._exact("pool count slot %d" % m, gpu["cnt_emb"][:, m], n.astype(np.float32))
-            self._exact("pool first-order count slot %d" % m, gpu["cnt_first"][:, m], n1.astype(np.float32))
+            if fm:
+                self._exact("pool first-order count slot %d" % m, gpu["cnt_first"][:, m], n1.astype(np.float32))
             dv = np.where(n > 0, n, 1)[:, None].astype(F64)
             pooled.append(np.where(n[:, None] > 0, v32.astype(F64).sum(1) / dv, 0))
             pooled_a.append(np.where(n[:, None] > 0, np.abs(v32.astype(F64)).sum(1) / dv, 0))
@@ -126,18 +130,22 @@ class StepAudit:
             pg = np.zeros((B, 0, E))
             p1 = np.zeros((B, 0))
         # ---- FM first / second order (deepfm_pipeline.py:89-110) from the GPU's pooled rows
-        ei = rows32(idx).astype(F64) * val[:, :, None]
-        e = np.concatenate([ei, pg], 1)
-        ea = np.abs(e)
-        s64, sa = e.sum(1), ea.sum(1)
-        fo = gpu["fm_out"].astype(F64)
-        fs = gpu["fm_sum"].astype(F64)
-        self._close("fm first order", fo[:, :nI], w1(idx) * val, np.abs(w1(idx) * val), 4)
-        if M:
-            self._close("fm pooled first order", fo[:, nI:nF], p1, p1_a, 128)
-        self._close("fm sum", fs, s64, sa, 128)
-        second = 0.5 * (fs * fs - (e * e).sum(1))
-        self._close("fm second order", fo[:, nF:nF + E], second, 0.5 * (fs * fs + (ea * ea).sum(1) + 2 * sa * sa), 256)
+        e = ea = fs = sa = None
+        fo = np.zeros((B, 0))
+        if fm:
+            ei = rows32(idx).astype(F64) * val[:, :, None]
+            e = np.concatenate([ei, pg], 1)
+            ea = np.abs(e)
+            s64, sa = e.sum(1), ea.sum(1)
+            fo = gpu["fm_out"].astype(F64)
+            fs = gpu["fm_sum"].astype(F64)
+            self._close("fm first order", fo[:, :nI], w1(idx) * val, np.abs(w1(idx) * val), 4)
+            if M:
+                self._close("fm pooled first order", fo[:, nI:nF], p1, p1_a, 128)
+            self._close("fm sum", fs, s64, sa, 128)
+            second = 0.5 * (fs * fs - (e * e).sum(1))
+            self._close("fm second order", fo[:, nF:nF + E], second,
+                        0.5 * (fs * fs + (ea * ea).sum(1) + 2 * sa * sa), 256)
         # ---- tower forward: h_l = relu(X_l W_l + b_l) from the GPU's X_l
         Ws = [P["deep_%d" % i].astype(F64) for i in range(L)]
         bs = [P["deep_bias_%d" % i].astype(F64) for i in range(L)]
@@ -162,8 +170,8 @@ class StepAudit:
         dzg = gpu["dz"].astype(F64)
         self._close("dz", dzg, dz64, np.abs(dz64) + 1.0 / B, 64)
         # ---- tower backward from the GPU's own gradients
-        Wa = np.abs(Wh)
-        dh_top = np.outer(dzg, Wh[nF + E:-1]) * (X[L] > 0)
+        hoff = nF + E if fm else 0          # head weights of the last hidden layer (FM outputs first)
+        dh_top = np.outer(dzg, Wh[hoff:-1]) * (X[L] > 0)
         G = [gpu["dh"][i].astype(F64) for i in range(L)]
         self._close("dh %d" % (L - 1), G[L - 1], dh_top, np.abs(dh_top), 4)
         for i in range(L - 1, 0, -1):
@@ -175,15 +183,17 @@ class StepAudit:
         self._close("dx0", dx0g, dx0, np.abs(G[0]) @ np.abs(Ws[0][emb]).T, K_GEMM)
         # ---- parameter gradients of the GPU's own terms (values and scales), per element on demand
         l2 = cfg.l2
-        Wfm = P["deep_fm_weight"][:, 0].astype(F64)
-        self.dense = {"deep_fm_weight": ((feats.T @ dzg + l2 * Wfm)[:, None],
-                                         (np.abs(feats).T @ np.abs(dzg) + l2 * np.abs(Wfm))[:, None]),
-                      "deep_fm_bias": (np.array([dzg.sum()]), np.array([np.abs(dzg).sum()]))}
+        hw, hb = ("deep_fm_weight", "deep_fm_bias") if fm else ("deep_res", "deep_res_bias")
+        Wfm = P[hw][:, 0].astype(F64)       # the head's L2 term (deepfm_pipeline.py:167, dnn_pipeline.py)
+        self.dense = {hw: ((feats.T @ dzg + l2 * Wfm)[:, None],
+                           (np.abs(feats).T @ np.abs(dzg) + l2 * np.abs(Wfm))[:, None]),
+                      hb: (np.array([dzg.sum()]).reshape(P[hb].shape),
+                           np.array([np.abs(dzg).sum()]).reshape(P[hb].shape))}
         for i in range(L):
             self.dense["deep_%d" % i] = (X[i].T @ G[i], np.abs(X[i]).T @ np.abs(G[i]))
             self.dense["deep_bias_%d" % i] = (G[i].sum(0, keepdims=True), np.abs(G[i]).sum(0, keepdims=True))
-        dsec = np.outer(dzg, Wh[nF:nF + E])
-        dfirst = np.outer(dzg, Wh[:nF])
+        dsec = np.outer(dzg, Wh[nF:nF + E]) if fm else None
+        dfirst = np.outer(dzg, Wh[:nF]) if fm else None
         self.ref = dict(idx=idx, val=val, nI=nI, single=single, multi=multi, e=e, ea=ea, fs=fs, sa=sa, dsec=dsec,
                         dfirst=dfirst, dx0=dx0g, cnt=gpu.get("cnt_emb"), cnt1=gpu.get("cnt_first"))
 
@@ -236,6 +246,9 @@ class StepAudit:
         if first:
             t = r["dfirst"][:, :nI] * val
             add(idx, t[..., None], np.abs(t)[..., None])
+        elif not self.fm:                                          # DNN: the deep lookups only
+            dx = r["dx0"][:, :S * E].reshape(B, S, E)
+            add(r["single"], dx, np.abs(dx))
         else:
             de = r["dsec"][:, None, :] * (r["fs"][:, None, :] - r["e"][:, :nI]) * val[..., None]
             dea = np.abs(r["dsec"])[:, None, :] * (r["sa"][:, None, :] + r["ea"][:, :nI]) * np.abs(val)[..., None]
@@ -252,8 +265,8 @@ class StepAudit:
                 add(ids, np.repeat(g[:, None], Lm, 1)[..., None], np.repeat(np.abs(g)[:, None], Lm, 1)[..., None])
                 continue
             n = r["cnt"][:, m][:, None]
-            fm = r["dsec"] * (r["fs"] - r["e"][:, j])
-            fma = np.abs(r["dsec"]) * (r["sa"] + r["ea"][:, j])
+            fm = r["dsec"] * (r["fs"] - r["e"][:, j]) if self.fm else 0
+            fma = np.abs(r["dsec"]) * (r["sa"] + r["ea"][:, j]) if self.fm else 0
             dp = r["dx0"][:, (S + m) * E:(S + m + 1) * E]
             g = np.where(n > 0, (dp + fm) / np.where(n > 0, n, 1), 0)
             ga = np.where(n > 0, (np.abs(dp) + fma) / np.where(n > 0, n, 1), 0)

@@ -16,6 +16,8 @@ CASES = {
     "deepfm_multi_cate": (dict(C=0, V=0, S=6, E=16, cate_index_size=3000, hidden=[48, 32],
                                multi_ranges=[[0, 20, "a"], [20, 50, "b"]]),
                           dict(cont=0, cate_fields=6, multi_slots=2, multi_width=25, cate_only=True)),
+    "dnn_pipeline": (dict(C=13, V=0, S=26, E=8, cate_index_size=4000, hidden=[96, 48, 32]),
+                     dict(cont=13, cate_fields=26)),
 }
 
 
@@ -24,12 +26,18 @@ def _oracle_mid(cfg, P, fw, trace, dz):
     S, E, M = cfg.S, cfg.E, len(cfg.multi_ranges)
     col = cfg.C + cfg.V
     W0 = P["deep_0"][col:col + (S + M) * E]
+    B = fw["z"].shape[0]
+    fm = R.is_fm(cfg)
     d = dict(x0=fw["x0"], h=fw["hs"], dh=[trace["g"][i] for i in range(len(cfg.hidden))],
              dx0=(trace["g"][0] @ W0.T).astype(np.float32), z=fw["z"], dz=dz,
-             fm_out=np.concatenate([fw["first"], fw["second"]], 1), fm_sum=fw["s"],
-             w_head=np.concatenate([P["deep_fm_weight"][:, 0], P["deep_fm_bias"]]))
+             fm_out=np.concatenate([fw["first"], fw["second"]], 1) if fm else np.zeros((B, 0), np.float32),
+             fm_sum=fw["s"] if fm else np.zeros((B, E), np.float32),
+             w_head=np.concatenate([P["deep_fm_weight"][:, 0], P["deep_fm_bias"]]) if fm else
+             np.concatenate([P["deep_res"][:, 0], P["deep_res_bias"].reshape(-1)]))
     if M:
-        d["cnt_emb"], d["cnt_first"] = fw["cnt_emb"], fw["cnt_first"]
+        d["cnt_emb"] = fw["cnt_emb"]
+        if fm:
+            d["cnt_first"] = fw["cnt_first"]
     return d
 
 

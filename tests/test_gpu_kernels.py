@@ -186,13 +186,14 @@ def _s3_kpos(k, K):
     return (k & ~31) | (8 * (kk >> 2) + (kk & 3) if kk < 16 else 8 * ((kk - 16) >> 2) + 4 + (kk & 3))
 
 
+@pytest.mark.parametrize("ldc_pad", [3, 4])   # ldc % 4 == 0 (pad 4, N % 4 == 0): the register epilogue
 @pytest.mark.parametrize("epi", [0, 1, 2])
 @pytest.mark.parametrize("M,N,K", [(65536, 400, 432), (300, 400, 416), (257, 416, 400), (1000, 80, 64),
                                    (513, 16, 8), (100, 213, 40)])
-def test_gemm_s3_nt_matches_fp64(hip_lib, epi, M, N, K):
+def test_gemm_s3_nt_matches_fp64(hip_lib, epi, M, N, K, ldc_pad):
     """C = A . B^T (+ ReLU / ReluGrad mask) on the three-plane split, against fp64: the same
     2e-6 relative bound as the f32 kernel; columns past N untouched."""
-    if M == 65536 and epi == 2:
+    if M == 65536 and (epi == 2 or ldc_pad == 3):
         pytest.skip("one full-size case per epilogue pair is enough")
     g = torch.Generator().manual_seed(M + 3 * N + K + epi)
     lda = K + 4
@@ -209,7 +210,7 @@ def test_gemm_s3_nt_matches_fp64(hip_lib, epi, M, N, K):
     Ad, mk = A.cuda(), mask.cuda()
     Bp = _planes(Bm.cuda(), False)     # B given as [N][K]: planes with ld K
     ldb = K
-    ldc = N + 3
+    ldc = N + ldc_pad
     C = torch.full((M, ldc), 7.0, device="cuda")
     call("dl_gemm_s3_nt", M, N, K, ptr(Ad), lda, ptr(Bp), ldb, N * K, ptr(C), ldc, epi,
          ptr(mk) if epi == 2 else None, N + 5, _s())
@@ -219,8 +220,9 @@ def test_gemm_s3_nt_matches_fp64(hip_lib, epi, M, N, K):
     assert (C[:, N:].cpu() == 7.0).all()
 
 
-@pytest.mark.parametrize("M,N,K", [(65536, 400, 416), (300, 400, 416), (257, 213, 40), (513, 16, 8)])
-def test_gemm_s3_relu_bitmask_round_trip(hip_lib, M, N, K):
+@pytest.mark.parametrize("aligned", [False, True])
+@pytest.mark.parametrize("M,N,K", [(65536, 400, 416), (300, 400, 416), (257, 213, 40), (513, 16, 8), (77, 48, 72)])
+def test_gemm_s3_relu_bitmask_round_trip(hip_lib, M, N, K, aligned):
     """dl_gemm_s3_nt_bits: the ReLU forward writes bit (c & 15) of halfword [i][c >> 4] =
     (h[i][c] > 0) (checked against the f32 output it writes beside it, every bit of every
     row, padding halfwords untouched), and the bitmask ReluGrad epilogue (epi 3) gives exactly
@@ -229,7 +231,9 @@ def test_gemm_s3_relu_bitmask_round_trip(hip_lib, M, N, K):
     A = torch.randn(M, K + 4, generator=g).cuda()
     Bm = (torch.randn(N, K, generator=g) * 0.05).cuda()
     Bp = _planes(Bm, False)
-    ldc, ldb16 = N + 3, (N + 15) // 16 + 2
+    # aligned: ldc % 4 == 0 and an even ldbits (the engine's layout: 32 halfwords a row), which
+    # selects the register epilogue (DIRECT) wherever N % 4 == 0; else the LDS epilogue
+    ldc, ldb16 = (N + 4, 32) if aligned else (N + 3, (N + 15) // 16 + 2)
     h = torch.full((M, ldc), 7.0, device="cuda")
     bits = torch.full((M, ldb16), -1, dtype=torch.int16, device="cuda")
     call("dl_gemm_s3_nt_bits", M, N, K, ptr(A), K + 4, ptr(Bp), K, N * K, ptr(h), ldc, 1, None, 0,

@@ -106,13 +106,16 @@ def test_train_steps_match_oracle(hip_lib, name, B, bwd):
 def test_dnn_pipeline_c1_defaults_same_state(hip_lib, B, adam):
     """BASELINE config C1 at the reference's own defaults: dnn_pipeline, 13 dense + 26 cate over
     a 10k vocab, embedding 8, hidden [512, 256, 128] (local_run.py:28-35), batch 256 (configs[0])
-    and 1,024 (local_run.py:35).  At these widths two correct f32 evaluation orders drift apart
-    along a never re-synced trajectory (elements whose summed gradient is within rounding of zero
-    take Adam's sign-saturated step either way), so every step is checked from the GPU's own
-    state (the full-size tests' same-state track): the oracle takes the GPU's exported
-    parameters and Adam moments, then the f32 TF1 step — every logit and the loss within 1e-5,
-    every parameter element within 1e-5 except at most 1e-3 of an array, each within the flip
-    bound 2 (1 - b1) / sqrt(1 - b2) alpha."""
+    and 1,024 (local_run.py:35).  Every step is checked from the GPU's own state (the full-size
+    tests' same-state track): the oracle takes the GPU's exported parameters and Adam moments,
+    then the f32 TF1 step — every logit and the loss within 1e-5; every stage of the GPU's step
+    against fp64 of its own inputs (tests/_fp64_audit.py); every parameter element within 1e-5 or
+    else audited in fp64 (the gradient the GPU applied, from its moments, against the fp64 sum of
+    its own terms within that sum's f32 bound, and TF1 Adam on it).  At these widths the f32
+    oracle's own ReLU decisions near zero differ from the GPU's for a few units a step, and each
+    such unit moves a whole column of W_0's gradient: a count bar on the elements off by more than
+    1e-5 would measure the oracle's conditioning, not the GPU's step."""
+    from tests import _fp64_audit as A
     kw = dict(C=13, V=0, S=26, E=8, cate_index_size=10000, hidden=[512, 256, 128])
     cfg = R.make_cfg("dnn_pipeline", **kw)
     P = R.init_params(cfg, np.random.default_rng(42))
@@ -121,14 +124,17 @@ def test_dnn_pipeline_c1_defaults_same_state(hip_lib, B, adam):
     opt = R.AdamTF1(cfg, P)
     tk = eng.spec.table_key
     flip = (1 - 0.9) / np.sqrt(1 - 0.999)
-    worst = 0.0
+    worst, audited = 0.0, 0
+    fails = []
     for step, b in enumerate(_batches("dnn_pipeline", kw, B, 6)):
         # the oracle from the GPU's state: parameters and both moments
         gp = eng.params()
         ds, st = eng.dense_state(), eng.adam_state()
+        m0 = {k: (st["m"].reshape(P[k].shape) if k == tk else ds["m"][k]) for k in gp}
+        v0 = {k: (st["v"].reshape(P[k].shape) if k == tk else ds["v"][k]) for k in gp}
         Ps = {k: v.copy() for k, v in gp.items()}
-        opt.m = {k: (st["m"].reshape(P[k].shape) if k == tk else ds["m"][k]).copy() for k in gp}
-        opt.v = {k: (st["v"].reshape(P[k].shape) if k == tk else ds["v"][k]).copy() for k in gp}
+        opt.m = {k: v.copy() for k, v in m0.items()}
+        opt.v = {k: v.copy() for k, v in v0.items()}
         alpha = float(opt.alpha())
         fw = R.train_step(cfg, Ps, opt, b)
         eng.train_step(b, graph=(step >= 2))
@@ -137,12 +143,30 @@ def test_dnn_pipeline_c1_defaults_same_state(hip_lib, B, adam):
         worst = max(worst, float(np.abs(z - fw["z"]).max()))
         np.testing.assert_allclose(z, fw["z"], atol=TOL, rtol=0, err_msg="logits step %d" % step)
         assert abs(eng.loss() - fw["loss"]) < TOL
+        audit = A.StepAudit(cfg, gp, b, A.read_gpu(eng, B))
+        fails += ["step %d: %s" % (step, f) for f in audit.fails]
         got = eng.params()
+        ds1, st1 = eng.dense_state(), eng.adam_state()
+        m1 = {k: (st1["m"].reshape(P[k].shape) if k == tk else ds1["m"][k]) for k in gp}
+        v1 = {k: (st1["v"].reshape(P[k].shape) if k == tk else ds1["v"][k]) for k in gp}
         for k in Ps:
             d = np.abs(got[k].astype(np.float64) - Ps[k])
-            assert (d > TOL).sum() <= max(1, 1e-3 * d.size) and d.max() <= 2 * flip * alpha + TOL, (
-                k, step, int((d > TOL).sum()), float(d.max()))
-    _stat("c1 defaults B=%d %s" % (B, adam), z_max_err=worst)
+            assert d.max() <= 2 * flip * alpha + TOL, (k, step, float(d.max()))
+            idx = np.flatnonzero(d.reshape(-1) > TOL)
+            if not len(idx):
+                continue
+            fl = lambda a: np.asarray(a).reshape(-1)[idx]
+            ok, st_, (g, G64, S) = A.audit_elements(audit, k, idx, P[k].shape, fl(m0[k]), fl(m1[k]), fl(v0[k]),
+                                                    fl(v1[k]), fl(gp[k]), fl(got[k]), alpha, cfg.beta1, cfg.beta2,
+                                                    cfg.eps)
+            audited = max(audited, len(idx))
+            _stat("c1 defaults B=%d %s step %d %s audited" % (B, adam, step, k), **st_)
+            if not ok.all():
+                j = int(np.flatnonzero(~ok)[0])
+                fails.append("step %d %s: %d of %d audited elements fail (e.g. flat %d: GPU gradient %r, fp64 %r, "
+                             "scale %r)" % (step, k, (~ok).sum(), len(idx), idx[j], g[j], G64[j], S[j]))
+    assert not fails, fails[:8]
+    _stat("c1 defaults B=%d %s" % (B, adam), z_max_err=worst, audited_max=audited)
 
 
 def test_graph_replay_equals_eager(hip_lib):
