@@ -183,6 +183,34 @@ def test_graph_replay_equals_eager(hip_lib):
     np.testing.assert_allclose(res[0], res[1], atol=1e-6)
 
 
+def test_opt_restore_mid_process_keeps_status_ring(hip_lib):
+    """A checkpoint's optimizer block restored into an engine that has already trained
+    (_ctr_model.py _restore -> set_opt): the status ring's step sequence stays the device's, so
+    the next steps report on time — no 10-s resynchronisation stall — and train exactly as an
+    engine given the same state from the start."""
+    import time
+    kw = CASES["deepfm_pipeline"]
+    spec = ModelSpec("deepfm_pipeline", **kw)
+    bs = _batches("deepfm_pipeline", kw, 512, 8)
+    eng = CTREngine(spec, max_batch=512, seed=5, adam="lazy")
+    assert eng._ring is not None
+    for b in bs[:3]:
+        eng.train_step(b, graph=True)
+    torch.cuda.synchronize()
+    saved = eng.opt.clone()
+    for b in bs[3:5]:
+        eng.train_step(b, graph=True)
+    eng.set_opt(saved)
+    t0 = time.perf_counter()
+    for b in bs[5:]:
+        eng.train_step(b, graph=True)
+    torch.cuda.synchronize()
+    eng.check_error()
+    assert time.perf_counter() - t0 < 5.0
+    assert eng.host_wait < 5.0
+    assert np.isfinite(eng.z[:512].cpu().numpy()).all()
+
+
 @pytest.mark.parametrize("stash", [False, True])
 # (multi-hot models are left out: the dense engine adds pooled gradients with atomics, whose
 # order varies, while the record path sums every row's references in a fixed order)
