@@ -29,6 +29,15 @@ class EmbLayout(C.Structure):
     ]
 
 
+class AdamLayer(C.Structure):
+    """Mirror of ``dl_adam_layer`` (include/dlamd.h)."""
+    _fields_ = [
+        ("p", C.c_void_p), ("m", C.c_void_p), ("v", C.c_void_p), ("slab", C.c_void_p), ("slab_stride", C.c_int64),
+        ("reg_count", C.c_int64), ("acc_out", C.c_void_p), ("wp", C.c_void_p), ("wtp", C.c_void_p),
+        ("nslab", C.c_int32), ("rows", C.c_int32), ("cols", C.c_int32), ("reg_kind", C.c_int32), ("reg", C.c_float),
+        ("pad_", C.c_int32)]
+
+
 class PoolDesc(C.Structure):
     """Mirror of ``dl_pool_desc`` (include/dlamd.h)."""
     _fields_ = [
@@ -101,6 +110,7 @@ SIGNATURES = {
     "dl_adam_dense": (I32, [P, P, P, P, I32, I64, I64, F, I64, P, P, P, P]),
     "dl_adam_dense_split3": (I32, [P, P, P, P, I32, I64, I32, I32, F, I64, I32, P, P, P, P, P]),
     "dl_adam_dense_bf16": (I32, [P, P, P, P, I32, I64, I32, I32, F, I64, I32, P, P, P, P, P]),
+    "dl_adam_dense_layers": (I32, [I32, P, I32, P, P]),
     "dl_adam_dense_reg": (I32, [P, P, P, P, I32, I64, I64, F, I64, I32, P, P, P, P]),
     "dl_adam_rows": (I32, [P, P, P, P, P, I64, I32, F, I32, P, P, P]),
     "dl_init_random": (I32, [P, I64, I32, F, F, U64, U64, P]),

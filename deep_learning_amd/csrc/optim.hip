@@ -229,6 +229,78 @@ __global__ __launch_bounds__(256) void adam_dense_thread_kernel(float* __restric
   if (sq_out) block_atomic_add(sq, sq_out);
 }
 
+// Several tower weights in one launch (dl_adam_dense_layers): thread i of the concatenated
+// element ranges runs adam_dense_thread_kernel's per-element code for its layer.
+struct AdamLayersArg {
+  dl_adam_layer l[DL_ADAM_MAX_LAYERS];
+  long long start[DL_ADAM_MAX_LAYERS + 1];   // element offsets of the layers in the concatenation
+  int nl;
+};
+
+template <int NPL>
+__global__ __launch_bounds__(256) void adam_dense_layers_kernel(AdamLayersArg a, const float* __restrict__ opt) {
+  if (step_poisoned(opt)) return;
+  const float alpha = opt[3], omb1 = 1.f - opt[4], omb2 = 1.f - opt[5], eps = opt[6];
+  float sq[DL_ADAM_MAX_LAYERS] = {0.f, 0.f, 0.f, 0.f};
+  const long long total = a.start[a.nl];
+  for (long long gi = (long long)blockIdx.x * blockDim.x + threadIdx.x; gi < total;
+       gi += (long long)gridDim.x * blockDim.x) {
+    int k = 0;
+#pragma unroll
+    for (int j = 1; j < DL_ADAM_MAX_LAYERS; ++j) k += (j < a.nl && gi >= a.start[j]) ? 1 : 0;
+    const dl_adam_layer& L = a.l[k];
+    const long long i = gi - a.start[k];
+    const float* __restrict__ slab = L.slab;
+    const long long stride = L.slab_stride;
+    const int nslab = L.nslab;
+    float g = 0.f;
+    int s = 0;
+    for (; s + 32 <= nslab; s += 32) {
+      float t[32];
+#pragma unroll
+      for (int j = 0; j < 32; ++j) t[j] = slab[(s + j) * stride + i];
+#pragma unroll
+      for (int j = 0; j < 32; ++j) g += t[j];
+    }
+    for (; s + 16 <= nslab; s += 16) {
+      float t[16];
+#pragma unroll
+      for (int j = 0; j < 16; ++j) t[j] = slab[(s + j) * stride + i];
+#pragma unroll
+      for (int j = 0; j < 16; ++j) g += t[j];
+    }
+    for (; s < nslab; ++s) g += slab[s * stride + i];
+    float pi = L.p[i], mi = L.m[i], vi = L.v[i];
+    if (i < L.reg_count) {
+      if (L.reg_kind == 0) { g += L.reg * pi; sq[k] += pi * pi; }
+      else { g += L.reg * (pi > 0.f ? 1.f : pi < 0.f ? -1.f : 0.f); sq[k] += fabsf(pi); }
+    }
+    adam_elem(pi, mi, vi, g, alpha, omb1, omb2, eps);
+    L.p[i] = pi; L.m[i] = mi; L.v[i] = vi;
+    unsigned short* wp = reinterpret_cast<unsigned short*>(L.wp);
+    unsigned short* wtp = reinterpret_cast<unsigned short*>(L.wtp);
+    const int r = (int)(i / L.cols), c = (int)(i - (long long)r * L.cols);
+    if (NPL == 3) {
+      const long long plane = (long long)L.rows * L.cols;
+      unsigned short h, mm, l;
+      split3_one(pi, h, mm, l);
+      const long long w = (long long)r * L.cols + s3_kpos(c, L.cols);   // dl_split3's layouts
+      wp[w] = h; wp[plane + w] = mm; wp[2 * plane + w] = l;
+      const long long t = (long long)c * L.rows + s3_kpos(r, L.rows);
+      wtp[t] = h; wtp[plane + t] = mm; wtp[2 * plane + t] = l;
+    } else if (NPL == 1) {
+      const unsigned short h = f2bf(pi);
+      wp[i] = h;
+      wtp[(long long)c * L.rows + r] = h;
+    }
+  }
+  for (int k = 0; k < a.nl; ++k)   // the regulariser terms (uniform branch: every thread joins)
+    if (a.l[k].acc_out) {
+      block_atomic_add(sq[k], a.l[k].acc_out);
+      __syncthreads();             // block_atomic_add's partials are reused by the next layer
+    }
+}
+
 // Few elements, many slabs (head weights): one wave per element.
 template <int REG>
 __global__ __launch_bounds__(256) void adam_dense_wave_kernel(float* __restrict__ p, float* __restrict__ m,
@@ -519,6 +591,32 @@ extern "C" int dl_adam_dense_split3(float* p, float* m, float* v, const float* s
                                     void* stream) {
   return adam_dense_copies<3>(p, m, v, slab, nslab, slab_stride, rows, cols, reg, reg_count, reg_kind, opt, acc_out,
                               wp, wtp, stream);
+}
+
+extern "C" int dl_adam_dense_layers(int32_t n_layers, const dl_adam_layer* layers, int32_t copies, const float* opt,
+                                    void* stream) {
+  DL_CHECK_ARG(n_layers >= 1 && n_layers <= DL_ADAM_MAX_LAYERS && layers && opt,
+               "n_layers %d: 1..%d and non-NULL arguments", n_layers, DL_ADAM_MAX_LAYERS);
+  DL_CHECK_ARG(copies == 3 || copies == 1, "copies %d: 3 (s3 planes) or 1 (bf16)", copies);
+  AdamLayersArg a{};
+  a.nl = n_layers;
+  long long off = 0;
+  for (int k = 0; k < n_layers; ++k) {
+    const dl_adam_layer& L = layers[k];
+    const long long n = (long long)L.rows * L.cols;
+    DL_CHECK_ARG(L.p && L.m && L.v && L.slab && L.wp && L.wtp, "layer %d: NULL pointer", k);
+    DL_CHECK_ARG(L.rows > 0 && L.cols > 0 && L.nslab >= 1 && L.slab_stride >= n, "layer %d: bad shape / slabs", k);
+    DL_CHECK_ARG(L.reg_kind == 0 || L.reg_kind == 1, "layer %d: reg_kind must be 0 (L2) or 1 (L1)", k);
+    a.l[k] = L;
+    a.start[k] = off;
+    off += n;
+  }
+  for (int k = n_layers; k <= DL_ADAM_MAX_LAYERS; ++k) a.start[k] = off;
+  if (copies == 3)
+    hipLaunchKernelGGL(adam_dense_layers_kernel<3>, dim3(grid_for(off)), dim3(256), 0, as_stream(stream), a, opt);
+  else
+    hipLaunchKernelGGL(adam_dense_layers_kernel<1>, dim3(grid_for(off)), dim3(256), 0, as_stream(stream), a, opt);
+  DL_RETURN_LAUNCH("dl_adam_dense_layers");
 }
 
 extern "C" int dl_adam_dense_bf16(float* p, float* m, float* v, const float* slab, int32_t nslab,

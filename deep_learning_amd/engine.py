@@ -416,7 +416,13 @@ class CTREngine:
         self.splits = max(1, min(int(os.environ.get("DLAMD_DW_SPLITS", dflt)), B // (512 if self.bf else 1024)))
         self.dw_splits = self._dw_splits(B, fixed="DLAMD_DW_SPLITS" in os.environ)
         # sized for the cap: a smaller batch may choose more splits than the largest one did
-        self.w_slab = z(max(self.splits * i * o for i, o in zip(self.in_ld, self.out_ld)))
+        # (one slab set per layer when the dense Adams run as one launch after the backward's
+        # GEMMs, _adam_fused: each layer's slabs must survive until then)
+        per = [self.splits * i * o for i, o in zip(self.in_ld, self.out_ld)]
+        self.w_slab = z(sum(per) if self._adam_fused() else max(per))
+        offs = np.cumsum([0] + per)
+        self.w_slabs = [self.w_slab[offs[l]:offs[l + 1]] if self._adam_fused() else self.w_slab
+                        for l in range(len(per))]
         self.layout = self._layout(B)
         self.bwd_blocks = _lib.lib().dl_embed_bwd_grid(C_ref(self.layout))
         self.cont_slab = z(max(1, self.bwd_blocks * sp.C * (E + 1)))
@@ -1068,13 +1074,13 @@ class CTREngine:
                 # (transposing LDS reads inside the kernel: no X^T / dY^T copies)
                 xl = self.x0b if l == 0 else self.hb[l - 1]
                 self._c("gemm_dw_l%d" % l, "dl_gemm_bf16", 1, 0, self.in_ld[l], hdim, B, ptr(xl), self.in_ld[l],
-                        ptr(self.dhb[l]), self.h_ld[l], ptr(self.w_slab), self.out_ld[l], 0, 3, None, 0, splits,
+                        ptr(self.dhb[l]), self.h_ld[l], ptr(self.w_slabs[l]), self.out_ld[l], 0, 3, None, 0, splits,
                         stride, s)
             elif self.s3:   # dW = X^T dY (split-K slabs over the batch)
                 xin = self.x0 if l == 0 else self.h[l - 1]
                 i, o = self.in_ld[l], self.out_ld[l]
                 self._c("gemm_dw_l%d" % l, "dl_gemm_s3_tn", i, hdim, B, ptr(xin), i, ptr(self.dh[l]), self.h_ld[l],
-                        ptr(self.w_slab), o, splits, stride, s)
+                        ptr(self.w_slabs[l]), o, splits, stride, s)
             else:
                 xin = self.x0 if l == 0 else self.h[l - 1]
                 self._c("gemm_dw_l%d" % l, "dl_gemm_f32", 1, 0, self.in_ld[l], hdim, B, ptr(xin), self.in_ld[l],
@@ -1123,7 +1129,7 @@ class CTREngine:
             l2, l2n = (sp.l2, ([self.D0] + sp.hidden)[l] * self.out_ld[l]) if reg else (0.0, 0)
             if self.s3 or self.bf:   # the update writes the GEMM operand copies of W and W^T itself
                 self._c("adam_dense_l%d" % l, "dl_adam_dense_split3" if self.s3 else "dl_adam_dense_bf16", ptr(self.W[l]), ptr(self.Wm[l]), ptr(self.Wv[l]),
-                        ptr(self.w_slab), nsplit, stride, self.in_ld[l], self.out_ld[l], l2, l2n,
+                        ptr(self.w_slabs[l]), nsplit, stride, self.in_ld[l], self.out_ld[l], l2, l2n,
                         1 if reg == "l1" else 0, ptr(self.opt), ptr(self.opt[8:]) if reg else None,
                         ptr(self.Wp[l] if self.s3 else self.Wb[l]), ptr(self.WTp[l] if self.s3 else self.WbT[l]), s)
                 return
@@ -1132,12 +1138,38 @@ class CTREngine:
                     None, ptr(self.opt[8:]) if reg else None, s)
             self._refresh_wb(l, s)
 
-        for l in reversed(range(nl)):
-            dw(l)
-            dx(l)
-            adam(l)
+        if self._adam_fused():
+            # every layer's weight and input gradients, then one launch for the dense Adams (each
+            # layer's W planes are read by its dX first; nothing else reads W before the next step)
+            for l in reversed(range(nl)):
+                dw(l)
+                dx(l)
+            reg = sp.hidden_reg
+            lay = (_lib.AdamLayer * nl)()
+            for l in range(nl):
+                stride = self.in_ld[l] * self.out_ld[l]
+                l2, l2n = (sp.l2, ([self.D0] + sp.hidden)[l] * self.out_ld[l]) if reg else (0.0, 0)
+                lay[l] = _lib.AdamLayer(ptr(self.W[l]), ptr(self.Wm[l]), ptr(self.Wv[l]), ptr(self.w_slabs[l]), stride,
+                                        l2n, ptr(self.opt[8:]) if reg else None,
+                                        ptr(self.Wp[l] if self.s3 else self.Wb[l]),
+                                        ptr(self.WTp[l] if self.s3 else self.WbT[l]),
+                                        _num_splits(B, dws[l], 64), self.in_ld[l], self.out_ld[l],
+                                        1 if reg == "l1" else 0, l2, 0)
+            self._adam_lay = lay   # kept alive: a captured graph's kernel arguments were copied at launch
+            self._c("adam_dense", "dl_adam_dense_layers", nl, C_ref(lay), 3 if self.s3 else 1, ptr(self.opt), s)
+        else:
+            for l in reversed(range(nl)):
+                dw(l)
+                dx(l)
+                adam(l)
         if part == "all":
             self._train_back(B, s, L)
+
+    def _adam_fused(self):
+        """The tower's dense Adams as one launch (dl_adam_dense_layers) after the backward's GEMMs
+        (DLAMD_ADAM_FUSED=0: one launch per layer, after its input gradient)."""
+        return ((self.s3 or self.bf) and len(self.spec.hidden) <= 4 and type(self) is CTREngine
+                and os.environ.get("DLAMD_ADAM_FUSED", "1") != "0")
 
     def _train_back(self, B, s, L):
         sp = self.spec

@@ -450,6 +450,33 @@ int dl_adam_dense_bf16(float* p, float* m, float* v, const float* slab, int32_t 
 int dl_adam_dense(float* p, float* m, float* v, const float* slab, int32_t nslab,
                   int64_t slab_stride, int64_t n, float l2, int64_t l2_count, const float* opt,
                   float* p_prev, float* sq_out, void* stream);
+/* One tower weight's update for dl_adam_dense_layers: W [rows][cols] (p, m, v), its gradient as
+ * `nslab` partial slabs `slab_stride` floats apart, the regulariser (reg_kind 0 = L2, 1 = L1) on
+ * the first reg_count elements with its loss term added to *acc_out (may be NULL), and the
+ * operand copies wp / wtp the update writes (dl_adam_dense_split3 / dl_adam_dense_bf16). */
+typedef struct dl_adam_layer {
+  float* p;
+  float* m;
+  float* v;
+  const float* slab;
+  int64_t slab_stride;
+  int64_t reg_count;
+  float* acc_out;
+  uint16_t* wp;
+  uint16_t* wtp;
+  int32_t nslab;
+  int32_t rows, cols;
+  int32_t reg_kind;
+  float reg;
+  int32_t pad_;
+} dl_adam_layer;
+/* dl_adam_dense_layers: dl_adam_dense_split3 (copies = 3) or dl_adam_dense_bf16 (copies = 1) on
+ * up to DL_ADAM_MAX_LAYERS tower weights in one launch — the same per-element operations, so the
+ * same results as one launch per layer (the regulariser sums excepted: atomics in another
+ * grouping).  One launch instead of one per hidden layer at the end of the backward. */
+#define DL_ADAM_MAX_LAYERS 4
+int dl_adam_dense_layers(int32_t n_layers, const dl_adam_layer* layers, int32_t copies, const float* opt,
+                         void* stream);
 /* dl_adam_dense with the regulariser kind explicit: reg_kind 0 = L2 as above, 1 = L1
  * (tf.contrib.layers.l1_regularizer at models/dnn.py:88-90: g += reg * sign(p) for
  * i < reg_count, acc_out += |p_pre|). */

@@ -183,6 +183,31 @@ def test_graph_replay_equals_eager(hip_lib):
     np.testing.assert_allclose(res[0], res[1], atol=1e-6)
 
 
+@pytest.mark.parametrize("name,tower", [("deepfm_pipeline", "f32"), ("wdl", "bf16"), ("dnn_pipeline", "f32")])
+def test_fused_dense_adam_bit_identical(hip_lib, name, tower, monkeypatch):
+    """The tower's dense Adams as one launch after the backward's GEMMs (dl_adam_dense_layers)
+    against one launch per layer after its input gradient: the same per-element operations, so
+    parameters, moments and the GEMM operand copies the next steps read are bit-identical."""
+    kw = CASES[name]
+    spec = ModelSpec(name, tower=tower, **kw)
+    bs = _batches(name, kw, 512, 4)
+    res = []
+    for fused in ("0", "1"):
+        monkeypatch.setenv("DLAMD_ADAM_FUSED", fused)
+        eng = CTREngine(spec, max_batch=512, seed=5, adam="lazy")
+        assert eng._adam_fused() == (fused == "1")
+        for i, b in enumerate(bs):
+            eng.train_step(b, graph=i >= 1)
+        torch.cuda.synchronize()
+        res.append((eng.z[:512].cpu().numpy(), eng.params(), eng.dense_state()))
+    (z0, p0, d0), (z1, p1, d1) = res
+    assert np.array_equal(z0, z1)
+    for k in p0:
+        assert np.array_equal(p0[k], p1[k]), k
+    for k in d0["m"]:
+        assert np.array_equal(d0["m"][k], d1["m"][k]) and np.array_equal(d0["v"][k], d1["v"][k]), k
+
+
 def test_opt_restore_mid_process_keeps_status_ring(hip_lib):
     """A checkpoint's optimizer block restored into an engine that has already trained
     (_ctr_model.py _restore -> set_opt): the status ring's step sequence stays the device's, so
