@@ -20,10 +20,13 @@
 // Block -> tile mapping is XCD-aware: tiles that share the A rows are dealt to
 // blocks b, b+8, ... which the dispatcher places on one XCD (speed only).
 #include "common.h"
+#include <cstdlib>
 
 namespace dl {
 
 typedef float floatx4 __attribute__((ext_vector_type(4)));
+typedef unsigned int dl_u32x4_t __attribute__((__vector_size__(4 * sizeof(unsigned int))));
+typedef unsigned int dl_u32x2_t __attribute__((__vector_size__(2 * sizeof(unsigned int))));
 
 #ifndef DL_GEMM_BK
 #define DL_GEMM_BK 16   // k-slab per LDS stage of the f32 GEMM
@@ -742,7 +745,12 @@ __device__ __forceinline__ int bn_slot(int j, int kq) { return kq ^ ((j >> 2) & 
 // s_waitcnt vmcnt(n) (n < 64), other counters untouched
 #define DL_BN_VMCNT(n) __builtin_amdgcn_s_waitcnt(((n) & 0xF) | (((n) >> 4) << 14) | (0x7 << 4) | (0xF << 8))
 
-template <int EPI, bool CBF16>
+// DIRECT: the operands' roles swapped in each MFMA (the weight fragment as src A), so a lane's
+// accumulator holds four consecutive columns of one output row, and the epilogue stores them
+// straight from registers (8 B of bf16 or 16 B of f32 per lane and fragment; the ReluGrad mask's
+// four bf16 read the same way) instead of transposing each wave's tile through LDS (gemm_s3.hip's
+// register epilogue).  Needs N, ldc, ldm multiples of 4 (the host picks it then).
+template <int EPI, bool CBF16, bool DIRECT = false>
 __global__ __launch_bounds__(512) void gemm_bf16_nt_kernel(GemmParams p) {
   extern __shared__ __attribute__((aligned(16))) unsigned short lds[];   // [3 bufs][BN][32], then the epilogue
   const unsigned short* __restrict__ Bm = reinterpret_cast<const unsigned short*>(p.B);
@@ -824,8 +832,13 @@ __global__ __launch_bounds__(512) void gemm_bf16_nt_kernel(GemmParams p) {
     for (int f = 0; f < kBnNF; ++f) {
       if (f + PF < kBnNF) bb[(f + PF) % NB] = *reinterpret_cast<const shortx8*>(Bs + 512 * (f + PF));
       const shortx8 bv = bb[f % NB];
-      acc[0][f] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0, bv, acc[0][f], 0, 0, 0);
-      acc[1][f] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1, bv, acc[1][f], 0, 0, 0);
+      if (DIRECT) {
+        acc[0][f] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bv, a0, acc[0][f], 0, 0, 0);
+        acc[1][f] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bv, a1, acc[1][f], 0, 0, 0);
+      } else {
+        acc[0][f] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0, bv, acc[0][f], 0, 0, 0);
+        acc[1][f] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1, bv, acc[1][f], 0, 0, 0);
+      }
     }
     publish(c);
   };
@@ -836,6 +849,54 @@ __global__ __launch_bounds__(512) void gemm_bf16_nt_kernel(GemmParams p) {
   }
   if (c < KC) step(c, raA);
 
+  if constexpr (DIRECT) {
+    // lane (kq, cl): acc[a][f][j] = C[r0 + 16a + cl][j0 + 16f + 4kq + j]; stores and mask loads
+    // through buffer descriptors (pieces past M or N: offsets past the range, dropped / zeros)
+    constexpr int EB = CBF16 ? 2 : 4;
+    const auto c_rsrc = __builtin_amdgcn_make_buffer_rsrc(p.C, (short)0, p.M * p.ldc * EB, 0x00020000);
+    const auto m_rsrc = __builtin_amdgcn_make_buffer_rsrc((void*)p.mask, (short)0,
+                                                          EPI == EPI_MASK ? p.M * p.ldm * 2 : 0, 0x00020000);
+#pragma unroll
+    for (int a = 0; a < 2; ++a) {
+      const int row = r0 + 16 * a + cl;
+      // the ReluGrad mask's pieces of these 13 fragments first, all in flight together
+      uint2 mk[EPI == EPI_MASK ? kBnNF : 1];
+      if constexpr (EPI == EPI_MASK) {
+#pragma unroll
+        for (int f = 0; f < kBnNF; ++f) {
+          const int col = j0 + 16 * f + 4 * kq;
+          const uint32_t off = (row < p.M && col + 4 <= p.N) ? 2u * (uint32_t)(row * p.ldm + col) : 0x80000000u;
+          mk[f] = __builtin_bit_cast(uint2, __builtin_amdgcn_raw_buffer_load_b64(m_rsrc, (int)off, 0, 0));
+        }
+      }
+#pragma unroll
+      for (int f = 0; f < kBnNF; ++f) {
+        const int col = j0 + 16 * f + 4 * kq;
+        float x[4] = {acc[a][f][0], acc[a][f][1], acc[a][f][2], acc[a][f][3]};
+        if (EPI == EPI_RELU) {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) x[e] = fmaxf(x[e], 0.f);
+        }
+        if constexpr (EPI == EPI_MASK) {
+          const unsigned short mv[4] = {(unsigned short)(mk[f].x & 0xffffu), (unsigned short)(mk[f].x >> 16),
+                                        (unsigned short)(mk[f].y & 0xffffu), (unsigned short)(mk[f].y >> 16)};
+#pragma unroll
+          for (int e = 0; e < 4; ++e) x[e] = bf2f(mv[e]) > 0.f ? x[e] : 0.f;
+        }
+        const bool ok = row < p.M && col + 4 <= p.N;
+        const uint32_t off = ok ? (uint32_t)EB * (uint32_t)(row * p.ldc + col) : 0x80000000u;
+        if (CBF16)
+          __builtin_amdgcn_raw_buffer_store_b64(
+              __builtin_bit_cast(dl_u32x2_t, make_uint2(f2bf(x[0]) | ((unsigned)f2bf(x[1]) << 16),
+                                                        f2bf(x[2]) | ((unsigned)f2bf(x[3]) << 16))),
+              c_rsrc, (int)off, 0, 0);
+        else
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(dl_u32x4_t, make_float4(x[0], x[1], x[2], x[3])),
+                                                 c_rsrc, (int)off, 0, 0);
+      }
+    }
+    return;
+  }
   // Epilogue through LDS (free after the last barrier): per wave and half (rows 16h .. 16h + 15
   // of its 32) the 16 x 208 f32 tile is written from the MFMA layout, then each lane moves
   // whole row pieces (8 bf16 or 4 f32 = 16 B), ReLU / ReluGrad mask applied there.
@@ -919,6 +980,15 @@ __global__ __launch_bounds__(512) void gemm_bf16_nt_kernel(GemmParams p) {
 #define DL_BF16_NT 1   // forward / dX products on gemm_bf16_nt_kernel (0: the B-resident kernel)
 #endif
 
+// DL_BF16_DIRECT=0 in the environment: the LDS epilogue (A/B measurements)
+static bool bf16_direct_enabled() {
+  static const bool on = [] {
+    const char* e = getenv("DL_BF16_DIRECT");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
 // true if the streamed-weight kernel takes the product (and launches it)
 static bool launch_bf16_nt(const GemmParams& gp, int epi, bool cb, hipStream_t s) {
   if (!DL_BF16_NT || epi == EPI_SPLIT || gp.K < 8 || gp.K % 8 || gp.lda % 8 || gp.ldb % 8 || gp.lda < gp.K ||
@@ -926,7 +996,13 @@ static bool launch_bf16_nt(const GemmParams& gp, int epi, bool cb, hipStream_t s
       (reinterpret_cast<uintptr_t>(gp.B) & 15) || (long long)gp.M * gp.lda * 2 >= (1LL << 31))
     return false;
   const dim3 grid((unsigned)(ceil_div(gp.M, kBnBM) * ceil_div(gp.N, kBnBN))), block(512);
-#define DL_BNT(E_, C_) hipLaunchKernelGGL((gemm_bf16_nt_kernel<E_, C_>), grid, block, kBnLds, s, gp)
+  const bool direct = bf16_direct_enabled() && gp.N % 4 == 0 && gp.ldc % 4 == 0 &&
+                      (epi != EPI_MASK || gp.ldm % 4 == 0) && (long long)gp.M * gp.ldc * 4 < (1LL << 31);
+#define DL_BNT(E_, C_)                                                                                     \
+  do {                                                                                                     \
+    if (direct) hipLaunchKernelGGL((gemm_bf16_nt_kernel<E_, C_, true>), grid, block, kBnLds, s, gp);      \
+    else hipLaunchKernelGGL((gemm_bf16_nt_kernel<E_, C_>), grid, block, kBnLds, s, gp);                    \
+  } while (0)
   if (epi == EPI_STORE) {
     if (cb) DL_BNT(EPI_STORE, true); else DL_BNT(EPI_STORE, false);
   } else if (epi == EPI_RELU) {

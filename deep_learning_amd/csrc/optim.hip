@@ -195,14 +195,14 @@ __global__ __launch_bounds__(256) void adam_dense_thread_kernel(float* __restric
 #pragma unroll
       for (int j = 0; j < 32; ++j) g += a[j];
     }
-    for (; s + 16 <= nslab; s += 16) {
+    for (; s < nslab; s += 16) {   // the rest 16 at a time, loads past the last slab masked
       float a[16];
 #pragma unroll
-      for (int j = 0; j < 16; ++j) a[j] = slab[(s + j) * stride + i];
+      for (int j = 0; j < 16; ++j) a[j] = s + j < nslab ? slab[(s + j) * stride + i] : 0.f;
 #pragma unroll
-      for (int j = 0; j < 16; ++j) g += a[j];
+      for (int j = 0; j < 16; ++j)
+        if (s + j < nslab) g += a[j];
     }
-    for (; s < nslab; ++s) g += slab[s * stride + i];
     float pi = p[i], mi = m[i], vi = v[i];
     if (p_prev) p_prev[i] = pi;
     if (i < l2_count) {
@@ -262,14 +262,14 @@ __global__ __launch_bounds__(256) void adam_dense_layers_kernel(AdamLayersArg a,
 #pragma unroll
       for (int j = 0; j < 32; ++j) g += t[j];
     }
-    for (; s + 16 <= nslab; s += 16) {
+    for (; s < nslab; s += 16) {   // the rest 16 at a time, loads past the last slab masked
       float t[16];
 #pragma unroll
-      for (int j = 0; j < 16; ++j) t[j] = slab[(s + j) * stride + i];
+      for (int j = 0; j < 16; ++j) t[j] = s + j < nslab ? slab[(s + j) * stride + i] : 0.f;
 #pragma unroll
-      for (int j = 0; j < 16; ++j) g += t[j];
+      for (int j = 0; j < 16; ++j)
+        if (s + j < nslab) g += t[j];
     }
-    for (; s < nslab; ++s) g += slab[s * stride + i];
     float pi = L.p[i], mi = L.m[i], vi = L.v[i];
     if (i < L.reg_count) {
       if (L.reg_kind == 0) { g += L.reg * pi; sq[k] += pi * pi; }

@@ -191,14 +191,28 @@ __global__ __launch_bounds__(kRsThreads) void rs_rowscan(int32_t* __restrict__ c
   int32_t* row = counts + (long long)blockIdx.x * tiles;
   const int per = (tiles + kRsThreads - 1) / kRsThreads;
   const int a = threadIdx.x * per, b = min(tiles, a + per);
+  // a thread's run of counts read 16 at a time, all in flight together (a serial loop paid one
+  // memory round trip per count: C3's 16.6 k tiles a digit, 82 us a pass, profiles/r05p/)
   int s = 0;
-  for (int i = a; i < b; ++i) s += row[i];
+  for (int i0 = a; i0 < b; i0 += 16) {
+    int v[16];
+#pragma unroll
+    for (int j = 0; j < 16; ++j) v[j] = i0 + j < b ? row[i0 + j] : 0;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) s += v[j];
+  }
   int all;
   int run = rs_block_scan(s, wsum, &all);
-  for (int i = a; i < b; ++i) {
-    const int c = row[i];
-    row[i] = run;
-    run += c;
+  for (int i0 = a; i0 < b; i0 += 16) {
+    int v[16];
+#pragma unroll
+    for (int j = 0; j < 16; ++j) v[j] = i0 + j < b ? row[i0 + j] : 0;
+#pragma unroll
+    for (int j = 0; j < 16; ++j)
+      if (i0 + j < b) {
+        row[i0 + j] = run;
+        run += v[j];
+      }
   }
   if (threadIdx.x == 0) total[blockIdx.x] = all;
 }

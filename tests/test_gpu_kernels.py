@@ -731,7 +731,8 @@ def test_sort_unique_matches_numpy(hip_lib, n, distinct):
                                            (4100, 37, 200, 1, 0), (8192, 400, 416, 1, 0), (300, 209, 40, 2, 1),
                                            (777, 208, 8, 1, 1), (1000, 100, 1000, 2, 0), (257, 400, 432, 0, 1),
                                            (1000, 300, 72, 2, 0), (129, 416, 48, 1, 1), (65536, 416, 400, 0, 0)])
-def test_gemm_bf16_b_resident(hip_lib, M, N, K, epi, cbf):
+@pytest.mark.parametrize("ldc_pad", [3, 4])   # ldc % 4 == 0 (pad 4, N % 4 == 0): the register epilogue
+def test_gemm_bf16_b_resident(hip_lib, M, N, K, epi, cbf, ldc_pad):
     """The tall-skinny bf16 path (ta=0, tb=1: the streamed-weight kernel gemm_bf16_nt_kernel,
     the B-resident kernel where it declines): relu / ReluGrad-mask / store epilogues, bf16 or
     f32 output, ragged M, N and K chunks (K past one chunk, not a multiple of 32, beyond the
@@ -749,7 +750,7 @@ def test_gemm_bf16_b_resident(hip_lib, M, N, K, epi, cbf):
         ref = ref.clamp(min=0)
     elif epi == 2:
         ref = torch.where(mask[:, :N].double() > 0, ref, torch.zeros_like(ref))
-    ldc = N + 3
+    ldc = N + ldc_pad
     C = torch.full((M, ldc), 5.0, device="cuda", dtype=torch.bfloat16 if cbf else torch.float32)
     md, Ad, Bd = mask.cuda(), A.cuda(), Bt.cuda()    # held for the launch (no freed temporaries)
     call("dl_gemm_bf16", 0, 1, M, N, K, ptr(Ad), lda, ptr(Bd), lda, ptr(C), ldc, cbf, epi,
