@@ -147,6 +147,25 @@ class LoadStyleModel:
         eng = self.model_optimizer()
         eng.loss_sum_begin()
         steps = 0
+        if os.environ.get("DLAMD_PINNED_FEED", "0") != "1":
+            # the next batch unpickled and staged (pageable host-to-device) on this thread while
+            # the current step runs.  (PinnedFeed, worker threads copying each unpickled batch
+            # into pinned buffers, measured 2.4 -> 6.8 ms a C5 step: the extra host copy of 31 MB
+            # a batch under the GIL-bound unpickling outweighs the faster transfer;
+            # profiles/r05t/bench_default.json, round 5)
+            items = iter(train_data)
+            b = next(items, None)
+            b = self.batch(b) if b is not None else None
+            while b is not None:
+                nxt = next(items, None)
+                nxt = self.batch(nxt) if nxt is not None else None
+                eng.train_step(b, graph=b["label"].shape[0] == eng.B, **({"next_batch": nxt} if nxt is not None else {}))
+                steps += 1
+                b = nxt
+            loss_sum, counted = eng.loss_sum_end()
+            if counted != steps:
+                eng.check_error()
+            return loss_sum, steps
         feed = PinnedFeed(self, train_data)
         try:
             items = iter(feed)
