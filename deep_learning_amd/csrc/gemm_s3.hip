@@ -22,6 +22,7 @@
 //       (8 waves x 32 rows x 13 column fragments).
 #include "common.h"
 #include <cstdlib>
+#include <type_traits>
 
 namespace dl {
 
@@ -188,11 +189,12 @@ __device__ __forceinline__ void nt_rd3(uint32_t a, shortx8& h, shortx8& m, short
 template <int EPI, bool DIRECT = false>
 __global__ __launch_bounds__(512) void gemm_s3_nt_kernel(S3Params p) {
   extern __shared__ __attribute__((aligned(16))) unsigned short lds[];   // [3 bufs][3 planes][BN][32]
+  constexpr int NW = 8, BM = kNtBM, DMAW = kNtDmaW;
   const unsigned short* __restrict__ Bp = reinterpret_cast<const unsigned short*>(p.B);
   const int tid = threadIdx.x, lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int ntm = (p.M + kNtBM - 1) / kNtBM, ntn = (p.N + kNtBN - 1) / kNtBN;
+  const int ntm = (p.M + BM - 1) / BM, ntn = (p.N + kNtBN - 1) / kNtBN;
   const int t = s3_xcd_tile(blockIdx.x, ntm * ntn);
-  const int i0 = (t / ntn) * kNtBM, j0 = (t % ntn) * kNtBN;
+  const int i0 = (t / ntn) * BM, j0 = (t % ntn) * kNtBN;
   const int cl = lane & 15, kq = lane >> 4;
   const int r0 = i0 + wid * 32;
   const bool ok0 = r0 + cl < p.M, ok1 = r0 + 16 + cl < p.M;
@@ -216,20 +218,26 @@ __global__ __launch_bounds__(512) void gemm_s3_nt_kernel(S3Params p) {
   // Every wave issues exactly kNtDmaW instructions (the last one clamped: wave 7 repeats
   // instruction kNtDma - 1, the same bytes to the same place), so the vmcnt bookkeeping below
   // is one straight-line count for every wave and the compiler's own waits can count too.
+  // Addressing: a scalar base per instruction (plane, first row of its 16) and one 32-bit
+  // lane offset per chunk (row within the 16, k piece) shared by all of a wave's instructions,
+  // so the prefetch holds one VGPR rather than a 64-bit address per instruction.
   auto dma_b = [&](int c, int buf) {
+    const uint32_t vk = 2u * (uint32_t)min(32 * c + 8 * nt_slot(lane >> 2, lane & 3), p.K - 8);
+    const uint32_t vrow = vk + 2u * (uint32_t)((lane >> 2) * p.ldb);
+    int lim = p.N - 1 - j0;   // opaque per call: the rows past N's offsets are not hoisted
+    asm volatile("" : "+s"(lim));
 #pragma unroll
-    for (int i = 0; i < kNtDmaW; ++i) {
-      const int g = min(wid + 8 * i, kNtDma - 1);
+    for (int i = 0; i < DMAW; ++i) {
+      const int g = min(wid + NW * i, kNtDma - 1);
       const int pl = g / 13, rb = 16 * (g % 13);
-      const int j = rb + (lane >> 2);
-      const int kpc = nt_slot(j, lane & 3);        // the piece that belongs in slot lane & 3
-      const int gj = min(j0 + j, p.N - 1);
-      const int gk = min(32 * c + 8 * kpc, p.K - 8);
-      const unsigned short* src = Bp + pl * p.b_plane + (long long)gj * p.ldb + gk;
+      const int rbase = j0 + min(rb, lim);
+      // rows past N read row N - 1 (their products are discarded)
+      const uint32_t voff = rb + 15 <= lim ? vrow : vk + 2u * (uint32_t)(min(lane >> 2, lim - min(rb, lim)) * p.ldb);
+      const unsigned short* sb = Bp + pl * p.b_plane + (long long)rbase * p.ldb;
       const uint32_t dst = lds_base + 2u * (uint32_t)(buf * kNtBuf + pl * kNtPlane + rb * 32);
       unsigned keep;
-      asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
-                   : "=&s"(keep) : "v"(src), "s"(__builtin_amdgcn_readfirstlane(dst)) : "memory");
+      asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2\n\ts_mov_b32 m0, %0"
+                   : "=&s"(keep) : "v"(voff), "s"(sb), "s"(__builtin_amdgcn_readfirstlane(dst)) : "memory");
     }
   };
   // A: this lane's 8 floats of rows r0 + cl, r0 + 16 + cl at k = 32c + 8kq
@@ -290,7 +298,7 @@ __global__ __launch_bounds__(512) void gemm_s3_nt_kernel(S3Params p) {
   // older than the one it just issued (vmcnt counts in issue order), which include its DMA of
   // the chunk the barrier publishes.
   auto publish = [&](int c) {           // chunk c + 1's weights -> every wave
-    if (c + 1 < KC) DL_WAIT_VMCNT(kNtDmaW + 4);   // every batch but chunk c + 2's: chunk c + 1's DMA too
+    if (c + 1 < KC) DL_WAIT_VMCNT(DMAW + 4);   // every batch but chunk c + 2's: chunk c + 1's DMA too
     else DL_WAIT_VMCNT(0);                // the epilogue reuses the ring: nothing may still land
 
     __builtin_amdgcn_s_waitcnt(0xc07f);   // lgkmcnt(0): this wave's fragment reads are done
@@ -909,6 +917,11 @@ __global__ __launch_bounds__(512) void gemm_s3_tn2_kernel(S3Params p) {
 #endif
 
 
+// SKIP: a wave whose row fragments lie past M (the last row tile: M = 400 leaves 1 of its 8
+// fragment rows in range, 432 leaves 3) skips their MFMAs and fragment reads, and the waves of
+// one fragment row sit on different SIMDs (wm = wid >> 1), so such a block costs about its
+// split work plus the valid rows' MFMAs instead of a full tile's.
+template <bool SKIP>
 __global__ __launch_bounds__(512) void gemm_s3_tn3_kernel(S3Params p) {
   extern __shared__ __attribute__((aligned(16))) unsigned short lds[];   // [2][3 A planes | 3 B planes]
   const int tid = threadIdx.x, lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -921,32 +934,35 @@ __global__ __launch_bounds__(512) void gemm_s3_tn3_kernel(S3Params p) {
   const auto xr = __builtin_amdgcn_make_buffer_rsrc((void*)p.A, (short)0, p.K * p.lda * 4, 0x00020000);
   const auto yr = __builtin_amdgcn_make_buffer_rsrc((void*)p.B, (short)0, p.K * p.ldb * 4, 0x00020000);
   int pr[kT2Q], pc[kT2Q];
-  bool pok[kT2Q];
 #pragma unroll
   for (int u = 0; u < kT2Q; ++u) {
     if (u < 2) {
       pr[u] = (tid >> 5) + 16 * u;
       pc[u] = 4 * (tid & 31);
-      pok[u] = m0 + pc[u] < p.M;
     } else {
       const int qb = tid + 512 * (u - 2);
       pr[u] = qb / (kT2BN / 4);
       pc[u] = 4 * (qb % (kT2BN / 4));
-      pok[u] = n0 + pc[u] < p.N && (u < 5 || tid < 256);
     }
   }
+  // Loads need no bounds selects: a piece past M / N (or one of the unused u = 5 pieces) only
+  // reaches rows / columns of C the epilogue discards, whatever it reads; a split's steps end at
+  // its kend (k_per_split is a multiple of the step) except the last split's, whose rows past K
+  // fall past the descriptor's range and read as zeros; loads for steps past nk are never
+  // stored.  So each piece's offset is a per-thread constant plus the step's (one add).
+  // (the host checks (K + 1) * ld * 4 < 2^31: no offset wraps into range)
+  uint32_t vo[kT2Q];
+#pragma unroll
+  for (int u = 0; u < kT2Q; ++u)
+    vo[u] = u < 2 ? 4u * (uint32_t)(pr[u] * p.lda + m0 + pc[u]) : 4u * (uint32_t)(pr[u] * p.ldb + n0 + pc[u]);
   auto load = [&](int k0, float4 (&rs)[kT2Q]) {
+    const uint32_t sa = 4u * (uint32_t)(k0 * p.lda), sb = 4u * (uint32_t)(k0 * p.ldb);
 #pragma unroll
     for (int u = 0; u < kT2Q; ++u) {
-      const int gk = k0 + pr[u];
-      const bool ok = pok[u] & (gk < kend);
-      if (u < 2) {
-        const uint32_t o = 4u * (uint32_t)(gk * p.lda + m0 + pc[u]);
-        rs[u] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(xr, (int)(ok ? o : 0x80000000u), 0, 0));
-      } else {
-        const uint32_t o = 4u * (uint32_t)(gk * p.ldb + n0 + pc[u]);
-        rs[u] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(yr, (int)(ok ? o : 0x80000000u), 0, 0));
-      }
+      if (u < 2)
+        rs[u] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(xr, (int)(vo[u] + sa), 0, 0));
+      else
+        rs[u] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(yr, (int)(vo[u] + sb), 0, 0));
     }
   };
   auto store_piece = [&](int buf, int u, const float4& r) {
@@ -968,13 +984,14 @@ __global__ __launch_bounds__(512) void gemm_s3_tn3_kernel(S3Params p) {
   for (int a = 0; a < 2; ++a)
 #pragma unroll
     for (int b = 0; b < kT2NF; ++b) acc[a][b] = floatx4{0.f, 0.f, 0.f, 0.f};
-  const int wm = wid & 3, wn = wid >> 2;
+  const int wm = SKIP ? wid >> 1 : wid & 3, wn = SKIP ? wid & 1 : wid >> 2;
   const int cl = lane & 15, kq = lane >> 4, rq = cl >> 2, cp = cl & 3;
   const int ra = 4 * kq + rq, rb = 16 + 4 * kq + rq;
+  // some row of this wave's fragments inside M (wave-uniform)
+  const bool live = __builtin_amdgcn_readfirstlane(m0 + 32 * wm) < p.M;
   // step kt from buffer kt & 1; `nx` (step kt + 1's tiles) split into buffer (kt + 1) & 1 piece by
   // piece between the fragment groups (skipped past the last step: nothing left to stage)
-  auto step = [&](int kt, const float4 (&nx)[kT2Q]) {
-    const int buf = kt & 1;
+  auto step = [&](int kt, int buf, const float4 (&nx)[kT2Q]) {   // buf == kt & 1, a literal at each call
     const bool more = kt + 1 < nk;
     const unsigned short* As = lds + buf * kT2Buf;
     const unsigned short* Bs = As + 3 * kT2AE;
@@ -1007,10 +1024,17 @@ __global__ __launch_bounds__(512) void gemm_s3_tn3_kernel(S3Params p) {
       if (b < kT2Q && more) store_piece(buf ^ 1, b, nx[b]);
     }
   };
+  // a wave whose rows all lie past M only stages its pieces (wave-uniform branch)
+  auto stage_only = [&](int kt, int buf, const float4 (&nx)[kT2Q]) {
+    if (kt + 1 < nk) {
+#pragma unroll
+      for (int u = 0; u < kT2Q; ++u) store_piece(buf ^ 1, u, nx[u]);
+    }
+  };
   float4 rA[kT2Q], rB[kT2Q];
   if (nk > 0) {
     load(kbeg, rA);
-    load(kbeg + kT2KS, rB);   // past kend: zeros (never stored)
+    load(kbeg + kT2KS, rB);   // past kend: never stored
 #pragma unroll
     for (int u = 0; u < kT2Q; ++u) store_piece(0, u, rA[u]);
   }
@@ -1020,17 +1044,30 @@ __global__ __launch_bounds__(512) void gemm_s3_tn3_kernel(S3Params p) {
   // (a bare s_barrier after lgkmcnt(0): __syncthreads' fence would also wait for the loads of
   // two steps ahead)
   int kt = 0;
-  for (; kt + 1 < nk; kt += 2) {
-    load(kbeg + (kt + 2) * kT2KS, rA);
-    step(kt, rB);
-    __builtin_amdgcn_s_waitcnt(0xc07f);
-    __builtin_amdgcn_s_barrier();
-    load(kbeg + (kt + 3) * kT2KS, rB);
-    step(kt + 1, rA);
-    __builtin_amdgcn_s_waitcnt(0xc07f);
-    __builtin_amdgcn_s_barrier();
+  if (!SKIP || live) {
+    for (; kt + 1 < nk; kt += 2) {
+      load(kbeg + (kt + 2) * kT2KS, rA);
+      step(kt, 0, rB);
+      __builtin_amdgcn_s_waitcnt(0xc07f);
+      __builtin_amdgcn_s_barrier();
+      load(kbeg + (kt + 3) * kT2KS, rB);
+      step(kt + 1, 1, rA);
+      __builtin_amdgcn_s_waitcnt(0xc07f);
+      __builtin_amdgcn_s_barrier();
+    }
+    if (kt < nk) step(kt, 0, rB);
+  } else {
+    for (; kt + 1 < nk; kt += 2) {
+      load(kbeg + (kt + 2) * kT2KS, rA);
+      stage_only(kt, 0, rB);
+      __builtin_amdgcn_s_waitcnt(0xc07f);
+      __builtin_amdgcn_s_barrier();
+      load(kbeg + (kt + 3) * kT2KS, rB);
+      stage_only(kt + 1, 1, rA);
+      __builtin_amdgcn_s_waitcnt(0xc07f);
+      __builtin_amdgcn_s_barrier();
+    }
   }
-  if (kt < nk) step(kt, rB);
   float* __restrict__ C = p.C + (long long)z * p.c_split_stride;
 #pragma unroll
   for (int a = 0; a < 2; ++a)
@@ -1079,6 +1116,15 @@ static bool s3_direct_enabled() {
   return on;
 }
 
+// DL_S3_TNSKIP=0: every wave of a TN block runs all its MFMAs (A/B measurements)
+static bool s3_tnskip_enabled() {
+  static const bool on = [] {
+    const char* e = getenv("DL_S3_TNSKIP");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
 extern "C" int dl_split3(const float* src, int32_t rows, int32_t cols, int32_t lds, int32_t transpose,
                          uint16_t* dst, int32_t ldd, int64_t plane_stride, void* stream) {
   DL_CHECK_ARG(src && dst, "NULL pointer");
@@ -1116,11 +1162,11 @@ extern "C" int dl_gemm_s3_nt_bits(int32_t M, int32_t N, int32_t K, const float* 
   p.A = A; p.B = Bp; p.C = C; p.mask = mask;
   p.M = M; p.N = N; p.K = K; p.lda = lda; p.ldb = ldb; p.ldc = ldc; p.ldm = ldm; p.b_plane = b_plane;
   p.bits = bits; p.ldbits = ldbits;
-  const int tiles = (int)(ceil_div(M, kNtBM) * ceil_div(N, kNtBN));
   hipStream_t s = as_stream(stream);
   const bool direct = s3_direct_enabled() && N % 4 == 0 && ldc % 4 == 0 && (!bits || ldbits % 2 == 0) &&
                       epi != S3_MASK && (long long)M * ldc * 4 < (1LL << 31) &&
                       (epi != S3_MASKBITS || ldbits >= 2 * ((((int)ceil_div(N, kNtBN) - 1) * kNtBN >> 5) + 7));
+  const int tiles = (int)(ceil_div(M, kNtBM) * ceil_div(N, kNtBN));
   if (direct) {
     if (epi == S3_STORE) hipLaunchKernelGGL((gemm_s3_nt_kernel<S3_STORE, true>), dim3(tiles), dim3(512), kNtLds, s, p);
     else if (epi == S3_RELU) hipLaunchKernelGGL((gemm_s3_nt_kernel<S3_RELU, true>), dim3(tiles), dim3(512), kNtLds, s, p);
@@ -1146,7 +1192,7 @@ extern "C" int dl_gemm_s3_tn(int32_t M, int32_t N, int32_t K, const float* X, in
   DL_CHECK_ARG(X && Y && C, "NULL operand");
   DL_CHECK_ARG(DL_S3_TN2 || N <= kTnBN, "N %d > %d", N, kTnBN);
   DL_CHECK_ARG(M % 4 == 0 && N % 4 == 0 && (M == 0 || M >= 4) && (N == 0 || N >= 4), "M, N must be multiples of 4");
-  DL_CHECK_ARG(!DL_S3_TN2 || ((long long)K * lda * 4 < (1LL << 31) && (long long)K * ldb * 4 < (1LL << 31)),
+  DL_CHECK_ARG(!DL_S3_TN2 || ((long long)(K + 1) * lda * 4 < (1LL << 31) && (long long)(K + 1) * ldb * 4 < (1LL << 31)),
                "X / Y past the 31-bit buffer range");
   DL_CHECK_ARG(lda % 4 == 0 && ldb % 4 == 0 && lda >= (M + 3) / 4 * 4 && ldb >= (N + 3) / 4 * 4 && ldc >= N,
                "bad leading dims");
@@ -1164,7 +1210,10 @@ extern "C" int dl_gemm_s3_tn(int32_t M, int32_t N, int32_t K, const float* X, in
   splits = (int)ceil_div(K > 0 ? K : 1, kps);
   if (DL_S3_TN2 && DL_S3_TN3) {
     const int tiles = (int)(ceil_div(M, kT2BM) * ceil_div(N, kT2BN));
-    hipLaunchKernelGGL(gemm_s3_tn3_kernel, dim3((unsigned)(tiles * splits)), dim3(512), kT2Lds, as_stream(stream), p);
+    if (s3_tnskip_enabled())
+      hipLaunchKernelGGL(gemm_s3_tn3_kernel<true>, dim3((unsigned)(tiles * splits)), dim3(512), kT2Lds, as_stream(stream), p);
+    else
+      hipLaunchKernelGGL(gemm_s3_tn3_kernel<false>, dim3((unsigned)(tiles * splits)), dim3(512), kT2Lds, as_stream(stream), p);
   } else if (DL_S3_TN2) {
     const int tiles = (int)(ceil_div(M, kT2BM) * ceil_div(N, kT2BN));
     hipLaunchKernelGGL(gemm_s3_tn2_kernel, dim3((unsigned)(tiles * splits)), dim3(512), kT2Lds, as_stream(stream), p);

@@ -45,6 +45,13 @@ print('$a', d['ms_per_step'], {n: k[n]['us'] for n in k if n.startswith('gemm')}
 import json,sys;d=json.loads(sys.stdin.read().strip().splitlines()[-1]);k=d['kernels']
 print('$var=$a $wl $dist', d['ms_per_step'], {n: k[n]['us'] for n in k})" >> $OUT/envab.txt
       done ;;
+    s3env_*)   # s3env_<VAR>: the s3 / GEMM kernel tests with VAR=1, then s3_bench VAR=0 / 1 / 0 / 1
+      var=${step#s3env_}
+      run ${var}_tests 600 env $var=1 $PYT tests/test_gpu_kernels.py -m gpu -k "s3"
+      for a in 0 1 0 1; do
+        run s3_${var}_$a 200 env $var=$a python scripts/s3_bench.py 20
+        grep -v amdgpu.ids $OUT/s3_${var}_$a.log | sed "s/^/[$var=$a] /" >> $OUT/s3_ab.txt
+      done ;;
     tests_*)   # tests_<pattern>: the GPU tests whose names match
       run tests_sel 900 $PYT tests -m gpu -k "${step#tests_}" ;;
     bench) run bench 900 python bench.py ;;

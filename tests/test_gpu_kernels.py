@@ -256,7 +256,8 @@ def test_gemm_s3_relu_bitmask_round_trip(hip_lib, M, N, K, aligned):
 
 
 @pytest.mark.parametrize("M,N,K,splits", [(432, 400, 65536, 64), (416, 400, 8192, 8), (428, 396, 5000, 3),
-                                            (64, 16, 100, 1), (16, 416, 4096, 16)])
+                                            (64, 16, 100, 1), (16, 416, 4096, 16), (400, 400, 8192, 8),
+                                            (404, 400, 2048, 2), (144, 400, 1024, 1)])
 def test_gemm_s3_tn_split_slabs(hip_lib, M, N, K, splits):
     """Weight gradients X^T . dY as split-K slabs (K chunks rounded to 64): slab sums against
     fp64, slabs past the used count untouched."""
