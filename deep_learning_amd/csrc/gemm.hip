@@ -753,11 +753,12 @@ __device__ __forceinline__ int bn_slot(int j, int kq) { return kq ^ ((j >> 2) & 
 template <int EPI, bool CBF16, bool DIRECT = false>
 __global__ __launch_bounds__(512) void gemm_bf16_nt_kernel(GemmParams p) {
   extern __shared__ __attribute__((aligned(16))) unsigned short lds[];   // [3 bufs][BN][32], then the epilogue
+  constexpr int NW = 8, BM = kBnBM, DMAW = kBnDmaW;
   const unsigned short* __restrict__ Bm = reinterpret_cast<const unsigned short*>(p.B);
   const int tid = threadIdx.x, lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int ntm = (p.M + kBnBM - 1) / kBnBM, ntn = (p.N + kBnBN - 1) / kBnBN;
+  const int ntm = (p.M + BM - 1) / BM, ntn = (p.N + kBnBN - 1) / kBnBN;
   const int t = xcd_tile(blockIdx.x, ntm * ntn);     // the column tiles of a row tile on one XCD: A from L2
-  const int i0 = (t / ntn) * kBnBM, j0 = (t % ntn) * kBnBN;
+  const int i0 = (t / ntn) * BM, j0 = (t % ntn) * kBnBN;
   const int cl = lane & 15, kq = lane >> 4;
   const int r0 = i0 + wid * 32;
   const bool ok0 = r0 + cl < p.M, ok1 = r0 + 16 + cl < p.M;
@@ -776,8 +777,8 @@ __global__ __launch_bounds__(512) void gemm_bf16_nt_kernel(GemmParams p) {
   // straight-line.
   auto dma_b = [&](int c, int buf) {
 #pragma unroll
-    for (int i = 0; i < kBnDmaW; ++i) {
-      const int g = min(wid + 8 * i, kBnDma - 1);
+    for (int i = 0; i < DMAW; ++i) {
+      const int g = min(wid + NW * i, kBnDma - 1);
       const int rb = 16 * g;
       const int j = rb + (lane >> 2);
       const int kpc = bn_slot(j, lane & 3);
@@ -810,7 +811,7 @@ __global__ __launch_bounds__(512) void gemm_bf16_nt_kernel(GemmParams p) {
   // chunk c + 1's weights -> every wave: wait for every batch but the newest (chunk c + 2's),
   // then a bare s_barrier (a __syncthreads would drain the prefetch: vmcnt(0))
   auto publish = [&](int c) {
-    if (c + 1 < KC) DL_BN_VMCNT(kBnDmaW + 2);
+    if (c + 1 < KC) DL_BN_VMCNT(DMAW + 2);
     else DL_BN_VMCNT(0);                  // the epilogue reuses the LDS: nothing may still land
     __builtin_amdgcn_s_waitcnt(0xc07f);   // lgkmcnt(0): this wave's fragment reads are done
     __builtin_amdgcn_s_barrier();
@@ -998,9 +999,12 @@ static bool launch_bf16_nt(const GemmParams& gp, int epi, bool cb, hipStream_t s
   const dim3 grid((unsigned)(ceil_div(gp.M, kBnBM) * ceil_div(gp.N, kBnBN))), block(512);
   const bool direct = bf16_direct_enabled() && gp.N % 4 == 0 && gp.ldc % 4 == 0 &&
                       (epi != EPI_MASK || gp.ldm % 4 == 0) && (long long)gp.M * gp.ldc * 4 < (1LL << 31);
+  // the register epilogue needs only the ring (39,936 B instead of the 108,544-B tiles), so other
+  // kernels' blocks (the side stream's index build) can share the CU
+  constexpr size_t ring = 3 * kBnPlane * sizeof(unsigned short);
 #define DL_BNT(E_, C_)                                                                                     \
   do {                                                                                                     \
-    if (direct) hipLaunchKernelGGL((gemm_bf16_nt_kernel<E_, C_, true>), grid, block, kBnLds, s, gp);      \
+    if (direct) hipLaunchKernelGGL((gemm_bf16_nt_kernel<E_, C_, true>), grid, block, ring, s, gp);   \
     else hipLaunchKernelGGL((gemm_bf16_nt_kernel<E_, C_>), grid, block, kBnLds, s, gp);                    \
   } while (0)
   if (epi == EPI_STORE) {
