@@ -1,5 +1,5 @@
 """Times the C5 bf16 tower's GEMM shapes through the C ABI (HIP events).
-python scripts/gemm_bf16_bench.py [reps]"""
+python scripts/gemm_bf16_bench.py [reps] [case substring]"""
 import sys
 
 import torch
@@ -9,6 +9,7 @@ from deep_learning_amd import _lib  # noqa: E402
 from deep_learning_amd._lib import call, ptr  # noqa: E402
 
 reps = int(sys.argv[1]) if len(sys.argv) > 1 else 20
+only = sys.argv[2] if len(sys.argv) > 2 else None   # run the cases whose names contain this (profiling)
 B = 65536
 s = _lib.stream_handle()
 bf = lambda *sh: torch.randn(*sh, device="cuda").to(torch.bfloat16)
@@ -41,6 +42,8 @@ cases = {
     "cast_bf16 [B,416]": (lambda: call("dl_cast_bf16", ptr(out_f), B, 416, 416, u16(out_b), 416, s), 0),
 }
 for name, (fn, fl) in cases.items():
+    if only and only not in name:
+        continue
     for _ in range(3):
         fn()
     torch.cuda.synchronize()

@@ -52,6 +52,11 @@ print('$var=$a $wl $dist', d['ms_per_step'], {n: k[n]['us'] for n in k})" >> $OU
         run s3_${var}_$a 200 env $var=$a python scripts/s3_bench.py 20
         grep -v amdgpu.ids $OUT/s3_${var}_$a.log | sed "s/^/[$var=$a] /" >> $OUT/s3_ab.txt
       done ;;
+    bf16pmc)   # counters of the C5 tower's bf16 NT products (gemm_bf16_bench cases)
+      run bf16pmc 600 bash scripts/pmc_bf16.sh $OUT/bf16pmc "fwd_l0 bf16 out relu" "dx_l1 mask bf16" &&
+      SQ_KERNEL=gemm_bf16 python scripts/sq_summary.py $OUT/bf16pmc $OUT/bf16_sq_counters.json \
+        fwd_l0_bf16_out_relu dx_l1_mask_bf16 > $OUT/bf16_sq.txt 2>&1
+      run bf16bench 200 python scripts/gemm_bf16_bench.py 20 ;;
     tests_*)   # tests_<pattern>: the GPU tests whose names match
       run tests_sel 900 $PYT tests -m gpu -k "${step#tests_}" ;;
     bench) run bench 900 python bench.py ;;

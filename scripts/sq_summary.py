@@ -1,5 +1,6 @@
 """SQ counter passes of scripts/pmc_s3.sh -> one JSON: per case, the s3 GEMM kernel's counters
-(mean over its dispatches).  python scripts/sq_summary.py <s3pmc dir> <out.json> case..."""
+(mean over its dispatches).  python scripts/sq_summary.py <s3pmc dir> <out.json> case...
+(SQ_KERNEL=<substring> in the environment picks another kernel than gemm_s3)"""
 import csv
 import glob
 import json
@@ -8,12 +9,13 @@ import sys
 from collections import defaultdict
 
 d, out, cases = sys.argv[1], sys.argv[2], sys.argv[3:]
+want = os.environ.get("SQ_KERNEL", "gemm_s3")
 res = {}
 for case in cases:
     acc, kern = defaultdict(list), None
     for f in sorted(glob.glob(os.path.join(d, case + "_pass*_counter_collection.csv"))):
         for row in csv.DictReader(open(f)):
-            if "gemm_s3" not in row["Kernel_Name"]:
+            if want not in row["Kernel_Name"]:
                 continue
             kern = row["Kernel_Name"]
             acc[(row["Counter_Name"], row["Dispatch_Id"])].append(float(row["Counter_Value"]))
