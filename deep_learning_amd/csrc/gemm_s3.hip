@@ -131,6 +131,12 @@ enum { S3_STORE = 0, S3_RELU = 1, S3_MASK = 2, S3_MASKBITS = 3 };
 #define DL_S3_ESPLIT 1   // NT: chunk c + 1's A planes split in the middle of chunk c's MFMAs
                          // (fwd_l1 114.7 -> 110.9 us alone, profiles/r05f/s3_ab.txt)
 #endif
+#ifndef DL_S3_ESASM
+#define DL_S3_ESASM 1   // early-split step: weight fragment reads as asm, DL_S3_ES_PF fragments ahead
+#endif
+#ifndef DL_S3_ES_PF
+#define DL_S3_ES_PF 2
+#endif
 
 #ifndef DL_S3_TNSTAG
 #define DL_S3_TNSTAG 0   // TN2: waves 4-7 split + store the next step's tiles BEFORE their MFMAs
@@ -336,12 +342,33 @@ __global__ __launch_bounds__(512) void gemm_s3_nt_kernel(S3Params p) {
         bl = *reinterpret_cast<const shortx8*>(&Bs[2 * kNtPlane + o]);
       };
       (void)b_addr;
-      shortx8 bb[2][3];
-      rd_b(0, bb[0][0], bb[0][1], bb[0][2]);
+      (void)rd_b;
+      // DL_S3_ESASM: each fragment's three plane reads as asm issued ES_PF fragments ahead, and an
+      // lgkmcnt wait tied to its registers right before its MFMAs (hipcc, left alone, issued
+      // each pair of fragments' reads just ahead of their MFMAs: the LDS latency in the MFMA
+      // stream once a pair); same operands, same order of products
+      constexpr int EPF = DL_S3_ESASM ? DL_S3_ES_PF : 1, ENB = EPF + 1;
+      shortx8 bb[ENB][3];
+#pragma unroll
+      for (int i = 0; i < EPF; ++i) {
+        if (DL_S3_ESASM) nt_rd3(b_addr + 1024u * i, bb[i][0], bb[i][1], bb[i][2]);
+        else rd_b(i, bb[i][0], bb[i][1], bb[i][2]);
+      }
 #pragma unroll
       for (int f = 0; f < kNtNF; ++f) {
-        if (f + 1 < kNtNF) rd_b(f + 1, bb[(f + 1) & 1][0], bb[(f + 1) & 1][1], bb[(f + 1) & 1][2]);
-        const shortx8 bh = bb[f & 1][0], bm = bb[f & 1][1], bl = bb[f & 1][2];
+        if (f + EPF < kNtNF) {
+          if (DL_S3_ESASM) nt_rd3(b_addr + 1024u * (f + EPF), bb[(f + EPF) % ENB][0], bb[(f + EPF) % ENB][1], bb[(f + EPF) % ENB][2]);
+          else rd_b(f + EPF, bb[(f + EPF) % ENB][0], bb[(f + EPF) % ENB][1], bb[(f + EPF) % ENB][2]);
+        }
+        if (DL_S3_ESASM) {
+          shortx8 &h = bb[f % ENB][0], &m = bb[f % ENB][1], &l = bb[f % ENB][2];
+          const int younger = min(EPF, kNtNF - 1 - f);   // fragments whose reads follow f's
+          if (younger >= 3) DL_LDS_WAIT(9, h, m, l);
+          else if (younger == 2) DL_LDS_WAIT(6, h, m, l);
+          else if (younger == 1) DL_LDS_WAIT(3, h, m, l);
+          else DL_LDS_WAIT(0, h, m, l);
+        }
+        const shortx8 bh = bb[f % ENB][0], bm = bb[f % ENB][1], bl = bb[f % ENB][2];
         if (DIRECT) {
           acc[0][f] = mfma_s3_t(P[0], P[1], P[2], bh, bm, bl, acc[0][f]);
           acc[1][f] = mfma_s3_t(P[3], P[4], P[5], bh, bm, bl, acc[1][f]);
