@@ -1,0 +1,44 @@
+"""The north-star lookup alone (C2 shape, B = 65,536, 26 M rows): dl_embed_fwd over the dense
+p / first-order planes of a flushed table, the kernel CTREngine.predict runs — nothing else
+launches embed_fwd_kernel here (no training step), so rocprofv3 PMC passes over this script
+count the lookup alone.  python scripts/lookup_bench.py [uniform|zipf] [reps]"""
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from deep_learning_amd import _lib  # noqa: E402
+from deep_learning_amd._lib import call, ptr  # noqa: E402
+from deep_learning_amd.engine import C_ref, CTREngine, ModelSpec  # noqa: E402
+from deep_learning_amd.synthetic import make_batch  # noqa: E402
+
+dist = sys.argv[1] if len(sys.argv) > 1 else "uniform"
+reps = int(sys.argv[2]) if len(sys.argv) > 2 else 20
+B, N = 65536, 26_000_000
+spec = ModelSpec("deepfm_pipeline", C=13, V=0, S=26, E=16, cate_index_size=N, hidden=[400, 400, 400])
+eng = CTREngine(spec, max_batch=B, seed=2019, adam="lazy")
+eng.flush(planes=True)
+b = {k: torch.from_numpy(v).cuda() for k, v in make_batch(B, cate_index_size=N, seed=4242, dist=dist).items()}
+eng.stage(b)
+FL = eng._flat_layout(B)
+s = _lib.stream_handle()
+x0 = eng.x0b if eng.x0_direct else eng.x0
+
+
+def run():
+    call("dl_embed_fwd", C_ref(FL), ptr(eng.p_plane), ptr(eng.w1_plane), ptr(eng.in_cate), ptr(eng.in_cont),
+         ptr(eng.in_vec), ptr(x0), ptr(eng.fm_out), ptr(eng.fm_sum), ptr(eng.err), s)
+
+
+run()
+torch.cuda.synchronize()
+e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+e0.record()
+for _ in range(reps):
+    run()
+e1.record()
+torch.cuda.synchronize()
+eng.check_error()
+us = e0.elapsed_time(e1) * 1e3 / reps
+print("lookup %s %.1f us  %.3f of 8 TB/s by the 3,640-B rule" % (dist, us, B * 3640 / us / 1e3 / 8000), flush=True)
