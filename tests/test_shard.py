@@ -1,4 +1,4 @@
-"""Multi-rank (world_size 2) tests of the row-sharded path.
+"""Multi-rank (world_size 2, 4 and 8) tests of the row-sharded path.
 
 CPU (gloo): the sharded algorithm restated in numpy over the real Exchange
 collectives equals single-process training on the global batch.
@@ -28,30 +28,31 @@ def _free_port():
     return p
 
 
-def _launch(mode, tmp_path):
+def _launch(mode, tmp_path, world=WORLD):
     env = dict(os.environ, MASTER_ADDR="127.0.0.1", OMP_NUM_THREADS="1")
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(WORLD),
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(world),
            "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
            os.path.join(ROOT, "tests", "shard_worker.py"), mode, str(STEPS), str(BL), str(tmp_path)]
     r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=600, cwd=ROOT)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
 
 
-def _oracle():
+def _oracle(world=WORLD):
     cfg = R.make_cfg("deepfm_pipeline", **KW)
     P = R.init_params(cfg, np.random.default_rng(42))
     opt = R.AdamTF1(cfg, P)
     zs = []
-    for b in global_batches(BL * WORLD, STEPS):
+    for b in global_batches(BL * world, STEPS):
         zs.append(R.train_step(cfg, P, opt, b)["z"])
     return P, zs
 
 
-def test_shard_sim_gloo_equals_global_batch(tmp_path):
-    _launch("sim", tmp_path)
-    P, zs = _oracle()
+@pytest.mark.parametrize("world", [2, 4])
+def test_shard_sim_gloo_equals_global_batch(tmp_path, world):
+    _launch("sim", tmp_path, world)
+    P, zs = _oracle(world)
     for step in range(STEPS):
-        z = np.concatenate([np.load(tmp_path / ("rank%d_step%d.npz" % (r, step)))["z"] for r in range(WORLD)])
+        z = np.concatenate([np.load(tmp_path / ("rank%d_step%d.npz" % (r, step)))["z"] for r in range(world)])
         np.testing.assert_allclose(z, zs[step], atol=1e-5, rtol=0, err_msg="step %d" % step)
     got = np.load(tmp_path / "rank0.npz")
     for k in P:
@@ -67,20 +68,35 @@ def test_sharded_engine_two_ranks_equals_global_batch(tmp_path, mode):
     sized below these batches' unique rows per owner, so the first step overflows on the device,
     every rank skips it and those after it, grows its blocks and replays them in order — the
     result must still be the oracle's."""
-    _launch(mode, tmp_path)
+    _check_engine(tmp_path, mode, WORLD)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world,mode", [(4, "gpu_lazy_pf"), (8, "gpu_lazy_pf"), (8, "gpu_lazy_ovf_pf")])
+def test_sharded_engine_many_ranks_equals_global_batch(tmp_path, world, mode):
+    """BASELINE C4's world (8 ranks, owner r % 8, 15 exchange blocks a rank, one header
+    consensus over 8 ranks), here 4 and 8 ranks sharing cuda:0 over the gloo-staged exchange:
+    every step's logits, the sharded table, the replicated state on every rank and the
+    all-gathered eval AUC equal the oracle trained on the global batch (8 x 96 samples); the
+    overflow case replays its skipped steps with grown blocks on all 8 ranks."""
+    _check_engine(tmp_path, mode, world)
+
+
+def _check_engine(tmp_path, mode, world):
+    _launch(mode, tmp_path, world)
     if "_ovf" in mode:
-        for r in range(WORLD):
+        for r in range(world):
             d = np.load(tmp_path / ("rank%d.npz" % r))
             assert int(d["overflows"]) >= 1 and d["cap"][1] > d["cap"][0], (int(d["overflows"]), d["cap"])
-    P, zs = _oracle()
+    P, zs = _oracle(world)
     for step in range(STEPS):
         if "_ovf" in mode and step < 2:   # skipped, then replayed by the call that read its report
             continue
-        z = np.concatenate([np.load(tmp_path / ("rank%d_step%d.npz" % (r, step)))["z"] for r in range(WORLD)])
+        z = np.concatenate([np.load(tmp_path / ("rank%d_step%d.npz" % (r, step)))["z"] for r in range(world)])
         np.testing.assert_allclose(z, zs[step], atol=1e-5, rtol=0, err_msg="logits step %d" % step)
     table = np.zeros_like(P["feats_emb"])
     first = np.zeros_like(P["fm_first_order_emb"][:, 0])
-    for r in range(WORLD):
+    for r in range(world):
         d = np.load(tmp_path / ("rank%d.npz" % r), allow_pickle=False)
         table[d["rows"]] = d["table"]
         first[d["rows"]] = d["first"]
@@ -89,14 +105,15 @@ def test_sharded_engine_two_ranks_equals_global_batch(tmp_path, mode):
     np.testing.assert_allclose(rep, P["feats_emb"][:C], atol=1e-5, rtol=0)
     np.testing.assert_allclose(table[C:], P["feats_emb"][C:], atol=1e-5, rtol=0)
     np.testing.assert_allclose(first[C:], P["fm_first_order_emb"][C:, 0], atol=1e-5, rtol=0)
-    d0, d1 = np.load(tmp_path / "rank0.npz"), np.load(tmp_path / "rank1.npz")
-    np.testing.assert_array_equal(d0["head"], d1["head"])       # replicated dense state identical
+    d0 = np.load(tmp_path / "rank0.npz")
+    for r in range(1, world):                                    # replicated dense state identical
+        np.testing.assert_array_equal(np.load(tmp_path / ("rank%d.npz" % r))["head"], d0["head"])
     # sharded eval: every rank's predictions of two unseen global batches equal the oracle's
     # forward on the trained parameters; the all-gathered AUC equals the oracle AUC of the
     # whole set (north star: AUC within 1e-4), identically on both ranks
     cfg = R.make_cfg("deepfm_pipeline", **KW)
-    ev = [np.load(tmp_path / ("rank%d_eval.npz" % r)) for r in range(WORLD)]
-    evb = global_batches(BL * WORLD, STEPS + 2)[STEPS:]
+    ev = [np.load(tmp_path / ("rank%d_eval.npz" % r)) for r in range(world)]
+    evb = global_batches(BL * world, STEPS + 2)[STEPS:]
     all_s, all_y = [], []
     for j, b in enumerate(evb):
         want = 1.0 / (1.0 + np.exp(-R.forward(cfg, P, b)["z"].astype(np.float64)))
@@ -105,7 +122,7 @@ def test_sharded_engine_two_ranks_equals_global_batch(tmp_path, mode):
         all_s.append(want)
         all_y.append(b["label"].reshape(-1))
     want_auc = R.auc(np.concatenate(all_y), np.concatenate(all_s))
-    assert float(ev[0]["auc"]) == float(ev[1]["auc"])
+    assert all(float(e["auc"]) == float(ev[0]["auc"]) for e in ev)
     assert abs(float(ev[0]["auc"]) - want_auc) < 1e-4
 
 
@@ -145,19 +162,30 @@ def test_sharded_wdl_two_ranks_equals_global_batch(tmp_path, mode):
     of wdl_weights (aliasing wide ids Fw..Fw+H) updated by their owners and re-broadcast.
     Against the fp32 oracle on the global batch: 1e-5 for the fp32 tower, the bf16 tower's
     stated tolerance (test_gpu_parity.py::test_wdl_bf16_tower_tracks_oracle) for bf16."""
-    _launch(mode, tmp_path)
+    _check_wdl(tmp_path, mode, WORLD)
+
+
+@pytest.mark.gpu
+def test_sharded_wdl_eight_ranks_equals_global_batch(tmp_path):
+    """C5 at BASELINE's 8 ranks (sharing cuda:0, gloo-staged): the lazy fp32 Wide&Deep step with
+    prefetch against the oracle on the global batch, as the two-rank test."""
+    _check_wdl(tmp_path, "gpu_wdl_lazy_pf", 8)
+
+
+def _check_wdl(tmp_path, mode, world):
+    _launch(mode, tmp_path, world)
     bf = "bf16" in mode
     ztol, ptol = (3e-2, 5e-3) if bf else (1e-5, 1e-5)
     cfg = R.make_cfg("wdl", **WKW)
     P = R.init_params(cfg, np.random.default_rng(42))
     opt = R.AdamTF1(cfg, P)
-    for step, b in enumerate(wdl_batches(BL * WORLD, STEPS)):
+    for step, b in enumerate(wdl_batches(BL * world, STEPS)):
         fw = R.train_step(cfg, P, opt, b)
-        z = np.concatenate([np.load(tmp_path / ("rank%d_step%d.npz" % (r, step)))["z"] for r in range(WORLD)])
+        z = np.concatenate([np.load(tmp_path / ("rank%d_step%d.npz" % (r, step)))["z"] for r in range(world)])
         np.testing.assert_allclose(z, fw["z"], atol=ztol, rtol=0, err_msg="logits step %d" % step)
         loss = float(np.load(tmp_path / ("rank0_step%d.npz" % step))["loss"])
         assert abs(loss - fw["loss"]) < (5e-3 if bf else 1e-5), (step, loss, fw["loss"])
-    d = [np.load(tmp_path / ("rank%d.npz" % r)) for r in range(WORLD)]
+    d = [np.load(tmp_path / ("rank%d.npz" % r)) for r in range(world)]
     table = np.zeros_like(P["weight_mat"])
     ww = np.zeros_like(P["wdl_weights"][:, 0])
     for e in d:
@@ -166,9 +194,10 @@ def test_sharded_wdl_two_ranks_equals_global_batch(tmp_path, mode):
     np.testing.assert_allclose(table, P["weight_mat"], atol=ptol, rtol=0)
     np.testing.assert_allclose(ww, P["wdl_weights"][:, 0], atol=ptol, rtol=0)
     np.testing.assert_allclose(d[0]["wb"], P["wdl_bias"], atol=ptol, rtol=0)
-    np.testing.assert_array_equal(d[0]["W0"], d[1]["W0"])      # replicated dense state identical
+    for e in d[1:]:                                             # replicated dense state identical
+        np.testing.assert_array_equal(e["W0"], d[0]["W0"])
     # sharded eval on two unseen global batches
-    evb = wdl_batches(BL * WORLD, STEPS + 2)[STEPS:]
+    evb = wdl_batches(BL * world, STEPS + 2)[STEPS:]
     all_s, all_y = [], []
     for j, b in enumerate(evb):
         want = 1.0 / (1.0 + np.exp(-R.forward(cfg, P, b)["z"].astype(np.float64)))
@@ -176,7 +205,7 @@ def test_sharded_wdl_two_ranks_equals_global_batch(tmp_path, mode):
         np.testing.assert_allclose(got, want, atol=ztol, rtol=0, err_msg="eval batch %d" % j)
         all_s.append(want)
         all_y.append(b["label"].reshape(-1))
-    assert float(d[0]["auc"]) == float(d[1]["auc"])
+    assert all(float(e["auc"]) == float(d[0]["auc"]) for e in d)
     assert abs(float(d[0]["auc"]) - R.auc(np.concatenate(all_y), np.concatenate(all_s))) < (2e-3 if bf else 1e-4)
 
 
