@@ -997,8 +997,13 @@ __global__ __launch_bounds__(512) void gemm_s3_tn3_kernel(S3Params p) {
     unsigned short* As = lds + buf * kT2Buf;
     unsigned short* Bs = As + 3 * kT2AE;
     uint32_t h0, m0_, l0, h1, m1_, l1;
-    split2(r.x, r.y, h0, m0_, l0);
-    split2(r.z, r.w, h1, m1_, l1);
+    if (DL_S3_DIAG == 6) {   // timing only: no split
+      h0 = __float_as_uint(r.x); m0_ = __float_as_uint(r.y); l0 = h0;
+      h1 = __float_as_uint(r.z); m1_ = __float_as_uint(r.w); l1 = h1;
+    } else {
+      split2(r.x, r.y, h0, m0_, l0);
+      split2(r.z, r.w, h1, m1_, l1);
+    }
     unsigned short* img = u < 2 ? As : Bs;
     const int pe = u < 2 ? kT2AE : kT2BE;
     const int o = pr[u] * (u < 2 ? kT2PA : kT2PB) + pc[u];
