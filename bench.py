@@ -241,8 +241,9 @@ def workload_name(wl, vocab, n_rows, sharded):
 
 def lookup_alone(eng, batch, B, per_sample, reps=20):
     """SURVEY §8(d)'s embedding gather as a lookup kernel alone, the one CTREngine.predict runs
-    on a flushed table: the flush writes every row's p and first-order weight out as dense planes
-    (dl_rec_flush with planes) and the lookup reads 64-B rows from them (dl_embed_fwd: the FM
+    on a flushed table: the flush writes every row's p and first-order weight out as a slot plane
+    (dl_rec_flush with DL_REC_PLANE_SLOTS: 128-B slots, the weight beside the row) and the lookup
+    reads them (dl_embed_fwd_slots: an FM reference's row and weight one random request; the FM
     sums and x0 assembled) — bit-identical to the rec_gather + embed_fwd pair at lag 0 by test.
     Also timed: the same lookup reading each record's first 128-B line (dl_embed_fwd_rec_flat,
     the form without planes).  HIP events on the launch stream."""
@@ -260,8 +261,12 @@ def lookup_alone(eng, batch, B, per_sample, reps=20):
     x0 = eng.x0b if eng.x0_direct else eng.x0
 
     def planes():
-        call("dl_embed_fwd", C_ref(FL), ptr(eng.p_plane), ptr(eng.w1_plane), ptr(eng.in_cate), ptr(eng.in_cont),
-             ptr(eng.in_vec), ptr(x0), ptr(eng.fm_out), ptr(eng.fm_sum), ptr(eng.err), s)
+        if sp.fm:   # the slot plane: an FM reference's row and first-order weight in one 128-B slot
+            call("dl_embed_fwd_slots", C_ref(FL), ptr(eng.p_plane), ptr(eng.in_cate), ptr(eng.in_cont), ptr(eng.in_vec),
+                 ptr(x0), ptr(eng.fm_out), ptr(eng.fm_sum), ptr(eng.err), s)
+        else:
+            call("dl_embed_fwd", C_ref(FL), ptr(eng.p_plane), None, ptr(eng.in_cate), ptr(eng.in_cont),
+                 ptr(eng.in_vec), ptr(x0), ptr(eng.fm_out), ptr(eng.fm_sum), ptr(eng.err), s)
 
     def records():
         if eng.n_rep:

@@ -50,7 +50,7 @@ class PoolDesc(C.Structure):
 # include/dlamd.h constants
 OPT_LEN, OPT_STATUS, OPT_SKIP, OPT_BAD_STEP, OPT_BAD_COUNT, OPT_SEQ, OPT_BAD_RANKS = 32, 16, 17, 18, 19, 20, 21
 STATUS_BAD_ID, STATUS_LAG, STATUS_INDEX, STATUS_OVERFLOW, STATUS_DESYNC = 1, 2, 4, 8, 16
-REC_FIRST, REC_SPARSE_ADAM = 1, 2
+REC_FIRST, REC_SPARSE_ADAM, REC_PLANE_SLOTS = 1, 2, 4
 ROWS_CLEAR_TOUCHED, ROWS_SPARSE_ADAM, ROWS_GRAD_FIXED = 1, 2, 4
 WIDE_GRAD_SCALE = 2.0 ** 48
 LOSS_ACC_SLOTS = 65536
@@ -69,6 +69,7 @@ SIGNATURES = {
     "dl_embed_bwd_grid": (I32, [LP]),
     "dl_embed_cont_reduce": (I32, [LP, P, I32, P, P, P, P]),
     "dl_embed_fwd_indexed": (I32, [LP, P, P, P, I32, P, P, P, P, P, P]),
+    "dl_embed_fwd_slots": (I32, [LP, P, P, P, P, P, P, P, P, P]),
     "dl_embed_fwd_rec": (I32, [LP, P, I32, I32, P, P, P, P, P, P, I32, P, I32, P, P, P, P, P]),
     "dl_embed_fwd_rec_flat": (I32, [LP, P, I32, I32, P, P, P, P, P, P, P, P, P, P, P]),
     "dl_shard_gather": (I32, [P, P, P, I64, I32, P, P, P]),

@@ -81,6 +81,9 @@ __global__ __launch_bounds__(256, (REC == 1 || NPS > 5) ? 1 : DL_FWD_MIN_WAVES) 
   // zeroed by select, never by a branch around the load.
   constexpr int LPR = E / 4;
   constexpr int RPI = 64 / LPR;
+  constexpr bool RECS = REC == 1 || REC == 2;          // the record modes
+  constexpr int TP = REC == 3 ? 2 * LPR : LPR;         // float4s between table rows (slot plane: 2E floats)
+  constexpr int W1S = REC == 3 ? 2 * E : 1;            // floats between first-order weights
   __shared__ int rows_s[kTileSamples][kMaxSlots];
   __shared__ float vals_s[kTileSamples][kMaxHotContFwd];
   const dl_emb_layout& L = a.L;
@@ -174,9 +177,9 @@ __global__ __launch_bounds__(256, (REC == 1 || NPS > 5) ? 1 : DL_FWD_MIN_WAVES) 
         rw[p] = rows_s[j][sl < nslot ? sl : 0];
         if (sl >= nslot) rw[p] = -1;
       }
-      if (REC == 0) {
+      if (!RECS) {
 #pragma unroll
-        for (int p = 0; p < NPS; ++p) v[p] = tab4[(rw[p] < 0 ? 0 : rw[p]) * LPR + q];
+        for (int p = 0; p < NPS; ++p) v[p] = tab4[(int64_t)(rw[p] < 0 ? 0 : rw[p]) * TP + q];
       } else if (REC == 2) {
         float4 t4[NPS];
 #pragma unroll
@@ -235,10 +238,10 @@ __global__ __launch_bounds__(256, (REC == 1 || NPS > 5) ? 1 : DL_FWD_MIN_WAVES) 
       // staged: the FM cate fields' first-order outputs were written by the gather (their rows
       // index the staging rows, not first_order) — only the zero rows' are written here
       const bool w1_done = a.staged && lane >= Cf && lane < Fs && rows_s[j][lane] >= 0;
-      if (lane < (REC != 0 ? Cf : Fs)) {
+      if (lane < (RECS ? Cf : Fs)) {
         frow = rows_s[j][lane];
         val = lane < Cf ? vals_s[j][lane] : 1.f;
-        w1 = DL_POOL_DIAG_NO_W1 ? 1.f : a.first_order[(frow < 0 || w1_done) ? 0 : frow];
+        w1 = DL_POOL_DIAG_NO_W1 ? 1.f : a.first_order[(int64_t)((frow < 0 || w1_done) ? 0 : frow) * W1S];
       }
       float4 s = z4, ss = z4;
 #pragma unroll
@@ -265,12 +268,12 @@ __global__ __launch_bounds__(256, (REC == 1 || NPS > 5) ? 1 : DL_FWD_MIN_WAVES) 
           }
         }
       }
-      if (lane < (REC != 0 ? Cf : Fs) && !w1_done) a.fm_out[(int64_t)b * L.fm_ld + lane] = frow < 0 ? 0.f : w1 * val;
-      for (int f = 64 + lane; f < (REC != 0 ? 0 : Fs); f += 64) {   // > 64 FM fields (rare; record mode: <= 64)
+      if (lane < (RECS ? Cf : Fs) && !w1_done) a.fm_out[(int64_t)b * L.fm_ld + lane] = frow < 0 ? 0.f : w1 * val;
+      for (int f = 64 + lane; f < (RECS ? 0 : Fs); f += 64) {   // > 64 FM fields (rare; record mode: <= 64)
         const int fr = rows_s[j][f];
         if (a.staged && f >= Cf && fr >= 0) continue;
         const float vv = f < Cf ? vals_s[j][f] : 1.f;
-        a.fm_out[(int64_t)b * L.fm_ld + f] = fr < 0 ? 0.f : a.first_order[fr] * vv;
+        a.fm_out[(int64_t)b * L.fm_ld + f] = fr < 0 ? 0.f : a.first_order[(int64_t)fr * W1S] * vv;
       }
       if (L.use_fm) {
         for (int f0 = 0; f0 < L.fm_extra; f0 += RPI) {
@@ -955,6 +958,18 @@ extern "C" int dl_embed_fwd(const dl_emb_layout* L, const float* table, const fl
   if (L->batch == 0) return 0;
   EmbArgs a{*L, nullptr, 0, table, first_order, cate, cont, vector, x0, fm_out, fm_sum, err};
   return launch_embed_fwd<0>(L, a, stream);
+}
+
+extern "C" int dl_embed_fwd_slots(const dl_emb_layout* L, const float* slots, const int64_t* cate, const float* cont,
+                                  const float* vector, float* x0, float* fm_out, float* fm_sum, int32_t* err,
+                                  void* stream) {
+  if (int rc = check_layout(L)) return rc;
+  DL_CHECK_ARG(slots && cate && x0, "NULL slots/cate/x0");
+  DL_CHECK_ARG(!L->use_fm || (fm_out && fm_sum), "FM outputs required");
+  DL_CHECK_ARG((uintptr_t)slots % 16 == 0, "the slot plane must be 16-B aligned");
+  if (L->batch == 0) return 0;
+  EmbArgs a{*L, nullptr, 0, slots, slots + L->emb_dim, cate, cont, vector, x0, fm_out, fm_sum, err};
+  return launch_embed_fwd<3>(L, a, stream);
 }
 
 extern "C" int dl_embed_fwd_indexed(const dl_emb_layout* L, const float* rows, const float* rows_first,

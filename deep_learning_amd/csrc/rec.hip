@@ -856,7 +856,7 @@ template <int E>
 __global__ __launch_bounds__(256) void rec_flush_kernel(float* __restrict__ rec, RecCfg c, long long n_rows,
                                                         const float* __restrict__ hist,
                                                         const float* __restrict__ opt, float* __restrict__ p_plane,
-                                                        float* __restrict__ w1_plane) {
+                                                        float* __restrict__ w1_plane, int slots) {
   rec_load_hyper(c, opt);
   __shared__ float hw[kHistWin];
   const RingW ring = load_hist_window(hw, hist, (int)opt[7], c);
@@ -864,14 +864,19 @@ __global__ __launch_bounds__(256) void rec_flush_kernel(float* __restrict__ rec,
   const long long gt = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   const int q = (int)(gt % LPR);
   const int target = (int)opt[7];
+  // planes: p at p_plane + row * pitch, the first-order weight at w1_plane[row * w1s] (slot plane:
+  // pitch 2E, the weight in column E of the same slot)
+  const int pitch = slots ? 2 * E : E;
+  const long long w1s = slots ? 2 * E : 1;
+  float* w1p = slots ? (p_plane && c.has_first ? p_plane + E : nullptr) : w1_plane;
   for (long long row = gt / LPR; row < n_rows; row += (long long)gridDim.x * blockDim.x / LPR) {
     float* r = rec + row * c.ld;
     const float4 tail = *reinterpret_cast<const float4*>(r + E);
     const int stamp = __float_as_int(tail.w);
     if (stamp >= target) {
       if (p_plane) {   // caught up already: its p (and first-order weight) into the planes
-        *reinterpret_cast<float4*>(p_plane + row * E + 4 * q) = *reinterpret_cast<const float4*>(r + 4 * q);
-        if (w1_plane && q == 0) w1_plane[row] = tail.x;
+        *reinterpret_cast<float4*>(p_plane + row * pitch + 4 * q) = *reinterpret_cast<const float4*>(r + 4 * q);
+        if (w1p && q == 0) w1p[row * w1s] = tail.x;
       }
       continue;
     }
@@ -882,8 +887,8 @@ __global__ __launch_bounds__(256) void rec_flush_kernel(float* __restrict__ rec,
     const bool first = c.has_first && q == 0;
     catch_up4(p, m, v, w, wm, wv, first, stamp, target, ring, c);
     if (p_plane) {
-      *reinterpret_cast<float4*>(p_plane + row * E + 4 * q) = p;
-      if (w1_plane && q == 0) w1_plane[row] = w;
+      *reinterpret_cast<float4*>(p_plane + row * pitch + 4 * q) = p;
+      if (w1p && q == 0) w1p[row * w1s] = w;
     }
     *reinterpret_cast<float4*>(r + 4 * q) = p;
     *reinterpret_cast<float4*>(r + E + 4 + 4 * q) = m;
@@ -1271,7 +1276,7 @@ extern "C" int dl_rec_flush(float* rec, int32_t rec_ld, int32_t emb_dim, int32_t
   DL_DISPATCH_E(emb_dim, {
     hipLaunchKernelGGL(rec_flush_kernel<kE>, dim3(grid_cap(n_rows * (kE / 4))), dim3(256), 0, as_stream(stream),
                        rec, make_rec_cfg(kE, rec_ld, rec_flags, hist_len), (long long)n_rows, hist,
-                       opt, p_plane, has_first ? w1_plane : nullptr);
+                       opt, p_plane, has_first ? w1_plane : nullptr, (rec_flags & DL_REC_PLANE_SLOTS) ? 1 : 0);
   });
   DL_RETURN_LAUNCH("dl_rec_flush");
 }

@@ -773,25 +773,44 @@ class CTREngine:
         if not self.lazy:
             return
         pp = w1 = None
+        flags = self.rec_flags
         if planes and getattr(self, "p_plane", None) is None:
-            # rows x E f32 (+ rows f32): 1.7 GB at 26 M rows, E = 16 — dropped again when training
-            # resumes (train_step); without the memory, predict reads the records instead
+            # FM models: one slot plane, rows x 2E f32 (p, then the first-order weight in column E:
+            # an FM reference's row and weight in one 128-B slot, one random request instead of
+            # two — 3.3 GB at 26 M rows, E = 16); otherwise a rows x E p plane (1.7 GB).  Dropped
+            # again when training resumes (train_step); without the memory, predict reads the
+            # records instead
             try:
-                self.p_plane = torch.empty(self.rec.shape[0], self.spec.E, device=self.dev)
-                self.w1_plane = torch.empty(self.rec.shape[0], device=self.dev) if self.spec.fm else None
+                self.p_plane = torch.empty(self.rec.shape[0], 2 * self.spec.E if self.spec.fm else self.spec.E,
+                                           device=self.dev)
+                self.w1_plane = None
             except torch.cuda.OutOfMemoryError:
                 self.p_plane = self.w1_plane = None
                 self.flat_planes = False
                 planes = False
         if planes:
             pp, w1 = self.p_plane, self.w1_plane
-        self._c("rec_flush", "dl_rec_flush", ptr(self.rec), self.rec_ld, self.spec.E, self.rec_flags,
+            if self.spec.fm:
+                flags |= _lib.REC_PLANE_SLOTS
+        self._c("rec_flush", "dl_rec_flush", ptr(self.rec), self.rec_ld, self.spec.E, flags,
                 self.rec.shape[0], ptr(self.hist), self.hist_len, ptr(self.opt), ptr(pp), ptr(w1),
                 _lib.stream_handle())
         self.planes_step = self.steps if planes else getattr(self, "planes_step", -1)
         if getattr(self, "wide_lazy", False):
             self._wide_flush()
         self.since_flush = 0
+
+    def plane_lookup(self, B, x0, s):
+        """The lookup over flush(planes=True)'s planes: FM models read the slot plane (row and
+        first-order weight in one 128-B slot, dl_embed_fwd_slots), the others the p plane."""
+        if self.spec.fm:
+            self._c("embed_fwd", "dl_embed_fwd_slots", C_ref(self._flat_layout(B)), ptr(self.p_plane),
+                    ptr(self.in_cate), ptr(self.in_cont), ptr(self.in_vec), ptr(x0), ptr(self.fm_out),
+                    ptr(self.fm_sum), ptr(self.err), s)
+        else:
+            self._c("embed_fwd", "dl_embed_fwd", C_ref(self._flat_layout(B)), ptr(self.p_plane), None,
+                    ptr(self.in_cate), ptr(self.in_cont), ptr(self.in_vec), ptr(x0), ptr(self.fm_out),
+                    ptr(self.fm_sum), ptr(self.err), s)
 
     def adam_state(self):
         """Table Adam state in the dense layout (tests, checkpoints): dict of m, v (+ m1, v1) as
@@ -877,11 +896,9 @@ class CTREngine:
                  ptr(self.x0), ptr(self.fm_out), ptr(self.cnt_emb), ptr(self.cnt_first), ptr(self.err), s)
         if (not train and self.lazy and not sp.M and self.since_flush == 0 and type(self) is CTREngine
                 and getattr(self, "planes_step", -1) == self.steps):
-            # predict on a flushed table whose p / first-order planes are current (flush(planes=
-            # True) at this step): the plain lookup of the dense layout, 64-B rows (dl_embed_fwd)
-            self._c("embed_fwd", "dl_embed_fwd", C_ref(self._flat_layout(B)), ptr(self.p_plane), ptr(self.w1_plane),
-                    ptr(self.in_cate), ptr(self.in_cont), ptr(self.in_vec), ptr(x0), ptr(self.fm_out),
-                    ptr(self.fm_sum), ptr(self.err), s)
+            # predict on a flushed table whose planes are current (flush(planes=True) at this
+            # step): the plain lookup of the dense layout (dl_embed_fwd_slots / dl_embed_fwd)
+            self.plane_lookup(B, x0, s)
         elif not train and self.lazy and not sp.M and self.since_flush == 0 and type(self) is CTREngine:
             # predict on a flushed table (every record caught up to the current step): the plain
             # lookup, each reference reading its record's first line (dl_embed_fwd_rec_flat)

@@ -93,6 +93,12 @@ typedef struct dl_emb_layout {
 int dl_embed_fwd(const dl_emb_layout* L, const float* table, const float* first_order,
                  const int64_t* cate, const float* cont, const float* vector,
                  float* x0, float* fm_out, float* fm_sum, int32_t* err, void* stream);
+/* dl_embed_fwd over a slot plane [n_rows][2E] (dl_rec_flush with DL_REC_PLANE_SLOTS): row r's
+ * embedding in columns 0..E-1, its first-order weight in column E — an FM reference's row and
+ * weight in one 128-B slot (E = 16), one random request instead of two (predict on a flushed
+ * lazy table; same outputs as dl_embed_fwd on separate planes, bit for bit). */
+int dl_embed_fwd_slots(const dl_emb_layout* L, const float* slots, const int64_t* cate, const float* cont,
+                       const float* vector, float* x0, float* fm_out, float* fm_sum, int32_t* err, void* stream);
 
 /* Backward of dl_embed_fwd for the FM (single fields) and deep lookups.
  * dz [B] = dL/dlogit, w_head = head weights whose first F+E entries weight
@@ -523,6 +529,9 @@ int dl_adam_rows(float* p, float* m, float* v, void* g, uint8_t* touched, int64_
  * dl_adam_rows), else ApplyAdam's.  The catch-up replays the same form. */
 #define DL_REC_FIRST 1
 #define DL_REC_SPARSE_ADAM 2
+/* dl_rec_flush only: p_plane is a slot plane [n_rows][2E] — row r's p in columns 0..E-1 and its
+ * first-order weight in column E (128-B slots for E = 16; columns E+1.. unwritten), w1_plane unused */
+#define DL_REC_PLANE_SLOTS 4
 /* hist[step & (hist_len-1)] = alpha of the step dl_adam_begin_step just began. */
 int dl_adam_hist_record(const float* opt, float* hist, int32_t hist_len, void* stream);
 /* rows_u[i] = p(row_i) caught up to step opt[7]-lag (rows_u1[i] = w1), row_i =
@@ -617,7 +626,8 @@ int dl_rec_apply_segments(float* rec, int32_t rec_ld, int32_t emb_dim, int32_t r
 /* Every row caught up to step opt[7] (before export/checkpoint, and every hist_len steps).
  * p_plane [n_rows][E] / w1_plane [n_rows] (may be NULL): every row's caught-up p and first-order
  * weight written out densely — the table predict's plain lookup then reads (dl_embed_fwd on the
- * planes: 64-B rows instead of the records' 128-B first lines). */
+ * planes: 64-B rows instead of the records' 128-B first lines); with DL_REC_PLANE_SLOTS in
+ * rec_flags, one slot plane [n_rows][2E] holding both (dl_embed_fwd_slots). */
 int dl_rec_flush(float* rec, int32_t rec_ld, int32_t emb_dim, int32_t rec_flags, int64_t n_rows,
                  const float* hist, int32_t hist_len, const float* opt, float* p_plane, float* w1_plane,
                  void* stream);

@@ -16,7 +16,7 @@ from deep_learning_amd.synthetic import make_batch  # noqa: E402
 dist = sys.argv[1] if len(sys.argv) > 1 else "uniform"
 reps = int(sys.argv[2]) if len(sys.argv) > 2 else 20
 B, N = 65536, 26_000_000
-spec = ModelSpec("deepfm_pipeline", C=13, V=0, S=26, E=16, cate_index_size=N, hidden=[400, 400, 400])
+spec = sp = ModelSpec("deepfm_pipeline", C=13, V=0, S=26, E=16, cate_index_size=N, hidden=[400, 400, 400])
 eng = CTREngine(spec, max_batch=B, seed=2019, adam="lazy")
 eng.flush(planes=True)
 b = {k: torch.from_numpy(v).cuda() for k, v in make_batch(B, cate_index_size=N, seed=4242, dist=dist).items()}
@@ -27,8 +27,12 @@ x0 = eng.x0b if eng.x0_direct else eng.x0
 
 
 def run():
-    call("dl_embed_fwd", C_ref(FL), ptr(eng.p_plane), ptr(eng.w1_plane), ptr(eng.in_cate), ptr(eng.in_cont),
-         ptr(eng.in_vec), ptr(x0), ptr(eng.fm_out), ptr(eng.fm_sum), ptr(eng.err), s)
+    if sp.fm:   # the slot plane: an FM reference's row and first-order weight in one 128-B slot
+        call("dl_embed_fwd_slots", C_ref(FL), ptr(eng.p_plane), ptr(eng.in_cate), ptr(eng.in_cont), ptr(eng.in_vec),
+             ptr(x0), ptr(eng.fm_out), ptr(eng.fm_sum), ptr(eng.err), s)
+    else:
+        call("dl_embed_fwd", C_ref(FL), ptr(eng.p_plane), None, ptr(eng.in_cate), ptr(eng.in_cont),
+             ptr(eng.in_vec), ptr(x0), ptr(eng.fm_out), ptr(eng.fm_sum), ptr(eng.err), s)
 
 
 run()

@@ -58,6 +58,30 @@ __global__ void g_scalar(const float* __restrict__ tab, const int* __restrict__ 
 #pragma unroll
   for (int u = 0; u < U; ++u) { long i = base + (long)u * blockDim.x; if (i < n) out[i] = v[u]; }
 }
+// variant 4: 64-B row + its 4-B first-order weight, the weight in a separate [rows] array
+// (the predict planes' layout) or at byte 64 of a 128-B slot (row, weight, pad): two loads per
+// reference either way; do they cost two random requests or one?
+template <int U, bool SAME>
+__global__ void g_row_w1(const float4* __restrict__ tab, const float* __restrict__ w1, const int* __restrict__ idx,
+                         float* __restrict__ out, long n) {
+  long base = ((long)blockIdx.x * blockDim.x) * U + threadIdx.x;
+  float4 v[U];
+  float w[U];
+  int r[U];
+#pragma unroll
+  for (int u = 0; u < U; ++u) { long i = base + (long)u * blockDim.x; r[u] = i < n * 4 ? idx[i >> 2] : 0; }
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    long i = base + (long)u * blockDim.x;
+    v[u] = tab[(long)r[u] * (SAME ? 8 : 4) + (i & 3)];
+    const bool q0 = (i & 3) == 0;
+    w[u] = q0 ? (SAME ? reinterpret_cast<const float*>(tab)[(long)r[u] * 32 + 16] : w1[r[u]]) : 0.f;
+  }
+  float s = 0;
+#pragma unroll
+  for (int u = 0; u < U; ++u) s += v[u].x + v[u].y + v[u].z + v[u].w + w[u];
+  if (s == 123.456f) out[0] = s;
+}
 // streaming copy for reference
 __global__ void copy4(const float4* __restrict__ a, float4* __restrict__ b, long n4) {
   for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += (long)gridDim.x * blockDim.x) b[i] = a[i];
@@ -72,6 +96,11 @@ int main(int argc, char** argv) {
   CK(hipMalloc(&out, nreq * 64));
   CK(hipMalloc(&outs, nreq * 4));
   CK(hipMemset(tab, 0, rows * 64));
+  float4* tab128; float* w1;
+  CK(hipMalloc(&tab128, rows * 128));
+  CK(hipMalloc(&w1, rows * 4));
+  CK(hipMemset(tab128, 0, rows * 128));
+  CK(hipMemset(w1, 0, rows * 4));
   std::vector<int> h(nreq);
   srand(1);
   for (long i = 0; i < nreq; ++i) h[i] = (int)(((unsigned long)rand() * 2654435761UL + rand()) % rows);
@@ -98,6 +127,8 @@ int main(int argc, char** argv) {
     timeit("f4u U=8 (+write)", [&] { hipLaunchKernelGGL(g_f4u<8>, dim3((nreq * 4 + 2047) / 2048), dim3(256), 0, 0, tab, idx, out, nreq); }, 2 * rb);
     timeit("sum U=4 (read only)", [&] { hipLaunchKernelGGL(g_sum<4>, dim3((nreq * 4 + 1023) / 1024), dim3(256), 0, 0, tab, idx, outs, nreq); }, rb);
     timeit("sum U=8 (read only)", [&] { hipLaunchKernelGGL(g_sum<8>, dim3((nreq * 4 + 2047) / 2048), dim3(256), 0, 0, tab, idx, outs, nreq); }, rb);
+    timeit("row + w1 separate array U=4 (read only)", [&] { hipLaunchKernelGGL((g_row_w1<4, false>), dim3((nreq * 4 + 1023) / 1024), dim3(256), 0, 0, tab, w1, idx, outs, nreq); }, rb);
+    timeit("row + w1 same 128-B slot U=4 (read only)", [&] { hipLaunchKernelGGL((g_row_w1<4, true>), dim3((nreq * 4 + 1023) / 1024), dim3(256), 0, 0, tab128, w1, idx, outs, nreq); }, rb);
     timeit("scalar 4B U=8 (+write)", [&] { hipLaunchKernelGGL(g_scalar<8>, dim3((nreq + 2047) / 2048), dim3(256), 0, 0, (const float*)tab, idx, outs, nreq); }, nreq * 8.0);
   }
   const long n4 = rows * 4;
