@@ -49,20 +49,21 @@ def _compile(src):
     return obj
 
 
-HOST_SRC = os.path.join(HERE, "csrc_host", "dlio.cpp")
+HOST_SRCS = [os.path.join(HERE, "csrc_host", f) for f in ("dlio.cpp", "dlpk.cpp")]
 HOST_OUT = os.path.join(HERE, "libdlio.so")
 
 
 def build_host(verbose=True):
-    """The native TFRecord reader (include/dlio.h): plain host C++, g++, no GPU code."""
-    deps = [HOST_SRC, os.path.join(ROOT, "include", "dlio.h")]
+    """The native TFRecord reader and load-style batch decoder (include/dlio.h): plain host C++,
+    g++, no GPU code."""
+    deps = HOST_SRCS + [os.path.join(ROOT, "include", "dlio.h")]
     if os.path.exists(HOST_OUT) and os.path.getmtime(HOST_OUT) >= max(os.path.getmtime(d) for d in deps):
         return HOST_OUT
     cmd = [os.environ.get("CXX", "g++"), "-O3", "-std=c++17", "-fPIC", "-shared", "-pthread", "-Wall",
-           "-I" + os.path.join(ROOT, "include"), HOST_SRC, "-o", HOST_OUT]
+           "-I" + os.path.join(ROOT, "include")] + HOST_SRCS + ["-o", HOST_OUT]
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
-        raise RuntimeError("g++ failed for %s:\n%s\n%s" % (HOST_SRC, r.stdout, r.stderr))
+        raise RuntimeError("g++ failed for %s:\n%s\n%s" % (HOST_SRCS, r.stdout, r.stderr))
     if verbose:
         print("built", HOST_OUT)
     return HOST_OUT

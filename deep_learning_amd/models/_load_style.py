@@ -33,12 +33,14 @@ def unpickle(item):
 
 
 class PinnedFeed:
-    """The load-style batches (pickled dicts, wdl.py:296) unpickled and converted on worker
-    threads into a ring of pinned host buffers, in order, ahead of the training loop: the engine
-    then stages each one with an asynchronous host-to-device copy on its side stream
-    (engine._copy_in) instead of the loop unpickling and copying 31 MB of pageable memory a C5
-    batch between steps.  A ring slot is refilled only after the step that consumed it has run
-    (release(): an event on the compute stream after that step)."""
+    """The load-style batches (pickled dicts, wdl.py:296) decoded on worker threads into a ring
+    of pinned host buffers, in order, ahead of the training loop: libdlio's pickle decoder
+    (dlio_unpickle_batch) writes each field straight into its pinned buffer with the GIL released
+    (pickle.loads + a copy under the GIL for forms it does not take), and the engine stages each
+    batch with an asynchronous host-to-device copy on its side stream (engine._copy_in) instead
+    of the loop unpickling and copying 31 MB of pageable memory a C5 batch between steps.  A ring
+    slot is refilled only after the step that consumed it has run (release(): an event on the
+    compute stream after that step)."""
 
     def __init__(self, model, items, workers=None, depth=None):
         self.model = model
@@ -70,6 +72,28 @@ class PinnedFeed:
             self.k += 1
         self.pending.append(self.pool.submit(self._prepare, k, item))
 
+    def _native(self, s, item):
+        """The batch decoded by libdlio's pickle decoder straight into slot s's pinned buffers
+        (GIL released, one host copy); None when the pickle is not a form it takes."""
+        from ..utils.native_reader import unpickle_batch_into
+        fields = self.model.native_fields()
+        if fields is None or not isinstance(item, bytes):
+            return None
+        cap = self.model.batch_size
+        outs = []
+        for key, out_key, kind, size in fields:
+            dt = torch.float32 if kind == 0 else torch.int64
+            buf = self.bufs[s].get(out_key)
+            if buf is None or buf.numel() < cap * size or buf.dtype != dt:
+                buf = self.bufs[s][out_key] = torch.empty(max(cap * size, 1), dtype=dt).pin_memory()
+            outs.append(buf)
+        rows = unpickle_batch_into(item, [(key, kind, size) for key, _, kind, size in fields], outs, cap)
+        if rows is None:
+            return None
+        out = {out_key: buf[: rows * size].view(rows, size) for (_, out_key, _, size), buf in zip(fields, outs)}
+        out.update(self.model.native_extra(rows))
+        return out
+
     def _prepare(self, k, item):
         s = k % self.depth
         self.free[s].wait()       # the slot's previous batch has been released (one claimant a slot:
@@ -77,6 +101,10 @@ class PinnedFeed:
         ev = self.events[s]
         if ev is not None:
             ev.synchronize()
+        out = self._native(s, item)
+        if out is not None:
+            out["_slot"] = s
+            return out
         d = self.model.batch(item)
         out = {}
         for key, a in d.items():
@@ -129,6 +157,15 @@ class LoadStyleModel:
     def make_spec(self, args):
         raise NotImplementedError
 
+    def native_fields(self):
+        """(pickle key, batch key, 0 float32 / 1 int64, values per row) of the fields batch()
+        reads, for libdlio's pickle decoder (PinnedFeed); None: always unpickle in Python."""
+        return None
+
+    def native_extra(self, rows):
+        """Batch entries the decoder does not fill (empty fields)."""
+        return {}
+
     def batch(self, item):
         """One pickled batch dict (data_loader_load.py:128-135 keys) -> engine batch."""
         raise NotImplementedError
@@ -147,12 +184,11 @@ class LoadStyleModel:
         eng = self.model_optimizer()
         eng.loss_sum_begin()
         steps = 0
-        if os.environ.get("DLAMD_PINNED_FEED", "0") != "1":
-            # the next batch unpickled and staged (pageable host-to-device) on this thread while
-            # the current step runs.  (PinnedFeed, worker threads copying each unpickled batch
-            # into pinned buffers, measured 2.4 -> 6.8 ms a C5 step: the extra host copy of 31 MB
-            # a batch under the GIL-bound unpickling outweighs the faster transfer;
-            # profiles/r05t/bench_default.json, round 5)
+        if os.environ.get("DLAMD_PINNED_FEED", "1") == "0":
+            # DLAMD_PINNED_FEED=0: the next batch unpickled (pickle.loads) and staged (pageable
+            # host-to-device) on this thread while the current step runs.  The default is the
+            # PinnedFeed below: worker threads decode each pickled batch with libdlio's decoder
+            # (no GIL, one host copy) straight into pinned buffers (profiles/r05au/)
             items = iter(train_data)
             b = next(items, None)
             b = self.batch(b) if b is not None else None

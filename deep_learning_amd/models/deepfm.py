@@ -34,6 +34,14 @@ class DeepModel(LoadStyleModel):
                          decay_steps=float(args.learning_rate_decay_steps),
                          decay_rate=float(args.learning_rate_decay_rate))
 
+    def native_fields(self):
+        f = [("labels", "label", 0, 1), ("cont_feats", "cont_feats", 0, self.cont_field_size),
+             ("cate_feats", "cate_feats", 1, self.cate_field_size)]
+        return f + ([("vector_feats", "vector_feats", 0, self.vector_field_size)] if self.vector_field_size else [])
+
+    def native_extra(self, rows):
+        return {} if self.vector_field_size else {"vector_feats": np.zeros((rows, 0), np.float32)}
+
     def batch(self, item):
         d = unpickle(item)
         B = len(d["labels"])

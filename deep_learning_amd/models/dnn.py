@@ -29,6 +29,10 @@ class DeepModel(LoadStyleModel):
                          decay_steps=float(args.learning_rate_decay_steps),
                          decay_rate=float(args.learning_rate_decay_rate))
 
+    def native_fields(self):
+        return [("labels", "label", 0, 1), ("cont_feats", "cont_feats", 0, self.cont_field_size),
+                ("cate_feats", "cate_feats", 1, self.cate_field_size)]
+
     def batch(self, item):
         d = unpickle(item)
         B = len(d["labels"])

@@ -33,6 +33,11 @@ class DeepModel(LoadStyleModel):
                          decay_rate=float(args.learning_rate_decay_rate),
                          tower=str(getattr(args, "tower_dtype", "f32")))
 
+    def native_fields(self):
+        sp = self.spec
+        return [("labels", "label", 0, 1), ("cont_feats", "cont_feats", 0, sp.C), ("cate_feats", "cate_feats", 1, sp.S),
+                ("wide_feats", "wide_feats", 1, sp.Fw)]
+
     def batch(self, item):
         d = unpickle(item)
         return {"label": np.asarray(d["labels"], np.float32).reshape(-1, 1),

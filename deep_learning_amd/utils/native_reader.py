@@ -27,6 +27,8 @@ SIGNATURES = {
     "dlio_last_error": (C.c_char_p, [C.c_void_p]),
     "dlio_open_error": (C.c_char_p, []),
     "dlio_close": (None, [C.c_void_p]),
+    "dlio_unpickle_batch": (C.c_int32, [C.c_char_p, C.c_int64, C.POINTER(_Feature), C.c_int32, C.c_int64,
+                                        C.POINTER(C.c_void_p), C.POINTER(C.c_int64)]),
     "dlio_crc32c": (C.c_uint32, [C.c_void_p, C.c_int64]),
     "dlio_masked_crc32c": (C.c_uint32, [C.c_void_p, C.c_int64]),
 }
@@ -47,6 +49,22 @@ def lib():
             fn.argtypes = args
         _LIB = L
     return _LIB
+
+
+def unpickle_batch_into(item, fields, outs, cap_rows):
+    """Decode one pickled load-style batch (a dict of arrays or lists of rows,
+    utils/data_loader_load.py:128-136) straight into `outs` (C-contiguous numpy arrays or CPU
+    tensors, e.g. pinned, room for cap_rows rows each) without building Python objects — the
+    native decoder runs with the GIL released.  fields: (key, FLOAT | INT64, values per row).
+    Returns the batch's rows, or None when the pickle is not a form the decoder takes (the
+    caller unpickles it in Python then; malformed data raises there, as pickle.loads does)."""
+    if not isinstance(item, bytes):
+        return None
+    feats = (_Feature * len(fields))(*[_Feature(k.encode(), kind, size) for k, kind, size in fields])
+    ptrs = (C.c_void_p * len(outs))(*[o.data_ptr() if hasattr(o, "data_ptr") else o.ctypes.data for o in outs])
+    rows = C.c_int64(0)
+    rc = lib().dlio_unpickle_batch(item, len(item), feats, len(fields), int(cap_rows), ptrs, C.byref(rows))
+    return int(rows.value) if rc == 0 else None
 
 
 def crc32c(data):

@@ -53,6 +53,18 @@ const char* dlio_last_error(void* h);
 const char* dlio_open_error(void);
 void dlio_close(void* h);
 
+/* One pickled load-style batch (utils/data_loader_load.py:128-136: a dict per batch whose values
+ * are numpy arrays or lists of rows; models/wdl.py:296 unpickles one a step) decoded straight
+ * into caller buffers: field j's dict value, rows x fields[j].size values, converted to float32
+ * (DLIO_FLOAT) or int64 (DLIO_INT64), into outs[j] (room for cap_rows rows); *rows = the batch's
+ * rows (every field the same).  No Python object is built and nothing named in the pickle is
+ * constructed: protocols 3-5 of numpy arrays (numpy's reconstructors) and nested lists of
+ * numbers only.  Returns 0 = decoded, 1 = a form this decoder does not take (a missing key,
+ * another global, an object array, a shape that does not match: the caller unpickles in
+ * Python), < 0 = malformed / bad arguments. */
+int32_t dlio_unpickle_batch(const void* data, int64_t n, const dlio_feature* fields, int32_t n_fields,
+                            int64_t cap_rows, void* const* outs, int64_t* rows);
+
 /* CRC-32C (Castagnoli) of n bytes, and the TFRecord mask of it (SSE4.2 when present). */
 uint32_t dlio_crc32c(const void* data, int64_t n);
 uint32_t dlio_masked_crc32c(const void* data, int64_t n);

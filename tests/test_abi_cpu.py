@@ -48,7 +48,8 @@ def test_layout_struct_size(lib):
 
 
 def test_reader_header_symbols_exported():
-    """libdlio.so (native TFRecord reader) exports exactly what include/dlio.h declares."""
+    """libdlio.so (native TFRecord reader, load-style batch decoder) exports exactly what include/dlio.h
+    declares."""
     from deep_learning_amd.utils import native_reader as nr
     if not os.path.exists(nr.LIB_PATH):
         from deep_learning_amd import build
@@ -59,5 +60,5 @@ def test_reader_header_symbols_exported():
                               src, flags=re.M))
     out = subprocess.run(["nm", "-D", "--defined-only", nr.LIB_PATH], capture_output=True, text=True).stdout
     exported = {l.split()[-1] for l in out.splitlines() if " T dlio_" in l}
-    assert len(declared) == 8 and declared == exported == set(nr.SIGNATURES)
+    assert len(declared) == 9 and declared == exported == set(nr.SIGNATURES)
     nr.lib()

@@ -170,6 +170,53 @@ def test_wdl_load_style_fit_evaluate_predict(hip_lib, tmp_path):
     assert abs(auc_eval - auc_pred) < 1e-6 and 0.0 < auc_pred < 1.0
 
 
+@pytest.mark.parametrize("alg", ["wdl", "deepfm", "dnn"])
+def test_native_pickle_feed_trains_like_the_default_loop(hip_lib, tmp_path, alg, monkeypatch):
+    """DLAMD_PINNED_FEED=1: worker threads decode each pickled batch with libdlio's decoder
+    (dlio_unpickle_batch, no GIL) straight into pinned buffers and the engine stages them with
+    async copies — two epochs over the same batches (the last one partial, lists-of-lists
+    batches as the reference's own loader pickles them, and numpy-array batches) end with the
+    same parameters, bit for bit, as the default loop's pickle.loads path (and the same epoch
+    losses to a double's rounding)."""
+    import importlib
+    import pickle
+    from deep_learning_amd.synthetic import make_batch
+    from deep_learning_amd.utils import data_loader_load as dll
+    mod = importlib.import_module("deep_learning_amd.models." + alg)
+
+    class Args:
+        hidden_units, epochs, batch_size, learning_rate = [32, 16], 1, 64, 0.001
+        model_pb, learning_rate_decay_steps, learning_rate_decay_rate, l2_reg = str(tmp_path / "pb"), 10000000, 0.9, 1e-5
+        cont_field_size, cate_field_size, embedding_size, wide_field_size = 13, 26, 8, 26
+        cate_index_size = cate_feats_size = 4000
+        vector_feats_size = vector_field_size = 0
+        alg_name = alg
+    (tmp_path / "tr").mkdir()
+    dll.write_lines(str(tmp_path / "tr" / "part-0"),
+                    make_batch(300, cate_index_size=4000, seed=1, wide_fields=26 if alg == "wdl" else 0))
+    tr = dll.load_input_file(Args, str(tmp_path / "tr"))
+    # half the batches re-pickled as the reference's loader writes them: lists of rows
+    tr = [pickle.dumps({k: (v.tolist() if hasattr(v, "tolist") else v) for k, v in pickle.loads(it).items()})
+          if i % 2 else it for i, it in enumerate(tr)]
+    from deep_learning_amd.utils.native_reader import unpickle_batch_into
+    m0 = mod.DeepModel(Args)
+    f = m0.native_fields()
+    outs = [np.zeros((64, sz), np.float32 if kind == 0 else np.int64) for _, _, kind, sz in f]
+    assert all(unpickle_batch_into(it, [(k, kind, sz) for k, _, kind, sz in f], outs, 64) is not None for it in tr)
+    res = {}
+    for feed in ("0", "1"):
+        monkeypatch.setenv("DLAMD_PINNED_FEED", feed)
+        m = mod.DeepModel(Args)
+        losses = [m.train_epoch(tr) for _ in range(2)]
+        res[feed] = (losses, m.model_optimizer().params())
+    for k in res["0"][1]:
+        np.testing.assert_array_equal(res["1"][1][k], res["0"][1][k], err_msg=k)
+    # the epoch loss: the same per-step losses, summed on the device in double by block atomics
+    # (dl_loss_accumulate), so equal to the last few bits of a double, not bit for bit
+    for (a, na), (b, nb) in zip(res["0"][0], res["1"][0]):
+        assert na == nb and abs(a - b) <= 1e-9 * abs(a), (res["0"][0], res["1"][0])
+
+
 @pytest.mark.parametrize("alg", ["deepfm", "dnn"])
 def test_load_style_deepfm_dnn_fit_evaluate_predict(hip_lib, tmp_path, alg):
     """models/deepfm.py and models/dnn.py surfaces over the load-style loader

@@ -289,6 +289,42 @@ def test_native_reader_wire_variants(tmp_path):
     np.testing.assert_array_equal(b["label"], [[1.0]] * 3)
 
 
+@pytest.mark.parametrize("proto", [3, 4, 5, "lists"])
+def test_native_unpickle_batch_matches_pickle(proto):
+    """dlio_unpickle_batch (the load-style feed's decoder): a batch dict pickled with protocols
+    3-5 (numpy arrays of several dtypes, converted to float32 / int64) or as the reference's
+    lists of rows decodes to exactly what pickle.loads + np.asarray give; forms it does not take
+    (a missing key, an object array, protocols 0 and 2, another global, Fortran or big-endian
+    arrays, truncated data, more rows than the buffers hold) return None, so the caller falls back
+    to pickle.loads."""
+    import collections
+    import pickle
+    from deep_learning_amd.utils import native_reader as nr
+    rng = np.random.default_rng(0)
+    B, C, S = 777, 13, 26
+    d = {"labels": rng.integers(0, 2, (B, 1)).astype(np.float32), "cont_feats": rng.random((B, C)),
+         "cate_feats": rng.integers(0, 1 << 40, (B, S)), "wide_feats": rng.integers(0, 1000, (B, S)).astype(np.int32),
+         "other": np.arange(3)}
+    fields = [("labels", nr.FLOAT, 1), ("cont_feats", nr.FLOAT, C), ("cate_feats", nr.INT64, S),
+              ("wide_feats", nr.INT64, S)]
+    item = pickle.dumps({k: v.tolist() for k, v in d.items()}) if proto == "lists" else pickle.dumps(d, protocol=proto)
+    outs = [np.full((B + 3, sz), 7, np.float32 if k == nr.FLOAT else np.int64) for _, k, sz in fields]
+    assert nr.unpickle_batch_into(item, fields, outs, B + 3) == B
+    ref = pickle.loads(item)
+    for (key, k, sz), o in zip(fields, outs):
+        np.testing.assert_array_equal(o[:B], np.asarray(ref[key], o.dtype).reshape(B, sz), err_msg=key)
+        assert (o[B:] == 7).all()
+    if proto != 4:
+        return
+    bad = [pickle.dumps({"labels": d["labels"]}), pickle.dumps(dict(d, cont_feats=d["cont_feats"].astype(object))),
+           pickle.dumps(d, protocol=0), pickle.dumps(d, protocol=2), pickle.dumps(collections.OrderedDict(d)),
+           pickle.dumps(dict(d, cont_feats=np.asfortranarray(d["cont_feats"]))),
+           pickle.dumps(dict(d, cont_feats=d["cont_feats"].astype(">f8"))), item[:-40]]
+    for b in bad:
+        assert nr.unpickle_batch_into(b, fields, outs, B) is None
+    assert nr.unpickle_batch_into(item, fields, outs, B - 1) is None
+
+
 def test_s3_dw_split_counts():
     """engine._s3_dw_splits: the split-K count of an s3 weight gradient fills the CUs in as few
     rounds of 128 x 224 blocks as possible (C2's 8-tile layers keep 32 slabs; C3's layer 0,
