@@ -46,7 +46,7 @@ class PinnedFeed:
         self.model = model
         self.items = iter(items)
         self.workers = workers or int(os.environ.get("DLAMD_FEED_WORKERS", "2"))
-        self.depth = depth or self.workers + 2
+        self.depth = depth or int(os.environ.get("DLAMD_FEED_DEPTH", "0")) or self.workers + 2
         self.bufs = [dict() for _ in range(self.depth)]
         self.events = [None] * self.depth
         self.free = [threading.Event() for _ in range(self.depth)]
