@@ -292,11 +292,12 @@ def lookup_alone(eng, batch, B, per_sample, reps=20):
 
     us, gb, fr = timed(planes)
     rus, rgb, rfr = timed(records)
-    return {"kernels": ["embed_fwd (dense planes)"], "us": us, "GB/s": gb, "frac": fr,
+    return {"kernels": ["embed_fwd (slot plane)"], "us": us, "GB/s": gb, "frac": fr,
             "records": {"kernels": ["rec_gather (13 cont rows)", "embed_fwd_rec_flat"], "us": rus, "GB/s": rgb,
                         "frac": rfr},
             "note": "flushed table: the lookup without lazy Adam's catch-up, as predict runs it (the flush writes "
-                    "dense p / first-order planes; 'records' reads each record's first line instead); the "
+                    "a slot plane, each row's p and first-order weight in one 128-B slot; 'records' reads each "
+                    "record's first line instead); the "
                     "training step's gather above also replays each row's pending zero-gradient Adam steps and "
                     "stashes its moments"}
 
