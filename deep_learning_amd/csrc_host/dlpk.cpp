@@ -14,6 +14,8 @@
 // only globals it accepts are those data descriptions (numpy's reconstructors, ndarray, dtype),
 // anything else — another global, an object array, an out-of-band buffer — returns 1 and the
 // caller falls back to pickle.loads.
+#include <algorithm>
+#include <atomic>
 #include <cstdint>
 #include <cstdlib>
 #include <cstring>
@@ -360,9 +362,9 @@ inline T elem(const uint8_t* p, char dk, int isz) {
   }
 }
 
-// One field into out (rows x size of T); returns rows, or -2 unsupported / -3 shape mismatch.
-template <typename T>
-int64_t emit(const Parser& P, int vi, int32_t size, int64_t cap_rows, T* out, char want_dk) {
+// One field's rows before any copy: rows, or -2 unsupported / -3 shape mismatch.  (A list's
+// rows are checked as they are copied: fill.)
+int64_t check(const Parser& P, int vi, int32_t size, int64_t cap_rows) {
   const Val& v = P.vals[vi];
   if (v.k == K_ARRAY) {
     const Val& t = P.vals[v.dt];
@@ -371,37 +373,60 @@ int64_t emit(const Parser& P, int vi, int32_t size, int64_t cap_rows, T* out, ch
     for (size_t j = 1; j < v.shape.size(); ++j) cols *= v.shape[j];
     if (v.fortran && v.shape.size() > 1 && rows > 1 && cols > 1) return -2;
     if (cols != size || rows > cap_rows || rows < 0) return -3;
-    const int64_t cnt = rows * cols;
-    if (v.n != cnt * t.isz) return -3;
-    if (t.dk == want_dk && t.isz == (int)sizeof(T)) {
-      memcpy(out, v.p, (size_t)cnt * sizeof(T));
-    } else {
-      for (int64_t j = 0; j < cnt; ++j) out[j] = elem<T>(v.p + j * t.isz, t.dk, t.isz);
-    }
+    if (v.n != rows * cols * t.isz) return -3;
     return rows;
   }
   if (v.k == K_SEQ) {   // a list of rows: each a list / tuple of numbers, or a number (size 1)
     const int64_t rows = (int64_t)v.items.size();
-    if (rows > cap_rows) return -3;
-    for (int64_t r = 0; r < rows; ++r) {
-      const Val& row = P.vals[v.items[r]];
-      if (row.k == K_SEQ) {
-        if ((int64_t)row.items.size() != size) return -3;
-        for (int32_t c = 0; c < size; ++c) {
-          const Val& x = P.vals[row.items[c]];
-          if (x.k != K_INT && x.k != K_FLOAT && x.k != K_BOOL) return -2;
-          out[r * size + c] = num_of<T>(x);
-        }
-      } else if (row.k == K_INT || row.k == K_FLOAT || row.k == K_BOOL) {
-        if (size != 1) return -3;
-        out[r] = num_of<T>(row);
-      } else {
-        return -2;
-      }
-    }
-    return rows;
+    return rows > cap_rows ? -3 : rows;
   }
   return -2;
+}
+
+// Rows [r0, r1) of a checked field into out (rows x size of T): 0, or -2 / -3 for a list row
+// of another form.  Row ranges are disjoint pieces of out, so ranges can run on any threads.
+template <typename T>
+int fill(const Parser& P, int vi, int32_t size, T* out, char want_dk, int64_t r0, int64_t r1) {
+  const Val& v = P.vals[vi];
+  if (v.k == K_ARRAY) {
+    const Val& t = P.vals[v.dt];
+    const int64_t j0 = r0 * size, j1 = r1 * size;
+    if (t.dk == want_dk && t.isz == (int)sizeof(T))
+      memcpy(out + j0, v.p + j0 * (int64_t)sizeof(T), (size_t)(j1 - j0) * sizeof(T));
+    else
+      for (int64_t j = j0; j < j1; ++j) out[j] = elem<T>(v.p + j * t.isz, t.dk, t.isz);
+    return 0;
+  }
+  for (int64_t r = r0; r < r1; ++r) {
+    const Val& row = P.vals[v.items[r]];
+    if (row.k == K_SEQ) {
+      if ((int64_t)row.items.size() != size) return -3;
+      for (int32_t c = 0; c < size; ++c) {
+        const Val& x = P.vals[row.items[c]];
+        if (x.k != K_INT && x.k != K_FLOAT && x.k != K_BOOL) return -2;
+        out[r * size + c] = num_of<T>(x);
+      }
+    } else if (row.k == K_INT || row.k == K_FLOAT || row.k == K_BOOL) {
+      if (size != 1) return -3;
+      out[r] = num_of<T>(row);
+    } else {
+      return -2;
+    }
+  }
+  return 0;
+}
+
+// Threads one decode may use for its copies (DLIO_DECODE_THREADS, default 4).  A C5 batch is
+// 31 MB: on the GPU box a worker's decode took 1.80-2.25 ms on one thread, 1.43-1.44 ms on 4 and
+// 1.46-1.65 ms on 8, the drop-in step the same 2.2 ms throughout (profiles/r05bg/) — the feed
+// is bound by the host's memory traffic (two workers' copies beside the staging DMA).
+int decode_threads() {
+  static const int n = [] {
+    const char* e = getenv("DLIO_DECODE_THREADS");
+    const int v = e ? atoi(e) : 4;
+    return v < 1 ? 1 : (v > 64 ? 64 : v);
+  }();
+  return n;
 }
 
 }  // namespace
@@ -420,26 +445,44 @@ extern "C" int32_t dlio_unpickle_batch(const void* data, int64_t n, const dlio_f
       if (P.str_is(P.vals[D.items[j]], fields[f].name)) vis[f] = D.items[j + 1];
     if (vis[f] < 0) return 1;   // a missing key: pickle.loads and the model's own KeyError
   }
-  // the fields' copies / conversions in parallel once the batch is large (one thread a field:
-  // a C5 batch is 31 MB, and one core's copy rate, not the memory's, bounds a single thread)
+  // every field checked first; then the copies / conversions as row pieces of at least 1 MB
+  // (once the batch is large: 4 MB or more), the pieces dealt to a team of threads
   std::vector<int64_t> rs(n_fields, -2);
-  auto one = [&](int32_t f) {
-    if (fields[f].kind == DLIO_FLOAT)
-      rs[f] = emit<float>(P, vis[f], fields[f].size, cap_rows, reinterpret_cast<float*>(outs[f]), 'f');
-    else
-      rs[f] = emit<int64_t>(P, vis[f], fields[f].size, cap_rows, reinterpret_cast<int64_t*>(outs[f]), 'i');
-  };
-  if (n >= (4 << 20) && n_fields > 1) {
-    std::vector<std::thread> th;
-    for (int32_t f = 1; f < n_fields; ++f) th.emplace_back(one, f);
-    one(0);
-    for (auto& t : th) t.join();
-  } else {
-    for (int32_t f = 0; f < n_fields; ++f) one(f);
+  for (int32_t f = 0; f < n_fields; ++f) {
+    rs[f] = check(P, vis[f], fields[f].size, cap_rows);
+    if (rs[f] < 0) return 1;    // unsupported form or shape: the Python path decides (and raises)
   }
+  struct Piece { int32_t f; int64_t r0, r1; };
+  std::vector<Piece> pieces;
+  const int nt = n >= (4 << 20) ? decode_threads() : 1;
+  int64_t total = 0;
+  for (int32_t f = 0; f < n_fields; ++f) total += rs[f] * (int64_t)fields[f].size * 8;
+  const int64_t piece_bytes = nt > 1 ? std::max<int64_t>(1 << 20, total / (2 * nt)) : INT64_MAX;
+  for (int32_t f = 0; f < n_fields; ++f) {
+    const int64_t row_bytes = std::max<int64_t>(1, (int64_t)fields[f].size * 8);
+    const int64_t step = std::max<int64_t>(1, piece_bytes / row_bytes);
+    for (int64_t r = 0; r < rs[f]; r += step) pieces.push_back({f, r, std::min(rs[f], r + step)});
+  }
+  std::vector<int> st(pieces.size(), 0);
+  std::atomic<size_t> next{0};
+  auto work = [&]() {
+    for (size_t i; (i = next.fetch_add(1)) < pieces.size();) {
+      const Piece& q = pieces[i];
+      st[i] = fields[q.f].kind == DLIO_FLOAT
+                  ? fill<float>(P, vis[q.f], fields[q.f].size, reinterpret_cast<float*>(outs[q.f]), 'f', q.r0, q.r1)
+                  : fill<int64_t>(P, vis[q.f], fields[q.f].size, reinterpret_cast<int64_t*>(outs[q.f]), 'i', q.r0,
+                                  q.r1);
+    }
+  };
+  const int helpers = (int)std::min<size_t>((size_t)nt, pieces.size()) - 1;
+  std::vector<std::thread> th;
+  for (int i = 0; i < helpers; ++i) th.emplace_back(work);
+  work();
+  for (auto& t : th) t.join();
+  for (int v : st)
+    if (v < 0) return 1;
   int64_t rows = -1;
   for (int32_t f = 0; f < n_fields; ++f) {
-    if (rs[f] < 0) return 1;    // unsupported form or shape: the Python path decides (and raises)
     if (rows >= 0 && rs[f] != rows) return 1;
     rows = rs[f];
   }

@@ -325,6 +325,36 @@ def test_native_unpickle_batch_matches_pickle(proto):
     assert nr.unpickle_batch_into(item, fields, outs, B - 1) is None
 
 
+def test_native_unpickle_large_batch_in_row_pieces():
+    """A batch of 4 MB or more is copied as row pieces on a team of threads: a C5-sized dict
+    (arrays that are copied, and arrays converted from float64 / int32) and a lists-of-rows
+    batch decode exactly as pickle.loads gives them; a bad row deep inside the lists (its piece
+    on some helper thread) still makes the whole decode decline."""
+    import pickle
+    from deep_learning_amd.utils import native_reader as nr
+    rng = np.random.default_rng(5)
+    B, C, S = 60000, 13, 26
+    d = {"labels": rng.integers(0, 2, B).astype(np.float32), "cont_feats": rng.random((B, C)),
+         "cate_feats": rng.integers(0, 1 << 40, (B, S)), "wide_feats": rng.integers(0, 1 << 30, (B, S)).astype(np.int32)}
+    fields = [("labels", nr.FLOAT, 1), ("cont_feats", nr.FLOAT, C), ("cate_feats", nr.INT64, S),
+              ("wide_feats", nr.INT64, S)]
+    outs = [np.full((B, sz), 7, np.float32 if k == nr.FLOAT else np.int64) for _, k, sz in fields]
+    for item in (pickle.dumps(d, protocol=5), pickle.dumps({"labels": d["labels"].tolist(),
+                                                           "cont_feats": d["cont_feats"].tolist(),
+                                                           "cate_feats": d["cate_feats"].tolist(),
+                                                           "wide_feats": d["wide_feats"].tolist()})):
+        assert len(item) >= 4 << 20
+        for o in outs:
+            o.fill(7)
+        assert nr.unpickle_batch_into(item, fields, outs, B) == B
+        for (key, k, sz), o in zip(fields, outs):
+            np.testing.assert_array_equal(o, np.asarray(d[key], o.dtype).reshape(B, sz), err_msg=key)
+    rows = d["cate_feats"].tolist()
+    rows[B - 123] = rows[B - 123][:-1]          # one short row, far from the first piece
+    bad = pickle.dumps(dict(d, cate_feats=rows))
+    assert nr.unpickle_batch_into(bad, fields, outs, B) is None
+
+
 def test_s3_dw_split_counts():
     """engine._s3_dw_splits: the split-K count of an s3 weight gradient fills the CUs in as few
     rounds of 128 x 224 blocks as possible (C2's 8-tile layers keep 32 slabs; C3's layer 0,
