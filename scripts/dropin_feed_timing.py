@@ -12,7 +12,9 @@ import bench  # noqa: E402
 from deep_learning_amd.models import _load_style as ls  # noqa: E402
 from deep_learning_amd.engine import CTREngine  # noqa: E402
 
-T = {"wait": 0.0, "step": 0.0, "decode": 0.0, "n": 0}
+T = {"wait": 0.0, "step": 0.0, "decode": 0.0, "ring": 0.0, "n": 0}
+if os.environ.get("DLAMD_SWITCH"):   # the interpreter's GIL switch interval (s), for A/B
+    sys.setswitchinterval(float(os.environ["DLAMD_SWITCH"]))
 
 
 class TimedFeed(ls.PinnedFeed):
@@ -45,6 +47,17 @@ def timed_step(self, *a, **k):
 
 
 CTREngine.train_step = timed_step
+_rs = CTREngine._ring_status
+
+
+def timed_ring(self, *a, **k):
+    t0 = time.perf_counter()
+    r = _rs(self, *a, **k)
+    T["ring"] += time.perf_counter() - t0
+    return r
+
+
+CTREngine._ring_status = timed_ring
 n = int(sys.argv[1]) if len(sys.argv) > 1 else 16
 _epoch = ls.LoadStyleModel.train_epoch
 passes = []
@@ -65,5 +78,6 @@ ls.LoadStyleModel.train_epoch = timed_epoch
 r = bench.dropin_fit(types.SimpleNamespace(batch=65536), n_batches=n)
 dt, t = passes[-1]
 steps = t["n"]
-print("ms/step %.3f (pass %.3f) | per step: wait %.3f, train_step %.3f, decode (workers) %.3f ms"
-      % (r["ms_per_step"], dt / steps * 1e3, t["wait"] / steps * 1e3, t["step"] / steps * 1e3, t["decode"] / steps * 1e3))
+print("ms/step %.3f (pass %.3f) | per step: wait %.3f, train_step %.3f (ring wait %.3f), decode (workers) %.3f ms"
+      % (r["ms_per_step"], dt / steps * 1e3, t["wait"] / steps * 1e3, t["step"] / steps * 1e3, t["ring"] / steps * 1e3,
+         t["decode"] / steps * 1e3))
