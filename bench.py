@@ -302,7 +302,7 @@ def lookup_alone(eng, batch, B, per_sample, reps=20):
                     "stashes its moments"}
 
 
-def dropin_fit(args, n_batches=12, warm=3):
+def dropin_fit(args, n_batches=24, warm=3):
     """The Wide&Deep drop-in's own training loop at C5 shapes: models/wdl.DeepModel (the
     load-style surface of /root/reference/models/wdl.py:287-316) trained over pickled host
     batches (utils/data_loader_load.py's format: a dict of arrays per batch, unpickled each
@@ -327,16 +327,26 @@ def dropin_fit(args, n_batches=12, warm=3):
                                    "wide_feats": b["wide_feats"]}, protocol=pickle.HIGHEST_PROTOCOL))
     m = wdl.DeepModel(A)
     m.train_epoch(items[:warm])
+    eng = m.model_optimizer()
+    eng.step_events = []     # the compute stream's step spans and the gaps between steps
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     loss_sum, steps = m.train_epoch(items)
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
+    ev, eng.step_events = eng.step_events or [], None
+    starts = [e for k, e in ev if k == 0]
+    ends = [e for k, e in ev if k == 1]
+    span = [a.elapsed_time(b) for a, b in zip(starts, ends)]
+    gap = [b.elapsed_time(a) for b, a in zip(ends, starts[1:])]
     out = {"ms_per_step": round(dt / steps * 1e3, 4), "steps": steps, "samples_per_s": round(steps * args.batch / dt, 1),
            "epoch_mean_loss": round(loss_sum / steps, 6),
-           "note": "wdl.DeepModel.train_epoch over %d pickled C5 batches (B=%d, 26M-row table, bf16 tower): "
-                   "unpickle + staging + step + device-summed loss per step; after a %d-batch warmup pass"
-                   % (n_batches, args.batch, warm)}
+           "compute_stream": {"step_span_ms": round(sum(span) / max(1, len(span)), 4),
+                              "gap_ms": round(sum(gap) / max(1, len(gap)), 4)},
+           "note": "wdl.DeepModel.train_epoch over one %d-batch epoch of pickled C5 batches (B=%d, 26M-row table, "
+                   "bf16 tower): decode + staging + step + device-summed loss per step, the epoch's start included; "
+                   "after a %d-batch warmup pass. compute_stream: the steps' own span and the gap between steps "
+                   "on the device" % (n_batches, args.batch, warm)}
     del m
     torch.cuda.synchronize()
     torch.cuda.empty_cache()

@@ -45,10 +45,20 @@ class PinnedFeed:
     def __init__(self, model, items, workers=None, depth=None):
         self.model = model
         self.items = iter(items)
-        self.workers = workers or int(os.environ.get("DLAMD_FEED_WORKERS", "2"))
+        # one decoding worker (its copies on libdlio's own thread team), three slots: on two boxes
+        # 1.79-1.88 ms a 24-batch C5 epoch step against 1.88-2.09 ms with two workers and four
+        # slots — concurrent decodes slow each other down (0.5 -> 1.0-1.5 ms a batch; profiles/r05bk/)
+        self.workers = workers or int(os.environ.get("DLAMD_FEED_WORKERS", "1"))
         self.depth = depth or int(os.environ.get("DLAMD_FEED_DEPTH", "0")) or self.workers + 2
-        self.bufs = [dict() for _ in range(self.depth)]
-        self.events = [None] * self.depth
+        # the ring's pinned buffers (and each slot's last-use event) are the model's, kept across
+        # epochs: pinning 124 MB afresh made each C5 epoch start 18-22 ms late (profiles/r05bi/)
+        st = getattr(model, "_feed_ring", None)
+        if st is None:
+            st = model._feed_ring = ([], [])
+        while len(st[0]) < self.depth:
+            st[0].append(dict())
+            st[1].append(None)
+        self.bufs, self.events = st
         self.free = [threading.Event() for _ in range(self.depth)]
         for f in self.free:
             f.set()

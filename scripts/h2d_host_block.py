@@ -39,3 +39,40 @@ for i in range(15):
         dst[k].copy_(src[k], non_blocking=True)
     host.append(time.perf_counter() - t0)
 print("behind queued work: host return %.3f ms" % (statistics.median(host[5:]) * 1e3))
+# a side stream that waits on an event of the busy stream, then copies (the engine's prefetch)
+host, wait_host = [], []
+for i in range(15):
+    torch.cuda.synchronize()
+    for _ in range(4):
+        a = a @ a / 64.0
+    ev = torch.cuda.Event()
+    ev.record()
+    t0 = time.perf_counter()
+    side.wait_event(ev)
+    t1 = time.perf_counter()
+    with torch.cuda.stream(side):
+        for k in src:
+            dst[k].copy_(src[k], non_blocking=True)
+    host.append(time.perf_counter() - t1)
+    wait_host.append(t1 - t0)
+print("side stream behind a cross-stream event: wait_event %.3f ms, copies' host return %.3f ms"
+      % (statistics.median(wait_host[5:]) * 1e3, statistics.median(host[5:]) * 1e3))
+# the matmuls alone, for scale
+torch.cuda.synchronize()
+t0 = time.perf_counter()
+for _ in range(4):
+    a = a @ a / 64.0
+torch.cuda.synchronize()
+print("the 4 queued products take %.3f ms on the device" % ((time.perf_counter() - t0) * 1e3))
+# the first copy after the copy path has been idle (the drop-in's epoch start)
+for idle in (0.002, 0.01, 0.05, 0.2):
+    r = []
+    for i in range(6):
+        torch.cuda.synchronize()
+        time.sleep(idle)
+        t0 = time.perf_counter()
+        with torch.cuda.stream(side):
+            dst["label"].copy_(src["label"], non_blocking=True)
+        r.append(time.perf_counter() - t0)
+        torch.cuda.synchronize()
+    print("after %.0f ms idle: first copy's host return %s ms" % (idle * 1e3, [round(x * 1e3, 3) for x in r]))
