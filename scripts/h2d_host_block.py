@@ -76,3 +76,29 @@ for idle in (0.002, 0.01, 0.05, 0.2):
         r.append(time.perf_counter() - t0)
         torch.cuda.synchronize()
     print("after %.0f ms idle: first copy's host return %s ms" % (idle * 1e3, [round(x * 1e3, 3) for x in r]))
+# the side stream behind an event that follows host-to-device copies on the current stream (the
+# drop-in's first step of an epoch: its batch staged on the compute stream, the next one prefetched)
+r = []
+big = {k: v for k, v in src.items() if k != "label"}
+for i in range(8):
+    torch.cuda.synchronize()
+    for k in big:
+        dst[k].copy_(big[k], non_blocking=True)
+    ev = torch.cuda.Event()
+    ev.record()
+    side.wait_event(ev)
+    t0 = time.perf_counter()
+    with torch.cuda.stream(side):
+        dst["label"].copy_(src["label"], non_blocking=True)
+    r.append(time.perf_counter() - t0)
+print("side copy behind the current stream's copies: host return %s ms" % [round(x * 1e3, 3) for x in r])
+r = []
+for i in range(8):
+    torch.cuda.synchronize()
+    for k in big:
+        dst[k].copy_(big[k], non_blocking=True)
+    t0 = time.perf_counter()
+    with torch.cuda.stream(side):
+        dst["label"].copy_(src["label"], non_blocking=True)
+    r.append(time.perf_counter() - t0)
+print("side copy beside (no dependency on) the current stream's copies: host return %s ms" % [round(x * 1e3, 3) for x in r])

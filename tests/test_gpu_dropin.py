@@ -211,10 +211,11 @@ def test_native_pickle_feed_trains_like_the_default_loop(hip_lib, tmp_path, alg,
         res[feed] = (losses, m.model_optimizer().params())
     for k in res["0"][1]:
         np.testing.assert_array_equal(res["1"][1][k], res["0"][1][k], err_msg=k)
-    # the epoch loss: the same per-step losses, summed on the device in double by block atomics
-    # (dl_loss_accumulate), so equal to the last few bits of a double, not bit for bit
+    # the epoch loss: the same per-step losses (the parameters above are bit-identical), summed on
+    # the device by block atomics whose order varies from run to run (dl_loss_accumulate), so
+    # equal to within an f32 unit, not bit for bit (a dnn run differed by 1.2e-9 relative)
     for (a, na), (b, nb) in zip(res["0"][0], res["1"][0]):
-        assert na == nb and abs(a - b) <= 1e-9 * abs(a), (res["0"][0], res["1"][0])
+        assert na == nb and abs(a - b) <= 1e-7 * abs(a), (res["0"][0], res["1"][0])
 
 
 @pytest.mark.parametrize("alg", ["deepfm", "dnn"])
