@@ -177,7 +177,7 @@ def test_native_pickle_feed_trains_like_the_default_loop(hip_lib, tmp_path, alg,
     async copies — two epochs over the same batches (the last one partial, lists-of-lists
     batches as the reference's own loader pickles them, and numpy-array batches) end with the
     same parameters, bit for bit, as the default loop's pickle.loads path (and the same epoch
-    losses to a double's rounding)."""
+    losses to an f32 unit); the second epoch decodes into the first epoch's pinned ring."""
     import importlib
     import pickle
     from deep_learning_amd.synthetic import make_batch
@@ -207,7 +207,13 @@ def test_native_pickle_feed_trains_like_the_default_loop(hip_lib, tmp_path, alg,
     for feed in ("0", "1"):
         monkeypatch.setenv("DLAMD_PINNED_FEED", feed)
         m = mod.DeepModel(Args)
-        losses = [m.train_epoch(tr) for _ in range(2)]
+        losses, ptrs = [], []
+        for _ in range(2):
+            losses.append(m.train_epoch(tr))
+            ring = getattr(m, "_feed_ring", ([], []))[0]
+            ptrs.append(sorted(t.data_ptr() for d in ring for t in d.values()))
+        if feed == "1":   # the ring's pinned buffers are the model's: the second epoch reuses them
+            assert ptrs[0] and ptrs[0] == ptrs[1]
         res[feed] = (losses, m.model_optimizer().params())
     for k in res["0"][1]:
         np.testing.assert_array_equal(res["1"][1][k], res["0"][1][k], err_msg=k)
