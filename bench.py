@@ -209,6 +209,93 @@ def cpu_baseline(spec_kw, B, steps_big=12, warm_big=2, steps_small=50, warm_smal
             "b1024": {"value": 1024 / med1, "median_s": round(med1, 3), "steps": n1, "warmup": w1}}
 
 
+C1 = dict(C=13, V=0, S=26, E=8, cate_index_size=10_000, hidden=[512, 256, 128])
+
+
+def hbm_peak_measured(gib=1.0, reps=10):
+    """The chip's streaming rate measured here (dl_hbm_copy: 16-B pieces, read once, written once),
+    reported beside HBM_PEAK_GBS (the 8 TB/s specification the roofline fractions use)."""
+    import torch
+    from deep_learning_amd import _lib
+    from deep_learning_amd._lib import call, ptr
+    n = int(gib * (1 << 30))
+    a = torch.empty(n, dtype=torch.uint8, device="cuda").fill_(1)
+    b = torch.empty_like(a)
+    s = _lib.stream_handle()
+    for _ in range(3):
+        call("dl_hbm_copy", ptr(a), ptr(b), n, s)
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        call("dl_hbm_copy", ptr(a), ptr(b), n, s)
+    e1.record()
+    torch.cuda.synchronize()
+    us = e0.elapsed_time(e1) * 1e3 / reps
+    assert bool((b[:: 1 << 20] == 1).all())
+    del a, b
+    torch.cuda.empty_cache()
+    return {"GB/s": round(2 * n / (us * 1e-6) / 1e9, 1), "kernel": "dl_hbm_copy (metrics.hip)",
+            "bytes_per_launch": 2 * n, "us": round(us, 1)}
+
+
+def c1_leg(steps_time=50, warm=10, steps_auc=60, n_eval=4, seed=11):
+    """BASELINE configs[0] (C1): models/dnn_pipeline.py at local_run.py's defaults (13 dense +
+    26 cat over a 10k vocab, embedding 8, hidden [512, 256, 128]) — the reference's CPU-runnable
+    plumbing case.  The torch-CPU restatement (oracle/torch_cpu.py, fm=False; TF is absent) is
+    timed at B = 256 (configs[0]) and 1,024 (local_run.py:35): median of `steps_time` steps after
+    `warm`.  Then the restatement and the GPU engine train `steps_auc` steps at B = 256 from the
+    same initial parameters on the same seeded batches, and both score the same `n_eval` unseen
+    batches: their ROC-AUCs (exact tie-aware AUC on each side) and the difference (north star:
+    AUC within 1e-4 of the CPU path)."""
+    import torch
+    from oracle import ctr_ref as R
+    from oracle.torch_cpu import DeepFMPipelineCPU
+    from deep_learning_amd.engine import CTREngine, ModelSpec
+    from deep_learning_amd.synthetic import make_batch
+    threads = torch.get_num_threads()
+    cfg = R.make_cfg("dnn_pipeline", **C1)
+    P0 = R.init_params(cfg, np.random.default_rng(seed))
+    new_cpu = lambda: DeepFMPipelineCPU(C1["C"], C1["S"], C1["E"], C1["cate_index_size"], C1["hidden"], P0, fm=False)
+    out = {"workload": "C1 dnn_pipeline: 13 dense + 26 cat over a 10k vocab, E=8, MLP [512,256,128], TF1 Adam",
+           "kind": "port", "cores": threads}
+    for bsz in (256, 1024):
+        m = new_cpu()
+        bs = [make_batch(bsz, cate_index_size=C1["cate_index_size"], seed=seed + 1 + i) for i in range(8)]
+        for i in range(warm):
+            m.train_step(bs[i % 8])
+        ts = []
+        for i in range(steps_time):
+            t0 = time.perf_counter()
+            m.train_step(bs[i % 8])
+            ts.append(time.perf_counter() - t0)
+        med = float(np.median(ts))
+        out["b%d" % bsz] = {"samples_per_s": round(bsz / med, 1), "median_ms": round(med * 1e3, 3),
+                            "steps": steps_time, "warmup": warm}
+    tr = [make_batch(256, cate_index_size=C1["cate_index_size"], seed=1000 + i) for i in range(steps_auc)]
+    ev = [make_batch(1024, cate_index_size=C1["cate_index_size"], seed=2000 + i) for i in range(n_eval)]
+    m = new_cpu()
+    for b in tr:
+        m.train_step(b)
+    with torch.no_grad():
+        s_cpu = np.concatenate([torch.sigmoid(m.forward(b)[0]).double().numpy() for b in ev])
+    eng = CTREngine(ModelSpec("dnn_pipeline", **C1), max_batch=1024, init="none")
+    eng.load_params(P0)
+    for b in tr:
+        eng.train_step(b)
+    s_gpu = np.concatenate([eng.predict(b).astype(np.float64) for b in ev])
+    y = np.concatenate([b["label"].reshape(-1) for b in ev])
+    a_cpu, a_gpu = R.auc(y, s_cpu), R.auc(y, s_gpu)
+    out["auc"] = {"cpu_restatement": round(a_cpu, 6), "gpu_engine": round(a_gpu, 6),
+                  "abs_diff": float("%.3g" % abs(a_cpu - a_gpu)), "train_steps": steps_auc, "batch": 256,
+                  "eval_samples": int(y.size), "max_abs_score_diff": float("%.3g" % np.abs(s_cpu - s_gpu).max())}
+    del eng
+    torch.cuda.synchronize()
+    torch.cuda.empty_cache()
+    log("C1 leg: CPU %s samples/s at B=256, AUC cpu %.6f gpu %.6f" % (out["b256"]["samples_per_s"], a_cpu, a_gpu))
+    return out
+
+
 def vocab_for(wl, args, sharded):
     """Per-field vocab of a workload: --vocab, else 1M (C2, C3, C5 at every N) or, for the
     sharded DeepFM (C4), 100M rows over the 26 fields."""
@@ -505,7 +592,13 @@ def _run_workload(wl, args, world, rank, sharded, steps, warmup, age, ksteps, ba
             else:
                 ent["TFLOP/s"] = round(amount / (us * 1e-6) / 1e12, 2)
                 ent["frac_mfma"] = round(amount / (us * 1e-6) / 1e12 / gemm_peak, 3)
+                if s3:   # against the native f32 matrix peak too (157.3 TF): above 1.0 by design
+                    ent["frac_f32_mfma_peak"] = round(amount / (us * 1e-6) / 1e12 / F32_MFMA_PEAK_TFLOPS, 3)
         kernels[label] = ent
+    # where the step's time went, one compact line on stderr (kept by a log's tail)
+    log("%s per-kernel us/launch: %s" % (wl, ", ".join(
+        "%s %.0f%s" % (k, v["us"], "x%d" % v["launches"] if v["launches"] > 1 else "")
+        for k, v in sorted(kernels.items(), key=lambda kv: -kv[1]["us"] * kv[1]["launches"]))))
     # the dominant kernel among those with an algorithmic work figure
     dom = max((l for l in kernels if l in work), key=lambda l: kernels[l]["us"])
     kind, amount = work.get(dom, ("hbm", 0))
@@ -519,6 +612,8 @@ def _run_workload(wl, args, world, rank, sharded, steps, warmup, age, ksteps, ba
         roof = {"kernel": dom, "bound": "mfma", "achieved": round(ach, 2), "peak": round(gemm_peak, 1),
                 "unit": "TFLOP/s", "frac": round(ach / gemm_peak, 3), "traffic": None,
                 "algorithmic_flops": amount}
+        if s3:
+            roof["frac_f32_mfma_peak"] = round(ach / F32_MFMA_PEAK_TFLOPS, 3)
     pmc = pmc_traffic(dom, world, lazy=uniq is not None, workload=wl, id_dist=id_dist)
     if pmc is not None:
         roof["traffic"] = pmc["hbm_bytes"]
@@ -565,7 +660,8 @@ def _run_workload(wl, args, world, rank, sharded, steps, warmup, age, ksteps, ba
                kernel_sum=sum(k["us"] for k in kernels.values()), nb=nb, gemm_peak=gemm_peak, host_ms=host_ms,
                step_events=step_ev)
     if sharded:
-        out["shard"] = {"cap": eng.cap, "overflows": getattr(eng, "overflows", 0), "report_lag": eng.lag}
+        out["shard"] = {"cap": eng.cap, "overflows": getattr(eng, "overflows", 0), "report_lag": eng.lag,
+                        "all_reduce_serial": eng.ar_serial, "exchange_bytes_per_rank": eng.exchange_bytes()}
         eng.exch.close()
     del eng, batches
     torch.cuda.synchronize()
@@ -740,6 +836,20 @@ def main():
             cpu = cpu_baseline(C2, B)
         except Exception as e:  # reported, never fatal for the GPU number
             cpu = {"value": None, "error": repr(e)}
+        try:
+            cpu["c1"] = c1_leg()
+        except Exception as e:  # reported, never fatal
+            cpu["c1"] = {"error": repr(e)}
+    peak_meas = None
+    if rank == 0:
+        try:
+            peak_meas = hbm_peak_measured()
+            log("measured HBM copy peak %.1f GB/s" % peak_meas["GB/s"])
+        except Exception as e:  # reported, never fatal
+            peak_meas = {"error": repr(e)}
+        if r["roofline"]["bound"] == "hbm" and "GB/s" in peak_meas:
+            r["roofline"]["peak_measured"] = peak_meas["GB/s"]
+            r["roofline"]["frac_of_measured"] = round(r["roofline"]["achieved"] / peak_meas["GB/s"], 3)
 
     if rank == 0:
         out = {
@@ -773,6 +883,7 @@ def main():
             "distinct_batches": r["nb"],
             "table_age_steps": args.age_steps,
             "gemm_peak_tflops": round(r["gemm_peak"], 1),
+            "hbm_copy_measured": peak_meas,
             "kernels": r["kernels"],
             "kernel_sum_us_per_step": round(r["kernel_sum"], 1),
             "host_submit_ms_per_step": round(r["host_ms"], 4),

@@ -53,6 +53,17 @@ STATUS_BAD_ID, STATUS_LAG, STATUS_INDEX, STATUS_OVERFLOW, STATUS_DESYNC = 1, 2, 
 REC_FIRST, REC_SPARSE_ADAM, REC_PLANE_SLOTS = 1, 2, 4
 ROWS_CLEAR_TOUCHED, ROWS_SPARSE_ADAM, ROWS_GRAD_FIXED = 1, 2, 4
 WIDE_GRAD_SCALE = 2.0 ** 48
+REG_SUM_SCALE = 2.0 ** 32   # int64 fixed-point regulariser sums (DL_REG_SUM_SCALE, opt[DL_OPT_REG])
+OPT_REG = 8
+
+
+def reg_sum(q):
+    """A fixed-point regulariser sum (an int64 device or host tensor element, or the opt block:
+    its opt[DL_OPT_REG..+1]) as a Python float."""
+    import torch
+    if q.dtype == torch.float32:
+        q = q[OPT_REG: OPT_REG + 2].view(torch.int64)
+    return int(q.reshape(-1)[0].item()) / REG_SUM_SCALE
 LOSS_ACC_SLOTS = 65536
 
 P = C.c_void_p
@@ -134,6 +145,7 @@ SIGNATURES = {
     "dl_rec_apply_chain": (I32, [P, I32, I32, I32, P, I64, P, P, P, P, P, I32, P, P]),
     "dl_auc_workspace_bytes": (I64, [I64]),
     "dl_auc": (I32, [P, I64, P, I64, I64, P, I64, P, P]),
+    "dl_hbm_copy": (I32, [P, P, I64, P]),
     "dl_shard_gather_scalar": (I32, [P, P, I64, P, P]),
     "dl_shard_add_fixed": (I32, [P, P, I64, P, P, P]),
     "dl_wide_fold_owned": (I32, [P, I32, I64, I32, I32, P, P, P]),

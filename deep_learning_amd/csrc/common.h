@@ -45,8 +45,12 @@ __device__ __forceinline__ float wave_sum(float v) {
 // device-scope atomics on one address serialise across the XCDs (~12 ns each measured — a
 // per-wave atomic over a 26 M-row sweep cost ~100 us, over 1.7 M wide rows ~300 us), so
 // kernels that use it also cap their grid (kSumGrid blocks, grid-stride loops).
+// The block's partial (a fixed-order wave and block sum) is added as 64-bit fixed point
+// (units 1/DL_REG_SUM_SCALE, include/dlamd.h): integer adds are associative, so the total is
+// the same bits whichever order the blocks land in (a float atomic made the printed loss vary
+// from run to run in its last bits).
 constexpr unsigned kSumGrid = 1024;
-__device__ __forceinline__ void block_atomic_add(float x, float* out) {
+__device__ __forceinline__ void block_fixed_add(float x, int64_t* out) {
   __shared__ float part[16];
   x = wave_sum(x);
   if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = x;
@@ -54,9 +58,13 @@ __device__ __forceinline__ void block_atomic_add(float x, float* out) {
   if (threadIdx.x == 0) {
     float t = 0.f;
     for (int w = 0; w < (int)(blockDim.x >> 6); ++w) t += part[w];
-    if (t != 0.f) atomicAdd(out, t);
+    if (t != 0.f)
+      atomicAdd(reinterpret_cast<unsigned long long*>(out),
+                (unsigned long long)__double2ll_rn((double)t * DL_REG_SUM_SCALE));
   }
 }
+// a fixed-point regulariser sum as a double
+__device__ __forceinline__ double reg_sum_value(const int64_t* q) { return (double)*q * (1.0 / DL_REG_SUM_SCALE); }
 
 // Reads id and validates it against [0, n); out-of-range -> row -1 + error word.
 __device__ __forceinline__ int64_t checked_row(int64_t id, int64_t off, int64_t n, int32_t* err) {

@@ -250,3 +250,35 @@ extern "C" int dl_auc(const float* scores, int64_t s_stride, const float* labels
   hipLaunchKernelGGL(auc_final_kernel, dim3(1), dim3(1), 0, s, w.acc, m, out);
   DL_RETURN_LAUNCH("dl_auc");
 }
+
+// ---------------------------------------------------------------------------
+// The measured HBM yardstick (bench.py roofline.peak_measured): a streaming copy of whole 16-B
+// pieces, four in flight per thread, grid-stride over a grid that fills every CU.  What a plain
+// read-once / write-once stream reaches on this chip, beside the 8 TB/s specification the
+// roofline fractions are priced against.
+__global__ __launch_bounds__(256) void hbm_copy_kernel(const uint4* __restrict__ src, uint4* __restrict__ dst,
+                                                       long long n16) {
+  const long long stride = (long long)gridDim.x * blockDim.x;
+  long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  for (; i + 3 * stride < n16; i += 4 * stride) {
+    const uint4 a = src[i], b = src[i + stride], c = src[i + 2 * stride], d = src[i + 3 * stride];
+    dst[i] = a;
+    dst[i + stride] = b;
+    dst[i + 2 * stride] = c;
+    dst[i + 3 * stride] = d;
+  }
+  for (; i < n16; i += stride) dst[i] = src[i];
+}
+
+extern "C" int dl_hbm_copy(const void* src, void* dst, int64_t bytes, void* stream) {
+  DL_CHECK_ARG(src && dst && bytes >= 0 && bytes % 16 == 0, "dl_hbm_copy: bad arguments (bytes %lld)",
+               (long long)bytes);
+  DL_CHECK_ARG(((uintptr_t)src | (uintptr_t)dst) % 16 == 0, "dl_hbm_copy: 16-B alignment");
+  if (bytes == 0) return 0;
+  const long long n16 = bytes / 16;
+  const long long want = (n16 + 1023) / 1024;   // ~4 pieces a thread a round
+  const unsigned grid = (unsigned)std::max(1LL, std::min(want, 256LL * 16));
+  hipLaunchKernelGGL(hbm_copy_kernel, dim3(grid), dim3(256), 0, as_stream(stream), reinterpret_cast<const uint4*>(src),
+                     reinterpret_cast<uint4*>(dst), n16);
+  DL_RETURN_LAUNCH("dl_hbm_copy");
+}

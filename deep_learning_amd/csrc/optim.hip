@@ -23,7 +23,7 @@ __device__ __forceinline__ void adam_begin_body(float* opt, float decay_rate, fl
   opt[0] = b1p * opt[4];                                         // Adam._finish
   opt[1] = b2p * opt[5];
   opt[7] = step + 1.f;                                           // global_step += 1
-  for (int i = 8; i < 16; ++i) opt[i] = 0.f;                     // per-step L2 accumulators
+  for (int i = 8; i < 16; ++i) opt[i] = 0.f;                     // per-step L2 accumulators (all-zero bits)
 }
 
 __global__ void adam_begin_kernel(float* opt, float decay_rate, float decay_steps) {
@@ -50,8 +50,8 @@ __global__ void step_guard_kernel(const int32_t* batch_err, float* opt) { step_g
 // The running loss of a training loop — the load-style fit's epoch mean of the per-step loss
 // (wdl.py:305-313, deepfm.py:172-190, dnn.py:111-127 sum loss_t * batch_size over the epoch):
 // acc[0] += the step's data term (the head slab's loss column summed in a fixed order, in
-// double, times inv_b); acc[1] += reg_coef * opt[8] (the step's regulariser sum, accumulated by
-// the Adam kernels); acc[2] += 1.  A skipped step (bad batch) adds nothing.  One block, so the
+// double, times inv_b); acc[1] += reg_coef * the step's regulariser sum (the int64 fixed-point
+// accumulator at opt[DL_OPT_REG], added to by the Adam kernels); acc[2] += 1.  A skipped step (bad batch) adds nothing.  One block, so the
 // step needs no host read; the host reads acc once per epoch.
 // ring (may be NULL): the step's status report into pinned host memory, in place of a
 // device-to-host copy after the step — every step (skipped ones too) advances the sequence
@@ -85,7 +85,7 @@ __global__ __launch_bounds__(256) void loss_accumulate_kernel(const float* __res
   }
   if (threadIdx.x == 0) {
     acc[0] += part[0] * inv_b;
-    acc[1] += (double)reg_coef * (double)opt[8];
+    acc[1] += (double)reg_coef * reg_sum_value(reinterpret_cast<const int64_t*>(opt + DL_OPT_REG));
     acc[2] += 1.0;
   }
 }
@@ -176,7 +176,7 @@ __global__ __launch_bounds__(256) void adam_dense_thread_kernel(float* __restric
                                                                 const float* __restrict__ slab, int nslab,
                                                                 long long stride, long long n, float l2,
                                                                 long long l2_count, const float* __restrict__ opt,
-                                                                float* __restrict__ p_prev, float* __restrict__ sq_out,
+                                                                float* __restrict__ p_prev, int64_t* __restrict__ sq_out,
                                                                 Split3Out so = {}) {
   if (step_poisoned(opt)) return;
   const float alpha = opt[3], omb1 = 1.f - opt[4], omb2 = 1.f - opt[5], eps = opt[6];
@@ -226,7 +226,7 @@ __global__ __launch_bounds__(256) void adam_dense_thread_kernel(float* __restric
       so.wtp[(long long)c * so.rows + r] = h;
     }
   }
-  if (sq_out) block_atomic_add(sq, sq_out);
+  if (sq_out) block_fixed_add(sq, sq_out);
 }
 
 // Several tower weights in one launch (dl_adam_dense_layers): thread i of the concatenated
@@ -296,7 +296,7 @@ __global__ __launch_bounds__(256) void adam_dense_layers_kernel(AdamLayersArg a,
   }
   for (int k = 0; k < a.nl; ++k)   // the regulariser terms (uniform branch: every thread joins)
     if (a.l[k].acc_out) {
-      block_atomic_add(sq[k], a.l[k].acc_out);
+      block_fixed_add(sq[k], a.l[k].acc_out);
       __syncthreads();             // block_atomic_add's partials are reused by the next layer
     }
 }
@@ -308,7 +308,7 @@ __global__ __launch_bounds__(256) void adam_dense_wave_kernel(float* __restrict_
                                                               const float* __restrict__ slab, int nslab,
                                                               long long stride, long long n, float l2,
                                                               long long l2_count, const float* __restrict__ opt,
-                                                              float* __restrict__ p_prev, float* __restrict__ sq_out) {
+                                                              float* __restrict__ p_prev, int64_t* __restrict__ sq_out) {
   if (step_poisoned(opt)) return;
   const long long i = ((long long)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   const int lane = threadIdx.x & 63;
@@ -328,7 +328,7 @@ __global__ __launch_bounds__(256) void adam_dense_wave_kernel(float* __restrict_
       p[i] = pi; m[i] = mi; v[i] = vi;
     }
   }
-  if (sq_out) block_atomic_add(sq, sq_out);
+  if (sq_out) block_fixed_add(sq, sq_out);
 }
 
 // Table element update in the reference's form for the table: ApplyAdam (dense) or the
@@ -353,7 +353,7 @@ __global__ __launch_bounds__(256) void adam_rows4_kernel(float4* __restrict__ p,
                                                          float4* __restrict__ v, float4* __restrict__ g,
                                                          const uint8_t* __restrict__ touched, long long n4,
                                                          int lpr, float l2, const float* __restrict__ opt,
-                                                         float* __restrict__ sq_out) {
+                                                         int64_t* __restrict__ sq_out) {
   const float alpha = opt[3], b1 = opt[4], b2 = opt[5], omb1 = 1.f - opt[4], omb2 = 1.f - opt[5], eps = opt[6];
   const RootDecay rd = root_decay(b2);
   const bool skip = step_poisoned(opt);   // consume the gradients, apply nothing
@@ -376,7 +376,7 @@ __global__ __launch_bounds__(256) void adam_rows4_kernel(float4* __restrict__ p,
     table_adam<SPARSE, true>(pi.w, mi.w, vi.w, gi.w, alpha, b1, b2, omb1, omb2, rd, eps);
     p[i] = pi; m[i] = mi; v[i] = vi;
   }
-  if (sq_out) block_atomic_add(sq, sq_out);
+  if (sq_out) block_fixed_add(sq, sq_out);
 }
 
 // Width-1 tables (first-order weights): one thread per 4 rows.
@@ -385,7 +385,7 @@ __global__ __launch_bounds__(256) void adam_rows1_kernel(float* __restrict__ p, 
                                                          float* __restrict__ v, void* __restrict__ g_,
                                                          uint8_t* __restrict__ touched, long long n,
                                                          float l2, int clear, const float* __restrict__ opt,
-                                                         float* __restrict__ sq_out) {
+                                                         int64_t* __restrict__ sq_out) {
   const float alpha = opt[3], b1 = opt[4], b2 = opt[5], omb1 = 1.f - opt[4], omb2 = 1.f - opt[5], eps = opt[6];
   const RootDecay rd = root_decay(b2);
   const bool skip = step_poisoned(opt);
@@ -444,7 +444,7 @@ __global__ __launch_bounds__(256) void adam_rows1_kernel(float* __restrict__ p, 
       }
     }
   }
-  if (sq_out) block_atomic_add(sq, sq_out);
+  if (sq_out) block_fixed_add(sq, sq_out);
 }
 
 __global__ void clear_touched_kernel(uint8_t* touched, long long n) {
@@ -546,7 +546,7 @@ extern "C" int dl_step_begin(const int32_t* batch_err, float* opt, float decay_r
 
 extern "C" int dl_adam_dense_reg(float* p, float* m, float* v, const float* slab, int32_t nslab,
                                  int64_t slab_stride, int64_t n, float reg, int64_t reg_count, int32_t reg_kind,
-                                 const float* opt, float* p_prev, float* acc_out, void* stream) {
+                                 const float* opt, float* p_prev, int64_t* acc_out, void* stream) {
   DL_CHECK_ARG(p && m && v && slab && opt, "NULL pointer");
   DL_CHECK_ARG(nslab >= 1 && slab_stride >= n, "bad slabs");
   DL_CHECK_ARG(reg_kind == 0 || reg_kind == 1, "reg_kind must be 0 (L2) or 1 (L1)");
@@ -570,7 +570,7 @@ extern "C" int dl_adam_dense_reg(float* p, float* m, float* v, const float* slab
 template <int NPL>
 static int adam_dense_copies(float* p, float* m, float* v, const float* slab, int32_t nslab, int64_t slab_stride,
                              int32_t rows, int32_t cols, float reg, int64_t reg_count, int32_t reg_kind,
-                             const float* opt, float* acc_out, uint16_t* wp, uint16_t* wtp, void* stream) {
+                             const float* opt, int64_t* acc_out, uint16_t* wp, uint16_t* wtp, void* stream) {
   DL_CHECK_ARG(p && m && v && slab && opt && wp && wtp, "NULL pointer");
   const long long n = (long long)rows * cols;
   DL_CHECK_ARG(rows > 0 && cols > 0 && nslab >= 1 && slab_stride >= n, "bad shape / slabs");
@@ -587,7 +587,7 @@ static int adam_dense_copies(float* p, float* m, float* v, const float* slab, in
 
 extern "C" int dl_adam_dense_split3(float* p, float* m, float* v, const float* slab, int32_t nslab,
                                     int64_t slab_stride, int32_t rows, int32_t cols, float reg, int64_t reg_count,
-                                    int32_t reg_kind, const float* opt, float* acc_out, uint16_t* wp, uint16_t* wtp,
+                                    int32_t reg_kind, const float* opt, int64_t* acc_out, uint16_t* wp, uint16_t* wtp,
                                     void* stream) {
   return adam_dense_copies<3>(p, m, v, slab, nslab, slab_stride, rows, cols, reg, reg_count, reg_kind, opt, acc_out,
                               wp, wtp, stream);
@@ -621,7 +621,7 @@ extern "C" int dl_adam_dense_layers(int32_t n_layers, const dl_adam_layer* layer
 
 extern "C" int dl_adam_dense_bf16(float* p, float* m, float* v, const float* slab, int32_t nslab,
                                   int64_t slab_stride, int32_t rows, int32_t cols, float reg, int64_t reg_count,
-                                  int32_t reg_kind, const float* opt, float* acc_out, uint16_t* wb, uint16_t* wbt,
+                                  int32_t reg_kind, const float* opt, int64_t* acc_out, uint16_t* wb, uint16_t* wbt,
                                   void* stream) {
   return adam_dense_copies<1>(p, m, v, slab, nslab, slab_stride, rows, cols, reg, reg_count, reg_kind, opt, acc_out,
                               wb, wbt, stream);
@@ -629,12 +629,12 @@ extern "C" int dl_adam_dense_bf16(float* p, float* m, float* v, const float* sla
 
 extern "C" int dl_adam_dense(float* p, float* m, float* v, const float* slab, int32_t nslab,
                              int64_t slab_stride, int64_t n, float l2, int64_t l2_count,
-                             const float* opt, float* p_prev, float* sq_out, void* stream) {
+                             const float* opt, float* p_prev, int64_t* sq_out, void* stream) {
   return dl_adam_dense_reg(p, m, v, slab, nslab, slab_stride, n, l2, l2_count, 0, opt, p_prev, sq_out, stream);
 }
 
 extern "C" int dl_adam_rows(float* p, float* m, float* v, void* g, uint8_t* touched, int64_t n_rows,
-                            int32_t width, float l2, int32_t rows_flags, const float* opt, float* sq_out,
+                            int32_t width, float l2, int32_t rows_flags, const float* opt, int64_t* sq_out,
                             void* stream) {
   const int clear_touched = rows_flags & DL_ROWS_CLEAR_TOUCHED;
   const bool sparse = (rows_flags & DL_ROWS_SPARSE_ADAM) != 0;

@@ -219,7 +219,7 @@ __global__ __launch_bounds__(256) void wide_rec_update_deep_kernel(float4* __res
 __global__ __launch_bounds__(256) void wide_rec_flush_kernel(float4* __restrict__ rec, long long w_rows, float l2,
                                                              const float* __restrict__ hist, int hist_len,
                                                              const float* __restrict__ opt,
-                                                             float* __restrict__ sq_untouched, double* __restrict__ acc) {
+                                                             int64_t* __restrict__ sq_untouched, double* __restrict__ acc) {
   const WideHyper h = wide_hyper(opt, l2, hist_len);
   const int t = (int)opt[7];
   float sq = 0.f, run = 0.f;
@@ -234,7 +234,7 @@ __global__ __launch_bounds__(256) void wide_rec_flush_kernel(float4* __restrict_
     wide_catch_up(r.x, r.y, r.z, t - 1, t, hist, h);
     rec[row * kWideRecF4] = make_float4(r.x, r.y, r.z, __int_as_float(t));
   }
-  if (sq_untouched) block_atomic_add(sq, sq_untouched);
+  if (sq_untouched) block_fixed_add(sq, sq_untouched);
   if (acc) block_sum_accumulate(run, acc);
 }
 
@@ -364,7 +364,7 @@ extern "C" int dl_wide_rec_update(float* rec, const int32_t* n_uniq, int64_t max
 }
 
 extern "C" int dl_wide_rec_flush(float* rec, int64_t w_rows, float l2, const float* hist, int32_t hist_len,
-                                 const float* opt, float* sq_untouched, double* acc, void* stream) {
+                                 const float* opt, int64_t* sq_untouched, double* acc, void* stream) {
   DL_CHECK_ARG(rec && hist && opt, "NULL argument");
   DL_CHECK_ARG(hist_len >= 2 && (hist_len & (hist_len - 1)) == 0, "hist_len must be a power of two");
   if (w_rows <= 0) return 0;

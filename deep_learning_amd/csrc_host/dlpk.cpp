@@ -57,8 +57,8 @@ struct Parser {
 
   Parser(const uint8_t* data, int64_t len) : d(data), n(len) { vals.reserve(1024); }
 
-  bool need(int64_t k) {
-    if (pos + k > n) { status = -1; return false; }
+  bool need(int64_t k) {   // k more bytes at pos; k from an 8-byte length may be near INT64_MAX
+    if (k < 0 || k > n - pos) { status = -1; return false; }
     return true;
   }
   uint64_t rd(int k) {   // little-endian unsigned

@@ -325,7 +325,7 @@ class CTREngine:
             self.wlong = z(nw + 1, dt=torch.int32)   # dl_wide_seg_grad's hot-row list
             # the update kernels' per-block partial sums of the touched rows' L2 term
             self.wsq_part = z(max(1, int(_lib.lib().dl_wide_update_blocks(nw, Hh))))
-            self.wsq = z(4)                      # L2 term of the rows the last step left (from a flush)
+            self.wsq = z(2, dt=torch.int64)      # L2 term of the rows the last step left (a flush; fixed point)
             self._wsq_step = -1
             # the running loss's wide L2 term (loss_sum_begin / loss_sum_end): per-block slots the
             # update and flush kernels add to, and each unique row's replayed steps' w^2 (gather)
@@ -1492,7 +1492,7 @@ class CTREngine:
 
     def loss(self):
         """Loss of the last training step: data term + the L2 terms on the pre-update
-        weights (accumulated by the Adam kernels into opt[8])."""
+        weights (accumulated by the Adam kernels into opt[DL_OPT_REG], int64 fixed point)."""
         sp = self.spec
         H = sp.hidden[-1]
         B = self.last_batch
@@ -1500,15 +1500,15 @@ class CTREngine:
         rows = call_int(self.head_grid, B)
         data = self.head_slab[:rows, width - 1].double().sum().item() / B
         if sp.hidden_reg == "l1":   # l1_regularizer: scale * sum |W| (dnn.py:88-90)
-            return data + sp.l2 * float(self.opt[8].item())
-        reg = float(self.opt[8].item())
+            return data + sp.l2 * _lib.reg_sum(self.opt)
+        reg = _lib.reg_sum(self.opt)
         if getattr(self, "wide_lazy", False):
             # the wide rows the step left untouched: their L2 term from a flush (wide.hip); the
             # touched rows' from the update's block partials — only the blocks this batch size
             # launched (a smaller last batch leaves an earlier batch's partials beyond them)
             self._wide_flush()
             nparts = int(_lib.lib().dl_wide_update_blocks(B * sp.Fw, H))
-            reg += float(self.wsq[0].item()) + float(self.wsq_part[:nparts].double().sum().item())
+            reg += _lib.reg_sum(self.wsq) + float(self.wsq_part[:nparts].double().sum().item())
         return data + sp.l2 * 0.5 * reg
 
     def loss_sum_begin(self):

@@ -67,6 +67,7 @@ class PinnedFeed:
         self.k = 0
         self.lock = threading.Lock()
         self.done = False
+        self.aborted = False
         for _ in range(self.depth):
             self._submit()
 
@@ -107,7 +108,9 @@ class PinnedFeed:
     def _prepare(self, k, item):
         s = k % self.depth
         self.free[s].wait()       # the slot's previous batch has been released (one claimant a slot:
-        self.free[s].clear()      # batch k + depth is submitted only once batch k was taken)
+        if self.aborted:          # batch k + depth is submitted only once batch k was taken), or the
+            return None           # loop stopped on an exception (close(abort=True) sets every slot)
+        self.free[s].clear()
         ev = self.events[s]
         if ev is not None:
             ev.synchronize()
@@ -143,8 +146,17 @@ class PinnedFeed:
         self.events[s] = ev
         self.free[s].set()
 
-    def close(self):
-        self.pool.shutdown(wait=True)
+    def close(self, abort=False):
+        """Wait for the workers.  abort (the loop stopped on an exception — a bad-id DLError, an
+        interrupt — with batches still held): every slot is released and the queued decodes are
+        dropped first, so a worker waiting for a slot the loop will never release returns at
+        once instead of hanging the shutdown."""
+        if abort:
+            with self.lock:
+                self.aborted = self.done = True
+            for f in self.free:
+                f.set()
+        self.pool.shutdown(wait=True, cancel_futures=abort)
 
 
 class LoadStyleModel:
@@ -213,6 +225,7 @@ class LoadStyleModel:
                 eng.check_error()
             return loss_sum, steps
         feed = PinnedFeed(self, train_data)
+        ok = False
         try:
             items = iter(feed)
             b = next(items, None)
@@ -222,8 +235,9 @@ class LoadStyleModel:
                 feed.release(b)
                 steps += 1
                 b = nxt
+            ok = True
         finally:
-            feed.close()
+            feed.close(abort=not ok)
         loss_sum, counted = eng.loss_sum_end()
         if counted != steps:
             eng.check_error()   # a skipped (bad) batch raises here, as its sess.run did

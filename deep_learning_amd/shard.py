@@ -121,8 +121,9 @@ class Exchange:
                 if p != me:
                     a[p if direction == 0 else self.block(p)].copy_(recv[p])
 
-    def all_reduce(self, t, stream=None):
-        """Sum over the ranks, in place (inside the step: RCCL on `stream`)."""
+    def all_reduce(self, t, stream=None, serial=False):
+        """Sum over the ranks, in place (inside the step: RCCL on `stream`; serial: on the block
+        exchanges' communicator, else on the all-reduce's own)."""
         if self.world == 1:
             return t
         if self.staged:
@@ -130,8 +131,8 @@ class Exchange:
             dist.all_reduce(c, group=self.group)
             t.copy_(c)
             return t
-        _, comm_ar = self._comms()
-        call("dl_all_reduce_f32", comm_ar, ptr(t), ptr(t), t.numel(), _lib.stream_handle(stream))
+        comm, comm_ar = self._comms()
+        call("dl_all_reduce_f32", comm if serial else comm_ar, ptr(t), ptr(t), t.numel(), _lib.stream_handle(stream))
         return t
 
     def host_sum(self, t):
@@ -167,6 +168,10 @@ class ShardedCTREngine(CTREngine):
                  owner_update=None, slack=None, lag=2):
         if spec.model not in ("deepfm_pipeline", "dnn_pipeline", "wdl"):
             raise ValueError("sharded path supports deepfm_pipeline / dnn_pipeline / wdl")
+        # the status ring holds 4 reports (slot k & 3) and the host reads report k only after
+        # k + lag was submitted: lag <= 3, or report k + 4 overwrites k before it is read
+        if not 0 <= int(lag) <= 3:
+            raise ValueError("lag must be 0..3 (the status ring holds 4 reports), got %r" % (lag,))
         self.exch = exch
         self.world, self.rank = exch.world, exch.rank
         N = spec.n_rows
@@ -180,7 +185,15 @@ class ShardedCTREngine(CTREngine):
         self.side = None
         self.host_marks = [] if os.environ.get("DLAMD_HOST_TIMING") else None
         self.slack = float(os.environ.get("DLAMD_SHARD_SLACK", self.SLACK)) if slack is None else float(slack)
-        self.lag = max(0, int(lag))
+        self.lag = int(lag)
+        # DLAMD_SHARD_AR_SERIAL (default 1): the flat all-reduce on the exchange communicator and
+        # stream, after the gradient exchange — every RCCL kernel of the step on one communicator
+        # in one order; 0: on a second communicator and stream, beside the gradient exchange
+        # (why serial is the default)
+        self.ar_serial = os.environ.get("DLAMD_SHARD_AR_SERIAL", "1") != "0"
+        # the host's wait for a step's status report: past this many seconds the process exits
+        # non-zero (a peer stuck in a collective cannot keep the job hanging silently)
+        self.guard_s = float(os.environ.get("DLAMD_SHARD_GUARD_S", "60"))
         if self.lazy:
             # owners group a step's arrivals by row with a sort (dl_sort_unique + apply_segments) or
             # per-row arrival chains (dl_rec_chain_link + apply_chain); bit-identical records
@@ -313,7 +326,7 @@ class ShardedCTREngine(CTREngine):
         self.ww, self.wm, self.wv = z(wl), z(wl), z(wl)
         self.wg = z(wl, dt=torch.int64)
         self.w_touched = z(wl, dt=torch.uint8)
-        self.wide_reg = z(4)
+        self.wide_reg = z(2, dt=torch.int64)   # the shard's L2 sum (fixed point, DL_REG_SUM_SCALE)
         nw = B * Fw
         self.n_wrefs = nw
         self.in_wide_loc = z(B, Fw, dt=torch.int64)
@@ -464,6 +477,26 @@ class ShardedCTREngine(CTREngine):
         oc = self.owner_counts.tolist()
         h = self.hdr_all[: 4 * W].view(W, 4)[:, 0].tolist()
         return sum(oc[:W]), oc[W], sum(h)
+
+    def exchange_bytes(self):
+        """Bytes this rank SENDS over the interconnect per training step (its own block never
+        moves; every exchange moves whole fixed-size blocks, so these are the step's sizes, not
+        its counts): the requests (ids + 16-B headers), the answers (rows + first-order weights
+        + wide values), the gradients back to the owners, and the flat all-reduce as a ring sends
+        it (2 (W - 1) / W of the buffer)."""
+        W, cap, E = self.world, self.cap, self.spec.E
+        p = W - 1
+        fm = 4 if self.spec.fm else 0
+        out = {"requests": p * (cap * 4 + 16), "answers": p * cap * (E * 4 + fm),
+               "gradients": p * cap * (E * 4 + fm)}
+        if self.wdl:
+            out["requests"] += p * (self.wcap * 4 + 16)
+            out["answers"] += p * self.wcap * 4
+            out["gradients"] += p * self.wcap * 8
+        out["all_reduce"] = int(self.flat.numel() * 4 * 2 * p / W) if W > 1 else 0
+        out["total"] = sum(out.values())
+        out["block_slots"] = cap
+        return out
 
     # ------------------------------------------------------------ the step's pieces
     def _mark(self, name):
@@ -874,12 +907,20 @@ class ShardedCTREngine(CTREngine):
         with torch.cuda.stream(x):
             self._c("x_grads", "exchange", lambda: self.exch.blocks(garrs, 0, x))
         self._weight_grads(B, s)
-        # the dense all-reduce on the second communicator's stream, beside the gradient exchange
-        a = self.ar_stream
-        a.wait_stream(main)
-        with torch.cuda.stream(a):
-            self._c("all_reduce", "exchange", lambda: self.exch.all_reduce(self.flat, a))
-        main.wait_stream(a)
+        if self.ar_serial:
+            # the dense all-reduce after the gradient exchange, on its communicator and stream:
+            # one RCCL kernel at a time, in the same order on every rank
+            x.wait_stream(main)
+            with torch.cuda.stream(x):
+                self._c("all_reduce", "exchange", lambda: self.exch.all_reduce(self.flat, x, serial=True))
+            main.wait_stream(x)
+        else:
+            # the dense all-reduce on the second communicator's stream, beside the gradient exchange
+            a = self.ar_stream
+            a.wait_stream(main)
+            with torch.cuda.stream(a):
+                self._c("all_reduce", "exchange", lambda: self.exch.all_reduce(self.flat, a))
+            main.wait_stream(a)
         self._dense_adam(B, s)
         main.wait_stream(x)
         if own:
@@ -980,8 +1021,8 @@ class ShardedCTREngine(CTREngine):
                 spins += 1
                 if spins > 1000:
                     time.sleep(2e-5)
-                if time.perf_counter() - t0 > 60.0:
-                    raise _lib.DLError("sharded step %d reported no status within 60 s (a rank stopped?)" % k)
+                if time.perf_counter() - t0 > self.guard_s:
+                    self._guard_exit(k)
             self.host_wait += time.perf_counter() - t0
             word = int(r[j + 1]) & 0xffffffff
             skip = word >> 16
@@ -1006,9 +1047,28 @@ class ShardedCTREngine(CTREngine):
                                "— %d step(s) skipped on every rank with no update, the last at global_step %d"
                                % (self.N, [p for p in range(self.world) if ranks >> p & 1], len(bad), step))
 
+    def _guard_exit(self, k):
+        """The status report of step k did not arrive within guard_s seconds: a peer stopped, or
+        this rank's step is stuck in a collective.  Raising would leave the process (and the job)
+        waiting on the device at its next synchronisation; instead say where it stopped, from host
+        memory only (the device may be the thing that hangs), and exit non-zero — the launcher then
+        stops the other ranks."""
+        import sys
+        r = self._ring_np
+        last = [(int(r[2 * j]), int(r[2 * j + 1]) & 0xffffffff) for j in range(4)]
+        sys.stderr.write("[shard] rank %d/%d: the status report of step %d (sequence) did not arrive within %.0f s; "
+                         "submitted %d, reports read %d, train_step calls %d, cap %d; status ring (k, word) %s — "
+                         "a peer stopped or a collective is stuck: exiting with status 75\n"
+                         % (self.rank, self.world, k, self.guard_s, self._ring_sent, self._ring_checked,
+                            self.steps, self.cap, last))
+        sys.stderr.flush()
+        os._exit(75)
+
     def _recover(self, k, batch):
         """Step k overflowed a block on some rank, so it and every step after it were skipped on
-        every rank: wait for them, clear the fault, grow the blocks and replay them in order."""
+        every rank: wait for them, clear the fault, grow the blocks and replay them in order.
+        The replay needs each skipped step's batch argument as it was submitted: a step submitted
+        with batch None (its inputs staged by the caller) cannot be replayed, which raises."""
         torch.cuda.synchronize()
         replay = [batch] + [self._hist_b[q] for q in sorted(self._hist_b)]
         self._hist_b.clear()
@@ -1016,6 +1076,11 @@ class ShardedCTREngine(CTREngine):
         self._grow()
         self.steps -= len(replay)
         self._ring_sent = None
+        if any(b is None for b in replay):   # the engine goes on with grown blocks; these steps are lost
+            raise _lib.DLError("sharded step %d overflowed a block and was skipped with the %d step(s) after it: "
+                               "their replay needs each step's batch, but one was submitted as train_step(None) "
+                               "(inputs already staged); pass the batch to train_step, unmodified for `lag` calls, "
+                               "when blocks may overflow" % (k, len(replay) - 1))
         self.overflows = getattr(self, "overflows", 0) + 1
         for b in replay:
             self._submit(b, False, None)
@@ -1093,8 +1158,8 @@ class ShardedCTREngine(CTREngine):
             data = float(self.flat[hoff + H + 1].item())
             wr = self.wide_reg.clone()
             self.exch.host_sum(wr)
-            return data / (self.last_batch * self.world) + sp.l2 * 0.5 * (float(self.opt[8].item()) +
-                                                                           float(wr[0].item()))
+            return data / (self.last_batch * self.world) + sp.l2 * 0.5 * (_lib.reg_sum(self.opt) +
+                                                                           _lib.reg_sum(wr))
         data = float(self.flat[hoff + self.head_w - 1].item())
         w = self.w_head_prev[: self.head_n - 1].double()
         return data / (self.last_batch * self.world) + sp.l2 * 0.5 * float((w * w).sum().item())

@@ -374,7 +374,8 @@ int dl_slab_fold_rows(const float* slab, int32_t blocks, int32_t width, int32_t 
  * decay each step — SURVEY.md ledger item 6).  `opt` is a device float[16]:
  * [0] beta1_power [1] beta2_power [2] lr [3] alpha [4] beta1 [5] beta2
  * [6] epsilon [7] step (as float, exact < 2^24), [8..15] per-step accumulators
- * (zeroed by dl_adam_begin_step; sq_out targets), [16] the status word (int32
+ * (zeroed by dl_adam_begin_step; [8..9] = opt + DL_OPT_REG is the step's regulariser sum as
+ * int64 fixed point, the sq_out / acc_out target), [16] the status word (int32
  * bits, sticky until the host clears it: what the host reports), [17] the skip
  * word (int32 bits of the CURRENT step only, rewritten by dl_step_guard /
  * dl_step_begin), [18] the global step at which the last bad batch was skipped,
@@ -394,6 +395,11 @@ int dl_slab_fold_rows(const float* slab, int32_t blocks, int32_t width, int32_t 
  * Internal faults (DL_STATUS_LAG / DL_STATUS_INDEX) set both words and keep every
  * later step skipped until the host clears the status. */
 #define DL_OPT_LEN 32
+#define DL_OPT_REG 8        /* int64 fixed point (units 1/DL_REG_SUM_SCALE) in opt[8..9]: the step's regulariser sum */
+/* Regulariser sums (every sq_out / acc_out / sq_untouched below) are signed 64-bit fixed point
+ * in units of 1/DL_REG_SUM_SCALE, 8-byte aligned: each block adds its fixed-order partial as an
+ * integer, so the sum is the same bits whatever order the blocks land in (|sum| < 2^31). */
+#define DL_REG_SUM_SCALE 4294967296.0 /* 2^32 */
 #define DL_OPT_STATUS 16
 #define DL_OPT_SKIP 17
 #define DL_OPT_BAD_STEP 18
@@ -427,7 +433,7 @@ int dl_step_begin(const int32_t* batch_err, float* opt, float decay_rate, float 
                   int32_t hist_len, void* stream);
 /* The running loss of a training loop (the load-style fit's per-epoch mean, wdl.py:305-313):
  * acc[0] += sum_r slab[r * pitch + col] * inv_b (the step's data term; double, fixed order),
- * acc[1] += reg_coef * opt[8] (the step's regulariser sum), acc[2] += 1; nothing for a skipped
+ * acc[1] += reg_coef * the step's regulariser sum (opt + DL_OPT_REG), acc[2] += 1; nothing for a skipped
  * step.  acc: double[3] on the device, read by the host once per epoch.  (Wide&Deep with lazy
  * wide records adds the wide L2 term per record step through dl_wide_rec_update / _flush acc.)
  * status_ring (may be NULL): int32[8] of pinned host memory; every call (skipped steps too)
@@ -438,24 +444,24 @@ int dl_loss_accumulate(const float* slab, int32_t rows, int32_t pitch, int32_t c
                        float reg_coef, double* acc, int32_t* status_ring, void* stream);
 /* Dense parameter whose gradient is the sum of `nslab` partial slabs
  * (g = sum_s slab[s*slab_stride + i]); l2 * p is added for i < l2_count;
- * p_prev (may be NULL) receives the pre-update values; sq_out (may be NULL) gets
- * sum p_pre^2 over the L2-regularised elements added (atomically) — the loss's
- * l2_regularizer term of the step, read back without copying the parameters. */
+ * p_prev (may be NULL) receives the pre-update values; sq_out (may be NULL, int64 fixed
+ * point, DL_REG_SUM_SCALE) gets sum p_pre^2 over the L2-regularised elements added — the
+ * loss's l2_regularizer term of the step, read back without copying the parameters. */
 /* dl_adam_dense_split3: dl_adam_dense_reg on a tower weight W [rows][cols] (n = rows * cols,
  * no p_prev) that also writes the updated W's three bf16 planes in dl_split3's two layouts —
  * wp[q][r][c] and wtp[q][c][r], plane stride rows * cols — in place of two dl_split3 launches
  * after the update (the s3 GEMMs' operands; deepfm_pipeline.py:184-188 ApplyAdam on W). */
 int dl_adam_dense_split3(float* p, float* m, float* v, const float* slab, int32_t nslab, int64_t slab_stride,
                          int32_t rows, int32_t cols, float reg, int64_t reg_count, int32_t reg_kind, const float* opt,
-                         float* acc_out, uint16_t* wp, uint16_t* wtp, void* stream);
+                         int64_t* acc_out, uint16_t* wp, uint16_t* wtp, void* stream);
 /* dl_adam_dense_bf16: the same for the bf16 tower (C5): the updated W's bf16 copy wb [rows][cols]
  * and its transpose wbt [cols][rows] (dl_cast_bf16 / dl_transpose_bf16's rounding). */
 int dl_adam_dense_bf16(float* p, float* m, float* v, const float* slab, int32_t nslab, int64_t slab_stride,
                        int32_t rows, int32_t cols, float reg, int64_t reg_count, int32_t reg_kind, const float* opt,
-                       float* acc_out, uint16_t* wb, uint16_t* wbt, void* stream);
+                       int64_t* acc_out, uint16_t* wb, uint16_t* wbt, void* stream);
 int dl_adam_dense(float* p, float* m, float* v, const float* slab, int32_t nslab,
                   int64_t slab_stride, int64_t n, float l2, int64_t l2_count, const float* opt,
-                  float* p_prev, float* sq_out, void* stream);
+                  float* p_prev, int64_t* sq_out, void* stream);
 /* One tower weight's update for dl_adam_dense_layers: W [rows][cols] (p, m, v), its gradient as
  * `nslab` partial slabs `slab_stride` floats apart, the regulariser (reg_kind 0 = L2, 1 = L1) on
  * the first reg_count elements with its loss term added to *acc_out (may be NULL), and the
@@ -467,7 +473,7 @@ typedef struct dl_adam_layer {
   const float* slab;
   int64_t slab_stride;
   int64_t reg_count;
-  float* acc_out;
+  int64_t* acc_out;
   uint16_t* wp;
   uint16_t* wtp;
   int32_t nslab;
@@ -478,8 +484,8 @@ typedef struct dl_adam_layer {
 } dl_adam_layer;
 /* dl_adam_dense_layers: dl_adam_dense_split3 (copies = 3) or dl_adam_dense_bf16 (copies = 1) on
  * up to DL_ADAM_MAX_LAYERS tower weights in one launch — the same per-element operations, so the
- * same results as one launch per layer (the regulariser sums excepted: atomics in another
- * grouping).  One launch instead of one per hidden layer at the end of the backward. */
+ * same results as one launch per layer (the regulariser sum: the same total, other block
+ * partials).  One launch instead of one per hidden layer at the end of the backward. */
 #define DL_ADAM_MAX_LAYERS 4
 int dl_adam_dense_layers(int32_t n_layers, const dl_adam_layer* layers, int32_t copies, const float* opt,
                          void* stream);
@@ -488,7 +494,7 @@ int dl_adam_dense_layers(int32_t n_layers, const dl_adam_layer* layers, int32_t 
  * i < reg_count, acc_out += |p_pre|). */
 int dl_adam_dense_reg(float* p, float* m, float* v, const float* slab, int32_t nslab,
                       int64_t slab_stride, int64_t n, float reg, int64_t reg_count, int32_t reg_kind,
-                      const float* opt, float* p_prev, float* acc_out, void* stream);
+                      const float* opt, float* p_prev, int64_t* acc_out, void* stream);
 /* Embedding tables, every row updated: g = g_table row if touched else 0;
  * consumed gradients are reset to 0.  rows_flags: DL_ROWS_CLEAR_TOUCHED resets the
  * flags (on the last table that shares them); DL_ROWS_SPARSE_ADAM selects the update
@@ -509,7 +515,7 @@ int dl_adam_dense_reg(float* p, float* m, float* v, const float* slab, int32_t n
 #define DL_ROWS_GRAD_FIXED 4
 #define DL_WIDE_GRAD_SCALE 281474976710656.0 /* 2^48 */
 int dl_adam_rows(float* p, float* m, float* v, void* g, uint8_t* touched, int64_t n_rows,
-                 int32_t width, float l2, int32_t rows_flags, const float* opt, float* sq_out,
+                 int32_t width, float l2, int32_t rows_flags, const float* opt, int64_t* sq_out,
                  void* stream);
 
 /* ------------------------------------------------------------------------
@@ -713,7 +719,8 @@ int dl_wide_local_ids(const int32_t* inv, int64_t n, int64_t offset, int64_t* ou
  * term — every pre-update w^2 of the rows this step applies, and of the steps replayed for
  * them (rep_sq, or the deep rows' own replay) — added per block.
  * dl_wide_rec_flush: every row caught up to step opt[7]; the pre-update w^2 of the rows the
- * last step left untouched (the loss's L2 term for them) added to sq_untouched; every replayed
+ * last step left untouched (the loss's L2 term for them) added to sq_untouched (int64 fixed
+ * point, DL_REG_SUM_SCALE); every replayed
  * step's pre-update w^2 added to acc's slots (may be NULL).  Summed over acc after a flush, the
  * slots hold sum_t sum_r w_r(t-1)^2 over the steps since acc was zeroed on a flushed table. */
 int dl_wide_rec_gather(const float* rec, int64_t w_rows, const uint32_t* uniq_rows, const int32_t* n_uniq,
@@ -728,7 +735,7 @@ int dl_wide_rec_update(float* rec, const int32_t* n_uniq, int64_t max_uniq, cons
                        const float* opt, uint8_t* dmark, float* sq_out, const float* rep_sq, double* acc,
                        void* stream);
 int dl_wide_rec_flush(float* rec, int64_t w_rows, float l2, const float* hist, int32_t hist_len,
-                      const float* opt, float* sq_untouched, double* acc, void* stream);
+                      const float* opt, int64_t* sq_untouched, double* acc, void* stream);
 #define DL_LOSS_ACC_SLOTS 65536   /* slots of the wide running-loss accumulator (>= any grid above) */
 
 /* ------------------------------------------------------------------------
@@ -777,6 +784,9 @@ int dl_init_random(float* p, int64_t n, int32_t dist, float mean, float scale, u
 int64_t dl_auc_workspace_bytes(int64_t n);
 int dl_auc(const float* scores, int64_t s_stride, const float* labels, int64_t l_stride, int64_t n,
            void* ws, int64_t ws_bytes, double* out, void* stream);
+/* Streaming copy of `bytes` (a multiple of 16, both pointers 16-B aligned) from src to dst: the
+ * measured HBM yardstick bench.py reports beside the 8 TB/s specification (roofline.peak_measured). */
+int dl_hbm_copy(const void* src, void* dst, int64_t bytes, void* stream);
 
 #ifdef __cplusplus
 }

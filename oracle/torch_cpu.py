@@ -24,8 +24,13 @@ import torch
 
 
 class DeepFMPipelineCPU:
+    """fm=False: models/dnn_pipeline.py (BASELINE C1) — the same deep input [cont | V[cate]] over
+    the row-0-zeroed table (dnn_pipeline.py:68-107), no FM terms, the `deep_res` output layer
+    with L2 on it (:114-131)."""
+
     def __init__(self, C, S, E, cate_index_size, hidden, P, lr=0.001, l2=1e-5, beta1=0.9, beta2=0.999,
-                 eps=1e-8, logloss_eps=1e-7):
+                 eps=1e-8, logloss_eps=1e-7, fm=True):
+        self.fm = fm
         self.C, self.S, self.E, self.hidden = C, S, E, list(hidden)
         self.lr, self.l2, self.b1, self.b2, self.eps, self.leps = lr, l2, beta1, beta2, eps, logloss_eps
         t = lambda a: torch.from_numpy(a.copy()).float().requires_grad_(True)
@@ -43,6 +48,14 @@ class DeepFMPipelineCPU:
         lab = torch.from_numpy(batch["label"]).float().reshape(-1)
         B = lab.shape[0]
         V = torch.cat([torch.zeros(1, E), P["feats_emb"][1:]], 0)                     # :83-84
+        if not self.fm:                                                              # dnn_pipeline.py
+            h = torch.cat([cont, V[cate].reshape(B, S * E)], 1)
+            for i in range(len(self.hidden)):
+                h = torch.relu(h @ P["deep_%d" % i] + P["deep_bias_%d" % i])
+            z = (h @ P["deep_res"])[:, 0] + P["deep_res_bias"][0, 0]                  # :119
+            p = torch.sigmoid(z)
+            loss = (-lab * torch.log(p + self.leps) - (1 - lab) * torch.log(1 - p + self.leps)).mean()
+            return z, loss + self.l2 * 0.5 * (P["deep_res"] ** 2).sum()              # :131
         w1 = torch.cat([torch.zeros(1, 1), P["fm_first_order_emb"][1:]], 0)          # :85-86
         if self.cidx is None or self.cidx.shape[0] != B:
             self.cidx = torch.arange(C, dtype=torch.long).repeat(B, 1)               # :58-61

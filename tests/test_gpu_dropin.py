@@ -217,11 +217,55 @@ def test_native_pickle_feed_trains_like_the_default_loop(hip_lib, tmp_path, alg,
         res[feed] = (losses, m.model_optimizer().params())
     for k in res["0"][1]:
         np.testing.assert_array_equal(res["1"][1][k], res["0"][1][k], err_msg=k)
-    # the epoch loss: the same per-step losses (the parameters above are bit-identical), summed on
-    # the device by block atomics whose order varies from run to run (dl_loss_accumulate), so
-    # equal to within an f32 unit, not bit for bit (a dnn run differed by 1.2e-9 relative)
-    for (a, na), (b, nb) in zip(res["0"][0], res["1"][0]):
-        assert na == nb and abs(a - b) <= 1e-7 * abs(a), (res["0"][0], res["1"][0])
+    # the epoch loss: the same per-step losses, bit for bit (the parameters above are
+    # bit-identical, the data term is summed in a fixed order and the regulariser sums are int64
+    # fixed point, so the order in which blocks land does not matter: common.h block_fixed_add)
+    assert res["1"][0] == res["0"][0], (res["0"][0], res["1"][0])
+
+
+def test_pinned_feed_bad_id_batch_raises_without_hang(hip_lib, tmp_path, monkeypatch):
+    """A DLError raised mid-epoch by the default PinnedFeed loop (a batch with an out-of-range id,
+    reported through the status ring a step or two later, while the loop still holds batches)
+    propagates as the reference's InvalidArgumentError does: the feed's workers that wait for a
+    slot the loop will never release are let go, so the pool's shutdown cannot hang
+    (PinnedFeed.close(abort=True)); a later epoch on the same model still trains."""
+    import pickle
+    import threading
+    from deep_learning_amd import _lib
+    from deep_learning_amd.models import wdl
+    from deep_learning_amd.synthetic import make_batch
+    from deep_learning_amd.utils import data_loader_load as dll
+
+    class Args:
+        hidden_units, epochs, batch_size, learning_rate = [32, 16], 1, 64, 0.001
+        model_pb, learning_rate_decay_steps, learning_rate_decay_rate, l2_reg = str(tmp_path / "pb"), 10000000, 0.9, 1e-5
+        cont_field_size, cate_field_size, embedding_size, wide_field_size = 13, 26, 8, 26
+        cate_index_size = cate_feats_size = 4000
+        vector_feats_size = vector_field_size = 0
+        alg_name = "wdl"
+    monkeypatch.setenv("DLAMD_PINNED_FEED", "1")
+    (tmp_path / "tr").mkdir()
+    dll.write_lines(str(tmp_path / "tr" / "part-0"), make_batch(64 * 8, cate_index_size=4000, seed=3, wide_fields=26))
+    tr = dll.load_input_file(Args, str(tmp_path / "tr"))
+    d = pickle.loads(tr[1])
+    d["cate_feats"][5, 3] = 10 ** 7          # batch 1: one id far outside [0, 4000)
+    bad = list(tr)
+    bad[1] = pickle.dumps(d)
+    m = wdl.DeepModel(Args)
+    out = {}
+
+    def run():
+        try:
+            m.train_epoch(bad)
+        except Exception as e:   # noqa: BLE001 — the thread reports what ended the epoch
+            out["err"] = e
+    t = threading.Thread(target=run, daemon=True)
+    t.start()
+    t.join(60)
+    assert not t.is_alive(), "train_epoch hung after the bad-id error"
+    assert isinstance(out.get("err"), _lib.DLError) and "InvalidArgumentError" in str(out["err"]), out
+    loss, steps = m.train_epoch(tr)
+    assert steps == 8 and np.isfinite(loss)
 
 
 @pytest.mark.parametrize("alg", ["deepfm", "dnn"])

@@ -858,7 +858,7 @@ def test_adam_rows_width1_sweep(hip_lib, n, flags):
     opt = torch.zeros(_lib.OPT_LEN, dtype=torch.float32)
     opt[3], opt[4], opt[5], opt[6] = float(alpha), float(b1), float(b2), float(eps)
     opt = opt.cuda()
-    sq = torch.zeros(1, dtype=torch.float32, device="cuda")
+    sq = torch.zeros(1, dtype=torch.int64, device="cuda")   # fixed point (DL_REG_SUM_SCALE)
     pd, md, vd = (torch.from_numpy(a.copy()).cuda() for a in (p, m, v))
     td = torch.from_numpy(touched.copy()).cuda()
     call("dl_adam_rows", ptr(pd), ptr(md), ptr(vd), ptr(g_d), ptr(td), n, 1, float(l2),
@@ -883,4 +883,4 @@ def test_adam_rows_width1_sweep(hip_lib, n, flags):
     np.testing.assert_allclose(pd.cpu().numpy(), p1, rtol=1e-6, atol=1e-7)
     assert int(td.sum()) == 0
     assert not torch.any(g_d != 0)
-    np.testing.assert_allclose(float(sq.item()), float(np.sum(p.astype(np.float64) ** 2)), rtol=1e-4)
+    np.testing.assert_allclose(_lib.reg_sum(sq), float(np.sum(p.astype(np.float64) ** 2)), rtol=1e-4)

@@ -323,6 +323,13 @@ def test_native_unpickle_batch_matches_pickle(proto):
     for b in bad:
         assert nr.unpickle_batch_into(b, fields, outs, B) is None
     assert nr.unpickle_batch_into(item, fields, outs, B - 1) is None
+    # 8-byte length opcodes (BINUNICODE8, BINBYTES8, BYTEARRAY8) whose length is near INT64_MAX:
+    # the bounds check must not overflow into a pass (a read far past the buffer)
+    import struct
+    for op in (b"\x8d", b"\x8e", b"\x96"):
+        for ln in (0x7FFFFFFFFFFFFFF0, 0x7FFFFFFFFFFFFFFF, 1 << 62):
+            evil = b"\x80\x05\x95" + struct.pack("<Q", 11 + 4) + op + struct.pack("<Q", ln) + b"abcd."
+            assert nr.unpickle_batch_into(evil, fields, outs, B) is None
 
 
 def test_native_unpickle_large_batch_in_row_pieces():

@@ -238,3 +238,22 @@ def test_torch_cpu_restatement_matches_numpy_oracle():
         assert abs(loss - fw["loss"]) < 1e-5
     for k in P:
         np.testing.assert_allclose(m.params[k].detach().numpy(), P[k], atol=1e-5, rtol=0, err_msg=k)
+
+
+def test_torch_cpu_restatement_dnn_pipeline_matches_numpy_oracle():
+    """The C1 leg of bench.py's cpu_baseline (dnn_pipeline, fm=False) against the numpy oracle:
+    3 steps, logits, loss and every parameter."""
+    from oracle.torch_cpu import DeepFMPipelineCPU
+    kw = dict(C=13, V=0, S=26, E=8, cate_index_size=2000, hidden=[48, 32, 16])
+    cfg = R.make_cfg("dnn_pipeline", **kw)
+    P = R.init_params(cfg, np.random.default_rng(4))
+    m = DeepFMPipelineCPU(13, 26, 8, 2000, [48, 32, 16], P, fm=False)
+    opt = R.AdamTF1(cfg, P)
+    for i in range(3):
+        b = make_batch(256, cate_index_size=2000, seed=60 + i)
+        fw = R.train_step(cfg, P, opt, b)
+        z, loss = m.train_step(b)
+        np.testing.assert_allclose(z.numpy(), fw["z"], atol=1e-5, rtol=0)
+        assert abs(loss - fw["loss"]) < 1e-5
+    for k in P:
+        np.testing.assert_allclose(m.params[k].detach().numpy(), P[k], atol=1e-5, rtol=0, err_msg=k)

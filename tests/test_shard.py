@@ -8,6 +8,7 @@ import os
 import socket
 import subprocess
 import sys
+import time
 
 import numpy as np
 import pytest
@@ -127,6 +128,28 @@ def _check_engine(tmp_path, mode, world):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("serial", ["0", "1"])
+def test_sharded_all_reduce_placement_equals_global_batch(tmp_path, serial, monkeypatch):
+    """DLAMD_SHARD_AR_SERIAL: the flat all-reduce after the gradient exchange on its stream
+    (1, the default) or on a stream of its own beside it (0) — the same global-batch result."""
+    monkeypatch.setenv("DLAMD_SHARD_AR_SERIAL", serial)
+    _check_engine(tmp_path, "gpu_lazy_pf", WORLD)
+
+
+def test_sharded_report_lag_bounded_by_the_status_ring():
+    """The status ring holds 4 reports, so a report lag past 3 would let report k + 4 overwrite
+    report k before the host reads it: refused up front (CPU: before any device work)."""
+    import types
+    from deep_learning_amd.engine import ModelSpec
+    from deep_learning_amd.shard import ShardedCTREngine
+    ex = types.SimpleNamespace(world=2, rank=0)
+    spec = ModelSpec("deepfm_pipeline", **KW)
+    for lag in (-1, 4, 8):
+        with pytest.raises(ValueError, match="lag must be 0..3"):
+            ShardedCTREngine(spec, 64, ex, lag=lag)
+
+
+@pytest.mark.gpu
 def test_sharded_bad_id_on_one_rank_raises_everywhere(tmp_path):
     """A bad id in one rank's batch (here rank 1's half of global batch 1, prefetched during
     step 0): its validation bit travels in the request headers, so every rank's step-begin node
@@ -220,3 +243,21 @@ def test_block_exchange_moves_every_block(world):
            os.path.join(ROOT, "tests", "exchange_worker.py")]
     r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=300, cwd=ROOT)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+
+
+def test_status_guard_exits_when_a_peer_is_stuck():
+    """The sharded step's status guard (ShardedCTREngine._guard_exit): a rank whose step report
+    does not arrive within DLAMD_SHARD_GUARD_S exits non-zero naming its rank, the step and its
+    status ring, while its peer sits in a collective it will never complete (a peer stuck in
+    RCCL); the launcher then stops the peer, so the job ends within the guard's time instead of
+    hanging.  gloo, 2 ranks, CPU."""
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", OMP_NUM_THREADS="1", DLAMD_SHARD_GUARD_S="3")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
+           os.path.join(ROOT, "tests", "guard_worker.py")]
+    t0 = time.time()
+    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=120, cwd=ROOT)
+    out = r.stdout + r.stderr
+    assert r.returncode != 0 and "guard did not fire" not in out, out[-3000:]
+    assert "rank 0/2: the status report of step 3" in out and "exiting with status 75" in out, out[-3000:]
+    assert time.time() - t0 < 90, "the stuck peer kept the job alive"
