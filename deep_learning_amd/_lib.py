@@ -130,6 +130,7 @@ SIGNATURES = {
     "dl_cast_bf16": (I32, [P, I32, I32, I32, P, I32, P]),
     "dl_transpose_bf16": (I32, [P, I32, I32, I32, I32, P, I32, P]),
     "dl_adam_hist_record": (I32, [P, P, I32, P]),
+    "dl_rec_stash_floats": (I32, [I32]),
     "dl_rec_gather": (I32, [LP, P, I32, I32, I32, P, P, I64, I32, P, I32, P, I32, P, P, P, P]),
     "dl_rec_gather_scatter": (I32, [LP, P, I32, I32, I32, P, P, I64, P, P, P, I32, P, I32, P, P, P, P, P, P, P, P, P]),
     "dl_pool_fwd_staged": (I32, [LP, P, P, P, P, P, I32, I32, P, P, P, P, P]),

@@ -739,6 +739,28 @@ static_assert(3 * kBnPlane * sizeof(unsigned short) <= kBnLds, "the ring fits in
 #ifndef DL_BN_PF
 #define DL_BN_PF 4   // weight fragments read this many fragments ahead of their MFMAs
 #endif
+// DL_BN_ASMA: where each step takes its A chunk.  hipcc counts only its own loads in vmcnt (not
+// the weight LDS-DMA, inline asm), and it hoisted the copy of the next step's A registers into
+// the current step, where that load is the youngest it knows of: a vmcnt(0) drain in the middle
+// of every chunk's MFMAs (the weights two chunks ahead included).  With the copy made by an asm
+// statement it stays at its step's start, after the barrier (also asm), where hipcc's wait for
+// the chunk's A is vmcnt(2): it lets the next chunk's A loads stay in flight.
+#ifndef DL_BN_ASMA
+#define DL_BN_ASMA 1
+#endif
+// DL_BN_WIDE: bf16 output stored as 16-B pieces (two fragments' lane rows exchanged by
+// v_permlane16_swap, so a lane holds 8 consecutive columns) instead of 8-B pieces
+#ifndef DL_BN_WIDE
+#define DL_BN_WIDE 1
+#endif
+typedef unsigned int bn_u32x4 __attribute__((ext_vector_type(4)));
+typedef __bf16 bn_bf16x2 __attribute__((ext_vector_type(2)));
+typedef float bn_f32x2 __attribute__((ext_vector_type(2)));
+// two f32 -> packed bf16 (v_cvt_pk_bf16_f32: round to nearest even, the same bits as f2bf for
+// every non-NaN value; a NaN stays a NaN)
+__device__ __forceinline__ unsigned bn_pack2(float lo, float hi) {
+  return __builtin_bit_cast(unsigned, __builtin_convertvector((bn_f32x2){lo, hi}, bn_bf16x2));
+}
 
 __device__ __forceinline__ int bn_slot(int j, int kq) { return kq ^ ((j >> 2) & 2); }   // an involution in kq
 
@@ -791,36 +813,51 @@ __global__ __launch_bounds__(512) void gemm_bf16_nt_kernel(GemmParams p) {
                    : "=&s"(keep) : "v"(src), "s"(__builtin_amdgcn_readfirstlane(dst)) : "memory");
     }
   };
-  auto load_a = [&](int c, uint4 (&ra)[2]) {
+  auto load_a = [&](int c, bn_u32x4 (&ra)[2]) {
     const bool kin = 32 * c + 8 * kq < p.K;
-    ra[0] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(
-                                          a_rsrc, (int)((ok0 & kin) ? a_off0 + 64u * c : 0x80000000u), 0, 0));
-    ra[1] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(
-                                          a_rsrc, (int)((ok1 & kin) ? a_off1 + 64u * c : 0x80000000u), 0, 0));
+    const uint32_t o0 = (ok0 & kin) ? a_off0 + 64u * c : 0x80000000u;
+    const uint32_t o1 = (ok1 & kin) ? a_off1 + 64u * c : 0x80000000u;
+    ra[0] = __builtin_bit_cast(bn_u32x4, __builtin_amdgcn_raw_buffer_load_b128(a_rsrc, (int)o0, 0, 0));
+    ra[1] = __builtin_bit_cast(bn_u32x4, __builtin_amdgcn_raw_buffer_load_b128(a_rsrc, (int)o1, 0, 0));
   };
   floatx4 acc[2][kBnNF];
 #pragma unroll
   for (int a = 0; a < 2; ++a)
 #pragma unroll
     for (int f = 0; f < kBnNF; ++f) acc[a][f] = floatx4{0.f, 0.f, 0.f, 0.f};
-  uint4 raA[2], raB[2];
+  bn_u32x4 raA[2], raB[2];
+  // every step issues chunk c + 2's weight DMA (DMAW instructions) and then its A loads (2): the
+  // vector-memory queue of a wave is ... DMA(c+1) A(c+1) | DMA(c+2) A(c+2)
   dma_b(0, 0);
   load_a(0, raA);
   dma_b(1, 1);     // unconditional, like every prefetch below: chunks past KC read clamped
   load_a(1, raB);  // weights into a free buffer and zeros for A
-  // chunk c + 1's weights -> every wave: wait for every batch but the newest (chunk c + 2's),
-  // then a bare s_barrier (a __syncthreads would drain the prefetch: vmcnt(0))
+  // chunk c + 1's weights -> every wave: wait for this wave's DMA(c+1) (younger: A(c+1),
+  // DMA(c+2), A(c+2)), then a bare s_barrier (a __syncthreads would drain the prefetch: vmcnt(0))
   auto publish = [&](int c) {
+    if (DL_BN_ASMA) {   // as asm: it keeps its place among the DMA and the A copies
+      if (c + 1 < KC) asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"n"(DMAW + 4) : "memory");
+      else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+      return;
+    }
     if (c + 1 < KC) DL_BN_VMCNT(DMAW + 2);
-    else DL_BN_VMCNT(0);                  // the epilogue reuses the LDS: nothing may still land
+    else DL_BN_VMCNT(0);                  // nothing may still land after the loop
     __builtin_amdgcn_s_waitcnt(0xc07f);   // lgkmcnt(0): this wave's fragment reads are done
     __builtin_amdgcn_s_barrier();
   };
   publish(-1);
-  auto step = [&](int c, uint4 (&ra)[2]) {
-    shortx8 a0 = __builtin_bit_cast(shortx8, ra[0]), a1 = __builtin_bit_cast(shortx8, ra[1]);
-    // chunk c's A in registers of their own before the next batch reuses ra (hipcc's wait for
-    // it counts only its own loads)
+  auto step = [&](int c, bn_u32x4 (&ra)[2]) {
+    shortx8 a0, a1;
+    if (DL_BN_ASMA) {   // chunk c's A copied here (hipcc waits for its loads right before)
+      bn_u32x4 x0, x1;
+      asm volatile("" : "=v"(x0), "=v"(x1) : "0"(ra[0]), "1"(ra[1]));
+      a0 = __builtin_bit_cast(shortx8, x0);
+      a1 = __builtin_bit_cast(shortx8, x1);
+    } else {
+      a0 = __builtin_bit_cast(shortx8, ra[0]);
+      a1 = __builtin_bit_cast(shortx8, ra[1]);
+    }
+    // chunk c's A in registers of their own before the next batch reuses ra
     asm volatile("" : "+v"(a0), "+v"(a1));
     dma_b(c + 2, (c + 2) % 3);
     load_a(c + 2, ra);
@@ -857,9 +894,12 @@ __global__ __launch_bounds__(512) void gemm_bf16_nt_kernel(GemmParams p) {
     const auto c_rsrc = __builtin_amdgcn_make_buffer_rsrc(p.C, (short)0, p.M * p.ldc * EB, 0x00020000);
     const auto m_rsrc = __builtin_amdgcn_make_buffer_rsrc((void*)p.mask, (short)0,
                                                           EPI == EPI_MASK ? p.M * p.ldm * 2 : 0, 0x00020000);
+    // 16-B bf16 pieces need N, ldc multiples of 8 (the swapped lane holds 8 columns)
+    const bool wide = CBF16 && DL_BN_WIDE && p.N % 8 == 0 && p.ldc % 8 == 0;
 #pragma unroll
     for (int a = 0; a < 2; ++a) {
       const int row = r0 + 16 * a + cl;
+      unsigned plo = 0u, phi = 0u;   // the even fragment's packed words, until its pair's swap
       // the ReluGrad mask's pieces of these 13 fragments first, all in flight together
       uint2 mk[EPI == EPI_MASK ? kBnNF : 1];
       if constexpr (EPI == EPI_MASK) {
@@ -884,13 +924,40 @@ __global__ __launch_bounds__(512) void gemm_bf16_nt_kernel(GemmParams p) {
 #pragma unroll
           for (int e = 0; e < 4; ++e) x[e] = bf2f(mv[e]) > 0.f ? x[e] : 0.f;
         }
+        if (CBF16 && wide) {
+          // fragment pairs (f, f + 1): v_permlane16_swap exchanges lane rows kq = 1, 3 of f's
+          // two packed words with rows kq = 0, 2 of f + 1's, so an even-kq lane holds f's columns
+          // 4kq .. 4kq + 7 and an odd-kq lane f + 1's columns 4(kq - 1) .. 4kq + 3: one 16-B
+          // store each (64 contiguous bytes of a row per lane-row quad) instead of two 8-B ones
+          const unsigned lo = bn_pack2(x[0], x[1]), hi = bn_pack2(x[2], x[3]);
+          if ((f & 1) == 0 && f + 1 < kBnNF) {
+            plo = lo;
+            phi = hi;
+            continue;
+          }
+          if (f & 1) {
+            const auto sl = __builtin_amdgcn_permlane16_swap(plo, lo, false, false);
+            const auto sh = __builtin_amdgcn_permlane16_swap(phi, hi, false, false);
+            const int c8 = (kq & 1) ? j0 + 16 * f + 4 * (kq - 1) : j0 + 16 * (f - 1) + 4 * kq;
+            const bool ok = row < p.M && c8 + 8 <= p.N;
+            const uint32_t off = ok ? 2u * (uint32_t)(row * p.ldc + c8) : 0x80000000u;
+            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(dl_u32x4_t, make_uint4(sl[0], sh[0], sl[1], sh[1])),
+                                                   c_rsrc, (int)off, 0, 0);
+            continue;
+          }
+          // the odd fragment left over (kBnNF = 13): its 8-B pieces
+          const bool ok = row < p.M && col + 4 <= p.N;
+          const uint32_t off = ok ? 2u * (uint32_t)(row * p.ldc + col) : 0x80000000u;
+          __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(dl_u32x2_t, make_uint2(lo, hi)), c_rsrc, (int)off, 0,
+                                                0);
+          continue;
+        }
         const bool ok = row < p.M && col + 4 <= p.N;
         const uint32_t off = ok ? (uint32_t)EB * (uint32_t)(row * p.ldc + col) : 0x80000000u;
         if (CBF16)
           __builtin_amdgcn_raw_buffer_store_b64(
-              __builtin_bit_cast(dl_u32x2_t, make_uint2(f2bf(x[0]) | ((unsigned)f2bf(x[1]) << 16),
-                                                        f2bf(x[2]) | ((unsigned)f2bf(x[3]) << 16))),
-              c_rsrc, (int)off, 0, 0);
+              __builtin_bit_cast(dl_u32x2_t, make_uint2(bn_pack2(x[0], x[1]), bn_pack2(x[2], x[3]))), c_rsrc,
+              (int)off, 0, 0);
         else
           __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(dl_u32x4_t, make_float4(x[0], x[1], x[2], x[3])),
                                                  c_rsrc, (int)off, 0, 0);

@@ -34,6 +34,22 @@
 #define DL_REC_FULL_LINES 1   // record updates also write the pad (see rec_write_pad)
 #endif
 
+// The gather's moment stash (mv: what the backward updates from, so it never re-reads and
+// replays a record).  DL_STASH_M = 0: [m (E) | s (E) | m1 s1 0 0] per unique row, 2E + 4 floats.
+// DL_STASH_M = 1 (root state only): [m (E) | m1 s1 lag 0], E + 4 floats — the backward reads the
+// row's stale s from the record line it rewrites anyway and applies the `lag` zero-gradient
+// decays itself: with g = 0 a step's s' = fma(s, c_hi, s c_lo) does not depend on p, m or the
+// step's alpha (common.h adam_elem_root), so the same operations give the same bits as the
+// gather's replay.  64 B a row less written by the gather and read back by the backward, for
+// one random 64-B read of the record's second line.
+#ifndef DL_STASH_M
+#define DL_STASH_M 1
+#endif
+#if DL_STASH_M && !DL_ROOT_STATE
+#error "DL_STASH_M needs the root state (DL_ROOT_STATE=1)"
+#endif
+__host__ __device__ constexpr int rec_stash_floats(int E) { return DL_STASH_M ? E + 4 : 2 * E + 4; }
+
 // The record / stash streams' float4 accesses (round 4 tried them non-temporal, so the random
 // per-reference reads might stay cached: gather 328 -> 410 us, backward 439 -> 723 us at C2,
 // profiles/r04f_nt/ — removed).
@@ -339,11 +355,15 @@ __global__ __launch_bounds__(256) void rec_gather_kernel(const float* __restrict
     }
     *reinterpret_cast<float4*>(out + i * E + 4 * q) = p;
     if (out1 && q == 0) out1[i] = w;
-    if (mv) {   // caught-up moments for the backward's update: [m(E) | v(E) | m1 v1 0 0]
-      float* o = mv + i * (2 * E + 4);
+    if (mv) {   // caught-up moments for the backward's update (rec_stash_floats)
+      float* o = mv + i * rec_stash_floats(E);
       rec_st4(o + 4 * q, m);
-      rec_st4(o + E + 4 * q, v);
-      if (q == 0) rec_st4(o + 2 * E, make_float4(wm, wv, 0.f, 0.f));
+      if (DL_STASH_M) {
+        if (q == 0) rec_st4(o + E, make_float4(wm, wv, __int_as_float(target - from), 0.f));
+      } else {
+        rec_st4(o + E + 4 * q, v);
+        if (q == 0) rec_st4(o + 2 * E, make_float4(wm, wv, 0.f, 0.f));
+      }
     }
   }
 }
@@ -467,6 +487,19 @@ __device__ __forceinline__ void rec_write_pad(float* __restrict__ r, int q, int 
 #endif
 }
 
+// DL_STASH_M: the row's s caught up over `lag` zero-gradient steps — the replay's own s update
+// (rec_adam0_x1 / _x2 on the root state), alone
+__device__ __forceinline__ float4 stash_decay(float4 s, int lag, const RecCfg& c) {
+#pragma clang fp contract(off)
+  for (int j = 0; j < lag; ++j) {
+    s.x = root_decay_step(s.x, c.rd);
+    s.y = root_decay_step(s.y, c.rd);
+    s.z = root_decay_step(s.z, c.rd);
+    s.w = root_decay_step(s.w, c.rd);
+  }
+  return s;
+}
+
 // The backward's per-row state: the caught-up p, m, v (and first-order triple) of unique
 // row u — from the gather's stash, or the record caught up again without one.
 template <int E, bool STASH = false>   // STASH: the stash is known present (no catch-up code)
@@ -477,10 +510,18 @@ __device__ __forceinline__ void rec_bwd_state(int64_t row, long long iu, int q, 
                                               float4& v, float& w, float& wm, float& wv) {
   if (STASH || mv) {
     p = rec_ld4(rows_u + iu * E + 4 * q);
-    const float* o = mv + iu * (2 * E + 4);
+    const float* o = mv + iu * rec_stash_floats(E);
     m = rec_ld4(o + 4 * q);
-    v = rec_ld4(o + E + 4 * q);
-    if (first) { w = rows_u1[iu]; wm = o[2 * E]; wv = o[2 * E + 1]; }
+    if (DL_STASH_M) {
+      const float4 tl = rec_ld4(o + E);
+      // the stale s from the record (the caller checked the row: row_ok) and the gather's lag
+      if (row_ok) v = rec_ld4(rec + row * c.ld + 2 * E + 4 + 4 * q);
+      v = stash_decay(v, __float_as_int(tl.z), c);
+      if (first) { w = rows_u1[iu]; wm = tl.x; wv = tl.y; }
+    } else {
+      v = rec_ld4(o + E + 4 * q);
+      if (first) { w = rows_u1[iu]; wm = o[2 * E]; wv = o[2 * E + 1]; }
+    }
   } else if (!STASH && row_ok) {   // no stash: re-read the record and replay its catch-up
     const float* r = rec + row * c.ld;
     p = *reinterpret_cast<const float4*>(r + 4 * q);
@@ -942,10 +983,16 @@ __global__ __launch_bounds__(256) void rec_apply_segments_kernel(float* __restri
         continue;
       }
       p = *reinterpret_cast<const float4*>(rows + (long long)k0 * E + 4 * q);
-      const float* o = mv + (long long)k0 * (2 * E + 4);
+      const float* o = mv + (long long)k0 * rec_stash_floats(E);
       m = *reinterpret_cast<const float4*>(o + 4 * q);
-      v = *reinterpret_cast<const float4*>(o + E + 4 * q);
-      if (first) { w = rows1[k0]; wm = o[2 * E]; wv = o[2 * E + 1]; }
+      if (DL_STASH_M) {   // the stale s from the record, decayed over the gather's lag
+        const float4 tl = *reinterpret_cast<const float4*>(o + E);
+        v = stash_decay(*reinterpret_cast<const float4*>(r + 2 * E + 4 + 4 * q), __float_as_int(tl.z), c);
+        if (first) { w = rows1[k0]; wm = tl.x; wv = tl.y; }
+      } else {
+        v = *reinterpret_cast<const float4*>(o + E + 4 * q);
+        if (first) { w = rows1[k0]; wm = o[2 * E]; wv = o[2 * E + 1]; }
+      }
     } else {
       p = *reinterpret_cast<const float4*>(r + 4 * q);
       m = *reinterpret_cast<const float4*>(r + E + 4 + 4 * q);
@@ -1092,6 +1139,8 @@ extern "C" int dl_adam_hist_record(const float* opt, float* hist, int32_t hist_l
   hipLaunchKernelGGL(hist_record_kernel, dim3(1), dim3(1), 0, as_stream(stream), opt, hist, hist_len - 1);
   DL_RETURN_LAUNCH("dl_adam_hist_record");
 }
+
+extern "C" int32_t dl_rec_stash_floats(int32_t emb_dim) { return rec_stash_floats(emb_dim); }
 
 extern "C" int dl_rec_gather(const dl_emb_layout* L, const float* rec, int32_t rec_ld, int32_t rec_flags,
                              int32_t n_rep, const uint32_t* uniq_keys, const int32_t* n_uniq, int64_t max_uniq,

@@ -471,7 +471,7 @@ class CTREngine:
             # rec_stash: the gather also stashes the caught-up moments for the backward's update.
             # Off by default — re-reading the record in the backward measured faster on both
             # kernels (gather 328 -> 232 us, backward 505 -> 447 us at C2; profiles/r01l).
-            self.mv_u = z(self.n_rep + self.n_refs, 2 * E + 4) if rec_stash else None
+            self.mv_u = z(self.n_rep + self.n_refs, int(_lib.lib().dl_rec_stash_floats(E))) if rec_stash else None
             # hot rows' chunked segment sums (dl_rec_bwd_adam: Zipf rows over many blocks)
             self.hot_ws = z(int(_lib.lib().dl_rec_bwd_workspace_bytes(self.n_refs, E)), dt=torch.uint8)
         # fwd_rec: the forward reads the cate rows straight from the records (dl_embed_fwd_rec)

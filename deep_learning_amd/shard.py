@@ -293,7 +293,7 @@ class ShardedCTREngine(CTREngine):
             self._pfq = []
             self._slot_free = [None] * len(self._slots)
         if self.lazy:
-            self.own_mv = z(W * cap, 2 * E + 4) if self.owner_update == "sort" else None
+            self.own_mv = z(W * cap, int(_lib.lib().dl_rec_stash_floats(E))) if self.owner_update == "sort" else None
             if self.owner_update == "chain":
                 self.own_next = z(W * cap, dt=torch.int32)
             elif W > 1:

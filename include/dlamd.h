@@ -544,8 +544,11 @@ int dl_adam_hist_record(const float* opt, float* hist, int32_t hist_len, void* s
  * L->fm_cont_offset + i for i < n_rep (the replicated FM cont-field rows) else the row of uniq_keys[i-n_rep] (batch index,
  * dl_index_build keys; n_uniq = NULL: max_uniq keys, e.g. an owner's received local
  * rows with world = 1).  Records are only read.  mv_u (may be NULL) receives the
- * caught-up moments [i][2E+4] = m(E) | s(E) | m1 s1 0 0 for dl_rec_bwd_adam.
+ * moment stash for dl_rec_bwd_adam / dl_rec_apply_segments, dl_rec_stash_floats(E) floats a row:
+ * m(E) | m1 s1 lag 0 (the backward takes s from the record it rewrites, decayed over `lag`
+ * zero-gradient steps: the same bits), or, in builds with DL_STASH_M=0, m(E) | s(E) | m1 s1 0 0.
  * lag = 1 inside a training step, 0 for predict. */
+int32_t dl_rec_stash_floats(int32_t emb_dim);
 int dl_rec_gather(const dl_emb_layout* L, const float* rec, int32_t rec_ld, int32_t rec_flags,
                   int32_t n_rep, const uint32_t* uniq_keys, const int32_t* n_uniq, int64_t max_uniq,
                   int32_t world, const float* hist, int32_t hist_len, const float* opt, int32_t lag,
@@ -621,7 +624,7 @@ int dl_rec_apply_rows(float* rec, int32_t rec_ld, int32_t emb_dim, int32_t rec_f
                       const float* opt, void* stream);
 /* Sharded owners, deterministic: per unique received row (dl_sort_unique over the received
  * ids) the ordered sum of its arrivals g[pos][E], g1[pos] is applied (step opt[7]).  With
- * mv (the owner gather's moment stash, [n][2E+4]) the row's caught-up state is taken from
+ * mv (the owner gather's moment stash, [n][dl_rec_stash_floats(E)]) the row's caught-up state is taken from
  * rows[pos][E] / rows1[pos] / mv[pos] at its first arrival — the owner gather's outputs —
  * and the record is only written; without it the record is read and caught up again. */
 int dl_rec_apply_segments(float* rec, int32_t rec_ld, int32_t emb_dim, int32_t rec_flags, const int32_t* uniq,

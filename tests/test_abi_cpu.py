@@ -12,7 +12,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 def _declared():
     src = open(os.path.join(ROOT, "include", "dlamd.h")).read()
     src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
-    return set(re.findall(r"^\s*(?:int|int64_t|const char\*)\s+(dl_\w+)\s*\(", src, flags=re.M))
+    return set(re.findall(r"^\s*(?:int|int32_t|int64_t|const char\*)\s+(dl_\w+)\s*\(", src, flags=re.M))
 
 
 @pytest.fixture(scope="module")

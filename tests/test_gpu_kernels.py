@@ -546,7 +546,7 @@ def test_chain_apply_equals_sorted_segment_apply(hip_lib):
     L = _lib.EmbLayout()
     L.n_rows, L.batch, L.emb_dim = rows, 1, E
     rows_u, rows_u1 = torch.empty(n, E, device="cuda"), torch.empty(n, device="cuda")
-    mv = torch.empty(n, 2 * E + 4, device="cuda")
+    mv = torch.empty(n, hip_lib.dl_rec_stash_floats(E), device="cuda")   # the moment stash (rec.hip)
     call("dl_rec_gather", C.byref(L), ptr(recC), ld, 1, 0, ptr(ids_d), None, n, 1, ptr(hist_d), hist_len,
          ptr(opt_d), 1, ptr(rows_u), ptr(rows_u1), ptr(mv), _s())
     call("dl_rec_apply_segments", ptr(recC), ld, E, 1, ptr(uniq), ptr(off), ptr(nu), n, n, ptr(pos), ptr(gr_d),
