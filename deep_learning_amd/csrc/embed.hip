@@ -67,6 +67,9 @@ constexpr int kMaxSlots = 128;     // FM slots + deep slots per sample
 #ifndef DL_POOL_DIAG_NO_W1
 #define DL_POOL_DIAG_NO_W1 0   // diagnostics build: first-order weights not read by the forward / pooling (wrong fm_out)
 #endif
+#ifndef DL_POOL_DIAG
+#define DL_POOL_DIAG 0   // diagnostics builds (wrong results; the compacted pooling): 1 = every row read from row 0
+#endif                   // (cache-resident), 2 = no pooled / count / first-order output stores
 // REC: 0 dense table; 1 row records caught up in registers (lazy training); 2 row records
 // already caught up (a flushed table: predict after dl_rec_flush) — only each record's first
 // 128-B line is read (p and the first-order triple + stamp), a stale row faults (DL_STATUS_LAG).
@@ -749,8 +752,8 @@ __global__ __launch_bounds__(256) void pool_fwd_compact_kernel(PoolArgs a) {
         const bool in = j < n;
         const int src = in ? qs[j] : -1;
         mm[it] = in ? qm[j] : kPoolMaxSlots;
-        e[it] = src >= 0 ? tab4[(long long)src * LPR + q] : f4_zero();
-        w[it] = (a.first_order && src >= 0 && q == 0) ? a.first_order[src] : 0.f;
+        e[it] = src >= 0 ? tab4[(long long)((DL_POOL_DIAG & 1) ? 0 : src) * LPR + q] : f4_zero();
+        w[it] = (a.first_order && src >= 0 && q == 0) ? (DL_POOL_DIAG_NO_W1 ? 1.f : a.first_order[src]) : 0.f;
       }
 #pragma unroll
       for (int it = 0; it < NIT; ++it) {
@@ -832,6 +835,11 @@ __global__ __launch_bounds__(256) void pool_fwd_compact_kernel(PoolArgs a) {
         t.z += __shfl_xor(t.z, o, 64); t.w += __shfl_xor(t.w, o, 64);
       }
       const float cn = wave_sum(cnt[m]);
+      if (DL_POOL_DIAG & 2) {   // diagnostics: no output stores (one lane keeps the sums live)
+        const float sv = wave_sum(s1[m]);
+        if (t.x + cn + sv == 1234.5f) a.x0[0] = t.y;
+        continue;
+      }
       if (r == 0) {
         float4 o4 = f4_zero();
         if (cn > 0.f) { o4.x = t.x / cn; o4.y = t.y / cn; o4.z = t.z / cn; o4.w = t.w / cn; }

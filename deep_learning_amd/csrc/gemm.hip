@@ -753,6 +753,9 @@ static_assert(3 * kBnPlane * sizeof(unsigned short) <= kBnLds, "the ring fits in
 #ifndef DL_BN_WIDE
 #define DL_BN_WIDE 1
 #endif
+#ifndef DL_BN_NW
+#define DL_BN_NW 8   // waves a block of the register-epilogue NT kernel (gemm_bf16_nt_kernel NWV)
+#endif
 typedef unsigned int bn_u32x4 __attribute__((ext_vector_type(4)));
 typedef __bf16 bn_bf16x2 __attribute__((ext_vector_type(2)));
 typedef float bn_f32x2 __attribute__((ext_vector_type(2)));
@@ -772,10 +775,13 @@ __device__ __forceinline__ int bn_slot(int j, int kq) { return kq ^ ((j >> 2) & 
 // straight from registers (8 B of bf16 or 16 B of f32 per lane and fragment; the ReluGrad mask's
 // four bf16 read the same way) instead of transposing each wave's tile through LDS (gemm_s3.hip's
 // register epilogue).  Needs N, ldc, ldm multiples of 4 (the host picks it then).
-template <int EPI, bool CBF16, bool DIRECT = false>
-__global__ __launch_bounds__(512) void gemm_bf16_nt_kernel(GemmParams p) {
+// NWV: waves a block (32 rows each; 8 = 256-row blocks, one a CU; 4 = 128-row blocks, three a
+// CU at 155 VGPRs — the register epilogue only, its LDS being the 40-KB ring).
+template <int EPI, bool CBF16, bool DIRECT = false, int NWV = 8>
+__global__ __launch_bounds__(64 * NWV) void gemm_bf16_nt_kernel(GemmParams p) {
   extern __shared__ __attribute__((aligned(16))) unsigned short lds[];   // [3 bufs][BN][32], then the epilogue
-  constexpr int NW = 8, BM = kBnBM, DMAW = kBnDmaW;
+  static_assert(NWV == 8 || DIRECT, "the LDS epilogue's tiles assume 8 waves");
+  constexpr int NW = NWV, BM = 32 * NWV, DMAW = (kBnDma + NWV - 1) / NWV;
   const unsigned short* __restrict__ Bm = reinterpret_cast<const unsigned short*>(p.B);
   const int tid = threadIdx.x, lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int ntm = (p.M + BM - 1) / BM, ntn = (p.N + kBnBN - 1) / kBnBN;
@@ -1063,15 +1069,17 @@ static bool launch_bf16_nt(const GemmParams& gp, int epi, bool cb, hipStream_t s
       gp.ldb < gp.K || (epi == EPI_MASK && gp.ldm % 8) || (reinterpret_cast<uintptr_t>(gp.A) & 15) ||
       (reinterpret_cast<uintptr_t>(gp.B) & 15) || (long long)gp.M * gp.lda * 2 >= (1LL << 31))
     return false;
-  const dim3 grid((unsigned)(ceil_div(gp.M, kBnBM) * ceil_div(gp.N, kBnBN))), block(512);
   const bool direct = bf16_direct_enabled() && gp.N % 4 == 0 && gp.ldc % 4 == 0 &&
                       (epi != EPI_MASK || gp.ldm % 4 == 0) && (long long)gp.M * gp.ldc * 4 < (1LL << 31);
+  constexpr int NWD = DL_BN_NW;   // waves a block of the register-epilogue kernel
+  const dim3 grid((unsigned)(ceil_div(gp.M, direct ? 32 * NWD : kBnBM) * ceil_div(gp.N, kBnBN))),
+      block(direct ? 64 * NWD : 512);
   // the register epilogue needs only the ring (39,936 B instead of the 108,544-B tiles), so other
   // kernels' blocks (the side stream's index build) can share the CU
   constexpr size_t ring = 3 * kBnPlane * sizeof(unsigned short);
 #define DL_BNT(E_, C_)                                                                                     \
   do {                                                                                                     \
-    if (direct) hipLaunchKernelGGL((gemm_bf16_nt_kernel<E_, C_, true>), grid, block, ring, s, gp);   \
+    if (direct) hipLaunchKernelGGL((gemm_bf16_nt_kernel<E_, C_, true, NWD>), grid, block, ring, s, gp);   \
     else hipLaunchKernelGGL((gemm_bf16_nt_kernel<E_, C_>), grid, block, kBnLds, s, gp);                    \
   } while (0)
   if (epi == EPI_STORE) {

@@ -163,7 +163,13 @@ __global__ __launch_bounds__(256) void head_kernel(int B, int fm_cols, int H, co
 // reduced: ids two samples ahead, weights one ahead; only the h row load is left on
 // a sample's critical path.  DHB: dh written as bf16 (the bf16 tower's dY operand,
 // no separate cast pass).
-template <bool DHB>
+// H4M: float4 chunks of a hidden row per lane (2: H <= 512, 4: H <= 1024).  The next sample's h
+// row is loaded while this one is reduced (a wave walks ~8 samples, each a dependent chain:
+// row -> wave sum -> loss -> gradient stores), as the wide ids (two ahead) and weights (one).
+#ifndef DL_WDL_HEAD_PF
+#define DL_WDL_HEAD_PF 1
+#endif
+template <bool DHB, int H4M = kHeadMaxH4>
 __global__ __launch_bounds__(256) void wdl_head_kernel(int B, int Fw, int H, const int64_t* __restrict__ wide,
                                                        int wide_ld, const float* __restrict__ h, int ldh,
                                                        const float* __restrict__ w, const float* __restrict__ bias,
@@ -178,9 +184,9 @@ __global__ __launch_bounds__(256) void wdl_head_kernel(int B, int Fw, int H, con
   const int nwaves = (gridDim.x * blockDim.x) >> 6;
   const int H4 = (H + 3) / 4;
   const float b0 = bias[0];
-  float4 wh[kHeadMaxH4], gh[kHeadMaxH4];
+  float4 wh[H4M], gh[H4M];
 #pragma unroll
-  for (int k = 0; k < kHeadMaxH4; ++k) {
+  for (int k = 0; k < H4M; ++k) {
     const int c = 4 * (lane + 64 * k);
     wh[k].x = c + 0 < H ? w[Fw + c + 0] : 0.f;
     wh[k].y = c + 1 < H ? w[Fw + c + 1] : 0.f;
@@ -199,20 +205,34 @@ __global__ __launch_bounds__(256) void wdl_head_kernel(int B, int Fw, int H, con
   float wv_n = id_n >= 0 ? w[id_n] : 0.f;
   long long id_nn = load_id(wave + nwaves);
   float gb = 0.f, lsum = 0.f;
+  // sample bb's h row (zeros past B or H)
+  auto load_h = [&](int bb, float4 (&r)[H4M]) {
+    const float* hb = h + (long long)min(bb, B - 1) * ldh;
+#pragma unroll
+    for (int k = 0; k < H4M; ++k) {
+      const int c4 = lane + 64 * k;
+      r[k] = (c4 < H4 && bb < B) ? *reinterpret_cast<const float4*>(hb + 4 * c4) : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+  };
+  float4 hn[H4M];
+  if (DL_WDL_HEAD_PF) load_h(wave, hn);
   for (int b = wave; b < B; b += nwaves) {
     const long long wr = id_n;
     float part = wv_n;
     id_n = id_nn;
     wv_n = id_n >= 0 ? w[id_n] : 0.f;
     id_nn = load_id(b + 2 * nwaves);
-    float4 hh[kHeadMaxH4];
-    const float* hb = h + (long long)b * ldh;
+    float4 hh[H4M];
+    if (DL_WDL_HEAD_PF) {
 #pragma unroll
-    for (int k = 0; k < kHeadMaxH4; ++k) {
-      const int c4 = lane + 64 * k;
-      hh[k] = c4 < H4 ? *reinterpret_cast<const float4*>(hb + 4 * c4) : make_float4(0.f, 0.f, 0.f, 0.f);
-      part += hh[k].x * wh[k].x + hh[k].y * wh[k].y + hh[k].z * wh[k].z + hh[k].w * wh[k].w;
+      for (int k = 0; k < H4M; ++k) hh[k] = hn[k];
+      load_h(b + nwaves, hn);   // the next sample's row, in flight during this one
+    } else {
+      load_h(b, hh);
     }
+#pragma unroll
+    for (int k = 0; k < H4M; ++k)
+      part += hh[k].x * wh[k].x + hh[k].y * wh[k].y + hh[k].z * wh[k].z + hh[k].w * wh[k].w;
     const float z = wave_sum(part) + b0;
     const float p = 1.f / (1.f + expf(-z));
     const float y = label[b];
@@ -229,7 +249,7 @@ __global__ __launch_bounds__(256) void wdl_head_kernel(int B, int Fw, int H, con
       if (touched) touched[wr] = 1;
     }
 #pragma unroll
-    for (int k = 0; k < kHeadMaxH4; ++k) {
+    for (int k = 0; k < H4M; ++k) {
       const int c4 = lane + 64 * k;
       gh[k].x += g * hh[k].x; gh[k].y += g * hh[k].y; gh[k].z += g * hh[k].z; gh[k].w += g * hh[k].w;
       if (c4 < H4) {
@@ -260,7 +280,7 @@ __global__ __launch_bounds__(256) void wdl_head_kernel(int B, int Fw, int H, con
   const int width = H + 2;
   extern __shared__ __attribute__((aligned(16))) float red[];
 #pragma unroll
-  for (int k = 0; k < kHeadMaxH4; ++k) {
+  for (int k = 0; k < H4M; ++k) {
     const int c = 4 * (lane + 64 * k);
     float* o = red + wid * width;
     if (c + 0 < H) o[c + 0] = gh[k].x;
@@ -315,7 +335,8 @@ static int wdl_head(int32_t B, int32_t Fw, int32_t H, const int64_t* wide, int32
   DL_CHECK_ARG(slab_blocks >= grid, "slab needs %d blocks", grid);
   if (B == 0) return 0;
   const size_t lds = 4 * (size_t)(H + 2) * sizeof(float);
-  hipLaunchKernelGGL(wdl_head_kernel<DHB>, dim3(grid), dim3(256), lds, as_stream(stream), B, Fw, H, wide, wide_ld,
+  auto kern = H <= 4 * 64 * 2 ? wdl_head_kernel<DHB, 2> : wdl_head_kernel<DHB, kHeadMaxH4>;
+  hipLaunchKernelGGL(kern, dim3(grid), dim3(256), lds, as_stream(stream), B, Fw, H, wide, wide_ld,
                      h, ldh, w, bias, (long long)w_rows, label, eps, inv_batch, score, z_out, dz, dh,
                      reinterpret_cast<long long*>(g_w), touched,
                      slab, err);

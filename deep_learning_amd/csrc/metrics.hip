@@ -252,22 +252,27 @@ extern "C" int dl_auc(const float* scores, int64_t s_stride, const float* labels
 }
 
 // ---------------------------------------------------------------------------
-// The measured HBM yardstick (bench.py roofline.peak_measured): a streaming copy of whole 16-B
-// pieces, four in flight per thread, grid-stride over a grid that fills every CU.  What a plain
-// read-once / write-once stream reaches on this chip, beside the 8 TB/s specification the
-// roofline fractions are priced against.
-__global__ __launch_bounds__(256) void hbm_copy_kernel(const uint4* __restrict__ src, uint4* __restrict__ dst,
+// The measured HBM yardstick (bench.py roofline.peak_measured): a streaming copy, each block one
+// chunk of 8 x 256 16-B pieces, all eight non-temporal loads in flight before the non-temporal
+// stores — the fastest of the copy forms scripts/ubench_copy.hip measured on this chip (5.56
+// TB/s at 1 and 4 GiB; grid-stride plain copies 4.2-4.7, torch's copy_ 5.0-5.2,
+// profiles/r06d/ubench_copy.txt): what a read-once / write-once stream reaches here, beside the
+// 8 TB/s specification the roofline fractions are priced against.
+typedef unsigned int hbm_u4 __attribute__((ext_vector_type(4)));
+__global__ __launch_bounds__(256) void hbm_copy_kernel(const hbm_u4* __restrict__ src, hbm_u4* __restrict__ dst,
                                                        long long n16) {
-  const long long stride = (long long)gridDim.x * blockDim.x;
-  long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-  for (; i + 3 * stride < n16; i += 4 * stride) {
-    const uint4 a = src[i], b = src[i + stride], c = src[i + 2 * stride], d = src[i + 3 * stride];
-    dst[i] = a;
-    dst[i + stride] = b;
-    dst[i + 2 * stride] = c;
-    dst[i + 3 * stride] = d;
+  const long long c0 = (long long)blockIdx.x * 2048;
+  hbm_u4 v[8];
+#pragma unroll
+  for (int u = 0; u < 8; ++u) {
+    const long long i = c0 + u * 256 + threadIdx.x;
+    if (i < n16) v[u] = __builtin_nontemporal_load(src + i);
   }
-  for (; i < n16; i += stride) dst[i] = src[i];
+#pragma unroll
+  for (int u = 0; u < 8; ++u) {
+    const long long i = c0 + u * 256 + threadIdx.x;
+    if (i < n16) __builtin_nontemporal_store(v[u], dst + i);
+  }
 }
 
 extern "C" int dl_hbm_copy(const void* src, void* dst, int64_t bytes, void* stream) {
@@ -276,9 +281,8 @@ extern "C" int dl_hbm_copy(const void* src, void* dst, int64_t bytes, void* stre
   DL_CHECK_ARG(((uintptr_t)src | (uintptr_t)dst) % 16 == 0, "dl_hbm_copy: 16-B alignment");
   if (bytes == 0) return 0;
   const long long n16 = bytes / 16;
-  const long long want = (n16 + 1023) / 1024;   // ~4 pieces a thread a round
-  const unsigned grid = (unsigned)std::max(1LL, std::min(want, 256LL * 16));
-  hipLaunchKernelGGL(hbm_copy_kernel, dim3(grid), dim3(256), 0, as_stream(stream), reinterpret_cast<const uint4*>(src),
-                     reinterpret_cast<uint4*>(dst), n16);
+  DL_CHECK_ARG((n16 + 2047) / 2048 < (1LL << 31), "dl_hbm_copy: too many bytes");
+  hipLaunchKernelGGL(hbm_copy_kernel, dim3((unsigned)((n16 + 2047) / 2048)), dim3(256), 0, as_stream(stream),
+                     reinterpret_cast<const hbm_u4*>(src), reinterpret_cast<hbm_u4*>(dst), n16);
   DL_RETURN_LAUNCH("dl_hbm_copy");
 }

@@ -43,7 +43,7 @@
 // gather's replay.  64 B a row less written by the gather and read back by the backward, for
 // one random 64-B read of the record's second line.
 #ifndef DL_STASH_M
-#define DL_STASH_M 1
+#define DL_STASH_M 0
 #endif
 #if DL_STASH_M && !DL_ROOT_STATE
 #error "DL_STASH_M needs the root state (DL_ROOT_STATE=1)"
@@ -509,6 +509,7 @@ __device__ __forceinline__ void rec_bwd_state(int64_t row, long long iu, int q, 
                                               const RecCfg& c, int t, const RingW& ring, float4& p, float4& m,
                                               float4& v, float& w, float& wm, float& wv) {
   if (STASH || mv) {
+    if (DL_BWD_DIAG & 4) iu = 0;   // diagnostics: the stash and compact rows from one cached row
     p = rec_ld4(rows_u + iu * E + 4 * q);
     const float* o = mv + iu * rec_stash_floats(E);
     m = rec_ld4(o + 4 * q);

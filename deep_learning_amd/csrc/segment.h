@@ -11,8 +11,8 @@
 
 // Diagnostics builds only (wrong results): DL_BWD_DIAG bits redirect one of the backward's
 // access streams to a cache-resident address, so PMC bytes and time split by stream —
-// 1: the dx0 slices, 2: the fm_sum rows (segment_grad4_range), 4: the stash rows,
-// 8: the record writes (rec.hip rec_bwd_state / rec_bwd_apply).
+// 1: the dx0 slices, 2: the fm_sum rows, 16: the pooled-slot gradients (segment_grad4_range,
+// seg_fetch), 4: the stash rows, 8: the record writes (rec.hip rec_bwd_state / rec_bwd_apply).
 #ifndef DL_BWD_DIAG
 #define DL_BWD_DIAG 0
 #endif
@@ -157,9 +157,10 @@ __device__ __forceinline__ SegGrad4 segment_grad4_range(const SegGradIn& a, int 
       const int m = seg_slot_of(a, sl - mb);
       if (m == a.n_slots) continue;
       const long long bm = (long long)b * a.n_slots + m;
-      const float4 gp = *reinterpret_cast<const float4*>(a.g_pool + bm * a.g_pitch + 4 * q);
+      const long long bmd = (DL_BWD_DIAG & 16) ? 0 : bm;
+      const float4 gp = *reinterpret_cast<const float4*>(a.g_pool + bmd * a.g_pitch + 4 * q);
       r.x.x += gp.x; r.x.y += gp.y; r.x.z += gp.z; r.x.w += gp.w;
-      if (a.g1_pool) r.g1 += a.g1_pool[bm * a.g1_stride];
+      if (a.g1_pool) r.g1 += a.g1_pool[bmd * a.g1_stride];
     } else if (L.use_fm && sl < S) {
       const float dzb = a.dz[b];
       const float4 fs = *reinterpret_cast<const float4*>(a.fm_sum + (long long)((DL_BWD_DIAG & 2) ? 0 : b) * E + 4 * q);
@@ -204,17 +205,19 @@ __device__ __forceinline__ SegRef seg_fetch(const SegGradIn& a, bool in, int k, 
     if (m == a.n_slots) return f;
     const long long bm = (long long)b * a.n_slots + m;
     f.kind = 1;
-    f.v = *reinterpret_cast<const float4*>(a.g_pool + bm * a.g_pitch + 4 * q);
-    f.w = a.g1_pool ? a.g1_pool[bm * a.g1_stride] : 0.f;
+    const long long bmd = (DL_BWD_DIAG & 16) ? 0 : bm;
+    f.v = *reinterpret_cast<const float4*>(a.g_pool + bmd * a.g_pitch + 4 * q);
+    f.w = a.g1_pool ? a.g1_pool[bmd * a.g1_stride] : 0.f;
   } else if (L.use_fm && sl < S) {
     f.kind = 2;
     f.dzb = a.dz[b];
-    f.v = *reinterpret_cast<const float4*>(a.fm_sum + (long long)b * E + 4 * q);
+    f.v = *reinterpret_cast<const float4*>(a.fm_sum + (long long)((DL_BWD_DIAG & 2) ? 0 : b) * E + 4 * q);
     f.w = a.w_head[Cf + sl];
   } else {
     const int fi = L.use_fm ? sl - S : sl;
     f.kind = 3;
-    f.v = *reinterpret_cast<const float4*>(a.dx0 + (long long)b * L.dx0_ld + L.dx0_cat_col + fi * E + 4 * q);
+    f.v = *reinterpret_cast<const float4*>(a.dx0 + (long long)((DL_BWD_DIAG & 1) ? 0 : b) * L.dx0_ld + L.dx0_cat_col +
+                                           fi * E + 4 * q);
   }
   return f;
 }
