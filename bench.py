@@ -217,8 +217,10 @@ C1 = dict(C=13, V=0, S=26, E=8, cate_index_size=10_000, hidden=[512, 256, 128])
 
 
 def hbm_peak_measured(gib=1.0, reps=10):
-    """The chip's streaming rate measured here (dl_hbm_copy: 16-B pieces, read once, written once),
-    reported beside HBM_PEAK_GBS (the 8 TB/s specification the roofline fractions use)."""
+    """The chip's streaming rate measured here, reported beside HBM_PEAK_GBS (the 8 TB/s
+    specification the roofline fractions use): dl_hbm_copy (metrics.hip: 16-B pieces, read once,
+    written once) and torch's own device copy (a yardstick only) on the same buffers; the faster
+    of the two is the measured peak (the two trade places from box to box, profiles/r06f)."""
     import torch
     from deep_learning_amd import _lib
     from deep_learning_amd._lib import call, ptr
@@ -226,21 +228,32 @@ def hbm_peak_measured(gib=1.0, reps=10):
     a = torch.empty(n, dtype=torch.uint8, device="cuda").fill_(1)
     b = torch.empty_like(a)
     s = _lib.stream_handle()
-    for _ in range(3):
-        call("dl_hbm_copy", ptr(a), ptr(b), n, s)
-    torch.cuda.synchronize()
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    e0.record()
-    for _ in range(reps):
-        call("dl_hbm_copy", ptr(a), ptr(b), n, s)
-    e1.record()
-    torch.cuda.synchronize()
-    us = e0.elapsed_time(e1) * 1e3 / reps
+
+    def timed(fn):
+        for _ in range(3):
+            fn()
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(reps):
+            fn()
+        e1.record()
+        torch.cuda.synchronize()
+        return e0.elapsed_time(e1) * 1e3 / reps
+
+    us_dl = timed(lambda: call("dl_hbm_copy", ptr(a), ptr(b), n, s))
+    assert bool((b[:: 1 << 20] == 1).all())
+    b.zero_()
+    us_t = timed(lambda: b.copy_(a))
     assert bool((b[:: 1 << 20] == 1).all())
     del a, b
     torch.cuda.empty_cache()
-    return {"GB/s": round(2 * n / (us * 1e-6) / 1e9, 1), "kernel": "dl_hbm_copy (metrics.hip)",
-            "bytes_per_launch": 2 * n, "us": round(us, 1)}
+    gbs = lambda us: round(2 * n / (us * 1e-6) / 1e9, 1)
+    best = min(us_dl, us_t)
+    return {"GB/s": gbs(best), "kernel": "dl_hbm_copy (metrics.hip)" if us_dl <= us_t else "torch copy_",
+            "bytes_per_launch": 2 * n, "us": round(best, 1),
+            "dl_hbm_copy": {"us": round(us_dl, 1), "GB/s": gbs(us_dl)},
+            "torch_copy": {"us": round(us_t, 1), "GB/s": gbs(us_t)}}
 
 
 def c1_leg(steps_time=50, warm=10, steps_auc=60, n_eval=4, seed=11):
@@ -404,7 +417,49 @@ def lookup_alone(eng, batch, B, per_sample, reps=20):
 
     us, gb, fr = timed(planes)
     rus, rgb, rfr = timed(records)
-    return {"kernels": ["embed_fwd (slot plane)"], "us": us, "GB/s": gb, "frac": fr,
+    fused = None
+    if eng.fused_gather_l0():
+        # predict's fused form (the default on current planes): the lookup writes only the FM
+        # outputs and x0's cont columns, the first tower layer reads the deep rows from the plane
+        # through the ids (dl_gemm_s3_nt_gather).  What the gather costs there is the FM lookup
+        # plus what the fused layer takes beyond the same layer over a written x0.
+        FLn = eng._flat_layout(B)
+        FLn.x0_cat_col = -1
+        hd, ld0, ol0 = sp.hidden[0], eng.in_ld[0], eng.out_ld[0]
+        bits = (ptr(eng.hbits[0]), eng.hbits_ld[0]) if eng.hbits else (None, 0)
+
+        def fm_only():
+            if sp.fm:
+                call("dl_embed_fwd_slots", C_ref(FLn), ptr(eng.p_plane), ptr(eng.in_cate), ptr(eng.in_cont),
+                     ptr(eng.in_vec), ptr(x0), ptr(eng.fm_out), ptr(eng.fm_sum), ptr(eng.err), s)
+            else:
+                call("dl_embed_fwd", C_ref(FLn), ptr(eng.p_plane), None, ptr(eng.in_cate), ptr(eng.in_cont),
+                     ptr(eng.in_vec), ptr(x0), ptr(eng.fm_out), ptr(eng.fm_sum), ptr(eng.err), s)
+
+        def l0_plain():
+            call("dl_gemm_s3_nt_bits", B, hd, ld0, ptr(x0), ld0, ptr(eng.WTp[0]), ld0, ld0 * ol0, ptr(eng.h[0]),
+                 eng.h_ld[0], 1, None, 0, *bits, s)
+
+        def l0_gather():
+            call("dl_gemm_s3_nt_gather", B, hd, ld0, ptr(x0), ld0, ptr(eng.p_plane), FLn.n_rows,
+                 eng.p_plane.shape[1], ptr(eng.in_cate), FLn.cate_ld, FLn.deep_cate_offset, FLn.zero_row0, sp.S,
+                 sp.E, ptr(eng.WTp[0]), ld0, ld0 * ol0, ptr(eng.h[0]), eng.h_ld[0], 1, *bits, s)
+
+        fus = timed(fm_only)[0]
+        l0u = timed(l0_plain)[0]
+        l0g = timed(l0_gather)[0]
+        pair_u = timed(lambda: (planes(), l0_plain()))[0]
+        pair_f = timed(lambda: (fm_only(), l0_gather()))[0]
+        g_us = fus + max(l0g - l0u, 0.0)
+        g_gb = B * per_sample / (g_us * 1e-6) / 1e9
+        fused = {"kernels": ["embed_fwd (FM only)", "gemm_fwd_l0 (gather)"], "fm_lookup_us": fus,
+                 "fwd_l0_gather_us": l0g, "fwd_l0_plain_us": l0u,
+                 "us": round(g_us, 1), "GB/s": round(g_gb, 1), "frac": round(g_gb / HBM_PEAK_GBS, 3),
+                 "lookup_plus_l0_us": {"unfused": pair_u, "fused": pair_f},
+                 "note": "us = the FM-only lookup + (fused first layer - the same layer over a written x0): "
+                         "what the 3,640 B/sample gather adds to predict's forward when it feeds the MFMA "
+                         "tiles directly"}
+    return {"kernels": ["embed_fwd (slot plane)"], "us": us, "GB/s": gb, "frac": fr, "fused": fused,
             "records": {"kernels": ["rec_gather (13 cont rows)", "embed_fwd_rec_flat"], "us": rus, "GB/s": rgb,
                         "frac": rfr},
             "note": "flushed table: the lookup without lazy Adam's catch-up, as predict runs it (the flush writes "
@@ -678,6 +733,7 @@ def _run_workload(wl, args, world, rank, sharded, steps, warmup, age, ksteps, ba
                 z = lookup_alone(eng, zb, B, per_sample)
                 gather_lookup["zipf"] = {k: z[k] for k in ("us", "GB/s", "frac")}
                 gather_lookup["zipf"]["records"] = z["records"]
+                gather_lookup["zipf"]["fused"] = z["fused"]
                 del zb
             if gather is not None:
                 gather["lookup_alone"] = gather_lookup

@@ -74,7 +74,9 @@ constexpr int kMaxSlots = 128;     // FM slots + deep slots per sample
 // already caught up (a flushed table: predict after dl_rec_flush) — only each record's first
 // 128-B line is read (p and the first-order triple + stamp), a stale row faults (DL_STATUS_LAG).
 template <int E, int NPS, int REC = 0>
-__global__ __launch_bounds__(256, (REC == 1 || NPS > 5) ? 1 : DL_FWD_MIN_WAVES) void embed_fwd_kernel(EmbArgs a) {
+// (two samples in flight a wave, SPW below: 4 waves a SIMD, up to 128 VGPRs)
+__global__ __launch_bounds__(256, (REC == 1 || NPS > 5) ? 1 : ((REC == 0 || REC == 3) && NPS <= 3) ? 4 : DL_FWD_MIN_WAVES)
+void embed_fwd_kernel(EmbArgs a) {
   // Per block iteration a tile of 16 samples is staged: every (sample, slot)
   // row index is resolved once into LDS by a coalesced pass over the id matrix
   // (slot = FM field f < Fs, or deep field Fs + f).  Each wave then owns 4
@@ -96,7 +98,7 @@ __global__ __launch_bounds__(256, (REC == 1 || NPS > 5) ? 1 : DL_FWD_MIN_WAVES) 
   const int S = L.cate_fields;
   const int Fs = L.use_fm ? Cf + S : 0;
   const int F = Fs + L.fm_extra;
-  const int nslot = Fs + S;
+  const int nslot = Fs + (L.x0_cat_col >= 0 ? S : 0);   // -1: the deep rows are not looked up here
   const float4* tab4 = reinterpret_cast<const float4*>(a.table);
   const float4 z4 = f4_zero();
   const int ntiles = (L.batch + kTileSamples - 1) / kTileSamples;
@@ -167,91 +169,108 @@ __global__ __launch_bounds__(256, (REC == 1 || NPS > 5) ? 1 : DL_FWD_MIN_WAVES) 
     for (int k = threadIdx.x; k < nb * Cf; k += blockDim.x)
       vals_s[k / Cf][k % Cf] = a.cont[(int64_t)(b0 + k / Cf) * L.cont_fields + k % Cf];
     __syncthreads();
-    for (int j = wid; j < nb; j += 4) {
+    // SPW samples per wave iteration, all their row loads issued before any is consumed (the
+    // plain / slot-plane lookups with few passes a sample — e.g. the FM-only lookup of the fused
+    // predict — are latency-bound with one sample's rows in flight); the record modes keep one
+    constexpr int SPW = (REC == 0 || REC == 3) && NPS <= 3 ? 2 : 1;
+    for (int jw = wid; jw < nb; jw += 4 * SPW) {
+      float4 v[SPW][NPS];
+      int rw[SPW][NPS];
+      float w1[SPW], val[SPW];
+      int frow[SPW];
+      bool w1_done[SPW];
+#pragma unroll
+      for (int u = 0; u < SPW; ++u) {
+        const int j = min(jw + 4 * u, nb - 1);   // past the tile: repeats its last sample, not written
+        const int b = b0 + j;
+#pragma unroll
+        for (int p = 0; p < NPS; ++p) {
+          const int sl = p * RPI + r;
+          rw[u][p] = rows_s[j][sl < nslot ? sl : 0];
+          if (sl >= nslot) rw[u][p] = -1;
+        }
+        if (!RECS) {
+#pragma unroll
+          for (int p = 0; p < NPS; ++p) v[u][p] = tab4[(int64_t)(rw[u][p] < 0 ? 0 : rw[u][p]) * TP + q];
+        } else if (REC == 2) {
+          float4 t4[NPS];
+#pragma unroll
+          for (int p = 0; p < NPS; ++p) {
+            const int sl = p * RPI + r;
+            if (sl < Cf) {
+              v[u][p] = tab4[(rw[u][p] < 0 ? 0 : rw[u][p]) * LPR + q];
+            } else {
+              const float* rr = a.rec + (int64_t)(rw[u][p] < 0 ? 0 : rw[u][p]) * rc.ld;
+              v[u][p] = *reinterpret_cast<const float4*>(rr + 4 * q);
+              t4[p] = *reinterpret_cast<const float4*>(rr + E);
+            }
+          }
+#pragma unroll
+          for (int p = 0; p < NPS; ++p) {
+            const int sl = p * RPI + r;
+            if (sl >= Cf && sl < nslot) {
+              if (rw[u][p] >= 0 && __float_as_int(t4[p].w) != target) raise_fault(rc.status, DL_STATUS_LAG);
+              if (sl < Fs && rc.has_first && q == 0) a.fm_out[(int64_t)b * L.fm_ld + sl] = rw[u][p] < 0 ? 0.f : t4[p].x * 1.f;
+            }
+          }
+        } else {
+          // slots >= Cf: the whole record (p, m, v, first-order triple + stamp) is loaded for
+          // every pass before any is consumed, then caught up exactly as dl_rec_gather does
+          // (same catch_up4 on the same float4): the values are bit-identical to the
+          // gathered rows the indexed forward reads.
+          float4 m4[NPS], v4[NPS], t4[NPS];
+#pragma unroll
+          for (int p = 0; p < NPS; ++p) {
+            const int sl = p * RPI + r;
+            if (sl < Cf) {
+              v[u][p] = tab4[(rw[u][p] < 0 ? 0 : rw[u][p]) * LPR + q];
+            } else {
+              const float* rr = a.rec + (int64_t)(rw[u][p] < 0 ? 0 : rw[u][p]) * rc.ld;
+              v[u][p] = *reinterpret_cast<const float4*>(rr + 4 * q);
+              m4[p] = *reinterpret_cast<const float4*>(rr + E + 4 + 4 * q);
+              v4[p] = *reinterpret_cast<const float4*>(rr + 2 * E + 4 + 4 * q);
+              t4[p] = *reinterpret_cast<const float4*>(rr + E);
+            }
+          }
+#pragma unroll
+          for (int p = 0; p < NPS; ++p) {
+            const int sl = p * RPI + r;
+            if (sl >= Cf && sl < nslot) {
+              const bool fmf = sl < Fs && rc.has_first && q == 0;   // FM slot: its first-order weight too
+              float w = t4[p].x, wm = t4[p].y, wv = t4[p].z;
+              const int stamp = __float_as_int(t4[p].w);
+              if (stamp < target) catch_up4(v[u][p], m4[p], v4[p], w, wm, wv, fmf, stamp, target, RingG{hist_s, rc.hist_mask}, rc);
+              if (fmf) a.fm_out[(int64_t)b * L.fm_ld + sl] = rw[u][p] < 0 ? 0.f : w * 1.f;
+            }
+          }
+        }
+        // first-order terms (one lane per FM field; record mode: the cont fields only)
+        w1[u] = 0.f;
+        val[u] = 0.f;
+        frow[u] = -1;
+        // staged: the FM cate fields' first-order outputs were written by the gather (their rows
+        // index the staging rows, not first_order) — only the zero rows' are written here
+        w1_done[u] = a.staged && lane >= Cf && lane < Fs && rows_s[j][lane] >= 0;
+        if (lane < (RECS ? Cf : Fs)) {
+          frow[u] = rows_s[j][lane];
+          val[u] = lane < Cf ? vals_s[j][lane] : 1.f;
+          w1[u] = DL_POOL_DIAG_NO_W1 ? 1.f : a.first_order[(int64_t)((frow[u] < 0 || w1_done[u]) ? 0 : frow[u]) * W1S];
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < SPW; ++u) {
+      const int j = jw + 4 * u;
+      if (u > 0 && j >= nb) break;   // wave-uniform
       const int b = b0 + j;
       float* xb = a.x0 + (int64_t)b * L.x0_ld;
       // bf16 x0 (L.x0_bf16): the same columns, as bf16 (a.x0 then points at uint16 storage)
       unsigned short* xbb = reinterpret_cast<unsigned short*>(a.x0) + (int64_t)b * L.x0_ld;
-      float4 v[NPS];
-      int rw[NPS];
-#pragma unroll
-      for (int p = 0; p < NPS; ++p) {
-        const int sl = p * RPI + r;
-        rw[p] = rows_s[j][sl < nslot ? sl : 0];
-        if (sl >= nslot) rw[p] = -1;
-      }
-      if (!RECS) {
-#pragma unroll
-        for (int p = 0; p < NPS; ++p) v[p] = tab4[(int64_t)(rw[p] < 0 ? 0 : rw[p]) * TP + q];
-      } else if (REC == 2) {
-        float4 t4[NPS];
-#pragma unroll
-        for (int p = 0; p < NPS; ++p) {
-          const int sl = p * RPI + r;
-          if (sl < Cf) {
-            v[p] = tab4[(rw[p] < 0 ? 0 : rw[p]) * LPR + q];
-          } else {
-            const float* rr = a.rec + (int64_t)(rw[p] < 0 ? 0 : rw[p]) * rc.ld;
-            v[p] = *reinterpret_cast<const float4*>(rr + 4 * q);
-            t4[p] = *reinterpret_cast<const float4*>(rr + E);
-          }
-        }
-#pragma unroll
-        for (int p = 0; p < NPS; ++p) {
-          const int sl = p * RPI + r;
-          if (sl >= Cf && sl < nslot) {
-            if (rw[p] >= 0 && __float_as_int(t4[p].w) != target) raise_fault(rc.status, DL_STATUS_LAG);
-            if (sl < Fs && rc.has_first && q == 0) a.fm_out[(int64_t)b * L.fm_ld + sl] = rw[p] < 0 ? 0.f : t4[p].x * 1.f;
-          }
-        }
-      } else {
-        // slots >= Cf: the whole record (p, m, v, first-order triple + stamp) is loaded for
-        // every pass before any is consumed, then caught up exactly as dl_rec_gather does
-        // (same catch_up4 on the same float4): the values are bit-identical to the
-        // gathered rows the indexed forward reads.
-        float4 m4[NPS], v4[NPS], t4[NPS];
-#pragma unroll
-        for (int p = 0; p < NPS; ++p) {
-          const int sl = p * RPI + r;
-          if (sl < Cf) {
-            v[p] = tab4[(rw[p] < 0 ? 0 : rw[p]) * LPR + q];
-          } else {
-            const float* rr = a.rec + (int64_t)(rw[p] < 0 ? 0 : rw[p]) * rc.ld;
-            v[p] = *reinterpret_cast<const float4*>(rr + 4 * q);
-            m4[p] = *reinterpret_cast<const float4*>(rr + E + 4 + 4 * q);
-            v4[p] = *reinterpret_cast<const float4*>(rr + 2 * E + 4 + 4 * q);
-            t4[p] = *reinterpret_cast<const float4*>(rr + E);
-          }
-        }
-#pragma unroll
-        for (int p = 0; p < NPS; ++p) {
-          const int sl = p * RPI + r;
-          if (sl >= Cf && sl < nslot) {
-            const bool fmf = sl < Fs && rc.has_first && q == 0;   // FM slot: its first-order weight too
-            float w = t4[p].x, wm = t4[p].y, wv = t4[p].z;
-            const int stamp = __float_as_int(t4[p].w);
-            if (stamp < target) catch_up4(v[p], m4[p], v4[p], w, wm, wv, fmf, stamp, target, RingG{hist_s, rc.hist_mask}, rc);
-            if (fmf) a.fm_out[(int64_t)b * L.fm_ld + sl] = rw[p] < 0 ? 0.f : w * 1.f;
-          }
-        }
-      }
-      // first-order terms (one lane per FM field; record mode: the cont fields only)
-      float w1 = 0.f, val = 0.f;
-      int frow = -1;
-      // staged: the FM cate fields' first-order outputs were written by the gather (their rows
-      // index the staging rows, not first_order) — only the zero rows' are written here
-      const bool w1_done = a.staged && lane >= Cf && lane < Fs && rows_s[j][lane] >= 0;
-      if (lane < (RECS ? Cf : Fs)) {
-        frow = rows_s[j][lane];
-        val = lane < Cf ? vals_s[j][lane] : 1.f;
-        w1 = DL_POOL_DIAG_NO_W1 ? 1.f : a.first_order[(int64_t)((frow < 0 || w1_done) ? 0 : frow) * W1S];
-      }
       float4 s = z4, ss = z4;
 #pragma unroll
       for (int p = 0; p < NPS; ++p) {
         {
           const int sl = p * RPI + r;
-          const float4 t4 = rw[p] < 0 ? z4 : v[p];
+          const float4 t4 = rw[u][p] < 0 ? z4 : v[u][p];
           if (sl < Fs) {
             const float vv = sl < Cf ? vals_s[j][sl] : 1.f;
             // explicit roundings (no contraction left to the compiler): every instantiation
@@ -261,7 +280,7 @@ __global__ __launch_bounds__(256, (REC == 1 || NPS > 5) ? 1 : DL_FWD_MIN_WAVES) 
             s.x += ev.x; s.y += ev.y; s.z += ev.z; s.w += ev.w;
             ss.x = fmaf(ev.x, ev.x, ss.x); ss.y = fmaf(ev.y, ev.y, ss.y);
             ss.z = fmaf(ev.z, ev.z, ss.z); ss.w = fmaf(ev.w, ev.w, ss.w);
-          } else if (sl < nslot && rw[p] != -2) {
+          } else if (sl < nslot && rw[u][p] != -2) {
             const int col = L.x0_cat_col + (sl - Fs) * E + 4 * q;
             if (L.x0_bf16)
               *reinterpret_cast<uint2*>(xbb + col) = make_uint2(f2bf(t4.x) | ((unsigned)f2bf(t4.y) << 16),
@@ -271,7 +290,7 @@ __global__ __launch_bounds__(256, (REC == 1 || NPS > 5) ? 1 : DL_FWD_MIN_WAVES) 
           }
         }
       }
-      if (lane < (RECS ? Cf : Fs) && !w1_done) a.fm_out[(int64_t)b * L.fm_ld + lane] = frow < 0 ? 0.f : w1 * val;
+      if (lane < (RECS ? Cf : Fs) && !w1_done[u]) a.fm_out[(int64_t)b * L.fm_ld + lane] = frow[u] < 0 ? 0.f : w1[u] * val[u];
       for (int f = 64 + lane; f < (RECS ? 0 : Fs); f += 64) {   // > 64 FM fields (rare; record mode: <= 64)
         const int fr = rows_s[j][f];
         if (a.staged && f >= Cf && fr >= 0) continue;
@@ -312,6 +331,7 @@ __global__ __launch_bounds__(256, (REC == 1 || NPS > 5) ? 1 : DL_FWD_MIN_WAVES) 
           const float c = a.vec[(int64_t)b * L.vector_size + jj];
           if (L.x0_bf16) xbb[L.x0_vec_col + jj] = f2bf(c); else xb[L.x0_vec_col + jj] = c;
         }
+      }
     }
     __syncthreads();
   }
@@ -931,12 +951,15 @@ __global__ __launch_bounds__(256) void pool_bwd_kernel(PoolBwdArgs a) {
   }
 }
 
-static int check_layout(const dl_emb_layout* L) {
+// no_cat_ok: x0_cat_col == -1 accepted (the plain table lookups only: the single-cate
+// embeddings are then not written, dl_gemm_s3_nt_gather reads them from the table itself)
+static int check_layout(const dl_emb_layout* L, bool no_cat_ok = false) {
   DL_CHECK_ARG(L != nullptr, "layout is NULL");
   const int E = L->emb_dim;
   DL_CHECK_ARG(E == 4 || E == 8 || E == 16 || E == 32 || E == 64, "emb_dim %d not in {4,8,16,32,64}", E);
   DL_CHECK_ARG(L->batch >= 0 && L->n_rows > 0, "bad batch/n_rows");
-  DL_CHECK_ARG(L->x0_ld % 4 == 0 && L->x0_cat_col % 4 == 0, "x0_ld and x0_cat_col must be multiples of 4");
+  DL_CHECK_ARG(L->x0_ld % 4 == 0 && (L->x0_cat_col % 4 == 0 || (no_cat_ok && L->x0_cat_col == -1)),
+               "x0_ld and x0_cat_col must be multiples of 4");
   DL_CHECK_ARG(!L->x0_bf16 || L->fm_extra == 0, "bf16 x0 needs fm_extra == 0 (pooled vectors are read as f32)");
   DL_CHECK_ARG(!L->fm_extra || L->x0_pool_col % 4 == 0, "x0_pool_col must be a multiple of 4");
   DL_CHECK_ARG(L->cont_fields <= kMaxHotCont || !(L->use_fm && L->fm_cont),
@@ -960,7 +983,7 @@ static int launch_embed_fwd(const dl_emb_layout* L, const EmbArgs& a, void* stre
 extern "C" int dl_embed_fwd(const dl_emb_layout* L, const float* table, const float* first_order,
                             const int64_t* cate, const float* cont, const float* vector,
                             float* x0, float* fm_out, float* fm_sum, int32_t* err, void* stream) {
-  if (int rc = check_layout(L)) return rc;
+  if (int rc = check_layout(L, true)) return rc;
   DL_CHECK_ARG(table && cate && x0, "NULL table/cate/x0");
   DL_CHECK_ARG(!L->use_fm || (first_order && fm_out && fm_sum), "FM outputs required");
   if (L->batch == 0) return 0;
@@ -971,7 +994,7 @@ extern "C" int dl_embed_fwd(const dl_emb_layout* L, const float* table, const fl
 extern "C" int dl_embed_fwd_slots(const dl_emb_layout* L, const float* slots, const int64_t* cate, const float* cont,
                                   const float* vector, float* x0, float* fm_out, float* fm_sum, int32_t* err,
                                   void* stream) {
-  if (int rc = check_layout(L)) return rc;
+  if (int rc = check_layout(L, true)) return rc;
   DL_CHECK_ARG(slots && cate && x0, "NULL slots/cate/x0");
   DL_CHECK_ARG(!L->use_fm || (fm_out && fm_sum), "FM outputs required");
   DL_CHECK_ARG((uintptr_t)slots % 16 == 0, "the slot plane must be 16-B aligned");
@@ -1052,9 +1075,10 @@ static int launch_embed_fwd(const dl_emb_layout* L, const EmbArgs& a, void* stre
   const int tiles = (L->batch + kTileSamples - 1) / kTileSamples;
   const int gmax = REC == 1 ? 1024 : 8192;   // record mode: each block stages the alpha ring once
   const dim3 grid(tiles < gmax ? tiles : gmax), block(256);
-  const int nslot = (L->use_fm ? (L->fm_cont ? L->cont_fields : 0) + L->cate_fields : 0) + L->cate_fields;
+  const int nslot = (L->use_fm ? (L->fm_cont ? L->cont_fields : 0) + L->cate_fields : 0) +
+                    (L->x0_cat_col >= 0 ? L->cate_fields : 0);
   const int rpi = 64 / (L->emb_dim / 4);
-  const int nps = (nslot + rpi - 1) / rpi;
+  const int nps = nslot > 0 ? (nslot + rpi - 1) / rpi : 1;
   const size_t lds = REC == 1 ? (size_t)(a.rc.hist_mask + 1) * sizeof(float) : 0;
   hipStream_t st = as_stream(stream);
 #define DL_FWD(E_, N_) hipLaunchKernelGGL((embed_fwd_kernel<E_, N_, REC>), grid, block, lds, st, a)

@@ -106,12 +106,23 @@ struct S3Params {
   long long c_split_stride;  // TN
   uint16_t* bits;            // NT: the ReLU sign bitmask [M][ldbits] (written by S3_RELU, read by S3_MASKBITS)
   int ldbits;
+  // NT gather (dl_gemm_s3_nt_gather): A's columns [0, 32 g_chunks) are the embedding rows of
+  // the row's ids (row ids[m][f] + id_off, f = k >> g_esh, column k & (2^g_esh - 1)), read
+  // straight from the table G (g_ld floats a row; a masked or invalid row reads as zeros)
+  const float* G;
+  const int64_t* ids;
+  long long id_off, n_rows;
+  int ids_ld, g_ld, g_fields, g_esh, g_chunks, zero_row0;
+  unsigned g_bytes;          // G's buffer range (bytes, < 0xFFFFFF00: the masked rows' offset)
 };
 
 // S3_MASKBITS: the ReluGrad mask from the forward's bitmask (bit c & 15 of halfword
 // [row][c >> 4] = h[row][c] > 0) instead of the f32 activations — 1/32 of the mask bytes
 enum { S3_STORE = 0, S3_RELU = 1, S3_MASK = 2, S3_MASKBITS = 3 };
 
+#ifndef DL_S3_GDIAG
+#define DL_S3_GDIAG 0   // diagnostics build: the gathered A rows all read table row 0 (timing only)
+#endif
 #ifndef DL_S3_BPF
 #define DL_S3_BPF 0   // 1: NT pins the next fragment's weight reads ahead of this one's MFMAs
 #endif                // (sched_barrier; measured slower than leaving the order to the scheduler)
@@ -169,6 +180,12 @@ constexpr int kNtDmaW = (kNtDma + 7) / 8;                        // per wave (5)
 constexpr size_t kNtLds = 3 * kNtBuf * sizeof(unsigned short);  // 119,808 B
 constexpr int kNtEP = kNtBN + 4;                                 // epilogue tile pitch (floats)
 static_assert(8 * 16 * kNtEP * sizeof(float) <= kNtLds, "epilogue tiles fit the ring");
+// NT gather: the block's row offsets into G, one u32 per (field, row) after the ring, fields
+// kNtGfs words apart (272 = 16 mod 64 banks: the 2-4 fields a wave instruction reads fall in
+// disjoint banks); at most kNtGmaxF fields within 160 KB of LDS
+constexpr int kNtGfs = 272;
+constexpr int kNtGmaxF = (160 * 1024 - (int)kNtLds) / (kNtGfs * 4);
+constexpr uint32_t kNtGmasked = 0xFFFFFF00u;
 
 __device__ __forceinline__ int nt_slot(int j, int kq) { return kq ^ ((j >> 2) & 2); }   // an involution in kq
 
@@ -192,7 +209,11 @@ __device__ __forceinline__ void nt_rd3(uint32_t a, shortx8& h, shortx8& m, short
 // 16 rows x 64 B), ReLU / ReluGrad bitmask in registers — instead of the transpose through the
 // LDS ring; the bitmask words the dX epilogue needs are loaded before the main loop.  Needs
 // N % 4 == 0, ldc % 4 == 0 and an even ldbits (the host picks it then; otherwise the LDS form).
-template <int EPI, bool DIRECT = false>
+// GATHER: the embedding-lookup fusion of the flushed-table forward (dl_gemm_s3_nt_gather): the
+// first 32 g_chunks columns of A are fetched row by row from the table through the ids (an 8-float
+// piece never straddles two rows: E % 8 == 0), the rest from A as usual.  The values are the
+// ones the lookup would have written to A (a copy), so C is bit-identical to the unfused pair.
+template <int EPI, bool DIRECT = false, bool GATHER = false>
 __global__ __launch_bounds__(512) void gemm_s3_nt_kernel(S3Params p) {
   extern __shared__ __attribute__((aligned(16))) unsigned short lds[];   // [3 bufs][3 planes][BN][32]
   constexpr int NW = 8, BM = kNtBM, DMAW = kNtDmaW;
@@ -250,7 +271,31 @@ __global__ __launch_bounds__(512) void gemm_s3_nt_kernel(S3Params p) {
   // A through a buffer descriptor: a piece outside M or K gets an offset past the descriptor's
   // range and reads as zeros, so no fixup follows a load (overwriting a register whose load
   // is in flight would cost a wait for it).
+  uint32_t* gtab = reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(lds) + kNtLds);
+  const auto g_rsrc = __builtin_amdgcn_make_buffer_rsrc((void*)p.G, (short)0, (int)p.g_bytes, 0x00020000);
   auto load_a = [&](int c, float4 (&ra)[4]) {
+    if constexpr (GATHER) {
+      if (c < p.g_chunks) {   // uniform: the chunk lies in the gathered columns
+        // this lane's two pieces of a row: k and k + 4 (natural order), or k = 32c + 4kq and
+        // k + 16 (DL_S3_KPERM: a wave instruction then reads whole 64-B rows, 16 B a lane)
+        const int ka = DL_S3_KPERM ? 32 * c + 4 * kq : 32 * c + 8 * kq;
+        const int kb = DL_S3_KPERM ? ka + 16 : ka + 4;
+        const uint32_t em = (1u << p.g_esh) - 1u;
+        const int fa = ka >> p.g_esh, fb = kb >> p.g_esh;
+        const uint32_t ca = 4u * ((uint32_t)ka & em), cb = 4u * ((uint32_t)kb & em);
+        const int r0l = wid * 32 + cl;
+        const uint32_t ta0 = gtab[fa * kNtGfs + r0l], ta1 = gtab[fa * kNtGfs + r0l + 16];
+        const uint32_t tb0 = fb == fa ? ta0 : gtab[fb * kNtGfs + r0l];
+        const uint32_t tb1 = fb == fa ? ta1 : gtab[fb * kNtGfs + r0l + 16];
+        const uint32_t a0 = ok0 ? ta0 + ca : kNtGmasked, b0 = ok0 ? tb0 + cb : kNtGmasked;
+        const uint32_t a1 = ok1 ? ta1 + ca : kNtGmasked, b1 = ok1 ? tb1 + cb : kNtGmasked;
+        ra[0] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(g_rsrc, (int)a0, 0, 0));
+        ra[1] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(g_rsrc, (int)b0, 0, 0));
+        ra[2] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(g_rsrc, (int)a1, 0, 0));
+        ra[3] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(g_rsrc, (int)b1, 0, 0));
+        return;
+      }
+    }
     if (DL_S3_DIAG == 3) {
       ra[0] = ra[1] = ra[2] = ra[3] = make_float4(1.f + c, 2.f, 3.f, 4.f);
       return;
@@ -292,10 +337,43 @@ __global__ __launch_bounds__(512) void gemm_s3_nt_kernel(S3Params p) {
 
   float4 raA[4], raB[4];
   // prologue: B chunks 0 and 1 in flight, A chunks 0 and 1
+  if constexpr (GATHER) {
+    // the weight DMA first, then the block's (field, row) table of row offsets from its ids
+    // (coalesced over the id matrix), published by a barrier before any A piece is fetched
+    dma_b(0, 0);
+    dma_b(1, 1);
+    // (eight ids a thread in flight at once: one memory round trip per 4,096 entries)
+    const int tot = BM * p.g_fields;
+    constexpr int kGU = 8;
+    for (int b = 0; b < tot; b += kGU * NW * 64) {
+      long long idv[kGU];
+#pragma unroll
+      for (int u = 0; u < kGU; ++u) {
+        const int i = min(b + u * NW * 64 + tid, tot - 1);
+        const int rr = i / p.g_fields, f = i - rr * p.g_fields;
+        idv[u] = p.ids[(long long)min(i0 + rr, p.M - 1) * p.ids_ld + f];
+      }
+#pragma unroll
+      for (int u = 0; u < kGU; ++u) {
+        const int i = b + u * NW * 64 + tid;
+        if (i < tot) {
+          const int rr = i / p.g_fields, f = i - rr * p.g_fields;
+          const long long id = idv[u] + p.id_off;
+          const bool v = id >= 0 && id < p.n_rows && (id > 0 || !p.zero_row0);
+          // DL_S3_GDIAG (diagnostics build, wrong results): every valid reference reads row 0
+          gtab[f * kNtGfs + rr] = v ? (DL_S3_GDIAG ? 0u : (uint32_t)id * (uint32_t)(4 * p.g_ld)) : kNtGmasked;
+        }
+      }
+    }
+    __syncthreads();
+    load_a(0, raA);
+    load_a(1, raB);
+  } else {
   dma_b(0, 0);
   load_a(0, raA);
   dma_b(1, 1);     // unconditional, like every prefetch below: chunks past KC read clamped
   load_a(1, raB);  // weights into a free buffer and zeros for A
+  }
 
   // The per-chunk barrier is a bare s_barrier after explicit counter waits: __syncthreads()
   // carries a workgroup release fence, which the compiler lowers to vmcnt(0) — a wait for
@@ -1172,9 +1250,9 @@ extern "C" int dl_split3(const float* src, int32_t rows, int32_t cols, int32_t l
   DL_RETURN_LAUNCH("dl_split3");
 }
 
-extern "C" int dl_gemm_s3_nt_bits(int32_t M, int32_t N, int32_t K, const float* A, int32_t lda, const uint16_t* Bp,
-                                  int32_t ldb, int64_t b_plane, float* C, int32_t ldc, int32_t epi, const float* mask,
-                                  int32_t ldm, uint16_t* bits, int32_t ldbits, void* stream) {
+static int s3_nt_check(int32_t M, int32_t N, int32_t K, const float* A, int32_t lda, const uint16_t* Bp,
+                       int32_t ldb, int64_t b_plane, float* C, int32_t ldc, int32_t epi, const float* mask,
+                       uint16_t* bits, int32_t ldbits) {
   DL_CHECK_ARG(M >= 0 && N >= 0 && K >= 0, "negative dims");
   DL_CHECK_ARG(A && Bp && C, "NULL operand");
   DL_CHECK_ARG(K % 8 == 0 && K >= 8, "K %d must be a positive multiple of 8", K);
@@ -1189,15 +1267,26 @@ extern "C" int dl_gemm_s3_nt_bits(int32_t M, int32_t N, int32_t K, const float* 
   DL_CHECK_ARG(!bits || epi == S3_RELU || epi == S3_MASKBITS, "a bitmask goes with the relu / bitmask epilogues");
   DL_CHECK_ARG((long long)M * lda * 4 < (1LL << 31), "A spans %lld bytes: past the 31-bit buffer range",
                (long long)M * lda * 4);
+  return 0;
+}
+
+static bool s3_nt_direct(int32_t M, int32_t N, int32_t ldc, int32_t epi, const uint16_t* bits, int32_t ldbits) {
+  return s3_direct_enabled() && N % 4 == 0 && ldc % 4 == 0 && (!bits || ldbits % 2 == 0) &&
+         epi != S3_MASK && (long long)M * ldc * 4 < (1LL << 31) &&
+         (epi != S3_MASKBITS || ldbits >= 2 * ((((int)ceil_div(N, kNtBN) - 1) * kNtBN >> 5) + 7));
+}
+
+extern "C" int dl_gemm_s3_nt_bits(int32_t M, int32_t N, int32_t K, const float* A, int32_t lda, const uint16_t* Bp,
+                                  int32_t ldb, int64_t b_plane, float* C, int32_t ldc, int32_t epi, const float* mask,
+                                  int32_t ldm, uint16_t* bits, int32_t ldbits, void* stream) {
+  if (int rc = s3_nt_check(M, N, K, A, lda, Bp, ldb, b_plane, C, ldc, epi, mask, bits, ldbits)) return rc;
   if (M == 0 || N == 0) return 0;
   S3Params p{};
   p.A = A; p.B = Bp; p.C = C; p.mask = mask;
   p.M = M; p.N = N; p.K = K; p.lda = lda; p.ldb = ldb; p.ldc = ldc; p.ldm = ldm; p.b_plane = b_plane;
   p.bits = bits; p.ldbits = ldbits;
   hipStream_t s = as_stream(stream);
-  const bool direct = s3_direct_enabled() && N % 4 == 0 && ldc % 4 == 0 && (!bits || ldbits % 2 == 0) &&
-                      epi != S3_MASK && (long long)M * ldc * 4 < (1LL << 31) &&
-                      (epi != S3_MASKBITS || ldbits >= 2 * ((((int)ceil_div(N, kNtBN) - 1) * kNtBN >> 5) + 7));
+  const bool direct = s3_nt_direct(M, N, ldc, epi, bits, ldbits);
   const int tiles = (int)(ceil_div(M, kNtBM) * ceil_div(N, kNtBN));
   if (direct) {
     if (epi == S3_STORE) hipLaunchKernelGGL((gemm_s3_nt_kernel<S3_STORE, true>), dim3(tiles), dim3(512), kNtLds, s, p);
@@ -1208,6 +1297,44 @@ extern "C" int dl_gemm_s3_nt_bits(int32_t M, int32_t N, int32_t K, const float* 
   else if (epi == S3_MASK) hipLaunchKernelGGL(gemm_s3_nt_kernel<S3_MASK>, dim3(tiles), dim3(512), kNtLds, s, p);
   else hipLaunchKernelGGL(gemm_s3_nt_kernel<S3_MASKBITS>, dim3(tiles), dim3(512), kNtLds, s, p);
   DL_RETURN_LAUNCH("dl_gemm_s3_nt");
+}
+
+extern "C" int dl_gemm_s3_nt_gather(int32_t M, int32_t N, int32_t K, const float* A, int32_t lda,
+                                    const float* table, int64_t n_rows, int32_t table_ld, const int64_t* ids,
+                                    int32_t ids_ld, int64_t id_offset, int32_t zero_row0, int32_t fields,
+                                    int32_t emb_dim, const uint16_t* Bp, int32_t ldb, int64_t b_plane, float* C,
+                                    int32_t ldc, int32_t epi, uint16_t* bits, int32_t ldbits, void* stream) {
+  if (int rc = s3_nt_check(M, N, K, A, lda, Bp, ldb, b_plane, C, ldc, epi, nullptr, bits, ldbits)) return rc;
+  DL_CHECK_ARG(epi == S3_STORE || epi == S3_RELU, "gather: epilogue %d (store / relu only)", epi);
+  DL_CHECK_ARG(table && ids, "gather: NULL table / ids");
+  DL_CHECK_ARG(emb_dim == 8 || emb_dim == 16 || emb_dim == 32 || emb_dim == 64, "gather: emb_dim %d", emb_dim);
+  DL_CHECK_ARG(fields > 0 && fields <= kNtGmaxF, "gather: %d fields (1..%d)", fields, kNtGmaxF);
+  DL_CHECK_ARG((fields * emb_dim) % 32 == 0 && fields * emb_dim <= K,
+               "gather: the gathered columns (%d) must be whole 32-deep chunks within K", fields * emb_dim);
+  DL_CHECK_ARG(table_ld >= emb_dim && table_ld % 4 == 0 && (uintptr_t)table % 16 == 0,
+               "gather: the table rows must be 16-B aligned");
+  DL_CHECK_ARG(ids_ld >= fields && n_rows > 0, "gather: bad id matrix / rows");
+  DL_CHECK_ARG((unsigned long long)n_rows * table_ld * 4 < kNtGmasked,
+               "gather: the table spans %lld bytes (past the 32-bit buffer range)", (long long)n_rows * table_ld * 4);
+  if (M == 0 || N == 0) return 0;
+  S3Params p{};
+  p.A = A; p.B = Bp; p.C = C;
+  p.M = M; p.N = N; p.K = K; p.lda = lda; p.ldb = ldb; p.ldc = ldc; p.b_plane = b_plane;
+  p.bits = bits; p.ldbits = ldbits;
+  p.G = table; p.ids = ids; p.id_off = id_offset; p.n_rows = n_rows; p.ids_ld = ids_ld; p.g_ld = table_ld;
+  p.g_fields = fields; p.g_esh = __builtin_ctz(emb_dim); p.g_chunks = fields * emb_dim / 32;
+  p.zero_row0 = zero_row0 ? 1 : 0;
+  p.g_bytes = (unsigned)(n_rows * table_ld * 4);
+  hipStream_t s = as_stream(stream);
+  const bool direct = s3_nt_direct(M, N, ldc, epi, bits, ldbits);
+  const int tiles = (int)(ceil_div(M, kNtBM) * ceil_div(N, kNtBN));
+  const size_t lds = kNtLds + (size_t)fields * kNtGfs * 4;
+  if (direct) {
+    if (epi == S3_STORE) hipLaunchKernelGGL((gemm_s3_nt_kernel<S3_STORE, true, true>), dim3(tiles), dim3(512), lds, s, p);
+    else hipLaunchKernelGGL((gemm_s3_nt_kernel<S3_RELU, true, true>), dim3(tiles), dim3(512), lds, s, p);
+  } else if (epi == S3_STORE) hipLaunchKernelGGL((gemm_s3_nt_kernel<S3_STORE, false, true>), dim3(tiles), dim3(512), lds, s, p);
+  else hipLaunchKernelGGL((gemm_s3_nt_kernel<S3_RELU, false, true>), dim3(tiles), dim3(512), lds, s, p);
+  DL_RETURN_LAUNCH("dl_gemm_s3_nt_gather");
 }
 
 extern "C" int dl_gemm_s3_nt(int32_t M, int32_t N, int32_t K, const float* A, int32_t lda, const uint16_t* Bp,

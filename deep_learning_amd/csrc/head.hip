@@ -163,11 +163,11 @@ __global__ __launch_bounds__(256) void head_kernel(int B, int fm_cols, int H, co
 // reduced: ids two samples ahead, weights one ahead; only the h row load is left on
 // a sample's critical path.  DHB: dh written as bf16 (the bf16 tower's dY operand,
 // no separate cast pass).
-// H4M: float4 chunks of a hidden row per lane (2: H <= 512, 4: H <= 1024).  The next sample's h
-// row is loaded while this one is reduced (a wave walks ~8 samples, each a dependent chain:
+// H4M: float4 chunks of a hidden row per lane (2: H <= 512, 4: H <= 1024).  With DL_WDL_HEAD_PF the
+// next sample's h row is loaded while this one is reduced (a wave walks ~8 samples, each a dependent chain:
 // row -> wave sum -> loss -> gradient stores), as the wide ids (two ahead) and weights (one).
 #ifndef DL_WDL_HEAD_PF
-#define DL_WDL_HEAD_PF 1
+#define DL_WDL_HEAD_PF 0   // 1: prefetch the next sample's h row (measured neutral, C5 head 64 us both: profiles/r06f)
 #endif
 template <bool DHB, int H4M = kHeadMaxH4>
 __global__ __launch_bounds__(256) void wdl_head_kernel(int B, int Fw, int H, const int64_t* __restrict__ wide,

@@ -800,17 +800,37 @@ class CTREngine:
             self._wide_flush()
         self.since_flush = 0
 
-    def plane_lookup(self, B, x0, s):
+    def plane_lookup(self, B, x0, s, deep=True):
         """The lookup over flush(planes=True)'s planes: FM models read the slot plane (row and
-        first-order weight in one 128-B slot, dl_embed_fwd_slots), the others the p plane."""
+        first-order weight in one 128-B slot, dl_embed_fwd_slots), the others the p plane.
+        deep=False: the deep embeddings are not written to x0 (x0_cat_col = -1): the first tower
+        layer reads them from the plane itself (fused_gather_l0)."""
+        L = self._flat_layout(B)
+        if not deep:
+            L.x0_cat_col = -1
         if self.spec.fm:
-            self._c("embed_fwd", "dl_embed_fwd_slots", C_ref(self._flat_layout(B)), ptr(self.p_plane),
+            self._c("embed_fwd", "dl_embed_fwd_slots", C_ref(L), ptr(self.p_plane),
                     ptr(self.in_cate), ptr(self.in_cont), ptr(self.in_vec), ptr(x0), ptr(self.fm_out),
                     ptr(self.fm_sum), ptr(self.err), s)
         else:
-            self._c("embed_fwd", "dl_embed_fwd", C_ref(self._flat_layout(B)), ptr(self.p_plane), None,
+            self._c("embed_fwd", "dl_embed_fwd", C_ref(L), ptr(self.p_plane), None,
                     ptr(self.in_cate), ptr(self.in_cont), ptr(self.in_vec), ptr(x0), ptr(self.fm_out),
                     ptr(self.fm_sum), ptr(self.err), s)
+
+    def fused_gather_l0(self):
+        """Whether predict on current planes fuses the deep lookup into the first tower layer
+        (dl_gemm_s3_nt_gather: the f32 tower's A stream reads each sample's embedding rows from
+        the plane through its ids, x0's deep columns are never written or read — bit-identical
+        to the lookup + GEMM pair, tests/test_gpu_parity.py).  The s3 tower only, the deep
+        columns first in x0 and whole 32-deep chunks, a plane within one 32-bit buffer range;
+        DLAMD_FUSED_GATHER=0 turns it off."""
+        sp = self.spec
+        if os.environ.get("DLAMD_FUSED_GATHER", "1") == "0" or not self.s3 or self.bf or sp.M:
+            return False
+        pl = getattr(self, "p_plane", None)
+        return (pl is not None and self.cat_col == 0 and sp.E in (8, 16, 32, 64) and 0 < sp.S <= 40
+                and (sp.S * sp.E) % 32 == 0 and sp.S * sp.E <= self.in_ld[0]
+                and pl.shape[0] * pl.shape[1] * 4 < 0xFFFFFF00)
 
     def adam_state(self):
         """Table Adam state in the dense layout (tests, checkpoints): dict of m, v (+ m1, v1) as
@@ -890,6 +910,7 @@ class CTREngine:
         L = self.layout
         L.batch = B
         x0 = self.x0b if self.x0_direct else self.x0
+        fused = False   # the deep lookup inside the first tower layer (predict on planes only)
         if sp.M and not self.lazy:  # pooled vectors must be in x0 before the FM second order reads them
             self._c("pool_fwd", "dl_pool_fwd", C_ref(L), ptr(self.table), ptr(self.first) if sp.fm else None,
                  ptr(self.in_cate), sp.S, ptr(self.slot_start), ptr(self.slot_end), sp.M, self.fm_pool_col,
@@ -897,8 +918,10 @@ class CTREngine:
         if (not train and self.lazy and not sp.M and self.since_flush == 0 and type(self) is CTREngine
                 and getattr(self, "planes_step", -1) == self.steps):
             # predict on a flushed table whose planes are current (flush(planes=True) at this
-            # step): the plain lookup of the dense layout (dl_embed_fwd_slots / dl_embed_fwd)
-            self.plane_lookup(B, x0, s)
+            # step): the plain lookup of the dense layout (dl_embed_fwd_slots / dl_embed_fwd),
+            # its deep rows read by the first tower layer itself where it can (fused_gather_l0)
+            fused = self.fused_gather_l0()
+            self.plane_lookup(B, x0, s, deep=not fused)
         elif not train and self.lazy and not sp.M and self.since_flush == 0 and type(self) is CTREngine:
             # predict on a flushed table (every record caught up to the current step): the plain
             # lookup, each reference reading its record's first line (dl_embed_fwd_rec_flat)
@@ -971,9 +994,16 @@ class CTREngine:
             x = self.x0
             for l, hdim in enumerate(sp.hidden):
                 bits = (ptr(self.hbits[l]), self.hbits_ld[l]) if l < len(self.hbits) else (None, 0)
-                self._c("gemm_fwd_l%d" % l, "dl_gemm_s3_nt_bits", B, hdim, self.in_ld[l], ptr(x), self.in_ld[l],
-                        ptr(self.WTp[l]), self.in_ld[l], self.in_ld[l] * self.out_ld[l], ptr(self.h[l]),
-                        self.h_ld[l], 1, None, 0, *bits, s)
+                if l == 0 and fused:
+                    FL = self._flat_layout(B)
+                    self._c("gemm_fwd_l0", "dl_gemm_s3_nt_gather", B, hdim, self.in_ld[0], ptr(x), self.in_ld[0],
+                            ptr(self.p_plane), FL.n_rows, self.p_plane.shape[1], ptr(self.in_cate), FL.cate_ld,
+                            FL.deep_cate_offset, FL.zero_row0, sp.S, sp.E, ptr(self.WTp[0]), self.in_ld[0],
+                            self.in_ld[0] * self.out_ld[0], ptr(self.h[0]), self.h_ld[0], 1, *bits, s)
+                else:
+                    self._c("gemm_fwd_l%d" % l, "dl_gemm_s3_nt_bits", B, hdim, self.in_ld[l], ptr(x), self.in_ld[l],
+                            ptr(self.WTp[l]), self.in_ld[l], self.in_ld[l] * self.out_ld[l], ptr(self.h[l]),
+                            self.h_ld[l], 1, None, 0, *bits, s)
                 x = self.h[l]
         else:
             x = self.x0

@@ -65,7 +65,9 @@ typedef struct dl_emb_layout {
   int32_t x0_ld;            /* floats between samples in x0                          */
   int32_t x0_cont_col;      /* -1: cont not copied into x0                           */
   int32_t x0_vec_col;       /* -1: vector not copied into x0                         */
-  int32_t x0_cat_col;       /* column of the first single-cate embedding in x0       */
+  int32_t x0_cat_col;       /* column of the first single-cate embedding in x0 (-1:
+                               not written — dl_embed_fwd / _slots only, the embeddings
+                               then read by dl_gemm_s3_nt_gather from the table)       */
   int32_t x0_pool_col;      /* column of the first pooled vector in x0 (fm_extra>0)  */
   int32_t fm_ld;            /* floats between samples in fm_out                      */
   int32_t dx0_ld;           /* floats between samples in dx0 (backward)              */
@@ -328,6 +330,23 @@ int dl_gemm_s3_tn(int32_t M, int32_t N, int32_t K, const float* X, int32_t lda, 
 int dl_gemm_s3_nt_bits(int32_t M, int32_t N, int32_t K, const float* A, int32_t lda, const uint16_t* B,
                        int32_t ldb, int64_t b_plane, float* C, int32_t ldc, int32_t epi, const float* mask,
                        int32_t ldm, uint16_t* bits, int32_t ldbits, void* stream);
+/* dl_gemm_s3_nt_gather: dl_gemm_s3_nt_bits (epi 0 / 1) for the first tower layer of the
+ * flushed-table forward with the embedding lookup fused into its A stream (the north star's
+ * "gather into tiles feeding MFMA"; replaces the GatherV2 -> ConcatV2 -> MatMul chain of
+ * deepfm_pipeline.py:117-153 / dnn_pipeline.py:72-96 at predict): columns [0, fields * emb_dim)
+ * of A's row m are not read from A but from table row (ids[m * ids_ld + f] + id_offset) —
+ * f = k / emb_dim, column k % emb_dim, table rows table_ld floats apart (the slot or p plane
+ * of dl_rec_flush) — a row outside [0, n_rows), or row 0 with zero_row0, reads as zeros (the
+ * lookup's zero row; the lookup itself reports invalid ids).  The remaining columns come from A
+ * (the cont / vector / bias columns the lookup writes with x0_cat_col = -1).  Bit-identical
+ * to dl_embed_fwd(_slots) writing those columns followed by dl_gemm_s3_nt_bits.  Requires
+ * emb_dim in {8, 16, 32, 64}, fields * emb_dim a multiple of 32 and <= K, fields <= 40,
+ * n_rows * table_ld * 4 < 0xFFFFFF00 bytes (one buffer range). */
+int dl_gemm_s3_nt_gather(int32_t M, int32_t N, int32_t K, const float* A, int32_t lda, const float* table,
+                         int64_t n_rows, int32_t table_ld, const int64_t* ids, int32_t ids_ld, int64_t id_offset,
+                         int32_t zero_row0, int32_t fields, int32_t emb_dim, const uint16_t* B, int32_t ldb,
+                         int64_t b_plane, float* C, int32_t ldc, int32_t epi, uint16_t* bits, int32_t ldbits,
+                         void* stream);
 
 /* ------------------------------------------------------------------------
  * Output layer + sigmoid + eps-log-loss, forward and backward fused

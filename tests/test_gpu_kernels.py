@@ -255,6 +255,71 @@ def test_gemm_s3_relu_bitmask_round_trip(hip_lib, M, N, K, aligned):
     assert torch.equal(c2, c3)
 
 
+@pytest.mark.parametrize("aligned", [False, True])
+@pytest.mark.parametrize("M,N,K,F,E,tld", [(65536, 400, 432, 26, 16, 32), (300, 400, 432, 26, 16, 16),
+                                           (257, 213, 72, 8, 8, 8), (77, 48, 96, 3, 32, 32),
+                                           (513, 16, 64, 1, 64, 64), (40, 400, 416, 26, 16, 32)])
+def test_gemm_s3_nt_gather_equals_lookup_then_gemm(hip_lib, M, N, K, F, E, tld, aligned):
+    """dl_gemm_s3_nt_gather (the deep lookup inside the first tower layer's A stream) against
+    the same GEMM over an x0 whose first F * E columns hold the looked-up rows: output and ReLU
+    bitmask bit-identical.  Ids include the zero row (zero_row0), ids past the table and
+    negative ids after the offset (all read as zeros), the slot plane's stride (tld = 2E) and a
+    batch that is not a multiple of the 256-row block."""
+    g = torch.Generator().manual_seed(M + N + K + F)
+    n_rows, off = 5000, 3
+    table = torch.randn(n_rows, tld, generator=g)
+    ids = torch.randint(0, n_rows - off, (M, F + 2), generator=g, dtype=torch.int64)
+    ids[::7, 0] = -off                      # row 0 (zero_row0)
+    ids[5::11, F - 1] = n_rows              # past the table
+    ids[3::13, F // 2] = -off - 1           # negative row
+    rows = ids[:, :F] + off
+    valid = (rows > 0) & (rows < n_rows)
+    look = table[rows.clamp(0, n_rows - 1)][:, :, :E] * valid[:, :, None]
+    A = torch.randn(M, K + 4, generator=g)
+    A_ref = A.clone()
+    A_ref[:, :F * E] = look.reshape(M, F * E)
+    A[:, :F * E] = float("nan")             # never read by the gather
+    Bm = (torch.randn(N, K, generator=g) * 0.05).cuda()
+    Bp = _planes(Bm, False)
+    ldc, ldb16 = (N + 4, 32) if aligned else (N + 3, (N + 15) // 16 + 2)
+    Ad, Ar, Td, Id = A.cuda(), A_ref.cuda(), table.cuda(), ids.cuda()
+    h_ref = torch.full((M, ldc), 7.0, device="cuda")
+    h = torch.full((M, ldc), 7.0, device="cuda")
+    b_ref = torch.full((M, ldb16), -1, dtype=torch.int16, device="cuda")
+    b = torch.full((M, ldb16), -1, dtype=torch.int16, device="cuda")
+    call("dl_gemm_s3_nt_bits", M, N, K, ptr(Ar), K + 4, ptr(Bp), K, N * K, ptr(h_ref), ldc, 1, None, 0,
+         ptr(b_ref), ldb16, _s())
+    call("dl_gemm_s3_nt_gather", M, N, K, ptr(Ad), K + 4, ptr(Td), n_rows, tld, ptr(Id), F + 2, off, 1, F, E,
+         ptr(Bp), K, N * K, ptr(h), ldc, 1, ptr(b), ldb16, _s())
+    torch.cuda.synchronize()
+    assert torch.equal(h, h_ref)
+    assert torch.equal(b, b_ref)
+    # the store epilogue, no bitmask
+    c_ref = torch.full((M, ldc), 5.0, device="cuda")
+    c = torch.full((M, ldc), 5.0, device="cuda")
+    call("dl_gemm_s3_nt", M, N, K, ptr(Ar), K + 4, ptr(Bp), K, N * K, ptr(c_ref), ldc, 0, None, 0, _s())
+    call("dl_gemm_s3_nt_gather", M, N, K, ptr(Ad), K + 4, ptr(Td), n_rows, tld, ptr(Id), F + 2, off, 1, F, E,
+         ptr(Bp), K, N * K, ptr(c), ldc, 0, None, 0, _s())
+    torch.cuda.synchronize()
+    assert torch.equal(c, c_ref)
+
+
+def test_gemm_s3_nt_gather_argument_checks(hip_lib):
+    """The gather's preconditions fail loudly: a partial 32-deep chunk, too many fields, an
+    emb_dim outside {8..64}, the mask epilogue, a table past one 32-bit buffer range."""
+    A = torch.zeros(64, 440, device="cuda")
+    Bp = _planes(torch.zeros(16, 432, device="cuda"), False)
+    T = torch.zeros(100, 16, device="cuda")
+    I = torch.zeros(64, 30, dtype=torch.int64, device="cuda")
+    C_ = torch.zeros(64, 16, device="cuda")
+    base = lambda F, E, epi=1, n_rows=100: (64, 16, 432, ptr(A), 440, ptr(T), n_rows, 16, ptr(I), 30, 0, 1, F, E,
+                                            ptr(Bp), 432, 16 * 432, ptr(C_), 16, epi, None, 0, _s())
+    for args, msg in [(base(3, 16), "32-deep"), (base(41, 8), "fields"), (base(8, 4), "emb_dim"),
+                      (base(2, 16, epi=2), "epilogue"), (base(2, 16, n_rows=1 << 26), "buffer range")]:
+        with pytest.raises(_lib.DLError, match=msg):
+            call("dl_gemm_s3_nt_gather", *args)
+
+
 @pytest.mark.parametrize("M,N,K,splits", [(432, 400, 65536, 64), (416, 400, 8192, 8), (428, 396, 5000, 3),
                                             (64, 16, 100, 1), (16, 416, 4096, 16), (400, 400, 8192, 8),
                                             (404, 400, 2048, 2), (144, 400, 1024, 1)])

@@ -343,6 +343,43 @@ def test_flat_lookup_after_flush_bit_identical(hip_lib, name):
         e.predict(bs[5])
 
 
+@pytest.mark.parametrize("name,kw", [
+    ("deepfm_pipeline", dict(CASES["deepfm_pipeline"], cate_index_size=50000)),
+    ("dnn_pipeline", dict(C=13, V=3, S=24, E=8, cate_index_size=10000, hidden=[64, 32])),
+    ("deepfm_pipeline", dict(C=13, V=0, S=6, E=16, cate_index_size=7000, hidden=[48, 32]))])
+def test_fused_gather_predict_bit_identical(hip_lib, name, kw, monkeypatch):
+    """predict() on current planes with the deep lookup inside the first tower layer
+    (dl_gemm_s3_nt_gather, the default) against the lookup writing x0 followed by the plain
+    GEMM (DLAMD_FUSED_GATHER=0): logits, FM outputs and the first layer's activations
+    bit-identical, over a batch that is not a multiple of the 256-row block with padding ids
+    (the zero row) in every field; and the engine really took the fused path."""
+    spec = ModelSpec(name, **kw)
+    e = CTREngine(spec, max_batch=300, seed=3, adam="lazy", hist_len=8)
+    bs = _batches(name, kw, 300, 5, seed=29)
+    for i, bt in enumerate(bs[:4]):
+        e.train_step(bt, graph=i >= 2)
+    b = dict(bs[4])
+    cate = np.array(b["cate_feats"], copy=True)
+    cate[::9, :] = 0                         # padding ids: the zero row
+    b["cate_feats"] = cate
+    e.flush(planes=True)
+    assert e.fused_gather_l0()
+    calls = []
+    orig = e._c
+    monkeypatch.setattr(e, "_c", lambda tag, fn, *a: (calls.append(fn), orig(tag, fn, *a))[1])
+    got = e.predict(b, logits=True)
+    got_fm = e.fm_out[:300].cpu().numpy().copy()
+    got_h = e.h[0][:300].cpu().numpy().copy()
+    assert "dl_gemm_s3_nt_gather" in calls
+    monkeypatch.setenv("DLAMD_FUSED_GATHER", "0")
+    calls.clear()
+    ref = e.predict(b, logits=True)
+    assert "dl_gemm_s3_nt_gather" not in calls
+    np.testing.assert_array_equal(got, ref)
+    np.testing.assert_array_equal(got_fm, e.fm_out[:300].cpu().numpy())
+    np.testing.assert_array_equal(got_h, e.h[0][:300].cpu().numpy())
+
+
 def test_lazy_multi_hot_tracks_oracle(hip_lib):
     """Multi-hot pooling on row records (deepfm_multi_cate): pooled rows come from the
     caught-up records through the batch index, their gradients join each row's ordered
