@@ -59,6 +59,9 @@ constexpr int kMaxHotContFwd = 32;
 constexpr int kTileSamples = 16;   // samples staged per block iteration
 constexpr int kMaxSlots = 128;     // FM slots + deep slots per sample
 
+#ifndef DL_FWD_SPW
+#define DL_FWD_SPW 1   // samples a wave keeps in flight in the plain / slot lookups (see the kernel)
+#endif
 #ifndef DL_FWD_MIN_WAVES
 #define DL_FWD_MIN_WAVES 5
 #endif
@@ -74,8 +77,9 @@ constexpr int kMaxSlots = 128;     // FM slots + deep slots per sample
 // already caught up (a flushed table: predict after dl_rec_flush) — only each record's first
 // 128-B line is read (p and the first-order triple + stamp), a stale row faults (DL_STATUS_LAG).
 template <int E, int NPS, int REC = 0>
-// (two samples in flight a wave, SPW below: 4 waves a SIMD, up to 128 VGPRs)
-__global__ __launch_bounds__(256, (REC == 1 || NPS > 5) ? 1 : ((REC == 0 || REC == 3) && NPS <= 3) ? 4 : DL_FWD_MIN_WAVES)
+// (two samples in flight a wave, DL_FWD_SPW below: 4 waves a SIMD, up to 128 VGPRs)
+__global__ __launch_bounds__(256, (REC == 1 || NPS > 5) ? 1
+                                  : (DL_FWD_SPW > 1 && (REC == 0 || REC == 3) && NPS <= 3) ? 4 : DL_FWD_MIN_WAVES)
 void embed_fwd_kernel(EmbArgs a) {
   // Per block iteration a tile of 16 samples is staged: every (sample, slot)
   // row index is resolved once into LDS by a coalesced pass over the id matrix
@@ -169,10 +173,10 @@ void embed_fwd_kernel(EmbArgs a) {
     for (int k = threadIdx.x; k < nb * Cf; k += blockDim.x)
       vals_s[k / Cf][k % Cf] = a.cont[(int64_t)(b0 + k / Cf) * L.cont_fields + k % Cf];
     __syncthreads();
-    // SPW samples per wave iteration, all their row loads issued before any is consumed (the
-    // plain / slot-plane lookups with few passes a sample — e.g. the FM-only lookup of the fused
-    // predict — are latency-bound with one sample's rows in flight); the record modes keep one
-    constexpr int SPW = (REC == 0 || REC == 3) && NPS <= 3 ? 2 : 1;
+    // SPW samples per wave iteration, all their row loads issued before any is consumed
+    // (DL_FWD_SPW = 2: the plain / slot-plane lookups with at most 3 passes a sample; measured
+    // neutral on the FM-only lookup of the fused predict, 60 us both, profiles/r06i): one
+    constexpr int SPW = DL_FWD_SPW > 1 && (REC == 0 || REC == 3) && NPS <= 3 ? DL_FWD_SPW : 1;
     for (int jw = wid; jw < nb; jw += 4 * SPW) {
       float4 v[SPW][NPS];
       int rw[SPW][NPS];

@@ -342,7 +342,7 @@ __global__ __launch_bounds__(512) void gemm_s3_nt_kernel(S3Params p) {
     // (coalesced over the id matrix), published by a barrier before any A piece is fetched
     dma_b(0, 0);
     dma_b(1, 1);
-    // (eight ids a thread in flight at once: one memory round trip per 4,096 entries)
+    // (eight ids a thread in flight at once: one memory round trip per 4,096 entries; sixteen spill)
     const int tot = BM * p.g_fields;
     constexpr int kGU = 8;
     for (int b = 0; b < tot; b += kGU * NW * 64) {

@@ -1,16 +1,16 @@
 #!/bin/bash
 # The north-star lookup alone, uniform and Zipf ids: time, rocprofv3 stats, FETCH / WRITE / L2
 # hit passes (one counter set a run), then the random 64-B gather microbenchmark on the same
-# box as the access-pattern ceiling: bash scripts/gpu_lookup_pmc.sh TAG
-cd "$GRAFT_REPO_ROOT"; export TMPDIR=/tmp; OUT=gpurun_out/${1:-lk}; mkdir -p $OUT
+# box as the access-pattern ceiling: bash scripts/gpu_lookup_pmc.sh TAG [full|fm]
+cd "$GRAFT_REPO_ROOT"; export TMPDIR=/tmp; OUT=gpurun_out/${1:-lk}; MODE=${2:-full}; mkdir -p $OUT
 for d in uniform zipf; do
-  timeout -k 10 200 python scripts/lookup_bench.py $d 20 > $OUT/lookup_$d.txt 2>&1 || { tail -5 $OUT/lookup_$d.txt; exit 1; }
+  timeout -k 10 200 python scripts/lookup_bench.py $d 20 $MODE > $OUT/lookup_$d.txt 2>&1 || { tail -5 $OUT/lookup_$d.txt; exit 1; }
   grep lookup $OUT/lookup_$d.txt
-  timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/st_$d -o t -- python scripts/lookup_bench.py $d 20 > /dev/null 2>&1 || { echo "stats $d failed"; exit 1; }
+  timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/st_$d -o t -- python scripts/lookup_bench.py $d 20 $MODE > /dev/null 2>&1 || { echo "stats $d failed"; exit 1; }
   i=0
   for ctr in "FETCH_SIZE" "WRITE_SIZE TCC_HIT_sum TCC_MISS_sum" "TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_32B_sum TCC_EA0_WRREQ_sum TCC_EA0_WRREQ_64B_sum"; do
     i=$((i+1))
-    timeout -s KILL 120 rocprofv3 --pmc $ctr --output-format csv -d $OUT/pmc_${d}_$i -o p -- python scripts/lookup_bench.py $d 5 > /dev/null 2>&1 || { echo "pmc $d pass $i failed"; exit 1; }
+    timeout -s KILL 120 rocprofv3 --pmc $ctr --output-format csv -d $OUT/pmc_${d}_$i -o p -- python scripts/lookup_bench.py $d 5 $MODE > /dev/null 2>&1 || { echo "pmc $d pass $i failed"; exit 1; }
   done
 done
 python - <<PY

@@ -1,7 +1,9 @@
 """The north-star lookup alone (C2 shape, B = 65,536, 26 M rows): dl_embed_fwd over the dense
 p / first-order planes of a flushed table, the kernel CTREngine.predict runs — nothing else
 launches embed_fwd_kernel here (no training step), so rocprofv3 PMC passes over this script
-count the lookup alone.  python scripts/lookup_bench.py [uniform|zipf] [reps]"""
+count the lookup alone.  python scripts/lookup_bench.py [uniform|zipf] [reps] [full|fm]
+(fm: the FM-only lookup of the fused predict, x0_cat_col = -1 — the deep rows are then read by
+dl_gemm_s3_nt_gather, not here)"""
 import os
 import sys
 
@@ -15,6 +17,7 @@ from deep_learning_amd.synthetic import make_batch  # noqa: E402
 
 dist = sys.argv[1] if len(sys.argv) > 1 else "uniform"
 reps = int(sys.argv[2]) if len(sys.argv) > 2 else 20
+mode = sys.argv[3] if len(sys.argv) > 3 else "full"
 B, N = 65536, 26_000_000
 spec = sp = ModelSpec("deepfm_pipeline", C=13, V=0, S=26, E=16, cate_index_size=N, hidden=[400, 400, 400])
 eng = CTREngine(spec, max_batch=B, seed=2019, adam="lazy")
@@ -22,6 +25,8 @@ eng.flush(planes=True)
 b = {k: torch.from_numpy(v).cuda() for k, v in make_batch(B, cate_index_size=N, seed=4242, dist=dist).items()}
 eng.stage(b)
 FL = eng._flat_layout(B)
+if mode == "fm":
+    FL.x0_cat_col = -1
 s = _lib.stream_handle()
 x0 = eng.x0b if eng.x0_direct else eng.x0
 
@@ -45,4 +50,4 @@ e1.record()
 torch.cuda.synchronize()
 eng.check_error()
 us = e0.elapsed_time(e1) * 1e3 / reps
-print("lookup %s %.1f us  %.3f of 8 TB/s by the 3,640-B rule" % (dist, us, B * 3640 / us / 1e3 / 8000), flush=True)
+print("lookup %s %s %.1f us  %.3f of 8 TB/s by the 3,640-B rule" % (mode, dist, us, B * 3640 / us / 1e3 / 8000), flush=True)
