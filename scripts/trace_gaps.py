@@ -17,7 +17,7 @@ ks.sort()
 dur, gap, cnt = defaultdict(float), defaultdict(float), defaultdict(int)
 steps = [i for i, k in enumerate(ks) if first in k[2]]
 if len(steps) > 3:
-    ks = ks[steps[-4]:]          # the last three whole steps
+    ks = ks[steps[-4]:steps[-1]]          # the last three whole steps
 prev_end = None
 for s, e, n in ks:
     name = n.split("(")[0].split("<")[0].split("::")[-1][:40]
