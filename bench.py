@@ -462,9 +462,10 @@ def lookup_alone(eng, batch, B, per_sample, reps=20):
     return {"kernels": ["embed_fwd (slot plane)"], "us": us, "GB/s": gb, "frac": fr, "fused": fused,
             "records": {"kernels": ["rec_gather (13 cont rows)", "embed_fwd_rec_flat"], "us": rus, "GB/s": rgb,
                         "frac": rfr},
-            "note": "flushed table: the lookup without lazy Adam's catch-up, as predict runs it (the flush writes "
-                    "a slot plane, each row's p and first-order weight in one 128-B slot; 'records' reads each "
-                    "record's first line instead); the "
+            "note": "flushed table: the lookup without lazy Adam's catch-up, as predict runs it with "
+                    "DLAMD_FUSED_GATHER=0 (the flush writes a slot plane, each row's p and first-order weight in one "
+                    "128-B slot; 'records' reads each record's first line instead; 'fused': predict's default on "
+                    "current planes, the deep rows read by the first tower layer itself); the "
                     "training step's gather above also replays each row's pending zero-gradient Adam steps and "
                     "stashes its moments"}
 
