@@ -16,23 +16,27 @@ done
 python - <<PY
 import csv, glob, json
 out = {}
+KEEP = ("embed_fwd", "gemm_s3_nt")
+def short(n):
+    return n.split("(")[0].replace("void ", "").replace("dl::", "")[:60]
 for d in ("uniform", "zipf"):
     r = {}
     f = glob.glob("$OUT/st_%s/**/t_kernel_stats.csv" % d, recursive=True)[0]
     for row in csv.DictReader(open(f)):
-        if "embed_fwd" in row["Name"]:
-            r["kernel"] = row["Name"][:60]; r["avg_us"] = float(row["AverageNs"]) / 1e3; r["calls"] = int(row["Calls"])
+        if any(k in row["Name"] for k in KEEP):
+            r.setdefault(short(row["Name"]), {}).update(avg_us=float(row["AverageNs"]) / 1e3, calls=int(row["Calls"]))
     ctr = {}
     for f in glob.glob("$OUT/pmc_%s_*/**/p_counter_collection.csv" % d, recursive=True):
         for row in csv.DictReader(open(f)):
-            if "embed_fwd" not in row["Kernel_Name"]:
+            if not any(k in row["Kernel_Name"] for k in KEEP):
                 continue
-            key = (row["Counter_Name"], f, row["Dispatch_Id"])
+            key = (short(row["Kernel_Name"]), row["Counter_Name"], f, row["Dispatch_Id"])
             ctr[key] = ctr.get(key, 0.0) + float(row["Counter_Value"])   # summed over instances
     per = {}
-    for (name, _, _), v in ctr.items():
-        per.setdefault(name, []).append(v)
-    r["counters_per_launch"] = {k: sum(v) / len(v) for k, v in per.items()}
+    for (kn, name, _, _), v in ctr.items():
+        per.setdefault(kn, {}).setdefault(name, []).append(v)
+    for kn, cs in per.items():
+        r.setdefault(kn, {})["counters_per_launch"] = {k: sum(v) / len(v) for k, v in cs.items()}
     out[d] = r
 json.dump(out, open("$OUT/lookup_pmc.json", "w"), indent=1)
 print(json.dumps(out, indent=1))

@@ -1,9 +1,10 @@
 """The north-star lookup alone (C2 shape, B = 65,536, 26 M rows): dl_embed_fwd over the dense
 p / first-order planes of a flushed table, the kernel CTREngine.predict runs — nothing else
 launches embed_fwd_kernel here (no training step), so rocprofv3 PMC passes over this script
-count the lookup alone.  python scripts/lookup_bench.py [uniform|zipf] [reps] [full|fm]
+count the lookup alone.  python scripts/lookup_bench.py [uniform|zipf] [reps] [full|fm|fused|pair]
 (fm: the FM-only lookup of the fused predict, x0_cat_col = -1 — the deep rows are then read by
-dl_gemm_s3_nt_gather, not here)"""
+dl_gemm_s3_nt_gather, not here; fused: that lookup + the gathering first tower layer, predict's
+default front; pair: the full lookup + the plain first layer, the unfused front)"""
 import os
 import sys
 
@@ -25,8 +26,22 @@ eng.flush(planes=True)
 b = {k: torch.from_numpy(v).cuda() for k, v in make_batch(B, cate_index_size=N, seed=4242, dist=dist).items()}
 eng.stage(b)
 FL = eng._flat_layout(B)
-if mode == "fm":
-    FL.x0_cat_col = -1
+FN = eng._flat_layout(B)
+FN.x0_cat_col = -1
+if mode in ("fm", "fused"):
+    FL = FN
+hd, ld0, ol0 = sp.hidden[0], eng.in_ld[0], eng.out_ld[0]
+bits = (ptr(eng.hbits[0]), eng.hbits_ld[0]) if eng.hbits else (None, 0)
+
+
+def layer0():
+    if mode == "fused":
+        call("dl_gemm_s3_nt_gather", B, hd, ld0, ptr(x0), ld0, ptr(eng.p_plane), FN.n_rows, eng.p_plane.shape[1],
+             ptr(eng.in_cate), FN.cate_ld, FN.deep_cate_offset, FN.zero_row0, sp.S, sp.E, ptr(eng.WTp[0]), ld0,
+             ld0 * ol0, ptr(eng.h[0]), eng.h_ld[0], 1, *bits, s)
+    elif mode == "pair":
+        call("dl_gemm_s3_nt_bits", B, hd, ld0, ptr(x0), ld0, ptr(eng.WTp[0]), ld0, ld0 * ol0, ptr(eng.h[0]),
+             eng.h_ld[0], 1, None, 0, *bits, s)
 s = _lib.stream_handle()
 x0 = eng.x0b if eng.x0_direct else eng.x0
 
@@ -38,6 +53,7 @@ def run():
     else:
         call("dl_embed_fwd", C_ref(FL), ptr(eng.p_plane), None, ptr(eng.in_cate), ptr(eng.in_cont),
              ptr(eng.in_vec), ptr(x0), ptr(eng.fm_out), ptr(eng.fm_sum), ptr(eng.err), s)
+    layer0()
 
 
 run()
