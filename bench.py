@@ -975,6 +975,13 @@ def main():
             "extra_workloads": extra or None,
         }
         os.write(json_fd, (json.dumps(out) + "\n").encode())
+        # the headline's own summary once more, last on stderr (the extra workloads, the CPU
+        # baseline and the C1 leg log after the headline's per-kernel line: a 4-KB tail drops it)
+        k = r["kernels"]
+        log("headline %s: %.4f ms/step, %.4g %s; per-kernel us/launch: %s" % (
+            out["config"]["workload"].split(":")[0], r["ms"], out["value"], out["unit"], ", ".join(
+                "%s %.0f%s" % (n, v["us"], "x%d" % v["launches"] if v["launches"] > 1 else "")
+                for n, v in sorted(k.items(), key=lambda kv: -kv[1]["us"] * kv[1]["launches"]))))
     if sharded:
         dist.destroy_process_group()
 
