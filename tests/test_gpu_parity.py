@@ -380,6 +380,46 @@ def test_fused_gather_predict_bit_identical(hip_lib, name, kw, monkeypatch):
     np.testing.assert_array_equal(got_h, e.h[0][:300].cpu().numpy())
 
 
+@pytest.mark.parametrize("name", ["deepfm_pipeline", "dnn_pipeline"])
+def test_lookup_without_deep_columns(hip_lib, name):
+    """The FM-only form of the plane lookup (x0_cat_col = -1, what the fused predict runs):
+    FM outputs and sums bit-identical to the full lookup's, x0's cont / vector columns the same,
+    its deep columns never written (a sentinel survives), and a bad id still reported."""
+    kw = dict(CASES[name], cate_index_size=30000)
+    e = CTREngine(ModelSpec(_model(name), **kw), max_batch=200, seed=5, adam="lazy", hist_len=8)
+    bs = _batches(name, kw, 200, 3, seed=41)
+    for bt in bs[:2]:
+        e.train_step(bt)
+    e.flush(planes=True)
+    B = 200
+    e.stage(bs[2])
+    s = _lib.stream_handle()
+    D = e.spec.S * e.spec.E
+    e.x0.fill_(7.0)
+    e.plane_lookup(B, e.x0, s, deep=True)
+    full_x0 = e.x0[:B].clone()
+    full_fm = (e.fm_out[:B].clone(), e.fm_sum[:B].clone()) if e.spec.fm else None
+    e.x0.fill_(7.0)
+    e.fm_out.fill_(3.0)
+    e.plane_lookup(B, e.x0, s, deep=False)
+    torch.cuda.synchronize()
+    e.check_error()
+    assert (e.x0[:B, e.cat_col:e.cat_col + D] == 7.0).all()
+    assert torch.equal(e.x0[:B, D:], full_x0[:, D:])
+    if full_fm is not None:
+        nf = e.spec.fm_cols   # the pad columns past fm_cols are not outputs
+        assert torch.equal(e.fm_out[:B, :nf], full_fm[0][:, :nf])
+        assert torch.equal(e.fm_sum[:B], full_fm[1])
+    bad = dict(bs[2])
+    cate = np.array(bad["cate_feats"], copy=True)
+    cate[3, 2] = kw["cate_index_size"] * 10          # outside the table
+    bad["cate_feats"] = cate
+    e.stage(bad)
+    e.plane_lookup(B, e.x0, s, deep=False)
+    with pytest.raises(_lib.DLError):
+        e.check_error()
+
+
 def test_lazy_multi_hot_tracks_oracle(hip_lib):
     """Multi-hot pooling on row records (deepfm_multi_cate): pooled rows come from the
     caught-up records through the batch index, their gradients join each row's ordered
