@@ -108,6 +108,8 @@ SIGNATURES = {
     "dl_gemm_s3_nt_bits": (I32, [I32, I32, I32, P, I32, P, I32, I64, P, I32, I32, P, I32, P, I32, P]),
     "dl_gemm_s3_nt_gather": (I32, [I32, I32, I32, P, I32, P, I64, I32, P, I32, I64, I32, I32, I32, P, I32, I64, P,
                                    I32, I32, P, I32, P]),
+    "dl_gemm_s3_nt_gather_rows": (I32, [I32, I32, I32, P, I32, P, I64, I32, P, I32, I32, I32, I32, P, I32, I64, P,
+                                        I32, I32, P, I32, P]),
     "dl_gemm_s3_tn": (I32, [I32, I32, I32, P, I32, P, I32, P, I32, I32, I64, P]),
     "dl_head_fwd_bwd": (I32, [I32, I32, I32, P, I32, P, I32, P, P, F, F, P, P, P, P, P, I32, P]),
     "dl_head_grid": (I32, [I32]),

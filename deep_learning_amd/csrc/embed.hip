@@ -955,8 +955,9 @@ __global__ __launch_bounds__(256) void pool_bwd_kernel(PoolBwdArgs a) {
   }
 }
 
-// no_cat_ok: x0_cat_col == -1 accepted (the plain table lookups only: the single-cate
-// embeddings are then not written, dl_gemm_s3_nt_gather reads them from the table itself)
+// no_cat_ok: x0_cat_col == -1 accepted (the plain table and the indexed lookups: the single-cate
+// embeddings are then not written, dl_gemm_s3_nt_gather reads them from the table or the
+// compact rows itself)
 static int check_layout(const dl_emb_layout* L, bool no_cat_ok = false) {
   DL_CHECK_ARG(L != nullptr, "layout is NULL");
   const int E = L->emb_dim;
@@ -1010,7 +1011,7 @@ extern "C" int dl_embed_fwd_slots(const dl_emb_layout* L, const float* slots, co
 extern "C" int dl_embed_fwd_indexed(const dl_emb_layout* L, const float* rows, const float* rows_first,
                                     const int32_t* inv, int32_t inv_base, const float* cont, const float* vector,
                                     float* x0, float* fm_out, float* fm_sum, void* stream) {
-  if (int rc = check_layout(L)) return rc;
+  if (int rc = check_layout(L, true)) return rc;
   DL_CHECK_ARG(rows && inv && x0, "NULL rows/inv/x0");
   DL_CHECK_ARG(!L->use_fm || (rows_first && fm_out && fm_sum), "FM outputs required");
   if (L->batch == 0) return 0;

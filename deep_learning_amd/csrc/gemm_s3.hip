@@ -111,6 +111,8 @@ struct S3Params {
   // straight from the table G (g_ld floats a row; a masked or invalid row reads as zeros)
   const float* G;
   const int64_t* ids;
+  const int32_t* ids32;      // (training form) int32 row indices instead of ids: < 0 = the zero row
+  float* a_store;            // (training form) the gathered columns also written here (x0, ld lda)
   long long id_off, n_rows;
   int ids_ld, g_ld, g_fields, g_esh, g_chunks, zero_row0;
   unsigned g_bytes;          // G's buffer range (bytes, < 0xFFFFFF00: the masked rows' offset)
@@ -213,7 +215,11 @@ __device__ __forceinline__ void nt_rd3(uint32_t a, shortx8& h, shortx8& m, short
 // first 32 g_chunks columns of A are fetched row by row from the table through the ids (an 8-float
 // piece never straddles two rows: E % 8 == 0), the rest from A as usual.  The values are the
 // ones the lookup would have written to A (a copy), so C is bit-identical to the unfused pair.
-template <int EPI, bool DIRECT = false, bool GATHER = false>
+// STORE_A (with GATHER: the training form): the column-tile-0 blocks also write the gathered A
+// pieces into p.a_store (x0) as they split them, for the weight gradient that streams x0 later —
+// four 16-B stores a lane and step, past the range (dropped) where there is nothing to write,
+// so every wave's vector-memory queue keeps one straight-line count.
+template <int EPI, bool DIRECT = false, bool GATHER = false, bool STORE_A = false>
 __global__ __launch_bounds__(512) void gemm_s3_nt_kernel(S3Params p) {
   extern __shared__ __attribute__((aligned(16))) unsigned short lds[];   // [3 bufs][3 planes][BN][32]
   constexpr int NW = 8, BM = kNtBM, DMAW = kNtDmaW;
@@ -276,23 +282,34 @@ __global__ __launch_bounds__(512) void gemm_s3_nt_kernel(S3Params p) {
   auto load_a = [&](int c, float4 (&ra)[4]) {
     if constexpr (GATHER) {
       if (c < p.g_chunks) {   // uniform: the chunk lies in the gathered columns
-        // this lane's two pieces of a row: k and k + 4 (natural order), or k = 32c + 4kq and
-        // k + 16 (DL_S3_KPERM: a wave instruction then reads whole 64-B rows, 16 B a lane)
-        const int ka = DL_S3_KPERM ? 32 * c + 4 * kq : 32 * c + 8 * kq;
-        const int kb = DL_S3_KPERM ? ka + 16 : ka + 4;
         const uint32_t em = (1u << p.g_esh) - 1u;
-        const int fa = ka >> p.g_esh, fb = kb >> p.g_esh;
-        const uint32_t ca = 4u * ((uint32_t)ka & em), cb = 4u * ((uint32_t)kb & em);
         const int r0l = wid * 32 + cl;
-        const uint32_t ta0 = gtab[fa * kNtGfs + r0l], ta1 = gtab[fa * kNtGfs + r0l + 16];
-        const uint32_t tb0 = fb == fa ? ta0 : gtab[fb * kNtGfs + r0l];
-        const uint32_t tb1 = fb == fa ? ta1 : gtab[fb * kNtGfs + r0l + 16];
-        const uint32_t a0 = ok0 ? ta0 + ca : kNtGmasked, b0 = ok0 ? tb0 + cb : kNtGmasked;
-        const uint32_t a1 = ok1 ? ta1 + ca : kNtGmasked, b1 = ok1 ? tb1 + cb : kNtGmasked;
-        ra[0] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(g_rsrc, (int)a0, 0, 0));
-        ra[1] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(g_rsrc, (int)b0, 0, 0));
-        ra[2] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(g_rsrc, (int)a1, 0, 0));
-        ra[3] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(g_rsrc, (int)b1, 0, 0));
+        if (DL_S3_KPERM) {
+          // the k-permuted planes: this lane's pieces at k = 32c + 4kq and k + 16 (a wave
+          // instruction then reads whole 64-B rows, 16 B a lane): two fields a row for E < 32
+          const int ka = 32 * c + 4 * kq, kb = ka + 16;
+          const int fa = ka >> p.g_esh, fb = kb >> p.g_esh;
+          const uint32_t ca = 4u * ((uint32_t)ka & em), cb = 4u * ((uint32_t)kb & em);
+          const uint32_t ta0 = gtab[fa * kNtGfs + r0l], ta1 = gtab[fa * kNtGfs + r0l + 16];
+          const uint32_t tb0 = gtab[fb * kNtGfs + r0l], tb1 = gtab[fb * kNtGfs + r0l + 16];
+          const uint32_t a0 = ok0 ? ta0 + ca : kNtGmasked, b0 = ok0 ? tb0 + cb : kNtGmasked;
+          const uint32_t a1 = ok1 ? ta1 + ca : kNtGmasked, b1 = ok1 ? tb1 + cb : kNtGmasked;
+          ra[0] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(g_rsrc, (int)a0, 0, 0));
+          ra[1] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(g_rsrc, (int)b0, 0, 0));
+          ra[2] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(g_rsrc, (int)a1, 0, 0));
+          ra[3] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(g_rsrc, (int)b1, 0, 0));
+        } else {
+          // natural order: this lane's 8 floats k = 32c + 8kq .. + 7 of each row lie in one field
+          const int k = 32 * c + 8 * kq;
+          const int f = k >> p.g_esh;
+          const uint32_t col = 4u * ((uint32_t)k & em);
+          const uint32_t t0 = gtab[f * kNtGfs + r0l], t1 = gtab[f * kNtGfs + r0l + 16];
+          const uint32_t o0 = ok0 ? t0 + col : kNtGmasked, o1 = ok1 ? t1 + col : kNtGmasked;
+          ra[0] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(g_rsrc, (int)o0, 0, 0));
+          ra[1] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(g_rsrc, (int)(o0 + 16u), 0, 0));
+          ra[2] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(g_rsrc, (int)o1, 0, 0));
+          ra[3] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(g_rsrc, (int)(o1 + 16u), 0, 0));
+        }
         return;
       }
     }
@@ -351,7 +368,13 @@ __global__ __launch_bounds__(512) void gemm_s3_nt_kernel(S3Params p) {
       for (int u = 0; u < kGU; ++u) {
         const int i = min(b + u * NW * 64 + tid, tot - 1);
         const int rr = i / p.g_fields, f = i - rr * p.g_fields;
-        idv[u] = p.ids[(long long)min(i0 + rr, p.M - 1) * p.ids_ld + f];
+        const long long at = (long long)min(i0 + rr, p.M - 1) * p.ids_ld + f;
+        if (STORE_A) {
+          const int32_t r32 = p.ids32[at];
+          idv[u] = r32 < 0 ? -1 - p.id_off : (long long)r32;   // < 0: below row 0 after the offset
+        } else {
+          idv[u] = p.ids[at];
+        }
       }
 #pragma unroll
       for (int u = 0; u < kGU; ++u) {
@@ -382,8 +405,13 @@ __global__ __launch_bounds__(512) void gemm_s3_nt_kernel(S3Params p) {
   // older than the one it just issued (vmcnt counts in issue order), which include its DMA of
   // the chunk the barrier publishes.
   auto publish = [&](int c) {           // chunk c + 1's weights -> every wave
-    if (c + 1 < KC) DL_WAIT_VMCNT(DMAW + 4);   // every batch but chunk c + 2's: chunk c + 1's DMA too
-    else DL_WAIT_VMCNT(0);                // the epilogue reuses the ring: nothing may still land
+    if (c + 1 < KC) {
+      if (STORE_A) DL_WAIT_VMCNT(DMAW + 8);    // ... and the step's four x0 stores, issued before the DMA
+      else DL_WAIT_VMCNT(DMAW + 4);   // every batch but chunk c + 2's: chunk c + 1's DMA too
+    }
+    else {
+      DL_WAIT_VMCNT(0);                   // the epilogue reuses the ring: nothing may still land
+    }
 
     __builtin_amdgcn_s_waitcnt(0xc07f);   // lgkmcnt(0): this wave's fragment reads are done
     __builtin_amdgcn_s_barrier();
@@ -406,7 +434,22 @@ __global__ __launch_bounds__(512) void gemm_s3_nt_kernel(S3Params p) {
       split8(ra[2], ra[3], P[3], P[4], P[5]);
       asm volatile("" : "+v"(P[0]), "+v"(P[1]), "+v"(P[2]), "+v"(P[3]), "+v"(P[4]), "+v"(P[5]));
     };
+    // STORE_A: chunk c's raw A pieces into x0 (column-tile-0 blocks, gathered chunks, rows < M)
+    const auto st_rsrc = __builtin_amdgcn_make_buffer_rsrc((void*)p.a_store, (short)0, STORE_A ? p.M * p.lda * 4 : 0,
+                                                           0x00020000);
+    auto store_a = [&](int c, const float4 (&ra)[4]) {
+      if constexpr (STORE_A) {
+        const bool on = j0 == 0 && c < p.g_chunks;
+        const uint32_t k4 = 4u * (uint32_t)(32 * c + 8 * kq);
+        const uint32_t o0 = on && ok0 ? a_off0 + k4 : 0x80000000u, o1 = on && ok1 ? a_off1 + k4 : 0x80000000u;
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(s3_u32x4_t, ra[0]), st_rsrc, (int)o0, 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(s3_u32x4_t, ra[1]), st_rsrc, (int)(o0 + 16u), 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(s3_u32x4_t, ra[2]), st_rsrc, (int)o1, 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(s3_u32x4_t, ra[3]), st_rsrc, (int)(o1 + 16u), 0, 0);
+      }
+    };
     splitp(raA, pA);
+    store_a(0, raA);
     auto step_es = [&](int c, shortx8 (&P)[6], shortx8 (&Pn)[6], float4 (&R)[4], float4 (&F)[4]) {
       load_a(c + 2, F);
       asm volatile("" ::: "memory");   // the loads issue here, not sunk to the mid-step split
@@ -456,6 +499,7 @@ __global__ __launch_bounds__(512) void gemm_s3_nt_kernel(S3Params p) {
         }
         if (f == kNtEsAt) {
           if (c + 1 < KC) splitp(R, Pn);
+          store_a(c + 1, R);   // (past KC: chunk KC's pieces fall outside the gathered chunks: dropped)
           dma_b(c + 2, (c + 2) % 3);
         }
       }
@@ -1299,14 +1343,14 @@ extern "C" int dl_gemm_s3_nt_bits(int32_t M, int32_t N, int32_t K, const float* 
   DL_RETURN_LAUNCH("dl_gemm_s3_nt");
 }
 
-extern "C" int dl_gemm_s3_nt_gather(int32_t M, int32_t N, int32_t K, const float* A, int32_t lda,
-                                    const float* table, int64_t n_rows, int32_t table_ld, const int64_t* ids,
-                                    int32_t ids_ld, int64_t id_offset, int32_t zero_row0, int32_t fields,
-                                    int32_t emb_dim, const uint16_t* Bp, int32_t ldb, int64_t b_plane, float* C,
-                                    int32_t ldc, int32_t epi, uint16_t* bits, int32_t ldbits, void* stream) {
+static int s3_nt_gather_launch(int32_t M, int32_t N, int32_t K, const float* A, int32_t lda, const float* table,
+                               int64_t n_rows, int32_t table_ld, const int64_t* ids, const int32_t* ids32,
+                               int32_t ids_ld, int64_t id_offset, int32_t zero_row0, int32_t fields, int32_t emb_dim,
+                               const uint16_t* Bp, int32_t ldb, int64_t b_plane, float* C, int32_t ldc, int32_t epi,
+                               uint16_t* bits, int32_t ldbits, float* a_store, void* stream) {
   if (int rc = s3_nt_check(M, N, K, A, lda, Bp, ldb, b_plane, C, ldc, epi, nullptr, bits, ldbits)) return rc;
   DL_CHECK_ARG(epi == S3_STORE || epi == S3_RELU, "gather: epilogue %d (store / relu only)", epi);
-  DL_CHECK_ARG(table && ids, "gather: NULL table / ids");
+  DL_CHECK_ARG(table && (ids || ids32), "gather: NULL table / ids");
   DL_CHECK_ARG(emb_dim == 8 || emb_dim == 16 || emb_dim == 32 || emb_dim == 64, "gather: emb_dim %d", emb_dim);
   DL_CHECK_ARG(fields > 0 && fields <= kNtGmaxF, "gather: %d fields (1..%d)", fields, kNtGmaxF);
   DL_CHECK_ARG((fields * emb_dim) % 32 == 0 && fields * emb_dim <= K,
@@ -1321,7 +1365,8 @@ extern "C" int dl_gemm_s3_nt_gather(int32_t M, int32_t N, int32_t K, const float
   p.A = A; p.B = Bp; p.C = C;
   p.M = M; p.N = N; p.K = K; p.lda = lda; p.ldb = ldb; p.ldc = ldc; p.b_plane = b_plane;
   p.bits = bits; p.ldbits = ldbits;
-  p.G = table; p.ids = ids; p.id_off = id_offset; p.n_rows = n_rows; p.ids_ld = ids_ld; p.g_ld = table_ld;
+  p.G = table; p.ids = ids; p.ids32 = ids32; p.a_store = a_store;
+  p.id_off = id_offset; p.n_rows = n_rows; p.ids_ld = ids_ld; p.g_ld = table_ld;
   p.g_fields = fields; p.g_esh = __builtin_ctz(emb_dim); p.g_chunks = fields * emb_dim / 32;
   p.zero_row0 = zero_row0 ? 1 : 0;
   p.g_bytes = (unsigned)(n_rows * table_ld * 4);
@@ -1329,12 +1374,38 @@ extern "C" int dl_gemm_s3_nt_gather(int32_t M, int32_t N, int32_t K, const float
   const bool direct = s3_nt_direct(M, N, ldc, epi, bits, ldbits);
   const int tiles = (int)(ceil_div(M, kNtBM) * ceil_div(N, kNtBN));
   const size_t lds = kNtLds + (size_t)fields * kNtGfs * 4;
-  if (direct) {
-    if (epi == S3_STORE) hipLaunchKernelGGL((gemm_s3_nt_kernel<S3_STORE, true, true>), dim3(tiles), dim3(512), lds, s, p);
-    else hipLaunchKernelGGL((gemm_s3_nt_kernel<S3_RELU, true, true>), dim3(tiles), dim3(512), lds, s, p);
-  } else if (epi == S3_STORE) hipLaunchKernelGGL((gemm_s3_nt_kernel<S3_STORE, false, true>), dim3(tiles), dim3(512), lds, s, p);
-  else hipLaunchKernelGGL((gemm_s3_nt_kernel<S3_RELU, false, true>), dim3(tiles), dim3(512), lds, s, p);
+#define DL_S3G(E_, D_, ST_) hipLaunchKernelGGL((gemm_s3_nt_kernel<E_, D_, true, ST_>), dim3(tiles), dim3(512), lds, s, p)
+  if (a_store) {   // the training form: int32 rows, x0 written
+    if (direct) { if (epi == S3_STORE) DL_S3G(S3_STORE, true, true); else DL_S3G(S3_RELU, true, true); }
+    else if (epi == S3_STORE) DL_S3G(S3_STORE, false, true);
+    else DL_S3G(S3_RELU, false, true);
+  } else if (direct) {
+    if (epi == S3_STORE) DL_S3G(S3_STORE, true, false); else DL_S3G(S3_RELU, true, false);
+  } else if (epi == S3_STORE) DL_S3G(S3_STORE, false, false);
+  else DL_S3G(S3_RELU, false, false);
+#undef DL_S3G
   DL_RETURN_LAUNCH("dl_gemm_s3_nt_gather");
+}
+
+extern "C" int dl_gemm_s3_nt_gather(int32_t M, int32_t N, int32_t K, const float* A, int32_t lda,
+                                    const float* table, int64_t n_rows, int32_t table_ld, const int64_t* ids,
+                                    int32_t ids_ld, int64_t id_offset, int32_t zero_row0, int32_t fields,
+                                    int32_t emb_dim, const uint16_t* Bp, int32_t ldb, int64_t b_plane, float* C,
+                                    int32_t ldc, int32_t epi, uint16_t* bits, int32_t ldbits, void* stream) {
+  DL_CHECK_ARG(ids, "gather: NULL ids");
+  return s3_nt_gather_launch(M, N, K, A, lda, table, n_rows, table_ld, ids, nullptr, ids_ld, id_offset, zero_row0,
+                             fields, emb_dim, Bp, ldb, b_plane, C, ldc, epi, bits, ldbits, nullptr, stream);
+}
+
+extern "C" int dl_gemm_s3_nt_gather_rows(int32_t M, int32_t N, int32_t K, float* A, int32_t lda, const float* rows,
+                                         int64_t n_rows, int32_t rows_ld, const int32_t* idx, int32_t idx_ld,
+                                         int32_t idx_base, int32_t fields, int32_t emb_dim, const uint16_t* Bp,
+                                         int32_t ldb, int64_t b_plane, float* C, int32_t ldc, int32_t epi,
+                                         uint16_t* bits, int32_t ldbits, void* stream) {
+  DL_CHECK_ARG(idx && A, "gather rows: NULL idx / A");
+  DL_CHECK_ARG(idx_base >= 0, "gather rows: idx_base %d", idx_base);
+  return s3_nt_gather_launch(M, N, K, A, lda, rows, n_rows, rows_ld, nullptr, idx, idx_ld, idx_base, 0, fields,
+                             emb_dim, Bp, ldb, b_plane, C, ldc, epi, bits, ldbits, A, stream);
 }
 
 extern "C" int dl_gemm_s3_nt(int32_t M, int32_t N, int32_t K, const float* A, int32_t lda, const uint16_t* Bp,

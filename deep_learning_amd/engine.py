@@ -817,6 +817,21 @@ class CTREngine:
                     ptr(self.in_cate), ptr(self.in_cont), ptr(self.in_vec), ptr(x0), ptr(self.fm_out),
                     ptr(self.fm_sum), ptr(self.err), s)
 
+    def fused_gather_rows(self):
+        """Whether the lazy single-GPU forward (rec_gather + the indexed lookup) lets the first
+        s3 tower layer gather the deep rows from the batch's compact rows itself
+        (dl_gemm_s3_nt_gather_rows: the lookup writes the FM side and x0's cont / pooled columns,
+        the layer reads rows_u through the inverse map and writes x0's deep columns for dw_l0 —
+        bit-identical to the lookup writing them, tests/test_gpu_parity.py).  Same requirements
+        as fused_gather_l0; DLAMD_FUSED_GATHER=0 turns both off."""
+        sp = self.spec
+        if (os.environ.get("DLAMD_FUSED_GATHER", "1") == "0" or not self.s3 or self.bf or not self.lazy
+                or type(self) is not CTREngine or self.fwd_rec or self.fwd_scatter):
+            return False
+        return (self.cat_col == 0 and sp.E in (8, 16, 32, 64) and 0 < sp.S <= 40 and (sp.S * sp.E) % 32 == 0
+                and sp.S * sp.E <= self.in_ld[0] and self.rows_u.numel() * 4 < 0xFFFFFF00
+                and self.idx_inv is not None)
+
     def fused_gather_l0(self):
         """Whether predict on current planes fuses the deep lookup into the first tower layer
         (dl_gemm_s3_nt_gather: the f32 tower's A stream reads each sample's embedding rows from
@@ -967,7 +982,14 @@ class CTREngine:
                         ptr(self.rows_u1) if sp.fm else None, ptr(self.idx_inv), self.n_rep, ptr(self.slot_start),
                         ptr(self.slot_end), sp.M, self.fm_pool_col, ptr(self.x0), ptr(self.fm_out), ptr(self.cnt_emb),
                         ptr(self.cnt_first), s)
-            self._c("embed_fwd", "dl_embed_fwd_indexed", C_ref(L), ptr(self.rows_u),
+            # the deep rows go to x0 through the first tower layer where it can gather them
+            # (fused_gather_rows: dl_gemm_s3_nt_gather_rows writes x0's deep columns itself)
+            fused = "rows" if self.fused_gather_rows() else False
+            Lx = L
+            if fused:
+                Lx = type(L).from_buffer_copy(L)
+                Lx.x0_cat_col = -1
+            self._c("embed_fwd", "dl_embed_fwd_indexed", C_ref(Lx), ptr(self.rows_u),
                     ptr(self.rows_u1) if sp.fm else None, ptr(self.idx_inv), self.n_rep, ptr(self.in_cont),
                     ptr(self.in_vec), ptr(x0), ptr(self.fm_out), ptr(self.fm_sum), s)
         else:
@@ -994,7 +1016,15 @@ class CTREngine:
             x = self.x0
             for l, hdim in enumerate(sp.hidden):
                 bits = (ptr(self.hbits[l]), self.hbits_ld[l]) if l < len(self.hbits) else (None, 0)
-                if l == 0 and fused:
+                if l == 0 and fused == "rows":
+                    # the training form: rows_u through the inverse map (deep slots after the FM
+                    # slots), x0's deep columns written for the weight gradient
+                    off = sp.S if sp.fm else 0
+                    self._c("gemm_fwd_l0", "dl_gemm_s3_nt_gather_rows", B, hdim, self.in_ld[0], ptr(x), self.in_ld[0],
+                            ptr(self.rows_u), self.rows_u.shape[0], sp.E, ptr(self.idx_inv[off:]), self.n_slot,
+                            self.n_rep, sp.S, sp.E, ptr(self.WTp[0]), self.in_ld[0], self.in_ld[0] * self.out_ld[0],
+                            ptr(self.h[0]), self.h_ld[0], 1, *bits, s)
+                elif l == 0 and fused:
                     FL = self._flat_layout(B)
                     self._c("gemm_fwd_l0", "dl_gemm_s3_nt_gather", B, hdim, self.in_ld[0], ptr(x), self.in_ld[0],
                             ptr(self.p_plane), FL.n_rows, self.p_plane.shape[1], ptr(self.in_cate), FL.cate_ld,

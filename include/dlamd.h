@@ -66,8 +66,8 @@ typedef struct dl_emb_layout {
   int32_t x0_cont_col;      /* -1: cont not copied into x0                           */
   int32_t x0_vec_col;       /* -1: vector not copied into x0                         */
   int32_t x0_cat_col;       /* column of the first single-cate embedding in x0 (-1:
-                               not written — dl_embed_fwd / _slots only, the embeddings
-                               then read by dl_gemm_s3_nt_gather from the table)       */
+                               not written — dl_embed_fwd / _slots / _indexed only, the
+                               embeddings then read by dl_gemm_s3_nt_gather)          */
   int32_t x0_pool_col;      /* column of the first pooled vector in x0 (fm_extra>0)  */
   int32_t fm_ld;            /* floats between samples in fm_out                      */
   int32_t dx0_ld;           /* floats between samples in dx0 (backward)              */
@@ -347,6 +347,16 @@ int dl_gemm_s3_nt_gather(int32_t M, int32_t N, int32_t K, const float* A, int32_
                          int32_t zero_row0, int32_t fields, int32_t emb_dim, const uint16_t* B, int32_t ldb,
                          int64_t b_plane, float* C, int32_t ldc, int32_t epi, uint16_t* bits, int32_t ldbits,
                          void* stream);
+/* dl_gemm_s3_nt_gather_rows: the training form — the deep rows of the batch's compact caught-up
+ * rows (dl_rec_gather's rows_u) through the batch index's inverse map: row idx_base + idx[m *
+ * idx_ld + f] (idx < 0: the zero row), and the gathered columns also written into A (x0) by the
+ * first column tile's blocks, for the weight gradient that streams x0 (the lookup then runs with
+ * x0_cat_col = -1).  Bit-identical to dl_embed_fwd_indexed writing those columns followed by
+ * dl_gemm_s3_nt_bits. */
+int dl_gemm_s3_nt_gather_rows(int32_t M, int32_t N, int32_t K, float* A, int32_t lda, const float* rows,
+                              int64_t n_rows, int32_t rows_ld, const int32_t* idx, int32_t idx_ld, int32_t idx_base,
+                              int32_t fields, int32_t emb_dim, const uint16_t* B, int32_t ldb, int64_t b_plane,
+                              float* C, int32_t ldc, int32_t epi, uint16_t* bits, int32_t ldbits, void* stream);
 
 /* ------------------------------------------------------------------------
  * Output layer + sigmoid + eps-log-loss, forward and backward fused

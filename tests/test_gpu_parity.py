@@ -420,6 +420,36 @@ def test_lookup_without_deep_columns(hip_lib, name):
         e.check_error()
 
 
+@pytest.mark.parametrize("name,kw", [
+    ("deepfm_pipeline", dict(CASES["deepfm_pipeline"], cate_index_size=40000)),
+    ("deepfm_multi_cate", dict(V=4, S=8, E=16, cate_index_size=6000, hidden=[48, 32],
+                               multi_ranges=[[0, 30, "a"], [30, 50, "b"]])),
+    ("dnn", dict(CASES["dnn"], cate_index_size=9000))])
+def test_fused_gather_training_bit_identical(hip_lib, name, kw, monkeypatch):
+    """The lazy training forward with the deep rows gathered by the first s3 layer
+    (dl_gemm_s3_nt_gather_rows, the default where it applies: the lookup writes only the FM side
+    and x0's cont / pooled columns, the layer writes x0's deep columns for dw_l0) against the
+    indexed lookup writing them (DLAMD_FUSED_GATHER=0): the same losses, logits and tables, bit
+    for bit, over graph-captured steps with a prefetched next batch."""
+    bs = _batches(name, kw, 300, 6, seed=53)
+    out = {}
+    for mode in ("1", "0"):
+        monkeypatch.setenv("DLAMD_FUSED_GATHER", mode)
+        e = CTREngine(ModelSpec(_model(name), **kw), max_batch=300, seed=9, adam="lazy", hist_len=8)
+        assert e.fused_gather_rows() == (mode == "1")
+        losses = []
+        for i, bt in enumerate(bs[:5]):
+            e.train_step(bt, graph=i >= 1, next_batch=bs[i + 1] if i + 1 < 5 else None)
+            losses.append(e.loss())
+        z = e.predict(bs[5], logits=True)
+        out[mode] = (losses, z, e.params())
+        del e
+    assert out["1"][0] == out["0"][0]
+    np.testing.assert_array_equal(out["1"][1], out["0"][1])
+    for k in out["0"][2]:
+        np.testing.assert_array_equal(out["1"][2][k], out["0"][2][k], err_msg=k)
+
+
 def test_lazy_multi_hot_tracks_oracle(hip_lib):
     """Multi-hot pooling on row records (deepfm_multi_cate): pooled rows come from the
     caught-up records through the batch index, their gradients join each row's ordered
