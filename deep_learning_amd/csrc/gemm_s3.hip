@@ -122,6 +122,9 @@ struct S3Params {
 // [row][c >> 4] = h[row][c] > 0) instead of the f32 activations — 1/32 of the mask bytes
 enum { S3_STORE = 0, S3_RELU = 1, S3_MASK = 2, S3_MASKBITS = 3 };
 
+#ifndef DL_S3_MWLATE
+#define DL_S3_MWLATE 1   // dX bitmask words loaded before the last k step (0: before the main loop)
+#endif
 #ifndef DL_S3_GDIAG
 #define DL_S3_GDIAG 0   // diagnostics build: the gathered A rows all read table row 0 (timing only)
 #endif
@@ -340,17 +343,22 @@ __global__ __launch_bounds__(512) void gemm_s3_nt_kernel(S3Params p) {
 
   // DIRECT ReluGrad: this lane's rows' bitmask words for the tile's 13 halfwords (j0 / 16 ..
   // + 12), 7 dwords from the dword holding the first (ldbits even: rows are dword aligned),
-  // loaded here so the epilogue does not wait a memory round trip for them
+  // loaded before the last k chunk's step (load_mw below), so the epilogue does not wait a
+  // memory round trip for them and their 14 registers are not held through the main loop
+  // (loaded before it they cost 7 spilled VGPRs)
   uint32_t mw[DIRECT && EPI == S3_MASKBITS ? 2 : 1][7];
-  if constexpr (DIRECT && EPI == S3_MASKBITS) {
+  auto load_mw = [&]() {
+    if constexpr (DIRECT && EPI == S3_MASKBITS) {
 #pragma unroll
-    for (int a = 0; a < 2; ++a) {
-      const int row = min(r0 + 16 * a + cl, p.M - 1);
-      const uint32_t* wp = reinterpret_cast<const uint32_t*>(p.bits + (long long)row * p.ldbits) + (j0 >> 5);
+      for (int a = 0; a < 2; ++a) {
+        const int row = min(r0 + 16 * a + cl, p.M - 1);
+        const uint32_t* wp = reinterpret_cast<const uint32_t*>(p.bits + (long long)row * p.ldbits) + (j0 >> 5);
 #pragma unroll
-      for (int i = 0; i < 7; ++i) mw[a][i] = wp[i];
+        for (int i = 0; i < 7; ++i) mw[a][i] = wp[i];
+      }
     }
-  }
+  };
+  if (!DL_S3_MWLATE) load_mw();
 
   float4 raA[4], raB[4];
   // prologue: B chunks 0 and 1 in flight, A chunks 0 and 1
@@ -510,6 +518,7 @@ __global__ __launch_bounds__(512) void gemm_s3_nt_kernel(S3Params p) {
       step_es(c, pA, pB, raB, raA);
       step_es(c + 1, pB, pA, raA, raB);
     }
+    if (DL_S3_MWLATE) load_mw();   // under the peeled last step's MFMAs (odd KC), else before the epilogue
     if (c < KC) step_es(c, pA, pB, raB, raA);
   } else
 #endif
@@ -602,6 +611,7 @@ __global__ __launch_bounds__(512) void gemm_s3_nt_kernel(S3Params p) {
     step(c, raA);
     step(c + 1, raB);
   }
+  if (DL_S3_MWLATE) load_mw();
   if (c < KC) step(c, raA);
   }
 
