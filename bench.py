@@ -459,6 +459,37 @@ def lookup_alone(eng, batch, B, per_sample, reps=20):
                  "note": "us = the FM-only lookup + (fused first layer - the same layer over a written x0): "
                          "what the 3,640 B/sample gather adds to predict's forward when it feeds the MFMA "
                          "tiles directly"}
+        # the same cost read off the back-to-back pair (lookup + fused layer, minus the plain
+        # layer alone): the two kernels' cache interactions included
+        fused["pair_minus_plain_us"] = round(pair_f - l0u, 1)
+        fused["frac_by_pair"] = round(B * per_sample / ((pair_f - l0u) * 1e-6) / 1e9 / HBM_PEAK_GBS, 3)
+        if eng.fused_gather_tab(B, force=True):
+            # the table form (DLAMD_GATHER_TAB=1, not the default): the lookup writes the deep rows'
+            # plane offsets too (dl_embed_fwd_gtab, no fm_sum) and the first layer stages them as
+            # they stand instead of loading and range-checking the ids
+            def fm_tab():
+                call("dl_embed_fwd_gtab", C_ref(FLn), ptr(eng.p_plane), 1 if sp.fm else 0, ptr(eng.in_cate),
+                     ptr(eng.in_cont), ptr(eng.in_vec), ptr(x0), ptr(eng.fm_out), None, ptr(eng.gtab),
+                     ptr(eng.err), s)
+
+            def l0_tab():
+                call("dl_gemm_s3_nt_gather_tab", B, hd, ld0, ptr(x0), ld0, ptr(eng.p_plane), FLn.n_rows,
+                     eng.p_plane.shape[1], ptr(eng.gtab), sp.S, sp.E, ptr(eng.WTp[0]), ld0, ld0 * ol0,
+                     ptr(eng.h[0]), eng.h_ld[0], 1, *bits, s)
+
+            fut = timed(fm_tab)[0]
+            l0t = timed(l0_tab)[0]
+            pair_t = timed(lambda: (fm_tab(), l0_tab()))[0]
+            t_us = fut + max(l0t - l0u, 0.0)
+            t_gb = B * per_sample / (t_us * 1e-6) / 1e9
+            fused["table_form"] = {
+                "kernels": ["embed_fwd (FM + row offsets)", "gemm_fwd_l0 (gather, offset table)"],
+                "fm_lookup_us": fut, "fwd_l0_gather_us": l0t, "us": round(t_us, 1), "GB/s": round(t_gb, 1),
+                "frac": round(t_gb / HBM_PEAK_GBS, 3), "lookup_plus_l0_us": pair_t,
+                "pair_minus_plain_us": round(pair_t - l0u, 1),
+                "frac_by_pair": round(B * per_sample / ((pair_t - l0u) * 1e-6) / 1e9 / HBM_PEAK_GBS, 3),
+                "note": "DLAMD_GATHER_TAB=1, not the default: its layer alone is faster than the id form's, "
+                        "the back-to-back pair is not (frac_by_pair)"}
     return {"kernels": ["embed_fwd (slot plane)"], "us": us, "GB/s": gb, "frac": fr, "fused": fused,
             "records": {"kernels": ["rec_gather (13 cont rows)", "embed_fwd_rec_flat"], "us": rus, "GB/s": rgb,
                         "frac": rfr},

@@ -81,6 +81,8 @@ SIGNATURES = {
     "dl_embed_cont_reduce": (I32, [LP, P, I32, P, P, P, P]),
     "dl_embed_fwd_indexed": (I32, [LP, P, P, P, I32, P, P, P, P, P, P]),
     "dl_embed_fwd_slots": (I32, [LP, P, P, P, P, P, P, P, P, P]),
+    "dl_embed_fwd_gtab": (I32, [LP, P, I32, P, P, P, P, P, P, P, P, P]),
+    "dl_embed_fwd_gtab_ok": (I32, [LP]),
     "dl_embed_fwd_rec": (I32, [LP, P, I32, I32, P, P, P, P, P, P, I32, P, I32, P, P, P, P, P]),
     "dl_embed_fwd_rec_flat": (I32, [LP, P, I32, I32, P, P, P, P, P, P, P, P, P, P, P]),
     "dl_shard_gather": (I32, [P, P, P, I64, I32, P, P, P]),
@@ -110,6 +112,8 @@ SIGNATURES = {
                                    I32, I32, P, I32, P]),
     "dl_gemm_s3_nt_gather_rows": (I32, [I32, I32, I32, P, I32, P, I64, I32, P, I32, I32, I32, I32, P, I32, I64, P,
                                         I32, I32, P, I32, P]),
+    "dl_gemm_s3_nt_gather_tab": (I32, [I32, I32, I32, P, I32, P, I64, I32, P, I32, I32, P, I32, I64, P, I32, I32,
+                                       P, I32, P]),
     "dl_gemm_s3_tn": (I32, [I32, I32, I32, P, I32, P, I32, P, I32, I32, I64, P]),
     "dl_head_fwd_bwd": (I32, [I32, I32, I32, P, I32, P, I32, P, P, F, F, P, P, P, P, P, I32, P]),
     "dl_head_grid": (I32, [I32]),

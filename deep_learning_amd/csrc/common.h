@@ -180,6 +180,14 @@ __host__ __device__ __forceinline__ int s3_kpos(int k, int K) {
   return (k & ~31) | (kk < 16 ? 8 * (kk >> 2) + (kk & 3) : 8 * ((kk - 16) >> 2) + 4 + (kk & 3));
 }
 
+// The row-offset table of the fused predict front (dl_embed_fwd_gtab writes it,
+// dl_gemm_s3_nt_gather_tab stages it in LDS as it stands): per 256-sample tile of the batch,
+// per deep field, kGtabPitch u32 — sample b's entry at [b / 256][f][b % 256] holds the byte
+// offset of its row in the plane, or kGtabMasked (past any plane: reads as zeros) for a masked
+// or invalid id.  The pitch keeps a wave's reads of two fields in disjoint LDS banks.
+constexpr int kGtabRows = 256, kGtabPitch = 272;
+constexpr uint32_t kGtabMasked = 0xFFFFFF00u;
+
 // DL_ROOT_STATE=0 (A/B builds only: the host's adam_state conversions assume the root form)
 // keeps TF's v in the tables as before.
 #ifndef DL_ROOT_STATE

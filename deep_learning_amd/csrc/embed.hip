@@ -46,6 +46,9 @@ struct EmbArgs {
   // output and the deep references' x0 columns are already written — only references whose
   // row has no key (inv < 0: the zero row) are written here, as zeros
   int staged;
+  // (dl_embed_fwd_gtab) the deep references' row byte offsets for the fused first tower layer,
+  // common.h kGtab* layout; the deep rows themselves are then not read here
+  uint32_t* gtab;
 };
 
 __device__ __forceinline__ bool row_ok(int64_t row, int zero_row0) {
@@ -57,6 +60,7 @@ __device__ __forceinline__ float4 f4_zero() { return make_float4(0.f, 0.f, 0.f, 
 constexpr int kMaxHotContFwd = 32;
 
 constexpr int kTileSamples = 16;   // samples staged per block iteration
+constexpr int kGtabMaxNps = 4;     // dl_embed_fwd_gtab: at most 4 passes of FM slots a sample
 constexpr int kMaxSlots = 128;     // FM slots + deep slots per sample
 
 #ifndef DL_FWD_SPW
@@ -173,6 +177,21 @@ void embed_fwd_kernel(EmbArgs a) {
     for (int k = threadIdx.x; k < nb * Cf; k += blockDim.x)
       vals_s[k / Cf][k % Cf] = a.cont[(int64_t)(b0 + k / Cf) * L.cont_fields + k % Cf];
     __syncthreads();
+    // (the instantiations the gtab lookup launches: with x0_cat_col = -1 a sample's slots are its
+    // FM fields only; instantiated in the others it costs the NPS = 5 forms spilled registers)
+    if constexpr ((REC == 0 || REC == 3) && NPS <= kGtabMaxNps) if (a.gtab) {
+      // the tile's deep rows as byte offsets, field-major: 16 samples = one 64-B piece a field
+      // (a tile never straddles two 256-sample tables: kGtabRows % kTileSamples == 0)
+      uint32_t* gt = a.gtab + (int64_t)(b0 / kGtabRows) * S * kGtabPitch + b0 % kGtabRows;
+      const uint32_t rb = 16u * (uint32_t)TP;   // bytes between plane rows
+      for (int k = threadIdx.x; k < S * kTileSamples; k += blockDim.x) {
+        const int f = k / kTileSamples, j = k % kTileSamples;
+        if (j < nb) {
+          const int dr = rows_s[j][Fs + f];
+          gt[f * kGtabPitch + j] = dr >= 0 ? (uint32_t)dr * rb : kGtabMasked;
+        }
+      }
+    }
     // SPW samples per wave iteration, all their row loads issued before any is consumed
     // (DL_FWD_SPW = 2: the plain / slot-plane lookups with at most 3 passes a sample; measured
     // neutral on the FM-only lookup of the fused predict, 60 us both, profiles/r06i): one
@@ -1006,6 +1025,35 @@ extern "C" int dl_embed_fwd_slots(const dl_emb_layout* L, const float* slots, co
   if (L->batch == 0) return 0;
   EmbArgs a{*L, nullptr, 0, slots, slots + L->emb_dim, cate, cont, vector, x0, fm_out, fm_sum, err};
   return launch_embed_fwd<3>(L, a, stream);
+}
+
+// whether dl_embed_fwd_gtab takes this layout: E = 8 / 16 (the lookup's instantiations with at
+// most kGtabMaxNps passes; E = 32 / 64 run one all-slots form) and the FM slots within them
+extern "C" int dl_embed_fwd_gtab_ok(const dl_emb_layout* L) {
+  if (!L || (L->emb_dim != 8 && L->emb_dim != 16)) return 0;
+  const int fs = L->use_fm ? (L->fm_cont ? L->cont_fields : 0) + L->cate_fields : 0;
+  const int rpi = 64 / (L->emb_dim / 4);
+  return (fs + rpi - 1) / rpi <= kGtabMaxNps ? 1 : 0;
+}
+
+extern "C" int dl_embed_fwd_gtab(const dl_emb_layout* L, const float* plane, int32_t slot_plane, const int64_t* cate,
+                                 const float* cont, const float* vector, float* x0, float* fm_out, float* fm_sum,
+                                 uint32_t* gtab, int32_t* err, void* stream) {
+  if (int rc = check_layout(L, true)) return rc;
+  DL_CHECK_ARG(plane && cate && gtab, "NULL plane/cate/gtab");
+  DL_CHECK_ARG(L->x0_cat_col == -1, "gtab: the deep rows go to the offset table, not x0 (x0_cat_col -1)");
+  DL_CHECK_ARG(x0 || (L->x0_cont_col < 0 && L->x0_vec_col < 0), "gtab: x0 columns to write but x0 NULL");
+  DL_CHECK_ARG(L->fm_extra == 0 && L->multi_width == 0, "gtab: single-valued fields only");
+  DL_CHECK_ARG(!L->use_fm || (slot_plane && fm_out), "gtab: FM models read the slot plane and write fm_out");
+  DL_CHECK_ARG((uintptr_t)plane % 16 == 0 && (uintptr_t)gtab % 16 == 0, "gtab: plane / table must be 16-B aligned");
+  DL_CHECK_ARG((unsigned long long)L->n_rows * L->emb_dim * (slot_plane ? 8 : 4) < kGtabMasked,
+               "gtab: the plane spans past the 32-bit offsets");
+  DL_CHECK_ARG(dl_embed_fwd_gtab_ok(L), "gtab: more than %d passes of FM slots a sample", kGtabMaxNps);
+  if (L->batch == 0) return 0;
+  EmbArgs a{*L, nullptr, 0, plane, slot_plane ? plane + L->emb_dim : nullptr, cate, cont, vector, x0, fm_out, fm_sum,
+            err};
+  a.gtab = gtab;
+  return slot_plane ? launch_embed_fwd<3>(L, a, stream) : launch_embed_fwd<0>(L, a, stream);
 }
 
 extern "C" int dl_embed_fwd_indexed(const dl_emb_layout* L, const float* rows, const float* rows_first,

@@ -116,6 +116,9 @@ struct S3Params {
   long long id_off, n_rows;
   int ids_ld, g_ld, g_fields, g_esh, g_chunks, zero_row0;
   unsigned g_bytes;          // G's buffer range (bytes, < 0xFFFFFF00: the masked rows' offset)
+  // (the table form, dl_gemm_s3_nt_gather_tab) the rows' byte offsets already resolved by the
+  // lookup (common.h kGtab*): the block stages its part of the table as it stands
+  const uint32_t* gofs;
 };
 
 // S3_MASKBITS: the ReluGrad mask from the forward's bitmask (bit c & 15 of halfword
@@ -191,6 +194,8 @@ static_assert(8 * 16 * kNtEP * sizeof(float) <= kNtLds, "epilogue tiles fit the 
 constexpr int kNtGfs = 272;
 constexpr int kNtGmaxF = (160 * 1024 - (int)kNtLds) / (kNtGfs * 4);
 constexpr uint32_t kNtGmasked = 0xFFFFFF00u;
+static_assert(kNtBM == kGtabRows && kNtGfs == kGtabPitch && kNtGmasked == kGtabMasked,
+              "the lookup's offset table is the block's LDS table as it stands");
 
 __device__ __forceinline__ int nt_slot(int j, int kq) { return kq ^ ((j >> 2) & 2); }   // an involution in kq
 
@@ -367,8 +372,23 @@ __global__ __launch_bounds__(512) void gemm_s3_nt_kernel(S3Params p) {
     // (coalesced over the id matrix), published by a barrier before any A piece is fetched
     dma_b(0, 0);
     dma_b(1, 1);
+    if (!STORE_A && p.gofs) {
+      // the table form: the lookup resolved the offsets already, in this table's layout — one
+      // contiguous copy (four 16-B pieces a thread in flight: one round trip for 26 fields)
+      const uint4* src = reinterpret_cast<const uint4*>(p.gofs + (long long)(i0 / BM) * p.g_fields * kNtGfs);
+      uint4* dst = reinterpret_cast<uint4*>(gtab);
+      const int n16 = p.g_fields * (kNtGfs / 4);
+      for (int b = 0; b < n16; b += 4 * NW * 64) {
+        uint4 v[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) v[u] = src[min(b + u * NW * 64 + tid, n16 - 1)];
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+          if (b + u * NW * 64 + tid < n16) dst[b + u * NW * 64 + tid] = v[u];
+      }
+    }
     // (eight ids a thread in flight at once: one memory round trip per 4,096 entries; sixteen spill)
-    const int tot = BM * p.g_fields;
+    const int tot = !STORE_A && p.gofs ? 0 : BM * p.g_fields;
     constexpr int kGU = 8;
     for (int b = 0; b < tot; b += kGU * NW * 64) {
       long long idv[kGU];
@@ -1357,10 +1377,11 @@ static int s3_nt_gather_launch(int32_t M, int32_t N, int32_t K, const float* A, 
                                int64_t n_rows, int32_t table_ld, const int64_t* ids, const int32_t* ids32,
                                int32_t ids_ld, int64_t id_offset, int32_t zero_row0, int32_t fields, int32_t emb_dim,
                                const uint16_t* Bp, int32_t ldb, int64_t b_plane, float* C, int32_t ldc, int32_t epi,
-                               uint16_t* bits, int32_t ldbits, float* a_store, void* stream) {
+                               uint16_t* bits, int32_t ldbits, float* a_store, void* stream,
+                               const uint32_t* gofs = nullptr) {
   if (int rc = s3_nt_check(M, N, K, A, lda, Bp, ldb, b_plane, C, ldc, epi, nullptr, bits, ldbits)) return rc;
   DL_CHECK_ARG(epi == S3_STORE || epi == S3_RELU, "gather: epilogue %d (store / relu only)", epi);
-  DL_CHECK_ARG(table && (ids || ids32), "gather: NULL table / ids");
+  DL_CHECK_ARG(table && (ids || ids32 || gofs), "gather: NULL table / ids");
   DL_CHECK_ARG(emb_dim == 8 || emb_dim == 16 || emb_dim == 32 || emb_dim == 64, "gather: emb_dim %d", emb_dim);
   DL_CHECK_ARG(fields > 0 && fields <= kNtGmaxF, "gather: %d fields (1..%d)", fields, kNtGmaxF);
   DL_CHECK_ARG((fields * emb_dim) % 32 == 0 && fields * emb_dim <= K,
@@ -1380,6 +1401,7 @@ static int s3_nt_gather_launch(int32_t M, int32_t N, int32_t K, const float* A, 
   p.g_fields = fields; p.g_esh = __builtin_ctz(emb_dim); p.g_chunks = fields * emb_dim / 32;
   p.zero_row0 = zero_row0 ? 1 : 0;
   p.g_bytes = (unsigned)(n_rows * table_ld * 4);
+  p.gofs = gofs;
   hipStream_t s = as_stream(stream);
   const bool direct = s3_nt_direct(M, N, ldc, epi, bits, ldbits);
   const int tiles = (int)(ceil_div(M, kNtBM) * ceil_div(N, kNtBN));
@@ -1416,6 +1438,17 @@ extern "C" int dl_gemm_s3_nt_gather_rows(int32_t M, int32_t N, int32_t K, float*
   DL_CHECK_ARG(idx_base >= 0, "gather rows: idx_base %d", idx_base);
   return s3_nt_gather_launch(M, N, K, A, lda, rows, n_rows, rows_ld, nullptr, idx, idx_ld, idx_base, 0, fields,
                              emb_dim, Bp, ldb, b_plane, C, ldc, epi, bits, ldbits, A, stream);
+}
+
+extern "C" int dl_gemm_s3_nt_gather_tab(int32_t M, int32_t N, int32_t K, const float* A, int32_t lda,
+                                        const float* table, int64_t n_rows, int32_t table_ld, const uint32_t* gtab,
+                                        int32_t fields, int32_t emb_dim, const uint16_t* Bp, int32_t ldb,
+                                        int64_t b_plane, float* C, int32_t ldc, int32_t epi, uint16_t* bits,
+                                        int32_t ldbits, void* stream) {
+  DL_CHECK_ARG(gtab, "gather tab: NULL offset table");
+  DL_CHECK_ARG(((uintptr_t)gtab % 16) == 0, "gather tab: the offset table must be 16-B aligned");
+  return s3_nt_gather_launch(M, N, K, A, lda, table, n_rows, table_ld, nullptr, nullptr, fields, 0, 0, fields, emb_dim,
+                             Bp, ldb, b_plane, C, ldc, epi, bits, ldbits, nullptr, stream, gtab);
 }
 
 extern "C" int dl_gemm_s3_nt(int32_t M, int32_t N, int32_t K, const float* A, int32_t lda, const uint16_t* Bp,

@@ -800,15 +800,21 @@ class CTREngine:
             self._wide_flush()
         self.since_flush = 0
 
-    def plane_lookup(self, B, x0, s, deep=True):
+    def plane_lookup(self, B, x0, s, deep=True, gtab=None):
         """The lookup over flush(planes=True)'s planes: FM models read the slot plane (row and
         first-order weight in one 128-B slot, dl_embed_fwd_slots), the others the p plane.
         deep=False: the deep embeddings are not written to x0 (x0_cat_col = -1): the first tower
-        layer reads them from the plane itself (fused_gather_l0)."""
+        layer reads them from the plane itself (fused_gather_l0).  gtab: the deep rows' plane
+        offsets go to gtab as well (dl_embed_fwd_gtab, fused_gather_tab) and fm_sum (backward
+        only) is not written."""
         L = self._flat_layout(B)
         if not deep:
             L.x0_cat_col = -1
-        if self.spec.fm:
+        if gtab is not None:
+            self._c("embed_fwd", "dl_embed_fwd_gtab", C_ref(L), ptr(self.p_plane), 1 if self.spec.fm else 0,
+                    ptr(self.in_cate), ptr(self.in_cont), ptr(self.in_vec), ptr(x0), ptr(self.fm_out), None,
+                    ptr(gtab), ptr(self.err), s)
+        elif self.spec.fm:
             self._c("embed_fwd", "dl_embed_fwd_slots", C_ref(L), ptr(self.p_plane),
                     ptr(self.in_cate), ptr(self.in_cont), ptr(self.in_vec), ptr(x0), ptr(self.fm_out),
                     ptr(self.fm_sum), ptr(self.err), s)
@@ -831,6 +837,24 @@ class CTREngine:
         return (self.cat_col == 0 and sp.E in (8, 16, 32, 64) and 0 < sp.S <= 40 and (sp.S * sp.E) % 32 == 0
                 and sp.S * sp.E <= self.in_ld[0] and self.rows_u.numel() * 4 < 0xFFFFFF00
                 and self.idx_inv is not None)
+
+    def fused_gather_tab(self, B, force=False):
+        """Whether predict's fused front takes the table form: the FM-side lookup writes the deep
+        rows' plane offsets (dl_embed_fwd_gtab, which reads the same ids) and the first layer
+        stages them as they stand instead of loading and range-checking the ids itself
+        (dl_gemm_s3_nt_gather_tab) — bit-identical (tests/test_gpu_parity.py).  On top of
+        fused_gather_l0: E = 8 / 16 with the FM slots in the lookup's short forms.  Off by
+        default (DLAMD_GATHER_TAB=1 turns it on; force: the bench's A/B): measured alone the layer
+        runs 7-17 us faster, but the lookup + layer pair moves 0-1 us (profiles/r06y/)."""
+        sp = self.spec
+        if (os.environ.get("DLAMD_GATHER_TAB", "0") != "1" and not force) or sp.M:
+            return False
+        if _lib.lib().dl_embed_fwd_gtab_ok(C_ref(self._flat_layout(B))) != 1:
+            return False
+        n = -(-B // 256) * sp.S * 272
+        if getattr(self, "gtab", None) is None or self.gtab.numel() < n:
+            self.gtab = torch.empty(n, dtype=torch.int32, device=self.dev)
+        return True
 
     def fused_gather_l0(self):
         """Whether predict on current planes fuses the deep lookup into the first tower layer
@@ -936,7 +960,9 @@ class CTREngine:
             # step): the plain lookup of the dense layout (dl_embed_fwd_slots / dl_embed_fwd),
             # its deep rows read by the first tower layer itself where it can (fused_gather_l0)
             fused = self.fused_gather_l0()
-            self.plane_lookup(B, x0, s, deep=not fused)
+            if fused and self.fused_gather_tab(B):
+                fused = "tab"
+            self.plane_lookup(B, x0, s, deep=not fused, gtab=self.gtab if fused == "tab" else None)
         elif not train and self.lazy and not sp.M and self.since_flush == 0 and type(self) is CTREngine:
             # predict on a flushed table (every record caught up to the current step): the plain
             # lookup, each reference reading its record's first line (dl_embed_fwd_rec_flat)
@@ -1024,6 +1050,13 @@ class CTREngine:
                             ptr(self.rows_u), self.rows_u.shape[0], sp.E, ptr(self.idx_inv[off:]), self.n_slot,
                             self.n_rep, sp.S, sp.E, ptr(self.WTp[0]), self.in_ld[0], self.in_ld[0] * self.out_ld[0],
                             ptr(self.h[0]), self.h_ld[0], 1, *bits, s)
+                elif l == 0 and fused == "tab":
+                    # predict's table form: the rows' offsets staged from gtab
+                    FL = self._flat_layout(B)
+                    self._c("gemm_fwd_l0", "dl_gemm_s3_nt_gather_tab", B, hdim, self.in_ld[0], ptr(x), self.in_ld[0],
+                            ptr(self.p_plane), FL.n_rows, self.p_plane.shape[1], ptr(self.gtab), sp.S, sp.E,
+                            ptr(self.WTp[0]), self.in_ld[0], self.in_ld[0] * self.out_ld[0], ptr(self.h[0]),
+                            self.h_ld[0], 1, *bits, s)
                 elif l == 0 and fused:
                     FL = self._flat_layout(B)
                     self._c("gemm_fwd_l0", "dl_gemm_s3_nt_gather", B, hdim, self.in_ld[0], ptr(x), self.in_ld[0],

@@ -101,6 +101,18 @@ int dl_embed_fwd(const dl_emb_layout* L, const float* table, const float* first_
  * lazy table; same outputs as dl_embed_fwd on separate planes, bit for bit). */
 int dl_embed_fwd_slots(const dl_emb_layout* L, const float* slots, const int64_t* cate, const float* cont,
                        const float* vector, float* x0, float* fm_out, float* fm_sum, int32_t* err, void* stream);
+/* The FM side of predict's fused front (with dl_gemm_s3_nt_gather_tab): dl_embed_fwd_slots
+ * (slot_plane = 1) or dl_embed_fwd on the p plane (slot_plane = 0, models without FM) with
+ * x0_cat_col = -1, which instead of the deep rows writes their byte offsets in the plane into
+ * gtab ([ceil(B / 256)][fields][272] u32, 0xFFFFFF00 for a masked or invalid id — the first
+ * tower layer's LDS table as it stands: 16 samples of a field one 64-B write).  x0 may be NULL
+ * when x0_cont_col and x0_vec_col are -1 too (nothing of x0 written), fm_sum may be NULL
+ * (predict: no backward reads it).  Same fm_out and x0 cont / vector columns as
+ * dl_embed_fwd_slots bit for bit. */
+int dl_embed_fwd_gtab_ok(const dl_emb_layout* L);   /* 1: the layout qualifies (E = 8 / 16, FM slots in <= 4 passes) */
+int dl_embed_fwd_gtab(const dl_emb_layout* L, const float* plane, int32_t slot_plane, const int64_t* cate,
+                      const float* cont, const float* vector, float* x0, float* fm_out, float* fm_sum, uint32_t* gtab,
+                      int32_t* err, void* stream);
 
 /* Backward of dl_embed_fwd for the FM (single fields) and deep lookups.
  * dz [B] = dL/dlogit, w_head = head weights whose first F+E entries weight
@@ -357,6 +369,16 @@ int dl_gemm_s3_nt_gather_rows(int32_t M, int32_t N, int32_t K, float* A, int32_t
                               int64_t n_rows, int32_t rows_ld, const int32_t* idx, int32_t idx_ld, int32_t idx_base,
                               int32_t fields, int32_t emb_dim, const uint16_t* B, int32_t ldb, int64_t b_plane,
                               float* C, int32_t ldc, int32_t epi, uint16_t* bits, int32_t ldbits, void* stream);
+/* dl_gemm_s3_nt_gather_tab: dl_gemm_s3_nt_gather with the rows resolved beforehand — the deep
+ * rows' byte offsets come in gtab (dl_embed_fwd_gtab's table, staged into the block's LDS as it
+ * stands, one contiguous copy instead of the ids' loads and range checks: entry
+ * [m / 256][f * 272 + m % 256], 0xFFFFFF00 = a zero row); A's other columns from A (x0 with its
+ * cont / ones columns written).  Bit-identical to dl_embed_fwd(_slots) + dl_gemm_s3_nt_bits
+ * and to dl_gemm_s3_nt_gather.  gtab holds ceil(M / 256) * fields * 272 u32, 16-B aligned. */
+int dl_gemm_s3_nt_gather_tab(int32_t M, int32_t N, int32_t K, const float* A, int32_t lda, const float* table,
+                             int64_t n_rows, int32_t table_ld, const uint32_t* gtab, int32_t fields, int32_t emb_dim,
+                             const uint16_t* B, int32_t ldb, int64_t b_plane, float* C, int32_t ldc, int32_t epi,
+                             uint16_t* bits, int32_t ldbits, void* stream);
 
 /* ------------------------------------------------------------------------
  * Output layer + sigmoid + eps-log-loss, forward and backward fused

@@ -1,10 +1,12 @@
 """The north-star lookup alone (C2 shape, B = 65,536, 26 M rows): dl_embed_fwd over the dense
 p / first-order planes of a flushed table, the kernel CTREngine.predict runs — nothing else
 launches embed_fwd_kernel here (no training step), so rocprofv3 PMC passes over this script
-count the lookup alone.  python scripts/lookup_bench.py [uniform|zipf] [reps] [full|fm|fused|pair]
+count the lookup alone.  python scripts/lookup_bench.py [uniform|zipf] [reps] [full|fm|fused|pair|fmtab|tab]
 (fm: the FM-only lookup of the fused predict, x0_cat_col = -1 — the deep rows are then read by
 dl_gemm_s3_nt_gather, not here; fused: that lookup + the gathering first tower layer, predict's
-default front; pair: the full lookup + the plain first layer, the unfused front)"""
+id form; pair: the full lookup + the plain first layer, the unfused front; fmtab: the lookup of
+the table form, dl_embed_fwd_gtab — FM outputs, x0's cont columns and the deep rows' plane
+offsets; tab: that + dl_gemm_s3_nt_gather_tab, predict's front with DLAMD_GATHER_TAB=1)"""
 import os
 import sys
 
@@ -30,6 +32,9 @@ FN = eng._flat_layout(B)
 FN.x0_cat_col = -1
 if mode in ("fm", "fused"):
     FL = FN
+tab = mode in ("fmtab", "tab")
+if tab:
+    assert eng.fused_gather_tab(B, force=True)
 hd, ld0, ol0 = sp.hidden[0], eng.in_ld[0], eng.out_ld[0]
 bits = (ptr(eng.hbits[0]), eng.hbits_ld[0]) if eng.hbits else (None, 0)
 
@@ -39,6 +44,9 @@ def layer0():
         call("dl_gemm_s3_nt_gather", B, hd, ld0, ptr(x0), ld0, ptr(eng.p_plane), FN.n_rows, eng.p_plane.shape[1],
              ptr(eng.in_cate), FN.cate_ld, FN.deep_cate_offset, FN.zero_row0, sp.S, sp.E, ptr(eng.WTp[0]), ld0,
              ld0 * ol0, ptr(eng.h[0]), eng.h_ld[0], 1, *bits, s)
+    elif mode == "tab":
+        call("dl_gemm_s3_nt_gather_tab", B, hd, ld0, ptr(x0), ld0, ptr(eng.p_plane), FN.n_rows, eng.p_plane.shape[1],
+             ptr(eng.gtab), sp.S, sp.E, ptr(eng.WTp[0]), ld0, ld0 * ol0, ptr(eng.h[0]), eng.h_ld[0], 1, *bits, s)
     elif mode == "pair":
         call("dl_gemm_s3_nt_bits", B, hd, ld0, ptr(x0), ld0, ptr(eng.WTp[0]), ld0, ld0 * ol0, ptr(eng.h[0]),
              eng.h_ld[0], 1, None, 0, *bits, s)
@@ -47,7 +55,10 @@ x0 = eng.x0b if eng.x0_direct else eng.x0
 
 
 def run():
-    if sp.fm:   # the slot plane: an FM reference's row and first-order weight in one 128-B slot
+    if tab:
+        call("dl_embed_fwd_gtab", C_ref(FN), ptr(eng.p_plane), 1, ptr(eng.in_cate), ptr(eng.in_cont), ptr(eng.in_vec),
+             ptr(x0), ptr(eng.fm_out), None, ptr(eng.gtab), ptr(eng.err), s)
+    elif sp.fm:   # the slot plane: an FM reference's row and first-order weight in one 128-B slot
         call("dl_embed_fwd_slots", C_ref(FL), ptr(eng.p_plane), ptr(eng.in_cate), ptr(eng.in_cont), ptr(eng.in_vec),
              ptr(x0), ptr(eng.fm_out), ptr(eng.fm_sum), ptr(eng.err), s)
     else:

@@ -304,6 +304,49 @@ def test_gemm_s3_nt_gather_equals_lookup_then_gemm(hip_lib, M, N, K, F, E, tld, 
     assert torch.equal(c, c_ref)
 
 
+@pytest.mark.parametrize("M,N,K,F,E,tld", [(65536, 400, 432, 26, 16, 32), (300, 400, 432, 26, 16, 16),
+                                           (257, 213, 72, 8, 8, 8), (77, 48, 96, 3, 32, 32),
+                                           (513, 16, 64, 1, 64, 64), (40, 400, 480, 26, 16, 32)])
+def test_gemm_s3_nt_gather_tab_equals_x0_gemm(hip_lib, M, N, K, F, E, tld):
+    """dl_gemm_s3_nt_gather_tab (predict's table form: the rows' byte offsets resolved beforehand
+    and staged as they stand) against dl_gemm_s3_nt_bits over the x0 that holds the looked-up
+    rows: output and ReLU bitmask bit-identical.  The offset table is built here by the layout
+    rule (common.h kGtab*) with masked entries and junk in the pitch padding; x0's gathered
+    columns are NaN (never read); a ragged batch."""
+    g = torch.Generator().manual_seed(M + N + K + F)
+    n_rows = 5000
+    table = torch.randn(n_rows, tld, generator=g)
+    rows = torch.randint(0, n_rows, (M, F), generator=g, dtype=torch.int64)
+    masked = torch.rand(M, F, generator=g) < 0.1
+    look = table[rows][:, :, :E] * (~masked)[:, :, None]
+    tiles = (M + 255) // 256
+    gt = np.full((tiles, F, 272), 0x12345678, dtype=np.uint32)   # pad entries: never read
+    m = np.arange(M)
+    gt[m // 256, :, m % 256] = np.where(masked.numpy(), 0xFFFFFF00, rows.numpy() * tld * 4).astype(np.uint32)
+    A_ref = torch.randn(M, K + 4, generator=g)
+    A_ref[:, :F * E] = look.reshape(M, F * E)
+    Ax = A_ref.clone()
+    Ax[:, :F * E] = float("nan")
+    Bm = (torch.randn(N, K, generator=g) * 0.05).cuda()
+    Bp = _planes(Bm, False)
+    ldc, ldb16 = N + 4, 32
+    Ar, Ad, Td = A_ref.cuda(), Ax.cuda(), table.cuda()
+    Gd = torch.from_numpy(gt.view(np.int32).reshape(-1)).cuda()
+    for epi, bits in ((1, True), (0, False)):
+        h_ref = torch.full((M, ldc), 7.0, device="cuda")
+        h = torch.full((M, ldc), 7.0, device="cuda")
+        b_ref = torch.full((M, ldb16), -1, dtype=torch.int16, device="cuda")
+        b = torch.full((M, ldb16), -1, dtype=torch.int16, device="cuda")
+        bb = lambda t: (ptr(t), ldb16) if bits else (None, 0)
+        call("dl_gemm_s3_nt_bits", M, N, K, ptr(Ar), K + 4, ptr(Bp), K, N * K, ptr(h_ref), ldc, epi, None, 0,
+             *bb(b_ref), _s())
+        call("dl_gemm_s3_nt_gather_tab", M, N, K, ptr(Ad), K + 4, ptr(Td), n_rows, tld, ptr(Gd), F, E, ptr(Bp), K,
+             N * K, ptr(h), ldc, epi, *bb(b), _s())
+        torch.cuda.synchronize()
+        assert torch.equal(h, h_ref)
+        assert torch.equal(b, b_ref)
+
+
 def test_gemm_s3_nt_gather_argument_checks(hip_lib):
     """The gather's preconditions fail loudly: a partial 32-deep chunk, too many fields, an
     emb_dim outside {8..64}, the mask epilogue, a table past one 32-bit buffer range."""
@@ -318,6 +361,13 @@ def test_gemm_s3_nt_gather_argument_checks(hip_lib):
                       (base(2, 16, epi=2), "epilogue"), (base(2, 16, n_rows=1 << 26), "buffer range")]:
         with pytest.raises(_lib.DLError, match=msg):
             call("dl_gemm_s3_nt_gather", *args)
+    G = torch.zeros(26 * 272 + 1, dtype=torch.int32, device="cuda")
+    with pytest.raises(_lib.DLError, match="offset table"):
+        call("dl_gemm_s3_nt_gather_tab", 64, 16, 432, ptr(A), 440, ptr(T), 100, 16, None, 26, 16, ptr(Bp), 432,
+             16 * 432, ptr(C_), 16, 1, None, 0, _s())
+    with pytest.raises(_lib.DLError, match="16-B aligned"):
+        call("dl_gemm_s3_nt_gather_tab", 64, 16, 432, ptr(A), 440, ptr(T), 100, 16, ptr(G[1:]), 26, 16, ptr(Bp),
+             432, 16 * 432, ptr(C_), 16, 1, None, 0, _s())
 
 
 @pytest.mark.parametrize("M,N,K,splits", [(432, 400, 65536, 64), (416, 400, 8192, 8), (428, 396, 5000, 3),

@@ -348,11 +348,15 @@ def test_flat_lookup_after_flush_bit_identical(hip_lib, name):
     ("dnn_pipeline", dict(C=13, V=3, S=24, E=8, cate_index_size=10000, hidden=[64, 32])),
     ("deepfm_pipeline", dict(C=13, V=0, S=6, E=16, cate_index_size=7000, hidden=[48, 32]))])
 def test_fused_gather_predict_bit_identical(hip_lib, name, kw, monkeypatch):
-    """predict() on current planes with the deep lookup inside the first tower layer
-    (dl_gemm_s3_nt_gather, the default) against the lookup writing x0 followed by the plain
-    GEMM (DLAMD_FUSED_GATHER=0): logits, FM outputs and the first layer's activations
-    bit-identical, over a batch that is not a multiple of the 256-row block with padding ids
-    (the zero row) in every field; and the engine really took the fused path."""
+    """predict() on current planes with the deep lookup inside the first tower layer against
+    the lookup writing x0 followed by the plain GEMM (DLAMD_FUSED_GATHER=0): logits, FM outputs
+    and the first layer's activations bit-identical, over a batch that is not a multiple of the
+    256-row block with padding ids (the zero row) in every field; and the engine really took
+    the fused path.  The table form (DLAMD_GATHER_TAB=1: dl_embed_fwd_gtab +
+    dl_gemm_s3_nt_gather_tab; the offset table the lookup wrote equals the ids' rows times the
+    plane stride) and the id form (the default, dl_gemm_s3_nt_gather) both; x0's deep columns
+    are neither written nor read by either — they keep a NaN sentinel."""
+    monkeypatch.setenv("DLAMD_GATHER_TAB", "1")
     spec = ModelSpec(name, **kw)
     e = CTREngine(spec, max_batch=300, seed=3, adam="lazy", hist_len=8)
     bs = _batches(name, kw, 300, 5, seed=29)
@@ -364,17 +368,42 @@ def test_fused_gather_predict_bit_identical(hip_lib, name, kw, monkeypatch):
     b["cate_feats"] = cate
     e.flush(planes=True)
     assert e.fused_gather_l0()
+    tab = e.fused_gather_tab(300)
+    assert tab
     calls = []
     orig = e._c
     monkeypatch.setattr(e, "_c", lambda tag, fn, *a: (calls.append(fn), orig(tag, fn, *a))[1])
+    D = spec.S * spec.E
+    e.x0[:, :D] = float("nan")
     got = e.predict(b, logits=True)
     got_fm = e.fm_out[:300].cpu().numpy().copy()
     got_h = e.h[0][:300].cpu().numpy().copy()
-    assert "dl_gemm_s3_nt_gather" in calls
+    if tab:
+        assert "dl_gemm_s3_nt_gather_tab" in calls and "dl_embed_fwd_gtab" in calls
+        assert torch.isnan(e.x0[:, :D]).all()   # x0's deep columns not written (nor read: finite outputs)
+        S, E = spec.S, spec.E
+        ids = e.in_cate[:300, :S].cpu().numpy().astype(np.int64)
+        FL = e._flat_layout(300)
+        rows = ids + FL.deep_cate_offset
+        ok = (rows >= (1 if FL.zero_row0 else 0)) & (rows < FL.n_rows)
+        want = np.where(ok, rows * e.p_plane.shape[1] * 4, 0xFFFFFF00).astype(np.uint32)
+        gt = e.gtab.cpu().numpy().view(np.uint32).reshape(-1, S, 272)
+        m = np.arange(300)
+        np.testing.assert_array_equal(gt[m // 256, :, m % 256], want)
+        calls.clear()
+        monkeypatch.setenv("DLAMD_GATHER_TAB", "0")
+        ref_id = e.predict(b, logits=True)
+        assert "dl_gemm_s3_nt_gather" in calls and "dl_gemm_s3_nt_gather_tab" not in calls
+        assert torch.isnan(e.x0[:, :D]).all()
+        np.testing.assert_array_equal(got, ref_id)
+        np.testing.assert_array_equal(got_h, e.h[0][:300].cpu().numpy())
+    else:
+        assert "dl_gemm_s3_nt_gather" in calls
+    assert np.isfinite(got).all()
     monkeypatch.setenv("DLAMD_FUSED_GATHER", "0")
     calls.clear()
     ref = e.predict(b, logits=True)
-    assert "dl_gemm_s3_nt_gather" not in calls
+    assert "dl_gemm_s3_nt_gather" not in calls and "dl_gemm_s3_nt_gather_tab" not in calls
     np.testing.assert_array_equal(got, ref)
     np.testing.assert_array_equal(got_fm, e.fm_out[:300].cpu().numpy())
     np.testing.assert_array_equal(got_h, e.h[0][:300].cpu().numpy())
