@@ -368,8 +368,7 @@ def test_fused_gather_predict_bit_identical(hip_lib, name, kw, monkeypatch):
     b["cate_feats"] = cate
     e.flush(planes=True)
     assert e.fused_gather_l0()
-    tab = e.fused_gather_tab(300)
-    assert tab
+    assert e.fused_gather_tab(300)
     calls = []
     orig = e._c
     monkeypatch.setattr(e, "_c", lambda tag, fn, *a: (calls.append(fn), orig(tag, fn, *a))[1])
@@ -378,27 +377,24 @@ def test_fused_gather_predict_bit_identical(hip_lib, name, kw, monkeypatch):
     got = e.predict(b, logits=True)
     got_fm = e.fm_out[:300].cpu().numpy().copy()
     got_h = e.h[0][:300].cpu().numpy().copy()
-    if tab:
-        assert "dl_gemm_s3_nt_gather_tab" in calls and "dl_embed_fwd_gtab" in calls
-        assert torch.isnan(e.x0[:, :D]).all()   # x0's deep columns not written (nor read: finite outputs)
-        S, E = spec.S, spec.E
-        ids = e.in_cate[:300, :S].cpu().numpy().astype(np.int64)
-        FL = e._flat_layout(300)
-        rows = ids + FL.deep_cate_offset
-        ok = (rows >= (1 if FL.zero_row0 else 0)) & (rows < FL.n_rows)
-        want = np.where(ok, rows * e.p_plane.shape[1] * 4, 0xFFFFFF00).astype(np.uint32)
-        gt = e.gtab.cpu().numpy().view(np.uint32).reshape(-1, S, 272)
-        m = np.arange(300)
-        np.testing.assert_array_equal(gt[m // 256, :, m % 256], want)
-        calls.clear()
-        monkeypatch.setenv("DLAMD_GATHER_TAB", "0")
-        ref_id = e.predict(b, logits=True)
-        assert "dl_gemm_s3_nt_gather" in calls and "dl_gemm_s3_nt_gather_tab" not in calls
-        assert torch.isnan(e.x0[:, :D]).all()
-        np.testing.assert_array_equal(got, ref_id)
-        np.testing.assert_array_equal(got_h, e.h[0][:300].cpu().numpy())
-    else:
-        assert "dl_gemm_s3_nt_gather" in calls
+    assert "dl_gemm_s3_nt_gather_tab" in calls and "dl_embed_fwd_gtab" in calls
+    assert torch.isnan(e.x0[:, :D]).all()   # x0's deep columns not written (nor read: finite outputs)
+    S, E = spec.S, spec.E
+    ids = e.in_cate[:300, :S].cpu().numpy().astype(np.int64)
+    FL = e._flat_layout(300)
+    rows = ids + FL.deep_cate_offset
+    ok = (rows >= (1 if FL.zero_row0 else 0)) & (rows < FL.n_rows)
+    want = np.where(ok, rows * e.p_plane.shape[1] * 4, 0xFFFFFF00).astype(np.uint32)
+    gt = e.gtab.cpu().numpy().view(np.uint32).reshape(-1, S, 272)
+    m = np.arange(300)
+    np.testing.assert_array_equal(gt[m // 256, :, m % 256], want)
+    calls.clear()
+    monkeypatch.setenv("DLAMD_GATHER_TAB", "0")
+    ref_id = e.predict(b, logits=True)
+    assert "dl_gemm_s3_nt_gather" in calls and "dl_gemm_s3_nt_gather_tab" not in calls
+    assert torch.isnan(e.x0[:, :D]).all()
+    np.testing.assert_array_equal(got, ref_id)
+    np.testing.assert_array_equal(got_h, e.h[0][:300].cpu().numpy())
     assert np.isfinite(got).all()
     monkeypatch.setenv("DLAMD_FUSED_GATHER", "0")
     calls.clear()
