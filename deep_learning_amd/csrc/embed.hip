@@ -69,8 +69,9 @@ constexpr int kMaxSlots = 128;     // FM slots + deep slots per sample
 #ifndef DL_FWD_MIN_WAVES
 #define DL_FWD_MIN_WAVES 5
 #endif
-// Occupancy: the gathered-rows form (C2: E = 16, NPS = 5) needs 97 VGPRs unbounded — one past
-// the 5-waves-per-SIMD line; the bound keeps it at 96 (no spill; NPS > 5 would spill: unbounded).
+// Occupancy: NPS <= 4 fits 5 waves a SIMD (83-92 VGPRs); the NPS = 5 forms (C2's full lookup: 13 +
+// 26 FM + 26 deep slots) need 100 VGPRs — at 5 waves they spilled 3, so they take 4 (the plain
+// slot-plane lookup 131.7 -> 128.5 us uniform, 92.5 -> 90.8 Zipf, profiles/r06z5/); NPS > 5: unbounded.
 #ifndef DL_POOL_DIAG_NO_W1
 #define DL_POOL_DIAG_NO_W1 0   // diagnostics build: first-order weights not read by the forward / pooling (wrong fm_out)
 #endif
@@ -83,7 +84,8 @@ constexpr int kMaxSlots = 128;     // FM slots + deep slots per sample
 template <int E, int NPS, int REC = 0>
 // (two samples in flight a wave, DL_FWD_SPW below: 4 waves a SIMD, up to 128 VGPRs)
 __global__ __launch_bounds__(256, (REC == 1 || NPS > 5) ? 1
-                                  : (DL_FWD_SPW > 1 && (REC == 0 || REC == 3) && NPS <= 3) ? 4 : DL_FWD_MIN_WAVES)
+                                  : (NPS == 5 || (DL_FWD_SPW > 1 && (REC == 0 || REC == 3) && NPS <= 3)) ? 4
+                                  : DL_FWD_MIN_WAVES)
 void embed_fwd_kernel(EmbArgs a) {
   // Per block iteration a tile of 16 samples is staged: every (sample, slot)
   // row index is resolved once into LDS by a coalesced pass over the id matrix
